@@ -1,0 +1,594 @@
+// libgpbs: the C ABI (libxl/libxc analog).  Validation mirrors libxl
+// (X:tools/libxl/libxl.c:4007-4116) so every frontend (ctypes, RPC daemon,
+// gpbsctl) sees the same ranges and error codes.
+#include <cstring>
+#include <mutex>
+
+#include "../core/engine.h"
+#include "../include/gpbs/gpbs.h"
+
+using namespace gpbs;
+
+struct gpbs_engine {
+  Engine* e;
+};
+
+namespace gpbs {
+const char* const kPerfcNames[PC_COUNT] = {
+#define GPBS_PERFC_NAME(n) #n,
+    GPBS_PERFC_LIST(GPBS_PERFC_NAME)
+#undef GPBS_PERFC_NAME
+};
+}  // namespace gpbs
+
+static_assert(sizeof(gpbs_adapt_state_t) == sizeof(AdaptState), "adapt state layout");
+static_assert(sizeof(gpbs_adapt_params_t) == sizeof(AdaptParams), "adapt params layout");
+static_assert(sizeof(gpbs_atc_params_t) == sizeof(AtcParams), "atc params layout");
+static_assert(sizeof(gpbs_trace_record_t) == sizeof(TraceRecord), "trace layout");
+
+#define LOCK(E) std::lock_guard<std::recursive_mutex> _g((E)->e->mu)
+#define DONE(E)                 \
+  do {                          \
+    (E)->e->process_softirqs(); \
+    (E)->e->flush_actuation();  \
+    (E)->e->kick();             \
+  } while (0)
+
+static int copy_str(const std::string& s, char* out, int len) {
+  if (!out || len <= 0) return (int)s.size();
+  int n = (int)std::min<size_t>(s.size(), (size_t)len - 1);
+  std::memcpy(out, s.data(), n);
+  out[n] = 0;
+  return (int)s.size();
+}
+
+static Tenant* live(gpbs_engine_t* e, int t) {
+  Tenant* d = e->e->tenant(t);
+  return d && d->alive ? d : nullptr;
+}
+
+int gpbs_tenant_pause(gpbs_engine_t* e, int t) {
+  LOCK(e);
+  Tenant* d = live(e, t);
+  if (!d) return GPBS_ENOENT;
+  d->pause_count++;
+  for (int sid : d->slots) e->e->vcpu_sleep_nosync(*e->e->slots[sid]);
+  DONE(e);
+  return GPBS_OK;
+}
+
+int gpbs_tenant_unpause(gpbs_engine_t* e, int t) {
+  LOCK(e);
+  Tenant* d = live(e, t);
+  if (!d) return GPBS_ENOENT;
+  if (d->pause_count == 0) return GPBS_EINVAL;
+  if (--d->pause_count == 0)
+    for (int sid : d->slots) e->e->vcpu_wake(*e->e->slots[sid]);
+  d->last_heartbeat = e->e->now();
+  DONE(e);
+  return GPBS_OK;
+}
+
+int gpbs_tenant_set_nslots(gpbs_engine_t* e, int t, int n) {
+  LOCK(e);
+  int r = e->e->tenant_set_nslots(t, n);
+  DONE(e);
+  return r;
+}
+
+int gpbs_slot_id(gpbs_engine_t* e, int t, int idx) {
+  LOCK(e);
+  Tenant* d = live(e, t);
+  if (!d || idx < 0 || idx >= (int)d->slots.size()) return GPBS_EINVAL;
+  return d->slots[idx];
+}
+
+template <typename F>
+static int each_slot(gpbs_engine_t* e, int t, int idx, F f) {
+  Tenant* d = live(e, t);
+  if (!d) return GPBS_ENOENT;
+  if (idx < 0) {
+    for (int sid : d->slots) f(*e->e->slots[sid]);
+  } else {
+    if (idx >= (int)d->slots.size()) return GPBS_EINVAL;
+    f(*e->e->slots[d->slots[idx]]);
+  }
+  return GPBS_OK;
+}
+
+
+extern "C" {
+
+void gpbs_boot_defaults(gpbs_boot_params_t* p) {
+  std::memset(p, 0, sizeof(*p));
+  std::strncpy(p->sched, "credit", sizeof(p->sched) - 1);
+  p->tslice_us = 100;        // CSCHED_DEFAULT_TSLICE_US (sched_credit.c:52)
+  p->ratelimit_us = 1000;    // SCHED_DEFAULT_RATELIMIT_US (sched-if.h:21) -> clamped to tslice
+  p->smt_power_savings = 0;
+  p->tickle_one_idle = 1;
+  p->default_yield = 0;
+  p->migration_delay_us = 0;
+  p->metric_period_us = 1000;  // CSCHED_METRIC_TICK_PERIOD
+  p->slice_apply_us = 3000;    // CSCHED_TIME_APPLY
+  p->sim_clock = 0;
+  p->pmu_refresh_us = 1111;
+  p->dom0_quirk = 1;
+  p->heartbeat_timeout_us = 0;
+  p->trace_capacity = 1 << 16;
+  AdaptParams a;
+  std::memcpy(&p->adapt, &a, sizeof(a));
+  AtcParams t;
+  std::memcpy(&p->atc, &t, sizeof(t));
+}
+
+int gpbs_abi_version(void) { return GPBS_ABI_VERSION; }
+
+const char* gpbs_strerror(int err) {
+  switch (err) {
+    case GPBS_OK: return "ok";
+    case GPBS_EINVAL: return "invalid argument";
+    case GPBS_ENOENT: return "no such tenant/pool";
+    case GPBS_EBUSY: return "busy";
+    case GPBS_ENOMEM: return "out of memory";
+    case GPBS_ERANGE: return "value out of range";
+    case GPBS_ENOSPC: return "no space";
+    case GPBS_EEXIST: return "already exists";
+    default: return "unknown error";
+  }
+}
+
+gpbs_engine_t* gpbs_engine_create(const gpbs_boot_params_t* p) {
+  gpbs_boot_params_t d;
+  if (!p) {
+    gpbs_boot_defaults(&d);
+    p = &d;
+  }
+  auto* h = new gpbs_engine;
+  h->e = new Engine(*p);
+  if (h->e->pools.empty() || !h->e->pools[0]) {
+    delete h->e;
+    delete h;
+    return nullptr;
+  }
+  return h;
+}
+
+void gpbs_engine_destroy(gpbs_engine_t* e) {
+  if (!e) return;
+  delete e->e;
+  delete e;
+}
+
+int gpbs_partition_add(gpbs_engine_t* e, int gpu, int xcd) {
+  LOCK(e);
+  return e->e->partition_add(gpu, xcd);
+}
+
+int gpbs_num_partitions(gpbs_engine_t* e) {
+  LOCK(e);
+  return (int)e->e->parts.size();
+}
+
+int gpbs_pool_create(gpbs_engine_t* e, const char* name, const char* sched) {
+  LOCK(e);
+  if (!name || !*name) return GPBS_EINVAL;
+  int r = e->e->pool_create(name, sched ? sched : "");
+  DONE(e);
+  return r;
+}
+
+int gpbs_pool_destroy(gpbs_engine_t* e, int pool) {
+  LOCK(e);
+  return e->e->pool_destroy(pool);
+}
+
+int gpbs_pool_rename(gpbs_engine_t* e, int pool, const char* name) {
+  LOCK(e);
+  Pool* p = e->e->pool(pool);
+  if (!p || !name || !*name) return GPBS_EINVAL;
+  for (auto& q : e->e->pools)
+    if (q && q->name == name && q.get() != p) return GPBS_EEXIST;
+  p->name = name;
+  return GPBS_OK;
+}
+
+int gpbs_pool_find(gpbs_engine_t* e, const char* name) {
+  LOCK(e);
+  for (auto& q : e->e->pools)
+    if (q && name && q->name == name) return q->id;
+  return GPBS_ENOENT;
+}
+
+int gpbs_pool_assign(gpbs_engine_t* e, int pool, int part) {
+  LOCK(e);
+  int r = e->e->pool_assign(pool, part);
+  DONE(e);
+  return r;
+}
+
+int gpbs_pool_unassign(gpbs_engine_t* e, int pool, int part) {
+  LOCK(e);
+  int r = e->e->pool_unassign(pool, part);
+  DONE(e);
+  return r;
+}
+
+int gpbs_pool_info(gpbs_engine_t* e, int pool, char* name, int name_len, char* sched, int sched_len, uint64_t* mask4,
+                   int* n_tenants) {
+  LOCK(e);
+  Pool* p = e->e->pool(pool);
+  if (!p) return GPBS_ENOENT;
+  copy_str(p->name, name, name_len);
+  copy_str(p->sched->opt_name(), sched, sched_len);
+  if (mask4)
+    for (int i = 0; i < 4; ++i) mask4[i] = p->cpus.w[i];
+  if (n_tenants) {
+    int n = 0;
+    for (auto& t : e->e->tenants)
+      if (t && t->alive && t->pool == pool) n++;
+    *n_tenants = n;
+  }
+  return GPBS_OK;
+}
+
+int gpbs_pool_list(gpbs_engine_t* e, int* ids, int max) {
+  LOCK(e);
+  int n = 0;
+  for (auto& p : e->e->pools)
+    if (p) {
+      if (ids && n < max) ids[n] = p->id;
+      n++;
+    }
+  return n;
+}
+
+int gpbs_partition_info(gpbs_engine_t* e, int part, gpbs_partition_info_t* o) {
+  LOCK(e);
+  Engine& E = *e->e;
+  if (part < 0 || part >= (int)E.parts.size()) return GPBS_EINVAL;
+  Partition& P = *E.parts[part];
+  std::memset(o, 0, sizeof(*o));
+  o->id = P.id;
+  o->gpu = P.gpu;
+  o->xcd = P.xcd;
+  o->pool = P.pool;
+  Slot& c = *E.slots[P.curr];
+  o->curr_slot = c.is_idle() ? -1 : c.id;
+  o->curr_tenant = c.tenant;
+  o->idle = c.is_idle();
+  o->switches = P.switches;
+  int rq = 0;
+  for (auto& s : E.slots)
+    if (s && !s->is_idle() && s->processor == part && !s->is_running && E.runnable(*s)) rq++;
+  o->runq_len = rq;
+  return GPBS_OK;
+}
+
+int gpbs_tenant_create(gpbs_engine_t* e, const char* name, int pool, int nslots, int weight, int cap) {
+  LOCK(e);
+  if (!name || !*name) return GPBS_EINVAL;
+  int r = e->e->tenant_create(name, pool, nslots, weight, cap);
+  DONE(e);
+  return r;
+}
+
+int gpbs_tenant_destroy(gpbs_engine_t* e, int t) {
+  LOCK(e);
+  int r = e->e->tenant_destroy(t);
+  DONE(e);
+  return r;
+}
+
+int gpbs_tenant_find(gpbs_engine_t* e, const char* name) {
+  LOCK(e);
+  for (auto& t : e->e->tenants)
+    if (t && t->alive && name && t->name == name) return t->id;
+  return GPBS_ENOENT;
+}
+
+int gpbs_tenant_list(gpbs_engine_t* e, int* ids, int max) {
+  LOCK(e);
+  int n = 0;
+  for (auto& t : e->e->tenants)
+    if (t && t->alive) {
+      if (ids && n < max) ids[n] = t->id;
+      n++;
+    }
+  return n;
+}
+
+int gpbs_tenant_move(gpbs_engine_t* e, int t, int pool) {
+  LOCK(e);
+  int r = e->e->tenant_move(t, pool);
+  DONE(e);
+  return r;
+}
+
+int gpbs_slot_wake(gpbs_engine_t* e, int t, int idx) {
+  LOCK(e);
+  int r = each_slot(e, t, idx, [&](Slot& v) { e->e->vcpu_unblock(v); });
+  DONE(e);
+  return r;
+}
+
+int gpbs_slot_block(gpbs_engine_t* e, int t, int idx) {
+  LOCK(e);
+  int r = each_slot(e, t, idx, [&](Slot& v) { e->e->vcpu_block(v); });
+  DONE(e);
+  return r;
+}
+
+int gpbs_slot_yield(gpbs_engine_t* e, int t, int idx) {
+  LOCK(e);
+  int r = each_slot(e, t, idx, [&](Slot& v) {
+    if (Scheduler* S = e->e->sched_of_tenant(v.tenant)) {
+      S->yield(v);
+      if (v.is_running) e->e->raise_softirq(v.processor);
+    }
+  });
+  DONE(e);
+  return r;
+}
+
+int gpbs_slot_pin(gpbs_engine_t* e, int t, int idx, const uint64_t* mask4) {
+  LOCK(e);
+  Mask m;
+  for (int i = 0; i < 4; ++i) m.w[i] = mask4[i];
+  Tenant* d = live(e, t);
+  if (!d) return GPBS_ENOENT;
+  if ((m & e->e->pools[d->pool]->cpus).empty()) return GPBS_EINVAL;
+  int r = each_slot(e, t, idx, [&](Slot& v) {
+    v.affinity = m;
+    if (!m.test(v.processor)) {  // vcpu_set_affinity: migrate off a forbidden cpu
+      v.pause_flags |= VPF_MIGRATING;
+      e->e->vcpu_sleep_nosync(v);
+      if (!v.is_running) e->e->vcpu_migrate(v);
+    }
+  });
+  DONE(e);
+  return r;
+}
+
+int gpbs_tenant_info(gpbs_engine_t* e, int t, gpbs_tenant_info_t* o) {
+  LOCK(e);
+  Engine& E = *e->e;
+  Tenant* d = E.tenant(t);
+  if (!d || !d->priv) return GPBS_ENOENT;
+  std::memset(o, 0, sizeof(*o));
+  o->id = d->id;
+  o->pool = d->pool;
+  o->nslots = (int)d->slots.size();
+  o->paused = d->pause_count;
+  o->alive = d->alive;
+  copy_str(d->name, o->name, sizeof(o->name));
+  if (Scheduler* S = E.sched_of_tenant(t)) S->fill_tenant_info(*d, *o);
+  const int64_t n = E.now();
+  for (int sid : d->slots) {
+    Slot& v = *E.slots[sid];
+    o->sched_count += v.sched_count;
+    o->run_ns += v.rs_time[RS_RUNNING] + (v.rs == RS_RUNNING ? n - v.rs_entry : 0);
+  }
+  return GPBS_OK;
+}
+
+int gpbs_slot_info(gpbs_engine_t* e, int sid, gpbs_slot_info_t* o) {
+  LOCK(e);
+  Engine& E = *e->e;
+  Slot* v = E.slot(sid);
+  if (!v) return GPBS_ENOENT;
+  std::memset(o, 0, sizeof(*o));
+  o->id = v->id;
+  o->tenant = v->tenant;
+  o->index = v->index;
+  o->processor = v->processor;
+  o->runstate = v->rs;
+  o->is_running = v->is_running;
+  for (int i = 0; i < 4; ++i) {
+    o->pmc[i] = v->pmc[i];
+    o->affinity[i] = v->affinity.w[i];
+  }
+  o->sched_count = v->sched_count;
+  const int64_t n = E.now();
+  int64_t extra = n - v->rs_entry;
+  o->run_ns = v->rs_time[RS_RUNNING] + (v->rs == RS_RUNNING ? extra : 0);
+  o->runnable_ns = v->rs_time[RS_RUNNABLE] + (v->rs == RS_RUNNABLE ? extra : 0);
+  o->blocked_ns = v->rs_time[RS_BLOCKED] + (v->rs == RS_BLOCKED ? extra : 0);
+  if (v->priv)
+    if (Scheduler* S = v->is_idle() ? E.sched_of_part(v->processor) : E.sched_of_tenant(v->tenant))
+      S->fill_slot_info(*v, *o);
+  return GPBS_OK;
+}
+
+int gpbs_tenant_adapt_state(gpbs_engine_t* e, int t, gpbs_adapt_state_t* out, int set) {
+  LOCK(e);
+  Tenant* d = live(e, t);
+  if (!d) return GPBS_ENOENT;
+  Scheduler* S = e->e->sched_of_tenant(t);
+  AdaptState st;
+  if (set) {
+    std::memcpy(&st, out, sizeof(st));
+    return S->set_tenant_adapt(*d, st) ? GPBS_OK : GPBS_EINVAL;
+  }
+  if (!S->tenant_adapt(*d, &st)) return GPBS_EINVAL;
+  std::memcpy(out, &st, sizeof(st));
+  return GPBS_OK;
+}
+
+int gpbs_tenant_heartbeat(gpbs_engine_t* e, int t) {
+  LOCK(e);
+  Tenant* d = live(e, t);
+  if (!d) return GPBS_ENOENT;
+  d->last_heartbeat = e->e->now();
+  return GPBS_OK;
+}
+
+int gpbs_sched_credit_get(gpbs_engine_t* e, int t, int* weight, int* cap) {
+  LOCK(e);
+  Tenant* d = live(e, t);
+  if (!d) return GPBS_ENOENT;
+  return e->e->sched_of_tenant(t)->adjust(*d, false, weight, cap);
+}
+
+int gpbs_sched_credit_set(gpbs_engine_t* e, int t, int weight, int cap) {
+  LOCK(e);
+  Tenant* d = live(e, t);
+  if (!d) return GPBS_ENOENT;
+  // libxl.c:4026-4045: weight 1..65535, cap 0..100*(max_vcpu_id+1)
+  if (weight != -1 && (weight < 1 || weight > GPBS_WEIGHT_MAX)) return GPBS_ERANGE;
+  if (cap != -1 && (cap < 0 || cap > 100 * (int)d->slots.size())) return GPBS_ERANGE;
+  int r = e->e->sched_of_tenant(t)->adjust(*d, true, &weight, &cap);
+  DONE(e);
+  return r;
+}
+
+int gpbs_sched_params_get(gpbs_engine_t* e, int pool, int* tslice_us, int* ratelimit_us) {
+  LOCK(e);
+  Pool* p = e->e->pool(pool);
+  if (!p) return GPBS_ENOENT;
+  return p->sched->adjust_global(false, tslice_us, ratelimit_us);
+}
+
+int gpbs_sched_params_set(gpbs_engine_t* e, int pool, int tslice_us, int ratelimit_us) {
+  LOCK(e);
+  Pool* p = e->e->pool(pool);
+  if (!p) return GPBS_ENOENT;
+  int r = p->sched->adjust_global(true, &tslice_us, &ratelimit_us);
+  DONE(e);
+  return r;
+}
+
+int gpbs_sched_name(gpbs_engine_t* e, int pool, char* out, int len) {
+  LOCK(e);
+  Pool* p = e->e->pool(pool);
+  if (!p) return GPBS_ENOENT;
+  return copy_str(p->sched->opt_name(), out, len);
+}
+
+int gpbs_report_wait(gpbs_engine_t* e, int t, uint64_t wait_ns, int kind) {
+  LOCK(e);
+  Tenant* d = live(e, t);
+  if (!d) return GPBS_ENOENT;
+  e->e->sched_of_tenant(t)->report(*d, wait_ns, kind);
+  e->e->perfc.incr(PC_report_rx);
+  e->e->emit(TRC_REPORT, 0, t, kind, (uint32_t)wait_ns, (uint32_t)(wait_ns >> 32));
+  return GPBS_OK;
+}
+
+int gpbs_report_requests(gpbs_engine_t* e, int t, uint64_t n) {
+  LOCK(e);
+  Tenant* d = live(e, t);
+  if (!d) return GPBS_ENOENT;
+  d->pending_requests += n;
+  return GPBS_OK;
+}
+
+int gpbs_set_counter_ops(gpbs_engine_t* e, const gpbs_counter_ops_t* ops) {
+  LOCK(e);
+  if (ops)
+    e->e->counter_ops = *ops;
+  else
+    e->e->counter_ops = gpbs_counter_ops_t{};
+  return GPBS_OK;
+}
+
+int gpbs_set_actuator_ops(gpbs_engine_t* e, const gpbs_actuator_ops_t* ops) {
+  LOCK(e);
+  if (ops)
+    e->e->actuator_ops = *ops;
+  else
+    e->e->actuator_ops = gpbs_actuator_ops_t{};
+  return GPBS_OK;
+}
+
+int gpbs_slot_set_pmc(gpbs_engine_t* e, int sid, const uint64_t* pmc4) {
+  LOCK(e);
+  Slot* v = e->e->slot(sid);
+  if (!v) return GPBS_ENOENT;
+  for (int i = 0; i < 4; ++i) v->pmc[i] = pmc4[i];
+  return GPBS_OK;
+}
+
+int64_t gpbs_now(gpbs_engine_t* e) { return e->e->now(); }
+
+int gpbs_advance(gpbs_engine_t* e, int64_t now_ns) {
+  LOCK(e);
+  if (!e->e->boot.sim_clock) return GPBS_EINVAL;
+  e->e->run_due(now_ns);
+  return GPBS_OK;
+}
+
+int gpbs_start(gpbs_engine_t* e) { return e->e->start(); }
+int gpbs_stop(gpbs_engine_t* e) { return e->e->stop(); }
+
+int gpbs_poll(gpbs_engine_t* e) {
+  LOCK(e);
+  e->e->run_due(e->e->now());
+  return GPBS_OK;
+}
+
+int64_t gpbs_next_event(gpbs_engine_t* e) {
+  LOCK(e);
+  return e->e->next_deadline();
+}
+
+int gpbs_debug_keys(gpbs_engine_t* e, const char* keys, char* out, int len) {
+  LOCK(e);
+  return copy_str(e->e->debug_keys(keys ? keys : ""), out, len);
+}
+
+int gpbs_dmesg(gpbs_engine_t* e, char* out, int len, int clear) {
+  LOCK(e);
+  return copy_str(e->e->dmesg(clear != 0), out, len);
+}
+
+int gpbs_trace_read(gpbs_engine_t* e, uint64_t* cursor, gpbs_trace_record_t* out, int max, uint64_t* lost) {
+  return (int)e->e->trace->read(cursor, reinterpret_cast<TraceRecord*>(out), (size_t)max, lost);
+}
+
+int gpbs_trace_set_mask(gpbs_engine_t* e, uint64_t mask) {
+  e->e->trace->set_mask(mask);
+  return GPBS_OK;
+}
+
+int gpbs_trace_emit(gpbs_engine_t* e, uint32_t ev, uint32_t cpu, uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3) {
+  LOCK(e);
+  e->e->emit(ev, cpu, a0, a1, a2, a3);
+  if (ev == TRC_GANG_EPOCH) e->e->perfc.incr(PC_gang_epoch);
+  return GPBS_OK;
+}
+
+int gpbs_perfc_count(void) { return PC_COUNT; }
+const char* gpbs_perfc_name(int i) { return i >= 0 && i < PC_COUNT ? kPerfcNames[i] : nullptr; }
+
+int gpbs_perfc_read(gpbs_engine_t* e, uint64_t* out, int max) {
+  int n = std::min(max, (int)PC_COUNT);
+  for (int i = 0; i < n; ++i) out[i] = e->e->perfc.get((PerfcId)i);
+  return n;
+}
+
+int gpbs_perfc_reset(gpbs_engine_t* e) {
+  e->e->perfc.reset();
+  return GPBS_OK;
+}
+
+int gpbs_check_invariants(gpbs_engine_t* e, char* out, int len) {
+  LOCK(e);
+  std::string s = e->e->check_invariants();
+  copy_str(s, out, len);
+  return s.empty() ? 0 : 1;
+}
+
+}  // extern "C"
+
+// Host reference adaptation exposed for oracle/device parity tests.
+extern "C" void gpbs_adapt_init(gpbs_adapt_state_t* s, const gpbs_adapt_params_t* p, uint32_t default_tslice_us) {
+  adapt_init(*reinterpret_cast<AdaptState*>(s), *reinterpret_cast<const AdaptParams*>(p), default_tslice_us);
+}
+
+extern "C" int gpbs_adapt_update(gpbs_adapt_state_t* s, const gpbs_adapt_params_t* p, uint64_t inst, uint64_t miss,
+                                 uint64_t spin_sum, uint64_t spin_cnt) {
+  bool rearm = false;
+  int d = adapt_update(*reinterpret_cast<AdaptState*>(s), *reinterpret_cast<const AdaptParams*>(p), inst, miss,
+                       spin_sum, spin_cnt, &rearm);
+  return (d + 1) | (rearm ? 4 : 0);
+}

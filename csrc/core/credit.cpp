@@ -1,0 +1,965 @@
+// Credit scheduler with the PBS per-tenant adaptive quantum.
+//
+// Behavior parity (X: = /root/reference/xen-4.2.1/):
+//   priorities / flags           X:xen/common/sched_credit.c:62-75
+//   __runq_insert / tickle       :489-525, :550-610
+//   burn_credits (1 credit/us)   :527-543
+//   _csched_cpu_pick             :765-852
+//   vcpu_acct (+migrate)         :907-949
+//   wake (BOOST) / sleep / yield :1021-1101
+//   dom_cntl / sys_cntl          :1103-1174  (Q2 fix: recompute derived fields)
+//   dom_init (PBS state)         :1196-1237
+//   runq_sort                    :1259-1300
+//   acct (+P1g ceiling)          :1302-1519
+//   tick (per-tenant period)     :1521-1557
+//   runq_steal / load_balance    :1559-1672
+//   do_schedule (per-tenant q)   :1678-1809
+//   metric tick / dom update     :391-465  (Q3/Q5 fixes)
+//   dumps r / z                  :1811-1974
+//   ATC policy (mode "atc")      X:xen/common/sched_credit_atc.c:462-543,1916
+//
+// Modes: "credit"       PBS adaptive credit (the reference's built default),
+//        "credit-fixed" upstream credit (global quantum, no adaptation),
+//        "atc"          spin-latency driven global re-slicing.
+#include <algorithm>
+#include <cinttypes>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <list>
+
+#include "engine.h"
+
+namespace gpbs {
+
+namespace {
+constexpr uint16_t FLAG_PARKED = 0x1;
+constexpr uint16_t FLAG_YIELD = 0x2;
+constexpr int kDefaultWeight = 256;
+
+std::string fmt(const char* f, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, f);
+  vsnprintf(buf, sizeof(buf), f, ap);
+  va_end(ap);
+  return buf;
+}
+
+enum class Mode { PBS, FIXED, ATC };
+
+struct CSlot : SchedSlotData {
+  int runq_cpu = -1;  // != -1 while on a runq (__vcpu_on_runq)
+  bool active = false;
+  int32_t credit = 0;
+  int64_t start_time = 0;
+  uint16_t flags = 0;
+  int16_t pri = PRI_UNDER;
+  uint64_t prev_pmc[kNumPmc] = {0, 0, 0, 0};
+  struct {
+    int32_t credit_last = 0;
+    uint32_t credit_incr = 0, state_active = 0, state_idle = 0, migrate_q = 0, migrate_r = 0;
+  } stats;
+};
+
+struct CDom : SchedTenantData {
+  std::list<int> active_vcpu;  // slot ids (list_add => push_front)
+  bool on_active = false;
+  uint16_t active_vcpu_count = 0;
+  uint16_t weight = kDefaultWeight;
+  uint16_t cap = 0;
+  AdaptState adapt{};
+  uint64_t pmc[kNumPmc] = {0, 0, 0, 0};  // last per-tenant deltas (sdom->pmc)
+  uint64_t spinlock_latency = 0, spinlock_metric_update = 0, spinlock_count = 0, report_total = 0;
+  uint64_t pending_requests = 0;
+  uint64_t cache_miss_rate = 0, cpi = 0;
+  AtcState atc{};
+};
+
+struct CPcpu : SchedPartData {
+  std::list<int> runq;
+  uint32_t runq_sort_last = 0;
+  int ticker = -1;
+  int metric_ticker = -1;
+  uint32_t tick = 0;
+  int idle_bias = 0;
+};
+
+class CreditScheduler : public Scheduler {
+ public:
+  CreditScheduler(Engine& e, int pool, Mode m) : Scheduler(e, pool), mode_(m) {}
+
+  const char* name() const override {
+    return mode_ == Mode::ATC ? "SMP Credit Scheduler (ATC)"
+                              : (mode_ == Mode::PBS ? "SMP Credit Scheduler (PBS)" : "SMP Credit Scheduler");
+  }
+  const char* opt_name() const override {
+    return mode_ == Mode::ATC ? "atc" : (mode_ == Mode::PBS ? "credit" : "credit-fixed");
+  }
+
+  // ------------------------------------------------------------- init ----
+  int init() override {
+    int ts = E.boot.tslice_us;
+    if (mode_ == Mode::ATC) ts = (int)E.atc_params.default_us;
+    if (ts > GPBS_TSLICE_UMAX || ts < GPBS_TSLICE_UMIN) {
+      E.printk(fmt("WARNING: sched_credit_tslice_us outside of valid range [%d,%d].\n Resetting to default %u\n",
+                   GPBS_TSLICE_UMIN, GPBS_TSLICE_UMAX, 100));
+      ts = 100;
+    }
+    int rl = E.boot.ratelimit_us;
+    if (rl > GPBS_RATELIMIT_MAX || (rl < GPBS_RATELIMIT_MIN && rl != 0)) {
+      E.printk(fmt("WARNING: sched_ratelimit_us outside of valid range [%d,%d].\n Resetting to default %u\n",
+                   GPBS_RATELIMIT_MIN, GPBS_RATELIMIT_MAX, 1000));
+      rl = 1000;
+    }
+    tslice_us_ = (uint32_t)ts;
+    recompute();
+    if (rl > ts) {
+      E.printk("WARNING: sched_ratelimit_us >sched_credit_tslice_us is undefined\nSetting ratelimit_us to tslice\n");
+      ratelimit_us_ = tslice_us_;
+    } else {
+      ratelimit_us_ = (uint32_t)rl;
+    }
+    master_ticker_ = E.timer_init([this](int64_t n) { acct(n); });
+    slice_ticker_ = E.timer_init([this](int64_t n) { dynamic_time_slice(n); });
+    return 0;
+  }
+
+  void deinit() override {
+    E.timer_kill(master_ticker_);
+    E.timer_kill(slice_ticker_);
+    master_ticker_ = slice_ticker_ = -1;
+  }
+
+  void recompute() {
+    ticks_per_tslice_ = 3;
+    if (E.adapt_params.ticks_per_tslice) ticks_per_tslice_ = E.adapt_params.ticks_per_tslice;
+    if (tslice_us_ < ticks_per_tslice_) ticks_per_tslice_ = 1;
+    tick_period_us_ = tslice_us_ / ticks_per_tslice_;
+    credits_per_tslice_ = tslice_us_;  // CSCHED_CREDIT_PER_US * tslice
+    credit_ = ncpus_ * credits_per_tslice_;
+  }
+
+  CPcpu& pc(int cpu) { return *static_cast<CPcpu*>(E.parts[cpu]->priv.get()); }
+  CSlot& sv(Slot& v) { return *static_cast<CSlot*>(v.priv.get()); }
+  CSlot& sv(int id) { return sv(*E.slots[id]); }
+  CDom& sd(Tenant& d) { return *static_cast<CDom*>(d.priv.get()); }
+  CDom& sd_of(Slot& v) { return sd(*E.tenants[v.tenant]); }
+  Slot& curr(int cpu) { return E.curr_of(cpu); }
+  Mask online() { return E.pools[pool_]->cpus; }
+
+  void alloc_pdata(int cpu) override {
+    auto p = std::make_unique<CPcpu>();
+    credit_ += credits_per_tslice_;
+    ncpus_++;
+    cpus_.set(cpu);
+    const int64_t n = E.now();
+    if (ncpus_ == 1) {
+      master_ = cpu;
+      E.timer_set(master_ticker_, n + (int64_t)tslice_us_ * 1000);
+      E.timer_set(slice_ticker_, n + (int64_t)slice_period_us() * 1000);
+    }
+    p->ticker = E.timer_init([this, cpu](int64_t t) { tick(cpu, t); });
+    p->metric_ticker = E.timer_init([this, cpu](int64_t t) { metric_tick(cpu, t); });
+    E.timer_set(p->ticker, n + std::max<int64_t>(1, tick_period_us_) * 1000);
+    E.timer_set(p->metric_ticker, n + (int64_t)E.boot.metric_period_us * 1000);
+    p->runq_sort_last = runq_sort_;
+    p->idle_bias = kMaxPartitions - 1;
+    E.parts[cpu]->priv = std::move(p);
+    idlers_.set(cpu);
+  }
+
+  void free_pdata(int cpu) override {
+    CPcpu& p = pc(cpu);
+    credit_ -= credits_per_tslice_;
+    ncpus_--;
+    idlers_.clear(cpu);
+    cpus_.clear(cpu);
+    if (master_ == cpu && ncpus_ > 0) master_ = cpus_.first();  // migrate_timer(master/slice)
+    E.timer_kill(p.ticker);
+    E.timer_kill(p.metric_ticker);
+    if (ncpus_ == 0) {
+      E.timer_stop(master_ticker_);
+      E.timer_stop(slice_ticker_);
+    }
+    for (int sid : p.runq) sv(sid).runq_cpu = -1;
+    E.parts[cpu]->priv.reset();
+  }
+
+  int init_domain(Tenant& d) override {
+    auto s = std::make_unique<CDom>();
+    adapt_init(s->adapt, E.adapt_params, mode_ == Mode::FIXED ? tslice_us_ : 100);
+    atc_init(s->atc, E.atc_params);
+    d.priv = std::move(s);
+    return 0;
+  }
+  void destroy_domain(Tenant& d) override { d.priv.reset(); }
+
+  void alloc_vdata(Slot& v) override {
+    auto s = std::make_unique<CSlot>();
+    s->pri = v.is_idle() ? PRI_IDLE : PRI_UNDER;
+    v.priv = std::move(s);
+  }
+
+  void insert_vcpu(Slot& v) override {
+    CSlot& s = sv(v);
+    if (s.runq_cpu < 0 && E.runnable(v) && !v.is_running) runq_insert(v.processor, v);
+  }
+
+  void remove_vcpu(Slot& v) override {
+    CSlot& s = sv(v);
+    if (s.runq_cpu >= 0) runq_remove(v);
+    if (s.active) acct_stop_locked(v);
+  }
+
+  // ------------------------------------------------------------ runq ----
+  void runq_insert(int cpu, Slot& v) {
+    CSlot& s = sv(v);
+    auto& rq = pc(cpu).runq;
+    auto it = rq.begin();
+    for (; it != rq.end(); ++it)
+      if (s.pri > sv(*it).pri) break;
+    // A yielding slot goes behind one lower-priority runnable slot.
+    if ((s.flags & FLAG_YIELD) && it != rq.end() && sv(*it).pri > PRI_IDLE) ++it;
+    rq.insert(it, v.id);
+    s.runq_cpu = cpu;
+  }
+
+  void runq_remove(Slot& v) {
+    CSlot& s = sv(v);
+    pc(s.runq_cpu).runq.remove(v.id);
+    s.runq_cpu = -1;
+  }
+
+  void burn_credits(Slot& v, int64_t now) {
+    CSlot& s = sv(v);
+    int64_t delta = now - s.start_time;
+    if (delta <= 0) return;
+    // credits = round(delta[ns] * 1000/ms) -> 1 credit per us
+    uint32_t credits = (uint32_t)((delta * 1000 + 500000) / 1000000);
+    s.credit -= (int32_t)credits;
+    s.start_time += (int64_t)credits * 1000000 / 1000;
+  }
+
+  void tickle(int cpu, Slot& nw) {
+    Slot& cur = curr(cpu);
+    CSlot& cs = sv(cur);
+    CSlot& ns = sv(nw);
+    Mask mask;
+    if (ns.pri > cs.pri) {
+      if (cs.pri == PRI_IDLE)
+        E.perfc.incr(PC_tickle_local_idler);
+      else if (cs.pri == PRI_OVER)
+        E.perfc.incr(PC_tickle_local_over);
+      else if (cs.pri == PRI_UNDER)
+        E.perfc.incr(PC_tickle_local_under);
+      else
+        E.perfc.incr(PC_tickle_local_other);
+      mask.set(cpu);
+    }
+    if (cs.pri > PRI_IDLE) {
+      if (idlers_.empty()) {
+        E.perfc.incr(PC_tickle_idlers_none);
+      } else {
+        Mask idle_mask = idlers_ & nw.affinity & online();
+        if (!idle_mask.empty()) {
+          E.perfc.incr(PC_tickle_idlers_some);
+          if (E.boot.tickle_one_idle) {
+            last_tickle_cpu_ = idle_mask.cycle(last_tickle_cpu_);
+            mask.set(last_tickle_cpu_);
+          } else {
+            mask = mask | idle_mask;
+          }
+        }
+        mask = mask & nw.affinity;
+      }
+    }
+    for (int c = mask.first(); c >= 0; c = mask.next(c + 1)) E.raise_softirq(c);
+  }
+
+  // --------------------------------------------------------- cpu pick ----
+  Mask sibling_mask(int cpu) {  // partitions sharing an XCD (SMT-sibling analog)
+    Mask m;
+    const Partition& P = *E.parts[cpu];
+    for (int c = cpus_.first(); c >= 0; c = cpus_.next(c + 1))
+      if (E.parts[c]->gpu == P.gpu && E.parts[c]->xcd == P.xcd) m.set(c);
+    m.set(cpu);
+    return m;
+  }
+  Mask core_mask(int cpu) {  // partitions on the same GPU (socket analog)
+    Mask m;
+    const Partition& P = *E.parts[cpu];
+    for (int c = cpus_.first(); c >= 0; c = cpus_.next(c + 1))
+      if (E.parts[c]->gpu == P.gpu) m.set(c);
+    m.set(cpu);
+    return m;
+  }
+
+  int cpu_pick(Slot& v, bool commit) {
+    Mask cpus = online() & v.affinity;
+    if (cpus.empty()) cpus = online();
+    if (cpus.empty()) return v.processor;
+    int cpu = cpus.test(v.processor) ? v.processor : cpus.cycle(v.processor);
+    Mask idlers = idlers_;
+    idlers.set(cpu);
+    cpus = cpus & idlers;
+    cpus.clear(cpu);
+    CPcpu* spc = nullptr;
+    while (!cpus.empty()) {
+      int nxt = cpus.cycle(cpu);
+      Mask cpu_idlers, nxt_idlers;
+      int factor;
+      if (E.parts[cpu]->gpu == E.parts[nxt]->gpu) {
+        factor = 1;
+        cpu_idlers = idlers & sibling_mask(cpu);
+        nxt_idlers = idlers & sibling_mask(nxt);
+      } else {
+        factor = 2;  // migrate across GPUs only if twice as idle
+        cpu_idlers = idlers & core_mask(cpu);
+        nxt_idlers = idlers & core_mask(nxt);
+      }
+      int wc = cpu_idlers.weight(), wn = nxt_idlers.weight();
+      if (E.boot.smt_power_savings ? wc > wn : wc * factor < wn) {
+        nxt_idlers = cpus & nxt_idlers;
+        spc = &pc(nxt);
+        cpu = nxt_idlers.cycle(spc->idle_bias);
+        cpus = cpus.andnot(sibling_mask(cpu));
+      } else {
+        cpus = cpus.andnot(nxt_idlers);
+      }
+    }
+    if (commit && spc) spc->idle_bias = cpu;
+    return cpu;
+  }
+  int pick_cpu(Slot& v) override { return cpu_pick(v, true); }
+
+  // ------------------------------------------------------- accounting ----
+  void acct_start(Slot& v) {
+    CSlot& s = sv(v);
+    CDom& d = sd_of(v);
+    if (!s.active) {
+      s.stats.state_active++;
+      E.perfc.incr(PC_acct_vcpu_active);
+      d.active_vcpu_count++;
+      d.active_vcpu.push_front(v.id);
+      s.active = true;
+      weight_ += d.weight;
+      if (!d.on_active) {
+        active_sdom_.push_front(v.tenant);
+        d.on_active = true;
+      }
+    }
+  }
+
+  void acct_stop_locked(Slot& v) {
+    CSlot& s = sv(v);
+    CDom& d = sd_of(v);
+    s.stats.state_idle++;
+    E.perfc.incr(PC_acct_vcpu_idle);
+    d.active_vcpu_count--;
+    d.active_vcpu.remove(v.id);
+    s.active = false;
+    weight_ -= d.weight;
+    if (d.active_vcpu.empty()) {
+      active_sdom_.remove(v.tenant);
+      d.on_active = false;
+    }
+  }
+
+  void vcpu_acct(int cpu, int64_t now) {
+    Slot& v = curr(cpu);
+    CSlot& s = sv(v);
+    if (s.pri == PRI_BOOST) s.pri = PRI_UNDER;
+    if (!v.is_idle()) burn_credits(v, now);
+    if (!s.active) {
+      acct_start(v);
+    } else if (cpu_pick(v, false) != cpu) {
+      s.stats.migrate_r++;
+      E.perfc.incr(PC_migrate_running);
+      v.pause_flags |= VPF_MIGRATING;
+      E.raise_softirq(cpu);
+    }
+  }
+
+  void acct(int64_t now) {
+    uint64_t weight_total = weight_;
+    uint64_t credit_total = credit_;
+    if (credit_balance_ < 0) {
+      credit_total += (uint64_t)(-credit_balance_);
+      E.perfc.incr(PC_acct_balance);
+    }
+    if (weight_total == 0) {
+      credit_balance_ = 0;
+      E.perfc.incr(PC_acct_no_work);
+      E.timer_set(master_ticker_, now + (int64_t)tslice_us_ * 1000);
+      return;
+    }
+    E.perfc.incr(PC_acct_run);
+    uint64_t weight_left = weight_total;
+    int64_t credit_balance = 0;
+    bool credit_xtra = false;
+    uint64_t credit_cap = 0;
+    const uint64_t cpt = credits_per_tslice_;
+
+    std::vector<int> doms(active_sdom_.begin(), active_sdom_.end());
+    for (int tid : doms) {
+      Tenant& dom = *E.tenants[tid];
+      CDom& d = sd(dom);
+      if (!d.on_active) continue;
+      const uint64_t n = d.active_vcpu_count;
+      const uint64_t w = d.weight;
+      weight_left -= w * n;
+      uint64_t credit_peak = n * cpt;
+      if (credit_balance_ < 0) credit_peak += ((uint64_t)(-credit_balance_) * w * n + (weight_total - 1)) / weight_total;
+      if (d.cap != 0) {
+        credit_cap = ((uint64_t)d.cap * cpt + 99) / 100;
+        if (credit_cap < credit_peak) credit_peak = credit_cap;
+        credit_cap = (credit_cap + (n - 1)) / n;
+      }
+      uint64_t credit_fair = (credit_total * w * n + (weight_total - 1)) / weight_total;
+      if (credit_fair < credit_peak) {
+        credit_xtra = true;
+      } else {
+        if (weight_left != 0)  // give other domains a chance at unused credits
+          credit_total += ((credit_fair - credit_peak) * weight_total + (weight_left - 1)) / weight_left;
+        if (credit_xtra) {
+          E.perfc.incr(PC_acct_reorder);
+          active_sdom_.remove(tid);
+          active_sdom_.push_front(tid);
+        }
+        credit_fair = credit_peak;
+      }
+      credit_fair = (credit_fair + (n - 1)) / n;  // per slot
+
+      std::vector<int> vs(d.active_vcpu.begin(), d.active_vcpu.end());
+      for (int sid : vs) {
+        Slot& v = *E.slots[sid];
+        CSlot& s = sv(v);
+        s.credit += (int32_t)credit_fair;
+        int32_t credit = s.credit;
+        if (credit < 0) {
+          s.pri = PRI_OVER;
+          // Park running slots of capped-out tenants (launch gate closes).
+          if (d.cap != 0 && credit < -(int32_t)credit_cap && !(s.flags & FLAG_PARKED)) {
+            E.perfc.incr(PC_vcpu_park);
+            E.vcpu_pause(v);
+            s.flags |= FLAG_PARKED;
+            E.emit(TRC_PARK, v.processor, v.tenant, v.index, 1);
+            if (E.actuator_ops.on_park) E.actuator_ops.on_park(E.actuator_ops.user, v.tenant, v.index, 1);
+          }
+          if (credit < -(int32_t)cpt) {  // lower bound
+            E.perfc.incr(PC_acct_min_credit);
+            credit = -(int32_t)cpt;
+            s.credit = credit;
+          }
+        } else {
+          s.pri = PRI_UNDER;
+          if (s.flags & FLAG_PARKED) {
+            E.perfc.incr(PC_vcpu_unpark);
+            E.vcpu_unpause(v);
+            s.flags &= ~FLAG_PARKED;
+            E.emit(TRC_PARK, v.processor, v.tenant, v.index, 0);
+            if (E.actuator_ops.on_park) E.actuator_ops.on_park(E.actuator_ops.user, v.tenant, v.index, 0);
+          }
+          if (E.boot.dom0_quirk) {
+            // P1g (:1486-1500): ceiling compared at /100 granularity; tenant 0
+            // (the control tenant) leaves the active list only with >=2 active
+            // slots and keeps its credit; others halve and stay active.
+            if (credit / 100 > (int32_t)cpt / 100 && tid == 0) {
+              if (d.active_vcpu_count >= 2) acct_stop_locked(v);
+              s.credit = credit;
+            } else if (credit / 100 > (int32_t)cpt / 100 && tid != 0) {
+              credit /= 2;
+              s.credit = credit;
+            }
+          } else if (credit > (int32_t)cpt) {  // upstream: stop earning, halve
+            acct_stop_locked(v);
+            credit /= 2;
+            s.credit = credit;
+          }
+        }
+        s.stats.credit_last = credit;
+        s.stats.credit_incr = (uint32_t)credit_fair;
+        credit_balance += credit;
+      }
+    }
+    credit_balance_ = (int32_t)credit_balance;
+    runq_sort_++;
+    E.emit(TRC_ACCT, master_, (uint32_t)pool_, (uint32_t)weight_total, (uint32_t)credit_total,
+           (uint32_t)credit_balance_);
+    E.timer_set(master_ticker_, now + (int64_t)tslice_us_ * 1000);
+  }
+
+  void runq_sort(int cpu) {
+    CPcpu& p = pc(cpu);
+    if (p.runq_sort_last == runq_sort_) return;
+    p.runq_sort_last = runq_sort_;
+    std::stable_partition(p.runq.begin(), p.runq.end(), [this](int sid) { return sv(sid).pri >= PRI_UNDER; });
+  }
+
+  void tick(int cpu, int64_t now) {
+    CPcpu& p = pc(cpu);
+    p.tick++;
+    Slot& c = curr(cpu);
+    if (!c.is_idle()) vcpu_acct(cpu, now);
+    if ((int)tslice_us_ > E.boot.pmu_refresh_us) E.pmu_refresh(curr(cpu));
+    runq_sort(cpu);
+    Slot& c2 = curr(cpu);
+    uint32_t period = tick_period_us_;
+    if (!c2.is_idle() && mode_ == Mode::PBS) period = sd_of(c2).adapt.tick_period_us;
+    E.timer_set(p.ticker, now + (int64_t)std::max<uint32_t>(1, period) * 1000);
+  }
+
+  // ---------------------------------------------------- PBS metric loop --
+  void metric_tick(int cpu, int64_t now) {
+    CPcpu& p = pc(cpu);
+    if ((int)tslice_us_ <= E.boot.pmu_refresh_us) E.pmu_refresh(curr(cpu));
+    if (cpu == master_) dom_metric_update(now);
+    E.timer_set(p.metric_ticker, now + (int64_t)E.boot.metric_period_us * 1000);
+  }
+
+  void dom_metric_update(int64_t now) {
+    E.perfc.incr(PC_metric_tick);
+    std::vector<int> ids;
+    for (auto& t : E.tenants)
+      if (t && t->alive && t->pool == pool_ && t->priv) ids.push_back(t->id);
+    if (ids.empty()) return;
+    const size_t n = ids.size();
+    std::vector<uint64_t> deltas(4 * n, 0), ssum(n), scnt(n);
+    bool have = false;
+    if (E.counter_ops.tenant_deltas) {
+      have = E.counter_ops.tenant_deltas(E.counter_ops.user, (int)n, ids.data(), deltas.data()) == 0;
+      if (!have) E.perfc.incr(PC_counter_stale);
+    }
+    for (size_t k = 0; k < n; ++k) {
+      Tenant& dom = *E.tenants[ids[k]];
+      CDom& d = sd(dom);
+      d.pending_requests = dom.pending_requests;  // P7
+      dom.pending_requests = 0;
+      if (!have) {
+        for (int sid : dom.slots) {
+          Slot& v = *E.slots[sid];
+          CSlot& s = sv(v);
+          for (int i = 0; i < kNumPmc; ++i) {
+            if (v.pmc[i] < s.prev_pmc[i]) {  // Q5: counter reset -> skip sample
+              E.perfc.incr(PC_counter_reset);
+            } else {
+              deltas[4 * k + i] += v.pmc[i] - s.prev_pmc[i];
+            }
+            s.prev_pmc[i] = v.pmc[i];
+          }
+        }
+      }
+      for (int i = 0; i < kNumPmc; ++i) d.pmc[i] = deltas[4 * k + i];
+      ssum[k] = d.spinlock_metric_update;
+      scnt[k] = d.spinlock_count;
+    }
+    if (mode_ == Mode::PBS) {
+      std::vector<AdaptState> before(n);
+      for (size_t k = 0; k < n; ++k) before[k] = sd(*E.tenants[ids[k]]).adapt;
+      bool dev = false;
+      if (E.counter_ops.adapt_batch) {
+        std::vector<gpbs_adapt_state_t> st(n);
+        for (size_t k = 0; k < n; ++k) std::memcpy(&st[k], &before[k], sizeof(AdaptState));
+        dev = E.counter_ops.adapt_batch(E.counter_ops.user, (int)n, ids.data(), deltas.data(), ssum.data(), scnt.data(),
+                                        st.data(), reinterpret_cast<const gpbs_adapt_params_t*>(&E.adapt_params)) == 0;
+        if (dev)
+          for (size_t k = 0; k < n; ++k) std::memcpy(&sd(*E.tenants[ids[k]]).adapt, &st[k], sizeof(AdaptState));
+      }
+      for (size_t k = 0; k < n; ++k) {
+        CDom& d = sd(*E.tenants[ids[k]]);
+        bool rearm = false;
+        int dir;
+        if (!dev) {
+          dir = adapt_update(d.adapt, E.adapt_params, deltas[4 * k + 0], deltas[4 * k + 3], ssum[k], scnt[k], &rearm);
+        } else {
+          dir = d.adapt.tslice_us > before[k].tslice_us ? 1 : (d.adapt.tslice_us < before[k].tslice_us ? -1 : 0);
+          rearm = d.adapt.window_left == kWindow - 1 && before[k].window_left == 0;
+        }
+        if (dir > 0) E.perfc.incr(PC_adapt_inc);
+        if (dir < 0) E.perfc.incr(PC_adapt_dec);
+        if (rearm) E.perfc.incr(PC_adapt_rearm);
+        if (dir || rearm)
+          E.emit(TRC_ADAPT, master_, (uint32_t)ids[k], before[k].tslice_us, d.adapt.tslice_us,
+                 (d.adapt.phase << 24) | ((uint32_t)d.adapt.last_err & 0xffffff));
+      }
+    }
+    for (size_t k = 0; k < n; ++k) {
+      CDom& d = sd(*E.tenants[ids[k]]);
+      const uint64_t inst = d.pmc[0], cyc = d.pmc[1], miss = d.pmc[3];
+      d.cache_miss_rate = inst ? miss * 100000 / inst : 0;  // Q3 fix: per tenant
+      d.cpi = inst ? cyc * 1000 / inst : 0;
+      E.emit(TRC_METRIC, master_, (uint32_t)ids[k], (uint32_t)inst, (uint32_t)miss, (uint32_t)d.cache_miss_rate);
+      d.spinlock_metric_update = 0;
+      d.spinlock_count = 0;
+    }
+  }
+
+  void dynamic_time_slice(int64_t now) {
+    if (mode_ == Mode::ATC) update_acct_atc();
+    E.timer_set(slice_ticker_, now + (int64_t)slice_period_us() * 1000);
+  }
+  uint32_t slice_period_us() const {
+    return mode_ == Mode::ATC ? E.atc_params.apply_period_us : (uint32_t)E.boot.slice_apply_us;
+  }
+
+  void update_acct_atc() {
+    uint32_t mn = 30000 * 10;
+    std::vector<int> doms(active_sdom_.begin(), active_sdom_.end());
+    for (int tid : doms) {
+      CDom& d = sd(*E.tenants[tid]);
+      atc_update(d.atc, E.atc_params);
+      mn = std::min(mn, d.atc.tslice_us);
+    }
+    if (doms.empty()) return;
+    for (int tid : doms) {
+      CDom& d = sd(*E.tenants[tid]);
+      d.atc.tslice_us = mn;
+      d.atc.hist[3].tslice = mn;
+    }
+    tslice_us_ = mn;
+    recompute();
+    E.perfc.incr(PC_atc_apply);
+    E.emit(TRC_ATC, master_, mn, (uint32_t)doms.size());
+  }
+
+  // ----------------------------------------------------- wake / sleep ----
+  void sleep(Slot& v) override {
+    E.perfc.incr(PC_vcpu_sleep);
+    if (E.parts[v.processor]->curr == v.id)
+      E.raise_softirq(v.processor);
+    else if (sv(v).runq_cpu >= 0)
+      runq_remove(v);
+  }
+
+  void wake(Slot& v) override {
+    CSlot& s = sv(v);
+    if (E.parts[v.processor]->curr == v.id) {
+      E.perfc.incr(PC_vcpu_wake_running);
+      return;
+    }
+    if (s.runq_cpu >= 0) {
+      E.perfc.incr(PC_vcpu_wake_onrunq);
+      return;
+    }
+    E.perfc.incr(E.runnable(v) ? PC_vcpu_wake_runnable : PC_vcpu_wake_not_runnable);
+    if (s.pri == PRI_UNDER && !(s.flags & FLAG_PARKED)) s.pri = PRI_BOOST;  // wake-boost
+    runq_insert(v.processor, v);
+    tickle(v.processor, v);
+  }
+
+  void yield(Slot& v) override {
+    if (!E.boot.default_yield) sv(v).flags |= FLAG_YIELD;
+  }
+
+  void report(Tenant& d, uint64_t wait, int) override {
+    CDom& s = sd(d);
+    if (mode_ == Mode::ATC) {
+      atc_report(s.atc, E.atc_params, wait);
+    } else {  // do_vcrd_op (:249-259)
+      s.spinlock_latency += wait;
+      s.spinlock_metric_update += wait;
+      s.spinlock_count++;
+    }
+    s.report_total++;
+  }
+
+  // -------------------------------------------------------- dispatch ----
+  Slot* runq_steal(int peer, int cpu, int pri) {
+    Slot& peer_cur = curr(peer);
+    if (E.parts[peer]->priv && !peer_cur.is_idle()) {
+      auto& rq = pc(peer).runq;
+      for (int sid : rq) {
+        Slot& v = *E.slots[sid];
+        CSlot& s = sv(v);
+        if (s.pri <= pri) break;
+        if (v.is_idle()) continue;
+        bool hot = (E.now() - v.last_run_time) < (int64_t)E.boot.migration_delay_us * 1000;
+        if (hot) E.perfc.incr(PC_vcpu_hot);
+        if (!v.is_running && !hot && v.affinity.test(cpu)) {
+          s.stats.migrate_q++;
+          E.perfc.incr(PC_migrate_queued);
+          runq_remove(v);
+          int from = v.processor;
+          v.processor = cpu;
+          E.emit(TRC_STEAL, cpu, v.tenant, v.index, from, cpu);
+          return &v;
+        }
+      }
+    }
+    E.perfc.incr(PC_steal_peer_idle);
+    return nullptr;
+  }
+
+  Slot& load_balance(int cpu, Slot& snext, bool* stolen) {
+    CSlot& s = sv(snext);
+    if (s.pri == PRI_IDLE)
+      E.perfc.incr(PC_load_balance_idle);
+    else if (s.pri == PRI_OVER)
+      E.perfc.incr(PC_load_balance_over);
+    else
+      E.perfc.incr(PC_load_balance_other);
+    Mask workers = online().andnot(idlers_);
+    workers.clear(cpu);
+    int peer = cpu;
+    while (!workers.empty()) {
+      peer = workers.cycle(peer);
+      workers.clear(peer);
+      // Single-dispatcher design: the peer's runqueue is always lockable.
+      Slot* sp = runq_steal(peer, cpu, s.pri);
+      if (sp) {
+        *stolen = true;
+        return *sp;
+      }
+    }
+    runq_remove(snext);
+    return snext;
+  }
+
+  TaskSlice do_schedule(int cpu, int64_t now) override {
+    Slot& scurr = curr(cpu);
+    CSlot& cs = sv(scurr);
+    E.perfc.incr(PC_schedule);
+    int64_t runtime = now - scurr.rs_entry;
+    if (runtime < 0) runtime = 0;
+    if (!scurr.is_idle()) {
+      burn_credits(scurr, now);
+      cs.start_time -= now;
+    } else {
+      cs.pri = PRI_IDLE;
+    }
+    Slot* snext = nullptr;
+    TaskSlice ret{0, 0, false};
+    int64_t tslice;
+    if (ratelimit_us_ && E.runnable(scurr) && !scurr.is_idle() && runtime < (int64_t)ratelimit_us_ * 1000) {
+      snext = &scurr;
+      cs.start_time += now;
+      E.perfc.incr(PC_delay_ms);
+      E.perfc.incr(PC_ratelimit_hold);
+      tslice = (int64_t)ratelimit_us_ * 1000;
+    } else {
+      tslice = (int64_t)tslice_us_ * 1000;
+      if (E.runnable(scurr)) runq_insert(cpu, scurr);
+      auto& rq = pc(cpu).runq;
+      snext = E.slots[rq.front()].get();
+      if (cs.flags & FLAG_YIELD) cs.flags &= ~FLAG_YIELD;
+      if (sv(*snext).pri > PRI_OVER)
+        runq_remove(*snext);
+      else
+        snext = &load_balance(cpu, *snext, &ret.migrated);
+      if (sv(*snext).pri == PRI_IDLE)
+        idlers_.set(cpu);
+      else
+        idlers_.clear(cpu);
+      if (!snext->is_idle()) sv(*snext).start_time += now;
+    }
+    // PBS (:1796-1804): the quantum is the next tenant's private tslice.
+    if (!snext->is_idle()) {
+      if (mode_ == Mode::PBS)
+        tslice = (int64_t)sd_of(*snext).adapt.tslice_us * 1000;
+      else if (mode_ == Mode::ATC)
+        tslice = (int64_t)tslice_us_ * 1000;  // global slice (atc :1916)
+    } else {
+      tslice = (int64_t)tslice_us_ * 1000;
+    }
+    ret.time_ns = snext->is_idle() ? -1 : tslice;
+    ret.slot = snext->id;
+    return ret;
+  }
+
+  // --------------------------------------------------------- control ----
+  int adjust(Tenant& dom, bool set, int* weight, int* cap) override {
+    CDom& d = sd(dom);
+    if (!set) {
+      *weight = d.weight;
+      *cap = d.cap;
+      return 0;
+    }
+    if (*weight != -1 && *weight != 0) {
+      if (*weight < 1 || *weight > GPBS_WEIGHT_MAX) return GPBS_ERANGE;
+      if (d.on_active) {
+        weight_ -= (uint32_t)d.weight * d.active_vcpu_count;
+        weight_ += (uint32_t)*weight * d.active_vcpu_count;
+      }
+      d.weight = (uint16_t)*weight;
+    }
+    if (*cap != -1) {
+      if (*cap < 0 || *cap > 100 * (int)dom.slots.size()) return GPBS_ERANGE;
+      d.cap = (uint16_t)*cap;
+    }
+    return 0;
+  }
+
+  int adjust_global(bool set, int* tslice_us, int* ratelimit_us) override {
+    if (set) {
+      if (*tslice_us > GPBS_TSLICE_UMAX || *tslice_us < GPBS_TSLICE_UMIN || *ratelimit_us > GPBS_RATELIMIT_MAX ||
+          (*ratelimit_us < GPBS_RATELIMIT_MIN && *ratelimit_us != 0) || *ratelimit_us > *tslice_us)
+        return GPBS_EINVAL;
+      tslice_us_ = (uint32_t)*tslice_us;
+      ratelimit_us_ = (uint32_t)*ratelimit_us;
+      recompute();  // Q2 fix
+      if (mode_ == Mode::FIXED)
+        for (auto& t : E.tenants)
+          if (t && t->alive && t->pool == pool_ && t->priv) {
+            sd(*t).adapt.tslice_us = tslice_us_;
+            sd(*t).adapt.tick_period_us = tick_period_us_;
+          }
+    }
+    *tslice_us = (int)tslice_us_;
+    *ratelimit_us = (int)ratelimit_us_;
+    return 0;
+  }
+
+  bool tenant_adapt(Tenant& d, AdaptState* out) override {
+    *out = sd(d).adapt;
+    return true;
+  }
+  bool set_tenant_adapt(Tenant& d, const AdaptState& st) override {
+    sd(d).adapt = st;
+    return true;
+  }
+
+  void fill_tenant_info(Tenant& dom, gpbs_tenant_info_t& o) override {
+    CDom& d = sd(dom);
+    o.weight = d.weight;
+    o.cap = d.cap;
+    o.active_slots = d.active_vcpu_count;
+    o.tslice_us = mode_ == Mode::PBS ? d.adapt.tslice_us : (mode_ == Mode::ATC ? tslice_us_ : tslice_us_);
+    o.tick_period_us = mode_ == Mode::PBS ? d.adapt.tick_period_us : tick_period_us_;
+    o.phase = d.adapt.phase;
+    o.window_left = d.adapt.window_left;
+    o.last_err = d.adapt.last_err;
+    o.last_curr = d.adapt.last_curr;
+    o.last_win = d.adapt.last_win;
+    for (int i = 0; i < 4; ++i) o.pmc[i] = d.pmc[i];
+    o.cache_miss_rate = d.cache_miss_rate;
+    o.cpi = d.cpi;
+    o.spin_latency = d.spinlock_latency;
+    o.report_count = d.report_total;
+    o.pending_requests = d.pending_requests;
+  }
+
+  void fill_slot_info(Slot& v, gpbs_slot_info_t& o) override {
+    CSlot& s = sv(v);
+    o.pri = s.pri;
+    o.flags = s.flags;
+    o.credit = s.credit;
+    o.on_runq = s.runq_cpu >= 0;
+  }
+
+  // ------------------------------------------------------------ dumps ----
+  void dump_vcpu(Slot& v, std::string& o) {
+    CSlot& s = sv(v);
+    o += fmt("[%d.%d] pri=%d flags=%x cpu=%d", v.tenant, v.index, s.pri, s.flags, v.processor);
+    if (!v.is_idle()) {
+      o += fmt(" credit=%d [w=%u]", s.credit, sd_of(v).weight);
+      o += fmt(" (%d+%u) {a/i=%u/%u m=%u+%u}", s.stats.credit_last, s.stats.credit_incr, s.stats.state_active,
+               s.stats.state_idle, s.stats.migrate_q, s.stats.migrate_r);
+    }
+    o += "\n";
+  }
+
+  void dump_cpu_state(int cpu, std::string& o) override {
+    CPcpu& p = pc(cpu);
+    o += fmt(" sort=%u, sibling=%s, ", p.runq_sort_last, sibling_mask(cpu).str().c_str());
+    o += fmt("core=%s\n", core_mask(cpu).str().c_str());
+    o += "\trun: ";
+    dump_vcpu(curr(cpu), o);
+    int loop = 0;
+    for (int sid : p.runq) {
+      o += fmt("\t%3d: ", ++loop);
+      dump_vcpu(*E.slots[sid], o);
+    }
+  }
+
+  void dump_settings(std::string& o) override {
+    o += fmt(
+        "info:\n\tncpus              = %u\n\tmaster             = %d\n\tcredit             = %u\n"
+        "\tcredit balance     = %d\n\tweight             = %u\n\trunq_sort          = %u\n"
+        "\tdefault-weight     = %d\n\ttslice             = %uus\n\tratelimit          = %uus\n"
+        "\tcredits per msec   = %d\n\tticks per tslice   = %u\n\tmigration delay    = %uus\n",
+        ncpus_, master_, credit_, credit_balance_, weight_, runq_sort_, kDefaultWeight, tslice_us_, ratelimit_us_,
+        1000, ticks_per_tslice_, (unsigned)E.boot.migration_delay_us);
+    o += fmt("idlers: %s\n", idlers_.str().c_str());
+    o += "active vcpus:\n";
+    int loop = 0;
+    for (int tid : active_sdom_)
+      for (int sid : sd(*E.tenants[tid]).active_vcpu) {
+        o += fmt("\t%3d: ", ++loop);
+        dump_vcpu(*E.slots[sid], o);
+      }
+    o += "\n";
+  }
+
+  void dump_admin_conf(std::string& o) override {
+    // csched_dump_customized (:1942-1974): cpus + per-slot pmuinfo/sched_count,
+    // plus the live PBS state (quantum, phase, miss rate) per tenant.
+    o += fmt("cpus: %s\n", cpus_.str().c_str());
+    for (auto& t : E.tenants) {
+      if (!t || !t->alive || t->pool != pool_ || !t->priv) continue;
+      CDom& d = sd(*t);
+      o += fmt("dom%d    (%s) tslice=%uus tick=%uus phase=%s miss_rate=%" PRIu64 " cpi=%" PRIu64
+               " window_left=%u reports=%" PRIu64 "\n",
+               t->id, t->name.c_str(), mode_ == Mode::PBS ? d.adapt.tslice_us : tslice_us_,
+               mode_ == Mode::PBS ? d.adapt.tick_period_us : tick_period_us_,
+               d.adapt.phase == kPhaseLow ? "LOW(cache-sensitive)" : "HIGH", d.cache_miss_rate, d.cpi,
+               d.adapt.window_left, d.report_total);
+      for (int sid : t->slots) {
+        Slot& v = *E.slots[sid];
+        o += fmt("    vcpu%d: \n", v.index);
+        o += fmt("        pmuinfo: INST_RETIRED=%" PRIu64 "  CPU_CLK_UNHALTED=%" PRIu64 "  LLC_REFERENCES=%" PRIu64
+                 "  LLC_MISSES=%" PRIu64 "\n",
+                 v.pmc[0], v.pmc[1], v.pmc[2], v.pmc[3]);
+        o += fmt("        sched_count: %" PRIu64 "\n", v.sched_count);
+      }
+    }
+    o += "\n";
+  }
+
+  std::string check() override {
+    std::string err;
+    uint64_t w = 0;
+    for (int tid : active_sdom_) {
+      CDom& d = sd(*E.tenants[tid]);
+      if (d.active_vcpu_count != d.active_vcpu.size()) err += fmt("dom%d active count mismatch\n", tid);
+      w += (uint64_t)d.weight * d.active_vcpu_count;
+    }
+    if (w != weight_) err += fmt("pool%d weight %u != sum %" PRIu64 "\n", pool_, weight_, w);
+    for (int c = cpus_.first(); c >= 0; c = cpus_.next(c + 1)) {
+      for (int sid : pc(c).runq) {
+        Slot& v = *E.slots[sid];
+        if (sv(v).runq_cpu != c) err += fmt("slot %d on runq %d but marks %d\n", sid, c, sv(v).runq_cpu);
+        if (v.processor != c) err += fmt("slot %d on runq %d but processor %d\n", sid, c, v.processor);
+        if (v.is_running) err += fmt("slot %d running and queued\n", sid);
+      }
+    }
+    return err;
+  }
+
+ private:
+  Mode mode_;
+  std::list<int> active_sdom_;
+  uint32_t ncpus_ = 0;
+  int master_ = -1;
+  int master_ticker_ = -1, slice_ticker_ = -1;
+  Mask idlers_, cpus_;
+  uint32_t weight_ = 0, credit_ = 0;
+  int32_t credit_balance_ = 0;
+  uint32_t runq_sort_ = 0;
+  uint32_t ratelimit_us_ = 0, tslice_us_ = 0, tick_period_us_ = 0, ticks_per_tslice_ = 3, credits_per_tslice_ = 0;
+  int last_tickle_cpu_ = 0;
+};
+
+}  // namespace
+
+std::unique_ptr<Scheduler> make_static_scheduler(Engine& e, int pool);
+
+std::unique_ptr<Scheduler> make_scheduler(const std::string& name, Engine& e, int pool) {
+  if (name == "credit" || name == "pbs") return std::make_unique<CreditScheduler>(e, pool, Mode::PBS);
+  if (name == "credit-fixed") return std::make_unique<CreditScheduler>(e, pool, Mode::FIXED);
+  if (name == "atc") return std::make_unique<CreditScheduler>(e, pool, Mode::ATC);
+  if (name == "static") return make_static_scheduler(e, pool);
+  return nullptr;
+}
+
+}  // namespace gpbs

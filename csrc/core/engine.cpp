@@ -1,0 +1,756 @@
+// Generic scheduling framework.  Behavior parity references:
+//   schedule()            X:xen/common/schedule.c:1082-1185
+//   vcpu_wake/sleep       X:xen/common/schedule.c:331-380
+//   vcpu_migrate          X:xen/common/schedule.c:404-470
+//   context_saved         X:xen/common/schedule.c:1187-1201
+//   cpupool ops           X:xen/common/cpupool.c:118-453
+//   keyhandlers r/q/z     X:xen/common/cpupool.c:604-646, X:xen/common/keyhandler.c:233-300,421-426
+#include "engine.h"
+
+#include <sys/prctl.h>
+#include <time.h>
+
+#include <algorithm>
+#include <cinttypes>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+
+namespace gpbs {
+
+namespace {
+int64_t mono_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (int64_t)ts.tv_sec * 1000000000ll + ts.tv_nsec;
+}
+std::string fmt(const char* f, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, f);
+  vsnprintf(buf, sizeof(buf), f, ap);
+  va_end(ap);
+  return buf;
+}
+}  // namespace
+
+Engine::Engine(const gpbs_boot_params_t& p) : boot(p) {
+  std::memcpy(&adapt_params, &p.adapt, sizeof(adapt_params));
+  std::memcpy(&atc_params, &p.atc, sizeof(atc_params));
+  size_t cap = 1;
+  while (cap < (size_t)std::max(1024, p.trace_capacity)) cap <<= 1;
+  trace = std::make_unique<TraceRing>(cap);
+  if (boot.sim_clock) sim_now = 0;
+  pool_create("Pool-0", boot.sched);
+  if (boot.heartbeat_timeout_us > 0) {
+    hb_timer_ = timer_init([this](int64_t n) { heartbeat_check(n); });
+    timer_set(hb_timer_, now() + (int64_t)boot.heartbeat_timeout_us * 1000 / 2);
+  }
+}
+
+Engine::~Engine() {
+  stop();
+  std::lock_guard<std::recursive_mutex> g(mu);
+  for (auto& p : pools)
+    if (p && p->sched) p->sched->deinit();
+}
+
+int64_t Engine::now() const { return boot.sim_clock ? sim_now : mono_ns(); }
+
+// ------------------------------------------------------------------ timers -
+
+int Engine::timer_init(std::function<void(int64_t)> fn) {
+  int id;
+  if (!free_timers_.empty()) {
+    id = free_timers_.back();
+    free_timers_.pop_back();
+  } else {
+    id = (int)timers_.size();
+    timers_.emplace_back();
+  }
+  TimerEnt& t = timers_[id];
+  t.fn = std::move(fn);
+  t.gen++;
+  t.armed = false;
+  t.alive = true;
+  return id;
+}
+
+void Engine::timer_set(int id, int64_t when) {
+  TimerEnt& t = timers_[id];
+  if (!t.alive) return;
+  t.gen++;
+  t.armed = true;
+  t.when = when;
+  heap_.push(HeapEnt{when, seq_++, id, t.gen});
+}
+
+void Engine::timer_stop(int id) {
+  if (id < 0) return;
+  TimerEnt& t = timers_[id];
+  t.armed = false;
+  t.gen++;
+}
+
+void Engine::timer_kill(int id) {
+  if (id < 0) return;
+  TimerEnt& t = timers_[id];
+  t.armed = false;
+  t.alive = false;
+  t.gen++;
+  t.fn = nullptr;
+  free_timers_.push_back(id);
+}
+
+bool Engine::timer_armed(int id) const { return id >= 0 && timers_[id].alive && timers_[id].armed; }
+
+int64_t Engine::next_deadline() const {
+  auto& h = const_cast<decltype(heap_)&>(heap_);
+  while (!h.empty()) {
+    const HeapEnt& e = h.top();
+    const TimerEnt& t = timers_[e.id];
+    if (t.alive && t.armed && t.gen == e.gen) return e.when;
+    h.pop();
+  }
+  return INT64_MAX;
+}
+
+void Engine::run_due(int64_t n) {
+  while (!heap_.empty() && heap_.top().when <= n) {
+    HeapEnt e = heap_.top();
+    heap_.pop();
+    TimerEnt& t = timers_[e.id];
+    if (!t.alive || !t.armed || t.gen != e.gen) continue;
+    t.armed = false;
+    int64_t tn = n;
+    if (boot.sim_clock) {
+      sim_now = e.when;
+      tn = e.when;
+    }
+    auto fn = t.fn;  // the handler may re-arm or kill its own timer
+    fn(tn);
+    process_softirqs();
+  }
+  if (boot.sim_clock && n > sim_now) sim_now = n;
+  process_softirqs();
+  flush_actuation();
+}
+
+void Engine::raise_softirq(int part) {
+  if (part >= 0 && part < (int)parts.size()) parts[part]->softirq = true;
+}
+
+void Engine::process_softirqs() {
+  if (in_softirq_) return;
+  in_softirq_ = true;
+  for (;;) {
+    bool any = false;
+    for (auto& p : parts) {
+      if (p->softirq) {
+        p->softirq = false;
+        any = true;
+        if (p->pool >= 0) schedule(p->id);
+      }
+    }
+    if (!any) break;
+  }
+  in_softirq_ = false;
+}
+
+void Engine::flush_actuation() {
+  if (dirty_actuation && actuator_ops.on_flush) actuator_ops.on_flush(actuator_ops.user, now());
+  dirty_actuation = false;
+}
+
+// --------------------------------------------------------------- lifecycle -
+
+int Engine::partition_add(int gpu, int xcd) {
+  if ((int)parts.size() >= kMaxPartitions) return GPBS_ENOSPC;
+  auto p = std::make_unique<Partition>();
+  p->id = (int)parts.size();
+  p->gpu = gpu;
+  p->xcd = xcd;
+  auto idle = std::make_unique<Slot>();
+  idle->id = (int)slots.size();
+  idle->tenant = -1;
+  idle->index = p->id;
+  idle->processor = p->id;
+  idle->affinity = Mask::of(p->id);
+  idle->is_running = true;
+  idle->rs = RS_RUNNING;
+  idle->rs_entry = now();
+  p->idle_slot = idle->id;
+  p->curr = idle->id;
+  const int pid = p->id;
+  p->s_timer = timer_init([this, pid](int64_t) {  // s_timer_fn
+    perfc.incr(PC_sched_irq);
+    raise_softirq(pid);
+  });
+  slots.push_back(std::move(idle));
+  parts.push_back(std::move(p));
+  return pid;
+}
+
+int Engine::pool_create(const std::string& name, const std::string& sched) {
+  for (auto& p : pools)
+    if (p && p->name == name) return GPBS_EEXIST;
+  auto pl = std::make_unique<Pool>();
+  pl->id = (int)pools.size();
+  pl->name = name;
+  pl->sched_name = sched.empty() ? std::string(boot.sched) : sched;
+  pl->sched = make_scheduler(pl->sched_name, *this, pl->id);
+  if (!pl->sched) return GPBS_EINVAL;
+  int rc = pl->sched->init();
+  if (rc) return rc;
+  int id = pl->id;
+  pools.push_back(std::move(pl));
+  emit(TRC_POOL, 0, id, 1, 0);
+  return id;
+}
+
+int Engine::pool_destroy(int id) {
+  Pool* pl = pool(id);
+  if (!pl || id == 0) return GPBS_EINVAL;  // Pool-0 cannot be destroyed
+  for (auto& t : tenants)
+    if (t && t->alive && t->pool == id) return GPBS_EBUSY;
+  if (!pl->cpus.empty()) return GPBS_EBUSY;  // cpupool_destroy requires no cpus
+  pl->sched->deinit();
+  pools[id].reset();
+  emit(TRC_POOL, 0, id, 2, 0);
+  return GPBS_OK;
+}
+
+int Engine::pool_assign(int id, int part) {
+  Pool* pl = pool(id);
+  if (!pl || part < 0 || part >= (int)parts.size()) return GPBS_EINVAL;
+  Partition& P = *parts[part];
+  if (P.pool >= 0) return GPBS_EBUSY;
+  P.pool = id;
+  pl->cpus.set(part);
+  Slot& idle = *slots[P.idle_slot];
+  pl->sched->alloc_vdata(idle);
+  pl->sched->alloc_pdata(part);
+  // Parked slots of this pool waiting for any partition can now run here.
+  for (auto& s : slots) {
+    if (!s || s->is_idle()) continue;
+    Tenant* t = tenant(s->tenant);
+    if (!t || t->pool != id) continue;
+    if (!pl->cpus.test(s->processor)) {
+      s->processor = part;
+    }
+  }
+  raise_softirq(part);
+  process_softirqs();
+  emit(TRC_POOL, part, id, 3, part);
+  return GPBS_OK;
+}
+
+int Engine::pool_unassign(int id, int part) {
+  Pool* pl = pool(id);
+  if (!pl || part < 0 || part >= (int)parts.size() || parts[part]->pool != id) return GPBS_EINVAL;
+  bool has_tenants = false;
+  for (auto& t : tenants)
+    if (t && t->alive && t->pool == id) has_tenants = true;
+  if (pl->cpus.weight() == 1 && has_tenants) return GPBS_EBUSY;  // last cpu of a busy pool
+  Partition& P = *parts[part];
+  pl->cpus.clear(part);
+  // Evacuate: the running slot and every queued slot move to remaining cpus.
+  std::vector<int> movers;
+  for (auto& s : slots)
+    if (s && !s->is_idle() && s->processor == part) movers.push_back(s->id);
+  for (int sid : movers) {
+    Slot& v = *slots[sid];
+    v.pause_flags |= VPF_MIGRATING;
+    vcpu_sleep_nosync(v);
+  }
+  // Deschedule whatever is running, then switch the cpu to its idle slot.
+  if (P.curr != P.idle_slot) {
+    raise_softirq(part);
+    process_softirqs();
+  }
+  pl->sched->free_pdata(part);
+  timer_stop(P.s_timer);
+  P.pool = -1;
+  for (int sid : movers) {
+    Slot& v = *slots[sid];
+    if (v.is_running) continue;  // handled by context_saved
+    if (v.pause_flags & VPF_MIGRATING) vcpu_migrate(v);
+  }
+  // Affinity masks referencing the removed cpu stay valid for other cpus.
+  process_softirqs();
+  emit(TRC_POOL, part, id, 4, part);
+  return GPBS_OK;
+}
+
+int Engine::tenant_create(const std::string& name, int poolid, int nslots, int weight, int cap) {
+  Pool* pl = pool(poolid);
+  if (!pl || nslots <= 0 || nslots > kMaxPartitions) return GPBS_EINVAL;
+  if (weight != -1 && (weight < 1 || weight > GPBS_WEIGHT_MAX)) return GPBS_ERANGE;
+  if (cap != -1 && (cap < 0 || cap > 100 * nslots)) return GPBS_ERANGE;
+  for (auto& t : tenants)
+    if (t && t->alive && t->name == name) return GPBS_EEXIST;
+  auto T = std::make_unique<Tenant>();
+  T->id = (int)tenants.size();
+  T->name = name;
+  T->pool = poolid;
+  T->last_heartbeat = now();
+  tenants.push_back(std::move(T));
+  Tenant& d = *tenants.back();
+  int rc = pl->sched->init_domain(d);
+  if (rc) {
+    tenants.pop_back();
+    return rc;
+  }
+  perfc.incr(PC_dom_init);
+  int cpu = pl->cpus.empty() ? 0 : pl->cpus.first();
+  for (int i = 0; i < nslots; ++i) {
+    auto s = std::make_unique<Slot>();
+    s->id = (int)slots.size();
+    s->tenant = d.id;
+    s->index = i;
+    s->processor = cpu;
+    s->affinity = Mask::all(kMaxPartitions);  // setall (schedule.c:201)
+    s->pause_flags = VPF_BLOCKED;             // no work yet
+    s->rs = RS_BLOCKED;
+    s->rs_entry = now();
+    d.slots.push_back(s->id);
+    Slot& v = *s;
+    slots.push_back(std::move(s));
+    pl->sched->alloc_vdata(v);
+    pl->sched->insert_vcpu(v);
+    perfc.incr(PC_vcpu_init);
+    if (!pl->cpus.empty()) cpu = pl->cpus.cycle(cpu);  // spread initial placement
+  }
+  int w = weight, c = cap;
+  if (w != -1 || c != -1) pl->sched->adjust(d, true, &w, &c);
+  return d.id;
+}
+
+int Engine::tenant_destroy(int tid) {
+  Tenant* d = tenant(tid);
+  if (!d || !d->alive) return GPBS_ENOENT;
+  Scheduler* S = sched_of_tenant(tid);
+  for (int sid : d->slots) {
+    Slot& v = *slots[sid];
+    v.pause_flags |= VPF_BLOCKED;
+    vcpu_sleep_nosync(v);
+  }
+  process_softirqs();
+  for (int sid : d->slots) {
+    Slot& v = *slots[sid];
+    S->remove_vcpu(v);
+    perfc.incr(PC_vcpu_destroy);
+    v.priv.reset();
+  }
+  S->destroy_domain(*d);
+  perfc.incr(PC_dom_destroy);
+  d->alive = false;
+  d->priv.reset();
+  for (int sid : d->slots) slots[sid].reset();
+  d->slots.clear();
+  flush_actuation();
+  return GPBS_OK;
+}
+
+int Engine::tenant_move(int tid, int newpool) {
+  Tenant* d = tenant(tid);
+  Pool* np = pool(newpool);
+  if (!d || !d->alive || !np) return GPBS_EINVAL;
+  if (d->pool == newpool) return GPBS_OK;
+  if (np->cpus.empty()) return GPBS_EINVAL;
+  Scheduler* S = sched_of_tenant(tid);
+  int w = -1, c = -1;
+  S->adjust(*d, false, &w, &c);
+  std::vector<bool> was_blocked;
+  for (int sid : d->slots) {
+    Slot& v = *slots[sid];
+    was_blocked.push_back(v.pause_flags & VPF_BLOCKED);
+    v.pause_flags |= VPF_BLOCKED;
+    vcpu_sleep_nosync(v);
+  }
+  process_softirqs();
+  for (int sid : d->slots) {
+    S->remove_vcpu(*slots[sid]);
+    slots[sid]->priv.reset();
+  }
+  S->destroy_domain(*d);
+  d->priv.reset();
+  d->pool = newpool;
+  // Q4 fix: full init_domain (PBS state re-initialised, not just domdata).
+  np->sched->init_domain(*d);
+  int cpu = np->cpus.first();
+  for (size_t i = 0; i < d->slots.size(); ++i) {
+    Slot& v = *slots[d->slots[i]];
+    v.processor = cpu;
+    v.affinity = Mask::all(kMaxPartitions);
+    np->sched->alloc_vdata(v);
+    np->sched->insert_vcpu(v);
+    cpu = np->cpus.cycle(cpu);
+  }
+  np->sched->adjust(*d, true, &w, &c);
+  for (size_t i = 0; i < d->slots.size(); ++i)
+    if (!was_blocked[i]) vcpu_unblock(*slots[d->slots[i]]);
+  process_softirqs();
+  flush_actuation();
+  return GPBS_OK;
+}
+
+int Engine::tenant_set_nslots(int tid, int n) {
+  Tenant* d = tenant(tid);
+  if (!d || !d->alive || n < 1 || n > kMaxPartitions) return GPBS_EINVAL;
+  Scheduler* S = sched_of_tenant(tid);
+  Pool* pl = pool(d->pool);
+  while ((int)d->slots.size() < n) {  // grow (max_vcpus)
+    auto s = std::make_unique<Slot>();
+    s->id = (int)slots.size();
+    s->tenant = d->id;
+    s->index = (int)d->slots.size();
+    s->processor = pl->cpus.empty() ? 0 : pl->cpus.first();
+    s->affinity = Mask::all(kMaxPartitions);
+    s->pause_flags = VPF_BLOCKED;
+    s->rs = RS_BLOCKED;
+    s->rs_entry = now();
+    d->slots.push_back(s->id);
+    Slot& v = *s;
+    slots.push_back(std::move(s));
+    S->alloc_vdata(v);
+    S->insert_vcpu(v);
+  }
+  for (size_t i = 0; i < d->slots.size(); ++i) {
+    Slot& v = *slots[d->slots[i]];
+    if ((int)i < n && (v.pause_flags & VPF_DOWN)) {
+      v.pause_flags &= ~VPF_DOWN;
+      vcpu_wake(v);
+    } else if ((int)i >= n && !(v.pause_flags & VPF_DOWN)) {
+      v.pause_flags |= VPF_DOWN;
+      vcpu_sleep_nosync(v);
+    }
+  }
+  process_softirqs();
+  flush_actuation();
+  return GPBS_OK;
+}
+
+Scheduler* Engine::sched_of_part(int part) {
+  int p = parts[part]->pool;
+  return p >= 0 && pools[p] ? pools[p]->sched.get() : nullptr;
+}
+
+Scheduler* Engine::sched_of_tenant(int t) {
+  Tenant* d = tenant(t);
+  return d && pools[d->pool] ? pools[d->pool]->sched.get() : nullptr;
+}
+
+// ------------------------------------------------------- generic vcpu ops --
+
+bool Engine::runnable(const Slot& v) const {
+  if (v.is_idle()) return true;
+  if (v.pause_flags || v.pause_count) return false;
+  const Tenant* d = tenants[v.tenant].get();
+  return d && d->alive && d->pause_count == 0;
+}
+
+void Engine::runstate_change(Slot& v, Runstate rs, int64_t n) {
+  if (n > v.rs_entry) v.rs_time[v.rs] += n - v.rs_entry;
+  v.rs = rs;
+  v.rs_entry = n;
+}
+
+void Engine::vcpu_wake(Slot& v) {
+  if (runnable(v)) {
+    if (v.rs >= RS_BLOCKED) runstate_change(v, RS_RUNNABLE, now());
+    if (Scheduler* S = sched_of_tenant(v.tenant)) {
+      if (pools[tenants[v.tenant]->pool]->cpus.empty()) return;  // pool without cpus: stays queued later
+      S->wake(v);
+    }
+  } else if (!(v.pause_flags & VPF_BLOCKED)) {
+    if (v.rs == RS_BLOCKED) runstate_change(v, RS_OFFLINE, now());
+  }
+  emit(TRC_WAKE, v.processor, v.tenant, v.index, v.processor);
+}
+
+void Engine::vcpu_sleep_nosync(Slot& v) {
+  if (!runnable(v)) {
+    if (v.rs == RS_RUNNABLE)
+      runstate_change(v, (v.pause_flags & VPF_BLOCKED) ? RS_BLOCKED : RS_OFFLINE, now());
+    if (Scheduler* S = sched_of_tenant(v.tenant)) S->sleep(v);
+  }
+  emit(TRC_SLEEP, v.processor, v.tenant, v.index, v.processor);
+}
+
+void Engine::vcpu_block(Slot& v) {
+  if (v.pause_flags & VPF_BLOCKED) return;
+  v.pause_flags |= VPF_BLOCKED;
+  vcpu_sleep_nosync(v);
+}
+
+void Engine::vcpu_unblock(Slot& v) {
+  if (!(v.pause_flags & VPF_BLOCKED)) return;
+  v.pause_flags &= ~VPF_BLOCKED;
+  vcpu_wake(v);
+}
+
+void Engine::vcpu_pause(Slot& v) {
+  v.pause_count++;
+  vcpu_sleep_nosync(v);
+}
+
+void Engine::vcpu_unpause(Slot& v) {
+  if (v.pause_count > 0 && --v.pause_count == 0) vcpu_wake(v);
+}
+
+void Engine::vcpu_migrate(Slot& v) {
+  Scheduler* S = sched_of_tenant(v.tenant);
+  if (!S) return;
+  Pool* pl = pools[tenants[v.tenant]->pool].get();
+  int old = v.processor;
+  v.pause_flags &= ~VPF_MIGRATING;
+  if (pl->cpus.empty()) return;
+  if (!pl->cpus.test(v.processor)) v.processor = pl->cpus.first();
+  int nc = S->pick_cpu(v);
+  v.processor = nc;
+  if (old != nc) emit(TRC_MIGRATE, nc, v.tenant, v.index, old, nc);
+  vcpu_wake(v);
+}
+
+void Engine::pmu_refresh(Slot& v) {
+  if (v.is_idle() || !counter_ops.slot_refresh) return;
+  counter_ops.slot_refresh(counter_ops.user, v.id, v.tenant, v.processor, v.pmc);
+}
+
+void Engine::schedule(int part) {
+  Partition& P = *parts[part];
+  Scheduler* S = sched_of_part(part);
+  if (!S) return;
+  const int64_t n = now();
+  perfc.incr(PC_sched_run);
+  Slot& prev = *slots[P.curr];
+  timer_stop(P.s_timer);
+  TaskSlice ts = S->do_schedule(part, n);
+  Slot& next = *slots[ts.slot];
+  P.curr = next.id;
+  if (ts.time_ns >= 0) timer_set(P.s_timer, n + ts.time_ns);
+  if (&prev == &next) return;  // continue_running
+  const int32_t q_us = ts.time_ns >= 0 ? (int32_t)(ts.time_ns / 1000) : -1;
+  emit(TRC_SWITCH, part, (uint32_t)prev.tenant, (uint32_t)next.tenant, (uint32_t)q_us);
+  runstate_change(prev,
+                  (prev.pause_flags & VPF_BLOCKED) ? RS_BLOCKED : (runnable(prev) ? RS_RUNNABLE : RS_OFFLINE), n);
+  prev.last_run_time = n;
+  runstate_change(next, RS_RUNNING, n);
+  next.is_running = true;
+  perfc.incr(PC_sched_ctx);
+  // context_switch: PMU save of prev (pmustate.c:87-111 / P4), count next.
+  pmu_refresh(prev);
+  if (!next.is_idle()) next.sched_count++;
+  P.switches++;
+  if (actuator_ops.on_switch) {
+    actuator_ops.on_switch(actuator_ops.user, part, prev.tenant, next.tenant, next.is_idle() ? -1 : next.id, q_us, n);
+    perfc.incr(PC_partition_switch);
+  }
+  dirty_actuation = true;
+  context_saved(prev);
+}
+
+void Engine::context_saved(Slot& prev) {
+  prev.is_running = false;
+  if (Scheduler* S = sched_of_tenant(prev.tenant)) S->context_saved(prev);
+  if (prev.pause_flags & VPF_MIGRATING) vcpu_migrate(prev);
+}
+
+// ------------------------------------------------------------ heartbeats ---
+
+void Engine::heartbeat_check(int64_t n) {
+  const int64_t tmo = (int64_t)boot.heartbeat_timeout_us * 1000;
+  for (auto& t : tenants) {
+    if (!t || !t->alive || t->id == 0) continue;
+    if (n - t->last_heartbeat > tmo && t->pause_count == 0) {
+      // Reclaim: the tenant is declared dead; its partitions go to others.
+      t->pause_count++;
+      for (int sid : t->slots) vcpu_sleep_nosync(*slots[sid]);
+      perfc.incr(PC_tenant_dead);
+      emit(TRC_DEAD, 0, t->id);
+      printk(fmt("(GPBS) tenant %d (%s) missed heartbeats for %" PRId64 "us: paused\n", t->id, t->name.c_str(),
+                 (n - t->last_heartbeat) / 1000));
+    }
+  }
+  timer_set(hb_timer_, n + tmo / 2);
+}
+
+// --------------------------------------------------------- observability ---
+
+void Engine::printk(const std::string& s) {
+  console_ += s;
+  if (console_.size() > (1u << 20)) console_.erase(0, console_.size() - (1u << 19));
+}
+
+std::string Engine::dmesg(bool clear) {
+  std::string s = console_;
+  if (clear) console_.clear();
+  return s;
+}
+
+std::string Engine::dump_runq() {
+  std::string o;
+  o += fmt("sched_smt_power_savings: %s\n", boot.smt_power_savings ? "enabled" : "disabled");
+  o += fmt("NOW=0x%016" PRIx64 "\n", (uint64_t)now());
+  std::string free_cpus;
+  for (auto& p : parts)
+    if (p->pool < 0) free_cpus += fmt("%d ", p->id);
+  o += "Idle cpupool:\n";
+  o += "  free partitions: " + (free_cpus.empty() ? std::string("none") : free_cpus) + "\n";
+  for (auto& pl : pools) {
+    if (!pl) continue;
+    o += fmt("Cpupool %d:\n", pl->id);
+    o += fmt("Scheduler: %s (%s)\n", pl->sched->name(), pl->sched->opt_name());
+    pl->sched->dump_settings(o);
+    for (int c = pl->cpus.first(); c >= 0; c = pl->cpus.next(c + 1)) {
+      o += fmt("CPU[%02d] (gpu%d xcd%d) ", c, parts[c]->gpu, parts[c]->xcd);
+      pl->sched->dump_cpu_state(c, o);
+    }
+  }
+  return o;
+}
+
+std::string Engine::dump_domains() {
+  std::string o = fmt("'q' pressed -> dumping domain info (now=0x%016" PRIx64 ")\n", (uint64_t)now());
+  for (auto& t : tenants) {
+    if (!t || !t->alive) continue;
+    o += fmt("General information for domain %d (%s):\n", t->id, t->name.c_str());
+    o += fmt("    pause_count=%d pool=%d pending_requests=%" PRIu64 "\n", t->pause_count, t->pool,
+             t->pending_requests);
+    o += fmt("VCPU information and callbacks for domain %d:\n", t->id);
+    for (int sid : t->slots) {
+      Slot& v = *slots[sid];
+      o += fmt("    VCPU%d: CPU%d [has=%c] cpu_affinity=%s\n", v.index, v.processor, v.is_running ? 'T' : 'F',
+               v.affinity.weight() >= kMaxPartitions ? "all" : v.affinity.str().c_str());
+      o += fmt("    pause_count=%d pause_flags=%x\n", v.pause_count, v.pause_flags);
+      // keyhandler.c:294 pmuinfo line
+      o += fmt("pmuinfo: pmc[0]=%" PRIu64 "    pmc[1]=%" PRIu64 "    pmc[2]=%" PRIu64 "    pmc[3]=%" PRIu64 "\n",
+               v.pmc[0], v.pmc[1], v.pmc[2], v.pmc[3]);
+    }
+  }
+  return o;
+}
+
+std::string Engine::dump_customized() {
+  std::string o;
+  for (auto& pl : pools) {
+    if (!pl) continue;
+    o += fmt("Cpupool %d:\n", pl->id);
+    o += fmt("Scheduler: %s (%s)\n", pl->sched->name(), pl->sched->opt_name());
+    pl->sched->dump_admin_conf(o);
+  }
+  return o;
+}
+
+std::string Engine::check_invariants() {
+  std::string err;
+  for (auto& pl : pools)
+    if (pl) err += pl->sched->check();
+  for (auto& p : parts) {
+    Slot* c = slot(p->curr);
+    if (!c) {
+      err += fmt("cpu%d: curr slot missing\n", p->id);
+      continue;
+    }
+    if (!c->is_running) err += fmt("cpu%d: curr slot %d not marked running\n", p->id, c->id);
+    if (!c->is_idle() && c->processor != p->id) err += fmt("cpu%d: curr slot %d on cpu%d\n", p->id, c->id, c->processor);
+  }
+  for (auto& s : slots) {
+    if (!s || s->is_idle() || !s->is_running) continue;
+    if (parts[s->processor]->curr != s->id) err += fmt("slot %d running but not curr of cpu%d\n", s->id, s->processor);
+  }
+  return err;
+}
+
+std::string Engine::debug_keys(const std::string& keys) {
+  std::string o;
+  for (char k : keys) {
+    std::string part;
+    switch (k) {
+      case 'r':
+        part = dump_runq();
+        break;
+      case 'q':
+        part = dump_domains();
+        break;
+      case 'z':
+        part = dump_customized();
+        break;
+      case 'p': {  // perfc printall
+        for (int i = 0; i < PC_COUNT; ++i) part += fmt("%-28s %" PRIu64 "\n", kPerfcNames[i], perfc.get((PerfcId)i));
+        break;
+      }
+      case 'P':
+        perfc.reset();
+        part = "perfc reset\n";
+        break;
+      case 'c': {
+        part = check_invariants();
+        if (part.empty()) part = "invariants ok\n";
+        break;
+      }
+      case 'h':
+        part =
+            " 'r' dump run queues\n 'q' dump domain (tenant) info\n 'z' dump customized settings (PBS)\n"
+            " 'p' print performance counters\n 'P' reset performance counters\n 'c' check invariants\n";
+        break;
+      default:
+        part = fmt("'%c' unknown key\n", k);
+    }
+    printk(part);
+    o += part;
+  }
+  return o;
+}
+
+// ------------------------------------------------------ dispatcher thread --
+
+int Engine::start() {
+  if (boot.sim_clock) return GPBS_EINVAL;
+  std::lock_guard<std::recursive_mutex> g(mu);
+  if (running_) return GPBS_OK;
+  running_ = true;
+  thread_ = std::thread([this] { loop(); });
+  return GPBS_OK;
+}
+
+int Engine::stop() {
+  {
+    std::lock_guard<std::recursive_mutex> g(mu);
+    if (!running_) return GPBS_OK;
+    running_ = false;
+  }
+  cv_.notify_all();
+  if (thread_.joinable()) thread_.join();
+  return GPBS_OK;
+}
+
+void Engine::kick() {
+  kicked_ = true;
+  cv_.notify_all();
+}
+
+void Engine::loop() {
+  prctl(PR_SET_TIMERSLACK, 1UL, 0, 0, 0);  // µs-accurate quanta
+  std::unique_lock<std::recursive_mutex> lk(mu);
+  while (running_) {
+    int64_t n = now();
+    run_due(n);
+    int64_t dl = next_deadline();
+    kicked_ = false;
+    n = now();
+    if (dl <= n) continue;
+    int64_t wait = dl == INT64_MAX ? 50000000 : dl - n;
+    if (wait > 40000) {
+      cv_.wait_for(lk, std::chrono::nanoseconds(wait - 20000), [this] { return kicked_ || !running_; });
+    } else {
+      // Final approach: drop the lock and spin-yield so API callers get in.
+      lk.unlock();
+      while (mono_ns() < dl && !kicked_) std::this_thread::yield();
+      lk.lock();
+    }
+  }
+}
+
+}  // namespace gpbs

@@ -1,0 +1,271 @@
+// gpbs engine: the generic scheduling framework (analog of
+// X:xen/common/schedule.c + cpupool.c + the vcpu/domain lifecycle in
+// X:xen/common/domain.c), hosting pluggable policies behind Scheduler
+// (X:xen/include/xen/sched-if.h:144-193).
+//
+// Design (MI355X-first): one engine per GPU-rank process.  Its partitions are
+// XCD-aligned CU groups (8 per MI355X).  All partitions are driven by ONE
+// dispatcher thread off a single timer heap (instead of per-pCPU softirqs);
+// "IPIs" are softirq bits processed in the same pass.  External threads
+// (tenant runners, the RPC server, the gang thread) enter through the C ABI
+// under one engine mutex; wake-ups raise softirqs that are processed before
+// the call returns, so a wake has µs latency without a context switch.
+#pragma once
+#include <condition_variable>
+#include <cstdint>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <queue>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../include/gpbs/gpbs.h"
+#include "../obs/perfc.h"
+#include "../obs/trace.h"
+#include "adapt.h"
+#include "bitmask.h"
+
+namespace gpbs {
+
+enum Pri : int16_t { PRI_BOOST = 0, PRI_UNDER = -1, PRI_OVER = -2, PRI_IDLE = -64 };
+enum Runstate : int { RS_RUNNING = 0, RS_RUNNABLE = 1, RS_BLOCKED = 2, RS_OFFLINE = 3 };
+constexpr uint32_t VPF_BLOCKED = 1u;    // _VPF_blocked
+constexpr uint32_t VPF_MIGRATING = 2u;  // _VPF_migrating
+constexpr uint32_t VPF_DOWN = 4u;       // _VPF_down (vcpu-set offline)
+
+constexpr int kNumPmc = 4;  // INST, CYCLES, L2_REFS (LLC_REFERENCES), L2_MISSES (LLC_MISSES)
+
+struct SchedSlotData {
+  virtual ~SchedSlotData() = default;
+};
+struct SchedTenantData {
+  virtual ~SchedTenantData() = default;
+};
+struct SchedPartData {
+  virtual ~SchedPartData() = default;
+};
+
+struct Slot {  // struct vcpu
+  int id = -1;
+  int tenant = -1;  // -1: idle slot of a partition
+  int index = 0;    // vcpu_id
+  int processor = 0;
+  Mask affinity;
+  uint32_t pause_flags = 0;
+  int pause_count = 0;
+  bool is_running = false;
+  Runstate rs = RS_OFFLINE;
+  int64_t rs_entry = 0;
+  int64_t rs_time[4] = {0, 0, 0, 0};
+  int64_t last_run_time = 0;
+  uint64_t pmc[kNumPmc] = {0, 0, 0, 0};  // v->pmc (P4), cumulative
+  uint64_t sched_count = 0;              // v->sched_count (P4)
+  std::unique_ptr<SchedSlotData> priv;
+  bool is_idle() const { return tenant < 0; }
+};
+
+struct Tenant {  // struct domain
+  int id = -1;
+  std::string name;
+  int pool = 0;
+  std::vector<int> slots;  // slot ids, index order
+  int pause_count = 0;
+  bool alive = true;
+  bool pinned = false;
+  uint64_t pending_requests = 0;  // P7 (live in gpbs: request-queue depth)
+  int64_t last_heartbeat = 0;
+  std::unique_ptr<SchedTenantData> priv;
+};
+
+struct Partition {  // pCPU + schedule_data
+  int id = -1;
+  int gpu = 0;
+  int xcd = 0;
+  int pool = -1;
+  int curr = -1;       // running slot (idle slot when idle)
+  int idle_slot = -1;  // this partition's idle vCPU
+  int s_timer = -1;
+  bool softirq = false;
+  uint64_t switches = 0;
+  std::unique_ptr<SchedPartData> priv;
+};
+
+struct TaskSlice {
+  int slot;
+  int64_t time_ns;  // < 0: no limit
+  bool migrated;
+};
+
+class Engine;
+
+// The pluggable scheduler interface (struct scheduler, sched-if.h:144-193).
+class Scheduler {
+ public:
+  Scheduler(Engine& e, int pool) : E(e), pool_(pool) {}
+  virtual ~Scheduler() = default;
+  virtual const char* name() const = 0;
+  virtual const char* opt_name() const = 0;
+  virtual int init() { return 0; }
+  virtual void deinit() {}
+  virtual void alloc_pdata(int part) = 0;
+  virtual void free_pdata(int part) = 0;
+  virtual int init_domain(Tenant& d) = 0;
+  virtual void destroy_domain(Tenant& d) = 0;
+  virtual void alloc_vdata(Slot& v) = 0;
+  virtual void insert_vcpu(Slot& v) = 0;
+  virtual void remove_vcpu(Slot& v) = 0;
+  virtual void sleep(Slot& v) = 0;
+  virtual void wake(Slot& v) = 0;
+  virtual void yield(Slot& v) = 0;
+  virtual TaskSlice do_schedule(int part, int64_t now) = 0;
+  virtual int pick_cpu(Slot& v) = 0;
+  virtual int adjust(Tenant& d, bool set, int* weight, int* cap) = 0;
+  virtual int adjust_global(bool set, int* tslice_us, int* ratelimit_us) = 0;
+  virtual void dump_settings(std::string& out) = 0;
+  virtual void dump_cpu_state(int part, std::string& out) = 0;
+  virtual void dump_admin_conf(std::string& out) = 0;
+  virtual void tick_suspend(int) {}
+  virtual void tick_resume(int) {}
+  virtual void context_saved(Slot&) {}
+  // gpbs additions: the paravirtual wait report routed by tenant id (Q6 fix)
+  virtual void report(Tenant&, uint64_t, int) {}
+  virtual bool tenant_adapt(Tenant&, AdaptState*) { return false; }
+  virtual bool set_tenant_adapt(Tenant&, const AdaptState&) { return false; }
+  virtual void fill_tenant_info(Tenant&, gpbs_tenant_info_t&) {}
+  virtual void fill_slot_info(Slot&, gpbs_slot_info_t&) {}
+  virtual std::string check() { return ""; }
+  int pool() const { return pool_; }
+
+ protected:
+  Engine& E;
+  int pool_;
+};
+
+struct Pool {
+  int id = -1;
+  std::string name;
+  std::string sched_name;
+  Mask cpus;
+  std::unique_ptr<Scheduler> sched;
+};
+
+std::unique_ptr<Scheduler> make_scheduler(const std::string& name, Engine& e, int pool);
+
+class Engine {
+ public:
+  explicit Engine(const gpbs_boot_params_t& p);
+  ~Engine();
+
+  gpbs_boot_params_t boot;
+  AdaptParams adapt_params;
+  AtcParams atc_params;
+  Perfc perfc;
+  std::unique_ptr<TraceRing> trace;
+  std::recursive_mutex mu;
+
+  std::vector<std::unique_ptr<Partition>> parts;
+  std::vector<std::unique_ptr<Slot>> slots;
+  std::vector<std::unique_ptr<Tenant>> tenants;
+  std::vector<std::unique_ptr<Pool>> pools;
+
+  gpbs_counter_ops_t counter_ops{};
+  gpbs_actuator_ops_t actuator_ops{};
+  bool dirty_actuation = false;
+
+  // --- time & timers (X:xen/common/timer.c analog) ---
+  int64_t now() const;
+  int timer_init(std::function<void(int64_t)> fn);
+  void timer_set(int id, int64_t when);
+  void timer_stop(int id);
+  void timer_kill(int id);
+  bool timer_armed(int id) const;
+  int64_t next_deadline() const;
+  void run_due(int64_t now);  // process timers and softirqs
+  void raise_softirq(int part);
+  void process_softirqs();
+  void flush_actuation();
+
+  // --- lifecycle ---
+  int partition_add(int gpu, int xcd);
+  int pool_create(const std::string& name, const std::string& sched);
+  int pool_destroy(int pool);
+  int pool_assign(int pool, int part);
+  int pool_unassign(int pool, int part);
+  int tenant_create(const std::string& name, int pool, int nslots, int weight, int cap);
+  int tenant_destroy(int t);
+  int tenant_move(int t, int pool);
+  int tenant_set_nslots(int t, int n);
+
+  // --- generic vcpu ops (schedule.c) ---
+  bool runnable(const Slot& v) const;
+  void runstate_change(Slot& v, Runstate rs, int64_t now);
+  void vcpu_wake(Slot& v);
+  void vcpu_sleep_nosync(Slot& v);
+  void vcpu_block(Slot& v);
+  void vcpu_unblock(Slot& v);
+  void vcpu_pause(Slot& v);
+  void vcpu_unpause(Slot& v);
+  void vcpu_migrate(Slot& v);
+  void schedule(int part);
+  void context_saved(Slot& prev);
+  void pmu_refresh(Slot& v);
+
+  Scheduler* sched_of_part(int part);
+  Scheduler* sched_of_tenant(int t);
+  Tenant* tenant(int id) { return (id >= 0 && id < (int)tenants.size()) ? tenants[id].get() : nullptr; }
+  Slot* slot(int id) { return (id >= 0 && id < (int)slots.size()) ? slots[id].get() : nullptr; }
+  Pool* pool(int id) { return (id >= 0 && id < (int)pools.size()) ? pools[id].get() : nullptr; }
+  Slot& curr_of(int part) { return *slots[parts[part]->curr]; }
+
+  // --- observability ---
+  void printk(const std::string& s);
+  std::string dmesg(bool clear);
+  std::string debug_keys(const std::string& keys);
+  std::string dump_runq();      // 'r'
+  std::string dump_domains();   // 'q'
+  std::string dump_customized();// 'z' (P5)
+  std::string check_invariants();
+  void emit(uint32_t ev, uint32_t cpu, uint32_t a0 = 0, uint32_t a1 = 0, uint32_t a2 = 0, uint32_t a3 = 0) {
+    trace->emit(now(), ev, cpu, a0, a1, a2, a3);
+  }
+
+  // --- dispatcher thread (real clock) ---
+  int start();
+  int stop();
+  void kick();
+  void heartbeat_check(int64_t now);
+
+  int64_t sim_now = 0;
+
+ private:
+  struct TimerEnt {
+    std::function<void(int64_t)> fn;
+    uint64_t gen = 0;
+    int64_t when = 0;
+    bool armed = false;
+    bool alive = false;
+  };
+  struct HeapEnt {
+    int64_t when;
+    uint64_t seq;
+    int id;
+    uint64_t gen;
+    bool operator>(const HeapEnt& o) const { return when != o.when ? when > o.when : seq > o.seq; }
+  };
+  std::vector<TimerEnt> timers_;
+  std::vector<int> free_timers_;
+  std::priority_queue<HeapEnt, std::vector<HeapEnt>, std::greater<HeapEnt>> heap_;
+  uint64_t seq_ = 0;
+  bool in_softirq_ = false;
+  std::string console_;
+  std::thread thread_;
+  std::condition_variable_any cv_;
+  bool running_ = false;
+  bool kicked_ = false;
+  int hb_timer_ = -1;
+  void loop();
+};
+
+}  // namespace gpbs

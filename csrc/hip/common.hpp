@@ -1,0 +1,98 @@
+// Shared definitions for the gfx950 (MI355X / CDNA4) kernels and runtime.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+
+namespace gpbs_hip {
+
+constexpr int kXcds = 8;          // MI355X: 8 XCDs x 32 CUs
+constexpr int kMaxTenants = 64;   // per GPU context
+constexpr int kNumPmc = 4;        // INST, CYCLES, L2_REFS, L2_MISSES (modeled)
+constexpr uint32_t kNoOwner = 0xFFFFFFFFu;
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16;
+typedef unsigned int u32;
+typedef unsigned long long u64;
+
+// Partition table shared by the scheduler (host) and tenant kernels.  Lives
+// in fine-grained pinned host memory: the dispatcher thread's store is seen
+// by the next system-scope load of a workgroup (~1-2 us over PCIe) without a
+// copy or a kernel launch.  A device-memory copy is maintained by the
+// partition_switch kernel when GPBS_TABLE=device.
+struct alignas(64) PartTable {
+  u32 epoch;
+  u32 flags;
+  u32 owner[kXcds];   // tenant id owning each XCD, kNoOwner when idle
+  u32 pad[6];
+};
+
+// Work queue of one tenant kernel invocation (tile / chunk queue).
+struct alignas(64) WorkQueue {
+  u32 next;       // next unit to grab (atomic)
+  u32 done;       // completed units
+  u32 exited;     // workgroups that finished (any path)
+  u32 stopped;    // workgroups that left because their XCD was revoked
+  u32 pad[12];
+};
+
+// Exit protocol of every tenant kernel: the last workgroup to leave publishes
+// the unit count to the host-visible status word (pinned, system scope), so the
+// runner learns "finished or revoked" from the completion event alone.
+__device__ __forceinline__ void finish(WorkQueue* q, u32* status) {
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const u32 old = atomicAdd(&q->exited, 1u);
+    if (old == gridDim.x - 1) {
+      __threadfence();
+      const u32 d = __hip_atomic_load(&q->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (status) __hip_atomic_store(status, d | 0x80000000u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+// Gate modes passed to tenant kernels.
+enum GateMode : u32 { GATE_NONE = 0, GATE_TABLE = 1 };
+
+#define HIPCHECK(x)                                                                              \
+  do {                                                                                           \
+    hipError_t _e = (x);                                                                         \
+    if (_e != hipSuccess) {                                                                      \
+      fprintf(stderr, "[gpbs-hip] %s:%d %s -> %s\n", __FILE__, __LINE__, #x, hipGetErrorString(_e)); \
+      return -(int)_e - 1000;                                                                    \
+    }                                                                                            \
+  } while (0)
+
+__device__ __forceinline__ u32 xcc_id() {
+  // s_getreg_b32 hwreg(HW_REG_XCC_ID, 0, 4): the XCD this wave runs on.
+  return __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);
+}
+
+__device__ __forceinline__ u32 hw_id() { return __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4); }
+
+__device__ __forceinline__ u32 load_sys(const u32* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Does tenant `me` own the XCD this workgroup runs on?
+__device__ __forceinline__ bool owns(const PartTable* t, u32 mode, u32 me, u32 xcc) {
+  if (mode == GATE_NONE) return true;
+  return load_sys(&t->owner[xcc & 7]) == me;
+}
+
+// Per-(tenant, xcd) software counter block, accumulated at workgroup exit.
+__device__ __forceinline__ void count(u64* cnt, u32 me, u32 xcc, u64 inst, u64 cyc, u64 refs, u64 miss) {
+  if (!cnt) return;
+  u64* c = cnt + ((size_t)me * kXcds + (xcc & 7)) * kNumPmc;
+  if (inst) atomicAdd(c + 0, inst);
+  if (cyc) atomicAdd(c + 1, cyc);
+  if (refs) atomicAdd(c + 2, refs);
+  if (miss) atomicAdd(c + 3, miss);
+}
+
+}  // namespace gpbs_hip

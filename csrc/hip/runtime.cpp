@@ -1,0 +1,608 @@
+// GPU runtime of gpbs on one MI355X (one process per GPU):
+//
+//  * GpuCtx     partition table (pinned, fine-grained host memory that tenant
+//               kernels poll with system-scope loads; optional device copy
+//               refreshed by k_partition_switch), per-(tenant,XCD) counter
+//               blocks in HBM, a high-priority scheduler stream, and the
+//               engine hooks: the actuator (context switch -> owner table) and
+//               the counter backend (device counter_reduce + adapt kernels).
+//  * Runner     a native tenant worker thread: it keeps up to `depth` units of
+//               its workload in flight on its own HIP stream, launching only
+//               while its tenant owns an XCD, relaunching revoked units, and
+//               tells the engine when it has work (slot wake) and when it
+//               drains (slot block).  This is the in-process tenant shim; the
+//               cross-process one is pbs_amd/runtime/tenant.py over ctl pages.
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../include/gpbs/gpbs.h"
+#include "common.hpp"
+
+using namespace gpbs_hip;
+
+extern "C" {
+int gpbs_hip_gemm_bf16(const void*, const void*, void*, int, int, int, void*, const void*, unsigned, unsigned, void*,
+                       void*, int, hipStream_t);
+int gpbs_hip_stream_copy(const void*, void*, unsigned long long, unsigned, void*, const void*, unsigned, unsigned,
+                         void*, void*, int, hipStream_t);
+int gpbs_hip_reduce_bf16(const void*, const void*, void*, unsigned long long, unsigned, void*, const void*, unsigned,
+                         unsigned, void*, void*, int, hipStream_t);
+int gpbs_hip_gemv_bf16(const void*, const void*, void*, int, int, void*, const void*, unsigned, unsigned, void*, void*,
+                       int, hipStream_t);
+int gpbs_hip_partition_switch(void*, unsigned, const unsigned*, hipStream_t);
+int gpbs_hip_counter_reduce(void*, void*, const int*, int, void*, hipStream_t);
+int gpbs_hip_adapt(void*, const void*, const void*, const void*, int, const gpbs_adapt_params_t*, int*, hipStream_t);
+}
+
+namespace {
+
+int64_t mono_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+struct GpuCtx {
+  int device = 0;
+  int part_base = 0;  // engine partition id of XCD 0
+  int table_mode = 0; // 0: pinned host table, 1: device table + partition_switch kernel
+  PartTable* h_table = nullptr;  // pinned host (device-visible)
+  PartTable* d_table = nullptr;  // device copy (table_mode 1)
+  u64* d_cnt = nullptr;          // [kMaxTenants][kXcds][kNumPmc]
+  u64* d_prev = nullptr;
+  u64* h_out = nullptr;          // pinned mapped: deltas [kMaxTenants][4]
+  int* h_ids = nullptr;          // pinned mapped
+  gpbs_adapt_state_t* h_states = nullptr;
+  u64* h_spin = nullptr;         // [2][kMaxTenants]
+  int* h_dirs = nullptr;
+  hipStream_t sched_stream = nullptr;
+  gpbs_engine_t* engine = nullptr;
+  u32 pending[kXcds];
+  u32 epoch = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::atomic<uint64_t> switches{0}, flushes{0}, metric_calls{0};
+  int64_t metric_ns = 0;
+};
+
+// ---------------------------------------------------------------- engine hooks
+
+void act_on_switch(void* user, int part, int, int next, int, int32_t, int64_t) {
+  GpuCtx* c = (GpuCtx*)user;
+  const int x = part - c->part_base;
+  if (x < 0 || x >= kXcds) return;
+  c->pending[x] = next >= 0 ? (u32)next : kNoOwner;
+  c->switches++;
+}
+
+void publish(GpuCtx* c) {
+  bool changed = false;
+  for (int x = 0; x < kXcds; ++x)
+    if (__atomic_load_n(&c->h_table->owner[x], __ATOMIC_RELAXED) != c->pending[x]) changed = true;
+  if (!changed) return;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    for (int x = 0; x < kXcds; ++x) __atomic_store_n(&c->h_table->owner[x], c->pending[x], __ATOMIC_RELEASE);
+    c->epoch++;
+    __atomic_store_n(&c->h_table->epoch, c->epoch, __ATOMIC_RELEASE);
+  }
+  if (c->table_mode == 1) gpbs_hip_partition_switch(c->d_table, c->epoch, c->pending, c->sched_stream);
+  c->flushes++;
+  c->cv.notify_all();
+}
+
+void act_on_flush(void* user, int64_t) { publish((GpuCtx*)user); }
+
+void act_on_park(void*, int, int, int) {}
+
+int ctr_tenant_deltas(void* user, int n, const int* tenants, uint64_t* out) {
+  GpuCtx* c = (GpuCtx*)user;
+  if (n > kMaxTenants) return -22;
+  const int64_t t0 = mono_ns();
+  for (int i = 0; i < n; ++i) c->h_ids[i] = tenants[i] < kMaxTenants ? tenants[i] : -1;
+  if (gpbs_hip_counter_reduce(c->d_cnt, c->d_prev, c->h_ids, n, c->h_out, c->sched_stream)) return -5;
+  if (hipStreamSynchronize(c->sched_stream) != hipSuccess) return -5;
+  std::memcpy(out, c->h_out, sizeof(u64) * 4 * n);
+  c->metric_calls++;
+  c->metric_ns += mono_ns() - t0;
+  return 0;
+}
+
+int ctr_adapt_batch(void* user, int n, const int*, const uint64_t* deltas, const uint64_t* ssum, const uint64_t* scnt,
+                    gpbs_adapt_state_t* states, const gpbs_adapt_params_t* p) {
+  GpuCtx* c = (GpuCtx*)user;
+  if (n > kMaxTenants) return -22;
+  const int64_t t0 = mono_ns();
+  std::memcpy(c->h_states, states, sizeof(gpbs_adapt_state_t) * n);
+  std::memcpy(c->h_out, deltas, sizeof(u64) * 4 * n);
+  std::memcpy(c->h_spin, ssum, sizeof(u64) * n);
+  std::memcpy(c->h_spin + kMaxTenants, scnt, sizeof(u64) * n);
+  if (gpbs_hip_adapt(c->h_states, c->h_out, c->h_spin, c->h_spin + kMaxTenants, n, p, c->h_dirs, c->sched_stream))
+    return -5;
+  if (hipStreamSynchronize(c->sched_stream) != hipSuccess) return -5;
+  std::memcpy(states, c->h_states, sizeof(gpbs_adapt_state_t) * n);
+  c->metric_ns += mono_ns() - t0;
+  return 0;
+}
+
+// --------------------------------------------------------------------- runner
+
+enum Kind { K_GEMM = 1, K_STREAM = 2, K_REDUCE = 3, K_GEMV = 4 };
+
+}  // namespace
+
+extern "C" {
+
+typedef struct gpbs_runner_cfg {
+  int kind;
+  int tenant;       // engine tenant id (< 64); also the kernel's owner id
+  int gate;         // 1: obey the partition table; 0: run anywhere (policy "none")
+  int priority;     // stream priority: 0 normal, 1 high
+  int depth;        // units in flight
+  int grid;         // 0 = default persistent grid
+  int M, N, K;      // GEMM / GEMV shapes
+  int chunk_bytes;  // stream / reduce chunk
+  int engine_wake;  // 1: wake/block engine slots as work arrives/drains
+  int reserved;
+  unsigned long long bytes;  // stream / reduce bytes
+  void *a, *b, *c;           // device buffers (caller-owned)
+} gpbs_runner_cfg_t;
+
+typedef struct gpbs_runner_stats {
+  uint64_t units_done, launches, relaunches, waits_owner, submitted;
+  int64_t busy_ns, wait_owner_ns, first_start_ns, last_done_ns;
+  int64_t lat_sum_ns, lat_max_ns;
+  uint64_t lat_count;
+} gpbs_runner_stats_t;
+
+}
+
+namespace {
+
+struct Runner {
+  GpuCtx* ctx;
+  gpbs_runner_cfg_t cfg;
+  hipStream_t stream = nullptr;
+  WorkQueue* d_q = nullptr;  // ring of depth+1 queues
+  u32* h_status = nullptr;   // pinned status words
+  int nq = 0;
+  std::thread th;
+  std::mutex mu;
+  std::condition_variable cv, idle_cv;
+  int64_t pending = 0;   // units submitted but not launched
+  int64_t inflight = 0;
+  bool stop = false;
+  std::deque<int64_t> submit_times;
+  gpbs_runner_stats_t st{};
+  std::vector<int64_t> lats;
+  hipEvent_t ev[16];
+  int err = 0;
+
+  u32 unit_total() const {
+    switch (cfg.kind) {
+      case K_GEMM: return (u32)((cfg.M / 128) * (cfg.N / 128));
+      case K_STREAM:
+      case K_REDUCE: return (u32)((cfg.bytes + cfg.chunk_bytes - 1) / cfg.chunk_bytes);
+      case K_GEMV: return (u32)((cfg.M + 15) / 16);
+    }
+    return 0;
+  }
+
+  int launch(int qi) {
+    WorkQueue* q = d_q + qi;
+    const void* tab = ctx->table_mode == 1 ? (const void*)ctx->d_table : (const void*)ctx->h_table;
+    const unsigned mode = cfg.gate ? GATE_TABLE : GATE_NONE;
+    const unsigned me = (unsigned)cfg.tenant;
+    __atomic_store_n(&h_status[qi], 0u, __ATOMIC_RELEASE);
+    st.launches++;
+    switch (cfg.kind) {
+      case K_GEMM:
+        return gpbs_hip_gemm_bf16(cfg.a, cfg.b, cfg.c, cfg.M, cfg.N, cfg.K, q, tab, mode, me, ctx->d_cnt,
+                                  &h_status[qi], cfg.grid, stream);
+      case K_STREAM:
+        return gpbs_hip_stream_copy(cfg.a, cfg.c, cfg.bytes, (unsigned)cfg.chunk_bytes, q, tab, mode, me, ctx->d_cnt,
+                                    &h_status[qi], cfg.grid, stream);
+      case K_REDUCE:
+        return gpbs_hip_reduce_bf16(cfg.a, cfg.b, cfg.c, cfg.bytes, (unsigned)cfg.chunk_bytes, q, tab, mode, me,
+                                    ctx->d_cnt, &h_status[qi], cfg.grid, stream);
+      case K_GEMV:
+        return gpbs_hip_gemv_bf16(cfg.a, cfg.b, cfg.c, cfg.M, cfg.K, q, tab, mode, me, ctx->d_cnt, &h_status[qi],
+                                  cfg.grid, stream);
+    }
+    return -22;
+  }
+
+  bool owns_any() {
+    if (!cfg.gate) return true;
+    for (int x = 0; x < kXcds; ++x)
+      if (__atomic_load_n(&ctx->h_table->owner[x], __ATOMIC_ACQUIRE) == (u32)cfg.tenant) return true;
+    return false;
+  }
+
+  void wait_owner() {
+    if (owns_any()) return;
+    st.waits_owner++;
+    const int64_t t0 = mono_ns();
+    std::unique_lock<std::mutex> lk(ctx->mu);
+    while (!stop && !owns_any()) ctx->cv.wait_for(lk, std::chrono::microseconds(200));
+    st.wait_owner_ns += mono_ns() - t0;
+  }
+
+  void engine_wake(bool on) {
+    if (!cfg.engine_wake || !ctx->engine) return;
+    if (on)
+      gpbs_slot_wake(ctx->engine, cfg.tenant, -1);
+    else
+      gpbs_slot_block(ctx->engine, cfg.tenant, -1);
+  }
+
+  void loop() {
+    hipSetDevice(ctx->device);
+    struct Fl {
+      int qi;
+      int ev;
+    };
+    std::deque<Fl> fl;
+    int next_q = 0;
+    std::vector<char> q_busy(nq, 0);
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return stop || pending > 0; });
+        if (stop) break;
+      }
+      engine_wake(true);
+      const int64_t batch_t0 = mono_ns();
+      if (!st.first_start_ns) st.first_start_ns = batch_t0;
+      std::deque<int> relaunch;  // queue indices with revoked (unfinished) units
+      for (;;) {
+        // Fill the pipeline.
+        for (;;) {
+          if ((int)fl.size() >= cfg.depth) break;
+          int qi = -1;
+          bool fresh = false;
+          if (!relaunch.empty()) {
+            qi = relaunch.front();
+          } else {
+            std::lock_guard<std::mutex> g(mu);
+            if (pending <= 0) break;
+            for (int k = 0; k < nq; ++k) {
+              int cand = (next_q + k) % nq;
+              if (!q_busy[cand]) {
+                qi = cand;
+                break;
+              }
+            }
+            if (qi < 0) break;
+            fresh = true;
+          }
+          wait_owner();
+          if (stop) break;
+          if (fresh) {
+            std::lock_guard<std::mutex> g(mu);
+            pending--;
+            inflight++;
+            next_q = (qi + 1) % nq;
+            q_busy[qi] = 1;
+            hipMemsetAsync(d_q + qi, 0, sizeof(WorkQueue), stream);
+          } else {
+            relaunch.pop_front();
+            st.relaunches++;
+            // resume the same queue: clear exit bookkeeping only
+            hipMemsetAsync(&d_q[qi].exited, 0, sizeof(u32) * 2, stream);
+          }
+          if (launch(qi) != 0) err = -5;
+          const int e = qi;  // one event per queue slot
+          hipEventRecord(ev[e], stream);
+          fl.push_back({qi, e});
+        }
+        if (fl.empty()) {
+          std::lock_guard<std::mutex> g(mu);
+          if (pending <= 0 && relaunch.empty()) break;
+          continue;
+        }
+        Fl f = fl.front();
+        fl.pop_front();
+        while (hipEventQuery(ev[f.ev]) == hipErrorNotReady) {
+          if (stop) break;
+          std::this_thread::yield();
+        }
+        const u32 s = __atomic_load_n(&h_status[f.qi], __ATOMIC_ACQUIRE);
+        const u32 done = s & 0x7fffffffu;
+        if ((s & 0x80000000u) && done >= unit_total()) {
+          const int64_t t = mono_ns();
+          std::lock_guard<std::mutex> g(mu);
+          q_busy[f.qi] = 0;
+          inflight--;
+          st.units_done++;
+          st.last_done_ns = t;
+          if (!submit_times.empty()) {
+            const int64_t lat = t - submit_times.front();
+            submit_times.pop_front();
+            st.lat_sum_ns += lat;
+            st.lat_count++;
+            if (lat > st.lat_max_ns) st.lat_max_ns = lat;
+            if (lats.size() < (1u << 20)) lats.push_back(lat);
+          }
+        } else {
+          relaunch.push_back(f.qi);  // revoked mid-unit: resume when owned
+        }
+        if (stop) break;
+      }
+      st.busy_ns += mono_ns() - batch_t0;
+      {
+        std::lock_guard<std::mutex> g(mu);
+        if (pending <= 0 && inflight <= 0) {
+          engine_wake(false);
+          idle_cv.notify_all();
+        }
+      }
+      if (stop) break;
+    }
+    hipStreamSynchronize(stream);
+    std::lock_guard<std::mutex> g(mu);
+    idle_cv.notify_all();
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode) {
+  if (hipSetDevice(device) != hipSuccess) return nullptr;
+  auto* c = new GpuCtx;
+  c->device = device;
+  c->part_base = part_base;
+  c->table_mode = table_mode;
+  bool ok = hipHostMalloc((void**)&c->h_table, sizeof(PartTable), hipHostMallocCoherent | hipHostMallocMapped) ==
+            hipSuccess;
+  ok = ok && hipMalloc((void**)&c->d_cnt, sizeof(u64) * kMaxTenants * kXcds * kNumPmc) == hipSuccess;
+  ok = ok && hipMalloc((void**)&c->d_prev, sizeof(u64) * kMaxTenants * kXcds * kNumPmc) == hipSuccess;
+  ok = ok && hipMemset(c->d_cnt, 0, sizeof(u64) * kMaxTenants * kXcds * kNumPmc) == hipSuccess;
+  ok = ok && hipMemset(c->d_prev, 0, sizeof(u64) * kMaxTenants * kXcds * kNumPmc) == hipSuccess;
+  ok = ok && hipHostMalloc((void**)&c->h_out, sizeof(u64) * 4 * kMaxTenants, hipHostMallocMapped) == hipSuccess;
+  ok = ok && hipHostMalloc((void**)&c->h_ids, sizeof(int) * kMaxTenants, hipHostMallocMapped) == hipSuccess;
+  ok = ok && hipHostMalloc((void**)&c->h_states, sizeof(gpbs_adapt_state_t) * kMaxTenants, hipHostMallocMapped) ==
+                 hipSuccess;
+  ok = ok && hipHostMalloc((void**)&c->h_spin, sizeof(u64) * 2 * kMaxTenants, hipHostMallocMapped) == hipSuccess;
+  ok = ok && hipHostMalloc((void**)&c->h_dirs, sizeof(int) * kMaxTenants, hipHostMallocMapped) == hipSuccess;
+  int lo = 0, hi = 0;
+  hipDeviceGetStreamPriorityRange(&lo, &hi);
+  ok = ok && hipStreamCreateWithPriority(&c->sched_stream, hipStreamNonBlocking, hi) == hipSuccess;
+  if (table_mode == 1) ok = ok && hipMalloc((void**)&c->d_table, sizeof(PartTable)) == hipSuccess;
+  if (!ok) {
+    fprintf(stderr, "[gpbs-hip] ctx_create failed on device %d\n", device);
+    return nullptr;
+  }
+  std::memset(c->h_table, 0, sizeof(PartTable));
+  for (int x = 0; x < kXcds; ++x) {
+    c->h_table->owner[x] = kNoOwner;
+    c->pending[x] = kNoOwner;
+  }
+  if (c->d_table) hipMemcpy(c->d_table, c->h_table, sizeof(PartTable), hipMemcpyHostToDevice);
+  return c;
+}
+
+void gpbs_gpu_ctx_destroy(void* p) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c) return;
+  hipSetDevice(c->device);
+  hipDeviceSynchronize();
+  if (c->engine) {
+    gpbs_set_actuator_ops(c->engine, nullptr);
+    gpbs_set_counter_ops(c->engine, nullptr);
+  }
+  hipStreamDestroy(c->sched_stream);
+  hipHostFree(c->h_table);
+  hipFree(c->d_cnt);
+  hipFree(c->d_prev);
+  hipHostFree(c->h_out);
+  hipHostFree(c->h_ids);
+  hipHostFree(c->h_states);
+  hipHostFree(c->h_spin);
+  hipHostFree(c->h_dirs);
+  if (c->d_table) hipFree(c->d_table);
+  delete c;
+}
+
+// Install the GPU actuator and counter backend on an engine.
+int gpbs_gpu_attach(void* p, gpbs_engine_t* e, int device_counters, int device_adapt) {
+  GpuCtx* c = (GpuCtx*)p;
+  c->engine = e;
+  gpbs_actuator_ops_t a{};
+  a.user = c;
+  a.on_switch = act_on_switch;
+  a.on_flush = act_on_flush;
+  a.on_park = act_on_park;
+  gpbs_set_actuator_ops(e, &a);
+  gpbs_counter_ops_t k{};
+  k.user = c;
+  if (device_counters) k.tenant_deltas = ctr_tenant_deltas;
+  if (device_adapt) k.adapt_batch = ctr_adapt_batch;
+  gpbs_set_counter_ops(e, &k);
+  return 0;
+}
+
+void* gpbs_gpu_table(void* p) { return ((GpuCtx*)p)->table_mode == 1 ? (void*)((GpuCtx*)p)->d_table : (void*)((GpuCtx*)p)->h_table; }
+void* gpbs_gpu_counters(void* p) { return ((GpuCtx*)p)->d_cnt; }
+
+int gpbs_gpu_set_owners(void* p, const int* owners) {
+  GpuCtx* c = (GpuCtx*)p;
+  for (int x = 0; x < kXcds; ++x) c->pending[x] = owners[x] >= 0 ? (u32)owners[x] : kNoOwner;
+  publish(c);
+  return 0;
+}
+
+int gpbs_gpu_get_owners(void* p, int* owners) {
+  GpuCtx* c = (GpuCtx*)p;
+  for (int x = 0; x < kXcds; ++x) {
+    u32 o = __atomic_load_n(&c->h_table->owner[x], __ATOMIC_ACQUIRE);
+    owners[x] = o == kNoOwner ? -1 : (int)o;
+  }
+  return (int)c->h_table->epoch;
+}
+
+// Cumulative counters of a tenant summed over XCDs (synchronous; tests/tools).
+int gpbs_gpu_read_counters(void* p, int tenant, uint64_t* out4, uint64_t* per_xcd32) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (tenant < 0 || tenant >= kMaxTenants) return -22;
+  u64 buf[kXcds * kNumPmc];
+  HIPCHECK(hipMemcpy(buf, c->d_cnt + (size_t)tenant * kXcds * kNumPmc, sizeof(buf), hipMemcpyDeviceToHost));
+  for (int i = 0; i < 4; ++i) {
+    out4[i] = 0;
+    for (int x = 0; x < kXcds; ++x) out4[i] += buf[x * 4 + i];
+  }
+  if (per_xcd32) std::memcpy(per_xcd32, buf, sizeof(buf));
+  return 0;
+}
+
+int gpbs_gpu_stats(void* p, uint64_t* out4) {
+  GpuCtx* c = (GpuCtx*)p;
+  out4[0] = c->switches.load();
+  out4[1] = c->flushes.load();
+  out4[2] = c->metric_calls.load();
+  out4[3] = (uint64_t)c->metric_ns;
+  return 0;
+}
+
+// CU-masked stream for foreign kernels (torch/hipBLASLt/RCCL tenants): a
+// stream whose hardware queue only dispatches to the CUs in `cu_mask`
+// (nwords x 32 bits, hipExtStreamCreateWithCUMask).
+void* gpbs_gpu_cumask_stream(int device, const uint32_t* cu_mask, int nwords, int priority) {
+  hipSetDevice(device);
+  hipStream_t s = nullptr;
+  if (hipExtStreamCreateWithCUMask(&s, (uint32_t)nwords, cu_mask) != hipSuccess) return nullptr;
+  (void)priority;
+  return (void*)s;
+}
+
+int gpbs_gpu_stream_destroy(void* s) { return hipStreamDestroy((hipStream_t)s) == hipSuccess ? 0 : -5; }
+
+void* gpbs_runner_create(void* ctx, const gpbs_runner_cfg_t* cfg) {
+  GpuCtx* c = (GpuCtx*)ctx;
+  if (!c || !cfg || cfg->tenant < 0 || cfg->tenant >= kMaxTenants) return nullptr;
+  if (cfg->kind == K_GEMM && (cfg->M % 128 || cfg->N % 128 || cfg->K % 64)) return nullptr;
+  if ((cfg->kind == K_STREAM || cfg->kind == K_REDUCE) && (cfg->bytes % 16 || cfg->chunk_bytes <= 0 || cfg->chunk_bytes % 16))
+    return nullptr;
+  if (cfg->kind == K_GEMV && cfg->K % 512) return nullptr;
+  hipSetDevice(c->device);
+  auto* r = new Runner;
+  r->ctx = c;
+  r->cfg = *cfg;
+  if (r->cfg.depth <= 0) r->cfg.depth = 2;
+  if (r->cfg.depth > 8) r->cfg.depth = 8;
+  r->nq = r->cfg.depth + 1;
+  int lo = 0, hi = 0;
+  hipDeviceGetStreamPriorityRange(&lo, &hi);
+  bool ok = hipStreamCreateWithPriority(&r->stream, hipStreamNonBlocking, cfg->priority ? hi : lo) == hipSuccess;
+  ok = ok && hipMalloc((void**)&r->d_q, sizeof(WorkQueue) * r->nq) == hipSuccess;
+  ok = ok && hipHostMalloc((void**)&r->h_status, sizeof(u32) * r->nq, hipHostMallocCoherent | hipHostMallocMapped) ==
+                 hipSuccess;
+  for (int i = 0; i < r->nq && ok; ++i) ok = hipEventCreateWithFlags(&r->ev[i], hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
+    delete r;
+    return nullptr;
+  }
+  r->th = std::thread([r] { r->loop(); });
+  return r;
+}
+
+int gpbs_runner_submit(void* p, int units) {
+  Runner* r = (Runner*)p;
+  const int64_t t = mono_ns();
+  {
+    std::lock_guard<std::mutex> g(r->mu);
+    r->pending += units;
+    r->st.submitted += units;
+    for (int i = 0; i < units; ++i) r->submit_times.push_back(t);
+  }
+  r->cv.notify_all();
+  return 0;
+}
+
+// Block until every submitted unit has completed. Returns 0, or -110 on timeout.
+int gpbs_runner_wait(void* p, int64_t timeout_ns) {
+  Runner* r = (Runner*)p;
+  std::unique_lock<std::mutex> lk(r->mu);
+  auto pred = [&] { return (r->pending <= 0 && r->inflight <= 0) || r->stop; };
+  if (timeout_ns <= 0) {
+    r->idle_cv.wait(lk, pred);
+    return r->err;
+  }
+  return r->idle_cv.wait_for(lk, std::chrono::nanoseconds(timeout_ns), pred) ? r->err : -110;
+}
+
+int gpbs_runner_stats(void* p, gpbs_runner_stats_t* out) {
+  Runner* r = (Runner*)p;
+  std::lock_guard<std::mutex> g(r->mu);
+  *out = r->st;
+  return 0;
+}
+
+// Copy up to max latency samples (ns); returns count.
+int gpbs_runner_latencies(void* p, int64_t* out, int max, int clear) {
+  Runner* r = (Runner*)p;
+  std::lock_guard<std::mutex> g(r->mu);
+  int n = (int)std::min<size_t>(r->lats.size(), (size_t)max);
+  if (out) std::memcpy(out, r->lats.data(), sizeof(int64_t) * n);
+  if (clear) {
+    r->lats.clear();
+    r->st.lat_sum_ns = r->st.lat_max_ns = 0;
+    r->st.lat_count = 0;
+  }
+  return n;
+}
+
+int gpbs_runner_reset_stats(void* p) {
+  Runner* r = (Runner*)p;
+  std::lock_guard<std::mutex> g(r->mu);
+  const uint64_t sub = r->st.submitted - r->st.units_done;
+  r->st = gpbs_runner_stats_t{};
+  r->st.submitted = sub;
+  r->lats.clear();
+  return 0;
+}
+
+int gpbs_runner_set_gate(void* p, int gate) {
+  Runner* r = (Runner*)p;
+  std::lock_guard<std::mutex> g(r->mu);
+  r->cfg.gate = gate;
+  return 0;
+}
+
+int gpbs_runner_set_engine_wake(void* p, int on) {
+  Runner* r = (Runner*)p;
+  std::lock_guard<std::mutex> g(r->mu);
+  r->cfg.engine_wake = on;
+  return 0;
+}
+
+void* gpbs_runner_stream(void* p) { return ((Runner*)p)->stream; }
+
+void gpbs_runner_destroy(void* p) {
+  Runner* r = (Runner*)p;
+  if (!r) return;
+  {
+    std::lock_guard<std::mutex> g(r->mu);
+    r->stop = true;
+  }
+  r->cv.notify_all();
+  r->ctx->cv.notify_all();
+  if (r->th.joinable()) r->th.join();
+  hipStreamSynchronize(r->stream);
+  for (int i = 0; i < r->nq; ++i) hipEventDestroy(r->ev[i]);
+  hipStreamDestroy(r->stream);
+  hipFree(r->d_q);
+  hipHostFree(r->h_status);
+  delete r;
+}
+
+}  // extern "C"

@@ -1,0 +1,220 @@
+/* libgpbs — stable C ABI of the gpbs co-scheduler (the libxl/libxc analog).
+ *
+ * Terminology map:  domain -> tenant, vCPU -> slot,
+ * pCPU -> partition (an XCD-aligned CU group of one GPU), cpupool -> pool.
+ *
+ * Reference control surface: X:tools/libxl/libxl.c:3987-4116 (sched params),
+ * X:xen/include/public/sysctl.h:568-579 (tslice/ratelimit ABI),
+ * X:xen/include/public/domctl.h:309-329 (weight/cap).
+ */
+#ifndef GPBS_H
+#define GPBS_H
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GPBS_ABI_VERSION 1
+
+/* Validation ranges (sysctl.h:568-579, libxl.c:4026-4101). Q1: the new API
+ * also accepts the reference's boot default of 100us (see docs). */
+#define GPBS_TSLICE_UMIN 100
+#define GPBS_TSLICE_UMAX 1000000
+#define GPBS_TSLICE_XL_UMIN 1000
+#define GPBS_RATELIMIT_MIN 100
+#define GPBS_RATELIMIT_MAX 500000
+#define GPBS_WEIGHT_DEFAULT 256
+#define GPBS_WEIGHT_MAX 65535
+
+/* Error codes (negative errno style, mirrored in pbs_amd/core/errors.py). */
+#define GPBS_OK 0
+#define GPBS_EINVAL -22
+#define GPBS_ENOENT -2
+#define GPBS_EBUSY -16
+#define GPBS_ENOMEM -12
+#define GPBS_ERANGE -34
+#define GPBS_ENOSPC -28
+#define GPBS_EEXIST -17
+
+typedef struct gpbs_adapt_params {
+  uint32_t threshold, band_lo, band_hi, min_us, max_us, inc_us, dec_us, switch_boundary;
+  uint32_t ticks_per_tslice, spin_floor, scale, strict_ref, reserved;
+} gpbs_adapt_params_t;
+
+typedef struct gpbs_atc_params {
+  uint32_t default_us, min_us, max_us, zero_step_us, climb_step_us, climb_floor_us, base_us, slope_us,
+      alpha, warmup, apply_period_us, reserved;
+} gpbs_atc_params_t;
+
+/* Boot parameters (level-1 config; X:xen/common/schedule.c:39-54,
+ * X:xen/common/sched_credit.c:124-127,545,728). */
+typedef struct gpbs_boot_params {
+  char sched[16];              /* "credit" (PBS adaptive credit, default), "credit-fixed", "atc", "static" */
+  int32_t tslice_us;           /* sched_credit_tslice_us, default 100 */
+  int32_t ratelimit_us;        /* sched_ratelimit_us, default 1000 (clamped to tslice) */
+  int32_t smt_power_savings;   /* sched_smt_power_savings */
+  int32_t tickle_one_idle;     /* tickle_one_idle_cpu, default 1 */
+  int32_t default_yield;       /* sched_credit_default_yield */
+  int32_t migration_delay_us;  /* vcpu_migration_delay */
+  int32_t metric_period_us;    /* CSCHED_METRIC_TICK_PERIOD, default 1000 */
+  int32_t slice_apply_us;      /* CSCHED_TIME_APPLY, default 3000 */
+  int32_t sim_clock;           /* 1 = deterministic simulated clock (tests / replay) */
+  int32_t pmu_refresh_us;      /* 1111: tick-vs-metric PMU refresh split (sched_credit.c:456,1538) */
+  int32_t dom0_quirk;          /* 1 = reference credit ceiling for tenant 0 (P1g) */
+  int32_t heartbeat_timeout_us;/* 0 = off; tenants missing heartbeats are reaped */
+  int32_t trace_capacity;      /* trace ring records (power of two), default 65536 */
+  gpbs_adapt_params_t adapt;
+  gpbs_atc_params_t atc;
+} gpbs_boot_params_t;
+
+typedef struct gpbs_engine gpbs_engine_t;
+
+/* Per-tenant adaptation state (device/host shared layout, see adapt.h). */
+typedef struct gpbs_filter_entry { uint64_t spin, inst, miss; } gpbs_filter_entry_t;
+typedef struct gpbs_adapt_state {
+  uint32_t tslice_us, tick_period_us, window_left, stable_count, phase;
+  int32_t last_err;
+  int64_t last_curr, last_win;
+  gpbs_filter_entry_t filter[5];
+} gpbs_adapt_state_t;
+
+/* Counter backend (vPMU analog).  All callbacks run under the engine lock. */
+typedef struct gpbs_counter_ops {
+  void* user;
+  /* pmu_save_regs analog: refresh cumulative pmc[4] of a slot. may be NULL */
+  int (*slot_refresh)(void* user, int slot_id, int tenant, int partition, uint64_t* pmc);
+  /* Tenant-delta mode: deltas since the previous call for n tenants (out[4*n]).
+   * When non-NULL it replaces the per-slot pmc reduction. */
+  int (*tenant_deltas)(void* user, int n, const int* tenants, uint64_t* out);
+  /* Optional batched adaptation (device kernel).  Updates states in place. */
+  int (*adapt_batch)(void* user, int n, const int* tenants, const uint64_t* deltas, const uint64_t* spin_sum,
+                     const uint64_t* spin_cnt, gpbs_adapt_state_t* states, const gpbs_adapt_params_t* p);
+} gpbs_counter_ops_t;
+
+/* Actuator (context switch analog).  on_switch is called for every partition
+ * switch; on_flush once after each batch of engine work (one device-side
+ * partition table update per batch). */
+typedef struct gpbs_actuator_ops {
+  void* user;
+  void (*on_switch)(void* user, int partition, int prev_tenant, int next_tenant, int next_slot, int32_t quantum_us,
+                    int64_t now_ns);
+  void (*on_flush)(void* user, int64_t now_ns);
+  void (*on_park)(void* user, int tenant, int slot, int parked);
+} gpbs_actuator_ops_t;
+
+/* Trace record (32 B), see csrc/obs/trace.h for event codes. */
+typedef struct gpbs_trace_record {
+  uint64_t t_ns;
+  uint32_t event, cpu;
+  uint32_t a[4];
+} gpbs_trace_record_t;
+
+typedef struct gpbs_tenant_info {
+  int32_t id, pool, nslots, weight, cap, paused, alive, active_slots;
+  uint32_t tslice_us, tick_period_us, phase, window_left;
+  int32_t last_err;
+  int32_t reserved;
+  int64_t last_curr, last_win;
+  uint64_t pmc[4];          /* last per-tenant deltas (INST, CYC, REF, MISS) */
+  uint64_t cache_miss_rate, cpi; /* per 100k inst, per 1k inst */
+  uint64_t spin_latency, report_count, pending_requests, sched_count;
+  int64_t run_ns;           /* total running time across slots */
+  char name[64];
+} gpbs_tenant_info_t;
+
+typedef struct gpbs_slot_info {
+  int32_t id, tenant, index, processor, pri, flags, runstate, is_running, credit, on_runq;
+  uint64_t pmc[4];
+  uint64_t sched_count;
+  int64_t run_ns, runnable_ns, blocked_ns;
+  uint64_t affinity[4];
+} gpbs_slot_info_t;
+
+typedef struct gpbs_partition_info {
+  int32_t id, gpu, xcd, pool, curr_tenant, curr_slot, runq_len, idle;
+  uint64_t switches;
+} gpbs_partition_info_t;
+
+/* --- lifecycle --- */
+void gpbs_boot_defaults(gpbs_boot_params_t* p);
+gpbs_engine_t* gpbs_engine_create(const gpbs_boot_params_t* p);
+void gpbs_engine_destroy(gpbs_engine_t* e);
+int gpbs_abi_version(void);
+const char* gpbs_strerror(int err);
+
+/* --- topology / pools (cpupool analog, X:xen/common/cpupool.c) --- */
+int gpbs_partition_add(gpbs_engine_t* e, int gpu, int xcd);       /* -> partition id, free (no pool) */
+int gpbs_pool_create(gpbs_engine_t* e, const char* name, const char* sched); /* -> pool id */
+int gpbs_pool_destroy(gpbs_engine_t* e, int pool);
+int gpbs_pool_rename(gpbs_engine_t* e, int pool, const char* name);
+int gpbs_pool_find(gpbs_engine_t* e, const char* name);
+int gpbs_pool_assign(gpbs_engine_t* e, int pool, int partition);   /* cpupool-cpu-add */
+int gpbs_pool_unassign(gpbs_engine_t* e, int pool, int partition); /* cpupool-cpu-remove */
+int gpbs_pool_info(gpbs_engine_t* e, int pool, char* name, int name_len, char* sched, int sched_len,
+                   uint64_t* mask4, int* n_tenants);
+int gpbs_pool_list(gpbs_engine_t* e, int* ids, int max);
+int gpbs_partition_info(gpbs_engine_t* e, int partition, gpbs_partition_info_t* out);
+int gpbs_num_partitions(gpbs_engine_t* e);
+
+/* --- tenants / slots (domain/vcpu analog) --- */
+int gpbs_tenant_create(gpbs_engine_t* e, const char* name, int pool, int nslots, int weight, int cap);
+int gpbs_tenant_destroy(gpbs_engine_t* e, int tenant);
+int gpbs_tenant_find(gpbs_engine_t* e, const char* name);
+int gpbs_tenant_list(gpbs_engine_t* e, int* ids, int max);
+int gpbs_tenant_move(gpbs_engine_t* e, int tenant, int pool);      /* cpupool-migrate */
+int gpbs_tenant_pause(gpbs_engine_t* e, int tenant);
+int gpbs_tenant_unpause(gpbs_engine_t* e, int tenant);
+int gpbs_tenant_set_nslots(gpbs_engine_t* e, int tenant, int nslots); /* vcpu-set: online count */
+int gpbs_slot_id(gpbs_engine_t* e, int tenant, int index);
+int gpbs_slot_wake(gpbs_engine_t* e, int tenant, int index);      /* index -1: all slots */
+int gpbs_slot_block(gpbs_engine_t* e, int tenant, int index);     /* index -1: all slots */
+int gpbs_slot_yield(gpbs_engine_t* e, int tenant, int index);
+int gpbs_slot_pin(gpbs_engine_t* e, int tenant, int index, const uint64_t* mask4); /* vcpu-pin */
+int gpbs_tenant_info(gpbs_engine_t* e, int tenant, gpbs_tenant_info_t* out);
+int gpbs_slot_info(gpbs_engine_t* e, int slot, gpbs_slot_info_t* out);
+int gpbs_tenant_adapt_state(gpbs_engine_t* e, int tenant, gpbs_adapt_state_t* out, int set);
+int gpbs_tenant_heartbeat(gpbs_engine_t* e, int tenant);
+
+/* --- scheduler control (sched-credit) --- */
+int gpbs_sched_credit_get(gpbs_engine_t* e, int tenant, int* weight, int* cap);
+int gpbs_sched_credit_set(gpbs_engine_t* e, int tenant, int weight, int cap); /* -1 = leave */
+int gpbs_sched_params_get(gpbs_engine_t* e, int pool, int* tslice_us, int* ratelimit_us);
+int gpbs_sched_params_set(gpbs_engine_t* e, int pool, int tslice_us, int ratelimit_us);
+int gpbs_sched_name(gpbs_engine_t* e, int pool, char* out, int len);
+
+/* --- paravirtual report channel (vcrd_op analog, P2) --- */
+int gpbs_report_wait(gpbs_engine_t* e, int tenant, uint64_t wait_ns, int kind);
+int gpbs_report_requests(gpbs_engine_t* e, int tenant, uint64_t n); /* pending_requests (P7) */
+
+/* --- counters / actuation backends --- */
+int gpbs_set_counter_ops(gpbs_engine_t* e, const gpbs_counter_ops_t* ops);
+int gpbs_set_actuator_ops(gpbs_engine_t* e, const gpbs_actuator_ops_t* ops);
+int gpbs_slot_set_pmc(gpbs_engine_t* e, int slot, const uint64_t* pmc4); /* fake/replay source */
+
+/* --- time --- */
+int64_t gpbs_now(gpbs_engine_t* e);
+int gpbs_advance(gpbs_engine_t* e, int64_t now_ns);  /* sim clock: run all events <= now */
+int gpbs_start(gpbs_engine_t* e);                     /* real clock: start dispatcher thread */
+int gpbs_stop(gpbs_engine_t* e);
+int gpbs_poll(gpbs_engine_t* e);                      /* real clock: run due events once */
+int64_t gpbs_next_event(gpbs_engine_t* e);
+
+/* --- observability --- */
+int gpbs_debug_keys(gpbs_engine_t* e, const char* keys, char* out, int len); /* r q z t ... */
+int gpbs_dmesg(gpbs_engine_t* e, char* out, int len, int clear);
+int gpbs_trace_read(gpbs_engine_t* e, uint64_t* cursor, gpbs_trace_record_t* out, int max, uint64_t* lost);
+int gpbs_trace_set_mask(gpbs_engine_t* e, uint64_t mask);
+int gpbs_trace_emit(gpbs_engine_t* e, uint32_t event, uint32_t cpu, uint32_t a0, uint32_t a1, uint32_t a2,
+                    uint32_t a3);
+int gpbs_perfc_count(void);
+const char* gpbs_perfc_name(int i);
+int gpbs_perfc_read(gpbs_engine_t* e, uint64_t* out, int max);
+int gpbs_perfc_reset(gpbs_engine_t* e);
+int gpbs_check_invariants(gpbs_engine_t* e, char* out, int len); /* CSCHED_VCPU_CHECK analog; 0 = ok */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPBS_H */

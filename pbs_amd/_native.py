@@ -1,0 +1,272 @@
+"""ctypes bindings to the native libraries (libgpbs.so, libgpbs_hip.so).
+
+The C ABI is declared in csrc/include/gpbs/gpbs.h; struct layouts here mirror
+it field for field.  Libraries are loaded from the in-tree ``pbs_amd/lib``
+(built by ``pbs_amd.build``) so GPU runs always load the in-tree ``.so``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+LIBDIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+
+u32, i32, u64, i64 = C.c_uint32, C.c_int32, C.c_uint64, C.c_int64
+
+
+class AdaptParams(C.Structure):
+    _fields_ = [(n, u32) for n in ("threshold", "band_lo", "band_hi", "min_us", "max_us", "inc_us", "dec_us",
+                                   "switch_boundary", "ticks_per_tslice", "spin_floor", "scale", "strict_ref",
+                                   "reserved")]
+
+
+class AtcParams(C.Structure):
+    _fields_ = [(n, u32) for n in ("default_us", "min_us", "max_us", "zero_step_us", "climb_step_us",
+                                   "climb_floor_us", "base_us", "slope_us", "alpha", "warmup", "apply_period_us",
+                                   "reserved")]
+
+
+class BootParams(C.Structure):
+    _fields_ = [("sched", C.c_char * 16)] + [(n, i32) for n in (
+        "tslice_us", "ratelimit_us", "smt_power_savings", "tickle_one_idle", "default_yield", "migration_delay_us",
+        "metric_period_us", "slice_apply_us", "sim_clock", "pmu_refresh_us", "dom0_quirk", "heartbeat_timeout_us",
+        "trace_capacity")] + [("adapt", AdaptParams), ("atc", AtcParams)]
+
+
+class FilterEntry(C.Structure):
+    _fields_ = [("spin", u64), ("inst", u64), ("miss", u64)]
+
+
+class AdaptState(C.Structure):
+    _fields_ = [("tslice_us", u32), ("tick_period_us", u32), ("window_left", u32), ("stable_count", u32),
+                ("phase", u32), ("last_err", i32), ("last_curr", i64), ("last_win", i64),
+                ("filter", FilterEntry * 5)]
+
+
+COUNTER_SLOT_REFRESH = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(u64))
+COUNTER_TENANT_DELTAS = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_int), C.POINTER(u64))
+COUNTER_ADAPT_BATCH = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_int), C.POINTER(u64), C.POINTER(u64),
+                                  C.POINTER(u64), C.POINTER(AdaptState), C.POINTER(AdaptParams))
+
+
+class CounterOps(C.Structure):
+    _fields_ = [("user", C.c_void_p), ("slot_refresh", COUNTER_SLOT_REFRESH),
+                ("tenant_deltas", COUNTER_TENANT_DELTAS), ("adapt_batch", COUNTER_ADAPT_BATCH)]
+
+
+ACT_ON_SWITCH = C.CFUNCTYPE(None, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, i32, i64)
+ACT_ON_FLUSH = C.CFUNCTYPE(None, C.c_void_p, i64)
+ACT_ON_PARK = C.CFUNCTYPE(None, C.c_void_p, C.c_int, C.c_int, C.c_int)
+
+
+class ActuatorOps(C.Structure):
+    _fields_ = [("user", C.c_void_p), ("on_switch", ACT_ON_SWITCH), ("on_flush", ACT_ON_FLUSH),
+                ("on_park", ACT_ON_PARK)]
+
+
+class TraceRecord(C.Structure):
+    _fields_ = [("t_ns", u64), ("event", u32), ("cpu", u32), ("a", u32 * 4)]
+
+
+class TenantInfo(C.Structure):
+    _fields_ = [(n, i32) for n in ("id", "pool", "nslots", "weight", "cap", "paused", "alive", "active_slots")] + \
+               [(n, u32) for n in ("tslice_us", "tick_period_us", "phase", "window_left")] + \
+               [("last_err", i32), ("reserved", i32), ("last_curr", i64), ("last_win", i64), ("pmc", u64 * 4),
+                ("cache_miss_rate", u64), ("cpi", u64), ("spin_latency", u64), ("report_count", u64),
+                ("pending_requests", u64), ("sched_count", u64), ("run_ns", i64), ("name", C.c_char * 64)]
+
+
+class SlotInfo(C.Structure):
+    _fields_ = [(n, i32) for n in ("id", "tenant", "index", "processor", "pri", "flags", "runstate",
+                                   "is_running", "credit", "on_runq")] + \
+               [("pmc", u64 * 4), ("sched_count", u64), ("run_ns", i64), ("runnable_ns", i64),
+                ("blocked_ns", i64), ("affinity", u64 * 4)]
+
+
+class PartitionInfo(C.Structure):
+    _fields_ = [(n, i32) for n in ("id", "gpu", "xcd", "pool", "curr_tenant", "curr_slot", "runq_len", "idle")] + \
+               [("switches", u64)]
+
+
+_lock = threading.Lock()
+_core = None
+_hip = None
+
+
+def _proto(lib, name, res, *args):
+    f = getattr(lib, name)
+    f.restype = res
+    f.argtypes = list(args)
+    return f
+
+
+def core_path():
+    return os.path.join(LIBDIR, "libgpbs.so")
+
+
+def hip_path():
+    return os.path.join(LIBDIR, "libgpbs_hip.so")
+
+
+def load_core(build_if_missing=True):
+    """Load libgpbs.so (builds it in-tree on first use if absent)."""
+    global _core
+    with _lock:
+        if _core is not None:
+            return _core
+        p = core_path()
+        if build_if_missing:
+            from . import build
+            build.build_core()
+        lib = C.CDLL(p, mode=C.RTLD_GLOBAL)
+        E = C.c_void_p
+        P = _proto
+        P(lib, "gpbs_boot_defaults", None, C.POINTER(BootParams))
+        P(lib, "gpbs_engine_create", E, C.POINTER(BootParams))
+        P(lib, "gpbs_engine_destroy", None, E)
+        P(lib, "gpbs_abi_version", C.c_int)
+        P(lib, "gpbs_strerror", C.c_char_p, C.c_int)
+        P(lib, "gpbs_partition_add", C.c_int, E, C.c_int, C.c_int)
+        P(lib, "gpbs_num_partitions", C.c_int, E)
+        P(lib, "gpbs_pool_create", C.c_int, E, C.c_char_p, C.c_char_p)
+        P(lib, "gpbs_pool_destroy", C.c_int, E, C.c_int)
+        P(lib, "gpbs_pool_rename", C.c_int, E, C.c_int, C.c_char_p)
+        P(lib, "gpbs_pool_find", C.c_int, E, C.c_char_p)
+        P(lib, "gpbs_pool_assign", C.c_int, E, C.c_int, C.c_int)
+        P(lib, "gpbs_pool_unassign", C.c_int, E, C.c_int, C.c_int)
+        P(lib, "gpbs_pool_info", C.c_int, E, C.c_int, C.c_char_p, C.c_int, C.c_char_p, C.c_int, C.POINTER(u64),
+          C.POINTER(C.c_int))
+        P(lib, "gpbs_pool_list", C.c_int, E, C.POINTER(C.c_int), C.c_int)
+        P(lib, "gpbs_partition_info", C.c_int, E, C.c_int, C.POINTER(PartitionInfo))
+        P(lib, "gpbs_tenant_create", C.c_int, E, C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int)
+        P(lib, "gpbs_tenant_destroy", C.c_int, E, C.c_int)
+        P(lib, "gpbs_tenant_find", C.c_int, E, C.c_char_p)
+        P(lib, "gpbs_tenant_list", C.c_int, E, C.POINTER(C.c_int), C.c_int)
+        P(lib, "gpbs_tenant_move", C.c_int, E, C.c_int, C.c_int)
+        P(lib, "gpbs_tenant_pause", C.c_int, E, C.c_int)
+        P(lib, "gpbs_tenant_unpause", C.c_int, E, C.c_int)
+        P(lib, "gpbs_tenant_set_nslots", C.c_int, E, C.c_int, C.c_int)
+        P(lib, "gpbs_slot_id", C.c_int, E, C.c_int, C.c_int)
+        P(lib, "gpbs_slot_wake", C.c_int, E, C.c_int, C.c_int)
+        P(lib, "gpbs_slot_block", C.c_int, E, C.c_int, C.c_int)
+        P(lib, "gpbs_slot_yield", C.c_int, E, C.c_int, C.c_int)
+        P(lib, "gpbs_slot_pin", C.c_int, E, C.c_int, C.c_int, C.POINTER(u64))
+        P(lib, "gpbs_tenant_info", C.c_int, E, C.c_int, C.POINTER(TenantInfo))
+        P(lib, "gpbs_slot_info", C.c_int, E, C.c_int, C.POINTER(SlotInfo))
+        P(lib, "gpbs_tenant_adapt_state", C.c_int, E, C.c_int, C.POINTER(AdaptState), C.c_int)
+        P(lib, "gpbs_tenant_heartbeat", C.c_int, E, C.c_int)
+        P(lib, "gpbs_sched_credit_get", C.c_int, E, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int))
+        P(lib, "gpbs_sched_credit_set", C.c_int, E, C.c_int, C.c_int, C.c_int)
+        P(lib, "gpbs_sched_params_get", C.c_int, E, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int))
+        P(lib, "gpbs_sched_params_set", C.c_int, E, C.c_int, C.c_int, C.c_int)
+        P(lib, "gpbs_sched_name", C.c_int, E, C.c_int, C.c_char_p, C.c_int)
+        P(lib, "gpbs_report_wait", C.c_int, E, C.c_int, u64, C.c_int)
+        P(lib, "gpbs_report_requests", C.c_int, E, C.c_int, u64)
+        P(lib, "gpbs_set_counter_ops", C.c_int, E, C.POINTER(CounterOps))
+        P(lib, "gpbs_set_actuator_ops", C.c_int, E, C.POINTER(ActuatorOps))
+        P(lib, "gpbs_slot_set_pmc", C.c_int, E, C.c_int, C.POINTER(u64))
+        P(lib, "gpbs_now", i64, E)
+        P(lib, "gpbs_advance", C.c_int, E, i64)
+        P(lib, "gpbs_start", C.c_int, E)
+        P(lib, "gpbs_stop", C.c_int, E)
+        P(lib, "gpbs_poll", C.c_int, E)
+        P(lib, "gpbs_next_event", i64, E)
+        P(lib, "gpbs_debug_keys", C.c_int, E, C.c_char_p, C.c_char_p, C.c_int)
+        P(lib, "gpbs_dmesg", C.c_int, E, C.c_char_p, C.c_int, C.c_int)
+        P(lib, "gpbs_trace_read", C.c_int, E, C.POINTER(u64), C.POINTER(TraceRecord), C.c_int, C.POINTER(u64))
+        P(lib, "gpbs_trace_set_mask", C.c_int, E, u64)
+        P(lib, "gpbs_trace_emit", C.c_int, E, u32, u32, u32, u32, u32, u32)
+        P(lib, "gpbs_perfc_count", C.c_int)
+        P(lib, "gpbs_perfc_name", C.c_char_p, C.c_int)
+        P(lib, "gpbs_perfc_read", C.c_int, E, C.POINTER(u64), C.c_int)
+        P(lib, "gpbs_perfc_reset", C.c_int, E)
+        P(lib, "gpbs_check_invariants", C.c_int, E, C.c_char_p, C.c_int)
+        # host-side adaptation helpers (oracle parity tests)
+        P(lib, "gpbs_adapt_init", None, C.POINTER(AdaptState), C.POINTER(AdaptParams), u32)
+        P(lib, "gpbs_adapt_update", C.c_int, C.POINTER(AdaptState), C.POINTER(AdaptParams), u64, u64, u64, u64)
+        # ipc: control pages, CPU counters/gates (optional components)
+        for binder in (_bind_ipc, _bind_counters):
+            try:
+                binder(lib)
+            except AttributeError:
+                pass
+        _core = lib
+        return lib
+
+
+def _bind_ipc(lib):
+    P = _proto
+    P(lib, "gpbs_ctl_create", C.c_void_p, C.c_char_p, C.c_int)
+    P(lib, "gpbs_ctl_open", C.c_void_p, C.c_char_p)
+    P(lib, "gpbs_ctl_close", None, C.c_void_p, C.c_int)
+    P(lib, "gpbs_ctl_ntenants", C.c_int, C.c_void_p)
+    P(lib, "gpbs_ctl_publish", None, C.c_void_p, C.c_int, u32, u64, u32, i32, i32, u32)
+    P(lib, "gpbs_ctl_read", C.c_int, C.c_void_p, C.c_int, C.POINTER(u32), C.POINTER(u64), C.POINTER(u32),
+      C.POINTER(i32), C.POINTER(i32), C.POINTER(u32))
+    P(lib, "gpbs_ctl_report", C.c_int, C.c_void_p, C.c_int, u64, u32, u32)
+    P(lib, "gpbs_ctl_drain", C.c_int, C.c_void_p, C.c_int, C.POINTER(u64), C.POINTER(u32), C.c_int)
+    P(lib, "gpbs_ctl_heartbeat", None, C.c_void_p, C.c_int, u64, u32)
+    P(lib, "gpbs_ctl_status", C.c_int, C.c_void_p, C.c_int, C.POINTER(u64), C.POINTER(u64), C.POINTER(u32),
+      C.POINTER(u32))
+    P(lib, "gpbs_ctl_set_counters", None, C.c_void_p, C.c_int, C.POINTER(u64))
+    P(lib, "gpbs_ctl_get_counters", None, C.c_void_p, C.c_int, C.POINTER(u64))
+    P(lib, "gpbs_ctl_wait_gate", C.c_int, C.c_void_p, C.c_int, i64)
+    P(lib, "gpbs_ctl_ring", None, C.c_void_p, C.c_int)
+    P(lib, "gpbs_ctl_doorbell_wait", C.c_int, C.c_void_p, C.c_int, i64)
+    P(lib, "gpbs_ctl_set_work", None, C.c_void_p, C.c_int, C.c_int)
+    P(lib, "gpbs_ctl_bind", C.c_int, C.c_void_p, C.c_void_p)
+
+
+def _bind_counters(lib):
+    P = _proto
+    P(lib, "gpbs_perf_open", C.c_void_p, C.c_int, C.c_int)
+    P(lib, "gpbs_perf_read", C.c_int, C.c_void_p, C.POINTER(u64))
+    P(lib, "gpbs_perf_close", None, C.c_void_p)
+    P(lib, "gpbs_perf_available", C.c_int)
+    P(lib, "gpbs_gate_create", C.c_void_p, C.c_char_p)
+    P(lib, "gpbs_gate_add_pid", C.c_int, C.c_void_p, C.c_int, C.c_int)
+    P(lib, "gpbs_gate_set", C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int)
+    P(lib, "gpbs_gate_destroy", None, C.c_void_p)
+    P(lib, "gpbs_gate_mode", C.c_int, C.c_void_p)
+    P(lib, "gpbs_attach_cpu_backend", C.c_int, C.c_void_p, C.c_void_p, C.c_void_p)
+
+
+def load_hip(required=False):
+    """Load libgpbs_hip.so.  On a GPU box (``required=True``) a missing or
+    unloadable library raises: GPU paths never silently fall back to eager
+    PyTorch."""
+    global _hip
+    with _lock:
+        if _hip is not None:
+            return _hip
+    load_core()
+    with _lock:
+        p = hip_path()
+        if not os.path.exists(p):
+            try:
+                from . import build
+                build.build_hip()
+            except Exception:
+                if required:
+                    raise
+                return None
+        try:
+            _hip = C.CDLL(p, mode=C.RTLD_GLOBAL)
+        except OSError:
+            if required:
+                raise
+            return None
+        from .ops import hipabi
+        hipabi.bind(_hip)
+        return _hip
+
+
+def check(rc, what=""):
+    """Raise GpbsError for negative return codes."""
+    if isinstance(rc, int) and rc < 0:
+        lib = load_core()
+        msg = lib.gpbs_strerror(rc).decode()
+        from .core.errors import GpbsError
+        raise GpbsError(rc, f"{what}: {msg}" if what else msg)
+    return rc

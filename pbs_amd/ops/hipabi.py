@@ -1,0 +1,66 @@
+"""ctypes prototypes of libgpbs_hip.so (csrc/hip/*.hip, csrc/hip/runtime.cpp)."""
+from __future__ import annotations
+
+import ctypes as C
+
+u32, i32, u64, i64 = C.c_uint32, C.c_int32, C.c_uint64, C.c_int64
+vp = C.c_void_p
+
+
+class RunnerCfg(C.Structure):
+    _fields_ = [(n, C.c_int) for n in ("kind", "tenant", "gate", "priority", "depth", "grid", "M", "N", "K",
+                                       "chunk_bytes", "engine_wake", "reserved")] + \
+               [("bytes", C.c_ulonglong), ("a", vp), ("b", vp), ("c", vp)]
+
+
+class RunnerStats(C.Structure):
+    _fields_ = [(n, u64) for n in ("units_done", "launches", "relaunches", "waits_owner", "submitted")] + \
+               [(n, i64) for n in ("busy_ns", "wait_owner_ns", "first_start_ns", "last_done_ns", "lat_sum_ns",
+                                   "lat_max_ns")] + [("lat_count", u64)]
+
+
+KIND = {"gemm": 1, "stream": 2, "reduce": 3, "gemv": 4}
+
+
+def _p(lib, name, res, *args):
+    f = getattr(lib, name)
+    f.restype = res
+    f.argtypes = list(args)
+
+
+def bind(lib):
+    # raw kernels
+    _p(lib, "gpbs_hip_gemm_bf16", C.c_int, vp, vp, vp, C.c_int, C.c_int, C.c_int, vp, vp, C.c_uint, C.c_uint, vp, vp,
+       C.c_int, vp)
+    _p(lib, "gpbs_hip_stream_copy", C.c_int, vp, vp, C.c_ulonglong, C.c_uint, vp, vp, C.c_uint, C.c_uint, vp, vp,
+       C.c_int, vp)
+    _p(lib, "gpbs_hip_reduce_bf16", C.c_int, vp, vp, vp, C.c_ulonglong, C.c_uint, vp, vp, C.c_uint, C.c_uint, vp, vp,
+       C.c_int, vp)
+    _p(lib, "gpbs_hip_gemv_bf16", C.c_int, vp, vp, vp, C.c_int, C.c_int, vp, vp, C.c_uint, C.c_uint, vp, vp, C.c_int,
+       vp)
+    _p(lib, "gpbs_hip_census", C.c_int, vp, C.c_int, vp, C.c_uint, C.c_uint, vp)
+    _p(lib, "gpbs_hip_partition_switch", C.c_int, vp, C.c_uint, C.POINTER(C.c_uint), vp)
+    _p(lib, "gpbs_hip_counter_reduce", C.c_int, vp, vp, vp, C.c_int, vp, vp)
+    _p(lib, "gpbs_hip_adapt", C.c_int, vp, vp, vp, vp, C.c_int, vp, vp, vp)
+    # runtime
+    _p(lib, "gpbs_gpu_ctx_create", vp, C.c_int, C.c_int, C.c_int)
+    _p(lib, "gpbs_gpu_ctx_destroy", None, vp)
+    _p(lib, "gpbs_gpu_attach", C.c_int, vp, vp, C.c_int, C.c_int)
+    _p(lib, "gpbs_gpu_table", vp, vp)
+    _p(lib, "gpbs_gpu_counters", vp, vp)
+    _p(lib, "gpbs_gpu_set_owners", C.c_int, vp, C.POINTER(C.c_int))
+    _p(lib, "gpbs_gpu_get_owners", C.c_int, vp, C.POINTER(C.c_int))
+    _p(lib, "gpbs_gpu_read_counters", C.c_int, vp, C.c_int, C.POINTER(u64), C.POINTER(u64))
+    _p(lib, "gpbs_gpu_stats", C.c_int, vp, C.POINTER(u64))
+    _p(lib, "gpbs_gpu_cumask_stream", vp, C.c_int, C.POINTER(C.c_uint32), C.c_int, C.c_int)
+    _p(lib, "gpbs_gpu_stream_destroy", C.c_int, vp)
+    _p(lib, "gpbs_runner_create", vp, vp, C.POINTER(RunnerCfg))
+    _p(lib, "gpbs_runner_submit", C.c_int, vp, C.c_int)
+    _p(lib, "gpbs_runner_wait", C.c_int, vp, i64)
+    _p(lib, "gpbs_runner_stats", C.c_int, vp, C.POINTER(RunnerStats))
+    _p(lib, "gpbs_runner_latencies", C.c_int, vp, C.POINTER(i64), C.c_int, C.c_int)
+    _p(lib, "gpbs_runner_reset_stats", C.c_int, vp)
+    _p(lib, "gpbs_runner_set_gate", C.c_int, vp, C.c_int)
+    _p(lib, "gpbs_runner_set_engine_wake", C.c_int, vp, C.c_int)
+    _p(lib, "gpbs_runner_stream", vp, vp)
+    _p(lib, "gpbs_runner_destroy", None, vp)

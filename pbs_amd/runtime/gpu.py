@@ -1,0 +1,207 @@
+"""GPU runtime: one GpuContext per MI355X, bound to the engine of that rank.
+
+* ``GpuContext`` owns the partition table (XCD -> tenant), the per-tenant
+  software counter blocks, and installs the GPU actuator + device counter
+  backend on the engine (``gpbs_gpu_attach``).
+* ``Runner`` is a native (C++) tenant worker: it owns a HIP stream and keeps
+  units of its workload in flight while its tenant owns XCDs.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import List, Optional
+
+import torch
+
+from .. import _native as N
+from ..ops import hipabi
+from ..ops.kernels import lib as hiplib
+
+XCDS = 8
+
+
+class GpuContext:
+    def __init__(self, device: int = 0, engine=None, part_base: int = 0, table_mode: str = "host",
+                 device_counters: bool = True, device_adapt: bool = True):
+        self.L = hiplib()
+        self.device = device
+        self.part_base = part_base
+        h = self.L.gpbs_gpu_ctx_create(device, part_base, 1 if table_mode == "device" else 0)
+        if not h:
+            raise RuntimeError(f"gpbs_gpu_ctx_create failed on device {device}")
+        self.h = C.c_void_p(h)
+        self.engine = None
+        if engine is not None:
+            self.attach(engine, device_counters, device_adapt)
+
+    def attach(self, engine, device_counters=True, device_adapt=True):
+        self.engine = engine
+        rc = self.L.gpbs_gpu_attach(self.h, engine.h, int(device_counters), int(device_adapt))
+        if rc:
+            raise RuntimeError("gpbs_gpu_attach failed")
+
+    @property
+    def table(self):
+        return C.c_void_p(self.L.gpbs_gpu_table(self.h))
+
+    @property
+    def counters(self):
+        return C.c_void_p(self.L.gpbs_gpu_counters(self.h))
+
+    def set_owners(self, owners: List[int]):
+        arr = (C.c_int * XCDS)(*owners)
+        return self.L.gpbs_gpu_set_owners(self.h, arr)
+
+    def owners(self) -> List[int]:
+        arr = (C.c_int * XCDS)()
+        self.L.gpbs_gpu_get_owners(self.h, arr)
+        return list(arr)
+
+    def read_counters(self, tenant: int, per_xcd=False):
+        out = (C.c_uint64 * 4)()
+        px = (C.c_uint64 * 32)()
+        rc = self.L.gpbs_gpu_read_counters(self.h, tenant, out, px)
+        if rc:
+            raise RuntimeError("read_counters failed")
+        if per_xcd:
+            return [tuple(px[x * 4:(x + 1) * 4]) for x in range(XCDS)]
+        return tuple(out)
+
+    def stats(self):
+        out = (C.c_uint64 * 4)()
+        self.L.gpbs_gpu_stats(self.h, out)
+        return {"switches": out[0], "flushes": out[1], "metric_calls": out[2], "metric_ns": out[3]}
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.gpbs_gpu_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+@dataclass
+class RunnerStats:
+    units_done: int
+    launches: int
+    relaunches: int
+    waits_owner: int
+    submitted: int
+    busy_ns: int
+    wait_owner_ns: int
+    first_start_ns: int
+    last_done_ns: int
+    lat_sum_ns: int
+    lat_max_ns: int
+    lat_count: int
+
+
+class Runner:
+    """Native tenant worker.  ``kind`` in {gemm, stream, reduce, gemv}."""
+
+    def __init__(self, ctx: GpuContext, kind: str, tenant: int, *, gate: bool = True, priority: int = 0,
+                 depth: int = 2, grid: int = 0, engine_wake: bool = True, **shape):
+        self.ctx = ctx
+        self.L = ctx.L
+        self.kind = kind
+        self.tenant = tenant
+        dev = torch.device("cuda", ctx.device)
+        g = torch.Generator(device=dev)
+        g.manual_seed(1234 + tenant)
+        cfg = hipabi.RunnerCfg()
+        cfg.kind = hipabi.KIND[kind]
+        cfg.tenant = tenant
+        cfg.gate = int(gate)
+        cfg.priority = priority
+        cfg.depth = depth
+        cfg.grid = grid
+        cfg.engine_wake = int(engine_wake)
+        self.buffers = []
+        if kind == "gemm":
+            M, Nn, K = shape.get("M", 4096), shape.get("N", 4096), shape.get("K", 4096)
+            a = torch.randn(M, K, device=dev, dtype=torch.bfloat16, generator=g)
+            b = torch.randn(Nn, K, device=dev, dtype=torch.bfloat16, generator=g)
+            c = torch.empty(M, Nn, device=dev, dtype=torch.bfloat16)
+            cfg.M, cfg.N, cfg.K = M, Nn, K
+            self.work_per_unit = 2.0 * M * Nn * K  # FLOP
+            self.unit_name = "FLOP"
+        elif kind in ("stream", "reduce"):
+            nbytes = int(shape.get("bytes", 1 << 30))
+            chunk = int(shape.get("chunk_bytes", 1 << 19))
+            cfg.bytes = nbytes
+            cfg.chunk_bytes = chunk
+            n = nbytes // 2
+            a = torch.randn(n, device=dev, dtype=torch.bfloat16, generator=g)
+            b = torch.randn(n, device=dev, dtype=torch.bfloat16, generator=g) if kind == "reduce" else None
+            c = torch.empty(n, device=dev, dtype=torch.bfloat16)
+            self.work_per_unit = float(nbytes * (2 if kind == "stream" else 3))  # bytes moved
+            self.unit_name = "B"
+        elif kind == "gemv":
+            R, K = shape.get("M", 8192), shape.get("K", 8192)
+            a = torch.randn(R, K, device=dev, dtype=torch.bfloat16, generator=g)
+            b = torch.randn(K, device=dev, dtype=torch.bfloat16, generator=g)
+            c = torch.empty(R, device=dev, dtype=torch.float32)
+            cfg.M, cfg.K = R, K
+            self.work_per_unit = float(R * K * 2)
+            self.unit_name = "B"
+        else:
+            raise ValueError(kind)
+        for t in (a, b, c):
+            if t is not None:
+                self.buffers.append(t)
+        cfg.a = a.data_ptr()
+        cfg.b = b.data_ptr() if b is not None else None
+        cfg.c = c.data_ptr()
+        torch.cuda.synchronize(dev)
+        self.cfg = cfg
+        h = self.L.gpbs_runner_create(ctx.h, C.byref(cfg))
+        if not h:
+            raise RuntimeError(f"runner_create failed for {kind}")
+        self.h = C.c_void_p(h)
+
+    def submit(self, units: int = 1):
+        self.L.gpbs_runner_submit(self.h, units)
+
+    def wait(self, timeout_s: float = 0.0) -> int:
+        rc = self.L.gpbs_runner_wait(self.h, int(timeout_s * 1e9))
+        if rc == -110:
+            raise TimeoutError(f"runner {self.kind} (tenant {self.tenant}) timed out")
+        if rc:
+            raise RuntimeError(f"runner {self.kind} failed rc={rc}")
+        return rc
+
+    def stats(self) -> RunnerStats:
+        s = hipabi.RunnerStats()
+        self.L.gpbs_runner_stats(self.h, C.byref(s))
+        return RunnerStats(**{k: getattr(s, k) for k, _ in s._fields_})
+
+    def latencies(self, clear=False) -> List[int]:
+        n = self.L.gpbs_runner_latencies(self.h, None, 0, 0)
+        arr = (C.c_int64 * max(1, n))()
+        n = self.L.gpbs_runner_latencies(self.h, arr, n, int(clear))
+        return list(arr[:n])
+
+    def reset_stats(self):
+        self.L.gpbs_runner_reset_stats(self.h)
+
+    def set_gate(self, gate: bool):
+        self.L.gpbs_runner_set_gate(self.h, int(gate))
+
+    def set_engine_wake(self, on: bool):
+        self.L.gpbs_runner_set_engine_wake(self.h, int(on))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.gpbs_runner_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,178 @@
+"""PBS adaptation (Appendix A) and ATC (Appendix B): native engine vs the
+pure-Python oracle, plus golden trajectories of the reference policy.
+
+Reference: X:xen/common/sched_credit.c:286-389, X:xen/common/sched_credit_atc.c:241-501.
+"""
+import ctypes as C
+import random
+
+import pytest
+
+from pbs_amd import _native as N
+from pbs_amd.core import oracle as O
+from pbs_amd.core.engine import Engine, boot_params
+
+
+def native_params(**kw):
+    bp = boot_params()
+    p = N.AdaptParams()
+    C.memmove(C.byref(p), C.byref(bp.adapt), C.sizeof(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def native_step(lib, s, p, inst, miss, ss=0, sc=0):
+    r = lib.gpbs_adapt_update(C.byref(s), C.byref(p), inst, miss, ss, sc)
+    return (r & 3) - 1, bool(r & 4)
+
+
+def same(ns: N.AdaptState, os_: O.AdaptState):
+    assert ns.tslice_us == os_.tslice_us
+    assert ns.tick_period_us == os_.tick_period_us
+    assert ns.window_left == os_.window_left
+    assert ns.stable_count == os_.stable_count
+    assert ns.phase == os_.phase
+    for i in range(5):
+        assert [ns.filter[i].spin, ns.filter[i].inst, ns.filter[i].miss] == list(os_.filter[i])
+
+
+@pytest.mark.parametrize("strict", [0, 1])
+@pytest.mark.parametrize("seed", range(6))
+def test_native_adapt_matches_oracle_random(seed, strict):
+    lib = N.load_core()
+    p = native_params(strict_ref=strict)
+    op = O.AdaptParams(strict_ref=strict)
+    s = N.AdaptState()
+    lib.gpbs_adapt_init(C.byref(s), C.byref(p), 100)
+    os_ = O.AdaptState.initial(op)
+    rng = random.Random(seed)
+    for _ in range(400):
+        mode = rng.random()
+        inst = 0 if mode < 0.05 else rng.randint(1, 10 ** rng.randint(3, 11))
+        ratio = rng.choice([10 ** 7, 2000, 1000, 999, 500, 100, 10])
+        miss = inst // ratio if ratio else 0
+        if rng.random() < 0.1:
+            miss = rng.randint(0, 10 ** 6)
+        ss, sc = rng.randint(0, 200000), rng.randint(0, 5)
+        d1 = native_step(lib, s, p, inst, miss, ss, sc)
+        d2 = O.adapt_update(os_, op, inst, miss, ss, sc)
+        assert d1 == d2
+        same(s, os_)
+
+
+def test_warmup_then_cache_sensitive_grows_to_max():
+    """Stable high miss rate (>= 1 MPKI): +100us per tick up to 1100us."""
+    p = O.AdaptParams()
+    s = O.AdaptState.initial(p)
+    traj = []
+    for _ in range(20):
+        O.adapt_update(s, p, 1_000_000, 5_000)  # 500 per 100k >= 100
+        traj.append(s.tslice_us)
+    # warm-up (5 samples, curr >= THR: no change) then +100 each stable tick
+    assert traj[:5] == [100] * 5
+    assert traj[5:15] == list(range(200, 1200, 100))
+    assert traj[15:] == [1100] * 5
+    assert s.phase == O.PHASE_LOW
+    assert s.tick_period_us == 1100 // 3
+
+
+def test_low_miss_shrinks_to_floor_and_divide_path():
+    p = O.AdaptParams()
+    s = O.AdaptState.initial(p, tslice_us=3000)
+    seq = []
+    for _ in range(12):
+        O.adapt_update(s, p, 1_000_000, 50)  # 5 per 100k < 100 (and > 0)
+        seq.append(s.tslice_us)
+    # >= 2700: /3 in 100us units; then -200 down to 100
+    assert seq[0] == 1000 and seq[1] == 800 and seq[2] == 600
+    assert seq[-1] == 100
+    assert s.phase == O.PHASE_HIGH
+
+
+def test_phase_change_rearms_window():
+    p = O.AdaptParams()
+    s = O.AdaptState.initial(p)
+    for _ in range(8):
+        O.adapt_update(s, p, 1_000_000, 5_000)
+    t = s.tslice_us
+    d, rearm = O.adapt_update(s, p, 1_000_000, 50_000)  # err = 1000% > 130 but win >= THR -> stable
+    assert not rearm
+    s2 = O.AdaptState.initial(p)
+    for _ in range(8):
+        O.adapt_update(s2, p, 1_000_000, 500)  # win = 50 (< THR)
+    d, rearm = O.adapt_update(s2, p, 1_000_000, 5_000)  # curr 500, win 50 -> err 1000, win < THR: unstable
+    assert rearm and s2.window_left == 4 and s2.stable_count == 0
+    assert s2.filter[0] == [0, 1_000_000, 5_000]
+    assert t >= 100
+
+
+def test_zero_counters_drive_minimum_quantum():
+    """PBS silently degrades to 100us when counters stay 0."""
+    p = O.AdaptParams()
+    s = O.AdaptState.initial(p, tslice_us=1100)
+    for _ in range(30):
+        O.adapt_update(s, p, 0, 0)
+    assert s.tslice_us == 100
+
+
+def test_engine_metric_tick_drives_adaptation_from_slot_pmcs():
+    """End to end in the engine (sim clock): per-slot pmc deltas summed per
+    tenant every 1 ms feed the detector; a cache-sensitive tenant's quantum
+    grows, a compute tenant's shrinks, and dispatch uses them."""
+    e = Engine(sim_clock=True, partitions=[(0, x) for x in range(2)])  # 4 slots contend for 2
+    e.tenant_create("Domain-0", nslots=1)
+    hot = e.tenant_create("hbm", nslots=2)
+    cold = e.tenant_create("gemm", nslots=2)
+    e.wake(hot)
+    e.wake(cold)
+    pm = {hot: [0, 0, 0, 0], cold: [0, 0, 0, 0]}
+    for ms in range(1, 25):
+        for t, (di, dm) in ((hot, (1_000_000, 4_000)), (cold, (1_000_000, 20))):
+            for idx in range(2):
+                sid = e.slot_id(t, idx)
+                pm[t][0] += di // 2
+                pm[t][3] += dm // 2
+                e.set_pmc(sid, pm[t])
+                pm[t] = list(pm[t])
+        e.advance(ms * 1_000_000)
+    ih, ic = e.tenant_info(hot), e.tenant_info(cold)
+    assert ih.tslice_us > 500 and ih.phase == 1
+    assert ic.tslice_us == 100 and ic.phase == 2
+    sw = [r for r in e.trace(from_start=True) if r.event == "SWITCH"]
+    quanta_hot = {r.a[2] for r in sw if r.a[1] == hot}
+    assert max(quanta_hot) > 500
+    assert e.check() == ""
+
+
+def test_native_atc_matches_oracle():
+    """ATC on the native engine vs oracle: global min re-slice every 21 ms."""
+    op = O.AtcParams()
+    e = Engine(sched="atc", sim_clock=True, partitions=[(0, x) for x in range(2)])
+    e.tenant_create("Domain-0", nslots=1)
+    ts = [e.tenant_create(f"t{i}", nslots=1) for i in range(3)]
+    for t in ts:
+        e.wake(t)
+    ostates = [O.AtcState.initial(op) for _ in ts]
+    rng = random.Random(3)
+    now = 0
+    for period in range(12):
+        for k, t in enumerate(ts):
+            for _ in range(rng.randint(0, 6)):
+                w = rng.choice([10, 900, 2000, 5000, 20000, 40000])
+                e.report_wait(t, w)
+                O.atc_report(ostates[k], op, w)
+        now += op.apply_period_us * 1000
+        e.advance(now)
+        # oracle: only tenants active in the credit sense are updated; all
+        # three are runnable so all are active.
+        mn = O.atc_apply(ostates, op)
+        assert e.sched_params_get(0)[0] == mn
+        for t in ts:
+            assert e.tenant_info(t).tslice_us == mn
+
+
+def test_atc_bucket_edges():
+    assert O.atc_bucket(0) == 1 and O.atc_bucket(1023) == 1
+    assert O.atc_bucket(1024) == 7 and O.atc_bucket(1535) == 7 and O.atc_bucket(1536) == 8
+    assert O.atc_bucket(32767) == 15 and O.atc_bucket(32768) == 16 and O.atc_bucket(10 ** 9) == 16
