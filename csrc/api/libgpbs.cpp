@@ -161,7 +161,12 @@ void gpbs_engine_destroy(gpbs_engine_t* e) {
 
 int gpbs_partition_add(gpbs_engine_t* e, int gpu, int xcd) {
   LOCK(e);
-  return e->e->partition_add(gpu, xcd);
+  return e->e->partition_add(gpu, xcd, 0);
+}
+
+int gpbs_partition_add_ctx(gpbs_engine_t* e, int gpu, int xcd, int ctx) {
+  LOCK(e);
+  return e->e->partition_add(gpu, xcd, ctx);
 }
 
 int gpbs_num_partitions(gpbs_engine_t* e) {
@@ -251,6 +256,7 @@ int gpbs_partition_info(gpbs_engine_t* e, int part, gpbs_partition_info_t* o) {
   o->id = P.id;
   o->gpu = P.gpu;
   o->xcd = P.xcd;
+  o->ctx = P.ctx;
   o->pool = P.pool;
   Slot& c = *E.slots[P.curr];
   o->curr_slot = c.is_idle() ? -1 : c.id;

@@ -23,7 +23,7 @@ GPBS_HD int64_t rate_int(uint64_t v, const P& p) { return p.strict_ref ? (int64_
 
 template <class P>
 GPBS_HD uint32_t dec(uint32_t t, const P& p) {
-  if (t >= p.switch_boundary * 3) return t / 300 * 100;
+  if (t >= p.switch_boundary * 3) return t / (3 * p.inc_us) * p.inc_us;  // /3 in quantum units (reference: /300*100)
   return t >= p.min_us + p.dec_us ? t - p.dec_us : p.min_us;
 }
 

@@ -716,6 +716,54 @@ class CreditScheduler : public Scheduler {
     return snext;
   }
 
+  // Contention-aware sibling selection (gpbs extension of _csched_cpu_pick's
+  // SMT awareness): the two issue contexts of an XCD run concurrently and
+  // share its CUs, L2 and the HBM path.  Among runnable slots of the head's
+  // priority class, prefer one whose tenant is not memory-bound when a sibling
+  // context already runs a memory-bound tenant (PBS miss-rate classification),
+  // and never double-book a tenant on both contexts of one XCD.
+  bool mem_bound(int tenant) {
+    if (tenant < 0) return false;
+    Tenant* t = E.tenant(tenant);
+    return t && t->priv && sd(*t).cache_miss_rate >= E.adapt_params.threshold;
+  }
+  int conflict(const Slot& v, int cpu) {
+    int score = 0;
+    const Partition& P = *E.parts[cpu];
+    for (int c = cpus_.first(); c >= 0; c = cpus_.next(c + 1)) {
+      if (c == cpu) continue;
+      const Partition& Q = *E.parts[c];
+      if (Q.gpu != P.gpu || Q.xcd != P.xcd) continue;
+      const int st = E.slots[Q.curr]->tenant;
+      if (st < 0) continue;
+      if (st == v.tenant)
+        score += 2;
+      else if (mem_bound(st) && mem_bound(v.tenant))
+        score += 1;
+    }
+    return score;
+  }
+  Slot* cosched_pick(int cpu) {
+    auto& rq = pc(cpu).runq;
+    Slot& head = *E.slots[rq.front()];
+    const int16_t pri0 = sv(head).pri;
+    int best_score = conflict(head, cpu);
+    if (best_score == 0) return nullptr;
+    Slot* best = nullptr;
+    for (int sid : rq) {
+      Slot& v = *E.slots[sid];
+      if (sv(v).pri != pri0) break;
+      if (v.is_idle()) continue;
+      int s = conflict(v, cpu);
+      if (s < best_score) {
+        best_score = s;
+        best = &v;
+        if (s == 0) break;
+      }
+    }
+    return best;
+  }
+
   TaskSlice do_schedule(int cpu, int64_t now) override {
     Slot& scurr = curr(cpu);
     CSlot& cs = sv(scurr);
@@ -742,6 +790,13 @@ class CreditScheduler : public Scheduler {
       if (E.runnable(scurr)) runq_insert(cpu, scurr);
       auto& rq = pc(cpu).runq;
       snext = E.slots[rq.front()].get();
+      if (E.boot.coschedule && !snext->is_idle()) {
+        if (Slot* alt = cosched_pick(cpu)) {  // same priority class, less contention
+          rq.remove(alt->id);
+          rq.push_front(alt->id);
+          snext = alt;
+        }
+      }
       if (cs.flags & FLAG_YIELD) cs.flags &= ~FLAG_YIELD;
       if (sv(*snext).pri > PRI_OVER)
         runq_remove(*snext);

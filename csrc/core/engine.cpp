@@ -164,12 +164,13 @@ void Engine::flush_actuation() {
 
 // --------------------------------------------------------------- lifecycle -
 
-int Engine::partition_add(int gpu, int xcd) {
+int Engine::partition_add(int gpu, int xcd, int ctx) {
   if ((int)parts.size() >= kMaxPartitions) return GPBS_ENOSPC;
   auto p = std::make_unique<Partition>();
   p->id = (int)parts.size();
   p->gpu = gpu;
   p->xcd = xcd;
+  p->ctx = ctx;
   auto idle = std::make_unique<Slot>();
   idle->id = (int)slots.size();
   idle->tenant = -1;
@@ -529,7 +530,14 @@ void Engine::schedule(int part) {
   TaskSlice ts = S->do_schedule(part, n);
   Slot& next = *slots[ts.slot];
   P.curr = next.id;
-  if (ts.time_ns >= 0) timer_set(P.s_timer, n + ts.time_ns);
+  if (ts.time_ns >= 0) {
+    int64_t when = n + ts.time_ns;
+    if (boot.quantum_align_us > 0) {  // batch switches of all partitions onto a common grid
+      const int64_t a = (int64_t)boot.quantum_align_us * 1000;
+      when = (when + a - 1) / a * a;
+    }
+    timer_set(P.s_timer, when);
+  }
   if (&prev == &next) return;  // continue_running
   const int32_t q_us = ts.time_ns >= 0 ? (int32_t)(ts.time_ns / 1000) : -1;
   emit(TRC_SWITCH, part, (uint32_t)prev.tenant, (uint32_t)next.tenant, (uint32_t)q_us);
@@ -604,7 +612,7 @@ std::string Engine::dump_runq() {
     o += fmt("Scheduler: %s (%s)\n", pl->sched->name(), pl->sched->opt_name());
     pl->sched->dump_settings(o);
     for (int c = pl->cpus.first(); c >= 0; c = pl->cpus.next(c + 1)) {
-      o += fmt("CPU[%02d] (gpu%d xcd%d) ", c, parts[c]->gpu, parts[c]->xcd);
+      o += fmt("CPU[%02d] (gpu%d xcd%d.%d) ", c, parts[c]->gpu, parts[c]->xcd, parts[c]->ctx);
       pl->sched->dump_cpu_state(c, o);
     }
   }

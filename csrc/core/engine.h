@@ -83,6 +83,7 @@ struct Partition {  // pCPU + schedule_data
   int id = -1;
   int gpu = 0;
   int xcd = 0;
+  int ctx = 0;  // issue context within the XCD (SMT-sibling analog)
   int pool = -1;
   int curr = -1;       // running slot (idle slot when idle)
   int idle_slot = -1;  // this partition's idle vCPU
@@ -188,7 +189,7 @@ class Engine {
   void flush_actuation();
 
   // --- lifecycle ---
-  int partition_add(int gpu, int xcd);
+  int partition_add(int gpu, int xcd, int ctx = 0);
   int pool_create(const std::string& name, const std::string& sched);
   int pool_destroy(int pool);
   int pool_assign(int pool, int part);

@@ -25,11 +25,18 @@ typedef unsigned long long u64;
 // by the next system-scope load of a workgroup (~1-2 us over PCIe) without a
 // copy or a kernel launch.  A device-memory copy is maintained by the
 // partition_switch kernel when GPBS_TABLE=device.
+// Each XCD exposes kCtx issue contexts (the SMT-sibling analog: two tenants'
+// waves co-reside on the XCD's CUs, one typically MFMA-bound and one
+// memory-bound).  owner[2*x + c] is the tenant running on context c of XCD x.
+constexpr int kCtx = 2;
 struct alignas(64) PartTable {
   u32 epoch;
   u32 flags;
-  u32 owner[kXcds];   // tenant id owning each XCD, kNoOwner when idle
-  u32 pad[6];
+  union {
+    u32 owner[kXcds * kCtx];  // tenant id per (XCD, context), kNoOwner when idle
+    u64 pair[kXcds];          // both contexts of an XCD in one 8-byte word
+  };
+  u32 pad[14];
 };
 
 // Work queue of one tenant kernel invocation (tile / chunk queue).
@@ -82,7 +89,9 @@ __device__ __forceinline__ u32 load_sys(const u32* p) {
 // Does tenant `me` own the XCD this workgroup runs on?
 __device__ __forceinline__ bool owns(const PartTable* t, u32 mode, u32 me, u32 xcc) {
   if (mode == GATE_NONE) return true;
-  return load_sys(&t->owner[xcc & 7]) == me;
+  // One 8-byte system-scope load covers both contexts of the XCD.
+  const u64 pair = __hip_atomic_load(&t->pair[xcc & 7], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return (u32)pair == me || (u32)(pair >> 32) == me;
 }
 
 // Per-(tenant, xcd) software counter block, accumulated at workgroup exit.

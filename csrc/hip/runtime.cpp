@@ -62,10 +62,20 @@ struct GpuCtx {
   gpbs_adapt_state_t* h_states = nullptr;
   u64* h_spin = nullptr;         // [2][kMaxTenants]
   int* h_dirs = nullptr;
+  u64* h_adelta = nullptr;        // adapt inputs (separate from the async reduce buffers)
   hipStream_t sched_stream = nullptr;
   gpbs_engine_t* engine = nullptr;
-  u32 pending[kXcds];
+  int nctx = 1;                  // issue contexts per XCD in use (1 or kCtx)
+  u32 pending[kXcds * kCtx];
   u32 epoch = 0;
+  // async counter reduce (one metric period of lag, never blocks the engine)
+  bool red_pending = false;
+  int red_n = 0;
+  int red_buf = 0;
+  int* h_ids2 = nullptr;
+  u64* h_out2 = nullptr;
+  hipEvent_t red_ev = nullptr;
+  u64 last_delta[kMaxTenants][kNumPmc];
   std::mutex mu;
   std::condition_variable cv;
   std::atomic<uint64_t> switches{0}, flushes{0}, metric_calls{0};
@@ -76,20 +86,21 @@ struct GpuCtx {
 
 void act_on_switch(void* user, int part, int, int next, int, int32_t, int64_t) {
   GpuCtx* c = (GpuCtx*)user;
-  const int x = part - c->part_base;
-  if (x < 0 || x >= kXcds) return;
-  c->pending[x] = next >= 0 ? (u32)next : kNoOwner;
+  const int i = part - c->part_base;
+  if (i < 0 || i >= kXcds * c->nctx) return;
+  const int x = i / c->nctx, ctx = i % c->nctx;
+  c->pending[x * kCtx + ctx] = next >= 0 ? (u32)next : kNoOwner;
   c->switches++;
 }
 
 void publish(GpuCtx* c) {
   bool changed = false;
-  for (int x = 0; x < kXcds; ++x)
+  for (int x = 0; x < kXcds * kCtx; ++x)
     if (__atomic_load_n(&c->h_table->owner[x], __ATOMIC_RELAXED) != c->pending[x]) changed = true;
   if (!changed) return;
   {
     std::lock_guard<std::mutex> g(c->mu);
-    for (int x = 0; x < kXcds; ++x) __atomic_store_n(&c->h_table->owner[x], c->pending[x], __ATOMIC_RELEASE);
+    for (int x = 0; x < kXcds * kCtx; ++x) __atomic_store_n(&c->h_table->owner[x], c->pending[x], __ATOMIC_RELEASE);
     c->epoch++;
     __atomic_store_n(&c->h_table->epoch, c->epoch, __ATOMIC_RELEASE);
   }
@@ -102,14 +113,37 @@ void act_on_flush(void* user, int64_t) { publish((GpuCtx*)user); }
 
 void act_on_park(void*, int, int, int) {}
 
+// Counter backend, asynchronous: tick k harvests the reduce launched at tick
+// k-1 (normally long finished) and launches the next one on the high-priority
+// scheduler stream, so the engine lock is never held across a device sync.
+// Every counted event is reported exactly once, one metric period late.
 int ctr_tenant_deltas(void* user, int n, const int* tenants, uint64_t* out) {
   GpuCtx* c = (GpuCtx*)user;
   if (n > kMaxTenants) return -22;
   const int64_t t0 = mono_ns();
-  for (int i = 0; i < n; ++i) c->h_ids[i] = tenants[i] < kMaxTenants ? tenants[i] : -1;
-  if (gpbs_hip_counter_reduce(c->d_cnt, c->d_prev, c->h_ids, n, c->h_out, c->sched_stream)) return -5;
-  if (hipStreamSynchronize(c->sched_stream) != hipSuccess) return -5;
-  std::memcpy(out, c->h_out, sizeof(u64) * 4 * n);
+  if (c->red_pending) {
+    if (hipEventQuery(c->red_ev) == hipErrorNotReady) hipEventSynchronize(c->red_ev);
+    const int* ids = c->red_buf ? c->h_ids2 : c->h_ids;
+    const u64* res = c->red_buf ? c->h_out2 : c->h_out;
+    for (int k = 0; k < c->red_n; ++k)
+      if (ids[k] >= 0 && ids[k] < kMaxTenants)
+        for (int i = 0; i < kNumPmc; ++i) c->last_delta[ids[k]][i] += res[k * kNumPmc + i];
+    c->red_pending = false;
+  }
+  for (int k = 0; k < n; ++k)
+    for (int i = 0; i < kNumPmc; ++i) {
+      const int t = tenants[k];
+      out[k * kNumPmc + i] = (t >= 0 && t < kMaxTenants) ? c->last_delta[t][i] : 0;
+      if (t >= 0 && t < kMaxTenants) c->last_delta[t][i] = 0;
+    }
+  c->red_buf ^= 1;
+  int* ids = c->red_buf ? c->h_ids2 : c->h_ids;
+  u64* res = c->red_buf ? c->h_out2 : c->h_out;
+  for (int i = 0; i < n; ++i) ids[i] = tenants[i] < kMaxTenants ? tenants[i] : -1;
+  if (gpbs_hip_counter_reduce(c->d_cnt, c->d_prev, ids, n, res, c->sched_stream)) return -5;
+  hipEventRecord(c->red_ev, c->sched_stream);
+  c->red_pending = true;
+  c->red_n = n;
   c->metric_calls++;
   c->metric_ns += mono_ns() - t0;
   return 0;
@@ -121,10 +155,10 @@ int ctr_adapt_batch(void* user, int n, const int*, const uint64_t* deltas, const
   if (n > kMaxTenants) return -22;
   const int64_t t0 = mono_ns();
   std::memcpy(c->h_states, states, sizeof(gpbs_adapt_state_t) * n);
-  std::memcpy(c->h_out, deltas, sizeof(u64) * 4 * n);
+  std::memcpy(c->h_adelta, deltas, sizeof(u64) * 4 * n);
   std::memcpy(c->h_spin, ssum, sizeof(u64) * n);
   std::memcpy(c->h_spin + kMaxTenants, scnt, sizeof(u64) * n);
-  if (gpbs_hip_adapt(c->h_states, c->h_out, c->h_spin, c->h_spin + kMaxTenants, n, p, c->h_dirs, c->sched_stream))
+  if (gpbs_hip_adapt(c->h_states, c->h_adelta, c->h_spin, c->h_spin + kMaxTenants, n, p, c->h_dirs, c->sched_stream))
     return -5;
   if (hipStreamSynchronize(c->sched_stream) != hipSuccess) return -5;
   std::memcpy(states, c->h_states, sizeof(gpbs_adapt_state_t) * n);
@@ -221,7 +255,7 @@ struct Runner {
 
   bool owns_any() {
     if (!cfg.gate) return true;
-    for (int x = 0; x < kXcds; ++x)
+    for (int x = 0; x < kXcds * kCtx; ++x)
       if (__atomic_load_n(&ctx->h_table->owner[x], __ATOMIC_ACQUIRE) == (u32)cfg.tenant) return true;
     return false;
   }
@@ -356,12 +390,14 @@ struct Runner {
 
 extern "C" {
 
-void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode) {
+void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
   if (hipSetDevice(device) != hipSuccess) return nullptr;
   auto* c = new GpuCtx;
   c->device = device;
   c->part_base = part_base;
   c->table_mode = table_mode;
+  c->nctx = nctx == kCtx ? kCtx : 1;
+  std::memset(c->last_delta, 0, sizeof(c->last_delta));
   bool ok = hipHostMalloc((void**)&c->h_table, sizeof(PartTable), hipHostMallocCoherent | hipHostMallocMapped) ==
             hipSuccess;
   ok = ok && hipMalloc((void**)&c->d_cnt, sizeof(u64) * kMaxTenants * kXcds * kNumPmc) == hipSuccess;
@@ -370,10 +406,14 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode) {
   ok = ok && hipMemset(c->d_prev, 0, sizeof(u64) * kMaxTenants * kXcds * kNumPmc) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_out, sizeof(u64) * 4 * kMaxTenants, hipHostMallocMapped) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_ids, sizeof(int) * kMaxTenants, hipHostMallocMapped) == hipSuccess;
+  ok = ok && hipHostMalloc((void**)&c->h_out2, sizeof(u64) * 4 * kMaxTenants, hipHostMallocMapped) == hipSuccess;
+  ok = ok && hipHostMalloc((void**)&c->h_ids2, sizeof(int) * kMaxTenants, hipHostMallocMapped) == hipSuccess;
+  ok = ok && hipEventCreateWithFlags(&c->red_ev, hipEventDisableTiming) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_states, sizeof(gpbs_adapt_state_t) * kMaxTenants, hipHostMallocMapped) ==
                  hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_spin, sizeof(u64) * 2 * kMaxTenants, hipHostMallocMapped) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_dirs, sizeof(int) * kMaxTenants, hipHostMallocMapped) == hipSuccess;
+  ok = ok && hipHostMalloc((void**)&c->h_adelta, sizeof(u64) * 4 * kMaxTenants, hipHostMallocMapped) == hipSuccess;
   int lo = 0, hi = 0;
   hipDeviceGetStreamPriorityRange(&lo, &hi);
   ok = ok && hipStreamCreateWithPriority(&c->sched_stream, hipStreamNonBlocking, hi) == hipSuccess;
@@ -383,7 +423,7 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode) {
     return nullptr;
   }
   std::memset(c->h_table, 0, sizeof(PartTable));
-  for (int x = 0; x < kXcds; ++x) {
+  for (int x = 0; x < kXcds * kCtx; ++x) {
     c->h_table->owner[x] = kNoOwner;
     c->pending[x] = kNoOwner;
   }
@@ -406,9 +446,13 @@ void gpbs_gpu_ctx_destroy(void* p) {
   hipFree(c->d_prev);
   hipHostFree(c->h_out);
   hipHostFree(c->h_ids);
+  hipHostFree(c->h_out2);
+  hipHostFree(c->h_ids2);
+  hipEventDestroy(c->red_ev);
   hipHostFree(c->h_states);
   hipHostFree(c->h_spin);
   hipHostFree(c->h_dirs);
+  hipHostFree(c->h_adelta);
   if (c->d_table) hipFree(c->d_table);
   delete c;
 }
@@ -431,19 +475,27 @@ int gpbs_gpu_attach(void* p, gpbs_engine_t* e, int device_counters, int device_a
   return 0;
 }
 
+// Issue contexts per XCD used by the attached engine's partitions (1 or 2).
+int gpbs_gpu_set_nctx(void* p, int nctx) {
+  GpuCtx* c = (GpuCtx*)p;
+  c->nctx = nctx == kCtx ? kCtx : 1;
+  return 0;
+}
+
 void* gpbs_gpu_table(void* p) { return ((GpuCtx*)p)->table_mode == 1 ? (void*)((GpuCtx*)p)->d_table : (void*)((GpuCtx*)p)->h_table; }
 void* gpbs_gpu_counters(void* p) { return ((GpuCtx*)p)->d_cnt; }
 
+// owners: [kXcds * kCtx] entries, (xcd, context) major, -1 = idle.
 int gpbs_gpu_set_owners(void* p, const int* owners) {
   GpuCtx* c = (GpuCtx*)p;
-  for (int x = 0; x < kXcds; ++x) c->pending[x] = owners[x] >= 0 ? (u32)owners[x] : kNoOwner;
+  for (int x = 0; x < kXcds * kCtx; ++x) c->pending[x] = owners[x] >= 0 ? (u32)owners[x] : kNoOwner;
   publish(c);
   return 0;
 }
 
 int gpbs_gpu_get_owners(void* p, int* owners) {
   GpuCtx* c = (GpuCtx*)p;
-  for (int x = 0; x < kXcds; ++x) {
+  for (int x = 0; x < kXcds * kCtx; ++x) {
     u32 o = __atomic_load_n(&c->h_table->owner[x], __ATOMIC_ACQUIRE);
     owners[x] = o == kNoOwner ? -1 : (int)o;
   }
@@ -551,8 +603,9 @@ int gpbs_runner_stats(void* p, gpbs_runner_stats_t* out) {
 int gpbs_runner_latencies(void* p, int64_t* out, int max, int clear) {
   Runner* r = (Runner*)p;
   std::lock_guard<std::mutex> g(r->mu);
+  if (!out) return (int)r->lats.size();
   int n = (int)std::min<size_t>(r->lats.size(), (size_t)max);
-  if (out) std::memcpy(out, r->lats.data(), sizeof(int64_t) * n);
+  std::memcpy(out, r->lats.data(), sizeof(int64_t) * n);
   if (clear) {
     r->lats.clear();
     r->st.lat_sum_ns = r->st.lat_max_ns = 0;

@@ -14,12 +14,15 @@
 
 namespace gpbs_hip {
 
-__global__ void k_partition_switch(PartTable* t, u32 epoch, u32 o0, u32 o1, u32 o2, u32 o3, u32 o4, u32 o5, u32 o6,
-                                   u32 o7) {
-  if (threadIdx.x != 0) return;
-  const u32 o[8] = {o0, o1, o2, o3, o4, o5, o6, o7};
-#pragma unroll
-  for (int i = 0; i < 8; ++i) __hip_atomic_store(&t->owner[i], o[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+struct Owners {
+  u32 o[kXcds * kCtx];
+};
+
+__global__ void k_partition_switch(PartTable* t, u32 epoch, Owners ow) {
+  const int i = threadIdx.x;
+  if (i < kXcds * kCtx) __hip_atomic_store(&t->owner[i], ow.o[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __syncthreads();
+  if (i != 0) return;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __hip_atomic_store(&t->epoch, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -67,8 +70,9 @@ using namespace gpbs_hip;
 extern "C" {
 
 int gpbs_hip_partition_switch(void* table, unsigned epoch, const unsigned* owners, hipStream_t s) {
-  hipLaunchKernelGGL(k_partition_switch, dim3(1), dim3(64), 0, s, (PartTable*)table, epoch, owners[0], owners[1],
-                     owners[2], owners[3], owners[4], owners[5], owners[6], owners[7]);
+  Owners ow;
+  for (int i = 0; i < kXcds * kCtx; ++i) ow.o[i] = owners[i];
+  hipLaunchKernelGGL(k_partition_switch, dim3(1), dim3(64), 0, s, (PartTable*)table, epoch, ow);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -65,6 +65,8 @@ typedef struct gpbs_boot_params {
   int32_t dom0_quirk;          /* 1 = reference credit ceiling for tenant 0 (P1g) */
   int32_t heartbeat_timeout_us;/* 0 = off; tenants missing heartbeats are reaped */
   int32_t trace_capacity;      /* trace ring records (power of two), default 65536 */
+  int32_t quantum_align_us;    /* 0 = off; round quantum expiries up to this grid (batched switches) */
+  int32_t coschedule;          /* 1 = contention-aware sibling selection (pair memory- with compute-bound) */
   gpbs_adapt_params_t adapt;
   gpbs_atc_params_t atc;
 } gpbs_boot_params_t;
@@ -133,7 +135,7 @@ typedef struct gpbs_slot_info {
 } gpbs_slot_info_t;
 
 typedef struct gpbs_partition_info {
-  int32_t id, gpu, xcd, pool, curr_tenant, curr_slot, runq_len, idle;
+  int32_t id, gpu, xcd, pool, curr_tenant, curr_slot, runq_len, idle, ctx, reserved;
   uint64_t switches;
 } gpbs_partition_info_t;
 
@@ -146,6 +148,7 @@ const char* gpbs_strerror(int err);
 
 /* --- topology / pools (cpupool analog, X:xen/common/cpupool.c) --- */
 int gpbs_partition_add(gpbs_engine_t* e, int gpu, int xcd);       /* -> partition id, free (no pool) */
+int gpbs_partition_add_ctx(gpbs_engine_t* e, int gpu, int xcd, int ctx); /* XCD issue context (sibling) */
 int gpbs_pool_create(gpbs_engine_t* e, const char* name, const char* sched); /* -> pool id */
 int gpbs_pool_destroy(gpbs_engine_t* e, int pool);
 int gpbs_pool_rename(gpbs_engine_t* e, int pool, const char* name);

@@ -31,7 +31,7 @@ class BootParams(C.Structure):
     _fields_ = [("sched", C.c_char * 16)] + [(n, i32) for n in (
         "tslice_us", "ratelimit_us", "smt_power_savings", "tickle_one_idle", "default_yield", "migration_delay_us",
         "metric_period_us", "slice_apply_us", "sim_clock", "pmu_refresh_us", "dom0_quirk", "heartbeat_timeout_us",
-        "trace_capacity")] + [("adapt", AdaptParams), ("atc", AtcParams)]
+        "trace_capacity", "quantum_align_us", "coschedule")] + [("adapt", AdaptParams), ("atc", AtcParams)]
 
 
 class FilterEntry(C.Structure):
@@ -85,7 +85,8 @@ class SlotInfo(C.Structure):
 
 
 class PartitionInfo(C.Structure):
-    _fields_ = [(n, i32) for n in ("id", "gpu", "xcd", "pool", "curr_tenant", "curr_slot", "runq_len", "idle")] + \
+    _fields_ = [(n, i32) for n in ("id", "gpu", "xcd", "pool", "curr_tenant", "curr_slot", "runq_len", "idle",
+                                   "ctx", "reserved")] + \
                [("switches", u64)]
 
 
@@ -128,6 +129,7 @@ def load_core(build_if_missing=True):
         P(lib, "gpbs_abi_version", C.c_int)
         P(lib, "gpbs_strerror", C.c_char_p, C.c_int)
         P(lib, "gpbs_partition_add", C.c_int, E, C.c_int, C.c_int)
+        P(lib, "gpbs_partition_add_ctx", C.c_int, E, C.c_int, C.c_int, C.c_int)
         P(lib, "gpbs_num_partitions", C.c_int, E)
         P(lib, "gpbs_pool_create", C.c_int, E, C.c_char_p, C.c_char_p)
         P(lib, "gpbs_pool_destroy", C.c_int, E, C.c_int)

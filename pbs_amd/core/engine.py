@@ -117,8 +117,8 @@ class Engine:
         return N.check(rc, what)
 
     # ------------------------------------------------------ topology/pools
-    def partition_add(self, gpu: int, xcd: int) -> int:
-        return self._chk(self.lib.gpbs_partition_add(self.h, gpu, xcd), "partition_add")
+    def partition_add(self, gpu: int, xcd: int, ctx: int = 0) -> int:
+        return self._chk(self.lib.gpbs_partition_add_ctx(self.h, gpu, xcd, ctx), "partition_add")
 
     @property
     def num_partitions(self) -> int:

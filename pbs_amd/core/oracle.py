@@ -70,7 +70,7 @@ def _cdiv(a: int, b: int) -> int:
 
 def dec(t: int, p: AdaptParams) -> int:
     if t >= p.switch_boundary * 3:
-        return t // 300 * 100
+        return t // (3 * p.inc_us) * p.inc_us
     return t - p.dec_us if t >= p.min_us + p.dec_us else p.min_us
 
 

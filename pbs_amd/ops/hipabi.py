@@ -43,7 +43,8 @@ def bind(lib):
     _p(lib, "gpbs_hip_counter_reduce", C.c_int, vp, vp, vp, C.c_int, vp, vp)
     _p(lib, "gpbs_hip_adapt", C.c_int, vp, vp, vp, vp, C.c_int, vp, vp, vp)
     # runtime
-    _p(lib, "gpbs_gpu_ctx_create", vp, C.c_int, C.c_int, C.c_int)
+    _p(lib, "gpbs_gpu_ctx_create", vp, C.c_int, C.c_int, C.c_int, C.c_int)
+    _p(lib, "gpbs_gpu_set_nctx", C.c_int, vp, C.c_int)
     _p(lib, "gpbs_gpu_ctx_destroy", None, vp)
     _p(lib, "gpbs_gpu_attach", C.c_int, vp, vp, C.c_int, C.c_int)
     _p(lib, "gpbs_gpu_table", vp, vp)

@@ -19,15 +19,17 @@ from ..ops import hipabi
 from ..ops.kernels import lib as hiplib
 
 XCDS = 8
+CTX = 2  # issue contexts per XCD in the partition table (SMT-sibling analog)
 
 
 class GpuContext:
     def __init__(self, device: int = 0, engine=None, part_base: int = 0, table_mode: str = "host",
-                 device_counters: bool = True, device_adapt: bool = True):
+                 device_counters: bool = True, device_adapt: bool = False, nctx: int = 1):
         self.L = hiplib()
         self.device = device
         self.part_base = part_base
-        h = self.L.gpbs_gpu_ctx_create(device, part_base, 1 if table_mode == "device" else 0)
+        self.nctx = nctx
+        h = self.L.gpbs_gpu_ctx_create(device, part_base, 1 if table_mode == "device" else 0, nctx)
         if not h:
             raise RuntimeError(f"gpbs_gpu_ctx_create failed on device {device}")
         self.h = C.c_void_p(h)
@@ -35,8 +37,13 @@ class GpuContext:
         if engine is not None:
             self.attach(engine, device_counters, device_adapt)
 
-    def attach(self, engine, device_counters=True, device_adapt=True):
+    def attach(self, engine, device_counters=True, device_adapt=False, nctx=None):
+        """Bind the GPU actuator + counter backend to ``engine`` (whose
+        partitions are (xcd, ctx) pairs numbered xcd*nctx + ctx)."""
         self.engine = engine
+        if nctx is not None:
+            self.nctx = nctx
+        self.L.gpbs_gpu_set_nctx(self.h, self.nctx)
         rc = self.L.gpbs_gpu_attach(self.h, engine.h, int(device_counters), int(device_adapt))
         if rc:
             raise RuntimeError("gpbs_gpu_attach failed")
@@ -50,11 +57,16 @@ class GpuContext:
         return C.c_void_p(self.L.gpbs_gpu_counters(self.h))
 
     def set_owners(self, owners: List[int]):
-        arr = (C.c_int * XCDS)(*owners)
+        """owners: 8 entries (one tenant per XCD, context 1 idle) or 16
+        entries ((xcd, ctx) major)."""
+        if len(owners) == XCDS:
+            owners = [o for x in owners for o in (x, -1)]
+        arr = (C.c_int * (XCDS * CTX))(*owners)
         return self.L.gpbs_gpu_set_owners(self.h, arr)
 
     def owners(self) -> List[int]:
-        arr = (C.c_int * XCDS)()
+        """16 entries: tenant on (xcd, ctx), -1 idle."""
+        arr = (C.c_int * (XCDS * CTX))()
         self.L.gpbs_gpu_get_owners(self.h, arr)
         return list(arr)
 

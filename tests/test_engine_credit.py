@@ -1,0 +1,265 @@
+"""Credit scheduler semantics on the native engine (simulated clock).
+
+Mirrors the xm-test sched-credit / cpupool / vcpu-pin / pause suites
+(X:tools/xm-test/tests/sched-credit/01_sched_credit_weight_cap_pos.py,
+tests/cpupool/*, tests/vcpu-pin/*, tests/pause/*) plus the credit mechanics
+of X:xen/common/sched_credit.c (acct, boost, park, steal).
+"""
+import pytest
+
+from pbs_amd.core import oracle as O
+from pbs_amd.core.engine import Engine
+from pbs_amd.core.errors import GpbsError
+
+MS = 1_000_000
+
+
+def mk(nparts=4, **kw):
+    e = Engine(sim_clock=True, partitions=[(0, x) for x in range(nparts)], **kw)
+    e.tenant_create("Domain-0", nslots=1)
+    return e
+
+
+def share(e, ts, dur_ms=200, step_us=50):
+    base = {t: e.tenant_info(t).run_ns for t in ts}
+    t0 = e.now()
+    end = t0 + dur_ms * MS
+    while e.now() < end:
+        e.advance(e.now() + step_us * 1000)
+    return {t: (e.tenant_info(t).run_ns - base[t]) / (end - t0) for t in ts}
+
+
+def test_defaults_weight_256_cap_0():
+    e = mk()
+    t = e.tenant_create("a", nslots=2)
+    assert e.sched_credit_get(t) == (256, 0)
+    e.sched_credit_set(t, weight=512, cap=100)
+    assert e.sched_credit_get(t) == (512, 100)
+
+
+@pytest.mark.parametrize("bad", [dict(weight=0), dict(weight=65536), dict(cap=-5), dict(cap=301)])
+def test_weight_cap_validation(bad):
+    e = mk()
+    t = e.tenant_create("a", nslots=3)
+    with pytest.raises(GpbsError):
+        e.sched_credit_set(t, **{**dict(weight=-1, cap=-1), **bad})
+
+
+def test_tslice_ratelimit_validation_and_recompute():
+    e = mk()
+    assert e.sched_params_get(0) == (100, 100)  # boot default; ratelimit clamped to tslice
+    e.sched_params_set(0, 5000, 1000)
+    assert e.sched_params_get(0) == (5000, 1000)
+    for ts, rl in [(99, 100), (1000001, 1000), (5000, 99), (5000, 500001), (1000, 2000)]:
+        with pytest.raises(GpbsError):
+            e.sched_params_set(0, ts, rl)
+    assert "tslice             = 5000us" in e.debug_keys("r")
+
+
+def test_proportional_share_by_weight():
+    e = mk(nparts=2)
+    a = e.tenant_create("a", nslots=2)
+    b = e.tenant_create("b", nslots=2, weight=768)
+    e.wake(a)
+    e.wake(b)
+    s = share(e, [a, b], dur_ms=400)
+    # 2 partitions, weights 1:3 -> shares 0.5 : 1.5 partitions
+    assert abs(s[a] - 0.5) < 0.12 and abs(s[b] - 1.5) < 0.12, s
+    assert e.check() == ""
+
+
+def test_cap_parks_tenant():
+    e = mk(nparts=2)
+    a = e.tenant_create("capped", nslots=2, cap=50)
+    b = e.tenant_create("b", nslots=2)
+    e.wake(a)
+    e.wake(b)
+    s = share(e, [a, b], dur_ms=400)
+    assert s[a] < 0.75, s  # at most ~half a partition
+    assert e.perfc()["vcpu_park"] > 0 and e.perfc()["vcpu_unpark"] > 0
+    assert any(r.event == "PARK" for r in e.trace(from_start=True))
+
+
+def test_work_conserving_single_tenant_uses_all_partitions():
+    e = mk(nparts=4)
+    a = e.tenant_create("a", nslots=4)
+    e.wake(a)
+    s = share(e, [a], dur_ms=50)
+    assert s[a] > 3.8
+
+
+def test_wake_boost_preempts_over_tenant():
+    e = mk(nparts=1)
+    hog = e.tenant_create("hog", nslots=1)
+    lat = e.tenant_create("lat", nslots=1)
+    e.wake(hog)
+    e.advance(e.now() + 20 * MS)
+    lat_delays = []
+    for _ in range(20):
+        e.advance(e.now() + 3 * MS)
+        t0 = e.now()
+        e.wake(lat)  # BOOST on wake, tickles the partition
+        si = e.slot_info(e.slot_id(lat, 0))
+        lat_delays.append(0 if si["is_running"] else 1)
+        e.advance(e.now() + 50_000)
+        e.block(lat)
+    assert sum(lat_delays) <= 4, lat_delays  # boosted wakeups run immediately
+    assert e.perfc()["tickle_local_under"] + e.perfc()["tickle_local_over"] > 0
+
+
+def test_idle_partition_steals_work():
+    e = mk(nparts=4)
+    a = e.tenant_create("a", nslots=4)
+    # home every (blocked) slot on partition 0, then allow all partitions
+    for i in range(4):
+        e.pin(a, i, [0])
+    for i in range(4):
+        e.pin(a, i, [0, 1, 2, 3])
+    assert all(e.slot_info(e.slot_id(a, i))["processor"] == 0 for i in range(4))
+    # wakes queue on the busy partition 0 and tickle idlers, which steal
+    for i in range(4):
+        e.wake(a, i)
+    s = share(e, [a], dur_ms=50)
+    assert s[a] > 3.0, s
+    assert e.perfc()["migrate_queued"] + e.perfc()["migrate_running"] > 0
+
+
+def test_pause_unpause_and_destroy():
+    e = mk(nparts=2)
+    a = e.tenant_create("a", nslots=2)
+    b = e.tenant_create("b", nslots=2)
+    e.wake(a)
+    e.wake(b)
+    e.pause(a)
+    s = share(e, [a, b], dur_ms=40)
+    assert s[a] == 0 and s[b] > 1.9
+    e.unpause(a)
+    s = share(e, [a, b], dur_ms=200)
+    assert s[a] > 0.7
+    e.tenant_destroy(b)
+    s = share(e, [a], dur_ms=40)
+    assert s[a] > 1.9
+    assert e.check() == ""
+    with pytest.raises(GpbsError):
+        e.tenant_info(b) if False else e.sched_credit_get(b)
+
+
+def test_pools_partition_cpus_and_migrate_tenant():
+    e = mk(nparts=4)
+    p1 = e.pool_create("Pool-gpu", "credit")
+    e.pool_unassign(0, 3)
+    e.pool_unassign(0, 2)
+    e.pool_assign(p1, 2)
+    e.pool_assign(p1, 3)
+    assert e.pool_info(0)["cpus"] == [0, 1] and e.pool_info(p1)["cpus"] == [2, 3]
+    a = e.tenant_create("a", nslots=2)
+    b = e.tenant_create("b", nslots=2, pool=p1)
+    e.wake(a)
+    e.wake(b)
+    e.advance(e.now() + 10 * MS)
+    for x in range(4):
+        inf = e.partition_info(x)
+        assert inf["curr_tenant"] == (a if x < 2 else b)
+    e.tenant_move(a, p1)
+    e.advance(e.now() + 20 * MS)
+    assert e.tenant_info(a).pool == p1
+    for x in range(2):
+        assert e.partition_info(x)["idle"] == 1
+    with pytest.raises(GpbsError):
+        e.pool_destroy(p1)  # has tenants
+    e.pool_rename(p1, "renamed")
+    assert e.pool_find("renamed") == p1
+    assert e.check() == ""
+
+
+def test_unassign_last_cpu_of_busy_pool_rejected():
+    e = mk(nparts=2)
+    with pytest.raises(GpbsError):
+        e.pool_unassign(0, 0) or e.pool_unassign(0, 1)
+
+
+def test_slot_set_offlines_slots():
+    e = mk(nparts=4)
+    a = e.tenant_create("a", nslots=4)
+    e.wake(a)
+    e.set_nslots(a, 2)
+    s = share(e, [a], dur_ms=20)
+    assert 1.8 < s[a] < 2.2
+    e.set_nslots(a, 6)
+    e.wake(a)
+    s = share(e, [a], dur_ms=20)
+    assert s[a] > 3.8
+
+
+def test_pin_restricts_processor():
+    e = mk(nparts=4)
+    a = e.tenant_create("a", nslots=2)
+    e.pin(a, 0, [3])
+    e.pin(a, 1, [3])
+    e.wake(a)
+    e.advance(e.now() + 20 * MS)
+    for i in range(2):
+        assert e.slot_info(e.slot_id(a, i))["processor"] == 3
+
+
+def test_acct_matches_oracle_fair_share():
+    """csched_acct fair-share over active domains == oracle (Appendix C)."""
+    doms = [O.ODom(id=1, weight=256, slots=[O.OSlot(), O.OSlot()]),
+            O.ODom(id=2, weight=512, cap=50, slots=[O.OSlot()]),
+            O.ODom(id=3, weight=100, slots=[O.OSlot(credit=-250)])]
+    bal, order, parks = O.credit_acct(doms, ncpus=4, cpt=100, balance=0)
+    # total credit 400 split by weight*active: 512, 512, 100
+    # dom1: fair = ceil(400*256*2/1124) = 183 < peak 200 -> 92 per slot
+    assert [s.credit for s in doms[0].slots] == [92, 92]
+    # dom2: capped at ceil(50*100/100) = 50; its unused share is redistributed
+    assert doms[1].slots[0].credit == 50
+    # dom3: -250 + 100 -> -150, floored at -cpt
+    assert doms[2].slots[0].credit == -100 and doms[2].slots[0].pri == O.PRI_OVER
+    assert bal == 92 + 92 + 50 - 100
+    # after a domain leaves credit unused (xtra), capped-out domains are moved to the head
+    assert order == [3, 2, 1]
+
+
+def test_dump_keys_and_dmesg():
+    e = mk(nparts=2)
+    a = e.tenant_create("a", nslots=1)
+    e.wake(a)
+    e.advance(e.now() + 5 * MS)
+    z = e.debug_keys("z")
+    assert "pmuinfo: INST_RETIRED=" in z and "sched_count:" in z and "cpus: 0-1" in z
+    q = e.debug_keys("q")
+    assert "pmuinfo: pmc[0]=" in q and "VCPU0: CPU" in q
+    r = e.debug_keys("r")
+    assert "Scheduler: SMP Credit Scheduler (PBS) (credit)" in r and "CPU[00]" in r
+    assert "pmuinfo" in e.dmesg()
+    assert "sched_ctx" in e.debug_keys("p")
+
+
+def test_heartbeat_reaps_dead_tenant():
+    e = Engine(sim_clock=True, partitions=[(0, x) for x in range(2)], heartbeat_timeout_us=5000)
+    e.tenant_create("Domain-0", nslots=1)
+    a = e.tenant_create("a", nslots=2)
+    b = e.tenant_create("b", nslots=2)
+    e.wake(a)
+    e.wake(b)
+    for _ in range(20):
+        e.advance(e.now() + 1 * MS)
+        e.heartbeat(b)
+    assert e.tenant_info(a).paused == 1 and e.tenant_info(b).paused == 0
+    assert e.perfc()["tenant_dead"] == 1
+    assert "missed heartbeats" in e.dmesg()
+
+
+def test_burn_credits_rounding():
+    assert O.burn_credits(499) == 0 and O.burn_credits(500) == 1 and O.burn_credits(1_000_000) == 1000
+
+
+def test_static_scheduler_splits_by_weight():
+    e = Engine(sched="static", sim_clock=True, partitions=[(0, x) for x in range(8)])
+    a = e.tenant_create("a", nslots=8)
+    b = e.tenant_create("b", nslots=8, weight=768)
+    e.wake(a)
+    e.wake(b)
+    s = share(e, [a, b], dur_ms=20)
+    assert abs(s[a] - 2.0) < 0.2 and abs(s[b] - 6.0) < 0.2, s
+    assert "partitions:" in e.debug_keys("z")
