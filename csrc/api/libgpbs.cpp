@@ -115,6 +115,9 @@ void gpbs_boot_defaults(gpbs_boot_params_t* p) {
   p->dom0_quirk = 1;
   p->heartbeat_timeout_us = 0;
   p->trace_capacity = 1 << 16;
+  p->quantum_align_us = 0;
+  p->coschedule = 0;
+  p->class_period_us = 2000;
   AdaptParams a;
   std::memcpy(&p->adapt, &a, sizeof(a));
   AtcParams t;
@@ -343,14 +346,7 @@ int gpbs_slot_pin(gpbs_engine_t* e, int t, int idx, const uint64_t* mask4) {
   Tenant* d = live(e, t);
   if (!d) return GPBS_ENOENT;
   if ((m & e->e->pools[d->pool]->cpus).empty()) return GPBS_EINVAL;
-  int r = each_slot(e, t, idx, [&](Slot& v) {
-    v.affinity = m;
-    if (!m.test(v.processor)) {  // vcpu_set_affinity: migrate off a forbidden cpu
-      v.pause_flags |= VPF_MIGRATING;
-      e->e->vcpu_sleep_nosync(v);
-      if (!v.is_running) e->e->vcpu_migrate(v);
-    }
-  });
+  int r = each_slot(e, t, idx, [&](Slot& v) { e->e->set_affinity(v, m); });  // vcpu_set_affinity
   DONE(e);
   return r;
 }
@@ -503,6 +499,18 @@ int gpbs_set_actuator_ops(gpbs_engine_t* e, const gpbs_actuator_ops_t* ops) {
     e->e->actuator_ops = *ops;
   else
     e->e->actuator_ops = gpbs_actuator_ops_t{};
+  return GPBS_OK;
+}
+
+int gpbs_get_actuator_ops(gpbs_engine_t* e, gpbs_actuator_ops_t* out) {
+  LOCK(e);
+  *out = e->e->actuator_ops;
+  return GPBS_OK;
+}
+
+int gpbs_get_counter_ops(gpbs_engine_t* e, gpbs_counter_ops_t* out) {
+  LOCK(e);
+  *out = e->e->counter_ops;
   return GPBS_OK;
 }
 

@@ -73,6 +73,7 @@ struct CDom : SchedTenantData {
   uint64_t spinlock_latency = 0, spinlock_metric_update = 0, spinlock_count = 0, report_total = 0;
   uint64_t pending_requests = 0;
   uint64_t cache_miss_rate = 0, cpi = 0;
+  uint64_t rate_ewma = 0;  // smoothed miss rate (alpha 1/4) for contention classes
   AtcState atc{};
 };
 
@@ -588,6 +589,7 @@ class CreditScheduler : public Scheduler {
       CDom& d = sd(*E.tenants[ids[k]]);
       const uint64_t inst = d.pmc[0], cyc = d.pmc[1], miss = d.pmc[3];
       d.cache_miss_rate = inst ? miss * 100000 / inst : 0;  // Q3 fix: per tenant
+      if (inst) d.rate_ewma = (3 * d.rate_ewma + d.cache_miss_rate) / 4;
       d.cpi = inst ? cyc * 1000 / inst : 0;
       E.emit(TRC_METRIC, master_, (uint32_t)ids[k], (uint32_t)inst, (uint32_t)miss, (uint32_t)d.cache_miss_rate);
       d.spinlock_metric_update = 0;
@@ -725,7 +727,7 @@ class CreditScheduler : public Scheduler {
   bool mem_bound(int tenant) {
     if (tenant < 0) return false;
     Tenant* t = E.tenant(tenant);
-    return t && t->priv && sd(*t).cache_miss_rate >= E.adapt_params.threshold;
+    return t && t->priv && sd(*t).rate_ewma >= E.adapt_params.threshold;
   }
   int conflict(const Slot& v, int cpu) {
     int score = 0;
@@ -863,6 +865,12 @@ class CreditScheduler : public Scheduler {
     *tslice_us = (int)tslice_us_;
     *ratelimit_us = (int)ratelimit_us_;
     return 0;
+  }
+
+  int classify(Tenant& t) override {
+    CDom& d = sd(t);
+    if (d.pmc[0] == 0) return -1;  // idle this period: keep the current class
+    return d.rate_ewma >= E.adapt_params.threshold ? 1 : 0;
   }
 
   bool tenant_adapt(Tenant& d, AdaptState* out) override {

@@ -42,6 +42,10 @@ Engine::Engine(const gpbs_boot_params_t& p) : boot(p) {
   trace = std::make_unique<TraceRing>(cap);
   if (boot.sim_clock) sim_now = 0;
   pool_create("Pool-0", boot.sched);
+  if (boot.coschedule >= 2) {
+    class_timer_ = timer_init([this](int64_t n) { classify_tick(n); });
+    timer_set(class_timer_, now() + (int64_t)std::max(100, boot.class_period_us) * 1000);
+  }
   if (boot.heartbeat_timeout_us > 0) {
     hb_timer_ = timer_init([this](int64_t n) { heartbeat_check(n); });
     timer_set(hb_timer_, now() + (int64_t)boot.heartbeat_timeout_us * 1000 / 2);
@@ -563,6 +567,51 @@ void Engine::context_saved(Slot& prev) {
   prev.is_running = false;
   if (Scheduler* S = sched_of_tenant(prev.tenant)) S->context_saved(prev);
   if (prev.pause_flags & VPF_MIGRATING) vcpu_migrate(prev);
+}
+
+// ------------------------------------------------- contention-class placement --
+// gpbs extension (MI355X): the issue contexts of an XCD are typed.  Context 0
+// hosts compute-bound (MFMA) tenants, context 1 memory-bound ones, so every
+// XCD co-runs one of each (their waves use different pipes of the same CUs)
+// while memory-bound tenants, which would only split HBM bandwidth, time-share
+// their context under credit fairness and PBS's long cache-sensitive quanta.
+// The class comes from the PBS counter rates, with two-tick hysteresis, and is
+// enforced through slot affinity (the vcpu-pin path, so migration is the
+// reference's own mechanism).
+void Engine::set_affinity(Slot& v, const Mask& m) {
+  v.affinity = m;
+  if (!m.test(v.processor)) {
+    v.pause_flags |= VPF_MIGRATING;
+    vcpu_sleep_nosync(v);
+    if (!v.is_running) vcpu_migrate(v);
+  }
+}
+
+void Engine::classify_tick(int64_t n) {
+  for (auto& tp : tenants) {
+    if (!tp || !tp->alive || !tp->priv) continue;
+    Tenant& t = *tp;
+    Pool* pl = pool(t.pool);
+    if (!pl) continue;
+    const int c = pl->sched->classify(t);
+    if (c < 0) continue;
+    if (c != t.cls_pending) {
+      t.cls_pending = c;
+      t.cls_count = 1;
+    } else {
+      t.cls_count++;
+    }
+    if (t.cls_count < 2 || c == t.cls) continue;
+    t.cls = c;
+    Mask m;
+    for (int p = pl->cpus.first(); p >= 0; p = pl->cpus.next(p + 1))
+      if (parts[p]->ctx == c) m.set(p);
+    if (m.empty()) m = pl->cpus;
+    for (int sid : t.slots) set_affinity(*slots[sid], m);
+    emit(TRC_CLASS, 0, t.id, (uint32_t)c, (uint32_t)m.weight());
+  }
+  process_softirqs();
+  timer_set(class_timer_, n + (int64_t)std::max(100, boot.class_period_us) * 1000);
 }
 
 // ------------------------------------------------------------ heartbeats ---

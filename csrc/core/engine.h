@@ -76,6 +76,9 @@ struct Tenant {  // struct domain
   bool pinned = false;
   uint64_t pending_requests = 0;  // P7 (live in gpbs: request-queue depth)
   int64_t last_heartbeat = 0;
+  int cls = -1;          // contention class: 0 compute-bound (MFMA ctx), 1 memory-bound (memory ctx)
+  int cls_pending = -1;  // hysteresis: a new class must be seen on consecutive ticks
+  int cls_count = 0;
   std::unique_ptr<SchedTenantData> priv;
 };
 
@@ -133,6 +136,8 @@ class Scheduler {
   // gpbs additions: the paravirtual wait report routed by tenant id (Q6 fix)
   virtual void report(Tenant&, uint64_t, int) {}
   virtual bool tenant_adapt(Tenant&, AdaptState*) { return false; }
+  // Contention class from the counters: -1 unknown (no recent samples), 0 compute-bound, 1 memory-bound.
+  virtual int classify(Tenant&) { return -1; }
   virtual bool set_tenant_adapt(Tenant&, const AdaptState&) { return false; }
   virtual void fill_tenant_info(Tenant&, gpbs_tenant_info_t&) {}
   virtual void fill_slot_info(Slot&, gpbs_slot_info_t&) {}
@@ -237,6 +242,8 @@ class Engine {
   int stop();
   void kick();
   void heartbeat_check(int64_t now);
+  void classify_tick(int64_t now);
+  void set_affinity(Slot& v, const Mask& m);
 
   int64_t sim_now = 0;
 
@@ -266,6 +273,7 @@ class Engine {
   bool running_ = false;
   bool kicked_ = false;
   int hb_timer_ = -1;
+  int class_timer_ = -1;
   void loop();
 };
 

@@ -37,6 +37,17 @@ __device__ __forceinline__ int grab_unit(WorkQueue* q, const PartTable* table, u
   return u;
 }
 
+// Per-unit counter accumulation by thread 0 (tile-granular vPMU: the scheduler
+// sees a smooth rate instead of bursts at kernel exit).
+__device__ __forceinline__ void count_unit(u64* cnt, u32 me, u32 xcc, u64 inst, u64* t_last, u64 refs, u64 miss,
+                                           WorkQueue* q) {
+  if (threadIdx.x != 0) return;
+  const u64 t = __builtin_amdgcn_s_memtime();
+  count(cnt, me, xcc, inst, t - *t_last, refs, miss);
+  *t_last = t;
+  atomicAdd(&q->done, 1u);
+}
+
 __device__ __forceinline__ u16 f2bf(float x) { return __builtin_bit_cast(u16, (__bf16)x); }
 __device__ __forceinline__ float bf2f(u16 x) { return __uint_as_float(((u32)x) << 16); }
 
@@ -67,13 +78,12 @@ __global__ __launch_bounds__(GNT, 2) void k_gemm_bf16_tn(const u16* __restrict__
   int* s_slot = (int*)(smem + kGemmLds);
   const u32 xcc = xcc_id();
   // Ownership is decided by thread 0 inside grab_unit (workgroup-uniform).
-  const u64 t0 = __builtin_amdgcn_s_memtime();
+  u64 t_last = __builtin_amdgcn_s_memtime();
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
   const int tiles_m = M / GBM, tiles_n = N / GBN, ntiles = tiles_m * tiles_n;
   const int nk = K / GBK;
   constexpr int GROUP_M = 8;
-  u32 done = 0;
 
   // Per-lane staging geometry: this wave loads chunks c = wid*4 + j (8 rows of
   // 128 B each); lane -> row 8c + lane/8, LDS slot lane%8, global k-chunk
@@ -154,12 +164,8 @@ __global__ __launch_bounds__(GNT, 2) void k_gemm_bf16_tn(const u16* __restrict__
 #pragma unroll
         for (int r = 0; r < 4; ++r) C[(size_t)(m + r) * N + n] = f2bf(acc[i][j][r]);
       }
-    done++;
-    if (tid == 0) atomicAdd(&q->done, 1u);
+    count_unit(cnt, me, xcc, inst_per_tile, &t_last, refs_per_tile, miss_per_tile, q);
   }
-  if (tid == 0 && done)
-    count(cnt, me, xcc, (u64)done * inst_per_tile, __builtin_amdgcn_s_memtime() - t0, (u64)done * refs_per_tile,
-          (u64)done * miss_per_tile);
   finish(q, status);
 }
 
@@ -173,9 +179,12 @@ __global__ __launch_bounds__(SNT) void k_stream_copy(const f32x4* __restrict__ s
   __shared__ int s_slot[4];
   const u32 xcc = xcc_id();
   // Ownership is decided by thread 0 inside grab_unit (workgroup-uniform).
-  const u64 t0 = __builtin_amdgcn_s_memtime();
+  u64 t_last = __builtin_amdgcn_s_memtime();
   const u32 nchunks = (u32)((n4 + chunk4 - 1) / chunk4);
-  u32 done = 0;
+  // 16 B/lane: one load + one store wave-instruction per 1 KiB moved; every
+  // line is a fill (streaming, no reuse).
+  const u64 lines = (u64)chunk4 * 16 / 128;
+  const u64 inst = (u64)chunk4 * 2 / 64 + 8;
   for (;;) {
     const int c = grab_unit(q, table, mode, me, xcc, s_slot, nchunks);
     if (c < 0) break;
@@ -194,14 +203,7 @@ __global__ __launch_bounds__(SNT) void k_stream_copy(const f32x4* __restrict__ s
         if (idx < end) __builtin_nontemporal_store(v[k], dst + idx);
       }
     }
-    done++;
-    if (threadIdx.x == 0) atomicAdd(&q->done, 1u);
-  }
-  if (threadIdx.x == 0 && done) {
-    // 16 B/lane: one load + one store wave-instruction per 1 KiB moved; every
-    // line is a fill (streaming, no reuse).
-    const u64 lines = (u64)done * chunk4 * 16 / 128;
-    count(cnt, me, xcc, (u64)done * chunk4 * 2 / 64 + done * 8, __builtin_amdgcn_s_memtime() - t0, 2 * lines, 2 * lines);
+    count_unit(cnt, me, xcc, inst, &t_last, 2 * lines, 2 * lines, q);
   }
   finish(q, status);
 }
@@ -217,9 +219,10 @@ __global__ __launch_bounds__(SNT) void k_reduce_bf16(const u32x4* __restrict__ a
   __shared__ int s_slot[4];
   const u32 xcc = xcc_id();
   // Ownership is decided by thread 0 inside grab_unit (workgroup-uniform).
-  const u64 t0 = __builtin_amdgcn_s_memtime();
+  u64 t_last = __builtin_amdgcn_s_memtime();
   const u32 nchunks = (u32)((n8 + chunk8 - 1) / chunk8);
-  u32 done = 0;
+  const u64 lines = (u64)chunk8 * 16 / 128;
+  const u64 inst = (u64)chunk8 * 3 / 64 + (u64)chunk8 * 16 / 64;
   for (;;) {
     const int c = grab_unit(q, table, mode, me, xcc, s_slot, nchunks);
     if (c < 0) break;
@@ -251,13 +254,7 @@ __global__ __launch_bounds__(SNT) void k_reduce_bf16(const u32x4* __restrict__ a
         __builtin_nontemporal_store(r, out + idx);
       }
     }
-    done++;
-    if (threadIdx.x == 0) atomicAdd(&q->done, 1u);
-  }
-  if (threadIdx.x == 0 && done) {
-    const u64 lines = (u64)done * chunk8 * 16 / 128;
-    count(cnt, me, xcc, (u64)done * chunk8 * 3 / 64 + (u64)done * chunk8 * 16 / 64, __builtin_amdgcn_s_memtime() - t0,
-          3 * lines, 3 * lines);
+    count_unit(cnt, me, xcc, inst, &t_last, 3 * lines, 3 * lines, q);
   }
   finish(q, status);
 }
@@ -272,10 +269,10 @@ __global__ __launch_bounds__(256) void k_gemv_bf16(const u16* __restrict__ W, co
   __shared__ int s_slot[4];
   const u32 xcc = xcc_id();
   // Ownership is decided by thread 0 inside grab_unit (workgroup-uniform).
-  const u64 t0 = __builtin_amdgcn_s_memtime();
+  u64 t_last = __builtin_amdgcn_s_memtime();
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const u32 nchunks = (u32)((R + 15) / 16);  // 16 rows per unit (4 per wave)
-  u32 done = 0;
+  const u64 lines = (u64)16 * K * 2 / 128;
   for (;;) {
     const int c = grab_unit(q, table, mode, me, xcc, s_slot, nchunks);
     if (c < 0) break;
@@ -299,12 +296,7 @@ __global__ __launch_bounds__(256) void k_gemv_bf16(const u16* __restrict__ W, co
       for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
       if (lane == 0) y[row] = s;
     }
-    done++;
-    if (threadIdx.x == 0) atomicAdd(&q->done, 1u);
-  }
-  if (threadIdx.x == 0 && done) {
-    const u64 lines = (u64)done * 16 * K * 2 / 128;
-    count(cnt, me, xcc, (u64)done * 16 * (K / 512 + 8), __builtin_amdgcn_s_memtime() - t0, lines, lines);
+    count_unit(cnt, me, xcc, (u64)16 * (K / 512 + 8), &t_last, lines, lines, q);
   }
   finish(q, status);
 }

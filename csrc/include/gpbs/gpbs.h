@@ -66,7 +66,8 @@ typedef struct gpbs_boot_params {
   int32_t heartbeat_timeout_us;/* 0 = off; tenants missing heartbeats are reaped */
   int32_t trace_capacity;      /* trace ring records (power of two), default 65536 */
   int32_t quantum_align_us;    /* 0 = off; round quantum expiries up to this grid (batched switches) */
-  int32_t coschedule;          /* 1 = contention-aware sibling selection (pair memory- with compute-bound) */
+  int32_t coschedule;          /* 1 = contention-aware sibling selection; 2 = + counter-driven context classes */
+  int32_t class_period_us;     /* contention-class re-evaluation period, default 2000 */
   gpbs_adapt_params_t adapt;
   gpbs_atc_params_t atc;
 } gpbs_boot_params_t;
@@ -195,6 +196,32 @@ int gpbs_report_requests(gpbs_engine_t* e, int tenant, uint64_t n); /* pending_r
 int gpbs_set_counter_ops(gpbs_engine_t* e, const gpbs_counter_ops_t* ops);
 int gpbs_set_actuator_ops(gpbs_engine_t* e, const gpbs_actuator_ops_t* ops);
 int gpbs_slot_set_pmc(gpbs_engine_t* e, int slot, const uint64_t* pmc4); /* fake/replay source */
+int gpbs_get_actuator_ops(gpbs_engine_t* e, gpbs_actuator_ops_t* out);
+int gpbs_get_counter_ops(gpbs_engine_t* e, gpbs_counter_ops_t* out);
+
+/* --- tenant control pages (csrc/ipc/ctlpage.cpp): POSIX shm, seqlock,
+ *     SPSC wait-report ring, futex doorbell; bridge to an engine --- */
+void* gpbs_ctl_create(const char* name, int ntenants);
+void* gpbs_ctl_open(const char* name);
+void gpbs_ctl_close(void* ctl, int unlink_region);
+int gpbs_ctl_ntenants(void* ctl);
+int gpbs_ctl_assign(void* ctl, int page, int tenant);
+void gpbs_ctl_publish(void* ctl, int page, uint32_t gate, uint64_t mask, uint32_t quantum_us, int32_t prio,
+                      int32_t tenant, uint32_t epoch);
+int gpbs_ctl_read(void* ctl, int page, uint32_t* gate, uint64_t* mask, uint32_t* quantum_us, int32_t* prio,
+                  int32_t* tenant, uint32_t* epoch);
+int gpbs_ctl_report(void* ctl, int page, uint64_t wait_ns, uint32_t kind, uint32_t gpu);
+int gpbs_ctl_drain(void* ctl, int page, uint64_t* waits, uint32_t* kinds, int max);
+void gpbs_ctl_heartbeat(void* ctl, int page, uint64_t now_ns, uint32_t progress);
+int gpbs_ctl_status(void* ctl, int page, uint64_t* heartbeat, uint64_t* dropped, uint32_t* has_work,
+                    uint32_t* progress);
+void gpbs_ctl_set_counters(void* ctl, int page, const uint64_t* c4);
+void gpbs_ctl_get_counters(void* ctl, int page, uint64_t* c4);
+void gpbs_ctl_set_work(void* ctl, int page, int has_work);
+void gpbs_ctl_ring(void* ctl, int page);
+int gpbs_ctl_doorbell_wait(void* ctl, int page, int64_t timeout_ns);
+int gpbs_ctl_wait_gate(void* ctl, int page, int64_t timeout_ns);
+int gpbs_ctl_bind(void* ctl, void* engine);
 
 /* --- time --- */
 int64_t gpbs_now(gpbs_engine_t* e);

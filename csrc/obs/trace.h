@@ -25,6 +25,7 @@ enum TraceEvent : uint32_t {
   TRC_POOL = 13,       // a0=pool a1=op a2=arg
   TRC_FAULT = 14,      // a0=fault kind a1=arg
   TRC_ATC = 15,        // a0=global min slice a1=ntenants
+  TRC_CLASS = 16,      // a0=tenant a1=class (0 compute, 1 memory) a2=partitions allowed
 };
 
 struct TraceRecord {

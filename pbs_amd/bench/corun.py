@@ -45,7 +45,7 @@ from ..core.engine import Engine
 from ..runtime.gpu import GpuContext, Runner
 
 THROUGHPUT = ("gemm", "hbm", "coll")
-TENANTS = (("gemm", 16), ("hbm", 16), ("coll", 16), ("idle", 1))
+TENANTS = (("gemm", 8), ("hbm", 8), ("coll", 8), ("idle", 8))  # one slot per XCD
 
 
 @dataclass
@@ -154,7 +154,7 @@ class Corun:
         e.tenant_create("Domain-0", nslots=1)
         ids = {}
         for name, ns in TENANTS:
-            ids[name] = e.tenant_create(name, nslots=min(ns, 8 * nctx))
+            ids[name] = e.tenant_create(name, nslots=ns)
         if self.tid and ids != self.tid:
             raise RuntimeError("tenant ids differ across engines")
         self.tid = ids

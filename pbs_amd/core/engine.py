@@ -14,7 +14,8 @@ from .. import _native as N
 from .errors import GpbsError
 
 TRACE_EVENTS = {1: "SWITCH", 2: "WAKE", 3: "SLEEP", 4: "ACCT", 5: "ADAPT", 6: "GANG_EPOCH", 7: "REPORT",
-                8: "MIGRATE", 9: "PARK", 10: "STEAL", 11: "METRIC", 12: "DEAD", 13: "POOL", 14: "FAULT", 15: "ATC"}
+                8: "MIGRATE", 9: "PARK", 10: "STEAL", 11: "METRIC", 12: "DEAD", 13: "POOL", 14: "FAULT", 15: "ATC",
+                16: "CLASS"}
 EVENT_CODES = {v: k for k, v in TRACE_EVENTS.items()}
 
 PMC_NAMES = ("INST_RETIRED", "CPU_CLK_UNHALTED", "LLC_REFERENCES", "LLC_MISSES")

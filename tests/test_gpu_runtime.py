@@ -75,7 +75,7 @@ def test_revocation_relaunch_completes_all_units():
     assert st.units_done == 20
     a, b, c = r.buffers
     ref = a.float() @ b.float().t()
-    assert (c.float() - ref).abs().max().item() < 0.5
+    assert (c.float() - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
     r.close()
     ctx.close()
 
