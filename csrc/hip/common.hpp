@@ -64,7 +64,13 @@ __device__ __forceinline__ void finish(WorkQueue* q, u32* status) {
 }
 
 // Gate modes passed to tenant kernels.
-enum GateMode : u32 { GATE_NONE = 0, GATE_TABLE = 1 };
+// GATE_NONE: run anywhere; GATE_TABLE: leave revoked XCDs; GATE_PARK: sleep
+// on revoked XCDs (bounded) and resume when the XCD is handed back.
+// Bit 2 (GATE_DEVTABLE): the table is the device-memory copy refreshed by
+// k_partition_switch (agent-scope polls served on chip) instead of the
+// pinned host table (system-scope polls over PCIe).
+enum GateMode : u32 { GATE_NONE = 0, GATE_TABLE = 1, GATE_PARK = 2, GATE_DEVTABLE = 4 };
+constexpr u32 kParkSpins = 100;  // x ~20 us
 
 #define HIPCHECK(x)                                                                              \
   do {                                                                                           \
@@ -88,9 +94,11 @@ __device__ __forceinline__ u32 load_sys(const u32* p) {
 
 // Does tenant `me` own the XCD this workgroup runs on?
 __device__ __forceinline__ bool owns(const PartTable* t, u32 mode, u32 me, u32 xcc) {
-  if (mode == GATE_NONE) return true;
-  // One 8-byte system-scope load covers both contexts of the XCD.
-  const u64 pair = __hip_atomic_load(&t->pair[xcc & 7], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if ((mode & 3) == GATE_NONE) return true;
+  // One 8-byte load covers both contexts of the XCD.
+  const u64 pair = (mode & GATE_DEVTABLE)
+                       ? __hip_atomic_load(&t->pair[xcc & 7], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                       : __hip_atomic_load(&t->pair[xcc & 7], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   return (u32)pair == me || (u32)(pair >> 32) == me;
 }
 

@@ -80,6 +80,9 @@ struct GpuCtx {
   std::condition_variable cv;
   std::atomic<uint64_t> switches{0}, flushes{0}, metric_calls{0};
   int64_t metric_ns = 0;
+  // ownership accounting: ns each tenant held a context, per context index
+  int64_t own_ns[kMaxTenants][kCtx];
+  int64_t last_pub_ns = 0;
 };
 
 // ---------------------------------------------------------------- engine hooks
@@ -100,6 +103,13 @@ void publish(GpuCtx* c) {
   if (!changed) return;
   {
     std::lock_guard<std::mutex> g(c->mu);
+    const int64_t t = mono_ns();
+    if (c->last_pub_ns)
+      for (int x = 0; x < kXcds * kCtx; ++x) {
+        const u32 o = c->h_table->owner[x];
+        if (o < (u32)kMaxTenants) c->own_ns[o][x % kCtx] += t - c->last_pub_ns;
+      }
+    c->last_pub_ns = t;
     for (int x = 0; x < kXcds * kCtx; ++x) __atomic_store_n(&c->h_table->owner[x], c->pending[x], __ATOMIC_RELEASE);
     c->epoch++;
     __atomic_store_n(&c->h_table->epoch, c->epoch, __ATOMIC_RELEASE);
@@ -231,8 +241,9 @@ struct Runner {
 
   int launch(int qi) {
     WorkQueue* q = d_q + qi;
-    const void* tab = ctx->table_mode == 1 ? (const void*)ctx->d_table : (const void*)ctx->h_table;
-    const unsigned mode = cfg.gate ? GATE_TABLE : GATE_NONE;
+    const bool dev = __atomic_load_n(&ctx->table_mode, __ATOMIC_ACQUIRE) == 1;
+    const void* tab = dev ? (const void*)ctx->d_table : (const void*)ctx->h_table;
+    const unsigned mode = (cfg.gate ? (cfg.gate == 2 ? GATE_PARK : GATE_TABLE) : GATE_NONE) | (dev ? GATE_DEVTABLE : 0);
     const unsigned me = (unsigned)cfg.tenant;
     __atomic_store_n(&h_status[qi], 0u, __ATOMIC_RELEASE);
     st.launches++;
@@ -398,6 +409,7 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
   c->table_mode = table_mode;
   c->nctx = nctx == kCtx ? kCtx : 1;
   std::memset(c->last_delta, 0, sizeof(c->last_delta));
+  std::memset(c->own_ns, 0, sizeof(c->own_ns));
   bool ok = hipHostMalloc((void**)&c->h_table, sizeof(PartTable), hipHostMallocCoherent | hipHostMallocMapped) ==
             hipSuccess;
   ok = ok && hipMalloc((void**)&c->d_cnt, sizeof(u64) * kMaxTenants * kXcds * kNumPmc) == hipSuccess;
@@ -417,7 +429,7 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
   int lo = 0, hi = 0;
   hipDeviceGetStreamPriorityRange(&lo, &hi);
   ok = ok && hipStreamCreateWithPriority(&c->sched_stream, hipStreamNonBlocking, hi) == hipSuccess;
-  if (table_mode == 1) ok = ok && hipMalloc((void**)&c->d_table, sizeof(PartTable)) == hipSuccess;
+  ok = ok && hipMalloc((void**)&c->d_table, sizeof(PartTable)) == hipSuccess;
   if (!ok) {
     fprintf(stderr, "[gpbs-hip] ctx_create failed on device %d\n", device);
     return nullptr;
@@ -427,7 +439,7 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
     c->h_table->owner[x] = kNoOwner;
     c->pending[x] = kNoOwner;
   }
-  if (c->d_table) hipMemcpy(c->d_table, c->h_table, sizeof(PartTable), hipMemcpyHostToDevice);
+  hipMemcpy(c->d_table, c->h_table, sizeof(PartTable), hipMemcpyHostToDevice);
   return c;
 }
 
@@ -482,6 +494,21 @@ int gpbs_gpu_set_nctx(void* p, int nctx) {
   return 0;
 }
 
+// Switch between the pinned host table (0) and the device table (1).  The
+// device copy is re-synchronised before device mode takes effect.
+int gpbs_gpu_set_table_mode(void* p, int mode) {
+  GpuCtx* c = (GpuCtx*)p;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (mode == 1) {
+    if (hipMemcpyAsync(c->d_table, c->h_table, sizeof(PartTable), hipMemcpyHostToDevice, c->sched_stream) !=
+            hipSuccess ||
+        hipStreamSynchronize(c->sched_stream) != hipSuccess)
+      return -5;
+  }
+  __atomic_store_n(&c->table_mode, mode == 1 ? 1 : 0, __ATOMIC_RELEASE);
+  return 0;
+}
+
 void* gpbs_gpu_table(void* p) { return ((GpuCtx*)p)->table_mode == 1 ? (void*)((GpuCtx*)p)->d_table : (void*)((GpuCtx*)p)->h_table; }
 void* gpbs_gpu_counters(void* p) { return ((GpuCtx*)p)->d_cnt; }
 
@@ -513,6 +540,18 @@ int gpbs_gpu_read_counters(void* p, int tenant, uint64_t* out4, uint64_t* per_xc
     for (int x = 0; x < kXcds; ++x) out4[i] += buf[x * 4 + i];
   }
   if (per_xcd32) std::memcpy(per_xcd32, buf, sizeof(buf));
+  return 0;
+}
+
+// ns tenant `t` held context c (summed over XCDs); reset when clear != 0.
+int gpbs_gpu_ownership(void* p, int t, int64_t* out2, int clear) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (t < 0 || t >= kMaxTenants) return -22;
+  std::lock_guard<std::mutex> g(c->mu);
+  for (int k = 0; k < kCtx; ++k) {
+    out2[k] = c->own_ns[t][k];
+    if (clear) c->own_ns[t][k] = 0;
+  }
   return 0;
 }
 

@@ -21,13 +21,24 @@ namespace gpbs_hip {
 __device__ __forceinline__ int grab_unit(WorkQueue* q, const PartTable* table, u32 mode, u32 me, u32 xcc,
                                          int* s_slot, u32 total) {
   if (threadIdx.x == 0) {
-    int u;
-    if (!owns(table, mode, me, xcc)) {
-      atomicAdd(&q->stopped, 1u);
-      u = -1;
-    } else {
-      u32 t = atomicAdd(&q->next, 1u);
-      u = t < total ? (int)t : -1;
+    int u = -1;
+    for (u32 spins = 0;; ++spins) {
+      if (owns(table, mode, me, xcc)) {
+        const u32 t = atomicAdd(&q->next, 1u);
+        u = t < total ? (int)t : -1;
+        break;
+      }
+      // GATE_PARK: stay resident (sleeping) on a revoked XCD so the workgroup
+      // resumes within ~20 us when the scheduler hands the XCD back, instead
+      // of waiting for the next launch.  Bounded (~2 ms): a workgroup that is
+      // not rescheduled leaves and the runner relaunches the rest of the unit.
+      if ((mode & 3) != GATE_PARK || spins >= kParkSpins ||
+          __hip_atomic_load(&q->next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= total) {
+        atomicAdd(&q->stopped, 1u);
+        break;
+      }
+#pragma unroll
+      for (int k = 0; k < 6; ++k) __builtin_amdgcn_s_sleep(127);
     }
     *s_slot = u;
   }

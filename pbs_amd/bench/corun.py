@@ -65,10 +65,12 @@ class CorunConfig:
 
 
 POLICY_ENGINES = {
-    # name: (nctx, engine overrides on top of MI355X_PROFILE)
-    "gpbs": (2, {}),
-    "gpbs1": (1, {"coschedule": 0}),
-    "credit2": (2, {"sched": "credit-fixed"}),
+    # name: (issue contexts per XCD, engine overrides on top of MI355X_PROFILE,
+    #        kernel gate mode, partition-table location)
+    "gpbs": (2, {}, "park", "device"),
+    "gpbs-exit": (2, {}, True, "host"),
+    "gpbs1": (1, {"coschedule": 0}, True, "host"),
+    "credit2": (2, {"sched": "credit-fixed"}, "park", "device"),
 }
 
 
@@ -144,7 +146,7 @@ class Corun:
         self.active_engine: Optional[Engine] = None
 
     def _make_engine(self, pol: str) -> Engine:
-        nctx, over = POLICY_ENGINES[pol]
+        nctx, over, _, _ = POLICY_ENGINES[pol]
         prof = {k: v for k, v in MI355X_PROFILE.items()}
         prof.update(over)
         e = Engine(**prof)
@@ -172,15 +174,18 @@ class Corun:
         coll = self.runners["coll"]
         if policy in self.engines:
             e = self.engines[policy]
+            _, _, gate, table = POLICY_ENGINES[policy]
+            self.ctx.set_table_mode(table)
             self.ctx.attach(e, nctx=e._gpbs_nctx)
             e.start()
             self.active_engine = e
             for r in self._natives():
-                r.set_gate(True)
+                r.set_gate(gate)
                 r.set_engine_wake(True)
             if not isinstance(coll, Runner):
                 coll.gate, coll.engine = True, e
             return
+        self.ctx.set_table_mode("host")
         for r in self._natives():
             r.set_engine_wake(False)
         if not isinstance(coll, Runner):
@@ -291,6 +296,8 @@ class Corun:
         for _ in range(warmup):
             self.step()
         self.runners["idle"].latencies(clear=True)
+        for n in self.tid:
+            self.ctx.ownership(self.tid[n], clear=True)
         e = self.active_engine
         if e is not None:
             e.perfc_reset()
@@ -338,6 +345,10 @@ class Corun:
             eng["run_share"] = {n: round((e.tenant_info(self.tid[n]).run_ns - run0[n]) / (wall_ms * 1e6), 3)
                                 for n in self.tid}
             eng["phase"] = {n: e.tenant_info(self.tid[n]).phase for n in self.tid}
+            eng["ctx_share"] = {n: [round(x / (wall_ms / 1e3), 2) for x in self.ctx.ownership(self.tid[n])]
+                                for n in self.tid}
+            eng["runner"] = {n: {k: getattr(r.stats(), k) for k in ("launches", "relaunches", "waits_owner")}
+                             for n, r in self.runners.items() if isinstance(r, Runner)}
             res["engine"] = eng
         self.log(f"[corun] {policy}: " + json.dumps(res))
         return res

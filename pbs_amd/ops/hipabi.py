@@ -45,6 +45,7 @@ def bind(lib):
     # runtime
     _p(lib, "gpbs_gpu_ctx_create", vp, C.c_int, C.c_int, C.c_int, C.c_int)
     _p(lib, "gpbs_gpu_set_nctx", C.c_int, vp, C.c_int)
+    _p(lib, "gpbs_gpu_set_table_mode", C.c_int, vp, C.c_int)
     _p(lib, "gpbs_gpu_ctx_destroy", None, vp)
     _p(lib, "gpbs_gpu_attach", C.c_int, vp, vp, C.c_int, C.c_int)
     _p(lib, "gpbs_gpu_table", vp, vp)
@@ -53,6 +54,7 @@ def bind(lib):
     _p(lib, "gpbs_gpu_get_owners", C.c_int, vp, C.POINTER(C.c_int))
     _p(lib, "gpbs_gpu_read_counters", C.c_int, vp, C.c_int, C.POINTER(u64), C.POINTER(u64))
     _p(lib, "gpbs_gpu_stats", C.c_int, vp, C.POINTER(u64))
+    _p(lib, "gpbs_gpu_ownership", C.c_int, vp, C.c_int, C.POINTER(i64), C.c_int)
     _p(lib, "gpbs_gpu_cumask_stream", vp, C.c_int, C.POINTER(C.c_uint32), C.c_int, C.c_int)
     _p(lib, "gpbs_gpu_stream_destroy", C.c_int, vp)
     _p(lib, "gpbs_runner_create", vp, vp, C.POINTER(RunnerCfg))

@@ -80,6 +80,19 @@ class GpuContext:
             return [tuple(px[x * 4:(x + 1) * 4]) for x in range(XCDS)]
         return tuple(out)
 
+    def set_table_mode(self, mode: str):
+        """'host': pinned host table polled over PCIe; 'device': device copy
+        refreshed by the partition_switch kernel, polled on chip."""
+        rc = self.L.gpbs_gpu_set_table_mode(self.h, 1 if mode == "device" else 0)
+        if rc:
+            raise RuntimeError("set_table_mode failed")
+
+    def ownership(self, tenant: int, clear: bool = False):
+        """Seconds `tenant` held each issue context (summed over XCDs)."""
+        out = (C.c_int64 * CTX)()
+        self.L.gpbs_gpu_ownership(self.h, tenant, out, int(clear))
+        return [x / 1e9 for x in out]
+
     def stats(self):
         out = (C.c_uint64 * 4)()
         self.L.gpbs_gpu_stats(self.h, out)
@@ -201,8 +214,9 @@ class Runner:
     def reset_stats(self):
         self.L.gpbs_runner_reset_stats(self.h)
 
-    def set_gate(self, gate: bool):
-        self.L.gpbs_runner_set_gate(self.h, int(gate))
+    def set_gate(self, gate):
+        """False: run anywhere; True: leave revoked XCDs; "park": sleep on them."""
+        self.L.gpbs_runner_set_gate(self.h, 2 if gate == "park" else int(bool(gate)))
 
     def set_engine_wake(self, on: bool):
         self.L.gpbs_runner_set_engine_wake(self.h, int(on))
