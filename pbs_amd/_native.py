@@ -218,6 +218,7 @@ def _bind_ipc(lib):
     P(lib, "gpbs_ctl_doorbell_wait", C.c_int, C.c_void_p, C.c_int, i64)
     P(lib, "gpbs_ctl_set_work", None, C.c_void_p, C.c_int, C.c_int)
     P(lib, "gpbs_ctl_bind", C.c_int, C.c_void_p, C.c_void_p)
+    P(lib, "gpbs_ctl_assign", C.c_int, C.c_void_p, C.c_int, C.c_int)
 
 
 def _bind_counters(lib):

@@ -1,0 +1,277 @@
+"""gpbsctl: the xl analog (X:tools/libxl/xl_cmdtable.c, xl_cmdimpl.c).
+
+Verbs, options, output formats and error strings follow xl with
+Domain -> tenant, VCPU -> slot, CPU -> partition (GPU:XCD:context) and
+cpupool -> pool:
+
+    gpbsctl sched-credit [-d <Tenant> [-w[=WEIGHT]|-c[=CAP]]] [-s [-t TSLICE] [-r RATELIMIT]] [-p POOL]
+    gpbsctl create NAME [--slots N] [--weight W] [--cap C] [--pool P]
+    gpbsctl destroy|pause|unpause TENANT
+    gpbsctl list | slot-list [TENANT...] | slot-pin TENANT SLOT|all PARTS|all | slot-set TENANT N
+    gpbsctl debug-keys KEYS | dmesg [-c] | top | trace [-n N] | perfc [-r] | info
+    gpbsctl pool-create NAME [--sched S] [--cpus C] | pool-list [-c] [POOL] | pool-destroy POOL
+    gpbsctl pool-rename POOL NEW | pool-gpu-add POOL PARTS|node:N | pool-gpu-remove POOL PARTS|node:N
+    gpbsctl pool-migrate TENANT POOL | pool-xgmi-split | snapshot PATH | restore PATH
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+from typing import List, Optional
+
+from .rpc import DEFAULT_SOCKET, Client, RpcError
+
+RUNSTATE = {0: "r", 1: "-", 2: "b", 3: "p"}
+
+
+def _err(msg: str) -> None:
+    print(msg, file=sys.stderr)
+
+
+def _dom_row(d):
+    print("%-33s %4d %6d %4d" % (d["name"], d["id"], d["weight"], d["cap"]))
+
+
+def _dom_header():
+    print("%-33s %4s %6s %4s" % ("Name", "ID", "Weight", "Cap"))
+
+
+def _pool_line(c: Client, pool) -> None:
+    try:
+        p = c.call("pool_params_get", pool=pool)
+        print("Cpupool %s: tslice=%dus ratelimit=%dus" % (p["name"], p["tslice_us"], p["ratelimit_us"]))
+    except RpcError:
+        print("Cpupool %s: [sched params unavailable]" % pool)
+
+
+def cmd_sched_credit(c: Client, argv: List[str]) -> int:
+    ap = argparse.ArgumentParser(prog="gpbsctl sched-credit", add_help=True)
+    ap.add_argument("-d", "--domain", "--tenant", dest="dom")
+    ap.add_argument("-w", "--weight", type=int)
+    ap.add_argument("-c", "--cap", type=int)
+    ap.add_argument("-s", "--schedparam", action="store_true")
+    ap.add_argument("-t", "--tslice_us", type=int)
+    ap.add_argument("-r", "--ratelimit_us", type=int)
+    ap.add_argument("-p", "--cpupool", "--pool", dest="pool")
+    a = ap.parse_args(argv)
+    opt_w, opt_c = a.weight is not None, a.cap is not None
+    opt_t, opt_r = a.tslice_us is not None, a.ratelimit_us is not None
+    if (a.pool or a.schedparam) and (a.dom or opt_w or opt_c):
+        _err("Specifying a cpupool or schedparam is not allowed with domain options.")
+        return 1
+    if not a.dom and (opt_w or opt_c):
+        _err("Must specify a domain.")
+        return 1
+    if not a.schedparam and (opt_t or opt_r):
+        _err("Must specify schedparam to set schedule parameter values.")
+        return 1
+    if a.schedparam:
+        pool = a.pool if a.pool is not None else 0
+        try:
+            c.call("pool_params_get", pool=pool)
+        except RpcError:
+            _err("unknown cpupool '%s'" % pool)
+            return 3
+        if not opt_t and not opt_r:
+            _pool_line(c, pool)
+            return 0
+        try:
+            c.call("pool_params_set", pool=pool, tslice_us=a.tslice_us, ratelimit_us=a.ratelimit_us)
+        except RpcError as e:
+            _err(str(e))
+            _err("libxl_sched_credit_params_set failed.")
+            return 3
+        return 0
+    if not a.dom:  # list every pool and its tenants
+        pools = c.call("pool_list")
+        if a.pool is not None:
+            match = [p for p in pools if str(p["id"]) == str(a.pool) or p["name"] == a.pool]
+            if not match:
+                _err("unknown cpupool '%s'" % a.pool)
+                return 3
+            pools = match
+        doms = c.call("domain_list")
+        for p in pools:
+            if p["sched"] not in ("credit", "credit-fixed", "atc"):
+                continue
+            _pool_line(c, p["id"])
+            _dom_header()
+            for d in doms:
+                if d["pool"] == p["id"]:
+                    _dom_row(d)
+        return 0
+    try:
+        if not opt_w and not opt_c:
+            d = c.call("domain_sched_get", domain=a.dom)
+            _dom_header()
+            _dom_row(d)
+            return 0
+        c.call("domain_sched_set", domain=a.dom, weight=a.weight if opt_w else -1, cap=a.cap if opt_c else -1)
+        return 0
+    except RpcError as e:
+        _err(str(e))
+        if opt_w or opt_c:
+            _err("libxl_domain_sched_params_set failed.")
+        return 3
+
+
+def cmd_list(c: Client, argv) -> int:
+    doms = c.call("domain_list")
+    print("%-40s %5s %5s %5s %10s %8s %6s" % ("Name", "ID", "Slots", "State", "Time(s)", "Tslice", "Phase"))
+    for d in doms:
+        st = "p" if d["paused"] else "r"
+        print("%-40s %5d %5d %5s %10.1f %6dus %6s" % (d["name"], d["id"], d["slots"], st, d["run_ns"] / 1e9,
+                                                    d["tslice_us"], {1: "LOW", 2: "HIGH"}.get(d["phase"], "-")))
+    return 0
+
+
+def cmd_slot_list(c: Client, argv) -> int:
+    rows = c.call("slot_list", domains=argv or None)
+    print("%-32s %5s %5s %5s %5s %9s %7s %4s" % ("Name", "ID", "SLOT", "PART", "State", "Time(s)", "Credit", "Pri"))
+    for r in rows:
+        print("%-32s %5d %5d %5d %5s %9.1f %7d %4d" % (r["name"], r["id"], r["slot"], r["cpu"],
+                                                      RUNSTATE.get(r["state"], "?"), r["time_s"], r["credit"],
+                                                      r["pri"]))
+    return 0
+
+
+def cmd_top(c: Client, argv) -> int:
+    t = c.call("top")
+    print("%-20s %4s %5s %6s %9s %8s %5s %10s %8s %7s" % ("NAME", "ID", "POOL", "SLOTS", "RUN(s)", "TSLICE", "PHASE",
+                                                       "MISSRATE", "CPI", "REPORTS"))
+    for r in t["tenants"]:
+        print("%-20s %4d %5d %3d/%-2d %9.2f %6dus %5s %10d %8d %7d" % (
+            r["name"][:20], r["id"], r["pool"], r["active"], r["slots"], r["run_s"], r["tslice_us"],
+            {1: "LOW", 2: "HIGH"}.get(r["phase"], "-"), r["miss_rate"], r["cpi"], r["reports"]))
+    busy = sum(1 for p in t["partitions"] if not p["idle"])
+    print(f"partitions busy: {busy}/{len(t['partitions'])}")
+    return 0
+
+
+def cmd_pool_list(c: Client, argv) -> int:
+    ap = argparse.ArgumentParser(prog="gpbsctl pool-list")
+    ap.add_argument("-c", "--cpus", action="store_true")
+    ap.add_argument("pool", nargs="?")
+    a = ap.parse_args(argv)
+    pools = c.call("pool_list")
+    if a.pool is not None:
+        pools = [p for p in pools if p["name"] == a.pool or str(p["id"]) == a.pool]
+        if not pools:
+            _err("unknown cpupool '%s'" % a.pool)
+            return 1
+    if a.cpus:
+        print("%-32s %s" % ("Name", "CPU list"))
+        for p in pools:
+            print("%-32s %s" % (p["name"], ",".join(str(x) for x in p["cpus"])))
+    else:
+        print("%-32s %6s %-10s %6s %7s" % ("Name", "CPUs", "Sched", "Active", "Domain count"))
+        for p in pools:
+            print("%-32s %6d %-10s %6s %7d" % (p["name"], len(p["cpus"]), p["sched"], "y", p["n_tenants"]))
+    return 0
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    sock = DEFAULT_SOCKET
+    if argv[:1] == ["--socket"] and len(argv) > 1:
+        sock = argv[1]
+        argv = argv[2:]
+    if not argv or argv[0] in ("-h", "--help", "help"):
+        print(__doc__)
+        return 0
+    cmd, rest = argv[0], argv[1:]
+    try:
+        c = Client(sock)
+    except OSError as e:
+        _err(f"cannot connect to gpbsd at {sock}: {e}")
+        return 2
+    try:
+        if cmd == "sched-credit":
+            return cmd_sched_credit(c, rest)
+        if cmd == "list":
+            return cmd_list(c, rest)
+        if cmd in ("slot-list", "vcpu-list"):
+            return cmd_slot_list(c, rest)
+        if cmd == "top":
+            return cmd_top(c, rest)
+        if cmd in ("pool-list", "cpupool-list"):
+            return cmd_pool_list(c, rest)
+        simple = {
+            "create": lambda r: c.call("create", **_kv(r, ("name",), dict(slots=int, weight=int, cap=int, pool=str))),
+            "destroy": lambda r: c.call("destroy", domain=r[0]),
+            "pause": lambda r: c.call("pause", domain=r[0]),
+            "unpause": lambda r: c.call("unpause", domain=r[0]),
+            "slot-pin": lambda r: c.call("slot_pin", domain=r[0], slot=r[1], cpus=r[2]),
+            "vcpu-pin": lambda r: c.call("slot_pin", domain=r[0], slot=r[1], cpus=r[2]),
+            "slot-set": lambda r: c.call("slot_set", domain=r[0], n=int(r[1])),
+            "vcpu-set": lambda r: c.call("slot_set", domain=r[0], n=int(r[1])),
+            "pool-create": lambda r: c.call("pool_create", **_kv(r, ("name",), dict(sched=str, cpus=str))),
+            "cpupool-create": lambda r: c.call("pool_create", **_kv(r, ("name",), dict(sched=str, cpus=str))),
+            "pool-destroy": lambda r: c.call("pool_destroy", pool=r[0]),
+            "cpupool-destroy": lambda r: c.call("pool_destroy", pool=r[0]),
+            "pool-rename": lambda r: c.call("pool_rename", pool=r[0], name=r[1]),
+            "cpupool-rename": lambda r: c.call("pool_rename", pool=r[0], name=r[1]),
+            "pool-gpu-add": lambda r: c.call("pool_cpu_add", pool=r[0], cpu=r[1]),
+            "cpupool-cpu-add": lambda r: c.call("pool_cpu_add", pool=r[0], cpu=r[1]),
+            "pool-gpu-remove": lambda r: c.call("pool_cpu_remove", pool=r[0], cpu=r[1]),
+            "cpupool-cpu-remove": lambda r: c.call("pool_cpu_remove", pool=r[0], cpu=r[1]),
+            "pool-migrate": lambda r: c.call("pool_migrate", domain=r[0], pool=r[1]),
+            "cpupool-migrate": lambda r: c.call("pool_migrate", domain=r[0], pool=r[1]),
+            "pool-xgmi-split": lambda r: c.call("pool_xgmi_split"),
+            "cpupool-numa-split": lambda r: c.call("pool_xgmi_split"),
+            "snapshot": lambda r: c.call("snapshot", path=r[0] if r else None),
+            "restore": lambda r: c.call("restore", path=r[0]),
+            "info": lambda r: c.call("info"),
+        }
+        if cmd == "debug-keys":
+            if not rest:
+                _err("'gpbsctl debug-keys' requires one argument.")
+                return 1
+            out = c.call("debug_keys", keys=rest[0])
+            sys.stdout.write(out)
+            return 0
+        if cmd == "dmesg":
+            sys.stdout.write(c.call("dmesg", clear="-c" in rest))
+            return 0
+        if cmd == "trace":
+            n = int(rest[rest.index("-n") + 1]) if "-n" in rest else 4096
+            for t, ev, cpu, a in c.call("trace", max_records=n, from_start=True):
+                print(f"{t / 1e9:14.6f} cpu{cpu:<3d} {ev:<10s} {a[0]:>10d} {a[1]:>10d} {a[2]:>10d} {a[3]:>10d}")
+            return 0
+        if cmd == "perfc":
+            for k, v in c.call("perfc", reset="-r" in rest).items():
+                print(f"{k:<28s} {v}")
+            return 0
+        if cmd in simple:
+            res = simple[cmd](rest)
+            if isinstance(res, (dict, list)):
+                print(json.dumps(res, indent=1))
+            elif cmd == "create":
+                print(res)
+            return 0
+        _err(f"command '{cmd}' not implemented")
+        return 1
+    except IndexError:
+        _err(f"'gpbsctl {cmd}' requires more arguments.")
+        return 1
+    except RpcError as e:
+        _err(str(e))
+        return 3
+    finally:
+        c.close()
+
+
+def _kv(rest, positional, types):
+    """Parse 'NAME --key val' style arguments."""
+    ap = argparse.ArgumentParser(add_help=False)
+    for p in positional:
+        ap.add_argument(p)
+    for k, ty in types.items():
+        ap.add_argument("--" + k, type=ty, default=None)
+    a = vars(ap.parse_args(rest))
+    return {k: v for k, v in a.items() if v is not None}
+
+
+if __name__ == "__main__":
+    sys.exit(main())
