@@ -112,7 +112,9 @@ Page* page(void* h, int t) {
 
 Ctl* map_region(const char* name, int ntenants, bool create) {
   std::string n = std::string("/gpbs-") + name;
-  int fd = create ? shm_open(n.c_str(), O_CREAT | O_RDWR | O_TRUNC, 0600) : shm_open(n.c_str(), O_RDWR, 0);
+  // O_EXCL: never truncate a region another live daemon (or this process) maps
+  // -- that would SIGBUS every tenant holding the old mapping.
+  int fd = create ? shm_open(n.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600) : shm_open(n.c_str(), O_RDWR, 0);
   if (fd < 0) return nullptr;
   size_t size;
   if (create) {

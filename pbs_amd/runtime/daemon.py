@@ -33,6 +33,8 @@ XCDS = 8
 
 
 class Daemon:
+    _seq = 0
+
     def __init__(self, socket_path: str = DEFAULT_SOCKET, gpus=(0,), nctx: int = 2, sim: bool = False,
                  profile: str = "mi355x", config_path: Optional[str] = None, ctl_name: str = "gpbs",
                  ctl_pages: int = 64, state_path: Optional[str] = None, attach_gpu: bool = False):
@@ -52,7 +54,8 @@ class Daemon:
                     self.engine.pool_assign(0, pid)
         self.dom0 = self.engine.tenant_create("Domain-0", nslots=1)
         self.lib = N.load_core()
-        self.ctl_name = f"{ctl_name}-{os.getpid()}"
+        Daemon._seq += 1
+        self.ctl_name = f"{ctl_name}-{os.getpid()}-{Daemon._seq}"
         self.ctl = self.lib.gpbs_ctl_create(self.ctl_name.encode(), ctl_pages)
         if not self.ctl:
             raise RuntimeError("cannot create control-page region")
