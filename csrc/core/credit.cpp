@@ -766,6 +766,58 @@ class CreditScheduler : public Scheduler {
     return best;
   }
 
+  // Gang alignment (coschedule >= 3; Ousterhout co-scheduling applied to the
+  // XCD partitions of one GPU): the partitions of one issue-context class on a
+  // GPU form a gang led by its lowest-numbered partition.  The leader decides
+  // by credit as usual; followers run the leader's tenant whenever they hold a
+  // runnable slot of it, and are re-scheduled at once when the leader switches.
+  // A memory-bound tenant then owns the whole HBM path for its quantum instead
+  // of several bandwidth tenants each driving a few XCDs (per-CU load paths
+  // cap what a partial-GPU tenant can pull, and their mixed streams thrash the
+  // MALL), while credit keeps the shares fair over time.
+  int gang_leader(int cpu) const {
+    const Partition& P = *E.parts[cpu];
+    for (int c = cpus_.first(); c >= 0; c = cpus_.next(c + 1)) {
+      const Partition& Q = *E.parts[c];
+      if (Q.gpu == P.gpu && Q.ctx == P.ctx) return c;
+    }
+    return cpu;
+  }
+  Slot* gang_pick(int cpu, Slot& head) {
+    const int lead = gang_leader(cpu);
+    if (lead == cpu) return nullptr;
+    const int L = E.slots[E.parts[lead]->curr]->tenant;
+    if (L < 0 || head.tenant == L) return nullptr;
+    const int16_t hp = sv(head).pri;
+    for (int sid : pc(cpu).runq) {
+      Slot& v = *E.slots[sid];
+      if (v.tenant != L) continue;
+      const int16_t p = sv(v).pri;
+      if (p < PRI_OVER) return nullptr;              // parked/idle
+      if (hp > PRI_UNDER && p < hp) return nullptr;  // never delay a BOOSTed waker
+      return &v;
+    }
+    return nullptr;
+  }
+  void gang_kick(int cpu) {
+    const Partition& P = *E.parts[cpu];
+    for (int c = cpus_.first(); c >= 0; c = cpus_.next(c + 1)) {
+      if (c == cpu) continue;
+      const Partition& Q = *E.parts[c];
+      if (Q.gpu == P.gpu && Q.ctx == P.ctx) E.raise_softirq(c);
+    }
+  }
+  bool gang_misaligned(int cpu, const Slot& scurr) {
+    if (E.boot.coschedule < 3 || scurr.is_idle()) return false;
+    const int lead = gang_leader(cpu);
+    if (lead == cpu) return false;
+    const int L = E.slots[E.parts[lead]->curr]->tenant;
+    if (L < 0 || L == scurr.tenant) return false;
+    for (int sid : pc(cpu).runq)
+      if (E.slots[sid]->tenant == L) return true;
+    return false;
+  }
+
   TaskSlice do_schedule(int cpu, int64_t now) override {
     Slot& scurr = curr(cpu);
     CSlot& cs = sv(scurr);
@@ -781,7 +833,9 @@ class CreditScheduler : public Scheduler {
     Slot* snext = nullptr;
     TaskSlice ret{0, 0, false};
     int64_t tslice;
-    if (ratelimit_us_ && E.runnable(scurr) && !scurr.is_idle() && runtime < (int64_t)ratelimit_us_ * 1000) {
+    const int prev_tenant = scurr.tenant;
+    if (ratelimit_us_ && E.runnable(scurr) && !scurr.is_idle() && runtime < (int64_t)ratelimit_us_ * 1000 &&
+        !gang_misaligned(cpu, scurr)) {
       snext = &scurr;
       cs.start_time += now;
       E.perfc.incr(PC_delay_ms);
@@ -792,7 +846,16 @@ class CreditScheduler : public Scheduler {
       if (E.runnable(scurr)) runq_insert(cpu, scurr);
       auto& rq = pc(cpu).runq;
       snext = E.slots[rq.front()].get();
-      if (E.boot.coschedule && !snext->is_idle()) {
+      bool follow = false;
+      if (E.boot.coschedule >= 3) {
+        if (Slot* g = gang_pick(cpu, *snext)) {
+          rq.remove(g->id);
+          rq.push_front(g->id);
+          snext = g;
+          follow = true;
+        }
+      }
+      if (!follow && E.boot.coschedule && !snext->is_idle()) {
         if (Slot* alt = cosched_pick(cpu)) {  // same priority class, less contention
           rq.remove(alt->id);
           rq.push_front(alt->id);
@@ -800,7 +863,7 @@ class CreditScheduler : public Scheduler {
         }
       }
       if (cs.flags & FLAG_YIELD) cs.flags &= ~FLAG_YIELD;
-      if (sv(*snext).pri > PRI_OVER)
+      if (sv(*snext).pri > PRI_OVER || follow)
         runq_remove(*snext);
       else
         snext = &load_balance(cpu, *snext, &ret.migrated);
@@ -821,6 +884,8 @@ class CreditScheduler : public Scheduler {
     }
     ret.time_ns = snext->is_idle() ? -1 : tslice;
     ret.slot = snext->id;
+    if (E.boot.coschedule >= 3 && snext->tenant != prev_tenant && !snext->is_idle() && gang_leader(cpu) == cpu)
+      gang_kick(cpu);
     return ret;
   }
 

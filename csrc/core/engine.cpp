@@ -512,7 +512,12 @@ void Engine::vcpu_migrate(Slot& v) {
   v.pause_flags &= ~VPF_MIGRATING;
   if (pl->cpus.empty()) return;
   if (!pl->cpus.test(v.processor)) v.processor = pl->cpus.first();
-  int nc = S->pick_cpu(v);
+  int nc;
+  if (v.home >= 0 && pl->cpus.test(v.home) && v.affinity.test(v.home))
+    nc = v.home;  // class placement spreads a tenant's slots one per partition
+  else
+    nc = S->pick_cpu(v);
+  v.home = -1;
   v.processor = nc;
   if (old != nc) emit(TRC_MIGRATE, nc, v.tenant, v.index, old, nc);
   vcpu_wake(v);
@@ -578,9 +583,10 @@ void Engine::context_saved(Slot& prev) {
 // The class comes from the PBS counter rates, with two-tick hysteresis, and is
 // enforced through slot affinity (the vcpu-pin path, so migration is the
 // reference's own mechanism).
-void Engine::set_affinity(Slot& v, const Mask& m) {
+void Engine::set_affinity(Slot& v, const Mask& m, int home) {
   v.affinity = m;
-  if (!m.test(v.processor)) {
+  v.home = (home >= 0 && m.test(home)) ? home : -1;
+  if (!m.test(v.processor) || (v.home >= 0 && v.processor != v.home)) {
     v.pause_flags |= VPF_MIGRATING;
     vcpu_sleep_nosync(v);
     if (!v.is_running) vcpu_migrate(v);
@@ -607,7 +613,13 @@ void Engine::classify_tick(int64_t n) {
     for (int p = pl->cpus.first(); p >= 0; p = pl->cpus.next(p + 1))
       if (parts[p]->ctx == c) m.set(p);
     if (m.empty()) m = pl->cpus;
-    for (int sid : t.slots) set_affinity(*slots[sid], m);
+    // Slot k goes to the k-th partition of the class (cycling), so a tenant
+    // with one slot per XCD lands on every XCD instead of wherever pick_cpu's
+    // cycle from its old processor would pile them up.
+    std::vector<int> order;
+    for (int p = m.first(); p >= 0; p = m.next(p + 1)) order.push_back(p);
+    for (size_t k = 0; k < t.slots.size(); ++k)
+      set_affinity(*slots[t.slots[k]], m, order.empty() ? -1 : order[k % order.size()]);
     emit(TRC_CLASS, 0, t.id, (uint32_t)c, (uint32_t)m.weight());
   }
   process_softirqs();

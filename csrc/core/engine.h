@@ -52,6 +52,7 @@ struct Slot {  // struct vcpu
   int tenant = -1;  // -1: idle slot of a partition
   int index = 0;    // vcpu_id
   int processor = 0;
+  int home = -1;  // one-shot placement hint for the next migration (class pinning)
   Mask affinity;
   uint32_t pause_flags = 0;
   int pause_count = 0;
@@ -243,7 +244,7 @@ class Engine {
   void kick();
   void heartbeat_check(int64_t now);
   void classify_tick(int64_t now);
-  void set_affinity(Slot& v, const Mask& m);
+  void set_affinity(Slot& v, const Mask& m, int home = -1);
 
   int64_t sim_now = 0;
 

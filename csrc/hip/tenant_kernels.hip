@@ -181,8 +181,12 @@ __global__ __launch_bounds__(GNT, 2) void k_gemm_bf16_tn(const u16* __restrict__
 }
 
 // ------------------------------------------------------------ HBM stream ---
-// dst = src (float4 copy), 16 B per lane, 8 loads in flight per thread.
-constexpr int SNT = 256, SUNROLL = 8;
+// dst = src (float4 copy), 16 B per lane, 16 loads in flight per thread: one
+// 256-thread workgroup per CU keeps 64 KiB of reads in flight (enough for
+// HBM3E at ~2 us loaded latency) while occupying only one wave slot per SIMD,
+// so a co-resident GEMM keeps its two waves/SIMD (VGPR budget 512/SIMD: GEMM
+// 2x136 + stream 80 + reduce 80 + gemv 40 fits; the old 4 WG/CU grids did not).
+constexpr int SNT = 256, SUNROLL = 16, RUNROLL = 8;
 
 __global__ __launch_bounds__(SNT) void k_stream_copy(const f32x4* __restrict__ src, f32x4* __restrict__ dst,
                                                     u64 n4, u32 chunk4, WorkQueue* q, const PartTable* table, u32 mode,
@@ -238,10 +242,10 @@ __global__ __launch_bounds__(SNT) void k_reduce_bf16(const u32x4* __restrict__ a
     const int c = grab_unit(q, table, mode, me, xcc, s_slot, nchunks);
     if (c < 0) break;
     const u64 base = (u64)c * chunk8, end = min(base + chunk8, n8);
-    for (u64 i = base + threadIdx.x; i < end; i += (u64)SNT * 4) {
-      u32x4 x[4], y[4];
+    for (u64 i = base + threadIdx.x; i < end; i += (u64)SNT * RUNROLL) {
+      u32x4 x[RUNROLL], y[RUNROLL];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < RUNROLL; ++k) {
         const u64 idx = i + (u64)k * SNT;
         if (idx < end) {
           x[k] = __builtin_nontemporal_load(a + idx);
@@ -249,7 +253,7 @@ __global__ __launch_bounds__(SNT) void k_reduce_bf16(const u32x4* __restrict__ a
         }
       }
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < RUNROLL; ++k) {
         const u64 idx = i + (u64)k * SNT;
         if (idx >= end) continue;
         const u32* px = (const u32*)&x[k];
@@ -356,7 +360,7 @@ int gpbs_hip_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int
 int gpbs_hip_stream_copy(const void* src, void* dst, unsigned long long bytes, unsigned chunk_bytes, void* q,
                          const void* table, unsigned mode, unsigned me, void* cnt, void* status, int grid, hipStream_t s) {
   if (bytes % 16 || chunk_bytes % 16 || chunk_bytes == 0) return -22;
-  if (grid <= 0) grid = 256 * 4;
+  if (grid <= 0) grid = 256;  // one workgroup per CU (see SUNROLL)
   hipLaunchKernelGGL(k_stream_copy, dim3(grid), dim3(SNT), 0, s, (const f32x4*)src, (f32x4*)dst, bytes / 16,
                      chunk_bytes / 16, (WorkQueue*)q, (const PartTable*)table, mode, me, (u64*)cnt, (u32*)status);
   return hipGetLastError() == hipSuccess ? 0 : -5;
@@ -365,7 +369,7 @@ int gpbs_hip_stream_copy(const void* src, void* dst, unsigned long long bytes, u
 int gpbs_hip_reduce_bf16(const void* a, const void* b, void* out, unsigned long long bytes, unsigned chunk_bytes,
                          void* q, const void* table, unsigned mode, unsigned me, void* cnt, void* status, int grid, hipStream_t s) {
   if (bytes % 16 || chunk_bytes % 16 || chunk_bytes == 0) return -22;
-  if (grid <= 0) grid = 256 * 4;
+  if (grid <= 0) grid = 256;
   hipLaunchKernelGGL(k_reduce_bf16, dim3(grid), dim3(SNT), 0, s, (const u32x4*)a, (const u32x4*)b, (u32x4*)out,
                      bytes / 16, chunk_bytes / 16, (WorkQueue*)q, (const PartTable*)table, mode, me, (u64*)cnt, (u32*)status);
   return hipGetLastError() == hipSuccess ? 0 : -5;
@@ -375,7 +379,7 @@ int gpbs_hip_gemv_bf16(const void* W, const void* x, void* y, int R, int K, void
                        unsigned me, void* cnt, void* status, int grid, hipStream_t s) {
   if (K % 512 || R <= 0) return -22;
   if (grid <= 0) grid = (R + 15) / 16;
-  if (grid > 1024) grid = 1024;
+  if (grid > 256) grid = 256;
   hipLaunchKernelGGL(k_gemv_bf16, dim3(grid), dim3(256), 0, s, (const u16*)W, (const u16*)x, (float*)y, R, K,
                      (WorkQueue*)q, (const PartTable*)table, mode, me, (u64*)cnt, (u32*)status);
   return hipGetLastError() == hipSuccess ? 0 : -5;

@@ -25,9 +25,13 @@ With t_i the time tenant i needed inside the step and T_i its solo time:
 Policies (same tenants, same box):
   none    default hardware sharing: every tenant launches ungated full-GPU grids
   static  equal static XCD split (2 XCDs per tenant, ARINC-653-like)
-  gpbs1   PBS adaptive credit scheduler, one exclusive context per XCD
-  gpbs    PBS adaptive credit scheduler over both issue contexts of every XCD
-          with contention-aware sibling selection (the flagship)
+  gpbs1   PBS adaptive credit scheduler, one exclusive context per XCD,
+          kernels exit on revoked XCDs
+  gpbs-exit   two issue contexts per XCD + contention classes, exit gating
+  gpbs-nogang the flagship without gang alignment of the context classes
+  gpbs    PBS adaptive credit scheduler over both issue contexts of every XCD:
+          counter-driven compute/memory classes, gang-aligned memory context,
+          parked gating on a device-resident partition table (the flagship)
 """
 from __future__ import annotations
 
@@ -68,6 +72,7 @@ POLICY_ENGINES = {
     # name: (issue contexts per XCD, engine overrides on top of MI355X_PROFILE,
     #        kernel gate mode, partition-table location)
     "gpbs": (2, {}, "park", "device"),
+    "gpbs-nogang": (2, {"coschedule": 2}, "park", "device"),
     "gpbs-exit": (2, {}, True, "host"),
     "gpbs1": (1, {"coschedule": 0}, True, "host"),
     "credit2": (2, {"sched": "credit-fixed"}, "park", "device"),

@@ -32,7 +32,7 @@ REFERENCE_PROFILE: Dict[str, Any] = dict(
 # are scheduled (SMT-sibling analog) with contention-aware sibling selection.
 MI355X_PROFILE: Dict[str, Any] = dict(
     sched="credit", tslice_us=1000, ratelimit_us=250, metric_period_us=1000, quantum_align_us=250,
-    coschedule=2, class_period_us=2000,
+    coschedule=3, class_period_us=2000,
     adapt=dict(threshold=20000, band_lo=70, band_hi=130, min_us=1000, max_us=11000, inc_us=1000, dec_us=2000,
                switch_boundary=9000, ticks_per_tslice=3),
 )

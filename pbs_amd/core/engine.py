@@ -92,8 +92,8 @@ class Engine:
         self._keep = []  # ctypes callbacks kept alive
         self._trace_cursor = C.c_uint64(0)
         if partitions is not None:
-            for gpu, xcd in partitions:
-                pid = self.partition_add(gpu, xcd)
+            for part in partitions:
+                pid = self.partition_add(*part)  # (gpu, xcd) or (gpu, xcd, ctx)
                 self.pool_assign(0, pid)
 
     # ------------------------------------------------------------ lifecycle

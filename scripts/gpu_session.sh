@@ -29,6 +29,7 @@ for step in "$@"; do
   case $step in
     warm)   run warm 400 python -c "import torch; print(torch.__version__, torch.cuda.get_device_name(0))" ;;
     tests)  run tests 900 python -m pytest tests -x -q -m gpu -p no:cacheprovider ;;
+    kbench) run kbench 300 python scripts/kbench.py ;;
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  run bench 600 python bench.py --steps 10 --warmup 2 --out gpurun_out/bench_detail.json ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --policies gpbs ;;

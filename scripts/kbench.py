@@ -1,0 +1,99 @@
+"""Solo kernel microbench for the tenant kernels (gfx950).
+
+Reports GEMM TF/s (bf16 MFMA, fp32 acc), stream-copy and reduce-copy TB/s
+(bytes read + written) across launch grids, each against the PyTorch/hipBLASLt
+equivalent, as one JSON line per measurement.  Used to size the default grids
+(see SUNROLL in csrc/hip/tenant_kernels.hip).
+
+    python scripts/kbench.py [--iters 20]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from pbs_amd.ops import kernels as K  # noqa: E402
+
+
+def timed(fn, iters, pre=None):
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
+    for _ in range(3):
+        if pre:
+            pre()
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for a, b in ev:
+        if pre:
+            pre()
+        a.record()
+        fn()
+        b.record()
+    torch.cuda.synchronize()
+    ts = sorted(a.elapsed_time(b) for a, b in ev)
+    return ts[len(ts) // 2]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    args = ap.parse_args()
+    L = K.lib()
+    s = K._stream()
+    q = K.work_queue()
+    zero = q.zero_
+    dev = "cuda"
+    out = []
+    n = 4096
+    A = torch.randn(n, n, device=dev, dtype=torch.bfloat16)
+    B = torch.randn(n, n, device=dev, dtype=torch.bfloat16)
+    Cm = torch.empty(n, n, device=dev, dtype=torch.bfloat16)
+    for grid in (256, 512, 1024):
+        ms = timed(lambda: L.gpbs_hip_gemm_bf16(K._ptr(A), K._ptr(B), K._ptr(Cm), n, n, n, K._ptr(q), None, 0, 0,
+                                                None, None, grid, s), args.iters, zero)
+        out.append({"kernel": "gemm_bf16", "shape": [n, n, n], "grid": grid, "ms": ms, "tflops": 2 * n ** 3 / ms / 1e9})
+    ms = timed(lambda: torch.mm(A, B.t(), out=Cm), args.iters)
+    out.append({"kernel": "torch.mm", "shape": [n, n, n], "ms": ms, "tflops": 2 * n ** 3 / ms / 1e9})
+
+    nbytes = 1 << 30
+    src = torch.empty(nbytes // 4, device=dev, dtype=torch.float32).normal_()
+    dst = torch.empty_like(src)
+    for grid in (256, 512, 1024, 2048):
+        ms = timed(lambda: L.gpbs_hip_stream_copy(K._ptr(src), K._ptr(dst), nbytes, 1 << 19, K._ptr(q), None, 0, 0,
+                                                  None, None, grid, s), args.iters, zero)
+        out.append({"kernel": "stream_copy", "bytes": nbytes, "grid": grid, "ms": ms, "tbps": 2 * nbytes / ms / 1e9})
+    ms = timed(lambda: dst.copy_(src), args.iters)
+    out.append({"kernel": "torch.copy_", "bytes": nbytes, "ms": ms, "tbps": 2 * nbytes / ms / 1e9})
+
+    rb = 256 << 20
+    a = torch.randn(rb // 2, device=dev, dtype=torch.bfloat16)
+    b = torch.randn_like(a)
+    o = torch.empty_like(a)
+    for grid in (256, 512, 1024):
+        ms = timed(lambda: L.gpbs_hip_reduce_bf16(K._ptr(a), K._ptr(b), K._ptr(o), rb, 1 << 19, K._ptr(q), None, 0, 0,
+                                                  None, None, grid, s), args.iters, zero)
+        out.append({"kernel": "reduce_bf16", "bytes": rb, "grid": grid, "ms": ms, "tbps": 3 * rb / ms / 1e9})
+    ms = timed(lambda: torch.add(a, b, out=o), args.iters)
+    out.append({"kernel": "torch.add", "bytes": rb, "ms": ms, "tbps": 3 * rb / ms / 1e9})
+
+    W = torch.randn(8192, 4096, device=dev, dtype=torch.bfloat16)
+    x = torch.randn(4096, device=dev, dtype=torch.bfloat16)
+    y = torch.empty(8192, device=dev, dtype=torch.float32)
+    for grid in (256, 512):
+        ms = timed(lambda: L.gpbs_hip_gemv_bf16(K._ptr(W), K._ptr(x), K._ptr(y), 8192, 4096, K._ptr(q), None, 0, 0,
+                                                None, None, grid, s), args.iters, zero)
+        out.append({"kernel": "gemv_bf16", "shape": [8192, 4096], "grid": grid, "ms": ms,
+                    "tbps": W.numel() * 2 / ms / 1e9})
+    for r in out:
+        print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}))
+
+
+if __name__ == "__main__":
+    main()

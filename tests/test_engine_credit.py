@@ -263,3 +263,50 @@ def test_static_scheduler_splits_by_weight():
     s = share(e, [a, b], dur_ms=20)
     assert abs(s[a] - 2.0) < 0.2 and abs(s[b] - 6.0) < 0.2, s
     assert "partitions:" in e.debug_keys("z")
+
+
+def _running_tenants(e, tenants, nparts):
+    on = {}
+    for t in tenants:
+        for k in range(e.tenant_info(t).nslots):
+            si = e.slot_info(e.slot_id(t, k))
+            if si["is_running"]:
+                on[si["processor"]] = t
+    return [on.get(p, -1) for p in range(nparts)]
+
+
+@pytest.mark.parametrize("cosched", [0, 3])
+def test_gang_alignment_of_memory_context(cosched):
+    """coschedule=3: the partitions of one (gpu, ctx) class follow the leader's
+    tenant, so two bandwidth tenants alternate whole-GPU quanta instead of
+    splitting the XCDs; credit shares stay fair either way."""
+    n = 8
+    e = mk(nparts=n, coschedule=cosched, quantum_align_us=0)
+    e.sched_params_set(0, 1000, 0)
+    a = e.tenant_create("a", nslots=n)
+    b = e.tenant_create("b", nslots=n)
+    for k in range(n):  # one slot of each tenant per partition
+        e.pin(a, k, [k])
+        e.pin(b, k, [k])
+    for k in range(n):  # start maximally misaligned
+        e.wake(a if k % 2 else b, k)
+    e.advance(e.now() + 200_000)
+    for k in range(n):
+        e.wake(b if k % 2 else a, k)
+    aligned = samples = 0
+    base = {t: e.tenant_info(t).run_ns for t in (a, b)}
+    t0 = e.now()
+    while e.now() < t0 + 300 * MS:
+        e.advance(e.now() + 100_000)
+        cur = _running_tenants(e, [a, b], n)
+        samples += 1
+        aligned += len(set(cur)) == 1
+    frac = aligned / samples
+    print("aligned", cosched, frac)
+    sh = {t: (e.tenant_info(t).run_ns - base[t]) / (e.now() - t0) for t in (a, b)}
+    assert abs(sh[a] - sh[b]) < 0.15 * n, sh
+    if cosched >= 3:
+        assert frac > 0.9, frac
+        assert e.check() == ""
+    else:
+        assert frac < 0.9, frac  # plain credit leaves the XCDs split
