@@ -650,6 +650,13 @@ class CreditScheduler : public Scheduler {
     tickle(v.processor, v);
   }
 
+  uint32_t trace_word(Slot& v) override {
+    if (!v.priv) return 0;
+    const CSlot& s = sv(v);
+    const int32_t c = std::max<int32_t>(-(1 << 23), std::min<int32_t>((1 << 23) - 1, s.credit));
+    return (uint32_t)(s.pri + 128) & 0xffu | ((uint32_t)c << 8);
+  }
+
   void yield(Slot& v) override {
     if (!E.boot.default_yield) sv(v).flags |= FLAG_YIELD;
   }
@@ -833,6 +840,7 @@ class CreditScheduler : public Scheduler {
     Slot* snext = nullptr;
     TaskSlice ret{0, 0, false};
     int64_t tslice;
+    bool held = false;
     const int prev_tenant = scurr.tenant;
     if (ratelimit_us_ && E.runnable(scurr) && !scurr.is_idle() && runtime < (int64_t)ratelimit_us_ * 1000 &&
         !gang_misaligned(cpu, scurr)) {
@@ -841,6 +849,7 @@ class CreditScheduler : public Scheduler {
       E.perfc.incr(PC_delay_ms);
       E.perfc.incr(PC_ratelimit_hold);
       tslice = (int64_t)ratelimit_us_ * 1000;
+      held = true;
     } else {
       tslice = (int64_t)tslice_us_ * 1000;
       if (E.runnable(scurr)) runq_insert(cpu, scurr);
@@ -874,7 +883,15 @@ class CreditScheduler : public Scheduler {
       if (!snext->is_idle()) sv(*snext).start_time += now;
     }
     // PBS (:1796-1804): the quantum is the next tenant's private tslice.
-    if (!snext->is_idle()) {
+    // Q13: the reference applies this at `out:` (:1792-1797), *after* the
+    // ratelimit hold of :1732, so a slot kept for ratelimit gets its whole
+    // adaptive quantum (up to 1.1 ms there, 11 ms in the MI355X profile) and a
+    // BOOSTed waker that tickled it waits that long.  gpbs holds for the
+    // remaining ratelimit only (Xen >= 4.3 semantics); strict_ref keeps the
+    // reference behaviour.
+    if (held && !E.adapt_params.strict_ref) {
+      tslice = std::max<int64_t>((int64_t)ratelimit_us_ * 1000 - runtime, 1000);
+    } else if (!snext->is_idle()) {
       if (mode_ == Mode::PBS)
         tslice = (int64_t)sd_of(*snext).adapt.tslice_us * 1000;
       else if (mode_ == Mode::ATC)

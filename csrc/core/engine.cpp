@@ -471,7 +471,12 @@ void Engine::vcpu_wake(Slot& v) {
   } else if (!(v.pause_flags & VPF_BLOCKED)) {
     if (v.rs == RS_BLOCKED) runstate_change(v, RS_OFFLINE, now());
   }
-  emit(TRC_WAKE, v.processor, v.tenant, v.index, v.processor);
+  uint32_t wv = 0, wc = 0;
+  if (Scheduler* S = sched_of_tenant(v.tenant)) {
+    wv = S->trace_word(v);
+    wc = S->trace_word(*slots[parts[v.processor]->curr]);
+  }
+  emit(TRC_WAKE, v.processor, v.tenant, v.index, wv, wc);
 }
 
 void Engine::vcpu_sleep_nosync(Slot& v) {

@@ -139,6 +139,9 @@ class Scheduler {
   virtual bool tenant_adapt(Tenant&, AdaptState*) { return false; }
   // Contention class from the counters: -1 unknown (no recent samples), 0 compute-bound, 1 memory-bound.
   virtual int classify(Tenant&) { return -1; }
+  // Trace word of a slot: (priority + 128) in bits 0-7, credit (clamped to
+  // +-2^23) in bits 8-31.  Carried by WAKE records (who could preempt whom).
+  virtual uint32_t trace_word(Slot&) { return 0; }
   virtual bool set_tenant_adapt(Tenant&, const AdaptState&) { return false; }
   virtual void fill_tenant_info(Tenant&, gpbs_tenant_info_t&) {}
   virtual void fill_slot_info(Slot&, gpbs_slot_info_t&) {}

@@ -36,6 +36,7 @@ Policies (same tenants, same box):
 from __future__ import annotations
 
 import json
+import os
 import statistics
 import threading
 import time
@@ -337,7 +338,8 @@ class Corun:
         slows.append((p50 / self.solo_lat_ms - 1.0) * 100.0 if self.solo_lat_ms > 0 else 0.0)
         res["tenants"]["idle"] = {"p50_ms": round(p50, 4), "p99_ms": round(p99, 4),
                                   "solo_p50_ms": round(self.solo_lat_ms, 4), "norm_perf": round(idle_perf, 4),
-                                  "slowdown_pct": round(slows[-1], 2), "requests": len(lats)}
+                                  "slowdown_pct": round(slows[-1], 2), "requests": len(lats),
+                                  "over_ms": {str(b): sum(1 for x in lats if x > b) for b in (0.5, 1, 2, 5)}}
         res["aggregate"] = agg
         res["aggregate_all_gpus"] = self._allreduce(agg, "sum")
         res["mean_slowdown_pct"] = statistics.mean(slows)
@@ -355,6 +357,13 @@ class Corun:
             eng["runner"] = {n: {k: getattr(r.stats(), k) for k in ("launches", "relaunches", "waits_owner")}
                              for n, r in self.runners.items() if isinstance(r, Runner)}
             res["engine"] = eng
+            diag = os.environ.get("GPBS_DIAG_DIR")
+            if diag and self.rank == 0:
+                os.makedirs(diag, exist_ok=True)
+                recs = e.trace(max_records=1 << 18, from_start=True)
+                with open(os.path.join(diag, f"trace_{policy}.json"), "w") as f:
+                    json.dump({"tid": self.tid, "lat_ms": lats,
+                               "trace": [[r.t_ns, r.event, r.cpu, *r.a] for r in recs]}, f)
         self.log(f"[corun] {policy}: " + json.dumps(res))
         return res
 

@@ -9,10 +9,18 @@
 from __future__ import annotations
 
 import ctypes as C
+import os
 from dataclasses import dataclass
 from typing import List, Optional
 
-import torch
+# One hardware queue per stream: every tenant runner stream plus the scheduler
+# stream (partition-table updates, counter reduce).  With the HIP default of 4
+# queues, streams share queues round-robin and a table update can sit behind
+# a parked tenant kernel on the same queue until its park bound expires.
+# Must be set before the HIP runtime initialises (first device call).
+os.environ["GPU_MAX_HW_QUEUES"] = str(max(8, int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)))
+
+import torch  # noqa: E402
 
 from .. import _native as N
 from ..ops import hipabi

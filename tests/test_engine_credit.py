@@ -310,3 +310,40 @@ def test_gang_alignment_of_memory_context(cosched):
         assert e.check() == ""
     else:
         assert frac < 0.9, frac  # plain credit leaves the XCDs split
+
+
+@pytest.mark.parametrize("strict", [0, 1])
+def test_ratelimit_hold_does_not_inherit_adaptive_quantum(strict):
+    """Q13: sched_credit.c:1732 holds a just-switched-in slot for ratelimit,
+    then :1795-1797 (`out:`) overwrite the hold with the tenant's adaptive
+    slice, so a BOOSTed waker that tickled it waits a whole PBS quantum.
+    gpbs holds for the remaining ratelimit only; strict_ref=1 reproduces."""
+    q = 11000
+    e = Engine(sim_clock=True, partitions=[(0, 0)], quantum_align_us=0,
+               adapt=dict(min_us=q, max_us=q, strict_ref=strict))
+    e.tenant_create("Domain-0", nslots=1)
+    e.sched_params_set(0, q, 250)
+    hog = e.tenant_create("hog", nslots=1)
+    lat = e.tenant_create("lat", nslots=1)
+    s = e.adapt_state(hog)
+    s.tslice_us = q
+    e.set_adapt_state(hog, s)
+    e.wake(hog)
+    e.advance(e.now() + 30 * MS)
+    waits = []
+    for _ in range(5):
+        e.wake(lat)                      # boost-preempts the hog
+        e.advance(e.now() + 100_000)
+        e.block(lat)                     # hog switches back in ...
+        e.advance(e.now() + 20_000)      # ... and 20 us later lat wakes again
+        e.wake(lat)
+        t0 = e.now()
+        while not e.slot_info(e.slot_id(lat, 0))["is_running"] and e.now() - t0 < 20 * MS:
+            e.advance(e.now() + 10_000)
+        waits.append(e.now() - t0)
+        e.block(lat)
+        e.advance(e.now() + 3 * MS)
+    if strict:
+        assert max(waits) > 5 * MS and min(waits) > 1 * MS, waits  # the reference quirk
+    else:
+        assert max(waits) <= 300_000, waits  # within the ratelimit
