@@ -300,6 +300,12 @@ class CreditScheduler : public Scheduler {
     Mask cpus = online() & v.affinity;
     if (cpus.empty()) cpus = online();
     if (cpus.empty()) return v.processor;
+    // Soft affinity (contention class): restrict to it when it is usable --
+    // it contains the current partition or an idler (Xen 4.5's soft step).
+    if (!v.soft.empty()) {
+      Mask sc = cpus & v.soft;
+      if (!sc.empty() && (sc.test(v.processor) || !(sc & idlers_).empty())) cpus = sc;
+    }
     int cpu = cpus.test(v.processor) ? v.processor : cpus.cycle(v.processor);
     Mask idlers = idlers_;
     idlers.set(cpu);
@@ -674,7 +680,7 @@ class CreditScheduler : public Scheduler {
   }
 
   // -------------------------------------------------------- dispatch ----
-  Slot* runq_steal(int peer, int cpu, int pri) {
+  Slot* runq_steal(int peer, int cpu, int pri, bool soft_pass) {
     Slot& peer_cur = curr(peer);
     if (E.parts[peer]->priv && !peer_cur.is_idle()) {
       auto& rq = pc(peer).runq;
@@ -685,6 +691,7 @@ class CreditScheduler : public Scheduler {
         if (v.is_idle()) continue;
         bool hot = (E.now() - v.last_run_time) < (int64_t)E.boot.migration_delay_us * 1000;
         if (hot) E.perfc.incr(PC_vcpu_hot);
+        if (soft_pass && !v.soft.empty() && !v.soft.test(cpu)) continue;
         if (!v.is_running && !hot && v.affinity.test(cpu)) {
           s.stats.migrate_q++;
           E.perfc.incr(PC_migrate_queued);
@@ -708,17 +715,23 @@ class CreditScheduler : public Scheduler {
       E.perfc.incr(PC_load_balance_over);
     else
       E.perfc.incr(PC_load_balance_other);
-    Mask workers = online().andnot(idlers_);
-    workers.clear(cpu);
-    int peer = cpu;
-    while (!workers.empty()) {
-      peer = workers.cycle(peer);
-      workers.clear(peer);
-      // Single-dispatcher design: the peer's runqueue is always lockable.
-      Slot* sp = runq_steal(peer, cpu, s.pri);
-      if (sp) {
-        *stolen = true;
-        return *sp;
+    // Two balance steps (Xen 4.5): slots whose soft affinity includes this
+    // partition first; then, only for an otherwise idle partition, any slot
+    // hard affinity allows (cross-class work conservation).
+    for (int step = 0; step < 2; ++step) {
+      if (step == 1 && s.pri != PRI_IDLE) break;
+      Mask workers = online().andnot(idlers_);
+      workers.clear(cpu);
+      int peer = cpu;
+      while (!workers.empty()) {
+        peer = workers.cycle(peer);
+        workers.clear(peer);
+        // Single-dispatcher design: the peer's runqueue is always lockable.
+        Slot* sp = runq_steal(peer, cpu, s.pri, step == 0);
+        if (sp) {
+          *stolen = true;
+          return *sp;
+        }
       }
     }
     runq_remove(snext);

@@ -586,8 +586,24 @@ void Engine::context_saved(Slot& prev) {
 // while memory-bound tenants, which would only split HBM bandwidth, time-share
 // their context under credit fairness and PBS's long cache-sensitive quanta.
 // The class comes from the PBS counter rates, with two-tick hysteresis, and is
-// enforced through slot affinity (the vcpu-pin path, so migration is the
-// reference's own mechanism).
+// a SOFT affinity (Xen 4.5 semantics): placement, cpu_pick and stealing prefer
+// the class's partitions, but an idle partition of the other class may still
+// steal a waiting slot (work conservation when a class runs dry), and the
+// class tick sends such slots home once they stop running.
+void Engine::send_home(Slot& v) {
+  if (v.class_home < 0 || v.processor == v.class_home || !v.affinity.test(v.class_home)) return;
+  v.home = v.class_home;
+  v.pause_flags |= VPF_MIGRATING;
+  vcpu_sleep_nosync(v);
+  if (!v.is_running) vcpu_migrate(v);
+}
+
+void Engine::place_class(Slot& v, const Mask& m, int home) {
+  v.soft = m;
+  v.class_home = (home >= 0 && m.test(home)) ? home : -1;
+  send_home(v);
+}
+
 void Engine::set_affinity(Slot& v, const Mask& m, int home) {
   v.affinity = m;
   v.home = (home >= 0 && m.test(home)) ? home : -1;
@@ -612,7 +628,14 @@ void Engine::classify_tick(int64_t n) {
     } else {
       t.cls_count++;
     }
-    if (t.cls_count < 2 || c == t.cls) continue;
+    if (t.cls_count < 2 || c == t.cls) {
+      // stolen across classes and no longer running: back to its class home
+      for (int sid : t.slots) {
+        Slot& v = *slots[sid];
+        if (!v.is_running && runnable(v) && !v.soft.empty() && !v.soft.test(v.processor)) send_home(v);
+      }
+      continue;
+    }
     t.cls = c;
     Mask m;
     for (int p = pl->cpus.first(); p >= 0; p = pl->cpus.next(p + 1))
@@ -624,7 +647,7 @@ void Engine::classify_tick(int64_t n) {
     std::vector<int> order;
     for (int p = m.first(); p >= 0; p = m.next(p + 1)) order.push_back(p);
     for (size_t k = 0; k < t.slots.size(); ++k)
-      set_affinity(*slots[t.slots[k]], m, order.empty() ? -1 : order[k % order.size()]);
+      place_class(*slots[t.slots[k]], m, order.empty() ? -1 : order[k % order.size()]);
     emit(TRC_CLASS, 0, t.id, (uint32_t)c, (uint32_t)m.weight());
   }
   process_softirqs();

@@ -52,8 +52,10 @@ struct Slot {  // struct vcpu
   int tenant = -1;  // -1: idle slot of a partition
   int index = 0;    // vcpu_id
   int processor = 0;
-  int home = -1;  // one-shot placement hint for the next migration (class pinning)
-  Mask affinity;
+  int home = -1;        // one-shot placement hint for the next migration
+  int class_home = -1;  // partition of this slot within its contention class
+  Mask affinity;        // hard affinity (vcpu-pin)
+  Mask soft;            // soft affinity (contention class); empty = none
   uint32_t pause_flags = 0;
   int pause_count = 0;
   bool is_running = false;
@@ -248,6 +250,8 @@ class Engine {
   void heartbeat_check(int64_t now);
   void classify_tick(int64_t now);
   void set_affinity(Slot& v, const Mask& m, int home = -1);
+  void place_class(Slot& v, const Mask& m, int home);
+  void send_home(Slot& v);
 
   int64_t sim_now = 0;
 

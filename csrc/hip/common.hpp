@@ -69,7 +69,10 @@ __device__ __forceinline__ void finish(WorkQueue* q, u32* status) {
 // Bit 2 (GATE_DEVTABLE): the table is the device-memory copy refreshed by
 // k_partition_switch (agent-scope polls served on chip) instead of the
 // pinned host table (system-scope polls over PCIe).
-enum GateMode : u32 { GATE_NONE = 0, GATE_TABLE = 1, GATE_PARK = 2, GATE_DEVTABLE = 4 };
+// Bit 3 (GATE_SPATIAL): the two partitions of an XCD are CU halves (shader
+// engines 0-1 vs 2-3) instead of co-resident issue contexts; a workgroup
+// checks only the entry of the half its CU belongs to.
+enum GateMode : u32 { GATE_NONE = 0, GATE_TABLE = 1, GATE_PARK = 2, GATE_DEVTABLE = 4, GATE_SPATIAL = 8 };
 constexpr u32 kParkSpins = 100;  // x ~20 us
 
 #define HIPCHECK(x)                                                                              \
@@ -88,6 +91,11 @@ __device__ __forceinline__ u32 xcc_id() {
 
 __device__ __forceinline__ u32 hw_id() { return __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4); }
 
+// CU half of this wave: HW_ID.SE_ID is bits 15:13; MI355X XCDs have four
+// shader engines (logical CU i of an XCD sits on SE i % 4, measured with the
+// census kernel under one-bit CU masks), so SE >> 1 splits an XCD 16/16.
+__device__ __forceinline__ u32 cu_half() { return (hw_id() >> 14) & 1u; }
+
 __device__ __forceinline__ u32 load_sys(const u32* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -99,6 +107,7 @@ __device__ __forceinline__ bool owns(const PartTable* t, u32 mode, u32 me, u32 x
   const u64 pair = (mode & GATE_DEVTABLE)
                        ? __hip_atomic_load(&t->pair[xcc & 7], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                        : __hip_atomic_load(&t->pair[xcc & 7], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (mode & GATE_SPATIAL) return (u32)(pair >> (32 * cu_half())) == me;
   return (u32)pair == me || (u32)(pair >> 32) == me;
 }
 

@@ -53,6 +53,7 @@ struct GpuCtx {
   int device = 0;
   int part_base = 0;  // engine partition id of XCD 0
   int table_mode = 0; // 0: pinned host table, 1: device table + partition_switch kernel
+  int spatial = 0;    // 1: the two partitions of an XCD are CU halves (GATE_SPATIAL)
   PartTable* h_table = nullptr;  // pinned host (device-visible)
   PartTable* d_table = nullptr;  // device copy (table_mode 1)
   u64* d_cnt = nullptr;          // [kMaxTenants][kXcds][kNumPmc]
@@ -210,10 +211,24 @@ typedef struct gpbs_runner_stats {
 
 namespace {
 
+// CU mask of one half of every XCD.  hipExtStreamCreateWithCUMask bit b
+// selects logical CU b/8 of XCD b%8 (an XCD left with no bit runs
+// unrestricted), and logical CU i sits on shader engine i%4, so half h is the
+// bits whose SE is 2h or 2h+1 (measured: scripts/interfere.py census map).
+hipStream_t make_half_stream(int h) {
+  uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int b = 0; b < 256; ++b)
+    if ((((b / 8) % 4) >> 1) == h) m[b / 32] |= 1u << (b % 32);
+  hipStream_t s = nullptr;
+  if (hipExtStreamCreateWithCUMask(&s, 8, m) != hipSuccess) return nullptr;
+  return s;
+}
+
 struct Runner {
   GpuCtx* ctx;
   gpbs_runner_cfg_t cfg;
   hipStream_t stream = nullptr;
+  hipStream_t half_stream[2] = {nullptr, nullptr};  // spatial mode: CU-masked to one half
   WorkQueue* d_q = nullptr;  // ring of depth+1 queues
   u32* h_status = nullptr;   // pinned status words
   int nq = 0;
@@ -239,11 +254,27 @@ struct Runner {
     return 0;
   }
 
-  int launch(int qi) {
+  // Spatial mode: launch on the stream masked to the CU half the tenant holds
+  // (class pinning keeps a classified tenant on one half); a tenant holding
+  // both halves or none (yet) launches unmasked and gates per workgroup.
+  hipStream_t pick_stream() {
+    if (!ctx->spatial || !cfg.gate) return stream;
+    bool h[2] = {false, false};
+    for (int x = 0; x < kXcds; ++x)
+      for (int c = 0; c < 2; ++c)
+        if (__atomic_load_n(&ctx->h_table->owner[2 * x + c], __ATOMIC_ACQUIRE) == (u32)cfg.tenant) h[c] = true;
+    if (h[0] == h[1]) return stream;
+    const int k = h[0] ? 0 : 1;
+    if (!half_stream[k]) half_stream[k] = make_half_stream(k);
+    return half_stream[k] ? half_stream[k] : stream;
+  }
+
+  int launch(int qi, hipStream_t stream) {
     WorkQueue* q = d_q + qi;
     const bool dev = __atomic_load_n(&ctx->table_mode, __ATOMIC_ACQUIRE) == 1;
     const void* tab = dev ? (const void*)ctx->d_table : (const void*)ctx->h_table;
-    const unsigned mode = (cfg.gate ? (cfg.gate == 2 ? GATE_PARK : GATE_TABLE) : GATE_NONE) | (dev ? GATE_DEVTABLE : 0);
+    const unsigned mode = (cfg.gate ? (cfg.gate == 2 ? GATE_PARK : GATE_TABLE) : GATE_NONE) | (dev ? GATE_DEVTABLE : 0) |
+                          (cfg.gate && ctx->spatial ? GATE_SPATIAL : 0);
     const unsigned me = (unsigned)cfg.tenant;
     __atomic_store_n(&h_status[qi], 0u, __ATOMIC_RELEASE);
     st.launches++;
@@ -330,6 +361,7 @@ struct Runner {
           }
           wait_owner();
           if (stop) break;
+          hipStream_t stream = pick_stream();
           if (fresh) {
             std::lock_guard<std::mutex> g(mu);
             pending--;
@@ -343,7 +375,7 @@ struct Runner {
             // resume the same queue: clear exit bookkeeping only
             hipMemsetAsync(&d_q[qi].exited, 0, sizeof(u32) * 2, stream);
           }
-          if (launch(qi) != 0) err = -5;
+          if (launch(qi, stream) != 0) err = -5;
           const int e = qi;  // one event per queue slot
           hipEventRecord(ev[e], stream);
           fl.push_back({qi, e});
@@ -392,6 +424,8 @@ struct Runner {
       if (stop) break;
     }
     hipStreamSynchronize(stream);
+    for (hipStream_t h : half_stream)
+      if (h) hipStreamSynchronize(h);
     std::lock_guard<std::mutex> g(mu);
     idle_cv.notify_all();
   }
@@ -496,6 +530,13 @@ int gpbs_gpu_set_nctx(void* p, int nctx) {
 
 // Switch between the pinned host table (0) and the device table (1).  The
 // device copy is re-synchronised before device mode takes effect.
+int gpbs_gpu_set_spatial(void* p, int on) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c) return -22;
+  __atomic_store_n(&c->spatial, on ? 1 : 0, __ATOMIC_RELEASE);
+  return 0;
+}
+
 int gpbs_gpu_set_table_mode(void* p, int mode) {
   GpuCtx* c = (GpuCtx*)p;
   std::lock_guard<std::mutex> g(c->mu);
@@ -692,6 +733,8 @@ void gpbs_runner_destroy(void* p) {
   hipStreamSynchronize(r->stream);
   for (int i = 0; i < r->nq; ++i) hipEventDestroy(r->ev[i]);
   hipStreamDestroy(r->stream);
+  for (hipStream_t h : r->half_stream)
+    if (h) hipStreamDestroy(h);
   hipFree(r->d_q);
   hipHostFree(r->h_status);
   delete r;

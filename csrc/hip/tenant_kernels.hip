@@ -185,8 +185,8 @@ __global__ __launch_bounds__(GNT, 2) void k_gemm_bf16_tn(const u16* __restrict__
 // 256-thread workgroup per CU keeps 64 KiB of reads in flight (enough for
 // HBM3E at ~2 us loaded latency) while occupying only one wave slot per SIMD,
 // so a co-resident GEMM keeps its two waves/SIMD (VGPR budget 512/SIMD: GEMM
-// 2x136 + stream 80 + reduce 80 + gemv 40 fits; the old 4 WG/CU grids did not).
-constexpr int SNT = 256, SUNROLL = 16, RUNROLL = 8;
+// 2x136 + stream 80 + reduce 64 + gemv 96 = 512 fits; the old 4 WG/CU grids did not).
+constexpr int SNT = 256, SUNROLL = 16, RUNROLL = 6;
 
 __global__ __launch_bounds__(SNT) void k_stream_copy(const f32x4* __restrict__ src, f32x4* __restrict__ dst,
                                                     u64 n4, u32 chunk4, WorkQueue* q, const PartTable* table, u32 mode,
@@ -276,8 +276,23 @@ __global__ __launch_bounds__(SNT) void k_reduce_bf16(const u32x4* __restrict__ a
 
 // --------------------------------------------------------------- GEMV -----
 // y[R] = W[R][K] x[K] (bf16 in, fp32 out): the latency-critical "idle" tenant
-// request (a decode-step sized matvec).  One wave per row, 16 B per lane.
-__global__ __launch_bounds__(256) void k_gemv_bf16(const u16* __restrict__ W, const u16* __restrict__ x,
+// request (a decode-step sized matvec).  A wave owns 4 rows; each lane streams
+// 16 B per row per 512-column chunk straight into VGPRs, GV_U chunks (4 rows
+// x GV_U W loads + GV_U x loads) in flight before the first use -- no LDS
+// round trip, no per-load guards (rows past R are clamped, not branched).
+constexpr int GV_U = 2;
+
+__device__ __forceinline__ float dot8(const u32x4 w, const u32x4 v) {
+  float s = 0.f;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    s += __uint_as_float(w[e] << 16) * __uint_as_float(v[e] << 16);
+    s += __uint_as_float(w[e] & 0xffff0000u) * __uint_as_float(v[e] & 0xffff0000u);
+  }
+  return s;
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_gemv_bf16(const u16* __restrict__ W, const u16* __restrict__ x,
                                                   float* __restrict__ y, int R, int K, WorkQueue* q,
                                                   const PartTable* table, u32 mode, u32 me, u64* cnt,
                                                   u32* status) {
@@ -288,28 +303,43 @@ __global__ __launch_bounds__(256) void k_gemv_bf16(const u16* __restrict__ W, co
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const u32 nchunks = (u32)((R + 15) / 16);  // 16 rows per unit (4 per wave)
   const u64 lines = (u64)16 * K * 2 / 128;
+  const int nk = K / 512;  // 512 columns per wave-wide chunk (8 per lane)
+  const u32x4* xv = (const u32x4*)x;
   for (;;) {
     const int c = grab_unit(q, table, mode, me, xcc, s_slot, nchunks);
     if (c < 0) break;
-    for (int rr = 0; rr < 4; ++rr) {
-      const int row = c * 16 + wid * 4 + rr;
-      if (row >= R) break;
-      float s = 0.f;
-      const uint4* wr = (const uint4*)(W + (size_t)row * K);
-      const uint4* xv = (const uint4*)x;
-      for (int k = lane; k < K / 8; k += 64) {
-        uint4 w = wr[k], v = xv[k];
-        const u32* pw = (const u32*)&w;
-        const u32* pv = (const u32*)&v;
+    const int row0 = c * 16 + wid * 4;
+    const u32x4* wr[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          s += bf2f((u16)(pw[e] & 0xffff)) * bf2f((u16)(pv[e] & 0xffff));
-          s += bf2f((u16)(pw[e] >> 16)) * bf2f((u16)(pv[e] >> 16));
-        }
+    for (int r = 0; r < 4; ++r) wr[r] = (const u32x4*)(W + (size_t)min(row0 + r, R - 1) * K);
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    int kc = 0;
+    for (; kc + GV_U <= nk; kc += GV_U) {
+      u32x4 xr[GV_U], wv[GV_U][4];
+#pragma unroll
+      for (int u = 0; u < GV_U; ++u) {
+        const int k = (kc + u) * 64 + lane;
+        xr[u] = xv[k];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) wv[u][r] = __builtin_nontemporal_load(wr[r] + k);
       }
 #pragma unroll
+      for (int u = 0; u < GV_U; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] += dot8(wv[u][r], xr[u]);
+    }
+    for (; kc < nk; ++kc) {
+      const int k = kc * 64 + lane;
+      const u32x4 xr = xv[k];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[r] += dot8(__builtin_nontemporal_load(wr[r] + k), xr);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float s = acc[r];
+#pragma unroll
       for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-      if (lane == 0) y[row] = s;
+      if (lane == 0 && row0 + r < R) y[row0 + r] = s;
     }
     count_unit(cnt, me, xcc, (u64)16 * (K / 512 + 8), &t_last, lines, lines, q);
   }

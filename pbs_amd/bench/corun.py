@@ -27,11 +27,15 @@ Policies (same tenants, same box):
   static  equal static XCD split (2 XCDs per tenant, ARINC-653-like)
   gpbs1   PBS adaptive credit scheduler, one exclusive context per XCD,
           kernels exit on revoked XCDs
-  gpbs-exit   two issue contexts per XCD + contention classes, exit gating
-  gpbs-nogang the flagship without gang alignment of the context classes
-  gpbs    PBS adaptive credit scheduler over both issue contexts of every XCD:
-          counter-driven compute/memory classes, gang-aligned memory context,
-          parked gating on a device-resident partition table (the flagship)
+  gpbs-exit   two co-resident issue contexts per XCD + contention classes,
+          workgroups exit on revocation, host table
+  gpbs-ctx    co-resident issue contexts, parked gating, device table
+  gpbs-nogang the flagship without gang alignment of the classes
+  gpbs    PBS adaptive credit scheduler over spatial partitions: each XCD is
+          split into two CU halves (shader engines 0-1 / 2-3) that host the
+          counter-driven compute and memory classes (soft affinity, work
+          conserving), gang-aligned per class, parked gating on a
+          device-resident partition table, half-masked streams (the flagship)
 """
 from __future__ import annotations
 
@@ -72,8 +76,9 @@ class CorunConfig:
 POLICY_ENGINES = {
     # name: (issue contexts per XCD, engine overrides on top of MI355X_PROFILE,
     #        kernel gate mode, partition-table location)
-    "gpbs": (2, {}, "park", "device"),
-    "gpbs-nogang": (2, {"coschedule": 2}, "park", "device"),
+    "gpbs": (2, {}, "park", "device,spatial"),
+    "gpbs-ctx": (2, {}, "park", "device"),
+    "gpbs-nogang": (2, {"coschedule": 2}, "park", "device,spatial"),
     "gpbs-exit": (2, {}, True, "host"),
     "gpbs1": (1, {"coschedule": 0}, True, "host"),
     "credit2": (2, {"sched": "credit-fixed"}, "park", "device"),
@@ -181,7 +186,8 @@ class Corun:
         if policy in self.engines:
             e = self.engines[policy]
             _, _, gate, table = POLICY_ENGINES[policy]
-            self.ctx.set_table_mode(table)
+            self.ctx.set_table_mode(table.split(",")[0])
+            self.ctx.set_spatial("spatial" in table)
             self.ctx.attach(e, nctx=e._gpbs_nctx)
             e.start()
             self.active_engine = e
@@ -192,6 +198,7 @@ class Corun:
                 coll.gate, coll.engine = True, e
             return
         self.ctx.set_table_mode("host")
+        self.ctx.set_spatial(False)
         for r in self._natives():
             r.set_engine_wake(False)
         if not isinstance(coll, Runner):

@@ -105,12 +105,37 @@ def gemv_bf16(W: torch.Tensor, x: torch.Tensor, out: Optional[torch.Tensor] = No
     return out
 
 
-def census(blocks: int = 2048, table=None, tenant: int = 0, stream=None) -> torch.Tensor:
-    """Per-workgroup (XCC_ID, HW_ID, owned, magic)."""
+GATE_SPATIAL = 8
+
+
+def census(blocks: int = 2048, table=None, tenant: int = 0, stream=None, spatial: bool = False) -> torch.Tensor:
+    """Per-workgroup (XCC_ID, HW_ID, owned, magic).  ``stream`` may be a torch
+    stream or a raw hipStream_t handle (int / c_void_p, e.g. a CU-masked one)."""
     out = torch.zeros(blocks * 4, dtype=torch.int32, device="cuda")
-    rc = lib().gpbs_hip_census(_ptr(out), blocks, table, GATE_TABLE if table else GATE_NONE, tenant, _stream(stream))
+    mode = (GATE_TABLE if table else GATE_NONE) | (GATE_SPATIAL if spatial and table else 0)
+    s = C.c_void_p(stream if isinstance(stream, int) else stream.value) if isinstance(stream, (int, C.c_void_p)) \
+        else _stream(stream)
+    rc = lib().gpbs_hip_census(_ptr(out), blocks, table, mode, tenant, s)
     _check(rc, "census")
     return out.view(blocks, 4)
+
+
+def half_cu_mask(h: int):
+    """CU-mask words selecting CU half ``h`` (shader engines 2h, 2h+1) of every
+    XCD: bit b = logical CU b/8 of XCD b%8, logical CU i on SE i%4."""
+    words = [0] * 8
+    for b in range(256):
+        if ((b // 8) % 4) >> 1 == h:
+            words[b // 32] |= 1 << (b % 32)
+    return words
+
+
+def cumask_stream(words, device: int = 0) -> int:
+    arr = (C.c_uint32 * len(words))(*words)
+    h = lib().gpbs_gpu_cumask_stream(device, arr, len(words), 0)
+    if not h:
+        raise RuntimeError("hipExtStreamCreateWithCUMask failed")
+    return h
 
 
 def counter_reduce(cnt: torch.Tensor, prev: torch.Tensor, ids: torch.Tensor, stream=None) -> torch.Tensor:

@@ -95,6 +95,15 @@ class GpuContext:
         if rc:
             raise RuntimeError("set_table_mode failed")
 
+    def set_spatial(self, on: bool):
+        """Spatial partitions: the two partitions of an XCD are CU halves
+        (shader engines 0-1 / 2-3) -- runners launch on half-masked streams
+        and workgroups gate on their CU's half -- instead of co-resident
+        issue contexts."""
+        rc = self.L.gpbs_gpu_set_spatial(self.h, 1 if on else 0)
+        if rc:
+            raise RuntimeError("set_spatial failed")
+
     def ownership(self, tenant: int, clear: bool = False):
         """Seconds `tenant` held each issue context (summed over XCDs)."""
         out = (C.c_int64 * CTX)()

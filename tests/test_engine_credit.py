@@ -347,3 +347,66 @@ def test_ratelimit_hold_does_not_inherit_adaptive_quantum(strict):
         assert max(waits) > 5 * MS and min(waits) > 1 * MS, waits  # the reference quirk
     else:
         assert max(waits) <= 300_000, waits  # within the ratelimit
+
+
+def _feed(e, rates, dt_us):
+    """Advance the sim clock, charging modeled counters to running slots:
+    rates[tenant] = (inst, miss) per us of run time."""
+    for t, (ins, miss) in rates.items():
+        for k in range(e.tenant_info(t).nslots):
+            sid = e.slot_id(t, k)
+            si = e.slot_info(sid)
+            if si["is_running"]:
+                p = list(si["pmc"])
+                p[0] += ins * dt_us
+                p[1] += dt_us * 2000
+                p[2] += miss * dt_us * 4
+                p[3] += miss * dt_us
+                e.set_pmc(sid, p)
+    e.advance(e.now() + dt_us * 1000)
+
+
+def _procs(e, t):
+    return [e.slot_info(e.slot_id(t, k))["processor"] for k in range(e.tenant_info(t).nslots)]
+
+
+def test_contention_classes_are_soft_affinity_and_work_conserving():
+    """coschedule=2: counter rates classify tenants (compute -> context 0,
+    memory -> context 1), slots spread one per partition of their class; the
+    class is soft: an idle compute context steals waiting memory slots, and
+    they go home once the compute tenant is back."""
+    parts = [(0, x, c) for x in range(4) for c in range(2)]
+    e = Engine(sim_clock=True, partitions=parts, coschedule=2, class_period_us=2000, quantum_align_us=0)
+    e.tenant_create("Domain-0", nslots=1)
+    comp = e.tenant_create("gemm", nslots=4)
+    mem = e.tenant_create("hbm", nslots=8)
+    rates = {comp: (1000, 1), mem: (100, 100)}
+    e.wake(comp)
+    e.wake(mem)
+    for _ in range(300):  # 30 ms
+        _feed(e, rates, 100)
+    ctx = {p: c for p, (_, _, c) in enumerate(parts)}
+    assert all(ctx[p] == 0 for p in _procs(e, comp)), _procs(e, comp)
+    home = _procs(e, mem)
+    assert sorted(home) == sorted([p for p in ctx if ctx[p] == 1] * 2), home  # two per memory partition
+    # compute tenant goes idle: its partitions steal waiting memory slots
+    e.block(comp)
+    base = e.tenant_info(mem).run_ns
+    t0 = e.now()
+    for _ in range(100):
+        _feed(e, rates, 100)
+    share = (e.tenant_info(mem).run_ns - base) / (e.now() - t0)
+    assert share > 6.0, share
+    # compute tenant returns: it gets its context back, strays go home
+    e.wake(comp)
+    for _ in range(100):
+        _feed(e, rates, 100)
+    base_c, t0 = e.tenant_info(comp).run_ns, e.now()
+    for _ in range(100):
+        _feed(e, rates, 100)
+    assert (e.tenant_info(comp).run_ns - base_c) / (e.now() - t0) > 3.5
+    for k in range(8):
+        si = e.slot_info(e.slot_id(mem, k))
+        if not si["is_running"]:
+            assert ctx[si["processor"]] == 1, (k, si["processor"])
+    assert e.check() == ""

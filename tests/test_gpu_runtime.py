@@ -95,3 +95,32 @@ def test_static_split_runs_concurrently():
     r1.close()
     r2.close()
     ctx.close()
+
+
+def _se(hwid):
+    return (int(hwid) >> 13) & 7
+
+
+def test_half_cu_mask_stream_confines_workgroups_to_one_half():
+    from pbs_amd.ops import kernels as K
+    for h in (0, 1):
+        s = K.cumask_stream(K.half_cu_mask(h))
+        out = K.census(1024, stream=s).cpu()
+        torch.cuda.synchronize()
+        K.lib().gpbs_gpu_stream_destroy(__import__("ctypes").c_void_p(s))
+        assert (out[:, 3] == 0xC0FFEE).all()
+        ses = {_se(v) for v in out[:, 1].tolist()}
+        assert ses and all(se >> 1 == h for se in ses), (h, ses)
+        assert len({int(x) for x in out[:, 0].tolist()}) == 8  # every XCD still used
+
+
+def test_spatial_gate_follows_the_cu_half():
+    from pbs_amd.ops import kernels as K
+    ctx = GpuContext(0, None, nctx=2)
+    ctx.set_owners([t for x in range(8) for t in (1, 2)])  # tenant 1: half 0, tenant 2: half 1
+    for me, half in ((1, 0), (2, 1)):
+        out = K.census(2048, table=ctx.table, tenant=me, spatial=True).cpu()
+        for xcc, hw, ok, magic in out.tolist():
+            assert magic == 0xC0FFEE
+            assert bool(ok) == ((_se(hw) >> 1) == half), (me, xcc, hex(hw))
+    ctx.close()
