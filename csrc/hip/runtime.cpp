@@ -29,6 +29,7 @@
 using namespace gpbs_hip;
 
 extern "C" {
+int gpbs_hip_gemm_units(int, int);
 int gpbs_hip_gemm_bf16(const void*, const void*, void*, int, int, int, void*, const void*, unsigned, unsigned, void*,
                        void*, int, hipStream_t);
 int gpbs_hip_stream_copy(const void*, void*, unsigned long long, unsigned, void*, const void*, unsigned, unsigned,
@@ -246,7 +247,7 @@ struct Runner {
 
   u32 unit_total() const {
     switch (cfg.kind) {
-      case K_GEMM: return (u32)((cfg.M / 128) * (cfg.N / 128));
+      case K_GEMM: return (u32)gpbs_hip_gemm_units(cfg.M, cfg.N);
       case K_STREAM:
       case K_REDUCE: return (u32)((cfg.bytes + cfg.chunk_bytes - 1) / cfg.chunk_bytes);
       case K_GEMV: return (u32)((cfg.M + 15) / 16);

@@ -180,6 +180,197 @@ __global__ __launch_bounds__(GNT, 2) void k_gemm_bf16_tn(const u16* __restrict__
   finish(q, status);
 }
 
+// -------------------------------------------------------- GEMM 256x256 ----
+// The fast path for M, N % 256 == 0 (the co-run GEMM tenant): 256x256 output
+// tile per workgroup, BK = 64, 8 waves as 2(M) x 4(N), 128x64 per wave, one
+// workgroup per CU (128 KiB LDS).  Halving the A/B panel traffic per FLOP vs
+// the 128x128 kernel matters twice here: solo throughput, and how hard the
+// GEMM leans on the L2 a co-running memory tenant also streams through.
+//
+// Schedule (8 phases per 2 K-tiles; one phase = one 64x32 C-quadrant x K=64
+// = 16 MFMA per wave), per K-tile t in LDS buffer t&1:
+//   phase  reads (ds_read_b128)     stages (global_load_lds, 2 per thread)
+//   k0     A rows mi=0 (8) + B ni=0 (4)   B-half1 of tile t+1
+//   k1     B ni=1 (4)                     A-half1 of tile t+1
+//   k2     A rows mi=1 (8)                B-half0 of tile t+2
+//   k3     --                             A-half0 of tile t+2, then vmcnt(4)
+// A half h = rows 128h.. (read only by waves wr == h), B half h = columns
+// 128h.. (waves wc >> 1 == h).  WAR: a buffer half is restaged one phase
+// after the phase that last read it (A halves: k2 -> k3, B halves: k1 -> k2);
+// every wave's ds_reads of a phase are retired (lgkmcnt(0)) before that
+// phase's closing barrier.  RAW: tile t+1 is retired by the counted vmcnt at
+// (t, k3) -- only tile t+2's two halves stay in flight across the barrier --
+// and first read at (t+1, k0).  Raw s_barrier (no __syncthreads: its fence
+// would drain the LDS-DMA queue), all LDS in one __shared__ array.
+// LDS image: [buf][A|B][half][128 rows][128 B], 16-B chunk c of row r stored
+// at slot c ^ ((r >> 1) & 7): a 16-lane ds_read_b128 group (16 consecutive
+// rows, one logical chunk) covers all 16 slots of a 256-B bank row.
+constexpr int G2_BM = 256, G2_BK = 64, G2_NT = 512;
+constexpr int kG2Half = 128 * 128;           // bytes per half-tile
+constexpr int kG2Buf = 4 * kG2Half;          // A0 A1 B0 B1
+constexpr int kG2Lds = 2 * kG2Buf;           // 128 KiB
+
+__device__ __forceinline__ int g2_swz(int r) { return (r >> 1) & 7; }
+
+__global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restrict__ A, const u16* __restrict__ Bt,
+                                                             u16* __restrict__ C, int M, int N, int K, WorkQueue* q,
+                                                             const PartTable* table, u32 mode, u32 me, u64* cnt,
+                                                             u32 inst_per_tile, u32 refs_per_tile, u32 miss_per_tile,
+                                                             u32* status) {
+  __shared__ __attribute__((aligned(16))) char smem[kG2Lds + 16];
+  lds_t* lds = (lds_t*)smem;
+  int* s_slot = (int*)(smem + kG2Lds);
+  const u32 xcc = xcc_id();
+  u64 t_last = __builtin_amdgcn_s_memtime();
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  const int tiles_m = M / G2_BM, tiles_n = N / G2_BM, ntiles = tiles_m * tiles_n;
+  const int nt = K / G2_BK;
+
+  // Staging geometry: wave w's glds j writes 1 KiB chunk c = 2w + j of a
+  // half-tile = rows 8c .. 8c+7; lane -> row 8c + lane/8, slot lane%8, source
+  // chunk slot ^ swz(row).  Same offsets for every half (A or B, h = 0/1).
+  int soff[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = 8 * (2 * wid + j) + (lane >> 3);
+    soff[j] = row * K + (((lane & 7) ^ g2_swz(row)) * 8);
+  }
+  const int l16 = lane & 15, lq = lane >> 4;
+
+  for (;;) {
+    const int tile = grab_unit(q, table, mode, me, xcc, s_slot, (u32)ntiles);
+    if (tile < 0) break;
+    const int tm = tile / tiles_n, tn = tile % tiles_n;
+    const u16* Ab = A + (size_t)tm * G2_BM * K;
+    const u16* Bb = Bt + (size_t)tn * G2_BM * K;
+
+    // stage(kind, h, t): kind 0 = A, 1 = B; half h of K-tile t.
+    auto stage = [&](int kind, int h, int t) {
+      if (t >= nt) return;
+      const u16* src = (kind ? Bb : Ab) + (size_t)h * 128 * K + t * G2_BK;
+      lds_t* dst = lds + (t & 1) * kG2Buf + (kind * 2 + h) * kG2Half + wid * 2048;
+      glds16(src + soff[0], dst);
+      glds16(src + soff[1], dst + 1024);
+    };
+    // Fragment read: 16 rows starting at `r0` of half-tile (kind, h) of
+    // buffer b, k-substep s (32 k): lane reads row r0 + l16, logical chunk 4s + lq.
+    auto frag = [&](int b, int kind, int h, int r0, int s) -> bf16x8 {
+      const int r = r0 + l16;
+      const lds_t* p = lds + b * kG2Buf + (kind * 2 + h) * kG2Half + r * 128 + (((4 * s + lq) ^ g2_swz(r)) << 4);
+      return *(const __attribute__((address_space(3))) bf16x8*)p;
+    };
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // Prologue: all of tile 0, the first two halves of tile 1.
+    stage(1, 0, 0); stage(0, 0, 0); stage(1, 1, 0); stage(0, 1, 0);
+    stage(1, 0, 1); stage(0, 0, 1);
+    if (nt > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+
+    const int bh = wc >> 1;          // B half this wave reads
+    const int bc = (wc & 1) * 64;    // its 64 columns within the half
+    bf16x8 a[4][2], b0[2][2], b1[2][2];
+    for (int t = 0; t < nt; ++t) {
+      const int buf = t & 1;
+      // ---- k0: quadrant (mi 0, ni 0)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) b0[j][s] = frag(buf, 1, bh, bc + j * 16, s);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) a[i][s] = frag(buf, 0, wr, i * 16, s);
+      stage(1, 1, t + 1);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[j][s], a[i][s], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_barrier();
+      // ---- k1: quadrant (mi 0, ni 1)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) b1[j][s] = frag(buf, 1, bh, bc + 32 + j * 16, s);
+      stage(0, 1, t + 1);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+            acc[i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j][s], a[i][s], acc[i][2 + j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_barrier();
+      // ---- k2: quadrant (mi 1, ni 1)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) a[i][s] = frag(buf, 0, wr, 64 + i * 16, s);
+      stage(1, 0, t + 2);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+            acc[4 + i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j][s], a[i][s], acc[4 + i][2 + j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_barrier();
+      // ---- k3: quadrant (mi 1, ni 0); retire tile t+1
+      stage(0, 0, t + 2);
+      if (t + 2 < nt) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+            acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[j][s], a[i][s], acc[4 + i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_barrier();
+    }
+    // Epilogue: mfma(B, A) holds C^T per 16x16 block -- lane owns
+    // C[m = .. + l16][n = .. + 4 lq + r], r = 0..3: one 8-byte store.
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = tm * G2_BM + wr * 128 + i * 16 + l16;
+        const int n = tn * G2_BM + wc * 64 + j * 16 + 4 * lq;
+        const u32 lo = (u32)f2bf(acc[i][j][0]) | ((u32)f2bf(acc[i][j][1]) << 16);
+        const u32 hi = (u32)f2bf(acc[i][j][2]) | ((u32)f2bf(acc[i][j][3]) << 16);
+        *(uint2*)(C + (size_t)m * N + n) = make_uint2(lo, hi);
+      }
+    count_unit(cnt, me, xcc, inst_per_tile, &t_last, refs_per_tile, miss_per_tile, q);
+  }
+  finish(q, status);
+}
+
 // ------------------------------------------------------------ HBM stream ---
 // dst = src (float4 copy), 16 B per lane, 16 loads in flight per thread: one
 // 256-thread workgroup per CU keeps 64 KiB of reads in flight (enough for
@@ -371,9 +562,25 @@ using namespace gpbs_hip;
 
 extern "C" {
 
+int gpbs_hip_gemm_units(int M, int N) {
+  if (M % G2_BM == 0 && N % G2_BM == 0) return (M / G2_BM) * (N / G2_BM);
+  return (M / GBM) * (N / GBN);
+}
+
 int gpbs_hip_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int K, void* q, const void* table,
                        unsigned mode, unsigned me, void* cnt, void* status, int grid, hipStream_t s) {
   if (M % GBM || N % GBN || K % GBK || M <= 0 || N <= 0 || K <= 0) return -22;
+  if (M % G2_BM == 0 && N % G2_BM == 0) {
+    const int ntiles = (M / G2_BM) * (N / G2_BM);
+    if (grid <= 0) grid = 256;  // one workgroup per CU
+    if (grid > ntiles) grid = ntiles;
+    const u32 inst = (u32)((G2_BM / 16) * (G2_BM / 16) * (K / 32) + (K / G2_BK) * 64 + 128);
+    const u32 refs = (u32)(((u64)2 * G2_BM * K * 2) / 128);
+    const u32 miss = (u32)((((u64)M + N) * K * 2 / 128) / ntiles + (u64)G2_BM * G2_BM * 2 / 128);
+    hipLaunchKernelGGL(k_gemm256_bf16_tn, dim3(grid), dim3(G2_NT), 0, s, (const u16*)A, (const u16*)Bt, (u16*)C, M, N,
+                       K, (WorkQueue*)q, (const PartTable*)table, mode, me, (u64*)cnt, inst, refs, miss, (u32*)status);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+  }
   const int ntiles = (M / GBM) * (N / GBN);
   if (grid <= 0) grid = 256 * 2;
   if (grid > ntiles) grid = ntiles;

@@ -21,7 +21,10 @@ def _lib():
     N.load_hip(required=True)
 
 
-@pytest.mark.parametrize("M,Nn,Kd", [(128, 128, 64), (256, 384, 512), (1024, 512, 1024), (4096, 4096, 4096)])
+# 128x128-tile path: (128,128,64), (256,384,512); 256x256 8-phase path (M, N %
+# 256 == 0): K-tile counts 1, 2, 3, 16 and 64 exercise prologue/tail waits.
+@pytest.mark.parametrize("M,Nn,Kd", [(128, 128, 64), (256, 384, 512), (256, 256, 64), (512, 768, 128),
+                                     (768, 512, 192), (1024, 512, 1024), (4096, 4096, 4096)])
 def test_gemm_bf16_matches_fp32_reference(M, Nn, Kd):
     g = torch.Generator(device="cuda").manual_seed(M + Nn + Kd)
     A = torch.randn(M, Kd, device="cuda", dtype=torch.bfloat16, generator=g)
@@ -35,9 +38,9 @@ def test_gemm_bf16_matches_fp32_reference(M, Nn, Kd):
     assert (err / (ref.abs() + 1)).mean().item() < 5e-3
 
 
-def test_gemm_asymmetric_identity():
+@pytest.mark.parametrize("n", [256, 384, 512])
+def test_gemm_asymmetric_identity(n):
     """A = I with an asymmetric B catches row/col swaps in the C write."""
-    n = 256
     A = torch.eye(n, device="cuda", dtype=torch.bfloat16)
     B = (torch.arange(n * n, device="cuda", dtype=torch.float32).view(n, n) % 97 - 48).to(torch.bfloat16)
     out = K.gemm_bf16(A, B)  # = A @ B^T = B^T
