@@ -71,6 +71,7 @@ struct CDom : SchedTenantData {
   AdaptState adapt{};
   uint64_t pmc[kNumPmc] = {0, 0, 0, 0};  // last per-tenant deltas (sdom->pmc)
   uint64_t spinlock_latency = 0, spinlock_metric_update = 0, spinlock_count = 0, report_total = 0;
+  uint64_t lock_hold_ns = 0, lock_hold_count = 0;
   uint64_t pending_requests = 0;
   uint64_t cache_miss_rate = 0, cpi = 0;
   uint64_t rate_ewma = 0;  // smoothed miss rate (alpha 1/4) for contention classes
@@ -200,6 +201,40 @@ class CreditScheduler : public Scheduler {
     auto s = std::make_unique<CSlot>();
     s->pri = v.is_idle() ? PRI_IDLE : PRI_UNDER;
     v.priv = std::move(s);
+    if (mode_ == Mode::ATC && !v.is_idle()) atc_place(v);
+  }
+
+  // ATC placement (X:xen/common/sched_credit_atc.c:634-651, called from
+  // alloc_vdata :1171): a new slot goes to the least-loaded partition (runq
+  // length, :572-632) not already used by a sibling slot, and every slot of
+  // the tenant is then hard-pinned away from its siblings' partitions
+  // (set_vcpu_affinity :545-570), so a tenant's slots never queue behind one
+  // another -- the ATC answer to lock-holder preemption.
+  void atc_place(Slot& v) {
+    Tenant* t = E.tenant(v.tenant);
+    if (!t || cpus_.empty()) return;
+    Mask used;
+    for (int sid : t->slots)
+      if (sid != v.id && E.slots[sid]) used.set(E.slots[sid]->processor);
+    Mask cand = (cpus_ & v.affinity).andnot(used);
+    if (cand.empty()) cand = cpus_ & v.affinity;
+    if (cand.empty()) cand = cpus_;
+    int best = cand.first();
+    size_t best_load = pc(best).runq.size();
+    for (int c = cand.first(); c >= 0; c = cand.next(c + 1))
+      if (pc(c).runq.size() < best_load) {
+        best = c;
+        best_load = pc(c).runq.size();
+      }
+    v.processor = best;
+    used.set(best);
+    for (int sid : t->slots) {
+      if (!E.slots[sid]) continue;
+      Slot& w = *E.slots[sid];
+      Mask aff = cpus_.andnot(used);
+      aff.set(w.processor);
+      w.affinity = aff;
+    }
   }
 
   void insert_vcpu(Slot& v) override {
@@ -667,8 +702,25 @@ class CreditScheduler : public Scheduler {
     if (!E.boot.default_yield) sv(v).flags |= FLAG_YIELD;
   }
 
-  void report(Tenant& d, uint64_t wait, int) override {
+  // Report kinds (GPBS_REPORT_*): 1 wait (the vcrd_op spin report, P2),
+  // 2 lock hold time (P8's prepared spinstat_op(holdtime, 2),
+  // L:kernel/lockdep.c:3754-3759 -- tracked, not fed to adaptation, as in the
+  // reference where the hook stayed commented out), 3 request arrivals (P7:
+  // `wait` carries the count, the event-channel port-44 counter of
+  // X:xen/common/event_channel.c:637-649 made live).
+  void report(Tenant& d, uint64_t wait, int kind) override {
     CDom& s = sd(d);
+    if (kind == GPBS_REPORT_HOLD) {
+      s.lock_hold_ns += wait;
+      s.lock_hold_count++;
+      s.report_total++;
+      return;
+    }
+    if (kind == GPBS_REPORT_REQUESTS) {
+      d.pending_requests += wait;
+      s.report_total++;
+      return;
+    }
     if (mode_ == Mode::ATC) {
       atc_report(s.atc, E.atc_params, wait);
     } else {  // do_vcrd_op (:249-259)
@@ -1062,6 +1114,10 @@ class CreditScheduler : public Scheduler {
                mode_ == Mode::PBS ? d.adapt.tick_period_us : tick_period_us_,
                d.adapt.phase == kPhaseLow ? "LOW(cache-sensitive)" : "HIGH", d.cache_miss_rate, d.cpi,
                d.adapt.window_left, d.report_total);
+      if (d.spinlock_count || d.lock_hold_count || t->pending_requests)
+        o += fmt("    waits: n=%" PRIu64 " total=%" PRIu64 "ns  holds: n=%" PRIu64 " total=%" PRIu64
+                 "ns  pending_requests=%" PRIu64 "\n",
+                 d.spinlock_count, d.spinlock_latency, d.lock_hold_count, d.lock_hold_ns, t->pending_requests);
       for (int sid : t->slots) {
         Slot& v = *E.slots[sid];
         o += fmt("    vcpu%d: \n", v.index);

@@ -41,11 +41,12 @@ struct alignas(64) PartTable {
 
 // Work queue of one tenant kernel invocation (tile / chunk queue).
 struct alignas(64) WorkQueue {
-  u32 next;       // next unit to grab (atomic)
+  u32 next;       // next unit to grab (atomic); XCD-range queues: units claimed
   u32 done;       // completed units
   u32 exited;     // workgroups that finished (any path)
   u32 stopped;    // workgroups that left because their XCD was revoked
-  u32 pad[12];
+  u32 xnext[kXcds];  // XCD-range queues: next offset within range x
+  u32 pad[4];
 };
 
 // Exit protocol of every tenant kernel: the last workgroup to leave publishes

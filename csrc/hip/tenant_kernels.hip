@@ -48,6 +48,48 @@ __device__ __forceinline__ int grab_unit(WorkQueue* q, const PartTable* table, u
   return u;
 }
 
+// XCD-range variant: units are split into 8 contiguous ranges and a
+// workgroup first drains the range of the XCD it runs on, then steals from
+// the others in ring order.  Neighbouring tiles (which share operand panels)
+// thus meet in one XCD's private L2 -- the XCD-aware blockIdx remap of a plain
+// grid, done on a work queue so gating, parking and relaunch still hold.
+__device__ __forceinline__ int grab_unit_x(WorkQueue* q, const PartTable* table, u32 mode, u32 me, u32 xcc,
+                                           int* s_slot, u32 total) {
+  if (threadIdx.x == 0) {
+    int u = -1;
+    const u32 per = (total + kXcds - 1) / kXcds;
+    for (u32 spins = 0;; ++spins) {
+      if (owns(table, mode, me, xcc)) {
+        for (u32 k = 0; k < (u32)kXcds; ++k) {
+          const u32 r = (xcc + k) & (kXcds - 1);
+          const u32 lo = r * per, hi = min(lo + per, total);
+          if (lo >= hi) continue;
+          if (__hip_atomic_load(&q->xnext[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= hi - lo) continue;
+          const u32 t = atomicAdd(&q->xnext[r], 1u);
+          if (t < hi - lo) {
+            u = (int)(lo + t);
+            atomicAdd(&q->next, 1u);
+            break;
+          }
+        }
+        break;
+      }
+      if ((mode & 3) != GATE_PARK || spins >= kParkSpins ||
+          __hip_atomic_load(&q->next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= total) {
+        atomicAdd(&q->stopped, 1u);
+        break;
+      }
+#pragma unroll
+      for (int k = 0; k < 6; ++k) __builtin_amdgcn_s_sleep(127);
+    }
+    *s_slot = u;
+  }
+  __syncthreads();
+  int u = *s_slot;
+  __syncthreads();
+  return u;
+}
+
 // Per-unit counter accumulation by thread 0 (tile-granular vPMU: the scheduler
 // sees a smooth rate instead of bursts at kernel exit).
 __device__ __forceinline__ void count_unit(u64* cnt, u32 me, u32 xcc, u64 inst, u64* t_last, u64 refs, u64 miss,
@@ -206,6 +248,12 @@ __global__ __launch_bounds__(GNT, 2) void k_gemm_bf16_tn(const u16* __restrict__
 // at slot c ^ ((r >> 1) & 7): a 16-lane ds_read_b128 group (16 consecutive
 // rows, one logical chunk) covers all 16 slots of a 256-B bank row.
 constexpr int G2_BM = 256, G2_BK = 64, G2_NT = 512;
+constexpr u32 kGemmXRange = 1u << 16;  // mode bit: XCD-range tile queues (grab_unit_x)
+// host: bit 0 = XCD-range tile queues.  Off by default: an interleaved A/B in
+// one process measured the plain queue faster at 4096^3 (1006 vs 937 TF/s,
+// profiles/kbench_r1.jsonl) -- dispatch already deals consecutive tiles
+// round-robin over the XCDs, which gives each XCD two B panels shared 16 ways.
+static int g_gemm_opts = 0;
 constexpr int kG2Half = 128 * 128;           // bytes per half-tile
 constexpr int kG2Buf = 4 * kG2Half;          // A0 A1 B0 B1
 constexpr int kG2Lds = 2 * kG2Buf;           // 128 KiB
@@ -239,9 +287,10 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restr
   const int l16 = lane & 15, lq = lane >> 4;
 
   for (;;) {
-    const int tile = grab_unit(q, table, mode, me, xcc, s_slot, (u32)ntiles);
+    const int tile = (mode & kGemmXRange) ? grab_unit_x(q, table, mode, me, xcc, s_slot, (u32)ntiles)
+                                          : grab_unit(q, table, mode, me, xcc, s_slot, (u32)ntiles);
     if (tile < 0) break;
-    const int tm = tile / tiles_n, tn = tile % tiles_n;
+    const int tm = tile / tiles_n, tn = tile % tiles_n;  // row-major: an XCD range shares A panels
     const u16* Ab = A + (size_t)tm * G2_BM * K;
     const u16* Bb = Bt + (size_t)tn * G2_BM * K;
 
@@ -562,6 +611,12 @@ using namespace gpbs_hip;
 
 extern "C" {
 
+int gpbs_hip_set_gemm_opts(int opts) {
+  const int old = g_gemm_opts;
+  if (opts >= 0) g_gemm_opts = opts;
+  return old;
+}
+
 int gpbs_hip_gemm_units(int M, int N) {
   if (M % G2_BM == 0 && N % G2_BM == 0) return (M / G2_BM) * (N / G2_BM);
   return (M / GBM) * (N / GBN);
@@ -577,8 +632,9 @@ int gpbs_hip_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int
     const u32 inst = (u32)((G2_BM / 16) * (G2_BM / 16) * (K / 32) + (K / G2_BK) * 64 + 128);
     const u32 refs = (u32)(((u64)2 * G2_BM * K * 2) / 128);
     const u32 miss = (u32)((((u64)M + N) * K * 2 / 128) / ntiles + (u64)G2_BM * G2_BM * 2 / 128);
+    const u32 m2 = mode | ((g_gemm_opts & 1) ? kGemmXRange : 0u);
     hipLaunchKernelGGL(k_gemm256_bf16_tn, dim3(grid), dim3(G2_NT), 0, s, (const u16*)A, (const u16*)Bt, (u16*)C, M, N,
-                       K, (WorkQueue*)q, (const PartTable*)table, mode, me, (u64*)cnt, inst, refs, miss, (u32*)status);
+                       K, (WorkQueue*)q, (const PartTable*)table, m2, me, (u64*)cnt, inst, refs, miss, (u32*)status);
     return hipGetLastError() == hipSuccess ? 0 : -5;
   }
   const int ntiles = (M / GBM) * (N / GBN);

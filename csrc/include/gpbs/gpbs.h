@@ -210,6 +210,11 @@ void gpbs_ctl_publish(void* ctl, int page, uint32_t gate, uint64_t mask, uint32_
                       int32_t tenant, uint32_t epoch);
 int gpbs_ctl_read(void* ctl, int page, uint32_t* gate, uint64_t* mask, uint32_t* quantum_us, int32_t* prio,
                   int32_t* tenant, uint32_t* epoch);
+/* wait-report kinds carried by gpbs_report_wait / gpbs_ctl_report */
+#define GPBS_REPORT_WAIT 1     /* spin / wait latency (vcrd_op) */
+#define GPBS_REPORT_HOLD 2     /* lock hold time (lockstat holdtime) */
+#define GPBS_REPORT_REQUESTS 3 /* request arrivals; wait_ns = count */
+int gpbs_ctl_read_mask(void* ctl, int page, uint64_t* mask2, uint32_t* epoch);
 int gpbs_ctl_report(void* ctl, int page, uint64_t wait_ns, uint32_t kind, uint32_t gpu);
 int gpbs_ctl_drain(void* ctl, int page, uint64_t* waits, uint32_t* kinds, int max);
 void gpbs_ctl_heartbeat(void* ctl, int page, uint64_t now_ns, uint32_t progress);

@@ -412,6 +412,29 @@ int gpbs_ctl_doorbell_wait(void* h, int t, int64_t timeout_ns) {
   return pg->doorbell.load(std::memory_order_acquire) != v ? 1 : 0;
 }
 
+// Full 128-partition assignment mask (8 GPUs x 8 XCDs x 2 halves) under the
+// seqlock; returns the gate word.
+int gpbs_ctl_read_mask(void* h, int t, uint64_t* mask2, uint32_t* epoch) {
+  Page* pg = page(h, t);
+  if (!pg) return -22;
+  for (;;) {
+    const uint32_t s0 = pg->seq.load(std::memory_order_acquire);
+    if (s0 & 1) continue;
+    const uint32_t g = pg->gate;
+    const uint64_t m0 = pg->mask[0], m1 = pg->mask[1];
+    const uint32_t e = pg->epoch;
+    std::atomic_thread_fence(std::memory_order_acquire);
+    if (pg->seq.load(std::memory_order_relaxed) == s0) {
+      if (mask2) {
+        mask2[0] = m0;
+        mask2[1] = m1;
+      }
+      if (epoch) *epoch = e;
+      return (int)g;
+    }
+  }
+}
+
 // Launch gate: wait until the scheduler lets the tenant launch. 1 open, 0 timeout.
 int gpbs_ctl_wait_gate(void* h, int t, int64_t timeout_ns) {
   Page* pg = page(h, t);

@@ -207,6 +207,7 @@ def _bind_ipc(lib):
     P(lib, "gpbs_ctl_read", C.c_int, C.c_void_p, C.c_int, C.POINTER(u32), C.POINTER(u64), C.POINTER(u32),
       C.POINTER(i32), C.POINTER(i32), C.POINTER(u32))
     P(lib, "gpbs_ctl_report", C.c_int, C.c_void_p, C.c_int, u64, u32, u32)
+    P(lib, "gpbs_ctl_read_mask", C.c_int, C.c_void_p, C.c_int, C.POINTER(u64), C.POINTER(u32))
     P(lib, "gpbs_ctl_drain", C.c_int, C.c_void_p, C.c_int, C.POINTER(u64), C.POINTER(u32), C.c_int)
     P(lib, "gpbs_ctl_heartbeat", None, C.c_void_p, C.c_int, u64, u32)
     P(lib, "gpbs_ctl_status", C.c_int, C.c_void_p, C.c_int, C.POINTER(u64), C.POINTER(u64), C.POINTER(u32),

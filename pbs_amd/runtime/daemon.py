@@ -61,6 +61,8 @@ class Daemon:
             raise RuntimeError("cannot create control-page region")
         self.ctl = C.c_void_p(self.ctl)
         self.pages: Dict[int, int] = {}  # tenant -> page
+        self.pids: Dict[int, int] = {}   # tenant -> registered process
+        self.reaped: List[str] = []
         self.gpu_ctx = None
         if attach_gpu:
             from .gpu import GpuContext
@@ -152,7 +154,10 @@ class Daemon:
             if t == self.dom0:
                 raise RpcError("cannot destroy Domain-0", -22)
             self.engine.tenant_destroy(t)
-            self.pages.pop(t, None)
+            page = self.pages.pop(t, None)
+            if page is not None:
+                self.lib.gpbs_ctl_assign(self.ctl, page, -1)
+            self.pids.pop(t, None)
             return 0
 
     def domain_list(self):
@@ -338,6 +343,8 @@ class Daemon:
                 self.pages[t] = page
                 self.lib.gpbs_ctl_assign(self.ctl, page, t)
             self.engine.heartbeat(t)
+            if pid:
+                self.pids[t] = int(pid)
             return {"tenant": t, "page": page, "ctl": self.ctl_name, "nctx": self.nctx,
                     "partitions": {f"{g}:{x}:{c}": p for (g, x, c), p in self.part_of.items()}}
 
@@ -376,12 +383,55 @@ class Daemon:
                  "unregister", "snapshot", "restore", "advance_us"]
         return {n: getattr(self, n) for n in names}
 
+    # ------------------------------------------------------------ reaper
+    @staticmethod
+    def _alive(pid: int) -> bool:
+        try:
+            os.kill(pid, 0)
+        except ProcessLookupError:
+            return False
+        except PermissionError:
+            return True
+        try:  # a zombie child counts as dead
+            with open(f"/proc/{pid}/stat") as f:
+                return f.read().rsplit(")", 1)[1].split()[0] != "Z"
+        except OSError:
+            return False
+
+    def reap(self) -> List[str]:
+        """Failure detection (S13): destroy tenants whose registered process
+        is gone, freeing their partitions and control page.  Tenants that
+        merely stop heartbeating are paused by the engine (heartbeat_check)
+        and resume nothing until they re-register."""
+        dead = []
+        with self.lock:
+            for t, pid in list(self.pids.items()):
+                if not self._alive(pid):
+                    name = self.engine.tenant_info(t).name
+                    try:
+                        self.destroy(t)
+                    except Exception:
+                        self.pids.pop(t, None)
+                    dead.append(name)
+                    self.reaped.append(name)
+        return dead
+
+    def _reaper(self, period: float):
+        while self.running:
+            time.sleep(period)
+            try:
+                self.reap()
+            except Exception as e:  # pragma: no cover
+                print(f"[gpbsd] reaper: {e}", file=sys.stderr)
+
     # ---------------------------------------------------------------- run
-    def start(self):
+    def start(self, reaper_s: float = 0.2):
         self.server.start()
         if not self.sim:
             self.engine.start()
         self.running = True
+        if reaper_s > 0:
+            threading.Thread(target=self._reaper, args=(reaper_s,), daemon=True, name="gpbsd-reaper").start()
         return self
 
     def stop(self):

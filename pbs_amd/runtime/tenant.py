@@ -1,0 +1,242 @@
+"""Tenant shim: makes a torch process a gpbs tenant.
+
+This is the guest side of the reference -- the Perfctr guest driver that
+publishes counters through shared pages (S2, C10), the `vcrd_op` spin report
+hypercall (P2, C7), the prepared lock-hold/I-O request hooks (P8, P7) and the
+VIRQ upcall that wakes a descheduled vCPU (C9) -- rebuilt on the gpbsd control
+plane:
+
+* ``register`` over the daemon's Unix-socket RPC creates (or re-attaches to)
+  the tenant and binds a 4 KiB control page in the daemon's POSIX shm region;
+* a heartbeat thread keeps the daemon's failure detector quiet (S13);
+* ``gate()`` blocks on the page's futex doorbell until the scheduler assigns
+  the tenant at least one partition (the launch gate: no kernel preemption,
+  the tenant stops launching at its next boundary);
+* ``stream()`` returns a HIP stream whose CU mask covers exactly the
+  (XCD, CU-half) partitions the tenant currently holds -- the actuation for
+  third-party kernels (torch / hipBLASLt / RCCL) that cannot gate themselves
+  through the partition table like the gpbs tenant kernels do;
+* ``report_wait`` / ``report_hold`` / ``report_requests`` feed the spin-latency
+  channel, ``account`` publishes modeled counters (vPMU mirror), ``busy`` /
+  ``idle`` set the has-work flag that wakes or blocks the tenant's slots.
+
+    with TenantClient("llm-infer", slots=8) as t:
+        for batch in loader:
+            with t.slice() as s:         # waits for the gate, runs on s
+                out = model(batch)
+            t.account(flops=..., bytes=...)
+"""
+from __future__ import annotations
+
+import contextlib
+import ctypes as C
+import os
+import threading
+import time
+from typing import Dict, List, Optional, Tuple
+
+from .. import _native as N
+from ..ctl.rpc import DEFAULT_SOCKET, Client
+
+XCDS = 8
+REPORT_WAIT, REPORT_HOLD, REPORT_REQUESTS = 1, 2, 3
+# Modeled-counter units shared with the gpbs tenant kernels: one MFMA
+# 16x16x32 bf16 = 16384 FLOP per instruction; 128-byte L2 lines.
+FLOP_PER_INST = 16384
+LINE = 128
+
+
+def half_cu_words(owned: List[Tuple[int, int]]) -> List[int]:
+    """CU-mask words (hipExtStreamCreateWithCUMask) covering the given
+    (xcd, half) partitions: bit b = logical CU b/8 of XCD b%8, logical CU i on
+    shader engine i%4, half = SE >> 1 (see csrc/hip/runtime.cpp)."""
+    want = set(owned)
+    words = [0] * 8
+    for b in range(256):
+        if (b % 8, ((b // 8) % 4) >> 1) in want:
+            words[b // 32] |= 1 << (b % 32)
+    return words
+
+
+class TenantClient:
+    def __init__(self, name: str, socket_path: str = DEFAULT_SOCKET, slots: int = 8, weight: int = -1,
+                 cap: int = -1, pool=None, gpu: int = 0, heartbeat_s: float = 0.05, spatial: bool = True):
+        self.name = name
+        self.gpu = gpu
+        self.spatial = spatial
+        self.rpc = Client(socket_path)
+        r = self.rpc.call("register", name=name, slots=slots, weight=weight, cap=cap, pool=pool, pid=os.getpid())
+        self.tenant: int = r["tenant"]
+        self.page: int = r["page"]
+        self.nctx: int = r.get("nctx", 2)
+        # partition id -> (gpu, xcd, ctx)
+        self.part: Dict[int, Tuple[int, int, int]] = {}
+        for k, pid in r["partitions"].items():
+            g, x, c = (int(v) for v in k.split(":"))
+            self.part[int(pid)] = (g, x, c)
+        self.lib = N.load_core()
+        h = self.lib.gpbs_ctl_open(r["ctl"].encode())
+        if not h:
+            raise RuntimeError(f"cannot open control region {r['ctl']!r}")
+        self.ctl = C.c_void_p(h)
+        self._streams: Dict[Tuple, object] = {}
+        self._progress = 0
+        self._stop = threading.Event()
+        self._hb = threading.Thread(target=self._beat, args=(heartbeat_s,), daemon=True, name=f"gpbs-hb-{name}")
+        self._hb.start()
+        self.counters = [0, 0, 0, 0]
+
+    # ------------------------------------------------------------ liveness
+    def _beat(self, period: float):
+        while not self._stop.wait(period):
+            self.lib.gpbs_ctl_heartbeat(self.ctl, self.page, time.monotonic_ns(), self._progress & 0xFFFFFFFF)
+
+    def heartbeat(self):
+        self.lib.gpbs_ctl_heartbeat(self.ctl, self.page, time.monotonic_ns(), self._progress & 0xFFFFFFFF)
+
+    # ---------------------------------------------------------- assignment
+    def assignment(self) -> Tuple[int, List[int], int]:
+        """(gate, owned partition ids, epoch) -- one seqlock read."""
+        m = (C.c_uint64 * 2)()
+        ep = C.c_uint32(0)
+        g = self.lib.gpbs_ctl_read_mask(self.ctl, self.page, m, C.byref(ep))
+        ids = [i for i in range(128) if (m[i // 64] >> (i % 64)) & 1]
+        return g, ids, ep.value
+
+    def owned(self) -> List[Tuple[int, int]]:
+        """(xcd, ctx) pairs of this tenant's GPU it currently holds."""
+        _, ids, _ = self.assignment()
+        return sorted({(x, c) for i in ids if i in self.part for (g, x, c) in [self.part[i]] if g == self.gpu})
+
+    def gate(self, timeout_s: float = 10.0) -> bool:
+        """Block until the scheduler lets this tenant launch (futex doorbell)."""
+        rc = self.lib.gpbs_ctl_wait_gate(self.ctl, self.page, int(timeout_s * 1e9))
+        if rc < 0:
+            raise RuntimeError(f"wait_gate failed ({rc})")
+        return rc == 1
+
+    # ------------------------------------------------------------- streams
+    def stream(self, owned: Optional[List[Tuple[int, int]]] = None):
+        """torch stream masked to the CUs of the partitions this tenant holds.
+        Co-resident-context partitions (``spatial=False``) map to whole XCDs."""
+        import torch
+
+        from ..ops import kernels as K
+        parts = self.owned() if owned is None else owned
+        if not parts:
+            return torch.cuda.current_stream()
+        if self.spatial:
+            key = tuple(parts)
+        else:
+            key = tuple(sorted({(x, h) for (x, _) in parts for h in (0, 1)}))
+        s = self._streams.get(key)
+        if s is None:
+            h = K.cumask_stream(half_cu_words(list(key)), device=self.gpu)
+            s = torch.cuda.ExternalStream(h)
+            self._streams[key] = s
+        return s
+
+    @contextlib.contextmanager
+    def slice(self, timeout_s: float = 10.0):
+        """Wait for the gate, mark the tenant busy, run the body on the
+        tenant's CU-masked stream."""
+        import torch
+        self.busy()
+        t0 = time.monotonic_ns()
+        if not self.gate(timeout_s):
+            raise TimeoutError(f"tenant {self.name}: gate closed for {timeout_s}s")
+        waited = time.monotonic_ns() - t0
+        s = self.stream()
+        with torch.cuda.stream(s):
+            yield s
+        self._progress += 1
+        if waited > 0:
+            self.report_wait(waited)
+
+    # ------------------------------------------------------------- signals
+    def busy(self):
+        self.lib.gpbs_ctl_set_work(self.ctl, self.page, 1)
+
+    def idle(self):
+        self.lib.gpbs_ctl_set_work(self.ctl, self.page, 0)
+
+    def report_wait(self, ns: int, gpu: Optional[int] = None):
+        return self.lib.gpbs_ctl_report(self.ctl, self.page, int(ns), REPORT_WAIT, self.gpu if gpu is None else gpu)
+
+    def report_hold(self, ns: int):
+        return self.lib.gpbs_ctl_report(self.ctl, self.page, int(ns), REPORT_HOLD, self.gpu)
+
+    def report_requests(self, n: int = 1):
+        return self.lib.gpbs_ctl_report(self.ctl, self.page, int(n), REPORT_REQUESTS, self.gpu)
+
+    def account(self, flops: float = 0.0, bytes_moved: float = 0.0, busy_ns: int = 0, l2_bytes: float = 0.0):
+        """Publish modeled counters (cumulative): instructions ~ MFMA issues,
+        cycles ~ busy time, L2 references ~ lines touched, misses ~ HBM lines."""
+        c = self.counters
+        c[0] += int(flops / FLOP_PER_INST) + 1
+        c[1] += int(busy_ns * 2.4)  # ~2.4 GHz shader clock
+        c[2] += int((l2_bytes or bytes_moved) / LINE)
+        c[3] += int(bytes_moved / LINE)
+        arr = (C.c_uint64 * 4)(*c)
+        self.lib.gpbs_ctl_set_counters(self.ctl, self.page, arr)
+
+    # ------------------------------------------------------------ teardown
+    def close(self, destroy: bool = True):
+        if self._stop.is_set():
+            return
+        self._stop.set()
+        self._hb.join(timeout=1.0)
+        try:
+            self.idle()
+            self.rpc.call("unregister", name=self.name, destroy=destroy)
+        except Exception:
+            pass
+        self.lib.gpbs_ctl_close(self.ctl, 0)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def run_synthetic(name: str, socket_path: str, seconds: float, result_q=None, slots: int = 4,
+                  crash: bool = False, flops: float = 1e9, bytes_moved: float = 1e6):
+    """A synthetic tenant loop (no GPU needed): gate, report, account, repeat.
+    ``crash`` exits without unregistering (failure-detection test)."""
+    t = TenantClient(name, socket_path, slots=slots)
+    t.busy()
+    opens = loops = 0
+    t_end = time.monotonic() + seconds
+    while time.monotonic() < t_end:
+        t0 = time.monotonic_ns()
+        if t.gate(timeout_s=0.5):
+            opens += 1
+        t.report_wait(time.monotonic_ns() - t0 + 1)
+        t.report_hold(500)
+        t.report_requests(1)
+        t.account(flops=flops, bytes_moved=bytes_moved, busy_ns=100_000)
+        loops += 1
+        time.sleep(0.001)
+    if crash:
+        os._exit(0)
+    info = {"name": name, "tenant": t.tenant, "opens": opens, "loops": loops, "owned_seen": t.owned()}
+    t.close(destroy=False)
+    if result_q is not None:
+        result_q.put(info)
+    return info
+
+
+def main(argv=None):
+    import argparse
+    ap = argparse.ArgumentParser(description="gpbs synthetic tenant")
+    ap.add_argument("--name", required=True)
+    ap.add_argument("--socket", default=DEFAULT_SOCKET)
+    ap.add_argument("--seconds", type=float, default=5.0)
+    ap.add_argument("--slots", type=int, default=4)
+    a = ap.parse_args(argv)
+    print(run_synthetic(a.name, a.socket, a.seconds, slots=a.slots))
+
+
+if __name__ == "__main__":
+    main()

@@ -410,3 +410,22 @@ def test_contention_classes_are_soft_affinity_and_work_conserving():
         if not si["is_running"]:
             assert ctx[si["processor"]] == 1, (k, si["processor"])
     assert e.check() == ""
+
+
+def test_atc_places_slots_least_loaded_and_apart():
+    """sched_credit_atc.c:634-651 + :545-570: new slots go to the least-loaded
+    partition not used by a sibling; siblings are pinned away from each other."""
+    e = mk(nparts=4, sched="atc")
+    busy = e.tenant_create("busy", nslots=4)
+    for k in range(4):
+        e.pin(busy, k, [0] if k < 3 else [1])   # queue load on partitions 0 and 1
+    e.wake(busy)
+    t = e.tenant_create("t", nslots=2)
+    procs = [e.slot_info(e.slot_id(t, k))["processor"] for k in range(2)]
+    assert len(set(procs)) == 2 and set(procs) <= {2, 3}, procs
+    for k in range(2):
+        sid = e.slot_id(t, k)
+        aff = __import__("pbs_amd.utils.snapshot", fromlist=["slot_affinity"]).slot_affinity(e, sid)
+        other = procs[1 - k]
+        assert other not in aff and procs[k] in aff, (k, aff)
+    assert e.check() == ""
