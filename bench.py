@@ -53,10 +53,14 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
         groups["ctrl"] = dist.new_group(backend="gloo")
+        groups["gang"] = dist.new_group(backend="gloo")  # cross-GPU gang epochs (own thread)
         groups["coll"] = dist.new_group(backend="nccl")
 
     from pbs_amd import build
-    build.build_all()
+    if rank == 0:  # one builder per node; the others wait (no concurrent relink)
+        build.build_all()
+    if world > 1:
+        dist.barrier(group=groups["ctrl"])
     from pbs_amd.bench.corun import Corun, CorunConfig
 
     pols = tuple(p for p in args.policies.split(",") if p)

@@ -476,6 +476,26 @@ int gpbs_report_wait(gpbs_engine_t* e, int t, uint64_t wait_ns, int kind) {
   return GPBS_OK;
 }
 
+// Gang window for a tenant (state 0 none, 1 favoured, 2 excluded) until
+// `until_ns` on the engine clock; every partition of its pool reschedules now.
+int gpbs_gang_set(gpbs_engine_t* e, int t, int state, int64_t until_ns) {
+  LOCK(e);
+  Tenant* d = live(e, t);
+  if (!d || state < 0 || state > 2) return d ? GPBS_EINVAL : GPBS_ENOENT;
+  const int before = d->gang(e->e->now());
+  d->gang_state = state;
+  d->gang_until = until_ns;
+  if (state != before) {
+    Pool* pl = e->e->pool(d->pool);
+    if (pl)
+      for (int p = pl->cpus.first(); p >= 0; p = pl->cpus.next(p + 1)) e->e->raise_softirq(p);
+    e->e->perfc.incr(PC_gang_epoch);
+    e->e->emit(TRC_GANG_EPOCH, 0, t, (uint32_t)state, (uint32_t)(until_ns / 1000));
+  }
+  DONE(e);
+  return GPBS_OK;
+}
+
 int gpbs_report_requests(gpbs_engine_t* e, int t, uint64_t n) {
   LOCK(e);
   Tenant* d = live(e, t);

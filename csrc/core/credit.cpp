@@ -744,6 +744,7 @@ class CreditScheduler : public Scheduler {
         bool hot = (E.now() - v.last_run_time) < (int64_t)E.boot.migration_delay_us * 1000;
         if (hot) E.perfc.incr(PC_vcpu_hot);
         if (soft_pass && !v.soft.empty() && !v.soft.test(cpu)) continue;
+        if (xgang(v, E.now()) == 2) continue;
         if (!v.is_running && !hot && v.affinity.test(cpu)) {
           s.stats.migrate_q++;
           E.perfc.incr(PC_migrate_queued);
@@ -860,6 +861,7 @@ class CreditScheduler : public Scheduler {
     if (lead == cpu) return nullptr;
     const int L = E.slots[E.parts[lead]->curr]->tenant;
     if (L < 0 || head.tenant == L) return nullptr;
+    if (Tenant* lt = E.tenant(L); lt && lt->gang(E.now()) == 2) return nullptr;  // leader not yet rescheduled
     const int16_t hp = sv(head).pri;
     for (int sid : pc(cpu).runq) {
       Slot& v = *E.slots[sid];
@@ -890,6 +892,35 @@ class CreditScheduler : public Scheduler {
     return false;
   }
 
+  // Cross-GPU gang windows (gpbs_gang_set, driven by parallel/gang.py): a
+  // favoured tenant runs on every partition holding one of its runnable
+  // slots (BOOSTed wakers of other tenants still preempt); an excluded one is
+  // passed over and never stolen, so a collective's ranks on different GPUs
+  // only run together.
+  int xgang(const Slot& v, int64_t now) {
+    if (v.is_idle()) return 0;
+    Tenant* t = E.tenant(v.tenant);
+    return t ? t->gang(now) : 0;
+  }
+  Slot* xgang_favoured(int cpu, Slot& head, int64_t now) {
+    if (xgang(head, now) == 1) return nullptr;
+    const int16_t hp = sv(head).pri;
+    for (int sid : pc(cpu).runq) {
+      Slot& v = *E.slots[sid];
+      if (v.is_idle() || xgang(v, now) != 1) continue;
+      const int16_t p = sv(v).pri;
+      if (p < PRI_OVER) return nullptr;
+      if (hp > PRI_UNDER && p < hp) return nullptr;
+      return &v;
+    }
+    return nullptr;
+  }
+  Slot* xgang_first_allowed(int cpu, int64_t now) {
+    for (int sid : pc(cpu).runq)
+      if (xgang(*E.slots[sid], now) != 2) return E.slots[sid].get();
+    return nullptr;
+  }
+
   TaskSlice do_schedule(int cpu, int64_t now) override {
     Slot& scurr = curr(cpu);
     CSlot& cs = sv(scurr);
@@ -908,7 +939,7 @@ class CreditScheduler : public Scheduler {
     bool held = false;
     const int prev_tenant = scurr.tenant;
     if (ratelimit_us_ && E.runnable(scurr) && !scurr.is_idle() && runtime < (int64_t)ratelimit_us_ * 1000 &&
-        !gang_misaligned(cpu, scurr)) {
+        !gang_misaligned(cpu, scurr) && xgang(scurr, now) != 2 && !xgang_favoured(cpu, scurr, now)) {
       snext = &scurr;
       cs.start_time += now;
       E.perfc.incr(PC_delay_ms);
@@ -921,7 +952,19 @@ class CreditScheduler : public Scheduler {
       auto& rq = pc(cpu).runq;
       snext = E.slots[rq.front()].get();
       bool follow = false;
-      if (E.boot.coschedule >= 3) {
+      if (Slot* f = xgang_favoured(cpu, *snext, now)) {
+        rq.remove(f->id);
+        rq.push_front(f->id);
+        snext = f;
+        follow = true;
+      } else if (xgang(*snext, now) == 2) {
+        if (Slot* a = xgang_first_allowed(cpu, now)) {
+          rq.remove(a->id);
+          rq.push_front(a->id);
+          snext = a;
+        }
+      }
+      if (!follow && E.boot.coschedule >= 3) {
         if (Slot* g = gang_pick(cpu, *snext)) {
           rq.remove(g->id);
           rq.push_front(g->id);
@@ -930,7 +973,8 @@ class CreditScheduler : public Scheduler {
         }
       }
       if (!follow && E.boot.coschedule && !snext->is_idle()) {
-        if (Slot* alt = cosched_pick(cpu)) {  // same priority class, less contention
+        Slot* alt = cosched_pick(cpu);
+        if (alt && xgang(*alt, now) != 2) {  // same priority class, less contention
           rq.remove(alt->id);
           rq.push_front(alt->id);
           snext = alt;

@@ -82,6 +82,12 @@ struct Tenant {  // struct domain
   int cls = -1;          // contention class: 0 compute-bound (MFMA ctx), 1 memory-bound (memory ctx)
   int cls_pending = -1;  // hysteresis: a new class must be seen on consecutive ticks
   int cls_count = 0;
+  // Cross-GPU gang window (parallel/gang.py): 1 favoured (run on every
+  // partition that holds a slot), 2 excluded (its peers on other GPUs are not
+  // running it), until gang_until (engine clock).
+  int gang_state = 0;
+  int64_t gang_until = 0;
+  int gang(int64_t now) const { return now < gang_until ? gang_state : 0; }
   std::unique_ptr<SchedTenantData> priv;
 };
 

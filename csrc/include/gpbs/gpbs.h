@@ -192,6 +192,9 @@ int gpbs_sched_name(gpbs_engine_t* e, int pool, char* out, int len);
 int gpbs_report_wait(gpbs_engine_t* e, int tenant, uint64_t wait_ns, int kind);
 int gpbs_report_requests(gpbs_engine_t* e, int tenant, uint64_t n); /* pending_requests (P7) */
 
+/* --- cross-GPU gang windows (pbs_amd/parallel/gang.py) --- */
+int gpbs_gang_set(gpbs_engine_t* e, int tenant, int state, int64_t until_ns); /* 0 none 1 favour 2 exclude */
+
 /* --- counters / actuation backends --- */
 int gpbs_set_counter_ops(gpbs_engine_t* e, const gpbs_counter_ops_t* ops);
 int gpbs_set_actuator_ops(gpbs_engine_t* e, const gpbs_actuator_ops_t* ops);

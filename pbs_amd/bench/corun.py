@@ -71,6 +71,8 @@ class CorunConfig:
     depth: int = 2
     table_mode: str = "host"
     calib_units: int = 8
+    gang_epoch_ms: float = 4.0   # N > 1: cross-GPU gang window length
+    gang_share: float = 0.5      # fraction of epochs that are the all-reduce tenant's
 
 
 POLICY_ENGINES = {
@@ -130,6 +132,8 @@ class Corun:
     def __init__(self, cfg: CorunConfig, rank: int = 0, world: int = 1, device: int = 0, groups=None, log=print):
         self.cfg, self.rank, self.world, self.device = cfg, rank, world, device
         self.groups = groups or {}
+        self.gang = None
+        self.gang_stats: Dict[str, float] = {}
         self.log = log if rank == 0 else (lambda *a, **k: None)
         torch.cuda.set_device(device)
         self.engines: Dict[str, Engine] = {}
@@ -178,7 +182,14 @@ class Corun:
     def _natives(self):
         return [r for r in self.runners.values() if isinstance(r, Runner)]
 
+    def _stop_gang(self):
+        if self.gang is not None:
+            self.gang_stats = self.gang.stats()
+            self.gang.stop()
+            self.gang = None
+
     def set_policy(self, policy: str):
+        self._stop_gang()
         if self.active_engine is not None:
             self.active_engine.stop()
             self.active_engine = None
@@ -196,6 +207,12 @@ class Corun:
                 r.set_engine_wake(True)
             if not isinstance(coll, Runner):
                 coll.gate, coll.engine = True, e
+                # Cross-GPU gang windows for the all-reduce tenant: its RCCL
+                # ranks on all GPUs get their partitions in the same epochs.
+                from ..parallel.gang import GangCoordinator
+                # own gloo group: the main thread's barriers use "ctrl"
+                self.gang = GangCoordinator(e, self.groups["gang"], [self.tid["coll"]],
+                                            epoch_ms=self.cfg.gang_epoch_ms, share=self.cfg.gang_share).start()
             return
         self.ctx.set_table_mode("host")
         self.ctx.set_spatial(False)
@@ -363,6 +380,8 @@ class Corun:
                                 for n in self.tid}
             eng["runner"] = {n: {k: getattr(r.stats(), k) for k in ("launches", "relaunches", "waits_owner")}
                              for n, r in self.runners.items() if isinstance(r, Runner)}
+            if self.gang is not None:
+                eng["gang"] = self.gang.stats()
             res["engine"] = eng
             diag = os.environ.get("GPBS_DIAG_DIR")
             if diag and self.rank == 0:
@@ -375,6 +394,7 @@ class Corun:
         return res
 
     def close(self):
+        self._stop_gang()
         if self.active_engine is not None:
             self.active_engine.stop()
         for r in self._natives():

@@ -47,6 +47,38 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def _digest(deps, extra=""):
+    import hashlib
+    h = hashlib.sha1(extra.encode())
+    for d in sorted(deps):
+        h.update(d.encode())
+        with open(d, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def _lib_stale(target, deps, extra=""):
+    """A library is stale when its stamp (content hash of every dependency
+    and the flags) differs -- robust to copies that do not keep mtimes (the
+    GPU-box snapshot), unlike an mtime comparison."""
+    stamp = target + ".stamp"
+    if not (os.path.exists(target) and os.path.exists(stamp)):
+        return True
+    with open(stamp) as f:
+        return f.read().strip() != _digest(deps, extra)
+
+
+def _link_atomic(cmd_prefix, target, cmd_suffix, verbose, deps, extra=""):
+    """Link into a temp file and rename over the target: a process that has
+    the old library mapped keeps it, a concurrent loader never sees a torn
+    file."""
+    tmp = f"{target}.tmp.{os.getpid()}"
+    _run(cmd_prefix + ["-o", tmp] + cmd_suffix, verbose)
+    os.replace(tmp, target)
+    with open(target + ".stamp", "w") as f:
+        f.write(_digest(deps, extra))
+
+
 def _run(cmd, verbose):
     if verbose:
         print("[build]", " ".join(cmd), flush=True)
@@ -84,7 +116,8 @@ def build_core(verbose=False, sanitize: str | None = None):
     srcs = _srcs(CORE_DIRS, [".cpp"])
     name = "libgpbs.so" if not sanitize else f"libgpbs_{sanitize}.so"
     target = os.path.join(LIBDIR, name)
-    if not _stale(target, srcs + _headers() + [__file__]):
+    deps = srcs + _headers() + [__file__]
+    if not _lib_stale(target, deps, str(sanitize)):
         return target
     objdir = os.path.join(ROOT, "build", "core" + (("_" + sanitize) if sanitize else ""))
     os.makedirs(objdir, exist_ok=True)
@@ -101,10 +134,8 @@ def build_core(verbose=False, sanitize: str | None = None):
         if _stale(obj, [s] + _headers()):
             jobs.append((["g++"] + flags + ["-c", s, "-o", obj], obj))
     _compile_parallel(jobs, verbose)
-    link = ["g++", "-shared", "-o", target] + objs + ["-pthread", "-lrt"]
-    if sanitize:
-        link += [f"-fsanitize={sanitize}"]
-    _run(link, verbose)
+    suffix = objs + ["-pthread", "-lrt"] + ([f"-fsanitize={sanitize}"] if sanitize else [])
+    _link_atomic(["g++", "-shared"], target, suffix, verbose, deps, str(sanitize))
     return target
 
 
@@ -123,7 +154,8 @@ def build_hip(verbose=False):
         return None
     target = os.path.join(LIBDIR, "libgpbs_hip.so")
     hdrs = _headers() + sorted(glob.glob(os.path.join(CSRC, HIP_DIR, "*.hpp")))
-    if not _stale(target, srcs + hdrs + [core, __file__]):
+    deps = srcs + hdrs + [__file__] + _srcs(CORE_DIRS, [".cpp"]) + _headers()
+    if not _lib_stale(target, deps, ARCH):
         return target
     objdir = os.path.join(ROOT, "build", "hip")
     os.makedirs(objdir, exist_ok=True)
@@ -137,9 +169,8 @@ def build_hip(verbose=False):
             lang = ["-x", "hip"] if s.endswith(".hip") or s.endswith(".cpp") else []
             jobs.append(([hipcc()] + flags + lang + ["-c", s, "-o", obj], obj))
     _compile_parallel(jobs, verbose)
-    link = [hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", target] + objs + [
-        "-L" + LIBDIR, "-lgpbs", "-Wl,-rpath,$ORIGIN", "-pthread"]
-    _run(link, verbose)
+    _link_atomic([hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}"], target,
+                 objs + ["-L" + LIBDIR, "-lgpbs", "-Wl,-rpath,$ORIGIN", "-pthread"], verbose, deps, ARCH)
     return target
 
 

@@ -237,6 +237,13 @@ class Engine:
     def set_adapt_state(self, t: int, s: N.AdaptState):
         return self._chk(self.lib.gpbs_tenant_adapt_state(self.h, t, C.byref(s), 1), "set_adapt_state")
 
+    GANG_NONE, GANG_FAVOUR, GANG_EXCLUDE = 0, 1, 2
+
+    def gang_set(self, t: int, state: int, until_ns: int):
+        """Cross-GPU gang window for tenant t (0 none, 1 favoured, 2 excluded)
+        until `until_ns` on this engine's clock."""
+        return self._chk(self.lib.gpbs_gang_set(self.h, t, int(state), int(until_ns)), "gang_set")
+
     def heartbeat(self, t: int):
         return self._chk(self.lib.gpbs_tenant_heartbeat(self.h, t), "heartbeat")
 

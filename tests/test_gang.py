@@ -1,0 +1,54 @@
+"""Cross-GPU gang windows over gloo, world_size 2 (CPU): both ranks' engines
+agree on every epoch's decision, and the gang tenant occupies its partitions
+in favoured epochs and none of them in excluded ones."""
+import multiprocessing as mp
+import socket
+import statistics
+
+from pbs_amd.parallel._gang_selftest import worker
+from pbs_amd.parallel.gang import EXCLUDE, FAVOUR, GangCoordinator
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_decision_is_a_pure_function_of_epoch_and_demand():
+    g = GangCoordinator(engine=None, group=None, tenants=[7, 9], share=0.5)
+    seq = [g.decide(k, [1, 1]) for k in range(16)]
+    assert sum(1 for d in seq if FAVOUR in d.values()) == 8          # share 0.5 of the epochs
+    assert {t for d in seq for t, s in d.items() if s == FAVOUR} == {7, 9}  # both get windows
+    assert g.decide(3, [0, 0]) == {7: 0, 9: 0}                       # no demand anywhere: no gang
+    d = g.decide(0, [0, 1])
+    assert d[7] == 0 and d[9] in (FAVOUR, EXCLUDE)
+
+
+def test_two_ranks_gang_schedule_the_collective_tenant():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = {}
+    for _ in ps:
+        r = q.get(timeout=120)
+        out[r["rank"]] = r
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    h0, h1 = dict(out[0]["history"]), dict(out[1]["history"])
+    common = sorted(set(h0) & set(h1))
+    assert len(common) >= 20
+    assert all(h0[k] == h1[k] for k in common)  # identical decisions on both ranks
+    for r in (0, 1):
+        fav = [f for ep, st, f in out[r]["samples"] if st == FAVOUR]
+        exc = [f for ep, st, f in out[r]["samples"] if st == EXCLUDE]
+        assert fav and exc
+        assert statistics.mean(fav) > 0.7, (r, statistics.mean(fav))
+        assert statistics.mean(exc) < 0.2, (r, statistics.mean(exc))
+        assert out[r]["stats"]["epochs"] >= 20
