@@ -37,6 +37,7 @@ extern "C" {
 #define GPBS_ERANGE -34
 #define GPBS_ENOSPC -28
 #define GPBS_EEXIST -17
+#define GPBS_EIO -5
 
 typedef struct gpbs_adapt_params {
   uint32_t threshold, band_lo, band_hi, min_us, max_us, inc_us, dec_us, switch_boundary;
@@ -191,6 +192,25 @@ int gpbs_sched_name(gpbs_engine_t* e, int pool, char* out, int len);
 /* --- paravirtual report channel (vcrd_op analog, P2) --- */
 int gpbs_report_wait(gpbs_engine_t* e, int tenant, uint64_t wait_ns, int kind);
 int gpbs_report_requests(gpbs_engine_t* e, int tenant, uint64_t n); /* pending_requests (P7) */
+
+/* --- host-CPU backend (config #1): perf_event counters + SIGSTOP/affinity gate --- */
+#define GPBS_PERF_HW 1 /* instructions, cycles, LLC refs, LLC misses */
+#define GPBS_PERF_SW 2 /* task-clock x2, minor/major faults (no hardware PMU) */
+void* gpbs_perf_open(int pid, int cpu);
+int gpbs_perf_read(void* h, uint64_t* out4);
+int gpbs_perf_mode(void* h);
+void gpbs_perf_close(void* h);
+int gpbs_perf_available(void);
+void* gpbs_gate_create(const char* mode); /* "signal" (default) */
+int gpbs_gate_mode(void* g);
+int gpbs_gate_add_pid(void* g, int tenant, int pid);
+int gpbs_gate_set(void* g, int tenant, int cpu, int on);
+int gpbs_gate_stats(void* g, uint64_t* signals, uint64_t* pins);
+void gpbs_gate_destroy(void* g);
+void* gpbs_cpu_backend_create(gpbs_engine_t* e, void* gate);
+int gpbs_cpu_backend_map(void* backend, int partition, int host_cpu);
+int gpbs_cpu_backend_add(void* backend, int tenant, int pid);
+void gpbs_cpu_backend_destroy(void* backend);
 
 /* --- cross-GPU gang windows (pbs_amd/parallel/gang.py) --- */
 int gpbs_gang_set(gpbs_engine_t* e, int tenant, int state, int64_t until_ns); /* 0 none 1 favour 2 exclude */

@@ -227,14 +227,19 @@ def _bind_counters(lib):
     P = _proto
     P(lib, "gpbs_perf_open", C.c_void_p, C.c_int, C.c_int)
     P(lib, "gpbs_perf_read", C.c_int, C.c_void_p, C.POINTER(u64))
+    P(lib, "gpbs_perf_mode", C.c_int, C.c_void_p)
     P(lib, "gpbs_perf_close", None, C.c_void_p)
     P(lib, "gpbs_perf_available", C.c_int)
     P(lib, "gpbs_gate_create", C.c_void_p, C.c_char_p)
     P(lib, "gpbs_gate_add_pid", C.c_int, C.c_void_p, C.c_int, C.c_int)
     P(lib, "gpbs_gate_set", C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int)
+    P(lib, "gpbs_gate_stats", C.c_int, C.c_void_p, C.POINTER(u64), C.POINTER(u64))
     P(lib, "gpbs_gate_destroy", None, C.c_void_p)
     P(lib, "gpbs_gate_mode", C.c_int, C.c_void_p)
-    P(lib, "gpbs_attach_cpu_backend", C.c_int, C.c_void_p, C.c_void_p, C.c_void_p)
+    P(lib, "gpbs_cpu_backend_create", C.c_void_p, C.c_void_p, C.c_void_p)
+    P(lib, "gpbs_cpu_backend_map", C.c_int, C.c_void_p, C.c_int, C.c_int)
+    P(lib, "gpbs_cpu_backend_add", C.c_int, C.c_void_p, C.c_int, C.c_int)
+    P(lib, "gpbs_cpu_backend_destroy", None, C.c_void_p)
 
 
 def load_hip(required=False):
