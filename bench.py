@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--target-ms", type=float, default=30.0)
     ap.add_argument("--table", default="host", choices=["host", "device"])
     ap.add_argument("--out", default="")
+    ap.add_argument("--mix", default="4mix", choices=["4mix", "gemm2"],
+                    help="4mix: BASELINE config #3/#4 (headline); gemm2: config #2 (two 4096^2 GEMM tenants)")
     args = ap.parse_args()
 
     import torch
@@ -67,7 +69,7 @@ def main():
     if "gpbs" not in pols:
         pols = pols + ("gpbs",)
     cfg = CorunConfig(steps=args.steps, warmup=args.warmup, target_ms=args.target_ms, policies=pols,
-                      table_mode=args.table)
+                      table_mode=args.table, mix=args.mix)
     log = (lambda *a: print(*a, file=sys.stderr, flush=True))
     c = Corun(cfg, rank=rank, world=world, device=local, groups=groups, log=log)
     c.calibrate()
@@ -91,9 +93,10 @@ def main():
         "dtype": "bf16",
         "data": "synthetic (random-init bf16 tensors; 4096^3 GEMM, 1 GiB stream, 256 MiB reduce/all-reduce, "
                 "8192^2 GEMV)",
-        "config": {"model": "4-tenant mix (MFMA GEMM + HBM-stream + all-reduce + idle)",
+        "config": {"model": ("4-tenant mix (MFMA GEMM + HBM-stream + all-reduce + idle)" if args.mix == "4mix"
+                             else "2 bf16 4096^2 GEMM tenants"),
                    "global_batch": world * 4, "seq_len": 0, "parallelism": f"dp{world}" if world > 1 else "dp1",
-                   "tenants_per_gpu": 4, "policy": "gpbs-pbs-credit"},
+                   "tenants_per_gpu": 4 if args.mix == "4mix" else 2, "policy": "gpbs-pbs-credit", "mix": args.mix},
         "mean_slowdown_pct": round(g["mean_slowdown_pct"], 2),
         "per_tenant": g["tenants"],
         "policies": {p: {"aggregate_all_gpus": round(r["aggregate_all_gpus"], 4),

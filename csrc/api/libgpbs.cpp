@@ -1,6 +1,8 @@
 // libgpbs: the C ABI (libxl/libxc analog).  Validation mirrors libxl
 // (X:tools/libxl/libxl.c:4007-4116) so every frontend (ctypes, RPC daemon,
 // gpbsctl) sees the same ranges and error codes.
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 
@@ -153,7 +155,20 @@ gpbs_engine_t* gpbs_engine_create(const gpbs_boot_params_t* p) {
     delete h;
     return nullptr;
   }
+  h->e->fault_parse(std::getenv("GPBS_FAULT"));
   return h;
+}
+
+int gpbs_fault_set(gpbs_engine_t* e, const char* spec) {
+  LOCK(e);
+  return e->e->fault_parse(spec);
+}
+
+int gpbs_fault_hits(gpbs_engine_t* e, uint64_t* out, int n) {
+  LOCK(e);
+  const int k = std::min<int>(n, Engine::F_NKIND);
+  for (int i = 0; i < k; ++i) out[i] = e->e->fault_hits[i];
+  return k;
 }
 
 void gpbs_engine_destroy(gpbs_engine_t* e) {
@@ -416,10 +431,17 @@ int gpbs_tenant_adapt_state(gpbs_engine_t* e, int t, gpbs_adapt_state_t* out, in
   return GPBS_OK;
 }
 
+int gpbs_tenant_class(gpbs_engine_t* e, int t) {
+  LOCK(e);
+  Tenant* d = live(e, t);
+  return d ? d->cls : -1;
+}
+
 int gpbs_tenant_heartbeat(gpbs_engine_t* e, int t) {
   LOCK(e);
   Tenant* d = live(e, t);
   if (!d) return GPBS_ENOENT;
+  if (e->e->fault(Engine::F_HEARTBEAT_DROP)) return GPBS_OK;  // lost on the way
   d->last_heartbeat = e->e->now();
   return GPBS_OK;
 }

@@ -125,6 +125,12 @@ void Engine::run_due(int64_t n) {
     heap_.pop();
     TimerEnt& t = timers_[e.id];
     if (!t.alive || !t.armed || t.gen != e.gen) continue;
+    if (!e.jittered && fault(F_TIMER_JITTER)) {  // fire late, once
+      e.when += std::max<int64_t>(1, fault_param[F_TIMER_JITTER]) * 1000;
+      e.jittered = true;
+      heap_.push(e);
+      continue;
+    }
     t.armed = false;
     int64_t tn = n;
     if (boot.sim_clock) {
@@ -162,8 +168,41 @@ void Engine::process_softirqs() {
 }
 
 void Engine::flush_actuation() {
+  if (dirty_actuation && fault(F_ACTUATE_DELAY)) return;  // held back: applied with the next batch
   if (dirty_actuation && actuator_ops.on_flush) actuator_ops.on_flush(actuator_ops.user, now());
   dirty_actuation = false;
+}
+
+int Engine::fault_parse(const char* spec) {
+  static const char* names[F_NKIND] = {"counter_drop", "counter_reset", "heartbeat_drop", "actuate_delay",
+                                       "timer_jitter"};
+  if (!spec) return 0;
+  int n = 0;
+  std::string s(spec);
+  size_t pos = 0;
+  while (pos < s.size()) {
+    size_t end = s.find(',', pos);
+    if (end == std::string::npos) end = s.size();
+    const std::string item = s.substr(pos, end - pos);
+    pos = end + 1;
+    const size_t eq = item.find('=');
+    if (eq == std::string::npos) continue;
+    const std::string key = item.substr(0, eq);
+    const std::string val = item.substr(eq + 1);
+    if (key == "seed") {
+      fault_rng = std::strtoull(val.c_str(), nullptr, 0) | 1ull;
+      continue;
+    }
+    for (int k = 0; k < F_NKIND; ++k)
+      if (key == names[k]) {
+        fault_ppm[k] = (uint32_t)std::min<unsigned long>(1000000ul, std::strtoul(val.c_str(), nullptr, 0));
+        const size_t colon = val.find(':');
+        if (colon != std::string::npos) fault_param[k] = std::strtoll(val.c_str() + colon + 1, nullptr, 0);
+        ++n;
+      }
+  }
+  if (n) printk(fmt("(GPBS) fault injection armed: %s\n", spec));
+  return n;
 }
 
 // --------------------------------------------------------------- lifecycle -
@@ -529,7 +568,12 @@ void Engine::vcpu_migrate(Slot& v) {
 }
 
 void Engine::pmu_refresh(Slot& v) {
-  if (v.is_idle() || !counter_ops.slot_refresh) return;
+  if (v.is_idle()) return;
+  if (fault(F_COUNTER_RESET)) {  // PMU reset under the scheduler (Q5)
+    for (int i = 0; i < kNumPmc; ++i) v.pmc[i] = 0;
+    return;
+  }
+  if (fault(F_COUNTER_DROP) || !counter_ops.slot_refresh) return;
   counter_ops.slot_refresh(counter_ops.user, v.id, v.tenant, v.processor, v.pmc);
 }
 

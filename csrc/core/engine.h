@@ -249,6 +249,30 @@ class Engine {
     trace->emit(now(), ev, cpu, a0, a1, a2, a3);
   }
 
+  // --- fault injection (S13; GPBS_FAULT="kind=ppm[:param],...") ---
+  // Each kind fires with probability ppm / 1e6 at its injection point, from a
+  // seeded xorshift stream (reproducible runs): counter_drop (slot counters
+  // not refreshed: stale vPMU), counter_reset (slot counters zeroed: a PMU
+  // reset, exercises the Q5 skip), heartbeat_drop (tenant heartbeats lost),
+  // actuate_delay (a flush of partition switches held back to the next
+  // batch), timer_jitter (a due timer fires `param` us late).
+  enum FaultKind { F_COUNTER_DROP = 0, F_COUNTER_RESET, F_HEARTBEAT_DROP, F_ACTUATE_DELAY, F_TIMER_JITTER, F_NKIND };
+  uint32_t fault_ppm[F_NKIND] = {0, 0, 0, 0, 0};
+  int64_t fault_param[F_NKIND] = {0, 0, 0, 0, 0};
+  uint64_t fault_hits[F_NKIND] = {0, 0, 0, 0, 0};
+  uint64_t fault_rng = 0x9E3779B97F4A7C15ull;
+  bool fault(int k) {
+    if (!fault_ppm[k]) return false;
+    fault_rng ^= fault_rng << 13;
+    fault_rng ^= fault_rng >> 7;
+    fault_rng ^= fault_rng << 17;
+    if (fault_rng % 1000000u >= fault_ppm[k]) return false;
+    fault_hits[k]++;
+    perfc.incr(PC_fault_injected);
+    return true;
+  }
+  int fault_parse(const char* spec);
+
   // --- dispatcher thread (real clock) ---
   int start();
   int stop();
@@ -274,6 +298,7 @@ class Engine {
     uint64_t seq;
     int id;
     uint64_t gen;
+    bool jittered = false;
     bool operator>(const HeapEnt& o) const { return when != o.when ? when > o.when : seq > o.seq; }
   };
   std::vector<TimerEnt> timers_;

@@ -12,6 +12,10 @@ constexpr int kXcds = 8;          // MI355X: 8 XCDs x 32 CUs
 constexpr int kMaxTenants = 64;   // per GPU context
 constexpr int kNumPmc = 4;        // INST, CYCLES, L2_REFS, L2_MISSES (modeled)
 constexpr uint32_t kNoOwner = 0xFFFFFFFFu;
+// Bit 31 of an owner word: XCD split into CU halves (spatial mode, set on both
+// words of the XCD when its two owners are of different contention classes).
+constexpr uint32_t kSplitBit = 0x80000000u;
+constexpr uint32_t kOwnerMask = 0x7FFFFFFFu;
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -108,8 +112,14 @@ __device__ __forceinline__ bool owns(const PartTable* t, u32 mode, u32 me, u32 x
   const u64 pair = (mode & GATE_DEVTABLE)
                        ? __hip_atomic_load(&t->pair[xcc & 7], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                        : __hip_atomic_load(&t->pair[xcc & 7], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  if (mode & GATE_SPATIAL) return (u32)(pair >> (32 * cu_half())) == me;
-  return (u32)pair == me || (u32)(pair >> 32) == me;
+  const u32 w0 = (u32)pair, w1 = (u32)(pair >> 32);
+  const bool h0 = (w0 & kOwnerMask) == me, h1 = (w1 & kOwnerMask) == me;
+  if (!(mode & GATE_SPATIAL) || (h0 && h1)) return h0 || h1;
+  // Spatial: a split XCD confines each owner to its CU half; an unsplit one
+  // (same-class owners, or the other side idle) is shared in full.
+  if (h0) return !(w0 & kSplitBit) || cu_half() == 0;
+  if (h1) return !(w1 & kSplitBit) || cu_half() == 1;
+  return false;
 }
 
 // Per-(tenant, xcd) software counter block, accumulated at workgroup exit.

@@ -98,7 +98,30 @@ void act_on_switch(void* user, int part, int, int next, int, int32_t, int64_t) {
   c->switches++;
 }
 
+// Spatial mode: mark an XCD split when its two owners are of different
+// contention classes (measured: CU-disjoint halves beat co-residence for
+// compute + memory pairs; same-class pairs -- two GEMMs filling each other's
+// kernel-boundary bubbles, two streams sharing HBM -- do better sharing the
+// whole XCD, and a lone owner takes all of it: work conservation).
+void mark_splits(GpuCtx* c) {
+  for (int x = 0; x < kXcds; ++x) {
+    u32& a = c->pending[x * kCtx];
+    u32& b = c->pending[x * kCtx + 1];
+    a &= kOwnerMask | (a == kNoOwner ? kSplitBit : 0u);
+    b &= kOwnerMask | (b == kNoOwner ? kSplitBit : 0u);
+    if (!c->spatial || c->nctx < 2 || a == kNoOwner || b == kNoOwner || a == b) continue;
+    // No engine attached (manual tables): distinct owners are split.
+    const int ca = c->engine ? gpbs_tenant_class(c->engine, (int)a) : 0;
+    const int cb = c->engine ? gpbs_tenant_class(c->engine, (int)b) : 1;
+    if (ca >= 0 && cb >= 0 && ca != cb) {
+      a |= kSplitBit;
+      b |= kSplitBit;
+    }
+  }
+}
+
 void publish(GpuCtx* c) {
+  mark_splits(c);
   bool changed = false;
   for (int x = 0; x < kXcds * kCtx; ++x)
     if (__atomic_load_n(&c->h_table->owner[x], __ATOMIC_RELAXED) != c->pending[x]) changed = true;
@@ -108,7 +131,7 @@ void publish(GpuCtx* c) {
     const int64_t t = mono_ns();
     if (c->last_pub_ns)
       for (int x = 0; x < kXcds * kCtx; ++x) {
-        const u32 o = c->h_table->owner[x];
+        const u32 o = c->h_table->owner[x] & kOwnerMask;
         if (o < (u32)kMaxTenants) c->own_ns[o][x % kCtx] += t - c->last_pub_ns;
       }
     c->last_pub_ns = t;
@@ -260,12 +283,21 @@ struct Runner {
   // both halves or none (yet) launches unmasked and gates per workgroup.
   hipStream_t pick_stream() {
     if (!ctx->spatial || !cfg.gate) return stream;
-    bool h[2] = {false, false};
-    for (int x = 0; x < kXcds; ++x)
-      for (int c = 0; c < 2; ++c)
-        if (__atomic_load_n(&ctx->h_table->owner[2 * x + c], __ATOMIC_ACQUIRE) == (u32)cfg.tenant) h[c] = true;
-    if (h[0] == h[1]) return stream;
-    const int k = h[0] ? 0 : 1;
+    // Masked only if every XCD the tenant holds is split and it holds the
+    // same half of all of them; otherwise unmasked + per-workgroup gating.
+    int half = -1;
+    for (int x = 0; x < kXcds; ++x) {
+      const u32 w0 = __atomic_load_n(&ctx->h_table->owner[2 * x], __ATOMIC_ACQUIRE);
+      const u32 w1 = __atomic_load_n(&ctx->h_table->owner[2 * x + 1], __ATOMIC_ACQUIRE);
+      const bool h0 = (w0 & kOwnerMask) == (u32)cfg.tenant, h1 = (w1 & kOwnerMask) == (u32)cfg.tenant;
+      if (!h0 && !h1) continue;
+      if ((h0 && h1) || !(w0 & kSplitBit)) return stream;
+      const int k = h0 ? 0 : 1;
+      if (half >= 0 && half != k) return stream;
+      half = k;
+    }
+    if (half < 0) return stream;
+    const int k = half;
     if (!half_stream[k]) half_stream[k] = make_half_stream(k);
     return half_stream[k] ? half_stream[k] : stream;
   }
@@ -299,7 +331,7 @@ struct Runner {
   bool owns_any() {
     if (!cfg.gate) return true;
     for (int x = 0; x < kXcds * kCtx; ++x)
-      if (__atomic_load_n(&ctx->h_table->owner[x], __ATOMIC_ACQUIRE) == (u32)cfg.tenant) return true;
+      if ((__atomic_load_n(&ctx->h_table->owner[x], __ATOMIC_ACQUIRE) & kOwnerMask) == (u32)cfg.tenant) return true;
     return false;
   }
 
@@ -566,6 +598,7 @@ int gpbs_gpu_get_owners(void* p, int* owners) {
   GpuCtx* c = (GpuCtx*)p;
   for (int x = 0; x < kXcds * kCtx; ++x) {
     u32 o = __atomic_load_n(&c->h_table->owner[x], __ATOMIC_ACQUIRE);
+    if (o != kNoOwner) o &= kOwnerMask;
     owners[x] = o == kNoOwner ? -1 : (int)o;
   }
   return (int)c->h_table->epoch;

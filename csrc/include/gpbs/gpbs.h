@@ -178,6 +178,7 @@ int gpbs_slot_block(gpbs_engine_t* e, int tenant, int index);     /* index -1: a
 int gpbs_slot_yield(gpbs_engine_t* e, int tenant, int index);
 int gpbs_slot_pin(gpbs_engine_t* e, int tenant, int index, const uint64_t* mask4); /* vcpu-pin */
 int gpbs_tenant_info(gpbs_engine_t* e, int tenant, gpbs_tenant_info_t* out);
+int gpbs_tenant_class(gpbs_engine_t* e, int tenant); /* contention class: 0 compute, 1 memory, -1 unknown */
 int gpbs_slot_info(gpbs_engine_t* e, int slot, gpbs_slot_info_t* out);
 int gpbs_tenant_adapt_state(gpbs_engine_t* e, int tenant, gpbs_adapt_state_t* out, int set);
 int gpbs_tenant_heartbeat(gpbs_engine_t* e, int tenant);
@@ -211,6 +212,12 @@ void* gpbs_cpu_backend_create(gpbs_engine_t* e, void* gate);
 int gpbs_cpu_backend_map(void* backend, int partition, int host_cpu);
 int gpbs_cpu_backend_add(void* backend, int tenant, int pid);
 void gpbs_cpu_backend_destroy(void* backend);
+
+/* --- fault injection: spec "kind=ppm[:param],...,seed=N" (also env GPBS_FAULT
+ *     at engine creation); kinds counter_drop counter_reset heartbeat_drop
+ *     actuate_delay timer_jitter (param = us late) --- */
+int gpbs_fault_set(gpbs_engine_t* e, const char* spec);
+int gpbs_fault_hits(gpbs_engine_t* e, uint64_t* out, int n);
 
 /* --- cross-GPU gang windows (pbs_amd/parallel/gang.py) --- */
 int gpbs_gang_set(gpbs_engine_t* e, int tenant, int state, int64_t until_ns); /* 0 none 1 favour 2 exclude */

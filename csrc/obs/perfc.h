@@ -17,7 +17,7 @@ namespace gpbs {
   X(load_balance_other) X(steal_trylock_failed) X(steal_peer_idle) X(migrate_queued)                  \
   X(migrate_running) X(dom_init) X(dom_destroy) X(vcpu_init) X(vcpu_destroy) X(vcpu_hot)              \
   X(vcpu_check) X(delay_ms) X(adapt_inc) X(adapt_dec) X(adapt_rearm) X(metric_tick) X(report_rx)     \
-  X(gang_epoch) X(gang_timeout) X(counter_stale) X(counter_reset) X(tenant_dead) X(atc_apply)         \
+  X(gang_epoch) X(gang_timeout) X(counter_stale) X(counter_reset) X(tenant_dead) X(atc_apply) X(fault_injected)         \
   X(partition_switch) X(sched_irq) X(ratelimit_hold)
 
 enum PerfcId : int {

@@ -55,6 +55,13 @@ from ..runtime.gpu import GpuContext, Runner
 
 THROUGHPUT = ("gemm", "hbm", "coll")
 TENANTS = (("gemm", 8), ("hbm", 8), ("coll", 8), ("idle", 8))  # one slot per XCD
+# Tenant mixes (BASELINE.json configs): "4mix" = config #3/#4 (MFMA GEMM +
+# HBM stream + all-reduce + latency-critical idle), "gemm2" = config #2 (two
+# bf16 4096^2 GEMM tenants split by the counter-driven partitions).
+MIXES = {
+    "4mix": {"tenants": TENANTS, "throughput": THROUGHPUT},
+    "gemm2": {"tenants": (("gemm", 8), ("gemm_b", 8)), "throughput": ("gemm", "gemm_b")},
+}
 
 
 @dataclass
@@ -73,6 +80,7 @@ class CorunConfig:
     calib_units: int = 8
     gang_epoch_ms: float = 4.0   # N > 1: cross-GPU gang window length
     gang_share: float = 0.5      # fraction of epochs that are the all-reduce tenant's
+    mix: str = "4mix"
 
 
 POLICY_ENGINES = {
@@ -138,27 +146,35 @@ class Corun:
         torch.cuda.set_device(device)
         self.engines: Dict[str, Engine] = {}
         self.tid: Dict[str, int] = {}
+        self.tenants = MIXES[cfg.mix]["tenants"]
+        self.throughput = MIXES[cfg.mix]["throughput"]
         for pol in cfg.policies:
             if pol in POLICY_ENGINES:
                 self.engines[pol] = self._make_engine(pol)
         self.ctx = GpuContext(device, table_mode=cfg.table_mode)
         if not self.tid:  # ids without an engine: fixed order (Domain-0 = 0)
-            self.tid = {n: i + 1 for i, (n, _) in enumerate(TENANTS)}
+            self.tid = {n: i + 1 for i, (n, _) in enumerate(self.tenants)}
         self.runners: Dict[str, object] = {}
-        self.runners["gemm"] = Runner(self.ctx, "gemm", self.tid["gemm"], depth=cfg.depth, M=cfg.gemm_n,
-                                      N=cfg.gemm_n, K=cfg.gemm_n)
-        self.runners["hbm"] = Runner(self.ctx, "stream", self.tid["hbm"], depth=cfg.depth, bytes=cfg.hbm_bytes)
-        if world > 1:
-            self.runners["coll"] = CollTenant(self.ctx, self.tid["coll"], cfg.coll_bytes, self.groups.get("coll"))
-        else:
-            self.runners["coll"] = Runner(self.ctx, "reduce", self.tid["coll"], depth=cfg.depth,
-                                          bytes=cfg.coll_bytes)
-        self.runners["idle"] = Runner(self.ctx, "gemv", self.tid["idle"], depth=1, priority=1, M=cfg.idle_rows,
-                                      K=cfg.idle_rows)
+        for name, _ in self.tenants:
+            self.runners[name] = self._make_runner(name)
         self.quota: Dict[str, int] = {}
         self.solo_unit_ms: Dict[str, float] = {}
         self.solo_lat_ms = 0.0
         self.active_engine: Optional[Engine] = None
+
+    def _make_runner(self, name: str):
+        cfg, t = self.cfg, self.tid[name]
+        if name.startswith("gemm"):
+            return Runner(self.ctx, "gemm", t, depth=cfg.depth, M=cfg.gemm_n, N=cfg.gemm_n, K=cfg.gemm_n)
+        if name == "hbm":
+            return Runner(self.ctx, "stream", t, depth=cfg.depth, bytes=cfg.hbm_bytes)
+        if name == "coll":
+            if self.world > 1:
+                return CollTenant(self.ctx, t, cfg.coll_bytes, self.groups.get("coll"))
+            return Runner(self.ctx, "reduce", t, depth=cfg.depth, bytes=cfg.coll_bytes)
+        if name == "idle":
+            return Runner(self.ctx, "gemv", t, depth=1, priority=1, M=cfg.idle_rows, K=cfg.idle_rows)
+        raise ValueError(name)
 
     def _make_engine(self, pol: str) -> Engine:
         nctx, over, _, _ = POLICY_ENGINES[pol]
@@ -170,7 +186,7 @@ class Corun:
                 e.pool_assign(0, e.partition_add(self.rank, x, c))
         e.tenant_create("Domain-0", nslots=1)
         ids = {}
-        for name, ns in TENANTS:
+        for name, ns in self.tenants:
             ids[name] = e.tenant_create(name, nslots=ns)
         if self.tid and ids != self.tid:
             raise RuntimeError("tenant ids differ across engines")
@@ -193,7 +209,7 @@ class Corun:
         if self.active_engine is not None:
             self.active_engine.stop()
             self.active_engine = None
-        coll = self.runners["coll"]
+        coll = self.runners.get("coll")
         if policy in self.engines:
             e = self.engines[policy]
             _, _, gate, table = POLICY_ENGINES[policy]
@@ -205,7 +221,7 @@ class Corun:
             for r in self._natives():
                 r.set_gate(gate)
                 r.set_engine_wake(True)
-            if not isinstance(coll, Runner):
+            if isinstance(coll, CollTenant):
                 coll.gate, coll.engine = True, e
                 # Cross-GPU gang windows for the all-reduce tenant: its RCCL
                 # ranks on all GPUs get their partitions in the same epochs.
@@ -218,19 +234,20 @@ class Corun:
         self.ctx.set_spatial(False)
         for r in self._natives():
             r.set_engine_wake(False)
-        if not isinstance(coll, Runner):
+        if isinstance(coll, CollTenant):
             coll.engine = None
         if policy in ("none", "solo"):
             for r in self._natives():
                 r.set_gate(False)
-            if not isinstance(coll, Runner):
+            if isinstance(coll, CollTenant):
                 coll.gate = False
-        elif policy == "static":
-            order = ["gemm", "hbm", "coll", "idle"]
-            self.ctx.set_owners([self.tid[order[x // 2]] for x in range(8)])
+        elif policy == "static":  # equal XCD split (ARINC-653-like), tenants in mix order
+            order = [n for n, _ in self.tenants]
+            per = 8 // len(order)
+            self.ctx.set_owners([self.tid[order[min(x // per, len(order) - 1)]] for x in range(8)])
             for r in self._natives():
                 r.set_gate(True)
-            if not isinstance(coll, Runner):
+            if isinstance(coll, CollTenant):
                 coll.gate = True
         else:
             raise ValueError(policy)
@@ -262,7 +279,7 @@ class Corun:
         """Solo time per unit for each throughput tenant (whole GPU, ungated)."""
         self.set_policy("solo")
         cfg = self.cfg
-        for name in THROUGHPUT:
+        for name in self.throughput:
             self._barrier()
             self._run_units(name, 2)
             self._barrier()
@@ -272,13 +289,14 @@ class Corun:
             dt = (time.perf_counter() - t0) * 1e3 / cfg.calib_units
             self.solo_unit_ms[name] = self._allreduce(dt, "max")
             self.quota[name] = max(1, int(round(cfg.target_ms / self.solo_unit_ms[name])))
-        r = self.runners["idle"]
-        r.latencies(clear=True)
-        for _ in range(20):
-            r.submit(1)
-            r.wait(10.0)
-            time.sleep(cfg.idle_period_ms / 1e3)
-        self.solo_lat_ms = _pct(r.latencies(clear=True), 0.5) / 1e6
+        r = self.runners.get("idle")
+        if r is not None:
+            r.latencies(clear=True)
+            for _ in range(20):
+                r.submit(1)
+                r.wait(10.0)
+                time.sleep(cfg.idle_period_ms / 1e3)
+            self.solo_lat_ms = _pct(r.latencies(clear=True), 0.5) / 1e6
         self.log(f"[corun] solo unit ms: {self.solo_unit_ms}  quota/step: {self.quota}  "
                  f"idle p50 {self.solo_lat_ms:.3f} ms")
 
@@ -288,7 +306,7 @@ class Corun:
         t0 = time.monotonic_ns()
         threads = []
         target = {}
-        for name in THROUGHPUT:
+        for name in self.throughput:
             r = self.runners[name]
             if isinstance(r, Runner):
                 target[name] = r.stats().units_done + self.quota[name]
@@ -297,23 +315,24 @@ class Corun:
                 th = threading.Thread(target=r.run_units, args=(self.quota[name],))
                 th.start()
                 threads.append(th)
-        idle = self.runners["idle"]
+        idle = self.runners.get("idle")
         nreq = 0
         while True:  # latency tenant: closed loop with think time while others run
-            idle.submit(1)
-            idle.wait(30.0)
-            nreq += 1
+            if idle is not None:
+                idle.submit(1)
+                idle.wait(30.0)
+                nreq += 1
             busy = any(self.runners[n].stats().units_done < target[n] for n in target) or \
                 any(t.is_alive() for t in threads)
             if not busy:
                 break
-            time.sleep(cfg.idle_period_ms / 1e3)
+            time.sleep(cfg.idle_period_ms / 1e3 if idle is not None else 2e-4)
         for name in target:
             self.runners[name].wait(120.0)
         for th in threads:
             th.join()
         done = {}
-        for name in THROUGHPUT:
+        for name in self.throughput:
             r = self.runners[name]
             last = r.stats().last_done_ns if isinstance(r, Runner) else r.last_done_ns
             done[name] = (last - t0) / 1e6
@@ -325,31 +344,32 @@ class Corun:
         self.set_policy(policy)
         for _ in range(warmup):
             self.step()
-        self.runners["idle"].latencies(clear=True)
+        if "idle" in self.runners:
+            self.runners["idle"].latencies(clear=True)
         for n in self.tid:
             self.ctx.ownership(self.tid[n], clear=True)
         e = self.active_engine
         if e is not None:
             e.perfc_reset()
             run0 = {n: e.tenant_info(self.tid[n]).run_ns for n in self.tid}
-        per = {n: [] for n in THROUGHPUT}
+        per = {n: [] for n in self.throughput}
         self._barrier()
         t0 = time.perf_counter()
         quanta = {n: [] for n in self.tid}
         for _ in range(steps):
             d = self.step()
-            for n in THROUGHPUT:
+            for n in self.throughput:
                 per[n].append(d[n])
             if e is not None:
                 for n in self.tid:
                     quanta[n].append(e.tenant_info(self.tid[n]).tslice_us)
         self._barrier()
         wall_ms = self._allreduce((time.perf_counter() - t0) * 1e3, "max")
-        lats = [x / 1e6 for x in self.runners["idle"].latencies(clear=True)]
+        lats = [x / 1e6 for x in self.runners["idle"].latencies(clear=True)] if "idle" in self.runners else []
         res = {"policy": policy, "wall_ms": wall_ms, "ms_per_step": wall_ms / steps, "tenants": {}}
         agg = 0.0
         slows = []
-        for n in THROUGHPUT:
+        for n in self.throughput:
             t_i = statistics.mean(per[n])
             T_i = self.quota[n] * self.solo_unit_ms[n]
             perf = T_i / t_i if t_i > 0 else 0.0
@@ -359,11 +379,12 @@ class Corun:
                                  "slowdown_pct": round(slows[-1], 2)}
         p50, p99 = _pct(lats, 0.5), _pct(lats, 0.99)
         idle_perf = self.solo_lat_ms / p50 if p50 > 0 else 0.0
-        slows.append((p50 / self.solo_lat_ms - 1.0) * 100.0 if self.solo_lat_ms > 0 else 0.0)
-        res["tenants"]["idle"] = {"p50_ms": round(p50, 4), "p99_ms": round(p99, 4),
-                                  "solo_p50_ms": round(self.solo_lat_ms, 4), "norm_perf": round(idle_perf, 4),
-                                  "slowdown_pct": round(slows[-1], 2), "requests": len(lats),
-                                  "over_ms": {str(b): sum(1 for x in lats if x > b) for b in (0.5, 1, 2, 5)}}
+        if "idle" in self.runners:
+            slows.append((p50 / self.solo_lat_ms - 1.0) * 100.0 if self.solo_lat_ms > 0 else 0.0)
+            res["tenants"]["idle"] = {"p50_ms": round(p50, 4), "p99_ms": round(p99, 4),
+                                      "solo_p50_ms": round(self.solo_lat_ms, 4), "norm_perf": round(idle_perf, 4),
+                                      "slowdown_pct": round(slows[-1], 2), "requests": len(lats),
+                                      "over_ms": {str(b): sum(1 for x in lats if x > b) for b in (0.5, 1, 2, 5)}}
         res["aggregate"] = agg
         res["aggregate_all_gpus"] = self._allreduce(agg, "sum")
         res["mean_slowdown_pct"] = statistics.mean(slows)

@@ -237,6 +237,17 @@ class Engine:
     def set_adapt_state(self, t: int, s: N.AdaptState):
         return self._chk(self.lib.gpbs_tenant_adapt_state(self.h, t, C.byref(s), 1), "set_adapt_state")
 
+    FAULT_KINDS = ("counter_drop", "counter_reset", "heartbeat_drop", "actuate_delay", "timer_jitter")
+
+    def fault_set(self, spec: str) -> int:
+        """Arm fault injection: "kind=ppm[:param],...,seed=N" (see gpbs.h)."""
+        return self.lib.gpbs_fault_set(self.h, spec.encode())
+
+    def fault_hits(self) -> Dict[str, int]:
+        arr = (C.c_uint64 * len(self.FAULT_KINDS))()
+        n = self.lib.gpbs_fault_hits(self.h, arr, len(self.FAULT_KINDS))
+        return {k: arr[i] for i, k in enumerate(self.FAULT_KINDS[:n])}
+
     GANG_NONE, GANG_FAVOUR, GANG_EXCLUDE = 0, 1, 2
 
     def gang_set(self, t: int, state: int, until_ns: int):

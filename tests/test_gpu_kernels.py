@@ -104,11 +104,14 @@ def test_gating_confines_work_to_owned_xcds():
 def test_counter_reduce_kernel():
     cnt = torch.randint(0, 1 << 40, (64, 8, 4), device="cuda", dtype=torch.int64)
     prev = torch.randint(0, 1 << 30, (64, 8, 4), device="cuda", dtype=torch.int64)
+    prev[3, 2, 1] = cnt[3, 2, 1] + 5  # force one reset
     prev0 = prev.clone()
     ids = torch.tensor([3, 0, 17, 63], device="cuda", dtype=torch.int32)
     out = K.counter_reduce(cnt, prev, ids)
     torch.cuda.synchronize()
-    ref = (cnt - prev0)[ids.long()].sum(dim=1)
+    # Q5: a counter that went backwards (reset) contributes 0, per element
+    delta = torch.where(cnt >= prev0, cnt - prev0, torch.zeros_like(cnt))
+    ref = delta[ids.long()].sum(dim=1)
     assert torch.equal(out, ref)
     assert torch.equal(prev[ids.long()], cnt[ids.long()])
 

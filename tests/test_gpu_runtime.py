@@ -117,10 +117,17 @@ def test_half_cu_mask_stream_confines_workgroups_to_one_half():
 def test_spatial_gate_follows_the_cu_half():
     from pbs_amd.ops import kernels as K
     ctx = GpuContext(0, None, nctx=2)
-    ctx.set_owners([t for x in range(8) for t in (1, 2)])  # tenant 1: half 0, tenant 2: half 1
+    ctx.set_spatial(True)
+    # XCDs 0-5: tenant 1 on half 0, tenant 2 on half 1 (split); XCDs 6-7:
+    # tenant 1 alone (unsplit: it gets the whole XCD)
+    ctx.set_owners([t for x in range(6) for t in (1, 2)] + [1, -1, 1, -1])
     for me, half in ((1, 0), (2, 1)):
         out = K.census(2048, table=ctx.table, tenant=me, spatial=True).cpu()
         for xcc, hw, ok, magic in out.tolist():
             assert magic == 0xC0FFEE
-            assert bool(ok) == ((_se(hw) >> 1) == half), (me, xcc, hex(hw))
+            if xcc < 6:
+                assert bool(ok) == ((_se(hw) >> 1) == half), (me, xcc, hex(hw))
+            else:
+                assert bool(ok) == (me == 1), (me, xcc)
+    assert ctx.owners()[:2] == [1, 2]  # split bit hidden from readers
     ctx.close()
