@@ -56,7 +56,7 @@ struct alignas(64) WorkQueue {
 // Exit protocol of every tenant kernel: the last workgroup to leave publishes
 // the unit count to the host-visible status word (pinned, system scope), so the
 // runner learns "finished or revoked" from the completion event alone.
-__device__ __forceinline__ void finish(WorkQueue* q, u32* status) {
+__device__ __forceinline__ void finish(WorkQueue* q, u32* status, u32 total) {
   if (threadIdx.x == 0) {
     __threadfence();
     const u32 old = atomicAdd(&q->exited, 1u);
@@ -64,6 +64,18 @@ __device__ __forceinline__ void finish(WorkQueue* q, u32* status) {
       __threadfence();
       const u32 d = __hip_atomic_load(&q->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (status) __hip_atomic_store(status, d | 0x80000000u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      // Last one out of a fully completed invocation leaves the queue zeroed
+      // for the next launch (no per-launch memset on the tenant stream); a
+      // revoked one keeps next/done for the runner's relaunch.
+      if (d >= total) {
+        q->next = 0;
+        q->done = 0;
+        q->exited = 0;
+        q->stopped = 0;
+#pragma unroll
+        for (int x = 0; x < kXcds; ++x) q->xnext[x] = 0;
+        __threadfence();
+      }
     }
   }
 }

@@ -401,7 +401,6 @@ struct Runner {
             inflight++;
             next_q = (qi + 1) % nq;
             q_busy[qi] = 1;
-            hipMemsetAsync(d_q + qi, 0, sizeof(WorkQueue), stream);
           } else {
             relaunch.pop_front();
             st.relaunches++;
@@ -670,6 +669,9 @@ void* gpbs_runner_create(void* ctx, const gpbs_runner_cfg_t* cfg) {
   hipDeviceGetStreamPriorityRange(&lo, &hi);
   bool ok = hipStreamCreateWithPriority(&r->stream, hipStreamNonBlocking, cfg->priority ? hi : lo) == hipSuccess;
   ok = ok && hipMalloc((void**)&r->d_q, sizeof(WorkQueue) * r->nq) == hipSuccess;
+  // zeroed once: a kernel that completes every unit leaves its queue zeroed
+  // (finish()), so fresh launches need no memset on the tenant stream
+  ok = ok && hipMemset(r->d_q, 0, sizeof(WorkQueue) * r->nq) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&r->h_status, sizeof(u32) * r->nq, hipHostMallocCoherent | hipHostMallocMapped) ==
                  hipSuccess;
   for (int i = 0; i < r->nq && ok; ++i) ok = hipEventCreateWithFlags(&r->ev[i], hipEventDisableTiming) == hipSuccess;

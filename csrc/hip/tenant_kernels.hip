@@ -219,7 +219,7 @@ __global__ __launch_bounds__(GNT, 2) void k_gemm_bf16_tn(const u16* __restrict__
       }
     count_unit(cnt, me, xcc, inst_per_tile, &t_last, refs_per_tile, miss_per_tile, q);
   }
-  finish(q, status);
+  finish(q, status, (u32)ntiles);
 }
 
 // -------------------------------------------------------- GEMM 256x256 ----
@@ -417,7 +417,7 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restr
       }
     count_unit(cnt, me, xcc, inst_per_tile, &t_last, refs_per_tile, miss_per_tile, q);
   }
-  finish(q, status);
+  finish(q, status, (u32)ntiles);
 }
 
 // ------------------------------------------------------------ HBM stream ---
@@ -460,7 +460,7 @@ __global__ __launch_bounds__(SNT) void k_stream_copy(const f32x4* __restrict__ s
     }
     count_unit(cnt, me, xcc, inst, &t_last, 2 * lines, 2 * lines, q);
   }
-  finish(q, status);
+  finish(q, status, nchunks);
 }
 
 // ------------------------------------------------- reduce-copy (all-reduce) -
@@ -511,7 +511,7 @@ __global__ __launch_bounds__(SNT) void k_reduce_bf16(const u32x4* __restrict__ a
     }
     count_unit(cnt, me, xcc, inst, &t_last, 3 * lines, 3 * lines, q);
   }
-  finish(q, status);
+  finish(q, status, nchunks);
 }
 
 // --------------------------------------------------------------- GEMV -----
@@ -583,7 +583,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
     }
     count_unit(cnt, me, xcc, (u64)16 * (K / 512 + 8), &t_last, lines, lines, q);
   }
-  finish(q, status);
+  finish(q, status, nchunks);
 }
 
 // ------------------------------------------------------------- census ------

@@ -1,0 +1,174 @@
+"""Config #5: Llama-3-8B inference co-located with a bf16 training tenant on
+one MI355X, under default hardware sharing ("none") and under gpbsd
+("gpbs": both are torch processes attached through the tenant shim, their
+kernels confined to the CU partitions the scheduler hands them, classes and
+quanta driven by the counters they publish).
+
+    python -m pbs_amd.bench.llm_corun [--seconds 8] [--policies solo,none,gpbs]
+
+Tenants (random-init weights of the real architectures, synthetic tokens):
+  infer  Llama-3-8B greedy decode, batch 8, 1024-token prompt, KV cache 2048
+  train  Llama-3.2-1B-shaped training step (bf16, fused AdamW), batch 4 x 2048
+
+Per tenant: throughput (decode tokens/s, train tokens/s), decode-step
+latency p50/p99; normalised to the solo run on the same box:
+aggregate = sum of co-run/solo throughputs, slowdown = mean over tenants.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import multiprocessing as mp
+import os
+import statistics
+import sys
+import tempfile
+import time
+from typing import Dict, Optional
+
+os.environ["GPU_MAX_HW_QUEUES"] = str(max(8, int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)))
+
+
+def _tenant(kind: str, seconds: float, warmup: float, socket: Optional[str], q, start_evt, args: dict):
+    import torch
+
+    from ..models.llama import PRESETS, LlamaDecoder, LlamaTrainer
+    torch.cuda.set_device(0)
+    t = None
+    if socket:
+        from ..runtime.tenant import TenantClient
+        t = TenantClient(kind, socket, slots=8, weight=args.get(f"{kind}_weight", 256))
+    if kind == "infer":
+        w = LlamaDecoder(PRESETS[args["infer_model"]], batch=args["infer_batch"], context=args["context"])
+        prompt = torch.randint(0, w.cfg.vocab, (w.batch, args["prompt"]), device="cuda")
+        nxt = w.prefill(prompt)
+        flops = 2.0 * w.cfg.n_params() * w.batch
+        bytes_ = 2.0 * w.cfg.n_params()
+
+        def unit():
+            nonlocal nxt
+            nxt = w.decode_step(nxt)
+        per_unit_tokens = w.batch
+    else:
+        w = LlamaTrainer(PRESETS[args["train_model"]], batch=args["train_batch"], seq=args["train_seq"])
+        flops = w.flops_per_step()
+        bytes_ = 16.0 * w.cfg.n_params()  # params + grads + fp32 Adam state traffic
+
+        def unit():
+            w.step()
+        per_unit_tokens = w.tokens_per_step()
+    torch.cuda.synchronize()
+    start_evt.wait()
+    lat = []
+    t_warm = time.monotonic() + warmup
+    t_end = t_warm + seconds
+    n = 0
+    while True:
+        now = time.monotonic()
+        if now >= t_end:
+            break
+        t0 = time.perf_counter()
+        if t is not None:
+            with t.slice(timeout_s=30.0):
+                unit()
+                torch.cuda.current_stream().synchronize()
+            t.account(flops=flops, bytes_moved=bytes_, busy_ns=int((time.perf_counter() - t0) * 1e9))
+        else:
+            unit()
+            torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        if now >= t_warm:
+            lat.append(dt)
+            n += 1
+    if t is not None:
+        t.close()
+    span = sum(lat)
+    q.put({"kind": kind, "units": n, "tokens_per_s": n * per_unit_tokens / span if span else 0.0,
+           "p50_ms": 1e3 * statistics.median(lat) if lat else 0.0,
+           "p99_ms": 1e3 * sorted(lat)[int(0.99 * (len(lat) - 1))] if lat else 0.0})
+
+
+def run(policy: str, kinds, args: dict, seconds: float, warmup: float) -> Dict[str, dict]:
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    start = ctx.Event()
+    daemon = None
+    sock = None
+    if policy == "gpbs":
+        from ..runtime.daemon import Daemon
+        sock = os.path.join(tempfile.mkdtemp(), "gpbsd.sock")
+        daemon = Daemon(sock, gpus=[0], nctx=2, sim=False, profile="mi355x").start()
+    ps = [ctx.Process(target=_tenant, args=(k, seconds, warmup, sock, q, start, args)) for k in kinds]
+    for p in ps:
+        p.start()
+    time.sleep(0.5)
+    start.set()
+    out = {}
+    try:
+        for _ in ps:
+            r = q.get(timeout=900)
+            out[r["kind"]] = r
+    finally:
+        for p in ps:
+            p.join(timeout=120)
+        if daemon is not None:
+            out["_engine"] = {"z": daemon.engine.debug_keys("z")[-2000:], "perfc": {
+                k: v for k, v in daemon.engine.perfc().items() if v and k in ("sched_ctx", "metric_tick",
+                                                                              "report_rx", "adapt_inc",
+                                                                              "adapt_dec")}}
+            daemon.stop()
+    return out
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=8.0)
+    ap.add_argument("--warmup", type=float, default=2.0)
+    ap.add_argument("--policies", default="solo,none,gpbs")
+    ap.add_argument("--infer-model", default="llama3-8b")
+    ap.add_argument("--train-model", default="llama3-1b")
+    ap.add_argument("--infer-batch", type=int, default=8)
+    ap.add_argument("--prompt", type=int, default=1024)
+    ap.add_argument("--context", type=int, default=2048)
+    ap.add_argument("--train-batch", type=int, default=4)
+    ap.add_argument("--train-seq", type=int, default=2048)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args(argv)
+    args = {"infer_model": a.infer_model, "train_model": a.train_model, "infer_batch": a.infer_batch,
+            "prompt": a.prompt, "context": a.context, "train_batch": a.train_batch, "train_seq": a.train_seq,
+            "infer_weight": 512, "train_weight": 256}
+    res = {}
+    pols = [p for p in a.policies.split(",") if p]
+    if "solo" in pols:
+        res["solo"] = {}
+        for k in ("infer", "train"):
+            res["solo"].update(run("solo", [k], args, a.seconds, a.warmup))
+            print(f"[llm] solo {k}: {json.dumps(res['solo'][k])}", file=sys.stderr, flush=True)
+    for p in pols:
+        if p == "solo":
+            continue
+        res[p] = run(p, ["infer", "train"], args, a.seconds, a.warmup)
+        print(f"[llm] {p}: {json.dumps({k: v for k, v in res[p].items() if not k.startswith('_')})}",
+              file=sys.stderr, flush=True)
+    summary = {}
+    if "solo" in res:
+        for p, r in res.items():
+            if p == "solo":
+                continue
+            norm = {k: r[k]["tokens_per_s"] / res["solo"][k]["tokens_per_s"] for k in ("infer", "train")
+                    if res["solo"][k]["tokens_per_s"]}
+            summary[p] = {"aggregate": round(sum(norm.values()), 4),
+                          "mean_slowdown_pct": round(statistics.mean((1 / v - 1) * 100 for v in norm.values()), 2),
+                          "norm": {k: round(v, 4) for k, v in norm.items()},
+                          "infer_p99_ms": round(r["infer"]["p99_ms"], 3),
+                          "infer_p50_ms": round(r["infer"]["p50_ms"], 3)}
+    line = {"config": "#5 Llama-3-8B decode + Llama-1B bf16 training, 1x MI355X", "data": "synthetic tokens, "
+            "random-init weights", "dtype": "bf16", "summary": summary, "raw": res}
+    print(json.dumps(line))
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(line, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

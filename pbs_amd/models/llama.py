@@ -1,0 +1,243 @@
+"""Llama-3 family tenants (BASELINE config #5: "Llama-3-8B inference
+co-located with a bf16 training tenant").
+
+Random-initialised weights of the published architecture (no checkpoints
+exist offline): GQA attention with RoPE (theta 500k), SwiGLU MLP, RMSNorm,
+bf16 parameters and activations.  Two entry points:
+
+* ``LlamaDecoder`` -- inference: prefill into a static KV cache sized for the
+  full context, then one-token decode steps.  On a GPU the decode path runs
+  the fused gfx950 kernels of ``pbs_amd.ops.llm`` (RMSNorm, SwiGLU, RoPE) and
+  hipBLASLt for the projections; ``fused=False`` is the eager reference.
+* ``LlamaTrainer`` -- training: causal-LM loss, backward, fused AdamW step
+  (autograd through the PyTorch ops; bf16 weights, fp32 optimizer state).
+
+Sizes are the real ones ("llama3-8b": 8.03 B parameters, 16 GB bf16); the
+small presets exist for tests.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+@dataclass
+class LlamaConfig:
+    dim: int = 4096
+    n_layers: int = 32
+    n_heads: int = 32
+    n_kv_heads: int = 8
+    ffn_dim: int = 14336
+    vocab: int = 128256
+    rope_theta: float = 500000.0
+    norm_eps: float = 1e-5
+    max_seq: int = 8192
+
+    @property
+    def head_dim(self) -> int:
+        return self.dim // self.n_heads
+
+    def n_params(self) -> int:
+        hd = self.head_dim
+        attn = self.dim * (self.n_heads * hd) * 2 + self.dim * (self.n_kv_heads * hd) * 2
+        mlp = 3 * self.dim * self.ffn_dim
+        return self.n_layers * (attn + mlp + 2 * self.dim) + 2 * self.vocab * self.dim + self.dim
+
+
+PRESETS = {
+    "llama3-8b": LlamaConfig(),
+    "llama3-1b": LlamaConfig(dim=2048, n_layers=16, n_heads=32, n_kv_heads=8, ffn_dim=8192),
+    "tiny": LlamaConfig(dim=256, n_layers=2, n_heads=8, n_kv_heads=2, ffn_dim=512, vocab=1024, max_seq=256),
+}
+
+
+def rope_tables(cfg: LlamaConfig, device, dtype=torch.float32):
+    hd = cfg.head_dim
+    inv = 1.0 / (cfg.rope_theta ** (torch.arange(0, hd, 2, device=device, dtype=torch.float64) / hd))
+    t = torch.arange(cfg.max_seq, device=device, dtype=torch.float64)
+    f = torch.outer(t, inv)
+    return f.cos().to(dtype), f.sin().to(dtype)  # [max_seq, hd/2]
+
+
+def apply_rope_ref(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    """x [B, S, H, hd] (interleaved pairs), cos/sin [S, hd/2]."""
+    xf = x.float().unflatten(-1, (-1, 2))
+    a, b = xf[..., 0], xf[..., 1]
+    c, s = cos[None, :, None, :], sin[None, :, None, :]
+    return torch.stack((a * c - b * s, a * s + b * c), dim=-1).flatten(-2).to(x.dtype)
+
+
+class RMSNorm(nn.Module):
+    def __init__(self, dim: int, eps: float):
+        super().__init__()
+        self.eps = eps
+        self.weight = nn.Parameter(torch.ones(dim))
+
+    def forward(self, x):
+        xf = x.float()
+        return (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + self.eps)).to(x.dtype) * self.weight
+
+
+class Block(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        hd = cfg.head_dim
+        self.cfg = cfg
+        self.attn_norm = RMSNorm(cfg.dim, cfg.norm_eps)
+        self.wq = nn.Linear(cfg.dim, cfg.n_heads * hd, bias=False)
+        self.wk = nn.Linear(cfg.dim, cfg.n_kv_heads * hd, bias=False)
+        self.wv = nn.Linear(cfg.dim, cfg.n_kv_heads * hd, bias=False)
+        self.wo = nn.Linear(cfg.n_heads * hd, cfg.dim, bias=False)
+        self.mlp_norm = RMSNorm(cfg.dim, cfg.norm_eps)
+        self.w1 = nn.Linear(cfg.dim, cfg.ffn_dim, bias=False)  # gate
+        self.w3 = nn.Linear(cfg.dim, cfg.ffn_dim, bias=False)  # up
+        self.w2 = nn.Linear(cfg.ffn_dim, cfg.dim, bias=False)  # down
+
+    def attention(self, h, cos, sin, cache=None, pos: int = 0, fused: bool = False):
+        B, S, _ = h.shape
+        cfg, hd = self.cfg, self.cfg.head_dim
+        q = self.wq(h).view(B, S, cfg.n_heads, hd)
+        k = self.wk(h).view(B, S, cfg.n_kv_heads, hd)
+        v = self.wv(h).view(B, S, cfg.n_kv_heads, hd)
+        if fused:
+            from ..ops import llm
+            q, k = llm.rope(q, cos, sin, pos), llm.rope(k, cos, sin, pos)
+        else:
+            q = apply_rope_ref(q, cos[pos:pos + S], sin[pos:pos + S])
+            k = apply_rope_ref(k, cos[pos:pos + S], sin[pos:pos + S])
+        if cache is not None:
+            kc, vc = cache
+            kc[:, :, pos:pos + S] = k.transpose(1, 2)
+            vc[:, :, pos:pos + S] = v.transpose(1, 2)
+            k_all, v_all = kc[:, :, :pos + S], vc[:, :, :pos + S]
+        else:
+            k_all, v_all = k.transpose(1, 2), v.transpose(1, 2)
+        # GQA without materialising repeated K/V (at decode the cache read is
+        # the attention cost; repeat_interleave would read+write it 4x more)
+        o = F.scaled_dot_product_attention(q.transpose(1, 2), k_all, v_all, is_causal=(S > 1), enable_gqa=True)
+        return self.wo(o.transpose(1, 2).reshape(B, S, cfg.n_heads * hd))
+
+    def forward(self, x, cos, sin, cache=None, pos: int = 0, fused: bool = False):
+        if fused:
+            from ..ops import llm
+            h = llm.rmsnorm(x, self.attn_norm.weight, self.attn_norm.eps)
+            x = x + self.attention(h, cos, sin, cache, pos, fused=True)
+            h = llm.rmsnorm(x, self.mlp_norm.weight, self.mlp_norm.eps)
+            return x + self.w2(llm.swiglu(self.w1(h), self.w3(h)))
+        x = x + self.attention(self.attn_norm(x), cos, sin, cache, pos)
+        h = self.mlp_norm(x)
+        return x + self.w2(F.silu(self.w1(h)) * self.w3(h))
+
+
+class Llama(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.cfg = cfg
+        self.embed = nn.Embedding(cfg.vocab, cfg.dim)
+        self.layers = nn.ModuleList(Block(cfg) for _ in range(cfg.n_layers))
+        self.norm = RMSNorm(cfg.dim, cfg.norm_eps)
+        self.lm_head = nn.Linear(cfg.dim, cfg.vocab, bias=False)
+        self._rope = None
+
+    @torch.no_grad()
+    def init_random(self, std: float = 0.02, seed: int = 0):
+        g = torch.Generator(device=next(self.parameters()).device).manual_seed(seed)
+        for n, p in self.named_parameters():
+            if n.endswith("norm.weight"):
+                p.fill_(1.0)
+            else:
+                p.normal_(0.0, std, generator=g)
+        return self
+
+    def rope(self, device):
+        if self._rope is None or self._rope[0].device != device:
+            self._rope = rope_tables(self.cfg, device)
+        return self._rope
+
+    def forward(self, tokens, cache=None, pos: int = 0, fused: bool = False, last_only: bool = False):
+        cos, sin = self.rope(tokens.device)
+        x = self.embed(tokens)
+        for i, layer in enumerate(self.layers):
+            x = layer(x, cos, sin, None if cache is None else cache[i], pos, fused)
+        if last_only:
+            x = x[:, -1:]
+        x = self.norm(x) if not fused else __import__("pbs_amd.ops.llm", fromlist=["rmsnorm"]).rmsnorm(
+            x, self.norm.weight, self.norm.eps)
+        return self.lm_head(x)
+
+
+def build(cfg: LlamaConfig, device, dtype) -> "Llama":
+    """Construct directly in `dtype` on `device` (no fp32 transient: 8B
+    parameters would otherwise pass through 32 GB of fp32)."""
+    prev = torch.get_default_dtype()
+    torch.set_default_dtype(dtype)
+    try:
+        with torch.device(device):
+            m = Llama(cfg)
+    finally:
+        torch.set_default_dtype(prev)
+    return m.init_random()
+
+
+class LlamaDecoder:
+    """Inference tenant: static KV cache, greedy decode."""
+
+    def __init__(self, cfg: LlamaConfig, batch: int, context: int, device="cuda", dtype=torch.bfloat16,
+                 fused: Optional[bool] = None):
+        self.cfg, self.batch, self.context = cfg, batch, context
+        self.model = build(cfg, device, dtype)
+        self.model.eval()
+        self.fused = (torch.cuda.is_available() and str(device).startswith("cuda")) if fused is None else fused
+        hd = cfg.head_dim
+        self.cache = [(torch.zeros(batch, cfg.n_kv_heads, context, hd, device=device, dtype=dtype),
+                       torch.zeros(batch, cfg.n_kv_heads, context, hd, device=device, dtype=dtype))
+                      for _ in range(cfg.n_layers)]
+        self.pos = 0
+
+    @torch.no_grad()
+    def prefill(self, tokens: torch.Tensor) -> torch.Tensor:
+        self.pos = 0
+        logits = self.model(tokens, cache=self.cache, pos=0, fused=self.fused, last_only=True)
+        self.pos = tokens.shape[1]
+        return logits[:, -1].argmax(-1, keepdim=True)
+
+    @torch.no_grad()
+    def decode_step(self, tok: torch.Tensor) -> torch.Tensor:
+        if self.pos >= self.context:
+            self.pos = self.context // 2  # slide: keep the cache bounded for long runs
+        logits = self.model(tok, cache=self.cache, pos=self.pos, fused=self.fused)
+        self.pos += 1
+        return logits[:, -1].argmax(-1, keepdim=True)
+
+
+class LlamaTrainer:
+    """Training tenant: next-token loss, backward, fused AdamW (fp32 state)."""
+
+    def __init__(self, cfg: LlamaConfig, batch: int, seq: int, device="cuda", dtype=torch.bfloat16, lr=1e-4):
+        self.cfg, self.batch, self.seq = cfg, batch, seq
+        self.model = build(cfg, device, dtype)
+        self.model.train()
+        kw = {"fused": True} if str(device).startswith("cuda") else {}
+        self.opt = torch.optim.AdamW(self.model.parameters(), lr=lr, weight_decay=0.1, **kw)
+        g = torch.Generator(device=device).manual_seed(1)
+        self.tokens = torch.randint(0, cfg.vocab, (batch, seq + 1), device=device, generator=g)
+
+    def step(self) -> torch.Tensor:
+        x, y = self.tokens[:, :-1], self.tokens[:, 1:]
+        logits = self.model(x)
+        loss = F.cross_entropy(logits.float().reshape(-1, self.cfg.vocab), y.reshape(-1))
+        loss.backward()
+        self.opt.step()
+        self.opt.zero_grad(set_to_none=True)
+        return loss.detach()
+
+    def tokens_per_step(self) -> int:
+        return self.batch * self.seq
+
+    def flops_per_step(self) -> float:
+        return 6.0 * self.cfg.n_params() * self.tokens_per_step()

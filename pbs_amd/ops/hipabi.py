@@ -39,6 +39,9 @@ def bind(lib):
     _p(lib, "gpbs_hip_gemv_bf16", C.c_int, vp, vp, vp, C.c_int, C.c_int, vp, vp, C.c_uint, C.c_uint, vp, vp, C.c_int,
        vp)
     _p(lib, "gpbs_hip_set_gemm_opts", C.c_int, C.c_int)
+    _p(lib, "gpbs_hip_rmsnorm_bf16", C.c_int, vp, vp, vp, C.c_int, C.c_int, C.c_float, vp)
+    _p(lib, "gpbs_hip_swiglu_bf16", C.c_int, vp, vp, vp, C.c_ulonglong, vp)
+    _p(lib, "gpbs_hip_rope_bf16", C.c_int, vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp)
     _p(lib, "gpbs_hip_census", C.c_int, vp, C.c_int, vp, C.c_uint, C.c_uint, vp)
     _p(lib, "gpbs_hip_partition_switch", C.c_int, vp, C.c_uint, C.POINTER(C.c_uint), vp)
     _p(lib, "gpbs_hip_counter_reduce", C.c_int, vp, vp, vp, C.c_int, vp, vp)

@@ -117,23 +117,24 @@ class TenantClient:
 
     # ------------------------------------------------------------- streams
     def stream(self, owned: Optional[List[Tuple[int, int]]] = None):
-        """torch stream masked to the CUs of the partitions this tenant holds.
-        Co-resident-context partitions (``spatial=False``) map to whole XCDs."""
+        """torch stream masked to the CU halves this tenant holds.  The mask is
+        quantised to {half 0, half 1, both} across all XCDs: a CU mask is a
+        hardware-queue property, so every distinct mask costs a queue, and
+        class placement keeps a tenant on one half anyway.  Co-resident
+        contexts (``spatial=False``) always get the whole GPU."""
         import torch
 
         from ..ops import kernels as K
         parts = self.owned() if owned is None else owned
         if not parts:
             return torch.cuda.current_stream()
-        if self.spatial:
-            key = tuple(parts)
-        else:
-            key = tuple(sorted({(x, h) for (x, _) in parts for h in (0, 1)}))
-        s = self._streams.get(key)
+        halves = tuple(sorted({c for (_, c) in parts})) if self.spatial else (0, 1)
+        s = self._streams.get(halves)
         if s is None:
-            h = K.cumask_stream(half_cu_words(list(key)), device=self.gpu)
+            key = [(x, h) for x in range(XCDS) for h in halves]
+            h = K.cumask_stream(half_cu_words(key), device=self.gpu)
             s = torch.cuda.ExternalStream(h)
-            self._streams[key] = s
+            self._streams[halves] = s
         return s
 
     @contextlib.contextmanager
