@@ -745,6 +745,14 @@ class CreditScheduler : public Scheduler {
         if (hot) E.perfc.incr(PC_vcpu_hot);
         if (soft_pass && !v.soft.empty() && !v.soft.test(cpu)) continue;
         if (xgang(v, E.now()) == 2) continue;
+        // A slot just sent to its class home is not stolen back across classes
+        // for a while: every class migration briefly leaves the partition it
+        // came from idle, and that partition would otherwise take the slot
+        // straight back (the cache-hot guard of Xen's migration_delay, applied
+        // to class placement).
+        if (!soft_pass && !v.soft.empty() && !v.soft.test(cpu) &&
+            E.now() - v.homed_at < std::max<int64_t>(1000000, 4 * (int64_t)ratelimit_us_ * 1000))
+          continue;
         if (!v.is_running && !hot && v.affinity.test(cpu)) {
           s.stats.migrate_q++;
           E.perfc.incr(PC_migrate_queued);

@@ -557,9 +557,10 @@ void Engine::vcpu_migrate(Slot& v) {
   if (pl->cpus.empty()) return;
   if (!pl->cpus.test(v.processor)) v.processor = pl->cpus.first();
   int nc;
-  if (v.home >= 0 && pl->cpus.test(v.home) && v.affinity.test(v.home))
+  if (v.home >= 0 && pl->cpus.test(v.home) && v.affinity.test(v.home)) {
     nc = v.home;  // class placement spreads a tenant's slots one per partition
-  else
+    v.homed_at = now();
+  } else
     nc = S->pick_cpu(v);
   v.home = -1;
   v.processor = nc;

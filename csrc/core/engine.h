@@ -54,6 +54,7 @@ struct Slot {  // struct vcpu
   int processor = 0;
   int home = -1;        // one-shot placement hint for the next migration
   int class_home = -1;  // partition of this slot within its contention class
+  int64_t homed_at = INT64_MIN / 2;  // last migration to class_home (steal guard)
   Mask affinity;        // hard affinity (vcpu-pin)
   Mask soft;            // soft affinity (contention class); empty = none
   uint32_t pause_flags = 0;

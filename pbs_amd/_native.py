@@ -207,6 +207,7 @@ def _bind_ipc(lib):
     P(lib, "gpbs_ctl_read", C.c_int, C.c_void_p, C.c_int, C.POINTER(u32), C.POINTER(u64), C.POINTER(u32),
       C.POINTER(i32), C.POINTER(i32), C.POINTER(u32))
     P(lib, "gpbs_gang_set", C.c_int, C.c_void_p, C.c_int, C.c_int, i64)
+    P(lib, "gpbs_tenant_class", C.c_int, C.c_void_p, C.c_int)
     P(lib, "gpbs_fault_set", C.c_int, C.c_void_p, C.c_char_p)
     P(lib, "gpbs_fault_hits", C.c_int, C.c_void_p, C.POINTER(u64), C.c_int)
     P(lib, "gpbs_ctl_report", C.c_int, C.c_void_p, C.c_int, u64, u32, u32)

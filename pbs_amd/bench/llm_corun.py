@@ -60,6 +60,7 @@ def _tenant(kind: str, seconds: float, warmup: float, socket: Optional[str], q, 
     torch.cuda.synchronize()
     start_evt.wait()
     lat = []
+    halves: Dict[str, int] = {}
     t_warm = time.monotonic() + warmup
     t_end = t_warm + seconds
     n = 0
@@ -70,6 +71,8 @@ def _tenant(kind: str, seconds: float, warmup: float, socket: Optional[str], q, 
         t0 = time.perf_counter()
         if t is not None:
             with t.slice(timeout_s=30.0):
+                key = ",".join(str(h) for h in sorted({c for (_, c) in t.owned()}))
+                halves[key] = halves.get(key, 0) + 1
                 unit()
                 torch.cuda.current_stream().synchronize()
             t.account(flops=flops, bytes_moved=bytes_, busy_ns=int((time.perf_counter() - t0) * 1e9))
@@ -81,11 +84,11 @@ def _tenant(kind: str, seconds: float, warmup: float, socket: Optional[str], q, 
             lat.append(dt)
             n += 1
     if t is not None:
-        t.close()
+        t.close(destroy=False)  # keep it registered for the daemon's dump
     span = sum(lat)
     q.put({"kind": kind, "units": n, "tokens_per_s": n * per_unit_tokens / span if span else 0.0,
            "p50_ms": 1e3 * statistics.median(lat) if lat else 0.0,
-           "p99_ms": 1e3 * sorted(lat)[int(0.99 * (len(lat) - 1))] if lat else 0.0})
+           "p99_ms": 1e3 * sorted(lat)[int(0.99 * (len(lat) - 1))] if lat else 0.0, "halves": halves})
 
 
 def run(policy: str, kinds, args: dict, seconds: float, warmup: float) -> Dict[str, dict]:
@@ -112,7 +115,11 @@ def run(policy: str, kinds, args: dict, seconds: float, warmup: float) -> Dict[s
         for p in ps:
             p.join(timeout=120)
         if daemon is not None:
-            out["_engine"] = {"z": daemon.engine.debug_keys("z")[-2000:], "perfc": {
+            e = daemon.engine
+            out["_engine"] = {"z": e.debug_keys("z")[-3000:], "tenants": {
+                e.tenant_info(t).name: {"tslice_us": e.tenant_info(t).tslice_us, "phase": e.tenant_info(t).phase,
+                                        "class": e.lib.gpbs_tenant_class(e.h, t), "run_ns": e.tenant_info(t).run_ns}
+                for t in e.tenants()}, "perfc": {
                 k: v for k, v in daemon.engine.perfc().items() if v and k in ("sched_ctx", "metric_tick",
                                                                               "report_rx", "adapt_inc",
                                                                               "adapt_dec")}}

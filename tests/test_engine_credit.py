@@ -429,3 +429,21 @@ def test_atc_places_slots_least_loaded_and_apart():
         other = procs[1 - k]
         assert other not in aff and procs[k] in aff, (k, aff)
     assert e.check() == ""
+
+
+def test_class_placement_is_not_undone_by_cross_class_steals():
+    """Regression: sending a running slot to its class home briefly idles the
+    partition it left, which used to steal it straight back (a cascade that
+    left both tenants spread over both halves of every XCD)."""
+    parts = [(0, x, c) for x in range(8) for c in range(2)]
+    e = Engine(sim_clock=True, partitions=parts, coschedule=3, class_period_us=2000, quantum_align_us=0)
+    e.tenant_create("Domain-0", nslots=1)
+    mem = e.tenant_create("infer", nslots=8)
+    comp = e.tenant_create("train", nslots=8)
+    e.wake(mem)
+    e.wake(comp)
+    for _ in range(300):
+        _feed(e, {mem: (100, 100), comp: (1000, 1)}, 100)
+    assert sorted(_procs(e, mem)) == list(range(1, 16, 2)), _procs(e, mem)
+    assert sorted(_procs(e, comp)) == list(range(0, 16, 2)), _procs(e, comp)
+    assert e.check() == ""
