@@ -11,6 +11,7 @@
 // under one engine mutex; wake-ups raise softirqs that are processed before
 // the call returns, so a wake has µs latency without a context switch.
 #pragma once
+#include <atomic>
 #include <condition_variable>
 #include <cstdint>
 #include <functional>
@@ -311,7 +312,7 @@ class Engine {
   std::thread thread_;
   std::condition_variable_any cv_;
   bool running_ = false;
-  bool kicked_ = false;
+  std::atomic<bool> kicked_{false};  // read lock-free by the final-approach spin
   int hb_timer_ = -1;
   int class_timer_ = -1;
   void loop();

@@ -44,13 +44,15 @@ struct Report {
 
 struct alignas(64) Page {
   // ---- scheduler -> tenant (seqlock: seq odd while writing)
+  // Payload words are relaxed atomics: the seqlock orders them, the atomics
+  // make the concurrent (retried) reads well-defined.
   std::atomic<uint32_t> seq;
-  uint32_t gate;        // 1: may launch, 0: gated (no partition / parked / paused)
-  uint64_t mask[2];     // partitions currently running the tenant (bit = partition id, < 128)
-  uint32_t quantum_us;
-  int32_t priority;     // stream priority hint: 1 high (BOOST), 0 normal
-  int32_t tenant_id;    // engine tenant id (-1: unused page)
-  uint32_t epoch;
+  std::atomic<uint32_t> gate;        // 1: may launch, 0: gated (no partition / parked / paused)
+  std::atomic<uint64_t> mask[2];     // partitions currently running the tenant (bit = partition id, < 128)
+  std::atomic<uint32_t> quantum_us;
+  std::atomic<int32_t> priority;     // stream priority hint: 1 high (BOOST), 0 normal
+  std::atomic<int32_t> tenant_id;    // engine tenant id (-1: unused page)
+  std::atomic<uint32_t> epoch;
   uint8_t pad0[64 - 40];
   // ---- tenant -> scheduler
   std::atomic<uint64_t> heartbeat_ns;
@@ -91,6 +93,7 @@ struct Ctl {
   std::thread th;
   std::atomic<bool> stop{false};
   std::mutex mu;
+  std::mutex pub_mu;  // one seqlock writer at a time (flush vs. assign/publish)
   uint32_t epoch = 0;
 };
 
@@ -149,7 +152,7 @@ Ctl* map_region(const char* name, int ntenants, bool create) {
     c->hdr->version = kVersion;
     c->hdr->ntenants = (uint32_t)ntenants;
     c->hdr->page_size = 4096;
-    for (int t = 0; t < ntenants; ++t) c->pages[t].tenant_id = -1;
+    for (int t = 0; t < ntenants; ++t) c->pages[t].tenant_id.store(-1, std::memory_order_relaxed);
   } else if (c->hdr->magic != kMagic || c->hdr->version != kVersion) {
     munmap(p, size);
     close(fd);
@@ -162,16 +165,16 @@ Ctl* map_region(const char* name, int ntenants, bool create) {
 void publish_page(Page* pg, uint32_t gate, const uint64_t* mask, uint32_t quantum, int32_t prio, int32_t tid,
                   uint32_t epoch) {
   uint32_t s = pg->seq.load(std::memory_order_relaxed);
-  const uint32_t old_gate = pg->gate;
+  const uint32_t old_gate = pg->gate.load(std::memory_order_relaxed);
   pg->seq.store(s + 1, std::memory_order_relaxed);
   std::atomic_thread_fence(std::memory_order_release);
-  pg->gate = gate;
-  pg->mask[0] = mask[0];
-  pg->mask[1] = mask[1];
-  pg->quantum_us = quantum;
-  pg->priority = prio;
-  pg->tenant_id = tid;
-  pg->epoch = epoch;
+  pg->gate.store(gate, std::memory_order_relaxed);
+  pg->mask[0].store(mask[0], std::memory_order_relaxed);
+  pg->mask[1].store(mask[1], std::memory_order_relaxed);
+  pg->quantum_us.store(quantum, std::memory_order_relaxed);
+  pg->priority.store(prio, std::memory_order_relaxed);
+  pg->tenant_id.store(tid, std::memory_order_relaxed);
+  pg->epoch.store(epoch, std::memory_order_relaxed);
   std::atomic_thread_fence(std::memory_order_release);
   pg->seq.store(s + 2, std::memory_order_release);
   if (gate != old_gate || gate) {
@@ -195,14 +198,15 @@ void br_on_switch(void* user, int part, int prev, int next, int slot, int32_t q,
 void br_on_flush(void* user, int64_t now) {
   Ctl* c = (Ctl*)user;
   if (c->chained.on_flush) c->chained.on_flush(c->chained.user, now);
+  std::lock_guard<std::mutex> g(c->pub_mu);
   c->epoch++;
   for (uint32_t i = 0; i < c->hdr->ntenants; ++i) {
     Page* pg = &c->pages[i];
-    const int tid = pg->tenant_id;
+    const int tid = pg->tenant_id.load(std::memory_order_relaxed);
     if (tid < 0 || tid >= (int)c->pend_mask.size() / 2) continue;
     const uint64_t m[2] = {c->pend_mask[2 * tid], c->pend_mask[2 * tid + 1]};
-    if (m[0] == pg->mask[0] && m[1] == pg->mask[1]) continue;
-    publish_page(pg, (m[0] | m[1]) ? 1u : 0u, m, pg->quantum_us, pg->priority, tid, c->epoch);
+    if (m[0] == pg->mask[0].load(std::memory_order_relaxed) && m[1] == pg->mask[1].load(std::memory_order_relaxed)) continue;
+    publish_page(pg, (m[0] | m[1]) ? 1u : 0u, m, pg->quantum_us.load(std::memory_order_relaxed), pg->priority.load(std::memory_order_relaxed), tid, c->epoch);
   }
 }
 
@@ -216,7 +220,7 @@ void bridge_loop(Ctl* c) {
   while (!c->stop.load(std::memory_order_acquire)) {
     for (uint32_t i = 0; i < c->hdr->ntenants; ++i) {
       Page* pg = &c->pages[i];
-      const int tid = pg->tenant_id;
+      const int tid = pg->tenant_id.load(std::memory_order_acquire);
       if (tid < 0) continue;
       // work state -> wake/block (vcpu_unblock / do_block)
       const uint32_t w = pg->has_work.load(std::memory_order_acquire);
@@ -294,6 +298,7 @@ void gpbs_ctl_publish(void* h, int t, uint32_t gate, uint64_t mask, uint32_t qua
   Page* pg = page(h, t);
   if (!pg) return;
   const uint64_t m[2] = {mask, 0};
+  std::lock_guard<std::mutex> g(((Ctl*)h)->pub_mu);
   publish_page(pg, gate, m, quantum_us, prio, tid, epoch);
 }
 
@@ -309,12 +314,12 @@ int gpbs_ctl_read(void* h, int t, uint32_t* gate, uint64_t* mask, uint32_t* quan
       ++retries;
       continue;
     }
-    const uint32_t g = pg->gate;
-    const uint64_t m = pg->mask[0];
-    const uint32_t q = pg->quantum_us;
-    const int32_t p = pg->priority;
-    const int32_t i = pg->tenant_id;
-    const uint32_t e = pg->epoch;
+    const uint32_t g = pg->gate.load(std::memory_order_relaxed);
+    const uint64_t m = pg->mask[0].load(std::memory_order_relaxed);
+    const uint32_t q = pg->quantum_us.load(std::memory_order_relaxed);
+    const int32_t p = pg->priority.load(std::memory_order_relaxed);
+    const int32_t i = pg->tenant_id.load(std::memory_order_relaxed);
+    const uint32_t e = pg->epoch.load(std::memory_order_relaxed);
     std::atomic_thread_fence(std::memory_order_acquire);
     if (pg->seq.load(std::memory_order_relaxed) == s0) {
       if (gate) *gate = g;
@@ -420,9 +425,9 @@ int gpbs_ctl_read_mask(void* h, int t, uint64_t* mask2, uint32_t* epoch) {
   for (;;) {
     const uint32_t s0 = pg->seq.load(std::memory_order_acquire);
     if (s0 & 1) continue;
-    const uint32_t g = pg->gate;
-    const uint64_t m0 = pg->mask[0], m1 = pg->mask[1];
-    const uint32_t e = pg->epoch;
+    const uint32_t g = pg->gate.load(std::memory_order_relaxed);
+    const uint64_t m0 = pg->mask[0].load(std::memory_order_relaxed), m1 = pg->mask[1].load(std::memory_order_relaxed);
+    const uint32_t e = pg->epoch.load(std::memory_order_relaxed);
     std::atomic_thread_fence(std::memory_order_acquire);
     if (pg->seq.load(std::memory_order_relaxed) == s0) {
       if (mask2) {
@@ -476,6 +481,7 @@ int gpbs_ctl_assign(void* h, int t, int tid) {
   Page* pg = page(h, t);
   if (!pg) return -22;
   const uint64_t m[2] = {0, 0};
+  std::lock_guard<std::mutex> g(((Ctl*)h)->pub_mu);
   publish_page(pg, 0, m, 0, 0, tid, 0);
   return 0;
 }

@@ -103,7 +103,9 @@ def _proto(lib, name, res, *args):
 
 
 def core_path():
-    return os.path.join(LIBDIR, "libgpbs.so")
+    """GPBS_CORE_LIB selects another build of the core (e.g. the ASan/TSan
+    builds of ``python -m pbs_amd.build --sanitize=address``)."""
+    return os.environ.get("GPBS_CORE_LIB") or os.path.join(LIBDIR, "libgpbs.so")
 
 
 def hip_path():
@@ -117,7 +119,7 @@ def load_core(build_if_missing=True):
         if _core is not None:
             return _core
         p = core_path()
-        if build_if_missing:
+        if build_if_missing and not os.environ.get("GPBS_CORE_LIB"):
             from . import build
             build.build_core()
         lib = C.CDLL(p, mode=C.RTLD_GLOBAL)

@@ -1,0 +1,89 @@
+"""Host-side race/memory checking (S12, the reference's debug=y latch and
+lockdep analog): the native engine built with AddressSanitizer and with
+ThreadSanitizer runs a credit workload -- including the real-time dispatcher
+thread against concurrent API calls and the control-page bridge -- with no
+sanitizer report.  CPU only; GPU sanitizers are not used."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+from pbs_amd import build
+
+WORKLOAD = r"""
+import os, threading, time
+from pbs_amd.core.engine import Engine
+# simulated clock: credit, PBS adaptation, pools, pause, pin, trace, dumps
+e = Engine(sim_clock=True, partitions=[(0, x, c) for x in range(4) for c in range(2)], coschedule=3)
+e.tenant_create("Domain-0", nslots=1)
+a = e.tenant_create("a", nslots=4); b = e.tenant_create("b", nslots=4, weight=512, cap=300)
+e.wake(a); e.wake(b)
+for i in range(2000):
+    e.advance(e.now() + 50_000)
+    if i % 100 == 0:
+        e.pause(a); e.advance(e.now() + 10_000); e.unpause(a)
+        e.pin(b, i % 4, [i % 8, (i + 3) % 8])
+e.debug_keys("rqz"); e.trace(from_start=True)
+assert e.check() == "", e.check()
+e.close()
+# real clock: dispatcher thread vs. concurrent wake/block/adjust from 4 threads
+r = Engine(partitions=[(0, x) for x in range(8)])
+r.tenant_create("Domain-0", nslots=1)
+ts = [r.tenant_create(f"t{i}", nslots=4) for i in range(4)]
+r.start()
+def hammer(t):
+    for k in range(300):
+        r.wake(t); r.block(t) if k % 3 == 0 else None
+        r.sched_credit_set(t, weight=128 + k % 512)
+        r.tenant_info(t)
+th = [threading.Thread(target=hammer, args=(t,)) for t in ts]
+[x.start() for x in th]; [x.join() for x in th]
+# control-page bridge thread vs. a tenant writing its page
+from pbs_amd import _native as N
+import ctypes as C
+lib = N.load_core()
+ctl = C.c_void_p(lib.gpbs_ctl_create(b"san-%d" % os.getpid(), 4))
+lib.gpbs_ctl_bind(ctl, r.h)
+lib.gpbs_ctl_assign(ctl, 0, ts[0])
+c4 = (C.c_uint64 * 4)(1, 2, 3, 4)
+for k in range(400):
+    lib.gpbs_ctl_set_work(ctl, 0, k % 2)
+    lib.gpbs_ctl_report(ctl, 0, 1000 + k, 1 + k % 3, 0)
+    lib.gpbs_ctl_heartbeat(ctl, 0, k, k)
+    c4[0] += 1000; lib.gpbs_ctl_set_counters(ctl, 0, c4)
+    lib.gpbs_ctl_wait_gate(ctl, 0, 10000)
+time.sleep(0.05)
+lib.gpbs_ctl_close(ctl, 1)
+r.stop(); r.close()
+print("OK")
+"""
+
+
+def _run(kind):
+    lib = build.build_core(sanitize=kind)
+    rt = subprocess.run(["g++", f"-print-file-name=lib{'a' if kind == 'address' else 't'}san.so"],
+                        capture_output=True, text=True).stdout.strip()
+    if not os.path.exists(rt):
+        pytest.skip(f"lib{kind} runtime not found")
+    env = dict(os.environ, GPBS_CORE_LIB=lib, LD_PRELOAD=rt, ASAN_OPTIONS="detect_leaks=0",
+               TSAN_OPTIONS="report_signal_unsafe=0 halt_on_error=1")
+    env.pop("GPBS_FAULT", None)
+    out = subprocess.run([sys.executable, "-c", WORKLOAD], env=env, capture_output=True, text=True, timeout=600,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    return out
+
+
+def test_engine_under_address_sanitizer():
+    out = _run("address")
+    assert "ERROR: AddressSanitizer" not in out.stderr, out.stderr[-4000:]
+    assert out.returncode == 0 and "OK" in out.stdout, out.stderr[-4000:]
+
+
+def test_engine_under_thread_sanitizer():
+    out = _run("thread")
+    # python itself is not instrumented: only reports that involve libgpbs matter
+    reports = [blk for blk in out.stderr.split("==================") if "WARNING: ThreadSanitizer" in blk]
+    ours = [blk for blk in reports if "libgpbs" in blk]
+    assert not ours, ours[0][-4000:]
+    assert "OK" in out.stdout, out.stderr[-4000:]
