@@ -249,17 +249,32 @@ __global__ __launch_bounds__(GNT, 2) void k_gemm_bf16_tn(const u16* __restrict__
 // rows, one logical chunk) covers all 16 slots of a 256-B bank row.
 constexpr int G2_BM = 256, G2_BK = 64, G2_NT = 512;
 constexpr u32 kGemmXRange = 1u << 16;  // mode bit: XCD-range tile queues (grab_unit_x)
-// host: bit 0 = XCD-range tile queues.  Off by default: an interleaved A/B in
-// one process measured the plain queue faster at 4096^3 (1006 vs 937 TF/s,
-// profiles/kbench_r1.jsonl) -- dispatch already deals consecutive tiles
-// round-robin over the XCDs, which gives each XCD two B panels shared 16 ways.
-static int g_gemm_opts = 0;
+// host: bit 0 = XCD-range tile queues, bit 1 = DEEP prefetch variant, bit 2 =
+// staggered wave groups.  Default = staggered, plain queue: interleaved A/B
+// in one process at 4096^3 (profiles/kbench_r1.jsonl) measured staggered
+// 1155 TF/s vs 1035 unstaggered, deep prefetch 1036 (no gain: the lead was
+// not the limit; MFMA busy was 41 % with the groups in lock-step), XCD-range
+// queue 946 (dispatch already deals consecutive tiles round-robin over the
+// XCDs, giving each XCD two B panels shared 16 ways).
+static int g_gemm_opts = 4;
 constexpr int kG2Half = 128 * 128;           // bytes per half-tile
 constexpr int kG2Buf = 4 * kG2Half;          // A0 A1 B0 B1
 constexpr int kG2Lds = 2 * kG2Buf;           // 128 KiB
 
 __device__ __forceinline__ int g2_swz(int r) { return (r >> 1) & 7; }
 
+// DEEP = 2 variant (staggered): the wr = 1 wave group runs one barrier (half
+// a phase) behind wr = 0, so on every SIMD one wave's ds_reads overlap the
+// other's MFMA cluster.  With the groups offset, a buffer half is restaged
+// only two phases after its last read, and a staged tile is read only after
+// a barrier both groups passed after their counted wait.  Staging per K-tile
+// t: (t-1,k3) both B halves of t+1, (t,k0) A-half0 of t+1, (t,k1) A-half1
+// of t+1, (t,k3) both B halves of t+2 then vmcnt(4) (retires tile t+1).
+// DEEP = 1 variant: all four halves of K-tile t+2 are issued in k2 (B halves)
+// and k3 (A halves) -- the earliest the WAR rule allows -- and the k3 wait is
+// vmcnt(8), so a whole K-tile stays in flight for four phases (DEEP = 0: one
+// half per phase, vmcnt(4), lead 2-6 phases).
+template <int DEEP>
 __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restrict__ A, const u16* __restrict__ Bt,
                                                              u16* __restrict__ C, int M, int N, int K, WorkQueue* q,
                                                              const PartTable* table, u32 mode, u32 me, u64* cnt,
@@ -318,11 +333,22 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restr
 
     // Prologue: all of tile 0, the first two halves of tile 1.
     stage(1, 0, 0); stage(0, 0, 0); stage(1, 1, 0); stage(0, 1, 0);
-    stage(1, 0, 1); stage(0, 0, 1);
-    if (nt > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (DEEP == 2) {
+      stage(1, 0, 1); stage(1, 1, 1);
+      if (nt > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (DEEP) {
+      stage(1, 0, 1); stage(1, 1, 1); stage(0, 0, 1); stage(0, 1, 1);
+      if (nt > 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      stage(1, 0, 1); stage(0, 0, 1);
+      if (nt > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_s_barrier();
 
+    if (DEEP == 2 && wr == 1) __builtin_amdgcn_s_barrier();  // start half a phase behind
     const int bh = wc >> 1;          // B half this wave reads
     const int bc = (wc & 1) * 64;    // its 64 columns within the half
     bf16x8 a[4][2], b0[2][2], b1[2][2];
@@ -338,7 +364,8 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restr
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int s = 0; s < 2; ++s) a[i][s] = frag(buf, 0, wr, i * 16, s);
-      stage(1, 1, t + 1);
+      if (DEEP == 0) stage(1, 1, t + 1);
+      if (DEEP == 2) stage(0, 0, t + 1);
       __builtin_amdgcn_s_barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_setprio(1);
@@ -356,7 +383,7 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restr
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int s = 0; s < 2; ++s) b1[j][s] = frag(buf, 1, bh, bc + 32 + j * 16, s);
-      stage(0, 1, t + 1);
+      if (DEEP == 0 || DEEP == 2) stage(0, 1, t + 1);
       __builtin_amdgcn_s_barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_setprio(1);
@@ -374,7 +401,8 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restr
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int s = 0; s < 2; ++s) a[i][s] = frag(buf, 0, wr, 64 + i * 16, s);
-      stage(1, 0, t + 2);
+      if (DEEP != 2) stage(1, 0, t + 2);
+      if (DEEP == 1) stage(1, 1, t + 2);
       __builtin_amdgcn_s_barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_setprio(1);
@@ -388,9 +416,21 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restr
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_s_barrier();
       // ---- k3: quadrant (mi 1, ni 0); retire tile t+1
-      stage(0, 0, t + 2);
-      if (t + 2 < nt) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (DEEP == 2) {
+        stage(1, 0, t + 2);
+        stage(1, 1, t + 2);
+        if (t + 2 < nt) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else if (DEEP) {
+        stage(0, 0, t + 2);
+        stage(0, 1, t + 2);
+        if (t + 2 < nt) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {
+        stage(0, 0, t + 2);
+        if (t + 2 < nt) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -403,6 +443,7 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restr
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_s_barrier();
     }
+    if (DEEP == 2 && wr == 0) __builtin_amdgcn_s_barrier();  // re-align the groups
     // Epilogue: mfma(B, A) holds C^T per 16x16 block -- lane owns
     // C[m = .. + l16][n = .. + 4 lq + r], r = 0..3: one 8-byte store.
 #pragma unroll
@@ -633,7 +674,8 @@ int gpbs_hip_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int
     const u32 refs = (u32)(((u64)2 * G2_BM * K * 2) / 128);
     const u32 miss = (u32)((((u64)M + N) * K * 2 / 128) / ntiles + (u64)G2_BM * G2_BM * 2 / 128);
     const u32 m2 = mode | ((g_gemm_opts & 1) ? kGemmXRange : 0u);
-    hipLaunchKernelGGL(k_gemm256_bf16_tn, dim3(grid), dim3(G2_NT), 0, s, (const u16*)A, (const u16*)Bt, (u16*)C, M, N,
+    auto kern = (g_gemm_opts & 4) ? k_gemm256_bf16_tn<2> : (g_gemm_opts & 2) ? k_gemm256_bf16_tn<1> : k_gemm256_bf16_tn<0>;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(G2_NT), 0, s, (const u16*)A, (const u16*)Bt, (u16*)C, M, N,
                        K, (WorkQueue*)q, (const PartTable*)table, m2, me, (u64*)cnt, inst, refs, miss, (u32*)status);
     return hipGetLastError() == hipSuccess ? 0 : -5;
   }

@@ -57,16 +57,17 @@ def main():
     Cm = torch.empty(n, n, device=dev, dtype=torch.bfloat16)
     # A/B of the tile queue (plain vs XCD-range), interleaved rounds in one
     # process (cross-box timings are not comparable: DVFS).
-    ab = {0: [], 1: []}
+    names = {0: "plain-queue", 1: "xcd-range", 2: "deep-prefetch", 4: "staggered-groups"}
+    ab = {k: [] for k in names}
     for _ in range(5):
-        for opt in (0, 1):
+        for opt in names:
             L.gpbs_hip_set_gemm_opts(opt)
             ab[opt].append(timed(lambda: L.gpbs_hip_gemm_bf16(K._ptr(A), K._ptr(B), K._ptr(Cm), n, n, n, K._ptr(q),
                                                               None, 0, 0, None, None, 0, s), args.iters, zero))
-    L.gpbs_hip_set_gemm_opts(0)
+    L.gpbs_hip_set_gemm_opts(4)
     for opt, v in ab.items():
         ms = sorted(v)[len(v) // 2]
-        out.append({"kernel": "gemm_bf16", "variant": "xcd-range" if opt else "plain-queue", "shape": [n, n, n],
+        out.append({"kernel": "gemm_bf16", "variant": names[opt], "shape": [n, n, n],
                     "ms": ms, "tflops": 2 * n ** 3 / ms / 1e9, "min_ms": min(v)})
     ms = timed(lambda: torch.mm(A, B.t(), out=Cm), args.iters)
     out.append({"kernel": "torch.mm", "shape": [n, n, n], "ms": ms, "tflops": 2 * n ** 3 / ms / 1e9})

@@ -147,3 +147,22 @@ def test_device_adapt_bit_exact_vs_host():
     for k in range(n):
         ref = bytes(C.string_at(C.byref(host[k]), C.sizeof(N.AdaptState)))
         assert bytes(got[k].numpy().tobytes()) == ref, k
+
+
+@pytest.mark.parametrize("opts", [0, 1, 2, 3, 4, 5])
+def test_gemm256_variants_match_reference(opts):
+    """Every 256x256 schedule variant (plain / XCD-range tile queue x one-half-
+    per-phase / deep prefetch) is exact against fp32 on prologue/tail shapes."""
+    L = K.lib()
+    old = L.gpbs_hip_set_gemm_opts(opts)
+    try:
+        for M, Nn, Kd in ((256, 256, 64), (512, 256, 128), (256, 512, 192), (1024, 768, 1024)):
+            g = torch.Generator(device="cuda").manual_seed(M * 7 + Kd)
+            A = torch.randn(M, Kd, device="cuda", dtype=torch.bfloat16, generator=g)
+            B = torch.randn(Nn, Kd, device="cuda", dtype=torch.bfloat16, generator=g)
+            out = K.gemm_bf16(A, B)
+            ref = A.float() @ B.float().t()
+            err = (out.float() - ref).abs().max().item()
+            assert err < 2e-2 * ref.abs().max().item() + 1e-2, (opts, M, Nn, Kd, err)
+    finally:
+        L.gpbs_hip_set_gemm_opts(old)
