@@ -37,6 +37,9 @@ def main():
     ap.add_argument("--target-ms", type=float, default=30.0)
     ap.add_argument("--table", default="host", choices=["host", "device"])
     ap.add_argument("--out", default="")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="multi-rank control-flow rehearsal on ONE GPU: every rank on cuda:0, gloo for the default "
+                         "group and the all-reduce tenant (CPU tensors); numbers are not a measurement")
     ap.add_argument("--mix", default="4mix", choices=["4mix", "gemm2"],
                     help="4mix: BASELINE config #3/#4 (headline); gemm2: config #2 (two 4096^2 GEMM tenants)")
     args = ap.parse_args()
@@ -48,15 +51,20 @@ def main():
     if args.gpus > 1 and world == 1:
         print("bench.py: --gpus > 1 must be launched with torch.distributed.run (one rank per GPU)", file=sys.stderr)
         sys.exit(2)
+    if args.rehearse:
+        local = 0
     torch.cuda.set_device(local)
     groups = {}
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        if args.rehearse:
+            dist.init_process_group(backend="gloo")
+        else:
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
         groups["ctrl"] = dist.new_group(backend="gloo")
         groups["gang"] = dist.new_group(backend="gloo")  # cross-GPU gang epochs (own thread)
-        groups["coll"] = dist.new_group(backend="nccl")
+        groups["coll"] = dist.new_group(backend="gloo" if args.rehearse else "nccl")
 
     from pbs_amd import build
     if rank == 0:  # one builder per node; the others wait (no concurrent relink)
@@ -70,8 +78,10 @@ def main():
         pols = pols + ("gpbs",)
     cfg = CorunConfig(steps=args.steps, warmup=args.warmup, target_ms=args.target_ms, policies=pols,
                       table_mode=args.table, mix=args.mix)
+    if args.rehearse:
+        cfg.coll_bytes = 4 << 20  # CPU gloo all-reduce stand-in
     log = (lambda *a: print(*a, file=sys.stderr, flush=True))
-    c = Corun(cfg, rank=rank, world=world, device=local, groups=groups, log=log)
+    c = Corun(cfg, rank=rank, world=world, device=local, groups=groups, log=log, coll_on_cpu=args.rehearse)
     c.calibrate()
     results = {}
     for p in pols:

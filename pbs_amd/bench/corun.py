@@ -100,10 +100,12 @@ class CollTenant:
     process group and stream, launch-gated on XCD ownership (RCCL kernels
     themselves are not CU-confined)."""
 
-    def __init__(self, ctx: GpuContext, tenant: int, nbytes: int, group):
+    def __init__(self, ctx: GpuContext, tenant: int, nbytes: int, group, on_cpu: bool = False):
         self.ctx, self.tenant, self.group = ctx, tenant, group
         self.engine: Optional[Engine] = None
-        self.buf = torch.randn(nbytes // 2, device="cuda", dtype=torch.bfloat16)
+        # on_cpu: bench --rehearse (gloo stand-in for RCCL, all ranks on one GPU)
+        self.buf = torch.randn(nbytes // 2, device="cpu" if on_cpu else "cuda",
+                               dtype=torch.float32 if on_cpu else torch.bfloat16)
         self.stream = torch.cuda.Stream()
         self.gate = False
         self.units_done = 0
@@ -137,8 +139,10 @@ def _pct(xs, q):
 
 
 class Corun:
-    def __init__(self, cfg: CorunConfig, rank: int = 0, world: int = 1, device: int = 0, groups=None, log=print):
+    def __init__(self, cfg: CorunConfig, rank: int = 0, world: int = 1, device: int = 0, groups=None, log=print,
+                 coll_on_cpu: bool = False):
         self.cfg, self.rank, self.world, self.device = cfg, rank, world, device
+        self.coll_on_cpu = coll_on_cpu
         self.groups = groups or {}
         self.gang = None
         self.gang_stats: Dict[str, float] = {}
@@ -170,7 +174,7 @@ class Corun:
             return Runner(self.ctx, "stream", t, depth=cfg.depth, bytes=cfg.hbm_bytes)
         if name == "coll":
             if self.world > 1:
-                return CollTenant(self.ctx, t, cfg.coll_bytes, self.groups.get("coll"))
+                return CollTenant(self.ctx, t, cfg.coll_bytes, self.groups.get("coll"), on_cpu=self.coll_on_cpu)
             return Runner(self.ctx, "reduce", t, depth=cfg.depth, bytes=cfg.coll_bytes)
         if name == "idle":
             return Runner(self.ctx, "gemv", t, depth=1, priority=1, M=cfg.idle_rows, K=cfg.idle_rows)
