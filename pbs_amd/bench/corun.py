@@ -29,13 +29,15 @@ Policies (same tenants, same box):
           kernels exit on revoked XCDs
   gpbs-exit   two co-resident issue contexts per XCD + contention classes,
           workgroups exit on revocation, host table
-  gpbs-ctx    co-resident issue contexts, parked gating, device table
+  gpbs-spatial  spatial partitions: an XCD whose two owners are of different
+          classes is split into CU halves (shader engines 0-1 / 2-3);
+          half-masked streams
   gpbs-nogang the flagship without gang alignment of the classes
-  gpbs    PBS adaptive credit scheduler over spatial partitions: each XCD is
-          split into two CU halves (shader engines 0-1 / 2-3) that host the
-          counter-driven compute and memory classes (soft affinity, work
+  gpbs    PBS adaptive credit scheduler over two co-resident issue contexts
+          per XCD: counter-driven compute/memory classes (soft affinity, work
           conserving), gang-aligned per class, parked gating on a
-          device-resident partition table, half-masked streams (the flagship)
+          device-resident partition table (the flagship: lowest mean co-run
+          slowdown and latency-tenant delay, profiles/corun_policies_1gpu.log)
 """
 from __future__ import annotations
 
@@ -86,9 +88,9 @@ class CorunConfig:
 POLICY_ENGINES = {
     # name: (issue contexts per XCD, engine overrides on top of MI355X_PROFILE,
     #        kernel gate mode, partition-table location)
-    "gpbs": (2, {}, "park", "device,spatial"),
-    "gpbs-ctx": (2, {}, "park", "device"),
-    "gpbs-nogang": (2, {"coschedule": 2}, "park", "device,spatial"),
+    "gpbs": (2, {}, "park", "device"),
+    "gpbs-spatial": (2, {}, "park", "device,spatial"),
+    "gpbs-nogang": (2, {"coschedule": 2}, "park", "device"),
     "gpbs-exit": (2, {}, True, "host"),
     "gpbs1": (1, {"coschedule": 0}, True, "host"),
     "credit2": (2, {"sched": "credit-fixed"}, "park", "device"),
