@@ -40,6 +40,9 @@ def main():
     ap.add_argument("--rehearse", action="store_true",
                     help="multi-rank control-flow rehearsal on ONE GPU: every rank on cuda:0, gloo for the default "
                          "group and the all-reduce tenant (CPU tensors); numbers are not a measurement")
+    ap.add_argument("--counters", default="model", choices=["model", "hw"],
+                    help="PBS metric source: modeled per-tile counters, or live CDNA4 hardware counters "
+                         "(rocprofiler-sdk device counting) attributed by the model")
     ap.add_argument("--mix", default="4mix", choices=["4mix", "gemm2"],
                     help="4mix: BASELINE config #3/#4 (headline); gemm2: config #2 (two 4096^2 GEMM tenants)")
     args = ap.parse_args()
@@ -53,7 +56,17 @@ def main():
         sys.exit(2)
     if args.rehearse:
         local = 0
+    if args.counters == "hw":  # must register with rocprofiler before the HIP runtime starts
+        from pbs_amd.counters import hwc
+        if not hwc.init(gpu=local):
+            print("bench.py: hardware counter init failed", file=sys.stderr)
+            sys.exit(3)
     torch.cuda.set_device(local)
+    if args.counters == "hw":
+        torch.zeros(1, device="cuda")
+        if not hwc.start():
+            print("bench.py: hardware counter start failed", file=sys.stderr)
+            sys.exit(3)
     groups = {}
     if world > 1:
         import torch.distributed as dist
@@ -77,7 +90,7 @@ def main():
     if "gpbs" not in pols:
         pols = pols + ("gpbs",)
     cfg = CorunConfig(steps=args.steps, warmup=args.warmup, target_ms=args.target_ms, policies=pols,
-                      table_mode=args.table, mix=args.mix)
+                      table_mode=args.table, mix=args.mix, hw_counters=(args.counters == "hw"))
     if args.rehearse:
         cfg.coll_bytes = 4 << 20  # CPU gloo all-reduce stand-in
     log = (lambda *a: print(*a, file=sys.stderr, flush=True))

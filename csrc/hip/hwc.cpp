@@ -1,0 +1,194 @@
+// Live CDNA4 hardware counters for the scheduler (the Perfctr-xen vPMU
+// analog, S1/P1c/P4): rocprofiler-sdk's device counting service, sampled on
+// demand by the GPU counter backend each metric period.
+//
+// Four counters per XCD, summed over shader engines / L2 channels -- the PBS
+// event set mapped onto gfx950 (X:xen/common/sched_credit.c:1966 labels):
+//   INST_RETIRED      -> SQ_INSTS_VALU + SQ_INSTS_MFMA ... (configurable list)
+//   CPU_CLK_UNHALTED  -> SQ_BUSY_CYCLES
+//   LLC_REFERENCES    -> TCC_REQ
+//   LLC_MISSES        -> TCC_MISS
+// Values are cumulative since the context started (measured:
+// scripts/hwc_probe.hip).  gpbs_hwc_init must run before the HIP runtime
+// initialises in the process (rocprofiler_force_configure); gpbs_hwc_start
+// after the first device call.
+#include <rocprofiler-sdk/registration.h>
+#include <rocprofiler-sdk/rocprofiler.h>
+
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace {
+
+constexpr int kX = 8;  // XCDs per MI355X
+constexpr int kSlots = 4;
+
+struct Hwc {
+  rocprofiler_context_id_t ctx{};
+  std::vector<rocprofiler_agent_id_t> gpus;
+  std::vector<rocprofiler_counter_config_id_t> cfg;
+  std::map<uint64_t, int> slot_of;            // counter id -> PBS slot (0..3)
+  rocprofiler_counter_dimension_id_t xcc_dim{};
+  bool have_xcc = false;
+  std::vector<std::string> names[kSlots];
+  bool configured = false, started = false;
+  int only_gpu = -1;  // count on this GPU agent only (rank-local), -1 = all
+  std::mutex mu;
+  std::vector<rocprofiler_counter_record_t> rec;
+};
+Hwc g;
+
+rocprofiler_status_t on_agents(rocprofiler_agent_version_t, const void** agents, size_t n, void*) {
+  for (size_t i = 0; i < n; ++i) {
+    auto* a = (const rocprofiler_agent_v0_t*)agents[i];
+    if (a->type == ROCPROFILER_AGENT_TYPE_GPU) g.gpus.push_back(a->id);
+  }
+  return ROCPROFILER_STATUS_SUCCESS;
+}
+
+rocprofiler_status_t on_counters(rocprofiler_agent_id_t, rocprofiler_counter_id_t* c, size_t n, void* ud) {
+  auto* out = (std::vector<rocprofiler_counter_id_t>*)ud;
+  for (size_t i = 0; i < n; ++i) {
+    rocprofiler_counter_info_v1_t info{};
+    info.size = sizeof(info);
+    if (rocprofiler_query_counter_info(c[i], ROCPROFILER_COUNTER_INFO_VERSION_1, &info) !=
+            ROCPROFILER_STATUS_SUCCESS || !info.name)
+      continue;
+    for (int s = 0; s < kSlots; ++s)
+      for (auto& w : g.names[s])
+        if (w == info.name) {
+          out->push_back(c[i]);
+          g.slot_of[c[i].handle] = s;
+          for (uint64_t d = 0; d < info.dimensions_count; ++d)
+            if (std::strcmp(info.dimensions[d]->name, "DIMENSION_XCC") == 0) {
+              g.xcc_dim = info.dimensions[d]->id;
+              g.have_xcc = true;
+            }
+        }
+  }
+  return ROCPROFILER_STATUS_SUCCESS;
+}
+
+void set_cfg(rocprofiler_context_id_t ctx, rocprofiler_agent_id_t, rocprofiler_device_counting_agent_cb_t set,
+             void* ud) {
+  set(ctx, *(rocprofiler_counter_config_id_t*)ud);
+}
+
+int tool_init(rocprofiler_client_finalize_t, void*) {
+  if (rocprofiler_create_context(&g.ctx) != ROCPROFILER_STATUS_SUCCESS) return -1;
+  rocprofiler_query_available_agents(ROCPROFILER_AGENT_INFO_VERSION_0, on_agents, sizeof(rocprofiler_agent_v0_t),
+                                     nullptr);
+  if (g.only_gpu >= 0) {
+    if (g.only_gpu >= (int)g.gpus.size()) return -1;
+    g.gpus = {g.gpus[g.only_gpu]};  // one process per GPU: never touch a peer's counters
+  }
+  g.cfg.resize(g.gpus.size());
+  for (size_t i = 0; i < g.gpus.size(); ++i) {
+    std::vector<rocprofiler_counter_id_t> ids;
+    rocprofiler_iterate_agent_supported_counters(g.gpus[i], on_counters, &ids);
+    if (ids.empty()) continue;
+    if (rocprofiler_create_counter_config(g.gpus[i], ids.data(), ids.size(), &g.cfg[i]) !=
+        ROCPROFILER_STATUS_SUCCESS)
+      continue;
+    rocprofiler_configure_device_counting_service(g.ctx, rocprofiler_buffer_id_t{0}, g.gpus[i], set_cfg, &g.cfg[i]);
+    g.configured = true;
+  }
+  return 0;
+}
+
+void tool_fini(void*) {}
+
+rocprofiler_tool_configure_result_t* configure(uint32_t, const char*, uint32_t, rocprofiler_client_id_t* id) {
+  id->name = "gpbs-hwc";
+  static rocprofiler_tool_configure_result_t r{sizeof(rocprofiler_tool_configure_result_t), tool_init, tool_fini,
+                                               nullptr};
+  return &r;
+}
+
+void split(const char* s, std::vector<std::string>& out) {
+  out.clear();
+  std::string cur;
+  for (const char* p = s; p && *p; ++p) {
+    if (*p == '+' || *p == ',') {
+      if (!cur.empty()) out.push_back(cur);
+      cur.clear();
+    } else {
+      cur += *p;
+    }
+  }
+  if (!cur.empty()) out.push_back(cur);
+}
+
+}  // namespace
+
+extern "C" {
+
+// spec: four '|'-separated groups of '+'-joined counter names, one per PBS
+// slot; NULL = "SQ_INSTS_VALU+SQ_INSTS_SALU|SQ_BUSY_CYCLES|TCC_REQ|TCC_MISS".
+// Must precede HIP runtime initialisation.  `gpu` >= 0 restricts counting to
+// that GPU agent (agents in enumeration order; one rank per GPU).  0 on success.
+int gpbs_hwc_init_gpu(const char* spec, int gpu);
+int gpbs_hwc_init(const char* spec) { return gpbs_hwc_init_gpu(spec, -1); }
+
+int gpbs_hwc_init_gpu(const char* spec, int gpu) {
+  std::lock_guard<std::mutex> l(g.mu);
+  g.only_gpu = gpu;
+  std::string sp = spec && *spec ? spec : "SQ_INSTS_VALU+SQ_INSTS_SALU|SQ_BUSY_CYCLES|TCC_REQ|TCC_MISS";
+  size_t pos = 0;
+  for (int s = 0; s < kSlots; ++s) {
+    const size_t e = sp.find('|', pos);
+    split(sp.substr(pos, e == std::string::npos ? std::string::npos : e - pos).c_str(), g.names[s]);
+    pos = e == std::string::npos ? sp.size() : e + 1;
+  }
+  return rocprofiler_force_configure(configure) == ROCPROFILER_STATUS_SUCCESS ? 0 : -1;
+}
+
+// After the first device call (the runtime is up): start counting.
+int gpbs_hwc_start(void) {
+  std::lock_guard<std::mutex> l(g.mu);
+  if (!g.configured) return -2;
+  if (g.started) return 0;
+  if (rocprofiler_start_context(g.ctx) != ROCPROFILER_STATUS_SUCCESS) return -1;
+  g.started = true;
+  return 0;
+}
+
+int gpbs_hwc_active(void) { return g.started ? 1 : 0; }
+
+// Cumulative counters per XCD: out[xcd * 4 + slot].  Synchronous sample.
+int gpbs_hwc_sample(uint64_t* out, int nxcd) {
+  std::lock_guard<std::mutex> l(g.mu);
+  if (!g.started || !out || nxcd < kX) return -1;
+  if (g.rec.empty()) g.rec.resize(16384);
+  size_t n = g.rec.size();
+  if (rocprofiler_sample_device_counting_service(g.ctx, {}, ROCPROFILER_COUNTER_FLAG_NONE, g.rec.data(), &n) !=
+      ROCPROFILER_STATUS_SUCCESS)
+    return -1;
+  double acc[kX][kSlots] = {};
+  for (size_t i = 0; i < n; ++i) {
+    rocprofiler_counter_id_t cid{};
+    if (rocprofiler_query_record_counter_id(g.rec[i].id, &cid) != ROCPROFILER_STATUS_SUCCESS) continue;
+    auto it = g.slot_of.find(cid.handle);
+    if (it == g.slot_of.end()) continue;
+    size_t x = 0;
+    if (g.have_xcc) rocprofiler_query_record_dimension_position(g.rec[i].id, g.xcc_dim, &x);
+    if (x < (size_t)kX) acc[x][it->second] += g.rec[i].counter_value;
+  }
+  for (int x = 0; x < kX; ++x)
+    for (int s = 0; s < kSlots; ++s) out[x * kSlots + s] = (uint64_t)acc[x][s];
+  return (int)n;
+}
+
+int gpbs_hwc_stop(void) {
+  std::lock_guard<std::mutex> l(g.mu);
+  if (!g.started) return 0;
+  rocprofiler_stop_context(g.ctx);
+  g.started = false;
+  return 0;
+}
+
+}  // extern "C"

@@ -30,6 +30,8 @@ using namespace gpbs_hip;
 
 extern "C" {
 int gpbs_hip_gemm_units(int, int);
+int gpbs_hwc_sample(uint64_t* out, int nxcd);
+int gpbs_hwc_active(void);
 int gpbs_hip_gemm_bf16(const void*, const void*, void*, int, int, int, void*, const void*, unsigned, unsigned, void*,
                        void*, int, hipStream_t);
 int gpbs_hip_stream_copy(const void*, void*, unsigned long long, unsigned, void*, const void*, unsigned, unsigned,
@@ -77,6 +79,27 @@ struct GpuCtx {
   int* h_ids2 = nullptr;
   u64* h_out2 = nullptr;
   hipEvent_t red_ev = nullptr;
+  // Live hardware counters (csrc/hip/hwc.cpp): per-XCD deltas attributed to
+  // tenants in proportion to their modeled per-XCD activity.
+  // A sampler thread snapshots the model block and the hardware at one
+  // instant every period (a synchronous device-counting sample costs
+  // ~0.2 ms -- never under the engine lock); the metric tick consumes the
+  // newest snapshot pair.
+  int hwc = 0;
+  u64* h_blk = nullptr;                 // pinned landing buffer of d_cnt copies
+  std::vector<u64> snap_blk, blk_prev;  // newest published / last consumed model block
+  u64 snap_hw[kXcds * kNumPmc] = {}, hw_prev[kXcds * kNumPmc] = {};
+  uint64_t snap_seq = 0, used_seq = 0;
+  bool hw_primed = false;
+  hipEvent_t blk_ev = nullptr;
+  hipStream_t hwc_stream = nullptr;
+  std::thread hwc_th;
+  std::atomic<bool> hwc_stop{false};
+  std::mutex snap_mu;
+  int hwc_period_us = 1000;
+  int64_t hwc_ns = 0;
+  uint64_t hwc_samples = 0;
+  double hw_sum[kNumPmc] = {}, model_sum[kNumPmc] = {};  // attributed vs modeled totals
   u64 last_delta[kMaxTenants][kNumPmc];
   std::mutex mu;
   std::condition_variable cv;
@@ -152,9 +175,77 @@ void act_on_park(void*, int, int, int) {}
 // k-1 (normally long finished) and launches the next one on the high-priority
 // scheduler stream, so the engine lock is never held across a device sync.
 // Every counted event is reported exactly once, one metric period late.
+void hwc_loop(GpuCtx* c) {
+  hipSetDevice(c->device);
+  constexpr int kBlk = kMaxTenants * kXcds * kNumPmc;
+  std::vector<u64> blk(kBlk);
+  u64 hw[kXcds * kNumPmc];
+  while (!c->hwc_stop.load(std::memory_order_acquire)) {
+    const int64_t t0 = mono_ns();
+    if (hipMemcpyAsync(c->h_blk, c->d_cnt, sizeof(u64) * kBlk, hipMemcpyDeviceToHost, c->hwc_stream) != hipSuccess)
+      break;
+    hipEventRecord(c->blk_ev, c->hwc_stream);
+    const int rc = gpbs_hwc_sample(reinterpret_cast<uint64_t*>(hw), kXcds);
+    hipEventSynchronize(c->blk_ev);
+    if (rc >= 0) {
+      std::memcpy(blk.data(), c->h_blk, sizeof(u64) * kBlk);
+      std::lock_guard<std::mutex> g(c->snap_mu);
+      c->snap_blk.swap(blk);
+      std::memcpy(c->snap_hw, hw, sizeof(hw));
+      c->snap_seq++;
+      c->hwc_ns += mono_ns() - t0;
+      c->hwc_samples++;
+    }
+    const int64_t rest = (int64_t)c->hwc_period_us * 1000 - (mono_ns() - t0);
+    if (rest > 0) std::this_thread::sleep_for(std::chrono::nanoseconds(rest));
+  }
+}
+
+int hwc_tenant_deltas(GpuCtx* c, int n, const int* tenants, uint64_t* out) {
+  const int64_t t0 = mono_ns();
+  {
+    std::lock_guard<std::mutex> g(c->snap_mu);
+    if (c->snap_seq != c->used_seq && (int)c->snap_blk.size() == kMaxTenants * kXcds * kNumPmc) {
+      c->used_seq = c->snap_seq;
+      if (c->hw_primed) {
+        for (int x = 0; x < kXcds; ++x)
+          for (int k = 0; k < kNumPmc; ++k) {
+            const u64 hw_d = c->snap_hw[x * kNumPmc + k] - c->hw_prev[x * kNumPmc + k];
+            double denom = 0;
+            for (int t = 0; t < kMaxTenants; ++t) {
+              const size_t i = ((size_t)t * kXcds + x) * kNumPmc + k;
+              denom += (double)(c->snap_blk[i] - c->blk_prev[i]);
+            }
+            if (denom <= 0) continue;
+            c->hw_sum[k] += (double)hw_d;
+            c->model_sum[k] += denom;
+            for (int t = 0; t < kMaxTenants; ++t) {
+              const size_t i = ((size_t)t * kXcds + x) * kNumPmc + k;
+              const u64 md = c->snap_blk[i] - c->blk_prev[i];
+              if (md) c->last_delta[t][k] += (u64)((double)hw_d * (double)md / denom);
+            }
+          }
+      }
+      c->blk_prev = c->snap_blk;
+      std::memcpy(c->hw_prev, c->snap_hw, sizeof(c->hw_prev));
+      c->hw_primed = true;
+    }
+  }
+  for (int k = 0; k < n; ++k)
+    for (int i = 0; i < kNumPmc; ++i) {
+      const int t = tenants[k];
+      out[k * kNumPmc + i] = (t >= 0 && t < kMaxTenants) ? c->last_delta[t][i] : 0;
+      if (t >= 0 && t < kMaxTenants) c->last_delta[t][i] = 0;
+    }
+  c->metric_calls++;
+  c->metric_ns += mono_ns() - t0;
+  return 0;
+}
+
 int ctr_tenant_deltas(void* user, int n, const int* tenants, uint64_t* out) {
   GpuCtx* c = (GpuCtx*)user;
   if (n > kMaxTenants) return -22;
+  if (c->hwc) return hwc_tenant_deltas(c, n, tenants, out);
   const int64_t t0 = mono_ns();
   if (c->red_pending) {
     if (hipEventQuery(c->red_ev) == hipErrorNotReady) hipEventSynchronize(c->red_ev);
@@ -480,6 +571,11 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
             hipSuccess;
   ok = ok && hipMalloc((void**)&c->d_cnt, sizeof(u64) * kMaxTenants * kXcds * kNumPmc) == hipSuccess;
   ok = ok && hipMalloc((void**)&c->d_prev, sizeof(u64) * kMaxTenants * kXcds * kNumPmc) == hipSuccess;
+  ok = ok && hipHostMalloc((void**)&c->h_blk, sizeof(u64) * kMaxTenants * kXcds * kNumPmc, hipHostMallocDefault) ==
+                 hipSuccess;
+  ok = ok && hipEventCreateWithFlags(&c->blk_ev, hipEventDisableTiming) == hipSuccess;
+  c->blk_prev.assign((size_t)kMaxTenants * kXcds * kNumPmc, 0);
+  c->snap_blk.assign((size_t)kMaxTenants * kXcds * kNumPmc, 0);
   ok = ok && hipMemset(c->d_cnt, 0, sizeof(u64) * kMaxTenants * kXcds * kNumPmc) == hipSuccess;
   ok = ok && hipMemset(c->d_prev, 0, sizeof(u64) * kMaxTenants * kXcds * kNumPmc) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_out, sizeof(u64) * 4 * kMaxTenants, hipHostMallocMapped) == hipSuccess;
@@ -513,6 +609,10 @@ void gpbs_gpu_ctx_destroy(void* p) {
   GpuCtx* c = (GpuCtx*)p;
   if (!c) return;
   hipSetDevice(c->device);
+  if (c->hwc_th.joinable()) {  // the sampler reads d_cnt: stop it first
+    c->hwc_stop = true;
+    c->hwc_th.join();
+  }
   hipDeviceSynchronize();
   if (c->engine) {
     gpbs_set_actuator_ops(c->engine, nullptr);
@@ -523,6 +623,9 @@ void gpbs_gpu_ctx_destroy(void* p) {
   hipFree(c->d_cnt);
   hipFree(c->d_prev);
   hipHostFree(c->h_out);
+  if (c->hwc_stream) hipStreamDestroy(c->hwc_stream);
+  if (c->h_blk) hipHostFree(c->h_blk);
+  if (c->blk_ev) hipEventDestroy(c->blk_ev);
   hipHostFree(c->h_ids);
   hipHostFree(c->h_out2);
   hipHostFree(c->h_ids2);
@@ -562,6 +665,39 @@ int gpbs_gpu_set_nctx(void* p, int nctx) {
 
 // Switch between the pinned host table (0) and the device table (1).  The
 // device copy is re-synchronised before device mode takes effect.
+// Drive the scheduler with live hardware counters (gpbs_hwc_* must be
+// initialised and started); 0 falls back to the modeled counters.
+int gpbs_gpu_set_hwc(void* p, int on) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c) return -22;
+  if (on && !gpbs_hwc_active()) return -19;
+  if (c->hwc_th.joinable()) {
+    c->hwc_stop = true;
+    c->hwc_th.join();
+  }
+  std::lock_guard<std::mutex> g(c->mu);
+  c->hwc = on ? 1 : 0;
+  c->hw_primed = false;
+  c->used_seq = c->snap_seq;
+  if (on) {
+    if (!c->hwc_stream && hipStreamCreateWithFlags(&c->hwc_stream, hipStreamNonBlocking) != hipSuccess) return -5;
+    c->hwc_stop = false;
+    c->hwc_th = std::thread(hwc_loop, c);
+  }
+  return 0;
+}
+
+// hwc stats: samples, mean sample cost (ns), attributed/modeled ratio per slot.
+int gpbs_gpu_hwc_stats(void* p, uint64_t* samples, uint64_t* mean_ns, double* ratio4) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c) return -22;
+  if (samples) *samples = c->hwc_samples;
+  if (mean_ns) *mean_ns = c->hwc_samples ? (uint64_t)(c->hwc_ns / (int64_t)c->hwc_samples) : 0;
+  if (ratio4)
+    for (int k = 0; k < kNumPmc; ++k) ratio4[k] = c->model_sum[k] > 0 ? c->hw_sum[k] / c->model_sum[k] : 0.0;
+  return 0;
+}
+
 int gpbs_gpu_set_spatial(void* p, int on) {
   GpuCtx* c = (GpuCtx*)p;
   if (!c) return -22;

@@ -83,6 +83,7 @@ class CorunConfig:
     gang_epoch_ms: float = 4.0   # N > 1: cross-GPU gang window length
     gang_share: float = 0.5      # fraction of epochs that are the all-reduce tenant's
     mix: str = "4mix"
+    hw_counters: bool = False    # PBS metric from live hardware counters
 
 
 POLICY_ENGINES = {
@@ -222,6 +223,8 @@ class Corun:
             self.ctx.set_table_mode(table.split(",")[0])
             self.ctx.set_spatial("spatial" in table)
             self.ctx.attach(e, nctx=e._gpbs_nctx)
+            if self.cfg.hw_counters:
+                self.ctx.set_hwc(True)
             e.start()
             self.active_engine = e
             for r in self._natives():
@@ -399,6 +402,10 @@ class Corun:
             eng = {k: pc[k] for k in ("sched_ctx", "acct_run", "metric_tick", "adapt_inc", "adapt_dec",
                                       "adapt_rearm", "migrate_queued", "vcpu_wake_runnable", "tickle_idlers_some")}
             eng["gpu"] = self.ctx.stats()
+            if self.cfg.hw_counters:
+                eng["hwc"] = self.ctx.hwc_stats()
+            eng["miss_rate"] = {n: e.tenant_info(self.tid[n]).cache_miss_rate for n in self.tid}
+            eng["class"] = {n: e.lib.gpbs_tenant_class(e.h, self.tid[n]) for n in self.tid}
             eng["mean_tslice_us"] = {n: round(statistics.mean(q), 1) for n, q in quanta.items() if q}
             eng["run_share"] = {n: round((e.tenant_info(self.tid[n]).run_ns - run0[n]) / (wall_ms * 1e6), 3)
                                 for n in self.tid}

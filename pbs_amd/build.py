@@ -170,7 +170,8 @@ def build_hip(verbose=False):
             jobs.append(([hipcc()] + flags + lang + ["-c", s, "-o", obj], obj))
     _compile_parallel(jobs, verbose)
     _link_atomic([hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}"], target,
-                 objs + ["-L" + LIBDIR, "-lgpbs", "-Wl,-rpath,$ORIGIN", "-pthread"], verbose, deps, ARCH)
+                 objs + ["-L" + LIBDIR, "-lgpbs", "-Wl,-rpath,$ORIGIN", "-L/opt/rocm/lib", "-lrocprofiler-sdk",
+                         "-Wl,-rpath,/opt/rocm/lib", "-pthread"], verbose, deps, ARCH)
     return target
 
 

@@ -1,0 +1,51 @@
+"""Live CDNA4 hardware counters (rocprofiler-sdk device counting service,
+csrc/hip/hwc.cpp): the Perfctr-xen vPMU analog.
+
+    from pbs_amd.counters import hwc
+    hwc.init()            # BEFORE the HIP runtime initialises (first torch.cuda call)
+    torch.cuda.set_device(0)
+    hwc.start()
+    per_xcd = hwc.sample()   # 8 x (INST, BUSY_CYCLES, L2_REQ, L2_MISS), cumulative
+
+``GpuContext.set_hwc(True)`` then drives the scheduler's PBS metric with
+per-XCD hardware deltas, attributed to tenants in proportion to their
+modeled per-XCD activity.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional, Tuple
+
+from .. import _native as N
+
+DEFAULT_SPEC = "SQ_INSTS_VALU+SQ_INSTS_SALU|SQ_BUSY_CYCLES|TCC_REQ|TCC_MISS"
+XCDS = 8
+
+
+def _lib():
+    return N.load_hip(required=True)
+
+
+def init(spec: Optional[str] = None, gpu: int = -1) -> bool:
+    """Register the sampler with rocprofiler-sdk; must precede HIP init.
+    ``gpu`` >= 0 counts on that GPU agent only (one rank per GPU)."""
+    return _lib().gpbs_hwc_init_gpu((spec or DEFAULT_SPEC).encode(), int(gpu)) == 0
+
+
+def start() -> bool:
+    return _lib().gpbs_hwc_start() == 0
+
+
+def active() -> bool:
+    return bool(_lib().gpbs_hwc_active())
+
+
+def sample() -> List[Tuple[int, int, int, int]]:
+    arr = (C.c_uint64 * (XCDS * 4))()
+    if _lib().gpbs_hwc_sample(arr, XCDS) < 0:
+        raise RuntimeError("hardware counter sample failed (init/start?)")
+    return [tuple(arr[x * 4:(x + 1) * 4]) for x in range(XCDS)]
+
+
+def stop():
+    _lib().gpbs_hwc_stop()

@@ -39,6 +39,14 @@ def bind(lib):
     _p(lib, "gpbs_hip_gemv_bf16", C.c_int, vp, vp, vp, C.c_int, C.c_int, vp, vp, C.c_uint, C.c_uint, vp, vp, C.c_int,
        vp)
     _p(lib, "gpbs_hip_set_gemm_opts", C.c_int, C.c_int)
+    _p(lib, "gpbs_hwc_init", C.c_int, C.c_char_p)
+    _p(lib, "gpbs_hwc_init_gpu", C.c_int, C.c_char_p, C.c_int)
+    _p(lib, "gpbs_hwc_start", C.c_int)
+    _p(lib, "gpbs_hwc_active", C.c_int)
+    _p(lib, "gpbs_hwc_sample", C.c_int, C.POINTER(C.c_uint64), C.c_int)
+    _p(lib, "gpbs_hwc_stop", C.c_int)
+    _p(lib, "gpbs_gpu_set_hwc", C.c_int, vp, C.c_int)
+    _p(lib, "gpbs_gpu_hwc_stats", C.c_int, vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_double))
     _p(lib, "gpbs_hip_rmsnorm_bf16", C.c_int, vp, vp, vp, C.c_int, C.c_int, C.c_float, vp)
     _p(lib, "gpbs_hip_swiglu_bf16", C.c_int, vp, vp, vp, C.c_ulonglong, vp)
     _p(lib, "gpbs_hip_rope_bf16", C.c_int, vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp)

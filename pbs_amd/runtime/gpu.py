@@ -95,6 +95,20 @@ class GpuContext:
         if rc:
             raise RuntimeError("set_table_mode failed")
 
+    def set_hwc(self, on: bool):
+        """Drive the PBS metric with live hardware counters (requires
+        pbs_amd.counters.hwc.init() before HIP init, then hwc.start())."""
+        rc = self.L.gpbs_gpu_set_hwc(self.h, 1 if on else 0)
+        if rc:
+            raise RuntimeError(f"set_hwc failed ({rc}): hardware counters not initialised/started")
+
+    def hwc_stats(self):
+        n, ns = C.c_uint64(0), C.c_uint64(0)
+        r = (C.c_double * 4)()
+        self.L.gpbs_gpu_hwc_stats(self.h, C.byref(n), C.byref(ns), r)
+        return {"samples": n.value, "mean_sample_us": ns.value / 1e3,
+                "hw_over_model": [round(x, 4) for x in r]}
+
     def set_spatial(self, on: bool):
         """Spatial partitions: the two partitions of an XCD are CU halves
         (shader engines 0-1 / 2-3) -- runners launch on half-masked streams
