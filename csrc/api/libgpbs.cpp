@@ -120,6 +120,7 @@ void gpbs_boot_defaults(gpbs_boot_params_t* p) {
   p->quantum_align_us = 0;
   p->coschedule = 0;
   p->class_period_us = 2000;
+  p->boost_exclusive = 0;
   AdaptParams a;
   std::memcpy(&p->adapt, &a, sizeof(a));
   AtcParams t;

@@ -55,6 +55,7 @@ struct CSlot : SchedSlotData {
   int64_t start_time = 0;
   uint16_t flags = 0;
   int16_t pri = PRI_UNDER;
+  int64_t req_until = 0;  // boost_exclusive: a BOOSTed wake's request window (ns)
   uint64_t prev_pmc[kNumPmc] = {0, 0, 0, 0};
   struct {
     int32_t credit_last = 0;
@@ -669,6 +670,7 @@ class CreditScheduler : public Scheduler {
   // ----------------------------------------------------- wake / sleep ----
   void sleep(Slot& v) override {
     E.perfc.incr(PC_vcpu_sleep);
+    sv(v).req_until = 0;
     if (E.parts[v.processor]->curr == v.id)
       E.raise_softirq(v.processor);
     else if (sv(v).runq_cpu >= 0)
@@ -686,7 +688,10 @@ class CreditScheduler : public Scheduler {
       return;
     }
     E.perfc.incr(E.runnable(v) ? PC_vcpu_wake_runnable : PC_vcpu_wake_not_runnable);
-    if (s.pri == PRI_UNDER && !(s.flags & FLAG_PARKED)) s.pri = PRI_BOOST;  // wake-boost
+    if (s.pri == PRI_UNDER && !(s.flags & FLAG_PARKED)) {
+      s.pri = PRI_BOOST;  // wake-boost
+      s.req_until = E.now() + kReqWindowNs;
+    }
     runq_insert(v.processor, v);
     tickle(v.processor, v);
   }
@@ -929,9 +934,42 @@ class CreditScheduler : public Scheduler {
     return nullptr;
   }
 
+  // BOOST exclusion (boost_exclusive; gpbs extension, no reference
+  // counterpart): while a sibling context of this XCD runs a request -- a
+  // slot inside the window opened by a BOOSTing wake (credit demotes BOOST at
+  // its first accounting tick, long before a request ends, so the window is
+  // tracked separately: it closes when the slot blocks, or after
+  // kReqWindowNs for a tenant that never does) -- a memory-class slot of
+  // another tenant parks instead of running, so the request gets the XCD's
+  // share of HBM to itself.  The bytes the parked tenant would have moved in
+  // that window are the ones the request moves instead, so throughput
+  // tenants lose ~nothing while the request finishes near its solo latency.
+  static constexpr int64_t kReqWindowNs = 1000000;
+  bool in_request(Slot& v, int64_t now) { return !v.is_idle() && sv(v).req_until > now; }
+  bool boost_excluded(int cpu, Slot& v) {
+    if (!E.boot.boost_exclusive || v.is_idle() || !mem_bound(v.tenant)) return false;
+    const int64_t now = E.now();
+    if (in_request(v, now)) return false;
+    const Partition& P = *E.parts[cpu];
+    for (int c = cpus_.first(); c >= 0; c = cpus_.next(c + 1)) {
+      if (c == cpu) continue;
+      const Partition& Q = *E.parts[c];
+      if (Q.gpu != P.gpu || Q.xcd != P.xcd) continue;
+      Slot& o = *E.slots[Q.curr];
+      if (o.tenant != v.tenant && in_request(o, now)) return true;
+    }
+    return false;
+  }
+  void kick_xcd(int cpu) {
+    const Partition& P = *E.parts[cpu];
+    for (int c = cpus_.first(); c >= 0; c = cpus_.next(c + 1))
+      if (c != cpu && E.parts[c]->gpu == P.gpu && E.parts[c]->xcd == P.xcd) E.raise_softirq(c);
+  }
+
   TaskSlice do_schedule(int cpu, int64_t now) override {
     Slot& scurr = curr(cpu);
     CSlot& cs = sv(scurr);
+    const bool was_req = in_request(scurr, now) || (!scurr.is_idle() && !E.runnable(scurr));
     E.perfc.incr(PC_schedule);
     int64_t runtime = now - scurr.rs_entry;
     if (runtime < 0) runtime = 0;
@@ -944,10 +982,11 @@ class CreditScheduler : public Scheduler {
     Slot* snext = nullptr;
     TaskSlice ret{0, 0, false};
     int64_t tslice;
-    bool held = false;
+    bool held = false, parked = false;
     const int prev_tenant = scurr.tenant;
     if (ratelimit_us_ && E.runnable(scurr) && !scurr.is_idle() && runtime < (int64_t)ratelimit_us_ * 1000 &&
-        !gang_misaligned(cpu, scurr) && xgang(scurr, now) != 2 && !xgang_favoured(cpu, scurr, now)) {
+        !gang_misaligned(cpu, scurr) && xgang(scurr, now) != 2 && !xgang_favoured(cpu, scurr, now) &&
+        !boost_excluded(cpu, scurr)) {
       snext = &scurr;
       cs.start_time += now;
       E.perfc.incr(PC_delay_ms);
@@ -993,7 +1032,13 @@ class CreditScheduler : public Scheduler {
         runq_remove(*snext);
       else
         snext = &load_balance(cpu, *snext, &ret.migrated);
-      if (sv(*snext).pri == PRI_IDLE)
+      if (boost_excluded(cpu, *snext)) {  // park behind the sibling's request
+        runq_insert(cpu, *snext);
+        snext = E.slots[E.parts[cpu]->idle_slot].get();
+        parked = true;
+        E.perfc.incr(PC_boost_park);
+      }
+      if (sv(*snext).pri == PRI_IDLE && !parked)
         idlers_.set(cpu);
       else
         idlers_.clear(cpu);
@@ -1016,8 +1061,13 @@ class CreditScheduler : public Scheduler {
     } else {
       tslice = (int64_t)tslice_us_ * 1000;
     }
-    ret.time_ns = snext->is_idle() ? -1 : tslice;
+    // A parked partition re-checks at least every 200 us (the request may
+    // lose BOOST while still running, which kicks nobody).
+    ret.time_ns = parked ? 200000 : (snext->is_idle() ? -1 : tslice);
     ret.slot = snext->id;
+    if (E.boot.boost_exclusive && snext != &scurr &&
+        (was_req || in_request(*snext, now)))
+      kick_xcd(cpu);
     if (E.boot.coschedule >= 3 && snext->tenant != prev_tenant && !snext->is_idle() && gang_leader(cpu) == cpu)
       gang_kick(cpu);
     return ret;

@@ -15,6 +15,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <tuple>
 
 namespace gpbs {
 
@@ -674,25 +675,66 @@ void Engine::classify_tick(int64_t n) {
       t.cls_count++;
     }
     if (t.cls_count < 2 || c == t.cls) {
-      // stolen across classes and no longer running: back to its class home
-      for (int sid : t.slots) {
-        Slot& v = *slots[sid];
-        if (!v.is_running && runnable(v) && !v.soft.empty() && !v.soft.test(v.processor)) send_home(v);
+      // Stolen across classes and no longer running: back to its class home.
+      // Stacked on an XCD that hosts more of the tenant's slots than its home
+      // XCD does (an in-class steal of a slot that waited behind a sibling):
+      // home too, even while running -- in a fully
+      // busy pool nothing else would ever undo it, and the tenant would miss
+      // XCDs it is entitled to.
+      // A slot alone on a foreign XCD whose home XCD has none of the
+      // tenant's slots goes home as well: neutral for the slot, but it
+      // unblocks a chain of displaced slots (B stacked behind A's home...).
+      auto on_xcd = [&](int part, size_t skip) {
+        int n = 0;
+        for (size_t j = 0; j < t.slots.size(); ++j) {
+          const Slot& w = *slots[t.slots[j]];
+          if (j == skip || !runnable(w)) continue;
+          const Partition& Q = *parts[w.processor];
+          n += Q.gpu == parts[part]->gpu && Q.xcd == parts[part]->xcd;
+        }
+        return n;
+      };
+      for (size_t k = 0; k < t.slots.size(); ++k) {
+        Slot& v = *slots[t.slots[k]];
+        if (!runnable(v) || v.class_home < 0 || v.processor == v.class_home) continue;
+        const Partition& P = *parts[v.processor];
+        const Partition& H = *parts[v.class_home];
+        const bool stray = !v.is_running && !v.soft.empty() && !v.soft.test(v.processor);
+        const int here = on_xcd(v.processor, k), there = on_xcd(v.class_home, k);
+        const bool foreign = P.gpu != H.gpu || P.xcd != H.xcd;
+        if (stray || (foreign && (there < here || (there == 0 && here == 0)))) send_home(v);
       }
       continue;
     }
     t.cls = c;
+    // Class 0 (compute) lives on context 0; the memory class on every other
+    // context (with two contexts per XCD: context 1).
     Mask m;
     for (int p = pl->cpus.first(); p >= 0; p = pl->cpus.next(p + 1))
-      if (parts[p]->ctx == c) m.set(p);
+      if (c == 0 ? parts[p]->ctx == 0 : parts[p]->ctx >= 1) m.set(p);
     if (m.empty()) m = pl->cpus;
-    // Slot k goes to the k-th partition of the class (cycling), so a tenant
-    // with one slot per XCD lands on every XCD instead of wherever pick_cpu's
-    // cycle from its old processor would pile them up.
+    // Slot k goes to the k-th partition of the class (cycling), ordered
+    // context-major, so a tenant with one slot per XCD lands on every XCD
+    // instead of wherever pick_cpu's cycle from its old processor would pile
+    // them up.  With several contexts in the class, tenants start on
+    // different contexts (rotation by id): co-class tenants co-reside rather
+    // than time-share one context.
     std::vector<int> order;
     for (int p = m.first(); p >= 0; p = m.next(p + 1)) order.push_back(p);
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+      return std::make_tuple(parts[a]->ctx, parts[a]->gpu, parts[a]->xcd) <
+             std::make_tuple(parts[b]->ctx, parts[b]->gpu, parts[b]->xcd);
+    });
+    size_t rot = 0;
+    if (!order.empty()) {
+      const int c0 = parts[order[0]]->ctx;
+      size_t per = 0;
+      while (per < order.size() && parts[order[per]]->ctx == c0) ++per;
+      const size_t nc = order.size() / std::max<size_t>(per, 1);
+      if (nc > 1) rot = (size_t)(t.id % (int)nc) * per;
+    }
     for (size_t k = 0; k < t.slots.size(); ++k)
-      place_class(*slots[t.slots[k]], m, order.empty() ? -1 : order[k % order.size()]);
+      place_class(*slots[t.slots[k]], m, order.empty() ? -1 : order[(k + rot) % order.size()]);
     emit(TRC_CLASS, 0, t.id, (uint32_t)c, (uint32_t)m.weight());
   }
   process_softirqs();

@@ -29,19 +29,23 @@ typedef unsigned long long u64;
 // by the next system-scope load of a workgroup (~1-2 us over PCIe) without a
 // copy or a kernel launch.  A device-memory copy is maintained by the
 // partition_switch kernel when GPBS_TABLE=device.
-// Each XCD exposes kCtx issue contexts (the SMT-sibling analog: two tenants'
-// waves co-reside on the XCD's CUs, one typically MFMA-bound and one
-// memory-bound).  owner[2*x + c] is the tenant running on context c of XCD x.
-constexpr int kCtx = 2;
+// Each XCD exposes up to kCtx issue contexts (the SMT-sibling analog: the
+// tenants' waves co-reside on the XCD's CUs, typically one MFMA-bound and
+// the others memory-bound).  owner[kCtx*x + c] is the tenant running on
+// context c of XCD x; an engine uses nctx <= kCtx of them, the rest stay
+// kNoOwner.
+constexpr int kCtx = 4;
 struct alignas(64) PartTable {
   u32 epoch;
   u32 flags;
+  u32 pad0[2];
   union {
     u32 owner[kXcds * kCtx];  // tenant id per (XCD, context), kNoOwner when idle
-    u64 pair[kXcds];          // both contexts of an XCD in one 8-byte word
+    u64 pair[kXcds][2];       // contexts {0,1} and {2,3} of an XCD, 8 bytes each
   };
-  u32 pad[14];
+  u32 pad[12];
 };
+static_assert(sizeof(PartTable) == 192, "partition table layout");
 
 // Work queue of one tenant kernel invocation (tile / chunk queue).
 struct alignas(64) WorkQueue {
@@ -120,15 +124,21 @@ __device__ __forceinline__ u32 load_sys(const u32* p) {
 // Does tenant `me` own the XCD this workgroup runs on?
 __device__ __forceinline__ bool owns(const PartTable* t, u32 mode, u32 me, u32 xcc) {
   if ((mode & 3) == GATE_NONE) return true;
-  // One 8-byte load covers both contexts of the XCD.
-  const u64 pair = (mode & GATE_DEVTABLE)
-                       ? __hip_atomic_load(&t->pair[xcc & 7], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                       : __hip_atomic_load(&t->pair[xcc & 7], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  const u32 w0 = (u32)pair, w1 = (u32)(pair >> 32);
+  // Two 8-byte loads (one cache line) cover the four contexts of the XCD.
+  const u64* q = t->pair[xcc & 7];
+  const u64 p01 = (mode & GATE_DEVTABLE) ? __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                         : __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const u32 w0 = (u32)p01, w1 = (u32)(p01 >> 32);
   const bool h0 = (w0 & kOwnerMask) == me, h1 = (w1 & kOwnerMask) == me;
-  if (!(mode & GATE_SPATIAL) || (h0 && h1)) return h0 || h1;
-  // Spatial: a split XCD confines each owner to its CU half; an unsplit one
-  // (same-class owners, or the other side idle) is shared in full.
+  if (!(mode & GATE_SPATIAL) || (h0 && h1)) {
+    if (h0 || h1) return true;
+    const u64 p23 = (mode & GATE_DEVTABLE) ? __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                           : __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return (u32)p23 == me || (u32)(p23 >> 32) == me;
+  }
+  // Spatial (contexts 0/1 only): a split XCD confines each owner to its CU
+  // half; an unsplit one (same-class owners, or the other side idle) is
+  // shared in full.
   if (h0) return !(w0 & kSplitBit) || cu_half() == 0;
   if (h1) return !(w1 & kSplitBit) || cu_half() == 1;
   return false;

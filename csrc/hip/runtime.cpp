@@ -69,7 +69,7 @@ struct GpuCtx {
   u64* h_adelta = nullptr;        // adapt inputs (separate from the async reduce buffers)
   hipStream_t sched_stream = nullptr;
   gpbs_engine_t* engine = nullptr;
-  int nctx = 1;                  // issue contexts per XCD in use (1 or kCtx)
+  int nctx = 1;                  // issue contexts per XCD in use (1..kCtx)
   u32 pending[kXcds * kCtx];
   u32 epoch = 0;
   // async counter reduce (one metric period of lag, never blocks the engine)
@@ -132,7 +132,7 @@ void mark_splits(GpuCtx* c) {
     u32& b = c->pending[x * kCtx + 1];
     a &= kOwnerMask | (a == kNoOwner ? kSplitBit : 0u);
     b &= kOwnerMask | (b == kNoOwner ? kSplitBit : 0u);
-    if (!c->spatial || c->nctx < 2 || a == kNoOwner || b == kNoOwner || a == b) continue;
+    if (!c->spatial || c->nctx != 2 || a == kNoOwner || b == kNoOwner || a == b) continue;
     // No engine attached (manual tables): distinct owners are split.
     const int ca = c->engine ? gpbs_tenant_class(c->engine, (int)a) : 0;
     const int cb = c->engine ? gpbs_tenant_class(c->engine, (int)b) : 1;
@@ -378,8 +378,8 @@ struct Runner {
     // same half of all of them; otherwise unmasked + per-workgroup gating.
     int half = -1;
     for (int x = 0; x < kXcds; ++x) {
-      const u32 w0 = __atomic_load_n(&ctx->h_table->owner[2 * x], __ATOMIC_ACQUIRE);
-      const u32 w1 = __atomic_load_n(&ctx->h_table->owner[2 * x + 1], __ATOMIC_ACQUIRE);
+      const u32 w0 = __atomic_load_n(&ctx->h_table->owner[kCtx * x], __ATOMIC_ACQUIRE);
+      const u32 w1 = __atomic_load_n(&ctx->h_table->owner[kCtx * x + 1], __ATOMIC_ACQUIRE);
       const bool h0 = (w0 & kOwnerMask) == (u32)cfg.tenant, h1 = (w1 & kOwnerMask) == (u32)cfg.tenant;
       if (!h0 && !h1) continue;
       if ((h0 && h1) || !(w0 & kSplitBit)) return stream;
@@ -564,7 +564,7 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
   c->device = device;
   c->part_base = part_base;
   c->table_mode = table_mode;
-  c->nctx = nctx == kCtx ? kCtx : 1;
+  c->nctx = nctx < 1 ? 1 : (nctx > kCtx ? kCtx : nctx);
   std::memset(c->last_delta, 0, sizeof(c->last_delta));
   std::memset(c->own_ns, 0, sizeof(c->own_ns));
   bool ok = hipHostMalloc((void**)&c->h_table, sizeof(PartTable), hipHostMallocCoherent | hipHostMallocMapped) ==
@@ -656,10 +656,10 @@ int gpbs_gpu_attach(void* p, gpbs_engine_t* e, int device_counters, int device_a
   return 0;
 }
 
-// Issue contexts per XCD used by the attached engine's partitions (1 or 2).
+// Issue contexts per XCD used by the attached engine's partitions (1..kCtx).
 int gpbs_gpu_set_nctx(void* p, int nctx) {
   GpuCtx* c = (GpuCtx*)p;
-  c->nctx = nctx == kCtx ? kCtx : 1;
+  c->nctx = nctx < 1 ? 1 : (nctx > kCtx ? kCtx : nctx);
   return 0;
 }
 
@@ -721,7 +721,7 @@ int gpbs_gpu_set_table_mode(void* p, int mode) {
 void* gpbs_gpu_table(void* p) { return ((GpuCtx*)p)->table_mode == 1 ? (void*)((GpuCtx*)p)->d_table : (void*)((GpuCtx*)p)->h_table; }
 void* gpbs_gpu_counters(void* p) { return ((GpuCtx*)p)->d_cnt; }
 
-// owners: [kXcds * kCtx] entries, (xcd, context) major, -1 = idle.
+// owners: [kXcds * kCtx] entries (kCtx = 4), (xcd, context) major, -1 = idle.
 int gpbs_gpu_set_owners(void* p, const int* owners) {
   GpuCtx* c = (GpuCtx*)p;
   for (int x = 0; x < kXcds * kCtx; ++x) c->pending[x] = owners[x] >= 0 ? (u32)owners[x] : kNoOwner;
@@ -753,7 +753,7 @@ int gpbs_gpu_read_counters(void* p, int tenant, uint64_t* out4, uint64_t* per_xc
   return 0;
 }
 
-// ns tenant `t` held context c (summed over XCDs); reset when clear != 0.
+// ns tenant `t` held context c (summed over XCDs), out[kCtx]; reset when clear != 0.
 int gpbs_gpu_ownership(void* p, int t, int64_t* out2, int clear) {
   GpuCtx* c = (GpuCtx*)p;
   if (t < 0 || t >= kMaxTenants) return -22;

@@ -69,6 +69,7 @@ typedef struct gpbs_boot_params {
   int32_t quantum_align_us;    /* 0 = off; round quantum expiries up to this grid (batched switches) */
   int32_t coschedule;          /* 1 = contention-aware sibling selection; 2 = + counter-driven context classes */
   int32_t class_period_us;     /* contention-class re-evaluation period, default 2000 */
+  int32_t boost_exclusive;     /* 1 = memory-class slots park while a sibling context of their XCD runs a BOOSTed waker */
   gpbs_adapt_params_t adapt;
   gpbs_atc_params_t atc;
 } gpbs_boot_params_t;

@@ -31,7 +31,7 @@ class BootParams(C.Structure):
     _fields_ = [("sched", C.c_char * 16)] + [(n, i32) for n in (
         "tslice_us", "ratelimit_us", "smt_power_savings", "tickle_one_idle", "default_yield", "migration_delay_us",
         "metric_period_us", "slice_apply_us", "sim_clock", "pmu_refresh_us", "dom0_quirk", "heartbeat_timeout_us",
-        "trace_capacity", "quantum_align_us", "coschedule", "class_period_us")] + [("adapt", AdaptParams), ("atc", AtcParams)]
+        "trace_capacity", "quantum_align_us", "coschedule", "class_period_us", "boost_exclusive")] + [("adapt", AdaptParams), ("atc", AtcParams)]
 
 
 class FilterEntry(C.Structure):

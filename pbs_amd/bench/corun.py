@@ -95,6 +95,10 @@ POLICY_ENGINES = {
     "gpbs-exit": (2, {}, True, "host"),
     "gpbs1": (1, {"coschedule": 0}, True, "host"),
     "credit2": (2, {"sched": "credit-fixed"}, "park", "device"),
+    "gpbs-c3": (3, {}, "park", "device"),
+    "gpbs-c4": (4, {}, "park", "device"),
+    "gpbs-c3x": (3, {"boost_exclusive": 1}, "park", "device"),
+    "gpbs-c4x": (4, {"boost_exclusive": 1}, "park", "device"),
 }
 
 

@@ -37,7 +37,8 @@ def _tenant(kind: str, seconds: float, warmup: float, socket: Optional[str], q, 
     t = None
     if socket:
         from ..runtime.tenant import TenantClient
-        t = TenantClient(kind, socket, slots=8, weight=args.get(f"{kind}_weight", 256))
+        t = TenantClient(kind, socket, slots=8, weight=args.get(f"{kind}_weight", 256),
+                         spatial=args.get("spatial", False), priority=args.get(f"{kind}_prio", 0))
     if kind == "infer":
         w = LlamaDecoder(PRESETS[args["infer_model"]], batch=args["infer_batch"], context=args["context"])
         prompt = torch.randint(0, w.cfg.vocab, (w.batch, args["prompt"]), device="cuda")
@@ -57,6 +58,9 @@ def _tenant(kind: str, seconds: float, warmup: float, socket: Optional[str], q, 
         def unit():
             w.step()
         per_unit_tokens = w.tokens_per_step()
+    prio_stream = None
+    if t is None and args.get(f"{kind}_prio", 0):
+        prio_stream = torch.cuda.Stream(priority=-abs(args[f"{kind}_prio"]))
     torch.cuda.synchronize()
     start_evt.wait()
     lat = []
@@ -76,6 +80,10 @@ def _tenant(kind: str, seconds: float, warmup: float, socket: Optional[str], q, 
                 unit()
                 torch.cuda.current_stream().synchronize()
             t.account(flops=flops, bytes_moved=bytes_, busy_ns=int((time.perf_counter() - t0) * 1e9))
+        elif prio_stream is not None:
+            with torch.cuda.stream(prio_stream):
+                unit()
+            prio_stream.synchronize()
         else:
             unit()
             torch.cuda.synchronize()
@@ -97,7 +105,11 @@ def run(policy: str, kinds, args: dict, seconds: float, warmup: float) -> Dict[s
     start = ctx.Event()
     daemon = None
     sock = None
-    if policy == "gpbs":
+    args = dict(args, spatial=policy == "gpbs-spatial")
+    if policy.endswith("+prio"):
+        args["infer_prio"] = 1
+        policy = policy[:-5]
+    if policy in ("gpbs", "gpbs-spatial"):
         from ..runtime.daemon import Daemon
         sock = os.path.join(tempfile.mkdtemp(), "gpbsd.sock")
         daemon = Daemon(sock, gpus=[0], nctx=2, sim=False, profile="mi355x").start()

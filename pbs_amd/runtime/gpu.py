@@ -27,7 +27,7 @@ from ..ops import hipabi
 from ..ops.kernels import lib as hiplib
 
 XCDS = 8
-CTX = 2  # issue contexts per XCD in the partition table (SMT-sibling analog)
+CTX = 4  # issue contexts per XCD in the partition table (SMT-sibling analog)
 
 
 class GpuContext:
@@ -65,15 +65,17 @@ class GpuContext:
         return C.c_void_p(self.L.gpbs_gpu_counters(self.h))
 
     def set_owners(self, owners: List[int]):
-        """owners: 8 entries (one tenant per XCD, context 1 idle) or 16
-        entries ((xcd, ctx) major)."""
-        if len(owners) == XCDS:
-            owners = [o for x in owners for o in (x, -1)]
+        """owners: 8 entries (one tenant per XCD, other contexts idle), 16
+        ((xcd, ctx) major, two contexts per XCD) or XCDS*CTX entries."""
+        if len(owners) % XCDS or not 1 <= len(owners) // XCDS <= CTX:
+            raise ValueError(f"owners: need a multiple of {XCDS} entries, at most {XCDS * CTX}")
+        per = len(owners) // XCDS
+        owners = [owners[x * per + c] if c < per else -1 for x in range(XCDS) for c in range(CTX)]
         arr = (C.c_int * (XCDS * CTX))(*owners)
         return self.L.gpbs_gpu_set_owners(self.h, arr)
 
     def owners(self) -> List[int]:
-        """16 entries: tenant on (xcd, ctx), -1 idle."""
+        """XCDS*CTX entries: tenant on (xcd, ctx), (xcd, ctx) major, -1 idle."""
         arr = (C.c_int * (XCDS * CTX))()
         self.L.gpbs_gpu_get_owners(self.h, arr)
         return list(arr)

@@ -60,10 +60,12 @@ def half_cu_words(owned: List[Tuple[int, int]]) -> List[int]:
 
 class TenantClient:
     def __init__(self, name: str, socket_path: str = DEFAULT_SOCKET, slots: int = 8, weight: int = -1,
-                 cap: int = -1, pool=None, gpu: int = 0, heartbeat_s: float = 0.05, spatial: bool = True):
+                 cap: int = -1, pool=None, gpu: int = 0, heartbeat_s: float = 0.05, spatial: bool = True,
+                 priority: int = 0):
         self.name = name
         self.gpu = gpu
         self.spatial = spatial
+        self.priority = priority
         self.rpc = Client(socket_path)
         r = self.rpc.call("register", name=name, slots=slots, weight=weight, cap=cap, pool=pool, pid=os.getpid())
         self.tenant: int = r["tenant"]
@@ -121,7 +123,9 @@ class TenantClient:
         quantised to {half 0, half 1, both} across all XCDs: a CU mask is a
         hardware-queue property, so every distinct mask costs a queue, and
         class placement keeps a tenant on one half anyway.  Co-resident
-        contexts (``spatial=False``) always get the whole GPU."""
+        contexts (``spatial=False``) always get the whole GPU, on a stream of
+        the tenant's queue priority (``priority`` > 0: the command processor
+        dispatches its workgroups ahead of normal-priority queues)."""
         import torch
 
         from ..ops import kernels as K
@@ -130,7 +134,10 @@ class TenantClient:
             return torch.cuda.current_stream()
         halves = tuple(sorted({c for (_, c) in parts})) if self.spatial else (0, 1)
         s = self._streams.get(halves)
-        if s is None:
+        if s is None and not self.spatial:
+            s = torch.cuda.Stream(device=self.gpu, priority=-1 if self.priority > 0 else 0)
+            self._streams[halves] = s
+        elif s is None:
             key = [(x, h) for x in range(XCDS) for h in halves]
             h = K.cumask_stream(half_cu_words(key), device=self.gpu)
             s = torch.cuda.ExternalStream(h)

@@ -447,3 +447,85 @@ def test_class_placement_is_not_undone_by_cross_class_steals():
     assert sorted(_procs(e, mem)) == list(range(1, 16, 2)), _procs(e, mem)
     assert sorted(_procs(e, comp)) == list(range(0, 16, 2)), _procs(e, comp)
     assert e.check() == ""
+
+
+def test_four_contexts_memory_tenants_coreside_on_distinct_contexts():
+    """nctx=4: the compute class keeps context 0, the memory class spans
+    contexts 1-3 and its tenants start on different contexts, so three memory
+    tenants and a compute tenant all co-reside on every XCD instead of
+    time-sharing one memory context.  Regression: an in-class steal used to
+    leave a tenant stacked on one XCD for good in a fully busy pool."""
+    parts = [(0, x, c) for x in range(8) for c in range(4)]
+    e = Engine(sim_clock=True, partitions=parts, coschedule=3, class_period_us=2000, quantum_align_us=0)
+    e.tenant_create("Domain-0", nslots=1)
+    comp = e.tenant_create("gemm", nslots=8)
+    mems = [e.tenant_create(n, nslots=8) for n in ("hbm", "coll", "kv")]
+    rates = {comp: (1000, 1), **{m: (100, 100) for m in mems}}
+    for t in (comp, *mems):
+        e.wake(t)
+    for _ in range(400):
+        _feed(e, rates, 100)
+    ctx = {p: c for p, (_, _, c) in enumerate(parts)}
+    xcd = {p: x for p, (_, x, _) in enumerate(parts)}
+    assert sorted(ctx[p] for p in _procs(e, comp)) == [0] * 8
+    for m in mems:
+        procs = _procs(e, m)
+        assert sorted(xcd[p] for p in procs) == list(range(8)), (m, procs)  # one slot per XCD
+        assert all(ctx[p] >= 1 for p in procs), (m, procs)
+    # every throughput tenant keeps running: no time-sharing of contexts
+    base = {t: e.tenant_info(t).run_ns for t in (comp, *mems)}
+    t0 = e.now()
+    for _ in range(100):
+        _feed(e, rates, 100)
+    for t in (comp, *mems):
+        assert (e.tenant_info(t).run_ns - base[t]) / (e.now() - t0) > 7.5, t
+    assert e.check() == ""
+
+
+def _boost_run(exclusive):
+    parts = [(0, x, c) for x in range(2) for c in range(4)]
+    e = Engine(sim_clock=True, partitions=parts, coschedule=3, class_period_us=2000, quantum_align_us=0,
+               boost_exclusive=exclusive)
+    e.tenant_create("Domain-0", nslots=1)
+    comp = e.tenant_create("gemm", nslots=2)
+    mems = [e.tenant_create(n, nslots=2) for n in ("hbm", "coll")]
+    lat = e.tenant_create("lat", nslots=2)
+    rates = {comp: (1000, 1), **{m: (100, 100) for m in mems}, lat: (100, 100)}
+    for t in (comp, *mems):
+        e.wake(t)
+    for _ in range(200):  # classify and settle
+        _feed(e, rates, 100)
+    base = {t: e.tenant_info(t).run_ns for t in (comp, *mems)}
+    e.perfc_reset()
+    overlap = 0  # 100-us steps in which the request and a memory tenant both ran on one XCD
+    for _ in range(20):  # requests: 300 us of work, 1.7 ms think time
+        e.wake(lat)
+        for _ in range(3):
+            _feed(e, rates, 100)
+            on = {(parts[p][1]) for p in _procs(e, lat) if e.slot_info(e.slot_id(lat, _procs(e, lat).index(p)))["is_running"]}
+            for m in mems:
+                for k in range(2):
+                    si = e.slot_info(e.slot_id(m, k))
+                    if si["is_running"] and parts[si["processor"]][1] in on:
+                        overlap += 1
+        e.block(lat)
+        for _ in range(17):
+            _feed(e, rates, 100)
+    run = {t: e.tenant_info(t).run_ns - base[t] for t in (comp, *mems)}
+    return e, overlap, run, comp, mems
+
+
+def test_boost_exclusive_parks_memory_siblings_during_a_request():
+    """boost_exclusive=1: while the latency tenant's BOOSTed request runs on
+    an XCD, memory-class tenants on the sibling contexts park (and resume
+    when it blocks); the compute tenant keeps running.  Off: they co-run."""
+    e0, ov0, run0, comp, mems = _boost_run(0)
+    e1, ov1, run1, _, _ = _boost_run(1)
+    assert ov0 > 0 and e0.perfc().get("boost_park", 0) == 0
+    assert ov1 == 0, ov1
+    assert e1.perfc()["boost_park"] > 0
+    # compute tenant unaffected, memory tenants lose at most the request time (~15 %)
+    assert run1[comp] >= 0.97 * run0[comp], (run0, run1)
+    for m in mems:
+        assert run1[m] >= 0.8 * run0[m], (m, run0, run1)
+    assert e1.check() == ""

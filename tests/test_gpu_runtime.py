@@ -131,3 +131,21 @@ def test_spatial_gate_follows_the_cu_half():
                 assert bool(ok) == (me == 1), (me, xcc)
     assert ctx.owners()[:2] == [1, 2]  # split bit hidden from readers
     ctx.close()
+
+
+def test_four_context_table_gates_each_context():
+    """kCtx = 4 co-resident issue contexts per XCD: a tenant holding only
+    context c of XCD x runs there and nowhere else, for every c."""
+    from pbs_amd.ops import kernels as K
+    ctx = GpuContext(0, None, nctx=4)
+    owners = [-1] * 32
+    for x in range(8):
+        owners[4 * x + (x % 4)] = 10 + (x % 4)  # tenant 10+c on context c of XCDs c and c+4
+    ctx.set_owners(owners)
+    assert ctx.owners() == owners
+    for c in range(4):
+        out = K.census(2048, table=ctx.table, tenant=10 + c).cpu()
+        for xcc, _hw, ok, magic in out.tolist():
+            assert magic == 0xC0FFEE
+            assert bool(ok) == (xcc % 4 == c), (c, xcc)
+    ctx.close()
