@@ -33,7 +33,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--policies", default="none,static,gpbs1,gpbs-spatial,gpbs", help="comma list; gpbs is the reported policy")
+    ap.add_argument("--policies", default="none,static,gpbs-ctx2,gpbs-spatial,gpbs", help="comma list; gpbs is the reported policy")
     ap.add_argument("--target-ms", type=float, default=30.0)
     ap.add_argument("--table", default="host", choices=["host", "device"])
     ap.add_argument("--out", default="")

@@ -93,7 +93,10 @@ __device__ __forceinline__ void finish(WorkQueue* q, u32* status, u32 total) {
 // Bit 3 (GATE_SPATIAL): the two partitions of an XCD are CU halves (shader
 // engines 0-1 vs 2-3) instead of co-resident issue contexts; a workgroup
 // checks only the entry of the half its CU belongs to.
-enum GateMode : u32 { GATE_NONE = 0, GATE_TABLE = 1, GATE_PARK = 2, GATE_DEVTABLE = 4, GATE_SPATIAL = 8 };
+enum GateMode : u32 {
+  GATE_NONE = 0, GATE_TABLE = 1, GATE_PARK = 2, GATE_DEVTABLE = 4, GATE_SPATIAL = 8,
+  GATE_WAVEPRIO = 16,  // latency-class tenant: its waves win SIMD issue arbitration (s_setprio 3)
+};
 constexpr u32 kParkSpins = 100;  // x ~20 us
 
 #define HIPCHECK(x)                                                                              \

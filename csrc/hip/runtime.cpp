@@ -70,6 +70,7 @@ struct GpuCtx {
   hipStream_t sched_stream = nullptr;
   gpbs_engine_t* engine = nullptr;
   int nctx = 1;                  // issue contexts per XCD in use (1..kCtx)
+  int waveprio = 0;              // latency-class runners raise their wave priority
   u32 pending[kXcds * kCtx];
   u32 epoch = 0;
   // async counter reduce (one metric period of lag, never blocks the engine)
@@ -398,7 +399,8 @@ struct Runner {
     const bool dev = __atomic_load_n(&ctx->table_mode, __ATOMIC_ACQUIRE) == 1;
     const void* tab = dev ? (const void*)ctx->d_table : (const void*)ctx->h_table;
     const unsigned mode = (cfg.gate ? (cfg.gate == 2 ? GATE_PARK : GATE_TABLE) : GATE_NONE) | (dev ? GATE_DEVTABLE : 0) |
-                          (cfg.gate && ctx->spatial ? GATE_SPATIAL : 0);
+                          (cfg.gate && ctx->spatial ? GATE_SPATIAL : 0) |
+                          (cfg.gate && cfg.priority > 0 && ctx->waveprio ? GATE_WAVEPRIO : 0);
     const unsigned me = (unsigned)cfg.tenant;
     __atomic_store_n(&h_status[qi], 0u, __ATOMIC_RELEASE);
     st.launches++;
@@ -695,6 +697,15 @@ int gpbs_gpu_hwc_stats(void* p, uint64_t* samples, uint64_t* mean_ns, double* ra
   if (mean_ns) *mean_ns = c->hwc_samples ? (uint64_t)(c->hwc_ns / (int64_t)c->hwc_samples) : 0;
   if (ratio4)
     for (int k = 0; k < kNumPmc; ++k) ratio4[k] = c->model_sum[k] > 0 ? c->hw_sum[k] / c->model_sum[k] : 0.0;
+  return 0;
+}
+
+// Latency-class runners (priority > 0) launch their kernels with raised wave
+// issue priority while a gated policy is active.
+int gpbs_gpu_set_waveprio(void* p, int on) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c) return -22;
+  __atomic_store_n(&c->waveprio, on ? 1 : 0, __ATOMIC_RELEASE);
   return 0;
 }
 

@@ -18,7 +18,10 @@ struct Owners {
   u32 o[kXcds * kCtx];
 };
 
+// The scheduler's kernels run at top SIMD issue priority: they share CUs with
+// the tenants' persistent waves, and their latency is the actuation latency.
 __global__ void k_partition_switch(PartTable* t, u32 epoch, Owners ow) {
+  __builtin_amdgcn_s_setprio(3);
   const int i = threadIdx.x;
   if (i < kXcds * kCtx) __hip_atomic_store(&t->owner[i], ow.o[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __syncthreads();
@@ -30,6 +33,7 @@ __global__ void k_partition_switch(PartTable* t, u32 epoch, Owners ow) {
 
 // cnt/prev: [kMaxTenants][kXcds][kNumPmc]; ids[n]; out[n][4] (host-mapped).
 __global__ __launch_bounds__(64) void k_counter_reduce(u64* cnt, u64* prev, const int* ids, int n, u64* out) {
+  __builtin_amdgcn_s_setprio(3);
   const int k = blockIdx.x;
   if (k >= n) return;
   const int lane = threadIdx.x;

@@ -578,6 +578,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
                                                   const PartTable* table, u32 mode, u32 me, u64* cnt,
                                                   u32* status) {
   __shared__ int s_slot[4];
+  if (mode & GATE_WAVEPRIO) __builtin_amdgcn_s_setprio(3);
   const u32 xcc = xcc_id();
   // Ownership is decided by thread 0 inside grab_unit (workgroup-uniform).
   u64 t_last = __builtin_amdgcn_s_memtime();

@@ -29,15 +29,23 @@ Policies (same tenants, same box):
           kernels exit on revoked XCDs
   gpbs-exit   two co-resident issue contexts per XCD + contention classes,
           workgroups exit on revocation, host table
-  gpbs-spatial  spatial partitions: an XCD whose two owners are of different
-          classes is split into CU halves (shader engines 0-1 / 2-3);
-          half-masked streams
+  gpbs-ctx2   two co-resident issue contexts per XCD, parked gating: three
+          throughput tenants time-share them (best latency-tenant delay, but
+          the forced time-slicing costs aggregate throughput)
+  gpbs-spatial  as gpbs-ctx2, but an XCD whose two owners are of different
+          classes is split into CU halves (shader engines 0-1 / 2-3)
+  gpbs-noprio the flagship without wave priority
+  gpbs-x  the flagship + BOOST exclusion (memory-class siblings park during a
+          latency request)
   gpbs-nogang the flagship without gang alignment of the classes
-  gpbs    PBS adaptive credit scheduler over two co-resident issue contexts
-          per XCD: counter-driven compute/memory classes (soft affinity, work
-          conserving), gang-aligned per class, parked gating on a
-          device-resident partition table (the flagship: lowest mean co-run
-          slowdown and latency-tenant delay, profiles/corun_policies_1gpu.log)
+  gpbs    PBS adaptive credit scheduler over four co-resident issue contexts
+          per XCD: counter-driven compute/memory classes (compute on context
+          0, memory tenants rotated over contexts 1-3, soft affinity, work
+          conserving), gang-aligned per context, parked gating on a
+          device-resident partition table, and latency-class tenants' waves
+          at raised SIMD issue priority (the flagship: aggregate at parity
+          with default sharing, lower latency-tenant delay and mean slowdown;
+          profiles/corun_flagship_1gpu.log)
 """
 from __future__ import annotations
 
@@ -88,17 +96,16 @@ class CorunConfig:
 
 POLICY_ENGINES = {
     # name: (issue contexts per XCD, engine overrides on top of MI355X_PROFILE,
-    #        kernel gate mode, partition-table location)
-    "gpbs": (2, {}, "park", "device"),
+    #        kernel gate mode, partition-table location + runtime options)
+    "gpbs": (4, {}, "park", "device,waveprio"),
+    "gpbs-x": (4, {"boost_exclusive": 1}, "park", "device,waveprio"),
+    "gpbs-noprio": (4, {}, "park", "device"),
+    "gpbs-ctx2": (2, {}, "park", "device"),
     "gpbs-spatial": (2, {}, "park", "device,spatial"),
-    "gpbs-nogang": (2, {"coschedule": 2}, "park", "device"),
+    "gpbs-nogang": (4, {"coschedule": 2}, "park", "device,waveprio"),
     "gpbs-exit": (2, {}, True, "host"),
     "gpbs1": (1, {"coschedule": 0}, True, "host"),
-    "credit2": (2, {"sched": "credit-fixed"}, "park", "device"),
-    "gpbs-c3": (3, {}, "park", "device"),
-    "gpbs-c4": (4, {}, "park", "device"),
-    "gpbs-c3x": (3, {"boost_exclusive": 1}, "park", "device"),
-    "gpbs-c4x": (4, {"boost_exclusive": 1}, "park", "device"),
+    "credit2": (4, {"sched": "credit-fixed"}, "park", "device,waveprio"),
 }
 
 
@@ -226,6 +233,7 @@ class Corun:
             _, _, gate, table = POLICY_ENGINES[policy]
             self.ctx.set_table_mode(table.split(",")[0])
             self.ctx.set_spatial("spatial" in table)
+            self.ctx.set_waveprio("waveprio" in table)
             self.ctx.attach(e, nctx=e._gpbs_nctx)
             if self.cfg.hw_counters:
                 self.ctx.set_hwc(True)
@@ -245,6 +253,7 @@ class Corun:
             return
         self.ctx.set_table_mode("host")
         self.ctx.set_spatial(False)
+        self.ctx.set_waveprio(False)
         for r in self._natives():
             r.set_engine_wake(False)
         if isinstance(coll, CollTenant):

@@ -59,6 +59,7 @@ def bind(lib):
     _p(lib, "gpbs_gpu_set_nctx", C.c_int, vp, C.c_int)
     _p(lib, "gpbs_gpu_set_table_mode", C.c_int, vp, C.c_int)
     _p(lib, "gpbs_gpu_set_spatial", C.c_int, vp, C.c_int)
+    _p(lib, "gpbs_gpu_set_waveprio", C.c_int, vp, C.c_int)
     _p(lib, "gpbs_gpu_ctx_destroy", None, vp)
     _p(lib, "gpbs_gpu_attach", C.c_int, vp, vp, C.c_int, C.c_int)
     _p(lib, "gpbs_gpu_table", vp, vp)

@@ -111,6 +111,13 @@ class GpuContext:
         return {"samples": n.value, "mean_sample_us": ns.value / 1e3,
                 "hw_over_model": [round(x, 4) for x in r]}
 
+    def set_waveprio(self, on: bool):
+        """Latency-class runners (priority > 0) raise their waves' SIMD issue
+        priority (s_setprio 3) under gated policies."""
+        rc = self.L.gpbs_gpu_set_waveprio(self.h, 1 if on else 0)
+        if rc:
+            raise RuntimeError("set_waveprio failed")
+
     def set_spatial(self, on: bool):
         """Spatial partitions: the two partitions of an XCD are CU halves
         (shader engines 0-1 / 2-3) -- runners launch on half-masked streams
