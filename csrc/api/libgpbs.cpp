@@ -466,6 +466,17 @@ int gpbs_sched_credit_set(gpbs_engine_t* e, int t, int weight, int cap) {
   return r;
 }
 
+// xl sched-credit2 / sched-sedf: scheduler-specific tenant parameters.
+int gpbs_sched_ext(gpbs_engine_t* e, int t, int set, gpbs_sched_ext_t* p) {
+  LOCK(e);
+  Tenant* d = live(e, t);
+  if (!d) return GPBS_ENOENT;
+  if (!p) return GPBS_EINVAL;
+  int r = e->e->sched_of_tenant(t)->adjust_ext(*d, set != 0, *p);
+  if (set) DONE(e);
+  return r;
+}
+
 int gpbs_sched_params_get(gpbs_engine_t* e, int pool, int* tslice_us, int* ratelimit_us) {
   LOCK(e);
   Pool* p = e->e->pool(pool);

@@ -347,7 +347,17 @@ int Engine::tenant_create(const std::string& name, int poolid, int nslots, int w
     return rc;
   }
   perfc.incr(PC_dom_init);
+  // Slot 0 goes to the least-populated partition of the pool, ties to the
+  // highest-numbered one (default_vcpu0_location, X:xen/common/domctl.c:167-214);
+  // the others cycle from there (:566-569).
   int cpu = pl->cpus.empty() ? 0 : pl->cpus.first();
+  if (!pl->cpus.empty()) {
+    std::vector<int> cnt(parts.size(), 0);
+    for (auto& s : slots)
+      if (s && !s->is_idle() && !(s->pause_flags & VPF_DOWN) && s->processor < (int)cnt.size()) cnt[s->processor]++;
+    for (int c = pl->cpus.first(); c >= 0; c = pl->cpus.next(c + 1))
+      if (cnt[c] <= cnt[cpu]) cpu = c;
+  }
   for (int i = 0; i < nslots; ++i) {
     auto s = std::make_unique<Slot>();
     s->id = (int)slots.size();

@@ -138,6 +138,8 @@ class Scheduler {
   virtual int pick_cpu(Slot& v) = 0;
   virtual int adjust(Tenant& d, bool set, int* weight, int* cap) = 0;
   virtual int adjust_global(bool set, int* tslice_us, int* ratelimit_us) = 0;
+  // Scheduler-specific tenant parameters (credit2 weight, sedf reservation).
+  virtual int adjust_ext(Tenant&, bool, gpbs_sched_ext_t&) { return GPBS_EINVAL; }
   virtual void dump_settings(std::string& out) = 0;
   virtual void dump_cpu_state(int part, std::string& out) = 0;
   virtual void dump_admin_conf(std::string& out) = 0;

@@ -137,10 +137,21 @@ typedef struct gpbs_slot_info {
   uint64_t affinity[4];
 } gpbs_slot_info_t;
 
+/* Scheduler-specific per-tenant parameters (xl sched-credit2 / sched-sedf).
+ * credit2: weight.  sedf: period/slice/latency (us), extratime (0/1), weight
+ * (weight-driven reservation; 0 = time-driven).  -1 = leave unchanged where
+ * noted.  credit (out): credit2 credit / sedf remaining slice, us. */
+typedef struct gpbs_sched_ext {
+  int32_t weight, period_us, slice_us, latency_us, extratime, credit;
+} gpbs_sched_ext_t;
+
 typedef struct gpbs_partition_info {
   int32_t id, gpu, xcd, pool, curr_tenant, curr_slot, runq_len, idle, ctx, reserved;
   uint64_t switches;
 } gpbs_partition_info_t;
+
+/* --- scheduler-specific tenant parameters (S4: credit2, sedf) --- */
+int gpbs_sched_ext(gpbs_engine_t* e, int tenant, int set, gpbs_sched_ext_t* p);
 
 /* --- lifecycle --- */
 void gpbs_boot_defaults(gpbs_boot_params_t* p);

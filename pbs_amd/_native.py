@@ -34,6 +34,10 @@ class BootParams(C.Structure):
         "trace_capacity", "quantum_align_us", "coschedule", "class_period_us", "boost_exclusive")] + [("adapt", AdaptParams), ("atc", AtcParams)]
 
 
+class SchedExt(C.Structure):
+    _fields_ = [(n, i32) for n in ("weight", "period_us", "slice_us", "latency_us", "extratime", "credit")]
+
+
 class FilterEntry(C.Structure):
     _fields_ = [("spin", u64), ("inst", u64), ("miss", u64)]
 
@@ -162,6 +166,7 @@ def load_core(build_if_missing=True):
         P(lib, "gpbs_tenant_heartbeat", C.c_int, E, C.c_int)
         P(lib, "gpbs_sched_credit_get", C.c_int, E, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int))
         P(lib, "gpbs_sched_credit_set", C.c_int, E, C.c_int, C.c_int, C.c_int)
+        P(lib, "gpbs_sched_ext", C.c_int, E, C.c_int, C.c_int, C.POINTER(SchedExt))
         P(lib, "gpbs_sched_params_get", C.c_int, E, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int))
         P(lib, "gpbs_sched_params_set", C.c_int, E, C.c_int, C.c_int, C.c_int)
         P(lib, "gpbs_sched_name", C.c_int, E, C.c_int, C.c_char_p, C.c_int)

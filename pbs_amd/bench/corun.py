@@ -38,6 +38,9 @@ Policies (same tenants, same box):
   gpbs-x  the flagship + BOOST exclusion (memory-class siblings park during a
           latency request)
   gpbs-nogang the flagship without gang alignment of the classes
+  credit-fixed  the flagship's contexts and actuation under the credit
+          scheduler with a fixed quantum (no PBS adaptation)
+  credit2 / sedf  the same under the credit2 / sedf schedulers (S4)
   gpbs    PBS adaptive credit scheduler over four co-resident issue contexts
           per XCD: counter-driven compute/memory classes (compute on context
           0, memory tenants rotated over contexts 1-3, soft affinity, work
@@ -105,7 +108,9 @@ POLICY_ENGINES = {
     "gpbs-nogang": (4, {"coschedule": 2}, "park", "device,waveprio"),
     "gpbs-exit": (2, {}, True, "host"),
     "gpbs1": (1, {"coschedule": 0}, True, "host"),
-    "credit2": (4, {"sched": "credit-fixed"}, "park", "device,waveprio"),
+    "credit-fixed": (4, {"sched": "credit-fixed"}, "park", "device,waveprio"),
+    "credit2": (4, {"sched": "credit2"}, "park", "device,waveprio"),
+    "sedf": (4, {"sched": "sedf"}, "park", "device,waveprio"),
 }
 
 

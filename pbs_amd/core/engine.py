@@ -267,6 +267,20 @@ class Engine:
     def sched_credit_set(self, t: int, weight: int = -1, cap: int = -1):
         return self._chk(self.lib.gpbs_sched_credit_set(self.h, t, weight, cap), "sched_credit_set")
 
+    def sched_ext_get(self, t: int) -> Dict[str, int]:
+        """Scheduler-specific parameters (credit2: weight; sedf: period_us,
+        slice_us, latency_us, extratime, weight), plus the slot-0 credit."""
+        x = N.SchedExt()
+        self._chk(self.lib.gpbs_sched_ext(self.h, t, 0, C.byref(x)), "sched_ext_get")
+        return {k: getattr(x, k) for k, _ in N.SchedExt._fields_}
+
+    def sched_ext_set(self, t: int, weight: int = 0, period_us: int = 0, slice_us: int = 0, latency_us: int = -1,
+                      extratime: int = -1):
+        """xl sched-credit2 -w / sched-sedf -p -s -l -e -w (0 / -1 = unset)."""
+        x = N.SchedExt(weight, period_us, slice_us, latency_us, extratime, 0)
+        self._chk(self.lib.gpbs_sched_ext(self.h, t, 1, C.byref(x)), "sched_ext_set")
+        return {k: getattr(x, k) for k, _ in N.SchedExt._fields_}
+
     def sched_params_get(self, pool: int = 0):
         ts, rl = C.c_int(), C.c_int()
         self._chk(self.lib.gpbs_sched_params_get(self.h, pool, C.byref(ts), C.byref(rl)), "sched_params_get")

@@ -5,6 +5,8 @@ Domain -> tenant, VCPU -> slot, CPU -> partition (GPU:XCD:context) and
 cpupool -> pool:
 
     gpbsctl sched-credit [-d <Tenant> [-w[=WEIGHT]|-c[=CAP]]] [-s [-t TSLICE] [-r RATELIMIT]] [-p POOL]
+    gpbsctl sched-credit2 [-d <Tenant> [-w[=WEIGHT]]] [-p POOL]
+    gpbsctl sched-sedf [-d <Tenant> [-p MS] [-s MS] [-l MS] [-e 0|1] [-w W]] [-c POOL]
     gpbsctl create NAME [--slots N] [--weight W] [--cap C] [--pool P]
     gpbsctl destroy|pause|unpause TENANT
     gpbsctl list | slot-list [TENANT...] | slot-pin TENANT SLOT|all PARTS|all | slot-set TENANT N
@@ -93,7 +95,7 @@ def cmd_sched_credit(c: Client, argv: List[str]) -> int:
             pools = match
         doms = c.call("domain_list")
         for p in pools:
-            if p["sched"] not in ("credit", "credit-fixed", "atc"):
+            if p["sched"] not in ("credit", "credit-fixed", "atc"):  # credit2 / sedf: their own verbs
                 continue
             _pool_line(c, p["id"])
             _dom_header()
@@ -113,6 +115,124 @@ def cmd_sched_credit(c: Client, argv: List[str]) -> int:
         _err(str(e))
         if opt_w or opt_c:
             _err("libxl_domain_sched_params_set failed.")
+        return 3
+
+
+def _sched_pools(c: Client, sched: str, pool: Optional[str]):
+    """Pools running `sched` (optionally one named pool), or None after an
+    error message (sched_domain_output, xl_cmdimpl.c:4739-4790)."""
+    pools = c.call("pool_list")
+    if pool is not None:
+        match = [p for p in pools if str(p["id"]) == str(pool) or p["name"] == pool]
+        if not match:
+            _err("unknown cpupool '%s'" % pool)
+            return None
+        pools = match
+    return [p for p in pools if p["sched"] == sched]
+
+
+def cmd_sched_credit2(c: Client, argv: List[str]) -> int:
+    """xl sched-credit2 (xl_cmdimpl.c:4932-5005): weight only, no caps."""
+    ap = argparse.ArgumentParser(prog="gpbsctl sched-credit2", add_help=True)
+    ap.add_argument("-d", "--domain", "--tenant", dest="dom")
+    ap.add_argument("-w", "--weight", type=int)
+    ap.add_argument("-p", "--cpupool", "--pool", dest="pool")
+    a = ap.parse_args(argv)
+    if a.pool is not None and (a.dom or a.weight is not None):
+        _err("Specifying a cpupool is not allowed with other options.")
+        return 1
+    if not a.dom and a.weight is not None:
+        _err("Must specify a domain.")
+        return 1
+    hdr = lambda: print("%-33s %4s %6s" % ("Name", "ID", "Weight"))
+    row = lambda d: print("%-33s %4d %6d" % (d["name"], d["id"], d["weight"]))
+    if not a.dom:
+        pools = _sched_pools(c, "credit2", a.pool)
+        if pools is None:
+            return 3
+        doms = c.call("domain_list")
+        for p in pools:
+            print("Cpupool %s:" % p["name"])
+            hdr()
+            for d in doms:
+                if d["pool"] == p["id"]:
+                    row(c.call("domain_sched_ext_get", domain=d["id"]))
+        return 0
+    try:
+        if a.weight is None:
+            hdr()
+            row(c.call("domain_sched_ext_get", domain=a.dom))
+        else:
+            c.call("domain_sched_ext_set", domain=a.dom, weight=a.weight)
+        return 0
+    except RpcError as e:
+        _err(str(e))
+        if a.weight is not None:
+            _err("libxl_domain_sched_params_set failed.")
+        return 3
+
+
+def cmd_sched_sedf(c: Client, argv: List[str]) -> int:
+    """xl sched-sedf (xl_cmdimpl.c:5007-5110).  Times are in ms, as in xl."""
+    ap = argparse.ArgumentParser(prog="gpbsctl sched-sedf", add_help=True)
+    ap.add_argument("-d", "--domain", "--tenant", dest="dom")
+    ap.add_argument("-p", "--period", type=int)
+    ap.add_argument("-s", "--slice", type=int)
+    ap.add_argument("-l", "--latency", type=int)
+    ap.add_argument("-e", "--extra", type=int)
+    ap.add_argument("-w", "--weight", type=int)
+    ap.add_argument("-c", "--cpupool", "--pool", dest="pool")
+    a = ap.parse_args(argv)
+    opts = [x is not None for x in (a.period, a.slice, a.latency, a.extra, a.weight)]
+    if a.pool is not None and (a.dom or any(opts)):
+        _err("Specifying a cpupool is not allowed with other options.")
+        return 1
+    if not a.dom and any(opts):
+        _err("Must specify a domain.")
+        return 1
+    if a.weight is not None and (a.period is not None or a.slice is not None):
+        _err("Specifying a weight AND period or slice is not allowed.")
+    hdr = lambda: print("%-33s %4s %6s %-6s %7s %5s %6s" % ("Name", "ID", "Period", "Slice", "Latency", "Extra",
+                                                           "Weight"))
+    row = lambda d: print("%-33s %4d %6d %6d %7d %5d %6d" % (d["name"], d["id"], d["period_us"] // 1000,
+                                                            d["slice_us"] // 1000, d["latency_us"] // 1000,
+                                                            d["extratime"], d["weight"]))
+    if not a.dom:
+        pools = _sched_pools(c, "sedf", a.pool)
+        if pools is None:
+            return 3
+        doms = c.call("domain_list")
+        for p in pools:
+            print("Cpupool %s:" % p["name"])
+            hdr()
+            for d in doms:
+                if d["pool"] == p["id"]:
+                    row(c.call("domain_sched_ext_get", domain=d["id"]))
+        return 0
+    try:
+        if not any(opts):
+            hdr()
+            row(c.call("domain_sched_ext_get", domain=a.dom))
+            return 0
+        cur = c.call("domain_sched_ext_get", domain=a.dom)
+        kw = dict(weight=0, period_us=cur["period_us"], slice_us=cur["slice_us"], latency_us=-1, extratime=-1)
+        if a.period is not None:
+            kw["period_us"] = a.period * 1000
+        if a.slice is not None:
+            kw["slice_us"] = a.slice * 1000
+        if a.latency is not None:
+            kw["latency_us"] = a.latency * 1000
+        if a.extra is not None:
+            kw["extratime"] = a.extra
+        if a.weight is not None:
+            kw.update(weight=a.weight, period_us=0, slice_us=0)
+        elif cur["weight"] and a.period is None and a.slice is None:
+            kw.update(weight=cur["weight"], period_us=0, slice_us=0)  # -l / -e on a weight-driven tenant
+        c.call("domain_sched_ext_set", domain=a.dom, **kw)
+        return 0
+    except RpcError as e:
+        _err(str(e))
+        _err("libxl_domain_sched_params_set failed.")
         return 3
 
 
@@ -189,6 +309,10 @@ def main(argv: Optional[List[str]] = None) -> int:
     try:
         if cmd == "sched-credit":
             return cmd_sched_credit(c, rest)
+        if cmd == "sched-credit2":
+            return cmd_sched_credit2(c, rest)
+        if cmd == "sched-sedf":
+            return cmd_sched_sedf(c, rest)
         if cmd == "list":
             return cmd_list(c, rest)
         if cmd in ("slot-list", "vcpu-list"):

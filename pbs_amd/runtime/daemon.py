@@ -180,6 +180,22 @@ class Daemon:
             self.engine.sched_credit_set(t, weight, cap)
             return self.domain_sched_get(t)
 
+    def domain_sched_ext_get(self, domain):
+        """xl sched-credit2 / sched-sedf -d: scheduler-specific parameters."""
+        t = self._resolve(domain)
+        x = self.engine.sched_ext_get(t)
+        i = self.engine.tenant_info(t)
+        x.update({"id": t, "name": i.name, "pool": i.pool, "sched": self.engine.pool_info(i.pool)["sched"]})
+        return x
+
+    def domain_sched_ext_set(self, domain, weight: int = 0, period_us: int = 0, slice_us: int = 0,
+                             latency_us: int = -1, extratime: int = -1):
+        with self.lock:
+            t = self._resolve(domain)
+            self.engine.sched_ext_set(t, weight=int(weight), period_us=int(period_us), slice_us=int(slice_us),
+                                      latency_us=int(latency_us), extratime=int(extratime))
+            return self.domain_sched_ext_get(t)
+
     def pool_params_get(self, pool=None):
         p = self._pool(pool)
         ts, rl = self.engine.sched_params_get(p)
@@ -377,6 +393,7 @@ class Daemon:
 
     def _handlers(self):
         names = ["info", "create", "destroy", "domain_list", "domain_sched_get", "domain_sched_set",
+                 "domain_sched_ext_get", "domain_sched_ext_set",
                  "pool_params_get", "pool_params_set", "pool_list", "pool_create", "pool_destroy", "pool_rename",
                  "pool_cpu_add", "pool_cpu_remove", "pool_migrate", "pool_xgmi_split", "pause", "unpause",
                  "slot_list", "slot_pin", "slot_set", "debug_keys", "dmesg", "trace", "perfc", "top", "register",

@@ -147,3 +147,41 @@ def test_snapshot_restore_roundtrip(daemon, tmp_path):
         assert "keep" in out and " 700  150" in out
     finally:
         d2.stop()
+
+
+def test_sched_credit2_and_sedf_verbs(daemon):
+    """xl sched-credit2 / sched-sedf (xl_cmdimpl.c:4675-4726, 4932-5110):
+    pools running those schedulers, list / show / set, formats and errors."""
+    assert run(daemon, "pool-gpu-remove", "Pool-0", "node:1")[0] == 0
+    assert run(daemon, "pool-create", "c2", "--sched", "credit2")[0] == 0
+    assert run(daemon, "pool-gpu-add", "c2", "node:1")[0] == 0
+    run(daemon, "create", "a", "--pool", "c2")
+    rc, out, _ = run(daemon, "sched-credit2")
+    assert rc == 0 and "Cpupool c2:" in out
+    assert "%-33s %4s %6s" % ("Name", "ID", "Weight") in out
+    assert run(daemon, "sched-credit2", "-d", "a", "-w", "768")[0] == 0
+    rc, out, _ = run(daemon, "sched-credit2", "-d", "a")
+    assert out.splitlines()[1].split()[-1] == "768"
+    rc, _, err = run(daemon, "sched-credit2", "-p", "c2", "-w", "3")
+    assert rc == 1 and "Specifying a cpupool is not allowed with other options." in err
+    rc, _, err = run(daemon, "sched-credit2", "-w", "3")
+    assert rc == 1 and "Must specify a domain." in err
+    # sedf pool on a split of Pool-0
+    assert run(daemon, "pool-create", "edf", "--sched", "sedf")[0] == 0
+    assert run(daemon, "pool-gpu-remove", "Pool-0", "3")[0] == 0
+    assert run(daemon, "pool-gpu-add", "edf", "3")[0] == 0
+    run(daemon, "create", "rt", "--pool", "edf")
+    assert run(daemon, "sched-sedf", "-d", "rt", "-p", "20", "-s", "5", "-e", "0")[0] == 0
+    rc, out, _ = run(daemon, "sched-sedf", "-d", "rt")
+    hdr = "%-33s %4s %6s %-6s %7s %5s %6s" % ("Name", "ID", "Period", "Slice", "Latency", "Extra", "Weight")
+    assert out.splitlines()[0] == hdr
+    assert out.splitlines()[1].split()[2:] == ["20", "5", "0", "0", "0"]
+    rc, _, err = run(daemon, "sched-sedf", "-d", "rt", "-p", "20", "-s", "30")
+    assert rc != 0 and "failed" in err  # slice > period
+    rc, out, _ = run(daemon, "sched-sedf", "-c", "edf")
+    assert "Cpupool edf:" in out and "rt" in out
+    rc, _, err = run(daemon, "sched-sedf", "-c", "edf", "-p", "3")
+    assert rc == 1 and "Specifying a cpupool is not allowed with other options." in err
+    # the credit verbs do not apply to a credit2 / sedf tenant's pool
+    rc, out, _ = run(daemon, "sched-credit")
+    assert "Cpupool c2:" not in out and "Cpupool edf:" not in out
