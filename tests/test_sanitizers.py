@@ -26,6 +26,21 @@ for i in range(2000):
         e.pin(b, i % 4, [i % 8, (i + 3) % 8])
 e.debug_keys("rqz"); e.trace(from_start=True)
 assert e.check() == "", e.check()
+# S4 pools side by side: credit2 and sedf, tenants moved between them
+for name, sched, parts in (("c2", "credit2", (4, 5)), ("edf", "sedf", (6, 7))):
+    p = e.pool_create(name, sched)
+    for q in parts:
+        e.pool_unassign(0, q); e.pool_assign(p, q)
+c = e.tenant_create("c", nslots=2, pool=e.pool_find("c2")); d = e.tenant_create("d", nslots=2, pool=e.pool_find("edf"))
+e.sched_ext_set(d, period_us=2000, slice_us=500, latency_us=200, extratime=1)
+e.wake(c); e.wake(d)
+for i in range(1500):
+    e.advance(e.now() + 50_000)
+    if i % 200 == 0:
+        e.block(d); e.advance(e.now() + 5_000_000); e.wake(d)
+        e.tenant_move(c, e.pool_find("edf") if i % 400 == 0 else e.pool_find("c2"))
+e.debug_keys("rqz")
+assert e.check() == "", e.check()
 e.close()
 # real clock: dispatcher thread vs. concurrent wake/block/adjust from 4 threads
 r = Engine(partitions=[(0, x) for x in range(8)])
