@@ -347,22 +347,37 @@ int Engine::tenant_create(const std::string& name, int poolid, int nslots, int w
     return rc;
   }
   perfc.incr(PC_dom_init);
-  // Slot 0 goes to the least-populated partition of the pool, ties to the
-  // highest-numbered one (default_vcpu0_location, X:xen/common/domctl.c:167-214);
-  // the others cycle from there (:566-569).
-  int cpu = pl->cpus.empty() ? 0 : pl->cpus.first();
-  if (!pl->cpus.empty()) {
-    std::vector<int> cnt(parts.size(), 0);
-    for (auto& s : slots)
-      if (s && !s->is_idle() && !(s->pause_flags & VPF_DOWN) && s->processor < (int)cnt.size()) cnt[s->processor]++;
-    for (int c = pl->cpus.first(); c >= 0; c = pl->cpus.next(c + 1))
-      if (cnt[c] <= cnt[cpu]) cpu = c;
-  }
+  // Initial placement: default_vcpu0_location (X:xen/common/domctl.c:167-214)
+  // puts vCPU 0 on the least-populated CPU (ties: highest-numbered) and
+  // cycles the rest from there (:566-569).  gpbs applies the least-populated
+  // rule to every slot, preferring XCDs the tenant does not occupy yet: the
+  // cycle stacks slots of different tenants on one partition while another
+  // idles, which schedulers without load balancing (sedf, static) never undo.
+  std::vector<int> cnt(parts.size(), 0);
+  for (auto& s : slots)
+    if (s && !s->is_idle() && !(s->pause_flags & VPF_DOWN) && s->processor < (int)cnt.size()) cnt[s->processor]++;
+  std::vector<int> mine;  // partitions holding this tenant's slots so far
+  auto place = [&]() {
+    int best = pl->cpus.empty() ? 0 : pl->cpus.first(), bkey = INT32_MAX;
+    for (int c = pl->cpus.first(); c >= 0; c = pl->cpus.next(c + 1)) {
+      int same_xcd = 0;
+      for (int m : mine) same_xcd += parts[m]->gpu == parts[c]->gpu && parts[m]->xcd == parts[c]->xcd;
+      const int key = cnt[c] * 1024 + same_xcd;
+      if (key <= bkey) {
+        bkey = key;
+        best = c;
+      }
+    }
+    return best;
+  };
   for (int i = 0; i < nslots; ++i) {
     auto s = std::make_unique<Slot>();
     s->id = (int)slots.size();
     s->tenant = d.id;
     s->index = i;
+    const int cpu = place();
+    cnt[cpu]++;
+    mine.push_back(cpu);
     s->processor = cpu;
     s->affinity = Mask::all(kMaxPartitions);  // setall (schedule.c:201)
     s->pause_flags = VPF_BLOCKED;             // no work yet
@@ -374,7 +389,6 @@ int Engine::tenant_create(const std::string& name, int poolid, int nslots, int w
     pl->sched->alloc_vdata(v);
     pl->sched->insert_vcpu(v);
     perfc.incr(PC_vcpu_init);
-    if (!pl->cpus.empty()) cpu = pl->cpus.cycle(cpu);  // spread initial placement
   }
   int w = weight, c = cap;
   if (w != -1 || c != -1) pl->sched->adjust(d, true, &w, &c);

@@ -67,8 +67,8 @@ struct SedfSlot : SchedSlotData {
   bool on_extra[2] = {false, false};
   int64_t period_begin() const { return deadl_abs - period; }
 };
-struct SedfDom : SchedTenantData {
-  int64_t period = kWeightPeriod, slice = 0, latency = 0;
+struct SedfDom : SchedTenantData {  // xl-visible parameters, in us
+  int64_t period = kWeightPeriod / kUs, slice = 0, latency = 0;
   int extratime = 1, weight = 0;
 };
 struct SedfPcpu : SchedPartData {
