@@ -209,13 +209,13 @@ def test_pools_with_different_schedulers_side_by_side():
     assert e.check() == ""
 
 
-@pytest.mark.parametrize("sched", ["credit", "credit2", "sedf", "static"])
+@pytest.mark.parametrize("sched", ["credit", "credit2", "sedf"])
 def test_initial_placement_spreads_slots_for_every_scheduler(sched):
     """Every slot starts on the least-populated partition, preferring XCDs the
     tenant does not occupy yet (default_vcpu0_location applied per slot):
     three 8-slot tenants on 8 XCDs x 4 contexts land one slot per XCD each and
-    never share a partition -- schedulers without load balancing (sedf,
-    static) would otherwise keep a stacked partition busy next to an idle one.
+    never share a partition -- a scheduler without load balancing (sedf)
+    would otherwise keep a stacked partition busy next to an idle one.
     Regression: sedf ran such a mix at 3.5 of 8 partitions per tenant."""
     e = Engine(sched=sched, sim_clock=True, partitions=[(0, x, c) for x in range(8) for c in range(4)])
     e.tenant_create("Domain-0", nslots=1)
@@ -225,8 +225,6 @@ def test_initial_placement_spreads_slots_for_every_scheduler(sched):
     assert len(set(flat)) == len(flat), procs
     for t in ts:
         assert sorted(p // 4 for p in procs[t]) == list(range(8)), procs  # one per XCD
-    if sched == "static":
-        return  # the ARINC splitter re-homes slots onto each tenant's own partitions
     for t in ts:
         e.wake(t)
     s = share(e, ts, dur_ms=100)
