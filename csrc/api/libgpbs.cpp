@@ -477,6 +477,15 @@ int gpbs_sched_ext(gpbs_engine_t* e, int t, int set, gpbs_sched_ext_t* p) {
   return r;
 }
 
+int gpbs_atc_sync(gpbs_engine_t* e, int pool, int global_min_us) {
+  LOCK(e);
+  Pool* p = e->e->pool(pool);
+  if (!p) return GPBS_ENOENT;
+  int r = p->sched->atc_sync(global_min_us);
+  DONE(e);
+  return r;
+}
+
 int gpbs_sched_params_get(gpbs_engine_t* e, int pool, int* tslice_us, int* ratelimit_us) {
   LOCK(e);
   Pool* p = e->e->pool(pool);

@@ -656,6 +656,9 @@ class CreditScheduler : public Scheduler {
       mn = std::min(mn, d.atc.tslice_us);
     }
     if (doms.empty()) return;
+    atc_local_min_ = mn;
+    // K11: the node-wide minimum from the other GPUs' pools (atc_sync), while fresh.
+    if (atc_ext_min_ && E.now() < atc_ext_until_) mn = std::min(mn, atc_ext_min_);
     for (int tid : doms) {
       CDom& d = sd(*E.tenants[tid]);
       d.atc.tslice_us = mn;
@@ -665,6 +668,30 @@ class CreditScheduler : public Scheduler {
     recompute();
     E.perfc.incr(PC_atc_apply);
     E.emit(TRC_ATC, master_, mn, (uint32_t)doms.size());
+  }
+
+  // ATC across GPUs: the reference applies the minimum slice of
+  // all domains every 21 ms; with one engine per GPU, the ranks MIN-reduce
+  // their local minima (parallel/gang.py) and apply the node-wide one here.
+  // Returns the local minimum of the last apply; a fresh global minimum is
+  // applied at once and folded into the next applies for 3 periods.
+  int atc_sync(int global_min_us) override {
+    if (mode_ != Mode::ATC) return GPBS_EINVAL;
+    if (global_min_us > 0) {
+      atc_ext_min_ = (uint32_t)global_min_us;
+      atc_ext_until_ = E.now() + 3 * (int64_t)slice_period_us() * 1000;
+      if (atc_ext_min_ < tslice_us_) {
+        for (int tid : active_sdom_) {
+          CDom& d = sd(*E.tenants[tid]);
+          d.atc.tslice_us = atc_ext_min_;
+          d.atc.hist[3].tslice = atc_ext_min_;
+        }
+        tslice_us_ = atc_ext_min_;
+        recompute();
+        E.emit(TRC_ATC, master_, atc_ext_min_, (uint32_t)active_sdom_.size());
+      }
+    }
+    return (int)(atc_local_min_ ? atc_local_min_ : tslice_us_);
   }
 
   // ----------------------------------------------------- wake / sleep ----
@@ -1263,6 +1290,8 @@ class CreditScheduler : public Scheduler {
   int32_t credit_balance_ = 0;
   uint32_t runq_sort_ = 0;
   uint32_t ratelimit_us_ = 0, tslice_us_ = 0, tick_period_us_ = 0, ticks_per_tslice_ = 3, credits_per_tslice_ = 0;
+  uint32_t atc_local_min_ = 0, atc_ext_min_ = 0;
+  int64_t atc_ext_until_ = 0;
   int last_tickle_cpu_ = 0;
 };
 

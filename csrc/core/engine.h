@@ -140,6 +140,8 @@ class Scheduler {
   virtual int adjust_global(bool set, int* tslice_us, int* ratelimit_us) = 0;
   // Scheduler-specific tenant parameters (credit2 weight, sedf reservation).
   virtual int adjust_ext(Tenant&, bool, gpbs_sched_ext_t&) { return GPBS_EINVAL; }
+  // ATC across GPUs: local minimum slice out, node-wide minimum in (us).
+  virtual int atc_sync(int) { return GPBS_EINVAL; }
   virtual void dump_settings(std::string& out) = 0;
   virtual void dump_cpu_state(int part, std::string& out) = 0;
   virtual void dump_admin_conf(std::string& out) = 0;

@@ -152,6 +152,9 @@ typedef struct gpbs_partition_info {
 
 /* --- scheduler-specific tenant parameters (S4: credit2, sedf) --- */
 int gpbs_sched_ext(gpbs_engine_t* e, int tenant, int set, gpbs_sched_ext_t* p);
+/* ATC pool across GPUs: applies global_min_us (> 0) and returns the pool's
+ * local minimum slice of its last apply (us); GPBS_EINVAL if not ATC. */
+int gpbs_atc_sync(gpbs_engine_t* e, int pool, int global_min_us);
 
 /* --- lifecycle --- */
 void gpbs_boot_defaults(gpbs_boot_params_t* p);

@@ -167,6 +167,7 @@ def load_core(build_if_missing=True):
         P(lib, "gpbs_sched_credit_get", C.c_int, E, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int))
         P(lib, "gpbs_sched_credit_set", C.c_int, E, C.c_int, C.c_int, C.c_int)
         P(lib, "gpbs_sched_ext", C.c_int, E, C.c_int, C.c_int, C.POINTER(SchedExt))
+        P(lib, "gpbs_atc_sync", C.c_int, E, C.c_int, C.c_int)
         P(lib, "gpbs_sched_params_get", C.c_int, E, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int))
         P(lib, "gpbs_sched_params_set", C.c_int, E, C.c_int, C.c_int, C.c_int)
         P(lib, "gpbs_sched_name", C.c_int, E, C.c_int, C.c_char_p, C.c_int)

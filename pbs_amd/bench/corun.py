@@ -253,8 +253,11 @@ class Corun:
                 # ranks on all GPUs get their partitions in the same epochs.
                 from ..parallel.gang import GangCoordinator
                 # own gloo group: the main thread's barriers use "ctrl"
+                # The same epochs SUM-reduce the throughput tenants' counters
+                # into node-wide metrics (C11).
                 self.gang = GangCoordinator(e, self.groups["gang"], [self.tid["coll"]],
-                                            epoch_ms=self.cfg.gang_epoch_ms, share=self.cfg.gang_share).start()
+                                            epoch_ms=self.cfg.gang_epoch_ms, share=self.cfg.gang_share,
+                                            metric_tenants=[self.tid[n] for n in self.throughput]).start()
             return
         self.ctx.set_table_mode("host")
         self.ctx.set_spatial(False)
@@ -434,6 +437,8 @@ class Corun:
                              for n, r in self.runners.items() if isinstance(r, Runner)}
             if self.gang is not None:
                 eng["gang"] = self.gang.stats()
+                names = {v: k for k, v in self.tid.items()}
+                eng["node_metrics"] = {names.get(t, t): m for t, m in self.gang.node_metrics.items()}
             res["engine"] = eng
             diag = os.environ.get("GPBS_DIAG_DIR")
             if diag and self.rank == 0:

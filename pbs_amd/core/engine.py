@@ -281,6 +281,11 @@ class Engine:
         self._chk(self.lib.gpbs_sched_ext(self.h, t, 1, C.byref(x)), "sched_ext_set")
         return {k: getattr(x, k) for k, _ in N.SchedExt._fields_}
 
+    def atc_sync(self, pool: int = 0, global_min_us: int = 0) -> int:
+        """ATC pool across GPUs: apply a node-wide minimum slice (> 0) and
+        return this pool's local minimum (us) of its last apply."""
+        return self._chk(self.lib.gpbs_atc_sync(self.h, pool, int(global_min_us)), "atc_sync")
+
     def sched_params_get(self, pool: int = 0):
         ts, rl = C.c_int(), C.c_int()
         self._chk(self.lib.gpbs_sched_params_get(self.h, pool, C.byref(ts), C.byref(rl)), "sched_params_get")

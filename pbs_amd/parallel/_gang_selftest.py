@@ -43,3 +43,44 @@ def worker(rank: int, world: int, port: int, q, seconds: float = 0.8, epoch_ms: 
     e.stop()
     q.put({"rank": rank, "samples": samples, "history": g.history, "stats": st, "favour": FAVOUR})
     dist.destroy_process_group()
+
+
+def atc_worker(rank: int, world: int, port: int, q, seconds: float = 0.8, epoch_ms: float = 5.0):
+    """Node-level sync over the gang epochs: an ATC pool per rank (rank 0's
+    tenant reports heavy spin-waits, so its local minimum slice is small) and
+    per-rank counters; returns each rank's applied slice and node metrics."""
+    import torch.distributed as dist
+
+    from pbs_amd.core.engine import Engine
+    from pbs_amd.parallel.gang import GangCoordinator
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    e = Engine(sched="atc", partitions=[(rank, x) for x in range(2)], quantum_align_us=0)
+    e.tenant_create("Domain-0", nslots=1)
+    t = e.tenant_create("t", nslots=2)
+    e.start()
+    e.wake(t)
+    g = GangCoordinator(e, None, [t], epoch_ms=epoch_ms, share=0.0, atc_pool=0, metric_tenants=[t],
+                        metric_every=2).start()
+    t_end = time.monotonic() + seconds
+    k = 0
+    node = {}
+    while time.monotonic() < t_end:
+        k += 1
+        m = g.node_metrics.get(t, {})
+        if m.get("inst", 0) > node.get("inst", 0):
+            node = dict(m)
+        if rank == 0:
+            e.report_wait(t, 200_000)  # heavy lock-holder preemption symptom
+        for s in range(2):  # modeled counters: rank r retires (r+1) x 1e6 instructions per ms
+            e.set_pmc(e.slot_id(t, s), [k * (rank + 1) * 500_000, k * 1_000_000, k * 1000, k * 100 * (rank + 1)])
+        time.sleep(0.001)
+    time.sleep(0.05)
+    local = e.atc_sync(0, 0)
+    g.stop()
+    info = e.tenant_info(t)
+    e.stop()
+    q.put({"rank": rank, "local_min": local, "tslice": info.tslice_us, "stats": g.stats(),
+           "node": node})
+    dist.destroy_process_group()

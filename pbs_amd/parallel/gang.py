@@ -21,6 +21,17 @@ the default group is node-local gloo (shared-memory/TCP loopback, ~50-100 us);
 an RCCL group can be passed instead (``device="cuda"``) to ride xGMI.
 Stopping is collective too: a rank that wants to stop contributes 0 to the
 flag and every rank leaves at the same epoch.
+
+The same epoch carries two node-level exchanges of the reference's
+intra-host traffic:
+
+* ``atc_pool``: the pool's local ATC minimum slice rides the MIN vector and
+  the node-wide minimum is applied on every GPU (sched_credit_atc.c applies
+  the global minimum to every domain each 21 ms period);
+* ``metric_tenants``: every ``metric_every`` epochs the tenants' last-period
+  counter deltas (INST, CYCLES, L2 refs, L2 misses) are SUM-reduced, so every
+  rank sees node-wide per-tenant metrics (``node_metrics``) -- the master's
+  cross-CPU pmc gather of csched_dom_metric_update, without a master.
 """
 from __future__ import annotations
 
@@ -32,12 +43,14 @@ import torch
 import torch.distributed as dist
 
 FAVOUR, EXCLUDE, NONE = 1, 2, 0
+NO_ATC = 1 << 30  # MIN-neutral stand-in for "no ATC pool on this rank"
 
 
 class GangCoordinator:
     def __init__(self, engine, group, tenants: List[int], epoch_ms: float = 4.0, share: float = 0.5,
                  device: Optional[str] = None, demand: Optional[Callable[[int], bool]] = None,
-                 slack_ms: float = 1.0):
+                 slack_ms: float = 1.0, atc_pool: Optional[int] = None,
+                 metric_tenants: Optional[List[int]] = None, metric_every: int = 5):
         self.engine = engine
         self.group = group
         self.tenants = list(tenants)
@@ -53,6 +66,12 @@ class GangCoordinator:
         self._want_stop = False
         self._th: Optional[threading.Thread] = None
         self.error: Optional[BaseException] = None
+        self.atc_pool = atc_pool
+        self.atc_global_us = 0
+        self.metric_tenants = list(metric_tenants or [])
+        self.metric_every = max(1, int(metric_every))
+        self.node_metrics: Dict[int, Dict[str, int]] = {}
+        self.metric_syncs = 0
 
     # ------------------------------------------------------------ demand
     def _engine_demand(self, t: int) -> bool:
@@ -91,7 +110,8 @@ class GangCoordinator:
         try:
             while True:
                 t0 = time.monotonic_ns()
-                vec = [1 if self.demand(t) else 0 for t in self.tenants] + [0 if self._want_stop else 1]
+                vec = [1 if self.demand(t) else 0 for t in self.tenants]
+                vec += [self._atc_local(), 0 if self._want_stop else 1]
                 buf = torch.tensor(vec, dtype=torch.int32, device=dev)
                 dist.all_reduce(buf, op=dist.ReduceOp.MIN, group=self.group)
                 red = buf.tolist()
@@ -101,7 +121,12 @@ class GangCoordinator:
                     del self.lat_ns[:2048]
                 if not red[-1]:
                     break
-                dec = self.decide(self.epoch, red[:-1])
+                if self.atc_pool is not None and 0 < red[-2] < NO_ATC:
+                    self.atc_global_us = red[-2]
+                    self.engine.atc_sync(self.atc_pool, red[-2])
+                if self.metric_tenants and self.epoch % self.metric_every == 0:
+                    self._sync_metrics(dev)
+                dec = self.decide(self.epoch, red[:-2])
                 until = self.engine.now() + self.epoch_ns + self.slack_ns
                 for t, st in dec.items():
                     self.engine.gang_set(t, st, until)
@@ -122,6 +147,34 @@ class GangCoordinator:
                 except Exception:
                     pass
 
+    def _atc_local(self) -> int:
+        if self.atc_pool is None:
+            return NO_ATC
+        try:
+            v = self.engine.atc_sync(self.atc_pool, 0)
+        except Exception:
+            return NO_ATC
+        return v if v > 0 else NO_ATC
+
+    def _sync_metrics(self, dev):
+        """SUM-reduce the metric tenants' last-period counter deltas."""
+        vals = []
+        for t in self.metric_tenants:
+            try:
+                vals += [int(x) for x in self.engine.tenant_info(t).pmc]
+            except Exception:
+                vals += [0, 0, 0, 0]
+        buf = torch.tensor(vals, dtype=torch.int64, device=dev)
+        dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group)
+        red = buf.tolist()
+        out = {}
+        for i, t in enumerate(self.metric_tenants):
+            inst, cyc, ref, miss = red[4 * i:4 * i + 4]
+            out[t] = {"inst": inst, "cycles": cyc, "l2_refs": ref, "l2_misses": miss,
+                      "miss_rate": miss * 100000 // inst if inst else 0}
+        self.node_metrics = out
+        self.metric_syncs += 1
+
     def start(self):
         self._th = threading.Thread(target=self._loop, daemon=True, name="gpbs-gang")
         self._th.start()
@@ -137,4 +190,5 @@ class GangCoordinator:
 
     def stats(self) -> Dict[str, float]:
         lat = sorted(self.lat_ns) or [0]
-        return {"epochs": self.epoch, "sync_p50_us": lat[len(lat) // 2] / 1e3, "sync_max_us": lat[-1] / 1e3}
+        return {"epochs": self.epoch, "sync_p50_us": lat[len(lat) // 2] / 1e3, "sync_max_us": lat[-1] / 1e3,
+                "atc_global_us": self.atc_global_us, "metric_syncs": self.metric_syncs}

@@ -52,3 +52,31 @@ def test_two_ranks_gang_schedule_the_collective_tenant():
         assert statistics.mean(fav) > 0.7, (r, statistics.mean(fav))
         assert statistics.mean(exc) < 0.2, (r, statistics.mean(exc))
         assert out[r]["stats"]["epochs"] >= 20
+
+
+def test_two_ranks_share_atc_minimum_and_node_metrics():
+    """K11 / C11 over the gang epochs: each GPU's ATC pool computes a local
+    minimum slice, the node-wide minimum is applied on every rank, and the
+    tenants' counters are SUM-reduced into node-wide metrics."""
+    from pbs_amd.parallel._gang_selftest import atc_worker
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=atc_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = {}
+    for _ in ps:
+        r = q.get(timeout=120)
+        out[r["rank"]] = r
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    lo, hi = sorted((out[0]["local_min"], out[1]["local_min"]))
+    assert lo < hi, out  # the spinning rank wants a shorter slice
+    for r in (0, 1):
+        assert out[r]["tslice"] == lo, out  # node-wide minimum applied everywhere
+        assert out[r]["stats"]["atc_global_us"] == lo
+        assert out[r]["stats"]["metric_syncs"] > 0
+    # node metrics agree on both ranks and include both ranks' instructions
+    assert out[0]["node"] and out[0]["node"]["inst"] > 0
