@@ -28,7 +28,7 @@ static_assert(sizeof(gpbs_adapt_params_t) == sizeof(AdaptParams), "adapt params 
 static_assert(sizeof(gpbs_atc_params_t) == sizeof(AtcParams), "atc params layout");
 static_assert(sizeof(gpbs_trace_record_t) == sizeof(TraceRecord), "trace layout");
 
-#define LOCK(E) std::lock_guard<std::recursive_mutex> _g((E)->e->mu)
+#define LOCK(E) Engine::ApiLock _g((E)->e)
 #define DONE(E)                 \
   do {                          \
     (E)->e->process_softirqs(); \
@@ -64,8 +64,10 @@ int gpbs_tenant_unpause(gpbs_engine_t* e, int t) {
   Tenant* d = live(e, t);
   if (!d) return GPBS_ENOENT;
   if (d->pause_count == 0) return GPBS_EINVAL;
-  if (--d->pause_count == 0)
+  if (--d->pause_count == 0) {
+    d->shutdown = 0;  // operator restart of a watchdog-shut-down tenant
     for (int sid : d->slots) e->e->vcpu_wake(*e->e->slots[sid]);
+  }
   d->last_heartbeat = e->e->now();
   DONE(e);
   return GPBS_OK;
@@ -378,6 +380,7 @@ int gpbs_tenant_info(gpbs_engine_t* e, int t, gpbs_tenant_info_t* o) {
   o->nslots = (int)d->slots.size();
   o->paused = d->pause_count;
   o->alive = d->alive;
+  o->shutdown = d->shutdown;
   copy_str(d->name, o->name, sizeof(o->name));
   if (Scheduler* S = E.sched_of_tenant(t)) S->fill_tenant_info(*d, *o);
   const int64_t n = E.now();
@@ -653,6 +656,28 @@ int gpbs_check_invariants(gpbs_engine_t* e, char* out, int len) {
   std::string s = e->e->check_invariants();
   copy_str(s, out, len);
   return s.empty() ? 0 : 1;
+}
+
+int gpbs_lockprof(gpbs_engine_t* e, gpbs_lockprof_t* out, int reset) {
+  LockProfile& p = e->e->lockprof;
+  if (out) {
+    out->lock_cnt = p.lock_cnt.load();
+    out->block_cnt = p.block_cnt.load();
+    out->time_block_ns = p.time_block_ns.load();
+    out->time_hold_ns = p.time_hold_ns.load();
+    out->max_block_ns = p.max_block_ns.load();
+    out->max_hold_ns = p.max_hold_ns.load();
+    out->handoffs = p.handoffs.load();
+  }
+  if (reset) p.reset();
+  return GPBS_OK;
+}
+
+int gpbs_watchdog(gpbs_engine_t* e, int tenant, uint32_t id, uint32_t timeout_ms) {
+  LOCK(e);
+  int rc = e->e->watchdog(tenant, id, timeout_ms);
+  DONE(e);
+  return rc;
 }
 
 }  // extern "C"

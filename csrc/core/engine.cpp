@@ -55,7 +55,7 @@ Engine::Engine(const gpbs_boot_params_t& p) : boot(p) {
 
 Engine::~Engine() {
   stop();
-  std::lock_guard<std::recursive_mutex> g(mu);
+  ApiLock g(this);
   for (auto& p : pools)
     if (p && p->sched) p->sched->deinit();
 }
@@ -413,6 +413,7 @@ int Engine::tenant_destroy(int tid) {
   }
   S->destroy_domain(*d);
   perfc.incr(PC_dom_destroy);
+  watchdog_kill(*d);  // watchdog_domain_destroy
   d->alive = false;
   d->priv.reset();
   for (int sid : d->slots) slots[sid].reset();
@@ -784,6 +785,59 @@ void Engine::heartbeat_check(int64_t n) {
   timer_set(hb_timer_, n + tmo / 2);
 }
 
+// -------------------------------------------------------------- watchdogs ---
+// SCHEDOP_watchdog (X:xen/common/schedule.c:738-788): a tenant arms up to
+// GPBS_WATCHDOGS timers and must re-arm them before they expire; an expired
+// one shuts the tenant down (domain_shutdown(d, SHUTDOWN_watchdog) there; here
+// its slots are paused and its partitions go to the other tenants).  Unlike
+// the heartbeat detector, the deadline is the tenant's own choice.
+
+int Engine::watchdog(int tid, uint32_t id, uint32_t timeout_ms) {
+  Tenant* t = tenant(tid);
+  if (!t || !t->alive) return GPBS_ENOENT;
+  if (id > (uint32_t)GPBS_WATCHDOGS) return GPBS_EINVAL;
+  if (id == 0) {
+    for (int k = 0; k < GPBS_WATCHDOGS; ++k) {
+      if (t->wd_inuse & (1u << k)) continue;
+      t->wd_inuse |= 1u << k;
+      if (t->wd_timer[k] < 0) t->wd_timer[k] = timer_init([this, tid, k](int64_t) { watchdog_fire(tid, k); });
+      timer_set(t->wd_timer[k], now() + (int64_t)timeout_ms * 1000000);
+      return k + 1;
+    }
+    return GPBS_ENOSPC;
+  }
+  const int k = (int)id - 1;
+  if (!(t->wd_inuse & (1u << k))) return GPBS_EINVAL;
+  if (timeout_ms == 0) {
+    timer_stop(t->wd_timer[k]);
+    t->wd_inuse &= ~(1u << k);
+  } else {
+    timer_set(t->wd_timer[k], now() + (int64_t)timeout_ms * 1000000);
+  }
+  return GPBS_OK;
+}
+
+void Engine::watchdog_fire(int tid, int k) {
+  Tenant* t = tenant(tid);
+  if (!t || !t->alive || t->shutdown) return;  // is_shutting_down / is_dying
+  printk(fmt("(GPBS) Watchdog timer %d fired for tenant %d (%s)\n", k + 1, t->id, t->name.c_str()));
+  t->shutdown = GPBS_SHUTDOWN_WATCHDOG;
+  t->pause_count++;
+  for (int sid : t->slots) vcpu_sleep_nosync(*slots[sid]);
+  perfc.incr(PC_watchdog_fired);
+  emit(TRC_DEAD, 0, t->id, GPBS_SHUTDOWN_WATCHDOG);
+  process_softirqs();
+}
+
+void Engine::watchdog_kill(Tenant& t) {
+  for (int k = 0; k < GPBS_WATCHDOGS; ++k)
+    if (t.wd_timer[k] >= 0) {
+      timer_kill(t.wd_timer[k]);
+      t.wd_timer[k] = -1;
+    }
+  t.wd_inuse = 0;
+}
+
 // --------------------------------------------------------- observability ---
 
 void Engine::printk(const std::string& s) {
@@ -916,7 +970,7 @@ std::string Engine::debug_keys(const std::string& keys) {
 
 int Engine::start() {
   if (boot.sim_clock) return GPBS_EINVAL;
-  std::lock_guard<std::recursive_mutex> g(mu);
+  ApiLock g(this);
   if (running_) return GPBS_OK;
   running_ = true;
   thread_ = std::thread([this] { loop(); });
@@ -925,7 +979,7 @@ int Engine::start() {
 
 int Engine::stop() {
   {
-    std::lock_guard<std::recursive_mutex> g(mu);
+    ApiLock g(this);  // counted as a waiter: a dispatcher behind schedule hands off
     if (!running_) return GPBS_OK;
     running_ = false;
   }
@@ -942,23 +996,55 @@ void Engine::kick() {
 void Engine::loop() {
   prctl(PR_SET_TIMERSLACK, 1UL, 0, 0, 0);  // µs-accurate quanta
   std::unique_lock<std::recursive_mutex> lk(mu);
+  uint64_t t_acq = 0;
+  auto held = [&](bool blocked, uint64_t wait_ns) {
+    lock_depth_++;
+    lockprof.acquired(blocked, wait_ns);
+    t_acq = LockProfile::clock_ns();
+  };
+  auto releasing = [&] {
+    lockprof.released(LockProfile::clock_ns() - t_acq);
+    lock_depth_--;
+  };
+  auto relock = [&] {
+    const uint64_t t0 = LockProfile::clock_ns();
+    const bool blocked = !lk.try_lock();
+    if (blocked) lk.lock();
+    held(blocked, LockProfile::clock_ns() - t0);
+  };
+  held(false, 0);
   while (running_) {
     int64_t n = now();
     run_due(n);
     int64_t dl = next_deadline();
     kicked_ = false;
     n = now();
-    if (dl <= n) continue;
+    if (dl <= n) {
+      // Behind schedule: let blocked API callers in before catching up.
+      if (api_waiters_.load(std::memory_order_relaxed) > 0) {
+        lockprof.handoffs.fetch_add(1, std::memory_order_relaxed);
+        releasing();
+        lk.unlock();
+        const int64_t until = mono_ns() + 200000;
+        while (api_waiters_.load(std::memory_order_relaxed) > 0 && mono_ns() < until) std::this_thread::yield();
+        relock();
+      }
+      continue;
+    }
     int64_t wait = dl == INT64_MAX ? 50000000 : dl - n;
     if (wait > 40000) {
+      releasing();
       cv_.wait_for(lk, std::chrono::nanoseconds(wait - 20000), [this] { return kicked_ || !running_; });
+      held(false, 0);
     } else {
       // Final approach: drop the lock and spin-yield so API callers get in.
+      releasing();
       lk.unlock();
       while (mono_ns() < dl && !kicked_) std::this_thread::yield();
-      lk.lock();
+      relock();
     }
   }
+  releasing();
 }
 
 }  // namespace gpbs

@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "../include/gpbs/gpbs.h"
+#include "../obs/lockprof.h"
 #include "../obs/perfc.h"
 #include "../obs/trace.h"
 #include "adapt.h"
@@ -90,6 +91,10 @@ struct Tenant {  // struct domain
   int gang_state = 0;
   int64_t gang_until = 0;
   int gang(int64_t now) const { return now < gang_until ? gang_state : 0; }
+  // Watchdogs (SCHEDOP_watchdog): timer ids, in-use bits, shutdown reason.
+  int wd_timer[GPBS_WATCHDOGS] = {-1, -1};
+  uint32_t wd_inuse = 0;
+  int shutdown = 0;
   std::unique_ptr<SchedTenantData> priv;
 };
 
@@ -188,6 +193,43 @@ class Engine {
   Perfc perfc;
   std::unique_ptr<TraceRing> trace;
   std::recursive_mutex mu;
+  LockProfile lockprof;  // xenlockprof analog for `mu`
+  // API callers blocked on `mu`.  The dispatcher hands the lock off while it
+  // is behind schedule; otherwise a host too slow for the timer periods
+  // (sanitizer builds, oversubscribed CPUs) would starve every API call.
+  std::atomic<int> api_waiters_{0};
+  int lock_depth_ = 0;  // recursion depth of `mu` (only touched with `mu` held)
+  // RAII for C ABI entries: profiles the outermost acquisition.
+  struct ApiLock {
+    Engine* e;
+    uint64_t t_acq = 0;
+    bool outer = false;
+    explicit ApiLock(Engine* x) : e(x) {
+      if (e->mu.try_lock()) {
+        take(false, 0);
+        return;
+      }
+      const uint64_t t0 = LockProfile::clock_ns();
+      e->api_waiters_.fetch_add(1, std::memory_order_relaxed);
+      e->mu.lock();
+      e->api_waiters_.fetch_sub(1, std::memory_order_relaxed);
+      take(true, LockProfile::clock_ns() - t0);
+    }
+    void take(bool blocked, uint64_t wait_ns) {
+      outer = e->lock_depth_++ == 0;
+      if (outer) {
+        e->lockprof.acquired(blocked, wait_ns);
+        t_acq = LockProfile::clock_ns();
+      }
+    }
+    ~ApiLock() {
+      if (outer) e->lockprof.released(LockProfile::clock_ns() - t_acq);
+      e->lock_depth_--;
+      e->mu.unlock();
+    }
+    ApiLock(const ApiLock&) = delete;
+    ApiLock& operator=(const ApiLock&) = delete;
+  };
 
   std::vector<std::unique_ptr<Partition>> parts;
   std::vector<std::unique_ptr<Slot>> slots;
@@ -284,6 +326,9 @@ class Engine {
   int stop();
   void kick();
   void heartbeat_check(int64_t now);
+  int watchdog(int tenant, uint32_t id, uint32_t timeout_ms);
+  void watchdog_fire(int tenant, int id);
+  void watchdog_kill(Tenant& t);
   void classify_tick(int64_t now);
   void set_affinity(Slot& v, const Mask& m, int home = -1);
   void place_class(Slot& v, const Mask& m, int home);

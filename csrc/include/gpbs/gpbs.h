@@ -120,7 +120,7 @@ typedef struct gpbs_tenant_info {
   int32_t id, pool, nslots, weight, cap, paused, alive, active_slots;
   uint32_t tslice_us, tick_period_us, phase, window_left;
   int32_t last_err;
-  int32_t reserved;
+  int32_t shutdown;         /* 0, or GPBS_SHUTDOWN_WATCHDOG */
   int64_t last_curr, last_win;
   uint64_t pmc[4];          /* last per-tenant deltas (INST, CYC, REF, MISS) */
   uint64_t cache_miss_rate, cpi; /* per 100k inst, per 1k inst */
@@ -293,6 +293,21 @@ const char* gpbs_perfc_name(int i);
 int gpbs_perfc_read(gpbs_engine_t* e, uint64_t* out, int max);
 int gpbs_perfc_reset(gpbs_engine_t* e);
 int gpbs_check_invariants(gpbs_engine_t* e, char* out, int len); /* CSCHED_VCPU_CHECK analog; 0 = ok */
+
+/* Lock profile of the engine mutex (xenlockprof analog, X:xen/common/spinlock.c:88-115). */
+typedef struct gpbs_lockprof {
+  uint64_t lock_cnt, block_cnt, time_block_ns, time_hold_ns, max_block_ns, max_hold_ns, handoffs;
+} gpbs_lockprof_t;
+int gpbs_lockprof(gpbs_engine_t* e, gpbs_lockprof_t* out, int reset);
+
+/* Tenant watchdogs (SCHEDOP_watchdog analog, X:xen/common/schedule.c:738-788):
+ * id 0 allocates one of GPBS_WATCHDOGS timers and returns its id (1-based);
+ * id > 0 re-arms it (timeout_ms > 0) or frees it (timeout_ms == 0).  A timer
+ * that expires shuts the tenant down: its slots are paused and its info
+ * reports shutdown = GPBS_SHUTDOWN_WATCHDOG. */
+#define GPBS_WATCHDOGS 2
+#define GPBS_SHUTDOWN_WATCHDOG 4
+int gpbs_watchdog(gpbs_engine_t* e, int tenant, uint32_t id, uint32_t timeout_ms);
 
 #ifdef __cplusplus
 }

@@ -76,7 +76,7 @@ class TraceRecord(C.Structure):
 class TenantInfo(C.Structure):
     _fields_ = [(n, i32) for n in ("id", "pool", "nslots", "weight", "cap", "paused", "alive", "active_slots")] + \
                [(n, u32) for n in ("tslice_us", "tick_period_us", "phase", "window_left")] + \
-               [("last_err", i32), ("reserved", i32), ("last_curr", i64), ("last_win", i64), ("pmc", u64 * 4),
+               [("last_err", i32), ("shutdown", i32), ("last_curr", i64), ("last_win", i64), ("pmc", u64 * 4),
                 ("cache_miss_rate", u64), ("cpi", u64), ("spin_latency", u64), ("report_count", u64),
                 ("pending_requests", u64), ("sched_count", u64), ("run_ns", i64), ("name", C.c_char * 64)]
 
@@ -92,6 +92,11 @@ class PartitionInfo(C.Structure):
     _fields_ = [(n, i32) for n in ("id", "gpu", "xcd", "pool", "curr_tenant", "curr_slot", "runq_len", "idle",
                                    "ctx", "reserved")] + \
                [("switches", u64)]
+
+
+class LockProf(C.Structure):
+    _fields_ = [(n, u64) for n in ("lock_cnt", "block_cnt", "time_block_ns", "time_hold_ns", "max_block_ns",
+                                   "max_hold_ns", "handoffs")]
 
 
 _lock = threading.Lock()
@@ -192,6 +197,8 @@ def load_core(build_if_missing=True):
         P(lib, "gpbs_perfc_read", C.c_int, E, C.POINTER(u64), C.c_int)
         P(lib, "gpbs_perfc_reset", C.c_int, E)
         P(lib, "gpbs_check_invariants", C.c_int, E, C.c_char_p, C.c_int)
+        P(lib, "gpbs_lockprof", C.c_int, E, C.POINTER(LockProf), C.c_int)
+        P(lib, "gpbs_watchdog", C.c_int, E, C.c_int, u32, u32)
         # host-side adaptation helpers (oracle parity tests)
         P(lib, "gpbs_adapt_init", None, C.POINTER(AdaptState), C.POINTER(AdaptParams), u32)
         P(lib, "gpbs_adapt_update", C.c_int, C.POINTER(AdaptState), C.POINTER(AdaptParams), u64, u64, u64, u64)

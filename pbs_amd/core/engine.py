@@ -67,6 +67,7 @@ class TenantInfo:
     pending_requests: int
     sched_count: int
     run_ns: int
+    shutdown: int = 0
 
 
 @dataclass
@@ -220,7 +221,7 @@ class Engine:
                           last_err=o.last_err, last_curr=o.last_curr, last_win=o.last_win, pmc=tuple(o.pmc),
                           cache_miss_rate=o.cache_miss_rate, cpi=o.cpi, spin_latency=o.spin_latency,
                           report_count=o.report_count, pending_requests=o.pending_requests,
-                          sched_count=o.sched_count, run_ns=o.run_ns)
+                          sched_count=o.sched_count, run_ns=o.run_ns, shutdown=o.shutdown)
 
     def slot_info(self, sid: int) -> Dict:
         o = N.SlotInfo()
@@ -379,6 +380,27 @@ class Engine:
 
     def perfc_reset(self):
         return self.lib.gpbs_perfc_reset(self.h)
+
+    def perfc_prometheus(self, prefix: str = "gpbs") -> str:
+        """perfc counters in the Prometheus text exposition format."""
+        lines = [f"# TYPE {prefix}_perfc_total counter"]
+        lines += [f'{prefix}_perfc_total{{name="{k}"}} {v}' for k, v in self.perfc().items()]
+        lp = self.lockprof()
+        lines.append(f"# TYPE {prefix}_lock_seconds_total counter")
+        lines.append(f'{prefix}_lock_seconds_total{{lock="engine",kind="hold"}} {lp["time_hold_ns"] / 1e9:.9f}')
+        lines.append(f'{prefix}_lock_seconds_total{{lock="engine",kind="block"}} {lp["time_block_ns"] / 1e9:.9f}')
+        return "\n".join(lines) + "\n"
+
+    def lockprof(self, reset: bool = False) -> Dict[str, int]:
+        """Engine-mutex lock profile (xenlockprof analog)."""
+        o = N.LockProf()
+        self.lib.gpbs_lockprof(self.h, C.byref(o), int(reset))
+        return {k: getattr(o, k) for k, _ in o._fields_}
+
+    def watchdog(self, t: int, wid: int = 0, timeout_ms: int = 0) -> int:
+        """SCHEDOP_watchdog: wid 0 allocates (returns the id), else re-arm
+        (timeout_ms > 0) or free (0)."""
+        return self._chk(self.lib.gpbs_watchdog(self.h, t, wid, timeout_ms), "watchdog")
 
     def check(self) -> str:
         buf = C.create_string_buffer(1 << 16)

@@ -10,7 +10,8 @@ cpupool -> pool:
     gpbsctl create NAME [--slots N] [--weight W] [--cap C] [--pool P]
     gpbsctl destroy|pause|unpause TENANT
     gpbsctl list | slot-list [TENANT...] | slot-pin TENANT SLOT|all PARTS|all | slot-set TENANT N
-    gpbsctl debug-keys KEYS | dmesg [-c] | top | trace [-n N] | perfc [-r] | info
+    gpbsctl debug-keys KEYS | dmesg [-c] | top | mon [-i S] | trace [-n N] | perfc [-r|--prom] | lockprof [-r] | info
+    gpbsctl watchdog DOMAIN ID TIMEOUT_MS        (SCHEDOP_watchdog: ID 0 allocates, TIMEOUT 0 frees)
     gpbsctl pool-create NAME [--sched S] [--cpus C] | pool-list [-c] [POOL] | pool-destroy POOL
     gpbsctl pool-rename POOL NEW | pool-gpu-add POOL PARTS|node:N | pool-gpu-remove POOL PARTS|node:N
     gpbsctl pool-migrate TENANT POOL | pool-xgmi-split | snapshot PATH | restore PATH
@@ -269,6 +270,34 @@ def cmd_top(c: Client, argv) -> int:
     return 0
 
 
+def cmd_lockprof(c: Client, argv) -> int:
+    """xenlockprof output shape: lock count(time), block count(time)."""
+    p = c.call("lockprof", reset="-r" in argv)
+    print("%-32s: lock:%12d(%8.6fs), block:%12d(%8.6fs)" % ("gpbs engine lock", p["lock_cnt"],
+                                                            p["time_hold_ns"] / 1e9, p["block_cnt"],
+                                                            p["time_block_ns"] / 1e9))
+    print("%-32s: max hold %.1fus, max block %.1fus, dispatcher hand-offs %d" % (
+        "", p["max_hold_ns"] / 1e3, p["max_block_ns"] / 1e3, p["handoffs"]))
+    return 0
+
+
+def cmd_mon(c: Client, argv) -> int:
+    """xenmon: gotten / waited / blocked per tenant over an interval."""
+    ap = argparse.ArgumentParser(prog="gpbsctl mon")
+    ap.add_argument("-i", "--interval", type=float, default=1.0)
+    a = ap.parse_args(argv)
+    c.call("mon", reset=True)
+    import time as _t
+    _t.sleep(max(0.0, a.interval))
+    m = c.call("mon")
+    print("interval %.3fs" % m["interval_s"])
+    print("%-24s %4s %5s %9s %9s %9s %10s" % ("Name", "ID", "Slots", "Gotten%", "Waited%", "Blocked%", "Execs/s"))
+    for r in m["tenants"]:
+        print("%-24s %4d %5d %9.2f %9.2f %9.2f %10.1f" % (r["name"][:24], r["id"], r["slots"], r["gotten_pct"],
+                                                        r["waited_pct"], r["blocked_pct"], r["execs_per_s"]))
+    return 0
+
+
 def cmd_pool_list(c: Client, argv) -> int:
     ap = argparse.ArgumentParser(prog="gpbsctl pool-list")
     ap.add_argument("-c", "--cpus", action="store_true")
@@ -364,8 +393,21 @@ def main(argv: Optional[List[str]] = None) -> int:
                 print(f"{t / 1e9:14.6f} cpu{cpu:<3d} {ev:<10s} {a[0]:>10d} {a[1]:>10d} {a[2]:>10d} {a[3]:>10d}")
             return 0
         if cmd == "perfc":
+            if "--prom" in rest:
+                sys.stdout.write(c.call("perfc_prom"))
+                return 0
             for k, v in c.call("perfc", reset="-r" in rest).items():
                 print(f"{k:<28s} {v}")
+            return 0
+        if cmd == "lockprof":
+            return cmd_lockprof(c, rest)
+        if cmd == "mon":
+            return cmd_mon(c, rest)
+        if cmd == "watchdog":
+            if len(rest) < 3:
+                _err("'gpbsctl watchdog' requires <Domain> <ID> <TimeoutMs>.")
+                return 1
+            print(c.call("watchdog", domain=rest[0], id=int(rest[1]), timeout_ms=int(rest[2])))
             return 0
         if cmd in simple:
             res = simple[cmd](rest)

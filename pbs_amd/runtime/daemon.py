@@ -330,6 +330,50 @@ class Daemon:
             self.engine.perfc_reset()
         return pc
 
+    def perfc_prom(self):
+        """perfc + lock profile in the Prometheus text format (scrape target)."""
+        return self.engine.perfc_prometheus()
+
+    def lockprof(self, reset: bool = False):
+        """xenlockprof analog: the engine mutex's lock/block counts and times."""
+        return self.engine.lockprof(reset=bool(reset))
+
+    def watchdog(self, domain, id: int = 0, timeout_ms: int = 0):
+        """SCHEDOP_watchdog on behalf of a tenant (the shim's watchdog())."""
+        return self.engine.watchdog(self._resolve(domain), int(id), int(timeout_ms))
+
+    def mon(self, reset: bool = False):
+        """xenmon analog (X:tools/xenmon/README): per-tenant share of the
+        interval since the previous call that its slots spent running
+        ("gotten"), runnable but not running ("waited") and blocked, plus
+        dispatches per second, summed over slots and normalised per slot."""
+        now = self.engine.now()
+        cur = {}
+        for t in self.engine.tenants():
+            i = self.engine.tenant_info(t)
+            tot = {"run": 0, "runnable": 0, "blocked": 0, "execs": 0}
+            for k in range(i.nslots):
+                si = self.engine.slot_info(self.engine.slot_id(t, k))
+                tot["run"] += si["run_ns"]
+                tot["runnable"] += si["runnable_ns"]
+                tot["blocked"] += si["blocked_ns"]
+                tot["execs"] += si["sched_count"]
+            cur[t] = (i.name, i.nslots, tot)
+        prev_t, prev = getattr(self, "_mon_prev", (None, {}))
+        self._mon_prev = (now, cur)
+        if reset or prev_t is None or now <= prev_t:
+            return {"interval_s": 0.0, "tenants": []}
+        dt = now - prev_t
+        rows = []
+        for t, (name, n, tot) in cur.items():
+            p = prev.get(t, (name, n, {k: 0 for k in tot}))[2]
+            d = {k: tot[k] - p[k] for k in tot}
+            span = dt * max(1, n)
+            rows.append({"id": t, "name": name, "slots": n, "gotten_pct": 100.0 * d["run"] / span,
+                         "waited_pct": 100.0 * d["runnable"] / span, "blocked_pct": 100.0 * d["blocked"] / span,
+                         "execs_per_s": d["execs"] / (dt / 1e9)})
+        return {"interval_s": dt / 1e9, "tenants": rows}
+
     def top(self):
         """xentop analog: per-tenant share, quantum, phase, miss rate, counters."""
         now = self.engine.now()
@@ -397,7 +441,7 @@ class Daemon:
                  "pool_params_get", "pool_params_set", "pool_list", "pool_create", "pool_destroy", "pool_rename",
                  "pool_cpu_add", "pool_cpu_remove", "pool_migrate", "pool_xgmi_split", "pause", "unpause",
                  "slot_list", "slot_pin", "slot_set", "debug_keys", "dmesg", "trace", "perfc", "top", "register",
-                 "unregister", "snapshot", "restore", "advance_us"]
+                 "unregister", "snapshot", "restore", "advance_us", "perfc_prom", "lockprof", "watchdog", "mon"]
         return {n: getattr(self, n) for n in names}
 
     # ------------------------------------------------------------ reaper
