@@ -1,0 +1,190 @@
+// fp8 (OCP e4m3fn) weight-streaming linear for the Llama inference tenant
+// (BASELINE config #5: "Llama-3-8B inference ... (CDNA4 fp8 MFMA)").
+//
+// Decode is a skinny GEMM: Y[M, N] = X[M, K] . W[N, K]^T with M = batch (<= 64)
+// and N, K in the thousands, so its cost is streaming W from HBM once.  Storing
+// W as fp8 halves those bytes against bf16.  Both operands go through the gfx950
+// fp8 MFMA (v_mfma_f32_16x16x32_fp8_fp8, OCP e4m3); the accumulation is fp32 and
+// the per-row scales are applied in the epilogue:
+//     Y[m, n] = (sum_k Xq[m, k] Wq[n, k]) * sx[m] * sw[n]
+// with sx / sw the absmax / 448 of each activation / weight row
+// (k_quant_rows_fp8 produces both: run over W once at load time, over X per call).
+//
+// Work shape (CDNA4, 64-wide waves): one workgroup per 16 output columns, 8 waves
+// splitting K in 256-byte blocks.  Lane (r = l & 15, g = l >> 4) streams row
+// n0 + r of W, 16 bytes at k = kb + 64u + 16g (u = 0..3), i.e. 64 contiguous bytes
+// per row per u and 8 x 16 B loads in flight per lane.  The A fragment (X rows, from
+// L2) uses the SAME lane -> k permutation, so each MFMA sums a consistent set of 32
+// k's and the product is exact regardless of the hardware's in-fragment k order.
+// The eight wave partials are reduced through LDS.
+#include "common.hpp"
+
+namespace gpbs_fp8 {
+
+using namespace gpbs_hip;
+
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int kWaves = 8;
+constexpr int kThreads = kWaves * 64;
+constexpr int kQuantThreads = 256;
+constexpr float kE4M3Max = 448.0f;
+
+__device__ __forceinline__ float bf_lo(u32 v) { return __uint_as_float(v << 16); }
+__device__ __forceinline__ float bf_hi(u32 v) { return __uint_as_float(v & 0xffff0000u); }
+
+__device__ __forceinline__ unsigned short f2bf(float f) {
+  u32 u = __float_as_uint(f);
+  u += 0x7fffu + ((u >> 16) & 1u);  // round to nearest even
+  return (unsigned short)(u >> 16);
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Per-row symmetric quantisation bf16 -> e4m3fn.  grid = rows, block = 256.
+// x: rows x (k8 * 8) bf16, q: rows x (k8 * 8) fp8, scale[row] = absmax / 448.
+__global__ __launch_bounds__(kQuantThreads) void k_quant_rows_fp8(const u32x4* __restrict__ x, u32x2* __restrict__ q,
+                                                                float* __restrict__ scale, int k8) {
+  __shared__ float red[kQuantThreads / 64];
+  const size_t row = blockIdx.x;
+  const u32x4* xr = x + row * k8;
+  float m = 0.f;
+  for (int i = threadIdx.x; i < k8; i += kQuantThreads) {
+    const u32x4 v = xr[i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) m = fmaxf(m, fmaxf(fabsf(bf_lo(v[e])), fabsf(bf_hi(v[e]))));
+  }
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  float amax = red[0];
+#pragma unroll
+  for (int w = 1; w < kQuantThreads / 64; ++w) amax = fmaxf(amax, red[w]);
+  const float s = amax > 0.f ? amax / kE4M3Max : 1.f;
+  const float inv = amax > 0.f ? kE4M3Max / amax : 1.f;
+  if (threadIdx.x == 0) scale[row] = s;
+  u32x2* qr = q + row * k8;
+  for (int i = threadIdx.x; i < k8; i += kQuantThreads) {
+    const u32x4 v = xr[i];
+    u32x2 o;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float a = fminf(fmaxf(bf_lo(v[2 * h]) * inv, -kE4M3Max), kE4M3Max);
+      const float b = fminf(fmaxf(bf_hi(v[2 * h]) * inv, -kE4M3Max), kE4M3Max);
+      const float c = fminf(fmaxf(bf_lo(v[2 * h + 1]) * inv, -kE4M3Max), kE4M3Max);
+      const float d = fminf(fmaxf(bf_hi(v[2 * h + 1]) * inv, -kE4M3Max), kE4M3Max);
+      int p = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+      p = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, p, true);
+      o[h] = (u32)p;
+    }
+    qr[i] = o;
+  }
+}
+
+__device__ __forceinline__ long lo64(u32x4 v) { return (long)(((u64)v[1] << 32) | v[0]); }
+__device__ __forceinline__ long hi64(u32x4 v) { return (long)(((u64)v[3] << 32) | v[2]); }
+
+// MT = number of 16-row M tiles (M <= 16 * MT).  K % 256 == 0, N % 16 == 0.
+template <int MT>
+__global__ __launch_bounds__(kThreads) void k_fp8_gemm_skinny(const unsigned char* __restrict__ xq,
+                                                              const float* __restrict__ sx,
+                                                              const unsigned char* __restrict__ wq,
+                                                              const float* __restrict__ sw,
+                                                              unsigned short* __restrict__ y, int M, int N, int K) {
+  __shared__ f32x4 red[kWaves][MT][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.x * 16;
+  const int k16 = K >> 4;  // 16-byte units per row
+  const u32x4* wrow = reinterpret_cast<const u32x4*>(wq) + (size_t)(n0 + r) * k16 + g;
+  const u32x4* xb = reinterpret_cast<const u32x4*>(xq);
+  f32x4 acc[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nkb = K >> 8;  // 256-byte blocks
+  for (int kb = w; kb < nkb; kb += 2 * kWaves) {
+    const bool two = kb + kWaves < nkb;
+    u32x4 b0[4], b1[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) b0[u] = __builtin_nontemporal_load(wrow + kb * 16 + u * 4);
+    if (two) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) b1[u] = __builtin_nontemporal_load(wrow + (kb + kWaves) * 16 + u * 4);
+    }
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      const int m = t * 16 + r;
+      const u32x4* xr = xb + (size_t)m * k16 + g;
+      u32x4 a[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] = m < M ? xr[kb * 16 + u * 4] : u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(lo64(a[u]), lo64(b0[u]), acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(hi64(a[u]), hi64(b0[u]), acc[t], 0, 0, 0);
+      }
+      if (two) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) a[u] = m < M ? xr[(kb + kWaves) * 16 + u * 4] : u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(lo64(a[u]), lo64(b1[u]), acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(hi64(a[u]), hi64(b1[u]), acc[t], 0, 0, 0);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < MT; ++t) red[w][t][lane] = acc[t];
+  __syncthreads();
+  // C/D map of 16x16 MFMA: col = lane & 15 (n), row = 4 * (lane >> 4) + i (m).
+  for (int e = threadIdx.x; e < MT * 64; e += kThreads) {
+    const int t = e >> 6, l = e & 63;
+    f32x4 s = red[0][t][l];
+#pragma unroll
+    for (int v = 1; v < kWaves; ++v) s += red[v][t][l];
+    const int n = n0 + (l & 15);
+    const float wsc = sw[n];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = t * 16 + 4 * (l >> 4) + i;
+      if (m < M) y[(size_t)m * N + n] = f2bf(s[i] * sx[m] * wsc);
+    }
+  }
+}
+
+}  // namespace gpbs_fp8
+
+using namespace gpbs_fp8;
+
+extern "C" {
+
+int gpbs_hip_quant_rows_fp8(const void* x, void* q, float* scale, int rows, int k, hipStream_t s) {
+  if (rows <= 0 || k <= 0 || k % 8) return -22;
+  hipLaunchKernelGGL(k_quant_rows_fp8, dim3(rows), dim3(kQuantThreads), 0, s, (const u32x4*)x, (u32x2*)q, scale,
+                     k / 8);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+int gpbs_hip_fp8_linear(const void* xq, const float* sx, const void* wq, const float* sw, void* y, int M, int N, int K,
+                        hipStream_t s) {
+  if (M <= 0 || M > 64 || N <= 0 || N % 16 || K <= 0 || K % 256) return -22;
+  const dim3 grid(N / 16), block(kThreads);
+  const auto* xp = (const unsigned char*)xq;
+  const auto* wp = (const unsigned char*)wq;
+  auto* yp = (unsigned short*)y;
+  if (M <= 16)
+    hipLaunchKernelGGL(k_fp8_gemm_skinny<1>, grid, block, 0, s, xp, sx, wp, sw, yp, M, N, K);
+  else if (M <= 32)
+    hipLaunchKernelGGL(k_fp8_gemm_skinny<2>, grid, block, 0, s, xp, sx, wp, sw, yp, M, N, K);
+  else
+    hipLaunchKernelGGL(k_fp8_gemm_skinny<4>, grid, block, 0, s, xp, sx, wp, sw, yp, M, N, K);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+}  // extern "C"

@@ -122,6 +122,42 @@ class Block(nn.Module):
         o = F.scaled_dot_product_attention(q.transpose(1, 2), k_all, v_all, is_causal=(S > 1), enable_gqa=True)
         return self.wo(o.transpose(1, 2).reshape(B, S, cfg.n_heads * hd))
 
+    def attach_fp8(self):
+        """Quantise this block's linears to e4m3fn for the fp8 decode path:
+        q/k/v packed into one [(H + 2 Hkv) hd, dim] weight, gate/up into one
+        [2 ffn, dim] weight, so a decode step streams each layer in 4 launches."""
+        from ..ops import llm
+        self._fp8 = {
+            "qkv": llm.Fp8Weight(torch.cat([self.wq.weight, self.wk.weight, self.wv.weight], 0)),
+            "o": llm.Fp8Weight(self.wo.weight),
+            "w13": llm.Fp8Weight(torch.cat([self.w1.weight, self.w3.weight], 0)),
+            "w2": llm.Fp8Weight(self.w2.weight),
+        }
+
+    def forward_fp8(self, x, cos, sin, cache, pos: int):
+        """Decode/prefill block on fp8 weights (fp8 MFMA linears + fused gfx950
+        RMSNorm/RoPE/SwiGLU); inference only."""
+        from ..ops import llm
+        cfg, hd, f = self.cfg, self.cfg.head_dim, self._fp8
+        B, S, _ = x.shape
+        h = llm.rmsnorm(x, self.attn_norm.weight, self.attn_norm.eps)
+        qkv = llm.fp8_linear(h, f["qkv"])
+        nq, nkv = cfg.n_heads * hd, cfg.n_kv_heads * hd
+        q = qkv[..., :nq].reshape(B, S, cfg.n_heads, hd)
+        k = qkv[..., nq:nq + nkv].reshape(B, S, cfg.n_kv_heads, hd)
+        v = qkv[..., nq + nkv:].reshape(B, S, cfg.n_kv_heads, hd)
+        q, k = llm.rope(q, cos, sin, pos), llm.rope(k, cos, sin, pos)
+        kc, vc = cache
+        kc[:, :, pos:pos + S] = k.transpose(1, 2)
+        vc[:, :, pos:pos + S] = v.transpose(1, 2)
+        o = F.scaled_dot_product_attention(q.transpose(1, 2), kc[:, :, :pos + S], vc[:, :, :pos + S],
+                                           is_causal=(S > 1), enable_gqa=True)
+        x = x + llm.fp8_linear(o.transpose(1, 2).reshape(B, S, nq), f["o"])
+        h = llm.rmsnorm(x, self.mlp_norm.weight, self.mlp_norm.eps)
+        gu = llm.fp8_linear(h, f["w13"])
+        a, b = gu[..., :cfg.ffn_dim], gu[..., cfg.ffn_dim:]
+        return x + llm.fp8_linear(llm.swiglu(a, b), f["w2"])
+
     def forward(self, x, cos, sin, cache=None, pos: int = 0, fused: bool = False):
         if fused:
             from ..ops import llm
@@ -159,6 +195,24 @@ class Llama(nn.Module):
             self._rope = rope_tables(self.cfg, device)
         return self._rope
 
+    def attach_fp8(self):
+        """fp8 (e4m3fn) copies of every block linear and the LM head."""
+        from ..ops import llm
+        for layer in self.layers:
+            layer.attach_fp8()
+        self._fp8_head = llm.Fp8Weight(self.lm_head.weight)
+        return self
+
+    def forward_fp8(self, tokens, cache, pos: int = 0, last_only: bool = False):
+        from ..ops import llm
+        cos, sin = self.rope(tokens.device)
+        x = self.embed(tokens)
+        for i, layer in enumerate(self.layers):
+            x = layer.forward_fp8(x, cos, sin, cache[i], pos)
+        if last_only:
+            x = x[:, -1:].contiguous()
+        return llm.fp8_linear(llm.rmsnorm(x, self.norm.weight, self.norm.eps), self._fp8_head)
+
     def forward(self, tokens, cache=None, pos: int = 0, fused: bool = False, last_only: bool = False):
         cos, sin = self.rope(tokens.device)
         x = self.embed(tokens)
@@ -188,11 +242,15 @@ class LlamaDecoder:
     """Inference tenant: static KV cache, greedy decode."""
 
     def __init__(self, cfg: LlamaConfig, batch: int, context: int, device="cuda", dtype=torch.bfloat16,
-                 fused: Optional[bool] = None):
+                 fused: Optional[bool] = None, fp8: bool = False):
         self.cfg, self.batch, self.context = cfg, batch, context
         self.model = build(cfg, device, dtype)
         self.model.eval()
         self.fused = (torch.cuda.is_available() and str(device).startswith("cuda")) if fused is None else fused
+        self.fp8 = fp8
+        if fp8:  # weights streamed as e4m3fn through the fp8 MFMA linears (half the bytes of bf16)
+            with torch.no_grad():
+                self.model.attach_fp8()
         hd = cfg.head_dim
         self.cache = [(torch.zeros(batch, cfg.n_kv_heads, context, hd, device=device, dtype=dtype),
                        torch.zeros(batch, cfg.n_kv_heads, context, hd, device=device, dtype=dtype))
@@ -202,7 +260,10 @@ class LlamaDecoder:
     @torch.no_grad()
     def prefill(self, tokens: torch.Tensor) -> torch.Tensor:
         self.pos = 0
-        logits = self.model(tokens, cache=self.cache, pos=0, fused=self.fused, last_only=True)
+        if self.fp8:
+            logits = self.model.forward_fp8(tokens, self.cache, 0, last_only=True)
+        else:
+            logits = self.model(tokens, cache=self.cache, pos=0, fused=self.fused, last_only=True)
         self.pos = tokens.shape[1]
         return logits[:, -1].argmax(-1, keepdim=True)
 
@@ -210,7 +271,10 @@ class LlamaDecoder:
     def decode_step(self, tok: torch.Tensor) -> torch.Tensor:
         if self.pos >= self.context:
             self.pos = self.context // 2  # slide: keep the cache bounded for long runs
-        logits = self.model(tok, cache=self.cache, pos=self.pos, fused=self.fused)
+        if self.fp8:
+            logits = self.model.forward_fp8(tok, self.cache, self.pos)
+        else:
+            logits = self.model(tok, cache=self.cache, pos=self.pos, fused=self.fused)
         self.pos += 1
         return logits[:, -1].argmax(-1, keepdim=True)
 

@@ -57,3 +57,69 @@ def rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, pos: int) -> tor
     _check(lib().gpbs_hip_rope_bf16(_ptr(x), _ptr(y), _ptr(cos.contiguous()), _ptr(sin.contiguous()), B, S, H, hd,
                                     int(pos), _stream()), "rope_bf16")
     return y
+
+
+# --------------------------------------------------------------------------- fp8 (config #5, CDNA4 fp8 MFMA)
+FP8_MAX = 448.0  # OCP e4m3fn (gfx950), not the MI300 fnuz variant
+FP8_M_TILE = 64  # rows per gpbs_hip_fp8_linear launch
+
+
+def quant_rows_fp8(x: torch.Tensor):
+    """Per-row symmetric e4m3fn quantisation on device: returns (q [rows, K]
+    float8_e4m3fn, scale [rows] fp32) with scale = absmax / 448."""
+    x = x.contiguous()
+    _need(x, "quant_rows_fp8 x")
+    K = x.shape[-1]
+    if K % 8:
+        raise ValueError(f"quant_rows_fp8: K={K} must be a multiple of 8")
+    rows = x.numel() // K
+    q = torch.empty(x.shape, dtype=torch.float8_e4m3fn, device=x.device)
+    s = torch.empty(x.shape[:-1], dtype=torch.float32, device=x.device)
+    _check(lib().gpbs_hip_quant_rows_fp8(_ptr(x), _ptr(q), _ptr(s), rows, K, _stream()), "quant_rows_fp8")
+    return q, s
+
+
+def quant_rows_fp8_ref(x: torch.Tensor):
+    """fp32 PyTorch reference of quant_rows_fp8 (runs on CPU too)."""
+    xf = x.float()
+    amax = xf.abs().amax(-1)
+    s = torch.where(amax > 0, amax / FP8_MAX, torch.ones_like(amax))
+    q = (xf / s.unsqueeze(-1)).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
+    return q, s
+
+
+class Fp8Weight:
+    """A linear weight [N, K] stored as e4m3fn rows plus per-output-channel scales."""
+
+    def __init__(self, w: torch.Tensor):
+        w = w.detach().to(torch.bfloat16).contiguous()
+        self.N, self.K = w.shape
+        if self.N % 16 or self.K % 256:
+            raise ValueError(f"Fp8Weight: [N={self.N}, K={self.K}] needs N % 16 == 0 and K % 256 == 0")
+        self.q, self.s = quant_rows_fp8(w) if w.is_cuda else quant_rows_fp8_ref(w)
+
+    def nbytes(self) -> int:
+        return self.q.numel() + 4 * self.s.numel()
+
+
+def fp8_linear(x: torch.Tensor, w: Fp8Weight) -> torch.Tensor:
+    """y = x @ W^T with W in fp8 and x quantised per token to fp8 on the fly;
+    fp32 MFMA accumulation, bf16 output.  x [..., K] bf16."""
+    lead = x.shape[:-1]
+    x2 = x.reshape(-1, w.K).contiguous()
+    _need(x2, "fp8_linear x")
+    xq, sx = quant_rows_fp8(x2)
+    M = x2.shape[0]
+    y = torch.empty(M, w.N, dtype=torch.bfloat16, device=x.device)
+    for m0 in range(0, M, FP8_M_TILE):
+        m1 = min(M, m0 + FP8_M_TILE)
+        _check(lib().gpbs_hip_fp8_linear(_ptr(xq[m0:m1]), _ptr(sx[m0:m1]), _ptr(w.q), _ptr(w.s), _ptr(y[m0:m1]),
+                                         m1 - m0, w.N, w.K, _stream()), "fp8_linear")
+    return y.view(*lead, w.N)
+
+
+def fp8_linear_ref(x: torch.Tensor, w: Fp8Weight) -> torch.Tensor:
+    """fp32 reference of fp8_linear on the same quantised operands."""
+    xq, sx = quant_rows_fp8_ref(x.reshape(-1, w.K))
+    acc = xq.float() @ w.q.float().t()
+    return (acc * sx.unsqueeze(1) * w.s.float().unsqueeze(0)).view(*x.shape[:-1], w.N)

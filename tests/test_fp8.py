@@ -1,0 +1,91 @@
+"""fp8 (OCP e4m3fn) linears for the Llama inference tenant (config #5, CDNA4
+fp8 MFMA; csrc/hip/fp8_kernels.hip).  CPU: the fp32 reference semantics.
+GPU: the quantiser is checked bit-for-bit against PyTorch's e4m3fn cast and the
+MFMA linear against the fp32 product of the same quantised operands."""
+import pytest
+import torch
+
+from pbs_amd.models.llama import PRESETS, LlamaDecoder
+from pbs_amd.ops import llm
+
+
+def test_fp8_reference_semantics_cpu():
+    torch.manual_seed(0)
+    w = torch.randn(64, 512).bfloat16()
+    W = llm.Fp8Weight(w)
+    assert W.q.dtype == torch.float8_e4m3fn and W.s.shape == (64,)
+    # every row uses the full e4m3 range: max |q| == 448
+    assert torch.all(W.q.float().abs().amax(1) == llm.FP8_MAX)
+    x = torch.randn(5, 512).bfloat16()
+    ref = x.float() @ w.float().t()
+    y = llm.fp8_linear_ref(x, W)
+    rel = (y - ref).norm() / ref.norm()
+    assert rel < 0.06, rel
+    # a zero row gets scale 1 and zero output (no division by zero)
+    y0 = llm.fp8_linear_ref(torch.zeros(1, 512).bfloat16(), W)
+    assert torch.all(y0 == 0)
+    with pytest.raises(ValueError):
+        llm.Fp8Weight(torch.randn(10, 512))
+
+
+@pytest.mark.gpu
+def test_quant_rows_fp8_bit_exact():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = (torch.randn(67, 4096, device="cuda", generator=g) * 3).bfloat16()
+    x[3] = 0
+    q, s = llm.quant_rows_fp8(x)
+    qr, sr = llm.quant_rows_fp8_ref(x)
+    torch.testing.assert_close(s, sr, rtol=1e-6, atol=0)
+    mism = (q.view(torch.uint8) != qr.view(torch.uint8)).float().mean().item()
+    # RNE in both; x * (448 / amax) vs x / (amax / 448) may differ in the last fp32
+    # bit, which can flip a rounding tie
+    assert mism < 1e-3, mism
+    assert (q.float() - qr.float()).abs().max().item() <= 32  # at most one e4m3 step at the top binade
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(1, 4096, 4096), (8, 6144, 4096), (17, 1024, 14336), (40, 256, 512),
+                                   (64, 4096, 256), (100, 512, 1024)])
+def test_fp8_linear_matches_fp32_reference(M, N, K):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + N)
+    w = (torch.randn(N, K, device="cuda", generator=g) * 0.02).bfloat16()
+    x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    W = llm.Fp8Weight(w)
+    y = llm.fp8_linear(x, W)
+    assert y.shape == (M, N) and y.dtype == torch.bfloat16
+    xq, sx = llm.quant_rows_fp8(x)  # kernel operands -> fp32 product of exactly those
+    ref = (xq.float() @ W.q.float().t()) * sx[:, None] * W.s[None, :]
+    err = (y.float() - ref).abs().max().item()
+    assert err <= 1e-2 * ref.abs().max().item(), err  # fp32 accumulation order + bf16 output rounding
+    # and close to the unquantised bf16 product
+    full = x.float() @ w.float().t()
+    assert ((y.float() - full).norm() / full.norm()).item() < 0.06
+
+
+@pytest.mark.gpu
+def test_fp8_decoder_tracks_bf16_decoder():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.manual_seed(0)
+    cfg = PRESETS["tiny"]
+    d16 = LlamaDecoder(cfg, batch=4, context=64, device="cuda", fused=True)
+    d8 = LlamaDecoder(cfg, batch=4, context=64, device="cuda", fused=True, fp8=False)
+    d8.model.load_state_dict(d16.model.state_dict())
+    d8.model.attach_fp8()
+    d8.fp8 = True
+    toks = torch.randint(0, cfg.vocab, (4, 16), device="cuda")
+    with torch.no_grad():
+        l16 = d16.model(toks, cache=d16.cache, pos=0, fused=True)
+        l8 = d8.model.forward_fp8(toks, d8.cache, 0)
+        cos = torch.nn.functional.cosine_similarity(l8.float().flatten(1), l16.float().flatten(1)).min().item()
+        assert cos > 0.98, cos
+        # one cached decode step on each
+        nxt = l16[:, -1].argmax(-1, keepdim=True)
+        s16 = d16.model(nxt, cache=d16.cache, pos=16, fused=True)
+        s8 = d8.model.forward_fp8(nxt, d8.cache, 16)
+        cos = torch.nn.functional.cosine_similarity(s8.float().flatten(1), s16.float().flatten(1)).min().item()
+        assert cos > 0.98, cos
