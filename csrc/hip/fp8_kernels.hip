@@ -85,6 +85,108 @@ __global__ __launch_bounds__(kQuantThreads) void k_quant_rows_fp8(const u32x4* _
   }
 }
 
+__device__ __forceinline__ float block_max256(float m, float* red) {
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  float r = red[0];
+#pragma unroll
+  for (int w = 1; w < kQuantThreads / 64; ++w) r = fmaxf(r, red[w]);
+  return r;
+}
+
+__device__ __forceinline__ u32x2 pack_fp8x8(const float* v, float inv) {
+  u32x2 o;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    float c[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) c[e] = fminf(fmaxf(v[4 * h + e] * inv, -kE4M3Max), kE4M3Max);
+    int p = __builtin_amdgcn_cvt_pk_fp8_f32(c[0], c[1], 0, false);
+    o[h] = (u32)__builtin_amdgcn_cvt_pk_fp8_f32(c[2], c[3], p, true);
+  }
+  return o;
+}
+
+__device__ __forceinline__ float silu(float v) { return v / (1.f + __expf(-v)); }
+
+// RMSNorm fused with the fp8 row quantiser (the producer of the qkv / gate-up
+// linears' input): one workgroup per row, the normalised row never touches HBM in bf16.
+__global__ __launch_bounds__(kQuantThreads) void k_rmsnorm_quant_fp8(const u32x4* __restrict__ x,
+                                                                   const u32x4* __restrict__ w, u32x2* __restrict__ q,
+                                                                   float* __restrict__ scale, int dim8, float eps) {
+  __shared__ float red[2][kQuantThreads / 64];
+  const size_t row = blockIdx.x;
+  const u32x4* xr = x + row * dim8;
+  float ss = 0.f;
+  for (int i = threadIdx.x; i < dim8; i += kQuantThreads) {
+    const u32x4 v = xr[i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) ss += bf_lo(v[e]) * bf_lo(v[e]) + bf_hi(v[e]) * bf_hi(v[e]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  if ((threadIdx.x & 63) == 0) red[0][threadIdx.x >> 6] = ss;
+  __syncthreads();
+  float tot = 0.f;
+#pragma unroll
+  for (int k = 0; k < kQuantThreads / 64; ++k) tot += red[0][k];
+  const float rs = rsqrtf(tot / (float)(dim8 * 8) + eps);
+  float m = 0.f;
+  for (int i = threadIdx.x; i < dim8; i += kQuantThreads) {
+    const u32x4 v = xr[i], g = w[i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      m = fmaxf(m, fmaxf(fabsf(bf_lo(v[e]) * rs * bf_lo(g[e])), fabsf(bf_hi(v[e]) * rs * bf_hi(g[e]))));
+  }
+  const float amax = block_max256(m, red[1]);
+  const float inv = amax > 0.f ? kE4M3Max / amax : 1.f;
+  if (threadIdx.x == 0) scale[row] = amax > 0.f ? amax / kE4M3Max : 1.f;
+  u32x2* qr = q + row * dim8;
+  for (int i = threadIdx.x; i < dim8; i += kQuantThreads) {
+    const u32x4 v = xr[i], g = w[i];
+    float f[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      f[2 * e] = bf_lo(v[e]) * rs * bf_lo(g[e]);
+      f[2 * e + 1] = bf_hi(v[e]) * rs * bf_hi(g[e]);
+    }
+    qr[i] = pack_fp8x8(f, inv);
+  }
+}
+
+// SwiGLU on the packed gate|up output [rows, 2F] fused with the fp8 row
+// quantiser: y = silu(gu[:, :F]) * gu[:, F:], emitted as e4m3 + row scale.
+__global__ __launch_bounds__(kQuantThreads) void k_swiglu_quant_fp8(const u32x4* __restrict__ gu,
+                                                                  u32x2* __restrict__ q, float* __restrict__ scale,
+                                                                  int f8) {
+  __shared__ float red[kQuantThreads / 64];
+  const size_t row = blockIdx.x;
+  const u32x4* a = gu + row * 2 * f8;
+  const u32x4* b = a + f8;
+  float m = 0.f;
+  for (int i = threadIdx.x; i < f8; i += kQuantThreads) {
+    const u32x4 va = a[i], vb = b[i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      m = fmaxf(m, fmaxf(fabsf(silu(bf_lo(va[e])) * bf_lo(vb[e])), fabsf(silu(bf_hi(va[e])) * bf_hi(vb[e]))));
+  }
+  const float amax = block_max256(m, red);
+  const float inv = amax > 0.f ? kE4M3Max / amax : 1.f;
+  if (threadIdx.x == 0) scale[row] = amax > 0.f ? amax / kE4M3Max : 1.f;
+  u32x2* qr = q + row * f8;
+  for (int i = threadIdx.x; i < f8; i += kQuantThreads) {
+    const u32x4 va = a[i], vb = b[i];
+    float f[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      f[2 * e] = silu(bf_lo(va[e])) * bf_lo(vb[e]);
+      f[2 * e + 1] = silu(bf_hi(va[e])) * bf_hi(vb[e]);
+    }
+    qr[i] = pack_fp8x8(f, inv);
+  }
+}
+
 __device__ __forceinline__ long lo64(u32x4 v) { return (long)(((u64)v[1] << 32) | v[0]); }
 __device__ __forceinline__ long hi64(u32x4 v) { return (long)(((u64)v[3] << 32) | v[2]); }
 
@@ -168,6 +270,21 @@ int gpbs_hip_quant_rows_fp8(const void* x, void* q, float* scale, int rows, int 
   if (rows <= 0 || k <= 0 || k % 8) return -22;
   hipLaunchKernelGGL(k_quant_rows_fp8, dim3(rows), dim3(kQuantThreads), 0, s, (const u32x4*)x, (u32x2*)q, scale,
                      k / 8);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+int gpbs_hip_rmsnorm_quant_fp8(const void* x, const void* w, void* q, float* scale, int rows, int dim, float eps,
+                               hipStream_t s) {
+  if (rows <= 0 || dim <= 0 || dim % 8) return -22;
+  hipLaunchKernelGGL(k_rmsnorm_quant_fp8, dim3(rows), dim3(kQuantThreads), 0, s, (const u32x4*)x, (const u32x4*)w,
+                     (u32x2*)q, scale, dim / 8, eps);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+int gpbs_hip_swiglu_quant_fp8(const void* gu, void* q, float* scale, int rows, int f, hipStream_t s) {
+  if (rows <= 0 || f <= 0 || f % 8) return -22;
+  hipLaunchKernelGGL(k_swiglu_quant_fp8, dim3(rows), dim3(kQuantThreads), 0, s, (const u32x4*)gu, (u32x2*)q, scale,
+                     f / 8);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

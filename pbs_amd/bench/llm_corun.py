@@ -40,7 +40,8 @@ def _tenant(kind: str, seconds: float, warmup: float, socket: Optional[str], q, 
         t = TenantClient(kind, socket, slots=8, weight=args.get(f"{kind}_weight", 256),
                          spatial=args.get("spatial", False), priority=args.get(f"{kind}_prio", 0))
     if kind == "infer":
-        w = LlamaDecoder(PRESETS[args["infer_model"]], batch=args["infer_batch"], context=args["context"])
+        w = LlamaDecoder(PRESETS[args["infer_model"]], batch=args["infer_batch"], context=args["context"],
+                         fp8=args.get("fp8", False))
         prompt = torch.randint(0, w.cfg.vocab, (w.batch, args["prompt"]), device="cuda")
         nxt = w.prefill(prompt)
         flops = 2.0 * w.cfg.n_params() * w.batch
@@ -151,11 +152,12 @@ def main(argv=None):
     ap.add_argument("--context", type=int, default=2048)
     ap.add_argument("--train-batch", type=int, default=4)
     ap.add_argument("--train-seq", type=int, default=2048)
+    ap.add_argument("--fp8", action="store_true", help="decode tenant streams e4m3fn weights (fp8 MFMA linears)")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     args = {"infer_model": a.infer_model, "train_model": a.train_model, "infer_batch": a.infer_batch,
             "prompt": a.prompt, "context": a.context, "train_batch": a.train_batch, "train_seq": a.train_seq,
-            "infer_weight": 512, "train_weight": 256}
+            "infer_weight": 512, "train_weight": 256, "fp8": a.fp8}
     res = {}
     pols = [p for p in a.policies.split(",") if p]
     if "solo" in pols:
@@ -182,7 +184,7 @@ def main(argv=None):
                           "infer_p99_ms": round(r["infer"]["p99_ms"], 3),
                           "infer_p50_ms": round(r["infer"]["p50_ms"], 3)}
     line = {"config": "#5 Llama-3-8B decode + Llama-1B bf16 training, 1x MI355X", "data": "synthetic tokens, "
-            "random-init weights", "dtype": "bf16", "summary": summary, "raw": res}
+            "random-init weights", "dtype": "bf16" + (" (decode weights fp8 e4m3fn)" if a.fp8 else ""), "summary": summary, "raw": res}
     print(json.dumps(line))
     if a.out:
         with open(a.out, "w") as f:

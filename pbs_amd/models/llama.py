@@ -140,8 +140,7 @@ class Block(nn.Module):
         from ..ops import llm
         cfg, hd, f = self.cfg, self.cfg.head_dim, self._fp8
         B, S, _ = x.shape
-        h = llm.rmsnorm(x, self.attn_norm.weight, self.attn_norm.eps)
-        qkv = llm.fp8_linear(h, f["qkv"])
+        qkv = llm.fp8_linear_q(*llm.rmsnorm_quant_fp8(x, self.attn_norm.weight, self.attn_norm.eps), f["qkv"])
         nq, nkv = cfg.n_heads * hd, cfg.n_kv_heads * hd
         q = qkv[..., :nq].reshape(B, S, cfg.n_heads, hd)
         k = qkv[..., nq:nq + nkv].reshape(B, S, cfg.n_kv_heads, hd)
@@ -153,10 +152,8 @@ class Block(nn.Module):
         o = F.scaled_dot_product_attention(q.transpose(1, 2), kc[:, :, :pos + S], vc[:, :, :pos + S],
                                            is_causal=(S > 1), enable_gqa=True)
         x = x + llm.fp8_linear(o.transpose(1, 2).reshape(B, S, nq), f["o"])
-        h = llm.rmsnorm(x, self.mlp_norm.weight, self.mlp_norm.eps)
-        gu = llm.fp8_linear(h, f["w13"])
-        a, b = gu[..., :cfg.ffn_dim], gu[..., cfg.ffn_dim:]
-        return x + llm.fp8_linear(llm.swiglu(a, b), f["w2"])
+        gu = llm.fp8_linear_q(*llm.rmsnorm_quant_fp8(x, self.mlp_norm.weight, self.mlp_norm.eps), f["w13"])
+        return x + llm.fp8_linear_q(*llm.swiglu_quant_fp8(gu), f["w2"])
 
     def forward(self, x, cos, sin, cache=None, pos: int = 0, fused: bool = False):
         if fused:
@@ -211,7 +208,7 @@ class Llama(nn.Module):
             x = layer.forward_fp8(x, cos, sin, cache[i], pos)
         if last_only:
             x = x[:, -1:].contiguous()
-        return llm.fp8_linear(llm.rmsnorm(x, self.norm.weight, self.norm.eps), self._fp8_head)
+        return llm.fp8_linear_q(*llm.rmsnorm_quant_fp8(x, self.norm.weight, self.norm.eps), self._fp8_head)
 
     def forward(self, tokens, cache=None, pos: int = 0, fused: bool = False, last_only: bool = False):
         cos, sin = self.rope(tokens.device)

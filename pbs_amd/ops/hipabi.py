@@ -50,6 +50,8 @@ def bind(lib):
     _p(lib, "gpbs_hip_rmsnorm_bf16", C.c_int, vp, vp, vp, C.c_int, C.c_int, C.c_float, vp)
     _p(lib, "gpbs_hip_swiglu_bf16", C.c_int, vp, vp, vp, C.c_ulonglong, vp)
     _p(lib, "gpbs_hip_quant_rows_fp8", C.c_int, vp, vp, vp, C.c_int, C.c_int, vp)
+    _p(lib, "gpbs_hip_rmsnorm_quant_fp8", C.c_int, vp, vp, vp, vp, C.c_int, C.c_int, C.c_float, vp)
+    _p(lib, "gpbs_hip_swiglu_quant_fp8", C.c_int, vp, vp, vp, C.c_int, C.c_int, vp)
     _p(lib, "gpbs_hip_fp8_linear", C.c_int, vp, vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, vp)
     _p(lib, "gpbs_hip_rope_bf16", C.c_int, vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp)
     _p(lib, "gpbs_hip_census", C.c_int, vp, C.c_int, vp, C.c_uint, C.c_uint, vp)

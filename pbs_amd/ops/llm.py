@@ -84,7 +84,8 @@ def quant_rows_fp8_ref(x: torch.Tensor):
     xf = x.float()
     amax = xf.abs().amax(-1)
     s = torch.where(amax > 0, amax / FP8_MAX, torch.ones_like(amax))
-    q = (xf / s.unsqueeze(-1)).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
+    inv = torch.where(amax > 0, FP8_MAX / amax, torch.ones_like(amax))  # multiply, as the kernel does
+    q = (xf * inv.unsqueeze(-1)).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
     return q, s
 
 
@@ -102,20 +103,62 @@ class Fp8Weight:
         return self.q.numel() + 4 * self.s.numel()
 
 
+def fp8_linear_q(xq: torch.Tensor, sx: torch.Tensor, w: Fp8Weight) -> torch.Tensor:
+    """y = (xq @ Wq^T) * sx[m] * sw[n] on already-quantised rows (the output of
+    quant_rows_fp8 / rmsnorm_quant_fp8 / swiglu_quant_fp8); bf16 out."""
+    lead = xq.shape[:-1]
+    if xq.dtype != torch.float8_e4m3fn or xq.shape[-1] != w.K or not xq.is_contiguous():
+        raise ValueError(f"fp8_linear_q: need contiguous e4m3fn [..., {w.K}], got {xq.dtype} {tuple(xq.shape)}")
+    M = xq.numel() // w.K
+    y = torch.empty(*lead, w.N, dtype=torch.bfloat16, device=xq.device)
+    L, st = lib(), _stream()
+    if M <= FP8_M_TILE:
+        _check(L.gpbs_hip_fp8_linear(_ptr(xq), _ptr(sx), _ptr(w.q), _ptr(w.s), _ptr(y), M, w.N, w.K, st),
+               "fp8_linear")
+        return y
+    x2, s2, y2 = xq.view(M, w.K), sx.reshape(M), y.view(M, w.N)
+    for m0 in range(0, M, FP8_M_TILE):
+        m1 = min(M, m0 + FP8_M_TILE)
+        _check(L.gpbs_hip_fp8_linear(_ptr(x2[m0:m1]), _ptr(s2[m0:m1]), _ptr(w.q), _ptr(w.s), _ptr(y2[m0:m1]),
+                                     m1 - m0, w.N, w.K, st), "fp8_linear")
+    return y
+
+
 def fp8_linear(x: torch.Tensor, w: Fp8Weight) -> torch.Tensor:
     """y = x @ W^T with W in fp8 and x quantised per token to fp8 on the fly;
     fp32 MFMA accumulation, bf16 output.  x [..., K] bf16."""
-    lead = x.shape[:-1]
-    x2 = x.reshape(-1, w.K).contiguous()
-    _need(x2, "fp8_linear x")
-    xq, sx = quant_rows_fp8(x2)
-    M = x2.shape[0]
-    y = torch.empty(M, w.N, dtype=torch.bfloat16, device=x.device)
-    for m0 in range(0, M, FP8_M_TILE):
-        m1 = min(M, m0 + FP8_M_TILE)
-        _check(lib().gpbs_hip_fp8_linear(_ptr(xq[m0:m1]), _ptr(sx[m0:m1]), _ptr(w.q), _ptr(w.s), _ptr(y[m0:m1]),
-                                         m1 - m0, w.N, w.K, _stream()), "fp8_linear")
-    return y.view(*lead, w.N)
+    xq, sx = quant_rows_fp8(x)
+    return fp8_linear_q(xq, sx, w)
+
+
+def rmsnorm_quant_fp8(x: torch.Tensor, w: torch.Tensor, eps: float):
+    """e4m3 rows of rmsnorm(x) * w plus their scales, in one kernel."""
+    x = x.contiguous()
+    _need(x, "rmsnorm_quant_fp8 x")
+    dim = x.shape[-1]
+    w = w.to(torch.bfloat16).contiguous()
+    if w.numel() != dim or dim % 8:
+        raise ValueError(f"rmsnorm_quant_fp8: weight {tuple(w.shape)} vs dim {dim}")
+    q = torch.empty(x.shape, dtype=torch.float8_e4m3fn, device=x.device)
+    s = torch.empty(x.shape[:-1], dtype=torch.float32, device=x.device)
+    _check(lib().gpbs_hip_rmsnorm_quant_fp8(_ptr(x), _ptr(w), _ptr(q), _ptr(s), x.numel() // dim, dim,
+                                            C.c_float(eps), _stream()), "rmsnorm_quant_fp8")
+    return q, s
+
+
+def swiglu_quant_fp8(gu: torch.Tensor):
+    """e4m3 rows of silu(gu[..., :F]) * gu[..., F:] plus their scales (gu is the
+    packed gate|up linear output, read in place)."""
+    gu = gu.contiguous()
+    _need(gu, "swiglu_quant_fp8 gu")
+    F2 = gu.shape[-1]
+    if F2 % 16:
+        raise ValueError(f"swiglu_quant_fp8: packed width {F2} must be a multiple of 16")
+    q = torch.empty(*gu.shape[:-1], F2 // 2, dtype=torch.float8_e4m3fn, device=gu.device)
+    s = torch.empty(gu.shape[:-1], dtype=torch.float32, device=gu.device)
+    _check(lib().gpbs_hip_swiglu_quant_fp8(_ptr(gu), _ptr(q), _ptr(s), gu.numel() // F2, F2 // 2, _stream()),
+           "swiglu_quant_fp8")
+    return q, s
 
 
 def fp8_linear_ref(x: torch.Tensor, w: Fp8Weight) -> torch.Tensor:

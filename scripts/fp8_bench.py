@@ -73,7 +73,7 @@ def main():
     res = {}
     for fp8 in (False, True):
         torch.manual_seed(0)
-        t0 = time.time()
+        t0 = time.perf_counter()
         dec = LlamaDecoder(cfg, batch=a.batch, context=1024, device="cuda", fp8=fp8)
         toks = torch.randint(0, cfg.vocab, (a.batch, 128), device="cuda")
         nxt = dec.prefill(toks)
