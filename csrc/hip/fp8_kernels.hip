@@ -191,32 +191,36 @@ __device__ __forceinline__ long lo64(u32x4 v) { return (long)(((u64)v[1] << 32) 
 __device__ __forceinline__ long hi64(u32x4 v) { return (long)(((u64)v[3] << 32) | v[2]); }
 
 // MT = number of 16-row M tiles (M <= 16 * MT).  K % 256 == 0, N % 16 == 0.
-template <int MT>
-__global__ __launch_bounds__(kThreads) void k_fp8_gemm_skinny(const unsigned char* __restrict__ xq,
+template <int MT, int WV, bool NT>
+__global__ __launch_bounds__(WV * 64) void k_fp8_gemm_skinny(const unsigned char* __restrict__ xq,
                                                               const float* __restrict__ sx,
                                                               const unsigned char* __restrict__ wq,
                                                               const float* __restrict__ sw,
                                                               unsigned short* __restrict__ y, int M, int N, int K) {
-  __shared__ f32x4 red[kWaves][MT][64];
+  __shared__ f32x4 red[WV][MT][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int n0 = blockIdx.x * 16;
   const int k16 = K >> 4;  // 16-byte units per row
-  const u32x4* wrow = reinterpret_cast<const u32x4*>(wq) + (size_t)(n0 + r) * k16 + g;
+  const int nkb = K >> 8;  // 256-byte blocks
+  // W is pre-shuffled (Fp8Weight): for strip n0/16, block kb, step u, the 64 lanes'
+  // 16-byte pieces are one contiguous 1 KiB run in lane order, so every load
+  // instruction is a fully coalesced 1 KiB read.
+  const u32x4* wrow = reinterpret_cast<const u32x4*>(wq) + (size_t)blockIdx.x * nkb * 256 + lane;
   const u32x4* xb = reinterpret_cast<const u32x4*>(xq);
   f32x4 acc[MT];
 #pragma unroll
   for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nkb = K >> 8;  // 256-byte blocks
-  for (int kb = w; kb < nkb; kb += 2 * kWaves) {
-    const bool two = kb + kWaves < nkb;
+  for (int kb = w; kb < nkb; kb += 2 * WV) {
+    const bool two = kb + WV < nkb;
     u32x4 b0[4], b1[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) b0[u] = __builtin_nontemporal_load(wrow + kb * 16 + u * 4);
+    for (int u = 0; u < 4; ++u) b0[u] = NT ? __builtin_nontemporal_load(wrow + kb * 256 + u * 64) : wrow[kb * 256 + u * 64];
     if (two) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) b1[u] = __builtin_nontemporal_load(wrow + (kb + kWaves) * 16 + u * 4);
+      for (int u = 0; u < 4; ++u)
+        b1[u] = NT ? __builtin_nontemporal_load(wrow + (kb + WV) * 256 + u * 64) : wrow[(kb + WV) * 256 + u * 64];
     }
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
@@ -232,7 +236,7 @@ __global__ __launch_bounds__(kThreads) void k_fp8_gemm_skinny(const unsigned cha
       }
       if (two) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) a[u] = m < M ? xr[(kb + kWaves) * 16 + u * 4] : u32x4{0u, 0u, 0u, 0u};
+        for (int u = 0; u < 4; ++u) a[u] = m < M ? xr[(kb + WV) * 16 + u * 4] : u32x4{0u, 0u, 0u, 0u};
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(lo64(a[u]), lo64(b1[u]), acc[t], 0, 0, 0);
@@ -245,11 +249,11 @@ __global__ __launch_bounds__(kThreads) void k_fp8_gemm_skinny(const unsigned cha
   for (int t = 0; t < MT; ++t) red[w][t][lane] = acc[t];
   __syncthreads();
   // C/D map of 16x16 MFMA: col = lane & 15 (n), row = 4 * (lane >> 4) + i (m).
-  for (int e = threadIdx.x; e < MT * 64; e += kThreads) {
+  for (int e = threadIdx.x; e < MT * 64; e += WV * 64) {
     const int t = e >> 6, l = e & 63;
     f32x4 s = red[0][t][l];
 #pragma unroll
-    for (int v = 1; v < kWaves; ++v) s += red[v][t][l];
+    for (int v = 1; v < WV; ++v) s += red[v][t][l];
     const int n = n0 + (l & 15);
     const float wsc = sw[n];
 #pragma unroll
@@ -263,6 +267,22 @@ __global__ __launch_bounds__(kThreads) void k_fp8_gemm_skinny(const unsigned cha
 }  // namespace gpbs_fp8
 
 using namespace gpbs_fp8;
+
+// Launch variant (microbench knob): bit 0 = non-temporal W loads instead of
+// plain cached ones, bit 1 = 4 waves per workgroup instead of 8.
+static int g_fp8_opts = 0;
+
+template <int WV, bool NT>
+static void launch_fp8(const unsigned char* xp, const float* sx, const unsigned char* wp, const float* sw,
+                       unsigned short* yp, int M, int N, int K, hipStream_t s) {
+  const dim3 grid(N / 16), block(WV * 64);
+  if (M <= 16)
+    hipLaunchKernelGGL((k_fp8_gemm_skinny<1, WV, NT>), grid, block, 0, s, xp, sx, wp, sw, yp, M, N, K);
+  else if (M <= 32)
+    hipLaunchKernelGGL((k_fp8_gemm_skinny<2, WV, NT>), grid, block, 0, s, xp, sx, wp, sw, yp, M, N, K);
+  else
+    hipLaunchKernelGGL((k_fp8_gemm_skinny<4, WV, NT>), grid, block, 0, s, xp, sx, wp, sw, yp, M, N, K);
+}
 
 extern "C" {
 
@@ -288,19 +308,24 @@ int gpbs_hip_swiglu_quant_fp8(const void* gu, void* q, float* scale, int rows, i
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
+int gpbs_hip_fp8_set_opts(int opts) {
+  const int prev = g_fp8_opts;
+  g_fp8_opts = opts;
+  return prev;
+}
+
 int gpbs_hip_fp8_linear(const void* xq, const float* sx, const void* wq, const float* sw, void* y, int M, int N, int K,
                         hipStream_t s) {
   if (M <= 0 || M > 64 || N <= 0 || N % 16 || K <= 0 || K % 256) return -22;
-  const dim3 grid(N / 16), block(kThreads);
   const auto* xp = (const unsigned char*)xq;
   const auto* wp = (const unsigned char*)wq;
   auto* yp = (unsigned short*)y;
-  if (M <= 16)
-    hipLaunchKernelGGL(k_fp8_gemm_skinny<1>, grid, block, 0, s, xp, sx, wp, sw, yp, M, N, K);
-  else if (M <= 32)
-    hipLaunchKernelGGL(k_fp8_gemm_skinny<2>, grid, block, 0, s, xp, sx, wp, sw, yp, M, N, K);
-  else
-    hipLaunchKernelGGL(k_fp8_gemm_skinny<4>, grid, block, 0, s, xp, sx, wp, sw, yp, M, N, K);
+  switch (g_fp8_opts & 3) {
+    case 0: launch_fp8<kWaves, false>(xp, sx, wp, sw, yp, M, N, K, s); break;
+    case 1: launch_fp8<kWaves, true>(xp, sx, wp, sw, yp, M, N, K, s); break;
+    case 2: launch_fp8<4, true>(xp, sx, wp, sw, yp, M, N, K, s); break;
+    default: launch_fp8<4, false>(xp, sx, wp, sw, yp, M, N, K, s); break;
+  }
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -68,7 +68,9 @@ __global__ __launch_bounds__(256) void k_swiglu_bf16(const u32x4* __restrict__ a
 // Each thread rotates 4 interleaved pairs (16 B).
 __global__ __launch_bounds__(256) void k_rope_bf16(const u32x4* __restrict__ x, u32x4* __restrict__ y,
                                                   const float* __restrict__ cosb, const float* __restrict__ sinb,
-                                                  int S, int H, int hd, int pos, size_t n8) {
+                                                  int S, int H, int hd, int pos, const int* __restrict__ dpos,
+                                                  size_t n8) {
+  if (dpos) pos += *dpos;  // device-resident position (graph-captured decode)
   const int per_head = hd / 8;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (size_t)gridDim.x * blockDim.x) {
     const int c = (int)(i % per_head);                 // 8-element chunk within the head
@@ -115,7 +117,20 @@ int gpbs_hip_rope_bf16(const void* x, void* y, const float* cosb, const float* s
   int grid = (int)std::min<size_t>((n8 + 255) / 256, 256 * 8);
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(k_rope_bf16, dim3(grid), dim3(256), 0, s, (const u32x4*)x, (u32x4*)y, cosb, sinb, S, H, hd, pos,
-                     n8);
+                     (const int*)nullptr, n8);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// Same, with the start position read from device memory at run time (int32), so
+// a captured HIP graph replays at the current position.
+int gpbs_hip_rope_bf16_dpos(const void* x, void* y, const float* cosb, const float* sinb, int B, int S, int H, int hd,
+                            const int* dpos, hipStream_t s) {
+  if (hd % 8 || B <= 0 || S <= 0 || H <= 0 || !dpos) return -22;
+  const size_t n8 = (size_t)B * S * H * hd / 8;
+  int grid = (int)std::min<size_t>((n8 + 255) / 256, 256 * 8);
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(k_rope_bf16, dim3(grid), dim3(256), 0, s, (const u32x4*)x, (u32x4*)y, cosb, sinb, S, H, hd, 0,
+                     dpos, n8);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

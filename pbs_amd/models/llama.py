@@ -155,6 +155,30 @@ class Block(nn.Module):
         gu = llm.fp8_linear_q(*llm.rmsnorm_quant_fp8(x, self.mlp_norm.weight, self.mlp_norm.eps), f["w13"])
         return x + llm.fp8_linear_q(*llm.swiglu_quant_fp8(gu), f["w2"])
 
+    def decode_fp8_static(self, x, cos, sin, cache, pos_i32, pos_i64, mask):
+        """One-token decode with every shape static and the position on device
+        (capturable in a HIP graph): the KV row is written with index_copy_ at
+        pos, and attention runs over the whole static cache with an additive
+        mask, grouped per KV head (GQA without repeating K/V)."""
+        from ..ops import llm
+        cfg, hd, f = self.cfg, self.cfg.head_dim, self._fp8
+        B = x.shape[0]
+        G = cfg.n_heads // cfg.n_kv_heads
+        qkv = llm.fp8_linear_q(*llm.rmsnorm_quant_fp8(x, self.attn_norm.weight, self.attn_norm.eps), f["qkv"])
+        nq, nkv = cfg.n_heads * hd, cfg.n_kv_heads * hd
+        q = llm.rope_dpos(qkv[..., :nq].reshape(B, 1, cfg.n_heads, hd), cos, sin, pos_i32)
+        k = llm.rope_dpos(qkv[..., nq:nq + nkv].reshape(B, 1, cfg.n_kv_heads, hd), cos, sin, pos_i32)
+        v = qkv[..., nq + nkv:].reshape(B, 1, cfg.n_kv_heads, hd)
+        kc, vc = cache
+        kc.index_copy_(2, pos_i64, k.transpose(1, 2))
+        vc.index_copy_(2, pos_i64, v.transpose(1, 2))
+        qg = q.view(B, cfg.n_kv_heads, G, hd)
+        sc = torch.matmul(qg, kc.transpose(-1, -2)).float() * (hd ** -0.5) + mask
+        o = torch.matmul(torch.softmax(sc, -1).to(vc.dtype), vc)  # [B, Hkv, G, hd]
+        x = x + llm.fp8_linear(o.reshape(B, 1, nq), f["o"])
+        gu = llm.fp8_linear_q(*llm.rmsnorm_quant_fp8(x, self.mlp_norm.weight, self.mlp_norm.eps), f["w13"])
+        return x + llm.fp8_linear_q(*llm.swiglu_quant_fp8(gu), f["w2"])
+
     def forward(self, x, cos, sin, cache=None, pos: int = 0, fused: bool = False):
         if fused:
             from ..ops import llm
@@ -210,6 +234,14 @@ class Llama(nn.Module):
             x = x[:, -1:].contiguous()
         return llm.fp8_linear_q(*llm.rmsnorm_quant_fp8(x, self.norm.weight, self.norm.eps), self._fp8_head)
 
+    def decode_fp8_static(self, tok, cache, pos_i32, pos_i64, mask):
+        from ..ops import llm
+        cos, sin = self.rope(tok.device)
+        x = self.embed(tok)
+        for i, layer in enumerate(self.layers):
+            x = layer.decode_fp8_static(x, cos, sin, cache[i], pos_i32, pos_i64, mask)
+        return llm.fp8_linear_q(*llm.rmsnorm_quant_fp8(x, self.norm.weight, self.norm.eps), self._fp8_head)
+
     def forward(self, tokens, cache=None, pos: int = 0, fused: bool = False, last_only: bool = False):
         cos, sin = self.rope(tokens.device)
         x = self.embed(tokens)
@@ -239,7 +271,7 @@ class LlamaDecoder:
     """Inference tenant: static KV cache, greedy decode."""
 
     def __init__(self, cfg: LlamaConfig, batch: int, context: int, device="cuda", dtype=torch.bfloat16,
-                 fused: Optional[bool] = None, fp8: bool = False):
+                 fused: Optional[bool] = None, fp8: bool = False, graph: bool = False, static: bool = False):
         self.cfg, self.batch, self.context = cfg, batch, context
         self.model = build(cfg, device, dtype)
         self.model.eval()
@@ -248,6 +280,11 @@ class LlamaDecoder:
         if fp8:  # weights streamed as e4m3fn through the fp8 MFMA linears (half the bytes of bf16)
             with torch.no_grad():
                 self.model.attach_fp8()
+        if (graph or static) and not fp8:
+            raise ValueError("static-shape / graph decode is the fp8 path (needs fp8=True)")
+        self.graph = graph
+        self.static = static or graph  # static shapes + device position; graph=True also captures it
+        self._g = self._step = None
         hd = cfg.head_dim
         self.cache = [(torch.zeros(batch, cfg.n_kv_heads, context, hd, device=device, dtype=dtype),
                        torch.zeros(batch, cfg.n_kv_heads, context, hd, device=device, dtype=dtype))
@@ -264,10 +301,55 @@ class LlamaDecoder:
         self.pos = tokens.shape[1]
         return logits[:, -1].argmax(-1, keepdim=True)
 
+    def _graph_setup(self, tok: torch.Tensor):
+        """Build the static-shape step; with graph=True capture it (every launch
+        of it) into a HIP graph, so later steps are one graph launch plus the
+        position/token uploads."""
+        dev = tok.device
+        self._tok = tok.clone()
+        self._pos_i32 = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._pos_i64 = torch.zeros(1, dtype=torch.int64, device=dev)
+        self._ar = torch.arange(self.context, device=dev)
+
+        def step():
+            mask = torch.where(self._ar <= self._pos_i64, 0.0, float("-inf"))
+            logits = self.model.decode_fp8_static(self._tok, self.cache, self._pos_i32, self._pos_i64, mask)
+            return logits[:, -1].argmax(-1, keepdim=True)
+
+        self._step = step
+        if not self.graph:
+            return
+        self._set_pos()
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(2):  # warm the allocator / library handles outside capture
+                step()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        self._g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self._g):
+            self._out = step()
+
+    def _set_pos(self):
+        self._pos_i32.fill_(self.pos)
+        self._pos_i64.fill_(self.pos)
+
     @torch.no_grad()
     def decode_step(self, tok: torch.Tensor) -> torch.Tensor:
         if self.pos >= self.context:
             self.pos = self.context // 2  # slide: keep the cache bounded for long runs
+        if self.static:
+            if self._step is None:
+                self._graph_setup(tok)
+            self._tok.copy_(tok)
+            self._set_pos()
+            if self.graph:
+                self._g.replay()
+                out = self._out.clone()
+            else:
+                out = self._step()
+            self.pos += 1
+            return out
         if self.fp8:
             logits = self.model.forward_fp8(tok, self.cache, self.pos)
         else:

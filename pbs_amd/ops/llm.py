@@ -59,6 +59,21 @@ def rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, pos: int) -> tor
     return y
 
 
+
+def rope_dpos(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, pos_t: torch.Tensor) -> torch.Tensor:
+    """rope() with the start position in a 1-element int32 CUDA tensor (read by
+    the kernel at run time: valid inside a captured graph).  No bounds check on
+    the device value: the caller keeps pos + S <= cos.shape[0]."""
+    x = x.contiguous()
+    _need(x, "rope x")
+    B, S, H, hd = x.shape
+    if cos.dtype != torch.float32 or cos.shape[-1] * 2 != hd or pos_t.dtype != torch.int32 or not pos_t.is_cuda:
+        raise ValueError(f"rope_dpos: tables {tuple(cos.shape)} {cos.dtype}, pos {pos_t.dtype} {pos_t.device}")
+    y = torch.empty_like(x)
+    _check(lib().gpbs_hip_rope_bf16_dpos(_ptr(x), _ptr(y), _ptr(cos), _ptr(sin), B, S, H, hd, _ptr(pos_t),
+                                         _stream()), "rope_bf16_dpos")
+    return y
+
 # --------------------------------------------------------------------------- fp8 (config #5, CDNA4 fp8 MFMA)
 FP8_MAX = 448.0  # OCP e4m3fn (gfx950), not the MI300 fnuz variant
 FP8_M_TILE = 64  # rows per gpbs_hip_fp8_linear launch
@@ -97,10 +112,25 @@ class Fp8Weight:
         self.N, self.K = w.shape
         if self.N % 16 or self.K % 256:
             raise ValueError(f"Fp8Weight: [N={self.N}, K={self.K}] needs N % 16 == 0 and K % 256 == 0")
-        self.q, self.s = quant_rows_fp8(w) if w.is_cuda else quant_rows_fp8_ref(w)
+        q, self.s = quant_rows_fp8(w) if w.is_cuda else quant_rows_fp8_ref(w)
+        self.qs = self.shuffle(q)  # the only stored copy: the kernel's lane-order layout
+
+    # Kernel layout: [N/16 strips][K/256 blocks][4 steps u][4 lane groups g][16 rows r][16 B];
+    # lane l = 16 g + r of the wave that owns (strip, block) reads the 16 bytes
+    # W[16 strip + r][256 block + 64 u + 16 g : +16] at step u, so each load
+    # instruction is one contiguous 1 KiB run.
+    def shuffle(self, q: torch.Tensor) -> torch.Tensor:
+        b = q.view(torch.uint8).view(self.N // 16, 16, self.K // 256, 4, 4, 16)
+        return b.permute(0, 2, 3, 4, 1, 5).contiguous().view(torch.float8_e4m3fn).view(self.N, self.K)
+
+    @property
+    def q(self) -> torch.Tensor:
+        """Row-major [N, K] e4m3fn view (a copy; for references and tests)."""
+        b = self.qs.view(torch.uint8).view(self.N // 16, self.K // 256, 4, 4, 16, 16)
+        return b.permute(0, 4, 1, 2, 3, 5).contiguous().view(torch.float8_e4m3fn).view(self.N, self.K)
 
     def nbytes(self) -> int:
-        return self.q.numel() + 4 * self.s.numel()
+        return self.qs.numel() + 4 * self.s.numel()
 
 
 def fp8_linear_q(xq: torch.Tensor, sx: torch.Tensor, w: Fp8Weight) -> torch.Tensor:
@@ -113,13 +143,13 @@ def fp8_linear_q(xq: torch.Tensor, sx: torch.Tensor, w: Fp8Weight) -> torch.Tens
     y = torch.empty(*lead, w.N, dtype=torch.bfloat16, device=xq.device)
     L, st = lib(), _stream()
     if M <= FP8_M_TILE:
-        _check(L.gpbs_hip_fp8_linear(_ptr(xq), _ptr(sx), _ptr(w.q), _ptr(w.s), _ptr(y), M, w.N, w.K, st),
+        _check(L.gpbs_hip_fp8_linear(_ptr(xq), _ptr(sx), _ptr(w.qs), _ptr(w.s), _ptr(y), M, w.N, w.K, st),
                "fp8_linear")
         return y
     x2, s2, y2 = xq.view(M, w.K), sx.reshape(M), y.view(M, w.N)
     for m0 in range(0, M, FP8_M_TILE):
         m1 = min(M, m0 + FP8_M_TILE)
-        _check(L.gpbs_hip_fp8_linear(_ptr(x2[m0:m1]), _ptr(s2[m0:m1]), _ptr(w.q), _ptr(w.s), _ptr(y2[m0:m1]),
+        _check(L.gpbs_hip_fp8_linear(_ptr(x2[m0:m1]), _ptr(s2[m0:m1]), _ptr(w.qs), _ptr(w.s), _ptr(y2[m0:m1]),
                                      m1 - m0, w.N, w.K, st), "fp8_linear")
     return y
 
