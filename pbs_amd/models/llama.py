@@ -166,10 +166,15 @@ class Block(nn.Module):
         G = cfg.n_heads // cfg.n_kv_heads
         qkv = llm.fp8_linear_q(*llm.rmsnorm_quant_fp8(x, self.attn_norm.weight, self.attn_norm.eps), f["qkv"])
         nq, nkv = cfg.n_heads * hd, cfg.n_kv_heads * hd
+        kc, vc = cache
+        if hd == 128 and G in (1, 2, 4, 8):  # fused gfx950 path: 2 launches between the qkv and o linears
+            q = llm.qkv_rope_cache(qkv, cos, sin, pos_i32, kc, vc, cfg.n_heads)
+            x = x + llm.fp8_linear(llm.decode_attn(q, kc, vc, pos_i32).view(B, 1, nq), f["o"])
+            gu = llm.fp8_linear_q(*llm.rmsnorm_quant_fp8(x, self.mlp_norm.weight, self.mlp_norm.eps), f["w13"])
+            return x + llm.fp8_linear_q(*llm.swiglu_quant_fp8(gu), f["w2"])
         q = llm.rope_dpos(qkv[..., :nq].reshape(B, 1, cfg.n_heads, hd), cos, sin, pos_i32)
         k = llm.rope_dpos(qkv[..., nq:nq + nkv].reshape(B, 1, cfg.n_kv_heads, hd), cos, sin, pos_i32)
         v = qkv[..., nq + nkv:].reshape(B, 1, cfg.n_kv_heads, hd)
-        kc, vc = cache
         kc.index_copy_(2, pos_i64, k.transpose(1, 2))
         vc.index_copy_(2, pos_i64, v.transpose(1, 2))
         qg = q.view(B, cfg.n_kv_heads, G, hd)

@@ -74,6 +74,38 @@ def rope_dpos(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, pos_t: torc
                                          _stream()), "rope_bf16_dpos")
     return y
 
+
+def qkv_rope_cache(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, pos_t: torch.Tensor, kc: torch.Tensor,
+                   vc: torch.Tensor, n_heads: int) -> torch.Tensor:
+    """One-token decode: split the packed qkv [B, 1, (H + 2 Hkv) hd], RoPE q and k
+    at the device position pos_t (int32 [1]), write k / v into the caches
+    [B, Hkv, C, hd] at that row, return q [B, H, hd]."""
+    B, Hkv, Cn, hd = kc.shape
+    _need(qkv, "qkv_rope_cache qkv")
+    _need(kc, "qkv_rope_cache kc")
+    _need(vc, "qkv_rope_cache vc")
+    if qkv.numel() != B * (n_heads + 2 * Hkv) * hd or vc.shape != kc.shape or cos.shape[-1] * 2 != hd \
+            or pos_t.dtype != torch.int32:
+        raise ValueError(f"qkv_rope_cache: qkv {tuple(qkv.shape)} vs cache {tuple(kc.shape)}, H={n_heads}")
+    q = torch.empty(B, n_heads, hd, dtype=torch.bfloat16, device=qkv.device)
+    _check(lib().gpbs_hip_qkv_rope_cache(_ptr(qkv), _ptr(cos), _ptr(sin), _ptr(pos_t), _ptr(q), _ptr(kc), _ptr(vc),
+                                         B, n_heads, Hkv, Cn, hd, _stream()), "qkv_rope_cache")
+    return q
+
+
+def decode_attn(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, pos_t: torch.Tensor) -> torch.Tensor:
+    """Grouped-query attention of one new token per sequence over cache rows
+    0..pos (pos_t int32 [1] on device): q [B, H, 128] -> [B, H * 128]."""
+    B, Hkv, Cn, hd = kc.shape
+    H = q.shape[1]
+    _need(q, "decode_attn q")
+    if hd != 128 or H % Hkv or (H // Hkv) not in (1, 2, 4, 8) or q.shape != (B, H, hd):
+        raise ValueError(f"decode_attn: q {tuple(q.shape)}, cache {tuple(kc.shape)} (head_dim 128, G in 1/2/4/8)")
+    out = torch.empty(B, H * hd, dtype=torch.bfloat16, device=q.device)
+    _check(lib().gpbs_hip_decode_attn(_ptr(q), _ptr(kc), _ptr(vc), _ptr(pos_t), _ptr(out), B, H, Hkv, Cn, hd,
+                                      C.c_float(hd ** -0.5), _stream()), "decode_attn")
+    return out
+
 # --------------------------------------------------------------------------- fp8 (config #5, CDNA4 fp8 MFMA)
 FP8_MAX = 448.0  # OCP e4m3fn (gfx950), not the MI300 fnuz variant
 FP8_M_TILE = 64  # rows per gpbs_hip_fp8_linear launch

@@ -143,7 +143,11 @@ def test_graph_captured_fp8_decode_matches_eager_fp8_decode():
     (k1, v1), (k2, v2) = cache_s[0], de.cache[0]
     assert (k1.float() - k2.float()).abs().max().item() < 1e-2
     assert (v1.float() - v2.float()).abs().max().item() < 1e-2
-    # graph replay == the same static step run eagerly (identical kernels)
+    # graph replay == the same static step run eagerly (identical kernels); head_dim
+    # 128 so the fused RoPE/cache + decode-attention kernels are the ones captured
+    from pbs_amd.models.llama import LlamaConfig
+    cfg = LlamaConfig(dim=512, n_layers=2, n_heads=4, n_kv_heads=1, ffn_dim=1024, vocab=1024, max_seq=256)
+    de = LlamaDecoder(cfg, batch=4, context=64, device="cuda", fp8=True)
     ds = LlamaDecoder(cfg, batch=4, context=64, device="cuda", fp8=True, static=True)
     dg = LlamaDecoder(cfg, batch=4, context=64, device="cuda", fp8=True, graph=True)
     ds.model.load_state_dict(de.model.state_dict())
@@ -155,3 +159,42 @@ def test_graph_captured_fp8_decode_matches_eager_fp8_decode():
         a, b = ds.decode_step(a), dg.decode_step(a)
         assert torch.equal(a, b)
     assert dg._g is not None and dg.pos == ds.pos == 20
+
+
+@pytest.mark.gpu
+def test_fused_decode_rope_cache_and_attention_match_reference():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from pbs_amd.models.llama import LlamaConfig, apply_rope_ref, rope_tables
+    cfg = LlamaConfig(dim=1024, n_layers=2, n_heads=8, n_kv_heads=2, ffn_dim=2048, vocab=1024, max_seq=256)
+    g = torch.Generator(device="cuda").manual_seed(2)
+    B, H, Hkv, hd, Cn, pos = 3, 8, 2, 128, 200, 137
+    cos, sin = rope_tables(cfg, "cuda")
+    kc = torch.randn(B, Hkv, Cn, hd, device="cuda", generator=g).bfloat16()
+    vc = torch.randn(B, Hkv, Cn, hd, device="cuda", generator=g).bfloat16()
+    k0, v0 = kc.clone(), vc.clone()
+    qkv = torch.randn(B, 1, (H + 2 * Hkv) * hd, device="cuda", generator=g).bfloat16()
+    pos_t = torch.full((1,), pos, dtype=torch.int32, device="cuda")
+    q = llm.qkv_rope_cache(qkv, cos, sin, pos_t, kc, vc, H)
+    qr = apply_rope_ref(qkv[..., :H * hd].float().view(B, 1, H, hd), cos[pos:pos + 1], sin[pos:pos + 1])
+    kr = apply_rope_ref(qkv[..., H * hd:(H + Hkv) * hd].float().view(B, 1, Hkv, hd), cos[pos:pos + 1],
+                        sin[pos:pos + 1])
+    assert (q.float() - qr[:, 0]).abs().max().item() < 3e-2
+    assert (kc[:, :, pos].float() - kr[:, 0]).abs().max().item() < 3e-2
+    assert torch.equal(vc[:, :, pos], qkv[..., (H + Hkv) * hd:].view(B, Hkv, hd))
+    others = torch.ones(Cn, dtype=torch.bool, device="cuda")
+    others[pos] = False
+    assert torch.equal(kc[:, :, others], k0[:, :, others]) and torch.equal(vc[:, :, others], v0[:, :, others])
+    out = llm.decode_attn(q, kc, vc, pos_t)
+    G = H // Hkv
+    qf = q.float().view(B, Hkv, G, hd)
+    sc = qf @ kc[:, :, :pos + 1].float().transpose(-1, -2) * hd ** -0.5
+    ref = (torch.softmax(sc, -1) @ vc[:, :, :pos + 1].float()).reshape(B, H * hd)
+    assert (out.float() - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
+    # short prefix (fewer keys than one wave) and pos 0
+    for p in (0, 5, 63, 64, 199):
+        pos_t.fill_(p)
+        out = llm.decode_attn(q, kc, vc, pos_t)
+        sc = qf @ kc[:, :, :p + 1].float().transpose(-1, -2) * hd ** -0.5
+        ref = (torch.softmax(sc, -1) @ vc[:, :, :p + 1].float()).reshape(B, H * hd)
+        assert (out.float() - ref).abs().max().item() < 2e-2 * ref.abs().max().item(), p
