@@ -196,7 +196,9 @@ __global__ __launch_bounds__(WV * 64) void k_fp8_gemm_skinny(const unsigned char
                                                               const float* __restrict__ sx,
                                                               const unsigned char* __restrict__ wq,
                                                               const float* __restrict__ sw,
-                                                              unsigned short* __restrict__ y, int M, int N, int K) {
+                                                              unsigned short* __restrict__ y,
+                                                              const unsigned short* __restrict__ resid, int M, int N,
+                                                              int K) {
   __shared__ f32x4 red[WV][MT][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
@@ -259,7 +261,11 @@ __global__ __launch_bounds__(WV * 64) void k_fp8_gemm_skinny(const unsigned char
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = t * 16 + 4 * (l >> 4) + i;
-      if (m < M) y[(size_t)m * N + n] = f2bf(s[i] * sx[m] * wsc);
+      if (m < M) {
+        float v = s[i] * sx[m] * wsc;
+        if (resid) v += __uint_as_float((u32)resid[(size_t)m * N + n] << 16);  // fused residual add
+        y[(size_t)m * N + n] = f2bf(v);
+      }
     }
   }
 }
@@ -274,14 +280,14 @@ static int g_fp8_opts = 0;
 
 template <int WV, bool NT>
 static void launch_fp8(const unsigned char* xp, const float* sx, const unsigned char* wp, const float* sw,
-                       unsigned short* yp, int M, int N, int K, hipStream_t s) {
+                       unsigned short* yp, const unsigned short* rp, int M, int N, int K, hipStream_t s) {
   const dim3 grid(N / 16), block(WV * 64);
   if (M <= 16)
-    hipLaunchKernelGGL((k_fp8_gemm_skinny<1, WV, NT>), grid, block, 0, s, xp, sx, wp, sw, yp, M, N, K);
+    hipLaunchKernelGGL((k_fp8_gemm_skinny<1, WV, NT>), grid, block, 0, s, xp, sx, wp, sw, yp, rp, M, N, K);
   else if (M <= 32)
-    hipLaunchKernelGGL((k_fp8_gemm_skinny<2, WV, NT>), grid, block, 0, s, xp, sx, wp, sw, yp, M, N, K);
+    hipLaunchKernelGGL((k_fp8_gemm_skinny<2, WV, NT>), grid, block, 0, s, xp, sx, wp, sw, yp, rp, M, N, K);
   else
-    hipLaunchKernelGGL((k_fp8_gemm_skinny<4, WV, NT>), grid, block, 0, s, xp, sx, wp, sw, yp, M, N, K);
+    hipLaunchKernelGGL((k_fp8_gemm_skinny<4, WV, NT>), grid, block, 0, s, xp, sx, wp, sw, yp, rp, M, N, K);
 }
 
 extern "C" {
@@ -314,19 +320,25 @@ int gpbs_hip_fp8_set_opts(int opts) {
   return prev;
 }
 
-int gpbs_hip_fp8_linear(const void* xq, const float* sx, const void* wq, const float* sw, void* y, int M, int N, int K,
-                        hipStream_t s) {
+int gpbs_hip_fp8_linear_res(const void* xq, const float* sx, const void* wq, const float* sw, void* y,
+                            const void* resid, int M, int N, int K, hipStream_t s) {
   if (M <= 0 || M > 64 || N <= 0 || N % 16 || K <= 0 || K % 256) return -22;
   const auto* xp = (const unsigned char*)xq;
   const auto* wp = (const unsigned char*)wq;
   auto* yp = (unsigned short*)y;
+  const auto* rp = (const unsigned short*)resid;
   switch (g_fp8_opts & 3) {
-    case 0: launch_fp8<kWaves, false>(xp, sx, wp, sw, yp, M, N, K, s); break;
-    case 1: launch_fp8<kWaves, true>(xp, sx, wp, sw, yp, M, N, K, s); break;
-    case 2: launch_fp8<4, true>(xp, sx, wp, sw, yp, M, N, K, s); break;
-    default: launch_fp8<4, false>(xp, sx, wp, sw, yp, M, N, K, s); break;
+    case 0: launch_fp8<kWaves, false>(xp, sx, wp, sw, yp, rp, M, N, K, s); break;
+    case 1: launch_fp8<kWaves, true>(xp, sx, wp, sw, yp, rp, M, N, K, s); break;
+    case 2: launch_fp8<4, true>(xp, sx, wp, sw, yp, rp, M, N, K, s); break;
+    default: launch_fp8<4, false>(xp, sx, wp, sw, yp, rp, M, N, K, s); break;
   }
   return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+int gpbs_hip_fp8_linear(const void* xq, const float* sx, const void* wq, const float* sw, void* y, int M, int N, int K,
+                        hipStream_t s) {
+  return gpbs_hip_fp8_linear_res(xq, sx, wq, sw, y, nullptr, M, N, K, s);
 }
 
 }  // extern "C"

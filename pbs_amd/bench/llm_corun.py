@@ -41,11 +41,12 @@ def _tenant(kind: str, seconds: float, warmup: float, socket: Optional[str], q, 
                          spatial=args.get("spatial", False), priority=args.get(f"{kind}_prio", 0))
     if kind == "infer":
         w = LlamaDecoder(PRESETS[args["infer_model"]], batch=args["infer_batch"], context=args["context"],
-                         fp8=args.get("fp8", False))
+                         fp8=args.get("fp8", False), graph=args.get("graph", False))
         prompt = torch.randint(0, w.cfg.vocab, (w.batch, args["prompt"]), device="cuda")
         nxt = w.prefill(prompt)
+        nxt = w.decode_step(nxt)  # graph mode captures here, outside any tenant slice
         flops = 2.0 * w.cfg.n_params() * w.batch
-        bytes_ = 2.0 * w.cfg.n_params()
+        bytes_ = (1.0 if w.fp8 else 2.0) * w.cfg.n_params()  # weight bytes streamed per decode step
 
         def unit():
             nonlocal nxt
@@ -153,11 +154,12 @@ def main(argv=None):
     ap.add_argument("--train-batch", type=int, default=4)
     ap.add_argument("--train-seq", type=int, default=2048)
     ap.add_argument("--fp8", action="store_true", help="decode tenant streams e4m3fn weights (fp8 MFMA linears)")
+    ap.add_argument("--graph", action="store_true", help="with --fp8: decode step replayed from a HIP graph")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     args = {"infer_model": a.infer_model, "train_model": a.train_model, "infer_batch": a.infer_batch,
             "prompt": a.prompt, "context": a.context, "train_batch": a.train_batch, "train_seq": a.train_seq,
-            "infer_weight": 512, "train_weight": 256, "fp8": a.fp8}
+            "infer_weight": 512, "train_weight": 256, "fp8": a.fp8, "graph": a.graph and a.fp8}
     res = {}
     pols = [p for p in a.policies.split(",") if p]
     if "solo" in pols:

@@ -169,9 +169,10 @@ class Block(nn.Module):
         kc, vc = cache
         if hd == 128 and G in (1, 2, 4, 8):  # fused gfx950 path: 2 launches between the qkv and o linears
             q = llm.qkv_rope_cache(qkv, cos, sin, pos_i32, kc, vc, cfg.n_heads)
-            x = x + llm.fp8_linear(llm.decode_attn(q, kc, vc, pos_i32).view(B, 1, nq), f["o"])
+            x = llm.fp8_linear_q(*llm.quant_rows_fp8(llm.decode_attn(q, kc, vc, pos_i32).view(B, 1, nq)), f["o"],
+                                 resid=x)
             gu = llm.fp8_linear_q(*llm.rmsnorm_quant_fp8(x, self.mlp_norm.weight, self.mlp_norm.eps), f["w13"])
-            return x + llm.fp8_linear_q(*llm.swiglu_quant_fp8(gu), f["w2"])
+            return llm.fp8_linear_q(*llm.swiglu_quant_fp8(gu), f["w2"], resid=x)
         q = llm.rope_dpos(qkv[..., :nq].reshape(B, 1, cfg.n_heads, hd), cos, sin, pos_i32)
         k = llm.rope_dpos(qkv[..., nq:nq + nkv].reshape(B, 1, cfg.n_kv_heads, hd), cos, sin, pos_i32)
         v = qkv[..., nq + nkv:].reshape(B, 1, cfg.n_kv_heads, hd)

@@ -53,6 +53,7 @@ def bind(lib):
     _p(lib, "gpbs_hip_rmsnorm_quant_fp8", C.c_int, vp, vp, vp, vp, C.c_int, C.c_int, C.c_float, vp)
     _p(lib, "gpbs_hip_swiglu_quant_fp8", C.c_int, vp, vp, vp, C.c_int, C.c_int, vp)
     _p(lib, "gpbs_hip_fp8_set_opts", C.c_int, C.c_int)
+    _p(lib, "gpbs_hip_fp8_linear_res", C.c_int, vp, vp, vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, vp)
     _p(lib, "gpbs_hip_fp8_linear", C.c_int, vp, vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, vp)
     _p(lib, "gpbs_hip_rope_bf16_dpos", C.c_int, vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp)
     _p(lib, "gpbs_hip_qkv_rope_cache", C.c_int, vp, vp, vp, vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int,

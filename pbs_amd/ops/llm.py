@@ -7,6 +7,7 @@ falling back to eager PyTorch.
 from __future__ import annotations
 
 import ctypes as C
+from typing import Optional
 
 import torch
 
@@ -165,15 +166,24 @@ class Fp8Weight:
         return self.qs.numel() + 4 * self.s.numel()
 
 
-def fp8_linear_q(xq: torch.Tensor, sx: torch.Tensor, w: Fp8Weight) -> torch.Tensor:
-    """y = (xq @ Wq^T) * sx[m] * sw[n] on already-quantised rows (the output of
-    quant_rows_fp8 / rmsnorm_quant_fp8 / swiglu_quant_fp8); bf16 out."""
+def fp8_linear_q(xq: torch.Tensor, sx: torch.Tensor, w: Fp8Weight, resid: Optional[torch.Tensor] = None
+                 ) -> torch.Tensor:
+    """y = (xq @ Wq^T) * sx[m] * sw[n] (+ resid, fused into the epilogue) on
+    already-quantised rows (the output of quant_rows_fp8 / rmsnorm_quant_fp8 /
+    swiglu_quant_fp8); bf16 out."""
     lead = xq.shape[:-1]
     if xq.dtype != torch.float8_e4m3fn or xq.shape[-1] != w.K or not xq.is_contiguous():
         raise ValueError(f"fp8_linear_q: need contiguous e4m3fn [..., {w.K}], got {xq.dtype} {tuple(xq.shape)}")
     M = xq.numel() // w.K
     y = torch.empty(*lead, w.N, dtype=torch.bfloat16, device=xq.device)
     L, st = lib(), _stream()
+    if resid is not None:
+        _need(resid, "fp8_linear_q resid")
+        if resid.numel() != M * w.N or M > FP8_M_TILE:
+            raise ValueError(f"fp8_linear_q: resid {tuple(resid.shape)} for [{M}, {w.N}] (M <= {FP8_M_TILE})")
+        _check(L.gpbs_hip_fp8_linear_res(_ptr(xq), _ptr(sx), _ptr(w.qs), _ptr(w.s), _ptr(y), _ptr(resid), M, w.N,
+                                         w.K, st), "fp8_linear_res")
+        return y
     if M <= FP8_M_TILE:
         _check(L.gpbs_hip_fp8_linear(_ptr(xq), _ptr(sx), _ptr(w.qs), _ptr(w.s), _ptr(y), M, w.N, w.K, st),
                "fp8_linear")

@@ -198,3 +198,17 @@ def test_fused_decode_rope_cache_and_attention_match_reference():
         sc = qf @ kc[:, :, :p + 1].float().transpose(-1, -2) * hd ** -0.5
         ref = (torch.softmax(sc, -1) @ vc[:, :, :p + 1].float()).reshape(B, H * hd)
         assert (out.float() - ref).abs().max().item() < 2e-2 * ref.abs().max().item(), p
+
+
+@pytest.mark.gpu
+def test_fp8_linear_fused_residual():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    g = torch.Generator(device="cuda").manual_seed(9)
+    W = llm.Fp8Weight((torch.randn(4096, 4096, device="cuda", generator=g) * 0.02).bfloat16())
+    x = torch.randn(8, 1, 4096, device="cuda", generator=g).bfloat16()
+    r = torch.randn(8, 1, 4096, device="cuda", generator=g).bfloat16()
+    xq, sx = llm.quant_rows_fp8(x)
+    y = llm.fp8_linear_q(xq, sx, W, resid=r)
+    ref = llm.fp8_linear_q(xq, sx, W).float() + r.float()
+    assert (y.float() - ref).abs().max().item() < 3e-2
