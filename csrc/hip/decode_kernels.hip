@@ -58,7 +58,7 @@ __global__ __launch_bounds__(256) void k_qkv_rope_cache(const u32x4* __restrict_
 }
 
 constexpr int kHd = 128;  // head_dim of every Llama-3 size
-constexpr int kAttnWaves = 4;
+constexpr int kAttnWaves = 8;
 
 __device__ __forceinline__ float wmax(float v) {
 #pragma unroll
@@ -108,16 +108,24 @@ __global__ __launch_bounds__(kAttnWaves * 64) void k_decode_attn(const u32x4* __
     float s[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) s[g] = 0.f;
+    // opaque zero: keeps the (loop-invariant) LDS query reads inside this loop, so
+    // the compiler does not hoist G x 128 floats into registers and spill
+    int z = 0;
+    asm volatile("" : "+s"(z));
+    const float* qz = &qs[0][0] + z;
     if (j < L) {
       const u32x4* kr = kh + (size_t)j * (kHd / 8);
-#pragma unroll 4
+      u32x4 krow[kHd / 8];  // the lane's whole 256-byte key row in flight at once
+#pragma unroll
+      for (int c = 0; c < kHd / 8; ++c) krow[c] = kr[c];
+#pragma unroll
       for (int c = 0; c < kHd / 8; ++c) {
-        const u32x4 kv = kr[c];
+        const u32x4 kv = krow[c];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const float k0 = bfl(kv[k]), k1 = bfh(kv[k]);
 #pragma unroll
-          for (int g = 0; g < G; ++g) s[g] += qs[g][c * 8 + 2 * k] * k0 + qs[g][c * 8 + 2 * k + 1] * k1;
+          for (int g = 0; g < G; ++g) s[g] += qz[g * kHd + c * 8 + 2 * k] * k0 + qz[g * kHd + c * 8 + 2 * k + 1] * k1;
         }
       }
     }
@@ -134,13 +142,16 @@ __global__ __launch_bounds__(kAttnWaves * 64) void k_decode_attn(const u32x4* __
       o1[g] *= corr;
       m[g] = mn;
     }
-    // PV: lane owns dims 2 lane, 2 lane + 1; key jj's weights broadcast by shuffle
+    // PV: lane owns dims 2 lane, 2 lane + 1; key jj's weight is a scalar
+    // broadcast (v_readlane), V rows are coalesced 256-byte reads, 8 in flight
+    const u32* vb = vh + (size_t)base * (kHd / 2) + lane;
+#pragma unroll 8
     for (int jj = 0; jj < nk; ++jj) {
-      const u32 vv = vh[(size_t)(base + jj) * (kHd / 2) + lane];
+      const u32 vv = vb[(size_t)jj * (kHd / 2)];
       const float v0 = bfl(vv), v1 = bfh(vv);
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        const float pj = __shfl(p[g], jj, 64);
+        const float pj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p[g]), jj));
         o0[g] += pj * v0;
         o1[g] += pj * v1;
       }

@@ -85,15 +85,18 @@ __global__ __launch_bounds__(kQuantThreads) void k_quant_rows_fp8(const u32x4* _
   }
 }
 
+template <int NT = kQuantThreads>
 __device__ __forceinline__ float block_max256(float m, float* red) {
   m = wave_max(m);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
   float r = red[0];
 #pragma unroll
-  for (int w = 1; w < kQuantThreads / 64; ++w) r = fmaxf(r, red[w]);
+  for (int w = 1; w < NT / 64; ++w) r = fmaxf(r, red[w]);
   return r;
 }
+
+constexpr int kSwigluThreads = 1024;
 
 __device__ __forceinline__ u32x2 pack_fp8x8(const float* v, float inv) {
   u32x2 o;
@@ -157,25 +160,25 @@ __global__ __launch_bounds__(kQuantThreads) void k_rmsnorm_quant_fp8(const u32x4
 
 // SwiGLU on the packed gate|up output [rows, 2F] fused with the fp8 row
 // quantiser: y = silu(gu[:, :F]) * gu[:, F:], emitted as e4m3 + row scale.
-__global__ __launch_bounds__(kQuantThreads) void k_swiglu_quant_fp8(const u32x4* __restrict__ gu,
+__global__ __launch_bounds__(kSwigluThreads) void k_swiglu_quant_fp8(const u32x4* __restrict__ gu,
                                                                   u32x2* __restrict__ q, float* __restrict__ scale,
                                                                   int f8) {
-  __shared__ float red[kQuantThreads / 64];
+  __shared__ float red[kSwigluThreads / 64];
   const size_t row = blockIdx.x;
   const u32x4* a = gu + row * 2 * f8;
   const u32x4* b = a + f8;
   float m = 0.f;
-  for (int i = threadIdx.x; i < f8; i += kQuantThreads) {
+  for (int i = threadIdx.x; i < f8; i += kSwigluThreads) {
     const u32x4 va = a[i], vb = b[i];
 #pragma unroll
     for (int e = 0; e < 4; ++e)
       m = fmaxf(m, fmaxf(fabsf(silu(bf_lo(va[e])) * bf_lo(vb[e])), fabsf(silu(bf_hi(va[e])) * bf_hi(vb[e]))));
   }
-  const float amax = block_max256(m, red);
+  const float amax = block_max256<kSwigluThreads>(m, red);
   const float inv = amax > 0.f ? kE4M3Max / amax : 1.f;
   if (threadIdx.x == 0) scale[row] = amax > 0.f ? amax / kE4M3Max : 1.f;
   u32x2* qr = q + row * f8;
-  for (int i = threadIdx.x; i < f8; i += kQuantThreads) {
+  for (int i = threadIdx.x; i < f8; i += kSwigluThreads) {
     const u32x4 va = a[i], vb = b[i];
     float f[8];
 #pragma unroll
@@ -309,7 +312,7 @@ int gpbs_hip_rmsnorm_quant_fp8(const void* x, const void* w, void* q, float* sca
 
 int gpbs_hip_swiglu_quant_fp8(const void* gu, void* q, float* scale, int rows, int f, hipStream_t s) {
   if (rows <= 0 || f <= 0 || f % 8) return -22;
-  hipLaunchKernelGGL(k_swiglu_quant_fp8, dim3(rows), dim3(kQuantThreads), 0, s, (const u32x4*)gu, (u32x2*)q, scale,
+  hipLaunchKernelGGL(k_swiglu_quant_fp8, dim3(rows), dim3(kSwigluThreads), 0, s, (const u32x4*)gu, (u32x2*)q, scale,
                      f / 8);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
