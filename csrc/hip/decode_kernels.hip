@@ -77,13 +77,18 @@ __global__ __launch_bounds__(kAttnWaves * 64) void k_decode_attn(const u32x4* __
                                                                const u32x4* __restrict__ kc,
                                                                const u32* __restrict__ vc,
                                                                const int* __restrict__ dpos, u32* __restrict__ out,
-                                                               int Hkv, int C, float scale) {
+                                                               float* __restrict__ ws, int Hkv, int C, float scale,
+                                                               int nsplit) {
   __shared__ float qs[G][kHd];
   __shared__ float ms[kAttnWaves][G], ls[kAttnWaves][G];
   __shared__ float os[kAttnWaves][G][kHd];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int b = blockIdx.x / Hkv, kvh = blockIdx.x % Hkv;
+  const int split = blockIdx.x % nsplit, bh = blockIdx.x / nsplit;
+  const int b = bh / Hkv, kvh = bh % Hkv;
   const int L = min(*dpos + 1, C);  // keys 0..pos
+  // flash-decoding split: this workgroup takes keys [k0, k1) (64-aligned chunks)
+  const int chunk = ((L + nsplit - 1) / nsplit + 63) & ~63;
+  const int k0 = split * chunk, k1 = min(L, k0 + chunk);
   const int H = G * Hkv;
   // stage the group's queries (pre-scaled) in LDS: read as broadcasts below
   for (int e = threadIdx.x; e < G * kHd / 8; e += kAttnWaves * 64) {
@@ -103,7 +108,7 @@ __global__ __launch_bounds__(kAttnWaves * 64) void k_decode_attn(const u32x4* __
 #pragma unroll
   for (int g = 0; g < G; ++g) m[g] = -INFINITY, l[g] = 0.f, o0[g] = 0.f, o1[g] = 0.f;
 
-  for (int base = w * 64; base < L; base += kAttnWaves * 64) {
+  for (int base = k0 + w * 64; base < k1; base += kAttnWaves * 64) {
     const int j = base + lane;
     float s[G];
 #pragma unroll
@@ -113,7 +118,7 @@ __global__ __launch_bounds__(kAttnWaves * 64) void k_decode_attn(const u32x4* __
     int z = 0;
     asm volatile("" : "+s"(z));
     const float* qz = &qs[0][0] + z;
-    if (j < L) {
+    if (j < k1) {
       const u32x4* kr = kh + (size_t)j * (kHd / 8);
       u32x4 krow[kHd / 8];  // the lane's whole 256-byte key row in flight at once
 #pragma unroll
@@ -129,14 +134,14 @@ __global__ __launch_bounds__(kAttnWaves * 64) void k_decode_attn(const u32x4* __
         }
       }
     }
-    const int nk = min(64, L - base);
+    const int nk = min(64, k1 - base);
     float p[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      const float sg = j < L ? s[g] : -INFINITY;
+      const float sg = j < k1 ? s[g] : -INFINITY;
       const float mn = fmaxf(m[g], wmax(sg));
       const float corr = __expf(m[g] - mn);
-      p[g] = j < L ? __expf(sg - mn) : 0.f;
+      p[g] = j < k1 ? __expf(sg - mn) : 0.f;
       l[g] = l[g] * corr + wsum(p[g]);
       o0[g] *= corr;
       o1[g] *= corr;
@@ -177,9 +182,36 @@ __global__ __launch_bounds__(kAttnWaves * 64) void k_decode_attn(const u32x4* __
       a0 += os[v][g][d] * f;
       a1 += os[v][g][d + 1] * f;
     }
-    const float inv = 1.f / Ls;
-    out[((size_t)b * H + kvh * G + g) * (kHd / 2) + d / 2] = pack2(a0 * inv, a1 * inv);
+    if (nsplit == 1) {
+      const float inv = 1.f / Ls;
+      out[((size_t)b * H + kvh * G + g) * (kHd / 2) + d / 2] = pack2(a0 * inv, a1 * inv);
+    } else {  // partial (max, sum, unnormalised o) for k_decode_attn_combine
+      float* p = ws + ((size_t)blockIdx.x * G + g) * (kHd + 2);
+      p[d] = a0;
+      p[d + 1] = a1;
+      if (d == 0) p[kHd] = M, p[kHd + 1] = Ls;
+    }
   }
+}
+
+// Merge the nsplit partials of each (batch, KV head): grid B * Hkv, G * 64 threads.
+__global__ __launch_bounds__(512) void k_decode_attn_combine(const float* __restrict__ ws, u32* __restrict__ out,
+                                                             int Hkv, int G, int nsplit) {
+  const int bh = blockIdx.x, b = bh / Hkv, kvh = bh % Hkv;
+  const int g = threadIdx.x / 64, d = 2 * (threadIdx.x % 64);
+  if (g >= G) return;
+  float M = -INFINITY;
+  for (int sp = 0; sp < nsplit; ++sp) M = fmaxf(M, ws[(((size_t)bh * nsplit + sp) * G + g) * (kHd + 2) + kHd]);
+  float Ls = 0.f, a0 = 0.f, a1 = 0.f;
+  for (int sp = 0; sp < nsplit; ++sp) {
+    const float* p = ws + (((size_t)bh * nsplit + sp) * G + g) * (kHd + 2);
+    const float f = p[kHd] == -INFINITY ? 0.f : __expf(p[kHd] - M);
+    Ls += p[kHd + 1] * f;
+    a0 += p[d] * f;
+    a1 += p[d + 1] * f;
+  }
+  const float inv = 1.f / Ls;
+  out[((size_t)b * Hkv * G + kvh * G + g) * (kHd / 2) + d / 2] = pack2(a0 * inv, a1 * inv);
 }
 
 }  // namespace gpbs_dec
@@ -198,21 +230,26 @@ int gpbs_hip_qkv_rope_cache(const void* qkv, const float* cosb, const float* sin
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-int gpbs_hip_decode_attn(const void* q, const void* kc, const void* vc, const int* dpos, void* out, int B, int H,
-                         int Hkv, int C, int hd, float scale, hipStream_t s) {
-  if (hd != kHd || B <= 0 || Hkv <= 0 || H % Hkv || C <= 0 || !dpos) return -22;
-  const dim3 grid(B * Hkv), block(kAttnWaves * 64);
-  switch (H / Hkv) {
+int gpbs_hip_decode_attn(const void* q, const void* kc, const void* vc, const int* dpos, void* out, void* ws,
+                         int nsplit, int B, int H, int Hkv, int C, int hd, float scale, hipStream_t s) {
+  if (hd != kHd || B <= 0 || Hkv <= 0 || H % Hkv || C <= 0 || !dpos || nsplit < 1 || (nsplit > 1 && !ws)) return -22;
+  const int G = H / Hkv;
+  const dim3 grid(B * Hkv * nsplit), block(kAttnWaves * 64);
+  float* w = (float*)ws;
+  switch (G) {
     case 1: hipLaunchKernelGGL(k_decode_attn<1>, grid, block, 0, s, (const u32x4*)q, (const u32x4*)kc, (const u32*)vc,
-                               dpos, (u32*)out, Hkv, C, scale); break;
+                               dpos, (u32*)out, w, Hkv, C, scale, nsplit); break;
     case 2: hipLaunchKernelGGL(k_decode_attn<2>, grid, block, 0, s, (const u32x4*)q, (const u32x4*)kc, (const u32*)vc,
-                               dpos, (u32*)out, Hkv, C, scale); break;
+                               dpos, (u32*)out, w, Hkv, C, scale, nsplit); break;
     case 4: hipLaunchKernelGGL(k_decode_attn<4>, grid, block, 0, s, (const u32x4*)q, (const u32x4*)kc, (const u32*)vc,
-                               dpos, (u32*)out, Hkv, C, scale); break;
+                               dpos, (u32*)out, w, Hkv, C, scale, nsplit); break;
     case 8: hipLaunchKernelGGL(k_decode_attn<8>, grid, block, 0, s, (const u32x4*)q, (const u32x4*)kc, (const u32*)vc,
-                               dpos, (u32*)out, Hkv, C, scale); break;
+                               dpos, (u32*)out, w, Hkv, C, scale, nsplit); break;
     default: return -22;
   }
+  if (nsplit > 1)
+    hipLaunchKernelGGL(k_decode_attn_combine, dim3(B * Hkv), dim3(G * 64), 0, s, (const float*)w, (u32*)out, Hkv, G,
+                       nsplit);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

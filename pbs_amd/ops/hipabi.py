@@ -58,8 +58,8 @@ def bind(lib):
     _p(lib, "gpbs_hip_rope_bf16_dpos", C.c_int, vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp)
     _p(lib, "gpbs_hip_qkv_rope_cache", C.c_int, vp, vp, vp, vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int,
        C.c_int, vp)
-    _p(lib, "gpbs_hip_decode_attn", C.c_int, vp, vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float,
-       vp)
+    _p(lib, "gpbs_hip_decode_attn", C.c_int, vp, vp, vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+       C.c_int, C.c_float, vp)
     _p(lib, "gpbs_hip_rope_bf16", C.c_int, vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp)
     _p(lib, "gpbs_hip_census", C.c_int, vp, C.c_int, vp, C.c_uint, C.c_uint, vp)
     _p(lib, "gpbs_hip_partition_switch", C.c_int, vp, C.c_uint, C.POINTER(C.c_uint), vp)

@@ -94,17 +94,25 @@ def qkv_rope_cache(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, pos_
     return q
 
 
-def decode_attn(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, pos_t: torch.Tensor) -> torch.Tensor:
+def decode_attn(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, pos_t: torch.Tensor,
+                nsplit: Optional[int] = None) -> torch.Tensor:
     """Grouped-query attention of one new token per sequence over cache rows
-    0..pos (pos_t int32 [1] on device): q [B, H, 128] -> [B, H * 128]."""
+    0..pos (pos_t int32 [1] on device): q [B, H, 128] -> [B, H * 128].  The keys
+    are split over `nsplit` workgroups per (batch, KV head) (flash-decoding,
+    default: enough to give the chip >= 256 workgroups) and merged by a combine
+    kernel."""
     B, Hkv, Cn, hd = kc.shape
     H = q.shape[1]
     _need(q, "decode_attn q")
     if hd != 128 or H % Hkv or (H // Hkv) not in (1, 2, 4, 8) or q.shape != (B, H, hd):
         raise ValueError(f"decode_attn: q {tuple(q.shape)}, cache {tuple(kc.shape)} (head_dim 128, G in 1/2/4/8)")
     out = torch.empty(B, H * hd, dtype=torch.bfloat16, device=q.device)
-    _check(lib().gpbs_hip_decode_attn(_ptr(q), _ptr(kc), _ptr(vc), _ptr(pos_t), _ptr(out), B, H, Hkv, Cn, hd,
-                                      C.c_float(hd ** -0.5), _stream()), "decode_attn")
+    if nsplit is None:
+        nsplit = max(1, min(8, -(-256 // (B * Hkv)), -(-Cn // 64)))
+    ws = torch.empty(B * Hkv * nsplit * (H // Hkv) * (hd + 2), dtype=torch.float32, device=q.device) \
+        if nsplit > 1 else None
+    _check(lib().gpbs_hip_decode_attn(_ptr(q), _ptr(kc), _ptr(vc), _ptr(pos_t), _ptr(out), _ptr(ws), nsplit, B, H,
+                                      Hkv, Cn, hd, C.c_float(hd ** -0.5), _stream()), "decode_attn")
     return out
 
 # --------------------------------------------------------------------------- fp8 (config #5, CDNA4 fp8 MFMA)

@@ -192,12 +192,12 @@ def test_fused_decode_rope_cache_and_attention_match_reference():
     ref = (torch.softmax(sc, -1) @ vc[:, :, :pos + 1].float()).reshape(B, H * hd)
     assert (out.float() - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
     # short prefix (fewer keys than one wave) and pos 0
-    for p in (0, 5, 63, 64, 199):
+    for p, ns in ((0, None), (5, None), (63, 4), (64, 3), (199, 1), (199, 8), (130, 2)):
         pos_t.fill_(p)
-        out = llm.decode_attn(q, kc, vc, pos_t)
+        out = llm.decode_attn(q, kc, vc, pos_t, nsplit=ns)
         sc = qf @ kc[:, :, :p + 1].float().transpose(-1, -2) * hd ** -0.5
         ref = (torch.softmax(sc, -1) @ vc[:, :, :p + 1].float()).reshape(B, H * hd)
-        assert (out.float() - ref).abs().max().item() < 2e-2 * ref.abs().max().item(), p
+        assert (out.float() - ref).abs().max().item() < 2e-2 * ref.abs().max().item(), (p, ns)
 
 
 @pytest.mark.gpu
