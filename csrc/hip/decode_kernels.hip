@@ -104,9 +104,16 @@ __global__ __launch_bounds__(kAttnWaves * 64) void k_decode_attn(const u32x4* __
   const size_t head = (size_t)b * Hkv + kvh;
   const u32x4* kh = kc + head * C * (kHd / 8);
   const u32* vh = vc + head * C * (kHd / 2);
-  float m[G], l[G], o0[G], o1[G];
+  // PV lane map: key group kg = lane >> 4 takes keys kg, kg + 4, ...; dl = lane & 15
+  // owns dims 8 dl .. 8 dl + 7 (one 16-byte V load per key)
+  const int kg = lane >> 4, dl = lane & 15;
+  float m[G], l[G], o[G][8];
 #pragma unroll
-  for (int g = 0; g < G; ++g) m[g] = -INFINITY, l[g] = 0.f, o0[g] = 0.f, o1[g] = 0.f;
+  for (int g = 0; g < G; ++g) {
+    m[g] = -INFINITY, l[g] = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[g][e] = 0.f;
+  }
 
   for (int base = k0 + w * 64; base < k1; base += kAttnWaves * 64) {
     const int j = base + lane;
@@ -143,29 +150,45 @@ __global__ __launch_bounds__(kAttnWaves * 64) void k_decode_attn(const u32x4* __
       const float corr = __expf(m[g] - mn);
       p[g] = j < k1 ? __expf(sg - mn) : 0.f;
       l[g] = l[g] * corr + wsum(p[g]);
-      o0[g] *= corr;
-      o1[g] *= corr;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[g][e] *= corr;
       m[g] = mn;
     }
-    // PV: lane owns dims 2 lane, 2 lane + 1; key jj's weight is a scalar
-    // broadcast (v_readlane), V rows are coalesced 256-byte reads, 8 in flight
-    const u32* vb = vh + (size_t)base * (kHd / 2) + lane;
-#pragma unroll 8
-    for (int jj = 0; jj < nk; ++jj) {
-      const u32 vv = vb[(size_t)jj * (kHd / 2)];
-      const float v0 = bfl(vv), v1 = bfh(vv);
+    // PV: 16 rounds of 4 keys (one per key group), 16-byte V loads, weights by shuffle
+    const u32x4* vb = reinterpret_cast<const u32x4*>(vh) + (size_t)base * (kHd / 8) + dl;
+#pragma unroll 4
+    for (int t = 0; t < 16; ++t) {
+      const int jj = 4 * t + kg;
+      float pj[G];
 #pragma unroll
-      for (int g = 0; g < G; ++g) {
-        const float pj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p[g]), jj));
-        o0[g] += pj * v0;
-        o1[g] += pj * v1;
+      for (int g = 0; g < G; ++g) pj[g] = __shfl(p[g], jj, 64);
+      if (jj < nk) {
+        const u32x4 vv = vb[(size_t)jj * (kHd / 8)];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float v0 = bfl(vv[e]), v1 = bfh(vv[e]);
+#pragma unroll
+          for (int g = 0; g < G; ++g) {
+            o[g][2 * e] += pj[g] * v0;
+            o[g][2 * e + 1] += pj[g] * v1;
+          }
+        }
       }
     }
   }
+  // sum the 4 key groups' partials (lanes dl, dl + 16, dl + 32, dl + 48)
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      o[g][e] += __shfl_xor(o[g][e], 16, 64);
+      o[g][e] += __shfl_xor(o[g][e], 32, 64);
+    }
 #pragma unroll
   for (int g = 0; g < G; ++g) {
-    os[w][g][2 * lane] = o0[g];
-    os[w][g][2 * lane + 1] = o1[g];
+    if (kg == 0)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) os[w][g][8 * dl + e] = o[g][e];
     if (lane == 0) ms[w][g] = m[g], ls[w][g] = l[g];
   }
   __syncthreads();
