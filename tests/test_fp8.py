@@ -212,3 +212,21 @@ def test_fp8_linear_fused_residual():
     y = llm.fp8_linear_q(xq, sx, W, resid=r)
     ref = llm.fp8_linear_q(xq, sx, W).float() + r.float()
     assert (y.float() - ref).abs().max().item() < 3e-2
+
+
+def test_fp8_weight_lane_order_layout_cpu():
+    """The pre-shuffled layout the MFMA kernel streams: lane l = 16 g + r of the
+    wave owning (strip, block) reads W[16 strip + r][256 block + 64 u + 16 g : +16]
+    at step u from one contiguous 1 KiB run."""
+    torch.manual_seed(1)
+    w = torch.randn(48, 768).bfloat16()
+    W = llm.Fp8Weight(w)
+    q, _ = llm.quant_rows_fp8_ref(w)
+    assert torch.equal(W.q.view(torch.uint8), q.view(torch.uint8))  # unshuffle round-trips
+    flat, rm = W.qs.view(torch.uint8).reshape(-1), q.view(torch.uint8)
+    nkb = 768 // 256
+    for strip, kb, u, lane in ((0, 0, 0, 0), (1, 2, 3, 63), (2, 1, 2, 17), (2, 2, 1, 40)):
+        g, r = lane // 16, lane % 16
+        off = ((strip * nkb + kb) * 4 + u) * 1024 + lane * 16
+        k0 = 256 * kb + 64 * u + 16 * g
+        assert torch.equal(flat[off:off + 16], rm[16 * strip + r, k0:k0 + 16])
