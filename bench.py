@@ -33,16 +33,25 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--policies", default="none,static,gpbs-ctx2,gpbs-spatial,gpbs", help="comma list; gpbs is the reported policy")
+    ap.add_argument("--policies", default="none,static,credit2,credit-fixed,gpbs-ts,credit-fixed-ts,gpbs",
+                    help="comma list; gpbs is the reported policy")
+    ap.add_argument("--reps", type=int, default=5,
+                    help="timed runs per policy, in a randomized order per repetition (median and IQR reported)")
+    ap.add_argument("--seed", type=int, default=20261016, help="policy-order shuffle seed (same on every rank)")
     ap.add_argument("--target-ms", type=float, default=30.0)
+    ap.add_argument("--protocol", default="steady", choices=["steady", "quota"],
+                    help="steady: tenants backlogged over common step windows (weighted speedup, default); "
+                         "quota: round-1 fixed per-step quotas (early finishers idle)")
+    ap.add_argument("--step-ms", type=float, default=80.0, help="steady protocol: step window length")
     ap.add_argument("--table", default="host", choices=["host", "device"])
     ap.add_argument("--out", default="")
     ap.add_argument("--rehearse", action="store_true",
                     help="multi-rank control-flow rehearsal on ONE GPU: every rank on cuda:0, gloo for the default "
                          "group and the all-reduce tenant (CPU tensors); numbers are not a measurement")
-    ap.add_argument("--counters", default="model", choices=["model", "hw"],
-                    help="PBS metric source: modeled per-tile counters, or live CDNA4 hardware counters "
-                         "(rocprofiler-sdk device counting) attributed by the model")
+    ap.add_argument("--counters", default="hw", choices=["model", "hw"],
+                    help="PBS metric source: live CDNA4 hardware counters (rocprofiler-sdk device counting, "
+                         "attributed to tenants by shader-engine ownership; default), or the modeled per-tile "
+                         "counters of the tenant kernels (debug cross-check)")
     ap.add_argument("--mix", default="4mix", choices=["4mix", "gemm2"],
                     help="4mix: BASELINE config #3/#4 (headline); gemm2: config #2 (two 4096^2 GEMM tenants)")
     args = ap.parse_args()
@@ -56,17 +65,18 @@ def main():
         sys.exit(2)
     if args.rehearse:
         local = 0
-    if args.counters == "hw":  # must register with rocprofiler before the HIP runtime starts
+    counters = args.counters
+    if counters == "hw":  # must register with rocprofiler before the HIP runtime starts
         from pbs_amd.counters import hwc
         if not hwc.init(gpu=local):
-            print("bench.py: hardware counter init failed", file=sys.stderr)
-            sys.exit(3)
+            print("bench.py: hardware counter init failed; falling back to modeled counters", file=sys.stderr)
+            counters = "model"
     torch.cuda.set_device(local)
-    if args.counters == "hw":
+    if counters == "hw":
         torch.zeros(1, device="cuda")
         if not hwc.start():
-            print("bench.py: hardware counter start failed", file=sys.stderr)
-            sys.exit(3)
+            print("bench.py: hardware counter start failed; falling back to modeled counters", file=sys.stderr)
+            counters = "model"
     groups = {}
     if world > 1:
         import torch.distributed as dist
@@ -90,26 +100,53 @@ def main():
     if "gpbs" not in pols:
         pols = pols + ("gpbs",)
     cfg = CorunConfig(steps=args.steps, warmup=args.warmup, target_ms=args.target_ms, policies=pols,
-                      table_mode=args.table, mix=args.mix, hw_counters=(args.counters == "hw"))
+                      table_mode=args.table, mix=args.mix, hw_counters=(counters == "hw"),
+                      protocol=args.protocol, step_ms=args.step_ms)
     if args.rehearse:
         cfg.coll_bytes = 4 << 20  # CPU gloo all-reduce stand-in
     log = (lambda *a: print(*a, file=sys.stderr, flush=True))
     c = Corun(cfg, rank=rank, world=world, device=local, groups=groups, log=log, coll_on_cpu=args.rehearse)
     c.calibrate()
-    results = {}
-    for p in pols:
-        results[p] = c.run_policy(p, args.steps, args.warmup)
-    g = results["gpbs"]
+    # Measurement protocol: every policy is measured `reps`
+    # times; each repetition runs the policies in a fresh random order (the
+    # same on every rank), each run = W untimed warmup steps + K timed steps.
+    import random
+    rng = random.Random(args.seed)
+    runs = {p: [] for p in pols}
+    order = []
+    for r in range(max(1, args.reps)):
+        perm = list(pols)
+        rng.shuffle(perm)
+        order += perm
+    for p in order:
+        runs[p].append(c.run_policy(p, args.steps, args.warmup))
+
+    def q(xs, f):
+        xs = sorted(xs)
+        k = (len(xs) - 1) * f
+        lo, hi = int(k), min(int(k) + 1, len(xs) - 1)
+        return xs[lo] + (xs[hi] - xs[lo]) * (k - lo)
+
+    def summ(rs, key):
+        xs = [r[key] for r in rs]
+        return {"median": round(q(xs, 0.5), 4), "iqr": round(q(xs, 0.75) - q(xs, 0.25), 4),
+                "min": round(min(xs), 4), "max": round(max(xs), 4)}
+
+    # headline run = the gpbs run with the median aggregate
+    gr = sorted(runs["gpbs"], key=lambda r: r["aggregate_all_gpus"])
+    g = gr[(len(gr) - 1) // 2]
     base = json.load(open(os.path.join(ROOT, "BASELINE.json")))
-    value = g["aggregate_all_gpus"]
+    value = q([r["aggregate_all_gpus"] for r in runs["gpbs"]], 0.5)
     line = {
         "metric": base["metric"],
         "value": round(value, 4),
-        "unit": "solo-equivalents (sum over GPUs and throughput tenants of solo_time/co-run_time)",
+        "unit": ("solo-equivalents (sum over GPUs and throughput tenants of co-run throughput / solo throughput, "
+                 "all tenants backlogged over common step windows)" if args.protocol == "steady" else
+                 "solo-equivalents (sum over GPUs and throughput tenants of solo_time/co-run_time per quota step)"),
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(g["ms_per_step"], 3),
+        "ms_per_step": round(g["ms_per_step"], 3),  # of the headline (median) gpbs run
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -119,12 +156,17 @@ def main():
         "config": {"model": ("4-tenant mix (MFMA GEMM + HBM-stream + all-reduce + idle)" if args.mix == "4mix"
                              else "2 bf16 4096^2 GEMM tenants"),
                    "global_batch": world * 4, "seq_len": 0, "parallelism": f"dp{world}" if world > 1 else "dp1",
-                   "tenants_per_gpu": 4 if args.mix == "4mix" else 2, "policy": "gpbs-pbs-credit", "mix": args.mix},
-        "mean_slowdown_pct": round(g["mean_slowdown_pct"], 2),
+                   "tenants_per_gpu": 4 if args.mix == "4mix" else 2, "policy": "gpbs (PBS credit, SE-exclusive partitions, hw counters)", "mix": args.mix},
+        "mean_slowdown_pct": round(q([r["mean_slowdown_pct"] for r in runs["gpbs"]], 0.5), 2),
+        "counters": counters,
+        "protocol": {"kind": args.protocol, "step_ms": args.step_ms if args.protocol == "steady" else None,
+                     "reps": max(1, args.reps), "order": "randomized per repetition", "seed": args.seed,
+                     "statistic": "median over reps (IQR = q75 - q25)"},
         "per_tenant": g["tenants"],
-        "policies": {p: {"aggregate_all_gpus": round(r["aggregate_all_gpus"], 4),
-                         "mean_slowdown_pct": round(r["mean_slowdown_pct"], 2),
-                         "ms_per_step": round(r["ms_per_step"], 3)} for p, r in results.items()},
+        "policies": {p: {"aggregate_all_gpus": summ(rs, "aggregate_all_gpus"),
+                         "mean_slowdown_pct": summ(rs, "mean_slowdown_pct"),
+                         "ms_per_step": round(q([r["ms_per_step"] for r in rs], 0.5), 3),
+                         "runs": [round(r["aggregate_all_gpus"], 4) for r in rs]} for p, rs in runs.items()},
         "solo_unit_ms": {k: round(v, 4) for k, v in c.solo_unit_ms.items()},
         "engine": g.get("engine", {}),
     }
@@ -133,7 +175,7 @@ def main():
         print(json.dumps(line), flush=True)
         if args.out:
             with open(args.out, "w") as f:
-                json.dump({"line": line, "results": results}, f, indent=1)
+                json.dump({"line": line, "runs": runs, "order": order}, f, indent=1)
     if world > 1:
         import torch.distributed as dist
         dist.barrier(group=groups["ctrl"])

@@ -123,6 +123,8 @@ void gpbs_boot_defaults(gpbs_boot_params_t* p) {
   p->coschedule = 0;
   p->class_period_us = 2000;
   p->boost_exclusive = 0;
+  p->class_split = 0;
+  p->idle_skip = 0;  // reference semantics (Appendix A feeds every period)
   AdaptParams a;
   std::memcpy(&p->adapt, &a, sizeof(a));
   AtcParams t;
@@ -566,6 +568,85 @@ int gpbs_set_actuator_ops(gpbs_engine_t* e, const gpbs_actuator_ops_t* ops) {
   else
     e->e->actuator_ops = gpbs_actuator_ops_t{};
   return GPBS_OK;
+}
+
+// ---------------------------------------------------- per-GPU backend mux
+// The engine lock is held by every caller of these trampolines.
+static void mux_on_switch(void* u, int part, int pt, int nt, int ns, int32_t q, int64_t now) {
+  Engine* E = (Engine*)u;
+  for (auto& m : E->mux)
+    if (part >= m.lo && part < m.hi && m.act.on_switch) m.act.on_switch(m.act.user, part, pt, nt, ns, q, now);
+}
+static void mux_on_flush(void* u, int64_t now) {
+  for (auto& m : ((Engine*)u)->mux)
+    if (m.act.on_flush) m.act.on_flush(m.act.user, now);
+}
+static void mux_on_park(void* u, int t, int s, int parked) {
+  for (auto& m : ((Engine*)u)->mux)
+    if (m.act.on_park) m.act.on_park(m.act.user, t, s, parked);
+}
+static int mux_slot_refresh(void* u, int sid, int t, int part, uint64_t* pmc) {
+  for (auto& m : ((Engine*)u)->mux)
+    if (part >= m.lo && part < m.hi && m.ctr.slot_refresh) return m.ctr.slot_refresh(m.ctr.user, sid, t, part, pmc);
+  return GPBS_ENOENT;
+}
+// Node-wide tenant deltas = the sum over the GPUs' backends (the cross-CPU
+// pmc gather of X:xen/common/sched_credit.c:416-424).  A backend that fails
+// this period contributes nothing; all failing is a stale period.
+static int mux_tenant_deltas(void* u, int n, const int* ids, uint64_t* out) {
+  Engine* E = (Engine*)u;
+  std::vector<uint64_t> part((size_t)4 * n);
+  std::fill(out, out + (size_t)4 * n, 0);
+  int ok = 0;
+  for (auto& m : E->mux) {
+    if (!m.ctr.tenant_deltas) continue;
+    if (m.ctr.tenant_deltas(m.ctr.user, n, ids, part.data()) != 0) continue;
+    ok++;
+    for (size_t i = 0; i < part.size(); ++i) out[i] += part[i];
+  }
+  return ok ? 0 : GPBS_EIO;
+}
+
+int gpbs_backend_mux_add(gpbs_engine_t* e, int part_lo, int part_hi, const gpbs_actuator_ops_t* act,
+                         const gpbs_counter_ops_t* ctr) {
+  LOCK(e);
+  if (part_lo < 0 || part_hi <= part_lo) return GPBS_EINVAL;
+  Engine* E = e->e;
+  for (auto& m : E->mux)
+    if (part_lo < m.hi && m.lo < part_hi) return GPBS_EBUSY;  // ranges are disjoint
+  Engine::MuxEntry m{part_lo, part_hi, act ? *act : gpbs_actuator_ops_t{}, ctr ? *ctr : gpbs_counter_ops_t{}};
+  E->mux.push_back(m);
+  gpbs_actuator_ops_t a{};
+  a.user = E;
+  a.on_switch = mux_on_switch;
+  a.on_flush = mux_on_flush;
+  a.on_park = mux_on_park;
+  E->actuator_ops = a;
+  gpbs_counter_ops_t k{};
+  k.user = E;
+  bool any_refresh = false, any_deltas = false;
+  for (auto& x : E->mux) {
+    any_refresh |= x.ctr.slot_refresh != nullptr;
+    any_deltas |= x.ctr.tenant_deltas != nullptr;
+  }
+  if (any_refresh) k.slot_refresh = mux_slot_refresh;
+  if (any_deltas) k.tenant_deltas = mux_tenant_deltas;
+  E->counter_ops = k;
+  return (int)E->mux.size() - 1;
+}
+
+int gpbs_backend_mux_clear(gpbs_engine_t* e) {
+  LOCK(e);
+  Engine* E = e->e;
+  E->mux.clear();
+  E->actuator_ops = gpbs_actuator_ops_t{};
+  E->counter_ops = gpbs_counter_ops_t{};
+  return GPBS_OK;
+}
+
+int gpbs_backend_mux_count(gpbs_engine_t* e) {
+  LOCK(e);
+  return (int)e->e->mux.size();
 }
 
 int gpbs_get_actuator_ops(gpbs_engine_t* e, gpbs_actuator_ops_t* out) {

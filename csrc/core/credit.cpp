@@ -579,14 +579,17 @@ class CreditScheduler : public Scheduler {
       CDom& d = sd(dom);
       d.pending_requests = dom.pending_requests;  // P7
       dom.pending_requests = 0;
-      if (!have) {
+      // The per-slot snapshots advance on every tick whichever source supplied
+      // the deltas, so a later host fallback never reports one delta spanning
+      // all the periods the device backend covered.
+      {
         for (int sid : dom.slots) {
           Slot& v = *E.slots[sid];
           CSlot& s = sv(v);
           for (int i = 0; i < kNumPmc; ++i) {
             if (v.pmc[i] < s.prev_pmc[i]) {  // Q5: counter reset -> skip sample
-              E.perfc.incr(PC_counter_reset);
-            } else {
+              if (!have) E.perfc.incr(PC_counter_reset);
+            } else if (!have) {
               deltas[4 * k + i] += v.pmc[i] - s.prev_pmc[i];
             }
             s.prev_pmc[i] = v.pmc[i];
@@ -613,6 +616,18 @@ class CreditScheduler : public Scheduler {
         CDom& d = sd(*E.tenants[ids[k]]);
         bool rearm = false;
         int dir;
+        // Q14 idle-sample rule (gpbs extension): a tenant that retired no
+        // instructions this period was not dispatched (it idles between
+        // work quotas, or its counters have not been harvested yet).  The
+        // reference feeds curr = 0 here, which the detector reads as
+        // "not cache-bound" and answers with DEC/re-arm, driving a
+        // memory-bound tenant that merely paused to the minimum quantum.
+        // The sample is skipped instead, as Q5 skips counter resets.
+        if (E.boot.idle_skip && deltas[4 * k + 0] == 0) {
+          if (dev) d.adapt = before[k];
+          E.perfc.incr(PC_adapt_idle_skip);
+          continue;
+        }
         if (!dev) {
           dir = adapt_update(d.adapt, E.adapt_params, deltas[4 * k + 0], deltas[4 * k + 3], ssum[k], scnt[k], &rearm);
         } else {
@@ -859,6 +874,9 @@ class CreditScheduler : public Scheduler {
     return score;
   }
   Slot* cosched_pick(int cpu) {
+    // SE-exclusive partitions share no issue slots: nothing to de-conflict,
+    // and a tenant on several SEs of one XCD is the intended layout.
+    if (E.boot.class_split > 1) return nullptr;
     auto& rq = pc(cpu).runq;
     Slot& head = *E.slots[rq.front()];
     const int16_t pri0 = sv(head).pri;
@@ -888,11 +906,20 @@ class CreditScheduler : public Scheduler {
   // of several bandwidth tenants each driving a few XCDs (per-CU load paths
   // cap what a partial-GPU tenant can pull, and their mixed streams thrash the
   // MALL), while credit keeps the shares fair over time.
+  // With class_split > 1 (SE-exclusive mode) a gang is a whole class group
+  // (all compute-class or all memory-class shader engines of the GPU), so a
+  // memory tenant gets every memory SE for its quantum instead of sharing
+  // them SE by SE with another memory tenant (per-CU load paths cap what one
+  // SE can pull: profiles/se_interfere_1gpu.jsonl).
+  int gang_key(int ctx) const {
+    const int split = E.boot.class_split;
+    return split > 1 ? (ctx < split ? 0 : 1) : ctx;
+  }
   int gang_leader(int cpu) const {
     const Partition& P = *E.parts[cpu];
     for (int c = cpus_.first(); c >= 0; c = cpus_.next(c + 1)) {
       const Partition& Q = *E.parts[c];
-      if (Q.gpu == P.gpu && Q.ctx == P.ctx) return c;
+      if (Q.gpu == P.gpu && gang_key(Q.ctx) == gang_key(P.ctx)) return c;
     }
     return cpu;
   }
@@ -918,7 +945,7 @@ class CreditScheduler : public Scheduler {
     for (int c = cpus_.first(); c >= 0; c = cpus_.next(c + 1)) {
       if (c == cpu) continue;
       const Partition& Q = *E.parts[c];
-      if (Q.gpu == P.gpu && Q.ctx == P.ctx) E.raise_softirq(c);
+      if (Q.gpu == P.gpu && gang_key(Q.ctx) == gang_key(P.ctx)) E.raise_softirq(c);
     }
   }
   bool gang_misaligned(int cpu, const Slot& scurr) {

@@ -732,11 +732,14 @@ void Engine::classify_tick(int64_t n) {
       continue;
     }
     t.cls = c;
-    // Class 0 (compute) lives on context 0; the memory class on every other
-    // context (with two contexts per XCD: context 1).
+    // Class 0 (compute) lives on contexts [0, class_split) -- context 0 by
+    // default; the memory class on every other context (with two contexts
+    // per XCD: context 1).  In SE-exclusive mode (class_split 2 of 4) the
+    // classes own shader engines {0,1} and {2,3} of every XCD.
+    const int split = std::max(1, boot.class_split);
     Mask m;
     for (int p = pl->cpus.first(); p >= 0; p = pl->cpus.next(p + 1))
-      if (c == 0 ? parts[p]->ctx == 0 : parts[p]->ctx >= 1) m.set(p);
+      if (c == 0 ? parts[p]->ctx < split : parts[p]->ctx >= split) m.set(p);
     if (m.empty()) m = pl->cpus;
     // Slot k goes to the k-th partition of the class (cycling), ordered
     // context-major, so a tenant with one slot per XCD lands on every XCD

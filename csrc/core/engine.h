@@ -239,6 +239,15 @@ class Engine {
   gpbs_counter_ops_t counter_ops{};
   gpbs_actuator_ops_t actuator_ops{};
   bool dirty_actuation = false;
+  // Per-GPU backend multiplexer (gpbs_backend_mux_add): one engine spanning
+  // several GPUs drives one actuator + counter backend per GPU.  Backend i
+  // serves partitions [lo, hi).
+  struct MuxEntry {
+    int lo, hi;
+    gpbs_actuator_ops_t act;
+    gpbs_counter_ops_t ctr;
+  };
+  std::vector<MuxEntry> mux;
 
   // --- time & timers (X:xen/common/timer.c analog) ---
   int64_t now() const;

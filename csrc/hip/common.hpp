@@ -96,6 +96,12 @@ __device__ __forceinline__ void finish(WorkQueue* q, u32* status, u32 total) {
 enum GateMode : u32 {
   GATE_NONE = 0, GATE_TABLE = 1, GATE_PARK = 2, GATE_DEVTABLE = 4, GATE_SPATIAL = 8,
   GATE_WAVEPRIO = 16,  // latency-class tenant: its waves win SIMD issue arbitration (s_setprio 3)
+  // Bit 5 (GATE_SE): the four partitions of an XCD are its four shader
+  // engines (8 CUs each), owned EXCLUSIVELY: a workgroup runs only on the SE
+  // whose owner word names its tenant.  Exclusive SE ownership is what makes
+  // the SE-resolved SQ/TCP hardware counters attributable per tenant
+  // (profiles/hwc/se_separation_probe.txt).
+  GATE_SE = 32,
 };
 constexpr u32 kParkSpins = 100;  // x ~20 us
 
@@ -120,6 +126,9 @@ __device__ __forceinline__ u32 hw_id() { return __builtin_amdgcn_s_getreg((31 <<
 // census kernel under one-bit CU masks), so SE >> 1 splits an XCD 16/16.
 __device__ __forceinline__ u32 cu_half() { return (hw_id() >> 14) & 1u; }
 
+// Shader engine of this wave within its XCD (HW_ID.SE_ID bits 14:13; 0..3).
+__device__ __forceinline__ u32 se_id() { return (hw_id() >> 13) & 3u; }
+
 __device__ __forceinline__ u32 load_sys(const u32* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -127,6 +136,13 @@ __device__ __forceinline__ u32 load_sys(const u32* p) {
 // Does tenant `me` own the XCD this workgroup runs on?
 __device__ __forceinline__ bool owns(const PartTable* t, u32 mode, u32 me, u32 xcc) {
   if ((mode & 3) == GATE_NONE) return true;
+  if (mode & GATE_SE) {
+    const u32 se = se_id();
+    const u32* w = t->owner + kCtx * (xcc & 7) + se;
+    const u32 o = (mode & GATE_DEVTABLE) ? __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                         : __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return (o & kOwnerMask) == me;
+  }
   // Two 8-byte loads (one cache line) cover the four contexts of the XCD.
   const u64* q = t->pair[xcc & 7];
   const u64 p01 = (mode & GATE_DEVTABLE) ? __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)

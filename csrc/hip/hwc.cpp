@@ -2,12 +2,14 @@
 // analog, S1/P1c/P4): rocprofiler-sdk's device counting service, sampled on
 // demand by the GPU counter backend each metric period.
 //
-// Four counters per XCD, summed over shader engines / L2 channels -- the PBS
-// event set mapped onto gfx950 (X:xen/common/sched_credit.c:1966 labels):
-//   INST_RETIRED      -> SQ_INSTS_VALU + SQ_INSTS_MFMA ... (configurable list)
-//   CPU_CLK_UNHALTED  -> SQ_BUSY_CYCLES
-//   LLC_REFERENCES    -> TCC_REQ
-//   LLC_MISSES        -> TCC_MISS
+// Four PBS slots, the reference event set (X:xen/common/sched_credit.c:1966
+// labels) mapped onto gfx950 counters (kDefaultSpec below).  SQ and TCP
+// counters resolve per shader engine (4 per XCD), TCC per XCD.  In the
+// SE-exclusive partition mode every SE has exactly one owner, so SE-resolved
+// deltas are attributed to tenants by ownership alone and the per-XCD TCC
+// misses by each tenant's share of the XCD's L2 requests -- the per-vCPU PMU
+// virtualisation of X:xen/arch/x86/pmustate.c:87-135, done spatially
+// (csrc/hip/runtime.cpp, hwc_tenant_deltas).
 // Values are cumulative since the context started (measured:
 // scripts/hwc_probe.hip).  gpbs_hwc_init must run before the HIP runtime
 // initialises in the process (rocprofiler_force_configure); gpbs_hwc_start
@@ -25,15 +27,21 @@
 namespace {
 
 constexpr int kX = 8;  // XCDs per MI355X
+constexpr int kSe = 4; // shader engines per XCD
 constexpr int kSlots = 4;
+constexpr const char* kDefaultSpec =
+    "SQ_INSTS_VALU+SQ_INSTS_SALU+SQ_INSTS_VMEM_RD+SQ_INSTS_VMEM_WR+SQ_INSTS_LDS+"
+    "SQ_INSTS_VALU_MFMA_MOPS_BF16|SQ_BUSY_CYCLES|"
+    "TCP_TCC_READ_REQ+TCP_TCC_WRITE_REQ|TCC_MISS";
 
 struct Hwc {
   rocprofiler_context_id_t ctx{};
   std::vector<rocprofiler_agent_id_t> gpus;
   std::vector<rocprofiler_counter_config_id_t> cfg;
   std::map<uint64_t, int> slot_of;            // counter id -> PBS slot (0..3)
-  rocprofiler_counter_dimension_id_t xcc_dim{};
-  bool have_xcc = false;
+  rocprofiler_counter_dimension_id_t xcc_dim{}, se_dim{};
+  bool have_xcc = false, have_se = false;
+  std::map<uint64_t, bool> per_se;            // counter id -> resolved per shader engine (SQ, TCP)
   std::vector<std::string> names[kSlots];
   bool configured = false, started = false;
   int only_gpu = -1;  // count on this GPU agent only (rank-local), -1 = all
@@ -63,11 +71,18 @@ rocprofiler_status_t on_counters(rocprofiler_agent_id_t, rocprofiler_counter_id_
         if (w == info.name) {
           out->push_back(c[i]);
           g.slot_of[c[i].handle] = s;
-          for (uint64_t d = 0; d < info.dimensions_count; ++d)
+          g.per_se[c[i].handle] = false;
+          for (uint64_t d = 0; d < info.dimensions_count; ++d) {
             if (std::strcmp(info.dimensions[d]->name, "DIMENSION_XCC") == 0) {
               g.xcc_dim = info.dimensions[d]->id;
               g.have_xcc = true;
             }
+            if (std::strcmp(info.dimensions[d]->name, "DIMENSION_SHADER_ENGINE") == 0) {
+              g.se_dim = info.dimensions[d]->id;
+              g.have_se = true;
+              g.per_se[c[i].handle] = true;
+            }
+          }
         }
   }
   return ROCPROFILER_STATUS_SUCCESS;
@@ -128,7 +143,17 @@ void split(const char* s, std::vector<std::string>& out) {
 extern "C" {
 
 // spec: four '|'-separated groups of '+'-joined counter names, one per PBS
-// slot; NULL = "SQ_INSTS_VALU+SQ_INSTS_SALU|SQ_BUSY_CYCLES|TCC_REQ|TCC_MISS".
+// slot; NULL = kDefaultSpec (the PBS event set on gfx950, one pass: 7 SQ,
+// 2 TCP and 1 TCC counters, within the 8/4/4 per-block limits):
+//   INST_RETIRED     SQ_INSTS_VALU + SALU + VMEM_RD + VMEM_WR + LDS wave-instructions
+//                    + SQ_INSTS_VALU_MFMA_MOPS_BF16 (matrix ops / 512)   (per SE)
+//                    -- work-normalised: one 16x16x32 MFMA does the arithmetic of
+//                    ~32 wave-instructions, and counting it once made an LDS-tiled
+//                    GEMM's panel re-reads (L2 misses that hit the Infinity Cache)
+//                    look as miss-dense as an HBM stream's (2.1e4 vs 1.1e5 per 1e5)
+//   CPU_CLK_UNHALTED SQ_BUSY_CYCLES                                   (per SE)
+//   LLC_REFERENCES   TCP_TCC_READ_REQ + TCP_TCC_WRITE_REQ (L1 misses = L2 requests, per SE)
+//   LLC_MISSES       TCC_MISS                                         (per XCD: the L2 is per XCD)
 // Must precede HIP runtime initialisation.  `gpu` >= 0 restricts counting to
 // that GPU agent (agents in enumeration order; one rank per GPU).  0 on success.
 int gpbs_hwc_init_gpu(const char* spec, int gpu);
@@ -137,7 +162,7 @@ int gpbs_hwc_init(const char* spec) { return gpbs_hwc_init_gpu(spec, -1); }
 int gpbs_hwc_init_gpu(const char* spec, int gpu) {
   std::lock_guard<std::mutex> l(g.mu);
   g.only_gpu = gpu;
-  std::string sp = spec && *spec ? spec : "SQ_INSTS_VALU+SQ_INSTS_SALU|SQ_BUSY_CYCLES|TCC_REQ|TCC_MISS";
+  std::string sp = spec && *spec ? spec : kDefaultSpec;
   size_t pos = 0;
   for (int s = 0; s < kSlots; ++s) {
     const size_t e = sp.find('|', pos);
@@ -181,6 +206,51 @@ int gpbs_hwc_sample(uint64_t* out, int nxcd) {
   for (int x = 0; x < kX; ++x)
     for (int s = 0; s < kSlots; ++s) out[x * kSlots + s] = (uint64_t)acc[x][s];
   return (int)n;
+}
+
+// Cumulative counters resolved per shader engine: se_out[(xcd*4 + se)*4 + slot]
+// for the SE-resolved counters (SQ, TCP; 0 for the others) and
+// x_out[xcd*4 + slot] summed over everything of the XCD (TCC, GRBM and the
+// SE-resolved ones).  Synchronous (~0.2 ms: profiles/hwc/sample_latency_probe.txt);
+// callers sample from their own thread, never under the engine lock.
+int gpbs_hwc_sample_se(uint64_t* se_out, uint64_t* x_out) {
+  std::lock_guard<std::mutex> l(g.mu);
+  if (!g.started || !se_out || !x_out) return -1;
+  if (g.rec.empty()) g.rec.resize(16384);
+  size_t n = g.rec.size();
+  if (rocprofiler_sample_device_counting_service(g.ctx, {}, ROCPROFILER_COUNTER_FLAG_NONE, g.rec.data(), &n) !=
+      ROCPROFILER_STATUS_SUCCESS)
+    return -1;
+  double se_acc[kX][kSe][kSlots] = {}, x_acc[kX][kSlots] = {};
+  for (size_t i = 0; i < n; ++i) {
+    rocprofiler_counter_id_t cid{};
+    if (rocprofiler_query_record_counter_id(g.rec[i].id, &cid) != ROCPROFILER_STATUS_SUCCESS) continue;
+    auto it = g.slot_of.find(cid.handle);
+    if (it == g.slot_of.end()) continue;
+    size_t x = 0, se = 0;
+    if (g.have_xcc) rocprofiler_query_record_dimension_position(g.rec[i].id, g.xcc_dim, &x);
+    if (x >= (size_t)kX) continue;
+    x_acc[x][it->second] += g.rec[i].counter_value;
+    if (g.per_se[cid.handle] &&
+        rocprofiler_query_record_dimension_position(g.rec[i].id, g.se_dim, &se) == ROCPROFILER_STATUS_SUCCESS &&
+        se < (size_t)kSe)
+      se_acc[x][se][it->second] += g.rec[i].counter_value;
+  }
+  for (int x = 0; x < kX; ++x)
+    for (int k = 0; k < kSlots; ++k) {
+      x_out[x * kSlots + k] = (uint64_t)x_acc[x][k];
+      for (int e = 0; e < kSe; ++e) se_out[(x * kSe + e) * kSlots + k] = (uint64_t)se_acc[x][e][k];
+    }
+  return (int)n;
+}
+
+// 1 if slot k's counters are resolved per shader engine.
+int gpbs_hwc_slot_per_se(int k) {
+  std::lock_guard<std::mutex> l(g.mu);
+  if (k < 0 || k >= kSlots) return 0;
+  for (auto& kv : g.slot_of)
+    if (kv.second == k) return g.per_se[kv.first] ? 1 : 0;
+  return 0;
 }
 
 int gpbs_hwc_stop(void) {

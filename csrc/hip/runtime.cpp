@@ -31,6 +31,8 @@ using namespace gpbs_hip;
 extern "C" {
 int gpbs_hip_gemm_units(int, int);
 int gpbs_hwc_sample(uint64_t* out, int nxcd);
+int gpbs_hwc_sample_se(uint64_t* se_out, uint64_t* x_out);
+int gpbs_hwc_slot_per_se(int k);
 int gpbs_hwc_active(void);
 int gpbs_hip_gemm_bf16(const void*, const void*, void*, int, int, int, void*, const void*, unsigned, unsigned, void*,
                        void*, int, hipStream_t);
@@ -80,16 +82,22 @@ struct GpuCtx {
   int* h_ids2 = nullptr;
   u64* h_out2 = nullptr;
   hipEvent_t red_ev = nullptr;
-  // Live hardware counters (csrc/hip/hwc.cpp): per-XCD deltas attributed to
-  // tenants in proportion to their modeled per-XCD activity.
-  // A sampler thread snapshots the model block and the hardware at one
-  // instant every period (a synchronous device-counting sample costs
-  // ~0.2 ms -- never under the engine lock); the metric tick consumes the
-  // newest snapshot pair.
+  // Live hardware counters (csrc/hip/hwc.cpp), attributed by OWNERSHIP (the
+  // per-vCPU PMU save/restore of X:xen/arch/x86/pmustate.c:87-135 done in
+  // space): a sampler thread snapshots, at one instant every period, the
+  // cumulative per-(XCD, SE) and per-XCD hardware counters together with
+  // the cumulative ns every tenant has owned every partition; the metric tick
+  // (engine lock held) only does arithmetic on the newest snapshot pair.  A
+  // synchronous device-counting sample costs ~0.2 ms, so it never runs under
+  // the engine lock.  The modeled per-tile block is snapshotted alongside as
+  // a cross-check (attribution error vs model), never as an input.
   int hwc = 0;
+  int slot_se[kNumPmc] = {1, 1, 1, 0};  // slot k resolved per shader engine
   u64* h_blk = nullptr;                 // pinned landing buffer of d_cnt copies
   std::vector<u64> snap_blk, blk_prev;  // newest published / last consumed model block
-  u64 snap_hw[kXcds * kNumPmc] = {}, hw_prev[kXcds * kNumPmc] = {};
+  std::vector<u64> snap_se, se_prev;    // [kXcds * kCtx(=SEs) * kNumPmc]
+  std::vector<u64> snap_x, x_prev;      // [kXcds * kNumPmc]
+  std::vector<int64_t> snap_own, own_prev;  // [kMaxTenants * kXcds * kCtx]
   uint64_t snap_seq = 0, used_seq = 0;
   bool hw_primed = false;
   hipEvent_t blk_ev = nullptr;
@@ -98,18 +106,36 @@ struct GpuCtx {
   std::atomic<bool> hwc_stop{false};
   std::mutex snap_mu;
   int hwc_period_us = 1000;
-  int64_t hwc_ns = 0;
+  int64_t hwc_ns = 0, hwc_ns_max = 0;
   uint64_t hwc_samples = 0;
   double hw_sum[kNumPmc] = {}, model_sum[kNumPmc] = {};  // attributed vs modeled totals
+  double unatt[kNumPmc] = {};                             // hardware counts no owner explains
+  double att_total[kMaxTenants][kNumPmc] = {};            // per-tenant attributed hardware totals
+  double mod_total[kMaxTenants][kNumPmc] = {};            // per-tenant modeled totals (cross-check)
   u64 last_delta[kMaxTenants][kNumPmc];
   std::mutex mu;
   std::condition_variable cv;
   std::atomic<uint64_t> switches{0}, flushes{0}, metric_calls{0};
   int64_t metric_ns = 0;
-  // ownership accounting: ns each tenant held a context, per context index
-  int64_t own_ns[kMaxTenants][kCtx];
+  // ownership accounting: cumulative ns each tenant held each partition
+  // (xcd * kCtx + ctx), and the base the ownership() query subtracts
+  int64_t own_ns[kMaxTenants][kXcds * kCtx];
+  int64_t own_base[kMaxTenants][kXcds * kCtx];
   int64_t last_pub_ns = 0;
+  int se_mode = 0;  // partitions are exclusive shader engines (GATE_SE)
 };
+
+// Cumulative ownership ns of every (tenant, partition) up to now, including
+// the interval since the last table change.  Caller holds c->mu.
+void own_snapshot_locked(const GpuCtx* c, int64_t* out) {
+  const int64_t t = mono_ns();
+  std::memcpy(out, c->own_ns, sizeof(c->own_ns));
+  if (!c->last_pub_ns) return;
+  for (int x = 0; x < kXcds * kCtx; ++x) {
+    const u32 o = c->h_table->owner[x] & kOwnerMask;
+    if (o < (u32)kMaxTenants) out[o * kXcds * kCtx + x] += t - c->last_pub_ns;
+  }
+}
 
 // ---------------------------------------------------------------- engine hooks
 
@@ -156,7 +182,7 @@ void publish(GpuCtx* c) {
     if (c->last_pub_ns)
       for (int x = 0; x < kXcds * kCtx; ++x) {
         const u32 o = c->h_table->owner[x] & kOwnerMask;
-        if (o < (u32)kMaxTenants) c->own_ns[o][x % kCtx] += t - c->last_pub_ns;
+        if (o < (u32)kMaxTenants) c->own_ns[o][x] += t - c->last_pub_ns;
       }
     c->last_pub_ns = t;
     for (int x = 0; x < kXcds * kCtx; ++x) __atomic_store_n(&c->h_table->owner[x], c->pending[x], __ATOMIC_RELEASE);
@@ -179,22 +205,31 @@ void act_on_park(void*, int, int, int) {}
 void hwc_loop(GpuCtx* c) {
   hipSetDevice(c->device);
   constexpr int kBlk = kMaxTenants * kXcds * kNumPmc;
-  std::vector<u64> blk(kBlk);
-  u64 hw[kXcds * kNumPmc];
+  constexpr int kOwn = kMaxTenants * kXcds * kCtx;
+  std::vector<u64> blk(kBlk), se(kXcds * kCtx * kNumPmc), xs(kXcds * kNumPmc);
+  std::vector<int64_t> own(kOwn);
   while (!c->hwc_stop.load(std::memory_order_acquire)) {
     const int64_t t0 = mono_ns();
     if (hipMemcpyAsync(c->h_blk, c->d_cnt, sizeof(u64) * kBlk, hipMemcpyDeviceToHost, c->hwc_stream) != hipSuccess)
       break;
     hipEventRecord(c->blk_ev, c->hwc_stream);
-    const int rc = gpbs_hwc_sample(reinterpret_cast<uint64_t*>(hw), kXcds);
+    const int rc = gpbs_hwc_sample_se(reinterpret_cast<uint64_t*>(se.data()), reinterpret_cast<uint64_t*>(xs.data()));
+    {
+      std::lock_guard<std::mutex> g(c->mu);
+      own_snapshot_locked(c, own.data());
+    }
     hipEventSynchronize(c->blk_ev);
     if (rc >= 0) {
       std::memcpy(blk.data(), c->h_blk, sizeof(u64) * kBlk);
       std::lock_guard<std::mutex> g(c->snap_mu);
       c->snap_blk.swap(blk);
-      std::memcpy(c->snap_hw, hw, sizeof(hw));
+      c->snap_se.swap(se);
+      c->snap_x.swap(xs);
+      c->snap_own.swap(own);
       c->snap_seq++;
-      c->hwc_ns += mono_ns() - t0;
+      const int64_t dt = mono_ns() - t0;
+      c->hwc_ns += dt;
+      if (dt > c->hwc_ns_max) c->hwc_ns_max = dt;
       c->hwc_samples++;
     }
     const int64_t rest = (int64_t)c->hwc_period_us * 1000 - (mono_ns() - t0);
@@ -202,36 +237,110 @@ void hwc_loop(GpuCtx* c) {
   }
 }
 
+inline u64 dpos(u64 a, u64 b) { return a >= b ? a - b : 0; }  // Q5: a counter reset is no negative delta
+
+// Ownership attribution of one snapshot interval (snap_mu held).
+//  * SE-resolved slots in SE-exclusive mode: the delta of partition (x, e)
+//    goes to the tenants that owned it in the interval, pro rata to owned
+//    time -- exact while ownership is stable over a sample interval.
+//  * Co-resident modes (every owner's waves run on all SEs of the XCD): the
+//    XCD's delta is split by owned time (an approximation, reported as such).
+//  * LLC misses (TCC, per XCD): split by each tenant's attributed share of the
+//    XCD's L2 requests (both measured).
+// Counts no owner explains (an SE nobody owned: stray workgroups draining
+// after a revocation, the scheduler's own kernels) are kept as unattributed.
+void hwc_attribute(GpuCtx* c) {
+  constexpr int P = kXcds * kCtx;
+  std::vector<double> own_d((size_t)kMaxTenants * P, 0.0);
+  for (int t = 0; t < kMaxTenants; ++t)
+    for (int p = 0; p < P; ++p) {
+      const size_t i = (size_t)t * P + p;
+      const int64_t d = c->snap_own[i] - c->own_prev[i];
+      own_d[i] = d > 0 ? (double)d : 0.0;
+    }
+  double refs_x[kMaxTenants][kXcds] = {};
+  double add[kMaxTenants][kNumPmc] = {};
+  for (int k = 0; k < kNumPmc; ++k) {
+    const bool miss_by_refs = k == 3;
+    for (int x = 0; x < kXcds; ++x) {
+      if (c->se_mode && c->slot_se[k]) {
+        for (int e = 0; e < kCtx; ++e) {
+          const int p = x * kCtx + e;
+          const double v = (double)dpos(c->snap_se[(size_t)p * kNumPmc + k], c->se_prev[(size_t)p * kNumPmc + k]);
+          c->hw_sum[k] += v;
+          double tot = 0;
+          for (int t = 0; t < kMaxTenants; ++t) tot += own_d[(size_t)t * P + p];
+          if (tot <= 0) {
+            c->unatt[k] += v;
+            continue;
+          }
+          for (int t = 0; t < kMaxTenants; ++t) {
+            const double w = own_d[(size_t)t * P + p];
+            if (w <= 0) continue;
+            add[t][k] += v * w / tot;
+            if (k == 2) refs_x[t][x] += v * w / tot;
+          }
+        }
+        continue;
+      }
+      const double v = (double)dpos(c->snap_x[(size_t)x * kNumPmc + k], c->x_prev[(size_t)x * kNumPmc + k]);
+      c->hw_sum[k] += v;
+      double wt[kMaxTenants] = {}, tot = 0;
+      if (miss_by_refs) {
+        for (int t = 0; t < kMaxTenants; ++t) tot += (wt[t] = refs_x[t][x]);
+      }
+      if (tot <= 0) {  // time share over every context of the XCD
+        tot = 0;
+        for (int t = 0; t < kMaxTenants; ++t) {
+          wt[t] = 0;
+          for (int e = 0; e < kCtx; ++e) wt[t] += own_d[(size_t)t * P + x * kCtx + e];
+          tot += wt[t];
+        }
+      }
+      if (tot <= 0) {
+        c->unatt[k] += v;
+        continue;
+      }
+      for (int t = 0; t < kMaxTenants; ++t)
+        if (wt[t] > 0) {
+          add[t][k] += v * wt[t] / tot;
+          if (k == 2) refs_x[t][x] += v * wt[t] / tot;
+        }
+    }
+  }
+  for (int t = 0; t < kMaxTenants; ++t)
+    for (int k = 0; k < kNumPmc; ++k) {
+      if (add[t][k] > 0) {
+        const u64 a = (u64)(add[t][k] + 0.5);
+        c->last_delta[t][k] += a;
+        c->att_total[t][k] += add[t][k];
+      }
+      double m = 0;
+      for (int x = 0; x < kXcds; ++x) {
+        const size_t i = ((size_t)t * kXcds + x) * kNumPmc + k;
+        m += (double)dpos(c->snap_blk[i], c->blk_prev[i]);
+      }
+      c->mod_total[t][k] += m;
+      c->model_sum[k] += m;
+    }
+}
+
 int hwc_tenant_deltas(GpuCtx* c, int n, const int* tenants, uint64_t* out) {
   const int64_t t0 = mono_ns();
   {
     std::lock_guard<std::mutex> g(c->snap_mu);
-    if (c->snap_seq != c->used_seq && (int)c->snap_blk.size() == kMaxTenants * kXcds * kNumPmc) {
+    if (c->snap_seq != c->used_seq && !c->snap_own.empty()) {
       c->used_seq = c->snap_seq;
-      if (c->hw_primed) {
-        for (int x = 0; x < kXcds; ++x)
-          for (int k = 0; k < kNumPmc; ++k) {
-            const u64 hw_d = c->snap_hw[x * kNumPmc + k] - c->hw_prev[x * kNumPmc + k];
-            double denom = 0;
-            for (int t = 0; t < kMaxTenants; ++t) {
-              const size_t i = ((size_t)t * kXcds + x) * kNumPmc + k;
-              denom += (double)(c->snap_blk[i] - c->blk_prev[i]);
-            }
-            if (denom <= 0) continue;
-            c->hw_sum[k] += (double)hw_d;
-            c->model_sum[k] += denom;
-            for (int t = 0; t < kMaxTenants; ++t) {
-              const size_t i = ((size_t)t * kXcds + x) * kNumPmc + k;
-              const u64 md = c->snap_blk[i] - c->blk_prev[i];
-              if (md) c->last_delta[t][k] += (u64)((double)hw_d * (double)md / denom);
-            }
-          }
-      }
+      if (c->hw_primed) hwc_attribute(c);
       c->blk_prev = c->snap_blk;
-      std::memcpy(c->hw_prev, c->snap_hw, sizeof(c->hw_prev));
+      c->se_prev = c->snap_se;
+      c->x_prev = c->snap_x;
+      c->own_prev = c->snap_own;
       c->hw_primed = true;
     }
   }
+  // No new snapshot since the previous tick: every tenant reads zero
+  // instructions and the PBS idle-sample rule (Q14) skips the period.
   for (int k = 0; k < n; ++k)
     for (int i = 0; i < kNumPmc; ++i) {
       const int t = tenants[k];
@@ -248,8 +357,16 @@ int ctr_tenant_deltas(void* user, int n, const int* tenants, uint64_t* out) {
   if (n > kMaxTenants) return -22;
   if (c->hwc) return hwc_tenant_deltas(c, n, tenants, out);
   const int64_t t0 = mono_ns();
+  if (c->red_pending && hipEventQuery(c->red_ev) == hipErrorNotReady) {
+    // The previous reduce has not finished (a tail, ~0.1 % of periods): never
+    // wait for it under the engine lock.  This period reports nothing (the
+    // idle-sample rule skips it) and the next tick harvests both periods.
+    for (int k = 0; k < n * kNumPmc; ++k) out[k] = 0;
+    c->metric_calls++;
+    c->metric_ns += mono_ns() - t0;
+    return 0;
+  }
   if (c->red_pending) {
-    if (hipEventQuery(c->red_ev) == hipErrorNotReady) hipEventSynchronize(c->red_ev);
     const int* ids = c->red_buf ? c->h_ids2 : c->h_ids;
     const u64* res = c->red_buf ? c->h_out2 : c->h_out;
     for (int k = 0; k < c->red_n; ++k)
@@ -340,11 +457,27 @@ hipStream_t make_half_stream(int h) {
   return s;
 }
 
+// CU mask of a set of (XCD, SE) partitions: bit b = logical CU b/8 of XCD
+// b%8, which sits on SE (b/8)%4.  se_bits[x] = SEs of XCD x in the set.
+void se_cu_mask(const u32 se_bits[kXcds], uint32_t m[8]) {
+  for (int w = 0; w < 8; ++w) m[w] = 0;
+  for (int b = 0; b < 256; ++b)
+    if (se_bits[b % 8] & (1u << ((b / 8) % 4))) m[b / 32] |= 1u << (b % 32);
+}
+
 struct Runner {
   GpuCtx* ctx;
   gpbs_runner_cfg_t cfg;
   hipStream_t stream = nullptr;
   hipStream_t half_stream[2] = {nullptr, nullptr};  // spatial mode: CU-masked to one half
+  // SE-exclusive mode: streams CU-masked to the class half the tenant
+  // owns.  A workgroup of a full-GPU grid that lands on a
+  // foreign SE cannot just exit: it may have to wait for that SE's owner to
+  // free resources before it is even dispatched, and the kernel -- and the
+  // next one on the stream -- completes only after it has.  Confining the
+  // grid to the owned CUs removes that coupling (GATE_SE still revokes).
+  hipStream_t se_stream[2] = {nullptr, nullptr};  // SEs {0,1} / {2,3} of every XCD
+  int cur_grid = 0;  // grid for the stream pick_stream chose (0: kernel default)
   WorkQueue* d_q = nullptr;  // ring of depth+1 queues
   u32* h_status = nullptr;   // pinned status words
   int nq = 0;
@@ -373,7 +506,51 @@ struct Runner {
   // Spatial mode: launch on the stream masked to the CU half the tenant holds
   // (class pinning keeps a classified tenant on one half); a tenant holding
   // both halves or none (yet) launches unmasked and gates per workgroup.
+  // The mask is quantised to the two class halves (SEs {0,1} / {2,3} of every
+  // XCD), so a runner creates at most two masked streams: every CU mask is a
+  // hardware queue of its own, and past the hardware's queue slots the
+  // scheduler time-multiplexes queues (measured: arbitrary per-(XCD, SE)
+  // masks over four runners collapsed even ungated co-runs to 0.42).  An
+  // owned set that fits neither half (work-conserving steals across
+  // classes) launches unmasked and gates per workgroup.
+  hipStream_t pick_se_stream() {
+    u32 any = 0;
+    for (int x = 0; x < kXcds; ++x)
+      for (int e = 0; e < kCtx; ++e)
+        if ((__atomic_load_n(&ctx->h_table->owner[kCtx * x + e], __ATOMIC_ACQUIRE) & kOwnerMask) == (u32)cfg.tenant)
+          any |= 1u << e;
+    const int half = (any & ~0x3u) == 0 ? 0 : ((any & ~0xCu) == 0 ? 1 : -1);
+    if (!any || half < 0) return stream;
+    if (!se_stream[half]) {
+      u32 bits[kXcds];
+      for (int x = 0; x < kXcds; ++x) bits[x] = half ? 0xCu : 0x3u;
+      uint32_t m[8];
+      se_cu_mask(bits, m);
+      if (hipExtStreamCreateWithCUMask(&se_stream[half], 8, m) != hipSuccess) {
+        se_stream[half] = nullptr;
+        return stream;
+      }
+    }
+    cur_grid = (cfg.kind == K_GEMV) ? 0 : 128;  // one persistent workgroup per CU of the half
+    return se_stream[half];
+  }
+
+  // Leaving SE mode releases the masked queues (a later ungated policy must
+  // not share the hardware with idle masked queues).  Runner thread only.
+  void drop_se_streams() {
+    for (auto& h : se_stream)
+      if (h) {
+        hipStreamSynchronize(h);
+        hipStreamDestroy(h);
+        h = nullptr;
+      }
+  }
+
   hipStream_t pick_stream() {
+    cur_grid = 0;
+    const bool se = __atomic_load_n(&ctx->se_mode, __ATOMIC_ACQUIRE);
+    if (cfg.gate && se) return pick_se_stream();
+    if (!se && (se_stream[0] || se_stream[1])) drop_se_streams();
     if (!ctx->spatial || !cfg.gate) return stream;
     // Masked only if every XCD the tenant holds is split and it holds the
     // same half of all of them; otherwise unmasked + per-workgroup gating.
@@ -400,23 +577,24 @@ struct Runner {
     const void* tab = dev ? (const void*)ctx->d_table : (const void*)ctx->h_table;
     const unsigned mode = (cfg.gate ? (cfg.gate == 2 ? GATE_PARK : GATE_TABLE) : GATE_NONE) | (dev ? GATE_DEVTABLE : 0) |
                           (cfg.gate && ctx->spatial ? GATE_SPATIAL : 0) |
-                          (cfg.gate && cfg.priority > 0 && ctx->waveprio ? GATE_WAVEPRIO : 0);
+                          (cfg.gate && __atomic_load_n(&ctx->se_mode, __ATOMIC_ACQUIRE) ? GATE_SE : 0) |
+                          (cfg.priority > 0 && ctx->waveprio ? GATE_WAVEPRIO : 0);
     const unsigned me = (unsigned)cfg.tenant;
     __atomic_store_n(&h_status[qi], 0u, __ATOMIC_RELEASE);
     st.launches++;
     switch (cfg.kind) {
       case K_GEMM:
         return gpbs_hip_gemm_bf16(cfg.a, cfg.b, cfg.c, cfg.M, cfg.N, cfg.K, q, tab, mode, me, ctx->d_cnt,
-                                  &h_status[qi], cfg.grid, stream);
+                                  &h_status[qi], cfg.grid ? cfg.grid : cur_grid, stream);
       case K_STREAM:
         return gpbs_hip_stream_copy(cfg.a, cfg.c, cfg.bytes, (unsigned)cfg.chunk_bytes, q, tab, mode, me, ctx->d_cnt,
-                                    &h_status[qi], cfg.grid, stream);
+                                    &h_status[qi], cfg.grid ? cfg.grid : cur_grid, stream);
       case K_REDUCE:
         return gpbs_hip_reduce_bf16(cfg.a, cfg.b, cfg.c, cfg.bytes, (unsigned)cfg.chunk_bytes, q, tab, mode, me,
-                                    ctx->d_cnt, &h_status[qi], cfg.grid, stream);
+                                    ctx->d_cnt, &h_status[qi], cfg.grid ? cfg.grid : cur_grid, stream);
       case K_GEMV:
         return gpbs_hip_gemv_bf16(cfg.a, cfg.b, cfg.c, cfg.M, cfg.K, q, tab, mode, me, ctx->d_cnt, &h_status[qi],
-                                  cfg.grid, stream);
+                                  cfg.grid ? cfg.grid : cur_grid, stream);
     }
     return -22;
   }
@@ -551,6 +729,8 @@ struct Runner {
     hipStreamSynchronize(stream);
     for (hipStream_t h : half_stream)
       if (h) hipStreamSynchronize(h);
+    for (hipStream_t h : se_stream)
+      if (h) hipStreamSynchronize(h);
     std::lock_guard<std::mutex> g(mu);
     idle_cv.notify_all();
   }
@@ -569,6 +749,7 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
   c->nctx = nctx < 1 ? 1 : (nctx > kCtx ? kCtx : nctx);
   std::memset(c->last_delta, 0, sizeof(c->last_delta));
   std::memset(c->own_ns, 0, sizeof(c->own_ns));
+  std::memset(c->own_base, 0, sizeof(c->own_base));
   bool ok = hipHostMalloc((void**)&c->h_table, sizeof(PartTable), hipHostMallocCoherent | hipHostMallocMapped) ==
             hipSuccess;
   ok = ok && hipMalloc((void**)&c->d_cnt, sizeof(u64) * kMaxTenants * kXcds * kNumPmc) == hipSuccess;
@@ -578,6 +759,12 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
   ok = ok && hipEventCreateWithFlags(&c->blk_ev, hipEventDisableTiming) == hipSuccess;
   c->blk_prev.assign((size_t)kMaxTenants * kXcds * kNumPmc, 0);
   c->snap_blk.assign((size_t)kMaxTenants * kXcds * kNumPmc, 0);
+  c->snap_se.assign((size_t)kXcds * kCtx * kNumPmc, 0);
+  c->se_prev = c->snap_se;
+  c->snap_x.assign((size_t)kXcds * kNumPmc, 0);
+  c->x_prev = c->snap_x;
+  c->snap_own.assign((size_t)kMaxTenants * kXcds * kCtx, 0);
+  c->own_prev = c->snap_own;
   ok = ok && hipMemset(c->d_cnt, 0, sizeof(u64) * kMaxTenants * kXcds * kNumPmc) == hipSuccess;
   ok = ok && hipMemset(c->d_prev, 0, sizeof(u64) * kMaxTenants * kXcds * kNumPmc) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_out, sizeof(u64) * 4 * kMaxTenants, hipHostMallocMapped) == hipSuccess;
@@ -681,6 +868,7 @@ int gpbs_gpu_set_hwc(void* p, int on) {
   c->hwc = on ? 1 : 0;
   c->hw_primed = false;
   c->used_seq = c->snap_seq;
+  for (int k = 0; k < kNumPmc; ++k) c->slot_se[k] = on ? gpbs_hwc_slot_per_se(k) : 0;
   if (on) {
     if (!c->hwc_stream && hipStreamCreateWithFlags(&c->hwc_stream, hipStreamNonBlocking) != hipSuccess) return -5;
     c->hwc_stop = false;
@@ -689,14 +877,85 @@ int gpbs_gpu_set_hwc(void* p, int on) {
   return 0;
 }
 
-// hwc stats: samples, mean sample cost (ns), attributed/modeled ratio per slot.
+// hwc stats: samples, mean sample cost (ns), hardware/modeled ratio per slot.
 int gpbs_gpu_hwc_stats(void* p, uint64_t* samples, uint64_t* mean_ns, double* ratio4) {
   GpuCtx* c = (GpuCtx*)p;
   if (!c) return -22;
+  std::lock_guard<std::mutex> g(c->snap_mu);
   if (samples) *samples = c->hwc_samples;
   if (mean_ns) *mean_ns = c->hwc_samples ? (uint64_t)(c->hwc_ns / (int64_t)c->hwc_samples) : 0;
   if (ratio4)
     for (int k = 0; k < kNumPmc; ++k) ratio4[k] = c->model_sum[k] > 0 ? c->hw_sum[k] / c->model_sum[k] : 0.0;
+  return 0;
+}
+
+// Attribution quality: max sample cost (ns), and per slot the fraction of
+// hardware counts no owner explains.  Slot mask of the SE-resolved slots.
+int gpbs_gpu_hwc_quality(void* p, uint64_t* max_ns, double* unatt_frac4, int* se_slots) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c) return -22;
+  std::lock_guard<std::mutex> g(c->snap_mu);
+  if (max_ns) *max_ns = (uint64_t)c->hwc_ns_max;
+  if (unatt_frac4)
+    for (int k = 0; k < kNumPmc; ++k) unatt_frac4[k] = c->hw_sum[k] > 0 ? c->unatt[k] / c->hw_sum[k] : 0.0;
+  if (se_slots) {
+    *se_slots = 0;
+    for (int k = 0; k < kNumPmc; ++k) *se_slots |= (c->slot_se[k] && c->se_mode) << k;
+  }
+  return 0;
+}
+
+// Per-tenant cumulative attributed hardware counts and modeled counts since
+// the last reset (PBS slots INST, CYCLES, LLC_REFS, LLC_MISSES).
+int gpbs_gpu_hwc_tenant(void* p, int t, double* att4, double* model4) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c || t < 0 || t >= kMaxTenants) return -22;
+  std::lock_guard<std::mutex> g(c->snap_mu);
+  for (int k = 0; k < kNumPmc; ++k) {
+    if (att4) att4[k] = c->att_total[t][k];
+    if (model4) model4[k] = c->mod_total[t][k];
+  }
+  return 0;
+}
+
+// Consume the newest sampler snapshot now (attribution into the per-tenant
+// totals and pending deltas) -- what the engine's metric tick does; for
+// tools and tests that run without an engine.
+int gpbs_gpu_hwc_poll(void* p) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c || !c->hwc) return -22;
+  std::lock_guard<std::mutex> g(c->snap_mu);
+  if (c->snap_seq == c->used_seq || c->snap_own.empty()) return 0;
+  c->used_seq = c->snap_seq;
+  if (c->hw_primed) hwc_attribute(c);
+  c->blk_prev = c->snap_blk;
+  c->se_prev = c->snap_se;
+  c->x_prev = c->snap_x;
+  c->own_prev = c->snap_own;
+  c->hw_primed = true;
+  return 1;
+}
+
+int gpbs_gpu_hwc_reset(void* p) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c) return -22;
+  std::lock_guard<std::mutex> g(c->snap_mu);
+  std::memset(c->att_total, 0, sizeof(c->att_total));
+  std::memset(c->mod_total, 0, sizeof(c->mod_total));
+  std::memset(c->hw_sum, 0, sizeof(c->hw_sum));
+  std::memset(c->model_sum, 0, sizeof(c->model_sum));
+  std::memset(c->unatt, 0, sizeof(c->unatt));
+  c->hwc_ns = c->hwc_ns_max = 0;
+  c->hwc_samples = 0;
+  return 0;
+}
+
+// SE-exclusive partitions: the nctx (= 4) partitions of an XCD are its shader
+// engines; gated tenant kernels run only on SEs their tenant owns.
+int gpbs_gpu_set_se_mode(void* p, int on) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c) return -22;
+  __atomic_store_n(&c->se_mode, on ? 1 : 0, __ATOMIC_RELEASE);
   return 0;
 }
 
@@ -769,10 +1028,14 @@ int gpbs_gpu_ownership(void* p, int t, int64_t* out2, int clear) {
   GpuCtx* c = (GpuCtx*)p;
   if (t < 0 || t >= kMaxTenants) return -22;
   std::lock_guard<std::mutex> g(c->mu);
+  std::vector<int64_t> cum((size_t)kMaxTenants * kXcds * kCtx);
+  own_snapshot_locked(c, cum.data());  // includes the interval since the last table change
+  const int64_t* ct = cum.data() + (size_t)t * kXcds * kCtx;
   for (int k = 0; k < kCtx; ++k) {
-    out2[k] = c->own_ns[t][k];
-    if (clear) c->own_ns[t][k] = 0;
+    out2[k] = 0;
+    for (int x = 0; x < kXcds; ++x) out2[k] += ct[x * kCtx + k] - c->own_base[t][x * kCtx + k];
   }
+  if (clear) std::memcpy(c->own_base[t], ct, sizeof(c->own_base[t]));
   return 0;
 }
 
@@ -887,6 +1150,20 @@ int gpbs_runner_reset_stats(void* p) {
   return 0;
 }
 
+// Drop every submitted unit that has not been launched yet (units in flight
+// complete); returns the number dropped.  Used to end a backlogged
+// (steady-state) measurement window.
+int64_t gpbs_runner_cancel(void* p) {
+  Runner* r = (Runner*)p;
+  std::lock_guard<std::mutex> g(r->mu);
+  const int64_t n = r->pending;
+  r->pending = 0;
+  for (int64_t i = 0; i < n && !r->submit_times.empty(); ++i) r->submit_times.pop_back();
+  r->st.submitted -= (uint64_t)n;
+  if (r->inflight <= 0) r->idle_cv.notify_all();
+  return n;
+}
+
 int gpbs_runner_set_gate(void* p, int gate) {
   Runner* r = (Runner*)p;
   std::lock_guard<std::mutex> g(r->mu);
@@ -917,6 +1194,8 @@ void gpbs_runner_destroy(void* p) {
   for (int i = 0; i < r->nq; ++i) hipEventDestroy(r->ev[i]);
   hipStreamDestroy(r->stream);
   for (hipStream_t h : r->half_stream)
+    if (h) hipStreamDestroy(h);
+  for (hipStream_t h : r->se_stream)
     if (h) hipStreamDestroy(h);
   hipFree(r->d_q);
   hipHostFree(r->h_status);

@@ -16,7 +16,7 @@
 extern "C" {
 #endif
 
-#define GPBS_ABI_VERSION 1
+#define GPBS_ABI_VERSION 2
 
 /* Validation ranges (sysctl.h:568-579, libxl.c:4026-4101). Q1: the new API
  * also accepts the reference's boot default of 100us (see docs). */
@@ -70,6 +70,10 @@ typedef struct gpbs_boot_params {
   int32_t coschedule;          /* 1 = contention-aware sibling selection; 2 = + counter-driven context classes */
   int32_t class_period_us;     /* contention-class re-evaluation period, default 2000 */
   int32_t boost_exclusive;     /* 1 = memory-class slots park while a sibling context of their XCD runs a BOOSTed waker */
+  int32_t class_split;         /* contexts [0, class_split) of an XCD host the compute class, the rest the memory class;
+                                  0/1 = context 0 only.  > 1 also makes each class one gang (SE-exclusive mode) */
+  int32_t idle_skip;           /* 1 = PBS idle-sample rule (Q14): a tenant with no counted instructions in a metric
+                                  period is not fed to the phase detector (curr = 0 would shrink its quantum) */
   gpbs_adapt_params_t adapt;
   gpbs_atc_params_t atc;
 } gpbs_boot_params_t;
@@ -110,6 +114,17 @@ typedef struct gpbs_actuator_ops {
 } gpbs_actuator_ops_t;
 
 /* Trace record (32 B), see csrc/obs/trace.h for event codes. */
+/* Per-GPU backend multiplexer: an engine spanning several GPUs drives one
+ * actuator + counter backend per GPU.  Backend i serves partitions
+ * [part_lo, part_hi) (disjoint ranges): switch events go to the backend whose
+ * range holds the partition, flushes and parks to all, and tenant counter
+ * deltas are summed over the backends.  Installs the mux as the engine's
+ * actuator/counter ops; returns the backend index or an error. */
+int gpbs_backend_mux_add(struct gpbs_engine* e, int part_lo, int part_hi, const gpbs_actuator_ops_t* act,
+                         const struct gpbs_counter_ops* ctr);
+int gpbs_backend_mux_clear(struct gpbs_engine* e);
+int gpbs_backend_mux_count(struct gpbs_engine* e);
+
 typedef struct gpbs_trace_record {
   uint64_t t_ns;
   uint32_t event, cpu;

@@ -27,11 +27,15 @@ class AtcParams(C.Structure):
                                    "reserved")]
 
 
+ABI_VERSION = 2  # GPBS_ABI_VERSION in csrc/include/gpbs/gpbs.h
+
+
 class BootParams(C.Structure):
     _fields_ = [("sched", C.c_char * 16)] + [(n, i32) for n in (
         "tslice_us", "ratelimit_us", "smt_power_savings", "tickle_one_idle", "default_yield", "migration_delay_us",
         "metric_period_us", "slice_apply_us", "sim_clock", "pmu_refresh_us", "dom0_quirk", "heartbeat_timeout_us",
-        "trace_capacity", "quantum_align_us", "coschedule", "class_period_us", "boost_exclusive")] + [("adapt", AdaptParams), ("atc", AtcParams)]
+        "trace_capacity", "quantum_align_us", "coschedule", "class_period_us", "boost_exclusive",
+        "class_split", "idle_skip")] + [("adapt", AdaptParams), ("atc", AtcParams)]
 
 
 class SchedExt(C.Structure):
@@ -138,6 +142,8 @@ def load_core(build_if_missing=True):
         P(lib, "gpbs_engine_create", E, C.POINTER(BootParams))
         P(lib, "gpbs_engine_destroy", None, E)
         P(lib, "gpbs_abi_version", C.c_int)
+        if lib.gpbs_abi_version() != ABI_VERSION:  # struct layouts below would be wrong
+            raise RuntimeError(f"{p}: ABI {lib.gpbs_abi_version()} != {ABI_VERSION}; rebuild (python -m pbs_amd.build)")
         P(lib, "gpbs_strerror", C.c_char_p, C.c_int)
         P(lib, "gpbs_partition_add", C.c_int, E, C.c_int, C.c_int)
         P(lib, "gpbs_partition_add_ctx", C.c_int, E, C.c_int, C.c_int, C.c_int)

@@ -11,44 +11,41 @@ Per GPU rank, four tenants share one MI355X:
             reduce-copy traffic kernel on one GPU              native runner / thread
 * ``idle``  latency tenant: 8192^2 GEMV requests, 2 ms think time, closed loop
 
-A *step* gives every throughput tenant a fixed quota of units, sized so that
-each quota takes ``target_ms`` when the tenant runs alone on the whole GPU
-(calibrated before the timed phase); the step ends when every quota is done.
-With t_i the time tenant i needed inside the step and T_i its solo time:
+Protocol "steady" (default; SURVEY §6 weighted speedup): every throughput
+tenant is kept backlogged for the whole run; a step is one ``step_ms``
+window; over the K timed steps
 
-  slowdown_i  = t_i / T_i - 1                 (per tenant, %)
-  norm_perf_i = T_i / t_i                     (idle tenant: solo/co-run p50 latency)
-  aggregate   = sum_i norm_perf_i over the throughput tenants (weighted speedup)
+  norm_perf_i = (units_i / t) / solo_rate_i    (idle tenant: solo/co-run p50 latency)
+  slowdown_i  = 1 / norm_perf_i - 1            (per tenant, %)
+  aggregate   = sum_i norm_perf_i over the throughput tenants
+
+Protocol "quota" (round 1): a step gives each throughput tenant a quota that
+takes ``target_ms`` solo and ends when all are done (t_i = its completion
+time, norm_perf_i = T_i / t_i); early finishers idle, so late ones run the
+step's tail alone, which rewards staggering completions rather than sharing.
 
 ``value`` = aggregate summed over all GPUs (whole-job, solo-equivalents).
 
 Policies (same tenants, same box):
-  none    default hardware sharing: every tenant launches ungated full-GPU grids
-  static  equal static XCD split (2 XCDs per tenant, ARINC-653-like)
-  gpbs1   PBS adaptive credit scheduler, one exclusive context per XCD,
-          kernels exit on revoked XCDs
-  gpbs-exit   two co-resident issue contexts per XCD + contention classes,
-          workgroups exit on revocation, host table
-  gpbs-ctx2   two co-resident issue contexts per XCD, parked gating: three
-          throughput tenants time-share them (best latency-tenant delay, but
-          the forced time-slicing costs aggregate throughput)
-  gpbs-spatial  as gpbs-ctx2, but an XCD whose two owners are of different
-          classes is split into CU halves (shader engines 0-1 / 2-3)
-  gpbs-noprio the flagship without wave priority
-  gpbs-x  the flagship + BOOST exclusion (memory-class siblings park during a
-          latency request)
-  gpbs-nogang the flagship without gang alignment of the classes
-  credit-fixed  the flagship's contexts and actuation under the credit
-          scheduler with a fixed quantum (no PBS adaptation)
-  credit2 / sedf  the same under the credit2 / sedf schedulers (S4)
-  gpbs    PBS adaptive credit scheduler over four co-resident issue contexts
-          per XCD: counter-driven compute/memory classes (compute on context
-          0, memory tenants rotated over contexts 1-3, soft affinity, work
-          conserving), gang-aligned per context, parked gating on a
-          device-resident partition table, and latency-class tenants' waves
-          at raised SIMD issue priority (the flagship: aggregate at parity
-          with default sharing, lower latency-tenant delay and mean slowdown;
-          profiles/corun_flagship_1gpu.log)
+  none     default hardware sharing: every tenant launches ungated full-GPU grids
+  static   equal static XCD split (2 XCDs per tenant, ARINC-653-like)
+  gpbs     (flagship) PBS adaptive credit scheduler over shader-engine (SE)
+           exclusive partitions: 4 per XCD, one owner each.  Live CDNA4
+           counters attributed by SE ownership drive the PBS phase detector
+           and the contention class; the compute class owns SEs {0,1} of every
+           XCD, each memory tenant one SE of {2,3} per XCD; runners launch on
+           CU-masked streams of their class half; the latency tenant runs
+           outside the partitions, co-resident at raised wave priority
+  credit-fixed / credit2   the same partitions and tenants under the credit
+           scheduler with a fixed quantum / under credit2 (no classes)
+  gpbs-ts  memory tenants time-share all memory SEs as one gang with PBS
+           quanta (credit-fixed-ts: fixed quantum) -- where the adaptive
+           quantum acts
+  gpbs-boost  latency tenant inside the partitions (wake-BOOST revokes SEs)
+  gpbs-ctx4   round-1 flagship: four co-resident issue contexts per XCD,
+           parked gating, wave priority (counters attributed by time share)
+  gpbs-ctx2 / gpbs-spatial / gpbs-x / gpbs-noprio / gpbs-nogang / gpbs1 /
+  gpbs-exit / sedf   round-1 variants kept for ablations
 """
 from __future__ import annotations
 
@@ -95,22 +92,53 @@ class CorunConfig:
     gang_share: float = 0.5      # fraction of epochs that are the all-reduce tenant's
     mix: str = "4mix"
     hw_counters: bool = False    # PBS metric from live hardware counters
+    # "steady": every throughput tenant is kept backlogged for the whole timed
+    # window (a step = one step_ms window); throughput_i = units done / time,
+    # normalised by the solo rate -- the weighted speedup of SURVEY §6.
+    # "quota" (round 1): a step gives each tenant a fixed quota and ends when
+    # all are done, so early finishers idle and late ones run the tail alone.
+    protocol: str = "steady"
+    step_ms: float = 80.0
 
+
+# SE-exclusive flagship (the four partitions of an XCD are its shader engines,
+# one owner each): the compute class owns SEs {0,1} of every XCD and the
+# memory class SEs {2,3}, each class group gang-switched as a whole, memory
+# tenants time-sharing their SEs under credit with PBS quanta, on
+# counters attributed exactly by SE ownership
+# (profiles/se_interfere_1gpu.jsonl, profiles/hwc/se_separation_probe.txt).
+SE_OVERRIDES = {"class_split": 2, "idle_skip": 1}
+SE_SLOTS = {"gemm": 16, "gemm_b": 16, "hbm": 16, "coll": 16, "idle": 8}
+# "se8": memory tenants get 8 slots each -- one SE per XCD, so the credit
+# scheduler places them on disjoint memory SEs instead of time-sharing both.
+SE8_SLOTS = {"gemm": 16, "gemm_b": 16, "hbm": 8, "coll": 8, "idle": 8}
 
 POLICY_ENGINES = {
     # name: (issue contexts per XCD, engine overrides on top of MI355X_PROFILE,
     #        kernel gate mode, partition-table location + runtime options)
-    "gpbs": (4, {}, "park", "device,waveprio"),
+    # flagship: counter-driven class split over exclusive SEs (compute class
+    # SEs {0,1}, each memory tenant one SE per XCD of {2,3}); the latency
+    # tenant runs outside the partitions, co-resident at raised wave priority
+    "gpbs": (4, dict(SE_OVERRIDES), True, "device,se,waveprio,latco,se8"),
+    "credit-fixed": (4, dict(SE_OVERRIDES, sched="credit-fixed"), True, "device,se,waveprio,latco,se8"),
+    "credit2": (4, dict(SE_OVERRIDES, sched="credit2"), True, "device,se,waveprio,latco,se8"),
+    # time-shared memory SEs: both memory tenants hold slots on all 16 memory
+    # SEs and alternate as one gang with PBS quanta (the regime where PBS's
+    # adaptive quantum acts); credit-fixed-ts is the same with a fixed quantum
+    "gpbs-ts": (4, dict(SE_OVERRIDES), True, "device,se,waveprio,latco"),
+    "credit-fixed-ts": (4, dict(SE_OVERRIDES, sched="credit-fixed"), True, "device,se,waveprio,latco"),
+    # latency tenant inside the partitions (BOOST on wake revokes memory SEs)
+    "gpbs-boost": (4, dict(SE_OVERRIDES), True, "device,se,waveprio"),
+    "gpbs-host": (4, dict(SE_OVERRIDES), True, "host,se,waveprio,latco,se8"),
+    "gpbs-ctx4": (4, {}, "park", "device,waveprio"),
     "gpbs-x": (4, {"boost_exclusive": 1}, "park", "device,waveprio"),
     "gpbs-noprio": (4, {}, "park", "device"),
     "gpbs-ctx2": (2, {}, "park", "device"),
     "gpbs-spatial": (2, {}, "park", "device,spatial"),
-    "gpbs-nogang": (4, {"coschedule": 2}, "park", "device,waveprio"),
+    "gpbs-nogang": (4, dict(SE_OVERRIDES, coschedule=2), True, "device,se,waveprio"),
     "gpbs-exit": (2, {}, True, "host"),
     "gpbs1": (1, {"coschedule": 0}, True, "host"),
-    "credit-fixed": (4, {"sched": "credit-fixed"}, "park", "device,waveprio"),
-    "credit2": (4, {"sched": "credit2"}, "park", "device,waveprio"),
-    "sedf": (4, {"sched": "sedf"}, "park", "device,waveprio"),
+    "sedf": (4, dict(SE_OVERRIDES, sched="sedf"), True, "device,se,waveprio"),
 }
 
 
@@ -148,6 +176,20 @@ class CollTenant:
         self.last_done_ns = time.monotonic_ns()
         if self.engine is not None and self.gate:
             self.engine.block(self.tenant)
+
+    # steady-state protocol: all-reduce back to back until stopped
+    def start_loop(self):
+        self._stop = threading.Event()
+        self._th = threading.Thread(target=self._loop, daemon=True)
+        self._th.start()
+
+    def _loop(self):
+        while not self._stop.is_set():
+            self.run_units(1)
+
+    def stop_loop(self):
+        self._stop.set()
+        self._th.join()
 
 
 def _pct(xs, q):
@@ -200,7 +242,7 @@ class Corun:
         raise ValueError(name)
 
     def _make_engine(self, pol: str) -> Engine:
-        nctx, over, _, _ = POLICY_ENGINES[pol]
+        nctx, over, _, table = POLICY_ENGINES[pol]
         prof = {k: v for k, v in MI355X_PROFILE.items()}
         prof.update(over)
         e = Engine(**prof)
@@ -208,9 +250,11 @@ class Corun:
             for c in range(nctx):
                 e.pool_assign(0, e.partition_add(self.rank, x, c))
         e.tenant_create("Domain-0", nslots=1)
+        opts = table.split(",")
+        slots = SE8_SLOTS if "se8" in opts else SE_SLOTS if "se" in opts else {}
         ids = {}
         for name, ns in self.tenants:
-            ids[name] = e.tenant_create(name, nslots=ns)
+            ids[name] = e.tenant_create(name, nslots=slots.get(name, ns))
         if self.tid and ids != self.tid:
             raise RuntimeError("tenant ids differ across engines")
         self.tid = ids
@@ -236,17 +280,22 @@ class Corun:
         if policy in self.engines:
             e = self.engines[policy]
             _, _, gate, table = POLICY_ENGINES[policy]
-            self.ctx.set_table_mode(table.split(",")[0])
-            self.ctx.set_spatial("spatial" in table)
-            self.ctx.set_waveprio("waveprio" in table)
+            opts = table.split(",")
+            self.ctx.set_table_mode(opts[0])
+            self.ctx.set_spatial("spatial" in opts)
+            self.ctx.set_se_mode("se" in opts)
+            self.ctx.set_waveprio("waveprio" in opts)
             self.ctx.attach(e, nctx=e._gpbs_nctx)
             if self.cfg.hw_counters:
                 self.ctx.set_hwc(True)
             e.start()
             self.active_engine = e
-            for r in self._natives():
-                r.set_gate(gate)
-                r.set_engine_wake(True)
+            for name, r in self.runners.items():
+                if not isinstance(r, Runner):
+                    continue
+                latco = name == "idle" and "latco" in opts
+                r.set_gate(False if latco else gate)
+                r.set_engine_wake(not latco)
             if isinstance(coll, CollTenant):
                 coll.gate, coll.engine = True, e
                 # Cross-GPU gang windows for the all-reduce tenant: its RCCL
@@ -261,7 +310,10 @@ class Corun:
             return
         self.ctx.set_table_mode("host")
         self.ctx.set_spatial(False)
+        self.ctx.set_se_mode(False)
         self.ctx.set_waveprio(False)
+        if self.cfg.hw_counters:
+            self.ctx.set_hwc(False)
         for r in self._natives():
             r.set_engine_wake(False)
         if isinstance(coll, CollTenant):
@@ -370,7 +422,103 @@ class Corun:
         done["_nreq"] = nreq
         return done
 
+    def _done(self, name: str) -> int:
+        r = self.runners[name]
+        return r.stats().units_done if isinstance(r, Runner) else r.units_done
+
+    def _idle_request(self, until_ns: int):
+        """Latency tenant: closed loop with think time until `until_ns`."""
+        idle = self.runners.get("idle")
+        n = 0
+        while time.monotonic_ns() < until_ns:
+            if idle is not None:
+                idle.submit(1)
+                idle.wait(30.0)
+                n += 1
+            self._topup()
+            time.sleep(self.cfg.idle_period_ms / 1e3 if idle is not None else 2e-4)
+        return n
+
+    def _topup(self):
+        """Keep every native throughput runner backlogged (>= 2 quotas queued)."""
+        for name in self.throughput:
+            r = self.runners[name]
+            if isinstance(r, Runner):
+                st = r.stats()
+                if st.submitted - st.units_done < 2 * self.quota[name]:
+                    r.submit(2 * self.quota[name])
+
+    def run_policy_steady(self, policy: str, steps: int, warmup: int) -> Dict:
+        """Steady-state weighted speedup: all throughput tenants backlogged for
+        W + K windows of step_ms; the K timed windows give each tenant's
+        co-run throughput (units / ms), normalised by its solo rate."""
+        self.set_policy(policy)
+        cfg = self.cfg
+        coll = self.runners.get("coll")
+        self._topup()
+        if isinstance(coll, CollTenant):
+            coll.start_loop()
+        step_ns = int(cfg.step_ms * 1e6)
+        for _ in range(warmup):
+            self._idle_request(time.monotonic_ns() + step_ns)
+        if "idle" in self.runners:
+            self.runners["idle"].latencies(clear=True)
+        for n in self.tid:
+            self.ctx.ownership(self.tid[n], clear=True)
+        e = self.active_engine
+        if e is not None:
+            e.perfc_reset()
+            run0 = {n: e.tenant_info(self.tid[n]).run_ns for n in self.tid}
+            if self.cfg.hw_counters:
+                self.ctx.hwc_reset()
+        quanta = {n: [] for n in self.tid}
+        self._barrier()
+        t0 = time.perf_counter()
+        d0 = {n: self._done(n) for n in self.throughput}
+        per_step = []
+        for _ in range(steps):
+            ts, ds = time.perf_counter(), {n: self._done(n) for n in self.throughput}
+            self._idle_request(time.monotonic_ns() + step_ns)
+            te = time.perf_counter()
+            per_step.append({n: (self._done(n) - ds[n]) / ((te - ts) * 1e3) for n in self.throughput})
+            if e is not None:
+                for n in self.tid:
+                    quanta[n].append(e.tenant_info(self.tid[n]).tslice_us)
+        d1 = {n: self._done(n) for n in self.throughput}
+        wall_ms_local = (time.perf_counter() - t0) * 1e3
+        self._barrier()
+        wall_ms = self._allreduce(wall_ms_local, "max")
+        # drain: drop the backlog, let in-flight units finish
+        for name in self.throughput:
+            r = self.runners[name]
+            if isinstance(r, Runner):
+                r.cancel()
+        if isinstance(coll, CollTenant):
+            coll.stop_loop()
+        for name in self.throughput:
+            r = self.runners[name]
+            if isinstance(r, Runner):
+                r.wait(120.0)
+        lats = [x / 1e6 for x in self.runners["idle"].latencies(clear=True)] if "idle" in self.runners else []
+        res = {"policy": policy, "protocol": "steady", "wall_ms": wall_ms, "ms_per_step": wall_ms / steps,
+               "tenants": {}}
+        agg, slows = 0.0, []
+        for n in self.throughput:
+            rate = (d1[n] - d0[n]) / wall_ms_local  # units per ms
+            perf = rate * self.solo_unit_ms[n]
+            agg += perf
+            slows.append((1.0 / perf - 1.0) * 100.0 if perf > 0 else 1e4)
+            res["tenants"][n] = {"units": d1[n] - d0[n], "units_per_ms": round(rate, 4),
+                                 "solo_units_per_ms": round(1.0 / self.solo_unit_ms[n], 4),
+                                 "norm_perf": round(perf, 4), "slowdown_pct": round(slows[-1], 2),
+                                 "step_norm_perf": [round(ps[n] * self.solo_unit_ms[n], 3) for ps in per_step]}
+        self._finish_result(res, e, lats, slows, agg, wall_ms, quanta, run0 if e is not None else None, policy)
+        self.log(f"[corun] {policy}: " + json.dumps(res))
+        return res
+
     def run_policy(self, policy: str, steps: int, warmup: int) -> Dict:
+        if self.cfg.protocol == "steady":
+            return self.run_policy_steady(policy, steps, warmup)
         self.set_policy(policy)
         for _ in range(warmup):
             self.step()
@@ -382,6 +530,8 @@ class Corun:
         if e is not None:
             e.perfc_reset()
             run0 = {n: e.tenant_info(self.tid[n]).run_ns for n in self.tid}
+            if self.cfg.hw_counters:
+                self.ctx.hwc_reset()
         per = {n: [] for n in self.throughput}
         self._barrier()
         t0 = time.perf_counter()
@@ -407,6 +557,11 @@ class Corun:
             slows.append((t_i / T_i - 1.0) * 100.0)
             res["tenants"][n] = {"corun_ms": round(t_i, 3), "solo_ms": round(T_i, 3), "norm_perf": round(perf, 4),
                                  "slowdown_pct": round(slows[-1], 2)}
+        self._finish_result(res, e, lats, slows, agg, wall_ms, quanta, run0 if e is not None else None, policy)
+        self.log(f"[corun] {policy}: " + json.dumps(res))
+        return res
+
+    def _finish_result(self, res, e, lats, slows, agg, wall_ms, quanta, run0, policy):
         p50, p99 = _pct(lats, 0.5), _pct(lats, 0.99)
         idle_perf = self.solo_lat_ms / p50 if p50 > 0 else 0.0
         if "idle" in self.runners:
@@ -425,6 +580,18 @@ class Corun:
             eng["gpu"] = self.ctx.stats()
             if self.cfg.hw_counters:
                 eng["hwc"] = self.ctx.hwc_stats()
+                # Hardware-derived PBS metrics per tenant over the timed window
+                # (ownership-attributed counts): L2 misses and L2 requests per
+                # 100k instructions, cycles per 1k instructions.
+                hw = {}
+                for n in self.tid:
+                    att, mod = self.ctx.hwc_tenant(self.tid[n])
+                    inst = att[0]
+                    hw[n] = {"inst": round(inst), "miss_rate": round(att[3] * 1e5 / inst) if inst else 0,
+                             "l2_req_rate": round(att[2] * 1e5 / inst) if inst else 0,
+                             "cpi_x1000": round(att[1] * 1e3 / inst) if inst else 0,
+                             "model_miss_rate": round(mod[3] * 1e5 / mod[0]) if mod[0] else 0}
+                eng["hw_tenant"] = hw
             eng["miss_rate"] = {n: e.tenant_info(self.tid[n]).cache_miss_rate for n in self.tid}
             eng["class"] = {n: e.lib.gpbs_tenant_class(e.h, self.tid[n]) for n in self.tid}
             eng["mean_tslice_us"] = {n: round(statistics.mean(q), 1) for n, q in quanta.items() if q}
@@ -447,8 +614,6 @@ class Corun:
                 with open(os.path.join(diag, f"trace_{policy}.json"), "w") as f:
                     json.dump({"tid": self.tid, "lat_ms": lats,
                                "trace": [[r.t_ns, r.event, r.cpu, *r.a] for r in recs]}, f)
-        self.log(f"[corun] {policy}: " + json.dumps(res))
-        return res
 
     def close(self):
         self._stop_gang()

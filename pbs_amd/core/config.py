@@ -26,10 +26,11 @@ REFERENCE_PROFILE: Dict[str, Any] = dict(
 # MI355X profile: the PBS algorithm structure is kept (window 5, band 70-130 %,
 # step ratio +1/-2, tick = quantum/3); time constants are rescaled x10 because
 # a GPU "context switch" (draining an XCD's workgroups between tiles and
-# relaunching) costs tens of microseconds, and the miss-rate threshold is
-# recalibrated for the modeled device counters (GEMM ~4e3, HBM streams ~8e5
-# fills per 100k instructions).  Both XCD issue contexts
-# are scheduled (SMT-sibling analog) with contention-aware sibling selection.
+# relaunching) costs tens of microseconds, and the miss-rate threshold
+# (L2 misses per 100k work-normalised instructions, csrc/hip/hwc.cpp) is
+# calibrated on live gfx950 counters attributed by shader-engine ownership
+# (tests/test_gpu_se_hwc.py, profiles/hwc/): HBM stream
+# ~1.1e5, reduce-copy ~4.6e4, GEMV ~3e4, LDS-tiled MFMA GEMM ~2e3.
 MI355X_PROFILE: Dict[str, Any] = dict(
     sched="credit", tslice_us=1000, ratelimit_us=250, metric_period_us=1000, quantum_align_us=250,
     coschedule=3, class_period_us=2000,
@@ -40,7 +41,7 @@ MI355X_PROFILE: Dict[str, Any] = dict(
 BOOT_KEYS = ("sched", "tslice_us", "ratelimit_us", "smt_power_savings", "tickle_one_idle", "default_yield",
              "migration_delay_us", "metric_period_us", "slice_apply_us", "pmu_refresh_us", "dom0_quirk",
              "heartbeat_timeout_us", "trace_capacity", "quantum_align_us", "coschedule", "class_period_us",
-             "boost_exclusive")
+             "boost_exclusive", "class_split", "idle_skip")
 
 
 def load(path: str | None = None, profile: Dict[str, Any] | None = None) -> Dict[str, Any]:

@@ -98,10 +98,28 @@ class Engine:
                 self.pool_assign(0, pid)
 
     # ------------------------------------------------------------ lifecycle
+    # Every ABI call goes through ``h``: once closed it raises instead of
+    # handing a NULL engine to C (a late reaper / RPC call after close()).
+    @property
+    def h(self):
+        h = self.__dict__.get("_h")
+        if h is None:
+            raise GpbsError(-19, "engine is closed")
+        return h
+
+    @h.setter
+    def h(self, v):
+        self.__dict__["_h"] = v
+
+    @property
+    def closed(self) -> bool:
+        return self.__dict__.get("_h") is None
+
     def close(self):
-        if getattr(self, "h", None):
-            self.lib.gpbs_engine_destroy(self.h)
-            self.h = None
+        h = self.__dict__.get("_h")
+        if h is not None:
+            self.__dict__["_h"] = None
+            self.lib.gpbs_engine_destroy(h)
 
     def __del__(self):
         try:

@@ -8,8 +8,9 @@ csrc/hip/hwc.cpp): the Perfctr-xen vPMU analog.
     per_xcd = hwc.sample()   # 8 x (INST, BUSY_CYCLES, L2_REQ, L2_MISS), cumulative
 
 ``GpuContext.set_hwc(True)`` then drives the scheduler's PBS metric with
-per-XCD hardware deltas, attributed to tenants in proportion to their
-modeled per-XCD activity.
+hardware deltas attributed to tenants by partition OWNERSHIP: exact per
+shader engine in the SE-exclusive mode, by owned time per XCD otherwise
+(csrc/hip/runtime.cpp, hwc_attribute).
 """
 from __future__ import annotations
 
@@ -18,7 +19,11 @@ from typing import List, Optional, Tuple
 
 from .. import _native as N
 
-DEFAULT_SPEC = "SQ_INSTS_VALU+SQ_INSTS_SALU|SQ_BUSY_CYCLES|TCC_REQ|TCC_MISS"
+# PBS slots INST | CYCLES | LLC_REFS | LLC_MISSES on gfx950 (csrc/hip/hwc.cpp):
+# SQ/TCP counters resolve per shader engine, TCC per XCD.
+DEFAULT_SPEC = ("SQ_INSTS_VALU+SQ_INSTS_SALU+SQ_INSTS_VMEM_RD+SQ_INSTS_VMEM_WR+SQ_INSTS_LDS+"
+                "SQ_INSTS_VALU_MFMA_MOPS_BF16|SQ_BUSY_CYCLES|"
+                "TCP_TCC_READ_REQ+TCP_TCC_WRITE_REQ|TCC_MISS")
 XCDS = 8
 
 
@@ -45,6 +50,16 @@ def sample() -> List[Tuple[int, int, int, int]]:
     if _lib().gpbs_hwc_sample(arr, XCDS) < 0:
         raise RuntimeError("hardware counter sample failed (init/start?)")
     return [tuple(arr[x * 4:(x + 1) * 4]) for x in range(XCDS)]
+
+
+def sample_se():
+    """Cumulative counters per (XCD, SE) for the SE-resolved slots and per
+    XCD for all: ([8][4][4], [8][4])."""
+    se, xs = (C.c_uint64 * (XCDS * 4 * 4))(), (C.c_uint64 * (XCDS * 4))()
+    if _lib().gpbs_hwc_sample_se(se, xs) < 0:
+        raise RuntimeError("hardware counter sample failed (init/start?)")
+    return ([[tuple(se[(x * 4 + e) * 4:(x * 4 + e + 1) * 4]) for e in range(4)] for x in range(XCDS)],
+            [tuple(xs[x * 4:(x + 1) * 4]) for x in range(XCDS)])
 
 
 def stop():

@@ -47,6 +47,13 @@ def bind(lib):
     _p(lib, "gpbs_hwc_stop", C.c_int)
     _p(lib, "gpbs_gpu_set_hwc", C.c_int, vp, C.c_int)
     _p(lib, "gpbs_gpu_hwc_stats", C.c_int, vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_double))
+    _p(lib, "gpbs_hwc_sample_se", C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64))
+    _p(lib, "gpbs_hwc_slot_per_se", C.c_int, C.c_int)
+    _p(lib, "gpbs_gpu_hwc_quality", C.c_int, vp, C.POINTER(C.c_uint64), C.POINTER(C.c_double), C.POINTER(C.c_int))
+    _p(lib, "gpbs_gpu_hwc_tenant", C.c_int, vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double))
+    _p(lib, "gpbs_gpu_hwc_reset", C.c_int, vp)
+    _p(lib, "gpbs_gpu_hwc_poll", C.c_int, vp)
+    _p(lib, "gpbs_gpu_set_se_mode", C.c_int, vp, C.c_int)
     _p(lib, "gpbs_hip_rmsnorm_bf16", C.c_int, vp, vp, vp, C.c_int, C.c_int, C.c_float, vp)
     _p(lib, "gpbs_hip_swiglu_bf16", C.c_int, vp, vp, vp, C.c_ulonglong, vp)
     _p(lib, "gpbs_hip_quant_rows_fp8", C.c_int, vp, vp, vp, C.c_int, C.c_int, vp)
@@ -89,6 +96,7 @@ def bind(lib):
     _p(lib, "gpbs_runner_latencies", C.c_int, vp, C.POINTER(i64), C.c_int, C.c_int)
     _p(lib, "gpbs_runner_reset_stats", C.c_int, vp)
     _p(lib, "gpbs_runner_set_gate", C.c_int, vp, C.c_int)
+    _p(lib, "gpbs_runner_cancel", i64, vp)
     _p(lib, "gpbs_runner_set_engine_wake", C.c_int, vp, C.c_int)
     _p(lib, "gpbs_runner_stream", vp, vp)
     _p(lib, "gpbs_runner_destroy", None, vp)

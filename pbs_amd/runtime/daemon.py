@@ -478,8 +478,7 @@ class Daemon:
         return dead
 
     def _reaper(self, period: float):
-        while self.running:
-            time.sleep(period)
+        while not self._stop_ev.wait(period):
             try:
                 self.reap()
             except Exception as e:  # pragma: no cover
@@ -491,24 +490,42 @@ class Daemon:
         if not self.sim:
             self.engine.start()
         self.running = True
+        self._stop_ev = threading.Event()
+        self._reaper_th = None
         if reaper_s > 0:
-            threading.Thread(target=self._reaper, args=(reaper_s,), daemon=True, name="gpbsd-reaper").start()
+            self._reaper_th = threading.Thread(target=self._reaper, args=(reaper_s,), daemon=True,
+                                               name="gpbsd-reaper")
+            self._reaper_th.start()
         return self
 
     def stop(self):
+        """Orderly teardown: the reaper is joined before anything it touches
+        goes away, RPC handlers are stopped, and the control-page bridge is
+        closed BEFORE the GPU context (ctl_close reinstalls the actuator ops
+        it chained at bind time; they must not point at a freed GpuCtx)."""
         if self.state_path:
             try:
                 self.snapshot(self.state_path)
             except Exception as e:  # pragma: no cover
                 print(f"[gpbsd] snapshot failed: {e}", file=sys.stderr)
         self.running = False
-        if not self.sim:
-            self.engine.stop()
+        ev = getattr(self, "_stop_ev", None)
+        if ev is not None:
+            ev.set()
+        th = getattr(self, "_reaper_th", None)
+        if th is not None:
+            th.join()
+            self._reaper_th = None
         self.server.stop()
-        if self.gpu_ctx is not None:
-            self.gpu_ctx.close()
-        self.lib.gpbs_ctl_close(self.ctl, 1)
-        self.engine.close()
+        with self.lock:
+            if not self.sim:
+                self.engine.stop()
+            self.lib.gpbs_ctl_close(self.ctl, 1)
+            if self.gpu_ctx is not None:
+                for g in self.gpu_ctxs if hasattr(self, "gpu_ctxs") else [self.gpu_ctx]:
+                    g.close()
+                self.gpu_ctx = None
+            self.engine.close()
 
 
 def cfgmod_min_tslice() -> int:

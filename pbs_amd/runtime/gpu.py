@@ -108,8 +108,35 @@ class GpuContext:
         n, ns = C.c_uint64(0), C.c_uint64(0)
         r = (C.c_double * 4)()
         self.L.gpbs_gpu_hwc_stats(self.h, C.byref(n), C.byref(ns), r)
-        return {"samples": n.value, "mean_sample_us": ns.value / 1e3,
-                "hw_over_model": [round(x, 4) for x in r]}
+        mx, sem = C.c_uint64(0), C.c_int(0)
+        u = (C.c_double * 4)()
+        self.L.gpbs_gpu_hwc_quality(self.h, C.byref(mx), u, C.byref(sem))
+        return {"samples": n.value, "mean_sample_us": round(ns.value / 1e3, 1), "max_sample_us": round(mx.value / 1e3, 1),
+                "hw_over_model": [round(x, 4) for x in r],
+                "unattributed_frac": [round(x, 4) for x in u],
+                "attribution": "exact-se" if sem.value & 1 else "xcd-time-share"}
+
+    def hwc_tenant(self, tenant: int):
+        """Cumulative hardware counts attributed to `tenant` since the last
+        reset, and its modeled counts: (att[4], model[4]) over the PBS slots
+        INST, CYCLES, LLC_REFS (L2 requests), LLC_MISSES (L2 misses)."""
+        a, m = (C.c_double * 4)(), (C.c_double * 4)()
+        self.L.gpbs_gpu_hwc_tenant(self.h, tenant, a, m)
+        return list(a), list(m)
+
+    def hwc_reset(self):
+        self.L.gpbs_gpu_hwc_reset(self.h)
+
+    def hwc_poll(self) -> int:
+        """Attribute the newest counter snapshot now (engine-less use)."""
+        return self.L.gpbs_gpu_hwc_poll(self.h)
+
+    def set_se_mode(self, on: bool):
+        """SE-exclusive partitions: the 4 partitions of each XCD are its shader
+        engines, each owned by one tenant at a time (GATE_SE gating)."""
+        rc = self.L.gpbs_gpu_set_se_mode(self.h, 1 if on else 0)
+        if rc:
+            raise RuntimeError("set_se_mode failed")
 
     def set_waveprio(self, on: bool):
         """Latency-class runners (priority > 0) raise their waves' SIMD issue
@@ -253,6 +280,10 @@ class Runner:
 
     def reset_stats(self):
         self.L.gpbs_runner_reset_stats(self.h)
+
+    def cancel(self) -> int:
+        """Drop the units not launched yet (in-flight ones complete)."""
+        return int(self.L.gpbs_runner_cancel(self.h))
 
     def set_gate(self, gate):
         """False: run anywhere; True: leave revoked XCDs; "park": sleep on them."""

@@ -1,0 +1,32 @@
+#!/bin/bash
+# Round-2 GPU session: each step under its own time limit; stop at the first
+# fault / abort / timeout.  usage: scripts/gpu_r2.sh STEP...
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+LOG=gpurun_out/session.log
+echo "session $(date) steps: $*" > "$LOG"
+run() {  # run NAME SECONDS CMD...
+  local name=$1 secs=$2; shift 2
+  echo "== $name ($(date +%T))" | tee -a "$LOG"
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc ($(date +%T))" | tee -a "$LOG"
+  tail -n 25 "gpurun_out/$name.log" | tee -a "$LOG"
+  if [ $rc -ne 0 ] && { [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; }; then
+    echo "fatal rc=$rc in $name: stopping" | tee -a "$LOG"; exit $rc
+  fi
+  return 0
+}
+for step in "$@"; do
+  case $step in
+    se)      run se 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_se_hwc.py -s ;;
+    tests)   run tests 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests ;;
+    smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bquick)  run bquick 600 python bench.py --steps 10 --warmup 2 --reps 2 --out gpurun_out/bquick.json ;;
+    bench)   run bench 900 python bench.py --steps 20 --warmup 5 --out gpurun_out/bench.json ;;
+    *) echo "unknown step $step" | tee -a "$LOG" ;;
+  esac
+done
+echo "session done $(date)" | tee -a "$LOG"
