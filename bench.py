@@ -33,7 +33,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--policies", default="none,static,credit2,credit-fixed,gpbs-ts,credit-fixed-ts,gpbs",
+    ap.add_argument("--policies", default="none,static,credit2,credit-fixed,gpbs-split,gpbs",
                     help="comma list; gpbs is the reported policy")
     ap.add_argument("--reps", type=int, default=5,
                     help="timed runs per policy, in a randomized order per repetition (median and IQR reported)")

@@ -123,6 +123,7 @@ struct GpuCtx {
   int64_t own_base[kMaxTenants][kXcds * kCtx];
   int64_t last_pub_ns = 0;
   int se_mode = 0;  // partitions are exclusive shader engines (GATE_SE)
+  int muxed = 0;    // ops installed through the engine's backend mux
 };
 
 // Cumulative ownership ns of every (tenant, partition) up to now, including
@@ -507,12 +508,14 @@ struct Runner {
   // (class pinning keeps a classified tenant on one half); a tenant holding
   // both halves or none (yet) launches unmasked and gates per workgroup.
   // The mask is quantised to the two class halves (SEs {0,1} / {2,3} of every
-  // XCD), so a runner creates at most two masked streams: every CU mask is a
-  // hardware queue of its own, and past the hardware's queue slots the
-  // scheduler time-multiplexes queues (measured: arbitrary per-(XCD, SE)
-  // masks over four runners collapsed even ungated co-runs to 0.42).  An
-  // owned set that fits neither half (work-conserving steals across
-  // classes) launches unmasked and gates per workgroup.
+  // XCD), so a runner creates at most two masked streams, once, and keeps
+  // them for its lifetime: every CU mask is a hardware queue of its own, and
+  // past the hardware's queue slots the scheduler time-multiplexes queues in
+  // ~10 ms slices (measured: arbitrary per-(XCD, SE) masks over four runners
+  // collapsed even ungated co-runs to 0.42; destroying and re-creating the
+  // masked streams at every policy change added ~10 ms stalls that grew run
+  // after run).  An owned set that fits neither half (work-conserving steals
+  // across classes) launches unmasked and gates per workgroup.
   hipStream_t pick_se_stream() {
     u32 any = 0;
     for (int x = 0; x < kXcds; ++x)
@@ -535,22 +538,10 @@ struct Runner {
     return se_stream[half];
   }
 
-  // Leaving SE mode releases the masked queues (a later ungated policy must
-  // not share the hardware with idle masked queues).  Runner thread only.
-  void drop_se_streams() {
-    for (auto& h : se_stream)
-      if (h) {
-        hipStreamSynchronize(h);
-        hipStreamDestroy(h);
-        h = nullptr;
-      }
-  }
-
   hipStream_t pick_stream() {
     cur_grid = 0;
     const bool se = __atomic_load_n(&ctx->se_mode, __ATOMIC_ACQUIRE);
     if (cfg.gate && se) return pick_se_stream();
-    if (!se && (se_stream[0] || se_stream[1])) drop_se_streams();
     if (!ctx->spatial || !cfg.gate) return stream;
     // Masked only if every XCD the tenant holds is split and it holds the
     // same half of all of them; otherwise unmasked + per-workgroup gating.
@@ -803,7 +794,7 @@ void gpbs_gpu_ctx_destroy(void* p) {
     c->hwc_th.join();
   }
   hipDeviceSynchronize();
-  if (c->engine) {
+  if (c->engine && !c->muxed) {
     gpbs_set_actuator_ops(c->engine, nullptr);
     gpbs_set_counter_ops(c->engine, nullptr);
   }
@@ -842,6 +833,27 @@ int gpbs_gpu_attach(void* p, gpbs_engine_t* e, int device_counters, int device_a
   if (device_counters) k.tenant_deltas = ctr_tenant_deltas;
   if (device_adapt) k.adapt_batch = ctr_adapt_batch;
   gpbs_set_counter_ops(e, &k);
+  return 0;
+}
+
+// Fill (do not install) this context's actuator + counter ops, for the
+// engine's per-GPU backend mux (gpbs_backend_mux_add): one engine spanning
+// several GPUs, one GpuCtx per GPU.  The caller clears the mux before
+// destroying the context.
+int gpbs_gpu_backend_ops(void* p, gpbs_engine_t* e, gpbs_actuator_ops_t* a, gpbs_counter_ops_t* k,
+                         int device_counters) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c || !a || !k) return -22;
+  c->engine = e;
+  c->muxed = 1;
+  *a = gpbs_actuator_ops_t{};
+  a->user = c;
+  a->on_switch = act_on_switch;
+  a->on_flush = act_on_flush;
+  a->on_park = act_on_park;
+  *k = gpbs_counter_ops_t{};
+  k->user = c;
+  if (device_counters) k->tenant_deltas = ctr_tenant_deltas;
   return 0;
 }
 

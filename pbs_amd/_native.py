@@ -186,6 +186,9 @@ def load_core(build_if_missing=True):
         P(lib, "gpbs_report_requests", C.c_int, E, C.c_int, u64)
         P(lib, "gpbs_set_counter_ops", C.c_int, E, C.POINTER(CounterOps))
         P(lib, "gpbs_set_actuator_ops", C.c_int, E, C.POINTER(ActuatorOps))
+        P(lib, "gpbs_backend_mux_add", C.c_int, E, C.c_int, C.c_int, C.POINTER(ActuatorOps), C.POINTER(CounterOps))
+        P(lib, "gpbs_backend_mux_clear", C.c_int, E)
+        P(lib, "gpbs_backend_mux_count", C.c_int, E)
         P(lib, "gpbs_slot_set_pmc", C.c_int, E, C.c_int, C.POINTER(u64))
         P(lib, "gpbs_now", i64, E)
         P(lib, "gpbs_advance", C.c_int, E, i64)

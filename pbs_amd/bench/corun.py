@@ -33,14 +33,14 @@ Policies (same tenants, same box):
            exclusive partitions: 4 per XCD, one owner each.  Live CDNA4
            counters attributed by SE ownership drive the PBS phase detector
            and the contention class; the compute class owns SEs {0,1} of every
-           XCD, each memory tenant one SE of {2,3} per XCD; runners launch on
-           CU-masked streams of their class half; the latency tenant runs
-           outside the partitions, co-resident at raised wave priority
+           XCD; the memory tenants alternate on SEs {2,3} as one gang with PBS
+           quanta; runners launch on CU-masked streams of their class half;
+           the latency tenant runs outside the partitions, co-resident at
+           raised wave priority
   credit-fixed / credit2   the same partitions and tenants under the credit
            scheduler with a fixed quantum / under credit2 (no classes)
-  gpbs-ts  memory tenants time-share all memory SEs as one gang with PBS
-           quanta (credit-fixed-ts: fixed quantum) -- where the adaptive
-           quantum acts
+  gpbs-split  each memory tenant owns one memory SE per XCD (no time-sharing;
+           credit-fixed-split: same with a fixed quantum)
   gpbs-boost  latency tenant inside the partitions (wake-BOOST revokes SEs)
   gpbs-ctx4   round-1 flagship: four co-resident issue contexts per XCD,
            parked gating, wave priority (counters attributed by time share)
@@ -116,20 +116,21 @@ SE8_SLOTS = {"gemm": 16, "gemm_b": 16, "hbm": 8, "coll": 8, "idle": 8}
 POLICY_ENGINES = {
     # name: (issue contexts per XCD, engine overrides on top of MI355X_PROFILE,
     #        kernel gate mode, partition-table location + runtime options)
-    # flagship: counter-driven class split over exclusive SEs (compute class
-    # SEs {0,1}, each memory tenant one SE per XCD of {2,3}); the latency
-    # tenant runs outside the partitions, co-resident at raised wave priority
-    "gpbs": (4, dict(SE_OVERRIDES), True, "device,se,waveprio,latco,se8"),
-    "credit-fixed": (4, dict(SE_OVERRIDES, sched="credit-fixed"), True, "device,se,waveprio,latco,se8"),
-    "credit2": (4, dict(SE_OVERRIDES, sched="credit2"), True, "device,se,waveprio,latco,se8"),
-    # time-shared memory SEs: both memory tenants hold slots on all 16 memory
-    # SEs and alternate as one gang with PBS quanta (the regime where PBS's
-    # adaptive quantum acts); credit-fixed-ts is the same with a fixed quantum
-    "gpbs-ts": (4, dict(SE_OVERRIDES), True, "device,se,waveprio,latco"),
-    "credit-fixed-ts": (4, dict(SE_OVERRIDES, sched="credit-fixed"), True, "device,se,waveprio,latco"),
+    # flagship: counter-driven class split over exclusive SEs -- the compute
+    # class owns SEs {0,1} of every XCD; the memory tenants hold slots on all
+    # memory SEs {2,3} and alternate on them as one gang under credit with
+    # PBS's adaptive quanta; the latency tenant runs outside the partitions,
+    # co-resident at raised wave priority (no BOOST revocations)
+    "gpbs": (4, dict(SE_OVERRIDES), True, "device,se,waveprio,latco"),
+    "credit-fixed": (4, dict(SE_OVERRIDES, sched="credit-fixed"), True, "device,se,waveprio,latco"),
+    "credit2": (4, dict(SE_OVERRIDES, sched="credit2"), True, "device,se,waveprio,latco"),
+    # spatial variant: each memory tenant one memory SE per XCD (no
+    # time-sharing, so no quanta to adapt)
+    "gpbs-split": (4, dict(SE_OVERRIDES), True, "device,se,waveprio,latco,se8"),
+    "credit-fixed-split": (4, dict(SE_OVERRIDES, sched="credit-fixed"), True, "device,se,waveprio,latco,se8"),
     # latency tenant inside the partitions (BOOST on wake revokes memory SEs)
     "gpbs-boost": (4, dict(SE_OVERRIDES), True, "device,se,waveprio"),
-    "gpbs-host": (4, dict(SE_OVERRIDES), True, "host,se,waveprio,latco,se8"),
+    "gpbs-host": (4, dict(SE_OVERRIDES), True, "host,se,waveprio,latco"),
     "gpbs-ctx4": (4, {}, "park", "device,waveprio"),
     "gpbs-x": (4, {"boost_exclusive": 1}, "park", "device,waveprio"),
     "gpbs-noprio": (4, {}, "park", "device"),

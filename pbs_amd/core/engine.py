@@ -336,6 +336,24 @@ class Engine:
             self._keep.append(ops)
         return self.lib.gpbs_set_actuator_ops(self.h, C.byref(ops) if ops is not None else None)
 
+    def mux_add(self, part_lo: int, part_hi: int, act: Optional[N.ActuatorOps] = None,
+                ctr: Optional[N.CounterOps] = None) -> int:
+        """Add a per-GPU backend serving partitions [part_lo, part_hi): one
+        engine spanning several GPUs drives one actuator + counter backend
+        per GPU (gpbs_backend_mux_add)."""
+        for o in (act, ctr):
+            if o is not None:
+                self._keep.append(o)
+        rc = self.lib.gpbs_backend_mux_add(self.h, part_lo, part_hi, C.byref(act) if act is not None else None,
+                                           C.byref(ctr) if ctr is not None else None)
+        return self._chk(rc, "backend_mux_add")
+
+    def mux_clear(self):
+        return self.lib.gpbs_backend_mux_clear(self.h)
+
+    def mux_count(self) -> int:
+        return self.lib.gpbs_backend_mux_count(self.h)
+
     def set_pmc(self, slot_id: int, pmc):
         arr = (C.c_uint64 * 4)(*[int(x) for x in pmc])
         return self._chk(self.lib.gpbs_slot_set_pmc(self.h, slot_id, arr), "set_pmc")

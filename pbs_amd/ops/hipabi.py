@@ -3,6 +3,8 @@ from __future__ import annotations
 
 import ctypes as C
 
+from .. import _native as N
+
 u32, i32, u64, i64 = C.c_uint32, C.c_int32, C.c_uint64, C.c_int64
 vp = C.c_void_p
 
@@ -80,6 +82,7 @@ def bind(lib):
     _p(lib, "gpbs_gpu_set_waveprio", C.c_int, vp, C.c_int)
     _p(lib, "gpbs_gpu_ctx_destroy", None, vp)
     _p(lib, "gpbs_gpu_attach", C.c_int, vp, vp, C.c_int, C.c_int)
+    _p(lib, "gpbs_gpu_backend_ops", C.c_int, vp, vp, C.POINTER(N.ActuatorOps), C.POINTER(N.CounterOps), C.c_int)
     _p(lib, "gpbs_gpu_table", vp, vp)
     _p(lib, "gpbs_gpu_counters", vp, vp)
     _p(lib, "gpbs_gpu_set_owners", C.c_int, vp, C.POINTER(C.c_int))

@@ -64,10 +64,9 @@ class Daemon:
         self.pids: Dict[int, int] = {}   # tenant -> registered process
         self.reaped: List[str] = []
         self.gpu_ctx = None
+        self.gpu_ctxs: List[Any] = []
         if attach_gpu:
-            from .gpu import GpuContext
-            self.gpu_ctx = GpuContext(self.gpus[0], self.engine, part_base=self.part_of[(self.gpus[0], 0, 0)],
-                                      nctx=nctx)
+            self.attach_backends(self._gpu_backend)
         self.lib.gpbs_ctl_bind(self.ctl, self.engine.h)
         self.state_path = state_path
         self.lock = threading.RLock()
@@ -78,6 +77,25 @@ class Daemon:
         self.server = Server(socket_path, self._handlers())
         self.sim = sim
         self.running = False
+
+    # ------------------------------------------------------ GPU backends
+    def _gpu_backend(self, gpu: int, part_lo: int):
+        from .gpu import GpuContext
+        ctx = GpuContext(gpu, part_base=part_lo, nctx=self.nctx)
+        ctx.attach_mux(self.engine, nctx=self.nctx)
+        return ctx
+
+    def attach_backends(self, factory):
+        """One actuator + counter backend per managed GPU.  ``factory(gpu,
+        part_lo)`` builds it and registers it on the engine's backend mux for
+        the GPU's partitions [part_lo, part_lo + 8 * nctx) (a GpuContext on a
+        GPU box; a fake in CPU tests).  Partitions of every GPU are driven --
+        the engine spans the node."""
+        for g in self.gpus:
+            b = factory(g, self.part_of[(g, 0, 0)])
+            self.gpu_ctxs.append(b)
+        self.gpu_ctx = self.gpu_ctxs[0] if self.gpu_ctxs else None
+        return self.gpu_ctxs
 
     # ----------------------------------------------------------- helpers
     def _resolve(self, dom) -> int:
@@ -521,9 +539,13 @@ class Daemon:
             if not self.sim:
                 self.engine.stop()
             self.lib.gpbs_ctl_close(self.ctl, 1)
-            if self.gpu_ctx is not None:
-                for g in self.gpu_ctxs if hasattr(self, "gpu_ctxs") else [self.gpu_ctx]:
-                    g.close()
+            if self.gpu_ctxs:
+                self.engine.mux_clear()
+                for g in self.gpu_ctxs:
+                    close = getattr(g, "close", None)
+                    if close:
+                        close()
+                self.gpu_ctxs = []
                 self.gpu_ctx = None
             self.engine.close()
 

@@ -56,6 +56,20 @@ class GpuContext:
         if rc:
             raise RuntimeError("gpbs_gpu_attach failed")
 
+    def attach_mux(self, engine, device_counters: bool = True, nctx: Optional[int] = None):
+        """Register this GPU as one backend of a multi-GPU engine: it serves the
+        partitions [part_base, part_base + 8 * nctx) (one engine spanning
+        several GPUs, gpbs_backend_mux_add).  Clear the engine's mux before
+        closing the context."""
+        self.engine = engine
+        if nctx is not None:
+            self.nctx = nctx
+        self.L.gpbs_gpu_set_nctx(self.h, self.nctx)
+        a, k = N.ActuatorOps(), N.CounterOps()
+        if self.L.gpbs_gpu_backend_ops(self.h, engine.h, C.byref(a), C.byref(k), int(device_counters)):
+            raise RuntimeError("gpbs_gpu_backend_ops failed")
+        return engine.mux_add(self.part_base, self.part_base + XCDS * self.nctx, a, k)
+
     @property
     def table(self):
         return C.c_void_p(self.L.gpbs_gpu_table(self.h))
