@@ -43,6 +43,10 @@ def main():
                     help="steady: tenants backlogged over common step windows (weighted speedup, default); "
                          "quota: round-1 fixed per-step quotas (early finishers idle)")
     ap.add_argument("--step-ms", type=float, default=80.0, help="steady protocol: step window length")
+    ap.add_argument("--gang-transport", default="shm", choices=["shm", "dist"],
+                    help="N > 1 gang epochs: native shared memory among the node's ranks, or the 'gang' process "
+                         "group (gloo; RCCL over xGMI with --gang-rccl)")
+    ap.add_argument("--gang-rccl", action="store_true", help="with --gang-transport dist: the gang group is RCCL")
     ap.add_argument("--table", default="host", choices=["host", "device"])
     ap.add_argument("--out", default="")
     ap.add_argument("--rehearse", action="store_true",
@@ -86,7 +90,8 @@ def main():
         else:
             dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
         groups["ctrl"] = dist.new_group(backend="gloo")
-        groups["gang"] = dist.new_group(backend="gloo")  # cross-GPU gang epochs (own thread)
+        # cross-GPU gang epochs (own thread); only used with --gang-transport dist
+        groups["gang"] = dist.new_group(backend="nccl" if args.gang_rccl and not args.rehearse else "gloo")
         groups["coll"] = dist.new_group(backend="gloo" if args.rehearse else "nccl")
 
     from pbs_amd import build
@@ -95,13 +100,21 @@ def main():
     if world > 1:
         dist.barrier(group=groups["ctrl"])
     from pbs_amd.bench.corun import Corun, CorunConfig
+    # gang epochs (N > 1): native shared-memory transport among the node's
+    # ranks; the region name is a nonce from rank 0 so no stale region matches
+    gang_base = ""
+    if world > 1:
+        nonce = torch.tensor([int.from_bytes(os.urandom(4), "little") if rank == 0 else 0], dtype=torch.int64)
+        dist.broadcast(nonce, src=0, group=groups["ctrl"])
+        gang_base = f"gpbs-gang-{int(nonce.item()):08x}"
 
     pols = tuple(p for p in args.policies.split(",") if p)
     if "gpbs" not in pols:
         pols = pols + ("gpbs",)
     cfg = CorunConfig(steps=args.steps, warmup=args.warmup, target_ms=args.target_ms, policies=pols,
                       table_mode=args.table, mix=args.mix, hw_counters=(counters == "hw"),
-                      protocol=args.protocol, step_ms=args.step_ms)
+                      protocol=args.protocol, step_ms=args.step_ms, gang_transport=args.gang_transport,
+                      gang_shm_base=gang_base)
     if args.rehearse:
         cfg.coll_bytes = 4 << 20  # CPU gloo all-reduce stand-in
     log = (lambda *a: print(*a, file=sys.stderr, flush=True))

@@ -3,6 +3,7 @@
 // gpbsctl) sees the same ranges and error codes.
 #include <algorithm>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <mutex>
 
@@ -167,6 +168,42 @@ gpbs_engine_t* gpbs_engine_create(const gpbs_boot_params_t* p) {
 int gpbs_fault_set(gpbs_engine_t* e, const char* spec) {
   LOCK(e);
   return e->e->fault_parse(spec);
+}
+
+int64_t gpbs_fault_fire(gpbs_engine_t* e, const char* kind) {
+  static const char* names[Engine::F_NKIND] = {"counter_drop", "counter_reset", "heartbeat_drop", "actuate_delay",
+                                               "timer_jitter", "rank_hang", "torn_page"};
+  if (!e || !kind) return -1;
+  LOCK(e);
+  for (int k = 0; k < Engine::F_NKIND; ++k)
+    if (std::strcmp(kind, names[k]) == 0) {
+      if (!e->e->fault(k)) return -1;
+      e->e->emit(TRC_FAULT, 0, (uint32_t)k, (uint32_t)e->e->fault_param[k]);
+      return e->e->fault_param[k] > 0 ? e->e->fault_param[k] : 0;
+    }
+  return -1;
+}
+
+// A gang epoch missed its deadline on this rank: degrade to local scheduling
+// (every cross-GPU gang window is cleared, so no tenant is favoured or
+// excluded for the sake of peers that may never arrive).
+int gpbs_gang_timeout(gpbs_engine_t* e, uint32_t epoch, uint32_t rank, uint32_t waited_us) {
+  LOCK(e);
+  Engine* E = e->e;
+  for (auto& t : E->tenants)
+    if (t && t->alive) {
+      t->gang_state = 0;
+      t->gang_until = 0;
+    }
+  for (auto& p : E->parts) E->raise_softirq(p->id);
+  E->perfc.incr(PC_gang_timeout);
+  E->emit(TRC_GANG_TIMEOUT, rank, epoch, rank, waited_us);
+  char msg[160];
+  std::snprintf(msg, sizeof(msg), "(GPBS) gang epoch %u: deadline missed after %u us on rank %u, scheduling locally\n",
+                epoch, waited_us, rank);
+  E->printk(msg);
+  DONE(e);
+  return GPBS_OK;
 }
 
 int gpbs_fault_hits(gpbs_engine_t* e, uint64_t* out, int n) {

@@ -176,7 +176,7 @@ void Engine::flush_actuation() {
 
 int Engine::fault_parse(const char* spec) {
   static const char* names[F_NKIND] = {"counter_drop", "counter_reset", "heartbeat_drop", "actuate_delay",
-                                       "timer_jitter"};
+                                       "timer_jitter", "rank_hang", "torn_page"};
   if (!spec) return 0;
   int n = 0;
   std::string s(spec);

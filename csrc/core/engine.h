@@ -313,10 +313,18 @@ class Engine {
   // reset, exercises the Q5 skip), heartbeat_drop (tenant heartbeats lost),
   // actuate_delay (a flush of partition switches held back to the next
   // batch), timer_jitter (a due timer fires `param` us late).
-  enum FaultKind { F_COUNTER_DROP = 0, F_COUNTER_RESET, F_HEARTBEAT_DROP, F_ACTUATE_DELAY, F_TIMER_JITTER, F_NKIND };
-  uint32_t fault_ppm[F_NKIND] = {0, 0, 0, 0, 0};
-  int64_t fault_param[F_NKIND] = {0, 0, 0, 0, 0};
-  uint64_t fault_hits[F_NKIND] = {0, 0, 0, 0, 0};
+  // rank_hang (the gang epoch thread of this rank stalls `param` ms before
+  // its collective: exercises the other ranks' gang deadline) and torn_page
+  // (a control-page publish pauses `param` us half-written: exercises the
+  // tenants' seqlock retry) fire at injection points outside the engine,
+  // through gpbs_fault_fire.
+  enum FaultKind {
+    F_COUNTER_DROP = 0, F_COUNTER_RESET, F_HEARTBEAT_DROP, F_ACTUATE_DELAY, F_TIMER_JITTER, F_RANK_HANG, F_TORN_PAGE,
+    F_NKIND
+  };
+  uint32_t fault_ppm[F_NKIND] = {};
+  int64_t fault_param[F_NKIND] = {};
+  uint64_t fault_hits[F_NKIND] = {};
   uint64_t fault_rng = 0x9E3779B97F4A7C15ull;
   bool fault(int k) {
     if (!fault_ppm[k]) return false;

@@ -125,6 +125,13 @@ int gpbs_backend_mux_add(struct gpbs_engine* e, int part_lo, int part_hi, const 
 int gpbs_backend_mux_clear(struct gpbs_engine* e);
 int gpbs_backend_mux_count(struct gpbs_engine* e);
 
+/* Fault-injection point outside the engine (gang thread, control-page
+ * writer): returns the kind's param (>= 0) when it fires, -1 otherwise. */
+int64_t gpbs_fault_fire(struct gpbs_engine* e, const char* kind);
+/* The gang epoch missed its deadline on this rank: clear every cross-GPU gang
+ * window, count it (perfc gang_timeout) and trace GANG_TIMEOUT. */
+int gpbs_gang_timeout(struct gpbs_engine* e, uint32_t epoch, uint32_t rank, uint32_t waited_us);
+
 typedef struct gpbs_trace_record {
   uint64_t t_ns;
   uint32_t event, cpu;

@@ -21,7 +21,9 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -163,13 +165,15 @@ Ctl* map_region(const char* name, int ntenants, bool create) {
 }
 
 void publish_page(Page* pg, uint32_t gate, const uint64_t* mask, uint32_t quantum, int32_t prio, int32_t tid,
-                  uint32_t epoch) {
+                  uint32_t epoch, int64_t torn_us = -1) {
   uint32_t s = pg->seq.load(std::memory_order_relaxed);
   const uint32_t old_gate = pg->gate.load(std::memory_order_relaxed);
   pg->seq.store(s + 1, std::memory_order_relaxed);
   std::atomic_thread_fence(std::memory_order_release);
   pg->gate.store(gate, std::memory_order_relaxed);
   pg->mask[0].store(mask[0], std::memory_order_relaxed);
+  if (torn_us >= 0)  // torn_page fault: readers see a half-written page (odd seq) for a while
+    std::this_thread::sleep_for(std::chrono::microseconds(std::max<int64_t>(torn_us, 50)));
   pg->mask[1].store(mask[1], std::memory_order_relaxed);
   pg->quantum_us.store(quantum, std::memory_order_relaxed);
   pg->priority.store(prio, std::memory_order_relaxed);
@@ -206,7 +210,8 @@ void br_on_flush(void* user, int64_t now) {
     if (tid < 0 || tid >= (int)c->pend_mask.size() / 2) continue;
     const uint64_t m[2] = {c->pend_mask[2 * tid], c->pend_mask[2 * tid + 1]};
     if (m[0] == pg->mask[0].load(std::memory_order_relaxed) && m[1] == pg->mask[1].load(std::memory_order_relaxed)) continue;
-    publish_page(pg, (m[0] | m[1]) ? 1u : 0u, m, pg->quantum_us.load(std::memory_order_relaxed), pg->priority.load(std::memory_order_relaxed), tid, c->epoch);
+    publish_page(pg, (m[0] | m[1]) ? 1u : 0u, m, pg->quantum_us.load(std::memory_order_relaxed),
+                 pg->priority.load(std::memory_order_relaxed), tid, c->epoch, gpbs_fault_fire(c->engine, "torn_page"));
   }
 }
 

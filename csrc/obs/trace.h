@@ -26,6 +26,7 @@ enum TraceEvent : uint32_t {
   TRC_FAULT = 14,      // a0=fault kind a1=arg
   TRC_ATC = 15,        // a0=global min slice a1=ntenants
   TRC_CLASS = 16,      // a0=tenant a1=class (0 compute, 1 memory) a2=partitions allowed
+  TRC_GANG_TIMEOUT = 17,  // a0=epoch a1=rank a2=waited_us: gang deadline missed, rank degraded to local
 };
 
 struct TraceRecord {

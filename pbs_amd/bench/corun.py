@@ -90,6 +90,9 @@ class CorunConfig:
     calib_units: int = 8
     gang_epoch_ms: float = 4.0   # N > 1: cross-GPU gang window length
     gang_share: float = 0.5      # fraction of epochs that are the all-reduce tenant's
+    gang_transport: str = "shm"  # shm (one node, native) | dist (the "gang" process group: gloo or RCCL)
+    gang_shm_base: str = ""      # region name prefix agreed by all ranks (a nonce broadcast by rank 0)
+    gang_deadline_ms: float = 200.0
     mix: str = "4mix"
     hw_counters: bool = False    # PBS metric from live hardware counters
     # "steady": every throughput tenant is kept backlogged for the whole timed
@@ -207,6 +210,7 @@ class Corun:
         self.coll_on_cpu = coll_on_cpu
         self.groups = groups or {}
         self.gang = None
+        self._gang_seq = 0
         self.gang_stats: Dict[str, float] = {}
         self.log = log if rank == 0 else (lambda *a, **k: None)
         torch.cuda.set_device(device)
@@ -266,6 +270,14 @@ class Corun:
     def _natives(self):
         return [r for r in self.runners.values() if isinstance(r, Runner)]
 
+    def _gang_device(self):
+        import torch.distributed as dist
+        g = self.groups.get("gang")
+        try:
+            return f"cuda:{self.device}" if g is not None and dist.get_backend(g) == "nccl" else None
+        except Exception:
+            return None
+
     def _stop_gang(self):
         if self.gang is not None:
             self.gang_stats = self.gang.stats()
@@ -305,9 +317,15 @@ class Corun:
                 # own gloo group: the main thread's barriers use "ctrl"
                 # The same epochs SUM-reduce the throughput tenants' counters
                 # into node-wide metrics (C11).
+                self._gang_seq += 1  # same policy order on every rank: same fresh region name
+                tr = self.cfg.gang_transport if self.cfg.gang_shm_base or self.cfg.gang_transport != "shm" else "dist"
                 self.gang = GangCoordinator(e, self.groups["gang"], [self.tid["coll"]],
                                             epoch_ms=self.cfg.gang_epoch_ms, share=self.cfg.gang_share,
-                                            metric_tenants=[self.tid[n] for n in self.throughput]).start()
+                                            metric_tenants=[self.tid[n] for n in self.throughput],
+                                            transport=tr, rank=self.rank, world=self.world,
+                                            shm_name=f"{self.cfg.gang_shm_base}-{self._gang_seq}",
+                                            deadline_ms=self.cfg.gang_deadline_ms,
+                                            device=self._gang_device()).start()
             return
         self.ctx.set_table_mode("host")
         self.ctx.set_spatial(False)

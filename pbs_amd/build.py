@@ -24,7 +24,7 @@ CSRC = os.path.join(ROOT, "csrc")
 LIBDIR = os.path.join(ROOT, "pbs_amd", "lib")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0] or "gfx950"
 
-CORE_DIRS = ["core", "obs", "ipc", "counters", "actuate", "api"]
+CORE_DIRS = ["core", "obs", "ipc", "counters", "actuate", "api", "comm"]
 HIP_DIR = "hip"
 
 

@@ -15,7 +15,7 @@ from .errors import GpbsError
 
 TRACE_EVENTS = {1: "SWITCH", 2: "WAKE", 3: "SLEEP", 4: "ACCT", 5: "ADAPT", 6: "GANG_EPOCH", 7: "REPORT",
                 8: "MIGRATE", 9: "PARK", 10: "STEAL", 11: "METRIC", 12: "DEAD", 13: "POOL", 14: "FAULT", 15: "ATC",
-                16: "CLASS"}
+                16: "CLASS", 17: "GANG_TIMEOUT"}
 EVENT_CODES = {v: k for k, v in TRACE_EVENTS.items()}
 
 PMC_NAMES = ("INST_RETIRED", "CPU_CLK_UNHALTED", "LLC_REFERENCES", "LLC_MISSES")
@@ -256,7 +256,8 @@ class Engine:
     def set_adapt_state(self, t: int, s: N.AdaptState):
         return self._chk(self.lib.gpbs_tenant_adapt_state(self.h, t, C.byref(s), 1), "set_adapt_state")
 
-    FAULT_KINDS = ("counter_drop", "counter_reset", "heartbeat_drop", "actuate_delay", "timer_jitter")
+    FAULT_KINDS = ("counter_drop", "counter_reset", "heartbeat_drop", "actuate_delay", "timer_jitter", "rank_hang",
+                   "torn_page")
 
     def fault_set(self, spec: str) -> int:
         """Arm fault injection: "kind=ppm[:param],...,seed=N" (see gpbs.h)."""
@@ -335,6 +336,16 @@ class Engine:
         if ops is not None:
             self._keep.append(ops)
         return self.lib.gpbs_set_actuator_ops(self.h, C.byref(ops) if ops is not None else None)
+
+    def fault_fire(self, kind: str) -> int:
+        """Injection point outside the engine: the kind's param (>= 0) when it
+        fires this time, -1 otherwise (GPBS_FAULT / fault_set)."""
+        return int(self.lib.gpbs_fault_fire(self.h, kind.encode()))
+
+    def gang_timeout(self, epoch: int, rank: int, waited_us: int):
+        """This rank missed a gang deadline: clear all cross-GPU windows,
+        count it and trace GANG_TIMEOUT (scheduling continues locally)."""
+        return self.lib.gpbs_gang_timeout(self.h, epoch & 0xFFFFFFFF, rank, min(int(waited_us), 0xFFFFFFFF))
 
     def mux_add(self, part_lo: int, part_hi: int, act: Optional[N.ActuatorOps] = None,
                 ctr: Optional[N.CounterOps] = None) -> int:

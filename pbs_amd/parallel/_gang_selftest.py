@@ -84,3 +84,48 @@ def atc_worker(rank: int, world: int, port: int, q, seconds: float = 0.8, epoch_
     q.put({"rank": rank, "local_min": local, "tslice": info.tslice_us, "stats": g.stats(),
            "node": node})
     dist.destroy_process_group()
+
+
+def hang_worker(rank: int, world: int, port: int, q, transport: str, shm_name: str, hang_rank: int,
+                hang_ms: int = 1500, deadline_ms: float = 200.0):
+    """One rank of the gang-deadline test: `hang_rank` stalls `hang_ms` before
+    its first exchange (GPBS_FAULT rank_hang); the others must time out
+    within the deadline, trace GANG_TIMEOUT and keep scheduling locally."""
+    import torch.distributed as dist
+
+    from pbs_amd.core.engine import Engine
+    from pbs_amd.parallel.gang import GangCoordinator
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    e = Engine(partitions=[(rank, x) for x in range(2)], quantum_align_us=0)
+    e.tenant_create("Domain-0", nslots=1)
+    coll = e.tenant_create("coll", nslots=2)
+    if rank == hang_rank:
+        e.fault_set(f"rank_hang=1000000:{hang_ms}")
+    e.start()
+    e.wake(coll)
+    dist.barrier()
+    t0 = time.monotonic()
+    g = GangCoordinator(e, None, [coll], epoch_ms=5.0, transport=transport, shm_name=shm_name,
+                        rank=rank, world=world, deadline_ms=deadline_ms).start()
+    degraded_at = None
+    # the hung rank stalls before EVERY exchange (ppm 1e6): it completes the
+    # epoch the others abandoned, then misses the next one itself
+    while time.monotonic() - t0 < (2 * hang_ms + 3 * deadline_ms) / 1e3 + 0.5:
+        if g.degraded and degraded_at is None:
+            degraded_at = time.monotonic() - t0
+            run0 = e.tenant_info(coll).run_ns
+            t_deg = time.monotonic()
+        time.sleep(0.002)
+    ran_after = None
+    if degraded_at is not None:
+        ran_after = (e.tenant_info(coll).run_ns - run0) / ((time.monotonic() - t_deg) * 1e9)
+    recs = [r.event for r in e.trace(from_start=True)]
+    q.put({"rank": rank, "degraded_at": degraded_at, "epochs": g.epoch, "stats": g.stats(),
+           "perfc_timeout": e.perfc().get("gang_timeout", 0), "traced": "GANG_TIMEOUT" in recs,
+           "ran_after": ran_after, "dmesg": e.dmesg()})
+    q.close()
+    q.join_thread()  # flush the result before the hard exit below
+    e.stop()
+    os._exit(0)  # a gloo collective abandoned at the deadline must not block exit

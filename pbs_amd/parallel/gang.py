@@ -32,9 +32,28 @@ intra-host traffic:
   counter deltas (INST, CYCLES, L2 refs, L2 misses) are SUM-reduced, so every
   rank sees node-wide per-tenant metrics (``node_metrics``) -- the master's
   cross-CPU pmc gather of csched_dom_metric_update, without a master.
+Transports (``transport=``):
+
+* ``shm`` -- all ranks of one node meet in a POSIX shared-memory region
+  (csrc/comm/gang_shm.cpp): microseconds per epoch, no kernel launch, no CU
+  time and no xGMI traffic next to the tenants' own RCCL all-reduce.  The
+  default for the one-node bench.
+* ``gloo`` -- node-local gloo (shared memory / TCP loopback, ~50-100 us).
+* ``rccl`` -- an RCCL group over xGMI (``device="cuda:N"``): the cross-node
+  capable path; latency-bound 4 KiB all-reduces cost tens of us and occupy
+  CUs for their kernels.
+
+Every epoch has a deadline (``deadline_ms``).  A rank that misses it -- one
+rank hung (GPBS_FAULT ``rank_hang``), descheduled or dead -- makes the others'
+exchange time out: they record GANG_TIMEOUT (trace + perfc ``gang_timeout``),
+clear every gang window and go on scheduling locally instead
+of stalling every GPU's gang thread.  Epoch-start skew across ranks (the
+spread of the previous epoch's return time, on the node's shared monotonic
+clock) rides the exchange and is reported in ``stats()``.
 """
 from __future__ import annotations
 
+import ctypes as C
 import threading
 import time
 from typing import Callable, Dict, List, Optional
@@ -46,11 +65,81 @@ FAVOUR, EXCLUDE, NONE = 1, 2, 0
 NO_ATC = 1 << 30  # MIN-neutral stand-in for "no ATC pool on this rank"
 
 
+class _DistTransport:
+    """gloo / RCCL: asynchronous collectives polled against the deadline."""
+
+    def __init__(self, group, device):
+        self.group = group
+        self.dev = torch.device(device) if device else torch.device("cpu")
+        if self.dev.type == "cuda":
+            torch.cuda.set_device(self.dev)
+
+    def _run(self, vals, op, deadline_ns):
+        buf = torch.tensor(vals, dtype=torch.int64, device=self.dev)
+        work = dist.all_reduce(buf, op=op, group=self.group, async_op=True)
+        while not work.is_completed():
+            if time.monotonic_ns() > deadline_ns:
+                return None  # left pending: this group is abandoned by the caller
+            time.sleep(20e-6)
+        work.wait()
+        return buf.tolist()
+
+    def reduce_min(self, vals, deadline_ns):
+        return self._run(vals, dist.ReduceOp.MIN, deadline_ns)
+
+    def reduce_sum(self, vals, deadline_ns):
+        return self._run(vals, dist.ReduceOp.SUM, deadline_ns)
+
+    def close(self):
+        pass
+
+
+class _ShmTransport:
+    """One-node ranks: native shared-memory all-gather (csrc/comm/gang_shm.cpp)."""
+
+    def __init__(self, name: str, rank: int, world: int, nvals: int):
+        from .. import _native as N
+        self.lib = N.load_core()
+        self.world, self.nvals = world, nvals
+        self.h = self.lib.gpbs_gang_shm_open(name.encode(), rank, world, nvals)
+        if not self.h:
+            raise RuntimeError(f"gang shm region {name!r} could not be opened")
+        self.seq = 0
+
+    def _gather(self, vals, deadline_ns):
+        n = self.nvals
+        vals = list(vals) + [0] * (n - len(vals))
+        self.seq += 1
+        src = (C.c_int64 * n)(*vals)
+        out = (C.c_int64 * (n * self.world))()
+        rc = self.lib.gpbs_gang_shm_allgather(C.c_void_p(self.h), self.seq, src, out, deadline_ns)
+        if rc == -110:
+            return None
+        if rc:
+            raise RuntimeError(f"gang shm all-gather failed ({rc})")
+        return [list(out[r * n:(r + 1) * n]) for r in range(self.world)]
+
+    def reduce_min(self, vals, deadline_ns):
+        rows = self._gather(vals, deadline_ns)
+        return None if rows is None else [min(c) for c in zip(*rows)][:len(vals)]
+
+    def reduce_sum(self, vals, deadline_ns):
+        rows = self._gather(vals, deadline_ns)
+        return None if rows is None else [sum(c) for c in zip(*rows)][:len(vals)]
+
+    def close(self):
+        if self.h:
+            self.lib.gpbs_gang_shm_close(C.c_void_p(self.h))
+            self.h = None
+
+
 class GangCoordinator:
     def __init__(self, engine, group, tenants: List[int], epoch_ms: float = 4.0, share: float = 0.5,
                  device: Optional[str] = None, demand: Optional[Callable[[int], bool]] = None,
                  slack_ms: float = 1.0, atc_pool: Optional[int] = None,
-                 metric_tenants: Optional[List[int]] = None, metric_every: int = 5):
+                 metric_tenants: Optional[List[int]] = None, metric_every: int = 5,
+                 transport: str = "dist", shm_name: Optional[str] = None, rank: Optional[int] = None,
+                 world: Optional[int] = None, deadline_ms: float = 200.0):
         self.engine = engine
         self.group = group
         self.tenants = list(tenants)
@@ -63,6 +152,7 @@ class GangCoordinator:
         self.state: Dict[int, int] = {t: NONE for t in self.tenants}
         self.history: List[tuple] = []  # (epoch, {tenant: state}) -- bounded
         self.lat_ns: List[int] = []
+        self.skew_ns: List[int] = []
         self._want_stop = False
         self._th: Optional[threading.Thread] = None
         self.error: Optional[BaseException] = None
@@ -72,6 +162,13 @@ class GangCoordinator:
         self.metric_every = max(1, int(metric_every))
         self.node_metrics: Dict[int, Dict[str, int]] = {}
         self.metric_syncs = 0
+        self.transport = transport
+        self.shm_name = shm_name
+        self.rank = rank if rank is not None else (dist.get_rank() if dist.is_initialized() else 0)
+        self.world = world if world is not None else (dist.get_world_size(group) if dist.is_initialized() else 1)
+        self.deadline_ns = int(deadline_ms * 1e6)
+        self.timeouts = 0
+        self.degraded = False
 
     # ------------------------------------------------------------ demand
     def _engine_demand(self, t: int) -> bool:
@@ -105,28 +202,54 @@ class GangCoordinator:
         return out
 
     # --------------------------------------------------------------- loop
+    def _make_transport(self, nvals: int):
+        if self.transport == "shm":
+            if not self.shm_name:
+                raise ValueError("transport 'shm' needs shm_name (the same fresh name on every rank)")
+            return _ShmTransport(self.shm_name, self.rank, self.world, max(nvals, 4 * len(self.metric_tenants)))
+        return _DistTransport(self.group, self.device)
+
+    def _timeout(self, waited_ns: int):
+        """Deadline missed: degrade this rank to local scheduling."""
+        self.timeouts += 1
+        self.degraded = True
+        if self.engine is not None:
+            self.engine.gang_timeout(self.epoch, self.rank, waited_ns // 1000)
+
     def _loop(self):
-        dev = torch.device(self.device) if self.device else torch.device("cpu")
+        tr = None
         try:
+            tr = self._make_transport(len(self.tenants) + 4)
+            t_prev = 0
             while True:
+                hang = self.engine.fault_fire("rank_hang") if self.engine is not None else -1
+                if hang >= 0:  # GPBS_FAULT rank_hang=ppm:ms -- this rank stalls before the exchange
+                    time.sleep(max(hang, 1) / 1e3)
                 t0 = time.monotonic_ns()
                 vec = [1 if self.demand(t) else 0 for t in self.tenants]
-                vec += [self._atc_local(), 0 if self._want_stop else 1]
-                buf = torch.tensor(vec, dtype=torch.int32, device=dev)
-                dist.all_reduce(buf, op=dist.ReduceOp.MIN, group=self.group)
-                red = buf.tolist()
+                vec += [self._atc_local(), 0 if self._want_stop else 1, t_prev, -t_prev]
+                red = tr.reduce_min(vec, t0 + self.deadline_ns)
                 t1 = time.monotonic_ns()
-                self.lat_ns.append(t1 - t0)
-                if len(self.lat_ns) > 4096:
-                    del self.lat_ns[:2048]
-                if not red[-1]:
+                if red is None:
+                    self._timeout(t1 - t0)
                     break
-                if self.atc_pool is not None and 0 < red[-2] < NO_ATC:
-                    self.atc_global_us = red[-2]
-                    self.engine.atc_sync(self.atc_pool, red[-2])
+                t_prev = t1
+                self.lat_ns.append(t1 - t0)
+                if red[-2] > 0:  # spread of the previous epoch's return time over the ranks
+                    self.skew_ns.append(-red[-1] - red[-2])
+                for lst in (self.lat_ns, self.skew_ns):
+                    if len(lst) > 4096:
+                        del lst[:2048]
+                if not red[-3]:
+                    break
+                if self.atc_pool is not None and 0 < red[-4] < NO_ATC:
+                    self.atc_global_us = red[-4]
+                    self.engine.atc_sync(self.atc_pool, red[-4])
                 if self.metric_tenants and self.epoch % self.metric_every == 0:
-                    self._sync_metrics(dev)
-                dec = self.decide(self.epoch, red[:-2])
+                    if not self._sync_metrics(tr):
+                        self._timeout(time.monotonic_ns() - t1)
+                        break
+                dec = self.decide(self.epoch, red[:len(self.tenants)])
                 until = self.engine.now() + self.epoch_ns + self.slack_ns
                 for t, st in dec.items():
                     self.engine.gang_set(t, st, until)
@@ -141,6 +264,8 @@ class GangCoordinator:
         except BaseException as e:  # pragma: no cover - surfaced via .error
             self.error = e
         finally:
+            if tr is not None and not self.degraded:
+                tr.close()
             for t in self.tenants:
                 try:
                     self.engine.gang_set(t, NONE, 0)
@@ -156,7 +281,7 @@ class GangCoordinator:
             return NO_ATC
         return v if v > 0 else NO_ATC
 
-    def _sync_metrics(self, dev):
+    def _sync_metrics(self, tr) -> bool:
         """SUM-reduce the metric tenants' last-period counter deltas."""
         vals = []
         for t in self.metric_tenants:
@@ -164,9 +289,9 @@ class GangCoordinator:
                 vals += [int(x) for x in self.engine.tenant_info(t).pmc]
             except Exception:
                 vals += [0, 0, 0, 0]
-        buf = torch.tensor(vals, dtype=torch.int64, device=dev)
-        dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group)
-        red = buf.tolist()
+        red = tr.reduce_sum(vals, time.monotonic_ns() + self.deadline_ns)
+        if red is None:
+            return False
         out = {}
         for i, t in enumerate(self.metric_tenants):
             inst, cyc, ref, miss = red[4 * i:4 * i + 4]
@@ -174,6 +299,7 @@ class GangCoordinator:
                       "miss_rate": miss * 100000 // inst if inst else 0}
         self.node_metrics = out
         self.metric_syncs += 1
+        return True
 
     def start(self):
         self._th = threading.Thread(target=self._loop, daemon=True, name="gpbs-gang")
@@ -181,7 +307,8 @@ class GangCoordinator:
         return self
 
     def stop(self, timeout: float = 30.0):
-        """Collective: returns once every rank has left the epoch loop."""
+        """Collective: returns once every rank has left the epoch loop (a
+        degraded rank has already left it)."""
         self._want_stop = True
         if self._th is not None:
             self._th.join(timeout)
@@ -190,5 +317,9 @@ class GangCoordinator:
 
     def stats(self) -> Dict[str, float]:
         lat = sorted(self.lat_ns) or [0]
-        return {"epochs": self.epoch, "sync_p50_us": lat[len(lat) // 2] / 1e3, "sync_max_us": lat[-1] / 1e3,
+        skew = sorted(self.skew_ns) or [0]
+        return {"epochs": self.epoch, "transport": self.transport, "sync_p50_us": lat[len(lat) // 2] / 1e3,
+                "sync_p99_us": lat[min(len(lat) - 1, int(0.99 * len(lat)))] / 1e3, "sync_max_us": lat[-1] / 1e3,
+                "skew_p50_us": skew[len(skew) // 2] / 1e3, "skew_max_us": skew[-1] / 1e3,
+                "timeouts": self.timeouts, "degraded": self.degraded,
                 "atc_global_us": self.atc_global_us, "metric_syncs": self.metric_syncs}

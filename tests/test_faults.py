@@ -91,3 +91,54 @@ def test_env_var_arms_faults_at_engine_creation():
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=60)
     hits, armed = out.stdout.split()
     assert int(hits) > 0 and armed == "True", out.stderr
+
+
+def test_torn_page_fault_is_caught_by_the_seqlock():
+    """torn_page: every control-page publish pauses half-written; a reader
+    polling the page concurrently retries (odd sequence / changed sequence)
+    and never returns a torn assignment (gate set iff the mask is non-empty)."""
+    import ctypes as C
+    import tempfile
+    import threading
+
+    from pbs_amd import _native as N
+    from pbs_amd.runtime.daemon import Daemon
+    d = Daemon(os.path.join(tempfile.mkdtemp(), "gpbsd.sock"), gpus=[0], nctx=2, sim=True, profile="mi355x")
+    d.start(reaper_s=0)
+    try:
+        regs = [d.register(name=n, slots=16, pid=os.getpid()) for n in ("a", "b")]
+        assert d.engine.fault_set("torn_page=1000000:300") == 1
+        lib = N.load_core()
+        h = lib.gpbs_ctl_open(regs[0]["ctl"].encode())
+        page = regs[0]["page"]
+        stop = threading.Event()
+        seen = {"reads": 0, "retries": 0, "bad": 0}
+
+        def reader():
+            g, q, ep = C.c_uint32(), C.c_uint32(), C.c_uint32()
+            m = (C.c_uint64 * 2)()
+            pr, tid = C.c_int32(), C.c_int32()
+            while not stop.is_set():
+                r = lib.gpbs_ctl_read(C.c_void_p(h), page, C.byref(g), m, C.byref(q), C.byref(pr), C.byref(tid),
+                                      C.byref(ep))
+                if r < 0:
+                    continue
+                seen["reads"] += 1
+                seen["retries"] += r
+                if bool(g.value) != bool(m[0] | m[1]):
+                    seen["bad"] += 1
+
+        th = threading.Thread(target=reader)
+        th.start()
+        for t in (r["tenant"] for r in regs):
+            d.engine.wake(t)
+        for _ in range(300):
+            d.advance_us(250)
+        stop.set()
+        th.join()
+        lib.gpbs_ctl_close(C.c_void_p(h), 0)
+        assert d.engine.fault_hits()["torn_page"] > 0
+        assert seen["reads"] > 0 and seen["retries"] > 0, seen
+        assert seen["bad"] == 0, seen
+    finally:
+        d.stop()

@@ -1,0 +1,50 @@
+"""Gang-barrier deadline: world 4, one rank hung
+by GPBS_FAULT rank_hang.  The other ranks must leave the epoch exchange at
+the deadline, trace GANG_TIMEOUT, count gang_timeout and keep scheduling
+locally; the hung rank degrades as well once it comes back.  Both the gloo
+and the native shared-memory transport."""
+import multiprocessing as mp
+import os
+import socket
+
+import pytest
+
+from pbs_amd.parallel._gang_selftest import hang_worker
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("transport", ["gloo", "shm"])
+def test_one_hung_rank_does_not_stall_the_others(transport):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    world, hung, hang_ms, deadline_ms = 4, 2, 1500, 200.0
+    name = f"gpbs-gang-test-{os.getpid()}-{port}"
+    ps = [ctx.Process(target=hang_worker, args=(r, world, port, q, "dist" if transport == "gloo" else "shm", name,
+                                                 hung, hang_ms, deadline_ms)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = {}
+    for _ in ps:
+        r = q.get(timeout=120)
+        out[r["rank"]] = r
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r, o in out.items():
+        assert o["degraded_at"] is not None, o
+        assert o["perfc_timeout"] == 1 and o["traced"], o
+        assert "deadline missed" in o["dmesg"]
+        assert o["ran_after"] > 1.5, o  # the engine keeps scheduling its partitions locally
+        if r != hung:
+            # out of the exchange within the deadline (+ scheduling slack), long before the hung rank returns
+            assert o["degraded_at"] < (deadline_ms + 300) / 1e3, o
+        else:
+            assert o["degraded_at"] > hang_ms / 1e3, o
