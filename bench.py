@@ -47,6 +47,9 @@ def main():
                     help="N > 1 gang epochs: native shared memory among the node's ranks, or the 'gang' process "
                          "group (gloo; RCCL over xGMI with --gang-rccl)")
     ap.add_argument("--gang-rccl", action="store_true", help="with --gang-transport dist: the gang group is RCCL")
+    ap.add_argument("--gang-wait-driven", action="store_true",
+                    help="N > 1: the all-reduce tenant gets aligned gang windows only while its K10 wait reports "
+                         "(peer-arrival skew of its RCCL all-reduces) say its peers lag")
     ap.add_argument("--table", default="host", choices=["host", "device"])
     ap.add_argument("--out", default="")
     ap.add_argument("--rehearse", action="store_true",
@@ -114,7 +117,7 @@ def main():
     cfg = CorunConfig(steps=args.steps, warmup=args.warmup, target_ms=args.target_ms, policies=pols,
                       table_mode=args.table, mix=args.mix, hw_counters=(counters == "hw"),
                       protocol=args.protocol, step_ms=args.step_ms, gang_transport=args.gang_transport,
-                      gang_shm_base=gang_base)
+                      gang_shm_base=gang_base, gang_wait_driven=args.gang_wait_driven)
     if args.rehearse:
         cfg.coll_bytes = 4 << 20  # CPU gloo all-reduce stand-in
     log = (lambda *a: print(*a, file=sys.stderr, flush=True))

@@ -46,6 +46,7 @@ void atc_init(AtcState& s, const AtcParams& p) {
 }
 
 void atc_report(AtcState& s, const AtcParams& p, uint64_t wait) {
+  if (p.wait_unit_ns > 1) wait /= p.wait_unit_ns;
   s.spin = s.spin / p.alpha + wait / p.alpha * (p.alpha - 1);
   s.spin_count++;
 }

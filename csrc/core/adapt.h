@@ -77,7 +77,10 @@ struct AtcParams {
   uint32_t alpha = 4;            // EWMA alpha (:217)
   uint32_t warmup = 3;           // sdom->count (:1415)
   uint32_t apply_period_us = 21000;  // CSCHED_TIME_APPLY (:50)
-  uint32_t reserved = 0;
+  // Reported waits are ns (K10 probes time RCCL collectives and stream
+  // syncs); the reference's buckets (:241-262) are in spin-loop iterations.
+  // wait_unit_ns converts (0/1 = feed raw values, reference-exact).
+  uint32_t wait_unit_ns = 0;
 };
 
 struct AtcHist {

@@ -770,6 +770,7 @@ class CreditScheduler : public Scheduler {
     }
     if (mode_ == Mode::ATC) {
       atc_report(s.atc, E.atc_params, wait);
+      s.spinlock_latency += wait;  // cumulative, for introspection / gang decisions
     } else {  // do_vcrd_op (:249-259)
       s.spinlock_latency += wait;
       s.spinlock_metric_update += wait;

@@ -13,8 +13,11 @@
 //               drains (slot block).  This is the in-process tenant shim; the
 //               cross-process one is pbs_amd/runtime/tenant.py over ctl pages.
 #include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <atomic>
+#include <cstdio>
+#include <cstdlib>
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
@@ -48,6 +51,23 @@ int gpbs_hip_adapt(void*, const void*, const void*, const void*, int, const gpbs
 }
 
 namespace {
+
+// roctx ranges/marks: scheduler decisions next to tenant kernels
+// on a rocprofv3 --marker-trace timeline.  Ranges (metric tick, counter
+// sample, table publish) are always emitted -- a no-op call without a tool;
+// per-switch marks format a string, so they need GPBS_ROCTX=1.
+bool roctx_switch_marks() {
+  static const bool on = [] {
+    const char* v = std::getenv("GPBS_ROCTX");
+    return v && std::atoi(v) > 0;
+  }();
+  return on;
+}
+
+struct RoctxRange {
+  explicit RoctxRange(const char* m) { roctxRangePushA(m); }
+  ~RoctxRange() { roctxRangePop(); }
+};
 
 int64_t mono_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
@@ -122,6 +142,9 @@ struct GpuCtx {
   int64_t own_ns[kMaxTenants][kXcds * kCtx];
   int64_t own_base[kMaxTenants][kXcds * kCtx];
   int64_t last_pub_ns = 0;
+  hipEvent_t adapt_ev = nullptr;  // device adapt: bounded poll, never a blocking sync
+  bool adapt_pending = false;
+  uint64_t adapt_late = 0;
   int se_mode = 0;  // partitions are exclusive shader engines (GATE_SE)
   int muxed = 0;    // ops installed through the engine's backend mux
 };
@@ -147,6 +170,11 @@ void act_on_switch(void* user, int part, int, int next, int, int32_t, int64_t) {
   const int x = i / c->nctx, ctx = i % c->nctx;
   c->pending[x * kCtx + ctx] = next >= 0 ? (u32)next : kNoOwner;
   c->switches++;
+  if (roctx_switch_marks()) {  // TRC_SCHED_SWITCH analog (X:xen/common/schedule.c:1138-1151)
+    char m[64];
+    std::snprintf(m, sizeof m, "gpbs:switch xcd%d.%d -> t%d", x, ctx, next);
+    roctxMarkA(m);
+  }
 }
 
 // Spatial mode: mark an XCD split when its two owners are of different
@@ -177,6 +205,7 @@ void publish(GpuCtx* c) {
   for (int x = 0; x < kXcds * kCtx; ++x)
     if (__atomic_load_n(&c->h_table->owner[x], __ATOMIC_RELAXED) != c->pending[x]) changed = true;
   if (!changed) return;
+  RoctxRange rr("gpbs:publish");
   {
     std::lock_guard<std::mutex> g(c->mu);
     const int64_t t = mono_ns();
@@ -209,8 +238,10 @@ void hwc_loop(GpuCtx* c) {
   constexpr int kOwn = kMaxTenants * kXcds * kCtx;
   std::vector<u64> blk(kBlk), se(kXcds * kCtx * kNumPmc), xs(kXcds * kNumPmc);
   std::vector<int64_t> own(kOwn);
+  roctxNameOsThread("gpbs-hwc-sampler");
   while (!c->hwc_stop.load(std::memory_order_acquire)) {
     const int64_t t0 = mono_ns();
+    RoctxRange rr("gpbs:hwc_sample");
     if (hipMemcpyAsync(c->h_blk, c->d_cnt, sizeof(u64) * kBlk, hipMemcpyDeviceToHost, c->hwc_stream) != hipSuccess)
       break;
     hipEventRecord(c->blk_ev, c->hwc_stream);
@@ -328,6 +359,7 @@ void hwc_attribute(GpuCtx* c) {
 
 int hwc_tenant_deltas(GpuCtx* c, int n, const int* tenants, uint64_t* out) {
   const int64_t t0 = mono_ns();
+  RoctxRange rr("gpbs:metric_tick");
   {
     std::lock_guard<std::mutex> g(c->snap_mu);
     if (c->snap_seq != c->used_seq && !c->snap_own.empty()) {
@@ -358,6 +390,7 @@ int ctr_tenant_deltas(void* user, int n, const int* tenants, uint64_t* out) {
   if (n > kMaxTenants) return -22;
   if (c->hwc) return hwc_tenant_deltas(c, n, tenants, out);
   const int64_t t0 = mono_ns();
+  RoctxRange rr("gpbs:metric_tick");
   if (c->red_pending && hipEventQuery(c->red_ev) == hipErrorNotReady) {
     // The previous reduce has not finished (a tail, ~0.1 % of periods): never
     // wait for it under the engine lock.  This period reports nothing (the
@@ -394,18 +427,41 @@ int ctr_tenant_deltas(void* user, int n, const int* tenants, uint64_t* out) {
   return 0;
 }
 
+constexpr int64_t kAdaptPollNs = 200000;  // 0.2 ms of the 1 ms metric period
+
 int ctr_adapt_batch(void* user, int n, const int*, const uint64_t* deltas, const uint64_t* ssum, const uint64_t* scnt,
                     gpbs_adapt_state_t* states, const gpbs_adapt_params_t* p) {
   GpuCtx* c = (GpuCtx*)user;
   if (n > kMaxTenants) return -22;
   const int64_t t0 = mono_ns();
+  RoctxRange rr("gpbs:adapt_device");
+  // The engine lock is held here: never block on the device.  A previous
+  // launch still running (its buffers are in use) or a result not back
+  // within the poll budget makes this period fall back to the host
+  // adapt_update (bit-identical), and the late result is discarded.
+  if (c->adapt_pending) {
+    if (hipEventQuery(c->adapt_ev) == hipErrorNotReady) return -11;
+    c->adapt_pending = false;
+  }
   std::memcpy(c->h_states, states, sizeof(gpbs_adapt_state_t) * n);
   std::memcpy(c->h_adelta, deltas, sizeof(u64) * 4 * n);
   std::memcpy(c->h_spin, ssum, sizeof(u64) * n);
   std::memcpy(c->h_spin + kMaxTenants, scnt, sizeof(u64) * n);
   if (gpbs_hip_adapt(c->h_states, c->h_adelta, c->h_spin, c->h_spin + kMaxTenants, n, p, c->h_dirs, c->sched_stream))
     return -5;
-  if (hipStreamSynchronize(c->sched_stream) != hipSuccess) return -5;
+  hipEventRecord(c->adapt_ev, c->sched_stream);
+  c->adapt_pending = true;
+  for (;;) {
+    const hipError_t q = hipEventQuery(c->adapt_ev);
+    if (q == hipSuccess) break;
+    if (q != hipErrorNotReady) return -5;
+    if (mono_ns() - t0 > kAdaptPollNs) {
+      c->adapt_late++;
+      c->metric_ns += mono_ns() - t0;
+      return -11;
+    }
+  }
+  c->adapt_pending = false;
   std::memcpy(states, c->h_states, sizeof(gpbs_adapt_state_t) * n);
   c->metric_ns += mono_ns() - t0;
   return 0;
@@ -763,6 +819,7 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
   ok = ok && hipHostMalloc((void**)&c->h_out2, sizeof(u64) * 4 * kMaxTenants, hipHostMallocMapped) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_ids2, sizeof(int) * kMaxTenants, hipHostMallocMapped) == hipSuccess;
   ok = ok && hipEventCreateWithFlags(&c->red_ev, hipEventDisableTiming) == hipSuccess;
+  ok = ok && hipEventCreateWithFlags(&c->adapt_ev, hipEventDisableTiming) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_states, sizeof(gpbs_adapt_state_t) * kMaxTenants, hipHostMallocMapped) ==
                  hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_spin, sizeof(u64) * 2 * kMaxTenants, hipHostMallocMapped) == hipSuccess;
@@ -810,6 +867,10 @@ void gpbs_gpu_ctx_destroy(void* p) {
   hipHostFree(c->h_out2);
   hipHostFree(c->h_ids2);
   hipEventDestroy(c->red_ev);
+  if (c->adapt_ev) {
+    hipEventSynchronize(c->adapt_ev);
+    hipEventDestroy(c->adapt_ev);
+  }
   hipHostFree(c->h_states);
   hipHostFree(c->h_spin);
   hipHostFree(c->h_dirs);
@@ -1063,6 +1124,11 @@ int gpbs_gpu_stats(void* p, uint64_t* out4) {
 // CU-masked stream for foreign kernels (torch/hipBLASLt/RCCL tenants): a
 // stream whose hardware queue only dispatches to the CUs in `cu_mask`
 // (nwords x 32 bits, hipExtStreamCreateWithCUMask).
+// roctx helpers for the Python side (gang epochs, bench policy windows).
+int gpbs_roctx_push(const char* m) { return roctxRangePushA(m); }
+int gpbs_roctx_pop(void) { return roctxRangePop(); }
+void gpbs_roctx_mark(const char* m) { roctxMarkA(m); }
+
 void* gpbs_gpu_cumask_stream(int device, const uint32_t* cu_mask, int nwords, int priority) {
   hipSetDevice(device);
   hipStream_t s = nullptr;

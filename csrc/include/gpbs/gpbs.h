@@ -46,7 +46,8 @@ typedef struct gpbs_adapt_params {
 
 typedef struct gpbs_atc_params {
   uint32_t default_us, min_us, max_us, zero_step_us, climb_step_us, climb_floor_us, base_us, slope_us,
-      alpha, warmup, apply_period_us, reserved;
+      alpha, warmup, apply_period_us,
+      wait_unit_ns; /* reported wait ns per reference spin iteration (0/1 = raw) */
 } gpbs_atc_params_t;
 
 /* Boot parameters (level-1 config; X:xen/common/schedule.c:39-54,

@@ -24,7 +24,7 @@ class AdaptParams(C.Structure):
 class AtcParams(C.Structure):
     _fields_ = [(n, u32) for n in ("default_us", "min_us", "max_us", "zero_step_us", "climb_step_us",
                                    "climb_floor_us", "base_us", "slope_us", "alpha", "warmup", "apply_period_us",
-                                   "reserved")]
+                                   "wait_unit_ns")]
 
 
 ABI_VERSION = 2  # GPBS_ABI_VERSION in csrc/include/gpbs/gpbs.h

@@ -93,6 +93,7 @@ class CorunConfig:
     gang_transport: str = "shm"  # shm (one node, native) | dist (the "gang" process group: gloo or RCCL)
     gang_shm_base: str = ""      # region name prefix agreed by all ranks (a nonce broadcast by rank 0)
     gang_deadline_ms: float = 200.0
+    gang_wait_driven: bool = False  # gang windows only while the coll tenant's K10 waits say its peers lag
     mix: str = "4mix"
     hw_counters: bool = False    # PBS metric from live hardware counters
     # "steady": every throughput tenant is kept backlogged for the whole timed
@@ -151,9 +152,15 @@ class CollTenant:
     process group and stream, launch-gated on XCD ownership (RCCL kernels
     themselves are not CU-confined)."""
 
-    def __init__(self, ctx: GpuContext, tenant: int, nbytes: int, group, on_cpu: bool = False):
+    def __init__(self, ctx: GpuContext, tenant: int, nbytes: int, group, on_cpu: bool = False,
+                 board_name: str = "", rank: int = 0, world: int = 1):
         self.ctx, self.tenant, self.group = ctx, tenant, group
         self.engine: Optional[Engine] = None
+        # K10: every all-reduce is timed against the node's arrival board and
+        # the wait for the slowest peer goes to the active engine (REPORT_WAIT)
+        from ..runtime.waitprobe import ArrivalBoard, WaitProbe
+        self.board = ArrivalBoard(board_name, rank, world) if board_name else None
+        self.probe = WaitProbe(self._report, board=self.board)
         # on_cpu: bench --rehearse (gloo stand-in for RCCL, all ranks on one GPU)
         self.buf = torch.randn(nbytes // 2, device="cpu" if on_cpu else "cuda",
                                dtype=torch.float32 if on_cpu else torch.bfloat16)
@@ -173,13 +180,27 @@ class CollTenant:
             for _ in range(n):
                 while not self._owns():
                     time.sleep(20e-6)
-                dist.all_reduce(self.buf, group=self.group)
+                self.probe.collective(dist.all_reduce, self.buf, group=self.group)
                 self.buf.mul_(0.5)
             self.stream.synchronize()
+            self.probe.poll()
         self.units_done += n
         self.last_done_ns = time.monotonic_ns()
         if self.engine is not None and self.gate:
             self.engine.block(self.tenant)
+
+    def _report(self, ns: int):
+        e = self.engine
+        if e is not None:
+            try:
+                e.report_wait(self.tenant, int(ns))
+            except Exception:
+                pass
+
+    def close(self):
+        if self.board is not None:
+            self.board.close()
+            self.board = None
 
     # steady-state protocol: all-reduce back to back until stopped
     def start_loop(self):
@@ -240,7 +261,9 @@ class Corun:
             return Runner(self.ctx, "stream", t, depth=cfg.depth, bytes=cfg.hbm_bytes)
         if name == "coll":
             if self.world > 1:
-                return CollTenant(self.ctx, t, cfg.coll_bytes, self.groups.get("coll"), on_cpu=self.coll_on_cpu)
+                return CollTenant(self.ctx, t, cfg.coll_bytes, self.groups.get("coll"), on_cpu=self.coll_on_cpu,
+                                  board_name=f"{cfg.gang_shm_base}-arr" if cfg.gang_shm_base else "",
+                                  rank=self.rank, world=self.world)
             return Runner(self.ctx, "reduce", t, depth=cfg.depth, bytes=cfg.coll_bytes)
         if name == "idle":
             return Runner(self.ctx, "gemv", t, depth=1, priority=1, M=cfg.idle_rows, K=cfg.idle_rows)
@@ -325,6 +348,7 @@ class Corun:
                                             transport=tr, rank=self.rank, world=self.world,
                                             shm_name=f"{self.cfg.gang_shm_base}-{self._gang_seq}",
                                             deadline_ms=self.cfg.gang_deadline_ms,
+                                            wait_driven=self.cfg.gang_wait_driven,
                                             device=self._gang_device()).start()
             return
         self.ctx.set_table_mode("host")
@@ -536,6 +560,11 @@ class Corun:
         return res
 
     def run_policy(self, policy: str, steps: int, warmup: int) -> Dict:
+        from ..utils import roctx
+        with roctx.range(f"gpbs:policy {policy}"):
+            return self._run_policy(policy, steps, warmup)
+
+    def _run_policy(self, policy: str, steps: int, warmup: int) -> Dict:
         if self.cfg.protocol == "steady":
             return self.run_policy_steady(policy, steps, warmup)
         self.set_policy(policy)
@@ -621,6 +650,9 @@ class Corun:
                                 for n in self.tid}
             eng["runner"] = {n: {k: getattr(r.stats(), k) for k in ("launches", "relaunches", "waits_owner")}
                              for n, r in self.runners.items() if isinstance(r, Runner)}
+            coll = self.runners.get("coll")
+            if isinstance(coll, CollTenant):
+                eng["coll_wait"] = coll.probe.stats()  # K10 reports (cumulative)
             if self.gang is not None:
                 eng["gang"] = self.gang.stats()
                 names = {v: k for k, v in self.tid.items()}
@@ -640,6 +672,9 @@ class Corun:
             self.active_engine.stop()
         for r in self._natives():
             r.close()
+        coll = self.runners.get("coll")
+        if isinstance(coll, CollTenant):
+            coll.close()
         self.ctx.close()
         for e in self.engines.values():
             e.close()

@@ -36,6 +36,10 @@ MI355X_PROFILE: Dict[str, Any] = dict(
     coschedule=3, class_period_us=2000,
     adapt=dict(threshold=20000, band_lo=70, band_hi=130, min_us=1000, max_us=11000, inc_us=1000, dec_us=2000,
                switch_boundary=9000, ticks_per_tslice=3),
+    # ATC (sched="atc"): waits arrive in ns from the K10 probes
+    # (runtime/waitprobe.py); the reference buckets spin-loop iterations, one
+    # PAUSE-loop iteration taken as ~8 ns.
+    atc=dict(wait_unit_ns=8),
 )
 
 BOOT_KEYS = ("sched", "tslice_us", "ratelimit_us", "smt_power_savings", "tickle_one_idle", "default_yield",

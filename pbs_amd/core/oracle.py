@@ -153,6 +153,7 @@ class AtcParams:
     alpha: int = 4
     warmup: int = 3
     apply_period_us: int = 21000
+    wait_unit_ns: int = 0  # gpbs: ns per reference spin iteration (0/1 = raw)
 
 
 @dataclass
@@ -185,6 +186,8 @@ def atc_bucket(x: int) -> int:
 
 
 def atc_report(s: AtcState, p: AtcParams, wait: int):
+    if p.wait_unit_ns > 1:
+        wait //= p.wait_unit_ns
     s.spin = s.spin // p.alpha + wait // p.alpha * (p.alpha - 1)
     s.spin_count += 1
 

@@ -278,6 +278,8 @@ class LlamaDecoder:
 
     def __init__(self, cfg: LlamaConfig, batch: int, context: int, device="cuda", dtype=torch.bfloat16,
                  fused: Optional[bool] = None, fp8: bool = False, graph: bool = False, static: bool = False):
+        if not 0 < context <= cfg.max_seq:  # the RoPE tables cover max_seq positions
+            raise ValueError(f"LlamaDecoder: context {context} must be in [1, max_seq={cfg.max_seq}]")
         self.cfg, self.batch, self.context = cfg, batch, context
         self.model = build(cfg, device, dtype)
         self.model.eval()

@@ -88,6 +88,12 @@ def qkv_rope_cache(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, pos_
     if qkv.numel() != B * (n_heads + 2 * Hkv) * hd or vc.shape != kc.shape or cos.shape[-1] * 2 != hd \
             or pos_t.dtype != torch.int32:
         raise ValueError(f"qkv_rope_cache: qkv {tuple(qkv.shape)} vs cache {tuple(kc.shape)}, H={n_heads}")
+    # the kernel indexes the RoPE tables and the cache rows with the device
+    # position: the tables must cover every cache row, dtypes as it assumes
+    if cos.shape[0] < Cn or sin.shape != cos.shape or cos.dtype != torch.float32 or sin.dtype != torch.float32 \
+            or kc.dtype != torch.bfloat16 or vc.dtype != torch.bfloat16 or qkv.dtype != torch.bfloat16:
+        raise ValueError(f"qkv_rope_cache: rope tables {tuple(cos.shape)} {cos.dtype} must cover {Cn} cache rows "
+                         f"(fp32), caches/qkv bf16")
     q = torch.empty(B, n_heads, hd, dtype=torch.bfloat16, device=qkv.device)
     _check(lib().gpbs_hip_qkv_rope_cache(_ptr(qkv), _ptr(cos), _ptr(sin), _ptr(pos_t), _ptr(q), _ptr(kc), _ptr(vc),
                                          B, n_heads, Hkv, Cn, hd, _stream()), "qkv_rope_cache")

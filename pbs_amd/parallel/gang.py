@@ -43,6 +43,13 @@ Transports (``transport=``):
   capable path; latency-bound 4 KiB all-reduces cost tens of us and occupy
   CUs for their kernels.
 
+Wait-driven windows (``wait_driven=True``): the vector also
+carries each gang tenant's wait reported on this GPU since the last epoch
+(RCCL-collective waits timed by runtime/waitprobe.py), MAX-reduced.  A gang
+tenant then gets aligned windows only while its worst rank waits on peers
+(EWMA >= ``wait_on_frac`` of the epoch) and is scheduled locally otherwise --
+gang scheduling driven by the lock-holder-preemption symptom P2 measures.
+
 Every epoch has a deadline (``deadline_ms``).  A rank that misses it -- one
 rank hung (GPBS_FAULT ``rank_hang``), descheduled or dead -- makes the others'
 exchange time out: they record GANG_TIMEOUT (trace + perfc ``gang_timeout``),
@@ -60,6 +67,8 @@ from typing import Callable, Dict, List, Optional
 
 import torch
 import torch.distributed as dist
+
+from ..utils import roctx
 
 FAVOUR, EXCLUDE, NONE = 1, 2, 0
 NO_ATC = 1 << 30  # MIN-neutral stand-in for "no ATC pool on this rank"
@@ -139,7 +148,8 @@ class GangCoordinator:
                  slack_ms: float = 1.0, atc_pool: Optional[int] = None,
                  metric_tenants: Optional[List[int]] = None, metric_every: int = 5,
                  transport: str = "dist", shm_name: Optional[str] = None, rank: Optional[int] = None,
-                 world: Optional[int] = None, deadline_ms: float = 200.0):
+                 world: Optional[int] = None, deadline_ms: float = 200.0, wait_driven: bool = False,
+                 wait_on_frac: float = 0.02, wait_hold_epochs: int = 64):
         self.engine = engine
         self.group = group
         self.tenants = list(tenants)
@@ -169,6 +179,16 @@ class GangCoordinator:
         self.deadline_ns = int(deadline_ms * 1e6)
         self.timeouts = 0
         self.degraded = False
+        # K10 -> gang decision: a gang tenant gets aligned windows only while
+        # its ranks report waiting on peers (wait reports: runtime/waitprobe.py)
+        self.wait_driven = bool(wait_driven)
+        self.wait_on_frac = float(wait_on_frac)
+        self.wait_hold = int(wait_hold_epochs)
+        self.gang_on: Dict[int, bool] = {t: not self.wait_driven for t in self.tenants}
+        self._on_since: Dict[int, int] = {t: 0 for t in self.tenants}
+        self.wait_ewma_us: Dict[int, int] = {t: 0 for t in self.tenants}
+        self._wait_prev: Dict[int, int] = {}
+        self.gang_switches = 0
 
     # ------------------------------------------------------------ demand
     def _engine_demand(self, t: int) -> bool:
@@ -184,9 +204,35 @@ class GangCoordinator:
         return False
 
     # ----------------------------------------------------------- decision
+    def _local_wait_us(self, t: int) -> int:
+        """Wait (us) this GPU's tenant reported since the previous epoch."""
+        try:
+            cur = int(self.engine.tenant_info(t).spin_latency)
+        except Exception:
+            return 0
+        prev = self._wait_prev.get(t, cur)
+        self._wait_prev[t] = cur
+        return max(0, cur - prev) // 1000
+
+    def update_gang_on(self, epoch: int, max_wait_us: List[int]):
+        """Wait-driven gang switch, a pure function of the reduced vector and
+        its own history (identical on every rank): on when the EWMA of the
+        worst rank's per-epoch wait reaches ``wait_on_frac`` of the epoch; off
+        after ``wait_hold`` epochs on if it fell below a quarter of that."""
+        on_us = self.wait_on_frac * self.epoch_ns / 1e3
+        for t, w in zip(self.tenants, max_wait_us):
+            ew = (3 * self.wait_ewma_us[t] + int(w)) // 4
+            self.wait_ewma_us[t] = ew
+            if not self.gang_on[t] and ew >= on_us:
+                self.gang_on[t], self._on_since[t] = True, epoch
+                self.gang_switches += 1
+            elif self.gang_on[t] and epoch - self._on_since[t] >= self.wait_hold and ew < on_us / 4:
+                self.gang_on[t] = False
+                self.gang_switches += 1
+
     def decide(self, epoch: int, demand_all: List[int]) -> Dict[int, int]:
         """Pure function of (epoch, all-rank demand): identical on every rank."""
-        eligible = [t for t, d in zip(self.tenants, demand_all) if d]
+        eligible = [t for t, d in zip(self.tenants, demand_all) if d and self.gang_on.get(t, True)]
         out = {t: NONE for t in self.tenants}
         if not eligible:
             return out
@@ -219,7 +265,8 @@ class GangCoordinator:
     def _loop(self):
         tr = None
         try:
-            tr = self._make_transport(len(self.tenants) + 4)
+            nt = len(self.tenants)
+            tr = self._make_transport(2 * nt + 4)
             t_prev = 0
             while True:
                 hang = self.engine.fault_fire("rank_hang") if self.engine is not None else -1
@@ -227,8 +274,10 @@ class GangCoordinator:
                     time.sleep(max(hang, 1) / 1e3)
                 t0 = time.monotonic_ns()
                 vec = [1 if self.demand(t) else 0 for t in self.tenants]
+                vec += [-self._local_wait_us(t) for t in self.tenants]  # MIN of -w = -(max over ranks)
                 vec += [self._atc_local(), 0 if self._want_stop else 1, t_prev, -t_prev]
-                red = tr.reduce_min(vec, t0 + self.deadline_ns)
+                with roctx.range(f"gpbs:gang_epoch {self.epoch}"):
+                    red = tr.reduce_min(vec, t0 + self.deadline_ns)
                 t1 = time.monotonic_ns()
                 if red is None:
                     self._timeout(t1 - t0)
@@ -249,7 +298,9 @@ class GangCoordinator:
                     if not self._sync_metrics(tr):
                         self._timeout(time.monotonic_ns() - t1)
                         break
-                dec = self.decide(self.epoch, red[:len(self.tenants)])
+                if self.wait_driven:
+                    self.update_gang_on(self.epoch, [-x for x in red[nt:2 * nt]])
+                dec = self.decide(self.epoch, red[:nt])
                 until = self.engine.now() + self.epoch_ns + self.slack_ns
                 for t, st in dec.items():
                     self.engine.gang_set(t, st, until)
@@ -322,4 +373,7 @@ class GangCoordinator:
                 "sync_p99_us": lat[min(len(lat) - 1, int(0.99 * len(lat)))] / 1e3, "sync_max_us": lat[-1] / 1e3,
                 "skew_p50_us": skew[len(skew) // 2] / 1e3, "skew_max_us": skew[-1] / 1e3,
                 "timeouts": self.timeouts, "degraded": self.degraded,
-                "atc_global_us": self.atc_global_us, "metric_syncs": self.metric_syncs}
+                "atc_global_us": self.atc_global_us, "metric_syncs": self.metric_syncs,
+                "wait_driven": self.wait_driven, "gang_on": {str(t): v for t, v in self.gang_on.items()},
+                "wait_ewma_us": {str(t): v for t, v in self.wait_ewma_us.items()},
+                "gang_switches": self.gang_switches}

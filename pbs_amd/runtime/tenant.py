@@ -17,7 +17,8 @@ plane:
   third-party kernels (torch / hipBLASLt / RCCL) that cannot gate themselves
   through the partition table like the gpbs tenant kernels do;
 * ``report_wait`` / ``report_hold`` / ``report_requests`` feed the spin-latency
-  channel, ``account`` publishes modeled counters (vPMU mirror), ``busy`` /
+  channel; ``wait_probe()`` produces the waits from timed RCCL collectives and
+  stream/event syncs (K10, runtime/waitprobe.py), ``account`` publishes modeled counters (vPMU mirror), ``busy`` /
   ``idle`` set the has-work flag that wakes or blocks the tenant's slots.
 
     with TenantClient("llm-infer", slots=8) as t:
@@ -170,6 +171,12 @@ class TenantClient:
 
     def report_wait(self, ns: int, gpu: Optional[int] = None):
         return self.lib.gpbs_ctl_report(self.ctl, self.page, int(ns), REPORT_WAIT, self.gpu if gpu is None else gpu)
+
+    def wait_probe(self, min_report_ns: int = 2000):
+        """K10 producer bound to this tenant's report ring: time RCCL
+        collectives and stream/event syncs, post the waits (waitprobe.py)."""
+        from .waitprobe import WaitProbe
+        return WaitProbe(self.report_wait, min_report_ns=min_report_ns)
 
     def report_hold(self, ns: int):
         return self.lib.gpbs_ctl_report(self.ctl, self.page, int(ns), REPORT_HOLD, self.gpu)

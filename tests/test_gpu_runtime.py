@@ -20,7 +20,39 @@ def _engine(sched="credit", **kw):
     return e
 
 
-def test_runners_complete_under_gpbs_and_share_by_weight():
+def test_backlogged_tenants_share_by_weight():
+    """Weight 512 vs 256, both backlogged on all 8 partitions: the credit
+    scheduler gives the heavier tenant ~2x the partition time (csched_acct
+    fair share, X:xen/common/sched_credit.c:1302-1519)."""
+    e = _engine()
+    e.sched_params_set(0, 1000, 100)
+    a = e.tenant_create("gemm", nslots=8)
+    b = e.tenant_create("hbm", nslots=8, weight=512)
+    ctx = GpuContext(0, e)
+    e.start()
+    ra = Runner(ctx, "gemm", a, M=2048, N=2048, K=2048)
+    rb = Runner(ctx, "stream", b, bytes=64 << 20)
+    ra.submit(1 << 20)
+    rb.submit(1 << 20)
+    time.sleep(0.3)
+    a0, b0 = e.tenant_info(a).run_ns, e.tenant_info(b).run_ns
+    time.sleep(1.0)
+    a1, b1 = e.tenant_info(a).run_ns, e.tenant_info(b).run_ns
+    ra.cancel()
+    rb.cancel()
+    ra.wait(60)
+    rb.wait(60)
+    e.stop()
+    ratio = (b1 - b0) / max(1, a1 - a0)
+    assert 1.6 <= ratio <= 2.5, ratio
+    assert ra.stats().units_done > 0 and rb.stats().units_done > 0
+    for r in (ra, rb):
+        r.close()
+    ctx.close()
+    e.close()
+
+
+def test_runners_complete_under_gpbs():
     e = _engine()
     a = e.tenant_create("gemm", nslots=8)
     b = e.tenant_create("hbm", nslots=8, weight=512)

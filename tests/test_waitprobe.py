@@ -1,0 +1,143 @@
+"""K10 / P2 wait-latency producer (runtime/waitprobe.py): timed collectives
+and syncs feed REPORT_WAIT; ATC shrinks the slice when a collective tenant's
+peer is descheduled (X:xen/common/sched_credit_atc.c:210-229,291-460, fed as
+L:arch/x86/include/asm/spinlock.h:55-80 feeds vcrd_op); the gang coordinator
+turns aligned windows on from the same signal."""
+import multiprocessing as mp
+import os
+import socket
+import time
+
+import pytest
+
+from pbs_amd.core import oracle as O
+from pbs_amd.core.engine import Engine
+from pbs_amd.parallel._wait_selftest import gang_wait_worker, wait_worker
+from pbs_amd.parallel.gang import EXCLUDE, FAVOUR, NONE, GangCoordinator
+from pbs_amd.runtime.waitprobe import WaitProbe, engine_sink
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class _Work:
+    def wait(self):
+        return True
+
+
+def _fake_op(delays):
+    it = iter(delays)
+
+    def op(tensor, async_op=False):
+        time.sleep(next(it) / 1e3)
+        return _Work()
+    op.__name__ = "all_reduce"
+    return op
+
+
+def test_baseline_excess_reports_only_the_extra_wait():
+    got = []
+    p = WaitProbe(got.append, min_report_ns=500_000)
+    op = _fake_op([2, 2, 2, 7, 2])
+    for _ in range(5):
+        p.collective(op, None)
+    assert len(got) == 1 and 4e6 <= got[0] <= 7e6, got  # only the 5 ms late one
+    assert p.stats()["timed"] == 5
+
+
+def test_sync_waits_are_reported_whole():
+    got = []
+    p = WaitProbe(got.append, min_report_ns=1000)
+
+    class S:
+        def synchronize(self):
+            time.sleep(0.003)
+    p.sync(S())
+    assert len(got) == 1 and got[0] >= 3e6
+
+
+def test_atc_wait_unit_matches_oracle():
+    """wait_unit_ns converts ns reports to the reference's spin iterations."""
+    op = O.AtcParams(wait_unit_ns=8)
+    e = Engine(sched="atc", sim_clock=True, partitions=[(0, 0)], atc={"wait_unit_ns": 8})
+    e.tenant_create("Domain-0", nslots=1)
+    t = e.tenant_create("t", nslots=1)
+    e.wake(t)
+    st = O.AtcState.initial(op)
+    now = 0
+    for w in (3_000_000, 3_000_000, 40_000, 9_000, 100):
+        e.report_wait(t, w)
+        O.atc_report(st, op, w)
+        now += op.apply_period_us * 1000
+        e.advance(now)
+        assert e.tenant_info(t).tslice_us == O.atc_apply([st], op)
+
+
+def _run(world, target, args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = {}
+    for _ in ps:
+        r = q.get(timeout=120)
+        out[r["rank"]] = r
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return out
+
+
+@pytest.mark.parametrize("lag_ms", [0.0, 3.0])
+def test_descheduled_peer_produces_waits_and_atc_shrinks(lag_ms):
+    out = _run(2, wait_worker, (lag_ms, f"gpbs-arr-{os.getpid()}-{int(lag_ms)}"))
+    r0, r1 = out[0], out[1]
+    if lag_ms:
+        # rank 0 waits ~lag at every collective; the late rank does not
+        assert r0["stats"]["reports"] >= 20, r0
+        assert r0["stats"]["wait_ns_total"] >= 20 * 0.7 * lag_ms * 1e6, r0
+        assert r1["stats"]["wait_ns_total"] < 0.2 * r0["stats"]["wait_ns_total"], r1
+        assert r0["spin_latency"] >= 20 * 0.7 * lag_ms * 1e6
+        # ATC: 3 ms waits (bucket 16) drive the slice to its 300 us floor
+        assert r0["tslice"] == 300 and min(r0["traj"]) == 300, r0["traj"]
+        assert r1["tslice"] > 300, r1["traj"]
+    else:
+        # only the natural arrival skew of two CPU processes (tens of us)
+        for r in (r0, r1):
+            assert r["stats"]["wait_ns_total"] < 0.3 * 24 * 3e6, r["stats"]
+
+
+def test_gang_windows_follow_wait_reports():
+    out = _run(2, gang_wait_worker, (f"gpbs-gwait-{os.getpid()}",))
+    h0 = dict(out[0]["history"])
+    h1 = dict(out[1]["history"])
+    common = sorted(set(h0) & set(h1))
+    assert len(common) > 50
+    assert all(h0[k] == h1[k] for k in common)  # identical decisions on every rank
+    states = [list(h0[k].values())[0] for k in common]
+    assert states[0] == NONE  # no waits yet: local scheduling
+    on = [i for i, s in enumerate(states) if s in (FAVOUR, EXCLUDE)]
+    assert on, states
+    # switched on by rank 1's reports, and back off after the hold once they stopped
+    assert states[-1] == NONE, states[-20:]
+    for r in out.values():
+        assert r["stats"]["gang_switches"] >= 2, r["stats"]
+
+
+def test_gang_on_is_a_pure_function_of_the_reduced_waits():
+    g = GangCoordinator(None, None, [5], epoch_ms=4.0, wait_driven=True, wait_on_frac=0.05, wait_hold_epochs=3)
+    assert g.decide(0, [1]) == {5: NONE}
+    for ep in range(4):
+        g.update_gang_on(ep, [2000])  # 2 ms of a 4 ms epoch
+    assert g.gang_on[5]
+    assert g.decide(8, [1])[5] in (FAVOUR, EXCLUDE)
+    for ep in range(4, 20):
+        g.update_gang_on(ep, [0])
+    assert not g.gang_on[5] and g.gang_switches == 2
