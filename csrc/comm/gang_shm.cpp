@@ -107,7 +107,13 @@ int gpbs_gang_shm_allgather(void* h, uint64_t epoch, const int64_t* in, int64_t*
     RankSlot& o = g->r->ranks[k];
     int spins = 0;
     while (o.seq.load(std::memory_order_acquire) < epoch) {
-      if (++spins < 256) {
+      // the peers normally arrive within microseconds: busy-poll first
+      // (PAUSE), then yield, then sleep until the deadline
+      if (++spins < 4096) {
+        __builtin_ia32_pause();
+        continue;
+      }
+      if (spins < 4096 + 256) {
         std::this_thread::yield();
         continue;
       }

@@ -48,6 +48,7 @@ int gpbs_hip_gemv_bf16(const void*, const void*, void*, int, int, void*, const v
 int gpbs_hip_partition_switch(void*, unsigned, const unsigned*, hipStream_t);
 int gpbs_hip_counter_reduce(void*, void*, const int*, int, void*, hipStream_t);
 int gpbs_hip_adapt(void*, const void*, const void*, const void*, int, const gpbs_adapt_params_t*, int*, hipStream_t);
+int gpbs_hip_switch_probe(const void*, int, unsigned*, int, unsigned, unsigned long long, hipStream_t);
 }
 
 namespace {
@@ -839,6 +840,14 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
     c->pending[x] = kNoOwner;
   }
   hipMemcpy(c->d_table, c->h_table, sizeof(PartTable), hipMemcpyHostToDevice);
+  // Warm the scheduler kernels once: the first launch of a kernel loads its
+  // code object (~3 ms), which must not land inside the first metric tick or
+  // table publish under the engine lock (seen as the 3 ms tails of the
+  // gpbs:metric_tick / gpbs:publish roctx ranges).
+  c->h_ids[0] = -1;
+  gpbs_hip_partition_switch(c->d_table, 0, c->pending, c->sched_stream);
+  gpbs_hip_counter_reduce(c->d_cnt, c->d_prev, c->h_ids, 1, c->h_out, c->sched_stream);
+  hipStreamSynchronize(c->sched_stream);
   return c;
 }
 
@@ -1124,6 +1133,73 @@ int gpbs_gpu_stats(void* p, uint64_t* out4) {
 // CU-masked stream for foreign kernels (torch/hipBLASLt/RCCL tenants): a
 // stream whose hardware queue only dispatches to the CUs in `cu_mask`
 // (nwords x 32 bits, hipExtStreamCreateWithCUMask).
+// End-to-end actuation latency (perf-regression microbench): the time from
+// the scheduler's publish of a new assignment to EVERY workgroup of a probe
+// grid (nwg one-wave workgroups spread over all XCDs / shader engines)
+// having observed the new epoch, per iteration, in out_ns[iters].  Uses the
+// context's own table in its current mode (host: one release store;
+// device: + the k_partition_switch launch on the scheduler stream).  Only
+// on a context with no engine attached.  Returns iterations measured or <0.
+int gpbs_gpu_switch_latency(void* p, int iters, int nwg, int64_t* out_ns) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (c->engine || iters <= 0 || nwg <= 0 || nwg > 4096) return -22;
+  hipSetDevice(c->device);
+  constexpr u32 kStop = 0xFFFFFFF0u;
+  u32* acks = nullptr;
+  if (hipHostMalloc((void**)&acks, sizeof(u32) * nwg, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
+    return -12;
+  for (int i = 0; i < nwg; ++i) __atomic_store_n(&acks[i], 0xFFFFFFFEu, __ATOMIC_RELAXED);
+  hipStream_t ps = nullptr;
+  hipStreamCreateWithFlags(&ps, hipStreamNonBlocking);
+  const int dev = c->table_mode == 1;
+  const void* tab = dev ? (const void*)c->d_table : (const void*)c->h_table;
+  // every wave exits after 20 s of device wall clock even if the host died
+  int rc = gpbs_hip_switch_probe(tab, dev, acks, nwg, kStop, 20ull * 100000000ull, ps);
+  // e == 0xFFFFFFFE: every wave has acknowledged some epoch (grid resident)
+  auto all_acked = [&](u32 e, int64_t timeout_ns) {
+    const int64_t t_end = mono_ns() + timeout_ns;
+    for (;;) {
+      bool ok = true;
+      for (int i = 0; i < nwg && ok; ++i) {
+        const u32 a = __atomic_load_n(&acks[i], __ATOMIC_ACQUIRE);
+        ok = e == 0xFFFFFFFEu ? a != e : a == e;
+      }
+      if (ok) return true;
+      if (mono_ns() > t_end) return false;
+    }
+  };
+  int done = 0;
+  if (rc == 0 && all_acked(0xFFFFFFFEu, 2000000000LL)) {
+    for (int it = 0; it < iters; ++it) {
+      for (int x = 0; x < kXcds * kCtx; ++x) c->pending[x] = (u32)((it + x) & 1);
+      const int64_t t0 = mono_ns();
+      publish(c);
+      const u32 e = c->epoch;
+      if (!all_acked(e, 100000000LL)) {
+        rc = -110;
+        break;
+      }
+      out_ns[it] = mono_ns() - t0;
+      done++;
+    }
+  } else if (rc == 0) {
+    rc = -110;  // the probe grid never became resident
+  }
+  // stop epoch, then drain the probe grid (bounded by its own wall-clock exit)
+  __atomic_store_n(&c->h_table->epoch, kStop, __ATOMIC_RELEASE);
+  if (dev) gpbs_hip_partition_switch(c->d_table, kStop, c->pending, c->sched_stream);
+  const int64_t t_end = mono_ns() + 25000000000LL;
+  while (hipStreamQuery(ps) == hipErrorNotReady && mono_ns() < t_end)
+    std::this_thread::sleep_for(std::chrono::microseconds(100));
+  hipStreamSynchronize(ps);
+  __atomic_store_n(&c->h_table->epoch, c->epoch, __ATOMIC_RELEASE);
+  if (dev) gpbs_hip_partition_switch(c->d_table, c->epoch, c->pending, c->sched_stream);
+  hipStreamSynchronize(c->sched_stream);
+  hipStreamDestroy(ps);
+  hipHostFree(acks);
+  return rc < 0 ? rc : done;
+}
+
 // roctx helpers for the Python side (gang epochs, bench policy windows).
 int gpbs_roctx_push(const char* m) { return roctxRangePushA(m); }
 int gpbs_roctx_pop(void) { return roctxRangePop(); }

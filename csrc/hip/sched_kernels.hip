@@ -73,6 +73,39 @@ using namespace gpbs_hip;
 
 extern "C" {
 
+// Switch-latency probe (perf-regression microbench, the analog of the perfctr
+// init-time tests L:drivers/perfctr/x86_tests.c:181-245): one wave per
+// workgroup polls the partition table's epoch exactly like a tenant
+// workgroup polls its owner word (system scope: pinned host table; agent
+// scope: device copy) and acknowledges every new epoch it sees into its own
+// word of a pinned host array.  The host times "decision -> every workgroup
+// observed it".  Every wave leaves at the stop epoch or after max_ticks of
+// the 100 MHz wall clock, so the grid always drains.
+__global__ __launch_bounds__(64) void k_switch_probe(const PartTable* t, u32 devtable, u32* acks, u32 stop,
+                                                     u64 max_ticks) {
+  if (threadIdx.x != 0) return;
+  const u64 t0 = wall_clock64();
+  u32 last = 0xFFFFFFFEu;
+  for (;;) {
+    const u32 e = devtable ? __hip_atomic_load(&t->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                           : __hip_atomic_load(&t->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (e != last) {
+      last = e;
+      __hip_atomic_store(&acks[blockIdx.x], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (e == stop || wall_clock64() - t0 > max_ticks) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+int gpbs_hip_switch_probe(const void* table, int devtable, unsigned* acks, int nwg, unsigned stop,
+                          unsigned long long max_ticks, hipStream_t s) {
+  if (nwg <= 0 || nwg > 65536) return -22;
+  hipLaunchKernelGGL(k_switch_probe, dim3(nwg), dim3(64), 0, s, (const PartTable*)table, (u32)devtable, acks, stop,
+                     (u64)max_ticks);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 int gpbs_hip_partition_switch(void* table, unsigned epoch, const unsigned* owners, hipStream_t s) {
   Owners ow;
   for (int i = 0; i < kXcds * kCtx; ++i) ow.o[i] = owners[i];

@@ -34,6 +34,7 @@ def bind(lib):
     _p(lib, "gpbs_roctx_push", C.c_int, C.c_char_p)
     _p(lib, "gpbs_roctx_pop", C.c_int)
     _p(lib, "gpbs_roctx_mark", None, C.c_char_p)
+    _p(lib, "gpbs_gpu_switch_latency", C.c_int, vp, C.c_int, C.c_int, vp)
     # raw kernels
     _p(lib, "gpbs_hip_gemm_bf16", C.c_int, vp, vp, vp, C.c_int, C.c_int, C.c_int, vp, vp, C.c_uint, C.c_uint, vp, vp,
        C.c_int, vp)

@@ -174,6 +174,16 @@ class GpuContext:
         self.L.gpbs_gpu_ownership(self.h, tenant, out, int(clear))
         return [x / 1e9 for x in out]
 
+    def switch_latency(self, iters: int = 200, nwg: int = 1024) -> List[int]:
+        """End-to-end actuation latency in ns per iteration: publish of a new
+        assignment -> every workgroup of an nwg-workgroup probe grid observed
+        it (the context's table mode; no engine may be attached)."""
+        out = (C.c_int64 * iters)()
+        n = self.L.gpbs_gpu_switch_latency(self.h, iters, nwg, out)
+        if n < 0:
+            raise RuntimeError(f"switch_latency failed ({n})")
+        return list(out[:n])
+
     def stats(self):
         out = (C.c_uint64 * 4)()
         self.L.gpbs_gpu_stats(self.h, out)

@@ -112,8 +112,9 @@ class ArrivalBoard:
         try:
             del self.a
             self.shm.close()
-            if self.owner:
-                self.shm.unlink()
+            if self.owner:  # not shm.unlink(): that also unregisters from the tracker
+                import _posixshmem
+                _posixshmem.shm_unlink(self.shm._name)
         except Exception:
             pass
 

@@ -26,6 +26,16 @@ for step in "$@"; do
     smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bquick)  run bquick 600 python bench.py --steps 10 --warmup 2 --reps 2 --out gpurun_out/bquick.json ;;
     bench)   run bench 900 python bench.py --steps 20 --warmup 5 --out gpurun_out/bench.json ;;
+    rehearse) run rehearse 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+                --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 1 --reps 1 --rehearse --policies none,gpbs \
+                --out gpurun_out/rehearse.json ;;
+    roctx)   export GPBS_ROCTX=1
+             run roctx 600 rocprofv3 --kernel-trace --marker-trace --stats --output-format csv -d gpurun_out/roctx \
+                -o run -- python bench.py --steps 5 --warmup 1 --reps 1 --policies gpbs --counters model \
+                --out gpurun_out/roctx_bench.json
+             unset GPBS_ROCTX ;;
+    micro)   run micro 600 python -u scripts/microbench.py --out gpurun_out/microbench.json ;;
+    tmicro)  run tmicro 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_microbench.py ;;
     *) echo "unknown step $step" | tee -a "$LOG" ;;
   esac
 done

@@ -1,0 +1,208 @@
+#!/usr/bin/env python3
+"""Scheduler-path micro-benchmarks with regression thresholds -- the analog of
+the perfctr init-time tests (L:drivers/perfctr/x86_tests.c:181-245, which time
+rdpmc / rdmsr / wrmsr / rdtsc at boot and print the cost).
+
+    python scripts/microbench.py [--only gang,switch,hwc] [--out FILE]
+
+* gang    gang-epoch barrier latency: the native shared-memory all-gather
+          (csrc/comm/gang_shm.cpp) back to back among W node-local processes,
+          W = 2 / 4 / 8, and a gloo all-reduce of the same vector for scale
+          (CPU only).
+* switch  end-to-end actuation latency on the GPU: scheduler publish of a new
+          assignment -> every workgroup of a 1024-workgroup probe grid has
+          observed the new epoch (GpuContext.switch_latency), for the pinned
+          host table and the device table (+ k_partition_switch launch).
+* hwc     counter-read latency: one synchronous rocprofiler-sdk device-counting
+          sample of the PBS counter set (subprocess: the sampler registers
+          before HIP initialises).
+
+Each section prints p50 / p99 / max in microseconds; THRESHOLDS below are the
+regression gates tests/test_microbench.py enforces (about 3x the committed
+measurements in profiles/micro/microbench_r2.json).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import multiprocessing as mp
+import os
+import socket
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+# regression gates, microseconds (p99 unless noted)
+THRESHOLDS = {
+    "gang_shm_w4_p99_us": 500.0,
+    "gang_shm_w4_p50_us": 60.0,
+    "switch_host_p99_us": 1200.0,   # 1024 pollers of a pinned host word over PCIe: ~340 us p50 measured
+    "switch_device_p99_us": 60.0,   # device table + k_partition_switch: ~16 us p50 measured
+    "hwc_sample_p50_us": 1200.0,    # synchronous device-counting sample: ~410 us measured
+}
+
+
+def pct(xs, q):
+    xs = sorted(xs)
+    if not xs:
+        return 0.0
+    return xs[min(len(xs) - 1, int(q * (len(xs) - 1) + 0.5))]
+
+
+def summ_us(ns):
+    return {"n": len(ns), "p50_us": round(pct(ns, 0.5) / 1e3, 2), "p99_us": round(pct(ns, 0.99) / 1e3, 2),
+            "max_us": round(max(ns) / 1e3, 2) if ns else 0.0}
+
+
+# ---------------------------------------------------------------- gang
+def _gang_worker(rank, world, name, iters, q):
+    from pbs_amd.parallel.gang import _ShmTransport
+    tr = _ShmTransport(name, rank, world, 16)
+    lat = []
+    vals = list(range(8))
+    for i in range(iters):
+        t0 = time.monotonic_ns()
+        r = tr.reduce_min(vals, t0 + 2_000_000_000)
+        if r is None:
+            raise RuntimeError("gang shm timeout")
+        lat.append(time.monotonic_ns() - t0)
+    tr.close()
+    q.put((rank, lat[iters // 10:]))  # drop warm-up
+
+
+def _gloo_worker(rank, world, port, iters, q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    buf = torch.zeros(8, dtype=torch.int64)
+    lat = []
+    for _ in range(iters):
+        t0 = time.monotonic_ns()
+        dist.all_reduce(buf, op=dist.ReduceOp.MIN)
+        lat.append(time.monotonic_ns() - t0)
+    dist.destroy_process_group()
+    q.put((rank, lat[iters // 10:]))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _spawn(target, world, args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=target, args=(r, world) + args + (q,)) for r in range(world)]
+    for p in ps:
+        p.start()
+    lat = []
+    for _ in ps:
+        _, xs = q.get(timeout=300)
+        lat += xs
+    for p in ps:
+        p.join(timeout=60)
+        if p.exitcode:
+            raise RuntimeError(f"worker exit {p.exitcode}")
+    return lat
+
+
+def bench_gang(worlds=(2, 4, 8), iters=3000, gloo=True):
+    out = {}
+    for w in worlds:
+        name = f"gpbs-mb-{os.getpid()}-{w}"
+        out[f"shm_w{w}"] = summ_us(_spawn(_gang_worker, w, (name, iters)))
+        if gloo:
+            out[f"gloo_w{w}"] = summ_us(_spawn(_gloo_worker, w, (_port(), iters // 3)))
+    return out
+
+
+# -------------------------------------------------------------- switch
+def bench_switch(iters=300, nwg=1024):
+    from pbs_amd.runtime.gpu import GpuContext
+    out = {}
+    for mode in ("host", "device"):
+        ctx = GpuContext(0, table_mode=mode)
+        ctx.switch_latency(20, nwg)  # warm-up
+        out[mode] = summ_us(ctx.switch_latency(iters, nwg))
+        out[mode]["nwg"] = nwg
+        ctx.close()
+    return out
+
+
+# ----------------------------------------------------------------- hwc
+HWC_CODE = r"""
+import json, sys, time
+sys.path.insert(0, %r)
+from pbs_amd.counters import hwc
+assert hwc.init(gpu=0)
+import torch
+torch.cuda.set_device(0)
+torch.zeros(1, device="cuda")
+assert hwc.start()
+lat = []
+for i in range(%d):
+    t0 = time.monotonic_ns()
+    hwc.sample()
+    lat.append(time.monotonic_ns() - t0)
+print(json.dumps(lat[10:]))
+"""
+
+
+def bench_hwc(iters=200):
+    r = subprocess.run([sys.executable, "-c", HWC_CODE % (ROOT, iters)], capture_output=True, text=True, timeout=300)
+    if r.returncode:
+        raise RuntimeError(r.stderr[-2000:])
+    return {"sample": summ_us(json.loads(r.stdout.strip().splitlines()[-1]))}
+
+
+def gates(res):
+    """Flatten the measurements the thresholds name; returns {gate: (value, limit, ok)}."""
+    vals = {}
+    g = res.get("gang", {})
+    if "shm_w4" in g:
+        vals["gang_shm_w4_p99_us"] = g["shm_w4"]["p99_us"]
+        vals["gang_shm_w4_p50_us"] = g["shm_w4"]["p50_us"]
+    s = res.get("switch", {})
+    if "host" in s:
+        vals["switch_host_p99_us"] = s["host"]["p99_us"]
+    if "device" in s:
+        vals["switch_device_p99_us"] = s["device"]["p99_us"]
+    h = res.get("hwc", {})
+    if "sample" in h:
+        vals["hwc_sample_p50_us"] = h["sample"]["p50_us"]
+    return {k: (v, THRESHOLDS[k], v <= THRESHOLDS[k]) for k, v in vals.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="gang,switch,hwc")
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    res = {}
+    for sec in a.only.split(","):
+        t0 = time.time()
+        if sec == "gang":
+            res["gang"] = bench_gang()
+        elif sec == "switch":
+            res["switch"] = bench_switch()
+        elif sec == "hwc":
+            res["hwc"] = bench_hwc()
+        print(f"[microbench] {sec}: {json.dumps(res.get(sec))} ({time.time() - t0:.1f}s)", flush=True)
+    res["gates"] = {k: {"value": v, "limit": lim, "ok": ok} for k, (v, lim, ok) in gates(res).items()}
+    print(json.dumps(res["gates"]), flush=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+    return 0 if all(g["ok"] for g in res["gates"].values()) else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
