@@ -58,35 +58,8 @@ def summ_us(ns):
 
 
 # ---------------------------------------------------------------- gang
-def _gang_worker(rank, world, name, iters, q):
-    from pbs_amd.parallel.gang import _ShmTransport
-    tr = _ShmTransport(name, rank, world, 16)
-    lat = []
-    vals = list(range(8))
-    for i in range(iters):
-        t0 = time.monotonic_ns()
-        r = tr.reduce_min(vals, t0 + 2_000_000_000)
-        if r is None:
-            raise RuntimeError("gang shm timeout")
-        lat.append(time.monotonic_ns() - t0)
-    tr.close()
-    q.put((rank, lat[iters // 10:]))  # drop warm-up
-
-
-def _gloo_worker(rank, world, port, iters, q):
-    import torch
-    import torch.distributed as dist
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    buf = torch.zeros(8, dtype=torch.int64)
-    lat = []
-    for _ in range(iters):
-        t0 = time.monotonic_ns()
-        dist.all_reduce(buf, op=dist.ReduceOp.MIN)
-        lat.append(time.monotonic_ns() - t0)
-    dist.destroy_process_group()
-    q.put((rank, lat[iters // 10:]))
+from pbs_amd.parallel._gang_selftest import gang_bench_worker as _gang_worker  # noqa: E402
+from pbs_amd.parallel._gang_selftest import gloo_bench_worker as _gloo_worker  # noqa: E402
 
 
 def _port():
