@@ -126,6 +126,7 @@ void gpbs_boot_defaults(gpbs_boot_params_t* p) {
   p->boost_exclusive = 0;
   p->class_split = 0;
   p->idle_skip = 0;  // reference semantics (Appendix A feeds every period)
+  p->class_dwell = 2;
   AdaptParams a;
   std::memcpy(&p->adapt, &a, sizeof(a));
   AtcParams t;

@@ -1174,7 +1174,14 @@ class CreditScheduler : public Scheduler {
   int classify(Tenant& t) override {
     CDom& d = sd(t);
     if (d.pmc[0] == 0) return -1;  // idle this period: keep the current class
-    return d.rate_ewma >= E.adapt_params.threshold ? 1 : 0;
+    // +-25 % band around the threshold: a tenant whose smoothed miss rate
+    // hovers near it (a decode step streaming weights next to its attention,
+    // a trainer's optimizer phase) keeps its class instead of flapping
+    // between the class homes (each flip drains and re-homes its slots).
+    const uint64_t thr = E.adapt_params.threshold;
+    if (t.cls == 1) return d.rate_ewma >= thr * 3 / 4 ? 1 : 0;
+    if (t.cls == 0) return d.rate_ewma >= thr * 5 / 4 ? 1 : 0;
+    return d.rate_ewma >= thr ? 1 : 0;
   }
 
   bool tenant_adapt(Tenant& d, AdaptState* out) override {

@@ -699,7 +699,7 @@ void Engine::classify_tick(int64_t n) {
     } else {
       t.cls_count++;
     }
-    if (t.cls_count < 2 || c == t.cls) {
+    if (t.cls_count < std::max(1, boot.class_dwell) || c == t.cls) {
       // Stolen across classes and no longer running: back to its class home.
       // Stacked on an XCD that hosts more of the tenant's slots than its home
       // XCD does (an in-class steal of a slot that waited behind a sibling):

@@ -75,6 +75,8 @@ typedef struct gpbs_boot_params {
                                   0/1 = context 0 only.  > 1 also makes each class one gang (SE-exclusive mode) */
   int32_t idle_skip;           /* 1 = PBS idle-sample rule (Q14): a tenant with no counted instructions in a metric
                                   period is not fed to the phase detector (curr = 0 would shrink its quantum) */
+  int32_t class_dwell;         /* class re-evaluations a new contention class must persist before a tenant is
+                                  re-homed (default 2); the classifier also has a +-25 % band around the threshold */
   gpbs_adapt_params_t adapt;
   gpbs_atc_params_t atc;
 } gpbs_boot_params_t;

@@ -37,7 +37,7 @@ def _tenant(kind: str, seconds: float, warmup: float, socket: Optional[str], q, 
     t = None
     if socket:
         from ..runtime.tenant import TenantClient
-        t = TenantClient(kind, socket, slots=8, weight=args.get(f"{kind}_weight", 256),
+        t = TenantClient(kind, socket, slots=args.get("slots", 8), weight=args.get(f"{kind}_weight", 256),
                          spatial=args.get("spatial", False), priority=args.get(f"{kind}_prio", 0))
     if kind == "infer":
         w = LlamaDecoder(PRESETS[args["infer_model"]], batch=args["infer_batch"], context=args["context"],
@@ -63,6 +63,11 @@ def _tenant(kind: str, seconds: float, warmup: float, socket: Optional[str], q, 
     prio_stream = None
     if t is None and args.get(f"{kind}_prio", 0):
         prio_stream = torch.cuda.Stream(priority=-abs(args[f"{kind}_prio"]))
+    ses = args.get(f"{kind}_ses")
+    if t is None and ses is not None:  # static shader-engine split (se:I/T policies)
+        from ..ops import kernels as K
+        from ..runtime.tenant import se_cu_words
+        prio_stream = torch.cuda.ExternalStream(K.cumask_stream(se_cu_words(ses)))
     torch.cuda.synchronize()
     start_evt.wait()
     lat = []
@@ -101,6 +106,26 @@ def _tenant(kind: str, seconds: float, warmup: float, socket: Optional[str], q, 
            "p99_ms": 1e3 * sorted(lat)[int(0.99 * (len(lat) - 1))] if lat else 0.0, "halves": halves})
 
 
+def parse_se_policy(policy: str):
+    """'se:I/T' -> (infer SEs, trainer SEs): the decode tenant on the top I
+    shader engines of every XCD, the trainer on the bottom T."""
+    i, t = (int(x) for x in policy.split(":", 1)[1].split("/"))
+    if not (1 <= i <= 4 and 1 <= t <= 4):
+        raise ValueError(policy)
+    return tuple(range(4 - i, 4)), tuple(range(t))
+
+
+_HWC = {"on": False}
+
+
+def _hwc_setup():
+    """Register the hardware-counter sampler in this (daemon) process before
+    anything initialises HIP here; tenants are separate processes."""
+    from ..counters import hwc
+    _HWC["on"] = hwc.init(gpu=0)
+    return _HWC["on"]
+
+
 def run(policy: str, kinds, args: dict, seconds: float, warmup: float) -> Dict[str, dict]:
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -108,6 +133,9 @@ def run(policy: str, kinds, args: dict, seconds: float, warmup: float) -> Dict[s
     daemon = None
     sock = None
     args = dict(args, spatial=policy == "gpbs-spatial")
+    base = policy.split("@")[0]
+    if base.startswith("se:"):  # static SE split; "se:I/T@solo" runs the given kinds alone on their masks
+        args["infer_ses"], args["train_ses"] = parse_se_policy(base)
     if policy.endswith("+prio"):
         args["infer_prio"] = 1
         policy = policy[:-5]
@@ -115,6 +143,17 @@ def run(policy: str, kinds, args: dict, seconds: float, warmup: float) -> Dict[s
         from ..runtime.daemon import Daemon
         sock = os.path.join(tempfile.mkdtemp(), "gpbsd.sock")
         daemon = Daemon(sock, gpus=[0], nctx=2, sim=False, profile="mi355x").start()
+    elif policy == "gpbs-se":
+        # SE-exclusive class split driven by LIVE hardware counters: the daemon
+        # owns the GPU actuator + rocprofiler-sdk sampler; the tenants' kernels
+        # run on streams masked to the shader engines they own, so the per-SE
+        # counters are attributed to them by ownership (no declared counters).
+        from ..runtime.daemon import Daemon
+        sock = os.path.join(tempfile.mkdtemp(), "gpbsd.sock")
+        daemon = Daemon(sock, gpus=[0], nctx=4, sim=False, profile="mi355x", attach_gpu=True, se_mode=True,
+                        hw_counters=_HWC["on"], overrides={"class_split": 2, "idle_skip": 1, "class_dwell": 8}).start()
+        args["slots"] = 16
+        args["spatial"] = True
     ps = [ctx.Process(target=_tenant, args=(k, seconds, warmup, sock, q, start, args)) for k in kinds]
     for p in ps:
         p.start()
@@ -130,6 +169,15 @@ def run(policy: str, kinds, args: dict, seconds: float, warmup: float) -> Dict[s
             p.join(timeout=120)
         if daemon is not None:
             e = daemon.engine
+            if daemon.gpu_ctx is not None and daemon.hw_counters:
+                hw = {}
+                for t in e.tenants():
+                    att, _ = daemon.gpu_ctx.hwc_tenant(t)
+                    if att[0]:
+                        hw[e.tenant_info(t).name] = {"inst": round(att[0]), "miss_rate": round(att[3] * 1e5 / att[0]),
+                                                     "cpi_x1000": round(att[1] * 1e3 / att[0])}
+                out["_hw"] = {"tenant": hw, "stats": daemon.gpu_ctx.hwc_stats(),
+                              "owned_s": {e.tenant_info(t).name: daemon.gpu_ctx.ownership(t) for t in e.tenants()}}
             out["_engine"] = {"z": e.debug_keys("z")[-3000:], "tenants": {
                 e.tenant_info(t).name: {"tslice_us": e.tenant_info(t).tslice_us, "phase": e.tenant_info(t).phase,
                                         "class": e.lib.gpbs_tenant_class(e.h, t), "run_ns": e.tenant_info(t).run_ns}
@@ -155,6 +203,7 @@ def main(argv=None):
     ap.add_argument("--train-seq", type=int, default=2048)
     ap.add_argument("--fp8", action="store_true", help="decode tenant streams e4m3fn weights (fp8 MFMA linears)")
     ap.add_argument("--graph", action="store_true", help="with --fp8: decode step replayed from a HIP graph")
+    ap.add_argument("--reps", type=int, default=1, help="repetitions of every co-run policy (median reported)")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     args = {"infer_model": a.infer_model, "train_model": a.train_model, "infer_batch": a.infer_batch,
@@ -162,29 +211,48 @@ def main(argv=None):
             "infer_weight": 512, "train_weight": 256, "fp8": a.fp8, "graph": a.graph and a.fp8}
     res = {}
     pols = [p for p in a.policies.split(",") if p]
+    if "gpbs-se" in pols:
+        _hwc_setup()
     if "solo" in pols:
         res["solo"] = {}
         for k in ("infer", "train"):
             res["solo"].update(run("solo", [k], args, a.seconds, a.warmup))
             print(f"[llm] solo {k}: {json.dumps(res['solo'][k])}", file=sys.stderr, flush=True)
-    for p in pols:
-        if p == "solo":
-            continue
-        res[p] = run(p, ["infer", "train"], args, a.seconds, a.warmup)
-        print(f"[llm] {p}: {json.dumps({k: v for k, v in res[p].items() if not k.startswith('_')})}",
-              file=sys.stderr, flush=True)
-    summary = {}
-    if "solo" in res:
-        for p, r in res.items():
+    reps = {p: [] for p in pols if p != "solo"}
+    for rep in range(max(1, a.reps)):
+        for p in pols:
             if p == "solo":
                 continue
-            norm = {k: r[k]["tokens_per_s"] / res["solo"][k]["tokens_per_s"] for k in ("infer", "train")
-                    if res["solo"][k]["tokens_per_s"]}
-            summary[p] = {"aggregate": round(sum(norm.values()), 4),
-                          "mean_slowdown_pct": round(statistics.mean((1 / v - 1) * 100 for v in norm.values()), 2),
-                          "norm": {k: round(v, 4) for k, v in norm.items()},
-                          "infer_p99_ms": round(r["infer"]["p99_ms"], 3),
-                          "infer_p50_ms": round(r["infer"]["p50_ms"], 3)}
+            if p.endswith("@solo"):  # each tenant alone on its SE mask
+                r = {}
+                for k in ("infer", "train"):
+                    r.update(run(p, [k], args, a.seconds, a.warmup))
+            else:
+                r = run(p, ["infer", "train"], args, a.seconds, a.warmup)
+            reps[p].append(r)
+            print(f"[llm] {p} rep {rep}: {json.dumps({k: v for k, v in r.items() if not k.startswith('_')})}",
+                  file=sys.stderr, flush=True)
+            if "_hw" in r:
+                print(f"[llm] {p} rep {rep} hw: {json.dumps(r['_hw'])}", file=sys.stderr, flush=True)
+    summary = {}
+    if "solo" in res:
+        for p, rs in reps.items():
+            runs = []
+            for r in rs:
+                norm = {k: r[k]["tokens_per_s"] / res["solo"][k]["tokens_per_s"] for k in ("infer", "train")
+                        if res["solo"][k]["tokens_per_s"]}
+                runs.append({"aggregate": round(sum(norm.values()), 4),
+                             "mean_slowdown_pct": round(statistics.mean((1 / v - 1) * 100 for v in norm.values()), 2),
+                             "norm": {k: round(v, 4) for k, v in norm.items()},
+                             "infer_p99_ms": round(r["infer"]["p99_ms"], 3),
+                             "infer_p50_ms": round(r["infer"]["p50_ms"], 3)})
+            med = lambda xs: round(statistics.median(xs), 4)
+            summary[p] = {"aggregate": med([x["aggregate"] for x in runs]),
+                          "mean_slowdown_pct": med([x["mean_slowdown_pct"] for x in runs]),
+                          "norm": {k: med([x["norm"][k] for x in runs]) for k in runs[0]["norm"]},
+                          "infer_p50_ms": med([x["infer_p50_ms"] for x in runs]),
+                          "infer_p99_ms": med([x["infer_p99_ms"] for x in runs]), "runs": runs}
+    res.update({p: rs for p, rs in reps.items()})
     line = {"config": "#5 Llama-3-8B decode + Llama-1B bf16 training, 1x MI355X", "data": "synthetic tokens, "
             "random-init weights", "dtype": "bf16" + (" (decode weights fp8 e4m3fn)" if a.fp8 else ""), "summary": summary, "raw": res}
     print(json.dumps(line))

@@ -37,11 +37,20 @@ class Daemon:
 
     def __init__(self, socket_path: str = DEFAULT_SOCKET, gpus=(0,), nctx: int = 2, sim: bool = False,
                  profile: str = "mi355x", config_path: Optional[str] = None, ctl_name: str = "gpbs",
-                 ctl_pages: int = 64, state_path: Optional[str] = None, attach_gpu: bool = False):
+                 ctl_pages: int = 64, state_path: Optional[str] = None, attach_gpu: bool = False,
+                 overrides: Optional[Dict[str, Any]] = None, se_mode: bool = False, hw_counters: bool = False):
         prof = cfgmod.MI355X_PROFILE if profile == "mi355x" else cfgmod.REFERENCE_PROFILE
         self.cfg = cfgmod.load(config_path, prof)
         kw = cfgmod.engine_kwargs(self.cfg)
+        kw.update(overrides or {})
         kw["sim_clock"] = int(sim)
+        # se_mode: the nctx(=4) partitions of an XCD are its shader engines,
+        # owned exclusively; torch tenants run on streams masked to the SEs
+        # they own, so the per-SE hardware counters (hw_counters; needs
+        # pbs_amd.counters.hwc.init() before HIP init and hwc.start()) are
+        # attributed to them by ownership -- measured, not declared.
+        self.se_mode = bool(se_mode)
+        self.hw_counters = bool(hw_counters)
         self.engine = Engine(**kw)
         self.gpus = list(gpus)
         self.nctx = nctx
@@ -83,6 +92,13 @@ class Daemon:
         from .gpu import GpuContext
         ctx = GpuContext(gpu, part_base=part_lo, nctx=self.nctx)
         ctx.attach_mux(self.engine, nctx=self.nctx)
+        if self.se_mode:
+            ctx.set_se_mode(True)
+        if self.hw_counters:
+            from ..counters import hwc
+            if not hwc.active():
+                hwc.start()  # after HIP init (the GpuContext above), once per process
+            ctx.set_hwc(True)
         return ctx
 
     def attach_backends(self, factory):
@@ -423,7 +439,7 @@ class Daemon:
             self.engine.heartbeat(t)
             if pid:
                 self.pids[t] = int(pid)
-            return {"tenant": t, "page": page, "ctl": self.ctl_name, "nctx": self.nctx,
+            return {"tenant": t, "page": page, "ctl": self.ctl_name, "nctx": self.nctx, "se_mode": self.se_mode,
                     "partitions": {f"{g}:{x}:{c}": p for (g, x, c), p in self.part_of.items()}}
 
     def unregister(self, name: str, destroy: bool = True):

@@ -59,6 +59,17 @@ def half_cu_words(owned: List[Tuple[int, int]]) -> List[int]:
     return words
 
 
+def se_cu_words(ses) -> List[int]:
+    """CU-mask words covering shader engines `ses` of every XCD (logical CU i
+    of an XCD on SE i % 4)."""
+    want = set(ses)
+    words = [0] * 8
+    for b in range(256):
+        if ((b // 8) % 4) in want:
+            words[b // 32] |= 1 << (b % 32)
+    return words
+
+
 class TenantClient:
     def __init__(self, name: str, socket_path: str = DEFAULT_SOCKET, slots: int = 8, weight: int = -1,
                  cap: int = -1, pool=None, gpu: int = 0, heartbeat_s: float = 0.05, spatial: bool = True,
@@ -72,6 +83,7 @@ class TenantClient:
         self.tenant: int = r["tenant"]
         self.page: int = r["page"]
         self.nctx: int = r.get("nctx", 2)
+        self.se_mode: bool = bool(r.get("se_mode", False))
         # partition id -> (gpu, xcd, ctx)
         self.part: Dict[int, Tuple[int, int, int]] = {}
         for k, pid in r["partitions"].items():
@@ -133,6 +145,13 @@ class TenantClient:
         parts = self.owned() if owned is None else owned
         if not parts:
             return torch.cuda.current_stream()
+        if self.se_mode:  # exclusive shader engines: mask = the owned SEs (union over XCDs)
+            ses = tuple(sorted({c for (_, c) in parts}))
+            s = self._streams.get(("se",) + ses)
+            if s is None:
+                s = torch.cuda.ExternalStream(K.cumask_stream(se_cu_words(ses), device=self.gpu))
+                self._streams[("se",) + ses] = s
+            return s
         halves = tuple(sorted({c for (_, c) in parts})) if self.spatial else (0, 1)
         s = self._streams.get(halves)
         if s is None and not self.spatial:

@@ -36,6 +36,9 @@ for step in "$@"; do
              unset GPBS_ROCTX ;;
     micro)   run micro 600 python -u scripts/microbench.py --out gpurun_out/microbench.json ;;
     tmicro)  run tmicro 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_microbench.py ;;
+    llmsplit) run llmsplit 1100 python -u -m pbs_amd.bench.llm_corun --fp8 --graph --seconds 5 --warmup 2 \
+                --policies "${LLM_POLICIES:-solo,none,se:1/3,se:2/2,se:1/3@solo,se:2/2@solo}" --reps "${LLM_REPS:-1}" \
+                --out gpurun_out/llm_split.json ;;
     *) echo "unknown step $step" | tee -a "$LOG" ;;
   esac
 done
