@@ -469,6 +469,7 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restr
 // 2x136 + stream 80 + reduce 64 + gemv 96 = 512 fits; the old 4 WG/CU grids did not).
 constexpr int SNT = 256, SUNROLL = 16, RUNROLL = 6;
 
+template <int U, bool NTS>
 __global__ __launch_bounds__(SNT) void k_stream_copy(const f32x4* __restrict__ src, f32x4* __restrict__ dst,
                                                     u64 n4, u32 chunk4, WorkQueue* q, const PartTable* table, u32 mode,
                                                     u32 me, u64* cnt, u32* status) {
@@ -486,17 +487,22 @@ __global__ __launch_bounds__(SNT) void k_stream_copy(const f32x4* __restrict__ s
     if (c < 0) break;
     const u64 base = (u64)c * chunk4;
     const u64 end = min(base + chunk4, n4);
-    for (u64 i = base + threadIdx.x; i < end; i += (u64)SNT * SUNROLL) {
-      f32x4 v[SUNROLL];
+    for (u64 i = base + threadIdx.x; i < end; i += (u64)SNT * U) {
+      f32x4 v[U];
 #pragma unroll
-      for (int k = 0; k < SUNROLL; ++k) {
+      for (int k = 0; k < U; ++k) {
         const u64 idx = i + (u64)k * SNT;
         if (idx < end) v[k] = __builtin_nontemporal_load(src + idx);
       }
 #pragma unroll
-      for (int k = 0; k < SUNROLL; ++k) {
+      for (int k = 0; k < U; ++k) {
         const u64 idx = i + (u64)k * SNT;
-        if (idx < end) __builtin_nontemporal_store(v[k], dst + idx);
+        if (idx < end) {
+          if constexpr (NTS)
+            __builtin_nontemporal_store(v[k], dst + idx);
+          else
+            dst[idx] = v[k];
+        }
       }
     }
     count_unit(cnt, me, xcc, inst, &t_last, 2 * lines, 2 * lines, q);
@@ -508,7 +514,11 @@ __global__ __launch_bounds__(SNT) void k_stream_copy(const f32x4* __restrict__ s
 // out = a + b on bf16 (the traffic shape of a ring all-reduce step: two reads
 // and one write per element).  Used as the collective tenant on one GPU; on
 // N > 1 GPUs the tenant issues RCCL all-reduce over xGMI instead.
-__global__ __launch_bounds__(SNT) void k_reduce_bf16(const u32x4* __restrict__ a, const u32x4* __restrict__ b,
+// Variants (gpbs_hip_set_reduce_opts, swept by scripts/kbench.py): NT threads
+// per workgroup, U 16-byte element pairs in flight per thread, non-temporal
+// (streaming) loads / stores on or off.
+template <int NT, int U, bool NTL, bool NTS>
+__global__ __launch_bounds__(NT) void k_reduce_bf16(const u32x4* __restrict__ a, const u32x4* __restrict__ b,
                                                     u32x4* __restrict__ out, u64 n8, u32 chunk8, WorkQueue* q,
                                                     const PartTable* table, u32 mode, u32 me, u64* cnt,
                                                     u32* status) {
@@ -523,19 +533,24 @@ __global__ __launch_bounds__(SNT) void k_reduce_bf16(const u32x4* __restrict__ a
     const int c = grab_unit(q, table, mode, me, xcc, s_slot, nchunks);
     if (c < 0) break;
     const u64 base = (u64)c * chunk8, end = min(base + chunk8, n8);
-    for (u64 i = base + threadIdx.x; i < end; i += (u64)SNT * RUNROLL) {
-      u32x4 x[RUNROLL], y[RUNROLL];
+    for (u64 i = base + threadIdx.x; i < end; i += (u64)NT * U) {
+      u32x4 x[U], y[U];
 #pragma unroll
-      for (int k = 0; k < RUNROLL; ++k) {
-        const u64 idx = i + (u64)k * SNT;
+      for (int k = 0; k < U; ++k) {
+        const u64 idx = i + (u64)k * NT;
         if (idx < end) {
-          x[k] = __builtin_nontemporal_load(a + idx);
-          y[k] = __builtin_nontemporal_load(b + idx);
+          if constexpr (NTL) {
+            x[k] = __builtin_nontemporal_load(a + idx);
+            y[k] = __builtin_nontemporal_load(b + idx);
+          } else {
+            x[k] = a[idx];
+            y[k] = b[idx];
+          }
         }
       }
 #pragma unroll
-      for (int k = 0; k < RUNROLL; ++k) {
-        const u64 idx = i + (u64)k * SNT;
+      for (int k = 0; k < U; ++k) {
+        const u64 idx = i + (u64)k * NT;
         if (idx >= end) continue;
         const u32* px = (const u32*)&x[k];
         const u32* py = (const u32*)&y[k];
@@ -547,7 +562,10 @@ __global__ __launch_bounds__(SNT) void k_reduce_bf16(const u32x4* __restrict__ a
           const float hi = bf2f((u16)(px[w] >> 16)) + bf2f((u16)(py[w] >> 16));
           pr[w] = (u32)f2bf(lo) | ((u32)f2bf(hi) << 16);
         }
-        __builtin_nontemporal_store(r, out + idx);
+        if constexpr (NTS)
+          __builtin_nontemporal_store(r, out + idx);
+        else
+          out[idx] = r;
       }
     }
     count_unit(cnt, me, xcc, inst, &t_last, 3 * lines, 3 * lines, q);
@@ -693,20 +711,55 @@ int gpbs_hip_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
+static int g_stream_opts = 0;
+
+// bit 0: temporal stores; bit 1: 8 (not 16) loads in flight per thread.
+int gpbs_hip_set_stream_opts(int opts) {
+  const int old = g_stream_opts;
+  if (opts >= 0) g_stream_opts = opts;
+  return old;
+}
+
 int gpbs_hip_stream_copy(const void* src, void* dst, unsigned long long bytes, unsigned chunk_bytes, void* q,
                          const void* table, unsigned mode, unsigned me, void* cnt, void* status, int grid, hipStream_t s) {
   if (bytes % 16 || chunk_bytes % 16 || chunk_bytes == 0) return -22;
   if (grid <= 0) grid = 256;  // one workgroup per CU (see SUNROLL)
-  hipLaunchKernelGGL(k_stream_copy, dim3(grid), dim3(SNT), 0, s, (const f32x4*)src, (f32x4*)dst, bytes / 16,
+  using K = void (*)(const f32x4*, f32x4*, u64, u32, WorkQueue*, const PartTable*, u32, u32, u64*, u32*);
+  static const K tab[4] = {k_stream_copy<SUNROLL, true>, k_stream_copy<SUNROLL, false>, k_stream_copy<8, true>,
+                           k_stream_copy<8, false>};
+  hipLaunchKernelGGL(tab[g_stream_opts & 3], dim3(grid), dim3(SNT), 0, s, (const f32x4*)src, (f32x4*)dst, bytes / 16,
                      chunk_bytes / 16, (WorkQueue*)q, (const PartTable*)table, mode, me, (u64*)cnt, (u32*)status);
   return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// Default: 6 pairs in flight, streaming (non-temporal) loads, TEMPORAL
+// stores: 5.57-5.76 TB/s vs 5.02-5.13 with non-temporal stores and 5.84 for
+// torch.add on the same box (profiles/kbench_r2.jsonl); unroll depth and
+// 512-thread workgroups are within noise.
+static int g_reduce_opts = 8;
+
+// bits 0-1: in-flight pairs per thread 6 / 8 / 4 / 12; bit 2: temporal loads;
+// bit 3: temporal stores; bit 4: 512-thread workgroups.  Returns the old value.
+int gpbs_hip_set_reduce_opts(int opts) {
+  const int old = g_reduce_opts;
+  if (opts >= 0) g_reduce_opts = opts;
+  return old;
 }
 
 int gpbs_hip_reduce_bf16(const void* a, const void* b, void* out, unsigned long long bytes, unsigned chunk_bytes,
                          void* q, const void* table, unsigned mode, unsigned me, void* cnt, void* status, int grid, hipStream_t s) {
   if (bytes % 16 || chunk_bytes % 16 || chunk_bytes == 0) return -22;
   if (grid <= 0) grid = 256;
-  hipLaunchKernelGGL(k_reduce_bf16, dim3(grid), dim3(SNT), 0, s, (const u32x4*)a, (const u32x4*)b, (u32x4*)out,
+  using K = void (*)(const u32x4*, const u32x4*, u32x4*, u64, u32, WorkQueue*, const PartTable*, u32, u32, u64*, u32*);
+#define RV(NT, U) {k_reduce_bf16<NT, U, true, true>, k_reduce_bf16<NT, U, false, true>, \
+                   k_reduce_bf16<NT, U, true, false>, k_reduce_bf16<NT, U, false, false>}
+  static const K table256[4][4] = {RV(256, 6), RV(256, 8), RV(256, 4), RV(256, 12)};
+  static const K table512[4][4] = {RV(512, 6), RV(512, 8), RV(512, 4), RV(512, 12)};
+#undef RV
+  const int o = g_reduce_opts;
+  const int nt = (o & 16) ? 512 : 256;
+  const K kern = ((o & 16) ? table512 : table256)[o & 3][((o >> 2) & 1) | (((o >> 3) & 1) << 1)];
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), 0, s, (const u32x4*)a, (const u32x4*)b, (u32x4*)out,
                      bytes / 16, chunk_bytes / 16, (WorkQueue*)q, (const PartTable*)table, mode, me, (u64*)cnt, (u32*)status);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }

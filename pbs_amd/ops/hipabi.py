@@ -45,6 +45,8 @@ def bind(lib):
     _p(lib, "gpbs_hip_gemv_bf16", C.c_int, vp, vp, vp, C.c_int, C.c_int, vp, vp, C.c_uint, C.c_uint, vp, vp, C.c_int,
        vp)
     _p(lib, "gpbs_hip_set_gemm_opts", C.c_int, C.c_int)
+    _p(lib, "gpbs_hip_set_reduce_opts", C.c_int, C.c_int)
+    _p(lib, "gpbs_hip_set_stream_opts", C.c_int, C.c_int)
     _p(lib, "gpbs_hwc_init", C.c_int, C.c_char_p)
     _p(lib, "gpbs_hwc_init_gpu", C.c_int, C.c_char_p, C.c_int)
     _p(lib, "gpbs_hwc_start", C.c_int)

@@ -39,6 +39,7 @@ for step in "$@"; do
     llmsplit) run llmsplit 1100 python -u -m pbs_amd.bench.llm_corun --fp8 --graph --seconds 5 --warmup 2 \
                 --policies "${LLM_POLICIES:-solo,none,se:1/3,se:2/2,se:1/3@solo,se:2/2@solo}" --reps "${LLM_REPS:-1}" \
                 --out gpurun_out/llm_split.json ;;
+    kbench)  run kbench 600 python -u scripts/kbench.py ;;
     *) echo "unknown step $step" | tee -a "$LOG" ;;
   esac
 done

@@ -81,6 +81,18 @@ def main():
         out.append({"kernel": "stream_copy", "bytes": nbytes, "grid": grid, "ms": ms, "tbps": 2 * nbytes / ms / 1e9})
     ms = timed(lambda: dst.copy_(src), args.iters)
     out.append({"kernel": "torch.copy_", "bytes": nbytes, "ms": ms, "tbps": 2 * nbytes / ms / 1e9})
+    sopts = {0: "u16-nt", 1: "u16-ts", 2: "u8-nt", 3: "u8-ts"}
+    sab = {k: [] for k in sopts}
+    for _ in range(3):
+        for opt in sopts:
+            L.gpbs_hip_set_stream_opts(opt)
+            sab[opt].append(timed(lambda: L.gpbs_hip_stream_copy(K._ptr(src), K._ptr(dst), nbytes, 1 << 19, K._ptr(q),
+                                                                 None, 0, 0, None, None, 256, s), args.iters, zero))
+    L.gpbs_hip_set_stream_opts(0)
+    for opt, v in sab.items():
+        ms = sorted(v)[len(v) // 2]
+        out.append({"kernel": "stream_copy", "variant": sopts[opt], "opts": opt, "bytes": nbytes, "grid": 256,
+                    "ms": ms, "tbps": 2 * nbytes / ms / 1e9})
 
     rb = 256 << 20
     a = torch.randn(rb // 2, device=dev, dtype=torch.bfloat16)
@@ -90,7 +102,25 @@ def main():
         ms = timed(lambda: L.gpbs_hip_reduce_bf16(K._ptr(a), K._ptr(b), K._ptr(o), rb, 1 << 19, K._ptr(q), None, 0, 0,
                                                   None, None, grid, s), args.iters, zero)
         out.append({"kernel": "reduce_bf16", "bytes": rb, "grid": grid, "ms": ms, "tbps": 3 * rb / ms / 1e9})
-    ms = timed(lambda: torch.add(a, b, out=o), args.iters)
+    # reduce variants (gpbs_hip_set_reduce_opts): unroll / temporal loads,
+    # stores / 512-thread workgroups, interleaved rounds against torch.add
+    ropts = {0: "u6-nt", 8: "u6-ts", 9: "u8-ts", 10: "u4-ts", 11: "u12-ts", 24: "w512-u6-ts", 25: "w512-u8-ts",
+             26: "w512-u4-ts"}
+    rab = {k: [] for k in ropts}
+    tadd = []
+    for _ in range(3):
+        for opt in ropts:
+            L.gpbs_hip_set_reduce_opts(opt)
+            rab[opt].append(timed(lambda: L.gpbs_hip_reduce_bf16(K._ptr(a), K._ptr(b), K._ptr(o), rb, 1 << 19,
+                                                                 K._ptr(q), None, 0, 0, None, None, 256, s),
+                                  args.iters, zero))
+        tadd.append(timed(lambda: torch.add(a, b, out=o), args.iters))
+    L.gpbs_hip_set_reduce_opts(8)
+    for opt, v in rab.items():
+        ms = sorted(v)[len(v) // 2]
+        out.append({"kernel": "reduce_bf16", "variant": ropts[opt], "opts": opt, "bytes": rb, "grid": 256, "ms": ms,
+                    "tbps": 3 * rb / ms / 1e9})
+    ms = sorted(tadd)[len(tadd) // 2]
     out.append({"kernel": "torch.add", "bytes": rb, "ms": ms, "tbps": 3 * rb / ms / 1e9})
 
     W = torch.randn(8192, 4096, device=dev, dtype=torch.bfloat16)
