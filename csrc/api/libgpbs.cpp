@@ -520,6 +520,35 @@ int gpbs_sched_ext(gpbs_engine_t* e, int t, int set, gpbs_sched_ext_t* p) {
   return r;
 }
 
+int gpbs_arinc653_set(gpbs_engine_t* e, int pool, const gpbs_arinc653_schedule_t* s) {
+  LOCK(e);
+  Pool* p = e->e->pool(pool);
+  if (!p) return GPBS_ENOENT;
+  if (!s || s->num_entries < 0 || s->num_entries > GPBS_ARINC653_MAX_ENTRIES) return GPBS_EINVAL;
+  std::vector<ArincEntry> es;
+  for (int i = 0; i < s->num_entries; ++i) es.push_back({s->entries[i].tenant, s->entries[i].slot, s->entries[i].runtime_ns});
+  int r = p->sched->set_schedule(s->major_frame_ns, es);
+  DONE(e);
+  return r;
+}
+
+int gpbs_arinc653_get(gpbs_engine_t* e, int pool, gpbs_arinc653_schedule_t* s) {
+  LOCK(e);
+  Pool* p = e->e->pool(pool);
+  if (!p) return GPBS_ENOENT;
+  if (!s) return GPBS_EINVAL;
+  int64_t major = 0;
+  std::vector<ArincEntry> es;
+  int r = p->sched->get_schedule(&major, &es);
+  if (r < 0) return r;
+  std::memset(s, 0, sizeof(*s));
+  s->major_frame_ns = major;
+  s->num_entries = (int32_t)std::min<size_t>(es.size(), GPBS_ARINC653_MAX_ENTRIES);
+  s->is_explicit = r;
+  for (int i = 0; i < s->num_entries; ++i) s->entries[i] = {es[i].tenant, es[i].slot, es[i].runtime};
+  return 0;
+}
+
 int gpbs_atc_sync(gpbs_engine_t* e, int pool, int global_min_us) {
   LOCK(e);
   Pool* p = e->e->pool(pool);

@@ -1335,12 +1335,14 @@ class CreditScheduler : public Scheduler {
 std::unique_ptr<Scheduler> make_static_scheduler(Engine& e, int pool);
 std::unique_ptr<Scheduler> make_credit2_scheduler(Engine& e, int pool);
 std::unique_ptr<Scheduler> make_sedf_scheduler(Engine& e, int pool);
+std::unique_ptr<Scheduler> make_arinc653_scheduler(Engine& e, int pool);
 
 std::unique_ptr<Scheduler> make_scheduler(const std::string& name, Engine& e, int pool) {
   if (name == "credit" || name == "pbs") return std::make_unique<CreditScheduler>(e, pool, Mode::PBS);
   if (name == "credit-fixed") return std::make_unique<CreditScheduler>(e, pool, Mode::FIXED);
   if (name == "atc") return std::make_unique<CreditScheduler>(e, pool, Mode::ATC);
-  if (name == "static" || name == "arinc653") return make_static_scheduler(e, pool);
+  if (name == "static") return make_static_scheduler(e, pool);
+  if (name == "arinc653") return make_arinc653_scheduler(e, pool);
   if (name == "credit2") return make_credit2_scheduler(e, pool);
   if (name == "sedf") return make_sedf_scheduler(e, pool);
   return nullptr;

@@ -120,6 +120,14 @@ struct TaskSlice {
 
 class Engine;
 
+// One window of an ARINC 653 major frame (xen_sysctl_arinc653_schedule's
+// sched_entries[]): the tenant (slot -1 = all its slots) and its runtime.
+struct ArincEntry {
+  int tenant;
+  int slot;
+  int64_t runtime;  // ns
+};
+
 // The pluggable scheduler interface (struct scheduler, sched-if.h:144-193).
 class Scheduler {
  public:
@@ -147,6 +155,10 @@ class Scheduler {
   virtual int adjust_ext(Tenant&, bool, gpbs_sched_ext_t&) { return GPBS_EINVAL; }
   // ATC across GPUs: local minimum slice out, node-wide minimum in (us).
   virtual int atc_sync(int) { return GPBS_EINVAL; }
+  // ARINC 653 schedule table (a653sched_adjust_global put/get); get returns
+  // 1 for an installed table, 0 for the automatic one.
+  virtual int set_schedule(int64_t, const std::vector<ArincEntry>&) { return GPBS_EINVAL; }
+  virtual int get_schedule(int64_t*, std::vector<ArincEntry>*) { return GPBS_EINVAL; }
   virtual void dump_settings(std::string& out) = 0;
   virtual void dump_cpu_state(int part, std::string& out) = 0;
   virtual void dump_admin_conf(std::string& out) = 0;

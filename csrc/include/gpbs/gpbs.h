@@ -175,6 +175,24 @@ typedef struct gpbs_partition_info {
   uint64_t switches;
 } gpbs_partition_info_t;
 
+/* ARINC 653 schedule (xen_sysctl_arinc653_schedule, public/sysctl.h:545-566):
+ * a major frame of windows, each owned by a tenant (slot -1: all of its
+ * slots; slot k: that slot only).  Times in ns. */
+#define GPBS_ARINC653_MAX_ENTRIES 64
+typedef struct gpbs_arinc653_entry {
+  int32_t tenant, slot;
+  int64_t runtime_ns;
+} gpbs_arinc653_entry_t;
+typedef struct gpbs_arinc653_schedule {
+  int64_t major_frame_ns;
+  int32_t num_entries, is_explicit; /* get: 0 = the automatic table */
+  gpbs_arinc653_entry_t entries[GPBS_ARINC653_MAX_ENTRIES];
+} gpbs_arinc653_schedule_t;
+/* put / get the pool's table; GPBS_EINVAL if the pool is not arinc653 or the
+ * table is invalid (frame <= 0, no entries, runtime <= 0, sum > frame). */
+int gpbs_arinc653_set(gpbs_engine_t* e, int pool, const gpbs_arinc653_schedule_t* s);
+int gpbs_arinc653_get(gpbs_engine_t* e, int pool, gpbs_arinc653_schedule_t* s);
+
 /* --- scheduler-specific tenant parameters (S4: credit2, sedf) --- */
 int gpbs_sched_ext(gpbs_engine_t* e, int tenant, int set, gpbs_sched_ext_t* p);
 /* ATC pool across GPUs: applies global_min_us (> 0) and returns the pool's

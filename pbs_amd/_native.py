@@ -58,6 +58,15 @@ COUNTER_ADAPT_BATCH = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_in
                                   C.POINTER(u64), C.POINTER(AdaptState), C.POINTER(AdaptParams))
 
 
+class ArincEntry(C.Structure):
+    _fields_ = [("tenant", i32), ("slot", i32), ("runtime_ns", C.c_int64)]
+
+
+class ArincSchedule(C.Structure):
+    _fields_ = [("major_frame_ns", C.c_int64), ("num_entries", i32), ("is_explicit", i32),
+                ("entries", ArincEntry * 64)]
+
+
 class CounterOps(C.Structure):
     _fields_ = [("user", C.c_void_p), ("slot_refresh", COUNTER_SLOT_REFRESH),
                 ("tenant_deltas", COUNTER_TENANT_DELTAS), ("adapt_batch", COUNTER_ADAPT_BATCH)]
@@ -179,6 +188,8 @@ def load_core(build_if_missing=True):
         P(lib, "gpbs_sched_credit_set", C.c_int, E, C.c_int, C.c_int, C.c_int)
         P(lib, "gpbs_sched_ext", C.c_int, E, C.c_int, C.c_int, C.POINTER(SchedExt))
         P(lib, "gpbs_atc_sync", C.c_int, E, C.c_int, C.c_int)
+        P(lib, "gpbs_arinc653_set", C.c_int, E, C.c_int, C.POINTER(ArincSchedule))
+        P(lib, "gpbs_arinc653_get", C.c_int, E, C.c_int, C.POINTER(ArincSchedule))
         P(lib, "gpbs_sched_params_get", C.c_int, E, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int))
         P(lib, "gpbs_sched_params_set", C.c_int, E, C.c_int, C.c_int, C.c_int)
         P(lib, "gpbs_sched_name", C.c_int, E, C.c_int, C.c_char_p, C.c_int)

@@ -306,6 +306,25 @@ class Engine:
         return this pool's local minimum (us) of its last apply."""
         return self._chk(self.lib.gpbs_atc_sync(self.h, pool, int(global_min_us)), "atc_sync")
 
+    def arinc653_set(self, pool: int, major_frame_us: float, entries):
+        """Install an ARINC 653 table on an arinc653 pool: entries =
+        [(tenant, slot or -1, runtime_us), ...] (a653sched_adjust_global put)."""
+        s = N.ArincSchedule()
+        s.major_frame_ns = int(major_frame_us * 1000)
+        s.num_entries = len(entries)
+        if len(entries) > 64:
+            raise GpbsError(-22, "at most 64 ARINC 653 entries")
+        for i, (t, slot, rt) in enumerate(entries):
+            s.entries[i].tenant, s.entries[i].slot, s.entries[i].runtime_ns = int(t), int(slot), int(rt * 1000)
+        self._chk(self.lib.gpbs_arinc653_set(self.h, pool, C.byref(s)), "arinc653_set")
+
+    def arinc653_get(self, pool: int = 0) -> Dict:
+        s = N.ArincSchedule()
+        self._chk(self.lib.gpbs_arinc653_get(self.h, pool, C.byref(s)), "arinc653_get")
+        return {"major_frame_us": s.major_frame_ns / 1000, "explicit": bool(s.is_explicit),
+                "entries": [(s.entries[i].tenant, s.entries[i].slot, s.entries[i].runtime_ns / 1000)
+                            for i in range(s.num_entries)]}
+
     def sched_params_get(self, pool: int = 0):
         ts, rl = C.c_int(), C.c_int()
         self._chk(self.lib.gpbs_sched_params_get(self.h, pool, C.byref(ts), C.byref(rl)), "sched_params_get")

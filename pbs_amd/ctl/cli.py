@@ -7,6 +7,7 @@ cpupool -> pool:
     gpbsctl sched-credit [-d <Tenant> [-w[=WEIGHT]|-c[=CAP]]] [-s [-t TSLICE] [-r RATELIMIT]] [-p POOL]
     gpbsctl sched-credit2 [-d <Tenant> [-w[=WEIGHT]]] [-p POOL]
     gpbsctl sched-sedf [-d <Tenant> [-p MS] [-s MS] [-l MS] [-e 0|1] [-w W]] [-c POOL]
+    gpbsctl sched-arinc653 [-p POOL] [-f MAJOR_FRAME_US TENANT[:SLOT]=RUNTIME_US ...]
     gpbsctl create NAME [--slots N] [--weight W] [--cap C] [--pool P]
     gpbsctl destroy|pause|unpause TENANT
     gpbsctl list | slot-list [TENANT...] | slot-pin TENANT SLOT|all PARTS|all | slot-set TENANT N
@@ -171,6 +172,36 @@ def cmd_sched_credit2(c: Client, argv: List[str]) -> int:
         if a.weight is not None:
             _err("libxl_domain_sched_params_set failed.")
         return 3
+
+
+def cmd_sched_arinc653(c: Client, argv: List[str]) -> int:
+    """ARINC 653 schedule table (the a653sched_adjust_global put/get that the
+    reference exposes through xc_sched_arinc653_schedule_set/get).  Without -f
+    prints the table; with -f installs a new one, effective at once."""
+    ap = argparse.ArgumentParser(prog="gpbsctl sched-arinc653", add_help=True)
+    ap.add_argument("-p", "--cpupool", "--pool", dest="pool")
+    ap.add_argument("-f", "--major-frame", dest="major", type=float)
+    ap.add_argument("entries", nargs="*", help="TENANT[:SLOT]=RUNTIME_US")
+    a = ap.parse_args(argv)
+    if a.entries and a.major is None:
+        _err("Must specify the major frame (-f) with schedule entries.")
+        return 1
+    if a.major is not None:
+        es = []
+        for x in a.entries:
+            if "=" not in x:
+                _err(f"Bad entry '{x}': expected TENANT[:SLOT]=RUNTIME_US")
+                return 1
+            who, rt = x.split("=", 1)
+            dom, slot = (who.split(":", 1) + ["-1"])[:2] if ":" in who else (who, "-1")
+            es.append({"domain": dom, "slot": int(slot), "runtime_us": float(rt)})
+        c.call("arinc653_set", pool=a.pool, major_frame_us=a.major, entries=es)
+    s = c.call("arinc653_get", pool=a.pool)
+    print("Cpupool %s: major_frame=%dus%s" % (s["name"], s["major_frame_us"], "" if s["explicit"] else " (automatic)"))
+    print("%-33s %4s %5s %10s" % ("Name", "ID", "Slot", "Runtime_us"))
+    for e in s["entries"]:
+        print("%-33s %4d %5s %10d" % (e["domain"], e["id"], "all" if e["slot"] < 0 else e["slot"], e["runtime_us"]))
+    return 0
 
 
 def cmd_sched_sedf(c: Client, argv: List[str]) -> int:
@@ -342,6 +373,8 @@ def main(argv: Optional[List[str]] = None) -> int:
             return cmd_sched_credit2(c, rest)
         if cmd == "sched-sedf":
             return cmd_sched_sedf(c, rest)
+        if cmd == "sched-arinc653":
+            return cmd_sched_arinc653(c, rest)
         if cmd == "list":
             return cmd_list(c, rest)
         if cmd in ("slot-list", "vcpu-list"):

@@ -251,6 +251,37 @@ class Daemon:
             self.engine.sched_params_set(p, ts, rl)
             return self.pool_params_get(p)
 
+    def arinc653_get(self, pool=None):
+        p = self._pool(pool)
+        try:
+            s = self.engine.arinc653_get(p)
+        except Exception:
+            raise RpcError("Pool is not using the arinc653 scheduler", -22)
+        names = {}
+        for t in self.engine.tenants():
+            names[t] = self.engine.tenant_info(t).name
+        s["entries"] = [{"domain": names.get(t, str(t)), "id": t, "slot": sl, "runtime_us": rt}
+                        for t, sl, rt in s["entries"]]
+        s.update(pool=p, name=self.engine.pool_info(p)["name"])
+        return s
+
+    def arinc653_set(self, pool=None, major_frame_us: float = 0, entries=()):
+        """entries: [{"domain": name|id, "slot": -1|k, "runtime_us": us}, ...]."""
+        with self.lock:
+            p = self._pool(pool)
+            es = [(self._resolve(x["domain"]), int(x.get("slot", -1)), float(x["runtime_us"])) for x in entries]
+            if not es:
+                raise RpcError("Schedule must have at least one entry", -22)
+            if float(major_frame_us) <= 0:
+                raise RpcError("Major frame must be positive", -22)
+            if sum(x[2] for x in es) > float(major_frame_us):
+                raise RpcError("Total runtime of the entries exceeds the major frame", -22)
+            try:
+                self.engine.arinc653_set(p, float(major_frame_us), es)
+            except Exception as e:
+                raise RpcError(f"Invalid ARINC 653 schedule: {e}", -22)
+            return self.arinc653_get(p)
+
     def pool_list(self):
         out = []
         for p in self.engine.pools():
@@ -471,7 +502,7 @@ class Daemon:
 
     def _handlers(self):
         names = ["info", "create", "destroy", "domain_list", "domain_sched_get", "domain_sched_set",
-                 "domain_sched_ext_get", "domain_sched_ext_set",
+                 "domain_sched_ext_get", "domain_sched_ext_set", "arinc653_get", "arinc653_set",
                  "pool_params_get", "pool_params_set", "pool_list", "pool_create", "pool_destroy", "pool_rename",
                  "pool_cpu_add", "pool_cpu_remove", "pool_migrate", "pool_xgmi_split", "pause", "unpause",
                  "slot_list", "slot_pin", "slot_set", "debug_keys", "dmesg", "trace", "perfc", "top", "register",

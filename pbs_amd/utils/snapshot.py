@@ -48,8 +48,14 @@ def capture(engine, extra: Optional[Dict] = None) -> Dict[str, Any]:
     for p in engine.pools():
         info = engine.pool_info(p)
         ts, rl = engine.sched_params_get(p)
-        doc["pools"].append({"id": p, "name": info["name"], "sched": info["sched"], "cpus": info["cpus"],
-                             "tslice_us": ts, "ratelimit_us": rl})
+        ent = {"id": p, "name": info["name"], "sched": info["sched"], "cpus": info["cpus"],
+               "tslice_us": ts, "ratelimit_us": rl}
+        if info["sched"] == "arinc653":  # an installed ARINC 653 table (by tenant NAME: ids change on restore)
+            a = engine.arinc653_get(p)
+            if a["explicit"]:
+                ent["arinc653"] = {"major_frame_us": a["major_frame_us"],
+                                   "entries": [[engine.tenant_info(t).name, sl, rt] for t, sl, rt in a["entries"]]}
+        doc["pools"].append(ent)
     for t in engine.tenants():
         i = engine.tenant_info(t)
         ent = {"id": t, "name": i.name, "pool": i.pool, "slots": i.nslots, "weight": i.weight, "cap": i.cap,
@@ -128,4 +134,13 @@ def restore(engine, path_or_doc) -> Dict[str, Any]:
         cur = engine.tenant_info(tid).paused
         for _ in range(max(0, t.get("paused", 0) - cur)):
             engine.pause(tid)
+    names = {engine.tenant_info(t).name: t for t in engine.tenants()}
+    for p in doc["pools"]:
+        a = p.get("arinc653")
+        if a:
+            try:
+                engine.arinc653_set(pool_map[p["id"]], a["major_frame_us"],
+                                    [(names[n], sl, rt) for n, sl, rt in a["entries"] if n in names])
+            except Exception:
+                pass
     return doc
