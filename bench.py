@@ -33,8 +33,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--policies", default="none,static,credit2,credit-fixed,gpbs-split,gpbs",
+    ap.add_argument("--policies", default="none,static,credit2,credit-fixed-ts,gpbs-ts,credit-fixed,gpbs",
                     help="comma list; gpbs is the reported policy")
+    ap.add_argument("--keep-engines", action="store_true",
+                    help="one engine per policy for the whole process (default: a fresh engine per timed run)")
     ap.add_argument("--reps", type=int, default=5,
                     help="timed runs per policy, in a randomized order per repetition (median and IQR reported)")
     ap.add_argument("--seed", type=int, default=20261016, help="policy-order shuffle seed (same on every rank)")
@@ -117,7 +119,8 @@ def main():
     cfg = CorunConfig(steps=args.steps, warmup=args.warmup, target_ms=args.target_ms, policies=pols,
                       table_mode=args.table, mix=args.mix, hw_counters=(counters == "hw"),
                       protocol=args.protocol, step_ms=args.step_ms, gang_transport=args.gang_transport,
-                      gang_shm_base=gang_base, gang_wait_driven=args.gang_wait_driven)
+                      gang_shm_base=gang_base, gang_wait_driven=args.gang_wait_driven,
+                      fresh_engine=not args.keep_engines)
     if args.rehearse:
         cfg.coll_bytes = 4 << 20  # CPU gloo all-reduce stand-in
     log = (lambda *a: print(*a, file=sys.stderr, flush=True))
@@ -172,7 +175,7 @@ def main():
         "config": {"model": ("4-tenant mix (MFMA GEMM + HBM-stream + all-reduce + idle)" if args.mix == "4mix"
                              else "2 bf16 4096^2 GEMM tenants"),
                    "global_batch": world * 4, "seq_len": 0, "parallelism": f"dp{world}" if world > 1 else "dp1",
-                   "tenants_per_gpu": 4 if args.mix == "4mix" else 2, "policy": "gpbs (PBS credit, SE-exclusive partitions, hw counters)", "mix": args.mix},
+                   "tenants_per_gpu": 4 if args.mix == "4mix" else 2, "policy": "gpbs (counter-driven SE classes, PBS credit, hw counters)", "mix": args.mix},
         "mean_slowdown_pct": round(q([r["mean_slowdown_pct"] for r in runs["gpbs"]], 0.5), 2),
         "counters": counters,
         "protocol": {"kind": args.protocol, "step_ms": args.step_ms if args.protocol == "steady" else None,

@@ -131,7 +131,10 @@ struct GpuCtx {
   uint64_t hwc_samples = 0;
   double hw_sum[kNumPmc] = {}, model_sum[kNumPmc] = {};  // attributed vs modeled totals
   double unatt[kNumPmc] = {};                             // hardware counts no owner explains
+  double metric_sum[kNumPmc] = {};                        // counts delivered to the PBS metric (clean windows)
+  int clean_pct = 90;  // exclusive-ownership window: min % of an interval one owner must hold (0: pro rata)
   double att_total[kMaxTenants][kNumPmc] = {};            // per-tenant attributed hardware totals
+  double met_total[kMaxTenants][kNumPmc] = {};            // per-tenant totals that reached the PBS metric
   double mod_total[kMaxTenants][kNumPmc] = {};            // per-tenant modeled totals (cross-check)
   u64 last_delta[kMaxTenants][kNumPmc];
   std::mutex mu;
@@ -282,6 +285,18 @@ inline u64 dpos(u64 a, u64 b) { return a >= b ? a - b : 0; }  // Q5: a counter r
 //    XCD's L2 requests (both measured).
 // Counts no owner explains (an SE nobody owned: stray workgroups draining
 // after a revocation, the scheduler's own kernels) are kept as unattributed.
+//
+// Exclusive-ownership windows (what the PBS metric and the contention class
+// see): a partition's delta reaches the per-tenant metric deltas only when one
+// tenant owned it for at least clean_pct % of the interval.  A time-shared
+// interval splits pro rata for the accounting totals, but the per-tenant
+// RATES of such a split are the mixture's, identical for every owner: a
+// reduce-copy tenant time-sharing an SE with a GEMM reads as the GEMM's miss
+// rate (its instructions are a few % of the interval's), is classed compute,
+// is placed beside the GEMM again, and never measures cleanly -- measured on
+// MI355X as a stable misclassification.  The per-vCPU PMU save/restore of
+// X:xen/arch/x86/pmustate.c:87-111 counts exactly one vCPU per interval; this
+// is its analog for partitions whose owner changes between two samples.
 void hwc_attribute(GpuCtx* c) {
   constexpr int P = kXcds * kCtx;
   std::vector<double> own_d((size_t)kMaxTenants * P, 0.0);
@@ -291,8 +306,40 @@ void hwc_attribute(GpuCtx* c) {
       const int64_t d = c->snap_own[i] - c->own_prev[i];
       own_d[i] = d > 0 ? (double)d : 0.0;
     }
-  double refs_x[kMaxTenants][kXcds] = {};
-  double add[kMaxTenants][kNumPmc] = {};
+  // interval length: the longest any partition was owned (owned ns of a
+  // partition sum to at most the interval)
+  double span = 0;
+  for (int p = 0; p < P; ++p) {
+    double tot = 0;
+    for (int t = 0; t < kMaxTenants; ++t) tot += own_d[(size_t)t * P + p];
+    span = std::max(span, tot);
+  }
+  // clean owner of each partition over this interval (-1: mixed / idle)
+  int clean_owner[P];
+  for (int p = 0; p < P; ++p) {
+    clean_owner[p] = -1;
+    if (span <= 0) continue;
+    for (int t = 0; t < kMaxTenants; ++t)
+      if (own_d[(size_t)t * P + p] * 100.0 >= span * c->clean_pct) clean_owner[p] = t;
+  }
+  // the single clean owner of a whole XCD (every partition of it either
+  // unowned in the interval or clean-owned by that tenant), else -1
+  int xcd_owner[kXcds];
+  for (int x = 0; x < kXcds; ++x) {
+    int o = -1;
+    bool ok = true;
+    for (int e = 0; e < kCtx && ok; ++e) {
+      const int p = x * kCtx + e;
+      double tot = 0;
+      for (int t = 0; t < kMaxTenants; ++t) tot += own_d[(size_t)t * P + p];
+      if (tot <= 0) continue;
+      ok = clean_owner[p] >= 0 && (o < 0 || o == clean_owner[p]);
+      o = clean_owner[p];
+    }
+    xcd_owner[x] = ok ? o : -1;
+  }
+  double refs_x[kMaxTenants][kXcds] = {}, refs_cx[kMaxTenants][kXcds] = {};
+  double add[kMaxTenants][kNumPmc] = {}, addc[kMaxTenants][kNumPmc] = {};
   for (int k = 0; k < kNumPmc; ++k) {
     const bool miss_by_refs = k == 3;
     for (int x = 0; x < kXcds; ++x) {
@@ -312,6 +359,10 @@ void hwc_attribute(GpuCtx* c) {
             if (w <= 0) continue;
             add[t][k] += v * w / tot;
             if (k == 2) refs_x[t][x] += v * w / tot;
+            if (clean_owner[p] == t) {
+              addc[t][k] += v * w / tot;
+              if (k == 2) refs_cx[t][x] += v * w / tot;
+            }
           }
         }
         continue;
@@ -338,23 +389,32 @@ void hwc_attribute(GpuCtx* c) {
         if (wt[t] > 0) {
           add[t][k] += v * wt[t] / tot;
           if (k == 2) refs_x[t][x] += v * wt[t] / tot;
+          if (miss_by_refs && c->se_mode && c->slot_se[2]) {
+            // the clean part of the tenant's share: its L2 requests from
+            // partitions it owned exclusively
+            addc[t][k] += v * refs_cx[t][x] / tot;
+          } else if (xcd_owner[x] == t) {  // XCD-wide counts: clean only with one owner on the XCD
+            addc[t][k] += v * wt[t] / tot;
+          }
         }
     }
   }
   for (int t = 0; t < kMaxTenants; ++t)
     for (int k = 0; k < kNumPmc; ++k) {
-      if (add[t][k] > 0) {
-        const u64 a = (u64)(add[t][k] + 0.5);
-        c->last_delta[t][k] += a;
-        c->att_total[t][k] += add[t][k];
+      if (add[t][k] > 0) c->att_total[t][k] += add[t][k];
+      const double m = c->clean_pct > 0 ? addc[t][k] : add[t][k];
+      if (m > 0) {
+        c->last_delta[t][k] += (u64)(m + 0.5);
+        c->metric_sum[k] += m;
+        c->met_total[t][k] += m;
       }
-      double m = 0;
+      double md = 0;
       for (int x = 0; x < kXcds; ++x) {
         const size_t i = ((size_t)t * kXcds + x) * kNumPmc + k;
-        m += (double)dpos(c->snap_blk[i], c->blk_prev[i]);
+        md += (double)dpos(c->snap_blk[i], c->blk_prev[i]);
       }
-      c->mod_total[t][k] += m;
-      c->model_sum[k] += m;
+      c->mod_total[t][k] += md;
+      c->model_sum[k] += md;
     }
 }
 
@@ -798,6 +858,7 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
   std::memset(c->last_delta, 0, sizeof(c->last_delta));
   std::memset(c->own_ns, 0, sizeof(c->own_ns));
   std::memset(c->own_base, 0, sizeof(c->own_base));
+  if (const char* v = std::getenv("GPBS_HWC_CLEAN")) c->clean_pct = std::max(0, std::min(100, std::atoi(v)));
   bool ok = hipHostMalloc((void**)&c->h_table, sizeof(PartTable), hipHostMallocCoherent | hipHostMallocMapped) ==
             hipSuccess;
   ok = ok && hipMalloc((void**)&c->d_cnt, sizeof(u64) * kMaxTenants * kXcds * kNumPmc) == hipSuccess;
@@ -987,6 +1048,22 @@ int gpbs_gpu_hwc_quality(void* p, uint64_t* max_ns, double* unatt_frac4, int* se
   return 0;
 }
 
+// Exclusive-ownership windows: set the minimum share (percent) of a sample
+// interval one tenant must own a partition for its delta to reach the PBS
+// metric (0: every interval, split pro rata).  Returns the previous value;
+// frac4 (optional) receives, per slot, the fraction of all hardware counts
+// since the last reset that reached the metric.
+int gpbs_gpu_hwc_clean(void* p, int pct, double* frac4) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c) return -22;
+  std::lock_guard<std::mutex> g(c->snap_mu);
+  const int old = c->clean_pct;
+  if (pct >= 0) c->clean_pct = std::min(pct, 100);
+  if (frac4)
+    for (int k = 0; k < kNumPmc; ++k) frac4[k] = c->hw_sum[k] > 0 ? c->metric_sum[k] / c->hw_sum[k] : 0.0;
+  return old;
+}
+
 // Per-tenant cumulative attributed hardware counts and modeled counts since
 // the last reset (PBS slots INST, CYCLES, LLC_REFS, LLC_MISSES).
 int gpbs_gpu_hwc_tenant(void* p, int t, double* att4, double* model4) {
@@ -997,6 +1074,16 @@ int gpbs_gpu_hwc_tenant(void* p, int t, double* att4, double* model4) {
     if (att4) att4[k] = c->att_total[t][k];
     if (model4) model4[k] = c->mod_total[t][k];
   }
+  return 0;
+}
+
+// Per-tenant cumulative counts that reached the PBS metric (exclusive-
+// ownership windows) since the last reset.
+int gpbs_gpu_hwc_tenant_metric(void* p, int t, double* m4) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c || t < 0 || t >= kMaxTenants || !m4) return -22;
+  std::lock_guard<std::mutex> g(c->snap_mu);
+  for (int k = 0; k < kNumPmc; ++k) m4[k] = c->met_total[t][k];
   return 0;
 }
 
@@ -1027,6 +1114,8 @@ int gpbs_gpu_hwc_reset(void* p) {
   std::memset(c->hw_sum, 0, sizeof(c->hw_sum));
   std::memset(c->model_sum, 0, sizeof(c->model_sum));
   std::memset(c->unatt, 0, sizeof(c->unatt));
+  std::memset(c->metric_sum, 0, sizeof(c->metric_sum));
+  std::memset(c->met_total, 0, sizeof(c->met_total));
   c->hwc_ns = c->hwc_ns_max = 0;
   c->hwc_samples = 0;
   return 0;

@@ -29,23 +29,32 @@ step's tail alone, which rewards staggering completions rather than sharing.
 Policies (same tenants, same box):
   none     default hardware sharing: every tenant launches ungated full-GPU grids
   static   equal static XCD split (2 XCDs per tenant, ARINC-653-like)
-  gpbs     (flagship) PBS adaptive credit scheduler over shader-engine (SE)
-           exclusive partitions: 4 per XCD, one owner each.  Live CDNA4
-           counters attributed by SE ownership drive the PBS phase detector
-           and the contention class; the compute class owns SEs {0,1} of every
-           XCD; the memory tenants alternate on SEs {2,3} as one gang with PBS
-           quanta; runners launch on CU-masked streams of their class half;
-           the latency tenant runs outside the partitions, co-resident at
-           raised wave priority
-  credit-fixed / credit2   the same partitions and tenants under the credit
-           scheduler with a fixed quantum / under credit2 (no classes)
-  gpbs-split  each memory tenant owns one memory SE per XCD (no time-sharing;
-           credit-fixed-split: same with a fixed quantum)
+  gpbs     (flagship) counter-driven contention classes over shader-engine (SE)
+           exclusive partitions, 4 per XCD, one owner each.  Live CDNA4
+           counters, attributed by SE ownership in exclusive-ownership
+           windows, drive the PBS phase detector and the contention class;
+           the compute class owns SEs {0,1} of every XCD, each memory-class
+           tenant one memory SE of every XCD (memory tenants never share an
+           SE: per-SE load paths cap a stream at ~0.5 of HBM on one SE and
+           ~0.93 on two, and time-sharing two SEs between memory tenants at
+           ms quanta measured below splitting them); runners launch on
+           CU-masked streams of their class half; the latency tenant runs
+           outside the partitions, co-resident at raised wave priority
+  credit-fixed   the same with a fixed credit quantum (PBS ablation: nothing
+           is time-shared in this mix, so adaptive quanta change nothing)
+  gpbs-ts  memory tenants alternate on the memory SEs {2,3} as one gang with
+           PBS adaptive quanta (round-2 first flagship; credit-fixed-ts: same
+           with a fixed quantum -- the PBS-quanta ablation)
+  credit2  the SE partitions under credit2 (no classes)
   gpbs-boost  latency tenant inside the partitions (wake-BOOST revokes SEs)
   gpbs-ctx4   round-1 flagship: four co-resident issue contexts per XCD,
            parked gating, wave priority (counters attributed by time share)
   gpbs-ctx2 / gpbs-spatial / gpbs-x / gpbs-noprio / gpbs-nogang / gpbs1 /
   gpbs-exit / sedf   round-1 variants kept for ablations
+
+Every timed run of a scheduler policy starts from a fresh engine (no
+classes, credits or quanta carried over from an earlier run of the policy);
+``fresh_engine=False`` keeps one engine per policy for the whole process.
 """
 from __future__ import annotations
 
@@ -103,6 +112,7 @@ class CorunConfig:
     # all are done, so early finishers idle and late ones run the tail alone.
     protocol: str = "steady"
     step_ms: float = 80.0
+    fresh_engine: bool = True    # every run of a scheduler policy starts from a new engine
 
 
 # SE-exclusive flagship (the four partitions of an XCD are its shader engines,
@@ -121,18 +131,18 @@ POLICY_ENGINES = {
     # name: (issue contexts per XCD, engine overrides on top of MI355X_PROFILE,
     #        kernel gate mode, partition-table location + runtime options)
     # flagship: counter-driven class split over exclusive SEs -- the compute
-    # class owns SEs {0,1} of every XCD; the memory tenants hold slots on all
-    # memory SEs {2,3} and alternate on them as one gang under credit with
-    # PBS's adaptive quanta; the latency tenant runs outside the partitions,
+    # class owns SEs {0,1} of every XCD, each memory tenant one memory SE of
+    # every XCD ("se8": 8 slots, so credit places the memory tenants on
+    # disjoint SEs); the latency tenant runs outside the partitions,
     # co-resident at raised wave priority (no BOOST revocations)
-    "gpbs": (4, dict(SE_OVERRIDES), True, "device,se,waveprio,latco"),
-    "credit-fixed": (4, dict(SE_OVERRIDES, sched="credit-fixed"), True, "device,se,waveprio,latco"),
+    "gpbs": (4, dict(SE_OVERRIDES), True, "device,se,waveprio,latco,se8"),
+    "credit-fixed": (4, dict(SE_OVERRIDES, sched="credit-fixed"), True, "device,se,waveprio,latco,se8"),
+    # time-shared variant: the memory tenants hold slots on all memory SEs
+    # {2,3} and alternate on them as one gang under credit with PBS's
+    # adaptive quanta (credit-fixed-ts: fixed quantum)
+    "gpbs-ts": (4, dict(SE_OVERRIDES), True, "device,se,waveprio,latco"),
+    "credit-fixed-ts": (4, dict(SE_OVERRIDES, sched="credit-fixed"), True, "device,se,waveprio,latco"),
     "credit2": (4, dict(SE_OVERRIDES, sched="credit2"), True, "device,se,waveprio,latco"),
-    # spatial variant: each memory tenant one memory SE per XCD (no
-    # time-sharing, so no quanta to adapt)
-    "gpbs-split": (4, dict(SE_OVERRIDES), True, "device,se,waveprio,latco,se8"),
-    "credit-fixed-split": (4, dict(SE_OVERRIDES, sched="credit-fixed"), True, "device,se,waveprio,latco,se8"),
-    # latency tenant inside the partitions (BOOST on wake revokes memory SEs)
     "gpbs-boost": (4, dict(SE_OVERRIDES), True, "device,se,waveprio"),
     "gpbs-host": (4, dict(SE_OVERRIDES), True, "host,se,waveprio,latco"),
     "gpbs-ctx4": (4, {}, "park", "device,waveprio"),
@@ -236,6 +246,7 @@ class Corun:
         self.log = log if rank == 0 else (lambda *a, **k: None)
         torch.cuda.set_device(device)
         self.engines: Dict[str, Engine] = {}
+        self._retired = []  # engines of earlier runs (fresh_engine), closed in close()
         self.tid: Dict[str, int] = {}
         self.tenants = MIXES[cfg.mix]["tenants"]
         self.throughput = MIXES[cfg.mix]["throughput"]
@@ -315,6 +326,13 @@ class Corun:
         coll = self.runners.get("coll")
         if policy in self.engines:
             e = self.engines[policy]
+            if self.cfg.fresh_engine and getattr(e, "_gpbs_used", False):
+                # the old engine stays alive (closed with the others at the
+                # end): the GPU context and runners still reference it until
+                # attach() below rebinds them
+                self._retired.append(e)
+                e = self.engines[policy] = self._make_engine(policy)
+            e._gpbs_used = True
             _, _, gate, table = POLICY_ENGINES[policy]
             opts = table.split(",")
             self.ctx.set_table_mode(opts[0])
@@ -676,5 +694,5 @@ class Corun:
         if isinstance(coll, CollTenant):
             coll.close()
         self.ctx.close()
-        for e in self.engines.values():
+        for e in list(self.engines.values()) + self._retired:
             e.close()

@@ -125,10 +125,20 @@ class GpuContext:
         mx, sem = C.c_uint64(0), C.c_int(0)
         u = (C.c_double * 4)()
         self.L.gpbs_gpu_hwc_quality(self.h, C.byref(mx), u, C.byref(sem))
+        cf = (C.c_double * 4)()
+        pct = self.L.gpbs_gpu_hwc_clean(self.h, -1, cf)
         return {"samples": n.value, "mean_sample_us": round(ns.value / 1e3, 1), "max_sample_us": round(mx.value / 1e3, 1),
                 "hw_over_model": [round(x, 4) for x in r],
                 "unattributed_frac": [round(x, 4) for x in u],
-                "attribution": "exact-se" if sem.value & 1 else "xcd-time-share"}
+                "attribution": "exact-se" if sem.value & 1 else "xcd-time-share",
+                # exclusive-ownership windows: share of the counts that reached the PBS metric
+                "clean_pct": pct, "metric_frac": [round(x, 4) for x in cf]}
+
+    def set_hwc_clean(self, pct: int) -> int:
+        """Exclusive-ownership window: a partition's counter delta reaches the
+        PBS metric only when one tenant owned it >= pct % of the sample
+        interval (0: split every interval pro rata).  Returns the old value."""
+        return self.L.gpbs_gpu_hwc_clean(self.h, int(pct), None)
 
     def hwc_tenant(self, tenant: int):
         """Cumulative hardware counts attributed to `tenant` since the last
@@ -137,6 +147,13 @@ class GpuContext:
         a, m = (C.c_double * 4)(), (C.c_double * 4)()
         self.L.gpbs_gpu_hwc_tenant(self.h, tenant, a, m)
         return list(a), list(m)
+
+    def hwc_tenant_metric(self, tenant: int):
+        """Cumulative counts of `tenant` that reached the PBS metric (the
+        exclusive-ownership windows) since the last reset."""
+        m = (C.c_double * 4)()
+        self.L.gpbs_gpu_hwc_tenant_metric(self.h, tenant, m)
+        return list(m)
 
     def hwc_reset(self):
         self.L.gpbs_gpu_hwc_reset(self.h)

@@ -26,6 +26,10 @@ for step in "$@"; do
     smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bquick)  run bquick 600 python bench.py --steps 10 --warmup 2 --reps 2 --out gpurun_out/bquick.json ;;
     bench)   run bench 900 python bench.py --steps 20 --warmup 5 --out gpurun_out/bench.json ;;
+    bclean0) GPBS_HWC_CLEAN=0 run bclean0 600 python bench.py --steps 20 --warmup 5 --reps 3 \
+                --policies none,gpbs-ts,credit-fixed-ts,gpbs --out gpurun_out/bclean0.json ;;
+    bkeep)   run bkeep 600 python bench.py --steps 20 --warmup 5 --reps 3 --keep-engines \
+                --policies none,gpbs-ts,gpbs --out gpurun_out/bkeep.json ;;
     rehearse) run rehearse 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
                 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 1 --reps 1 --rehearse --policies none,gpbs \
                 --out gpurun_out/rehearse.json ;;

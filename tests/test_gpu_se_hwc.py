@@ -111,6 +111,41 @@ rg.wait(120); rs.wait(120)
 e.stop()
 out["check"] = e.check()
 rg.close(); rs.close(); ctx.close(); e.close()
+# --- 3. exclusive-ownership windows: a GEMM and a reduce-copy tenant
+# time-share every SE, alternating every ~0.3 ms (far below the ~1 ms sample
+# interval) with a 6 ms exclusive hold each every ~20 ms.  Pro-rata
+# attribution gives both the mixture's miss rate; the PBS metric sees only
+# the exclusive windows and keeps them apart.
+ctx = GpuContext(0, nctx=4)
+ctx.set_se_mode(True)
+G, R = 1, 3
+ctx.set_owners([G] * (XCDS * CTX))
+ctx.set_hwc(True)
+assert ctx.set_hwc_clean(90) >= 0
+rg = Runner(ctx, "gemm", G, gate=True, engine_wake=False, M=4096, N=4096, K=4096)
+rr = Runner(ctx, "reduce", R, gate=True, engine_wake=False, bytes=256 << 20)
+time.sleep(0.05)
+ctx.hwc_poll(); ctx.hwc_reset()
+rg.submit(100000); rr.submit(100000)
+t0 = time.time(); k = 0
+while time.time() - t0 < 1.2:
+    k += 1
+    ph = k % 44
+    if ph in (0, 22):  # exclusive hold
+        who, dt = (G if ph == 0 else R), 0.006
+    else:              # fast alternation
+        who, dt = (G if k % 2 else R), 0.0003
+    ctx.set_owners([who] * (XCDS * CTX))
+    time.sleep(dt)
+    ctx.hwc_poll()
+rg.cancel(); rr.cancel(); rg.wait(120); rr.wait(120); ctx.hwc_poll()
+for name, t in (("ts_gemm", G), ("ts_reduce", R)):
+    att, _ = ctx.hwc_tenant(t)
+    met = ctx.hwc_tenant_metric(t)
+    out[name] = {"att_rate": att[3] * 1e5 / max(att[0], 1), "met_rate": met[3] * 1e5 / max(met[0], 1),
+                 "att_inst": att[0], "met_inst": met[0]}
+out["ts_quality"] = ctx.hwc_stats()
+rg.close(); rr.close(); ctx.set_hwc(False); ctx.close()
 print("RESULT " + json.dumps(out))
 """
 
@@ -134,3 +169,11 @@ def test_hw_counters_attributed_by_se_ownership_separate_stream_from_gemm():
     assert out["class"] == {"gemm": 0, "hbm": 1}, out
     assert out["rate"]["hbm"] > 20000 > out["rate"]["gemm"], out["rate"]
     assert out["check"] == ""
+    # exclusive-ownership windows keep a time-shared memory tenant apart from
+    # the GEMM it alternates with; the pro-rata split blurs the two
+    tg, tr = out["ts_gemm"], out["ts_reduce"]
+    assert tg["met_inst"] > 0 and tr["met_inst"] > 0, out
+    assert tr["met_rate"] > 5 * max(tg["met_rate"], 1), (tg, tr)
+    assert tr["met_rate"] > 20000, tr
+    assert tr["met_rate"] / max(tg["met_rate"], 1) > tr["att_rate"] / max(tg["att_rate"], 1), (tg, tr)
+    assert 0 < out["ts_quality"]["metric_frac"][0] < 1, out["ts_quality"]
