@@ -133,6 +133,7 @@ struct GpuCtx {
   double unatt[kNumPmc] = {};                             // hardware counts no owner explains
   double metric_sum[kNumPmc] = {};                        // counts delivered to the PBS metric (clean windows)
   int clean_pct = 90;  // exclusive-ownership window: min % of an interval one owner must hold (0: pro rata)
+  int prev_raw[kXcds * kCtx];  // per partition: its >= clean_pct owner over the previous interval, -1 none
   double att_total[kMaxTenants][kNumPmc] = {};            // per-tenant attributed hardware totals
   double met_total[kMaxTenants][kNumPmc] = {};            // per-tenant totals that reached the PBS metric
   double mod_total[kMaxTenants][kNumPmc] = {};            // per-tenant modeled totals (cross-check)
@@ -314,13 +315,18 @@ void hwc_attribute(GpuCtx* c) {
     for (int t = 0; t < kMaxTenants; ++t) tot += own_d[(size_t)t * P + p];
     span = std::max(span, tot);
   }
-  // clean owner of each partition over this interval (-1: mixed / idle)
+  // clean owner of each partition over this interval (-1: mixed / idle):
+  // it held the partition for clean_pct % of this interval AND of the
+  // previous one, so the previous owner's workgroups (a GEMM tile drains for
+  // ~0.1-0.3 ms after a revocation) have left before the interval began
   int clean_owner[P];
   for (int p = 0; p < P; ++p) {
-    clean_owner[p] = -1;
-    if (span <= 0) continue;
-    for (int t = 0; t < kMaxTenants; ++t)
-      if (own_d[(size_t)t * P + p] * 100.0 >= span * c->clean_pct) clean_owner[p] = t;
+    int raw = -1;
+    if (span > 0)
+      for (int t = 0; t < kMaxTenants; ++t)
+        if (own_d[(size_t)t * P + p] * 100.0 >= span * c->clean_pct) raw = t;
+    clean_owner[p] = (raw >= 0 && c->prev_raw[p] == raw) ? raw : -1;
+    c->prev_raw[p] = raw;
   }
   // the single clean owner of a whole XCD (every partition of it either
   // unowned in the interval or clean-owned by that tenant), else -1
@@ -858,6 +864,7 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
   std::memset(c->last_delta, 0, sizeof(c->last_delta));
   std::memset(c->own_ns, 0, sizeof(c->own_ns));
   std::memset(c->own_base, 0, sizeof(c->own_base));
+  for (int& r : c->prev_raw) r = -1;
   if (const char* v = std::getenv("GPBS_HWC_CLEAN")) c->clean_pct = std::max(0, std::min(100, std::atoi(v)));
   bool ok = hipHostMalloc((void**)&c->h_table, sizeof(PartTable), hipHostMallocCoherent | hipHostMallocMapped) ==
             hipSuccess;

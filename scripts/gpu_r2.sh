@@ -28,6 +28,8 @@ for step in "$@"; do
     bench)   run bench 900 python bench.py --steps 20 --warmup 5 --out gpurun_out/bench.json ;;
     bclean0) GPBS_HWC_CLEAN=0 run bclean0 600 python bench.py --steps 20 --warmup 5 --reps 3 \
                 --policies none,gpbs-ts,credit-fixed-ts,gpbs --out gpurun_out/bclean0.json ;;
+    bts)     run bts 600 python bench.py --steps 20 --warmup 5 --reps 3 \
+                --policies none,gpbs-ts,credit-fixed-ts,gpbs --out gpurun_out/bts.json ;;
     bkeep)   run bkeep 600 python bench.py --steps 20 --warmup 5 --reps 3 --keep-engines \
                 --policies none,gpbs-ts,gpbs --out gpurun_out/bkeep.json ;;
     rehearse) run rehearse 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \

@@ -130,21 +130,24 @@ rg.submit(100000); rr.submit(100000)
 t0 = time.time(); k = 0
 while time.time() - t0 < 1.2:
     k += 1
-    ph = k % 44
+    ph = k %% 44
     if ph in (0, 22):  # exclusive hold
-        who, dt = (G if ph == 0 else R), 0.006
+        who, dt = (G if ph == 0 else R), 0.008
     else:              # fast alternation
-        who, dt = (G if k % 2 else R), 0.0003
+        who, dt = (G if k %% 2 else R), 0.0003
     ctx.set_owners([who] * (XCDS * CTX))
     time.sleep(dt)
     ctx.hwc_poll()
-rg.cancel(); rr.cancel(); rg.wait(120); rr.wait(120); ctx.hwc_poll()
+# read before the drain (both own SEs again so revoked units can finish)
+ctx.hwc_poll()
+res = {t: (ctx.hwc_tenant(t)[0], ctx.hwc_tenant_metric(t)) for t in (G, R)}
+out["ts_quality"] = ctx.hwc_stats()
+ctx.set_owners([G if c < 2 else R for x in range(XCDS) for c in range(CTX)])
+rg.cancel(); rr.cancel(); rg.wait(120); rr.wait(120)
 for name, t in (("ts_gemm", G), ("ts_reduce", R)):
-    att, _ = ctx.hwc_tenant(t)
-    met = ctx.hwc_tenant_metric(t)
+    att, met = res[t]
     out[name] = {"att_rate": att[3] * 1e5 / max(att[0], 1), "met_rate": met[3] * 1e5 / max(met[0], 1),
                  "att_inst": att[0], "met_inst": met[0]}
-out["ts_quality"] = ctx.hwc_stats()
 rg.close(); rr.close(); ctx.set_hwc(False); ctx.close()
 print("RESULT " + json.dumps(out))
 """
