@@ -645,9 +645,14 @@ class CreditScheduler : public Scheduler {
     for (size_t k = 0; k < n; ++k) {
       CDom& d = sd(*E.tenants[ids[k]]);
       const uint64_t inst = d.pmc[0], cyc = d.pmc[1], miss = d.pmc[3];
-      d.cache_miss_rate = inst ? miss * 100000 / inst : 0;  // Q3 fix: per tenant
+      // Q14 (idle_skip): a period without instructions -- no dispatch, or no
+      // exclusive-ownership counter window -- keeps the last measured rates
+      // instead of reporting 0 for the tenant
+      if (inst || !E.boot.idle_skip) {
+        d.cache_miss_rate = inst ? miss * 100000 / inst : 0;  // Q3 fix: per tenant
+        d.cpi = inst ? cyc * 1000 / inst : 0;
+      }
       if (inst) d.rate_ewma = (3 * d.rate_ewma + d.cache_miss_rate) / 4;
-      d.cpi = inst ? cyc * 1000 / inst : 0;
       E.emit(TRC_METRIC, master_, (uint32_t)ids[k], (uint32_t)inst, (uint32_t)miss, (uint32_t)d.cache_miss_rate);
       d.spinlock_metric_update = 0;
       d.spinlock_count = 0;

