@@ -249,13 +249,17 @@ __global__ __launch_bounds__(GNT, 2) void k_gemm_bf16_tn(const u16* __restrict__
 // rows, one logical chunk) covers all 16 slots of a 256-B bank row.
 constexpr int G2_BM = 256, G2_BK = 64, G2_NT = 512;
 constexpr u32 kGemmXRange = 1u << 16;  // mode bit: XCD-range tile queues (grab_unit_x)
+constexpr u32 kGemmBlock2D = 1u << 17; // mode bit: 2-D per-XCD tile blocks
 // host: bit 0 = XCD-range tile queues, bit 1 = DEEP prefetch variant, bit 2 =
 // staggered wave groups.  Default = staggered, plain queue: interleaved A/B
 // in one process at 4096^3 (profiles/kbench_r1.jsonl) measured staggered
 // 1155 TF/s vs 1035 unstaggered, deep prefetch 1036 (no gain: the lead was
 // not the limit; MFMA busy was 41 % with the groups in lock-step), XCD-range
 // queue 946 (dispatch already deals consecutive tiles round-robin over the
-// XCDs, giving each XCD two B panels shared 16 ways).
+// XCDs, giving each XCD two B panels shared 16 ways).  Bit 3 = 2-D per-XCD
+// tile blocks (12 panel slices per XCD K-step instead of 18): 1129 vs 1117
+// TF/s plain, 1060 with the XCD-range queue (round 2, interleaved, same box;
+// torch.mm 1416) -- panel traffic is not what holds the kernel back.
 static int g_gemm_opts = 4;
 constexpr int kG2Half = 128 * 128;           // bytes per half-tile
 constexpr int kG2Buf = 4 * kG2Half;          // A0 A1 B0 B1
@@ -305,7 +309,20 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restr
     const int tile = (mode & kGemmXRange) ? grab_unit_x(q, table, mode, me, xcc, s_slot, (u32)ntiles)
                                           : grab_unit(q, table, mode, me, xcc, s_slot, (u32)ntiles);
     if (tile < 0) break;
-    const int tm = tile / tiles_n, tn = tile % tiles_n;  // row-major: an XCD range shares A panels
+    int tm = tile / tiles_n, tn = tile % tiles_n;  // row-major: an XCD range shares A panels
+    if ((mode & kGemmBlock2D) && (tiles_m & 3) == 0 && (tiles_n & 1) == 0) {
+      // 2-D XCD blocks: the tiles one XCD computes form a (tiles_m/4) x
+      // (tiles_n/2) block (4096^3: 4 A + 8 B panels per XCD instead of 2 A +
+      // 16 B row-major, or 16 A + 2 B dealt round-robin), so the 32
+      // concurrent tiles of an XCD pull 12 panel slices per K-step into its
+      // L2 instead of 18.  The XCD of a tile: its range (XCD-range queue), or
+      // ticket mod 8 (plain queue: tickets follow the round-robin dispatch).
+      const int per = ntiles / kXcds, bm = tiles_m / 4, bn = tiles_n / 2;
+      const int g = (mode & kGemmXRange) ? tile / per : tile % kXcds;
+      const int j = (mode & kGemmXRange) ? tile % per : tile / kXcds;
+      tm = (g >> 1) * bm + j / bn;
+      tn = (g & 1) * bn + j % bn;
+    }
     const u16* Ab = A + (size_t)tm * G2_BM * K;
     const u16* Bb = Bt + (size_t)tn * G2_BM * K;
 
@@ -692,7 +709,8 @@ int gpbs_hip_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int
     const u32 inst = (u32)((G2_BM / 16) * (G2_BM / 16) * (K / 32) + (K / G2_BK) * 64 + 128);
     const u32 refs = (u32)(((u64)2 * G2_BM * K * 2) / 128);
     const u32 miss = (u32)((((u64)M + N) * K * 2 / 128) / ntiles + (u64)G2_BM * G2_BM * 2 / 128);
-    const u32 m2 = mode | ((g_gemm_opts & 1) ? kGemmXRange : 0u);
+    const u32 m2 = mode | ((g_gemm_opts & 1) ? kGemmXRange : 0u) |
+                   ((g_gemm_opts & 8) && ntiles % kXcds == 0 ? kGemmBlock2D : 0u);
     auto kern = (g_gemm_opts & 4) ? k_gemm256_bf16_tn<2> : (g_gemm_opts & 2) ? k_gemm256_bf16_tn<1> : k_gemm256_bf16_tn<0>;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(G2_NT), 0, s, (const u16*)A, (const u16*)Bt, (u16*)C, M, N,
                        K, (WorkQueue*)q, (const PartTable*)table, m2, me, (u64*)cnt, inst, refs, miss, (u32*)status);

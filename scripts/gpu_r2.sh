@@ -40,6 +40,13 @@ for step in "$@"; do
                 -o run -- python bench.py --steps 5 --warmup 1 --reps 1 --policies gpbs --counters model \
                 --out gpurun_out/roctx_bench.json
              unset GPBS_ROCTX ;;
+    prof)    cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-.}"
+             run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r2 -o run -- python3 bench.py \
+                --steps 10 --warmup 2 --reps 1 --policies none,gpbs --out gpurun_out/prof_bench.json
+             if ls gpurun_out/prof_r2/*/run_results.db >/dev/null 2>&1 || ls gpurun_out/prof_r2/run_results.db >/dev/null 2>&1; then
+               db=$(ls gpurun_out/prof_r2/*/run_results.db gpurun_out/prof_r2/run_results.db 2>/dev/null | head -1)
+               python3 scripts/rocpd_summary.py "$db" -o gpurun_out/prof_r2_summary.txt
+             fi ;;
     micro)   run micro 600 python -u scripts/microbench.py --out gpurun_out/microbench.json ;;
     tmicro)  run tmicro 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_microbench.py ;;
     llmsplit) run llmsplit 1100 python -u -m pbs_amd.bench.llm_corun --fp8 --graph --seconds 5 --warmup 2 \

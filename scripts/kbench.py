@@ -57,7 +57,10 @@ def main():
     Cm = torch.empty(n, n, device=dev, dtype=torch.bfloat16)
     # A/B of the tile queue (plain vs XCD-range), interleaved rounds in one
     # process (cross-box timings are not comparable: DVFS).
-    names = {0: "plain-queue", 1: "xcd-range", 2: "deep-prefetch", 4: "staggered-groups"}
+    names = {0: "plain-queue", 1: "xcd-range", 2: "deep-prefetch", 4: "staggered-groups",
+             12: "staggered-2d-blocks", 13: "staggered-xcd-range-2d-blocks"}
+    if os.environ.get("KBENCH_GEMM_ONLY"):
+        names = {4: "staggered-groups", 12: "staggered-2d-blocks", 13: "staggered-xcd-range-2d-blocks"}
     ab = {k: [] for k in names}
     for _ in range(5):
         for opt in names:
@@ -71,6 +74,22 @@ def main():
                     "ms": ms, "tflops": 2 * n ** 3 / ms / 1e9, "min_ms": min(v)})
     ms = timed(lambda: torch.mm(A, B.t(), out=Cm), args.iters)
     out.append({"kernel": "torch.mm", "shape": [n, n, n], "ms": ms, "tflops": 2 * n ** 3 / ms / 1e9})
+    # correctness of every variant against torch (fp32 reference of a slice)
+    ref = (A[:512].float() @ B.float().t())
+    for opt in names:
+        L.gpbs_hip_set_gemm_opts(opt)
+        zero()
+        Cm.zero_()
+        L.gpbs_hip_gemm_bf16(K._ptr(A), K._ptr(B), K._ptr(Cm), n, n, n, K._ptr(q), None, 0, 0, None, None, 0, s)
+        torch.cuda.synchronize()
+        err = (Cm[:512].float() - ref).abs().max().item()
+        out.append({"kernel": "gemm_bf16", "variant": names[opt], "check_max_abs_err": err,
+                    "ok": err < 0.02 * ref.abs().max().item()})
+    L.gpbs_hip_set_gemm_opts(4)
+    if os.environ.get("KBENCH_GEMM_ONLY"):
+        for r in out:
+            print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}))
+        return
 
     nbytes = 1 << 30
     src = torch.empty(nbytes // 4, device=dev, dtype=torch.float32).normal_()
