@@ -12,10 +12,21 @@
 // that misses the deadline makes the call return -110 (ETIMEDOUT) on every
 // other rank: they degrade to local scheduling instead of stalling (§5.3).
 //
-// Layout: header, then per rank {seq, vals[2][kMaxVals]}.  A rank writes its
-// values for epoch e into vals[e & 1], then publishes seq = e (release).  It
-// cannot reach epoch e + 2 before every rank has published e + 1, so a slow
-// reader of vals[e & 1] is never overwritten.
+// Layout: header, then per rank {seq, want, vals[2][kMaxVals]}.  A rank writes
+// its values for epoch e into vals[e & 1], then publishes seq = e (release).
+// It cannot reach epoch e + 2 before every member has published e + 1, so a
+// slow reader of vals[e & 1] is never overwritten.
+//
+// Views (elastic re-formation, the analog of the reference moving the pool
+// master's timers to a surviving CPU, X:xen/common/sched_credit.c:628-633):
+// the gang starts as view 0 = every rank.  After a missed deadline the
+// survivors call gpbs_gang_shm_reform: the first one to claim generation g
+// becomes the master of the re-formation, waits a join window, and publishes
+// view g = the ranks that asked to join g (members mask) with a common first
+// epoch.  Exchanges then wait only for members.  A rank that was left out --
+// the hung one when it comes back -- finds the view changed under it and
+// gets -116 (ESTALE) from its next exchange instead of reading epochs that
+// are not its own.
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -28,6 +39,7 @@
 #include <cstring>
 #include <string>
 #include <thread>
+#include <algorithm>
 
 namespace {
 
@@ -36,12 +48,17 @@ constexpr int kMaxVals = 128;
 
 struct alignas(64) RankSlot {
   std::atomic<uint64_t> seq;
+  std::atomic<uint64_t> want;  // view generation this rank asked to join
   int64_t vals[2][kMaxVals];
 };
 
 struct Region {
   std::atomic<uint32_t> magic;
   uint32_t world, nvals, pad;
+  std::atomic<uint64_t> claim;         // highest generation a master claimed
+  std::atomic<uint64_t> view_gen;      // published view (0 = every rank)
+  std::atomic<uint64_t> view_members;  // member mask of view_gen (0 in view 0 = all)
+  std::atomic<uint64_t> view_base;     // first epoch of view_gen
   RankSlot ranks[kMaxRanks];
 };
 
@@ -50,8 +67,11 @@ struct Gang {
   size_t size = 0;
   int fd = -1;
   int rank = 0, world = 1, nvals = 0;
+  uint64_t gen = 0, members = 0;  // this rank's view
   std::string name;
 };
+
+uint64_t all_mask(int world) { return world >= 64 ? ~0ull : ((1ull << world) - 1); }
 
 int64_t now_ns() {
   timespec ts;
@@ -88,6 +108,7 @@ void* gpbs_gang_shm_open(const char* name, int rank, int world, int nvals) {
     return nullptr;
   }
   g->r = (Region*)p;  // zero-filled on creation: every seq starts at 0, epochs at 1
+  g->members = all_mask(world);
   return g;
 }
 
@@ -99,11 +120,13 @@ void* gpbs_gang_shm_open(const char* name, int rank, int world, int nvals) {
 int gpbs_gang_shm_allgather(void* h, uint64_t epoch, const int64_t* in, int64_t* out, int64_t deadline_ns) {
   Gang* g = (Gang*)h;
   if (!g || !epoch || (g->nvals && (!in || !out))) return -22;
+  if (g->r->view_gen.load(std::memory_order_acquire) != g->gen) return -116;  // re-formed without us
   RankSlot& me = g->r->ranks[g->rank];
   const int buf = (int)(epoch & 1);
   std::memcpy(me.vals[buf], in, sizeof(int64_t) * g->nvals);
   me.seq.store(epoch, std::memory_order_release);
   for (int k = 0; k < g->world; ++k) {
+    if (!((g->members >> k) & 1)) continue;
     RankSlot& o = g->r->ranks[k];
     int spins = 0;
     while (o.seq.load(std::memory_order_acquire) < epoch) {
@@ -118,11 +141,60 @@ int gpbs_gang_shm_allgather(void* h, uint64_t epoch, const int64_t* in, int64_t*
         continue;
       }
       if (now_ns() > deadline_ns) return -110;
+      if (g->r->view_gen.load(std::memory_order_acquire) != g->gen) return -116;
       timespec ts{0, 2000};  // 2 us
       nanosleep(&ts, nullptr);
     }
     std::memcpy(out + (size_t)k * g->nvals, o.vals[buf], sizeof(int64_t) * g->nvals);
   }
+  // a view published while we gathered may have started from other epochs
+  if (g->r->view_gen.load(std::memory_order_acquire) != g->gen) return -116;
+  return 0;
+}
+
+// Elastic re-formation after a missed deadline (see the header comment).
+// Every survivor calls this; the first to claim the next generation waits
+// `join_ns` for the others to ask, then publishes the view.  Returns 0 with
+// *members (mask over the original ranks) and *base_epoch (the first epoch
+// every member uses next) when this rank is a member, -1 when the view was
+// published without it, -110 when no view appeared by `deadline_ns`.
+int gpbs_gang_shm_reform(void* h, int64_t join_ns, int64_t deadline_ns, uint64_t* members, uint64_t* base_epoch) {
+  Gang* g = (Gang*)h;
+  if (!g) return -22;
+  Region* R = g->r;
+  const uint64_t want = std::max(g->gen, R->view_gen.load(std::memory_order_acquire)) + 1;
+  R->ranks[g->rank].want.store(want, std::memory_order_release);
+  uint64_t expect = want - 1;
+  if (R->claim.compare_exchange_strong(expect, want, std::memory_order_acq_rel)) {
+    // master of this re-formation: the join window, then the view
+    const int64_t close_at = now_ns() + join_ns;
+    while (now_ns() < close_at) {
+      timespec ts{0, 200000};  // 200 us
+      nanosleep(&ts, nullptr);
+    }
+    uint64_t m = 0, base = 0;
+    for (int k = 0; k < g->world; ++k)
+      if (R->ranks[k].want.load(std::memory_order_acquire) >= want) {
+        m |= 1ull << k;
+        base = std::max<uint64_t>(base, R->ranks[k].seq.load(std::memory_order_acquire));
+      }
+    R->view_members.store(m, std::memory_order_relaxed);
+    R->view_base.store(base + 2, std::memory_order_relaxed);
+    R->view_gen.store(want, std::memory_order_release);
+  } else {
+    while (R->view_gen.load(std::memory_order_acquire) < want) {
+      if (now_ns() > deadline_ns) return -110;
+      timespec ts{0, 200000};
+      nanosleep(&ts, nullptr);
+    }
+  }
+  const uint64_t vg = R->view_gen.load(std::memory_order_acquire);
+  const uint64_t m = R->view_members.load(std::memory_order_relaxed);
+  if (vg != want || !((m >> g->rank) & 1)) return -1;
+  g->gen = vg;
+  g->members = m;
+  if (members) *members = m;
+  if (base_epoch) *base_epoch = R->view_base.load(std::memory_order_relaxed);
   return 0;
 }
 

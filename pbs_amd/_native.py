@@ -205,6 +205,7 @@ def load_core(build_if_missing=True):
         P(lib, "gpbs_gang_shm_open", C.c_void_p, C.c_char_p, C.c_int, C.c_int, C.c_int)
         P(lib, "gpbs_gang_shm_allgather", C.c_int, C.c_void_p, u64, C.POINTER(i64), C.POINTER(i64), i64)
         P(lib, "gpbs_gang_shm_close", None, C.c_void_p)
+        P(lib, "gpbs_gang_shm_reform", C.c_int, C.c_void_p, i64, i64, C.POINTER(u64), C.POINTER(u64))
         P(lib, "gpbs_slot_set_pmc", C.c_int, E, C.c_int, C.POINTER(u64))
         P(lib, "gpbs_now", i64, E)
         P(lib, "gpbs_advance", C.c_int, E, i64)

@@ -367,6 +367,7 @@ class Corun:
                                             shm_name=f"{self.cfg.gang_shm_base}-{self._gang_seq}",
                                             deadline_ms=self.cfg.gang_deadline_ms,
                                             wait_driven=self.cfg.gang_wait_driven,
+                                            reform=(tr == "shm"),
                                             device=self._gang_device()).start()
             return
         self.ctx.set_table_mode("host")

@@ -87,7 +87,7 @@ def atc_worker(rank: int, world: int, port: int, q, seconds: float = 0.8, epoch_
 
 
 def hang_worker(rank: int, world: int, port: int, q, transport: str, shm_name: str, hang_rank: int,
-                hang_ms: int = 1500, deadline_ms: float = 200.0):
+                hang_ms: int = 1500, deadline_ms: float = 200.0, reform: bool = False):
     """One rank of the gang-deadline test: `hang_rank` stalls `hang_ms` before
     its first exchange (GPBS_FAULT rank_hang); the others must time out
     within the deadline, trace GANG_TIMEOUT and keep scheduling locally."""
@@ -108,7 +108,7 @@ def hang_worker(rank: int, world: int, port: int, q, transport: str, shm_name: s
     dist.barrier()
     t0 = time.monotonic()
     g = GangCoordinator(e, None, [coll], epoch_ms=5.0, transport=transport, shm_name=shm_name,
-                        rank=rank, world=world, deadline_ms=deadline_ms).start()
+                        rank=rank, world=world, deadline_ms=deadline_ms, reform=reform).start()
     degraded_at = None
     # the hung rank stalls before EVERY exchange (ppm 1e6): it completes the
     # epoch the others abandoned, then misses the next one itself
@@ -123,6 +123,7 @@ def hang_worker(rank: int, world: int, port: int, q, transport: str, shm_name: s
         ran_after = (e.tenant_info(coll).run_ns - run0) / ((time.monotonic() - t_deg) * 1e9)
     recs = [r.event for r in e.trace(from_start=True)]
     q.put({"rank": rank, "degraded_at": degraded_at, "epochs": g.epoch, "stats": g.stats(),
+           "history": [(ep, st) for ep, st in g.history][-400:],
            "perfc_timeout": e.perfc().get("gang_timeout", 0), "traced": "GANG_TIMEOUT" in recs,
            "ran_after": ran_after, "dmesg": e.dmesg()})
     q.close()

@@ -54,7 +54,12 @@ Every epoch has a deadline (``deadline_ms``).  A rank that misses it -- one
 rank hung (GPBS_FAULT ``rank_hang``), descheduled or dead -- makes the others'
 exchange time out: they record GANG_TIMEOUT (trace + perfc ``gang_timeout``),
 clear every gang window and go on scheduling locally instead
-of stalling every GPU's gang thread.  Epoch-start skew across ranks (the
+of stalling every GPU's gang thread.  With ``reform=True`` (shm transport)
+the survivors then re-form: the first to claim the next view generation
+waits a join window and publishes the member set and a common first epoch
+(csrc/comm/gang_shm.cpp), so gang windows continue among the members; the
+laggard finds the view changed when it returns and stays local (C12: the
+reference moves the pool master's timers to a surviving CPU).  Epoch-start skew across ranks (the
 spread of the previous epoch's return time, on the node's shared monotonic
 clock) rides the exchange and is reported in ``stats()``.
 """
@@ -104,7 +109,8 @@ class _DistTransport:
 
 
 class _ShmTransport:
-    """One-node ranks: native shared-memory all-gather (csrc/comm/gang_shm.cpp)."""
+    """One-node ranks: native shared-memory all-gather (csrc/comm/gang_shm.cpp),
+    with elastic re-formation of the member set after a missed deadline."""
 
     def __init__(self, name: str, rank: int, world: int, nvals: int):
         from .. import _native as N
@@ -114,6 +120,8 @@ class _ShmTransport:
         if not self.h:
             raise RuntimeError(f"gang shm region {name!r} could not be opened")
         self.seq = 0
+        self.members = list(range(world))
+        self.excluded = False  # the gang re-formed without this rank
 
     def _gather(self, vals, deadline_ns):
         n = self.nvals
@@ -124,9 +132,29 @@ class _ShmTransport:
         rc = self.lib.gpbs_gang_shm_allgather(C.c_void_p(self.h), self.seq, src, out, deadline_ns)
         if rc == -110:
             return None
+        if rc == -116:  # a view was published without us: we were the laggard
+            self.excluded = True
+            return None
         if rc:
             raise RuntimeError(f"gang shm all-gather failed ({rc})")
-        return [list(out[r * n:(r + 1) * n]) for r in range(self.world)]
+        return [list(out[r * n:(r + 1) * n]) for r in self.members]
+
+    def reform(self, join_ms: float, deadline_ms: float) -> Optional[int]:
+        """After a missed deadline: join the next view.  Returns the first
+        epoch of the new view (the same on every member) when this rank is a
+        member, None when it was left out or no view appeared."""
+        if self.excluded:
+            return None
+        m, base = C.c_uint64(0), C.c_uint64(0)
+        now = time.monotonic_ns()
+        rc = self.lib.gpbs_gang_shm_reform(C.c_void_p(self.h), int(join_ms * 1e6),
+                                           now + int((join_ms + deadline_ms) * 1e6), C.byref(m), C.byref(base))
+        if rc:
+            self.excluded = rc == -1
+            return None
+        self.members = [r for r in range(self.world) if (m.value >> r) & 1]
+        self.seq = base.value - 1
+        return base.value
 
     def reduce_min(self, vals, deadline_ns):
         rows = self._gather(vals, deadline_ns)
@@ -149,7 +177,8 @@ class GangCoordinator:
                  metric_tenants: Optional[List[int]] = None, metric_every: int = 5,
                  transport: str = "dist", shm_name: Optional[str] = None, rank: Optional[int] = None,
                  world: Optional[int] = None, deadline_ms: float = 200.0, wait_driven: bool = False,
-                 wait_on_frac: float = 0.02, wait_hold_epochs: int = 64):
+                 wait_on_frac: float = 0.02, wait_hold_epochs: int = 64, reform: bool = False,
+                 join_ms: Optional[float] = None):
         self.engine = engine
         self.group = group
         self.tenants = list(tenants)
@@ -179,6 +208,13 @@ class GangCoordinator:
         self.deadline_ns = int(deadline_ms * 1e6)
         self.timeouts = 0
         self.degraded = False
+        # elastic re-formation (shm transport): after a missed deadline the
+        # survivors form a new view without the laggard and keep their gang
+        # windows; False = degrade to local scheduling for good
+        self.reform = bool(reform)
+        self.join_ms = float(join_ms if join_ms is not None else deadline_ms / 2)
+        self.reforms = 0
+        self.members: List[int] = list(range(self.world))
         # K10 -> gang decision: a gang tenant gets aligned windows only while
         # its ranks report waiting on peers (wait reports: runtime/waitprobe.py)
         self.wait_driven = bool(wait_driven)
@@ -281,6 +317,8 @@ class GangCoordinator:
                 t1 = time.monotonic_ns()
                 if red is None:
                     self._timeout(t1 - t0)
+                    if self._reform(tr):
+                        continue
                     break
                 t_prev = t1
                 self.lat_ns.append(t1 - t0)
@@ -297,6 +335,8 @@ class GangCoordinator:
                 if self.metric_tenants and self.epoch % self.metric_every == 0:
                     if not self._sync_metrics(tr):
                         self._timeout(time.monotonic_ns() - t1)
+                        if self._reform(tr):
+                            continue
                         break
                 if self.wait_driven:
                     self.update_gang_on(self.epoch, [-x for x in red[nt:2 * nt]])
@@ -322,6 +362,22 @@ class GangCoordinator:
                     self.engine.gang_set(t, NONE, 0)
                 except Exception:
                     pass
+
+    def _reform(self, tr) -> bool:
+        """Elastic re-formation after a missed deadline (shm transport): the
+        survivors agree on a new member set and a common epoch; the gang
+        windows resume among them.  False: stay degraded (local scheduling)."""
+        if not self.reform or not hasattr(tr, "reform"):
+            return False
+        with roctx.range("gpbs:gang_reform"):
+            base = tr.reform(self.join_ms, self.deadline_ns / 1e6)
+        if base is None:
+            return False
+        self.reforms += 1
+        self.degraded = False
+        self.members = list(tr.members)
+        self.epoch = int(base)  # decisions are a function of the epoch: same on every member
+        return True
 
     def _atc_local(self) -> int:
         if self.atc_pool is None:
@@ -372,7 +428,8 @@ class GangCoordinator:
         return {"epochs": self.epoch, "transport": self.transport, "sync_p50_us": lat[len(lat) // 2] / 1e3,
                 "sync_p99_us": lat[min(len(lat) - 1, int(0.99 * len(lat)))] / 1e3, "sync_max_us": lat[-1] / 1e3,
                 "skew_p50_us": skew[len(skew) // 2] / 1e3, "skew_max_us": skew[-1] / 1e3,
-                "timeouts": self.timeouts, "degraded": self.degraded,
+                "timeouts": self.timeouts, "degraded": self.degraded, "reforms": self.reforms,
+                "members": list(self.members),
                 "atc_global_us": self.atc_global_us, "metric_syncs": self.metric_syncs,
                 "wait_driven": self.wait_driven, "gang_on": {str(t): v for t, v in self.gang_on.items()},
                 "wait_ewma_us": {str(t): v for t, v in self.wait_ewma_us.items()},

@@ -48,3 +48,41 @@ def test_one_hung_rank_does_not_stall_the_others(transport):
             assert o["degraded_at"] < (deadline_ms + 300) / 1e3, o
         else:
             assert o["degraded_at"] > hang_ms / 1e3, o
+
+
+def test_survivors_reform_the_gang_without_the_hung_rank():
+    """Elastic re-formation (C12 analog): with reform=True the three ranks
+    that time out on the hung one agree on a new view {0, 1, 3} and a common
+    epoch, and keep making identical gang decisions; the hung rank finds the
+    view changed when it returns and stays local."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    world, hung, hang_ms, deadline_ms = 4, 2, 1500, 200.0
+    name = f"gpbs-gang-reform-{os.getpid()}-{port}"
+    ps = [ctx.Process(target=hang_worker, args=(r, world, port, q, "shm", name, hung, hang_ms, deadline_ms, True))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    out = {}
+    for _ in ps:
+        r = q.get(timeout=120)
+        out[r["rank"]] = r
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    survivors = [r for r in range(world) if r != hung]
+    for r in survivors:
+        st = out[r]["stats"]
+        assert st["timeouts"] == 1 and st["reforms"] == 1, st
+        assert st["members"] == survivors, st
+        assert not st["degraded"], st
+        # the gang kept running long after the reform (epochs of 5 ms over ~3 s)
+        assert out[r]["epochs"] > 200, out[r]["epochs"]
+    # identical decisions on every member for the epochs after the reform
+    hs = [dict(out[r]["history"]) for r in survivors]
+    common = set(hs[0]) & set(hs[1]) & set(hs[2])
+    assert len(common) >= 100
+    assert all(hs[0][k] == hs[1][k] == hs[2][k] for k in common)
+    st = out[hung]["stats"]
+    assert st["degraded"] and st["reforms"] == 0, st
