@@ -475,6 +475,14 @@ int gpbs_tenant_adapt_state(gpbs_engine_t* e, int t, gpbs_adapt_state_t* out, in
   return GPBS_OK;
 }
 
+int gpbs_tenant_vpmu(gpbs_engine_t* e, int t, uint64_t* total4) {
+  LOCK(e);
+  Tenant* d = live(e, t);
+  if (!d || !total4) return GPBS_ENOENT;
+  for (int k = 0; k < 4; ++k) total4[k] = d->vpmu_total[k];
+  return GPBS_OK;
+}
+
 int gpbs_tenant_class(gpbs_engine_t* e, int t) {
   LOCK(e);
   Tenant* d = live(e, t);

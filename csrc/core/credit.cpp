@@ -596,7 +596,10 @@ class CreditScheduler : public Scheduler {
           }
         }
       }
-      for (int i = 0; i < kNumPmc; ++i) d.pmc[i] = deltas[4 * k + i];
+      for (int i = 0; i < kNumPmc; ++i) {
+        d.pmc[i] = deltas[4 * k + i];
+        dom.vpmu_total[i] += deltas[4 * k + i];
+      }
       ssum[k] = d.spinlock_metric_update;
       scnt[k] = d.spinlock_count;
     }

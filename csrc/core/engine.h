@@ -82,6 +82,10 @@ struct Tenant {  // struct domain
   bool pinned = false;
   uint64_t pending_requests = 0;  // P7 (live in gpbs: request-queue depth)
   int64_t last_heartbeat = 0;
+  // Cumulative counters the scheduler measured/attributed for this tenant
+  // (sum of the metric periods' deltas): what the vPMU mirror publishes on
+  // its control page (Perfctr-xen's per-vCPU state page, S1/S2).
+  uint64_t vpmu_total[4] = {0, 0, 0, 0};
   int cls = -1;          // contention class: 0 compute-bound (MFMA ctx), 1 memory-bound (memory ctx)
   int cls_pending = -1;  // hysteresis: a new class must be seen on consecutive ticks
   int cls_count = 0;

@@ -237,6 +237,9 @@ int gpbs_slot_yield(gpbs_engine_t* e, int tenant, int index);
 int gpbs_slot_pin(gpbs_engine_t* e, int tenant, int index, const uint64_t* mask4); /* vcpu-pin */
 int gpbs_tenant_info(gpbs_engine_t* e, int tenant, gpbs_tenant_info_t* out);
 int gpbs_tenant_class(gpbs_engine_t* e, int tenant); /* contention class: 0 compute, 1 memory, -1 unknown */
+/* Cumulative INST, CYCLES, LLC refs, LLC misses the scheduler measured and
+ * attributed to the tenant (sum over metric periods; the vPMU mirror). */
+int gpbs_tenant_vpmu(gpbs_engine_t* e, int tenant, uint64_t* total4);
 int gpbs_slot_info(gpbs_engine_t* e, int slot, gpbs_slot_info_t* out);
 int gpbs_tenant_adapt_state(gpbs_engine_t* e, int tenant, gpbs_adapt_state_t* out, int set);
 int gpbs_tenant_heartbeat(gpbs_engine_t* e, int tenant);
@@ -303,6 +306,12 @@ int gpbs_ctl_read(void* ctl, int page, uint32_t* gate, uint64_t* mask, uint32_t*
 #define GPBS_REPORT_HOLD 2     /* lock hold time (lockstat holdtime) */
 #define GPBS_REPORT_REQUESTS 3 /* request arrivals; wait_ns = count */
 int gpbs_ctl_read_mask(void* ctl, int page, uint64_t* mask2, uint32_t* epoch);
+/* vPMU mirror (tenant side, seqlock read): cumulative counters the scheduler
+ * attributed to the tenant, last period's miss rate (per 100k inst), current
+ * quantum, contention class and PBS phase; *seq counts publications.  Returns
+ * the retries (torn reads observed), or < 0. */
+int gpbs_ctl_read_vpmu(void* ctl, int page, uint64_t* c4, uint64_t* miss_rate, uint32_t* tslice_us, int32_t* cls,
+                       uint32_t* phase, uint32_t* seq);
 int gpbs_ctl_report(void* ctl, int page, uint64_t wait_ns, uint32_t kind, uint32_t gpu);
 int gpbs_ctl_drain(void* ctl, int page, uint64_t* waits, uint32_t* kinds, int max);
 void gpbs_ctl_heartbeat(void* ctl, int page, uint64_t now_ns, uint32_t progress);

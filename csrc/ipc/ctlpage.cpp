@@ -7,7 +7,12 @@
 //  * tenant -> scheduler: heartbeat, has-work flag, cumulative software
 //    counters (vPMU mirror, C10) and an SPSC ring of wait reports
 //    {u64 wait_ns, u32 kind, u32 gpu} (the vcrd_op hypercall, C7);
-//  * a futex doorbell per page (VIRQ analog, C9/C1) so gated tenants sleep.
+//  * a futex doorbell per page (VIRQ analog, C9/C1) so gated tenants sleep;
+//  * scheduler -> tenant vPMU mirror under its own seqlock: the cumulative
+//    counters the scheduler measured (live CDNA4 counters attributed by
+//    ownership, or the tenant's own declared ones) plus the PBS view of the
+//    tenant (miss rate, quantum, class, phase) -- the Perfctr-xen per-vCPU
+//    state page the guest reads with a version check (S1/S2, C10, K13).
 //
 // The bridge thread binds a region to an engine: it turns page traffic into
 // engine calls (wake/block, report_wait, heartbeat, slot pmc) and publishes
@@ -35,7 +40,7 @@
 namespace {
 
 constexpr uint32_t kMagic = 0x53425047;  // "GPBS"
-constexpr uint32_t kVersion = 1;
+constexpr uint32_t kVersion = 2;  // 2: vPMU mirror block
 constexpr int kRing = 192;
 
 struct Report {
@@ -69,6 +74,14 @@ struct alignas(64) Page {
   std::atomic<uint32_t> dropped;
   std::atomic<uint32_t> doorbell;  // futex word, bumped on every publish that opens the gate
   uint8_t pad2[64 - 16];
+  // ---- scheduler -> tenant vPMU mirror (seqlock vseq, odd while writing)
+  std::atomic<uint32_t> vseq;
+  std::atomic<uint32_t> vphase;
+  std::atomic<uint64_t> vpmu[4];     // cumulative INST, CYCLES, LLC refs, LLC misses
+  std::atomic<uint64_t> vmiss_rate;  // last period, per 100k instructions
+  std::atomic<uint32_t> vtslice_us;
+  std::atomic<int32_t> vclass;
+  uint8_t pad3[64 - 56];
   Report ring[kRing];
 };
 static_assert(sizeof(Page) <= 4096, "ctl page exceeds 4 KiB");
@@ -220,9 +233,27 @@ void br_on_park(void* user, int t, int s, int parked) {
   if (c->chained.on_park) c->chained.on_park(c->chained.user, t, s, parked);
 }
 
+// vPMU mirror publication (single writer: the bridge thread).
+void publish_vpmu(Page* pg, const uint64_t* c4, uint64_t miss_rate, uint32_t tslice, int32_t cls, uint32_t phase) {
+  const uint32_t s = pg->vseq.load(std::memory_order_relaxed);
+  pg->vseq.store(s + 1, std::memory_order_relaxed);
+  std::atomic_thread_fence(std::memory_order_release);
+  for (int k = 0; k < 4; ++k) pg->vpmu[k].store(c4[k], std::memory_order_relaxed);
+  pg->vmiss_rate.store(miss_rate, std::memory_order_relaxed);
+  pg->vtslice_us.store(tslice, std::memory_order_relaxed);
+  pg->vclass.store(cls, std::memory_order_relaxed);
+  pg->vphase.store(phase, std::memory_order_relaxed);
+  pg->vseq.store(s + 2, std::memory_order_release);
+}
+
 void bridge_loop(Ctl* c) {
   std::vector<Report> buf(kRing);
+  int64_t next_vpmu = 0;
   while (!c->stop.load(std::memory_order_acquire)) {
+    // vPMU mirror every metric period (1 ms), not every 100 us poll: each
+    // publication reads the tenant under the engine lock
+    const bool vpmu_due = now_ns() >= next_vpmu;
+    if (vpmu_due) next_vpmu = now_ns() + 1000000;
     for (uint32_t i = 0; i < c->hdr->ntenants; ++i) {
       Page* pg = &c->pages[i];
       const int tid = pg->tenant_id.load(std::memory_order_acquire);
@@ -261,6 +292,12 @@ void bridge_loop(Ctl* c) {
       if (any) {
         const int sid = gpbs_slot_id(c->engine, tid, 0);
         if (sid >= 0) gpbs_slot_set_pmc(c->engine, sid, pmc);
+      }
+      if (vpmu_due) {
+        uint64_t tot[4];
+        gpbs_tenant_info_t ti;
+        if (gpbs_tenant_vpmu(c->engine, tid, tot) == 0 && gpbs_tenant_info(c->engine, tid, &ti) == 0)
+          publish_vpmu(pg, tot, ti.cache_miss_rate, ti.tslice_us, gpbs_tenant_class(c->engine, tid), ti.phase);
       }
     }
     timespec ts{0, 100000};  // 100 us poll
@@ -333,6 +370,38 @@ int gpbs_ctl_read(void* h, int t, uint32_t* gate, uint64_t* mask, uint32_t* quan
       if (prio) *prio = p;
       if (tid) *tid = i;
       if (epoch) *epoch = e;
+      return retries;
+    }
+    ++retries;
+  }
+}
+
+int gpbs_ctl_read_vpmu(void* h, int t, uint64_t* c4, uint64_t* miss_rate, uint32_t* tslice_us, int32_t* cls,
+                       uint32_t* phase, uint32_t* seq) {
+  Page* pg = page(h, t);
+  if (!pg) return -22;
+  int retries = 0;
+  for (;;) {
+    const uint32_t s0 = pg->vseq.load(std::memory_order_acquire);
+    if (s0 & 1) {
+      ++retries;
+      continue;
+    }
+    uint64_t v[4];
+    for (int k = 0; k < 4; ++k) v[k] = pg->vpmu[k].load(std::memory_order_relaxed);
+    const uint64_t mr = pg->vmiss_rate.load(std::memory_order_relaxed);
+    const uint32_t ts = pg->vtslice_us.load(std::memory_order_relaxed);
+    const int32_t cl = pg->vclass.load(std::memory_order_relaxed);
+    const uint32_t ph = pg->vphase.load(std::memory_order_relaxed);
+    std::atomic_thread_fence(std::memory_order_acquire);
+    if (pg->vseq.load(std::memory_order_relaxed) == s0) {
+      if (c4)
+        for (int k = 0; k < 4; ++k) c4[k] = v[k];
+      if (miss_rate) *miss_rate = mr;
+      if (tslice_us) *tslice_us = ts;
+      if (cls) *cls = cl;
+      if (phase) *phase = ph;
+      if (seq) *seq = s0 / 2;
       return retries;
     }
     ++retries;
@@ -487,6 +556,10 @@ int gpbs_ctl_assign(void* h, int t, int tid) {
   if (!pg) return -22;
   const uint64_t m[2] = {0, 0};
   std::lock_guard<std::mutex> g(((Ctl*)h)->pub_mu);
+  if (pg->tenant_id.load(std::memory_order_acquire) < 0) {  // the bridge skips unassigned pages: no second writer
+    const uint64_t z[4] = {0, 0, 0, 0};
+    publish_vpmu(pg, z, 0, 0, -1, 0);
+  }
   publish_page(pg, 0, m, 0, 0, tid, 0);
   return 0;
 }

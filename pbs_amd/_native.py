@@ -249,10 +249,13 @@ def _bind_ipc(lib):
       C.POINTER(i32), C.POINTER(i32), C.POINTER(u32))
     P(lib, "gpbs_gang_set", C.c_int, C.c_void_p, C.c_int, C.c_int, i64)
     P(lib, "gpbs_tenant_class", C.c_int, C.c_void_p, C.c_int)
+    P(lib, "gpbs_tenant_vpmu", C.c_int, C.c_void_p, C.c_int, C.POINTER(u64))
     P(lib, "gpbs_fault_set", C.c_int, C.c_void_p, C.c_char_p)
     P(lib, "gpbs_fault_hits", C.c_int, C.c_void_p, C.POINTER(u64), C.c_int)
     P(lib, "gpbs_ctl_report", C.c_int, C.c_void_p, C.c_int, u64, u32, u32)
     P(lib, "gpbs_ctl_read_mask", C.c_int, C.c_void_p, C.c_int, C.POINTER(u64), C.POINTER(u32))
+    P(lib, "gpbs_ctl_read_vpmu", C.c_int, C.c_void_p, C.c_int, C.POINTER(u64), C.POINTER(u64), C.POINTER(u32),
+      C.POINTER(i32), C.POINTER(u32), C.POINTER(u32))
     P(lib, "gpbs_ctl_drain", C.c_int, C.c_void_p, C.c_int, C.POINTER(u64), C.POINTER(u32), C.c_int)
     P(lib, "gpbs_ctl_heartbeat", None, C.c_void_p, C.c_int, u64, u32)
     P(lib, "gpbs_ctl_status", C.c_int, C.c_void_p, C.c_int, C.POINTER(u64), C.POINTER(u64), C.POINTER(u32),

@@ -214,6 +214,23 @@ class TenantClient:
         arr = (C.c_uint64 * 4)(*c)
         self.lib.gpbs_ctl_set_counters(self.ctl, self.page, arr)
 
+    def vpmu(self) -> dict:
+        """The tenant's virtualized PMU as the scheduler sees it (control-page
+        mirror, one seqlock read -- the Perfctr-xen guest read of its
+        per-vCPU state page, L:drivers/perfctr/x86.c:252-277): cumulative
+        INST / CYCLES / LLC refs / LLC misses the scheduler measured and
+        attributed to this tenant (live hardware counters when the daemon runs
+        them), last period's miss rate, current quantum, class and phase."""
+        c4 = (C.c_uint64 * 4)()
+        mr, ts, cls, ph, seq = C.c_uint64(0), C.c_uint32(0), C.c_int32(0), C.c_uint32(0), C.c_uint32(0)
+        retries = self.lib.gpbs_ctl_read_vpmu(self.ctl, self.page, c4, C.byref(mr), C.byref(ts), C.byref(cls),
+                                              C.byref(ph), C.byref(seq))
+        if retries < 0:
+            raise RuntimeError(f"read_vpmu failed ({retries})")
+        return {"inst": c4[0], "cycles": c4[1], "l2_refs": c4[2], "l2_misses": c4[3], "miss_rate": mr.value,
+                "tslice_us": ts.value, "class": cls.value, "phase": ph.value, "updates": seq.value,
+                "retries": retries}
+
     # ------------------------------------------------------------ teardown
     def close(self, destroy: bool = True):
         if self._stop.is_set():
@@ -254,7 +271,9 @@ def run_synthetic(name: str, socket_path: str, seconds: float, result_q=None, sl
         time.sleep(0.001)
     if crash:
         os._exit(0)
-    info = {"name": name, "tenant": t.tenant, "opens": opens, "loops": loops, "owned_seen": t.owned()}
+    time.sleep(0.01)  # one more metric period + mirror publication
+    info = {"name": name, "tenant": t.tenant, "opens": opens, "loops": loops, "owned_seen": t.owned(),
+            "declared": list(t.counters), "vpmu": t.vpmu()}
     t.close(destroy=False)
     if result_q is not None:
         result_q.put(info)

@@ -1,6 +1,7 @@
 """Tenant shim <-> gpbsd over the shared-memory control plane, multi-process
 (CPU only): registration, launch gate, wait/hold/request reports (P2/P8/P7),
-published counters reaching the scheduler's vPMU (C10), heartbeat, and the
+published counters reaching the scheduler's vPMU (C10) and its mirror back on
+the tenant's page (S2/K13), heartbeat, and the
 reaper's failure detection (S13) when a tenant process dies."""
 import multiprocessing as mp
 import os
@@ -22,7 +23,9 @@ def test_half_cu_words_cover_exactly_the_owned_halves():
 
 def test_two_tenant_processes_share_the_gpu_through_the_control_plane():
     path = os.path.join(tempfile.mkdtemp(), "gpbsd.sock")
-    d = Daemon(path, gpus=[0], nctx=2, sim=False, profile="mi355x").start()
+    # no reaper here: the tenants unregister without destroy and exit; their
+    # engine state is inspected afterwards (the reaper has its own test)
+    d = Daemon(path, gpus=[0], nctx=2, sim=False, profile="mi355x").start(reaper_s=0)
     try:
         ctx = mp.get_context("spawn")
         q = ctx.Queue()
@@ -44,6 +47,16 @@ def test_two_tenant_processes_share_the_gpu_through_the_control_plane():
             assert info.run_ns > 0, name
             # published counters reached the scheduler (slot-0 vPMU mirror)
             assert e.slot_info(e.slot_id(r["tenant"], 0))["pmc"][0] > 0
+            # ... and came back through the scheduler's metric path into the
+            # tenant's own vPMU mirror (seqlock read of its control page):
+            # cumulative counts, miss rate = misses per 100k instructions
+            v = r["vpmu"]
+            assert v["updates"] > 10 and v["inst"] > 0, v
+            assert v["inst"] <= r["declared"][0] and v["inst"] >= 0.5 * r["declared"][0], (v, r["declared"])
+            assert v["l2_misses"] <= r["declared"][3]
+            want = r["declared"][3] * 100000 / r["declared"][0]
+            assert abs(v["l2_misses"] * 100000 / v["inst"] - want) <= 0.05 * want, (v, want)
+            assert v["tslice_us"] > 0
         z = e.debug_keys("z")
         assert "waits: n=" in z and "holds: n=" in z and "pending_requests=" in z
         assert e.perfc()["report_rx"] > 0
