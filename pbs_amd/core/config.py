@@ -25,8 +25,15 @@ REFERENCE_PROFILE: Dict[str, Any] = dict(
 
 # MI355X profile: the PBS algorithm structure is kept (window 5, band 70-130 %,
 # step ratio +1/-2, tick = quantum/3); time constants are rescaled x10 because
-# a GPU "context switch" (draining an XCD's workgroups between tiles and
-# relaunching) costs tens of microseconds, and the miss-rate threshold
+# of what a GPU "context switch" and its measurement cost (measured,
+# profiles/micro/microbench_r2.json and profiles/rocprof_flagship_r2_summary.txt):
+# publishing a table is seen by every workgroup of a 1024-WG grid 15.6 us p50
+# later (device table; 339 us polling the host table), a revoked 256x256 GEMM
+# tile drains for up to one tile (~0.12-0.28 ms), and one live-counter sample
+# takes ~0.4 ms of a ~1.4 ms interval -- a quantum must span two intervals to
+# be measured at all in a settled exclusive-ownership window
+# (csrc/hip/runtime.cpp hwc_attribute).  A 100 us reference quantum would be
+# all switch and drain; 1 ms is the floor.  The miss-rate threshold
 # (L2 misses per 100k work-normalised instructions, csrc/hip/hwc.cpp) is
 # calibrated on live gfx950 counters attributed by shader-engine ownership
 # (tests/test_gpu_se_hwc.py, profiles/hwc/): HBM stream
