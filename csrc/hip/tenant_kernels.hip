@@ -274,6 +274,9 @@ __device__ __forceinline__ int g2_swz(int r) { return (r >> 1) & 7; }
 // a barrier both groups passed after their counted wait.  Staging per K-tile
 // t: (t-1,k3) both B halves of t+1, (t,k0) A-half0 of t+1, (t,k1) A-half1
 // of t+1, (t,k3) both B halves of t+2 then vmcnt(4) (retires tile t+1).
+// DEEP = 3 (host bit 4): DEEP = 2 with both A halves of t+1 staged in k0 --
+// the earliest the two-phase rule allows: 1171 vs 1163 TF/s (round 2, same
+// process), so the load lead is not what limits the staggered schedule.
 // DEEP = 1 variant: all four halves of K-tile t+2 are issued in k2 (B halves)
 // and k3 (A halves) -- the earliest the WAR rule allows -- and the k3 wait is
 // vmcnt(8), so a whole K-tile stays in flight for four phases (DEEP = 0: one
@@ -350,7 +353,7 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restr
 
     // Prologue: all of tile 0, the first two halves of tile 1.
     stage(1, 0, 0); stage(0, 0, 0); stage(1, 1, 0); stage(0, 1, 0);
-    if (DEEP == 2) {
+    if (DEEP >= 2) {
       stage(1, 0, 1); stage(1, 1, 1);
       if (nt > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -365,7 +368,7 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restr
     }
     __builtin_amdgcn_s_barrier();
 
-    if (DEEP == 2 && wr == 1) __builtin_amdgcn_s_barrier();  // start half a phase behind
+    if (DEEP >= 2 && wr == 1) __builtin_amdgcn_s_barrier();  // start half a phase behind
     const int bh = wc >> 1;          // B half this wave reads
     const int bc = (wc & 1) * 64;    // its 64 columns within the half
     bf16x8 a[4][2], b0[2][2], b1[2][2];
@@ -382,7 +385,8 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restr
 #pragma unroll
         for (int s = 0; s < 2; ++s) a[i][s] = frag(buf, 0, wr, i * 16, s);
       if (DEEP == 0) stage(1, 1, t + 1);
-      if (DEEP == 2) stage(0, 0, t + 1);
+      if (DEEP >= 2) stage(0, 0, t + 1);
+      if (DEEP == 3) stage(0, 1, t + 1);  // both A halves of t+1 as early as the 2-phase WAR rule allows
       __builtin_amdgcn_s_barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_setprio(1);
@@ -418,7 +422,7 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restr
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int s = 0; s < 2; ++s) a[i][s] = frag(buf, 0, wr, 64 + i * 16, s);
-      if (DEEP != 2) stage(1, 0, t + 2);
+      if (DEEP < 2) stage(1, 0, t + 2);
       if (DEEP == 1) stage(1, 1, t + 2);
       __builtin_amdgcn_s_barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -433,7 +437,7 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restr
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_s_barrier();
       // ---- k3: quadrant (mi 1, ni 0); retire tile t+1
-      if (DEEP == 2) {
+      if (DEEP >= 2) {
         stage(1, 0, t + 2);
         stage(1, 1, t + 2);
         if (t + 2 < nt) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -460,7 +464,7 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restr
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_s_barrier();
     }
-    if (DEEP == 2 && wr == 0) __builtin_amdgcn_s_barrier();  // re-align the groups
+    if (DEEP >= 2 && wr == 0) __builtin_amdgcn_s_barrier();  // re-align the groups
     // Epilogue: mfma(B, A) holds C^T per 16x16 block -- lane owns
     // C[m = .. + l16][n = .. + 4 lq + r], r = 0..3: one 8-byte store.
 #pragma unroll
@@ -711,7 +715,10 @@ int gpbs_hip_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int
     const u32 miss = (u32)((((u64)M + N) * K * 2 / 128) / ntiles + (u64)G2_BM * G2_BM * 2 / 128);
     const u32 m2 = mode | ((g_gemm_opts & 1) ? kGemmXRange : 0u) |
                    ((g_gemm_opts & 8) && ntiles % kXcds == 0 ? kGemmBlock2D : 0u);
-    auto kern = (g_gemm_opts & 4) ? k_gemm256_bf16_tn<2> : (g_gemm_opts & 2) ? k_gemm256_bf16_tn<1> : k_gemm256_bf16_tn<0>;
+    auto kern = (g_gemm_opts & 16)  ? k_gemm256_bf16_tn<3>
+                : (g_gemm_opts & 4) ? k_gemm256_bf16_tn<2>
+                : (g_gemm_opts & 2) ? k_gemm256_bf16_tn<1>
+                                    : k_gemm256_bf16_tn<0>;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(G2_NT), 0, s, (const u16*)A, (const u16*)Bt, (u16*)C, M, N,
                        K, (WorkQueue*)q, (const PartTable*)table, m2, me, (u64*)cnt, inst, refs, miss, (u32*)status);
     return hipGetLastError() == hipSuccess ? 0 : -5;
