@@ -132,6 +132,31 @@ def hang_worker(rank: int, world: int, port: int, q, transport: str, shm_name: s
     os._exit(0)  # a gloo collective abandoned at the deadline must not block exit
 
 
+def node_worker(rank: int, world: int, name: str, q, seconds: float = 1.0, epoch_ms: float = 5.0):
+    """One of `world` node-local scheduler ranks on the native shm gang
+    transport (the 8-GPU node layout, rehearsed on CPU): every rank runs its
+    own engine with a hog and a gang tenant; returns the decision history and
+    the GANG_EPOCH records of its trace ring for the cross-rank check."""
+    from pbs_amd.core.engine import Engine
+    from pbs_amd.parallel.gang import GangCoordinator
+    e = Engine(partitions=[(rank, x) for x in range(2)], quantum_align_us=0)
+    e.tenant_create("Domain-0", nslots=1)
+    hog = e.tenant_create("hog", nslots=2)
+    coll = e.tenant_create("coll", nslots=2)
+    e.trace_set_mask(["GANG_EPOCH"])
+    e.start()
+    e.wake(hog)
+    e.wake(coll)
+    g = GangCoordinator(e, None, [coll], epoch_ms=epoch_ms, share=0.5, transport="shm", shm_name=name,
+                        rank=rank, world=world, deadline_ms=2000.0).start()
+    time.sleep(seconds)
+    g.stop()
+    recs = [r.a[1] for r in e.trace(max_records=1 << 16, from_start=True)
+            if r.event == "GANG_EPOCH" and r.a[0] == coll]
+    q.put({"rank": rank, "history": g.history, "stats": g.stats(), "trace_states": recs})
+    e.stop()
+
+
 # ---- scripts/microbench.py workers (module-level: spawn pickles them by name)
 def gang_bench_worker(rank, world, name, iters, q):
     from pbs_amd.parallel.gang import _ShmTransport
