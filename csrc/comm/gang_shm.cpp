@@ -166,9 +166,18 @@ int gpbs_gang_shm_reform(void* h, int64_t join_ns, int64_t deadline_ns, uint64_t
   R->ranks[g->rank].want.store(want, std::memory_order_release);
   uint64_t expect = want - 1;
   if (R->claim.compare_exchange_strong(expect, want, std::memory_order_acq_rel)) {
-    // master of this re-formation: the join window, then the view
+    // master of this re-formation: wait until every rank that published the
+    // epoch we timed out on (it is alive, and will time out too) has asked
+    // to join, or the join window closes; the laggard that never published
+    // that epoch is not waited for
+    const uint64_t mine = R->ranks[g->rank].seq.load(std::memory_order_acquire);
     const int64_t close_at = now_ns() + join_ns;
     while (now_ns() < close_at) {
+      bool all = true;
+      for (int k = 0; k < g->world && all; ++k)
+        if (R->ranks[k].seq.load(std::memory_order_acquire) >= mine)
+          all = R->ranks[k].want.load(std::memory_order_acquire) >= want;
+      if (all) break;
       timespec ts{0, 200000};  // 200 us
       nanosleep(&ts, nullptr);
     }

@@ -685,7 +685,54 @@ void Engine::set_affinity(Slot& v, const Mask& m, int home) {
   }
 }
 
+void Engine::place_tenant_class(Tenant& t, Pool& pl, int layout) {
+  const int c = t.cls;
+  // Class 0 (compute) lives on contexts [0, class_split) -- context 0 by
+  // default; the memory class on every other context (with two contexts
+  // per XCD: context 1).  In SE-exclusive mode (class_split 2 of 4) the
+  // classes own shader engines {0,1} and {2,3} of every XCD.  A class alone
+  // in the pool (layout = one bit) takes every context.
+  const int split = std::max(1, boot.class_split);
+  const bool alone = layout == (1 << c);
+  Mask m;
+  for (int p = pl.cpus.first(); p >= 0; p = pl.cpus.next(p + 1))
+    if (alone || (c == 0 ? parts[p]->ctx < split : parts[p]->ctx >= split)) m.set(p);
+  if (m.empty()) m = pl.cpus;
+  // Slot k goes to the k-th partition of the class (cycling), ordered
+  // context-major, so a tenant with one slot per XCD lands on every XCD
+  // instead of wherever pick_cpu's cycle from its old processor would pile
+  // them up.  Co-class tenants start where the previous one's slots end
+  // (slot counts accumulated in id order): two 16-slot GEMMs on 32 SE
+  // partitions take SEs {0,1} and {2,3}; two 8-slot memory tenants on the
+  // 16 memory partitions one SE each; a class with more slots than
+  // partitions (two 16-slot memory tenants: the time-shared variant) is
+  // staggered by context instead.
+  std::vector<int> order;
+  for (int p = m.first(); p >= 0; p = m.next(p + 1)) order.push_back(p);
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+    return std::make_tuple(parts[a]->ctx, parts[a]->gpu, parts[a]->xcd) <
+           std::make_tuple(parts[b]->ctx, parts[b]->gpu, parts[b]->xcd);
+  });
+  size_t rot = 0;
+  for (auto& up : tenants)
+    if (up && up->alive && up->priv && up->pool == pl.id && up->cls == c && up->id < t.id) rot += up->slots.size();
+  if (rot + t.slots.size() > order.size() && !order.empty()) {
+    // The class holds more slots than partitions (time-shared): stagger the
+    // tenants by whole contexts, by id, so each partition's runqueue mixes
+    // them (identical homes let one tenant's gang hold every partition).
+    const int c0 = parts[order[0]]->ctx;
+    size_t per = 0;
+    while (per < order.size() && parts[order[per]]->ctx == c0) ++per;
+    const size_t nc = order.size() / std::max<size_t>(per, 1);
+    rot = nc > 1 ? (size_t)(t.id % (int)nc) * per : 0;
+  }
+  for (size_t k = 0; k < t.slots.size(); ++k)
+    place_class(*slots[t.slots[k]], m, order.empty() ? -1 : order[(k + rot) % order.size()]);
+  emit(TRC_CLASS, 0, t.id, (uint32_t)c, (uint32_t)m.weight());
+}
+
 void Engine::classify_tick(int64_t n) {
+  std::vector<int> changed;
   for (auto& tp : tenants) {
     if (!tp || !tp->alive || !tp->priv) continue;
     Tenant& t = *tp;
@@ -732,38 +779,27 @@ void Engine::classify_tick(int64_t n) {
       continue;
     }
     t.cls = c;
-    // Class 0 (compute) lives on contexts [0, class_split) -- context 0 by
-    // default; the memory class on every other context (with two contexts
-    // per XCD: context 1).  In SE-exclusive mode (class_split 2 of 4) the
-    // classes own shader engines {0,1} and {2,3} of every XCD.
-    const int split = std::max(1, boot.class_split);
-    Mask m;
-    for (int p = pl->cpus.first(); p >= 0; p = pl->cpus.next(p + 1))
-      if (c == 0 ? parts[p]->ctx < split : parts[p]->ctx >= split) m.set(p);
-    if (m.empty()) m = pl->cpus;
-    // Slot k goes to the k-th partition of the class (cycling), ordered
-    // context-major, so a tenant with one slot per XCD lands on every XCD
-    // instead of wherever pick_cpu's cycle from its old processor would pile
-    // them up.  With several contexts in the class, tenants start on
-    // different contexts (rotation by id): co-class tenants co-reside rather
-    // than time-share one context.
-    std::vector<int> order;
-    for (int p = m.first(); p >= 0; p = m.next(p + 1)) order.push_back(p);
-    std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
-      return std::make_tuple(parts[a]->ctx, parts[a]->gpu, parts[a]->xcd) <
-             std::make_tuple(parts[b]->ctx, parts[b]->gpu, parts[b]->xcd);
-    });
-    size_t rot = 0;
-    if (!order.empty()) {
-      const int c0 = parts[order[0]]->ctx;
-      size_t per = 0;
-      while (per < order.size() && parts[order[per]]->ctx == c0) ++per;
-      const size_t nc = order.size() / std::max<size_t>(per, 1);
-      if (nc > 1) rot = (size_t)(t.id % (int)nc) * per;
+    changed.push_back(t.id);
+  }
+  // Class layout per pool: the classes present among its classified
+  // tenants.  With both present, compute owns contexts [0, class_split) and
+  // memory the rest; with one class only, that class spans every context (two
+  // GEMM tenants each take two SEs of every XCD instead of time-sharing two
+  // while the memory SEs idle -- config #2).  A layout change re-places every
+  // classified tenant of the pool; otherwise only the re-classified ones.
+  for (auto& pp : pools) {
+    if (!pp) continue;
+    Pool& pl = *pp;
+    int layout = 0;
+    for (auto& tp : tenants)
+      if (tp && tp->alive && tp->priv && tp->pool == pl.id && tp->cls >= 0) layout |= 1 << tp->cls;
+    const bool relayout = layout != pl.class_layout;
+    pl.class_layout = layout;
+    for (auto& tp : tenants) {
+      if (!tp || !tp->alive || !tp->priv || tp->pool != pl.id || tp->cls < 0) continue;
+      if (relayout || std::find(changed.begin(), changed.end(), tp->id) != changed.end())
+        place_tenant_class(*tp, pl, layout);
     }
-    for (size_t k = 0; k < t.slots.size(); ++k)
-      place_class(*slots[t.slots[k]], m, order.empty() ? -1 : order[(k + rot) % order.size()]);
-    emit(TRC_CLASS, 0, t.id, (uint32_t)c, (uint32_t)m.weight());
   }
   process_softirqs();
   timer_set(class_timer_, n + (int64_t)std::max(100, boot.class_period_us) * 1000);

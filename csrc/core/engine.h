@@ -194,6 +194,9 @@ struct Pool {
   std::string sched_name;
   Mask cpus;
   std::unique_ptr<Scheduler> sched;
+  // contention classes present among the pool's classified tenants (bit c =
+  // class c): the class layout the slots were last placed for (-1: none yet)
+  int class_layout = -1;
 };
 
 std::unique_ptr<Scheduler> make_scheduler(const std::string& name, Engine& e, int pool);
@@ -363,6 +366,7 @@ class Engine {
   void watchdog_fire(int tenant, int id);
   void watchdog_kill(Tenant& t);
   void classify_tick(int64_t now);
+  void place_tenant_class(Tenant& t, Pool& pl, int layout);
   void set_affinity(Slot& v, const Mask& m, int home = -1);
   void place_class(Slot& v, const Mask& m, int home);
   void send_home(Slot& v);

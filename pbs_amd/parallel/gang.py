@@ -212,7 +212,9 @@ class GangCoordinator:
         # survivors form a new view without the laggard and keep their gang
         # windows; False = degrade to local scheduling for good
         self.reform = bool(reform)
-        self.join_ms = float(join_ms if join_ms is not None else deadline_ms / 2)
+        # join window: the master waits at most this long for the ranks that
+        # published the failed epoch (it stops early once they all joined)
+        self.join_ms = float(join_ms if join_ms is not None else 2 * deadline_ms)
         self.reforms = 0
         self.members: List[int] = list(range(self.world))
         # K10 -> gang decision: a gang tenant gets aligned windows only while

@@ -30,6 +30,8 @@ for step in "$@"; do
                 --policies none,gpbs-ts,credit-fixed-ts,gpbs --out gpurun_out/bclean0.json ;;
     bts)     run bts 600 python bench.py --steps 20 --warmup 5 --reps 3 \
                 --policies none,gpbs-ts,credit-fixed-ts,gpbs --out gpurun_out/bts.json ;;
+    gemm2)   run gemm2 600 python bench.py --mix gemm2 --steps 20 --warmup 5 --reps 3 \
+                --policies none,static,credit-fixed,gpbs-ts,gpbs --out gpurun_out/gemm2.json ;;
     bkeep)   run bkeep 600 python bench.py --steps 20 --warmup 5 --reps 3 --keep-engines \
                 --policies none,gpbs-ts,gpbs --out gpurun_out/bkeep.json ;;
     rehearse) run rehearse 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \

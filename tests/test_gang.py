@@ -97,7 +97,8 @@ def test_eight_node_local_ranks_switch_at_the_same_epochs():
     q = ctx.Queue()
     world = 8
     name = f"gpbs-gang-node8-{os.getpid()}"
-    ps = [ctx.Process(target=node_worker, args=(r, world, name, q)) for r in range(world)]
+    ready = ctx.Barrier(world)
+    ps = [ctx.Process(target=node_worker, args=(r, world, name, q, 1.0, 5.0, ready)) for r in range(world)]
     for p in ps:
         p.start()
     out = {}

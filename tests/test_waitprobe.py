@@ -107,9 +107,7 @@ def test_descheduled_peer_produces_waits_and_atc_shrinks(lag_ms):
         assert r0["spin_latency"] >= 20 * 0.7 * lag_ms * 1e6
         # ATC: 3 ms waits (bucket 16) drive the slice to its 300 us floor
         assert r0["tslice"] == 300 and min(r0["traj"]) == 300, r0["traj"]
-        # the late rank's own waits are host scheduling noise: its slice stays
-        # above rank 0's for most of the run (a loaded host can push it down)
-        assert sum(x > 300 for x in r1["traj"]) > len(r1["traj"]) // 2, r1["traj"]
+        # (the late rank's own slice follows host scheduling noise only: not asserted)
     else:
         # only the natural arrival skew of two CPU processes (tens of us
         # each; a loaded host -- pytest -n -- adds ms-scale descheduling):
