@@ -1,7 +1,8 @@
 """Host-side race/memory checking (S12, the reference's debug=y latch and
 lockdep analog): the native engine built with AddressSanitizer and with
 ThreadSanitizer runs a credit workload -- including the real-time dispatcher
-thread against concurrent API calls and the control-page bridge -- with no
+thread against concurrent API calls, the control-page bridge with its vPMU
+mirror, and the gang shm transport through a re-formation -- with no
 sanitizer report.  CPU only; GPU sanitizers are not used."""
 import os
 import subprocess
@@ -68,8 +69,38 @@ for k in range(400):
     lib.gpbs_ctl_heartbeat(ctl, 0, k, k)
     c4[0] += 1000; lib.gpbs_ctl_set_counters(ctl, 0, c4)
     lib.gpbs_ctl_wait_gate(ctl, 0, 10000)
+    v4, mr, tsl, cl, ph, sq = (C.c_uint64 * 4)(), C.c_uint64(), C.c_uint32(), C.c_int32(), C.c_uint32(), C.c_uint32()
+    lib.gpbs_ctl_read_vpmu(ctl, 0, v4, C.byref(mr), C.byref(tsl), C.byref(cl), C.byref(ph), C.byref(sq))
 time.sleep(0.05)
 lib.gpbs_ctl_close(ctl, 1)
+# gang shm transport: three ranks as threads; rank 2 stops at epoch 20 and
+# the other two re-form the gang without it and keep exchanging
+gname = b"san-gang-%d" % os.getpid()
+gh = [C.c_void_p(lib.gpbs_gang_shm_open(gname, k, 3, 4)) for k in range(3)]
+res = {}
+def grank(k):
+    src, out = (C.c_int64 * 4)(k, k, k, k), (C.c_int64 * 12)()
+    ep, done, reforms = 1, 0, 0
+    while done < 60:
+        if k == 2 and ep == 20:
+            break
+        rc = lib.gpbs_gang_shm_allgather(gh[k], ep, src, out, time.monotonic_ns() + 300_000_000)
+        if rc == -110:
+            m, base = C.c_uint64(), C.c_uint64()
+            rc = lib.gpbs_gang_shm_reform(gh[k], 500_000_000, time.monotonic_ns() + 3_000_000_000, C.byref(m),
+                                          C.byref(base))
+            assert rc == 0 and m.value == 3, (k, rc, m.value)
+            ep, reforms = base.value, reforms + 1
+            continue
+        assert rc == 0, (k, rc)
+        ep += 1
+        done += 1
+    res[k] = (done, reforms)
+gt = [threading.Thread(target=grank, args=(k,)) for k in range(3)]
+[x.start() for x in gt]; [x.join() for x in gt]
+assert res[0] == (60, 1) and res[1] == (60, 1), res
+for h in gh[::-1]:
+    lib.gpbs_gang_shm_close(h)
 r.stop(); r.close()
 print("OK")
 """
