@@ -26,7 +26,10 @@
 // epoch.  Exchanges then wait only for members.  A rank that was left out --
 // the hung one when it comes back -- finds the view changed under it and
 // gets -116 (ESTALE) from its next exchange instead of reading epochs that
-// are not its own.
+// are not its own.  It may ask to rejoin (a re-formation it claims); the
+// members see the newer claim at their next exchange (-117) and join it.  A
+// rank dropped kMaxStrikes times stays out: a rank that keeps hanging would
+// otherwise cost the gang a deadline per cycle.
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -46,9 +49,12 @@ namespace {
 constexpr int kMaxRanks = 64;
 constexpr int kMaxVals = 128;
 
+constexpr uint32_t kMaxStrikes = 2;  // exclusions after which a rank may not rejoin
+
 struct alignas(64) RankSlot {
   std::atomic<uint64_t> seq;
-  std::atomic<uint64_t> want;  // view generation this rank asked to join
+  std::atomic<uint64_t> want;     // view generation this rank asked to join
+  std::atomic<uint32_t> strikes;  // times a published view dropped this rank
   int64_t vals[2][kMaxVals];
 };
 
@@ -121,6 +127,7 @@ int gpbs_gang_shm_allgather(void* h, uint64_t epoch, const int64_t* in, int64_t*
   Gang* g = (Gang*)h;
   if (!g || !epoch || (g->nvals && (!in || !out))) return -22;
   if (g->r->view_gen.load(std::memory_order_acquire) != g->gen) return -116;  // re-formed without us
+  if (g->r->claim.load(std::memory_order_acquire) > g->gen) return -117;     // a newer view is forming: join it
   RankSlot& me = g->r->ranks[g->rank];
   const int buf = (int)(epoch & 1);
   std::memcpy(me.vals[buf], in, sizeof(int64_t) * g->nvals);
@@ -142,6 +149,7 @@ int gpbs_gang_shm_allgather(void* h, uint64_t epoch, const int64_t* in, int64_t*
       }
       if (now_ns() > deadline_ns) return -110;
       if (g->r->view_gen.load(std::memory_order_acquire) != g->gen) return -116;
+      if (g->r->claim.load(std::memory_order_acquire) > g->gen) return -117;
       timespec ts{0, 2000};  // 2 us
       nanosleep(&ts, nullptr);
     }
@@ -162,7 +170,11 @@ int gpbs_gang_shm_reform(void* h, int64_t join_ns, int64_t deadline_ns, uint64_t
   Gang* g = (Gang*)h;
   if (!g) return -22;
   Region* R = g->r;
-  const uint64_t want = std::max(g->gen, R->view_gen.load(std::memory_order_acquire)) + 1;
+  if (R->ranks[g->rank].strikes.load(std::memory_order_acquire) >= kMaxStrikes) return -1;
+  // join the generation being formed, or claim the next one
+  const uint64_t vg0 = R->view_gen.load(std::memory_order_acquire);
+  const uint64_t cl0 = R->claim.load(std::memory_order_acquire);
+  const uint64_t want = cl0 > vg0 ? cl0 : vg0 + 1;
   R->ranks[g->rank].want.store(want, std::memory_order_release);
   uint64_t expect = want - 1;
   if (R->claim.compare_exchange_strong(expect, want, std::memory_order_acq_rel)) {
@@ -187,6 +199,10 @@ int gpbs_gang_shm_reform(void* h, int64_t join_ns, int64_t deadline_ns, uint64_t
         m |= 1ull << k;
         base = std::max<uint64_t>(base, R->ranks[k].seq.load(std::memory_order_acquire));
       }
+    const uint64_t prev_gen = R->view_gen.load(std::memory_order_acquire);
+    const uint64_t prev = prev_gen ? R->view_members.load(std::memory_order_relaxed) : all_mask(g->world);
+    for (int k = 0; k < g->world; ++k)
+      if (((prev >> k) & 1) && !((m >> k) & 1)) R->ranks[k].strikes.fetch_add(1, std::memory_order_acq_rel);
     R->view_members.store(m, std::memory_order_relaxed);
     R->view_base.store(base + 2, std::memory_order_relaxed);
     R->view_gen.store(want, std::memory_order_release);

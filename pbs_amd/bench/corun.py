@@ -359,6 +359,7 @@ class Corun:
                 # The same epochs SUM-reduce the throughput tenants' counters
                 # into node-wide metrics (C11).
                 self._gang_seq += 1  # same policy order on every rank: same fresh region name
+                self._barrier()  # every rank's engine is up before the first gang epoch (no start-up skew)
                 tr = self.cfg.gang_transport if self.cfg.gang_shm_base or self.cfg.gang_transport != "shm" else "dist"
                 self.gang = GangCoordinator(e, self.groups["gang"], [self.tid["coll"]],
                                             epoch_ms=self.cfg.gang_epoch_ms, share=self.cfg.gang_share,

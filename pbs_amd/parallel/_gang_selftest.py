@@ -108,7 +108,8 @@ def hang_worker(rank: int, world: int, port: int, q, transport: str, shm_name: s
     dist.barrier()
     t0 = time.monotonic()
     g = GangCoordinator(e, None, [coll], epoch_ms=5.0, transport=transport, shm_name=shm_name,
-                        rank=rank, world=world, deadline_ms=deadline_ms, reform=reform).start()
+                        rank=rank, world=world, deadline_ms=deadline_ms, reform=reform,
+                        start_grace_ms=deadline_ms).start()
     degraded_at = None
     # the hung rank stalls before EVERY exchange (ppm 1e6): it completes the
     # epoch the others abandoned, then misses the next one itself

@@ -58,8 +58,9 @@ of stalling every GPU's gang thread.  With ``reform=True`` (shm transport)
 the survivors then re-form: the first to claim the next view generation
 waits a join window and publishes the member set and a common first epoch
 (csrc/comm/gang_shm.cpp), so gang windows continue among the members; the
-laggard finds the view changed when it returns and stays local (C12: the
-reference moves the pool master's timers to a surviving CPU).  Epoch-start skew across ranks (the
+laggard finds the view changed when it returns and asks to rejoin (the
+members join that view at their next exchange); a rank dropped twice stays
+local (C12: the reference moves the pool master's timers to a surviving CPU).  Epoch-start skew across ranks (the
 spread of the previous epoch's return time, on the node's shared monotonic
 clock) rides the exchange and is reported in ``stats()``.
 """
@@ -122,6 +123,7 @@ class _ShmTransport:
         self.seq = 0
         self.members = list(range(world))
         self.excluded = False  # the gang re-formed without this rank
+        self.why = ""          # why the last exchange returned None: timeout / excluded / view
 
     def _gather(self, vals, deadline_ns):
         n = self.nvals
@@ -131,27 +133,31 @@ class _ShmTransport:
         out = (C.c_int64 * (n * self.world))()
         rc = self.lib.gpbs_gang_shm_allgather(C.c_void_p(self.h), self.seq, src, out, deadline_ns)
         if rc == -110:
+            self.why = "timeout"
             return None
         if rc == -116:  # a view was published without us: we were the laggard
-            self.excluded = True
+            self.excluded, self.why = True, "excluded"
+            return None
+        if rc == -117:  # a newer view is being formed (a rank asked to rejoin): join it
+            self.why = "view"
             return None
         if rc:
             raise RuntimeError(f"gang shm all-gather failed ({rc})")
         return [list(out[r * n:(r + 1) * n]) for r in self.members]
 
     def reform(self, join_ms: float, deadline_ms: float) -> Optional[int]:
-        """After a missed deadline: join the next view.  Returns the first
-        epoch of the new view (the same on every member) when this rank is a
-        member, None when it was left out or no view appeared."""
-        if self.excluded:
-            return None
+        """After a missed deadline, an exclusion (rejoin request) or a view
+        change: join the next view.  Returns the first epoch of the new view
+        (the same on every member) when this rank is a member, None when it
+        was left out, has used up its rejoins, or no view appeared."""
         m, base = C.c_uint64(0), C.c_uint64(0)
         now = time.monotonic_ns()
         rc = self.lib.gpbs_gang_shm_reform(C.c_void_p(self.h), int(join_ms * 1e6),
                                            now + int((join_ms + deadline_ms) * 1e6), C.byref(m), C.byref(base))
         if rc:
-            self.excluded = rc == -1
+            self.excluded = self.excluded or rc == -1
             return None
+        self.excluded = False
         self.members = [r for r in range(self.world) if (m.value >> r) & 1]
         self.seq = base.value - 1
         return base.value
@@ -178,7 +184,7 @@ class GangCoordinator:
                  transport: str = "dist", shm_name: Optional[str] = None, rank: Optional[int] = None,
                  world: Optional[int] = None, deadline_ms: float = 200.0, wait_driven: bool = False,
                  wait_on_frac: float = 0.02, wait_hold_epochs: int = 64, reform: bool = False,
-                 join_ms: Optional[float] = None):
+                 join_ms: Optional[float] = None, start_grace_ms: float = 2000.0):
         self.engine = engine
         self.group = group
         self.tenants = list(tenants)
@@ -206,6 +212,7 @@ class GangCoordinator:
         self.rank = rank if rank is not None else (dist.get_rank() if dist.is_initialized() else 0)
         self.world = world if world is not None else (dist.get_world_size(group) if dist.is_initialized() else 1)
         self.deadline_ns = int(deadline_ms * 1e6)
+        self.start_ns = int(max(deadline_ms, start_grace_ms) * 1e6)  # first exchange: start-up skew
         self.timeouts = 0
         self.degraded = False
         # elastic re-formation (shm transport): after a missed deadline the
@@ -314,13 +321,19 @@ class GangCoordinator:
                 vec = [1 if self.demand(t) else 0 for t in self.tenants]
                 vec += [-self._local_wait_us(t) for t in self.tenants]  # MIN of -w = -(max over ranks)
                 vec += [self._atc_local(), 0 if self._want_stop else 1, t_prev, -t_prev]
+                # the first exchange also absorbs the ranks' start-up skew
+                dl = self.deadline_ns if self.epoch else self.start_ns
                 with roctx.range(f"gpbs:gang_epoch {self.epoch}"):
-                    red = tr.reduce_min(vec, t0 + self.deadline_ns)
+                    red = tr.reduce_min(vec, t0 + dl)
                 t1 = time.monotonic_ns()
                 if red is None:
-                    self._timeout(t1 - t0)
+                    why = getattr(tr, "why", "timeout")
+                    if why == "timeout":
+                        self._timeout(t1 - t0)
                     if self._reform(tr):
                         continue
+                    if why != "timeout":  # excluded for good: recorded like a missed deadline
+                        self._timeout(t1 - t0)
                     break
                 t_prev = t1
                 self.lat_ns.append(t1 - t0)
@@ -336,9 +349,13 @@ class GangCoordinator:
                     self.engine.atc_sync(self.atc_pool, red[-4])
                 if self.metric_tenants and self.epoch % self.metric_every == 0:
                     if not self._sync_metrics(tr):
-                        self._timeout(time.monotonic_ns() - t1)
+                        why = getattr(tr, "why", "timeout")
+                        if why == "timeout":
+                            self._timeout(time.monotonic_ns() - t1)
                         if self._reform(tr):
                             continue
+                        if why != "timeout":
+                            self._timeout(time.monotonic_ns() - t1)
                         break
                 if self.wait_driven:
                     self.update_gang_on(self.epoch, [-x for x in red[nt:2 * nt]])

@@ -53,8 +53,9 @@ def test_one_hung_rank_does_not_stall_the_others(transport):
 def test_survivors_reform_the_gang_without_the_hung_rank():
     """Elastic re-formation (C12 analog): with reform=True the three ranks
     that time out on the hung one agree on a new view {0, 1, 3} and a common
-    epoch, and keep making identical gang decisions; the hung rank finds the
-    view changed when it returns and stays local."""
+    epoch, and keep making identical gang decisions.  The hung rank (it
+    stalls before EVERY exchange) rejoins once when it comes back, stalls the
+    gang again, is dropped a second time and then stays local."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
@@ -74,17 +75,20 @@ def test_survivors_reform_the_gang_without_the_hung_rank():
     survivors = [r for r in range(world) if r != hung]
     for r in survivors:
         st = out[r]["stats"]
-        # one re-formation; a host loaded by other tests can stretch an epoch
-        # past the deadline once more, which re-forms the same members again
-        assert st["timeouts"] >= 1 and st["reforms"] == st["timeouts"], st
+        # drop the hung rank, re-admit it, drop it again (a host loaded by
+        # other tests may add a hiccup re-formation; an alive laggard rejoins)
+        # (a member already waiting when a view forms joins it without a
+        # timeout of its own: at least one survivor saw each deadline)
+        assert st["reforms"] >= 3, st
         assert st["members"] == survivors, st
         assert not st["degraded"], st
-        # the gang kept running long after the reform (epochs of 5 ms over ~3 s)
-        assert out[r]["epochs"] > 200, out[r]["epochs"]
+        # the gang kept running after the re-formations (epochs of 5 ms over ~3 s)
+        assert out[r]["epochs"] > 100, out[r]["epochs"]
     # identical decisions on every member for the epochs after the reform
     hs = [dict(out[r]["history"]) for r in survivors]
     common = set(hs[0]) & set(hs[1]) & set(hs[2])
     assert len(common) >= 100
     assert all(hs[0][k] == hs[1][k] == hs[2][k] for k in common)
+    assert max(out[r]["stats"]["timeouts"] for r in survivors) >= 2
     st = out[hung]["stats"]
-    assert st["degraded"] and st["reforms"] == 0, st
+    assert st["degraded"] and st["reforms"] >= 1, st  # rejoined once, then out for good
