@@ -230,6 +230,13 @@ class Engine:
             m[p // 64] |= 1 << (p % 64)
         return self._chk(self.lib.gpbs_slot_pin(self.h, t, idx, m), "slot-pin")
 
+    def tenant_vpmu(self, t: int) -> Dict[str, int]:
+        """Cumulative counters the scheduler measured and attributed to the
+        tenant (the vPMU mirror's source): INST, CYCLES, LLC refs, LLC misses."""
+        a = (C.c_uint64 * 4)()
+        self._chk(self.lib.gpbs_tenant_vpmu(self.h, t, a), "tenant_vpmu")
+        return dict(zip(PMC_NAMES, list(a)))
+
     def tenant_info(self, t: int) -> TenantInfo:
         o = N.TenantInfo()
         self._chk(self.lib.gpbs_tenant_info(self.h, t, C.byref(o)), "tenant_info")

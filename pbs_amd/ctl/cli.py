@@ -290,12 +290,13 @@ def cmd_slot_list(c: Client, argv) -> int:
 
 def cmd_top(c: Client, argv) -> int:
     t = c.call("top")
-    print("%-20s %4s %5s %6s %9s %8s %5s %10s %8s %7s" % ("NAME", "ID", "POOL", "SLOTS", "RUN(s)", "TSLICE", "PHASE",
-                                                       "MISSRATE", "CPI", "REPORTS"))
+    print("%-20s %4s %5s %6s %9s %8s %5s %7s %10s %8s %7s %14s" % (
+        "NAME", "ID", "POOL", "SLOTS", "RUN(s)", "TSLICE", "PHASE", "CLASS", "MISSRATE", "CPI", "REPORTS", "VPMU_INST"))
     for r in t["tenants"]:
-        print("%-20s %4d %5d %3d/%-2d %9.2f %6dus %5s %10d %8d %7d" % (
+        print("%-20s %4d %5d %3d/%-2d %9.2f %6dus %5s %7s %10d %8d %7d %14d" % (
             r["name"][:20], r["id"], r["pool"], r["active"], r["slots"], r["run_s"], r["tslice_us"],
-            {1: "LOW", 2: "HIGH"}.get(r["phase"], "-"), r["miss_rate"], r["cpi"], r["reports"]))
+            {1: "LOW", 2: "HIGH"}.get(r["phase"], "-"), {0: "compute", 1: "memory"}.get(r.get("class", -1), "-"),
+            r["miss_rate"], r["cpi"], r["reports"], r.get("vpmu", {}).get("INST_RETIRED", 0)))
     busy = sum(1 for p in t["partitions"] if not p["idle"])
     print(f"partitions busy: {busy}/{len(t['partitions'])}")
     return 0

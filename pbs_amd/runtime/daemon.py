@@ -448,7 +448,9 @@ class Daemon:
             rows.append({"id": t, "name": i.name, "pool": i.pool, "slots": i.nslots, "active": i.active_slots,
                          "run_s": i.run_ns / 1e9, "tslice_us": i.tslice_us, "phase": i.phase,
                          "miss_rate": i.cache_miss_rate, "cpi": i.cpi, "pmc": dict(zip(PMC_NAMES, i.pmc)),
-                         "reports": i.report_count, "weight": i.weight, "cap": i.cap})
+                         "reports": i.report_count, "weight": i.weight, "cap": i.cap,
+                         "class": self.engine.lib.gpbs_tenant_class(self.engine.h, t),
+                         "vpmu": self.engine.tenant_vpmu(t)})
         parts = [self.engine.partition_info(p) for p in range(self.engine.num_partitions)]
         return {"now_ns": now, "tenants": rows, "partitions": parts}
 
