@@ -64,6 +64,9 @@ def main():
     ap.add_argument("--mix", default="4mix", choices=["4mix", "gemm2"],
                     help="4mix: BASELINE config #3/#4 (headline); gemm2: config #2 (two 4096^2 GEMM tenants)")
     args = ap.parse_args()
+    if os.environ.get("GPBS_HANG_DUMP_S"):  # diagnostics: every thread's stack when a run stops progressing
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["GPBS_HANG_DUMP_S"]), repeat=True)
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))

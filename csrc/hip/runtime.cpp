@@ -151,6 +151,16 @@ struct GpuCtx {
   bool adapt_pending = false;
   uint64_t adapt_late = 0;
   int se_mode = 0;  // partitions are exclusive shader engines (GATE_SE)
+  // Class-share mode (SE mode): when every tenant holding partitions is of
+  // ONE contention class, runners launch ungated full-GPU grids (co-resident:
+  // two GEMMs fill each other's MFMA stalls -- measured 1.24 co-resident vs
+  // 0.73 split over SEs) except in periodic exclusive probe windows that keep
+  // the per-tenant counters measurable (attribution skips shared intervals).
+  int share_enable = 1;
+  std::atomic<int> share{0};
+  int64_t share_ns = 0, share_since = 0;  // cumulative shared time (sampler thread)
+  uint64_t share_tick = 0;
+  int64_t snap_share = 0, share_prev = 0, share_base = 0;
   int muxed = 0;    // ops installed through the engine's backend mux
 };
 
@@ -237,6 +247,34 @@ void act_on_park(void*, int, int, int) {}
 // k-1 (normally long finished) and launches the next one on the high-priority
 // scheduler stream, so the engine lock is never held across a device sync.
 // Every counted event is reported exactly once, one metric period late.
+// Class-share decision (sampler thread, ~1 kHz): share while every distinct
+// owner in the table is classified and of one class (>= 2 owners); every 40th
+// decision opens a 4-decision exclusive probe window.
+void share_update(GpuCtx* c) {
+  int want = 0;
+  if (c->share_enable && c->se_mode && c->engine) {
+    int owners[kXcds * kCtx], n = 0;
+    for (int x = 0; x < kXcds * kCtx; ++x) {
+      const u32 o = __atomic_load_n(&c->h_table->owner[x], __ATOMIC_ACQUIRE) & kOwnerMask;
+      if (o >= (u32)kMaxTenants) continue;
+      bool seen = false;
+      for (int k = 0; k < n && !seen; ++k) seen = owners[k] == (int)o;
+      if (!seen) owners[n++] = (int)o;
+    }
+    if (n >= 2) {
+      const int c0 = gpbs_tenant_class(c->engine, owners[0]);
+      want = c0 >= 0;
+      for (int k = 1; k < n && want; ++k) want = gpbs_tenant_class(c->engine, owners[k]) == c0;
+    }
+    if (want && (c->share_tick++ % 40) < 4) want = 0;  // exclusive probe window
+  }
+  const int64_t t = mono_ns();
+  const int was = c->share.load(std::memory_order_relaxed);
+  if (was) c->share_ns += t - c->share_since;
+  c->share_since = t;
+  if (want != was) c->share.store(want, std::memory_order_release);
+}
+
 void hwc_loop(GpuCtx* c) {
   hipSetDevice(c->device);
   constexpr int kBlk = kMaxTenants * kXcds * kNumPmc;
@@ -255,6 +293,7 @@ void hwc_loop(GpuCtx* c) {
       std::lock_guard<std::mutex> g(c->mu);
       own_snapshot_locked(c, own.data());
     }
+    share_update(c);  // the interval just sampled: shared time counted up to now
     hipEventSynchronize(c->blk_ev);
     if (rc >= 0) {
       std::memcpy(blk.data(), c->h_blk, sizeof(u64) * kBlk);
@@ -263,6 +302,7 @@ void hwc_loop(GpuCtx* c) {
       c->snap_se.swap(se);
       c->snap_x.swap(xs);
       c->snap_own.swap(own);
+      c->snap_share = c->share_ns;
       c->snap_seq++;
       const int64_t dt = mono_ns() - t0;
       c->hwc_ns += dt;
@@ -319,10 +359,13 @@ void hwc_attribute(GpuCtx* c) {
   // it held the partition for clean_pct % of this interval AND of the
   // previous one, so the previous owner's workgroups (a GEMM tile drains for
   // ~0.1-0.3 ms after a revocation) have left before the interval began
+  // class-share time in the interval: kernels ran ungated on every SE, so
+  // no partition's delta is any single owner's
+  const bool shared = c->snap_share > c->share_prev;
   int clean_owner[P];
   for (int p = 0; p < P; ++p) {
     int raw = -1;
-    if (span > 0)
+    if (span > 0 && !shared)
       for (int t = 0; t < kMaxTenants; ++t)
         if (own_d[(size_t)t * P + p] * 100.0 >= span * c->clean_pct) raw = t;
     clean_owner[p] = (raw >= 0 && c->prev_raw[p] == raw) ? raw : -1;
@@ -436,6 +479,7 @@ int hwc_tenant_deltas(GpuCtx* c, int n, const int* tenants, uint64_t* out) {
       c->se_prev = c->snap_se;
       c->x_prev = c->snap_x;
       c->own_prev = c->snap_own;
+      c->share_prev = c->snap_share;
       c->hw_primed = true;
     }
   }
@@ -661,9 +705,12 @@ struct Runner {
     return se_stream[half];
   }
 
+  bool shared() const { return cfg.gate && ctx->share.load(std::memory_order_acquire); }
+
   hipStream_t pick_stream() {
     cur_grid = 0;
     const bool se = __atomic_load_n(&ctx->se_mode, __ATOMIC_ACQUIRE);
+    if (shared()) return stream;  // class-share mode: full-GPU grid, co-resident
     if (cfg.gate && se) return pick_se_stream();
     if (!ctx->spatial || !cfg.gate) return stream;
     // Masked only if every XCD the tenant holds is split and it holds the
@@ -689,9 +736,10 @@ struct Runner {
     WorkQueue* q = d_q + qi;
     const bool dev = __atomic_load_n(&ctx->table_mode, __ATOMIC_ACQUIRE) == 1;
     const void* tab = dev ? (const void*)ctx->d_table : (const void*)ctx->h_table;
-    const unsigned mode = (cfg.gate ? (cfg.gate == 2 ? GATE_PARK : GATE_TABLE) : GATE_NONE) | (dev ? GATE_DEVTABLE : 0) |
-                          (cfg.gate && ctx->spatial ? GATE_SPATIAL : 0) |
-                          (cfg.gate && __atomic_load_n(&ctx->se_mode, __ATOMIC_ACQUIRE) ? GATE_SE : 0) |
+    const bool gate = cfg.gate && !ctx->share.load(std::memory_order_acquire);
+    const unsigned mode = (gate ? (cfg.gate == 2 ? GATE_PARK : GATE_TABLE) : GATE_NONE) | (dev ? GATE_DEVTABLE : 0) |
+                          (gate && ctx->spatial ? GATE_SPATIAL : 0) |
+                          (gate && __atomic_load_n(&ctx->se_mode, __ATOMIC_ACQUIRE) ? GATE_SE : 0) |
                           (cfg.priority > 0 && ctx->waveprio ? GATE_WAVEPRIO : 0);
     const unsigned me = (unsigned)cfg.tenant;
     __atomic_store_n(&h_status[qi], 0u, __ATOMIC_RELEASE);
@@ -714,7 +762,7 @@ struct Runner {
   }
 
   bool owns_any() {
-    if (!cfg.gate) return true;
+    if (!cfg.gate || shared()) return true;
     for (int x = 0; x < kXcds * kCtx; ++x)
       if ((__atomic_load_n(&ctx->h_table->owner[x], __ATOMIC_ACQUIRE) & kOwnerMask) == (u32)cfg.tenant) return true;
     return false;
@@ -865,6 +913,7 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
   std::memset(c->own_ns, 0, sizeof(c->own_ns));
   std::memset(c->own_base, 0, sizeof(c->own_base));
   for (int& r : c->prev_raw) r = -1;
+  if (const char* v = std::getenv("GPBS_SHARE")) c->share_enable = std::atoi(v) != 0;
   if (const char* v = std::getenv("GPBS_HWC_CLEAN")) c->clean_pct = std::max(0, std::min(100, std::atoi(v)));
   bool ok = hipHostMalloc((void**)&c->h_table, sizeof(PartTable), hipHostMallocCoherent | hipHostMallocMapped) ==
             hipSuccess;
@@ -1014,6 +1063,7 @@ int gpbs_gpu_set_hwc(void* p, int on) {
     c->hwc_stop = true;
     c->hwc_th.join();
   }
+  c->share.store(0, std::memory_order_release);  // the sampler decides class sharing: none without it
   std::lock_guard<std::mutex> g(c->mu);
   c->hwc = on ? 1 : 0;
   c->hw_primed = false;
@@ -1108,6 +1158,7 @@ int gpbs_gpu_hwc_poll(void* p) {
   c->se_prev = c->snap_se;
   c->x_prev = c->snap_x;
   c->own_prev = c->snap_own;
+  c->share_prev = c->snap_share;
   c->hw_primed = true;
   return 1;
 }
@@ -1123,6 +1174,7 @@ int gpbs_gpu_hwc_reset(void* p) {
   std::memset(c->unatt, 0, sizeof(c->unatt));
   std::memset(c->metric_sum, 0, sizeof(c->metric_sum));
   std::memset(c->met_total, 0, sizeof(c->met_total));
+  c->share_base = c->snap_share;
   c->hwc_ns = c->hwc_ns_max = 0;
   c->hwc_samples = 0;
   return 0;
@@ -1130,10 +1182,29 @@ int gpbs_gpu_hwc_reset(void* p) {
 
 // SE-exclusive partitions: the nctx (= 4) partitions of an XCD are its shader
 // engines; gated tenant kernels run only on SEs their tenant owns.
+// Class-share mode on/off (default on; GPBS_SHARE=0 disables at creation).
+// Returns the previous setting; *share_ns (optional) = cumulative time in
+// class-share mode since the last hwc reset.
+int gpbs_gpu_set_share(void* p, int on, int64_t* share_ns) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c) return -22;
+  const int old = c->share_enable;
+  if (on >= 0) {
+    c->share_enable = on ? 1 : 0;
+    if (!on) c->share.store(0, std::memory_order_release);
+  }
+  if (share_ns) {
+    std::lock_guard<std::mutex> g(c->snap_mu);
+    *share_ns = c->snap_share - c->share_base;
+  }
+  return old;
+}
+
 int gpbs_gpu_set_se_mode(void* p, int on) {
   GpuCtx* c = (GpuCtx*)p;
   if (!c) return -22;
   __atomic_store_n(&c->se_mode, on ? 1 : 0, __ATOMIC_RELEASE);
+  if (!on) c->share.store(0, std::memory_order_release);  // class sharing exists only over SE partitions
   return 0;
 }
 

@@ -140,6 +140,8 @@ POLICY_ENGINES = {
     # time-shared variant: the memory tenants hold slots on all memory SEs
     # {2,3} and alternate on them as one gang under credit with PBS's
     # adaptive quanta (credit-fixed-ts: fixed quantum)
+    # ablation: SE-exclusive even when every tenant is of one class
+    "gpbs-noshare": (4, dict(SE_OVERRIDES), True, "device,se,waveprio,latco,se8,noshare"),
     "gpbs-ts": (4, dict(SE_OVERRIDES), True, "device,se,waveprio,latco"),
     "credit-fixed-ts": (4, dict(SE_OVERRIDES, sched="credit-fixed"), True, "device,se,waveprio,latco"),
     "credit2": (4, dict(SE_OVERRIDES, sched="credit2"), True, "device,se,waveprio,latco"),
@@ -339,6 +341,7 @@ class Corun:
             self.ctx.set_spatial("spatial" in opts)
             self.ctx.set_se_mode("se" in opts)
             self.ctx.set_waveprio("waveprio" in opts)
+            self.ctx.set_share("noshare" not in opts)
             self.ctx.attach(e, nctx=e._gpbs_nctx)
             if self.cfg.hw_counters:
                 self.ctx.set_hwc(True)
@@ -374,6 +377,7 @@ class Corun:
         self.ctx.set_table_mode("host")
         self.ctx.set_spatial(False)
         self.ctx.set_se_mode(False)
+        self.ctx.set_share(False)
         self.ctx.set_waveprio(False)
         if self.cfg.hw_counters:
             self.ctx.set_hwc(False)
@@ -648,6 +652,7 @@ class Corun:
             eng["gpu"] = self.ctx.stats()
             if self.cfg.hw_counters:
                 eng["hwc"] = self.ctx.hwc_stats()
+                eng["hwc"]["share_frac"] = round(self.ctx.share_ns() / (wall_ms * 1e6), 4)
                 # Hardware-derived PBS metrics per tenant over the timed window
                 # (ownership-attributed counts): L2 misses and L2 requests per
                 # 100k instructions, cycles per 1k instructions.

@@ -62,6 +62,7 @@ def bind(lib):
     _p(lib, "gpbs_gpu_hwc_reset", C.c_int, vp)
     _p(lib, "gpbs_gpu_hwc_clean", C.c_int, vp, C.c_int, C.POINTER(C.c_double))
     _p(lib, "gpbs_gpu_hwc_tenant_metric", C.c_int, vp, C.c_int, C.POINTER(C.c_double))
+    _p(lib, "gpbs_gpu_set_share", C.c_int, vp, C.c_int, C.POINTER(C.c_int64))
     _p(lib, "gpbs_gpu_hwc_poll", C.c_int, vp)
     _p(lib, "gpbs_gpu_set_se_mode", C.c_int, vp, C.c_int)
     _p(lib, "gpbs_hip_rmsnorm_bf16", C.c_int, vp, vp, vp, C.c_int, C.c_int, C.c_float, vp)

@@ -134,6 +134,18 @@ class GpuContext:
                 # exclusive-ownership windows: share of the counts that reached the PBS metric
                 "clean_pct": pct, "metric_frac": [round(x, 4) for x in cf]}
 
+    def set_share(self, on: bool) -> int:
+        """Class-share mode (SE mode): co-resident full-GPU grids while every
+        partition owner is of one contention class, with periodic exclusive
+        probe windows (needs the live-counter sampler).  Returns the old value."""
+        return self.L.gpbs_gpu_set_share(self.h, 1 if on else 0, None)
+
+    def share_ns(self) -> int:
+        """Time spent in class-share mode since the last hwc reset (ns)."""
+        v = C.c_int64(0)
+        self.L.gpbs_gpu_set_share(self.h, -1, C.byref(v))
+        return v.value
+
     def set_hwc_clean(self, pct: int) -> int:
         """Exclusive-ownership window: a partition's counter delta reaches the
         PBS metric only when one tenant owned it >= pct % of the sample

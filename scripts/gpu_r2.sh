@@ -31,10 +31,10 @@ for step in "$@"; do
     bts)     run bts 600 python bench.py --steps 20 --warmup 5 --reps 3 \
                 --policies none,gpbs-ts,credit-fixed-ts,gpbs --out gpurun_out/bts.json ;;
     gemm2)   run gemm2 600 python bench.py --mix gemm2 --steps 20 --warmup 5 --reps 3 \
-                --policies none,static,credit-fixed,gpbs-ts,gpbs --out gpurun_out/gemm2.json ;;
+                --policies none,static,gpbs-noshare,gpbs --out gpurun_out/gemm2.json ;;
     bkeep)   run bkeep 600 python bench.py --steps 20 --warmup 5 --reps 3 --keep-engines \
                 --policies none,gpbs-ts,gpbs --out gpurun_out/bkeep.json ;;
-    rehearse) run rehearse 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+    rehearse) GPBS_HANG_DUMP_S=${GPBS_HANG_DUMP_S:-45} run rehearse 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
                 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 1 --reps 1 --rehearse --policies none,gpbs \
                 --out gpurun_out/rehearse.json ;;
     roctx)   export GPBS_ROCTX=1
