@@ -766,6 +766,9 @@ void Engine::classify_tick(int64_t n) {
         }
         return n;
       };
+      uint32_t home_ctx = 0;  // contexts (shader engines) the tenant's class homes use
+      for (int sid : t.slots)
+        if (slots[sid]->class_home >= 0) home_ctx |= 1u << (parts[slots[sid]->class_home]->ctx & 31);
       for (size_t k = 0; k < t.slots.size(); ++k) {
         Slot& v = *slots[t.slots[k]];
         if (!runnable(v) || v.class_home < 0 || v.processor == v.class_home) continue;
@@ -774,7 +777,39 @@ void Engine::classify_tick(int64_t n) {
         const bool stray = !v.is_running && !v.soft.empty() && !v.soft.test(v.processor);
         const int here = on_xcd(v.processor, k), there = on_xcd(v.class_home, k);
         const bool foreign = P.gpu != H.gpu || P.xcd != H.xcd;
-        if (stray || (foreign && (there < here || (there == 0 && here == 0)))) send_home(v);
+        // SE-exclusive mode: a slot on a shader engine outside its tenant's
+        // home SEs is misplaced even when its XCD holds the right number of
+        // the tenant's slots -- the runner's CU-masked stream covers one
+        // class half ({0,1} or {2,3}), so a tenant holding SEs {0,3}
+        // launches unmasked and its workgroups queue behind the other
+        // owner's SEs (config #2 measured 0.73 vs 1.26 under none).  It goes
+        // to a home partition none of its siblings occupies, preferably on
+        // its own XCD, trading homes with the sibling that partition was
+        // home to (homes stay one per partition).
+        bool wrong_se = false;
+        if (boot.class_split > 1 && !((home_ctx >> P.ctx) & 1)) {
+          auto occupied = [&](int part) {
+            for (size_t j = 0; j < t.slots.size(); ++j)
+              if (j != k && runnable(*slots[t.slots[j]]) && slots[t.slots[j]]->processor == part) return true;
+            return false;
+          };
+          int target = -1;
+          size_t owner = k;
+          for (size_t j = 0; j < t.slots.size(); ++j) {
+            const int hp = slots[t.slots[j]]->class_home;
+            if (hp < 0 || occupied(hp)) continue;
+            const bool local = parts[hp]->gpu == P.gpu && parts[hp]->xcd == P.xcd;
+            if (target < 0 || (local && !(parts[target]->gpu == P.gpu && parts[target]->xcd == P.xcd))) {
+              target = hp;
+              owner = j;
+            }
+          }
+          if (target >= 0) {
+            if (owner != k) std::swap(slots[t.slots[owner]]->class_home, v.class_home);
+            wrong_se = true;
+          }
+        }
+        if (stray || wrong_se || (foreign && (there < here || (there == 0 && here == 0)))) send_home(v);
       }
       continue;
     }

@@ -160,6 +160,7 @@ struct GpuCtx {
   std::atomic<int> share{0};
   int64_t share_ns = 0, share_since = 0;  // cumulative shared time (sampler thread)
   uint64_t share_tick = 0;
+  int probe_every = 40, probe_len = 4;  // GPBS_SHARE_PROBE="every:len" (every 0: no probe windows)
   int64_t snap_share = 0, share_prev = 0, share_base = 0;
   int muxed = 0;    // ops installed through the engine's backend mux
 };
@@ -266,7 +267,8 @@ void share_update(GpuCtx* c) {
       want = c0 >= 0;
       for (int k = 1; k < n && want; ++k) want = gpbs_tenant_class(c->engine, owners[k]) == c0;
     }
-    if (want && (c->share_tick++ % 40) < 4) want = 0;  // exclusive probe window
+    if (want && c->probe_every > 0 && (c->share_tick++ % (uint64_t)c->probe_every) < (uint64_t)c->probe_len)
+      want = 0;  // exclusive probe window
   }
   const int64_t t = mono_ns();
   const int was = c->share.load(std::memory_order_relaxed);
@@ -914,6 +916,11 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
   std::memset(c->own_base, 0, sizeof(c->own_base));
   for (int& r : c->prev_raw) r = -1;
   if (const char* v = std::getenv("GPBS_SHARE")) c->share_enable = std::atoi(v) != 0;
+  if (const char* v = std::getenv("GPBS_HWC_PERIOD_US")) c->hwc_period_us = std::max(100, std::atoi(v));
+  if (const char* v = std::getenv("GPBS_SHARE_PROBE")) {
+    c->probe_every = std::max(0, std::atoi(v));
+    if (const char* k = std::strchr(v, ':')) c->probe_len = std::max(0, std::atoi(k + 1));
+  }
   if (const char* v = std::getenv("GPBS_HWC_CLEAN")) c->clean_pct = std::max(0, std::min(100, std::atoi(v)));
   bool ok = hipHostMalloc((void**)&c->h_table, sizeof(PartTable), hipHostMallocCoherent | hipHostMallocMapped) ==
             hipSuccess;

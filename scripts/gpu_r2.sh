@@ -32,6 +32,14 @@ for step in "$@"; do
                 --policies none,gpbs-ts,credit-fixed-ts,gpbs --out gpurun_out/bts.json ;;
     gemm2)   run gemm2 600 python bench.py --mix gemm2 --steps 20 --warmup 5 --reps 3 \
                 --policies none,static,gpbs-noshare,gpbs --out gpurun_out/gemm2.json ;;
+    gemm2m)  run gemm2m 600 python bench.py --mix gemm2 --steps 20 --warmup 5 --reps 2 --counters model \
+                --policies none,gpbs-noshare,gpbs --out gpurun_out/gemm2m.json ;;
+    gemm2np) GPBS_SHARE_PROBE=0 run gemm2np 600 python bench.py --mix gemm2 --steps 20 --warmup 5 --reps 2 \
+                --policies none,gpbs --out gpurun_out/gemm2np.json ;;
+    hwcper) for per in ${HWC_PERIODS:-1000 4000 10000}; do
+               GPBS_HWC_PERIOD_US=$per run hwcper_$per 600 python bench.py --mix ${HWC_MIX:-gemm2} --steps 20 --warmup 5 \
+                 --reps 2 --policies ${HWC_POLICIES:-none,gpbs} --out gpurun_out/hwcper_${HWC_MIX:-gemm2}_$per.json
+             done ;;
     bkeep)   run bkeep 600 python bench.py --steps 20 --warmup 5 --reps 3 --keep-engines \
                 --policies none,gpbs-ts,gpbs --out gpurun_out/bkeep.json ;;
     rehearse) GPBS_HANG_DUMP_S=${GPBS_HANG_DUMP_S:-45} run rehearse 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \

@@ -85,7 +85,7 @@ def grank(k):
         if k == 2 and ep == 20:
             break
         rc = lib.gpbs_gang_shm_allgather(gh[k], ep, src, out, time.monotonic_ns() + 300_000_000)
-        if rc == -110:
+        if rc in (-110, -117):  # deadline missed, or a peer already claimed the re-formation
             m, base = C.c_uint64(), C.c_uint64()
             rc = lib.gpbs_gang_shm_reform(gh[k], 500_000_000, time.monotonic_ns() + 3_000_000_000, C.byref(m),
                                           C.byref(base))

@@ -104,3 +104,27 @@ def test_idle_sample_rule_keeps_memory_bound_quantum():
     # feeding them (reference semantics) keeps knocking it down
     assert q1 == MI355X_PROFILE["adapt"]["max_us"], q1
     assert q0 < q1, (q0, q1)
+
+
+def test_se_mode_two_compute_tenants_take_aligned_halves():
+    """Config #2 (two GEMM tenants, one class alone in the pool): each tenant
+    ends on one class half -- SEs {0,1} or {2,3} of every XCD -- so its
+    runner's CU-masked stream covers exactly what it owns.  Before the
+    wrong-SE rule the credit dynamics settled at {0,3} / {1,2} (the XCD
+    counts were right, so nothing moved them), and both runners launched
+    unmasked full-GPU grids that queued behind the other's SEs (0.73 vs 1.26
+    solo-equivalents under plain sharing on MI355X)."""
+    e, parts = _se_engine()
+    a = e.tenant_create("gemm", nslots=16)
+    b = e.tenant_create("gemm_b", nslots=16)
+    rates = {a: (1000, 1), b: (1000, 1)}
+    e.wake(a)
+    e.wake(b)
+    for _ in range(300):
+        _feed(e, rates, 100)
+    ctx = {p: c for p, (_, _, c) in enumerate(parts)}
+    halves = [{ctx[p] // 2 for p in _procs(e, t)} for t in (a, b)]
+    assert all(len(h) == 1 for h in halves) and halves[0] != halves[1], halves
+    for t in (a, b):  # one slot per (XCD, SE) of the half
+        assert len(set(_procs(e, t))) == 16
+    assert e.check() == ""
