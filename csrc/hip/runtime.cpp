@@ -127,6 +127,15 @@ struct GpuCtx {
   std::atomic<bool> hwc_stop{false};
   std::mutex snap_mu;
   int hwc_period_us = 1000;
+  // Adaptive sampling: every device-counting sample perturbs the tenants
+  // (measured on MI355X: two GEMM tenants 1.09 solo-equivalents sampled every
+  // 1 ms, 1.23 every 4 ms, 1.23 every 10 ms; none 1.25-1.27 without a
+  // sampler, profiles/corun_r2/hwc_period.md).  While the partition table is
+  // changing (time-sharing, re-placement) the sampler runs every
+  // hwc_period_us, so exclusive-ownership windows stay short; once no owner
+  // has changed for 20 ms it backs off to hwc_slow_us.
+  int hwc_slow_us = 4000;  // GPBS_HWC_SLOW_US (0: never back off)
+  std::atomic<uint64_t> hwc_slow_samples{0};
   int64_t hwc_ns = 0, hwc_ns_max = 0;
   uint64_t hwc_samples = 0;
   double hw_sum[kNumPmc] = {}, model_sum[kNumPmc] = {};  // attributed vs modeled totals
@@ -153,10 +162,12 @@ struct GpuCtx {
   int se_mode = 0;  // partitions are exclusive shader engines (GATE_SE)
   // Class-share mode (SE mode): when every tenant holding partitions is of
   // ONE contention class, runners launch ungated full-GPU grids (co-resident:
-  // two GEMMs fill each other's MFMA stalls -- measured 1.24 co-resident vs
-  // 0.73 split over SEs) except in periodic exclusive probe windows that keep
-  // the per-tenant counters measurable (attribution skips shared intervals).
-  int share_enable = 1;
+  // two GEMMs fill each other's MFMA stalls) except in periodic exclusive
+  // probe windows that keep the per-tenant counters measurable (attribution
+  // skips shared intervals).  Opt-in: it was written against a misaligned
+  // split (0.73); with co-class tenants on aligned SE halves and the
+  // adaptive sampler the split measured 1.253 vs 1.240 shared (none 1.252).
+  int share_enable = 0;
   std::atomic<int> share{0};
   int64_t share_ns = 0, share_since = 0;  // cumulative shared time (sampler thread)
   uint64_t share_tick = 0;
@@ -284,6 +295,9 @@ void hwc_loop(GpuCtx* c) {
   std::vector<u64> blk(kBlk), se(kXcds * kCtx * kNumPmc), xs(kXcds * kNumPmc);
   std::vector<int64_t> own(kOwn);
   roctxNameOsThread("gpbs-hwc-sampler");
+  constexpr int64_t kSteadyNs = 20000000;  // no owner change for 20 ms: back off
+  uint64_t last_sw = c->flushes.load();
+  int64_t last_change = mono_ns();
   while (!c->hwc_stop.load(std::memory_order_acquire)) {
     const int64_t t0 = mono_ns();
     RoctxRange rr("gpbs:hwc_sample");
@@ -311,7 +325,13 @@ void hwc_loop(GpuCtx* c) {
       if (dt > c->hwc_ns_max) c->hwc_ns_max = dt;
       c->hwc_samples++;
     }
-    const int64_t rest = (int64_t)c->hwc_period_us * 1000 - (mono_ns() - t0);
+    const uint64_t sw = c->flushes.load(std::memory_order_relaxed);  // table publishes that changed an owner
+    const int64_t now = mono_ns();
+    if (sw != last_sw) last_change = now;
+    last_sw = sw;
+    const bool slow = c->hwc_slow_us > c->hwc_period_us && now - last_change >= kSteadyNs;
+    if (slow) c->hwc_slow_samples.fetch_add(1, std::memory_order_relaxed);
+    const int64_t rest = (int64_t)(slow ? c->hwc_slow_us : c->hwc_period_us) * 1000 - (mono_ns() - t0);
     if (rest > 0) std::this_thread::sleep_for(std::chrono::nanoseconds(rest));
   }
 }
@@ -917,6 +937,7 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
   for (int& r : c->prev_raw) r = -1;
   if (const char* v = std::getenv("GPBS_SHARE")) c->share_enable = std::atoi(v) != 0;
   if (const char* v = std::getenv("GPBS_HWC_PERIOD_US")) c->hwc_period_us = std::max(100, std::atoi(v));
+  if (const char* v = std::getenv("GPBS_HWC_SLOW_US")) c->hwc_slow_us = std::max(0, std::atoi(v));
   if (const char* v = std::getenv("GPBS_SHARE_PROBE")) {
     c->probe_every = std::max(0, std::atoi(v));
     if (const char* k = std::strchr(v, ':')) c->probe_len = std::max(0, std::atoi(k + 1));
@@ -1184,12 +1205,25 @@ int gpbs_gpu_hwc_reset(void* p) {
   c->share_base = c->snap_share;
   c->hwc_ns = c->hwc_ns_max = 0;
   c->hwc_samples = 0;
+  c->hwc_slow_samples = 0;
+  return 0;
+}
+
+// Sampler cadence: fast and steady-state periods (us, < 0 leaves them), and
+// *slow_samples = samples taken at the steady-state period since the last
+// hwc reset.
+int gpbs_gpu_hwc_period(void* p, int fast_us, int slow_us, uint64_t* slow_samples) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c) return -22;
+  if (fast_us >= 0) c->hwc_period_us = std::max(100, fast_us);
+  if (slow_us >= 0) c->hwc_slow_us = slow_us;
+  if (slow_samples) *slow_samples = c->hwc_slow_samples;
   return 0;
 }
 
 // SE-exclusive partitions: the nctx (= 4) partitions of an XCD are its shader
 // engines; gated tenant kernels run only on SEs their tenant owns.
-// Class-share mode on/off (default on; GPBS_SHARE=0 disables at creation).
+// Class-share mode on/off (default off; GPBS_SHARE=1 enables at creation).
 // Returns the previous setting; *share_ns (optional) = cumulative time in
 // class-share mode since the last hwc reset.
 int gpbs_gpu_set_share(void* p, int on, int64_t* share_ns) {

@@ -140,8 +140,12 @@ POLICY_ENGINES = {
     # time-shared variant: the memory tenants hold slots on all memory SEs
     # {2,3} and alternate on them as one gang under credit with PBS's
     # adaptive quanta (credit-fixed-ts: fixed quantum)
-    # ablation: SE-exclusive even when every tenant is of one class
-    "gpbs-noshare": (4, dict(SE_OVERRIDES), True, "device,se,waveprio,latco,se8,noshare"),
+    # ablation: class-share mode -- while every owner is of one class the
+    # runners launch co-resident full-GPU grids (exclusive probe windows keep
+    # the counters measurable).  Config #2 measured it at or below the plain
+    # class-half split once co-class tenants hold aligned halves (1.240 vs
+    # 1.253, none 1.252), so the flagship does not share.
+    "gpbs-share": (4, dict(SE_OVERRIDES), True, "device,se,waveprio,latco,se8,share"),
     "gpbs-ts": (4, dict(SE_OVERRIDES), True, "device,se,waveprio,latco"),
     "credit-fixed-ts": (4, dict(SE_OVERRIDES, sched="credit-fixed"), True, "device,se,waveprio,latco"),
     "credit2": (4, dict(SE_OVERRIDES, sched="credit2"), True, "device,se,waveprio,latco"),
@@ -341,7 +345,7 @@ class Corun:
             self.ctx.set_spatial("spatial" in opts)
             self.ctx.set_se_mode("se" in opts)
             self.ctx.set_waveprio("waveprio" in opts)
-            self.ctx.set_share("noshare" not in opts)
+            self.ctx.set_share("share" in opts)
             self.ctx.attach(e, nctx=e._gpbs_nctx)
             if self.cfg.hw_counters:
                 self.ctx.set_hwc(True)

@@ -57,6 +57,7 @@ def bind(lib):
     _p(lib, "gpbs_gpu_hwc_stats", C.c_int, vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_double))
     _p(lib, "gpbs_hwc_sample_se", C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64))
     _p(lib, "gpbs_hwc_slot_per_se", C.c_int, C.c_int)
+    _p(lib, "gpbs_gpu_hwc_period", C.c_int, vp, C.c_int, C.c_int, C.POINTER(C.c_uint64))
     _p(lib, "gpbs_gpu_hwc_quality", C.c_int, vp, C.POINTER(C.c_uint64), C.POINTER(C.c_double), C.POINTER(C.c_int))
     _p(lib, "gpbs_gpu_hwc_tenant", C.c_int, vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double))
     _p(lib, "gpbs_gpu_hwc_reset", C.c_int, vp)

@@ -127,12 +127,20 @@ class GpuContext:
         self.L.gpbs_gpu_hwc_quality(self.h, C.byref(mx), u, C.byref(sem))
         cf = (C.c_double * 4)()
         pct = self.L.gpbs_gpu_hwc_clean(self.h, -1, cf)
-        return {"samples": n.value, "mean_sample_us": round(ns.value / 1e3, 1), "max_sample_us": round(mx.value / 1e3, 1),
+        slow = C.c_uint64(0)
+        self.L.gpbs_gpu_hwc_period(self.h, -1, -1, C.byref(slow))
+        return {"samples": n.value, "slow_samples": slow.value, "mean_sample_us": round(ns.value / 1e3, 1), "max_sample_us": round(mx.value / 1e3, 1),
                 "hw_over_model": [round(x, 4) for x in r],
                 "unattributed_frac": [round(x, 4) for x in u],
                 "attribution": "exact-se" if sem.value & 1 else "xcd-time-share",
                 # exclusive-ownership windows: share of the counts that reached the PBS metric
                 "clean_pct": pct, "metric_frac": [round(x, 4) for x in cf]}
+
+    def set_hwc_period(self, fast_us: int = -1, slow_us: int = -1):
+        """Counter sampler cadence: every fast_us while the partition table is
+        changing, every slow_us once no owner has changed for 20 ms (0: no
+        back-off).  Each device-counting sample perturbs the tenants."""
+        self.L.gpbs_gpu_hwc_period(self.h, int(fast_us), int(slow_us), None)
 
     def set_share(self, on: bool) -> int:
         """Class-share mode (SE mode): co-resident full-GPU grids while every

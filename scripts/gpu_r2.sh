@@ -31,9 +31,9 @@ for step in "$@"; do
     bts)     run bts 600 python bench.py --steps 20 --warmup 5 --reps 3 \
                 --policies none,gpbs-ts,credit-fixed-ts,gpbs --out gpurun_out/bts.json ;;
     gemm2)   run gemm2 600 python bench.py --mix gemm2 --steps 20 --warmup 5 --reps 3 \
-                --policies none,static,gpbs-noshare,gpbs --out gpurun_out/gemm2.json ;;
+                --policies none,static,gpbs-share,gpbs --out gpurun_out/gemm2.json ;;
     gemm2m)  run gemm2m 600 python bench.py --mix gemm2 --steps 20 --warmup 5 --reps 2 --counters model \
-                --policies none,gpbs-noshare,gpbs --out gpurun_out/gemm2m.json ;;
+                --policies none,gpbs-share,gpbs --out gpurun_out/gemm2m.json ;;
     gemm2np) GPBS_SHARE_PROBE=0 run gemm2np 600 python bench.py --mix gemm2 --steps 20 --warmup 5 --reps 2 \
                 --policies none,gpbs --out gpurun_out/gemm2np.json ;;
     hwcper) for per in ${HWC_PERIODS:-1000 4000 10000}; do
