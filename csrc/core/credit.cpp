@@ -191,7 +191,16 @@ class CreditScheduler : public Scheduler {
 
   int init_domain(Tenant& d) override {
     auto s = std::make_unique<CDom>();
-    adapt_init(s->adapt, E.adapt_params, mode_ == Mode::FIXED ? tslice_us_ : 100);
+    // The reference starts every domain at 100 us (csched_dom_init :1217),
+    // its profile's floor.  Q15: under a profile whose floor is higher (MI355X:
+    // 1 ms) that start value sat below the floor, and a tenant whose miss rate
+    // never settled into the stable band kept it -- neither the window nor the
+    // unstable branch decrements a memory-bound tenant, and only dec() clamps
+    // -- so a time-shared HBM tenant ran 100 us quanta that were all switch
+    // and drain (0.05 of solo next to a reduce-copy tenant at 11 ms quanta).
+    // Start at the floor when it is above 100 us.
+    const uint32_t q0 = std::max<uint32_t>(100, E.adapt_params.min_us);
+    adapt_init(s->adapt, E.adapt_params, mode_ == Mode::FIXED ? tslice_us_ : q0);
     atc_init(s->atc, E.atc_params);
     d.priv = std::move(s);
     return 0;
