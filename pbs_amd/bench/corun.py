@@ -64,7 +64,7 @@ import statistics
 import threading
 import time
 from dataclasses import dataclass
-from typing import Dict, Optional
+from typing import Callable, Dict, Optional
 
 import torch
 
@@ -163,6 +163,49 @@ POLICY_ENGINES = {
 }
 
 
+class AgreedLoop:
+    """Runs ``body`` (one collective) back to back on a thread until stopped.
+    Every rank must issue the same number of collectives, but each rank's
+    main thread raises its stop at a slightly different moment: a rank that
+    starts collective k+1 just before its stop while a peer stopped after k
+    would wait in it forever (and so would the join).  The stop is therefore
+    agreed on a count: freeze the issue limit at this rank's count, take the
+    MAX over ranks (``agree``, e.g. an all-reduce on the ctrl group), and let
+    every rank issue up to it before the thread ends."""
+
+    def __init__(self, body: Callable[[], object]):
+        self.body = body
+        self.cv = threading.Condition()
+        self.issued, self.limit, self.stopping = 0, None, False
+        self.th = threading.Thread(target=self._run, daemon=True)
+
+    def start(self) -> "AgreedLoop":
+        self.th.start()
+        return self
+
+    def _run(self):
+        while True:
+            with self.cv:
+                while self.limit is not None and self.issued >= self.limit and not self.stopping:
+                    self.cv.wait()
+                if self.limit is not None and self.issued >= self.limit:
+                    return
+                self.issued += 1
+            self.body()
+
+    def stop(self, agree: Optional[Callable[[int], int]] = None) -> int:
+        """Stop after the agreed count; returns it."""
+        with self.cv:
+            self.limit = self.issued  # no new collective past this rank's count
+            mine = self.issued
+        target = max(int(agree(mine)) if agree is not None else mine, mine)
+        with self.cv:
+            self.limit, self.stopping = target, True
+            self.cv.notify_all()
+        self.th.join()
+        return target
+
+
 class CollTenant:
     """All-reduce tenant for N > 1: RCCL all-reduce over xGMI on its own
     process group and stream, launch-gated on XCD ownership (RCCL kernels
@@ -218,19 +261,13 @@ class CollTenant:
             self.board.close()
             self.board = None
 
-    # steady-state protocol: all-reduce back to back until stopped
+    # steady-state protocol: all-reduce back to back until stopped, the stop
+    # agreed on a collective count across ranks (AgreedLoop)
     def start_loop(self):
-        self._stop = threading.Event()
-        self._th = threading.Thread(target=self._loop, daemon=True)
-        self._th.start()
+        self._loop = AgreedLoop(lambda: self.run_units(1)).start()
 
-    def _loop(self):
-        while not self._stop.is_set():
-            self.run_units(1)
-
-    def stop_loop(self):
-        self._stop.set()
-        self._th.join()
+    def stop_loop(self, agree: Optional[Callable[[int], int]] = None):
+        self._loop.stop(agree)
 
 
 def _pct(xs, q):
@@ -565,7 +602,7 @@ class Corun:
             if isinstance(r, Runner):
                 r.cancel()
         if isinstance(coll, CollTenant):
-            coll.stop_loop()
+            coll.stop_loop(agree=lambda n: int(self._allreduce(float(n), "max")))
         for name in self.throughput:
             r = self.runners[name]
             if isinstance(r, Runner):
