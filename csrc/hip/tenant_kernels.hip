@@ -482,6 +482,139 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restr
   finish(q, status, (u32)ntiles);
 }
 
+// ------------------------------------------------ GEMM 256x256, 4 waves ----
+// The shape hipBLASLt picks for this GEMM on gfx950 (rocprofv3 kernel trace of
+// torch.mm 4096^3, profiles/kbench_r2_w4.md: MT256x256x64, MI16x16, 256
+// threads, 130 KiB LDS, one wave per SIMD).  Four waves as 2(M) x 2(N),
+// 128x128 per wave = 8x8 blocks of 16x16x32 (256 accumulator registers,
+// AGPRs), so a wave reads 32 KiB of fragments per K-tile: 128 KiB per CU
+// instead of the 8-wave kernel's 8 x 24 KiB, and ONE barrier per K-tile
+// instead of eight.  With one wave per SIMD there is no partner to cover LDS
+// latency, so the wave covers it itself: the fragments of the next K-substep
+// go into the other register set while this substep's 64 MFMAs run.
+// Per K-tile t (LDS buffer t&1; set X = substep (t, 0) already read):
+//   read (t, 1) -> Y;  64 MFMA on X;  lgkmcnt(0), vmcnt(0) (tile t+1 landed);
+//   s_barrier (every wave done with buffer t&1; tile t+1 in LDS everywhere);
+//   stage tile t+2 -> buffer t&1;  read (t+1, 0) -> X;  64 MFMA on Y.
+// Same LDS image and swizzle as k_gemm256_bf16_tn (a wave's 4 glds per half
+// write rows 32w .. 32w+31).  Host opts bit 5; measured (profiles/
+// kbench_r2_w4.md, same process): 1041 TF/s vs 1127 for the staggered 8-wave
+// kernel (default) and 1433 for hipBLASLt.  The compiler keeps copying ~96
+// accumulator registers AGPR <-> VGPR around every K-tile, and the 16-read /
+// 16-glds clumps leave the matrix pipe idle; interleaving them one per MFMA in
+// source order (sched_barrier fences) made the copies worse: 896 TF/s.
+// Reaching the library needs the schedule in assembly, not in HIP.
+constexpr int G4_NT = 256;
+
+__global__ __launch_bounds__(G4_NT, 1) void k_gemm256w4_bf16_tn(const u16* __restrict__ A,
+                                                               const u16* __restrict__ Bt, u16* __restrict__ C,
+                                                               int M, int N, int K, WorkQueue* q,
+                                                               const PartTable* table, u32 mode, u32 me, u64* cnt,
+                                                               u32 inst_per_tile, u32 refs_per_tile,
+                                                               u32 miss_per_tile, u32* status) {
+  __shared__ __attribute__((aligned(16))) char smem[kG2Lds + 16];
+  lds_t* lds = (lds_t*)smem;
+  int* s_slot = (int*)(smem + kG2Lds);
+  const u32 xcc = xcc_id();
+  u64 t_last = __builtin_amdgcn_s_memtime();
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int tiles_n = N / G2_BM, ntiles = (M / G2_BM) * tiles_n;
+  const int nt = K / G2_BK;
+  int soff[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = 8 * (4 * wid + j) + (lane >> 3);
+    soff[j] = row * K + (((lane & 7) ^ g2_swz(row)) * 8);
+  }
+  const int l16 = lane & 15, lq = lane >> 4;
+  for (;;) {
+    const int tile = grab_unit(q, table, mode, me, xcc, s_slot, (u32)ntiles);
+    if (tile < 0) break;
+    const int tm = tile / tiles_n, tn = tile % tiles_n;
+    const u16* Ab = A + (size_t)tm * G2_BM * K;
+    const u16* Bb = Bt + (size_t)tn * G2_BM * K;
+
+    auto stage_tile = [&](int t) {
+      if (t >= nt) return;
+#pragma unroll
+      for (int kind = 0; kind < 2; ++kind)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const u16* src = (kind ? Bb : Ab) + (size_t)h * 128 * K + t * G2_BK;
+          lds_t* dst = lds + (t & 1) * kG2Buf + (kind * 2 + h) * kG2Half + wid * 4096;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) glds16(src + soff[j], dst + j * 1024);
+        }
+    };
+    auto frag = [&](int b, int kind, int h, int r0, int s) -> bf16x8 {
+      const int r = r0 + l16;
+      const lds_t* p = lds + b * kG2Buf + (kind * 2 + h) * kG2Half + r * 128 + (((4 * s + lq) ^ g2_swz(r)) << 4);
+      return *(const __attribute__((address_space(3))) bf16x8*)p;
+    };
+
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 xa[8], xb[8], ya[8], yb[8];
+
+    stage_tile(0);
+    stage_tile(1);  // nt >= 2 (host: even K-tile count)
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // tile 0 landed (16 glds per wave per tile)
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) xa[i] = frag(0, 0, wr, i * 16, 0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xb[j] = frag(0, 1, wc, j * 16, 0);
+
+    for (int t = 0; t < nt; ++t) {
+      const int buf = t & 1;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) ya[i] = frag(buf, 0, wr, i * 16, 1);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) yb[j] = frag(buf, 1, wc, j * 16, 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xb[j], xa[i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (t + 1 < nt) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      stage_tile(t + 2);
+      if (t + 1 < nt) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) xa[i] = frag(buf ^ 1, 0, wr, i * 16, 0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xb[j] = frag(buf ^ 1, 1, wc, j * 16, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(yb[j], ya[i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // (every read of this unit fed an MFMA above; grab_unit's barriers keep
+    // the next unit's prologue staging behind all of them)
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int m = tm * G2_BM + wr * 128 + i * 16 + l16;
+        const int n = tn * G2_BM + wc * 128 + j * 16 + 4 * lq;
+        const u32 lo = (u32)f2bf(acc[i][j][0]) | ((u32)f2bf(acc[i][j][1]) << 16);
+        const u32 hi = (u32)f2bf(acc[i][j][2]) | ((u32)f2bf(acc[i][j][3]) << 16);
+        *(uint2*)(C + (size_t)m * N + n) = make_uint2(lo, hi);
+      }
+    count_unit(cnt, me, xcc, inst_per_tile, &t_last, refs_per_tile, miss_per_tile, q);
+  }
+  finish(q, status, (u32)ntiles);
+}
+
 // ------------------------------------------------------------ HBM stream ---
 // dst = src (float4 copy), 16 B per lane, 16 loads in flight per thread: one
 // 256-thread workgroup per CU keeps 64 KiB of reads in flight (enough for
@@ -715,6 +848,12 @@ int gpbs_hip_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int
     const u32 miss = (u32)((((u64)M + N) * K * 2 / 128) / ntiles + (u64)G2_BM * G2_BM * 2 / 128);
     const u32 m2 = mode | ((g_gemm_opts & 1) ? kGemmXRange : 0u) |
                    ((g_gemm_opts & 8) && ntiles % kXcds == 0 ? kGemmBlock2D : 0u);
+    if ((g_gemm_opts & 32) && (K / G2_BK) % 2 == 0) {  // 4-wave 128x128-per-wave variant (plain tile queue)
+      hipLaunchKernelGGL(k_gemm256w4_bf16_tn, dim3(grid), dim3(G4_NT), 0, s, (const u16*)A, (const u16*)Bt, (u16*)C,
+                         M, N, K, (WorkQueue*)q, (const PartTable*)table, mode, me, (u64*)cnt, inst, refs, miss,
+                         (u32*)status);
+      return hipGetLastError() == hipSuccess ? 0 : -5;
+    }
     auto kern = (g_gemm_opts & 16)  ? k_gemm256_bf16_tn<3>
                 : (g_gemm_opts & 4) ? k_gemm256_bf16_tn<2>
                 : (g_gemm_opts & 2) ? k_gemm256_bf16_tn<1>

@@ -66,6 +66,9 @@ for step in "$@"; do
                 --policies "${LLM_POLICIES:-solo,none,se:1/3,se:2/2,se:1/3@solo,se:2/2@solo}" --reps "${LLM_REPS:-1}" \
                 --out gpurun_out/llm_split.json ;;
     kbench)  run kbench 600 python -u scripts/kbench.py ;;
+    mmref)   cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-.}"
+             run mmref 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/mmref -o run -- \
+                python3 scripts/mm_ref.py 4096 ;;
     *) echo "unknown step $step" | tee -a "$LOG" ;;
   esac
 done

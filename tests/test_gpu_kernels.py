@@ -149,7 +149,7 @@ def test_device_adapt_bit_exact_vs_host():
         assert bytes(got[k].numpy().tobytes()) == ref, k
 
 
-@pytest.mark.parametrize("opts", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("opts", [0, 1, 2, 3, 4, 5, 16, 32])
 def test_gemm256_variants_match_reference(opts):
     """Every 256x256 schedule variant (plain / XCD-range tile queue x one-half-
     per-phase / deep prefetch) is exact against fp32 on prologue/tail shapes."""
