@@ -786,13 +786,19 @@ void Engine::classify_tick(int64_t n) {
         // to a home partition none of its siblings occupies, preferably on
         // its own XCD, trading homes with the sibling that partition was
         // home to (homes stay one per partition).
+        auto occupied = [&](int part) {
+          for (size_t j = 0; j < t.slots.size(); ++j)
+            if (j != k && runnable(*slots[t.slots[j]]) && slots[t.slots[j]]->processor == part) return true;
+          return false;
+        };
+        // Stacked behind a sibling on one partition while its own home --
+        // free of siblings -- sits on the same XCD: in a fully busy pool no
+        // steal ever separates them, and with the class's SEs time-shared
+        // (more slots than partitions) the tenant then holds one SE of that
+        // XCD permanently while the gang alternates everywhere else.
+        const bool stacked = !foreign && occupied(v.processor) && !occupied(v.class_home);
         bool wrong_se = false;
         if (boot.class_split > 1 && !((home_ctx >> P.ctx) & 1)) {
-          auto occupied = [&](int part) {
-            for (size_t j = 0; j < t.slots.size(); ++j)
-              if (j != k && runnable(*slots[t.slots[j]]) && slots[t.slots[j]]->processor == part) return true;
-            return false;
-          };
           int target = -1;
           size_t owner = k;
           for (size_t j = 0; j < t.slots.size(); ++j) {
@@ -809,7 +815,7 @@ void Engine::classify_tick(int64_t n) {
             wrong_se = true;
           }
         }
-        if (stray || wrong_se || (foreign && (there < here || (there == 0 && here == 0)))) send_home(v);
+        if (stray || wrong_se || stacked || (foreign && (there < here || (there == 0 && here == 0)))) send_home(v);
       }
       continue;
     }
