@@ -13,7 +13,10 @@
 //               drains (slot block).  This is the in-process tenant shim; the
 //               cross-process one is pbs_amd/runtime/tenant.py over ctl pages.
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 #include <rocprofiler-sdk-roctx/roctx.h>
+#include <x86intrin.h>
 
 #include <atomic>
 #include <cstdio>
@@ -75,13 +78,96 @@ int64_t mono_ns() {
       .count();
 }
 
+// ---- table mode 2: the partition table in VRAM, written by the host ----
+// A fine-grained VRAM allocation from the GPU agent's memory pool, made
+// accessible to the CPU agent (hsa_amd_agents_allow_access): the host stores
+// the owner words and then the epoch straight through the large-BAR mapping
+// (write-combined, so each group is fenced), and tenant kernels poll it with
+// agent-scope loads.  No kernel and no queue sits between a decision and the
+// workgroups: measured on MI355X, host store -> device sees -> host sees the
+// device's ack in 2.3 us (scripts/bar_probe.hip), where the k_partition_switch
+// path needs a dispatch that waits for a free wave slot behind the tenants'
+// persistent grids (37 us mean, 233 us max under the flagship co-run,
+// profiles/rocprof_flagship_r2s5_summary.txt).
+struct BarFind {
+  uint32_t bdf = 0;
+  hsa_agent_t gpu{}, cpu{};
+  hsa_amd_memory_pool_t pool{};
+  bool gpu_ok = false, cpu_ok = false, pool_ok = false;
+};
+
+hsa_status_t bar_pool_cb(hsa_amd_memory_pool_t p, void* ud) {
+  auto* F = (BarFind*)ud;
+  hsa_amd_segment_t seg;
+  uint32_t fl = 0;
+  if (hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg) != HSA_STATUS_SUCCESS ||
+      seg != HSA_AMD_SEGMENT_GLOBAL)
+    return HSA_STATUS_SUCCESS;
+  hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &fl);
+  if ((fl & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_FINE_GRAINED) && !F->pool_ok) {
+    F->pool = p;
+    F->pool_ok = true;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+hsa_status_t bar_agent_cb(hsa_agent_t a, void* ud) {
+  auto* F = (BarFind*)ud;
+  hsa_device_type_t t;
+  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS) return HSA_STATUS_SUCCESS;
+  if (t == HSA_DEVICE_TYPE_CPU && !F->cpu_ok) {
+    F->cpu = a;
+    F->cpu_ok = true;
+  } else if (t == HSA_DEVICE_TYPE_GPU && !F->gpu_ok) {
+    uint32_t bdf = 0;
+    hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf);
+    if ((bdf & ~7u) == F->bdf) {  // this process's GPU (bus, device; any function)
+      F->gpu = a;
+      F->gpu_ok = true;
+      hsa_amd_agent_iterate_memory_pools(a, bar_pool_cb, F);
+    }
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+PartTable* bar_alloc(int device) {
+  int bus = 0, dev = 0;
+  if (hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, device) != hipSuccess ||
+      hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, device) != hipSuccess)
+    return nullptr;
+  BarFind F;
+  F.bdf = ((uint32_t)bus << 8) | ((uint32_t)dev << 3);
+  hsa_iterate_agents(bar_agent_cb, &F);
+  if (!F.gpu_ok || !F.cpu_ok || !F.pool_ok) return nullptr;
+  void* p = nullptr;
+  if (hsa_amd_memory_pool_allocate(F.pool, 4096, 0, &p) != HSA_STATUS_SUCCESS) return nullptr;
+  hsa_agent_t both[2] = {F.gpu, F.cpu};
+  if (hsa_amd_agents_allow_access(2, both, nullptr, p) != HSA_STATUS_SUCCESS) {
+    hsa_amd_memory_pool_free(p);
+    return nullptr;
+  }
+  return (PartTable*)p;
+}
+
+// Owner words first, then the epoch, each group fenced out of the CPU's
+// write-combining buffers (a kernel that sees the new epoch sees the owners).
+void bar_write(PartTable* b, const u32* owners, u32 epoch) {
+  volatile u32* o = (volatile u32*)b->owner;
+  for (int x = 0; x < kXcds * kCtx; ++x) o[x] = owners[x];
+  _mm_sfence();
+  *(volatile u32*)&b->epoch = epoch;
+  _mm_sfence();
+}
+
 struct GpuCtx {
   int device = 0;
   int part_base = 0;  // engine partition id of XCD 0
-  int table_mode = 0; // 0: pinned host table, 1: device table + partition_switch kernel
+  int table_mode = 0; // 0: pinned host table, 1: device table + partition_switch kernel,
+                      // 2: device table the host writes directly (BAR; no kernel, no queue)
   int spatial = 0;    // 1: the two partitions of an XCD are CU halves (GATE_SPATIAL)
   PartTable* h_table = nullptr;  // pinned host (device-visible)
   PartTable* d_table = nullptr;  // device copy (table_mode 1)
+  PartTable* b_table = nullptr;  // host-writable VRAM table (table_mode 2), allocated on first use
   u64* d_cnt = nullptr;          // [kMaxTenants][kXcds][kNumPmc]
   u64* d_prev = nullptr;
   u64* h_out = nullptr;          // pinned mapped: deltas [kMaxTenants][4]
@@ -247,6 +333,7 @@ void publish(GpuCtx* c) {
     __atomic_store_n(&c->h_table->epoch, c->epoch, __ATOMIC_RELEASE);
   }
   if (c->table_mode == 1) gpbs_hip_partition_switch(c->d_table, c->epoch, c->pending, c->sched_stream);
+  else if (c->table_mode == 2) bar_write(c->b_table, c->h_table->owner, c->epoch);
   c->flushes++;
   c->cv.notify_all();
 }
@@ -756,8 +843,9 @@ struct Runner {
 
   int launch(int qi, hipStream_t stream) {
     WorkQueue* q = d_q + qi;
-    const bool dev = __atomic_load_n(&ctx->table_mode, __ATOMIC_ACQUIRE) == 1;
-    const void* tab = dev ? (const void*)ctx->d_table : (const void*)ctx->h_table;
+    const int tm = __atomic_load_n(&ctx->table_mode, __ATOMIC_ACQUIRE);
+    const bool dev = tm != 0;
+    const void* tab = tm == 1 ? (const void*)ctx->d_table : tm == 2 ? (const void*)ctx->b_table : (const void*)ctx->h_table;
     const bool gate = cfg.gate && !ctx->share.load(std::memory_order_acquire);
     const unsigned mode = (gate ? (cfg.gate == 2 ? GATE_PARK : GATE_TABLE) : GATE_NONE) | (dev ? GATE_DEVTABLE : 0) |
                           (gate && ctx->spatial ? GATE_SPATIAL : 0) |
@@ -1030,6 +1118,7 @@ void gpbs_gpu_ctx_destroy(void* p) {
   hipHostFree(c->h_dirs);
   hipHostFree(c->h_adelta);
   if (c->d_table) hipFree(c->d_table);
+  if (c->b_table) hsa_amd_memory_pool_free(c->b_table);
   delete c;
 }
 
@@ -1268,6 +1357,16 @@ int gpbs_gpu_set_spatial(void* p, int on) {
 int gpbs_gpu_set_table_mode(void* p, int mode) {
   GpuCtx* c = (GpuCtx*)p;
   std::lock_guard<std::mutex> g(c->mu);
+  if (mode == 2) {
+    if (!c->b_table) {
+      hipSetDevice(c->device);
+      c->b_table = bar_alloc(c->device);
+      if (!c->b_table) return -95;  // no host-accessible fine-grained VRAM pool on this system
+    }
+    bar_write(c->b_table, c->h_table->owner, c->h_table->epoch);
+    __atomic_store_n(&c->table_mode, 2, __ATOMIC_RELEASE);
+    return 0;
+  }
   if (mode == 1) {
     if (hipMemcpyAsync(c->d_table, c->h_table, sizeof(PartTable), hipMemcpyHostToDevice, c->sched_stream) !=
             hipSuccess ||
@@ -1278,7 +1377,11 @@ int gpbs_gpu_set_table_mode(void* p, int mode) {
   return 0;
 }
 
-void* gpbs_gpu_table(void* p) { return ((GpuCtx*)p)->table_mode == 1 ? (void*)((GpuCtx*)p)->d_table : (void*)((GpuCtx*)p)->h_table; }
+void* gpbs_gpu_table(void* p) {
+  GpuCtx* c = (GpuCtx*)p;
+  return c->table_mode == 1 ? (void*)c->d_table : c->table_mode == 2 ? (void*)c->b_table : (void*)c->h_table;
+}
+int gpbs_gpu_table_mode(void* p) { return ((GpuCtx*)p)->table_mode; }
 void* gpbs_gpu_counters(void* p) { return ((GpuCtx*)p)->d_cnt; }
 
 // owners: [kXcds * kCtx] entries (kCtx = 4), (xcd, context) major, -1 = idle.
@@ -1359,8 +1462,8 @@ int gpbs_gpu_switch_latency(void* p, int iters, int nwg, int64_t* out_ns) {
   for (int i = 0; i < nwg; ++i) __atomic_store_n(&acks[i], 0xFFFFFFFEu, __ATOMIC_RELAXED);
   hipStream_t ps = nullptr;
   hipStreamCreateWithFlags(&ps, hipStreamNonBlocking);
-  const int dev = c->table_mode == 1;
-  const void* tab = dev ? (const void*)c->d_table : (const void*)c->h_table;
+  const int tm = c->table_mode, dev = tm != 0;
+  const void* tab = tm == 1 ? (const void*)c->d_table : tm == 2 ? (const void*)c->b_table : (const void*)c->h_table;
   // every wave exits after 20 s of device wall clock even if the host died
   int rc = gpbs_hip_switch_probe(tab, dev, acks, nwg, kStop, 20ull * 100000000ull, ps);
   // e == 0xFFFFFFFE: every wave has acknowledged some epoch (grid resident)
@@ -1395,13 +1498,15 @@ int gpbs_gpu_switch_latency(void* p, int iters, int nwg, int64_t* out_ns) {
   }
   // stop epoch, then drain the probe grid (bounded by its own wall-clock exit)
   __atomic_store_n(&c->h_table->epoch, kStop, __ATOMIC_RELEASE);
-  if (dev) gpbs_hip_partition_switch(c->d_table, kStop, c->pending, c->sched_stream);
+  if (tm == 1) gpbs_hip_partition_switch(c->d_table, kStop, c->pending, c->sched_stream);
+  if (tm == 2) bar_write(c->b_table, c->h_table->owner, kStop);
   const int64_t t_end = mono_ns() + 25000000000LL;
   while (hipStreamQuery(ps) == hipErrorNotReady && mono_ns() < t_end)
     std::this_thread::sleep_for(std::chrono::microseconds(100));
   hipStreamSynchronize(ps);
   __atomic_store_n(&c->h_table->epoch, c->epoch, __ATOMIC_RELEASE);
-  if (dev) gpbs_hip_partition_switch(c->d_table, c->epoch, c->pending, c->sched_stream);
+  if (tm == 1) gpbs_hip_partition_switch(c->d_table, c->epoch, c->pending, c->sched_stream);
+  if (tm == 2) bar_write(c->b_table, c->h_table->owner, c->epoch);
   hipStreamSynchronize(c->sched_stream);
   hipStreamDestroy(ps);
   hipHostFree(acks);

@@ -378,7 +378,12 @@ class Corun:
             e._gpbs_used = True
             _, _, gate, table = POLICY_ENGINES[policy]
             opts = table.split(",")
-            self.ctx.set_table_mode(opts[0])
+            # GPBS_TABLE_MODE=bar: policies on the device table use the
+            # host-written VRAM table instead (no k_partition_switch dispatch)
+            tmode = opts[0]
+            if tmode == "device" and os.environ.get("GPBS_TABLE_MODE", "") in ("bar", "device"):
+                tmode = os.environ["GPBS_TABLE_MODE"]
+            self.ctx.set_table_mode(tmode)
             self.ctx.set_spatial("spatial" in opts)
             self.ctx.set_se_mode("se" in opts)
             self.ctx.set_waveprio("waveprio" in opts)

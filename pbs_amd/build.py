@@ -170,7 +170,7 @@ def build_hip(verbose=False):
             jobs.append(([hipcc()] + flags + lang + ["-c", s, "-o", obj], obj))
     _compile_parallel(jobs, verbose)
     _link_atomic([hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}"], target,
-                 objs + ["-L" + LIBDIR, "-lgpbs", "-Wl,-rpath,$ORIGIN", "-L/opt/rocm/lib", "-lrocprofiler-sdk", "-lrocprofiler-sdk-roctx",
+                 objs + ["-L" + LIBDIR, "-lgpbs", "-Wl,-rpath,$ORIGIN", "-L/opt/rocm/lib", "-lrocprofiler-sdk", "-lrocprofiler-sdk-roctx", "-lhsa-runtime64",
                          "-Wl,-rpath,/opt/rocm/lib", "-pthread"], verbose, deps, ARCH)
     return target
 

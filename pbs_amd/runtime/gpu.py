@@ -41,6 +41,8 @@ class GpuContext:
         if not h:
             raise RuntimeError(f"gpbs_gpu_ctx_create failed on device {device}")
         self.h = C.c_void_p(h)
+        if table_mode == "bar":
+            self.set_table_mode("bar")
         self.engine = None
         if engine is not None:
             self.attach(engine, device_counters, device_adapt)
@@ -104,12 +106,22 @@ class GpuContext:
             return [tuple(px[x * 4:(x + 1) * 4]) for x in range(XCDS)]
         return tuple(out)
 
+    TABLE_MODES = {"host": 0, "device": 1, "bar": 2}
+
     def set_table_mode(self, mode: str):
         """'host': pinned host table polled over PCIe; 'device': device copy
-        refreshed by the partition_switch kernel, polled on chip."""
-        rc = self.L.gpbs_gpu_set_table_mode(self.h, 1 if mode == "device" else 0)
+        refreshed by the partition_switch kernel, polled on chip; 'bar': a
+        fine-grained VRAM table the host writes directly through the BAR
+        (no kernel or queue on the switch path), polled on chip."""
+        if mode not in self.TABLE_MODES:
+            raise ValueError(f"table mode {mode!r}: one of {sorted(self.TABLE_MODES)}")
+        rc = self.L.gpbs_gpu_set_table_mode(self.h, self.TABLE_MODES[mode])
         if rc:
-            raise RuntimeError("set_table_mode failed")
+            raise RuntimeError(f"set_table_mode({mode!r}) failed: {rc}")
+
+    def table_mode(self) -> str:
+        m = self.L.gpbs_gpu_table_mode(self.h)
+        return {v: k for k, v in self.TABLE_MODES.items()}[m]
 
     def set_hwc(self, on: bool):
         """Drive the PBS metric with live hardware counters (requires

@@ -41,6 +41,7 @@ THRESHOLDS = {
     "gang_shm_w4_p50_us": 60.0,
     "switch_host_p99_us": 1200.0,   # 1024 pollers of a pinned host word over PCIe: ~340 us p50 measured
     "switch_device_p99_us": 60.0,   # device table + k_partition_switch: ~16 us p50 measured
+    "switch_bar_p99_us": 60.0,      # host-written VRAM table (no dispatch)
     "hwc_sample_p50_us": 1200.0,    # synchronous device-counting sample: ~410 us measured
 }
 
@@ -98,14 +99,30 @@ def bench_gang(worlds=(2, 4, 8), iters=3000, gloo=True):
 
 
 # -------------------------------------------------------------- switch
-def bench_switch(iters=300, nwg=1024):
-    from pbs_amd.runtime.gpu import GpuContext
+def bench_switch(iters=300, nwg=1024, loaded=False, modes=("host", "device", "bar")):
+    """Actuation latency per partition-table mode.  ``loaded``: an ungated
+    4096^3 GEMM runner keeps every CU busy meanwhile (its persistent 256x256
+    grid holds 128 KiB of LDS and 8 waves per CU), as the tenants do in a
+    co-run -- the k_partition_switch dispatch then waits for a wave slot,
+    while the BAR table has no dispatch to wait for."""
+    from pbs_amd.runtime.gpu import GpuContext, Runner
     out = {}
-    for mode in ("host", "device"):
+    for mode in modes:
         ctx = GpuContext(0, table_mode=mode)
+        load = None
+        if loaded:
+            load = Runner(ctx, "gemm", 1, engine_wake=False, M=4096, N=4096, K=4096)
+            load.set_gate(False)
+            load.submit(1 << 20)
+            time.sleep(0.05)
         ctx.switch_latency(20, nwg)  # warm-up
         out[mode] = summ_us(ctx.switch_latency(iters, nwg))
         out[mode]["nwg"] = nwg
+        if load is not None:
+            out[mode]["load"] = "gemm 4096^3 ungated"
+            load.cancel()
+            load.wait(60)
+            load.close()
         ctx.close()
     return out
 
@@ -148,6 +165,8 @@ def gates(res):
         vals["switch_host_p99_us"] = s["host"]["p99_us"]
     if "device" in s:
         vals["switch_device_p99_us"] = s["device"]["p99_us"]
+    if "bar" in s:
+        vals["switch_bar_p99_us"] = s["bar"]["p99_us"]
     h = res.get("hwc", {})
     if "sample" in h:
         vals["hwc_sample_p50_us"] = h["sample"]["p50_us"]
@@ -156,7 +175,7 @@ def gates(res):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="gang,switch,hwc")
+    ap.add_argument("--only", default="gang,switch,switch_loaded,hwc")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     res = {}
@@ -166,6 +185,8 @@ def main():
             res["gang"] = bench_gang()
         elif sec == "switch":
             res["switch"] = bench_switch()
+        elif sec == "switch_loaded":
+            res["switch_loaded"] = bench_switch(iters=200, loaded=True, modes=("device", "bar"))
         elif sec == "hwc":
             res["hwc"] = bench_hwc()
         print(f"[microbench] {sec}: {json.dumps(res.get(sec))} ({time.time() - t0:.1f}s)", flush=True)

@@ -181,3 +181,30 @@ def test_four_context_table_gates_each_context():
             assert magic == 0xC0FFEE
             assert bool(ok) == (xcc % 4 == c), (c, xcc)
     ctx.close()
+
+
+def test_bar_table_gates_runners_and_census():
+    """Table mode 'bar' (VRAM table written by the host through the BAR):
+    a static XCD split confines each runner to its XCDs, and the census
+    kernel reads the owners the host stored."""
+    from pbs_amd.ops import kernels as K
+    ctx = GpuContext(0, table_mode="bar")
+    assert ctx.table_mode() == "bar"
+    ctx.set_owners([1, 1, 1, 1, 2, 2, 2, 2])
+    out = K.census(2048, table=ctx.table, tenant=2).cpu()
+    for xcc, _hw, ok, magic in out.tolist():
+        assert magic == 0xC0FFEE
+        assert bool(ok) == (xcc >= 4), xcc
+    r1 = Runner(ctx, "gemm", 1, engine_wake=False, M=2048, N=2048, K=2048)
+    r2 = Runner(ctx, "stream", 2, engine_wake=False, bytes=256 << 20)
+    r1.submit(10)
+    r2.submit(10)
+    r1.wait(60)
+    r2.wait(60)
+    per1 = ctx.read_counters(1, per_xcd=True)
+    per2 = ctx.read_counters(2, per_xcd=True)
+    assert all(per1[x][0] == 0 for x in range(4, 8)) and all(per2[x][0] == 0 for x in range(4))
+    assert any(per1[x][0] > 0 for x in range(4)) and any(per2[x][0] > 0 for x in range(4, 8))
+    r1.close()
+    r2.close()
+    ctx.close()

@@ -33,7 +33,7 @@ def test_switch_actuation_latency():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     res = MB.bench_switch(iters=200)
-    for mode in ("host", "device"):
+    for mode in ("host", "device", "bar"):
         assert res[mode]["n"] == 200, res
     g = MB.gates({"switch": res})
     for k, (v, lim, ok) in g.items():
