@@ -33,7 +33,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--policies", default="none,static,credit2,credit-fixed-ts,gpbs-ts,credit-fixed,gpbs",
+    ap.add_argument("--policies", default="none,static,credit2,credit-fixed-ts,gpbs-ts,credit-fixed,gpbs-lat,gpbs",
                     help="comma list; gpbs is the reported policy")
     ap.add_argument("--keep-engines", action="store_true",
                     help="one engine per policy for the whole process (default: a fresh engine per timed run)")

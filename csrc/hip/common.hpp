@@ -38,7 +38,8 @@ constexpr int kCtx = 4;
 struct alignas(64) PartTable {
   u32 epoch;
   u32 flags;
-  u32 pad0[2];
+  u32 hold;     // latency request in flight: GATE_HOLD tenants pause at their next unit (host-written)
+  u32 pad0;
   union {
     u32 owner[kXcds * kCtx];  // tenant id per (XCD, context), kNoOwner when idle
     u64 pair[kXcds][2];       // contexts {0,1} and {2,3} of an XCD, 8 bytes each
@@ -102,8 +103,16 @@ enum GateMode : u32 {
   // the SE-resolved SQ/TCP hardware counters attributable per tenant
   // (profiles/hwc/se_separation_probe.txt).
   GATE_SE = 32,
+  // Bit 6 (GATE_HOLD): before grabbing a unit, wait (bounded) while the
+  // table's hold word is set -- the latency tenant's request is in flight.
+  // Given to memory-class tenants only: the request (a GEMV) is HBM-bound, and
+  // their next chunk boundary comes within ~25 us.  The wake-BOOST of
+  // X:xen/common/sched_credit.c:1080-1084 for an I/O-bound domain, as a pause
+  // of the tenants that contend with it instead of a preemption of all.
+  GATE_HOLD = 64,
 };
 constexpr u32 kParkSpins = 100;  // x ~20 us
+constexpr u32 kHoldSpins = 256;  // x ~0.9 us: a stuck hold word costs at most ~0.25 ms per unit
 
 #define HIPCHECK(x)                                                                              \
   do {                                                                                           \
@@ -131,6 +140,20 @@ __device__ __forceinline__ u32 se_id() { return (hw_id() >> 13) & 3u; }
 
 __device__ __forceinline__ u32 load_sys(const u32* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// GATE_HOLD (thread 0, before a unit grab): bounded wait while the hold word
+// is set.  The word lives in the table the kernel was given: the pinned host
+// table or the BAR-written VRAM table (the host raises and clears it); the
+// kernel-refreshed device table never carries it.
+__device__ __forceinline__ void hold_wait(const PartTable* t, u32 mode) {
+  if (!(mode & GATE_HOLD)) return;
+  for (u32 k = 0; k < kHoldSpins; ++k) {
+    const u32 h = (mode & GATE_DEVTABLE) ? __hip_atomic_load(&t->hold, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                         : __hip_atomic_load(&t->hold, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (!h) return;
+    __builtin_amdgcn_s_sleep(32);
+  }
 }
 
 // Does tenant `me` own the XCD this workgroup runs on?

@@ -159,6 +159,9 @@ void bar_write(PartTable* b, const u32* owners, u32 epoch) {
   _mm_sfence();
 }
 
+struct GpuCtx;
+void set_hold(GpuCtx* c, u32 v);
+
 struct GpuCtx {
   int device = 0;
   int part_base = 0;  // engine partition id of XCD 0
@@ -180,6 +183,9 @@ struct GpuCtx {
   gpbs_engine_t* engine = nullptr;
   int nctx = 1;                  // issue contexts per XCD in use (1..kCtx)
   int waveprio = 0;              // latency-class runners raise their wave priority
+  int hold_enable = 0;           // latency requests hold the memory-class tenants (GATE_HOLD)
+  std::atomic<int> holds{0};     // latency units in flight (the hold word is set while > 0)
+  std::atomic<uint64_t> hold_raises{0};
   u32 pending[kXcds * kCtx];
   u32 epoch = 0;
   // async counter reduce (one metric period of lag, never blocks the engine)
@@ -339,6 +345,16 @@ void publish(GpuCtx* c) {
 }
 
 void act_on_flush(void* user, int64_t) { publish((GpuCtx*)user); }
+
+// The hold word goes wherever the tenants read their table from: the pinned
+// host table (always) and the BAR-written VRAM table.
+void set_hold(GpuCtx* c, u32 v) {
+  __atomic_store_n(&c->h_table->hold, v, __ATOMIC_RELEASE);
+  if (c->table_mode == 2 && c->b_table) {
+    *(volatile u32*)&c->b_table->hold = v;
+    _mm_sfence();
+  }
+}
 
 void act_on_park(void*, int, int, int) {}
 
@@ -847,10 +863,14 @@ struct Runner {
     const bool dev = tm != 0;
     const void* tab = tm == 1 ? (const void*)ctx->d_table : tm == 2 ? (const void*)ctx->b_table : (const void*)ctx->h_table;
     const bool gate = cfg.gate && !ctx->share.load(std::memory_order_acquire);
+    // memory-class tenants pause at unit boundaries while a latency request
+    // is in flight (only where the host can write the hold word: host / BAR table)
+    const bool hold = gate && ctx->hold_enable && tm != 1 && cfg.kind != K_GEMV && ctx->engine &&
+                      gpbs_tenant_class(ctx->engine, cfg.tenant) == 1;
     const unsigned mode = (gate ? (cfg.gate == 2 ? GATE_PARK : GATE_TABLE) : GATE_NONE) | (dev ? GATE_DEVTABLE : 0) |
                           (gate && ctx->spatial ? GATE_SPATIAL : 0) |
                           (gate && __atomic_load_n(&ctx->se_mode, __ATOMIC_ACQUIRE) ? GATE_SE : 0) |
-                          (cfg.priority > 0 && ctx->waveprio ? GATE_WAVEPRIO : 0);
+                          (cfg.priority > 0 && ctx->waveprio ? GATE_WAVEPRIO : 0) | (hold ? GATE_HOLD : 0);
     const unsigned me = (unsigned)cfg.tenant;
     __atomic_store_n(&h_status[qi], 0u, __ATOMIC_RELEASE);
     st.launches++;
@@ -950,6 +970,11 @@ struct Runner {
             // resume the same queue: clear exit bookkeeping only
             hipMemsetAsync(&d_q[qi].exited, 0, sizeof(u32) * 2, stream);
           }
+          const bool lat_hold = cfg.priority > 0 && ctx->hold_enable && fresh;
+          if (lat_hold && ctx->holds.fetch_add(1) == 0) {
+            set_hold(ctx, 1);
+            ctx->hold_raises.fetch_add(1, std::memory_order_relaxed);
+          }
           if (launch(qi, stream) != 0) err = -5;
           const int e = qi;  // one event per queue slot
           hipEventRecord(ev[e], stream);
@@ -969,6 +994,8 @@ struct Runner {
         const u32 s = __atomic_load_n(&h_status[f.qi], __ATOMIC_ACQUIRE);
         const u32 done = s & 0x7fffffffu;
         if ((s & 0x80000000u) && done >= unit_total()) {
+          if (cfg.priority > 0 && ctx->hold_enable && ctx->holds.load() > 0 && ctx->holds.fetch_sub(1) == 1)
+            set_hold(ctx, 0);
           const int64_t t = mono_ns();
           std::lock_guard<std::mutex> g(mu);
           q_busy[f.qi] = 0;
@@ -1340,6 +1367,23 @@ int gpbs_gpu_set_se_mode(void* p, int on) {
 
 // Latency-class runners (priority > 0) launch their kernels with raised wave
 // issue priority while a gated policy is active.
+// Latency-request hold (GATE_HOLD) on/off; returns the previous setting.
+// *raises (optional): times the hold word was raised since the context began.
+int gpbs_gpu_set_hold(void* p, int on, uint64_t* raises) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c) return -22;
+  const int old = c->hold_enable;
+  if (on >= 0) {
+    __atomic_store_n(&c->hold_enable, on ? 1 : 0, __ATOMIC_RELEASE);
+    if (!on) {
+      c->holds.store(0);
+      set_hold(c, 0);
+    }
+  }
+  if (raises) *raises = c->hold_raises.load();
+  return old;
+}
+
 int gpbs_gpu_set_waveprio(void* p, int on) {
   GpuCtx* c = (GpuCtx*)p;
   if (!c) return -22;

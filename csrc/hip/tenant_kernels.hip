@@ -22,6 +22,7 @@ __device__ __forceinline__ int grab_unit(WorkQueue* q, const PartTable* table, u
                                          int* s_slot, u32 total) {
   if (threadIdx.x == 0) {
     int u = -1;
+    hold_wait(table, mode);
     for (u32 spins = 0;; ++spins) {
       if (owns(table, mode, me, xcc)) {
         const u32 t = atomicAdd(&q->next, 1u);
@@ -57,6 +58,7 @@ __device__ __forceinline__ int grab_unit_x(WorkQueue* q, const PartTable* table,
                                            int* s_slot, u32 total) {
   if (threadIdx.x == 0) {
     int u = -1;
+    hold_wait(table, mode);
     const u32 per = (total + kXcds - 1) / kXcds;
     for (u32 spins = 0;; ++spins) {
       if (owns(table, mode, me, xcc)) {

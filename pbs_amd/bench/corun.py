@@ -146,6 +146,10 @@ POLICY_ENGINES = {
     # class-half split once co-class tenants hold aligned halves (1.240 vs
     # 1.253, none 1.252), so the flagship does not share.
     "gpbs-share": (4, dict(SE_OVERRIDES), True, "device,se,waveprio,latco,se8,share"),
+    # flagship + latency hold: the table in host-written VRAM (BAR), and the
+    # memory-class tenants pause at their next unit boundary while a latency
+    # request is in flight (the wake-BOOST analog for the GEMV tenant)
+    "gpbs-lat": (4, dict(SE_OVERRIDES), True, "bar,se,waveprio,latco,se8,hold"),
     "gpbs-ts": (4, dict(SE_OVERRIDES), True, "device,se,waveprio,latco"),
     "credit-fixed-ts": (4, dict(SE_OVERRIDES, sched="credit-fixed"), True, "device,se,waveprio,latco"),
     "credit2": (4, dict(SE_OVERRIDES, sched="credit2"), True, "device,se,waveprio,latco"),
@@ -383,11 +387,18 @@ class Corun:
             tmode = opts[0]
             if tmode == "device" and os.environ.get("GPBS_TABLE_MODE", "") in ("bar", "device"):
                 tmode = os.environ["GPBS_TABLE_MODE"]
-            self.ctx.set_table_mode(tmode)
+            try:
+                self.ctx.set_table_mode(tmode)
+            except RuntimeError as ex:  # no host-accessible fine-grained VRAM pool: the pinned host table
+                if tmode != "bar":
+                    raise
+                self.log(f"[corun] {policy}: {ex}; using the pinned host table")
+                self.ctx.set_table_mode("host")
             self.ctx.set_spatial("spatial" in opts)
             self.ctx.set_se_mode("se" in opts)
             self.ctx.set_waveprio("waveprio" in opts)
             self.ctx.set_share("share" in opts)
+            self.ctx.set_hold("hold" in opts)
             self.ctx.attach(e, nctx=e._gpbs_nctx)
             if self.cfg.hw_counters:
                 self.ctx.set_hwc(True)
@@ -424,6 +435,7 @@ class Corun:
         self.ctx.set_spatial(False)
         self.ctx.set_se_mode(False)
         self.ctx.set_share(False)
+        self.ctx.set_hold(False)
         self.ctx.set_waveprio(False)
         if self.cfg.hw_counters:
             self.ctx.set_hwc(False)
@@ -721,6 +733,7 @@ class Corun:
                                 for n in self.tid}
             eng["runner"] = {n: {k: getattr(r.stats(), k) for k in ("launches", "relaunches", "waits_owner")}
                              for n, r in self.runners.items() if isinstance(r, Runner)}
+            eng["hold_raises"] = self.ctx.hold_raises()  # latency-request holds (cumulative, gpbs-lat)
             coll = self.runners.get("coll")
             if isinstance(coll, CollTenant):
                 eng["coll_wait"] = coll.probe.stats()  # K10 reports (cumulative)

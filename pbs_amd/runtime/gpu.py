@@ -106,6 +106,20 @@ class GpuContext:
             return [tuple(px[x * 4:(x + 1) * 4]) for x in range(XCDS)]
         return tuple(out)
 
+    def set_hold(self, on: bool) -> int:
+        """Latency-request hold: while a priority (latency) runner's unit is in
+        flight, memory-class runners pause at their next unit boundary
+        (GATE_HOLD; host and BAR table modes).  Returns the number of holds
+        raised so far."""
+        n = C.c_uint64(0)
+        self.L.gpbs_gpu_set_hold(self.h, 1 if on else 0, C.byref(n))
+        return int(n.value)
+
+    def hold_raises(self) -> int:
+        n = C.c_uint64(0)
+        self.L.gpbs_gpu_set_hold(self.h, -1, C.byref(n))
+        return int(n.value)
+
     TABLE_MODES = {"host": 0, "device": 1, "bar": 2}
 
     def set_table_mode(self, mode: str):

@@ -44,6 +44,8 @@ for step in "$@"; do
                 --out gpurun_out/bdev.json && \
              GPBS_TABLE_MODE=bar run bbar 600 python bench.py --steps 20 --warmup 5 --reps 3 --policies none,gpbs,credit-fixed \
                 --out gpurun_out/bbar.json ;;
+    blat)    run blat 900 python bench.py --steps 20 --warmup 5 --reps 3 --policies none,gpbs,gpbs-lat,credit-fixed \
+                --out gpurun_out/blat.json ;;
     bkeep)   run bkeep 600 python bench.py --steps 20 --warmup 5 --reps 3 --keep-engines \
                 --policies none,gpbs-ts,gpbs --out gpurun_out/bkeep.json ;;
     rehearse) GPBS_HANG_DUMP_S=${GPBS_HANG_DUMP_S:-45} run rehearse 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \

@@ -40,13 +40,28 @@ def _fake_op(delays):
     return op
 
 
-def test_baseline_excess_reports_only_the_extra_wait():
+def test_baseline_excess_reports_only_the_extra_wait(monkeypatch):
+    # a simulated clock the fake collective advances (no sleeps: a loaded host
+    # must not turn scheduling noise into reported waits)
+    import pbs_amd.runtime.waitprobe as WP
+    clock = [0]
+
+    class _T:
+        @staticmethod
+        def monotonic_ns():
+            return clock[0]
+    monkeypatch.setattr(WP, "time", _T)
+    delays = iter([2, 2, 2, 7, 2])
+
+    def op(tensor, async_op=False):
+        clock[0] += next(delays) * 1_000_000
+        return _Work()
+    op.__name__ = "all_reduce"
     got = []
     p = WaitProbe(got.append, min_report_ns=500_000)
-    op = _fake_op([2, 2, 2, 7, 2])
     for _ in range(5):
         p.collective(op, None)
-    assert len(got) == 1 and 4e6 <= got[0] <= 7e6, got  # only the 5 ms late one
+    assert len(got) == 1 and 4.9e6 <= got[0] <= 5.1e6, got  # only the 5 ms late one
     assert p.stats()["timed"] == 5
 
 
