@@ -52,7 +52,7 @@ for step in "$@"; do
                 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 1 --reps 1 --rehearse --policies none,gpbs \
                 --out gpurun_out/rehearse.json ;;
     rehearse4) GPBS_HANG_DUMP_S=${GPBS_HANG_DUMP_S:-60} run rehearse4 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
-                --master-port 29534 bench.py --gpus 4 --steps 5 --warmup 1 --reps 2 --rehearse --policies none,credit-fixed,gpbs \
+                --master-port 29534 bench.py --gpus 4 --steps 5 --warmup 1 --reps 2 --rehearse --policies none,gpbs-lat,gpbs \
                 --out gpurun_out/rehearse4.json ;;
     rehearse8) GPBS_HANG_DUMP_S=${GPBS_HANG_DUMP_S:-90} run rehearse8 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
                 --master-port 29535 bench.py --gpus 8 --steps 3 --warmup 1 --reps 1 --rehearse --policies none,gpbs \
