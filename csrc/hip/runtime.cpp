@@ -184,6 +184,7 @@ struct GpuCtx {
   int nctx = 1;                  // issue contexts per XCD in use (1..kCtx)
   int waveprio = 0;              // latency-class runners raise their wave priority
   int hold_enable = 0;           // latency requests hold the memory-class tenants (GATE_HOLD)
+  int hold_all = 0;              // GPBS_HOLD_ALL=1: hold every gated tenant, compute class too (ablation)
   std::atomic<int> holds{0};     // latency units in flight (the hold word is set while > 0)
   std::atomic<uint64_t> hold_raises{0};
   u32 pending[kXcds * kCtx];
@@ -866,7 +867,7 @@ struct Runner {
     // memory-class tenants pause at unit boundaries while a latency request
     // is in flight (only where the host can write the hold word: host / BAR table)
     const bool hold = gate && ctx->hold_enable && tm != 1 && cfg.kind != K_GEMV && ctx->engine &&
-                      gpbs_tenant_class(ctx->engine, cfg.tenant) == 1;
+                      (ctx->hold_all || gpbs_tenant_class(ctx->engine, cfg.tenant) == 1);
     const unsigned mode = (gate ? (cfg.gate == 2 ? GATE_PARK : GATE_TABLE) : GATE_NONE) | (dev ? GATE_DEVTABLE : 0) |
                           (gate && ctx->spatial ? GATE_SPATIAL : 0) |
                           (gate && __atomic_load_n(&ctx->se_mode, __ATOMIC_ACQUIRE) ? GATE_SE : 0) |
@@ -1051,6 +1052,7 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
   std::memset(c->own_base, 0, sizeof(c->own_base));
   for (int& r : c->prev_raw) r = -1;
   if (const char* v = std::getenv("GPBS_SHARE")) c->share_enable = std::atoi(v) != 0;
+  if (const char* v = std::getenv("GPBS_HOLD_ALL")) c->hold_all = std::atoi(v) != 0;
   if (const char* v = std::getenv("GPBS_HWC_PERIOD_US")) c->hwc_period_us = std::max(100, std::atoi(v));
   if (const char* v = std::getenv("GPBS_HWC_SLOW_US")) c->hwc_slow_us = std::max(0, std::atoi(v));
   if (const char* v = std::getenv("GPBS_SHARE_PROBE")) {

@@ -315,14 +315,18 @@ class Corun:
         cfg, t = self.cfg, self.tid[name]
         if name.startswith("gemm"):
             return Runner(self.ctx, "gemm", t, depth=cfg.depth, M=cfg.gemm_n, N=cfg.gemm_n, K=cfg.gemm_n)
+        # GPBS_MEM_CHUNK: unit-boundary granularity of the memory tenants (bytes
+        # per work-queue chunk, default 512 KiB) -- how soon a hold or a
+        # revocation takes effect
+        mem_chunk = {"chunk_bytes": int(os.environ["GPBS_MEM_CHUNK"])} if os.environ.get("GPBS_MEM_CHUNK") else {}
         if name == "hbm":
-            return Runner(self.ctx, "stream", t, depth=cfg.depth, bytes=cfg.hbm_bytes)
+            return Runner(self.ctx, "stream", t, depth=cfg.depth, bytes=cfg.hbm_bytes, **mem_chunk)
         if name == "coll":
             if self.world > 1:
                 return CollTenant(self.ctx, t, cfg.coll_bytes, self.groups.get("coll"), on_cpu=self.coll_on_cpu,
                                   board_name=f"{cfg.gang_shm_base}-arr" if cfg.gang_shm_base else "",
                                   rank=self.rank, world=self.world)
-            return Runner(self.ctx, "reduce", t, depth=cfg.depth, bytes=cfg.coll_bytes)
+            return Runner(self.ctx, "reduce", t, depth=cfg.depth, bytes=cfg.coll_bytes, **mem_chunk)
         if name == "idle":
             return Runner(self.ctx, "gemv", t, depth=1, priority=1, M=cfg.idle_rows, K=cfg.idle_rows)
         raise ValueError(name)

@@ -46,6 +46,12 @@ for step in "$@"; do
                 --out gpurun_out/bbar.json ;;
     blat)    run blat 900 python bench.py --steps 20 --warmup 5 --reps 3 --policies none,gpbs,gpbs-lat,credit-fixed \
                 --out gpurun_out/blat.json ;;
+    blatv)   run blat_base 600 python bench.py --steps 20 --warmup 5 --reps 3 --policies none,gpbs,gpbs-lat \
+                --out gpurun_out/blat_base.json && \
+             GPBS_MEM_CHUNK=131072 run blat_c128 600 python bench.py --steps 20 --warmup 5 --reps 3 --policies none,gpbs,gpbs-lat \
+                --out gpurun_out/blat_c128.json && \
+             GPBS_HOLD_ALL=1 run blat_all 600 python bench.py --steps 20 --warmup 5 --reps 3 --policies none,gpbs,gpbs-lat \
+                --out gpurun_out/blat_all.json ;;
     bkeep)   run bkeep 600 python bench.py --steps 20 --warmup 5 --reps 3 --keep-engines \
                 --policies none,gpbs-ts,gpbs --out gpurun_out/bkeep.json ;;
     rehearse) GPBS_HANG_DUMP_S=${GPBS_HANG_DUMP_S:-45} run rehearse 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
