@@ -1386,6 +1386,14 @@ int gpbs_gpu_set_hold(void* p, int on, uint64_t* raises) {
   return old;
 }
 
+// Test hook: raise (1) or clear (0) the hold word directly.
+int gpbs_gpu_force_hold(void* p, int v) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c) return -22;
+  set_hold(c, v ? 1u : 0u);
+  return 0;
+}
+
 int gpbs_gpu_set_waveprio(void* p, int on) {
   GpuCtx* c = (GpuCtx*)p;
   if (!c) return -22;

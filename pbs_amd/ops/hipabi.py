@@ -90,6 +90,7 @@ def bind(lib):
     _p(lib, "gpbs_gpu_set_table_mode", C.c_int, vp, C.c_int)
     _p(lib, "gpbs_gpu_table_mode", C.c_int, vp)
     _p(lib, "gpbs_gpu_set_hold", C.c_int, vp, C.c_int, C.POINTER(C.c_uint64))
+    _p(lib, "gpbs_gpu_force_hold", C.c_int, vp, C.c_int)
     _p(lib, "gpbs_gpu_set_spatial", C.c_int, vp, C.c_int)
     _p(lib, "gpbs_gpu_set_waveprio", C.c_int, vp, C.c_int)
     _p(lib, "gpbs_gpu_ctx_destroy", None, vp)

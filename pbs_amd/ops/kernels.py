@@ -67,12 +67,14 @@ def gemm_bf16(A: torch.Tensor, Bt: torch.Tensor, out: Optional[torch.Tensor] = N
 
 
 def stream_copy(src: torch.Tensor, dst: torch.Tensor, *, chunk_bytes: int = 1 << 19, table=None, tenant: int = 0,
-                counters=None, grid: int = 0, stream=None):
+                counters=None, grid: int = 0, stream=None, mode_extra: int = 0):
+    """``mode_extra``: gate-mode bits OR-ed in when ``table`` is given
+    (e.g. GATE_DEVTABLE | GATE_HOLD for a VRAM table with the hold word)."""
     nbytes = src.numel() * src.element_size()
     assert dst.numel() * dst.element_size() >= nbytes and nbytes % 16 == 0
     q = work_queue(src.device)
     rc = lib().gpbs_hip_stream_copy(_ptr(src), _ptr(dst), nbytes, chunk_bytes, _ptr(q), table,
-                                    GATE_TABLE if table else GATE_NONE, tenant, counters, None, grid,
+                                    (GATE_TABLE | mode_extra) if table else GATE_NONE, tenant, counters, None, grid,
                                     _stream(stream))
     _check(rc, "stream_copy")
     return dst
@@ -106,6 +108,7 @@ def gemv_bf16(W: torch.Tensor, x: torch.Tensor, out: Optional[torch.Tensor] = No
 
 
 GATE_SPATIAL = 8
+GATE_DEVTABLE, GATE_HOLD = 4, 64
 
 
 def census(blocks: int = 2048, table=None, tenant: int = 0, stream=None, spatial: bool = False) -> torch.Tensor:

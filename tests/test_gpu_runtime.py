@@ -208,3 +208,37 @@ def test_bar_table_gates_runners_and_census():
     r1.close()
     r2.close()
     ctx.close()
+
+
+def test_hold_word_pauses_gate_hold_kernels_bounded():
+    """GATE_HOLD: a kernel waits (bounded, ~0.25 ms per unit grab) while the
+    table's hold word is set, and runs at full speed once it is cleared; the
+    data is copied either way."""
+    from pbs_amd.ops import kernels as K
+    ctx = GpuContext(0, table_mode="bar")
+    ctx.set_owners([5] * 8)
+    x = torch.randn(1 << 20, device="cuda")
+    y = torch.empty_like(x)
+
+    def timed(hold):
+        ctx.L.gpbs_gpu_force_hold(ctx.h, 1 if hold else 0)
+        y.zero_()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        K.stream_copy(x, y, chunk_bytes=1 << 16, table=ctx.table, tenant=5, grid=64,
+                      mode_extra=K.GATE_DEVTABLE | K.GATE_HOLD)
+        e1.record()
+        torch.cuda.synchronize()
+        assert torch.equal(x, y)
+        return e0.elapsed_time(e1)
+
+    timed(False)  # warm-up
+    off = min(timed(False) for _ in range(3))
+    on = timed(True)
+    ctx.L.gpbs_gpu_force_hold(ctx.h, 0)
+    after = min(timed(False) for _ in range(3))
+    assert on > off + 0.2, (on, off)   # every grab waited out the bounded hold
+    assert on < 20.0, on               # bounded: a stuck hold word cannot stall a tenant
+    assert after < off + 0.1, (after, off)
+    ctx.close()
