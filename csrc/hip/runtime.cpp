@@ -338,9 +338,11 @@ void publish(GpuCtx* c) {
     for (int x = 0; x < kXcds * kCtx; ++x) __atomic_store_n(&c->h_table->owner[x], c->pending[x], __ATOMIC_RELEASE);
     c->epoch++;
     __atomic_store_n(&c->h_table->epoch, c->epoch, __ATOMIC_RELEASE);
+    // BAR table: written under the lock, so two publishers (dispatcher and
+    // API) cannot interleave their owner words in VRAM
+    if (c->table_mode == 2) bar_write(c->b_table, c->h_table->owner, c->epoch);
   }
   if (c->table_mode == 1) gpbs_hip_partition_switch(c->d_table, c->epoch, c->pending, c->sched_stream);
-  else if (c->table_mode == 2) bar_write(c->b_table, c->h_table->owner, c->epoch);
   c->flushes++;
   c->cv.notify_all();
 }
