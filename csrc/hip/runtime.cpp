@@ -146,11 +146,26 @@ PartTable* bar_alloc(int device) {
     hsa_amd_memory_pool_free(p);
     return nullptr;
   }
+  // Pool memory is not zeroed: clear the whole 4 KiB (a stale hold word
+  // would stall every GATE_HOLD grab until the first latency unit completes)
+  volatile u32* w = (volatile u32*)p;
+  for (int i = 0; i < 1024; ++i) w[i] = 0;
+  _mm_sfence();
   return (PartTable*)p;
 }
 
 // Owner words first, then the epoch, each group fenced out of the CPU's
 // write-combining buffers (a kernel that sees the new epoch sees the owners).
+void bar_write(PartTable* b, const u32* owners, u32 epoch);
+
+// Whole-table resync from the host table (entering BAR mode): flags and the
+// hold word too, not only the owners.
+void bar_sync(PartTable* b, const PartTable* h) {
+  *(volatile u32*)&b->flags = __atomic_load_n(&h->flags, __ATOMIC_ACQUIRE);
+  *(volatile u32*)&b->hold = __atomic_load_n(&h->hold, __ATOMIC_ACQUIRE);
+  bar_write(b, h->owner, __atomic_load_n(&h->epoch, __ATOMIC_ACQUIRE));
+}
+
 void bar_write(PartTable* b, const u32* owners, u32 epoch) {
   volatile u32* o = (volatile u32*)b->owner;
   for (int x = 0; x < kXcds * kCtx; ++x) o[x] = owners[x];
@@ -185,8 +200,18 @@ struct GpuCtx {
   int waveprio = 0;              // latency-class runners raise their wave priority
   int hold_enable = 0;           // latency requests hold the memory-class tenants (GATE_HOLD)
   int hold_all = 0;              // GPBS_HOLD_ALL=1: hold every gated tenant, compute class too (ablation)
-  std::atomic<int> holds{0};     // latency units in flight (the hold word is set while > 0)
+  // Latency-request hold: count of latency units in flight and the hold
+  // word derived from it, changed together under hold_mu.  hold_gen changes
+  // whenever the hold is switched off (holds reset): a runner releases only
+  // the raises it made in the current generation.
+  std::mutex hold_mu;
+  int holds = 0;
+  uint64_t hold_gen = 0;
   std::atomic<uint64_t> hold_raises{0};
+  // per-tenant contention class cache (-1 unknown), refreshed under the
+  // engine lock by the metric tick and table publishes: launch() reads it
+  // without taking the engine lock
+  std::atomic<int> cls_cache[kMaxTenants];
   u32 pending[kXcds * kCtx];
   u32 epoch = 0;
   // async counter reduce (one metric period of lag, never blocks the engine)
@@ -288,7 +313,10 @@ void act_on_switch(void* user, int part, int, int next, int, int32_t, int64_t) {
   const int i = part - c->part_base;
   if (i < 0 || i >= kXcds * c->nctx) return;
   const int x = i / c->nctx, ctx = i % c->nctx;
-  c->pending[x * kCtx + ctx] = next >= 0 ? (u32)next : kNoOwner;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    c->pending[x * kCtx + ctx] = next >= 0 ? (u32)next : kNoOwner;
+  }
   c->switches++;
   if (roctx_switch_marks()) {  // TRC_SCHED_SWITCH analog (X:xen/common/schedule.c:1138-1151)
     char m[64];
@@ -309,9 +337,11 @@ void mark_splits(GpuCtx* c) {
     a &= kOwnerMask | (a == kNoOwner ? kSplitBit : 0u);
     b &= kOwnerMask | (b == kNoOwner ? kSplitBit : 0u);
     if (!c->spatial || c->nctx != 2 || a == kNoOwner || b == kNoOwner || a == b) continue;
-    // No engine attached (manual tables): distinct owners are split.
-    const int ca = c->engine ? gpbs_tenant_class(c->engine, (int)a) : 0;
-    const int cb = c->engine ? gpbs_tenant_class(c->engine, (int)b) : 1;
+    // No engine attached (manual tables): distinct owners are split.  The
+    // class comes from the cache (c->mu is held: no engine lock from here,
+    // the dispatcher takes them in the opposite order).
+    const int ca = c->engine ? (a < (u32)kMaxTenants ? c->cls_cache[a].load(std::memory_order_relaxed) : -1) : 0;
+    const int cb = c->engine ? (b < (u32)kMaxTenants ? c->cls_cache[b].load(std::memory_order_relaxed) : -1) : 1;
     if (ca >= 0 && cb >= 0 && ca != cb) {
       a |= kSplitBit;
       b |= kSplitBit;
@@ -319,15 +349,18 @@ void mark_splits(GpuCtx* c) {
   }
 }
 
-void publish(GpuCtx* c) {
+// Publish the pending assignment.  Everything -- split marks, the change
+// test, the host / BAR table stores and the k_partition_switch enqueue (from
+// copies of pending and epoch) -- happens under c->mu, so two publishers (the
+// dispatcher and an API caller) cannot interleave owner words in any table.
+// publish_locked: caller holds c->mu; returns whether an owner changed.
+bool publish_locked(GpuCtx* c) {
   mark_splits(c);
   bool changed = false;
   for (int x = 0; x < kXcds * kCtx; ++x)
     if (__atomic_load_n(&c->h_table->owner[x], __ATOMIC_RELAXED) != c->pending[x]) changed = true;
-  if (!changed) return;
-  RoctxRange rr("gpbs:publish");
+  if (!changed) return false;
   {
-    std::lock_guard<std::mutex> g(c->mu);
     const int64_t t = mono_ns();
     if (c->last_pub_ns)
       for (int x = 0; x < kXcds * kCtx; ++x) {
@@ -338,25 +371,69 @@ void publish(GpuCtx* c) {
     for (int x = 0; x < kXcds * kCtx; ++x) __atomic_store_n(&c->h_table->owner[x], c->pending[x], __ATOMIC_RELEASE);
     c->epoch++;
     __atomic_store_n(&c->h_table->epoch, c->epoch, __ATOMIC_RELEASE);
-    // BAR table: written under the lock, so two publishers (dispatcher and
-    // API) cannot interleave their owner words in VRAM
     if (c->table_mode == 2) bar_write(c->b_table, c->h_table->owner, c->epoch);
+    if (c->table_mode == 1) {
+      u32 own[kXcds * kCtx];
+      std::memcpy(own, c->pending, sizeof(own));
+      gpbs_hip_partition_switch(c->d_table, c->epoch, own, c->sched_stream);
+    }
   }
-  if (c->table_mode == 1) gpbs_hip_partition_switch(c->d_table, c->epoch, c->pending, c->sched_stream);
   c->flushes++;
-  c->cv.notify_all();
+  return true;
 }
 
-void act_on_flush(void* user, int64_t) { publish((GpuCtx*)user); }
+void publish(GpuCtx* c) {
+  RoctxRange rr("gpbs:publish");
+  bool changed;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    changed = publish_locked(c);
+  }
+  if (changed) c->cv.notify_all();
+}
+
+// Refresh the class cache of every tenant (engine lock held by the caller).
+void refresh_classes(GpuCtx* c) {
+  if (!c->engine) return;
+  for (int t = 0; t < kMaxTenants; ++t) c->cls_cache[t].store(gpbs_tenant_class(c->engine, t), std::memory_order_relaxed);
+}
+
+void act_on_flush(void* user, int64_t) {
+  GpuCtx* c = (GpuCtx*)user;
+  refresh_classes(c);
+  publish(c);
+}
 
 // The hold word goes wherever the tenants read their table from: the pinned
-// host table (always) and the BAR-written VRAM table.
+// host table (always) and the BAR-written VRAM table whenever it exists (a
+// later switch into BAR mode must not find a stale word).  Caller holds
+// hold_mu (or has no concurrent hold users).
 void set_hold(GpuCtx* c, u32 v) {
   __atomic_store_n(&c->h_table->hold, v, __ATOMIC_RELEASE);
-  if (c->table_mode == 2 && c->b_table) {
+  if (c->b_table) {
     *(volatile u32*)&c->b_table->hold = v;
     _mm_sfence();
   }
+}
+
+// A latency unit enters flight: count it; the first one raises the word.
+// Returns the generation the raise belongs to.
+uint64_t hold_acquire(GpuCtx* c) {
+  std::lock_guard<std::mutex> g(c->hold_mu);
+  if (c->holds++ == 0) {
+    set_hold(c, 1);
+    c->hold_raises.fetch_add(1, std::memory_order_relaxed);
+  }
+  return c->hold_gen;
+}
+
+// A latency unit left flight (completed, or its runner stopped): the last one
+// clears the word.  Raises of an older generation (the hold was switched off
+// and the count reset since) are ignored.
+void hold_release(GpuCtx* c, uint64_t gen) {
+  std::lock_guard<std::mutex> g(c->hold_mu);
+  if (gen != c->hold_gen || c->holds <= 0) return;
+  if (--c->holds == 0) set_hold(c, 0);
 }
 
 void act_on_park(void*, int, int, int) {}
@@ -380,9 +457,9 @@ void share_update(GpuCtx* c) {
       if (!seen) owners[n++] = (int)o;
     }
     if (n >= 2) {
-      const int c0 = gpbs_tenant_class(c->engine, owners[0]);
+      const int c0 = c->cls_cache[owners[0]].load(std::memory_order_relaxed);
       want = c0 >= 0;
-      for (int k = 1; k < n && want; ++k) want = gpbs_tenant_class(c->engine, owners[k]) == c0;
+      for (int k = 1; k < n && want; ++k) want = c->cls_cache[owners[k]].load(std::memory_order_relaxed) == c0;
     }
     if (want && c->probe_every > 0 && (c->share_tick++ % (uint64_t)c->probe_every) < (uint64_t)c->probe_len)
       want = 0;  // exclusive probe window
@@ -627,6 +704,10 @@ int hwc_tenant_deltas(GpuCtx* c, int n, const int* tenants, uint64_t* out) {
 int ctr_tenant_deltas(void* user, int n, const int* tenants, uint64_t* out) {
   GpuCtx* c = (GpuCtx*)user;
   if (n > kMaxTenants) return -22;
+  if (c->engine)  // engine lock held: refresh the class cache launch() reads
+    for (int k = 0; k < n; ++k)
+      if (tenants[k] >= 0 && tenants[k] < kMaxTenants)
+        c->cls_cache[tenants[k]].store(gpbs_tenant_class(c->engine, tenants[k]), std::memory_order_relaxed);
   if (c->hwc) return hwc_tenant_deltas(c, n, tenants, out);
   const int64_t t0 = mono_ns();
   RoctxRange rr("gpbs:metric_tick");
@@ -788,6 +869,15 @@ struct Runner {
   std::vector<int64_t> lats;
   hipEvent_t ev[16];
   int err = 0;
+  // latency hold raised by the unit of queue slot qi (generation + 1; 0: none)
+  uint64_t q_hold[16] = {};
+
+  void hold_drop(int qi) {
+    if (q_hold[qi]) {
+      hold_release(ctx, q_hold[qi] - 1);
+      q_hold[qi] = 0;
+    }
+  }
 
   u32 unit_total() const {
     switch (cfg.kind) {
@@ -869,7 +959,7 @@ struct Runner {
     // memory-class tenants pause at unit boundaries while a latency request
     // is in flight (only where the host can write the hold word: host / BAR table)
     const bool hold = gate && ctx->hold_enable && tm != 1 && cfg.kind != K_GEMV && ctx->engine &&
-                      (ctx->hold_all || gpbs_tenant_class(ctx->engine, cfg.tenant) == 1);
+                      (ctx->hold_all || ctx->cls_cache[cfg.tenant].load(std::memory_order_relaxed) == 1);
     const unsigned mode = (gate ? (cfg.gate == 2 ? GATE_PARK : GATE_TABLE) : GATE_NONE) | (dev ? GATE_DEVTABLE : 0) |
                           (gate && ctx->spatial ? GATE_SPATIAL : 0) |
                           (gate && __atomic_load_n(&ctx->se_mode, __ATOMIC_ACQUIRE) ? GATE_SE : 0) |
@@ -973,11 +1063,7 @@ struct Runner {
             // resume the same queue: clear exit bookkeeping only
             hipMemsetAsync(&d_q[qi].exited, 0, sizeof(u32) * 2, stream);
           }
-          const bool lat_hold = cfg.priority > 0 && ctx->hold_enable && fresh;
-          if (lat_hold && ctx->holds.fetch_add(1) == 0) {
-            set_hold(ctx, 1);
-            ctx->hold_raises.fetch_add(1, std::memory_order_relaxed);
-          }
+          if (cfg.priority > 0 && ctx->hold_enable && fresh && !q_hold[qi]) q_hold[qi] = hold_acquire(ctx) + 1;
           if (launch(qi, stream) != 0) err = -5;
           const int e = qi;  // one event per queue slot
           hipEventRecord(ev[e], stream);
@@ -997,8 +1083,7 @@ struct Runner {
         const u32 s = __atomic_load_n(&h_status[f.qi], __ATOMIC_ACQUIRE);
         const u32 done = s & 0x7fffffffu;
         if ((s & 0x80000000u) && done >= unit_total()) {
-          if (cfg.priority > 0 && ctx->hold_enable && ctx->holds.load() > 0 && ctx->holds.fetch_sub(1) == 1)
-            set_hold(ctx, 0);
+          hold_drop(f.qi);
           const int64_t t = mono_ns();
           std::lock_guard<std::mutex> g(mu);
           q_busy[f.qi] = 0;
@@ -1033,6 +1118,7 @@ struct Runner {
       if (h) hipStreamSynchronize(h);
     for (hipStream_t h : se_stream)
       if (h) hipStreamSynchronize(h);
+    for (int qi = 0; qi < nq; ++qi) hold_drop(qi);  // stopped with latency units in flight
     std::lock_guard<std::mutex> g(mu);
     idle_cv.notify_all();
   }
@@ -1053,6 +1139,7 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
   std::memset(c->own_ns, 0, sizeof(c->own_ns));
   std::memset(c->own_base, 0, sizeof(c->own_base));
   for (int& r : c->prev_raw) r = -1;
+  for (auto& k : c->cls_cache) k.store(-1, std::memory_order_relaxed);
   if (const char* v = std::getenv("GPBS_SHARE")) c->share_enable = std::atoi(v) != 0;
   if (const char* v = std::getenv("GPBS_HOLD_ALL")) c->hold_all = std::atoi(v) != 0;
   if (const char* v = std::getenv("GPBS_HWC_PERIOD_US")) c->hwc_period_us = std::max(100, std::atoi(v));
@@ -1380,7 +1467,9 @@ int gpbs_gpu_set_hold(void* p, int on, uint64_t* raises) {
   if (on >= 0) {
     __atomic_store_n(&c->hold_enable, on ? 1 : 0, __ATOMIC_RELEASE);
     if (!on) {
-      c->holds.store(0);
+      std::lock_guard<std::mutex> g(c->hold_mu);
+      c->holds = 0;
+      c->hold_gen++;  // raises still held by runners belong to the old generation
       set_hold(c, 0);
     }
   }
@@ -1392,6 +1481,7 @@ int gpbs_gpu_set_hold(void* p, int on, uint64_t* raises) {
 int gpbs_gpu_force_hold(void* p, int v) {
   GpuCtx* c = (GpuCtx*)p;
   if (!c) return -22;
+  std::lock_guard<std::mutex> g(c->hold_mu);
   set_hold(c, v ? 1u : 0u);
   return 0;
 }
@@ -1419,7 +1509,10 @@ int gpbs_gpu_set_table_mode(void* p, int mode) {
       c->b_table = bar_alloc(c->device);
       if (!c->b_table) return -95;  // no host-accessible fine-grained VRAM pool on this system
     }
-    bar_write(c->b_table, c->h_table->owner, c->h_table->epoch);
+    {
+      std::lock_guard<std::mutex> hg(c->hold_mu);
+      bar_sync(c->b_table, c->h_table);
+    }
     __atomic_store_n(&c->table_mode, 2, __ATOMIC_RELEASE);
     return 0;
   }
@@ -1443,8 +1536,12 @@ void* gpbs_gpu_counters(void* p) { return ((GpuCtx*)p)->d_cnt; }
 // owners: [kXcds * kCtx] entries (kCtx = 4), (xcd, context) major, -1 = idle.
 int gpbs_gpu_set_owners(void* p, const int* owners) {
   GpuCtx* c = (GpuCtx*)p;
-  for (int x = 0; x < kXcds * kCtx; ++x) c->pending[x] = owners[x] >= 0 ? (u32)owners[x] : kNoOwner;
-  publish(c);
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    for (int x = 0; x < kXcds * kCtx; ++x) c->pending[x] = owners[x] >= 0 ? (u32)owners[x] : kNoOwner;
+    publish_locked(c);
+  }
+  c->cv.notify_all();
   return 0;
 }
 
@@ -1538,10 +1635,14 @@ int gpbs_gpu_switch_latency(void* p, int iters, int nwg, int64_t* out_ns) {
   int done = 0;
   if (rc == 0 && all_acked(0xFFFFFFFEu, 2000000000LL)) {
     for (int it = 0; it < iters; ++it) {
-      for (int x = 0; x < kXcds * kCtx; ++x) c->pending[x] = (u32)((it + x) & 1);
       const int64_t t0 = mono_ns();
-      publish(c);
-      const u32 e = c->epoch;
+      u32 e;
+      {
+        std::lock_guard<std::mutex> g(c->mu);
+        for (int x = 0; x < kXcds * kCtx; ++x) c->pending[x] = (u32)((it + x) & 1);
+        publish_locked(c);
+        e = c->epoch;
+      }
       if (!all_acked(e, 100000000LL)) {
         rc = -110;
         break;

@@ -20,6 +20,7 @@
 // e.g. the GPU partition-table actuator).
 #include <fcntl.h>
 #include <linux/futex.h>
+#include <sched.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <sys/syscall.h>
@@ -110,6 +111,16 @@ struct Ctl {
   std::mutex mu;
   std::mutex pub_mu;  // one seqlock writer at a time (flush vs. assign/publish)
   uint32_t epoch = 0;
+  // torn_page fault: a publish left half-written (seq odd) that the bridge
+  // thread completes at `due` -- never a sleep under the engine lock
+  struct Torn {
+    bool active = false;
+    int64_t due = 0;
+    uint64_t mask1 = 0;
+    uint32_t quantum = 0, epoch = 0, seq = 0, gate = 0, old_gate = 0;
+    int32_t prio = 0, tid = -1;
+  };
+  std::vector<Torn> torn;  // per page (pub_mu)
 };
 
 int64_t now_ns() {
@@ -177,16 +188,54 @@ Ctl* map_region(const char* name, int ntenants, bool create) {
   return c;
 }
 
+void ring_doorbell(Page* pg, uint32_t gate, uint32_t old_gate) {
+  if (gate != old_gate || gate) {
+    pg->doorbell.fetch_add(1, std::memory_order_acq_rel);
+    futex(&pg->doorbell, FUTEX_WAKE, 0x7fffffff, nullptr);
+  }
+}
+
+// Second half of a deferred (torn) publish: the remaining fields, then the
+// even sequence number.  Caller holds pub_mu.
+void complete_torn(Page* pg, Ctl::Torn& t) {
+  if (!t.active) return;
+  pg->mask[1].store(t.mask1, std::memory_order_relaxed);
+  pg->quantum_us.store(t.quantum, std::memory_order_relaxed);
+  pg->priority.store(t.prio, std::memory_order_relaxed);
+  pg->tenant_id.store(t.tid, std::memory_order_relaxed);
+  pg->epoch.store(t.epoch, std::memory_order_relaxed);
+  std::atomic_thread_fence(std::memory_order_release);
+  pg->seq.store(t.seq + 2, std::memory_order_release);
+  t.active = false;
+  ring_doorbell(pg, t.gate, t.old_gate);
+}
+
+// Seqlock publication of one page (caller holds pub_mu).  With `torn`, the
+// publish stops half-written (odd sequence) and the bridge thread completes
+// it after `torn_us` (the torn_page fault: readers must retry, never return
+// a half-written assignment).
 void publish_page(Page* pg, uint32_t gate, const uint64_t* mask, uint32_t quantum, int32_t prio, int32_t tid,
-                  uint32_t epoch, int64_t torn_us = -1) {
+                  uint32_t epoch, Ctl::Torn* torn = nullptr, int64_t torn_us = -1) {
+  if (torn) complete_torn(pg, *torn);  // a still-pending torn publish of this page lands first
   uint32_t s = pg->seq.load(std::memory_order_relaxed);
   const uint32_t old_gate = pg->gate.load(std::memory_order_relaxed);
   pg->seq.store(s + 1, std::memory_order_relaxed);
   std::atomic_thread_fence(std::memory_order_release);
   pg->gate.store(gate, std::memory_order_relaxed);
   pg->mask[0].store(mask[0], std::memory_order_relaxed);
-  if (torn_us >= 0)  // torn_page fault: readers see a half-written page (odd seq) for a while
-    std::this_thread::sleep_for(std::chrono::microseconds(std::max<int64_t>(torn_us, 50)));
+  if (torn && torn_us >= 0) {
+    torn->active = true;
+    torn->due = now_ns() + std::max<int64_t>(torn_us, 50) * 1000;
+    torn->mask1 = mask[1];
+    torn->quantum = quantum;
+    torn->prio = prio;
+    torn->tid = tid;
+    torn->epoch = epoch;
+    torn->seq = s;
+    torn->gate = gate;
+    torn->old_gate = old_gate;
+    return;
+  }
   pg->mask[1].store(mask[1], std::memory_order_relaxed);
   pg->quantum_us.store(quantum, std::memory_order_relaxed);
   pg->priority.store(prio, std::memory_order_relaxed);
@@ -194,11 +243,34 @@ void publish_page(Page* pg, uint32_t gate, const uint64_t* mask, uint32_t quantu
   pg->epoch.store(epoch, std::memory_order_relaxed);
   std::atomic_thread_fence(std::memory_order_release);
   pg->seq.store(s + 2, std::memory_order_release);
-  if (gate != old_gate || gate) {
-    pg->doorbell.fetch_add(1, std::memory_order_acq_rel);
-    futex(&pg->doorbell, FUTEX_WAKE, 0x7fffffff, nullptr);
-  }
+  ring_doorbell(pg, gate, old_gate);
 }
+
+// Complete every deferred publish that is due (all of them with force).
+void complete_due_torn(Ctl* c, bool force) {
+  std::lock_guard<std::mutex> g(c->pub_mu);
+  const int64_t t = now_ns();
+  for (size_t i = 0; i < c->torn.size(); ++i)
+    if (c->torn[i].active && (force || t >= c->torn[i].due)) complete_torn(&c->pages[i], c->torn[i]);
+}
+
+// Seqlock reader back-off: spin briefly, then yield; a writer that died
+// mid-publish (odd sequence forever) makes the read fail with -EAGAIN after
+// ~50 ms instead of hanging the tenant at 100 % CPU.
+struct SeqBackoff {
+  int spins = 0;
+  int64_t t0 = 0;
+  bool again() {
+    if (++spins < 64) {
+      __builtin_ia32_pause();
+      return true;
+    }
+    if (!t0) t0 = now_ns();
+    if (now_ns() - t0 > 50000000) return false;
+    sched_yield();
+    return true;
+  }
+};
 
 // ----------------------------------------------------------------- bridge --
 
@@ -224,7 +296,8 @@ void br_on_flush(void* user, int64_t now) {
     const uint64_t m[2] = {c->pend_mask[2 * tid], c->pend_mask[2 * tid + 1]};
     if (m[0] == pg->mask[0].load(std::memory_order_relaxed) && m[1] == pg->mask[1].load(std::memory_order_relaxed)) continue;
     publish_page(pg, (m[0] | m[1]) ? 1u : 0u, m, pg->quantum_us.load(std::memory_order_relaxed),
-                 pg->priority.load(std::memory_order_relaxed), tid, c->epoch, gpbs_fault_fire(c->engine, "torn_page"));
+                 pg->priority.load(std::memory_order_relaxed), tid, c->epoch, &c->torn[i],
+                 gpbs_fault_fire(c->engine, "torn_page"));
   }
 }
 
@@ -300,9 +373,11 @@ void bridge_loop(Ctl* c) {
           publish_vpmu(pg, tot, ti.cache_miss_rate, ti.tslice_us, gpbs_tenant_class(c->engine, tid), ti.phase);
       }
     }
+    complete_due_torn(c, false);
     timespec ts{0, 100000};  // 100 us poll
     nanosleep(&ts, nullptr);
   }
+  complete_due_torn(c, true);
 }
 
 }  // namespace
@@ -340,8 +415,9 @@ void gpbs_ctl_publish(void* h, int t, uint32_t gate, uint64_t mask, uint32_t qua
   Page* pg = page(h, t);
   if (!pg) return;
   const uint64_t m[2] = {mask, 0};
-  std::lock_guard<std::mutex> g(((Ctl*)h)->pub_mu);
-  publish_page(pg, gate, m, quantum_us, prio, tid, epoch);
+  Ctl* c = (Ctl*)h;
+  std::lock_guard<std::mutex> g(c->pub_mu);
+  publish_page(pg, gate, m, quantum_us, prio, tid, epoch, (size_t)t < c->torn.size() ? &c->torn[t] : nullptr);
 }
 
 // Seqlock read; returns the number of retries (torn reads observed).
@@ -350,10 +426,12 @@ int gpbs_ctl_read(void* h, int t, uint32_t* gate, uint64_t* mask, uint32_t* quan
   Page* pg = page(h, t);
   if (!pg) return -22;
   int retries = 0;
+  SeqBackoff bo;
   for (;;) {
     const uint32_t s0 = pg->seq.load(std::memory_order_acquire);
     if (s0 & 1) {
       ++retries;
+      if (!bo.again()) return -11;
       continue;
     }
     const uint32_t g = pg->gate.load(std::memory_order_relaxed);
@@ -373,6 +451,7 @@ int gpbs_ctl_read(void* h, int t, uint32_t* gate, uint64_t* mask, uint32_t* quan
       return retries;
     }
     ++retries;
+    if (!bo.again()) return -11;
   }
 }
 
@@ -381,10 +460,12 @@ int gpbs_ctl_read_vpmu(void* h, int t, uint64_t* c4, uint64_t* miss_rate, uint32
   Page* pg = page(h, t);
   if (!pg) return -22;
   int retries = 0;
+  SeqBackoff bo;
   for (;;) {
     const uint32_t s0 = pg->vseq.load(std::memory_order_acquire);
     if (s0 & 1) {
       ++retries;
+      if (!bo.again()) return -11;
       continue;
     }
     uint64_t v[4];
@@ -405,6 +486,7 @@ int gpbs_ctl_read_vpmu(void* h, int t, uint64_t* c4, uint64_t* miss_rate, uint32
       return retries;
     }
     ++retries;
+    if (!bo.again()) return -11;
   }
 }
 
@@ -496,9 +578,13 @@ int gpbs_ctl_doorbell_wait(void* h, int t, int64_t timeout_ns) {
 int gpbs_ctl_read_mask(void* h, int t, uint64_t* mask2, uint32_t* epoch) {
   Page* pg = page(h, t);
   if (!pg) return -22;
+  SeqBackoff bo;
   for (;;) {
     const uint32_t s0 = pg->seq.load(std::memory_order_acquire);
-    if (s0 & 1) continue;
+    if (s0 & 1) {
+      if (!bo.again()) return -11;
+      continue;
+    }
     const uint32_t g = pg->gate.load(std::memory_order_relaxed);
     const uint64_t m0 = pg->mask[0].load(std::memory_order_relaxed), m1 = pg->mask[1].load(std::memory_order_relaxed);
     const uint32_t e = pg->epoch.load(std::memory_order_relaxed);
@@ -511,6 +597,7 @@ int gpbs_ctl_read_mask(void* h, int t, uint64_t* mask2, uint32_t* epoch) {
       if (epoch) *epoch = e;
       return (int)g;
     }
+    if (!bo.again()) return -11;
   }
 }
 
@@ -537,6 +624,10 @@ int gpbs_ctl_bind(void* h, void* engine) {
   c->pend_mask.assign(2 * 4096, 0);
   c->last_work.assign(c->hdr->ntenants, 0);
   c->last_hb_sent.assign(c->hdr->ntenants, 0);
+  {
+    std::lock_guard<std::mutex> g(c->pub_mu);
+    c->torn.assign(c->hdr->ntenants, Ctl::Torn{});
+  }
   gpbs_actuator_ops_t a{};
   a.user = c;
   a.on_switch = br_on_switch;
@@ -555,12 +646,13 @@ int gpbs_ctl_assign(void* h, int t, int tid) {
   Page* pg = page(h, t);
   if (!pg) return -22;
   const uint64_t m[2] = {0, 0};
-  std::lock_guard<std::mutex> g(((Ctl*)h)->pub_mu);
+  Ctl* c = (Ctl*)h;
+  std::lock_guard<std::mutex> g(c->pub_mu);
   if (pg->tenant_id.load(std::memory_order_acquire) < 0) {  // the bridge skips unassigned pages: no second writer
     const uint64_t z[4] = {0, 0, 0, 0};
     publish_vpmu(pg, z, 0, 0, -1, 0);
   }
-  publish_page(pg, 0, m, 0, 0, tid, 0);
+  publish_page(pg, 0, m, 0, 0, tid, 0, (size_t)t < c->torn.size() ? &c->torn[t] : nullptr);
   return 0;
 }
 
