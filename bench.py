@@ -3,16 +3,26 @@
 
     python bench.py --gpus N --steps K --warmup W
 
-Runs the BASELINE.json metric — co-run slowdown vs solo + aggregate
+Runs the BASELINE.json metric -- co-run slowdown vs solo + aggregate
 throughput of the 4-tenant mix (MFMA GEMM + HBM stream + all-reduce + idle)
-per MI355X — under the gpbs PBS adaptive credit scheduler, one rank per GPU
-(weak scaling: every GPU hosts its own 4-tenant mix; the all-reduce tenant
-spans all GPUs over RCCL/xGMI when N > 1).  Rank 0 prints ONE JSON line.
+per MI355X -- under the gpbs PBS adaptive credit scheduler, one rank per GPU
+(weak scaling: every GPU hosts its own mix; the all-reduce tenant spans all
+GPUs over RCCL/xGMI when N > 1).  Rank 0 prints ONE JSON line.
 
-``value`` = aggregate normalized throughput summed over all GPUs
-(sum over tenants of solo_time/co-run_time, "solo-equivalents"; higher is
-better).  Comparison policies (none = default hardware sharing, static =
-equal XCD split) are measured on the same box and reported alongside.
+``value`` = aggregate normalized throughput of the headline mix summed over
+all GPUs (sum over throughput tenants of co-run rate / solo rate,
+"solo-equivalents"; higher is better).  Solo rates are measured with the
+same steady protocol as the co-run (backlogged, W + K windows, alone).
+Comparison policies run on the same box, 5 randomized reps each: none
+(default hardware sharing), static (equal XCD split), static-se (the
+hand-picked shader-engine layout, no engine, no counters), the PBS ablations
+(credit-fixed*, gpbs-ts) and gpbs-lat (latency hold).
+
+By default two more mixes run after the headline and are reported under
+``mixes``: "phase" (a tenant alternating GEMM <-> stream every 300 ms and a
+stream tenant stopping / starting every 500 ms: the counter-driven layout
+must follow, a static one cannot) and "8mix" (config #4's 8 tenants on one
+GPU: classes must time-share their shader engines, where PBS quanta apply).
 Data: synthetic random-init bf16 tensors of the named shapes.
 """
 from __future__ import annotations
@@ -33,8 +43,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--policies", default="none,static,credit2,credit-fixed-ts,gpbs-ts,credit-fixed,gpbs-lat,gpbs",
-                    help="comma list; gpbs is the reported policy")
+    ap.add_argument("--policies", default="",
+                    help="comma list for the headline mix (default: per-mix list below); gpbs is the reported policy")
     ap.add_argument("--keep-engines", action="store_true",
                     help="one engine per policy for the whole process (default: a fresh engine per timed run)")
     ap.add_argument("--reps", type=int, default=5,
@@ -61,8 +71,10 @@ def main():
                     help="PBS metric source: live CDNA4 hardware counters (rocprofiler-sdk device counting, "
                          "attributed to tenants by shader-engine ownership; default), or the modeled per-tile "
                          "counters of the tenant kernels (debug cross-check)")
-    ap.add_argument("--mix", default="4mix", choices=["4mix", "gemm2"],
-                    help="4mix: BASELINE config #3/#4 (headline); gemm2: config #2 (two 4096^2 GEMM tenants)")
+    ap.add_argument("--mix", default="all", choices=["all", "4mix", "gemm2", "phase", "8mix"],
+                    help="all (default): 4mix (headline, BASELINE config #3) + phase (phase-changing mix) + 8mix "
+                         "(config #4's 8 tenants on one GPU); gemm2: config #2 (two 4096^2 GEMM tenants)")
+    ap.add_argument("--reps-extra", type=int, default=5, help="reps of the non-headline mixes")
     args = ap.parse_args()
     if os.environ.get("GPBS_HANG_DUMP_S"):  # diagnostics: every thread's stack when a run stops progressing
         import faulthandler
@@ -107,7 +119,7 @@ def main():
         build.build_all()
     if world > 1:
         dist.barrier(group=groups["ctrl"])
-    from pbs_amd.bench.corun import Corun, CorunConfig
+    from pbs_amd.bench.corun import MIXES, Corun, CorunConfig
     # gang epochs (N > 1): native shared-memory transport among the node's
     # ranks; the region name is a nonce from rank 0 so no stale region matches
     gang_base = ""
@@ -116,32 +128,9 @@ def main():
         dist.broadcast(nonce, src=0, group=groups["ctrl"])
         gang_base = f"gpbs-gang-{int(nonce.item()):08x}"
 
-    pols = tuple(p for p in args.policies.split(",") if p)
-    if "gpbs" not in pols:
-        pols = pols + ("gpbs",)
-    cfg = CorunConfig(steps=args.steps, warmup=args.warmup, target_ms=args.target_ms, policies=pols,
-                      table_mode=args.table, mix=args.mix, hw_counters=(counters == "hw"),
-                      protocol=args.protocol, step_ms=args.step_ms, gang_transport=args.gang_transport,
-                      gang_shm_base=gang_base, gang_wait_driven=args.gang_wait_driven,
-                      fresh_engine=not args.keep_engines)
-    if args.rehearse:
-        cfg.coll_bytes = 4 << 20  # CPU gloo all-reduce stand-in
+    mixes = ["4mix", "phase", "8mix"] if args.mix == "all" else [args.mix]
     log = (lambda *a: print(*a, file=sys.stderr, flush=True))
-    c = Corun(cfg, rank=rank, world=world, device=local, groups=groups, log=log, coll_on_cpu=args.rehearse)
-    c.calibrate()
-    # Measurement protocol: every policy is measured `reps`
-    # times; each repetition runs the policies in a fresh random order (the
-    # same on every rank), each run = W untimed warmup steps + K timed steps.
     import random
-    rng = random.Random(args.seed)
-    runs = {p: [] for p in pols}
-    order = []
-    for r in range(max(1, args.reps)):
-        perm = list(pols)
-        rng.shuffle(perm)
-        order += perm
-    for p in order:
-        runs[p].append(c.run_policy(p, args.steps, args.warmup))
 
     def q(xs, f):
         xs = sorted(xs)
@@ -154,55 +143,127 @@ def main():
         return {"median": round(q(xs, 0.5), 4), "iqr": round(q(xs, 0.75) - q(xs, 0.25), 4),
                 "min": round(min(xs), 4), "max": round(max(xs), 4)}
 
-    # headline run = the gpbs run with the median aggregate
-    gr = sorted(runs["gpbs"], key=lambda r: r["aggregate_all_gpus"])
-    g = gr[(len(gr) - 1) // 2]
+    def run_mix(mix, pols, reps):
+        """Calibrate solo rates, then every policy `reps` times in a fresh
+        random order per repetition (the same on every rank)."""
+        if "gpbs" not in pols:
+            pols = pols + ("gpbs",)
+        cfg = CorunConfig(steps=args.steps, warmup=args.warmup, target_ms=args.target_ms, policies=pols,
+                          table_mode=args.table, mix=mix, hw_counters=(counters == "hw"),
+                          protocol=args.protocol, step_ms=args.step_ms, gang_transport=args.gang_transport,
+                          gang_shm_base=f"{gang_base}-{mix}" if gang_base else "",
+                          gang_wait_driven=args.gang_wait_driven, fresh_engine=not args.keep_engines)
+        if args.rehearse:
+            cfg.coll_bytes = 4 << 20  # CPU gloo all-reduce stand-in
+        c = Corun(cfg, rank=rank, world=world, device=local, groups=groups, log=log, coll_on_cpu=args.rehearse)
+        c.calibrate()
+        rng = random.Random(args.seed)
+        runs = {p: [] for p in pols}
+        order = []
+        for _ in range(max(1, reps)):
+            perm = list(pols)
+            rng.shuffle(perm)
+            order += perm
+        for p in order:
+            runs[p].append(c.run_policy(p, args.steps, args.warmup))
+        solo = c.solo_report()
+        c.close()
+        del c
+        torch.cuda.empty_cache()
+        return runs, order, solo
+
+    def mix_summary(mix, runs, solo, reps):
+        gr = sorted(runs["gpbs"], key=lambda r: r["aggregate_all_gpus"])
+        g = gr[(len(gr) - 1) // 2]  # headline run = the gpbs run with the median aggregate
+        pol = {p: {"aggregate_all_gpus": summ(rs, "aggregate_all_gpus"),
+                   "mean_slowdown_pct": summ(rs, "mean_slowdown_pct"),
+                   "ms_per_step": round(q([r["ms_per_step"] for r in rs], 0.5), 3),
+                   "runs": [round(r["aggregate_all_gpus"], 4) for r in rs]} for p, rs in runs.items()}
+        for p, rs in runs.items():
+            eng = [r.get("engine") for r in rs if r.get("engine")]
+            if eng:
+                pol[p]["adapt_rearm"] = [e.get("adapt_rearm", 0) for e in eng]
+                pol[p]["relayout"] = [e.get("relayout", 0) for e in eng]
+            if "idle" in rs[0]["tenants"]:
+                pol[p]["idle_p50_ms"] = round(q([r["tenants"]["idle"]["p50_ms"] for r in rs], 0.5), 4)
+        out = {"value": round(q([r["aggregate_all_gpus"] for r in runs["gpbs"]], 0.5), 4),
+               "mean_slowdown_pct": round(q([r["mean_slowdown_pct"] for r in runs["gpbs"]], 0.5), 2),
+               "reps": max(1, reps), "policies": pol, "per_tenant": g["tenants"], "engine": g.get("engine", {}),
+               "ms_per_step": round(g["ms_per_step"], 3), "solo": solo}
+        if "static-se" in runs:
+            a, b = pol["gpbs"]["aggregate_all_gpus"], pol["static-se"]["aggregate_all_gpus"]
+            out["gpbs_vs_static_se"] = {"delta_median": round(a["median"] - b["median"], 4),
+                                        "iqr_gpbs": a["iqr"], "iqr_static_se": b["iqr"],
+                                        "beats_by_more_than_iqr": a["median"] - b["median"] > max(a["iqr"], b["iqr"])}
+        return out
+
+    results = {}
+    for mix in mixes:
+        default = {"4mix": "none,static,static-se,credit-fixed-ts,gpbs-ts,credit-fixed,gpbs-lat,gpbs",
+                   "gemm2": "none,static,static-se,credit-fixed,gpbs",
+                   "phase": "none,static-se,credit-fixed,gpbs",
+                   "8mix": "none,static-se,credit-fixed,gpbs"}[mix]
+        spec = args.policies if (args.policies and mix == mixes[0]) else default
+        pols = tuple(p for p in spec.split(",") if p)
+        reps = args.reps if mix == mixes[0] else args.reps_extra
+        runs, order, solo = run_mix(mix, pols, reps)
+        results[mix] = {"runs": runs, "order": order, "summary": mix_summary(mix, runs, solo, reps)}
+
+    head = mixes[0]
+    hs = results[head]["summary"]
     base = json.load(open(os.path.join(ROOT, "BASELINE.json")))
-    value = q([r["aggregate_all_gpus"] for r in runs["gpbs"]], 0.5)
+    names = {"4mix": "4-tenant mix (MFMA GEMM + HBM-stream + all-reduce + idle)",
+             "gemm2": "2 bf16 4096^2 GEMM tenants",
+             "phase": "phase-changing mix (GEMM + GEMM<->stream phase tenant + on/off stream + idle)",
+             "8mix": "8-tenant mix (3 GEMMs + 3 streams + all-reduce + idle)"}
     line = {
         "metric": base["metric"],
-        "value": round(value, 4),
+        "value": hs["value"],
         "unit": ("solo-equivalents (sum over GPUs and throughput tenants of co-run throughput / solo throughput, "
-                 "all tenants backlogged over common step windows)" if args.protocol == "steady" else
+                 "all tenants backlogged over common step windows; solo rates measured with the same protocol)"
+                 if args.protocol == "steady" else
                  "solo-equivalents (sum over GPUs and throughput tenants of solo_time/co-run_time per quota step)"),
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(g["ms_per_step"], 3),  # of the headline (median) gpbs run
+        "ms_per_step": hs["ms_per_step"],  # of the headline (median) gpbs run
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "bf16",
         "data": "synthetic (random-init bf16 tensors; 4096^3 GEMM, 1 GiB stream, 256 MiB reduce/all-reduce, "
-                "8192^2 GEMV)",
-        "config": {"model": ("4-tenant mix (MFMA GEMM + HBM-stream + all-reduce + idle)" if args.mix == "4mix"
-                             else "2 bf16 4096^2 GEMM tenants"),
-                   "global_batch": world * 4, "seq_len": 0, "parallelism": f"dp{world}" if world > 1 else "dp1",
-                   "tenants_per_gpu": 4 if args.mix == "4mix" else 2, "policy": "gpbs (counter-driven SE classes, PBS credit, hw counters)", "mix": args.mix},
-        "mean_slowdown_pct": round(q([r["mean_slowdown_pct"] for r in runs["gpbs"]], 0.5), 2),
+                "8192^2 GEMV; the N=1 'all-reduce' tenant is a local reduce-copy kernel, RCCL all-reduce at N>1)",
+        "config": {"model": names[head], "global_batch": world * 4, "seq_len": 0,
+                   "parallelism": f"dp{world}" if world > 1 else "dp1",
+                   "tenants_per_gpu": len(MIXES[head]["tenants"]),
+                   "policy": "gpbs (counter-driven SE budgets, PBS credit, hw counters)", "mix": head},
+        "mean_slowdown_pct": hs["mean_slowdown_pct"],
         "counters": counters,
         "protocol": {"kind": args.protocol, "step_ms": args.step_ms if args.protocol == "steady" else None,
                      "reps": max(1, args.reps), "order": "randomized per repetition", "seed": args.seed,
-                     "statistic": "median over reps (IQR = q75 - q25)"},
-        "per_tenant": g["tenants"],
-        "policies": {p: {"aggregate_all_gpus": summ(rs, "aggregate_all_gpus"),
-                         "mean_slowdown_pct": summ(rs, "mean_slowdown_pct"),
-                         "ms_per_step": round(q([r["ms_per_step"] for r in rs], 0.5), 3),
-                         "runs": [round(r["aggregate_all_gpus"], 4) for r in rs]} for p, rs in runs.items()},
-        "solo_unit_ms": {k: round(v, 4) for k, v in c.solo_unit_ms.items()},
-        "engine": g.get("engine", {}),
+                     "statistic": "median over reps (IQR = q75 - q25)", "solo": "steady (same protocol, alone)"},
+        "per_tenant": hs["per_tenant"],
+        "policies": hs["policies"],
+        "solo": hs["solo"],
+        "engine": hs["engine"],
     }
-    c.close()
+    if "gpbs_vs_static_se" in hs:
+        line["gpbs_vs_static_se"] = hs["gpbs_vs_static_se"]
+    line["mixes"] = {m: {k: v for k, v in results[m]["summary"].items() if k not in ("per_tenant", "engine")}
+                     for m in mixes[1:]}
+    for m in mixes[1:]:
+        line["mixes"][m]["per_tenant"] = {n: {k: v for k, v in t.items() if k != "step_norm_perf"}
+                                          for n, t in results[m]["summary"]["per_tenant"].items()}
     if rank == 0:
         print(json.dumps(line), flush=True)
         if args.out:
             with open(args.out, "w") as f:
-                json.dump({"line": line, "runs": runs, "order": order}, f, indent=1)
+                json.dump({"line": line, "results": {m: {"runs": r["runs"], "order": r["order"]}
+                                                     for m, r in results.items()}}, f, indent=1)
     if world > 1:
         import torch.distributed as dist
         dist.barrier(group=groups["ctrl"])
         dist.destroy_process_group()
-
 
 if __name__ == "__main__":
     main()

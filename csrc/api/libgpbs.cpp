@@ -127,6 +127,8 @@ void gpbs_boot_defaults(gpbs_boot_params_t* p) {
   p->class_split = 0;
   p->idle_skip = 0;  // reference semantics (Appendix A feeds every period)
   p->class_dwell = 2;
+  p->class_budget = 0;
+  p->present_us = 10000;
   AdaptParams a;
   std::memcpy(&p->adapt, &a, sizeof(a));
   AtcParams t;
@@ -428,7 +430,10 @@ int gpbs_tenant_info(gpbs_engine_t* e, int t, gpbs_tenant_info_t* o) {
     Slot& v = *E.slots[sid];
     o->sched_count += v.sched_count;
     o->run_ns += v.rs_time[RS_RUNNING] + (v.rs == RS_RUNNING ? n - v.rs_entry : 0);
+    o->online_slots += !(v.pause_flags & VPF_DOWN);
   }
+  o->budget_ctx = d->budget_ctx;
+  o->budget_shared = d->budget_shared;
   return GPBS_OK;
 }
 

@@ -731,6 +731,128 @@ void Engine::place_tenant_class(Tenant& t, Pool& pl, int layout) {
   emit(TRC_CLASS, 0, t.id, (uint32_t)c, (uint32_t)m.weight());
 }
 
+// ------------------------------------------- demand-driven SE budgets ----
+// class_budget (gpbs extension, SE-exclusive mode): instead of fixed class
+// halves whose per-tenant share is whatever slot count the tenant was created
+// with, every classified tenant that is PRESENT (a runnable slot now, or
+// within present_us) gets a set of shader engines of every XCD, sized from
+// the classes present -- the cpupool-resize analog of a credit scheduler's
+// work conservation, at the granularity the hardware can confine:
+//   * both classes present: compute owns contexts [0, class_split), memory
+//     the rest; one class alone spans every context;
+//   * a class region of r contexts with n <= r tenants is split into aligned
+//     blocks (r = 4: one tenant 4, two 2+2, three 2+1+1, four 1 each; r = 2:
+//     2, or 1+1) -- never a 3-SE set, which no class-half CU-masked stream
+//     covers;
+//   * n > r: every tenant of the region gets the whole region, staggered, and
+//     credit time-shares it with PBS quanta (the class region is one gang).
+// A tenant gets exactly one online slot per partition of its set; surplus
+// slots go offline (VPF_DOWN, the vcpu-set path), so its share follows the
+// layout instead of a creation-time slot count.  An absent tenant keeps its
+// slots (blocked); it re-enters the layout at the first class tick after it
+// has work again.  Reference analog: credit's idle-CPU stealing and tickling
+// make the pCPUs a blocked domain leaves available to the others at once
+// (X:xen/common/sched_credit.c:1559-1672); here that happens per class tick,
+// in space.
+void Engine::place_budget(Tenant& t, Pool& pl, uint32_t ctx_mask, int stagger) {
+  Mask m;
+  for (int p = pl.cpus.first(); p >= 0; p = pl.cpus.next(p + 1))
+    if ((ctx_mask >> (parts[p]->ctx & 31)) & 1) m.set(p);
+  std::vector<int> order;
+  for (int p = m.first(); p >= 0; p = m.next(p + 1)) order.push_back(p);
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+    return std::make_tuple(parts[a]->ctx, parts[a]->gpu, parts[a]->xcd) <
+           std::make_tuple(parts[b]->ctx, parts[b]->gpu, parts[b]->xcd);
+  });
+  const size_t online = std::min(order.size(), t.slots.size());
+  for (size_t k = 0; k < t.slots.size(); ++k) {
+    Slot& v = *slots[t.slots[k]];
+    if (k < online) {
+      if (v.pause_flags & VPF_DOWN) {
+        v.pause_flags &= ~VPF_DOWN;
+        v.home = order[(k + (size_t)stagger) % order.size()];
+        v.soft = m;
+        v.class_home = v.home;
+        if (!v.is_running) {
+          v.processor = v.home;  // an offline slot is on no runqueue: place it before it wakes
+          v.home = -1;
+        }
+        vcpu_wake(v);
+      } else {
+        place_class(v, m, order[(k + (size_t)stagger) % order.size()]);
+      }
+    } else if (!(v.pause_flags & VPF_DOWN)) {
+      v.pause_flags |= VPF_DOWN;
+      v.class_home = -1;
+      v.soft = Mask();
+      vcpu_sleep_nosync(v);
+    }
+  }
+  t.budget_ctx = ctx_mask;
+  emit(TRC_CLASS, 0, t.id, (uint32_t)t.cls, (uint32_t)m.weight());
+}
+
+void Engine::budget_layout(Pool& pl, int64_t n, bool force) {
+  const int64_t present_ns = (int64_t)std::max(0, boot.present_us) * 1000;
+  std::vector<std::pair<int, int>> sig;  // (id, class) of present tenants, id order
+  for (auto& tp : tenants) {
+    if (!tp || !tp->alive || !tp->priv || tp->pool != pl.id) continue;
+    Tenant& t = *tp;
+    bool busy = false;
+    for (int sid : t.slots) {
+      const Slot& v = *slots[sid];
+      if (!(v.pause_flags & VPF_BLOCKED) && v.pause_count == 0) busy = true;
+    }
+    if (busy && t.pause_count == 0) t.last_busy = n;
+    const bool present = t.cls >= 0 && n - t.last_busy <= present_ns;
+    if (present) sig.emplace_back(t.id, t.cls);
+    else t.budget_ctx = 0;
+  }
+  if (!force && sig == pl.budget_sig) return;
+  pl.budget_sig = sig;
+  perfc.incr(PC_relayout);
+  int nctx = 0;
+  for (int p = pl.cpus.first(); p >= 0; p = pl.cpus.next(p + 1)) nctx = std::max(nctx, parts[p]->ctx + 1);
+  if (nctx <= 0) return;
+  const int split = std::min(std::max(1, boot.class_split), nctx);
+  std::vector<int> cls_t[2];
+  for (auto& e : sig) cls_t[e.second & 1].push_back(e.first);
+  for (int c = 0; c < 2; ++c) {
+    if (cls_t[c].empty()) continue;
+    int lo = 0, hi = nctx;  // class region [lo, hi)
+    if (!cls_t[0].empty() && !cls_t[1].empty()) {
+      if (c == 0) hi = split;
+      else lo = split;
+    }
+    const int r = hi - lo, k = (int)cls_t[c].size();
+    if (k > r) {  // time-shared region: every tenant on all of it, staggered by whole contexts
+      uint32_t all = 0;
+      for (int x = lo; x < hi; ++x) all |= 1u << x;
+      int per = 0;
+      for (int p = pl.cpus.first(); p >= 0; p = pl.cpus.next(p + 1)) per += parts[p]->ctx == lo;
+      for (int i = 0; i < k; ++i) {
+        Tenant& t = *tenants[cls_t[c][i]];
+        t.budget_shared = true;
+        place_budget(t, pl, all, (i % r) * per);
+      }
+      continue;
+    }
+    // aligned blocks: sizes r/k, the first r%k tenants one more; with r = 4
+    // and k = 3 that is 2+1+1 (a 2-block always starts on an even context)
+    int at = lo;
+    for (int i = 0; i < k; ++i) {
+      const int sz = r / k + (i < r % k ? 1 : 0);
+      uint32_t msk = 0;
+      for (int x = at; x < at + sz; ++x) msk |= 1u << x;
+      at += sz;
+      Tenant& t = *tenants[cls_t[c][i]];
+      t.budget_shared = false;
+      place_budget(t, pl, msk, 0);
+    }
+  }
+  process_softirqs();
+}
+
 void Engine::classify_tick(int64_t n) {
   std::vector<int> changed;
   for (auto& tp : tenants) {
@@ -820,6 +942,7 @@ void Engine::classify_tick(int64_t n) {
       continue;
     }
     t.cls = c;
+    perfc.incr(PC_class_change);
     changed.push_back(t.id);
   }
   // Class layout per pool: the classes present among its classified
@@ -831,6 +954,15 @@ void Engine::classify_tick(int64_t n) {
   for (auto& pp : pools) {
     if (!pp) continue;
     Pool& pl = *pp;
+    if (boot.class_split > 1 && boot.class_budget) {
+      bool any_changed = false;
+      for (auto& tp : tenants)
+        if (tp && tp->alive && tp->pool == pl.id &&
+            std::find(changed.begin(), changed.end(), tp->id) != changed.end())
+          any_changed = true;
+      budget_layout(pl, n, any_changed);
+      continue;
+    }
     int layout = 0;
     for (auto& tp : tenants)
       if (tp && tp->alive && tp->priv && tp->pool == pl.id && tp->cls >= 0) layout |= 1 << tp->cls;

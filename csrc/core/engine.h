@@ -87,6 +87,12 @@ struct Tenant {  // struct domain
   // its control page (Perfctr-xen's per-vCPU state page, S1/S2).
   uint64_t vpmu_total[4] = {0, 0, 0, 0};
   int cls = -1;          // contention class: 0 compute-bound (MFMA ctx), 1 memory-bound (memory ctx)
+  // class_budget layout: last time any slot was runnable, and the contexts
+  // (shader engines) of every XCD the layout gave the tenant (bit c = ctx c;
+  // 0 = not placed / absent); budget_shared: its class region is time-shared
+  int64_t last_busy = INT64_MIN / 2;
+  uint32_t budget_ctx = 0;
+  bool budget_shared = false;
   int cls_pending = -1;  // hysteresis: a new class must be seen on consecutive ticks
   int cls_count = 0;
   // Cross-GPU gang window (parallel/gang.py): 1 favoured (run on every
@@ -197,6 +203,9 @@ struct Pool {
   // contention classes present among the pool's classified tenants (bit c =
   // class c): the class layout the slots were last placed for (-1: none yet)
   int class_layout = -1;
+  // class_budget: (tenant id, class) of the present tenants the budgets were
+  // last computed for
+  std::vector<std::pair<int, int>> budget_sig;
 };
 
 std::unique_ptr<Scheduler> make_scheduler(const std::string& name, Engine& e, int pool);
@@ -367,6 +376,8 @@ class Engine {
   void watchdog_kill(Tenant& t);
   void classify_tick(int64_t now);
   void place_tenant_class(Tenant& t, Pool& pl, int layout);
+  void budget_layout(Pool& pl, int64_t now, bool force);
+  void place_budget(Tenant& t, Pool& pl, uint32_t ctx_mask, int stagger);
   void set_affinity(Slot& v, const Mask& m, int home = -1);
   void place_class(Slot& v, const Mask& m, int home);
   void send_home(Slot& v);

@@ -808,6 +808,16 @@ typedef struct gpbs_runner_cfg {
   int reserved;
   unsigned long long bytes;  // stream / reduce bytes
   void *a, *b, *c;           // device buffers (caller-owned)
+  // Alternate workload (phase-changing tenant): a second kind with its own
+  // shape and buffers; gpbs_runner_set_phase(r, 1) makes every FRESH unit use
+  // it (a revoked unit resumes with the kind it started with).  alt_kind 0:
+  // none.
+  int alt_kind;
+  int alt_M, alt_N, alt_K;
+  int alt_chunk_bytes;
+  int alt_reserved;
+  unsigned long long alt_bytes;
+  void *alt_a, *alt_b, *alt_c;
 } gpbs_runner_cfg_t;
 
 typedef struct gpbs_runner_stats {
@@ -815,6 +825,7 @@ typedef struct gpbs_runner_stats {
   int64_t busy_ns, wait_owner_ns, first_start_ns, last_done_ns;
   int64_t lat_sum_ns, lat_max_ns;
   uint64_t lat_count;
+  uint64_t units_alt;  // of units_done: units of the alternate workload
 } gpbs_runner_stats_t;
 
 }
@@ -879,12 +890,30 @@ struct Runner {
     }
   }
 
-  u32 unit_total() const {
-    switch (cfg.kind) {
-      case K_GEMM: return (u32)gpbs_hip_gemm_units(cfg.M, cfg.N);
+  // phase-changing tenant: fresh units use the alternate workload while
+  // `phase` is 1; q_alt[qi] = workload of the unit in queue slot qi
+  std::atomic<int> phase{0};
+  uint8_t q_alt[16] = {};
+  int cur_alt = 0;  // workload of the unit being launched
+
+  struct Work {
+    int kind, M, N, K, chunk;
+    unsigned long long bytes;
+    void *a, *b, *c;
+  };
+  Work work(int alt) const {
+    if (alt && cfg.alt_kind)
+      return Work{cfg.alt_kind, cfg.alt_M, cfg.alt_N, cfg.alt_K, cfg.alt_chunk_bytes, cfg.alt_bytes,
+                  cfg.alt_a, cfg.alt_b, cfg.alt_c};
+    return Work{cfg.kind, cfg.M, cfg.N, cfg.K, cfg.chunk_bytes, cfg.bytes, cfg.a, cfg.b, cfg.c};
+  }
+
+  static u32 unit_total(const Work& w) {
+    switch (w.kind) {
+      case K_GEMM: return (u32)gpbs_hip_gemm_units(w.M, w.N);
       case K_STREAM:
-      case K_REDUCE: return (u32)((cfg.bytes + cfg.chunk_bytes - 1) / cfg.chunk_bytes);
-      case K_GEMV: return (u32)((cfg.M + 15) / 16);
+      case K_REDUCE: return (u32)((w.bytes + w.chunk - 1) / w.chunk);
+      case K_GEMV: return (u32)((w.M + 15) / 16);
     }
     return 0;
   }
@@ -919,7 +948,7 @@ struct Runner {
         return stream;
       }
     }
-    cur_grid = (cfg.kind == K_GEMV) ? 0 : 128;  // one persistent workgroup per CU of the half
+    cur_grid = (work(cur_alt).kind == K_GEMV) ? 0 : 128;  // one persistent workgroup per CU of the half
     return se_stream[half];
   }
 
@@ -952,13 +981,14 @@ struct Runner {
 
   int launch(int qi, hipStream_t stream) {
     WorkQueue* q = d_q + qi;
+    const Work w = work(q_alt[qi]);
     const int tm = __atomic_load_n(&ctx->table_mode, __ATOMIC_ACQUIRE);
     const bool dev = tm != 0;
     const void* tab = tm == 1 ? (const void*)ctx->d_table : tm == 2 ? (const void*)ctx->b_table : (const void*)ctx->h_table;
     const bool gate = cfg.gate && !ctx->share.load(std::memory_order_acquire);
     // memory-class tenants pause at unit boundaries while a latency request
     // is in flight (only where the host can write the hold word: host / BAR table)
-    const bool hold = gate && ctx->hold_enable && tm != 1 && cfg.kind != K_GEMV && ctx->engine &&
+    const bool hold = gate && ctx->hold_enable && tm != 1 && w.kind != K_GEMV && ctx->engine &&
                       (ctx->hold_all || ctx->cls_cache[cfg.tenant].load(std::memory_order_relaxed) == 1);
     const unsigned mode = (gate ? (cfg.gate == 2 ? GATE_PARK : GATE_TABLE) : GATE_NONE) | (dev ? GATE_DEVTABLE : 0) |
                           (gate && ctx->spatial ? GATE_SPATIAL : 0) |
@@ -967,19 +997,20 @@ struct Runner {
     const unsigned me = (unsigned)cfg.tenant;
     __atomic_store_n(&h_status[qi], 0u, __ATOMIC_RELEASE);
     st.launches++;
-    switch (cfg.kind) {
+    const int grid = cfg.grid ? cfg.grid : cur_grid;
+    switch (w.kind) {
       case K_GEMM:
-        return gpbs_hip_gemm_bf16(cfg.a, cfg.b, cfg.c, cfg.M, cfg.N, cfg.K, q, tab, mode, me, ctx->d_cnt,
-                                  &h_status[qi], cfg.grid ? cfg.grid : cur_grid, stream);
+        return gpbs_hip_gemm_bf16(w.a, w.b, w.c, w.M, w.N, w.K, q, tab, mode, me, ctx->d_cnt, &h_status[qi], grid,
+                                  stream);
       case K_STREAM:
-        return gpbs_hip_stream_copy(cfg.a, cfg.c, cfg.bytes, (unsigned)cfg.chunk_bytes, q, tab, mode, me, ctx->d_cnt,
-                                    &h_status[qi], cfg.grid ? cfg.grid : cur_grid, stream);
+        return gpbs_hip_stream_copy(w.a, w.c, w.bytes, (unsigned)w.chunk, q, tab, mode, me, ctx->d_cnt,
+                                    &h_status[qi], grid, stream);
       case K_REDUCE:
-        return gpbs_hip_reduce_bf16(cfg.a, cfg.b, cfg.c, cfg.bytes, (unsigned)cfg.chunk_bytes, q, tab, mode, me,
-                                    ctx->d_cnt, &h_status[qi], cfg.grid ? cfg.grid : cur_grid, stream);
+        return gpbs_hip_reduce_bf16(w.a, w.b, w.c, w.bytes, (unsigned)w.chunk, q, tab, mode, me, ctx->d_cnt,
+                                    &h_status[qi], grid, stream);
       case K_GEMV:
-        return gpbs_hip_gemv_bf16(cfg.a, cfg.b, cfg.c, cfg.M, cfg.K, q, tab, mode, me, ctx->d_cnt, &h_status[qi],
-                                  cfg.grid ? cfg.grid : cur_grid, stream);
+        return gpbs_hip_gemv_bf16(w.a, w.b, w.c, w.M, w.K, q, tab, mode, me, ctx->d_cnt, &h_status[qi], grid,
+                                  stream);
     }
     return -22;
   }
@@ -1050,6 +1081,8 @@ struct Runner {
           }
           wait_owner();
           if (stop) break;
+          if (fresh) q_alt[qi] = (uint8_t)(cfg.alt_kind && phase.load(std::memory_order_acquire));
+          cur_alt = q_alt[qi];
           hipStream_t stream = pick_stream();
           if (fresh) {
             std::lock_guard<std::mutex> g(mu);
@@ -1082,13 +1115,14 @@ struct Runner {
         }
         const u32 s = __atomic_load_n(&h_status[f.qi], __ATOMIC_ACQUIRE);
         const u32 done = s & 0x7fffffffu;
-        if ((s & 0x80000000u) && done >= unit_total()) {
+        if ((s & 0x80000000u) && done >= unit_total(work(q_alt[f.qi]))) {
           hold_drop(f.qi);
           const int64_t t = mono_ns();
           std::lock_guard<std::mutex> g(mu);
           q_busy[f.qi] = 0;
           inflight--;
           st.units_done++;
+          st.units_alt += q_alt[f.qi];
           st.last_done_ns = t;
           if (!submit_times.empty()) {
             const int64_t lat = t - submit_times.front();
@@ -1692,6 +1726,12 @@ void* gpbs_runner_create(void* ctx, const gpbs_runner_cfg_t* cfg) {
   if ((cfg->kind == K_STREAM || cfg->kind == K_REDUCE) && (cfg->bytes % 16 || cfg->chunk_bytes <= 0 || cfg->chunk_bytes % 16))
     return nullptr;
   if (cfg->kind == K_GEMV && cfg->K % 512) return nullptr;
+  if (cfg->alt_kind == K_GEMM && (cfg->alt_M % 128 || cfg->alt_N % 128 || cfg->alt_K % 64)) return nullptr;
+  if ((cfg->alt_kind == K_STREAM || cfg->alt_kind == K_REDUCE) &&
+      (cfg->alt_bytes % 16 || cfg->alt_chunk_bytes <= 0 || cfg->alt_chunk_bytes % 16))
+    return nullptr;
+  if (cfg->alt_kind == K_GEMV && cfg->alt_K % 512) return nullptr;
+  if (cfg->alt_kind < 0 || cfg->alt_kind > K_GEMV) return nullptr;
   hipSetDevice(c->device);
   auto* r = new Runner;
   r->ctx = c;
@@ -1803,6 +1843,14 @@ int gpbs_runner_set_engine_wake(void* p, int on) {
 }
 
 void* gpbs_runner_stream(void* p) { return ((Runner*)p)->stream; }
+
+// Phase-changing tenant: fresh units use the alternate workload (1) or the
+// primary one (0).  Returns the previous phase, -22 without an alternate.
+int gpbs_runner_set_phase(void* p, int alt) {
+  Runner* r = (Runner*)p;
+  if (!r->cfg.alt_kind) return -22;
+  return r->phase.exchange(alt ? 1 : 0, std::memory_order_acq_rel);
+}
 
 void gpbs_runner_destroy(void* p) {
   Runner* r = (Runner*)p;

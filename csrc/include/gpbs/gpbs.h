@@ -16,7 +16,7 @@
 extern "C" {
 #endif
 
-#define GPBS_ABI_VERSION 2
+#define GPBS_ABI_VERSION 3
 
 /* Validation ranges (sysctl.h:568-579, libxl.c:4026-4101). Q1: the new API
  * also accepts the reference's boot default of 100us (see docs). */
@@ -77,6 +77,12 @@ typedef struct gpbs_boot_params {
                                   period is not fed to the phase detector (curr = 0 would shrink its quantum) */
   int32_t class_dwell;         /* class re-evaluations a new contention class must persist before a tenant is
                                   re-homed (default 2); the classifier also has a +-25 % band around the threshold */
+  int32_t class_budget;        /* 1 = demand-driven SE budgets (class_split > 1): each PRESENT classified tenant gets a
+                                  set of shader engines sized by the classes present (aligned halves, singles, or the
+                                  class region time-shared when it has more tenants than SEs); surplus slots go offline
+                                  (vcpu-set) -- no bench-side slot counts decide the layout */
+  int32_t present_us;          /* class_budget: a tenant with no runnable slot for this long leaves the layout
+                                  (default 10000) */
   gpbs_adapt_params_t adapt;
   gpbs_atc_params_t atc;
 } gpbs_boot_params_t;
@@ -152,6 +158,10 @@ typedef struct gpbs_tenant_info {
   uint64_t spin_latency, report_count, pending_requests, sched_count;
   int64_t run_ns;           /* total running time across slots */
   char name[64];
+  int32_t online_slots;     /* slots not offline (vcpu-set / class_budget) */
+  uint32_t budget_ctx;      /* class_budget: contexts (shader engines) of every XCD the layout gave it (bit c) */
+  int32_t budget_shared;    /* class_budget: its class region is time-shared */
+  int32_t reserved0;
 } gpbs_tenant_info_t;
 
 typedef struct gpbs_slot_info {

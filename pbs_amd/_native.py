@@ -27,7 +27,7 @@ class AtcParams(C.Structure):
                                    "wait_unit_ns")]
 
 
-ABI_VERSION = 2  # GPBS_ABI_VERSION in csrc/include/gpbs/gpbs.h
+ABI_VERSION = 3  # GPBS_ABI_VERSION in csrc/include/gpbs/gpbs.h
 
 
 class BootParams(C.Structure):
@@ -35,7 +35,8 @@ class BootParams(C.Structure):
         "tslice_us", "ratelimit_us", "smt_power_savings", "tickle_one_idle", "default_yield", "migration_delay_us",
         "metric_period_us", "slice_apply_us", "sim_clock", "pmu_refresh_us", "dom0_quirk", "heartbeat_timeout_us",
         "trace_capacity", "quantum_align_us", "coschedule", "class_period_us", "boost_exclusive",
-        "class_split", "idle_skip", "class_dwell")] + [("adapt", AdaptParams), ("atc", AtcParams)]
+        "class_split", "idle_skip", "class_dwell", "class_budget", "present_us")] + [("adapt", AdaptParams),
+                                                                                    ("atc", AtcParams)]
 
 
 class SchedExt(C.Structure):
@@ -91,7 +92,8 @@ class TenantInfo(C.Structure):
                [(n, u32) for n in ("tslice_us", "tick_period_us", "phase", "window_left")] + \
                [("last_err", i32), ("shutdown", i32), ("last_curr", i64), ("last_win", i64), ("pmc", u64 * 4),
                 ("cache_miss_rate", u64), ("cpi", u64), ("spin_latency", u64), ("report_count", u64),
-                ("pending_requests", u64), ("sched_count", u64), ("run_ns", i64), ("name", C.c_char * 64)]
+                ("pending_requests", u64), ("sched_count", u64), ("run_ns", i64), ("name", C.c_char * 64),
+                ("online_slots", i32), ("budget_ctx", u32), ("budget_shared", i32), ("reserved0", i32)]
 
 
 class SlotInfo(C.Structure):

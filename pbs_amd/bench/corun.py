@@ -70,16 +70,54 @@ import torch
 
 from ..core.config import MI355X_PROFILE
 from ..core.engine import Engine
-from ..runtime.gpu import GpuContext, Runner
+from ..runtime.gpu import XCDS, GpuContext, Runner
 
 THROUGHPUT = ("gemm", "hbm", "coll")
 TENANTS = (("gemm", 8), ("hbm", 8), ("coll", 8), ("idle", 8))  # one slot per XCD
-# Tenant mixes (BASELINE.json configs): "4mix" = config #3/#4 (MFMA GEMM +
-# HBM stream + all-reduce + latency-critical idle), "gemm2" = config #2 (two
-# bf16 4096^2 GEMM tenants split by the counter-driven partitions).
+# Tenant workloads (native runners; "coll" is the RCCL all-reduce tenant when
+# N > 1).  "phase" alternates between a 4096^3 GEMM (compute-bound) and a
+# 1 GiB stream copy (memory-bound) every phase_ms.
+SPECS = {
+    "gemm": dict(kind="gemm", M=4096, N=4096, K=4096),
+    "gemm_b": dict(kind="gemm", M=4096, N=4096, K=4096),
+    "gemm_s": dict(kind="gemm", M=2048, N=2048, K=2048),
+    "hbm": dict(kind="stream", bytes=1 << 30),
+    "hbm_b": dict(kind="stream", bytes=1 << 30),
+    "hbm_s": dict(kind="stream", bytes=256 << 20),
+    "coll": dict(kind="reduce"),  # bytes = cfg.coll_bytes
+    "phase": dict(kind="gemm", M=4096, N=4096, K=4096, alt=dict(kind="stream", bytes=1 << 30)),
+    "idle": dict(kind="gemv"),
+}
+# Tenant mixes (BASELINE.json configs): "4mix" = config #3 (MFMA GEMM + HBM
+# stream + all-reduce + latency-critical idle; the headline); "gemm2" =
+# config #2; "phase" = a phase-changing mix (the "phase" tenant alternates
+# compute <-> memory every phase_ms, the "hbm" tenant stops and starts every
+# onoff_ms) -- what a counter-driven scheduler must follow and a hand-picked
+# static layout cannot; "8mix" = config #4's 8-tenant mix on one GPU (3 GEMMs,
+# 3 streams + the reduce/all-reduce, latency GEMV): more tenants per class
+# than shader engines, so classes must time-share their SEs.
 MIXES = {
     "4mix": {"tenants": TENANTS, "throughput": THROUGHPUT},
     "gemm2": {"tenants": (("gemm", 8), ("gemm_b", 8)), "throughput": ("gemm", "gemm_b")},
+    "phase": {"tenants": (("gemm", 8), ("phase", 8), ("hbm", 8), ("idle", 8)),
+              "throughput": ("gemm", "phase", "hbm"), "dynamic": True},
+    "8mix": {"tenants": (("gemm", 8), ("gemm_b", 8), ("gemm_s", 8), ("hbm", 8), ("hbm_b", 8), ("hbm_s", 8),
+                         ("coll", 8), ("idle", 8)),
+             "throughput": ("gemm", "gemm_b", "gemm_s", "hbm", "hbm_b", "hbm_s", "coll")},
+}
+# Hand-picked static shader-engine layouts (policy "static-se": no engine, no
+# counters): tenant -> (XCDs, SEs) it owns.  The informed static alternative
+# to the counter-driven layout: for the 4mix the compute tenant on SEs {0,1}
+# and one memory SE per memory tenant (profiles/se_interfere_1gpu.jsonl
+# g2|s1|r1, the best split measured).
+_ALLX = tuple(range(8))
+STATIC_SE = {
+    "4mix": {"gemm": (_ALLX, (0, 1)), "hbm": (_ALLX, (2,)), "coll": (_ALLX, (3,))},
+    "gemm2": {"gemm": (_ALLX, (0, 1)), "gemm_b": (_ALLX, (2, 3))},
+    "phase": {"gemm": (_ALLX, (0, 1)), "phase": (_ALLX, (2,)), "hbm": (_ALLX, (3,))},
+    "8mix": {"gemm": (_ALLX, (0,)), "gemm_b": (tuple(range(6)), (1,)), "gemm_s": ((6, 7), (1,)),
+             "hbm": ((0, 1, 2, 3), (2,)), "hbm_b": ((4, 5, 6, 7), (2,)), "coll": ((0, 1, 2, 3), (3,)),
+             "hbm_s": ((4, 5, 6, 7), (3,))},
 }
 
 
@@ -113,6 +151,9 @@ class CorunConfig:
     protocol: str = "steady"
     step_ms: float = 80.0
     fresh_engine: bool = True    # every run of a scheduler policy starts from a new engine
+    phase_ms: float = 300.0      # mix "phase": the phase tenant alternates gemm <-> stream this often
+    onoff_ms: float = 500.0      # mix "phase": the hbm tenant runs / stops for this long, alternately
+    solo_steps: int = 0          # solo calibration windows (0: the co-run's K); warmup = the co-run's W
 
 
 # SE-exclusive flagship (the four partitions of an XCD are its shader engines,
@@ -122,6 +163,10 @@ class CorunConfig:
 # counters attributed exactly by SE ownership
 # (profiles/se_interfere_1gpu.jsonl, profiles/hwc/se_separation_probe.txt).
 SE_OVERRIDES = {"class_split": 2, "idle_skip": 1}
+# demand-driven SE budgets (csrc/core/engine.cpp budget_layout): the layout,
+# not a slot count, sizes each tenant's share -- every tenant is created with
+# one slot per partition and surplus slots go offline
+BUDGET_OVERRIDES = {"class_split": 2, "idle_skip": 1, "class_budget": 1, "present_us": 10000}
 SE_SLOTS = {"gemm": 16, "gemm_b": 16, "hbm": 16, "coll": 16, "idle": 8}
 # "se8": memory tenants get 8 slots each -- one SE per XCD, so the credit
 # scheduler places them on disjoint memory SEs instead of time-sharing both.
@@ -135,8 +180,11 @@ POLICY_ENGINES = {
     # every XCD ("se8": 8 slots, so credit places the memory tenants on
     # disjoint SEs); the latency tenant runs outside the partitions,
     # co-resident at raised wave priority (no BOOST revocations)
-    "gpbs": (4, dict(SE_OVERRIDES), True, "device,se,waveprio,latco,se8"),
-    "credit-fixed": (4, dict(SE_OVERRIDES, sched="credit-fixed"), True, "device,se,waveprio,latco,se8"),
+    "gpbs": (4, dict(BUDGET_OVERRIDES), True, "device,se,waveprio,latco,budget"),
+    "credit-fixed": (4, dict(BUDGET_OVERRIDES, sched="credit-fixed"), True, "device,se,waveprio,latco,budget"),
+    # round-2 flagship: fixed class halves, memory tenants one SE each by
+    # their bench-side slot count (se8)
+    "gpbs-se8": (4, dict(SE_OVERRIDES), True, "device,se,waveprio,latco,se8"),
     # time-shared variant: the memory tenants hold slots on all memory SEs
     # {2,3} and alternate on them as one gang under credit with PBS's
     # adaptive quanta (credit-fixed-ts: fixed quantum)
@@ -149,7 +197,7 @@ POLICY_ENGINES = {
     # flagship + latency hold: the table in host-written VRAM (BAR), and the
     # memory-class tenants pause at their next unit boundary while a latency
     # request is in flight (the wake-BOOST analog for the GEMV tenant)
-    "gpbs-lat": (4, dict(SE_OVERRIDES), True, "bar,se,waveprio,latco,se8,hold"),
+    "gpbs-lat": (4, dict(BUDGET_OVERRIDES), True, "bar,se,waveprio,latco,budget,hold"),
     "gpbs-ts": (4, dict(SE_OVERRIDES), True, "device,se,waveprio,latco"),
     "credit-fixed-ts": (4, dict(SE_OVERRIDES, sched="credit-fixed"), True, "device,se,waveprio,latco"),
     "credit2": (4, dict(SE_OVERRIDES, sched="credit2"), True, "device,se,waveprio,latco"),
@@ -308,26 +356,34 @@ class Corun:
             self.runners[name] = self._make_runner(name)
         self.quota: Dict[str, int] = {}
         self.solo_unit_ms: Dict[str, float] = {}
+        self.solo_est_ms: Dict[str, float] = {}
+        self._off: set = set()           # dynamic mix: tenants currently stopped
+        self._dyn_t0 = 0
+        self._dyn_state: Dict[str, int] = {}
         self.solo_lat_ms = 0.0
         self.active_engine: Optional[Engine] = None
 
     def _make_runner(self, name: str):
         cfg, t = self.cfg, self.tid[name]
-        if name.startswith("gemm"):
-            return Runner(self.ctx, "gemm", t, depth=cfg.depth, M=cfg.gemm_n, N=cfg.gemm_n, K=cfg.gemm_n)
+        spec = dict(SPECS[name])
+        kind = spec.pop("kind")
         # GPBS_MEM_CHUNK: unit-boundary granularity of the memory tenants (bytes
         # per work-queue chunk, default 512 KiB) -- how soon a hold or a
         # revocation takes effect
         mem_chunk = {"chunk_bytes": int(os.environ["GPBS_MEM_CHUNK"])} if os.environ.get("GPBS_MEM_CHUNK") else {}
-        if name == "hbm":
-            return Runner(self.ctx, "stream", t, depth=cfg.depth, bytes=cfg.hbm_bytes, **mem_chunk)
-        if name == "coll":
+        if "alt" in spec and spec["alt"]["kind"] in ("stream", "reduce"):
+            spec["alt"] = dict(spec["alt"], **mem_chunk)
+        if kind == "gemm":
+            return Runner(self.ctx, "gemm", t, depth=cfg.depth, **spec)
+        if kind == "stream":
+            return Runner(self.ctx, "stream", t, depth=cfg.depth, **spec, **mem_chunk)
+        if kind == "reduce":
             if self.world > 1:
                 return CollTenant(self.ctx, t, cfg.coll_bytes, self.groups.get("coll"), on_cpu=self.coll_on_cpu,
                                   board_name=f"{cfg.gang_shm_base}-arr" if cfg.gang_shm_base else "",
                                   rank=self.rank, world=self.world)
             return Runner(self.ctx, "reduce", t, depth=cfg.depth, bytes=cfg.coll_bytes, **mem_chunk)
-        if name == "idle":
+        if kind == "gemv":
             return Runner(self.ctx, "gemv", t, depth=1, priority=1, M=cfg.idle_rows, K=cfg.idle_rows)
         raise ValueError(name)
 
@@ -341,10 +397,15 @@ class Corun:
                 e.pool_assign(0, e.partition_add(self.rank, x, c))
         e.tenant_create("Domain-0", nslots=1)
         opts = table.split(",")
-        slots = SE8_SLOTS if "se8" in opts else SE_SLOTS if "se" in opts else {}
         ids = {}
         for name, ns in self.tenants:
-            ids[name] = e.tenant_create(name, nslots=slots.get(name, ns))
+            if "budget" in opts:  # one slot per partition; the layout sizes the share
+                n = ns if SPECS[name]["kind"] == "gemv" else XCDS * nctx
+            elif "se" in opts:
+                n = (SE8_SLOTS if "se8" in opts else SE_SLOTS).get(name, ns if SPECS[name]["kind"] == "gemv" else 16)
+            else:
+                n = ns
+            ids[name] = e.tenant_create(name, nslots=n)
         if self.tid and ids != self.tid:
             raise RuntimeError("tenant ids differ across engines")
         self.tid = ids
@@ -454,10 +515,28 @@ class Corun:
                 coll.gate = False
         elif policy == "static":  # equal XCD split (ARINC-653-like), tenants in mix order
             order = [n for n, _ in self.tenants]
-            per = 8 // len(order)
+            per = max(1, 8 // len(order))
             self.ctx.set_owners([self.tid[order[min(x // per, len(order) - 1)]] for x in range(8)])
             for r in self._natives():
                 r.set_gate(True)
+            if isinstance(coll, CollTenant):
+                coll.gate = True
+        elif policy == "static-se":
+            # hand-picked shader-engine layout (STATIC_SE), no engine, no
+            # counters: the same SE gating, CU-masked class-half streams and
+            # latency tenant (co-resident, raised wave priority) as gpbs
+            owners = [-1] * (XCDS * 4)
+            for name, (xs, ses) in STATIC_SE[self.cfg.mix].items():
+                for x in xs:
+                    for se in ses:
+                        owners[x * 4 + se] = self.tid[name]
+            self.ctx.set_table_mode("device")
+            self.ctx.set_se_mode(True)
+            self.ctx.set_waveprio(True)
+            self.ctx.set_owners(owners)
+            for name, r in self.runners.items():
+                if isinstance(r, Runner):
+                    r.set_gate(SPECS[name]["kind"] != "gemv")
             if isinstance(coll, CollTenant):
                 coll.gate = True
         else:
@@ -486,20 +565,83 @@ class Corun:
         else:
             r.run_units(n)
 
+    def _estimate_unit_ms(self, name: str) -> float:
+        """Rough solo ms per unit (sizes the backlog; not a measurement)."""
+        r = self.runners[name]
+        self._barrier()
+        t0 = time.perf_counter()
+        self._run_units(name, 4)
+        self._barrier()
+        return self._allreduce((time.perf_counter() - t0) * 1e3 / 4, "max")
+
+    def _solo_rate(self, name: str, alt: int, warmup: int, steps: int) -> float:
+        """Steady solo rate (units/ms) of one tenant workload: alone on the
+        GPU, ungated, backlogged over `warmup` + `steps` windows of step_ms
+        -- the same protocol as the co-run, so norm_perf compares like with
+        like (slowdown = solo / co-run throughput)."""
+        r = self.runners[name]
+        step_ns = int(self.cfg.step_ms * 1e6)
+        if alt:
+            r.set_phase(1)
+        if isinstance(r, Runner):
+            q = max(1, self.quota.get(name, 16))
+
+            def topup():
+                st = r.stats()
+                if st.submitted - st.units_done < 2 * q:
+                    r.submit(2 * q)
+            def done():
+                return r.stats().units_done
+        else:
+            r.start_loop()
+
+            def topup():
+                pass
+            def done():
+                return r.units_done
+        self._barrier()
+        t0 = d0 = None
+        for w in range(warmup + steps):
+            if w == warmup:
+                t0, d0 = time.perf_counter(), done()
+            end = time.monotonic_ns() + step_ns
+            while time.monotonic_ns() < end:
+                topup()
+                time.sleep(5e-4)
+        dt_ms = (time.perf_counter() - t0) * 1e3
+        rate = (done() - d0) / dt_ms
+        if isinstance(r, Runner):
+            r.cancel()
+            r.wait(120.0)
+        else:
+            r.stop_loop(agree=lambda n: int(self._allreduce(float(n), "max")))
+        if alt:
+            r.set_phase(0)
+        self._barrier()
+        return -self._allreduce(-rate, "max")  # min over ranks
+
     def calibrate(self):
-        """Solo time per unit for each throughput tenant (whole GPU, ungated)."""
+        """Solo rate of every throughput tenant -- and of each workload of a
+        phase-changing tenant -- under the steady protocol (W warmup + K timed
+        windows, backlogged, alone, ungated), and the latency tenant's solo p50."""
         self.set_policy("solo")
         cfg = self.cfg
+        steps = cfg.solo_steps or cfg.steps
         for name in self.throughput:
-            self._barrier()
-            self._run_units(name, 2)
-            self._barrier()
-            t0 = time.perf_counter()
-            self._run_units(name, cfg.calib_units)
-            self._barrier()
-            dt = (time.perf_counter() - t0) * 1e3 / cfg.calib_units
-            self.solo_unit_ms[name] = self._allreduce(dt, "max")
-            self.quota[name] = max(1, int(round(cfg.target_ms / self.solo_unit_ms[name])))
+            r = self.runners[name]
+            kinds = (0, 1) if getattr(r, "alt_kind", None) else (0,)
+            for alt in kinds:
+                key = f"{name}:alt" if alt else name
+                if alt:
+                    r.set_phase(1)
+                est = self._estimate_unit_ms(name)
+                if alt:
+                    r.set_phase(0)
+                self.quota[key] = max(1, int(round(cfg.target_ms / est)))
+                self.quota[name] = max(self.quota.get(name, 1), self.quota[key])
+                rate = self._solo_rate(name, alt, cfg.warmup, steps)
+                self.solo_unit_ms[key] = 1.0 / rate if rate > 0 else est
+                self.solo_est_ms[key] = est
         r = self.runners.get("idle")
         if r is not None:
             r.latencies(clear=True)
@@ -508,8 +650,27 @@ class Corun:
                 r.wait(10.0)
                 time.sleep(cfg.idle_period_ms / 1e3)
             self.solo_lat_ms = _pct(r.latencies(clear=True), 0.5) / 1e6
-        self.log(f"[corun] solo unit ms: {self.solo_unit_ms}  quota/step: {self.quota}  "
-                 f"idle p50 {self.solo_lat_ms:.3f} ms")
+        self.log(f"[corun] solo unit ms (steady): {self.solo_unit_ms}  (round-trip estimate {self.solo_est_ms})  "
+                 f"quota/step: {self.quota}  idle p50 {self.solo_lat_ms:.3f} ms")
+
+    def solo_report(self) -> Dict[str, Dict]:
+        """Solo rates with the workload's physical rate (TF/s, TB/s) for a
+        check against scripts/kbench.py."""
+        out = {}
+        for key, ms in self.solo_unit_ms.items():
+            name, alt = key.split(":")[0], key.endswith(":alt")
+            r = self.runners[name]
+            d = {"solo_units_per_ms": round(1.0 / ms, 4), "solo_unit_ms": round(ms, 5),
+                 "roundtrip_estimate_unit_ms": round(self.solo_est_ms.get(key, 0.0), 5)}
+            if isinstance(r, Runner):
+                work = r.alt_work_per_unit if alt else r.work_per_unit
+                kind = r.alt_kind if alt else r.kind
+                if kind == "gemm":
+                    d["solo_tflops"] = round(work / (ms * 1e-3) / 1e12, 1)
+                else:
+                    d["solo_tbps"] = round(work / (ms * 1e-3) / 1e12, 3)
+            out[key] = d
+        return out
 
     def step(self) -> Dict[str, float]:
         """One co-run step; returns per-tenant completion times (ms) in the step."""
@@ -555,11 +716,38 @@ class Corun:
         r = self.runners[name]
         return r.stats().units_done if isinstance(r, Runner) else r.units_done
 
+    def _dyn_apply(self):
+        """Mix "phase": the phase tenant's workload and the hbm tenant's
+        presence follow a fixed schedule from the start of the run (warmup
+        included), the same for every policy."""
+        if not MIXES[self.cfg.mix].get("dynamic"):
+            return
+        el = (time.monotonic_ns() - self._dyn_t0) / 1e6
+        want = {"phase": int(el // self.cfg.phase_ms) % 2, "hbm": int(el // self.cfg.onoff_ms) % 2 == 0}
+        if self._dyn_state.get("phase") != want["phase"]:
+            self.runners["phase"].set_phase(want["phase"])
+            self._dyn_state["phase"] = want["phase"]
+            self._dyn_state["flips"] = self._dyn_state.get("flips", 0) + 1
+        if self._dyn_state.get("hbm") != want["hbm"]:
+            self._dyn_state["hbm"] = want["hbm"]
+            if want["hbm"]:
+                self._off.discard("hbm")
+            else:
+                self._off.add("hbm")
+                self.runners["hbm"].cancel()  # drains its in-flight units, then blocks its slots
+
+    def _dyn_reset(self):
+        if MIXES[self.cfg.mix].get("dynamic"):
+            self.runners["phase"].set_phase(0)
+        self._off.clear()
+        self._dyn_state = {}
+
     def _idle_request(self, until_ns: int):
         """Latency tenant: closed loop with think time until `until_ns`."""
         idle = self.runners.get("idle")
         n = 0
         while time.monotonic_ns() < until_ns:
+            self._dyn_apply()
             if idle is not None:
                 idle.submit(1)
                 idle.wait(30.0)
@@ -571,11 +759,26 @@ class Corun:
     def _topup(self):
         """Keep every native throughput runner backlogged (>= 2 quotas queued)."""
         for name in self.throughput:
+            if name in self._off:
+                continue
             r = self.runners[name]
             if isinstance(r, Runner):
                 st = r.stats()
                 if st.submitted - st.units_done < 2 * self.quota[name]:
                     r.submit(2 * self.quota[name])
+
+    def _work(self, name: str):
+        """(units done, of which alternate-workload units)."""
+        r = self.runners[name]
+        if isinstance(r, Runner):
+            st = r.stats()
+            return st.units_done, st.units_alt
+        return r.units_done, 0
+
+    def _solo_equiv(self, name: str, du: int, da: int) -> float:
+        """Solo-time equivalent (ms) of du units, da of them alternate-workload."""
+        ms = self.solo_unit_ms[name]
+        return (du - da) * ms + da * self.solo_unit_ms.get(f"{name}:alt", ms)
 
     def run_policy_steady(self, policy: str, steps: int, warmup: int) -> Dict:
         """Steady-state weighted speedup: all throughput tenants backlogged for
@@ -584,6 +787,9 @@ class Corun:
         self.set_policy(policy)
         cfg = self.cfg
         coll = self.runners.get("coll")
+        self._dyn_state = {}
+        self._dyn_t0 = time.monotonic_ns()
+        self._dyn_apply()
         self._topup()
         if isinstance(coll, CollTenant):
             coll.start_loop()
@@ -601,19 +807,25 @@ class Corun:
             if self.cfg.hw_counters:
                 self.ctx.hwc_reset()
         quanta = {n: [] for n in self.tid}
+        layout = {n: [] for n in self.throughput}  # budget SE sets per step (bit c = SE c)
         self._barrier()
         t0 = time.perf_counter()
-        d0 = {n: self._done(n) for n in self.throughput}
+        d0 = {n: self._work(n) for n in self.throughput}
         per_step = []
         for _ in range(steps):
-            ts, ds = time.perf_counter(), {n: self._done(n) for n in self.throughput}
+            ts, ds = time.perf_counter(), {n: self._work(n) for n in self.throughput}
             self._idle_request(time.monotonic_ns() + step_ns)
             te = time.perf_counter()
-            per_step.append({n: (self._done(n) - ds[n]) / ((te - ts) * 1e3) for n in self.throughput})
+            dn = {n: self._work(n) for n in self.throughput}
+            per_step.append({n: self._solo_equiv(n, dn[n][0] - ds[n][0], dn[n][1] - ds[n][1]) / ((te - ts) * 1e3)
+                             for n in self.throughput})
             if e is not None:
                 for n in self.tid:
-                    quanta[n].append(e.tenant_info(self.tid[n]).tslice_us)
-        d1 = {n: self._done(n) for n in self.throughput}
+                    ti = e.tenant_info(self.tid[n])
+                    quanta[n].append(ti.tslice_us)
+                    if n in layout:
+                        layout[n].append(ti.budget_ctx)
+        d1 = {n: self._work(n) for n in self.throughput}
         wall_ms_local = (time.perf_counter() - t0) * 1e3
         self._barrier()
         wall_ms = self._allreduce(wall_ms_local, "max")
@@ -628,19 +840,28 @@ class Corun:
             r = self.runners[name]
             if isinstance(r, Runner):
                 r.wait(120.0)
+        flips = self._dyn_state.get("flips", 0)
+        self._dyn_reset()
         lats = [x / 1e6 for x in self.runners["idle"].latencies(clear=True)] if "idle" in self.runners else []
         res = {"policy": policy, "protocol": "steady", "wall_ms": wall_ms, "ms_per_step": wall_ms / steps,
                "tenants": {}}
+        if MIXES[cfg.mix].get("dynamic"):
+            res["phase_flips"] = flips
         agg, slows = 0.0, []
         for n in self.throughput:
-            rate = (d1[n] - d0[n]) / wall_ms_local  # units per ms
-            perf = rate * self.solo_unit_ms[n]
+            du, da = d1[n][0] - d0[n][0], d1[n][1] - d0[n][1]
+            rate = du / wall_ms_local  # units per ms
+            perf = self._solo_equiv(n, du, da) / wall_ms_local
             agg += perf
             slows.append((1.0 / perf - 1.0) * 100.0 if perf > 0 else 1e4)
-            res["tenants"][n] = {"units": d1[n] - d0[n], "units_per_ms": round(rate, 4),
+            res["tenants"][n] = {"units": du, "units_per_ms": round(rate, 4),
                                  "solo_units_per_ms": round(1.0 / self.solo_unit_ms[n], 4),
                                  "norm_perf": round(perf, 4), "slowdown_pct": round(slows[-1], 2),
-                                 "step_norm_perf": [round(ps[n] * self.solo_unit_ms[n], 3) for ps in per_step]}
+                                 "step_norm_perf": [round(ps[n], 3) for ps in per_step]}
+            if da:
+                res["tenants"][n]["units_alt"] = da
+            if e is not None and any(layout[n]):
+                res["tenants"][n]["se_layout"] = layout[n]
         self._finish_result(res, e, lats, slows, agg, wall_ms, quanta, run0 if e is not None else None, policy)
         self.log(f"[corun] {policy}: " + json.dumps(res))
         return res
@@ -710,7 +931,8 @@ class Corun:
         if e is not None:
             pc = e.perfc()
             eng = {k: pc[k] for k in ("sched_ctx", "acct_run", "metric_tick", "adapt_inc", "adapt_dec",
-                                      "adapt_rearm", "migrate_queued", "vcpu_wake_runnable", "tickle_idlers_some")}
+                                      "adapt_rearm", "migrate_queued", "vcpu_wake_runnable", "tickle_idlers_some",
+                                      "class_change", "relayout")}
             eng["gpu"] = self.ctx.stats()
             if self.cfg.hw_counters:
                 eng["hwc"] = self.ctx.hwc_stats()

@@ -68,6 +68,9 @@ class TenantInfo:
     sched_count: int
     run_ns: int
     shutdown: int = 0
+    online_slots: int = 0
+    budget_ctx: int = 0      # class_budget: shader engines of every XCD the layout gave the tenant (bit c)
+    budget_shared: bool = False
 
 
 @dataclass
@@ -246,7 +249,8 @@ class Engine:
                           last_err=o.last_err, last_curr=o.last_curr, last_win=o.last_win, pmc=tuple(o.pmc),
                           cache_miss_rate=o.cache_miss_rate, cpi=o.cpi, spin_latency=o.spin_latency,
                           report_count=o.report_count, pending_requests=o.pending_requests,
-                          sched_count=o.sched_count, run_ns=o.run_ns, shutdown=o.shutdown)
+                          sched_count=o.sched_count, run_ns=o.run_ns, shutdown=o.shutdown,
+                          online_slots=o.online_slots, budget_ctx=o.budget_ctx, budget_shared=bool(o.budget_shared))
 
     def slot_info(self, sid: int) -> Dict:
         o = N.SlotInfo()

@@ -12,13 +12,15 @@ vp = C.c_void_p
 class RunnerCfg(C.Structure):
     _fields_ = [(n, C.c_int) for n in ("kind", "tenant", "gate", "priority", "depth", "grid", "M", "N", "K",
                                        "chunk_bytes", "engine_wake", "reserved")] + \
-               [("bytes", C.c_ulonglong), ("a", vp), ("b", vp), ("c", vp)]
+               [("bytes", C.c_ulonglong), ("a", vp), ("b", vp), ("c", vp)] + \
+               [(n, C.c_int) for n in ("alt_kind", "alt_M", "alt_N", "alt_K", "alt_chunk_bytes", "alt_reserved")] + \
+               [("alt_bytes", C.c_ulonglong), ("alt_a", vp), ("alt_b", vp), ("alt_c", vp)]
 
 
 class RunnerStats(C.Structure):
     _fields_ = [(n, u64) for n in ("units_done", "launches", "relaunches", "waits_owner", "submitted")] + \
                [(n, i64) for n in ("busy_ns", "wait_owner_ns", "first_start_ns", "last_done_ns", "lat_sum_ns",
-                                   "lat_max_ns")] + [("lat_count", u64)]
+                                   "lat_max_ns")] + [("lat_count", u64), ("units_alt", u64)]
 
 
 KIND = {"gemm": 1, "stream": 2, "reduce": 3, "gemv": 4}
@@ -115,4 +117,5 @@ def bind(lib):
     _p(lib, "gpbs_runner_cancel", i64, vp)
     _p(lib, "gpbs_runner_set_engine_wake", C.c_int, vp, C.c_int)
     _p(lib, "gpbs_runner_stream", vp, vp)
+    _p(lib, "gpbs_runner_set_phase", C.c_int, vp, C.c_int)
     _p(lib, "gpbs_runner_destroy", None, vp)

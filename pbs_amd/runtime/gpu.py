@@ -278,13 +278,18 @@ class RunnerStats:
     lat_sum_ns: int
     lat_max_ns: int
     lat_count: int
+    units_alt: int = 0
 
 
 class Runner:
-    """Native tenant worker.  ``kind`` in {gemm, stream, reduce, gemv}."""
+    """Native tenant worker.  ``kind`` in {gemm, stream, reduce, gemv}.
+
+    ``alt`` (optional): a second workload ``dict(kind=..., **shape)`` for a
+    phase-changing tenant; ``set_phase(1)`` makes every fresh unit run it
+    (``stats().units_alt`` counts them)."""
 
     def __init__(self, ctx: GpuContext, kind: str, tenant: int, *, gate: bool = True, priority: int = 0,
-                 depth: int = 2, grid: int = 0, engine_wake: bool = True, **shape):
+                 depth: int = 2, grid: int = 0, engine_wake: bool = True, alt: Optional[dict] = None, **shape):
         self.ctx = ctx
         self.L = ctx.L
         self.kind = kind
@@ -293,7 +298,6 @@ class Runner:
         g = torch.Generator(device=dev)
         g.manual_seed(1234 + tenant)
         cfg = hipabi.RunnerCfg()
-        cfg.kind = hipabi.KIND[kind]
         cfg.tenant = tenant
         cfg.gate = int(gate)
         cfg.priority = priority
@@ -301,47 +305,66 @@ class Runner:
         cfg.grid = grid
         cfg.engine_wake = int(engine_wake)
         self.buffers = []
-        if kind == "gemm":
-            M, Nn, K = shape.get("M", 4096), shape.get("N", 4096), shape.get("K", 4096)
-            a = torch.randn(M, K, device=dev, dtype=torch.bfloat16, generator=g)
-            b = torch.randn(Nn, K, device=dev, dtype=torch.bfloat16, generator=g)
-            c = torch.empty(M, Nn, device=dev, dtype=torch.bfloat16)
-            cfg.M, cfg.N, cfg.K = M, Nn, K
-            self.work_per_unit = 2.0 * M * Nn * K  # FLOP
-            self.unit_name = "FLOP"
-        elif kind in ("stream", "reduce"):
-            nbytes = int(shape.get("bytes", 1 << 30))
-            chunk = int(shape.get("chunk_bytes", 1 << 19))
-            cfg.bytes = nbytes
-            cfg.chunk_bytes = chunk
-            n = nbytes // 2
-            a = torch.randn(n, device=dev, dtype=torch.bfloat16, generator=g)
-            b = torch.randn(n, device=dev, dtype=torch.bfloat16, generator=g) if kind == "reduce" else None
-            c = torch.empty(n, device=dev, dtype=torch.bfloat16)
-            self.work_per_unit = float(nbytes * (2 if kind == "stream" else 3))  # bytes moved
-            self.unit_name = "B"
-        elif kind == "gemv":
-            R, K = shape.get("M", 8192), shape.get("K", 8192)
-            a = torch.randn(R, K, device=dev, dtype=torch.bfloat16, generator=g)
-            b = torch.randn(K, device=dev, dtype=torch.bfloat16, generator=g)
-            c = torch.empty(R, device=dev, dtype=torch.float32)
-            cfg.M, cfg.K = R, K
-            self.work_per_unit = float(R * K * 2)
-            self.unit_name = "B"
-        else:
-            raise ValueError(kind)
-        for t in (a, b, c):
-            if t is not None:
-                self.buffers.append(t)
-        cfg.a = a.data_ptr()
-        cfg.b = b.data_ptr() if b is not None else None
-        cfg.c = c.data_ptr()
+        w = self._workload(kind, shape, dev, g)
+        cfg.kind, cfg.M, cfg.N, cfg.K, cfg.chunk_bytes, cfg.bytes = w["kind"], w["M"], w["N"], w["K"], w["chunk"], w["bytes"]
+        cfg.a, cfg.b, cfg.c = w["a"], w["b"], w["c"]
+        self.work_per_unit, self.unit_name = w["work"], w["unit"]
+        self.alt_kind = None
+        if alt:
+            alt = dict(alt)
+            self.alt_kind = alt.pop("kind")
+            v = self._workload(self.alt_kind, alt, dev, g)
+            cfg.alt_kind, cfg.alt_M, cfg.alt_N, cfg.alt_K = v["kind"], v["M"], v["N"], v["K"]
+            cfg.alt_chunk_bytes, cfg.alt_bytes = v["chunk"], v["bytes"]
+            cfg.alt_a, cfg.alt_b, cfg.alt_c = v["a"], v["b"], v["c"]
+            self.alt_work_per_unit = v["work"]
         torch.cuda.synchronize(dev)
         self.cfg = cfg
         h = self.L.gpbs_runner_create(ctx.h, C.byref(cfg))
         if not h:
             raise RuntimeError(f"runner_create failed for {kind}")
         self.h = C.c_void_p(h)
+
+    def _workload(self, kind, shape, dev, g) -> dict:
+        """Device buffers + ABI fields of one workload kind."""
+        M = Nn = K = chunk = nbytes = 0
+        b = None
+        if kind == "gemm":
+            M, Nn, K = shape.get("M", 4096), shape.get("N", 4096), shape.get("K", 4096)
+            a = torch.randn(M, K, device=dev, dtype=torch.bfloat16, generator=g)
+            b = torch.randn(Nn, K, device=dev, dtype=torch.bfloat16, generator=g)
+            c = torch.empty(M, Nn, device=dev, dtype=torch.bfloat16)
+            work, unit = 2.0 * M * Nn * K, "FLOP"
+        elif kind in ("stream", "reduce"):
+            nbytes = int(shape.get("bytes", 1 << 30))
+            chunk = int(shape.get("chunk_bytes", 1 << 19))
+            n = nbytes // 2
+            a = torch.randn(n, device=dev, dtype=torch.bfloat16, generator=g)
+            b = torch.randn(n, device=dev, dtype=torch.bfloat16, generator=g) if kind == "reduce" else None
+            c = torch.empty(n, device=dev, dtype=torch.bfloat16)
+            work, unit = float(nbytes * (2 if kind == "stream" else 3)), "B"  # bytes moved
+        elif kind == "gemv":
+            M, K = shape.get("M", 8192), shape.get("K", 8192)
+            a = torch.randn(M, K, device=dev, dtype=torch.bfloat16, generator=g)
+            b = torch.randn(K, device=dev, dtype=torch.bfloat16, generator=g)
+            c = torch.empty(M, device=dev, dtype=torch.float32)
+            work, unit = float(M * K * 2), "B"
+        else:
+            raise ValueError(kind)
+        for t in (a, b, c):
+            if t is not None:
+                self.buffers.append(t)
+        return {"kind": hipabi.KIND[kind], "M": M, "N": Nn, "K": K, "chunk": chunk, "bytes": nbytes,
+                "a": a.data_ptr(), "b": b.data_ptr() if b is not None else None, "c": c.data_ptr(),
+                "work": work, "unit": unit}
+
+    def set_phase(self, alt: int) -> int:
+        """Phase-changing tenant: fresh units run the alternate workload (1)
+        or the primary one (0); returns the previous phase."""
+        rc = self.L.gpbs_runner_set_phase(self.h, int(alt))
+        if rc < 0:
+            raise RuntimeError("set_phase: runner has no alternate workload")
+        return rc
 
     def submit(self, units: int = 1):
         self.L.gpbs_runner_submit(self.h, units)

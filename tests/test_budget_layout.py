@@ -1,0 +1,121 @@
+"""Demand-driven SE budgets (class_budget, simulated clock).
+
+Every PRESENT classified tenant gets a set of shader engines of every XCD,
+sized from the classes present (csrc/core/engine.cpp budget_layout); surplus
+slots go offline.  The layout follows phase changes (a tenant whose counters
+turn memory-bound) and tenants that stop and start, which a hand-picked
+static SE split cannot (bench.py --mix phase measures that on MI355X).
+"""
+from collections import Counter
+
+from pbs_amd.core.config import MI355X_PROFILE
+from pbs_amd.core.engine import Engine
+
+from test_engine_credit import _feed
+
+COMPUTE, MEMORY = (1000, 1), (100, 100)  # (inst, miss) per us: rate 100 vs 1e5 per 100k inst
+
+
+def _engine(**over):
+    parts = [(0, x, c) for x in range(8) for c in range(4)]
+    prof = dict(MI355X_PROFILE)
+    prof.update(class_split=2, idle_skip=1, quantum_align_us=0, class_budget=1, present_us=5000)
+    prof.update(over)
+    e = Engine(sim_clock=True, partitions=parts, **prof)
+    e.tenant_create("Domain-0", nslots=1)
+    return e, parts
+
+
+def _ctx_owners(e, parts):
+    """ctx -> Counter(tenant running there) over the 8 XCDs."""
+    out = {c: Counter() for c in range(4)}
+    for p, (_, _, c) in enumerate(parts):
+        out[c][e.partition_info(p)["curr_tenant"]] += 1
+    return out
+
+
+def _online(e, t):
+    return e.tenant_info(t).online_slots
+
+
+def _settle(e, rates, steps=400):
+    for _ in range(steps):
+        _feed(e, rates, 100)
+
+
+def test_budget_4mix_one_memory_se_each():
+    e, parts = _engine()
+    g, h, r = (e.tenant_create(n, nslots=32) for n in ("gemm", "hbm", "coll"))
+    rates = {g: COMPUTE, h: MEMORY, r: MEMORY}
+    for t in rates:
+        e.wake(t)
+    _settle(e, rates)
+    own = _ctx_owners(e, parts)
+    assert own[0][g] == 8 and own[1][g] == 8, own
+    assert own[2][h] == 8 and own[3][r] == 8, own
+    assert (_online(e, g), _online(e, h), _online(e, r)) == (16, 8, 8)
+    assert e.perfc()["relayout"] >= 1
+    assert e.check() == ""
+
+
+def test_budget_follows_phase_change_and_a_stopped_tenant():
+    e, parts = _engine()
+    g, p, s = (e.tenant_create(n, nslots=32) for n in ("gemm", "phase", "hbm"))
+    rates = {g: COMPUTE, p: COMPUTE, s: MEMORY}
+    for t in rates:
+        e.wake(t)
+    _settle(e, rates)
+    own = _ctx_owners(e, parts)
+    # two compute tenants share the compute half one SE each; the lone memory
+    # tenant takes both memory SEs
+    assert own[0][g] == 8 and own[1][p] == 8 and own[2][s] == 8 and own[3][s] == 8, own
+    # the phase tenant turns memory-bound: it moves to a memory SE, the GEMM
+    # gets the whole compute half
+    rates[p] = MEMORY
+    rearm0 = e.perfc()["adapt_rearm"]
+    _settle(e, rates)
+    own = _ctx_owners(e, parts)
+    assert own[0][g] == 8 and own[1][g] == 8, own
+    assert {own[2].most_common(1)[0][0], own[3].most_common(1)[0][0]} == {p, s}, own
+    assert e.perfc()["adapt_rearm"] > rearm0  # the PBS window re-armed on the phase change
+    # the stream tenant stops: after present_us the phase tenant holds both memory SEs
+    e.block(s)
+    rates.pop(s)
+    _settle(e, rates)
+    own = _ctx_owners(e, parts)
+    assert own[2][p] == 8 and own[3][p] == 8, own
+    # ... and with the phase tenant compute-bound again and the stream still
+    # gone, the two GEMMs split the GPU two SEs each
+    rates[p] = COMPUTE
+    _settle(e, rates, 600)
+    own = _ctx_owners(e, parts)
+    assert sorted([own[0][g] + own[1][g], own[2][p] + own[3][p]]) == [16, 16] or \
+        sorted([own[0][p] + own[1][p], own[2][g] + own[3][g]]) == [16, 16], own
+    # the stream comes back: it is re-placed on the memory half
+    e.wake(s)
+    rates[s] = MEMORY
+    _settle(e, rates)
+    own = _ctx_owners(e, parts)
+    assert own[2][s] == 8 and own[3][s] == 8, own
+    assert e.check() == ""
+
+
+def test_budget_time_shares_a_crowded_class_region():
+    e, parts = _engine()
+    g = e.tenant_create("gemm", nslots=32)
+    mem = [e.tenant_create(f"m{i}", nslots=32) for i in range(3)]
+    rates = {g: COMPUTE, **{m: MEMORY for m in mem}}
+    for t in rates:
+        e.wake(t)
+    _settle(e, rates)
+    assert [_online(e, m) for m in mem] == [16, 16, 16]
+    assert _online(e, g) == 16
+    base = {t: e.tenant_info(t).run_ns for t in rates}
+    t0 = e.now()
+    _settle(e, rates, 1500)
+    dt = e.now() - t0
+    share = {t: (e.tenant_info(t).run_ns - base[t]) / dt for t in rates}
+    assert share[g] > 15.5, share
+    ms = [share[m] for m in mem]
+    assert sum(ms) > 15.0 and max(ms) - min(ms) < 2.5, share
+    assert e.check() == ""

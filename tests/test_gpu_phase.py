@@ -1,0 +1,119 @@
+"""The counter-driven SE budget layout follows a phase change on a real MI355X.
+
+Three tenants under the PBS engine with class_budget, on live hardware
+counters attributed by SE ownership: a GEMM, an HBM stream, and a "phase"
+tenant that runs GEMM units, then stream units, then GEMM units again.  The
+classifier must see each change in the phase tenant's counters and the
+layout must move it between the compute half (one compute SE, next to the
+GEMM) and a memory SE (next to the stream), within a bounded number of
+metric periods -- what a hand-picked static layout cannot do.  The PBS
+phase detector re-arms its window on the change (adapt_rearm).
+
+Runs in a subprocess: the counter sampler registers with rocprofiler-sdk
+before the HIP runtime initialises.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("no GPU", allow_module_level=True)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CODE = r"""
+import json, sys, time
+sys.path.insert(0, %r)
+from pbs_amd.counters import hwc
+assert hwc.init()
+import torch
+torch.cuda.set_device(0)
+torch.zeros(1, device="cuda")
+assert hwc.start()
+from pbs_amd.runtime.gpu import GpuContext, Runner
+from pbs_amd.core.config import MI355X_PROFILE
+from pbs_amd.core.engine import Engine
+from pbs_amd.bench.corun import BUDGET_OVERRIDES
+prof = dict(MI355X_PROFILE); prof.update(BUDGET_OVERRIDES)
+e = Engine(**prof)
+for x in range(8):
+    for c in range(4):
+        e.pool_assign(0, e.partition_add(0, x, c))
+e.tenant_create("Domain-0", nslots=1)
+g = e.tenant_create("gemm", nslots=32)
+p = e.tenant_create("phase", nslots=32)
+s = e.tenant_create("hbm", nslots=32)
+ctx = GpuContext(0, nctx=4, table_mode="device")
+ctx.set_se_mode(True)
+ctx.attach(e, nctx=4)
+ctx.set_hwc(True)
+e.start()
+rg = Runner(ctx, "gemm", g, M=4096, N=4096, K=4096)
+rp = Runner(ctx, "gemm", p, M=4096, N=4096, K=4096, alt=dict(kind="stream", bytes=1 << 30))
+rs = Runner(ctx, "stream", s, bytes=1 << 30)
+def topup():
+    for r, q in ((rg, 400), (rp, 400), (rs, 100)):
+        st = r.stats()
+        if st.submitted - st.units_done < q:
+            r.submit(q)
+def info():
+    return {n: (e.lib.gpbs_tenant_class(e.h, t), e.tenant_info(t).budget_ctx) for n, t in (("gemm", g), ("phase", p), ("hbm", s))}
+def run_until(pred, limit_s):
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < limit_s:
+        topup()
+        if pred(info()):
+            return (time.perf_counter() - t0) * 1e3
+        time.sleep(0.001)
+    return -1.0
+out = {"metric_period_us": prof["metric_period_us"]}
+def compute_layout(i):
+    return i["phase"][0] == 0 and i["phase"][1] in (1, 2) and i["gemm"][1] in (1, 2) and i["hbm"][1] == 12
+def memory_layout(i):
+    return i["phase"][0] == 1 and i["phase"][1] in (4, 8) and i["gemm"][1] == 3 and i["hbm"][1] in (4, 8)
+out["settle_ms"] = run_until(compute_layout, 5.0)
+out["layout0"] = info()
+e.perfc_reset()
+rp.set_phase(1)
+out["to_memory_ms"] = run_until(memory_layout, 3.0)
+out["layout1"] = info()
+rp.set_phase(0)
+out["to_compute_ms"] = run_until(compute_layout, 3.0)
+out["layout2"] = info()
+pc = e.perfc()
+out["adapt_rearm"] = pc["adapt_rearm"]; out["relayout"] = pc["relayout"]; out["class_change"] = pc["class_change"]
+out["units_alt"] = rp.stats().units_alt
+out["hwc"] = ctx.hwc_stats()
+for r in (rg, rp, rs):
+    r.cancel()
+for r in (rg, rp, rs):
+    r.wait(120)
+e.stop()
+out["check"] = e.check()
+for r in (rg, rp, rs):
+    r.close()
+ctx.close(); e.close()
+print("RESULT " + json.dumps(out))
+"""
+
+
+def test_budget_layout_follows_a_phase_change_on_live_counters():
+    r = subprocess.run([sys.executable, "-c", CODE % ROOT], capture_output=True, text=True, timeout=180,
+                       env=dict(os.environ))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    out = json.loads([x for x in r.stdout.splitlines() if x.startswith("RESULT ")][-1][7:])
+    print(json.dumps(out, indent=1))
+    assert out["settle_ms"] >= 0, out
+    # within 100 metric periods (1 ms each) of the change in both directions:
+    # the classifier's EWMA (alpha 1/4), its dwell and the class tick
+    assert 0 <= out["to_memory_ms"] < 100, out
+    assert 0 <= out["to_compute_ms"] < 100, out
+    assert out["units_alt"] > 0
+    assert out["class_change"] >= 2 and out["relayout"] >= 2, out
+    assert out["adapt_rearm"] > 0, out
+    assert out["check"] == ""
