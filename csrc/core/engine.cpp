@@ -746,6 +746,8 @@ void Engine::place_tenant_class(Tenant& t, Pool& pl, int layout) {
 //     covers;
 //   * n > r: every tenant of the region gets the whole region, staggered, and
 //     credit time-shares it with PBS quanta (the class region is one gang).
+// A busy tenant that is not classified yet is placed as memory class until
+// its counters say otherwise.
 // A tenant gets exactly one online slot per partition of its set; surplus
 // slots go offline (VPF_DOWN, the vcpu-set path), so its share follows the
 // layout instead of a creation-time slot count.  An absent tenant keeps its
@@ -804,8 +806,12 @@ void Engine::budget_layout(Pool& pl, int64_t n, bool force) {
       if (!(v.pause_flags & VPF_BLOCKED) && v.pause_count == 0) busy = true;
     }
     if (busy && t.pause_count == 0) t.last_busy = n;
-    const bool present = t.cls >= 0 && n - t.last_busy <= present_ns;
-    if (present) sig.emplace_back(t.id, t.cls);
+    // A busy tenant not classified yet is placed provisionally with the
+    // memory class: on SEs of its own, its counters become attributable (a
+    // tenant left floating across time-shared partitions never gets a clean
+    // window, so it would never be classified at all).
+    const bool present = n - t.last_busy <= present_ns;
+    if (present) sig.emplace_back(t.id, t.cls >= 0 ? t.cls : 1);
     else t.budget_ctx = 0;
   }
   if (!force && sig == pl.budget_sig) return;

@@ -18,7 +18,9 @@
 #include <rocprofiler-sdk-roctx/roctx.h>
 #include <x86intrin.h>
 
+#include <algorithm>
 #include <atomic>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <chrono>
@@ -31,6 +33,7 @@
 
 #include "../include/gpbs/gpbs.h"
 #include "common.hpp"
+#include "hwc_attr.h"
 
 using namespace gpbs_hip;
 
@@ -52,6 +55,7 @@ int gpbs_hip_partition_switch(void*, unsigned, const unsigned*, hipStream_t);
 int gpbs_hip_counter_reduce(void*, void*, const int*, int, void*, hipStream_t);
 int gpbs_hip_adapt(void*, const void*, const void*, const void*, int, const gpbs_adapt_params_t*, int*, hipStream_t);
 int gpbs_hip_switch_probe(const void*, int, unsigned*, int, unsigned, unsigned long long, hipStream_t);
+int gpbs_hip_hwc_attribute(const void*, void*, void*, hipStream_t);
 }
 
 namespace {
@@ -198,6 +202,13 @@ struct GpuCtx {
   gpbs_engine_t* engine = nullptr;
   int nctx = 1;                  // issue contexts per XCD in use (1..kCtx)
   int waveprio = 0;              // latency-class runners raise their wave priority
+  // Latency lane: ungated latency-class runners (priority > 0) launch on a
+  // stream CU-masked to this class half (0: SEs {0,1}, 1: SEs {2,3}; -1:
+  // unmasked).  The memory half hosts small-footprint stream / reduce
+  // workgroups a GEMV can co-reside with; on the compute half its
+  // workgroups queue behind persistent GEMM workgroups holding the CUs' LDS
+  // until a whole GEMM unit ends.
+  int lat_half = -1;
   int hold_enable = 0;           // latency requests hold the memory-class tenants (GATE_HOLD)
   int hold_all = 0;              // GPBS_HOLD_ALL=1: hold every gated tenant, compute class too (ablation)
   // Latency-request hold: count of latency units in flight and the hold
@@ -234,11 +245,23 @@ struct GpuCtx {
   int slot_se[kNumPmc] = {1, 1, 1, 0};  // slot k resolved per shader engine
   u64* h_blk = nullptr;                 // pinned landing buffer of d_cnt copies
   std::vector<u64> snap_blk, blk_prev;  // newest published / last consumed model block
-  std::vector<u64> snap_se, se_prev;    // [kXcds * kCtx(=SEs) * kNumPmc]
-  std::vector<u64> snap_x, x_prev;      // [kXcds * kNumPmc]
-  std::vector<int64_t> snap_own, own_prev;  // [kMaxTenants * kXcds * kCtx]
+  std::vector<u64> snap_se;             // [kXcds * kCtx(=SEs) * kNumPmc]
+  std::vector<u64> snap_x;              // [kXcds * kNumPmc]
+  std::vector<int64_t> snap_own;        // [kMaxTenants * kXcds * kCtx]
   uint64_t snap_seq = 0, used_seq = 0;
   bool hw_primed = false;
+  // Attribution of a snapshot (csrc/hip/hwc_attr.h): on the GPU by default
+  // (k_hwc_attribute on the scheduler stream, launched by one metric tick and
+  // harvested by the next -- the engine lock is never held across a device
+  // wait), on the host with GPBS_HWC_DEVICE=0.
+  int dev_attr = 1;
+  HwcAttrPrev hst;                  // host path state
+  HwcAttrIn* h_ain = nullptr;       // pinned, read by the kernel
+  HwcAttrOut* h_aout = nullptr;     // pinned mapped, written by the kernel
+  HwcAttrPrev* d_ast = nullptr;     // device-resident previous snapshot
+  hipEvent_t attr_ev = nullptr;
+  bool attr_pending = false;
+  uint64_t attr_launches = 0, attr_busy_skips = 0, attr_host = 0;
   hipEvent_t blk_ev = nullptr;
   hipStream_t hwc_stream = nullptr;
   std::thread hwc_th;
@@ -260,7 +283,6 @@ struct GpuCtx {
   double unatt[kNumPmc] = {};                             // hardware counts no owner explains
   double metric_sum[kNumPmc] = {};                        // counts delivered to the PBS metric (clean windows)
   int clean_pct = 90;  // exclusive-ownership window: min % of an interval one owner must hold (0: pro rata)
-  int prev_raw[kXcds * kCtx];  // per partition: its >= clean_pct owner over the previous interval, -1 none
   double att_total[kMaxTenants][kNumPmc] = {};            // per-tenant attributed hardware totals
   double met_total[kMaxTenants][kNumPmc] = {};            // per-tenant totals that reached the PBS metric
   double mod_total[kMaxTenants][kNumPmc] = {};            // per-tenant modeled totals (cross-check)
@@ -276,7 +298,7 @@ struct GpuCtx {
   int64_t last_pub_ns = 0;
   hipEvent_t adapt_ev = nullptr;  // device adapt: bounded poll, never a blocking sync
   bool adapt_pending = false;
-  uint64_t adapt_late = 0;
+  uint64_t adapt_late = 0, adapt_calls = 0, adapt_busy = 0;
   int se_mode = 0;  // partitions are exclusive shader engines (GATE_SE)
   // Class-share mode (SE mode): when every tenant holding partitions is of
   // ONE contention class, runners launch ungated full-GPU grids (co-resident:
@@ -521,147 +543,43 @@ void hwc_loop(GpuCtx* c) {
 
 inline u64 dpos(u64 a, u64 b) { return a >= b ? a - b : 0; }  // Q5: a counter reset is no negative delta
 
-// Ownership attribution of one snapshot interval (snap_mu held).
-//  * SE-resolved slots in SE-exclusive mode: the delta of partition (x, e)
-//    goes to the tenants that owned it in the interval, pro rata to owned
-//    time -- exact while ownership is stable over a sample interval.
-//  * Co-resident modes (every owner's waves run on all SEs of the XCD): the
-//    XCD's delta is split by owned time (an approximation, reported as such).
-//  * LLC misses (TCC, per XCD): split by each tenant's attributed share of the
-//    XCD's L2 requests (both measured).
-// Counts no owner explains (an SE nobody owned: stray workgroups draining
-// after a revocation, the scheduler's own kernels) are kept as unattributed.
-//
-// Exclusive-ownership windows (what the PBS metric and the contention class
-// see): a partition's delta reaches the per-tenant metric deltas only when one
-// tenant owned it for at least clean_pct % of the interval.  A time-shared
-// interval splits pro rata for the accounting totals, but the per-tenant
-// RATES of such a split are the mixture's, identical for every owner: a
-// reduce-copy tenant time-sharing an SE with a GEMM reads as the GEMM's miss
-// rate (its instructions are a few % of the interval's), is classed compute,
-// is placed beside the GEMM again, and never measures cleanly -- measured on
-// MI355X as a stable misclassification.  The per-vCPU PMU save/restore of
-// X:xen/arch/x86/pmustate.c:87-111 counts exactly one vCPU per interval; this
-// is its analog for partitions whose owner changes between two samples.
-void hwc_attribute(GpuCtx* c) {
-  constexpr int P = kXcds * kCtx;
-  std::vector<double> own_d((size_t)kMaxTenants * P, 0.0);
-  for (int t = 0; t < kMaxTenants; ++t)
-    for (int p = 0; p < P; ++p) {
-      const size_t i = (size_t)t * P + p;
-      const int64_t d = c->snap_own[i] - c->own_prev[i];
-      own_d[i] = d > 0 ? (double)d : 0.0;
-    }
-  // interval length: the longest any partition was owned (owned ns of a
-  // partition sum to at most the interval)
-  double span = 0;
-  for (int p = 0; p < P; ++p) {
-    double tot = 0;
-    for (int t = 0; t < kMaxTenants; ++t) tot += own_d[(size_t)t * P + p];
-    span = std::max(span, tot);
-  }
-  // clean owner of each partition over this interval (-1: mixed / idle):
-  // it held the partition for clean_pct % of this interval AND of the
-  // previous one, so the previous owner's workgroups (a GEMM tile drains for
-  // ~0.1-0.3 ms after a revocation) have left before the interval began
-  // class-share time in the interval: kernels ran ungated on every SE, so
-  // no partition's delta is any single owner's
-  const bool shared = c->snap_share > c->share_prev;
-  int clean_owner[P];
-  for (int p = 0; p < P; ++p) {
-    int raw = -1;
-    if (span > 0 && !shared)
-      for (int t = 0; t < kMaxTenants; ++t)
-        if (own_d[(size_t)t * P + p] * 100.0 >= span * c->clean_pct) raw = t;
-    clean_owner[p] = (raw >= 0 && c->prev_raw[p] == raw) ? raw : -1;
-    c->prev_raw[p] = raw;
-  }
-  // the single clean owner of a whole XCD (every partition of it either
-  // unowned in the interval or clean-owned by that tenant), else -1
-  int xcd_owner[kXcds];
-  for (int x = 0; x < kXcds; ++x) {
-    int o = -1;
-    bool ok = true;
-    for (int e = 0; e < kCtx && ok; ++e) {
-      const int p = x * kCtx + e;
-      double tot = 0;
-      for (int t = 0; t < kMaxTenants; ++t) tot += own_d[(size_t)t * P + p];
-      if (tot <= 0) continue;
-      ok = clean_owner[p] >= 0 && (o < 0 || o == clean_owner[p]);
-      o = clean_owner[p];
-    }
-    xcd_owner[x] = ok ? o : -1;
-  }
-  double refs_x[kMaxTenants][kXcds] = {}, refs_cx[kMaxTenants][kXcds] = {};
-  double add[kMaxTenants][kNumPmc] = {}, addc[kMaxTenants][kNumPmc] = {};
-  for (int k = 0; k < kNumPmc; ++k) {
-    const bool miss_by_refs = k == 3;
-    for (int x = 0; x < kXcds; ++x) {
-      if (c->se_mode && c->slot_se[k]) {
-        for (int e = 0; e < kCtx; ++e) {
-          const int p = x * kCtx + e;
-          const double v = (double)dpos(c->snap_se[(size_t)p * kNumPmc + k], c->se_prev[(size_t)p * kNumPmc + k]);
-          c->hw_sum[k] += v;
-          double tot = 0;
-          for (int t = 0; t < kMaxTenants; ++t) tot += own_d[(size_t)t * P + p];
-          if (tot <= 0) {
-            c->unatt[k] += v;
-            continue;
-          }
-          for (int t = 0; t < kMaxTenants; ++t) {
-            const double w = own_d[(size_t)t * P + p];
-            if (w <= 0) continue;
-            add[t][k] += v * w / tot;
-            if (k == 2) refs_x[t][x] += v * w / tot;
-            if (clean_owner[p] == t) {
-              addc[t][k] += v * w / tot;
-              if (k == 2) refs_cx[t][x] += v * w / tot;
-            }
-          }
-        }
-        continue;
-      }
-      const double v = (double)dpos(c->snap_x[(size_t)x * kNumPmc + k], c->x_prev[(size_t)x * kNumPmc + k]);
-      c->hw_sum[k] += v;
-      double wt[kMaxTenants] = {}, tot = 0;
-      if (miss_by_refs) {
-        for (int t = 0; t < kMaxTenants; ++t) tot += (wt[t] = refs_x[t][x]);
-      }
-      if (tot <= 0) {  // time share over every context of the XCD
-        tot = 0;
-        for (int t = 0; t < kMaxTenants; ++t) {
-          wt[t] = 0;
-          for (int e = 0; e < kCtx; ++e) wt[t] += own_d[(size_t)t * P + x * kCtx + e];
-          tot += wt[t];
-        }
-      }
-      if (tot <= 0) {
-        c->unatt[k] += v;
-        continue;
-      }
-      for (int t = 0; t < kMaxTenants; ++t)
-        if (wt[t] > 0) {
-          add[t][k] += v * wt[t] / tot;
-          if (k == 2) refs_x[t][x] += v * wt[t] / tot;
-          if (miss_by_refs && c->se_mode && c->slot_se[2]) {
-            // the clean part of the tenant's share: its L2 requests from
-            // partitions it owned exclusively
-            addc[t][k] += v * refs_cx[t][x] / tot;
-          } else if (xcd_owner[x] == t) {  // XCD-wide counts: clean only with one owner on the XCD
-            addc[t][k] += v * wt[t] / tot;
-          }
-        }
-    }
-  }
+// Fold one attribution result into the per-tenant totals and the pending
+// metric deltas (snap_mu held).
+void hwc_fold(GpuCtx* c, const HwcAttrOut& o) {
+  if (!o.valid) return;
   for (int t = 0; t < kMaxTenants; ++t)
     for (int k = 0; k < kNumPmc; ++k) {
-      if (add[t][k] > 0) c->att_total[t][k] += add[t][k];
-      const double m = c->clean_pct > 0 ? addc[t][k] : add[t][k];
+      if (o.add[t][k] > 0) c->att_total[t][k] += o.add[t][k];
+      const double m = c->clean_pct > 0 ? o.addc[t][k] : o.add[t][k];
       if (m > 0) {
         c->last_delta[t][k] += (u64)(m + 0.5);
         c->metric_sum[k] += m;
         c->met_total[t][k] += m;
       }
+    }
+  for (int k = 0; k < kNumPmc; ++k) {
+    c->hw_sum[k] += o.hw_sum[k];
+    c->unatt[k] += o.unatt[k];
+  }
+}
+
+// The newest snapshot as attribution input (snap_mu held).
+void hwc_fill_in(GpuCtx* c, HwcAttrIn& in) {
+  std::memcpy(in.se_cur, c->snap_se.data(), sizeof(in.se_cur));
+  std::memcpy(in.x_cur, c->snap_x.data(), sizeof(in.x_cur));
+  std::memcpy(in.own_cur, c->snap_own.data(), sizeof(in.own_cur));
+  for (int k = 0; k < kNumPmc; ++k) in.slot_se[k] = (u32)c->slot_se[k];
+  in.se_mode = (u32)__atomic_load_n(&c->se_mode, __ATOMIC_ACQUIRE);
+  in.clean_pct = (u32)c->clean_pct;
+  in.shared = c->snap_share > c->share_prev;
+  in.prime = !c->hw_primed;
+}
+
+// Modeled per-tile counters over the same interval (cross-check, host).
+void hwc_model(GpuCtx* c) {
+  if (!c->hw_primed) return;
+  for (int t = 0; t < kMaxTenants; ++t)
+    for (int k = 0; k < kNumPmc; ++k) {
       double md = 0;
       for (int x = 0; x < kXcds; ++x) {
         const size_t i = ((size_t)t * kXcds + x) * kNumPmc + k;
@@ -672,21 +590,60 @@ void hwc_attribute(GpuCtx* c) {
     }
 }
 
+// Consume the newest sampler snapshot (snap_mu held).  Device path: harvest
+// the attribution launched at the previous call if it has finished, then
+// launch one for the newest snapshot; a launch still running (a tail) makes
+// this call launch nothing, and the next one covers both intervals.  With
+// `wait`, block until this call's launch is harvested (tools, not under the
+// engine lock).  Returns 1 if a snapshot was consumed.
+int hwc_consume(GpuCtx* c, bool wait) {
+  if (c->dev_attr && c->attr_pending) {
+    const hipError_t q = wait ? hipEventSynchronize(c->attr_ev) : hipEventQuery(c->attr_ev);
+    if (q == hipSuccess) {
+      hwc_fold(c, *c->h_aout);
+      c->attr_pending = false;
+    } else {
+      c->attr_busy_skips++;
+      return 0;
+    }
+  }
+  if (c->snap_seq == c->used_seq || c->snap_own.empty()) return 0;
+  c->used_seq = c->snap_seq;
+  hwc_model(c);
+  bool done = false;
+  if (c->dev_attr) {
+    hwc_fill_in(c, *c->h_ain);
+    if (gpbs_hip_hwc_attribute(c->h_ain, c->d_ast, c->h_aout, c->sched_stream) == 0 &&
+        hipEventRecord(c->attr_ev, c->sched_stream) == hipSuccess) {
+      c->attr_pending = true;
+      c->attr_launches++;
+      done = true;
+      if (wait && hipEventSynchronize(c->attr_ev) == hipSuccess) {
+        hwc_fold(c, *c->h_aout);
+        c->attr_pending = false;
+      }
+    }
+  }
+  if (!done) {  // host path (GPBS_HWC_DEVICE=0, or a failed launch)
+    static thread_local HwcAttrIn in;
+    static thread_local HwcAttrOut out;
+    hwc_fill_in(c, in);
+    hwc_attr_host(in, c->hst, out);
+    hwc_fold(c, out);
+    c->attr_host++;
+  }
+  c->blk_prev = c->snap_blk;
+  c->share_prev = c->snap_share;
+  c->hw_primed = true;
+  return 1;
+}
+
 int hwc_tenant_deltas(GpuCtx* c, int n, const int* tenants, uint64_t* out) {
   const int64_t t0 = mono_ns();
   RoctxRange rr("gpbs:metric_tick");
   {
     std::lock_guard<std::mutex> g(c->snap_mu);
-    if (c->snap_seq != c->used_seq && !c->snap_own.empty()) {
-      c->used_seq = c->snap_seq;
-      if (c->hw_primed) hwc_attribute(c);
-      c->blk_prev = c->snap_blk;
-      c->se_prev = c->snap_se;
-      c->x_prev = c->snap_x;
-      c->own_prev = c->snap_own;
-      c->share_prev = c->snap_share;
-      c->hw_primed = true;
-    }
+    hwc_consume(c, false);
   }
   // No new snapshot since the previous tick: every tenant reads zero
   // instructions and the PBS idle-sample rule (Q14) skips the period.
@@ -759,8 +716,12 @@ int ctr_adapt_batch(void* user, int n, const int*, const uint64_t* deltas, const
   // launch still running (its buffers are in use) or a result not back
   // within the poll budget makes this period fall back to the host
   // adapt_update (bit-identical), and the late result is discarded.
+  c->adapt_calls++;
   if (c->adapt_pending) {
-    if (hipEventQuery(c->adapt_ev) == hipErrorNotReady) return -11;
+    if (hipEventQuery(c->adapt_ev) == hipErrorNotReady) {
+      c->adapt_busy++;
+      return -11;
+    }
     c->adapt_pending = false;
   }
   std::memcpy(c->h_states, states, sizeof(gpbs_adapt_state_t) * n);
@@ -938,6 +899,14 @@ struct Runner {
           any |= 1u << e;
     const int half = (any & ~0x3u) == 0 ? 0 : ((any & ~0xCu) == 0 ? 1 : -1);
     if (!any || half < 0) return stream;
+    hipStream_t s = half_se_stream(half);
+    if (s != stream) cur_grid = (work(cur_alt).kind == K_GEMV) ? 0 : 128;  // one persistent WG per CU of the half
+    return s;
+  }
+
+  bool shared() const { return cfg.gate && ctx->share.load(std::memory_order_acquire); }
+
+  hipStream_t half_se_stream(int half) {
     if (!se_stream[half]) {
       u32 bits[kXcds];
       for (int x = 0; x < kXcds; ++x) bits[x] = half ? 0xCu : 0x3u;
@@ -948,15 +917,14 @@ struct Runner {
         return stream;
       }
     }
-    cur_grid = (work(cur_alt).kind == K_GEMV) ? 0 : 128;  // one persistent workgroup per CU of the half
     return se_stream[half];
   }
-
-  bool shared() const { return cfg.gate && ctx->share.load(std::memory_order_acquire); }
 
   hipStream_t pick_stream() {
     cur_grid = 0;
     const bool se = __atomic_load_n(&ctx->se_mode, __ATOMIC_ACQUIRE);
+    const int lh = __atomic_load_n(&ctx->lat_half, __ATOMIC_ACQUIRE);
+    if (cfg.priority > 0 && !cfg.gate && lh >= 0) return half_se_stream(lh & 1);  // latency lane
     if (shared()) return stream;  // class-share mode: full-GPU grid, co-resident
     if (cfg.gate && se) return pick_se_stream();
     if (!ctx->spatial || !cfg.gate) return stream;
@@ -1172,7 +1140,6 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
   std::memset(c->last_delta, 0, sizeof(c->last_delta));
   std::memset(c->own_ns, 0, sizeof(c->own_ns));
   std::memset(c->own_base, 0, sizeof(c->own_base));
-  for (int& r : c->prev_raw) r = -1;
   for (auto& k : c->cls_cache) k.store(-1, std::memory_order_relaxed);
   if (const char* v = std::getenv("GPBS_SHARE")) c->share_enable = std::atoi(v) != 0;
   if (const char* v = std::getenv("GPBS_HOLD_ALL")) c->hold_all = std::atoi(v) != 0;
@@ -1193,11 +1160,15 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
   c->blk_prev.assign((size_t)kMaxTenants * kXcds * kNumPmc, 0);
   c->snap_blk.assign((size_t)kMaxTenants * kXcds * kNumPmc, 0);
   c->snap_se.assign((size_t)kXcds * kCtx * kNumPmc, 0);
-  c->se_prev = c->snap_se;
   c->snap_x.assign((size_t)kXcds * kNumPmc, 0);
-  c->x_prev = c->snap_x;
   c->snap_own.assign((size_t)kMaxTenants * kXcds * kCtx, 0);
-  c->own_prev = c->snap_own;
+  hwc_attr_prev_init(c->hst);
+  if (const char* v = std::getenv("GPBS_HWC_DEVICE")) c->dev_attr = std::atoi(v) != 0;
+  ok = ok && hipHostMalloc((void**)&c->h_ain, sizeof(HwcAttrIn), hipHostMallocMapped) == hipSuccess;
+  ok = ok && hipHostMalloc((void**)&c->h_aout, sizeof(HwcAttrOut), hipHostMallocMapped) == hipSuccess;
+  ok = ok && hipMalloc((void**)&c->d_ast, sizeof(HwcAttrPrev)) == hipSuccess;
+  ok = ok && hipMemcpy(c->d_ast, &c->hst, sizeof(HwcAttrPrev), hipMemcpyHostToDevice) == hipSuccess;
+  ok = ok && hipEventCreateWithFlags(&c->attr_ev, hipEventDisableTiming) == hipSuccess;
   ok = ok && hipMemset(c->d_cnt, 0, sizeof(u64) * kMaxTenants * kXcds * kNumPmc) == hipSuccess;
   ok = ok && hipMemset(c->d_prev, 0, sizeof(u64) * kMaxTenants * kXcds * kNumPmc) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_out, sizeof(u64) * 4 * kMaxTenants, hipHostMallocMapped) == hipSuccess;
@@ -1265,6 +1236,13 @@ void gpbs_gpu_ctx_destroy(void* p) {
     hipEventSynchronize(c->adapt_ev);
     hipEventDestroy(c->adapt_ev);
   }
+  if (c->attr_ev) {
+    hipEventSynchronize(c->attr_ev);
+    hipEventDestroy(c->attr_ev);
+  }
+  if (c->h_ain) hipHostFree(c->h_ain);
+  if (c->h_aout) hipHostFree(c->h_aout);
+  if (c->d_ast) hipFree(c->d_ast);
   hipHostFree(c->h_states);
   hipHostFree(c->h_spin);
   hipHostFree(c->h_dirs);
@@ -1335,8 +1313,15 @@ int gpbs_gpu_set_hwc(void* p, int on) {
   c->share.store(0, std::memory_order_release);  // the sampler decides class sharing: none without it
   std::lock_guard<std::mutex> g(c->mu);
   c->hwc = on ? 1 : 0;
-  c->hw_primed = false;
-  c->used_seq = c->snap_seq;
+  {
+    std::lock_guard<std::mutex> sg(c->snap_mu);
+    if (c->attr_pending) {  // an attribution still in flight belongs to the old run
+      hipEventSynchronize(c->attr_ev);
+      c->attr_pending = false;
+    }
+    c->hw_primed = false;
+    c->used_seq = c->snap_seq;
+  }
   for (int k = 0; k < kNumPmc; ++k) c->slot_se[k] = on ? gpbs_hwc_slot_per_se(k) : 0;
   if (on) {
     if (!c->hwc_stream && hipStreamCreateWithFlags(&c->hwc_stream, hipStreamNonBlocking) != hipSuccess) return -5;
@@ -1420,16 +1405,111 @@ int gpbs_gpu_hwc_poll(void* p) {
   GpuCtx* c = (GpuCtx*)p;
   if (!c || !c->hwc) return -22;
   std::lock_guard<std::mutex> g(c->snap_mu);
-  if (c->snap_seq == c->used_seq || c->snap_own.empty()) return 0;
-  c->used_seq = c->snap_seq;
-  if (c->hw_primed) hwc_attribute(c);
-  c->blk_prev = c->snap_blk;
-  c->se_prev = c->snap_se;
-  c->x_prev = c->snap_x;
-  c->own_prev = c->snap_own;
-  c->share_prev = c->snap_share;
-  c->hw_primed = true;
-  return 1;
+  return hwc_consume(c, true);
+}
+
+// Attribution path counters: kernel launches, ticks that found the previous
+// launch still running, host-path attributions.  Returns dev_attr.
+int gpbs_gpu_hwc_attr_stats(void* p, uint64_t* launches, uint64_t* busy_skips, uint64_t* host) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c) return -22;
+  std::lock_guard<std::mutex> g(c->snap_mu);
+  if (launches) *launches = c->attr_launches;
+  if (busy_skips) *busy_skips = c->attr_busy_skips;
+  if (host) *host = c->attr_host;
+  return c->dev_attr;
+}
+
+// Device attribution on (1) / off (0, host reference); returns the old value.
+int gpbs_gpu_set_hwc_device(void* p, int on) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c) return -22;
+  std::lock_guard<std::mutex> g(c->snap_mu);
+  const int old = c->dev_attr;
+  if (on >= 0 && on != old) {
+    if (c->attr_pending) {
+      hipEventSynchronize(c->attr_ev);
+      hwc_fold(c, *c->h_aout);
+      c->attr_pending = false;
+    }
+    c->dev_attr = on ? 1 : 0;
+    c->hw_primed = false;  // the other path's previous snapshot is stale: re-prime
+  }
+  return old;
+}
+
+// Numerics check of k_hwc_attribute against hwc_attr_host on `iters` random
+// snapshot pairs (seeded): max relative difference of the attributed and
+// clean deltas and the interval totals.  Stand-alone (no context needed).
+int gpbs_hip_hwc_attr_selftest(int seed, int iters, double* max_rel) {
+  HwcAttrIn* in = nullptr;
+  HwcAttrOut* out = nullptr;
+  HwcAttrPrev* d_st = nullptr;
+  if (hipHostMalloc((void**)&in, sizeof(HwcAttrIn), hipHostMallocMapped) != hipSuccess ||
+      hipHostMalloc((void**)&out, sizeof(HwcAttrOut), hipHostMallocMapped) != hipSuccess ||
+      hipMalloc((void**)&d_st, sizeof(HwcAttrPrev)) != hipSuccess)
+    return -12;
+  static HwcAttrPrev hst;
+  static HwcAttrOut ref;
+  hwc_attr_prev_init(hst);
+  hipMemcpy(d_st, &hst, sizeof(hst), hipMemcpyHostToDevice);
+  uint64_t r = 0x9E3779B97F4A7C15ull ^ (uint64_t)seed;
+  auto rnd = [&]() {
+    r ^= r << 13;
+    r ^= r >> 7;
+    r ^= r << 17;
+    return r;
+  };
+  std::memset(in, 0, sizeof(HwcAttrIn));
+  double worst = 0;
+  int rc = 0;
+  for (int it = 0; it <= iters && rc == 0; ++it) {
+    // a random ownership pattern: most partitions with one dominant owner, some time-shared, some idle
+    for (int p = 0; p < kAttrP; ++p) {
+      const int kind = (int)(rnd() % 8);
+      const int a = 1 + (int)(rnd() % 6), b = 1 + (int)(rnd() % 6);
+      const long long span = 1000000;
+      for (int t = 0; t < kMaxTenants; ++t) {
+        long long add = 0;
+        if (kind < 5 && t == a) add = span;
+        else if (kind == 5 && t == a) add = span / 2 + (long long)(rnd() % 1000);
+        else if (kind == 5 && t == b) add = span / 2;
+        else if (kind == 6 && t == a) add = span * 95 / 100;
+        in->own_cur[t * kAttrP + p] += add;
+      }
+      for (int k = 0; k < kNumPmc; ++k) in->se_cur[p * kNumPmc + k] += rnd() % 100000000ull;
+    }
+    for (int i = 0; i < kXcds * kNumPmc; ++i) in->x_cur[i] += rnd() % 1000000000ull;
+    for (int k = 0; k < kNumPmc; ++k) in->slot_se[k] = k < 3;
+    in->se_mode = (it % 5) != 4;
+    in->clean_pct = it % 7 == 3 ? 0 : 90;
+    in->shared = it % 11 == 10;
+    in->prime = it == 0;
+    hwc_attr_host(*in, hst, ref);
+    if (gpbs_hip_hwc_attribute(in, d_st, out, nullptr) || hipDeviceSynchronize() != hipSuccess) {
+      rc = -5;
+      break;
+    }
+    if (out->valid != ref.valid) rc = -33;
+    auto rel = [](double x, double y) {
+      const double m = std::max(std::fabs(x), std::fabs(y));
+      return m > 0 ? std::fabs(x - y) / m : 0.0;
+    };
+    for (int t = 0; t < kMaxTenants; ++t)
+      for (int k = 0; k < kNumPmc; ++k) {
+        worst = std::max(worst, rel(out->add[t][k], ref.add[t][k]));
+        worst = std::max(worst, rel(out->addc[t][k], ref.addc[t][k]));
+      }
+    for (int k = 0; k < kNumPmc; ++k) {
+      worst = std::max(worst, rel(out->hw_sum[k], ref.hw_sum[k]));
+      worst = std::max(worst, rel(out->unatt[k], ref.unatt[k]));
+    }
+  }
+  if (max_rel) *max_rel = worst;
+  hipHostFree(in);
+  hipHostFree(out);
+  hipFree(d_st);
+  return rc;
 }
 
 int gpbs_gpu_hwc_reset(void* p) {
@@ -1517,6 +1597,14 @@ int gpbs_gpu_force_hold(void* p, int v) {
   if (!c) return -22;
   std::lock_guard<std::mutex> g(c->hold_mu);
   set_hold(c, v ? 1u : 0u);
+  return 0;
+}
+
+// Latency lane (see GpuCtx::lat_half): -1 off, 0 / 1 the class half.
+int gpbs_gpu_set_lat_half(void* p, int half) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c || half < -1 || half > 1) return -22;
+  __atomic_store_n(&c->lat_half, half, __ATOMIC_RELEASE);
   return 0;
 }
 
@@ -1616,6 +1704,17 @@ int gpbs_gpu_ownership(void* p, int t, int64_t* out2, int clear) {
     for (int x = 0; x < kXcds; ++x) out2[k] += ct[x * kCtx + k] - c->own_base[t][x * kCtx + k];
   }
   if (clear) std::memcpy(c->own_base[t], ct, sizeof(c->own_base[t]));
+  return 0;
+}
+
+// Device adapt: calls, results not back within the poll budget (host
+// fallback that period), calls that found the previous launch still running.
+int gpbs_gpu_adapt_stats(void* p, uint64_t* calls, uint64_t* late, uint64_t* busy) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c) return -22;
+  if (calls) *calls = c->adapt_calls;
+  if (late) *late = c->adapt_late;
+  if (busy) *busy = c->adapt_busy;
   return 0;
 }
 

@@ -197,7 +197,10 @@ POLICY_ENGINES = {
     # flagship + latency hold: the table in host-written VRAM (BAR), and the
     # memory-class tenants pause at their next unit boundary while a latency
     # request is in flight (the wake-BOOST analog for the GEMV tenant)
-    "gpbs-lat": (4, dict(BUDGET_OVERRIDES), True, "bar,se,waveprio,latco,budget,hold"),
+    "gpbs-lat": (4, dict(BUDGET_OVERRIDES), True, "bar,se,waveprio,latco,budget,hold,latmem"),
+    # latency lane only (GEMV CU-masked to the memory half, no hold) / hold only
+    "gpbs-lane": (4, dict(BUDGET_OVERRIDES), True, "device,se,waveprio,latco,budget,latmem"),
+    "gpbs-hold": (4, dict(BUDGET_OVERRIDES), True, "bar,se,waveprio,latco,budget,hold"),
     "gpbs-ts": (4, dict(SE_OVERRIDES), True, "device,se,waveprio,latco"),
     "credit-fixed-ts": (4, dict(SE_OVERRIDES, sched="credit-fixed"), True, "device,se,waveprio,latco"),
     "credit2": (4, dict(SE_OVERRIDES, sched="credit2"), True, "device,se,waveprio,latco"),
@@ -464,7 +467,10 @@ class Corun:
             self.ctx.set_waveprio("waveprio" in opts)
             self.ctx.set_share("share" in opts)
             self.ctx.set_hold("hold" in opts)
-            self.ctx.attach(e, nctx=e._gpbs_nctx)
+            self.ctx.set_lat_half(1 if "latmem" in opts else -1)
+            # device hot path: counter attribution (k_hwc_attribute) and the
+            # PBS update (k_adapt) run on the GPU
+            self.ctx.attach(e, nctx=e._gpbs_nctx, device_adapt=True)
             if self.cfg.hw_counters:
                 self.ctx.set_hwc(True)
             e.start()
@@ -501,6 +507,7 @@ class Corun:
         self.ctx.set_se_mode(False)
         self.ctx.set_share(False)
         self.ctx.set_hold(False)
+        self.ctx.set_lat_half(-1)
         self.ctx.set_waveprio(False)
         if self.cfg.hw_counters:
             self.ctx.set_hwc(False)

@@ -155,12 +155,21 @@ class GpuContext:
         pct = self.L.gpbs_gpu_hwc_clean(self.h, -1, cf)
         slow = C.c_uint64(0)
         self.L.gpbs_gpu_hwc_period(self.h, -1, -1, C.byref(slow))
-        return {"samples": n.value, "slow_samples": slow.value, "mean_sample_us": round(ns.value / 1e3, 1), "max_sample_us": round(mx.value / 1e3, 1),
+        la, bs, ho = C.c_uint64(0), C.c_uint64(0), C.c_uint64(0)
+        dev = self.L.gpbs_gpu_hwc_attr_stats(self.h, C.byref(la), C.byref(bs), C.byref(ho))
+        return {"attr_device": bool(dev), "attr_kernel_launches": la.value, "attr_busy_skips": bs.value,
+                "attr_host": ho.value,
+                "samples": n.value, "slow_samples": slow.value, "mean_sample_us": round(ns.value / 1e3, 1), "max_sample_us": round(mx.value / 1e3, 1),
                 "hw_over_model": [round(x, 4) for x in r],
                 "unattributed_frac": [round(x, 4) for x in u],
                 "attribution": "exact-se" if sem.value & 1 else "xcd-time-share",
                 # exclusive-ownership windows: share of the counts that reached the PBS metric
                 "clean_pct": pct, "metric_frac": [round(x, 4) for x in cf]}
+
+    def set_hwc_device(self, on: bool) -> bool:
+        """Attribute counter snapshots on the GPU (k_hwc_attribute, default)
+        or on the host (the reference implementation); returns the old setting."""
+        return bool(self.L.gpbs_gpu_set_hwc_device(self.h, 1 if on else 0))
 
     def set_hwc_period(self, fast_us: int = -1, slow_us: int = -1):
         """Counter sampler cadence: every fast_us while the partition table is
@@ -222,6 +231,13 @@ class GpuContext:
         if rc:
             raise RuntimeError("set_waveprio failed")
 
+    def set_lat_half(self, half: int):
+        """Latency lane: ungated latency-class runners launch on a stream
+        CU-masked to class half `half` (0: SEs {0,1}, 1: SEs {2,3}; -1: off)."""
+        rc = self.L.gpbs_gpu_set_lat_half(self.h, int(half))
+        if rc:
+            raise RuntimeError("set_lat_half failed")
+
     def set_spatial(self, on: bool):
         """Spatial partitions: the two partitions of an XCD are CU halves
         (shader engines 0-1 / 2-3) -- runners launch on half-masked streams
@@ -250,7 +266,10 @@ class GpuContext:
     def stats(self):
         out = (C.c_uint64 * 4)()
         self.L.gpbs_gpu_stats(self.h, out)
-        return {"switches": out[0], "flushes": out[1], "metric_calls": out[2], "metric_ns": out[3]}
+        ca, la, bu = C.c_uint64(0), C.c_uint64(0), C.c_uint64(0)
+        self.L.gpbs_gpu_adapt_stats(self.h, C.byref(ca), C.byref(la), C.byref(bu))
+        return {"switches": out[0], "flushes": out[1], "metric_calls": out[2], "metric_ns": out[3],
+                "adapt_device_calls": ca.value, "adapt_device_late": la.value, "adapt_device_busy": bu.value}
 
     def close(self):
         if getattr(self, "h", None):

@@ -100,6 +100,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ms", type=float, default=80.0)
     ap.add_argument("--out", default="")
+    ap.add_argument("--set", default="4mix", choices=["4mix", "phase"],
+                    help="4mix: the round-2 scans + GEMM/stream/reduce arrangements; phase: arrangements of the "
+                         "phase mix's tenant sets (two GEMMs + a stream, a GEMM + two streams, two tenants)")
     args = ap.parse_args()
     L = K.lib()
     n = 4096
@@ -138,6 +141,44 @@ def main():
 
     def norm(r, kinds):
         return {k: round(v / solo[kinds[k]], 3) for k, v in r.items()}
+
+    if args.set == "phase":
+        G, S = "gemm", "stream"
+        arrs = [
+            # two GEMMs + a stream (phase tenant in its GEMM phase, hbm on)
+            ("2g+s shared", {"g": (G, None, 1), "p": (G, None, 1), "s": (S, None, 1)}),
+            ("g1|p1|s2", {"g": (G, (0,), 1), "p": (G, (1,), 1), "s": (S, (2, 3), 2)}),
+            ("g2|p1|s1", {"g": (G, (0, 1), 1), "p": (G, (2,), 1), "s": (S, (3,), 4)}),
+            ("gp2|s2", {"g": (G, (0, 1), 1), "p": (G, (0, 1), 1), "s": (S, (2, 3), 2)}),
+            ("gp3|s1", {"g": (G, (0, 1, 2), 1), "p": (G, (0, 1, 2), 1), "s": (S, (3,), 4)}),
+            ("gp-all|s2", {"g": (G, None, 1), "p": (G, None, 1), "s": (S, (2, 3), 2)}),
+            ("gp-all|s1", {"g": (G, None, 1), "p": (G, None, 1), "s": (S, (3,), 4)}),
+            ("g2|p2|s-all", {"g": (G, (0, 1), 1), "p": (G, (2, 3), 1), "s": (S, None, 1)}),
+            # a GEMM + two streams (phase tenant streaming, hbm on)
+            ("g+2s shared", {"g": (G, None, 1), "p": (S, None, 1), "s": (S, None, 1)}),
+            ("g2|p1|s1 s", {"g": (G, (0, 1), 1), "p": (S, (2,), 4), "s": (S, (3,), 4)}),
+            ("g2|ps2", {"g": (G, (0, 1), 1), "p": (S, (2, 3), 2), "s": (S, (2, 3), 2)}),
+            ("g-all|ps2", {"g": (G, None, 1), "p": (S, (2, 3), 2), "s": (S, (2, 3), 2)}),
+            # two GEMMs (hbm off)
+            ("2g shared", {"g": (G, None, 1), "p": (G, None, 1)}),
+            ("g2|p2", {"g": (G, (0, 1), 1), "p": (G, (2, 3), 1)}),
+            ("g3|p1", {"g": (G, (0, 1, 2), 1), "p": (G, (3,), 1)}),
+            # a GEMM + a stream (hbm off, phase streaming)
+            ("g+s shared", {"g": (G, None, 1), "p": (S, None, 1)}),
+            ("g2|p2 s", {"g": (G, (0, 1), 1), "p": (S, (2, 3), 2)}),
+            ("g3|p1 s", {"g": (G, (0, 1, 2), 1), "p": (S, (3,), 4)}),
+            ("g-all|p2 s", {"g": (G, None, 1), "p": (S, (2, 3), 2)}),
+        ]
+        for name, spec in arrs:
+            r, win = run(loops_for(spec))
+            kinds = {k: v[0] for k, v in spec.items()}
+            nr = norm(r, kinds)
+            emit({"arrangement": name, "window_ms": round(win, 1), **nr, "sum": round(sum(nr.values()), 3)})
+        if args.out:
+            with open(args.out, "w") as f:
+                for rec in out:
+                    f.write(json.dumps(rec) + "\n")
+        return
 
     # --- single tenants on k SEs per XCD, w workgroups per CU
     for kind, wlist in (("stream", (1, 2, 4, 8)), ("reduce", (1, 2, 4)), ("gemm", (1,))):

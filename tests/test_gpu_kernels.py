@@ -116,6 +116,19 @@ def test_counter_reduce_kernel():
     assert torch.equal(prev[ids.long()], cnt[ids.long()])
 
 
+def test_hwc_attribute_kernel_matches_host_reference():
+    """k_hwc_attribute (one workgroup: per-partition ownership reductions,
+    per-tenant attribution) against the host implementation of the same
+    algorithm (csrc/hip/hwc_attr.h) on 40 random snapshot pairs: owned,
+    time-shared and idle partitions, SE and co-resident modes, clean windows
+    on and off, class-share intervals."""
+    L = K.lib()
+    worst = C.c_double(1.0)
+    rc = L.gpbs_hip_hwc_attr_selftest(7, 40, C.byref(worst))
+    assert rc == 0, rc
+    assert worst.value < 1e-12, worst.value
+
+
 def test_device_adapt_bit_exact_vs_host():
     """The batched HIP adapt kernel equals the host engine's adapt_update."""
     lib = N.load_core()
