@@ -63,6 +63,9 @@ def main():
                     help="N > 1: the all-reduce tenant gets aligned gang windows only while its K10 wait reports "
                          "(peer-arrival skew of its RCCL all-reduces) say its peers lag")
     ap.add_argument("--table", default="host", choices=["host", "device"])
+    ap.add_argument("--coll", default="ipc", choices=["ipc", "rccl"],
+                    help="N > 1 all-reduce tenant: ipc (gated gpbs kernel over IPC-mapped peer buffers, xGMI; "
+                         "default) or rccl (torch.distributed all-reduce, not CU-confined)")
     ap.add_argument("--out", default="")
     ap.add_argument("--rehearse", action="store_true",
                     help="multi-rank control-flow rehearsal on ONE GPU: every rank on cuda:0, gloo for the default "
@@ -152,7 +155,8 @@ def main():
                           table_mode=args.table, mix=mix, hw_counters=(counters == "hw"),
                           protocol=args.protocol, step_ms=args.step_ms, gang_transport=args.gang_transport,
                           gang_shm_base=f"{gang_base}-{mix}" if gang_base else "",
-                          gang_wait_driven=args.gang_wait_driven, fresh_engine=not args.keep_engines)
+                          gang_wait_driven=args.gang_wait_driven, fresh_engine=not args.keep_engines,
+                          coll_impl=args.coll)
         if args.rehearse:
             cfg.coll_bytes = 4 << 20  # CPU gloo all-reduce stand-in
         c = Corun(cfg, rank=rank, world=world, device=local, groups=groups, log=log, coll_on_cpu=args.rehearse)

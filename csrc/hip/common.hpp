@@ -196,4 +196,55 @@ __device__ __forceinline__ void count(u64* cnt, u32 me, u32 xcc, u64 inst, u64 c
   if (miss) atomicAdd(c + 3, miss);
 }
 
+// Work-queue unit grab of a persistent tenant workgroup (thread 0 decides,
+// workgroup-uniform): while its tenant owns the partition this workgroup runs
+// on, the next unit index; -1 when the queue is drained or the partition was
+// revoked (GATE_PARK: sleep there, bounded, and resume if handed back).
+__device__ __forceinline__ int grab_unit(WorkQueue* q, const PartTable* table, u32 mode, u32 me, u32 xcc,
+                                         int* s_slot, u32 total) {
+  if (threadIdx.x == 0) {
+    int u = -1;
+    hold_wait(table, mode);
+    for (u32 spins = 0;; ++spins) {
+      if (owns(table, mode, me, xcc)) {
+        const u32 t = atomicAdd(&q->next, 1u);
+        u = t < total ? (int)t : -1;
+        break;
+      }
+      // GATE_PARK: stay resident (sleeping) on a revoked XCD so the workgroup
+      // resumes within ~20 us when the scheduler hands the XCD back, instead
+      // of waiting for the next launch.  Bounded (~2 ms): a workgroup that is
+      // not rescheduled leaves and the runner relaunches the rest of the unit.
+      if ((mode & 3) != GATE_PARK || spins >= kParkSpins ||
+          __hip_atomic_load(&q->next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= total) {
+        atomicAdd(&q->stopped, 1u);
+        break;
+      }
+#pragma unroll
+      for (int k = 0; k < 6; ++k) __builtin_amdgcn_s_sleep(127);
+    }
+    *s_slot = u;
+  }
+  __syncthreads();
+  int u = *s_slot;
+  __syncthreads();
+  return u;
+}
+
+// XCD-range variant: units are split into 8 contiguous ranges and a
+// workgroup first drains the range of the XCD it runs on, then steals from
+// the others in ring order.  Neighbouring tiles (which share operand panels)
+// thus meet in one XCD's private L2 -- the XCD-aware blockIdx remap of a plain
+// grid, done on a work queue so gating, parking and relaunch still hold.
+
+// Per-unit counter accounting (modeled per-tile counters) + done count.
+__device__ __forceinline__ void count_unit(u64* cnt, u32 me, u32 xcc, u64 inst, u64* t_last, u64 refs, u64 miss,
+                                           WorkQueue* q) {
+  if (threadIdx.x != 0) return;
+  const u64 t = __builtin_amdgcn_s_memtime();
+  count(cnt, me, xcc, inst, t - *t_last, refs, miss);
+  *t_last = t;
+  atomicAdd(&q->done, 1u);
+}
+
 }  // namespace gpbs_hip

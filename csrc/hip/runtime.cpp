@@ -56,6 +56,9 @@ int gpbs_hip_counter_reduce(void*, void*, const int*, int, void*, hipStream_t);
 int gpbs_hip_adapt(void*, const void*, const void*, const void*, int, const gpbs_adapt_params_t*, int*, hipStream_t);
 int gpbs_hip_switch_probe(const void*, int, unsigned*, int, unsigned, unsigned long long, hipStream_t);
 int gpbs_hip_hwc_attribute(const void*, void*, void*, hipStream_t);
+int gpbs_hip_allreduce(const void*, unsigned, unsigned long long, unsigned, void*, const void*, unsigned, unsigned,
+                       void*, void*, int, unsigned long long, hipStream_t);
+int gpbs_hip_coll_desc_size(void);
 }
 
 namespace {
@@ -750,7 +753,31 @@ int ctr_adapt_batch(void* user, int n, const int*, const uint64_t* deltas, const
 
 // --------------------------------------------------------------------- runner
 
-enum Kind { K_GEMM = 1, K_STREAM = 2, K_REDUCE = 3, K_GEMV = 4 };
+enum Kind { K_GEMM = 1, K_STREAM = 2, K_REDUCE = 3, K_GEMV = 4, K_ALLREDUCE = 5 };
+
+// ---- all-reduce tenant over IPC-mapped peer buffers (coll_kernels.hip) ----
+// Host mirror of the device CollDesc: per rank its input, output and flag
+// words as mapped into this process (own buffers for our rank, IPC-opened
+// peers for the others).
+constexpr int kCollMax = 8;
+struct CollDescHost {
+  const void* in[kCollMax];
+  void* out[kCollMax];
+  u32* flags[kCollMax];
+  u32 rank, world;
+  u64 n8;
+};
+
+struct Coll {
+  int device = 0, rank = 0, world = 1;
+  size_t bytes = 0;
+  void* in = nullptr;
+  void* out = nullptr;
+  u32* flags = nullptr;
+  void* peer[3][kCollMax] = {};  // opened IPC mappings: in, out, flags
+  CollDescHost desc{};
+  void* d_desc = nullptr;
+};
 
 }  // namespace
 
@@ -856,6 +883,10 @@ struct Runner {
   std::atomic<int> phase{0};
   uint8_t q_alt[16] = {};
   int cur_alt = 0;  // workload of the unit being launched
+  // all-reduce tenant: collective sequence number of the unit in each queue
+  // slot (fresh units take the next one; a relaunch keeps its own)
+  u32 q_seq[16] = {};
+  u32 coll_seq = 0;
 
   struct Work {
     int kind, M, N, K, chunk;
@@ -871,6 +902,11 @@ struct Runner {
 
   static u32 unit_total(const Work& w) {
     switch (w.kind) {
+      case K_ALLREDUCE: {  // chunks of this rank's slice (M = world, N = rank)
+        const u64 n8 = w.bytes / 16, chunk8 = (u64)w.chunk / 16, per = (n8 + w.M - 1) / w.M;
+        const u64 lo = (u64)w.N * per, hi = std::min(lo + per, n8);
+        return hi > lo ? (u32)((hi - lo + chunk8 - 1) / chunk8) : 0u;
+      }
       case K_GEMM: return (u32)gpbs_hip_gemm_units(w.M, w.N);
       case K_STREAM:
       case K_REDUCE: return (u32)((w.bytes + w.chunk - 1) / w.chunk);
@@ -979,6 +1015,9 @@ struct Runner {
       case K_GEMV:
         return gpbs_hip_gemv_bf16(w.a, w.b, w.c, w.M, w.K, q, tab, mode, me, ctx->d_cnt, &h_status[qi], grid,
                                   stream);
+      case K_ALLREDUCE:  // K = barrier timeout (ms) -> 100 MHz wall-clock ticks
+        return gpbs_hip_allreduce(w.a, q_seq[qi], w.bytes, (unsigned)w.chunk, q, tab, mode, me, ctx->d_cnt,
+                                  &h_status[qi], grid, (unsigned long long)(w.K > 0 ? w.K : 5000) * 100000ull, stream);
     }
     return -22;
   }
@@ -1049,7 +1088,10 @@ struct Runner {
           }
           wait_owner();
           if (stop) break;
-          if (fresh) q_alt[qi] = (uint8_t)(cfg.alt_kind && phase.load(std::memory_order_acquire));
+          if (fresh) {
+            q_alt[qi] = (uint8_t)(cfg.alt_kind && phase.load(std::memory_order_acquire));
+            q_seq[qi] = coll_seq++;
+          }
           cur_alt = q_alt[qi];
           hipStream_t stream = pick_stream();
           if (fresh) {
@@ -1082,8 +1124,20 @@ struct Runner {
           std::this_thread::yield();
         }
         const u32 s = __atomic_load_n(&h_status[f.qi], __ATOMIC_ACQUIRE);
-        const u32 done = s & 0x7fffffffu;
-        if ((s & 0x80000000u) && done >= unit_total(work(q_alt[f.qi]))) {
+        const u32 done = s & 0x3fffffffu;
+        if ((s & 0x80000000u) && (s & 0x40000000u)) {
+          // all-reduce tenant: a peer barrier timed out (a peer is gone or
+          // stalled for seconds) -- fail the runner instead of retrying
+          std::fprintf(stderr, "[gpbs-hip] tenant %d: collective unit %u timed out waiting for its peers\n",
+                       cfg.tenant, q_seq[f.qi]);
+          err = -110;
+          hold_drop(f.qi);
+          std::lock_guard<std::mutex> g(mu);
+          q_busy[f.qi] = 0;
+          inflight--;
+          pending = 0;
+          if (!submit_times.empty()) submit_times.pop_front();
+        } else if ((s & 0x80000000u) && done >= unit_total(work(q_alt[f.qi]))) {
           hold_drop(f.qi);
           const int64_t t = mono_ns();
           std::lock_guard<std::mutex> g(mu);
@@ -1825,6 +1879,10 @@ void* gpbs_runner_create(void* ctx, const gpbs_runner_cfg_t* cfg) {
   if ((cfg->kind == K_STREAM || cfg->kind == K_REDUCE) && (cfg->bytes % 16 || cfg->chunk_bytes <= 0 || cfg->chunk_bytes % 16))
     return nullptr;
   if (cfg->kind == K_GEMV && cfg->K % 512) return nullptr;
+  if (cfg->kind == K_ALLREDUCE &&
+      (!cfg->a || cfg->M < 1 || cfg->M > kCollMax || cfg->N < 0 || cfg->N >= cfg->M || cfg->bytes % (16ull * cfg->M) ||
+       cfg->chunk_bytes <= 0 || cfg->chunk_bytes % 16))
+    return nullptr;
   if (cfg->alt_kind == K_GEMM && (cfg->alt_M % 128 || cfg->alt_N % 128 || cfg->alt_K % 64)) return nullptr;
   if ((cfg->alt_kind == K_STREAM || cfg->alt_kind == K_REDUCE) &&
       (cfg->alt_bytes % 16 || cfg->alt_chunk_bytes <= 0 || cfg->alt_chunk_bytes % 16))
@@ -1971,6 +2029,121 @@ void gpbs_runner_destroy(void* p) {
   hipFree(r->d_q);
   hipHostFree(r->h_status);
   delete r;
+}
+
+// ---- all-reduce tenant buffers: one Coll per rank, peers over IPC ----------
+void* gpbs_coll_create(int device, int rank, int world, unsigned long long bytes) {
+  if (world < 1 || world > kCollMax || rank < 0 || rank >= world || bytes == 0 || bytes % (16ull * world)) return nullptr;
+  if ((int)sizeof(CollDescHost) != gpbs_hip_coll_desc_size()) return nullptr;  // host / device layouts agree
+  if (hipSetDevice(device) != hipSuccess) return nullptr;
+  auto* c = new Coll;
+  c->device = device;
+  c->rank = rank;
+  c->world = world;
+  c->bytes = bytes;
+  bool ok = hipMalloc(&c->in, bytes) == hipSuccess && hipMalloc(&c->out, bytes) == hipSuccess &&
+            hipMalloc((void**)&c->flags, 4096) == hipSuccess && hipMemset(c->flags, 0, 4096) == hipSuccess &&
+            hipMemset(c->out, 0, bytes) == hipSuccess && hipMalloc(&c->d_desc, sizeof(CollDescHost)) == hipSuccess;
+  if (!ok) {
+    if (c->in) hipFree(c->in);
+    if (c->out) hipFree(c->out);
+    if (c->flags) hipFree(c->flags);
+    delete c;
+    return nullptr;
+  }
+  c->desc.rank = (u32)rank;
+  c->desc.world = (u32)world;
+  c->desc.n8 = bytes / 16;
+  c->desc.in[rank] = c->in;
+  c->desc.out[rank] = c->out;
+  c->desc.flags[rank] = c->flags;
+  return c;
+}
+
+// The three IPC handles (input, output, flags) of this rank's buffers, 3 x
+// sizeof(hipIpcMemHandle_t) bytes into out.  Returns the byte count.
+int gpbs_coll_export(void* p, void* out) {
+  Coll* c = (Coll*)p;
+  if (!c || !out) return -22;
+  hipSetDevice(c->device);
+  hipIpcMemHandle_t h[3];
+  if (hipIpcGetMemHandle(&h[0], c->in) != hipSuccess || hipIpcGetMemHandle(&h[1], c->out) != hipSuccess ||
+      hipIpcGetMemHandle(&h[2], c->flags) != hipSuccess)
+    return -5;
+  std::memcpy(out, h, sizeof(h));
+  return (int)sizeof(h);
+}
+
+int gpbs_coll_handle_bytes(void) { return (int)(3 * sizeof(hipIpcMemHandle_t)); }
+
+// Map peer `peer`'s buffers from its exported handles.
+int gpbs_coll_open(void* p, int peer, const void* handles) {
+  Coll* c = (Coll*)p;
+  if (!c || !handles || peer < 0 || peer >= c->world || peer == c->rank) return -22;
+  hipSetDevice(c->device);
+  hipIpcMemHandle_t h[3];
+  std::memcpy(h, handles, sizeof(h));
+  for (int k = 0; k < 3; ++k) {
+    if (c->peer[k][peer]) continue;
+    if (hipIpcOpenMemHandle(&c->peer[k][peer], h[k], hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+      c->peer[k][peer] = nullptr;
+      return -5;
+    }
+  }
+  c->desc.in[peer] = c->peer[0][peer];
+  c->desc.out[peer] = c->peer[1][peer];
+  c->desc.flags[peer] = (u32*)c->peer[2][peer];
+  return 0;
+}
+
+// Every peer mapped: upload the descriptor the kernel reads.
+int gpbs_coll_finalize(void* p) {
+  Coll* c = (Coll*)p;
+  if (!c) return -22;
+  for (int r = 0; r < c->world; ++r)
+    if (!c->desc.in[r] || !c->desc.out[r] || !c->desc.flags[r]) return -19;
+  hipSetDevice(c->device);
+  return hipMemcpy(c->d_desc, &c->desc, sizeof(c->desc), hipMemcpyHostToDevice) == hipSuccess ? 0 : -5;
+}
+
+// 0: input, 1: output, 2: flag words (this rank's device pointers); 3: the device descriptor.
+void* gpbs_coll_buffer(void* p, int which) {
+  Coll* c = (Coll*)p;
+  if (!c) return nullptr;
+  switch (which) {
+    case 0: return c->in;
+    case 1: return c->out;
+    case 2: return c->flags;
+    case 3: return c->d_desc;
+  }
+  return nullptr;
+}
+
+// Copy between a device buffer of the caller (a torch tensor) and this
+// rank's input (0) / output (1) buffer; to_coll: 1 caller -> coll.
+int gpbs_coll_copy(void* p, int which, void* dptr, unsigned long long bytes, int to_coll) {
+  Coll* c = (Coll*)p;
+  if (!c || !dptr || (which != 0 && which != 1) || bytes > c->bytes) return -22;
+  hipSetDevice(c->device);
+  void* buf = which ? c->out : c->in;
+  const hipError_t e = to_coll ? hipMemcpy(buf, dptr, bytes, hipMemcpyDeviceToDevice)
+                               : hipMemcpy(dptr, buf, bytes, hipMemcpyDeviceToDevice);
+  return e == hipSuccess ? 0 : -5;
+}
+
+void gpbs_coll_destroy(void* p) {
+  Coll* c = (Coll*)p;
+  if (!c) return;
+  hipSetDevice(c->device);
+  hipDeviceSynchronize();
+  for (int k = 0; k < 3; ++k)
+    for (int r = 0; r < kCollMax; ++r)
+      if (c->peer[k][r]) hipIpcCloseMemHandle(c->peer[k][r]);
+  hipFree(c->in);
+  hipFree(c->out);
+  hipFree(c->flags);
+  hipFree(c->d_desc);
+  delete c;
 }
 
 }  // extern "C"

@@ -141,6 +141,8 @@ class CorunConfig:
     gang_shm_base: str = ""      # region name prefix agreed by all ranks (a nonce broadcast by rank 0)
     gang_deadline_ms: float = 200.0
     gang_wait_driven: bool = False  # gang windows only while the coll tenant's K10 waits say its peers lag
+    coll_impl: str = "ipc"       # N > 1 all-reduce tenant: "ipc" (gated gpbs kernel over IPC-mapped peer
+                                 # buffers, csrc/hip/coll_kernels.hip) or "rccl" (torch.distributed, ungated)
     mix: str = "4mix"
     hw_counters: bool = False    # PBS metric from live hardware counters
     # "steady": every throughput tenant is kept backlogged for the whole timed
@@ -355,6 +357,7 @@ class Corun:
         if not self.tid:  # ids without an engine: fixed order (Domain-0 = 0)
             self.tid = {n: i + 1 for i, (n, _) in enumerate(self.tenants)}
         self.runners: Dict[str, object] = {}
+        self.coll_buf = None
         for name, _ in self.tenants:
             self.runners[name] = self._make_runner(name)
         self.quota: Dict[str, int] = {}
@@ -381,6 +384,11 @@ class Corun:
         if kind == "stream":
             return Runner(self.ctx, "stream", t, depth=cfg.depth, **spec, **mem_chunk)
         if kind == "reduce":
+            if self.world > 1 and cfg.coll_impl == "ipc" and not self.coll_on_cpu:
+                r = self._ipc_runner(t, mem_chunk)
+                if r is not None:
+                    return r
+                self.log("[corun] IPC all-reduce tenant failed its self-test on this node: using RCCL")
             if self.world > 1:
                 return CollTenant(self.ctx, t, cfg.coll_bytes, self.groups.get("coll"), on_cpu=self.coll_on_cpu,
                                   board_name=f"{cfg.gang_shm_base}-arr" if cfg.gang_shm_base else "",
@@ -389,6 +397,45 @@ class Corun:
         if kind == "gemv":
             return Runner(self.ctx, "gemv", t, depth=1, priority=1, M=cfg.idle_rows, K=cfg.idle_rows)
         raise ValueError(name)
+
+    def _ipc_runner(self, t: int, mem_chunk: dict):
+        """The gated IPC all-reduce tenant, after a one-unit self-test on
+        every rank: inputs rank + 1, every output element must be the sum
+        over ranks (exact in bf16); any rank failing makes all fall back."""
+        from ..parallel.ipc_coll import IpcColl
+        ok, r = 1.0, None
+        try:
+            self.coll_buf = IpcColl(self.device, self.rank, self.world, self.cfg.coll_bytes,
+                                    group=self.groups.get("ctrl"))
+            n = self.coll_buf.nbytes // 2
+            self.coll_buf.fill(torch.full((n,), float(self.rank + 1), dtype=torch.bfloat16, device="cuda"))
+            r = Runner(self.ctx, "allreduce", t, depth=self.cfg.depth, gate=False, engine_wake=False,
+                       coll=self.coll_buf, timeout_ms=10000, **mem_chunk)
+            self._barrier()
+            r.submit(1)
+            r.wait(60.0)
+            torch.cuda.synchronize()
+        except Exception as ex:  # noqa: BLE001 -- any failure: agree on the fallback
+            self.log(f"[corun] IPC all-reduce: {ex}")
+            ok = 0.0
+        ok = -self._allreduce(-ok, "max")  # min over ranks
+        if ok > 0:
+            self._barrier()
+            want = float(self.world * (self.world + 1) // 2)
+            good = bool((self.coll_buf.read(1) == want).all().item())
+            ok = -self._allreduce(-float(good), "max")
+        if ok <= 0:
+            if r is not None:
+                r.close()
+            if self.coll_buf is not None:
+                self.coll_buf.close()
+                self.coll_buf = None
+            return None
+        g = torch.Generator(device="cuda").manual_seed(4321 + self.rank)
+        self.coll_buf.fill(torch.randn(self.coll_buf.nbytes // 2, dtype=torch.bfloat16, device="cuda", generator=g))
+        r.set_engine_wake(True)
+        r.set_gate(True)
+        return r
 
     def _make_engine(self, pol: str) -> Engine:
         nctx, over, _, table = POLICY_ENGINES[pol]
@@ -483,6 +530,7 @@ class Corun:
                 r.set_engine_wake(not latco)
             if isinstance(coll, CollTenant):
                 coll.gate, coll.engine = True, e
+            if self.world > 1 and coll is not None:
                 # Cross-GPU gang windows for the all-reduce tenant: its RCCL
                 # ranks on all GPUs get their partitions in the same epochs.
                 from ..parallel.gang import GangCoordinator
@@ -572,6 +620,21 @@ class Corun:
         else:
             r.run_units(n)
 
+    def _collective(self, r) -> bool:
+        return isinstance(r, Runner) and r.kind == "allreduce"
+
+    def _drain(self, name: str):
+        """Drop a native runner's backlog and let its in-flight units finish;
+        the IPC all-reduce tenant stops on a unit count agreed over the ranks
+        (its units are collective)."""
+        r = self.runners[name]
+        if self._collective(r):
+            from ..parallel.ipc_coll import agreed_drain
+            agreed_drain(r, lambda n: int(self._allreduce(float(n), "max")))
+        else:
+            r.cancel()
+            r.wait(120.0)
+
     def _estimate_unit_ms(self, name: str) -> float:
         """Rough solo ms per unit (sizes the backlog; not a measurement)."""
         r = self.runners[name]
@@ -618,8 +681,7 @@ class Corun:
         dt_ms = (time.perf_counter() - t0) * 1e3
         rate = (done() - d0) / dt_ms
         if isinstance(r, Runner):
-            r.cancel()
-            r.wait(120.0)
+            self._drain(name)
         else:
             r.stop_loop(agree=lambda n: int(self._allreduce(float(n), "max")))
         if alt:
@@ -839,14 +901,17 @@ class Corun:
         # drain: drop the backlog, let in-flight units finish
         for name in self.throughput:
             r = self.runners[name]
-            if isinstance(r, Runner):
+            if isinstance(r, Runner) and not self._collective(r):
                 r.cancel()
         if isinstance(coll, CollTenant):
             coll.stop_loop(agree=lambda n: int(self._allreduce(float(n), "max")))
         for name in self.throughput:
             r = self.runners[name]
             if isinstance(r, Runner):
-                r.wait(120.0)
+                if self._collective(r):
+                    self._drain(name)
+                else:
+                    r.wait(120.0)
         flips = self._dyn_state.get("flips", 0)
         self._dyn_reset()
         lats = [x / 1e6 for x in self.runners["idle"].latencies(clear=True)] if "idle" in self.runners else []
@@ -989,6 +1054,9 @@ class Corun:
             self.active_engine.stop()
         for r in self._natives():
             r.close()
+        if self.coll_buf is not None:
+            self.coll_buf.close()
+            self.coll_buf = None
         coll = self.runners.get("coll")
         if isinstance(coll, CollTenant):
             coll.close()

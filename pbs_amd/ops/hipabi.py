@@ -23,7 +23,7 @@ class RunnerStats(C.Structure):
                                    "lat_max_ns")] + [("lat_count", u64), ("units_alt", u64)]
 
 
-KIND = {"gemm": 1, "stream": 2, "reduce": 3, "gemv": 4}
+KIND = {"gemm": 1, "stream": 2, "reduce": 3, "gemv": 4, "allreduce": 5}
 
 
 def _p(lib, name, res, *args):
@@ -123,4 +123,12 @@ def bind(lib):
     _p(lib, "gpbs_runner_set_engine_wake", C.c_int, vp, C.c_int)
     _p(lib, "gpbs_runner_stream", vp, vp)
     _p(lib, "gpbs_runner_set_phase", C.c_int, vp, C.c_int)
+    _p(lib, "gpbs_coll_create", vp, C.c_int, C.c_int, C.c_int, C.c_ulonglong)
+    _p(lib, "gpbs_coll_export", C.c_int, vp, vp)
+    _p(lib, "gpbs_coll_handle_bytes", C.c_int)
+    _p(lib, "gpbs_coll_open", C.c_int, vp, C.c_int, vp)
+    _p(lib, "gpbs_coll_finalize", C.c_int, vp)
+    _p(lib, "gpbs_coll_buffer", vp, vp, C.c_int)
+    _p(lib, "gpbs_coll_destroy", None, vp)
+    _p(lib, "gpbs_coll_copy", C.c_int, vp, C.c_int, vp, C.c_ulonglong, C.c_int)
     _p(lib, "gpbs_runner_destroy", None, vp)

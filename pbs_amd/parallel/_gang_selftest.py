@@ -86,6 +86,45 @@ def atc_worker(rank: int, world: int, port: int, q, seconds: float = 0.8, epoch_
     dist.destroy_process_group()
 
 
+def metrics_sum_worker(rank: int, world: int, port: int, q, transport: str = "dist", shm_name: str = "",
+                       epoch_ms: float = 4.0):
+    """C11 exactness: each rank's engine (simulated clock, frozen after one
+    metric period) holds fixed per-tenant counter deltas; after a few gang
+    epochs every rank's node_metrics must be exactly the SUM of every rank's
+    deltas for each metric tenant."""
+    import torch.distributed as dist
+
+    from pbs_amd.core.engine import Engine
+    from pbs_amd.parallel.gang import GangCoordinator
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    e = Engine(sim_clock=True, partitions=[(rank, x) for x in range(2)], quantum_align_us=0)
+    e.tenant_create("Domain-0", nslots=1)
+    ts = [e.tenant_create(n, nslots=2) for n in ("a", "b")]
+    for t in ts:
+        e.wake(t)
+    e.advance(e.now() + 100_000)
+    for i, t in enumerate(ts):  # rank- and tenant-specific counts, charged to slot 0
+        e.set_pmc(e.slot_id(t, 0), [(rank + 1) * 1_000_003 * (i + 1), (rank + 7) * 999 * (i + 2),
+                                    (rank + 3) * 77 * (i + 1), (rank + 2) * 13 * (i + 3)])
+    for _ in range(100):  # up to the first metric tick after the counts: the deltas land in tenant_info().pmc
+        e.advance(e.now() + 50_000)
+        if all(e.tenant_info(t).pmc[0] for t in ts):
+            break
+    local = {t: list(e.tenant_info(t).pmc) for t in ts}
+    g = GangCoordinator(e, None, [], epoch_ms=epoch_ms, share=0.0, metric_tenants=ts, metric_every=1,
+                        transport=transport, rank=rank, world=world, shm_name=shm_name).start()
+    t_end = time.monotonic() + 5.0
+    while g.metric_syncs < 3 and time.monotonic() < t_end:
+        time.sleep(0.005)
+    node = {t: dict(g.node_metrics.get(t, {})) for t in ts}
+    g.stop()
+    q.put({"rank": rank, "local": local, "node": node, "syncs": g.metric_syncs,
+           "still": {t: list(e.tenant_info(t).pmc) for t in ts}})
+    dist.destroy_process_group()
+
+
 def hang_worker(rank: int, world: int, port: int, q, transport: str, shm_name: str, hang_rank: int,
                 hang_ms: int = 1500, deadline_ms: float = 200.0, reform: bool = False):
     """One rank of the gang-deadline test: `hang_rank` stalls `hang_ms` before

@@ -362,6 +362,14 @@ class Runner:
             b = torch.randn(n, device=dev, dtype=torch.bfloat16, generator=g) if kind == "reduce" else None
             c = torch.empty(n, device=dev, dtype=torch.bfloat16)
             work, unit = float(nbytes * (2 if kind == "stream" else 3)), "B"  # bytes moved
+        elif kind == "allreduce":  # IPC all-reduce tenant: buffers live in the IpcColl
+            coll = shape["coll"]
+            nbytes, chunk = coll.nbytes, int(shape.get("chunk_bytes", 1 << 19))
+            M, Nn, K = coll.world, coll.rank, int(shape.get("timeout_ms", 5000))
+            # bytes moved per unit by this rank: world reads + world writes of its slice
+            work, unit = float(2 * nbytes), "B"
+            return {"kind": hipabi.KIND[kind], "M": M, "N": Nn, "K": K, "chunk": chunk, "bytes": nbytes,
+                    "a": coll.desc, "b": None, "c": None, "work": work, "unit": unit}
         elif kind == "gemv":
             M, K = shape.get("M", 8192), shape.get("K", 8192)
             a = torch.randn(M, K, device=dev, dtype=torch.bfloat16, generator=g)

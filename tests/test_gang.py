@@ -2,8 +2,11 @@
 agree on every epoch's decision, and the gang tenant occupies its partitions
 in favoured epochs and none of them in excluded ones."""
 import multiprocessing as mp
+import os
 import socket
 import statistics
+
+import pytest
 
 from pbs_amd.parallel._gang_selftest import worker
 from pbs_amd.parallel.gang import EXCLUDE, FAVOUR, GangCoordinator
@@ -87,6 +90,38 @@ def test_two_ranks_share_atc_minimum_and_node_metrics():
         assert out[r]["stats"]["metric_syncs"] > 0
     # node metrics agree on both ranks and include both ranks' instructions
     assert out[0]["node"] and out[0]["node"]["inst"] > 0
+
+
+@pytest.mark.parametrize("transport", ["dist", "shm"])
+def test_node_metrics_are_exactly_the_sum_of_per_rank_counters(transport):
+    """C11: the gang epochs' SUM-reduced per-tenant counters equal, exactly,
+    the sum of every rank's last-period deltas (frozen engines, 3 ranks)."""
+    from pbs_amd.parallel._gang_selftest import metrics_sum_worker
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    world = 3
+    shm = f"gpbs-test-msum-{os.getpid()}-{port}" if transport == "shm" else ""
+    ps = [ctx.Process(target=metrics_sum_worker, args=(r, world, port, q, transport, shm)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = {}
+    for _ in ps:
+        r = q.get(timeout=120)
+        out[r["rank"]] = r
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    tenants = list(out[0]["local"].keys())
+    for t in tenants:
+        want = [sum(out[r]["local"][t][k] for r in range(world)) for k in range(4)]
+        assert all(out[r]["still"][t] == out[r]["local"][t] for r in range(world))  # deltas frozen
+        assert want[0] > 0
+        for r in range(world):
+            assert out[r]["syncs"] >= 3, out[r]
+            n = out[r]["node"][t]
+            assert [n["inst"], n["cycles"], n["l2_refs"], n["l2_misses"]] == want, (t, r, n, want)
+            assert n["miss_rate"] == want[3] * 100000 // want[0]
 
 
 def test_eight_node_local_ranks_switch_at_the_same_epochs():
