@@ -278,7 +278,11 @@ struct GpuCtx {
   // changing (time-sharing, re-placement) the sampler runs every
   // hwc_period_us, so exclusive-ownership windows stay short; once no owner
   // has changed for 20 ms it backs off to hwc_slow_us.
-  int hwc_slow_us = 4000;  // GPBS_HWC_SLOW_US (0: never back off)
+  // Round 3: with the lean counter set a 1 ms sample costs a GEMM ~0.75 %
+  // (scripts/hwc_cost.py), so the sampler keeps the reference's 1 ms period
+  // (CSCHED_METRIC_TICK_PERIOD, X:xen/common/sched_credit.c:55) and no longer
+  // backs off; GPBS_HWC_SLOW_US=4000 restores the round-2 back-off.
+  int hwc_slow_us = 0;  // GPBS_HWC_SLOW_US (0: never back off)
   std::atomic<uint64_t> hwc_slow_samples{0};
   int64_t hwc_ns = 0, hwc_ns_max = 0;
   uint64_t hwc_samples = 0;

@@ -21,9 +21,20 @@ from .. import _native as N
 
 # PBS slots INST | CYCLES | LLC_REFS | LLC_MISSES on gfx950 (csrc/hip/hwc.cpp):
 # SQ/TCP counters resolve per shader engine, TCC per XCD.
-DEFAULT_SPEC = ("SQ_INSTS_VALU+SQ_INSTS_SALU+SQ_INSTS_VMEM_RD+SQ_INSTS_VMEM_WR+SQ_INSTS_LDS+"
-                "SQ_INSTS_VALU_MFMA_MOPS_BF16|SQ_BUSY_CYCLES|"
-                "TCP_TCC_READ_REQ+TCP_TCC_WRITE_REQ|TCC_MISS")
+# "lean" (default since round 3): 5 SQ + 1 TCP + 1 TCC counters.  A device-
+# counting sample's cost grows with the counter RECORDS it returns (SQ: one per
+# SE, TCP: one per CU, TCC: one per channel) and the memory-path (TCC) ones
+# perturb the tenants most; measured with a backlogged GEMM alone
+# (scripts/hwc_cost.py, profiles/hwc/hwc_cost_r3.jsonl): the round-2 "full"
+# set (7 SQ + 2 TCP + 1 TCC) costs 3.9 % of the GEMM's throughput at a 1 ms
+# period (324 us per sample), a 2 SQ + 1 TCP + 1 TCC set 0.75 % (188 us).
+LEAN_SPEC = ("SQ_INSTS_VALU+SQ_INSTS_VMEM_RD+SQ_INSTS_VMEM_WR+SQ_INSTS_VALU_MFMA_MOPS_BF16|SQ_BUSY_CYCLES|"
+             "TCP_TCC_READ_REQ|TCC_MISS")
+FULL_SPEC = ("SQ_INSTS_VALU+SQ_INSTS_SALU+SQ_INSTS_VMEM_RD+SQ_INSTS_VMEM_WR+SQ_INSTS_LDS+"
+             "SQ_INSTS_VALU_MFMA_MOPS_BF16|SQ_BUSY_CYCLES|"
+             "TCP_TCC_READ_REQ+TCP_TCC_WRITE_REQ|TCC_MISS")
+SPECS = {"lean": LEAN_SPEC, "full": FULL_SPEC}
+DEFAULT_SPEC = LEAN_SPEC
 XCDS = 8
 
 
@@ -33,8 +44,12 @@ def _lib():
 
 def init(spec: Optional[str] = None, gpu: int = -1) -> bool:
     """Register the sampler with rocprofiler-sdk; must precede HIP init.
-    ``gpu`` >= 0 counts on that GPU agent only (one rank per GPU)."""
-    return _lib().gpbs_hwc_init_gpu((spec or DEFAULT_SPEC).encode(), int(gpu)) == 0
+    ``spec``: a counter spec, a name in SPECS, or None (GPBS_HWC_SPEC, else
+    the lean set).  ``gpu`` >= 0 counts on that GPU agent only (one rank per GPU)."""
+    import os
+    spec = spec or os.environ.get("GPBS_HWC_SPEC") or DEFAULT_SPEC
+    spec = SPECS.get(spec, spec)
+    return _lib().gpbs_hwc_init_gpu(spec.encode(), int(gpu)) == 0
 
 
 def start() -> bool:

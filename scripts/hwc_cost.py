@@ -22,12 +22,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 # name -> counter spec (4 '|'-separated PBS slots, '+'-joined counters)
 SPECS = {
-    "default10": "",  # csrc/hip/hwc.cpp kDefaultSpec: 7 SQ + 2 TCP + 1 TCC
+    "full": "full",  # round-2 default: 7 SQ + 2 TCP + 1 TCC
+    "lean": "lean",  # round-3 default: 5 SQ + 1 TCP + 1 TCC
     "sq2_tcp1_tcc1": "SQ_INSTS_VALU+SQ_INSTS_VALU_MFMA_MOPS_BF16|SQ_BUSY_CYCLES|TCP_TCC_READ_REQ|TCC_MISS",
     "sq1_tcc1": "SQ_INSTS_VALU|SQ_WAVES|TCC_REQ|TCC_MISS",
     "tcc2": "TCC_HIT|TCC_REQ|TCC_EA0_RDREQ|TCC_MISS",
     "sq1": "SQ_INSTS_VALU|SQ_WAVES|SQ_INSTS_SALU|SQ_INSTS_LDS",
 }
+DEFAULT_SET = "full,lean,sq2_tcp1_tcc1,sq1_tcc1"
 
 CHILD = r"""
 import json, sys, time
@@ -78,7 +80,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tenant", default="gemm", choices=["gemm", "stream"])
     ap.add_argument("--secs", type=float, default=1.0)
-    ap.add_argument("--specs", default=",".join(SPECS))
+    ap.add_argument("--specs", default=DEFAULT_SET)
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     res = []

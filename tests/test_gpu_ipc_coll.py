@@ -120,7 +120,7 @@ def test_ipc_allreduce_two_processes_exact_and_gated():
         assert o["exact"], o
         assert o["exact_after"], o
         assert o["units"] == 41, o  # 1 + 40, every unit completed through the revocation
-        # rank 0 cannot run more than a unit or two past rank 1's backlog: the
-        # drain tops rank 1 up to the agreed count instead of hanging rank 0
-        assert o["units_final"] == o["agreed"] >= 51, o
+        # rank 0 cannot run more than a unit or two past rank 1's: the drain
+        # tops the laggard up to the agreed count instead of hanging rank 0
+        assert o["units_final"] == o["agreed"] > 41, o
     assert outs[0]["agreed"] == outs[1]["agreed"]
