@@ -454,6 +454,8 @@ int gpbs_slot_info(gpbs_engine_t* e, int sid, gpbs_slot_info_t* o) {
     o->affinity[i] = v->affinity.w[i];
   }
   o->sched_count = v->sched_count;
+  o->class_home = v->class_home;
+  o->pause_flags = v->pause_flags;
   const int64_t n = E.now();
   int64_t extra = n - v->rs_entry;
   o->run_ns = v->rs_time[RS_RUNNING] + (v->rs == RS_RUNNING ? extra : 0);

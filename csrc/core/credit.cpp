@@ -612,7 +612,9 @@ class CreditScheduler : public Scheduler {
       ssum[k] = d.spinlock_metric_update;
       scnt[k] = d.spinlock_count;
     }
-    if (mode_ == Mode::PBS) {
+    if (mode_ == Mode::PBS && E.counter_ops.adapt_launch && E.counter_ops.adapt_harvest) {
+      adapt_async(ids, deltas, ssum, scnt);
+    } else if (mode_ == Mode::PBS) {
       std::vector<AdaptState> before(n);
       for (size_t k = 0; k < n; ++k) before[k] = sd(*E.tenants[ids[k]]).adapt;
       bool dev = false;
@@ -646,12 +648,7 @@ class CreditScheduler : public Scheduler {
           dir = d.adapt.tslice_us > before[k].tslice_us ? 1 : (d.adapt.tslice_us < before[k].tslice_us ? -1 : 0);
           rearm = d.adapt.window_left == kWindow - 1 && before[k].window_left == 0;
         }
-        if (dir > 0) E.perfc.incr(PC_adapt_inc);
-        if (dir < 0) E.perfc.incr(PC_adapt_dec);
-        if (rearm) E.perfc.incr(PC_adapt_rearm);
-        if (dir || rearm)
-          E.emit(TRC_ADAPT, master_, (uint32_t)ids[k], before[k].tslice_us, d.adapt.tslice_us,
-                 (d.adapt.phase << 24) | ((uint32_t)d.adapt.last_err & 0xffffff));
+        adapt_account(ids[k], before[k], d.adapt, dir, rearm);
       }
     }
     for (size_t k = 0; k < n; ++k) {
@@ -669,6 +666,99 @@ class CreditScheduler : public Scheduler {
       d.spinlock_metric_update = 0;
       d.spinlock_count = 0;
     }
+  }
+
+  void adapt_account(int id, const AdaptState& before, const AdaptState& after, int dir, bool rearm) {
+    if (dir > 0) E.perfc.incr(PC_adapt_inc);
+    if (dir < 0) E.perfc.incr(PC_adapt_dec);
+    if (rearm) E.perfc.incr(PC_adapt_rearm);
+    if (dir || rearm)
+      E.emit(TRC_ADAPT, master_, (uint32_t)id, before.tslice_us, after.tslice_us,
+             (after.phase << 24) | ((uint32_t)after.last_err & 0xffffff));
+  }
+
+  // Asynchronous device adaptation: period k's PBS update runs on the GPU
+  // (k_adapt) while the dispatcher goes on; tick k+1 applies it, then starts
+  // k+1's.  Each launch starts from the states the previous one produced, so
+  // the sequence of states is exactly the host's, one metric period late.  A
+  // launch still running at the next tick (a tail: the GPU was full) is
+  // recomputed on the host from its saved inputs and its result discarded.
+  struct AsyncIn {
+    int id;
+    AdaptState before;
+    uint64_t inst, miss, ssum, scnt;
+  };
+  std::vector<AsyncIn> async_in_;
+  bool async_pending_ = false;
+
+  void async_apply(int id, const AdaptState& before, const AdaptState& after) {
+    Tenant* t = E.tenant(id);
+    if (!t || !t->alive || !t->priv || t->pool != pool_) return;
+    sd(*t).adapt = after;
+    const int dir = after.tslice_us > before.tslice_us ? 1 : (after.tslice_us < before.tslice_us ? -1 : 0);
+    const bool rearm = after.window_left == kWindow - 1 && before.window_left == 0;
+    adapt_account(id, before, after, dir, rearm);
+  }
+
+  void adapt_async(const std::vector<int>& ids, const std::vector<uint64_t>& deltas, const std::vector<uint64_t>& ssum,
+                   const std::vector<uint64_t>& scnt) {
+    const gpbs_adapt_params_t* pp = reinterpret_cast<const gpbs_adapt_params_t*>(&E.adapt_params);
+    // 1. the previous period's results
+    if (async_pending_) {
+      std::vector<int> hid(async_in_.size() + 1);
+      std::vector<gpbs_adapt_state_t> hst(async_in_.size() + 1);
+      const int nh = E.counter_ops.adapt_harvest(E.counter_ops.user, (int)async_in_.size(), hid.data(), hst.data());
+      if (nh >= 0) {
+        for (int i = 0; i < nh && i < (int)async_in_.size(); ++i) {
+          AdaptState after;
+          std::memcpy(&after, &hst[i], sizeof(after));
+          async_apply(async_in_[i].id, async_in_[i].before, after);
+        }
+      } else {  // late: the host recomputes that period (bit-identical), the device result is dropped
+        E.perfc.incr(PC_adapt_late);
+        for (auto& a : async_in_) {
+          AdaptState st = a.before;
+          bool rearm = false;
+          adapt_update(st, E.adapt_params, a.inst, a.miss, a.ssum, a.scnt, &rearm);
+          async_apply(a.id, a.before, st);
+        }
+      }
+      async_pending_ = false;
+    }
+    // 2. this period: every non-idle tenant (Q14), from its current state
+    async_in_.clear();
+    std::vector<int> lid;
+    std::vector<uint64_t> ld, ls, lc;
+    std::vector<gpbs_adapt_state_t> lst;
+    for (size_t k = 0; k < ids.size(); ++k) {
+      if (E.boot.idle_skip && deltas[4 * k + 0] == 0) {
+        E.perfc.incr(PC_adapt_idle_skip);
+        continue;
+      }
+      CDom& d = sd(*E.tenants[ids[k]]);
+      async_in_.push_back({ids[k], d.adapt, deltas[4 * k + 0], deltas[4 * k + 3], ssum[k], scnt[k]});
+      lid.push_back(ids[k]);
+      for (int i = 0; i < 4; ++i) ld.push_back(deltas[4 * k + i]);
+      ls.push_back(ssum[k]);
+      lc.push_back(scnt[k]);
+      gpbs_adapt_state_t g;
+      std::memcpy(&g, &d.adapt, sizeof(g));
+      lst.push_back(g);
+    }
+    if (async_in_.empty()) return;
+    if (E.counter_ops.adapt_launch(E.counter_ops.user, (int)lid.size(), lid.data(), ld.data(), ls.data(), lc.data(),
+                                   lst.data(), pp) == 0) {
+      async_pending_ = true;
+      E.perfc.incr(PC_adapt_device);
+      return;
+    }
+    for (auto& a : async_in_) {  // could not start (previous buffers busy): the host adapts now
+      AdaptState st = a.before;
+      bool rearm = false;
+      adapt_update(st, E.adapt_params, a.inst, a.miss, a.ssum, a.scnt, &rearm);
+      async_apply(a.id, a.before, st);
+    }
+    async_in_.clear();
   }
 
   void dynamic_time_slice(int64_t now) {

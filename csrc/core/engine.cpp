@@ -806,17 +806,69 @@ void Engine::budget_layout(Pool& pl, int64_t n, bool force) {
       if (!(v.pause_flags & VPF_BLOCKED) && v.pause_count == 0) busy = true;
     }
     if (busy && t.pause_count == 0) t.last_busy = n;
-    // A busy tenant not classified yet is placed provisionally with the
-    // memory class: on SEs of its own, its counters become attributable (a
-    // tenant left floating across time-shared partitions never gets a clean
-    // window, so it would never be classified at all).
+    // class -1: busy but not classified yet
     const bool present = n - t.last_busy <= present_ns;
-    if (present) sig.emplace_back(t.id, t.cls >= 0 ? t.cls : 1);
+    if (present) sig.emplace_back(t.id, t.cls >= 0 ? t.cls : -1);
     else t.budget_ctx = 0;
   }
   if (!force && sig == pl.budget_sig) return;
   pl.budget_sig = sig;
   perfc.incr(PC_relayout);
+  // Probe layout: while a present tenant is not classified yet, every
+  // present tenant gets an exclusive, equal share of the pool's partitions
+  // (dealt round-robin in context-major order, so each share spans SEs and
+  // XCDs).  Exclusive ownership is what makes a tenant's counters
+  // attributable -- a tenant time-sharing partitions never gets a clean
+  // window, so it would never be classified -- and a share per tenant keeps
+  // the warm-up fair.  The class layout follows once every tenant has a class.
+  bool probe = false;
+  for (auto& e : sig) probe |= e.second < 0;
+  if (probe) {
+    std::vector<int> order;
+    for (int p = pl.cpus.first(); p >= 0; p = pl.cpus.next(p + 1)) order.push_back(p);
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+      return std::make_tuple(parts[a]->ctx, parts[a]->gpu, parts[a]->xcd) <
+             std::make_tuple(parts[b]->ctx, parts[b]->gpu, parts[b]->xcd);
+    });
+    const size_t k = sig.size();
+    for (size_t i = 0; i < k; ++i) {
+      Tenant& t = *tenants[sig[i].first];
+      Mask m;
+      std::vector<int> homes;
+      for (size_t j = i; j < order.size(); j += k) {
+        m.set(order[j]);
+        homes.push_back(order[j]);
+      }
+      if (homes.empty()) {  // more tenants than partitions: share one
+        m.set(order[i % order.size()]);
+        homes.push_back(order[i % order.size()]);
+      }
+      for (size_t s = 0; s < t.slots.size(); ++s) {
+        Slot& v = *slots[t.slots[s]];
+        if (s < homes.size()) {
+          if (v.pause_flags & VPF_DOWN) {
+            v.pause_flags &= ~VPF_DOWN;
+            v.soft = m;
+            v.class_home = homes[s];
+            if (!v.is_running) v.processor = homes[s];
+            vcpu_wake(v);
+          } else {
+            place_class(v, m, homes[s]);
+          }
+        } else if (!(v.pause_flags & VPF_DOWN)) {
+          v.pause_flags |= VPF_DOWN;
+          v.class_home = -1;
+          v.soft = Mask();
+          vcpu_sleep_nosync(v);
+        }
+      }
+      t.budget_ctx = 0;
+      t.budget_shared = false;
+    }
+    perfc.incr(PC_probe_layout);
+    process_softirqs();
+    return;
+  }
   int nctx = 0;
   for (int p = pl.cpus.first(); p >= 0; p = pl.cpus.next(p + 1)) nctx = std::max(nctx, parts[p]->ctx + 1);
   if (nctx <= 0) return;
@@ -900,6 +952,14 @@ void Engine::classify_tick(int64_t n) {
       for (size_t k = 0; k < t.slots.size(); ++k) {
         Slot& v = *slots[t.slots[k]];
         if (!runnable(v) || v.class_home < 0 || v.processor == v.class_home) continue;
+        if (boot.class_budget && boot.class_split > 1) {
+          // Budget layout: every online slot has a partition of its own, so
+          // a slot away from home (stolen while its tenant's share was
+          // idle, or displaced by a relayout onto a sibling's home) always
+          // goes back; a chain of displaced slots unwinds in a few ticks.
+          send_home(v);
+          continue;
+        }
         const Partition& P = *parts[v.processor];
         const Partition& H = *parts[v.class_home];
         const bool stray = !v.is_running && !v.soft.empty() && !v.soft.test(v.processor);

@@ -283,6 +283,15 @@ struct GpuCtx {
   // (CSCHED_METRIC_TICK_PERIOD, X:xen/common/sched_credit.c:55) and no longer
   // backs off; GPBS_HWC_SLOW_US=4000 restores the round-2 back-off.
   int hwc_slow_us = 0;  // GPBS_HWC_SLOW_US (0: never back off)
+  // Duty-cycle cap: a sample stalls the command processor for its duration
+  // (every counter record is a register read it performs), and what that
+  // costs the tenants varies from box to box (145-190 us per lean sample on
+  // one MI355X, ~500 us on another: scripts/hwc_cost.py).  The period
+  // stretches so that sampling takes at most hwc_duty_pct % of the time
+  // (EWMA of the sample duration); 0 disables the cap.
+  int hwc_duty_pct = 25;  // GPBS_HWC_DUTY
+  double hwc_dt_ewma = 0;
+  int64_t hwc_period_sum_ns = 0;
   std::atomic<uint64_t> hwc_slow_samples{0};
   int64_t hwc_ns = 0, hwc_ns_max = 0;
   uint64_t hwc_samples = 0;
@@ -305,6 +314,19 @@ struct GpuCtx {
   int64_t last_pub_ns = 0;
   hipEvent_t adapt_ev = nullptr;  // device adapt: bounded poll, never a blocking sync
   bool adapt_pending = false;
+  // Asynchronous device adapt (engine adapt_launch / adapt_harvest): two
+  // pinned buffer sets; a launch uses a free one, the next tick harvests it.
+  struct AdaptBuf {
+    gpbs_adapt_state_t* st = nullptr;  // in/out, pinned mapped
+    u64* delta = nullptr;              // [kMaxTenants][4]
+    u64* spin = nullptr;               // [2][kMaxTenants]
+    int ids[kMaxTenants];
+    int n = 0;
+    int state = 0;  // 0 free, 1 pending, 2 pending + result discarded
+    hipEvent_t ev = nullptr;
+  } abuf[2];
+  int abuf_last = -1;
+  uint64_t async_launches = 0, async_late = 0, async_busy = 0;
   uint64_t adapt_late = 0, adapt_calls = 0, adapt_busy = 0;
   int se_mode = 0;  // partitions are exclusive shader engines (GATE_SE)
   // Class-share mode (SE mode): when every tenant holding partitions is of
@@ -543,7 +565,18 @@ void hwc_loop(GpuCtx* c) {
     last_sw = sw;
     const bool slow = c->hwc_slow_us > c->hwc_period_us && now - last_change >= kSteadyNs;
     if (slow) c->hwc_slow_samples.fetch_add(1, std::memory_order_relaxed);
-    const int64_t rest = (int64_t)(slow ? c->hwc_slow_us : c->hwc_period_us) * 1000 - (mono_ns() - t0);
+    int64_t period = (int64_t)(slow ? c->hwc_slow_us : c->hwc_period_us) * 1000;
+    if (rc >= 0) {
+      const double dt = (double)(now - t0);
+      c->hwc_dt_ewma = c->hwc_dt_ewma > 0 ? 0.875 * c->hwc_dt_ewma + 0.125 * dt : dt;
+    }
+    if (c->hwc_duty_pct > 0)
+      period = std::max(period, (int64_t)(c->hwc_dt_ewma * 100.0 / c->hwc_duty_pct));
+    {
+      std::lock_guard<std::mutex> g(c->snap_mu);
+      c->hwc_period_sum_ns += period;
+    }
+    const int64_t rest = period - (mono_ns() - t0);
     if (rest > 0) std::this_thread::sleep_for(std::chrono::nanoseconds(rest));
   }
 }
@@ -753,6 +786,54 @@ int ctr_adapt_batch(void* user, int n, const int*, const uint64_t* deltas, const
   std::memcpy(states, c->h_states, sizeof(gpbs_adapt_state_t) * n);
   c->metric_ns += mono_ns() - t0;
   return 0;
+}
+
+int ctr_adapt_launch(void* user, int n, const int* tenants, const uint64_t* deltas, const uint64_t* ssum,
+                     const uint64_t* scnt, const gpbs_adapt_state_t* states, const gpbs_adapt_params_t* p) {
+  GpuCtx* c = (GpuCtx*)user;
+  if (n <= 0 || n > kMaxTenants) return -22;
+  RoctxRange rr("gpbs:adapt_launch");
+  int b = -1;
+  for (int i = 0; i < 2 && b < 0; ++i) {
+    GpuCtx::AdaptBuf& B = c->abuf[i];
+    if (B.state != 0 && hipEventQuery(B.ev) == hipSuccess && B.state == 2) B.state = 0;  // a dropped result landed
+    if (B.state == 0) b = i;
+  }
+  if (b < 0) {
+    c->async_busy++;
+    return -11;
+  }
+  GpuCtx::AdaptBuf& B = c->abuf[b];
+  std::memcpy(B.st, states, sizeof(gpbs_adapt_state_t) * n);
+  std::memcpy(B.delta, deltas, sizeof(u64) * 4 * n);
+  std::memcpy(B.spin, ssum, sizeof(u64) * n);
+  std::memcpy(B.spin + kMaxTenants, scnt, sizeof(u64) * n);
+  std::memcpy(B.ids, tenants, sizeof(int) * n);
+  B.n = n;
+  if (gpbs_hip_adapt(B.st, B.delta, B.spin, B.spin + kMaxTenants, n, p, nullptr, c->sched_stream) ||
+      hipEventRecord(B.ev, c->sched_stream) != hipSuccess)
+    return -5;
+  B.state = 1;
+  c->abuf_last = b;
+  c->async_launches++;
+  return 0;
+}
+
+int ctr_adapt_harvest(void* user, int max, int* tenants_out, gpbs_adapt_state_t* states_out) {
+  GpuCtx* c = (GpuCtx*)user;
+  if (c->abuf_last < 0) return -22;
+  GpuCtx::AdaptBuf& B = c->abuf[c->abuf_last];
+  if (B.state != 1) return -22;
+  if (hipEventQuery(B.ev) != hipSuccess) {
+    B.state = 2;  // the engine recomputes this period on the host; drop the result when it lands
+    c->async_late++;
+    return -11;
+  }
+  const int n = std::min(B.n, max);
+  std::memcpy(states_out, B.st, sizeof(gpbs_adapt_state_t) * n);
+  std::memcpy(tenants_out, B.ids, sizeof(int) * n);
+  B.state = 0;
+  return n;
 }
 
 // --------------------------------------------------------------------- runner
@@ -1203,6 +1284,7 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
   if (const char* v = std::getenv("GPBS_HOLD_ALL")) c->hold_all = std::atoi(v) != 0;
   if (const char* v = std::getenv("GPBS_HWC_PERIOD_US")) c->hwc_period_us = std::max(100, std::atoi(v));
   if (const char* v = std::getenv("GPBS_HWC_SLOW_US")) c->hwc_slow_us = std::max(0, std::atoi(v));
+  if (const char* v = std::getenv("GPBS_HWC_DUTY")) c->hwc_duty_pct = std::max(0, std::min(100, std::atoi(v)));
   if (const char* v = std::getenv("GPBS_SHARE_PROBE")) {
     c->probe_every = std::max(0, std::atoi(v));
     if (const char* k = std::strchr(v, ':')) c->probe_len = std::max(0, std::atoi(k + 1));
@@ -1240,6 +1322,12 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
   ok = ok && hipHostMalloc((void**)&c->h_spin, sizeof(u64) * 2 * kMaxTenants, hipHostMallocMapped) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_dirs, sizeof(int) * kMaxTenants, hipHostMallocMapped) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_adelta, sizeof(u64) * 4 * kMaxTenants, hipHostMallocMapped) == hipSuccess;
+  for (auto& B : c->abuf) {
+    ok = ok && hipHostMalloc((void**)&B.st, sizeof(gpbs_adapt_state_t) * kMaxTenants, hipHostMallocMapped) == hipSuccess;
+    ok = ok && hipHostMalloc((void**)&B.delta, sizeof(u64) * 4 * kMaxTenants, hipHostMallocMapped) == hipSuccess;
+    ok = ok && hipHostMalloc((void**)&B.spin, sizeof(u64) * 2 * kMaxTenants, hipHostMallocMapped) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&B.ev, hipEventDisableTiming) == hipSuccess;
+  }
   int lo = 0, hi = 0;
   hipDeviceGetStreamPriorityRange(&lo, &hi);
   ok = ok && hipStreamCreateWithPriority(&c->sched_stream, hipStreamNonBlocking, hi) == hipSuccess;
@@ -1301,6 +1389,15 @@ void gpbs_gpu_ctx_destroy(void* p) {
   if (c->h_ain) hipHostFree(c->h_ain);
   if (c->h_aout) hipHostFree(c->h_aout);
   if (c->d_ast) hipFree(c->d_ast);
+  for (auto& B : c->abuf) {
+    if (B.ev) {
+      hipEventSynchronize(B.ev);
+      hipEventDestroy(B.ev);
+    }
+    if (B.st) hipHostFree(B.st);
+    if (B.delta) hipHostFree(B.delta);
+    if (B.spin) hipHostFree(B.spin);
+  }
   hipHostFree(c->h_states);
   hipHostFree(c->h_spin);
   hipHostFree(c->h_dirs);
@@ -1323,7 +1420,12 @@ int gpbs_gpu_attach(void* p, gpbs_engine_t* e, int device_counters, int device_a
   gpbs_counter_ops_t k{};
   k.user = c;
   if (device_counters) k.tenant_deltas = ctr_tenant_deltas;
-  if (device_adapt) k.adapt_batch = ctr_adapt_batch;
+  if (device_adapt == 1) {  // asynchronous: launched by one metric tick, applied by the next
+    k.adapt_launch = ctr_adapt_launch;
+    k.adapt_harvest = ctr_adapt_harvest;
+  } else if (device_adapt == 2) {  // synchronous, bounded poll under the engine lock (round 2)
+    k.adapt_batch = ctr_adapt_batch;
+  }
   gpbs_set_counter_ops(e, &k);
   return 0;
 }
@@ -1585,6 +1687,7 @@ int gpbs_gpu_hwc_reset(void* p) {
   c->hwc_ns = c->hwc_ns_max = 0;
   c->hwc_samples = 0;
   c->hwc_slow_samples = 0;
+  c->hwc_period_sum_ns = 0;
   return 0;
 }
 
@@ -1598,6 +1701,20 @@ int gpbs_gpu_hwc_period(void* p, int fast_us, int slow_us, uint64_t* slow_sample
   if (slow_us >= 0) c->hwc_slow_us = slow_us;
   if (slow_samples) *slow_samples = c->hwc_slow_samples;
   return 0;
+}
+
+// Duty-cycle cap (percent, < 0 leaves it; 0 off); *mean_period_ns = mean
+// sampler period since the last hwc reset.  Returns the old cap.
+int gpbs_gpu_hwc_duty(void* p, int pct, uint64_t* mean_period_ns) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c) return -22;
+  const int old = c->hwc_duty_pct;
+  if (pct >= 0) c->hwc_duty_pct = std::min(pct, 100);
+  if (mean_period_ns) {
+    std::lock_guard<std::mutex> g(c->snap_mu);
+    *mean_period_ns = c->hwc_samples ? (uint64_t)(c->hwc_period_sum_ns / (int64_t)c->hwc_samples) : 0;
+  }
+  return old;
 }
 
 // SE-exclusive partitions: the nctx (= 4) partitions of an XCD are its shader
@@ -1770,9 +1887,9 @@ int gpbs_gpu_ownership(void* p, int t, int64_t* out2, int clear) {
 int gpbs_gpu_adapt_stats(void* p, uint64_t* calls, uint64_t* late, uint64_t* busy) {
   GpuCtx* c = (GpuCtx*)p;
   if (!c) return -22;
-  if (calls) *calls = c->adapt_calls;
-  if (late) *late = c->adapt_late;
-  if (busy) *busy = c->adapt_busy;
+  if (calls) *calls = c->adapt_calls + c->async_launches;
+  if (late) *late = c->adapt_late + c->async_late;
+  if (busy) *busy = c->adapt_busy + c->async_busy;
   return 0;
 }
 

@@ -109,6 +109,16 @@ typedef struct gpbs_counter_ops {
   /* Optional batched adaptation (device kernel).  Updates states in place. */
   int (*adapt_batch)(void* user, int n, const int* tenants, const uint64_t* deltas, const uint64_t* spin_sum,
                      const uint64_t* spin_cnt, gpbs_adapt_state_t* states, const gpbs_adapt_params_t* p);
+  /* Asynchronous device adaptation (preferred over adapt_batch when both are
+   * set; the metric tick never waits on the GPU): adapt_launch starts this
+   * period's PBS update of n tenants (0, or < 0 when it cannot start now --
+   * the tick then adapts on the host); adapt_harvest returns the previous
+   * launch's results once complete (count, tenants_out / states_out) or -11
+   * while it still runs.  The engine applies results one metric period late
+   * and recomputes a late period on the host (bit-identical). */
+  int (*adapt_launch)(void* user, int n, const int* tenants, const uint64_t* deltas, const uint64_t* spin_sum,
+                      const uint64_t* spin_cnt, const gpbs_adapt_state_t* states, const gpbs_adapt_params_t* p);
+  int (*adapt_harvest)(void* user, int max, int* tenants_out, gpbs_adapt_state_t* states_out);
 } gpbs_counter_ops_t;
 
 /* Actuator (context switch analog).  on_switch is called for every partition
@@ -170,6 +180,8 @@ typedef struct gpbs_slot_info {
   uint64_t sched_count;
   int64_t run_ns, runnable_ns, blocked_ns;
   uint64_t affinity[4];
+  int32_t class_home;   /* contention-class / budget home partition, -1 none */
+  uint32_t pause_flags; /* VPF_* (1 blocked, 2 migrating, 4 offline) */
 } gpbs_slot_info_t;
 
 /* Scheduler-specific per-tenant parameters (xl sched-credit2 / sched-sedf).

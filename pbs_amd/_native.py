@@ -57,6 +57,9 @@ COUNTER_SLOT_REFRESH = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_in
 COUNTER_TENANT_DELTAS = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_int), C.POINTER(u64))
 COUNTER_ADAPT_BATCH = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_int), C.POINTER(u64), C.POINTER(u64),
                                   C.POINTER(u64), C.POINTER(AdaptState), C.POINTER(AdaptParams))
+COUNTER_ADAPT_LAUNCH = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_int), C.POINTER(u64), C.POINTER(u64),
+                                   C.POINTER(u64), C.POINTER(AdaptState), C.POINTER(AdaptParams))
+COUNTER_ADAPT_HARVEST = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_int), C.POINTER(AdaptState))
 
 
 class ArincEntry(C.Structure):
@@ -70,7 +73,8 @@ class ArincSchedule(C.Structure):
 
 class CounterOps(C.Structure):
     _fields_ = [("user", C.c_void_p), ("slot_refresh", COUNTER_SLOT_REFRESH),
-                ("tenant_deltas", COUNTER_TENANT_DELTAS), ("adapt_batch", COUNTER_ADAPT_BATCH)]
+                ("tenant_deltas", COUNTER_TENANT_DELTAS), ("adapt_batch", COUNTER_ADAPT_BATCH),
+                ("adapt_launch", COUNTER_ADAPT_LAUNCH), ("adapt_harvest", COUNTER_ADAPT_HARVEST)]
 
 
 ACT_ON_SWITCH = C.CFUNCTYPE(None, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, i32, i64)
@@ -100,7 +104,7 @@ class SlotInfo(C.Structure):
     _fields_ = [(n, i32) for n in ("id", "tenant", "index", "processor", "pri", "flags", "runstate",
                                    "is_running", "credit", "on_runq")] + \
                [("pmc", u64 * 4), ("sched_count", u64), ("run_ns", i64), ("runnable_ns", i64),
-                ("blocked_ns", i64), ("affinity", u64 * 4)]
+                ("blocked_ns", i64), ("affinity", u64 * 4), ("class_home", i32), ("pause_flags", u32)]
 
 
 class PartitionInfo(C.Structure):

@@ -157,14 +157,21 @@ class GpuContext:
         self.L.gpbs_gpu_hwc_period(self.h, -1, -1, C.byref(slow))
         la, bs, ho = C.c_uint64(0), C.c_uint64(0), C.c_uint64(0)
         dev = self.L.gpbs_gpu_hwc_attr_stats(self.h, C.byref(la), C.byref(bs), C.byref(ho))
+        mp = C.c_uint64(0)
+        duty = self.L.gpbs_gpu_hwc_duty(self.h, -1, C.byref(mp))
         return {"attr_device": bool(dev), "attr_kernel_launches": la.value, "attr_busy_skips": bs.value,
-                "attr_host": ho.value,
+                "attr_host": ho.value, "duty_cap_pct": duty, "mean_period_us": round(mp.value / 1e3, 1),
                 "samples": n.value, "slow_samples": slow.value, "mean_sample_us": round(ns.value / 1e3, 1), "max_sample_us": round(mx.value / 1e3, 1),
                 "hw_over_model": [round(x, 4) for x in r],
                 "unattributed_frac": [round(x, 4) for x in u],
                 "attribution": "exact-se" if sem.value & 1 else "xcd-time-share",
                 # exclusive-ownership windows: share of the counts that reached the PBS metric
                 "clean_pct": pct, "metric_frac": [round(x, 4) for x in cf]}
+
+    def set_hwc_duty(self, pct: int) -> int:
+        """Sampler duty-cycle cap: the period stretches so that sampling takes
+        at most `pct` % of the time (0: off).  Returns the old cap."""
+        return self.L.gpbs_gpu_hwc_duty(self.h, int(pct), None)
 
     def set_hwc_device(self, on: bool) -> bool:
         """Attribute counter snapshots on the GPU (k_hwc_attribute, default)

@@ -28,8 +28,11 @@ SPECS = {
     "sq1_tcc1": "SQ_INSTS_VALU|SQ_WAVES|TCC_REQ|TCC_MISS",
     "tcc2": "TCC_HIT|TCC_REQ|TCC_EA0_RDREQ|TCC_MISS",
     "sq1": "SQ_INSTS_VALU|SQ_WAVES|SQ_INSTS_SALU|SQ_INSTS_LDS",
+    # refs from SQ memory instructions instead of TCP requests: 6 SQ + 1 TCC
+    "lean2": "SQ_INSTS_VALU+SQ_INSTS_SALU+SQ_INSTS_VALU_MFMA_MOPS_BF16|SQ_BUSY_CYCLES|"
+             "SQ_INSTS_VMEM_RD+SQ_INSTS_VMEM_WR|TCC_MISS",
 }
-DEFAULT_SET = "full,lean,sq2_tcp1_tcc1,sq1_tcc1"
+DEFAULT_SET = "full,lean,lean2,sq1_tcc1"
 
 CHILD = r"""
 import json, sys, time
@@ -58,6 +61,7 @@ def rate(secs):
 r.submit(q); rate(0.3)  # warm
 out = {"spec": spec or "default", "kind": kind}
 out["off"] = rate(%(secs)f)
+ctx.set_hwc_duty(0)  # measure the raw period
 for per in (4000, 1000):
     ctx.set_hwc_period(per, 0)   # fixed period, no back-off
     ctx.set_hwc(True)

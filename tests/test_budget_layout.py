@@ -119,3 +119,31 @@ def test_budget_time_shares_a_crowded_class_region():
     ms = [share[m] for m in mem]
     assert sum(ms) > 15.0 and max(ms) - min(ms) < 2.5, share
     assert e.check() == ""
+
+
+def test_probe_layout_gives_unclassified_tenants_exclusive_partitions():
+    """Seven busy tenants, none classified yet: each gets an exclusive share
+    of the 32 partitions (a time-shared tenant would never see a clean
+    counter window and never be classified); once every tenant has a class
+    the class layout takes over (crowded regions time-share)."""
+    e, parts = _engine()
+    names = ["g0", "g1", "g2", "m0", "m1", "m2", "m3"]
+    ts = [e.tenant_create(n, nslots=32) for n in names]
+    rates = {t: (COMPUTE if n.startswith("g") else MEMORY) for t, n in zip(ts, names)}
+    for t in ts:
+        e.wake(t)
+    for _ in range(60):  # the first class ticks: probe layout
+        _feed(e, {}, 100)
+    owners = [e.partition_info(p)["curr_tenant"] for p in range(len(parts))]
+    per = Counter(o for o in owners if o in ts)
+    assert sorted(per.values()) == [4, 4, 4, 5, 5, 5, 5], per  # 32 partitions dealt to 7 tenants
+    assert sum(_online(e, t) for t in ts) == 32
+    assert e.perfc()["probe_layout"] >= 1
+    _settle(e, rates, 600)
+    classes = {n: e.lib.gpbs_tenant_class(e.h, t) for n, t in zip(names, ts)}
+    assert all(c == (0 if n.startswith("g") else 1) for n, c in classes.items()), classes
+    own = _ctx_owners(e, parts)
+    comp = {t for t, n in zip(ts, names) if n.startswith("g")}
+    assert all(t in comp for c in (0, 1) for t in own[c] if t >= 0), own
+    assert all(t not in comp for c in (2, 3) for t in own[c] if t >= 0), own
+    assert e.check() == ""
