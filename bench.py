@@ -203,10 +203,10 @@ def main():
 
     results = {}
     for mix in mixes:
-        default = {"4mix": "none,static,static-se,credit-fixed-ts,gpbs-ts,credit-fixed,gpbs-lat,gpbs",
+        default = {"4mix": "none,static,static-se,credit-fixed,gpbs-nolane,gpbs-lat,gpbs",
                    "gemm2": "none,static,static-se,credit-fixed,gpbs",
                    "phase": "none,static-se,credit-fixed,gpbs",
-                   "8mix": "none,static-se,credit-fixed,gpbs"}[mix]
+                   "8mix": "none,static-se,credit-fixed-ts,gpbs-ts,gpbs"}[mix]
         spec = args.policies if (args.policies and mix == mixes[0]) else default
         pols = tuple(p for p in spec.split(",") if p)
         reps = args.reps if mix == mixes[0] else args.reps_extra

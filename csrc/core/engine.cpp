@@ -756,10 +756,10 @@ void Engine::place_tenant_class(Tenant& t, Pool& pl, int layout) {
 // make the pCPUs a blocked domain leaves available to the others at once
 // (X:xen/common/sched_credit.c:1559-1672); here that happens per class tick,
 // in space.
-void Engine::place_budget(Tenant& t, Pool& pl, uint32_t ctx_mask, int stagger) {
+void Engine::place_budget(Tenant& t, Pool& pl, uint32_t ctx_mask, int stagger, uint32_t xcd_mask) {
   Mask m;
   for (int p = pl.cpus.first(); p >= 0; p = pl.cpus.next(p + 1))
-    if ((ctx_mask >> (parts[p]->ctx & 31)) & 1) m.set(p);
+    if (((ctx_mask >> (parts[p]->ctx & 31)) & 1) && (!xcd_mask || ((xcd_mask >> (parts[p]->xcd & 31)) & 1))) m.set(p);
   std::vector<int> order;
   for (int p = m.first(); p >= 0; p = m.next(p + 1)) order.push_back(p);
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
@@ -790,7 +790,7 @@ void Engine::place_budget(Tenant& t, Pool& pl, uint32_t ctx_mask, int stagger) {
       vcpu_sleep_nosync(v);
     }
   }
-  t.budget_ctx = ctx_mask;
+  t.budget_ctx = ctx_mask | ((xcd_mask & 0xffu) << 8);
   emit(TRC_CLASS, 0, t.id, (uint32_t)t.cls, (uint32_t)m.weight());
 }
 
@@ -823,7 +823,41 @@ void Engine::budget_layout(Pool& pl, int64_t n, bool force) {
   // the warm-up fair.  The class layout follows once every tenant has a class.
   bool probe = false;
   for (auto& e : sig) probe |= e.second < 0;
-  if (probe) {
+  int nctx = 0;
+  uint32_t xall = 0;
+  for (int p = pl.cpus.first(); p >= 0; p = pl.cpus.next(p + 1)) {
+    nctx = std::max(nctx, parts[p]->ctx + 1);
+    xall |= 1u << (parts[p]->xcd & 31);
+  }
+  if (nctx <= 0) return;
+  const int nx = __builtin_popcount(xall);
+  uint32_t ctx_all = 0;
+  for (int x = 0; x < nctx; ++x) ctx_all |= 1u << x;
+  // XCD blocks: tenant i of k gets nx/k whole XCDs (the first nx%k one more).
+  auto xcd_block = [&](int i, int k) {
+    int at = 0;
+    for (int j = 0; j < i; ++j) at += nx / k + (j < nx % k ? 1 : 0);
+    const int sz = nx / k + (i < nx % k ? 1 : 0);
+    uint32_t m = 0;
+    int seen = 0;
+    for (int x = 0; x < 32; ++x)
+      if ((xall >> x) & 1) {
+        if (seen >= at && seen < at + sz) m |= 1u << x;
+        ++seen;
+      }
+    return m;
+  };
+  if (probe && (int)sig.size() <= nx) {
+    for (size_t i = 0; i < sig.size(); ++i) {
+      Tenant& t = *tenants[sig[i].first];
+      t.budget_shared = false;
+      place_budget(t, pl, ctx_all, 0, xcd_block((int)i, (int)sig.size()));
+    }
+    perfc.incr(PC_probe_layout);
+    process_softirqs();
+    return;
+  }
+  if (probe) {  // more tenants than XCDs: deal single partitions
     std::vector<int> order;
     for (int p = pl.cpus.first(); p >= 0; p = pl.cpus.next(p + 1)) order.push_back(p);
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
@@ -869,9 +903,6 @@ void Engine::budget_layout(Pool& pl, int64_t n, bool force) {
     process_softirqs();
     return;
   }
-  int nctx = 0;
-  for (int p = pl.cpus.first(); p >= 0; p = pl.cpus.next(p + 1)) nctx = std::max(nctx, parts[p]->ctx + 1);
-  if (nctx <= 0) return;
   const int split = std::min(std::max(1, boot.class_split), nctx);
   std::vector<int> cls_t[2];
   for (auto& e : sig) cls_t[e.second & 1].push_back(e.first);
@@ -883,6 +914,20 @@ void Engine::budget_layout(Pool& pl, int64_t n, bool force) {
       else lo = split;
     }
     const int r = hi - lo, k = (int)cls_t[c].size();
+    if (k > r && boot.class_budget >= 2 && k <= nx) {
+      // Crowded region, spatial split: each tenant gets the region's SEs of
+      // a block of whole XCDs (its own L2s: the per-XCD L2 misses become
+      // exactly attributable too) -- the static split a human would pick,
+      // re-derived whenever the classes or the present tenants change.
+      uint32_t reg = 0;
+      for (int x = lo; x < hi; ++x) reg |= 1u << x;
+      for (int i = 0; i < k; ++i) {
+        Tenant& t = *tenants[cls_t[c][i]];
+        t.budget_shared = false;
+        place_budget(t, pl, reg, 0, xcd_block(i, k));
+      }
+      continue;
+    }
     if (k > r) {  // time-shared region: every tenant on all of it, staggered by whole contexts
       uint32_t all = 0;
       for (int x = lo; x < hi; ++x) all |= 1u << x;

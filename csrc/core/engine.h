@@ -88,8 +88,9 @@ struct Tenant {  // struct domain
   uint64_t vpmu_total[4] = {0, 0, 0, 0};
   int cls = -1;          // contention class: 0 compute-bound (MFMA ctx), 1 memory-bound (memory ctx)
   // class_budget layout: last time any slot was runnable, and the contexts
-  // (shader engines) of every XCD the layout gave the tenant (bit c = ctx c;
-  // 0 = not placed / absent); budget_shared: its class region is time-shared
+  // (shader engines) the layout gave the tenant (bit c = ctx c), with the
+  // XCDs in bits 8-15 when it is confined to a block of XCDs (0 = all; 0
+  // overall = not placed / absent); budget_shared: its region is time-shared
   int64_t last_busy = INT64_MIN / 2;
   uint32_t budget_ctx = 0;
   bool budget_shared = false;
@@ -377,7 +378,7 @@ class Engine {
   void classify_tick(int64_t now);
   void place_tenant_class(Tenant& t, Pool& pl, int layout);
   void budget_layout(Pool& pl, int64_t now, bool force);
-  void place_budget(Tenant& t, Pool& pl, uint32_t ctx_mask, int stagger);
+  void place_budget(Tenant& t, Pool& pl, uint32_t ctx_mask, int stagger, uint32_t xcd_mask = 0);
   void set_affinity(Slot& v, const Mask& m, int home = -1);
   void place_class(Slot& v, const Mask& m, int home);
   void send_home(Slot& v);

@@ -796,7 +796,9 @@ int ctr_adapt_launch(void* user, int n, const int* tenants, const uint64_t* delt
   int b = -1;
   for (int i = 0; i < 2 && b < 0; ++i) {
     GpuCtx::AdaptBuf& B = c->abuf[i];
-    if (B.state != 0 && hipEventQuery(B.ev) == hipSuccess && B.state == 2) B.state = 0;  // a dropped result landed
+    // a dropped result that landed, or an orphan (launched for an engine
+    // that stopped before harvesting it): free once the kernel is done
+    if ((B.state == 2 || (B.state == 1 && i != c->abuf_last)) && hipEventQuery(B.ev) == hipSuccess) B.state = 0;
     if (B.state == 0) b = i;
   }
   if (b < 0) {
@@ -1411,6 +1413,9 @@ void gpbs_gpu_ctx_destroy(void* p) {
 int gpbs_gpu_attach(void* p, gpbs_engine_t* e, int device_counters, int device_adapt) {
   GpuCtx* c = (GpuCtx*)p;
   c->engine = e;
+  for (auto& B : c->abuf)  // a new engine harvests nothing an old one launched
+    if (B.state == 1) B.state = 2;
+  c->abuf_last = -1;
   gpbs_actuator_ops_t a{};
   a.user = c;
   a.on_switch = act_on_switch;

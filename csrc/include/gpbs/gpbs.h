@@ -80,7 +80,8 @@ typedef struct gpbs_boot_params {
   int32_t class_budget;        /* 1 = demand-driven SE budgets (class_split > 1): each PRESENT classified tenant gets a
                                   set of shader engines sized by the classes present (aligned halves, singles, or the
                                   class region time-shared when it has more tenants than SEs); surplus slots go offline
-                                  (vcpu-set) -- no bench-side slot counts decide the layout */
+                                  (vcpu-set) -- no bench-side slot counts decide the layout.  2 = the same, but a
+                                  crowded region is split by blocks of whole XCDs instead of time-shared */
   int32_t present_us;          /* class_budget: a tenant with no runnable slot for this long leaves the layout
                                   (default 10000) */
   gpbs_adapt_params_t adapt;

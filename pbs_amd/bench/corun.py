@@ -168,7 +168,7 @@ SE_OVERRIDES = {"class_split": 2, "idle_skip": 1}
 # demand-driven SE budgets (csrc/core/engine.cpp budget_layout): the layout,
 # not a slot count, sizes each tenant's share -- every tenant is created with
 # one slot per partition and surplus slots go offline
-BUDGET_OVERRIDES = {"class_split": 2, "idle_skip": 1, "class_budget": 1, "present_us": 10000}
+BUDGET_OVERRIDES = {"class_split": 2, "idle_skip": 1, "class_budget": 2, "present_us": 10000}
 SE_SLOTS = {"gemm": 16, "gemm_b": 16, "hbm": 16, "coll": 16, "idle": 8}
 # "se8": memory tenants get 8 slots each -- one SE per XCD, so the credit
 # scheduler places them on disjoint memory SEs instead of time-sharing both.
@@ -177,34 +177,34 @@ SE8_SLOTS = {"gemm": 16, "gemm_b": 16, "hbm": 8, "coll": 8, "idle": 8}
 POLICY_ENGINES = {
     # name: (issue contexts per XCD, engine overrides on top of MI355X_PROFILE,
     #        kernel gate mode, partition-table location + runtime options)
-    # flagship: counter-driven class split over exclusive SEs -- the compute
-    # class owns SEs {0,1} of every XCD, each memory tenant one memory SE of
-    # every XCD ("se8": 8 slots, so credit places the memory tenants on
-    # disjoint SEs); the latency tenant runs outside the partitions,
-    # co-resident at raised wave priority (no BOOST revocations)
-    "gpbs": (4, dict(BUDGET_OVERRIDES), True, "device,se,waveprio,latco,budget"),
-    "credit-fixed": (4, dict(BUDGET_OVERRIDES, sched="credit-fixed"), True, "device,se,waveprio,latco,budget"),
+    # flagship: counter-driven SE budgets (csrc/core/engine.cpp budget_layout)
+    # -- every present tenant gets shader engines sized from the classes
+    # present, a crowded class region is split by whole-XCD blocks; runners
+    # launch on CU-masked class-half streams; the latency tenant runs outside
+    # the partitions in the latency lane (its GEMV CU-masked to the memory
+    # half, raised wave priority)
+    "gpbs": (4, dict(BUDGET_OVERRIDES), True, "device,se,waveprio,latco,budget,latmem"),
+    "credit-fixed": (4, dict(BUDGET_OVERRIDES, sched="credit-fixed"), True, "device,se,waveprio,latco,budget,latmem"),
+    # crowded class regions time-shared under credit with PBS adaptive quanta
+    # (credit-fixed-ts: the fixed quantum) -- where PBS quanta act (8mix)
+    "gpbs-ts": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
+    "credit-fixed-ts": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="credit-fixed"), True,
+                        "device,se,waveprio,latco,budget,latmem"),
+    # the same without the latency lane (GEMV co-resident on every CU)
+    "gpbs-nolane": (4, dict(BUDGET_OVERRIDES), True, "device,se,waveprio,latco,budget"),
     # round-2 flagship: fixed class halves, memory tenants one SE each by
     # their bench-side slot count (se8)
     "gpbs-se8": (4, dict(SE_OVERRIDES), True, "device,se,waveprio,latco,se8"),
-    # time-shared variant: the memory tenants hold slots on all memory SEs
-    # {2,3} and alternate on them as one gang under credit with PBS's
-    # adaptive quanta (credit-fixed-ts: fixed quantum)
-    # ablation: class-share mode -- while every owner is of one class the
-    # runners launch co-resident full-GPU grids (exclusive probe windows keep
-    # the counters measurable).  Config #2 measured it at or below the plain
-    # class-half split once co-class tenants hold aligned halves (1.240 vs
-    # 1.253, none 1.252), so the flagship does not share.
     "gpbs-share": (4, dict(SE_OVERRIDES), True, "device,se,waveprio,latco,se8,share"),
     # flagship + latency hold: the table in host-written VRAM (BAR), and the
     # memory-class tenants pause at their next unit boundary while a latency
     # request is in flight (the wake-BOOST analog for the GEMV tenant)
+    # flagship + latency hold (memory-class tenants pause at their next unit
+    # boundary while a latency request is in flight; BAR-written VRAM table)
     "gpbs-lat": (4, dict(BUDGET_OVERRIDES), True, "bar,se,waveprio,latco,budget,hold,latmem"),
-    # latency lane only (GEMV CU-masked to the memory half, no hold) / hold only
-    "gpbs-lane": (4, dict(BUDGET_OVERRIDES), True, "device,se,waveprio,latco,budget,latmem"),
-    "gpbs-hold": (4, dict(BUDGET_OVERRIDES), True, "bar,se,waveprio,latco,budget,hold"),
-    "gpbs-ts": (4, dict(SE_OVERRIDES), True, "device,se,waveprio,latco"),
-    "credit-fixed-ts": (4, dict(SE_OVERRIDES, sched="credit-fixed"), True, "device,se,waveprio,latco"),
+    # round-2 time-shared variant: memory tenants alternate on SEs {2,3}
+    "gpbs-ts-r2": (4, dict(SE_OVERRIDES), True, "device,se,waveprio,latco"),
+    "credit-fixed-ts-r2": (4, dict(SE_OVERRIDES, sched="credit-fixed"), True, "device,se,waveprio,latco"),
     "credit2": (4, dict(SE_OVERRIDES, sched="credit2"), True, "device,se,waveprio,latco"),
     "gpbs-boost": (4, dict(SE_OVERRIDES), True, "device,se,waveprio"),
     "gpbs-host": (4, dict(SE_OVERRIDES), True, "host,se,waveprio,latco"),

@@ -122,10 +122,11 @@ def test_budget_time_shares_a_crowded_class_region():
 
 
 def test_probe_layout_gives_unclassified_tenants_exclusive_partitions():
-    """Seven busy tenants, none classified yet: each gets an exclusive share
-    of the 32 partitions (a time-shared tenant would never see a clean
-    counter window and never be classified); once every tenant has a class
-    the class layout takes over (crowded regions time-share)."""
+    """Seven busy tenants, none classified yet: each gets whole XCDs of its
+    own (a time-shared tenant would never see a clean counter window, and an
+    XCD shared with a stream would charge it the stream's L2 misses); once
+    every tenant has a class the class layout takes over (crowded regions
+    time-share)."""
     e, parts = _engine()
     names = ["g0", "g1", "g2", "m0", "m1", "m2", "m3"]
     ts = [e.tenant_create(n, nslots=32) for n in names]
@@ -136,7 +137,10 @@ def test_probe_layout_gives_unclassified_tenants_exclusive_partitions():
         _feed(e, {}, 100)
     owners = [e.partition_info(p)["curr_tenant"] for p in range(len(parts))]
     per = Counter(o for o in owners if o in ts)
-    assert sorted(per.values()) == [4, 4, 4, 5, 5, 5, 5], per  # 32 partitions dealt to 7 tenants
+    assert sorted(per.values()) == [4, 4, 4, 4, 4, 4, 8], per  # 8 XCDs dealt to 7 tenants, all 4 SEs each
+    for t in ts:
+        xs = {parts[p][1] for p in range(len(parts)) if owners[p] == t}
+        assert all(owners[x * 4 + c] == t for x in xs for c in range(4)), (t, xs)
     assert sum(_online(e, t) for t in ts) == 32
     assert e.perfc()["probe_layout"] >= 1
     _settle(e, rates, 600)
@@ -146,4 +150,33 @@ def test_probe_layout_gives_unclassified_tenants_exclusive_partitions():
     comp = {t for t, n in zip(ts, names) if n.startswith("g")}
     assert all(t in comp for c in (0, 1) for t in own[c] if t >= 0), own
     assert all(t not in comp for c in (2, 3) for t in own[c] if t >= 0), own
+    assert e.check() == ""
+
+
+def test_crowded_regions_split_by_xcd_blocks_with_class_budget_2():
+    """class_budget = 2: a class region with more tenants than SEs is split
+    by blocks of whole XCDs (3 GEMMs on SEs {0,1}: 3+3+2 XCDs; 4 streams on
+    SEs {2,3}: 2 XCDs each) -- nothing is time-shared."""
+    e, parts = _engine(class_budget=2)
+    gs = [e.tenant_create(f"g{i}", nslots=32) for i in range(3)]
+    ms = [e.tenant_create(f"m{i}", nslots=32) for i in range(4)]
+    rates = {**{t: COMPUTE for t in gs}, **{t: MEMORY for t in ms}}
+    for t in rates:
+        e.wake(t)
+    _settle(e, rates, 800)
+    owners = {p: e.partition_info(p)["curr_tenant"] for p in range(len(parts))}
+    for p, (_, x, c) in enumerate(parts):
+        assert owners[p] in (gs if c < 2 else ms), (p, owners[p])
+    xcds = {t: sorted({parts[p][1] for p in owners if owners[p] == t}) for t in rates}
+    assert sorted(len(xcds[t]) for t in gs) == [2, 3, 3], xcds
+    assert all(len(xcds[t]) == 2 for t in ms), xcds
+    assert sorted(_online(e, t) for t in gs) == [4, 6, 6]
+    # every tenant runs all the time on its own partitions
+    base = {t: e.tenant_info(t).run_ns for t in rates}
+    t0 = e.now()
+    _settle(e, rates, 300)
+    dt = e.now() - t0
+    for t in rates:
+        share = (e.tenant_info(t).run_ns - base[t]) / dt
+        assert abs(share - _online(e, t)) < 0.2, (t, share, _online(e, t))
     assert e.check() == ""
