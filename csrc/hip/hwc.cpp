@@ -29,12 +29,13 @@ namespace {
 constexpr int kX = 8;  // XCDs per MI355X
 constexpr int kSe = 4; // shader engines per XCD
 constexpr int kSlots = 4;
-// The lean set (pbs_amd/counters/hwc.py LEAN_SPEC): a sample's cost grows
-// with the records it returns and the TCC (memory-path) counters perturb the
-// tenants most (scripts/hwc_cost.py).
+// The lean2 set (pbs_amd/counters/hwc.py LEAN2_SPEC): a sample's cost grows
+// with the records it returns (SQ: one per SE, TCP: one per CU, TCC: one per
+// channel), so the L2-request shares come from SQ memory instructions per SE
+// instead of TCP requests per CU (scripts/hwc_cost.py).
 constexpr const char* kDefaultSpec =
-    "SQ_INSTS_VALU+SQ_INSTS_VMEM_RD+SQ_INSTS_VMEM_WR+SQ_INSTS_VALU_MFMA_MOPS_BF16|SQ_BUSY_CYCLES|"
-    "TCP_TCC_READ_REQ|TCC_MISS";
+    "SQ_INSTS_VALU+SQ_INSTS_SALU+SQ_INSTS_VALU_MFMA_MOPS_BF16|SQ_BUSY_CYCLES|"
+    "SQ_INSTS_VMEM_RD+SQ_INSTS_VMEM_WR|TCC_MISS";
 
 struct Hwc {
   rocprofiler_context_id_t ctx{};

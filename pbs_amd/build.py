@@ -48,13 +48,34 @@ def _stale(target, deps):
 
 
 def _digest(deps, extra=""):
+    """Content hash of the dependencies, keyed by their path RELATIVE to the
+    repo: the same tree hashes the same wherever it is checked out (the GPU
+    box runs a copy under another root and must not rebuild)."""
     import hashlib
     h = hashlib.sha1(extra.encode())
-    for d in sorted(deps):
-        h.update(d.encode())
+    for d in sorted(deps, key=lambda x: os.path.relpath(x, ROOT)):
+        h.update(os.path.relpath(d, ROOT).encode())
         with open(d, "rb") as f:
             h.update(f.read())
     return h.hexdigest()
+
+
+class _BuildLock:
+    """Inter-process lock around a build (torchrun ranks and test
+    subprocesses load the libraries at the same time; two concurrent builds
+    sharing one object directory could link a half-written object)."""
+
+    def __enter__(self):
+        import fcntl
+        os.makedirs(LIBDIR, exist_ok=True)
+        self.f = open(os.path.join(LIBDIR, ".build.lock"), "w")
+        fcntl.flock(self.f, fcntl.LOCK_EX)
+        return self
+
+    def __exit__(self, *a):
+        import fcntl
+        fcntl.flock(self.f, fcntl.LOCK_UN)
+        self.f.close()
 
 
 def _lib_stale(target, deps, extra=""):
@@ -112,6 +133,11 @@ def _compile_parallel(jobs, verbose):
 
 def build_core(verbose=False, sanitize: str | None = None):
     """Build libgpbs.so.  sanitize in {None, 'address', 'thread', 'undefined'}."""
+    with _BuildLock():
+        return _build_core(verbose, sanitize)
+
+
+def _build_core(verbose=False, sanitize: str | None = None):
     os.makedirs(LIBDIR, exist_ok=True)
     srcs = _srcs(CORE_DIRS, [".cpp"])
     name = "libgpbs.so" if not sanitize else f"libgpbs_{sanitize}.so"
@@ -149,6 +175,11 @@ def hipcc():
 def build_hip(verbose=False):
     """Build libgpbs_hip.so for gfx950 (cross-compiles without a GPU)."""
     core = build_core(verbose)
+    with _BuildLock():
+        return _build_hip(verbose)
+
+
+def _build_hip(verbose=False):
     srcs = _srcs([HIP_DIR], [".hip", ".cpp"])
     if not srcs:
         return None

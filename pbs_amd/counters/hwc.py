@@ -21,7 +21,7 @@ from .. import _native as N
 
 # PBS slots INST | CYCLES | LLC_REFS | LLC_MISSES on gfx950 (csrc/hip/hwc.cpp):
 # SQ/TCP counters resolve per shader engine, TCC per XCD.
-# "lean" (default since round 3): 5 SQ + 1 TCP + 1 TCC counters.  A device-
+# "lean": 5 SQ + 1 TCP + 1 TCC counters.  A device-
 # counting sample's cost grows with the counter RECORDS it returns (SQ: one per
 # SE, TCP: one per CU, TCC: one per channel) and the memory-path (TCC) ones
 # perturb the tenants most; measured with a backlogged GEMM alone
@@ -33,8 +33,16 @@ LEAN_SPEC = ("SQ_INSTS_VALU+SQ_INSTS_VMEM_RD+SQ_INSTS_VMEM_WR+SQ_INSTS_VALU_MFMA
 FULL_SPEC = ("SQ_INSTS_VALU+SQ_INSTS_SALU+SQ_INSTS_VMEM_RD+SQ_INSTS_VMEM_WR+SQ_INSTS_LDS+"
              "SQ_INSTS_VALU_MFMA_MOPS_BF16|SQ_BUSY_CYCLES|"
              "TCP_TCC_READ_REQ+TCP_TCC_WRITE_REQ|TCC_MISS")
-SPECS = {"lean": LEAN_SPEC, "full": FULL_SPEC}
-DEFAULT_SPEC = LEAN_SPEC
+# "lean2": L2 request shares from SQ memory instructions (per SE) instead of
+# TCP requests (per CU): 6 SQ + 1 TCC counters, no TCP
+LEAN2_SPEC = ("SQ_INSTS_VALU+SQ_INSTS_SALU+SQ_INSTS_VALU_MFMA_MOPS_BF16|SQ_BUSY_CYCLES|"
+              "SQ_INSTS_VMEM_RD+SQ_INSTS_VMEM_WR|TCC_MISS")
+SPECS = {"lean": LEAN_SPEC, "full": FULL_SPEC, "lean2": LEAN2_SPEC}
+# Measured on one MI355X, 4-tenant mix, gpbs vs the same layout without a
+# sampler (profiles/r3/sampler_ab.md): lean at 1 ms -5 %, lean at 4 ms
+# -0.5 %, lean2 at 1 ms -2 % (131 us per sample).  Default: lean2, with the
+# runtime's duty-cycle cap stretching the period to ~20 sample times.
+DEFAULT_SPEC = LEAN2_SPEC
 XCDS = 8
 
 

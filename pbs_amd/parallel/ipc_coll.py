@@ -80,6 +80,13 @@ class IpcColl:
             raise RuntimeError("gpbs_coll_copy failed")
         return t
 
+    def flags(self):
+        """This rank's flag words: word s = units rank s has finished (diagnostics)."""
+        t = torch.zeros(8, dtype=torch.int32, device=torch.device("cuda", self.device))
+        if self.L.gpbs_coll_copy(self.h, 2, C.c_void_p(t.data_ptr()), 32, 0):
+            raise RuntimeError("gpbs_coll_copy failed")
+        return t.cpu().tolist()[:self.world]
+
     def close(self):
         if getattr(self, "h", None):
             self.L.gpbs_coll_destroy(self.h)

@@ -64,7 +64,13 @@ time.sleep(0.02 * (rank + 1))
 ctx.set_owners([-1] * (XCDS * CTX))
 time.sleep(0.05)
 ctx.set_owners(mine)
-r.wait(120)
+try:
+    r.wait(20)
+except Exception as ex:
+    st = r.stats()
+    print(f"rank {rank} stuck: units {st.units_done} submitted {st.submitted} launches {st.launches} "
+          f"relaunches {st.relaunches} waits_owner {st.waits_owner} owners {ctx.owners()[:8]}", file=sys.stderr, flush=True)
+    raise
 st = r.stats()
 out["units"] = st.units_done
 out["relaunches"] = st.relaunches
@@ -105,7 +111,7 @@ def test_ipc_allreduce_two_processes_exact_and_gated():
                    MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
         procs.append(subprocess.Popen([sys.executable, "-c", CODE % {"root": ROOT}], env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.PIPE, text=True))
-    outs = []
+    outs, logs = [], []
     for p in procs:
         try:
             so, se = p.communicate(timeout=150)
@@ -113,7 +119,9 @@ def test_ipc_allreduce_two_processes_exact_and_gated():
             for q in procs:
                 q.kill()
             raise
-        assert p.returncode == 0, so[-2000:] + se[-4000:]
+        logs.append((p.returncode, so, se))
+    for rank, (rc, so, se) in enumerate(logs):
+        assert rc == 0, "\n".join(f"--- rank {r} rc={c}\n{o[-1500:]}\n{e[-3000:]}" for r, (c, o, e) in enumerate(logs))
         outs.append(json.loads([x for x in so.splitlines() if x.startswith("RESULT ")][-1][7:]))
     print(json.dumps(outs, indent=1))
     for o in outs:
