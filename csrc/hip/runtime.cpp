@@ -292,6 +292,9 @@ struct GpuCtx {
   // Measured on the 4-tenant mix: a 25 % duty (lean set, 1.15 ms) cost the
   // flagship 5 % of its aggregate, 5 % duty (4 ms) 0.5 %.
   int hwc_duty_pct = 5;  // GPBS_HWC_DUTY
+  int hwc_burst_ms = 20;  // GPBS_HWC_BURST_MS: 1 ms hardware sampling after a trigger
+  std::atomic<uint64_t> hwc_triggers{0};
+  uint64_t hwc_burst_samples = 0;
   double hwc_dt_ewma = 0;
   int64_t hwc_period_sum_ns = 0;
   std::atomic<uint64_t> hwc_slow_samples{0};
@@ -524,66 +527,107 @@ void share_update(GpuCtx* c) {
   if (want != was) c->share.store(want, std::memory_order_release);
 }
 
+inline u64 dpos(u64 a, u64 b) { return a >= b ? a - b : 0; }  // Q5: a counter reset is no negative delta
+
+// Sampler thread.  Every hwc_period_us (1 ms) it reads the modeled per-tile
+// counter block (a 16 KiB device-to-host copy: no command-processor work) and
+// watches each tenant's modeled miss rate; a HARDWARE sample -- which stalls
+// the command processor for its duration and perturbs the tenants -- is taken
+//   * in a burst, every tick, for burst_ms after a trigger: an owner change
+//     in the partition table, or a tenant whose modeled miss rate moved by
+//     more than 3x (a phase change), so the classifier sees the change at
+//     1 ms resolution;
+//   * otherwise when the duty-cycle cap allows (sample time <= hwc_duty_pct %
+//     of the time), which bounds what steady-state sampling costs.
+// Classification and PBS decisions use the hardware counters only; the
+// modeled counters are the trigger.
 void hwc_loop(GpuCtx* c) {
   hipSetDevice(c->device);
   constexpr int kBlk = kMaxTenants * kXcds * kNumPmc;
   constexpr int kOwn = kMaxTenants * kXcds * kCtx;
   std::vector<u64> blk(kBlk), se(kXcds * kCtx * kNumPmc), xs(kXcds * kNumPmc);
+  std::vector<u64> watch_prev(kBlk, 0);
+  std::vector<double> watch_rate(kMaxTenants, -1.0);
   std::vector<int64_t> own(kOwn);
   roctxNameOsThread("gpbs-hwc-sampler");
-  constexpr int64_t kSteadyNs = 20000000;  // no owner change for 20 ms: back off
+  constexpr int64_t kSteadyNs = 20000000;  // slow_us back-off: no owner change for 20 ms
   uint64_t last_sw = c->flushes.load();
-  int64_t last_change = mono_ns();
+  int64_t last_change = mono_ns(), last_hw = 0, burst_until = mono_ns() + (int64_t)c->hwc_burst_ms * 1000000;
+  bool watch_primed = false;
   while (!c->hwc_stop.load(std::memory_order_acquire)) {
     const int64_t t0 = mono_ns();
-    RoctxRange rr("gpbs:hwc_sample");
+    const int64_t tick = (int64_t)c->hwc_period_us * 1000;
+    // 1. watch: the modeled block
     if (hipMemcpyAsync(c->h_blk, c->d_cnt, sizeof(u64) * kBlk, hipMemcpyDeviceToHost, c->hwc_stream) != hipSuccess)
       break;
     hipEventRecord(c->blk_ev, c->hwc_stream);
-    const int rc = gpbs_hwc_sample_se(reinterpret_cast<uint64_t*>(se.data()), reinterpret_cast<uint64_t*>(xs.data()));
-    {
-      std::lock_guard<std::mutex> g(c->mu);
-      own_snapshot_locked(c, own.data());
-    }
-    share_update(c);  // the interval just sampled: shared time counted up to now
     hipEventSynchronize(c->blk_ev);
-    if (rc >= 0) {
-      std::memcpy(blk.data(), c->h_blk, sizeof(u64) * kBlk);
-      std::lock_guard<std::mutex> g(c->snap_mu);
-      c->snap_blk.swap(blk);
-      c->snap_se.swap(se);
-      c->snap_x.swap(xs);
-      c->snap_own.swap(own);
-      c->snap_share = c->share_ns;
-      c->snap_seq++;
-      const int64_t dt = mono_ns() - t0;
-      c->hwc_ns += dt;
-      if (dt > c->hwc_ns_max) c->hwc_ns_max = dt;
-      c->hwc_samples++;
+    std::memcpy(blk.data(), c->h_blk, sizeof(u64) * kBlk);
+    bool trig = false;
+    for (int t = 0; t < kMaxTenants; ++t) {
+      u64 di = 0, dm = 0;
+      for (int x = 0; x < kXcds; ++x) {
+        const size_t i = ((size_t)t * kXcds + x) * kNumPmc;
+        di += dpos(blk[i], watch_prev[i]);
+        dm += dpos(blk[i + 3], watch_prev[i + 3]);
+      }
+      if (di < 1000000) continue;  // too little work in this tick to judge
+      const double r = (double)(dm + 1) / (double)di;
+      if (watch_primed && watch_rate[t] > 0 && (r > 3.0 * watch_rate[t] || r * 3.0 < watch_rate[t])) trig = true;
+      watch_rate[t] = watch_rate[t] > 0 ? 0.5 * watch_rate[t] + 0.5 * r : r;
     }
+    watch_prev.swap(blk);
+    blk = watch_prev;  // keep a copy for the snapshot below
+    watch_primed = true;
     const uint64_t sw = c->flushes.load(std::memory_order_relaxed);  // table publishes that changed an owner
-    const int64_t now = mono_ns();
-    if (sw != last_sw) last_change = now;
+    if (sw != last_sw) {
+      last_change = t0;
+      trig = true;
+    }
     last_sw = sw;
-    const bool slow = c->hwc_slow_us > c->hwc_period_us && now - last_change >= kSteadyNs;
-    if (slow) c->hwc_slow_samples.fetch_add(1, std::memory_order_relaxed);
-    int64_t period = (int64_t)(slow ? c->hwc_slow_us : c->hwc_period_us) * 1000;
-    if (rc >= 0) {
-      const double dt = (double)(now - t0);
-      c->hwc_dt_ewma = c->hwc_dt_ewma > 0 ? 0.875 * c->hwc_dt_ewma + 0.125 * dt : dt;
+    if (trig) {
+      burst_until = t0 + (int64_t)c->hwc_burst_ms * 1000000;
+      c->hwc_triggers.fetch_add(1, std::memory_order_relaxed);
     }
-    if (c->hwc_duty_pct > 0)
-      period = std::max(period, (int64_t)(c->hwc_dt_ewma * 100.0 / c->hwc_duty_pct));
-    {
-      std::lock_guard<std::mutex> g(c->snap_mu);
-      c->hwc_period_sum_ns += period;
+    // 2. hardware sample: in a burst every tick, else at the duty-capped /
+    //    back-off period
+    const bool slow = c->hwc_slow_us > c->hwc_period_us && t0 - last_change >= kSteadyNs;
+    int64_t period = slow ? (int64_t)c->hwc_slow_us * 1000 : tick;
+    if (c->hwc_duty_pct > 0) period = std::max(period, (int64_t)(c->hwc_dt_ewma * 100.0 / c->hwc_duty_pct));
+    const bool burst = t0 < burst_until;
+    if (burst || t0 - last_hw >= period - tick / 4) {
+      RoctxRange rr("gpbs:hwc_sample");
+      const int64_t s0 = mono_ns();
+      const int rc = gpbs_hwc_sample_se(reinterpret_cast<uint64_t*>(se.data()), reinterpret_cast<uint64_t*>(xs.data()));
+      {
+        std::lock_guard<std::mutex> g(c->mu);
+        own_snapshot_locked(c, own.data());
+      }
+      share_update(c);  // the interval just sampled: shared time counted up to now
+      if (rc >= 0) {
+        const int64_t dt = mono_ns() - s0;
+        c->hwc_dt_ewma = c->hwc_dt_ewma > 0 ? 0.875 * c->hwc_dt_ewma + 0.125 * (double)dt : (double)dt;
+        std::lock_guard<std::mutex> g(c->snap_mu);
+        c->snap_blk.swap(blk);
+        c->snap_se.swap(se);
+        c->snap_x.swap(xs);
+        c->snap_own.swap(own);
+        c->snap_share = c->share_ns;
+        c->snap_seq++;
+        c->hwc_ns += dt;
+        if (dt > c->hwc_ns_max) c->hwc_ns_max = dt;
+        c->hwc_samples++;
+        c->hwc_period_sum_ns += last_hw ? s0 - last_hw : tick;
+        if (burst) c->hwc_burst_samples++;
+        if (slow) c->hwc_slow_samples.fetch_add(1, std::memory_order_relaxed);
+      }
+      last_hw = s0;
     }
-    const int64_t rest = period - (mono_ns() - t0);
+    const int64_t rest = tick - (mono_ns() - t0);
     if (rest > 0) std::this_thread::sleep_for(std::chrono::nanoseconds(rest));
   }
 }
 
-inline u64 dpos(u64 a, u64 b) { return a >= b ? a - b : 0; }  // Q5: a counter reset is no negative delta
 
 // Fold one attribution result into the per-tenant totals and the pending
 // metric deltas (snap_mu held).
@@ -1289,6 +1333,7 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
   if (const char* v = std::getenv("GPBS_HWC_PERIOD_US")) c->hwc_period_us = std::max(100, std::atoi(v));
   if (const char* v = std::getenv("GPBS_HWC_SLOW_US")) c->hwc_slow_us = std::max(0, std::atoi(v));
   if (const char* v = std::getenv("GPBS_HWC_DUTY")) c->hwc_duty_pct = std::max(0, std::min(100, std::atoi(v)));
+  if (const char* v = std::getenv("GPBS_HWC_BURST_MS")) c->hwc_burst_ms = std::max(0, std::atoi(v));
   if (const char* v = std::getenv("GPBS_SHARE_PROBE")) {
     c->probe_every = std::max(0, std::atoi(v));
     if (const char* k = std::strchr(v, ':')) c->probe_len = std::max(0, std::atoi(k + 1));
@@ -1695,6 +1740,8 @@ int gpbs_gpu_hwc_reset(void* p) {
   c->hwc_samples = 0;
   c->hwc_slow_samples = 0;
   c->hwc_period_sum_ns = 0;
+  c->hwc_burst_samples = 0;
+  c->hwc_triggers = 0;
   return 0;
 }
 
@@ -1708,6 +1755,17 @@ int gpbs_gpu_hwc_period(void* p, int fast_us, int slow_us, uint64_t* slow_sample
   if (slow_us >= 0) c->hwc_slow_us = slow_us;
   if (slow_samples) *slow_samples = c->hwc_slow_samples;
   return 0;
+}
+
+// Burst statistics since the last hwc reset: triggers (owner changes and
+// modeled phase changes) and hardware samples taken in bursts.
+int gpbs_gpu_hwc_bursts(void* p, uint64_t* triggers, uint64_t* burst_samples) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c) return -22;
+  std::lock_guard<std::mutex> g(c->snap_mu);
+  if (triggers) *triggers = c->hwc_triggers.load();
+  if (burst_samples) *burst_samples = c->hwc_burst_samples;
+  return c->hwc_burst_ms;
 }
 
 // Duty-cycle cap (percent, < 0 leaves it; 0 off); *mean_period_ns = mean

@@ -159,8 +159,11 @@ class GpuContext:
         dev = self.L.gpbs_gpu_hwc_attr_stats(self.h, C.byref(la), C.byref(bs), C.byref(ho))
         mp = C.c_uint64(0)
         duty = self.L.gpbs_gpu_hwc_duty(self.h, -1, C.byref(mp))
+        tr, bsm = C.c_uint64(0), C.c_uint64(0)
+        self.L.gpbs_gpu_hwc_bursts(self.h, C.byref(tr), C.byref(bsm))
         return {"attr_device": bool(dev), "attr_kernel_launches": la.value, "attr_busy_skips": bs.value,
                 "attr_host": ho.value, "duty_cap_pct": duty, "mean_period_us": round(mp.value / 1e3, 1),
+                "burst_triggers": tr.value, "burst_samples": bsm.value,
                 "samples": n.value, "slow_samples": slow.value, "mean_sample_us": round(ns.value / 1e3, 1), "max_sample_us": round(mx.value / 1e3, 1),
                 "hw_over_model": [round(x, 4) for x in r],
                 "unattributed_frac": [round(x, 4) for x in u],

@@ -16,9 +16,11 @@ run() {  # run NAME [ENV=VAL ...] -- [bench args]
 }
 for v in ${VARIANTS:-lean1ms lean4ms lean2 model}; do
   case $v in
-    lean1ms) run lean1ms GPBS_HWC_SPEC=lean ;;
-    lean4ms) run lean4ms GPBS_HWC_SPEC=lean GPBS_HWC_PERIOD_US=4000 ;;
-    lean2)   run lean2 GPBS_HWC_SPEC=lean2 ;;
+    lean1ms) run lean1ms GPBS_HWC_SPEC=lean GPBS_HWC_DUTY=0 ;;
+    lean2_1ms) run lean2_1ms GPBS_HWC_SPEC=lean2 GPBS_HWC_DUTY=0 ;;
+    default) run default ;;
+    lean4ms) run lean4ms GPBS_HWC_SPEC=lean GPBS_HWC_PERIOD_US=4000 GPBS_HWC_DUTY=0 ;;
+    lean2)   run lean2 GPBS_HWC_SPEC=lean2 GPBS_HWC_DUTY=0 ;;
     full1ms) run full1ms GPBS_HWC_SPEC=full ;;
     model)   run model GPBS_HWC_SPEC=lean -- --counters model ;;
   esac

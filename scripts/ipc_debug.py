@@ -35,6 +35,23 @@ ok = ok and step("gated se23 x20", 20)
 if ok:
     ctx.set_owners([1] * (XCDS * CTX))
     ok = step("gated all x20", 20)
+if ok:  # revocation mid-run: rank r revokes every SE after (r + 1) x 20 ms for 50 ms
+    ctx.set_owners(mine)
+    dist.barrier()
+    t0 = time.perf_counter()
+    r.submit(40)
+    time.sleep(0.02 * (rank + 1))
+    ctx.set_owners([-1] * (XCDS * CTX))
+    log("revoked", r.stats().units_done, coll.flags())
+    time.sleep(0.05)
+    ctx.set_owners(mine)
+    log("restored", r.stats().units_done, coll.flags())
+    try:
+        r.wait(15)
+    except Exception as ex:
+        ok = False
+    st = r.stats()
+    log("revocation", "ok" if ok else "FAIL", f"units {st.units_done} launches {st.launches} relaunches {st.relaunches} flags {coll.flags()}")
 log("done", ok)
 r.close(); coll.close(); ctx.close()
 dist.barrier()
