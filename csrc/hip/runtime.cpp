@@ -293,6 +293,8 @@ struct GpuCtx {
   // flagship 5 % of its aggregate, 5 % duty (4 ms) 0.5 %.
   int hwc_duty_pct = 5;  // GPBS_HWC_DUTY
   int hwc_burst_ms = 20;  // GPBS_HWC_BURST_MS: 1 ms hardware sampling after a trigger
+  int hwc_watch = 1;      // GPBS_HWC_WATCH: read the modeled block every tick (the burst trigger)
+  int64_t hwc_next_period_ns = 1000000;
   std::atomic<uint64_t> hwc_triggers{0};
   uint64_t hwc_burst_samples = 0;
   double hwc_dt_ewma = 0;
@@ -557,12 +559,17 @@ void hwc_loop(GpuCtx* c) {
   while (!c->hwc_stop.load(std::memory_order_acquire)) {
     const int64_t t0 = mono_ns();
     const int64_t tick = (int64_t)c->hwc_period_us * 1000;
-    // 1. watch: the modeled block
-    if (hipMemcpyAsync(c->h_blk, c->d_cnt, sizeof(u64) * kBlk, hipMemcpyDeviceToHost, c->hwc_stream) != hipSuccess)
-      break;
-    hipEventRecord(c->blk_ev, c->hwc_stream);
-    hipEventSynchronize(c->blk_ev);
-    std::memcpy(blk.data(), c->h_blk, sizeof(u64) * kBlk);
+    // 1. watch: the modeled block (every tick with the watch on, else only
+    //    with a hardware sample)
+    const uint64_t sw = c->flushes.load(std::memory_order_relaxed);  // table publishes that changed an owner
+    const bool due_hw = sw != last_sw || t0 < burst_until || t0 - last_hw >= c->hwc_next_period_ns - tick / 4;
+    if (c->hwc_watch || due_hw) {
+      if (hipMemcpyAsync(c->h_blk, c->d_cnt, sizeof(u64) * kBlk, hipMemcpyDeviceToHost, c->hwc_stream) != hipSuccess)
+        break;
+      hipEventRecord(c->blk_ev, c->hwc_stream);
+      hipEventSynchronize(c->blk_ev);
+      std::memcpy(blk.data(), c->h_blk, sizeof(u64) * kBlk);
+    }
     bool trig = false;
     for (int t = 0; t < kMaxTenants; ++t) {
       u64 di = 0, dm = 0;
@@ -579,7 +586,6 @@ void hwc_loop(GpuCtx* c) {
     watch_prev.swap(blk);
     blk = watch_prev;  // keep a copy for the snapshot below
     watch_primed = true;
-    const uint64_t sw = c->flushes.load(std::memory_order_relaxed);  // table publishes that changed an owner
     if (sw != last_sw) {
       last_change = t0;
       trig = true;
@@ -594,6 +600,7 @@ void hwc_loop(GpuCtx* c) {
     const bool slow = c->hwc_slow_us > c->hwc_period_us && t0 - last_change >= kSteadyNs;
     int64_t period = slow ? (int64_t)c->hwc_slow_us * 1000 : tick;
     if (c->hwc_duty_pct > 0) period = std::max(period, (int64_t)(c->hwc_dt_ewma * 100.0 / c->hwc_duty_pct));
+    c->hwc_next_period_ns = period;
     const bool burst = t0 < burst_until;
     if (burst || t0 - last_hw >= period - tick / 4) {
       RoctxRange rr("gpbs:hwc_sample");
@@ -1334,6 +1341,7 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
   if (const char* v = std::getenv("GPBS_HWC_SLOW_US")) c->hwc_slow_us = std::max(0, std::atoi(v));
   if (const char* v = std::getenv("GPBS_HWC_DUTY")) c->hwc_duty_pct = std::max(0, std::min(100, std::atoi(v)));
   if (const char* v = std::getenv("GPBS_HWC_BURST_MS")) c->hwc_burst_ms = std::max(0, std::atoi(v));
+  if (const char* v = std::getenv("GPBS_HWC_WATCH")) c->hwc_watch = std::atoi(v) != 0;
   if (const char* v = std::getenv("GPBS_SHARE_PROBE")) {
     c->probe_every = std::max(0, std::atoi(v));
     if (const char* k = std::strchr(v, ':')) c->probe_len = std::max(0, std::atoi(k + 1));
@@ -2227,8 +2235,14 @@ void* gpbs_coll_create(int device, int rank, int world, unsigned long long bytes
   c->rank = rank;
   c->world = world;
   c->bytes = bytes;
+  // Flag words in UNCACHED device memory: they are written by other ranks
+  // (over xGMI, or from another process on the same GPU) and polled by
+  // workgroups on every XCD, and a coarse-grained line can sit stale in an
+  // XCD's L2 (measured: a barrier polled a value the host read as updated for
+  // 3 s until its timeout).
   bool ok = hipMalloc(&c->in, bytes) == hipSuccess && hipMalloc(&c->out, bytes) == hipSuccess &&
-            hipMalloc((void**)&c->flags, 4096) == hipSuccess && hipMemset(c->flags, 0, 4096) == hipSuccess &&
+            hipExtMallocWithFlags((void**)&c->flags, 4096, hipDeviceMallocUncached) == hipSuccess &&
+            hipMemset(c->flags, 0, 4096) == hipSuccess &&
             hipMemset(c->out, 0, bytes) == hipSuccess && hipMalloc(&c->d_desc, sizeof(CollDescHost)) == hipSuccess;
   if (!ok) {
     if (c->in) hipFree(c->in);

@@ -39,11 +39,12 @@ if ok:  # revocation mid-run: rank r revokes every SE after (r + 1) x 20 ms for 
     ctx.set_owners(mine)
     dist.barrier()
     t0 = time.perf_counter()
-    r.submit(40)
-    time.sleep(0.02 * (rank + 1))
+    r.submit(400)
+    time.sleep(0.002 * (rank + 1))
     ctx.set_owners([-1] * (XCDS * CTX))
     log("revoked", r.stats().units_done, coll.flags())
     time.sleep(0.05)
+    log("before restore", r.stats().units_done, r.stats().relaunches, coll.flags())
     ctx.set_owners(mine)
     log("restored", r.stats().units_done, coll.flags())
     try:
