@@ -291,7 +291,7 @@ struct GpuCtx {
   // (EWMA of the sample duration); 0 disables the cap.
   // Measured on the 4-tenant mix: a 25 % duty (lean set, 1.15 ms) cost the
   // flagship 5 % of its aggregate, 5 % duty (4 ms) 0.5 %.
-  int hwc_duty_pct = 5;  // GPBS_HWC_DUTY
+  int hwc_duty_pct = 2;  // GPBS_HWC_DUTY (profiles/r3/cmp_4mix_*: 5 % costs 0.01 of aggregate, 2 % 0.005)
   int hwc_burst_ms = 20;  // GPBS_HWC_BURST_MS: 1 ms hardware sampling after a trigger
   int hwc_watch = 1;      // GPBS_HWC_WATCH: read the modeled block every tick (the burst trigger)
   int64_t hwc_next_period_ns = 1000000;

@@ -239,19 +239,37 @@ __device__ __forceinline__ int g2_swz(int r) { return (r >> 1) & 7; }
 // and k3 (A halves) -- the earliest the WAR rule allows -- and the k3 wait is
 // vmcnt(8), so a whole K-tile stays in flight for four phases (DEEP = 0: one
 // half per phase, vmcnt(4), lead 2-6 phases).
-template <int DEEP>
+// STAMP = 1: diagnostic build (host opts bit 6, never the default) -- lane 0
+// of every wave records s_memtime after each barrier of K-tiles
+// kStampT0 .. kStampT0 + kStampTiles - 1 into spare LDS (so no vector-memory
+// op perturbs the counted vmcnt waits) and copies them to g_gemm_dbg after
+// the unit: [wg < kStampWgs][wave][tile][slot], slot 0 = tile start, 1..8 =
+// after the tile's 8 barriers, 9 = s_memrealtime at the tile start (100 MHz).
+constexpr int kStampT0 = 8, kStampTiles = 16, kStampSlots = 10, kStampWgs = 64;
+__device__ u32* g_gemm_dbg;
+
+template <int DEEP, int STAMP = 0>
 __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restrict__ A, const u16* __restrict__ Bt,
                                                              u16* __restrict__ C, int M, int N, int K, WorkQueue* q,
                                                              const PartTable* table, u32 mode, u32 me, u64* cnt,
                                                              u32 inst_per_tile, u32 refs_per_tile, u32 miss_per_tile,
                                                              u32* status) {
-  __shared__ __attribute__((aligned(16))) char smem[kG2Lds + 16];
+  constexpr int kStampLds = STAMP ? 8 * kStampTiles * kStampSlots * 4 : 0;
+  __shared__ __attribute__((aligned(16))) char smem[kG2Lds + 16 + kStampLds];
   lds_t* lds = (lds_t*)smem;
   int* s_slot = (int*)(smem + kG2Lds);
   const u32 xcc = xcc_id();
   u64 t_last = __builtin_amdgcn_s_memtime();
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 2, wc = wid & 3;
+  u32* st_lds = (u32*)(smem + kG2Lds + 16) + wid * kStampTiles * kStampSlots;
+  auto stamp = [&](int t, int slot) {
+    if constexpr (STAMP) {
+      if (lane == 0 && t >= kStampT0 && t < kStampT0 + kStampTiles)
+        st_lds[(t - kStampT0) * kStampSlots + slot] =
+            slot == 9 ? (u32)__builtin_amdgcn_s_memrealtime() : (u32)__builtin_amdgcn_s_memtime();
+    }
+  };
   const int tiles_m = M / G2_BM, tiles_n = N / G2_BM, ntiles = tiles_m * tiles_n;
   const int nt = K / G2_BK;
 
@@ -332,6 +350,8 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restr
     bf16x8 a[4][2], b0[2][2], b1[2][2];
     for (int t = 0; t < nt; ++t) {
       const int buf = t & 1;
+      stamp(t, 9);
+      stamp(t, 0);
       // ---- k0: quadrant (mi 0, ni 0)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
@@ -346,6 +366,7 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restr
       if (DEEP >= 2) stage(0, 0, t + 1);
       if (DEEP == 3) stage(0, 1, t + 1);  // both A halves of t+1 as early as the 2-phase WAR rule allows
       __builtin_amdgcn_s_barrier();
+      stamp(t, 1);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -357,6 +378,7 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restr
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[j][s], a[i][s], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_s_barrier();
+      stamp(t, 2);
       // ---- k1: quadrant (mi 0, ni 1)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
@@ -364,6 +386,7 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restr
         for (int s = 0; s < 2; ++s) b1[j][s] = frag(buf, 1, bh, bc + 32 + j * 16, s);
       if (DEEP == 0 || DEEP == 2) stage(0, 1, t + 1);
       __builtin_amdgcn_s_barrier();
+      stamp(t, 3);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -375,6 +398,7 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restr
             acc[i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j][s], a[i][s], acc[i][2 + j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_s_barrier();
+      stamp(t, 4);
       // ---- k2: quadrant (mi 1, ni 1)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -383,6 +407,7 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restr
       if (DEEP < 2) stage(1, 0, t + 2);
       if (DEEP == 1) stage(1, 1, t + 2);
       __builtin_amdgcn_s_barrier();
+      stamp(t, 5);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -394,6 +419,7 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restr
             acc[4 + i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j][s], a[i][s], acc[4 + i][2 + j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_s_barrier();
+      stamp(t, 6);
       // ---- k3: quadrant (mi 1, ni 0); retire tile t+1
       if (DEEP >= 2) {
         stage(1, 0, t + 2);
@@ -411,6 +437,7 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restr
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       __builtin_amdgcn_s_barrier();
+      stamp(t, 7);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -421,6 +448,7 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restr
             acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[j][s], a[i][s], acc[4 + i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_s_barrier();
+      stamp(t, 8);
     }
     if (DEEP >= 2 && wr == 0) __builtin_amdgcn_s_barrier();  // re-align the groups
     // Epilogue: mfma(B, A) holds C^T per 16x16 block -- lane owns
@@ -435,6 +463,12 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restr
         const u32 hi = (u32)f2bf(acc[i][j][2]) | ((u32)f2bf(acc[i][j][3]) << 16);
         *(uint2*)(C + (size_t)m * N + n) = make_uint2(lo, hi);
       }
+    if constexpr (STAMP) {
+      if (lane == 0 && blockIdx.x < kStampWgs && nt >= kStampT0 + kStampTiles && g_gemm_dbg) {
+        u32* dst = g_gemm_dbg + ((size_t)blockIdx.x * 8 + wid) * kStampTiles * kStampSlots;
+        for (int i = 0; i < kStampTiles * kStampSlots; ++i) dst[i] = st_lds[i];
+      }
+    }
     count_unit(cnt, me, xcc, inst_per_tile, &t_last, refs_per_tile, miss_per_tile, q);
   }
   finish(q, status, (u32)ntiles);
@@ -789,6 +823,14 @@ int gpbs_hip_set_gemm_opts(int opts) {
   return old;
 }
 
+// Diagnostic: the buffer the STAMP variant (opts bit 6) writes to (device
+// memory, kStampWgs * 8 * kStampTiles * kStampSlots u32); returns its size in
+// u32 words.
+int gpbs_hip_set_gemm_dbg(void* buf) {
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_gemm_dbg), &buf, sizeof(buf)) != hipSuccess) return -5;
+  return kStampWgs * 8 * kStampTiles * kStampSlots;
+}
+
 int gpbs_hip_gemm_units(int M, int N) {
   if (M % G2_BM == 0 && N % G2_BM == 0) return (M / G2_BM) * (N / G2_BM);
   return (M / GBM) * (N / GBN);
@@ -812,7 +854,8 @@ int gpbs_hip_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int
                          (u32*)status);
       return hipGetLastError() == hipSuccess ? 0 : -5;
     }
-    auto kern = (g_gemm_opts & 16)  ? k_gemm256_bf16_tn<3>
+    auto kern = (g_gemm_opts & 64)  ? k_gemm256_bf16_tn<2, 1>
+                : (g_gemm_opts & 16)  ? k_gemm256_bf16_tn<3>
                 : (g_gemm_opts & 4) ? k_gemm256_bf16_tn<2>
                 : (g_gemm_opts & 2) ? k_gemm256_bf16_tn<1>
                                     : k_gemm256_bf16_tn<0>;

@@ -116,6 +116,10 @@ def parse_se_policy(policy: str):
 
 
 _HWC = {"on": False}
+# Names shared with bench.py's mixes: "static-se" is the hand-picked static
+# shader-engine split (decode on SEs {2,3}, trainer on {0,1} of every XCD, the
+# best static point of profiles/llm5/frontier_explore_r2.md).
+ALIASES = {"static-se": "se:2/2"}
 
 
 def _hwc_setup():
@@ -133,6 +137,7 @@ def run(policy: str, kinds, args: dict, seconds: float, warmup: float) -> Dict[s
     daemon = None
     sock = None
     args = dict(args, spatial=policy == "gpbs-spatial")
+    policy = ALIASES.get(policy, policy)
     base = policy.split("@")[0]
     if base.startswith("se:"):  # static SE split; "se:I/T@solo" runs the given kinds alone on their masks
         args["infer_ses"], args["train_ses"] = parse_se_policy(base)
@@ -213,6 +218,8 @@ def main(argv=None):
     pols = [p for p in a.policies.split(",") if p]
     if "gpbs-se" in pols:
         _hwc_setup()
+    if a.out and os.path.exists(a.out):
+        raise SystemExit(f"{a.out} exists: results are never overwritten")
     if "solo" in pols:
         res["solo"] = {}
         for k in ("infer", "train"):

@@ -1,0 +1,88 @@
+"""Per-barrier timing of the tenant GEMM's K loop (diagnostic build, opts bit 6).
+
+Lane 0 of every wave of the first 64 workgroups records s_memtime after each
+of the 8 barriers of K-tiles 8..23 (csrc/hip/tenant_kernels.hip, STAMP);
+this prints, per wave group (wr = 0 / 1, the staggered halves), the median
+cycles of every barrier interval, the cycles per K-tile, the in-kernel clock
+(s_memtime over s_memrealtime) and the MFMA busy fraction they imply
+(2 waves x 64 MFMA x 16 cycles per SIMD per K-tile), next to the TF/s of the
+plain and the stamped build timed in the same process.
+
+    python scripts/gemm_stamps.py [n]
+"""
+import ctypes as C
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from pbs_amd.ops import kernels as K  # noqa: E402
+
+TILES, SLOTS, WGS = 16, 10, 64
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+    L = K.lib()
+    L.gpbs_hip_set_gemm_dbg.restype = C.c_int
+    L.gpbs_hip_set_gemm_dbg.argtypes = [C.c_void_p]
+    s = K._stream()
+    q = K.work_queue()
+    A = torch.rand(n, n, device="cuda", dtype=torch.bfloat16) * 2 - 1
+    B = torch.rand(n, n, device="cuda", dtype=torch.bfloat16) * 2 - 1
+    Cm = torch.empty(n, n, device="cuda", dtype=torch.bfloat16)
+    words = L.gpbs_hip_set_gemm_dbg(None)
+    dbg = torch.zeros(words, device="cuda", dtype=torch.int32)
+    assert L.gpbs_hip_set_gemm_dbg(C.c_void_p(dbg.data_ptr())) == words
+
+    def run(opts, iters=20):
+        L.gpbs_hip_set_gemm_opts(opts)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
+        for a, b in ev:
+            q.zero_()
+            a.record()
+            rc = L.gpbs_hip_gemm_bf16(K._ptr(A), K._ptr(B), K._ptr(Cm), n, n, n, K._ptr(q), None, 0, 0, None, None,
+                                      0, s)
+            assert rc == 0
+            b.record()
+        torch.cuda.synchronize()
+        return sorted(a.elapsed_time(b) for a, b in ev)[iters // 2]
+
+    # warm the clocks, then interleave plain / stamped rounds
+    for _ in range(3):
+        run(4)
+    res = {"plain": [], "stamp": []}
+    for _ in range(5):
+        res["plain"].append(run(4))
+        res["stamp"].append(run(4 | 64))
+    L.gpbs_hip_set_gemm_opts(4)
+    tf = {k: 2 * n ** 3 / (sorted(v)[2]) / 1e9 for k, v in res.items()}
+    ref = A[:256].float() @ B.float().t()
+    err = (Cm[:256].float() - ref).abs().max().item()
+    st = dbg.cpu().numpy().astype(np.uint32).reshape(WGS, 8, TILES, SLOTS).astype(np.int64)
+    cyc = st[..., :9]
+    d = np.diff(cyc, axis=-1) % (1 << 32)            # 8 intervals per tile
+    per_tile = (cyc[..., 8] - cyc[..., 0]) % (1 << 32)
+    real = (st[..., 9] % (1 << 32)).astype(np.int64)
+    # clock: memtime cycles over realtime (100 MHz) across the stamped tiles
+    dc = (cyc[:, :, -1, 0] - cyc[:, :, 0, 0]) % (1 << 32)
+    dr = (real[:, :, -1] - real[:, :, 0]) % (1 << 32)
+    ok = dr > 0
+    ghz = float(np.median(dc[ok] / dr[ok] * 0.1)) if ok.any() else None
+    out = {"n": n, "tflops_plain": round(tf["plain"], 1), "tflops_stamp": round(tf["stamp"], 1),
+           "max_abs_err": round(err, 4), "clock_ghz": round(ghz, 3) if ghz else None}
+    for g in (0, 1):
+        dd = d[:, 4 * g:4 * g + 4]
+        out[f"group{g}_interval_cycles_median"] = [int(np.median(dd[..., k])) for k in range(8)]
+        out[f"group{g}_interval_cycles_p90"] = [int(np.percentile(dd[..., k], 90)) for k in range(8)]
+    pt = float(np.median(per_tile))
+    out["cycles_per_ktile_median"] = int(pt)
+    out["mfma_busy_implied"] = round(2 * 64 * 16 / pt, 3)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
