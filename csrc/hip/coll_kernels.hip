@@ -20,8 +20,14 @@
 //     descheduled stalls its peers -- the symptom gang scheduling removes
 //     (C16), measured by the engine's K10 wait reports.
 // A workgroup that waits while its shader engine is revoked leaves (the
-// runner relaunches the unit later); every wait is bounded by the wall clock,
-// so a dead peer ends the kernel with an error bit instead of a hang.
+// runner relaunches the unit later).  So does one that has waited
+// yield_ticks: a kernel spinning on a peer must not hold the GPU, since when
+// ranks share a device (tests: 2 processes on one GPU) the hardware
+// scheduler time-slices their queues and a resident spinning grid can keep
+// the peer's kernel from ever being dispatched (measured: both ranks stuck
+// until the timeout).  Every wait is bounded by the wall clock, so a dead
+// peer ends the kernel with an error bit instead of a hang; the runner
+// bounds a unit's relaunches by the same timeout.
 #include "common.hpp"
 
 namespace gpbs_hip {
@@ -49,7 +55,7 @@ constexpr int CNT = 256, CU_ = 4;
 
 __global__ __launch_bounds__(CNT) void k_allreduce(const CollDesc* __restrict__ d, u32 seq, u32 chunk8, WorkQueue* q,
                                                    const PartTable* table, u32 mode, u32 me, u64* cnt, u32* status,
-                                                   u64 timeout_ticks) {
+                                                   u64 timeout_ticks, u64 yield_ticks) {
   __shared__ int s_slot[4];
   __shared__ int s_ok;
   const u32 xcc = xcc_id();
@@ -71,8 +77,13 @@ __global__ __launch_bounds__(CNT) void k_allreduce(const CollDesc* __restrict__ 
         ok = 0;  // revoked while waiting: leave, the runner relaunches the unit
         break;
       }
-      if (wall_clock64() - t0 > timeout_ticks) {
+      const u64 el = wall_clock64() - t0;
+      if (el > timeout_ticks) {
         ok = -1;
+        break;
+      }
+      if (el > yield_ticks) {
+        ok = 0;  // give the GPU back; the runner relaunches the unit
         break;
       }
       __builtin_amdgcn_s_sleep(4);
@@ -162,11 +173,13 @@ int gpbs_hip_coll_desc_size(void) { return (int)sizeof(CollDesc); }
 // seq: the unit's collective sequence number (0, 1, ...).
 int gpbs_hip_allreduce(const void* desc, unsigned seq, unsigned long long bytes, unsigned chunk_bytes, void* q,
                        const void* table, unsigned mode, unsigned me, void* cnt, void* status, int grid,
-                       unsigned long long timeout_ticks, hipStream_t s) {
+                       unsigned long long timeout_ticks, unsigned long long yield_ticks, hipStream_t s) {
   if (bytes % 16 || chunk_bytes % 16 || chunk_bytes == 0) return -22;
   if (grid <= 0) grid = 256;
+  if (yield_ticks == 0 || yield_ticks > timeout_ticks) yield_ticks = timeout_ticks;
   hipLaunchKernelGGL(k_allreduce, dim3(grid), dim3(CNT), 0, s, (const CollDesc*)desc, seq, chunk_bytes / 16,
-                     (WorkQueue*)q, (const PartTable*)table, mode, me, (u64*)cnt, (u32*)status, (u64)timeout_ticks);
+                     (WorkQueue*)q, (const PartTable*)table, mode, me, (u64*)cnt, (u32*)status, (u64)timeout_ticks,
+                     (u64)yield_ticks);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

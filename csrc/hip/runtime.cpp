@@ -57,7 +57,7 @@ int gpbs_hip_adapt(void*, const void*, const void*, const void*, int, const gpbs
 int gpbs_hip_switch_probe(const void*, int, unsigned*, int, unsigned, unsigned long long, hipStream_t);
 int gpbs_hip_hwc_attribute(const void*, void*, void*, hipStream_t);
 int gpbs_hip_allreduce(const void*, unsigned, unsigned long long, unsigned, void*, const void*, unsigned, unsigned,
-                       void*, void*, int, unsigned long long, hipStream_t);
+                       void*, void*, int, unsigned long long, unsigned long long, hipStream_t);
 int gpbs_hip_coll_desc_size(void);
 }
 
@@ -319,6 +319,7 @@ struct GpuCtx {
   int64_t own_ns[kMaxTenants][kXcds * kCtx];
   int64_t own_base[kMaxTenants][kXcds * kCtx];
   int64_t last_pub_ns = 0;
+  std::atomic<int64_t> revoke_ns[kMaxTenants] = {};  // last publish that took a partition from the tenant
   hipEvent_t adapt_ev = nullptr;  // device adapt: bounded poll, never a blocking sync
   bool adapt_pending = false;
   // Asynchronous device adapt (engine adapt_launch / adapt_harvest): two
@@ -426,6 +427,10 @@ bool publish_locked(GpuCtx* c) {
         if (o < (u32)kMaxTenants) c->own_ns[o][x] += t - c->last_pub_ns;
       }
     c->last_pub_ns = t;
+    for (int x = 0; x < kXcds * kCtx; ++x) {
+      const u32 o = c->h_table->owner[x] & kOwnerMask;
+      if (o < (u32)kMaxTenants && (c->pending[x] & kOwnerMask) != o) c->revoke_ns[o].store(t, std::memory_order_relaxed);
+    }
     for (int x = 0; x < kXcds * kCtx; ++x) __atomic_store_n(&c->h_table->owner[x], c->pending[x], __ATOMIC_RELEASE);
     c->epoch++;
     __atomic_store_n(&c->h_table->epoch, c->epoch, __ATOMIC_RELEASE);
@@ -954,6 +959,11 @@ typedef struct gpbs_runner_stats {
   int64_t lat_sum_ns, lat_max_ns;
   uint64_t lat_count;
   uint64_t units_alt;  // of units_done: units of the alternate workload
+  // revocation drain: from the table publish that took a partition from this
+  // tenant to the end of the unit it interrupted (the unit's grid has left
+  // every SE; until then the new owner's workgroups queue behind it)
+  int64_t drain_sum_ns, drain_max_ns;
+  uint64_t drain_count;
 } gpbs_runner_stats_t;
 
 }
@@ -1027,12 +1037,14 @@ struct Runner {
   // slot (fresh units take the next one; a relaunch keeps its own)
   u32 q_seq[16] = {};
   u32 coll_seq = 0;
+  int64_t q_t0[16] = {};  // first launch of the unit in each queue slot (all-reduce relaunch bound)
 
   struct Work {
     int kind, M, N, K, chunk;
     unsigned long long bytes;
     void *a, *b, *c;
   };
+  static int coll_timeout_ms(const Work& w) { return w.K > 0 ? w.K : 5000; }
   Work work(int alt) const {
     if (alt && cfg.alt_kind)
       return Work{cfg.alt_kind, cfg.alt_M, cfg.alt_N, cfg.alt_K, cfg.alt_chunk_bytes, cfg.alt_bytes,
@@ -1155,9 +1167,10 @@ struct Runner {
       case K_GEMV:
         return gpbs_hip_gemv_bf16(w.a, w.b, w.c, w.M, w.K, q, tab, mode, me, ctx->d_cnt, &h_status[qi], grid,
                                   stream);
-      case K_ALLREDUCE:  // K = barrier timeout (ms) -> 100 MHz wall-clock ticks
+      case K_ALLREDUCE:  // K = barrier timeout (ms) -> 100 MHz wall-clock ticks; a 1 ms wait yields the GPU
         return gpbs_hip_allreduce(w.a, q_seq[qi], w.bytes, (unsigned)w.chunk, q, tab, mode, me, ctx->d_cnt,
-                                  &h_status[qi], grid, (unsigned long long)(w.K > 0 ? w.K : 5000) * 100000ull, stream);
+                                  &h_status[qi], grid, (unsigned long long)coll_timeout_ms(w) * 100000ull,
+                                  100000ull, stream);
     }
     return -22;
   }
@@ -1231,6 +1244,7 @@ struct Runner {
           if (fresh) {
             q_alt[qi] = (uint8_t)(cfg.alt_kind && phase.load(std::memory_order_acquire));
             q_seq[qi] = coll_seq++;
+            q_t0[qi] = mono_ns();
           }
           cur_alt = q_alt[qi];
           hipStream_t stream = pick_stream();
@@ -1265,7 +1279,13 @@ struct Runner {
         }
         const u32 s = __atomic_load_n(&h_status[f.qi], __ATOMIC_ACQUIRE);
         const u32 done = s & 0x3fffffffu;
-        if ((s & 0x80000000u) && (s & 0x40000000u)) {
+        const Work fw = work(q_alt[f.qi]);
+        const bool unfinished = !((s & 0x80000000u) && done >= unit_total(fw));
+        // all-reduce: a unit still unfinished after the barrier timeout
+        // (counted over its relaunches: the kernel yields every 1 ms) fails too
+        const bool coll_late = fw.kind == K_ALLREDUCE && unfinished &&
+                               mono_ns() - q_t0[f.qi] > (int64_t)coll_timeout_ms(fw) * 1000000;
+        if (((s & 0x80000000u) && (s & 0x40000000u)) || coll_late) {
           // all-reduce tenant: a peer barrier timed out (a peer is gone or
           // stalled for seconds) -- fail the runner instead of retrying
           std::fprintf(stderr, "[gpbs-hip] tenant %d: collective unit %u timed out waiting for its peers\n",
@@ -1296,6 +1316,14 @@ struct Runner {
           }
         } else {
           relaunch.push_back(f.qi);  // revoked mid-unit: resume when owned
+          const int64_t rv = cfg.tenant >= 0 && cfg.tenant < kMaxTenants
+                                 ? ctx->revoke_ns[cfg.tenant].load(std::memory_order_relaxed) : 0;
+          const int64_t dr = rv ? mono_ns() - rv : -1;
+          if (dr >= 0 && dr < 1000000000) {
+            st.drain_sum_ns += dr;
+            st.drain_count++;
+            if (dr > st.drain_max_ns) st.drain_max_ns = dr;
+          }
         }
         if (stop) break;
       }

@@ -474,6 +474,182 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restr
   finish(q, status, (u32)ntiles);
 }
 
+// ------------------------------- GEMM 256x256, 8 waves, 2 phases per K-tile ---
+// Per-barrier stamps of the 4-phase kernel (scripts/gemm_stamps.py,
+// profiles/pmc/gemm_stamps_r3.json: 2.385 GHz in-kernel clock, 3996 cycles
+// per K-tile) put every one of its 8 barrier intervals at 400-700 cycles
+// against 256 cycles of MFMA work (16 MFMAs of one wave per SIMD): a fixed
+// ~200-cycle cost per interval (barrier round trip, the MFMA wave's restart)
+// that 8 intervals per K-tile pay 8 times.  This variant keeps the tile,
+// the LDS image, the staggered wave groups and glds staging, but runs TWO
+// phases per K-tile with 32 MFMAs each: phase A = rows 0-63 of the wave's
+// 128 x all 64 columns, phase B = rows 64-127 (the 8 B fragments stay in
+// registers across both), so a K-tile has 4 barrier intervals.
+// Global interval schedule (tile-relative; g0 = wr 0 reads in 0 and 2, g1
+// one barrier behind reads in 1 and 3):
+//   g0 int 0: read B (8) + A rows 0-63 (8); stage B0, B1, A0 of t+1;
+//             vmcnt(6) retires its A1(t) (issued int 2 of t-1)
+//   g1 int 1: same reads; stage all four halves of t+1
+//   g0 int 2: read A rows 64-127 (8); stage A1 of t+1; vmcnt(2)
+//   g1 int 3: same reads; vmcnt(0)
+// WAR: a half of buffer (t+1)&1 is restaged only after the barrier that
+// follows the lgkmcnt(0) retiring its last read in tile t-1 (B: read in
+// ints 0/1, free from 3 of t-1; A0: int 2, free from int 0 of t; A1: int 3,
+// free from int 1 of t).  RAW: every issuer's counted vmcnt precedes a
+// barrier the reader passes before its read (g0 reads B, A0 of t+1 at int 4:
+// g0 retired them at int 2, g1 at int 3; g1 reads A1 at int 5: g0 retired
+// it at int 4).  Host opts bit 8.
+template <int STAMP>
+__global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __restrict__ A, const u16* __restrict__ Bt,
+                                                               u16* __restrict__ C, int M, int N, int K, WorkQueue* q,
+                                                               const PartTable* table, u32 mode, u32 me, u64* cnt,
+                                                               u32 inst_per_tile, u32 refs_per_tile,
+                                                               u32 miss_per_tile, u32* status) {
+  constexpr int kStampLds = STAMP ? 8 * kStampTiles * kStampSlots * 4 : 0;
+  __shared__ __attribute__((aligned(16))) char smem[kG2Lds + 16 + kStampLds];
+  lds_t* lds = (lds_t*)smem;
+  int* s_slot = (int*)(smem + kG2Lds);
+  const u32 xcc = xcc_id();
+  u64 t_last = __builtin_amdgcn_s_memtime();
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wu = __builtin_amdgcn_readfirstlane(wid);  // wave-uniform: scalar branches on the group
+  const int wr = wu >> 2, wc = wu & 3;
+  const int tiles_m = M / G2_BM, tiles_n = N / G2_BM, ntiles = tiles_m * tiles_n;
+  const int nt = K / G2_BK;
+  u32* st_lds = (u32*)(smem + kG2Lds + 16) + wid * kStampTiles * kStampSlots;
+  auto stamp = [&](int t, int slot) {
+    if constexpr (STAMP) {
+      if (lane == 0 && t >= kStampT0 && t < kStampT0 + kStampTiles)
+        st_lds[(t - kStampT0) * kStampSlots + slot] =
+            slot == 9 ? (u32)__builtin_amdgcn_s_memrealtime() : (u32)__builtin_amdgcn_s_memtime();
+    }
+  };
+  int soff[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = 8 * (2 * wid + j) + (lane >> 3);
+    soff[j] = row * K + (((lane & 7) ^ g2_swz(row)) * 8);
+  }
+  const int l16 = lane & 15, lq = lane >> 4;
+  const int bh = wc >> 1, bc = (wc & 1) * 64;
+
+  for (;;) {
+    const int tile = grab_unit(q, table, mode, me, xcc, s_slot, (u32)ntiles);
+    if (tile < 0) break;
+    const int tm = tile / tiles_n, tn = tile % tiles_n;
+    const u16* Ab = A + (size_t)tm * G2_BM * K;
+    const u16* Bb = Bt + (size_t)tn * G2_BM * K;
+    auto stage = [&](int kind, int h, int t) {
+      const u16* src = (kind ? Bb : Ab) + (size_t)h * 128 * K + t * G2_BK;
+      lds_t* dst = lds + (t & 1) * kG2Buf + (kind * 2 + h) * kG2Half + wid * 2048;
+      glds16(src + soff[0], dst);
+      glds16(src + soff[1], dst + 1024);
+    };
+    auto frag = [&](int b, int kind, int h, int r0, int s) -> bf16x8 {
+      const int r = r0 + l16;
+      const lds_t* p = lds + b * kG2Buf + (kind * 2 + h) * kG2Half + r * 128 + (((4 * s + lq) ^ g2_swz(r)) << 4);
+      return *(const __attribute__((address_space(3))) bf16x8*)p;
+    };
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // prologue: all of tile 0 from every wave, landed and visible
+    stage(1, 0, 0); stage(1, 1, 0); stage(0, 0, 0); stage(0, 1, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (wr == 1) __builtin_amdgcn_s_barrier();  // g1 runs one barrier behind
+    bf16x8 a[4][2], b[4][2];
+    for (int t = 0; t < nt; ++t) {
+      const int buf = t & 1;
+      const bool more = t + 1 < nt;
+      stamp(t, 9);
+      stamp(t, 0);
+      // ---- R_A: B fragments (kept for both phases), A rows 0-63
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) b[j][s2] = frag(buf, 1, bh, bc + j * 16, s2);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) a[i][s2] = frag(buf, 0, wr, i * 16, s2);
+      if (wr == 0) {
+        if (more) {
+          stage(1, 0, t + 1); stage(1, 1, t + 1); stage(0, 0, t + 1);
+          asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+      } else if (more) {
+        stage(1, 0, t + 1); stage(1, 1, t + 1); stage(0, 0, t + 1); stage(0, 1, t + 1);
+      }
+      __builtin_amdgcn_s_barrier();
+      stamp(t, 1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j][s2], a[i][s2], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_barrier();
+      stamp(t, 2);
+      // ---- R_B: A rows 64-127
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) a[i][s2] = frag(buf, 0, wr, 64 + i * 16, s2);
+      if (wr == 0) {
+        if (more) {
+          stage(0, 1, t + 1);
+          asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        }
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      stamp(t, 3);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j][s2], a[i][s2], acc[4 + i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_barrier();
+      stamp(t, 4);
+    }
+    if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the groups
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = tm * G2_BM + wr * 128 + i * 16 + l16;
+        const int n = tn * G2_BM + wc * 64 + j * 16 + 4 * lq;
+        const u32 lo = (u32)f2bf(acc[i][j][0]) | ((u32)f2bf(acc[i][j][1]) << 16);
+        const u32 hi = (u32)f2bf(acc[i][j][2]) | ((u32)f2bf(acc[i][j][3]) << 16);
+        *(uint2*)(C + (size_t)m * N + n) = make_uint2(lo, hi);
+      }
+    if constexpr (STAMP) {
+      if (lane == 0 && blockIdx.x < kStampWgs && nt >= kStampT0 + kStampTiles && g_gemm_dbg) {
+        u32* dst = g_gemm_dbg + ((size_t)blockIdx.x * 8 + wid) * kStampTiles * kStampSlots;
+        for (int i = 0; i < kStampTiles * kStampSlots; ++i) dst[i] = st_lds[i];
+      }
+    }
+    count_unit(cnt, me, xcc, inst_per_tile, &t_last, refs_per_tile, miss_per_tile, q);
+  }
+  finish(q, status, (u32)ntiles);
+}
+
 // ------------------------------------------------ GEMM 256x256, 4 waves ----
 // The shape hipBLASLt picks for this GEMM on gfx950 (rocprofv3 kernel trace of
 // torch.mm 4096^3, profiles/kbench_r2_w4.md: MT256x256x64, MI16x16, 256
@@ -851,6 +1027,13 @@ int gpbs_hip_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int
     if ((g_gemm_opts & 32) && (K / G2_BK) % 2 == 0) {  // 4-wave 128x128-per-wave variant (plain tile queue)
       hipLaunchKernelGGL(k_gemm256w4_bf16_tn, dim3(grid), dim3(G4_NT), 0, s, (const u16*)A, (const u16*)Bt, (u16*)C,
                          M, N, K, (WorkQueue*)q, (const PartTable*)table, mode, me, (u64*)cnt, inst, refs, miss,
+                         (u32*)status);
+      return hipGetLastError() == hipSuccess ? 0 : -5;
+    }
+    if (g_gemm_opts & 256) {  // 2 phases per K-tile (4 barriers)
+      auto k2 = (g_gemm_opts & 64) ? k_gemm256s2_bf16_tn<1> : k_gemm256s2_bf16_tn<0>;
+      hipLaunchKernelGGL(k2, dim3(grid), dim3(G2_NT), 0, s, (const u16*)A, (const u16*)Bt, (u16*)C, M, N, K,
+                         (WorkQueue*)q, (const PartTable*)table, mode, me, (u64*)cnt, inst, refs, miss,
                          (u32*)status);
       return hipGetLastError() == hipSuccess ? 0 : -5;
     }

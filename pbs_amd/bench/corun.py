@@ -877,6 +877,7 @@ class Corun:
                 self.ctx.hwc_reset()
         quanta = {n: [] for n in self.tid}
         layout = {n: [] for n in self.throughput}  # budget SE sets per step (bit c = SE c)
+        self._rs0 = {n: r.stats() for n, r in self.runners.items() if isinstance(r, Runner)}
         self._barrier()
         t0 = time.perf_counter()
         d0 = {n: self._work(n) for n in self.throughput}
@@ -1029,8 +1030,17 @@ class Corun:
             eng["phase"] = {n: e.tenant_info(self.tid[n]).phase for n in self.tid}
             eng["ctx_share"] = {n: [round(x / (wall_ms / 1e3), 2) for x in self.ctx.ownership(self.tid[n])]
                                 for n in self.tid}
-            eng["runner"] = {n: {k: getattr(r.stats(), k) for k in ("launches", "relaunches", "waits_owner")}
-                             for n, r in self.runners.items() if isinstance(r, Runner)}
+            eng["runner"] = {}
+            rs0 = getattr(self, "_rs0", {})
+            for n, r in self.runners.items():
+                if not isinstance(r, Runner):
+                    continue
+                st, s0 = r.stats(), rs0.get(n)
+                d = {k: getattr(st, k) - (getattr(s0, k) if s0 else 0)
+                     for k in ("launches", "relaunches", "waits_owner", "drain_count", "drain_sum_ns")}
+                # revocation drain: table publish -> the interrupted unit's grid gone
+                d["drain_us_mean"] = round(d.pop("drain_sum_ns") / d["drain_count"] / 1e3, 1) if d["drain_count"] else None
+                eng["runner"][n] = d
             eng["hold_raises"] = self.ctx.hold_raises()  # latency-request holds (cumulative, gpbs-lat)
             coll = self.runners.get("coll")
             if isinstance(coll, CollTenant):

@@ -20,7 +20,8 @@ class RunnerCfg(C.Structure):
 class RunnerStats(C.Structure):
     _fields_ = [(n, u64) for n in ("units_done", "launches", "relaunches", "waits_owner", "submitted")] + \
                [(n, i64) for n in ("busy_ns", "wait_owner_ns", "first_start_ns", "last_done_ns", "lat_sum_ns",
-                                   "lat_max_ns")] + [("lat_count", u64), ("units_alt", u64)]
+                                   "lat_max_ns")] + [("lat_count", u64), ("units_alt", u64)] + \
+               [("drain_sum_ns", i64), ("drain_max_ns", i64), ("drain_count", u64)]
 
 
 KIND = {"gemm": 1, "stream": 2, "reduce": 3, "gemv": 4, "allreduce": 5}

@@ -308,6 +308,9 @@ class RunnerStats:
     lat_max_ns: int
     lat_count: int
     units_alt: int = 0
+    drain_sum_ns: int = 0   # revocation drain (publish -> interrupted unit's grid gone)
+    drain_max_ns: int = 0
+    drain_count: int = 0
 
 
 class Runner:

@@ -8,7 +8,7 @@ cycles of every barrier interval, the cycles per K-tile, the in-kernel clock
 (2 waves x 64 MFMA x 16 cycles per SIMD per K-tile), next to the TF/s of the
 plain and the stamped build timed in the same process.
 
-    python scripts/gemm_stamps.py [n]
+    python scripts/gemm_stamps.py [n] [opts]   (opts 256: the 2-phase kernel, 4 intervals per K-tile)
 """
 import ctypes as C
 import json
@@ -26,6 +26,8 @@ TILES, SLOTS, WGS = 16, 10, 64
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+    base = int(sys.argv[2]) if len(sys.argv) > 2 else 4
+    nint = 4 if base & 256 else 8  # barrier intervals per K-tile
     L = K.lib()
     L.gpbs_hip_set_gemm_dbg.restype = C.c_int
     L.gpbs_hip_set_gemm_dbg.argtypes = [C.c_void_p]
@@ -53,31 +55,31 @@ def main():
 
     # warm the clocks, then interleave plain / stamped rounds
     for _ in range(3):
-        run(4)
+        run(base)
     res = {"plain": [], "stamp": []}
     for _ in range(5):
-        res["plain"].append(run(4))
-        res["stamp"].append(run(4 | 64))
+        res["plain"].append(run(base))
+        res["stamp"].append(run(base | 64))
     L.gpbs_hip_set_gemm_opts(4)
     tf = {k: 2 * n ** 3 / (sorted(v)[2]) / 1e9 for k, v in res.items()}
     ref = A[:256].float() @ B.float().t()
     err = (Cm[:256].float() - ref).abs().max().item()
     st = dbg.cpu().numpy().astype(np.uint32).reshape(WGS, 8, TILES, SLOTS).astype(np.int64)
-    cyc = st[..., :9]
-    d = np.diff(cyc, axis=-1) % (1 << 32)            # 8 intervals per tile
-    per_tile = (cyc[..., 8] - cyc[..., 0]) % (1 << 32)
+    cyc = st[..., :nint + 1]
+    d = np.diff(cyc, axis=-1) % (1 << 32)            # nint intervals per tile
+    per_tile = (cyc[..., nint] - cyc[..., 0]) % (1 << 32)
     real = (st[..., 9] % (1 << 32)).astype(np.int64)
     # clock: memtime cycles over realtime (100 MHz) across the stamped tiles
     dc = (cyc[:, :, -1, 0] - cyc[:, :, 0, 0]) % (1 << 32)
     dr = (real[:, :, -1] - real[:, :, 0]) % (1 << 32)
     ok = dr > 0
     ghz = float(np.median(dc[ok] / dr[ok] * 0.1)) if ok.any() else None
-    out = {"n": n, "tflops_plain": round(tf["plain"], 1), "tflops_stamp": round(tf["stamp"], 1),
+    out = {"n": n, "opts": base, "tflops_plain": round(tf["plain"], 1), "tflops_stamp": round(tf["stamp"], 1),
            "max_abs_err": round(err, 4), "clock_ghz": round(ghz, 3) if ghz else None}
     for g in (0, 1):
         dd = d[:, 4 * g:4 * g + 4]
-        out[f"group{g}_interval_cycles_median"] = [int(np.median(dd[..., k])) for k in range(8)]
-        out[f"group{g}_interval_cycles_p90"] = [int(np.percentile(dd[..., k], 90)) for k in range(8)]
+        out[f"group{g}_interval_cycles_median"] = [int(np.median(dd[..., k])) for k in range(nint)]
+        out[f"group{g}_interval_cycles_p90"] = [int(np.percentile(dd[..., k], 90)) for k in range(nint)]
     pt = float(np.median(per_tile))
     out["cycles_per_ktile_median"] = int(pt)
     out["mfma_busy_implied"] = round(2 * 64 * 16 / pt, 3)

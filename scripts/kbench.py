@@ -60,7 +60,7 @@ def main():
     names = {0: "plain-queue", 1: "xcd-range", 2: "deep-prefetch", 4: "staggered-groups",
              12: "staggered-2d-blocks", 13: "staggered-xcd-range-2d-blocks"}
     if os.environ.get("KBENCH_GEMM_ONLY"):
-        names = {4: "staggered-groups", 32: "w4-128x128-per-wave", 16: "staggered-early-A"}
+        names = {4: "staggered-groups", 256: "staggered-2phase", 16: "staggered-early-A"}
     ab = {k: [] for k in names}
     for _ in range(5):
         for opt in names:
