@@ -970,17 +970,74 @@ typedef struct gpbs_runner_stats {
 
 namespace {
 
+// Process-wide pool of CU-masked streams.  Every CU-masked stream is a
+// hardware queue of its own, and destroying one does not give the queue back
+// for good: a process that built and tore down runners mix after mix (bench.py
+// --mix all: 4mix, then phase, then 8mix) ran its last mix with the
+// SE-partitioned policies at 0.71 of what the same mix measured in a fresh
+// process (1.14, profiles/r3/bench_full_5rep_a.json vs b8_alone.json) -- the
+// hardware scheduler time-slicing an over-subscribed queue set.  Runners
+// therefore take masked streams from this pool and return them (drained)
+// when they close, so the process holds at most as many masked queues as it
+// ever used at once.
+struct MaskedStreams {
+  struct Ent {
+    int device;
+    uint32_t m[8];
+    hipStream_t s;
+  };
+  std::mutex mu;
+  std::vector<Ent> free;
+  int created = 0;
+};
+MaskedStreams& masked_pool() {
+  static MaskedStreams* p = new MaskedStreams;  // never destroyed: streams outlive static teardown order
+  return *p;
+}
+hipStream_t masked_acquire(const uint32_t m[8]) {
+  int dev = 0;
+  hipGetDevice(&dev);
+  MaskedStreams& P = masked_pool();
+  {
+    std::lock_guard<std::mutex> g(P.mu);
+    for (size_t i = 0; i < P.free.size(); ++i)
+      if (P.free[i].device == dev && std::memcmp(P.free[i].m, m, sizeof(P.free[i].m)) == 0) {
+        hipStream_t s = P.free[i].s;
+        P.free.erase(P.free.begin() + (long)i);
+        return s;
+      }
+  }
+  hipStream_t s = nullptr;
+  if (hipExtStreamCreateWithCUMask(&s, 8, const_cast<uint32_t*>(m)) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> g(P.mu);
+  P.created++;
+  return s;
+}
+void masked_release(const uint32_t m[8], hipStream_t s) {
+  if (!s) return;
+  int dev = 0;
+  hipGetDevice(&dev);
+  hipStreamSynchronize(s);
+  MaskedStreams::Ent e{dev, {}, s};
+  std::memcpy(e.m, m, sizeof(e.m));
+  MaskedStreams& P = masked_pool();
+  std::lock_guard<std::mutex> g(P.mu);
+  P.free.push_back(e);
+}
+
 // CU mask of one half of every XCD.  hipExtStreamCreateWithCUMask bit b
 // selects logical CU b/8 of XCD b%8 (an XCD left with no bit runs
 // unrestricted), and logical CU i sits on shader engine i%4, so half h is the
 // bits whose SE is 2h or 2h+1 (measured: scripts/interfere.py census map).
-hipStream_t make_half_stream(int h) {
-  uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+void half_mask(int h, uint32_t m[8]) {
+  for (int w = 0; w < 8; ++w) m[w] = 0;
   for (int b = 0; b < 256; ++b)
     if ((((b / 8) % 4) >> 1) == h) m[b / 32] |= 1u << (b % 32);
-  hipStream_t s = nullptr;
-  if (hipExtStreamCreateWithCUMask(&s, 8, m) != hipSuccess) return nullptr;
-  return s;
+}
+hipStream_t make_half_stream(int h) {
+  uint32_t m[8];
+  half_mask(h, m);
+  return masked_acquire(m);
 }
 
 // CU mask of a set of (XCD, SE) partitions: bit b = logical CU b/8 of XCD
@@ -1094,16 +1151,17 @@ struct Runner {
 
   bool shared() const { return cfg.gate && ctx->share.load(std::memory_order_acquire); }
 
+  static void se_half_mask(int half, uint32_t m[8]) {
+    u32 bits[kXcds];
+    for (int x = 0; x < kXcds; ++x) bits[x] = half ? 0xCu : 0x3u;
+    se_cu_mask(bits, m);
+  }
   hipStream_t half_se_stream(int half) {
     if (!se_stream[half]) {
-      u32 bits[kXcds];
-      for (int x = 0; x < kXcds; ++x) bits[x] = half ? 0xCu : 0x3u;
       uint32_t m[8];
-      se_cu_mask(bits, m);
-      if (hipExtStreamCreateWithCUMask(&se_stream[half], 8, m) != hipSuccess) {
-        se_stream[half] = nullptr;
-        return stream;
-      }
+      se_half_mask(half, m);
+      se_stream[half] = masked_acquire(m);
+      if (!se_stream[half]) return stream;
     }
     return se_stream[half];
   }
@@ -2244,10 +2302,17 @@ void gpbs_runner_destroy(void* p) {
   hipStreamSynchronize(r->stream);
   for (int i = 0; i < r->nq; ++i) hipEventDestroy(r->ev[i]);
   hipStreamDestroy(r->stream);
-  for (hipStream_t h : r->half_stream)
-    if (h) hipStreamDestroy(h);
-  for (hipStream_t h : r->se_stream)
-    if (h) hipStreamDestroy(h);
+  for (int h = 0; h < 2; ++h) {  // masked streams go back to the process pool
+    uint32_t m[8];
+    if (r->half_stream[h]) {
+      half_mask(h, m);
+      masked_release(m, r->half_stream[h]);
+    }
+    if (r->se_stream[h]) {
+      Runner::se_half_mask(h, m);
+      masked_release(m, r->se_stream[h]);
+    }
+  }
   hipFree(r->d_q);
   hipHostFree(r->h_status);
   delete r;

@@ -245,7 +245,7 @@ __device__ __forceinline__ int g2_swz(int r) { return (r >> 1) & 7; }
 // op perturbs the counted vmcnt waits) and copies them to g_gemm_dbg after
 // the unit: [wg < kStampWgs][wave][tile][slot], slot 0 = tile start, 1..8 =
 // after the tile's 8 barriers, 9 = s_memrealtime at the tile start (100 MHz).
-constexpr int kStampT0 = 8, kStampTiles = 16, kStampSlots = 10, kStampWgs = 64;
+constexpr int kStampT0 = 8, kStampTiles = 16, kStampSlots = 10, kStampWgs = 64, kStampPhWgs = 1024;
 __device__ u32* g_gemm_dbg;
 
 template <int DEEP, int STAMP = 0>
@@ -532,6 +532,11 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
   }
   const int l16 = lane & 15, lq = lane >> 4;
   const int bh = wc >> 1, bc = (wc & 1) * 64;
+  // STAMP: per workgroup s_memrealtime (100 MHz) at kernel entry, loop start,
+  // loop end and after the epilogue stores of its first unit
+  u32 ph[4] = {0, 0, 0, 0};
+  if constexpr (STAMP) ph[0] = (u32)__builtin_amdgcn_s_memrealtime();
+  int units_seen = 0;
 
   for (;;) {
     const int tile = grab_unit(q, table, mode, me, xcc, s_slot, (u32)ntiles);
@@ -561,6 +566,9 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
     __builtin_amdgcn_s_barrier();
     if (wr == 1) __builtin_amdgcn_s_barrier();  // g1 runs one barrier behind
     bf16x8 a[4][2], b[4][2];
+    if constexpr (STAMP) {
+      if (units_seen == 0) ph[1] = (u32)__builtin_amdgcn_s_memrealtime();
+    }
     for (int t = 0; t < nt; ++t) {
       const int buf = t & 1;
       const bool more = t + 1 < nt;
@@ -629,6 +637,9 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
       stamp(t, 4);
     }
     if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the groups
+    if constexpr (STAMP) {
+      if (units_seen == 0) ph[2] = (u32)__builtin_amdgcn_s_memrealtime();
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -640,11 +651,19 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
         *(uint2*)(C + (size_t)m * N + n) = make_uint2(lo, hi);
       }
     if constexpr (STAMP) {
+      if (units_seen == 0) {
+        ph[3] = (u32)__builtin_amdgcn_s_memrealtime();
+        if (tid == 0 && g_gemm_dbg && blockIdx.x < kStampPhWgs) {
+          u32* dp = g_gemm_dbg + kStampWgs * 8 * kStampTiles * kStampSlots + blockIdx.x * 4;
+          for (int k = 0; k < 4; ++k) dp[k] = ph[k];
+        }
+      }
       if (lane == 0 && blockIdx.x < kStampWgs && nt >= kStampT0 + kStampTiles && g_gemm_dbg) {
         u32* dst = g_gemm_dbg + ((size_t)blockIdx.x * 8 + wid) * kStampTiles * kStampSlots;
         for (int i = 0; i < kStampTiles * kStampSlots; ++i) dst[i] = st_lds[i];
       }
     }
+    ++units_seen;
     count_unit(cnt, me, xcc, inst_per_tile, &t_last, refs_per_tile, miss_per_tile, q);
   }
   finish(q, status, (u32)ntiles);
@@ -1004,7 +1023,7 @@ int gpbs_hip_set_gemm_opts(int opts) {
 // u32 words.
 int gpbs_hip_set_gemm_dbg(void* buf) {
   if (hipMemcpyToSymbol(HIP_SYMBOL(g_gemm_dbg), &buf, sizeof(buf)) != hipSuccess) return -5;
-  return kStampWgs * 8 * kStampTiles * kStampSlots;
+  return kStampWgs * 8 * kStampTiles * kStampSlots + kStampPhWgs * 4;
 }
 
 int gpbs_hip_gemm_units(int M, int N) {

@@ -64,7 +64,10 @@ def main():
     tf = {k: 2 * n ** 3 / (sorted(v)[2]) / 1e9 for k, v in res.items()}
     ref = A[:256].float() @ B.float().t()
     err = (Cm[:256].float() - ref).abs().max().item()
-    st = dbg.cpu().numpy().astype(np.uint32).reshape(WGS, 8, TILES, SLOTS).astype(np.int64)
+    raw = dbg.cpu().numpy().astype(np.uint32).astype(np.int64)
+    st = raw[:WGS * 8 * TILES * SLOTS].reshape(WGS, 8, TILES, SLOTS)
+    ph = raw[WGS * 8 * TILES * SLOTS:].reshape(-1, 4)  # per WG: entry, loop start, loop end, stores done (10 ns)
+    ph = ph[(ph != 0).all(axis=1)]
     cyc = st[..., :nint + 1]
     d = np.diff(cyc, axis=-1) % (1 << 32)            # nint intervals per tile
     per_tile = (cyc[..., nint] - cyc[..., 0]) % (1 << 32)
@@ -80,6 +83,17 @@ def main():
         dd = d[:, 4 * g:4 * g + 4]
         out[f"group{g}_interval_cycles_median"] = [int(np.median(dd[..., k])) for k in range(nint)]
         out[f"group{g}_interval_cycles_p90"] = [int(np.percentile(dd[..., k], 90)) for k in range(nint)]
+    if len(ph):
+        t0 = ph[:, 0].min()
+        rel = (ph - t0) % (1 << 32) / 100.0  # us from the first workgroup's entry
+        out["wg_phase_us"] = {"n_wg": int(len(ph)),
+                              "entry_p50_max": [round(float(np.median(rel[:, 0])), 2), round(float(rel[:, 0].max()), 2)],
+                              "prologue_p50": round(float(np.median(rel[:, 1] - rel[:, 0])), 2),
+                              "loop_p50_max": [round(float(np.median(rel[:, 2] - rel[:, 1])), 2),
+                                               round(float((rel[:, 2] - rel[:, 1]).max()), 2)],
+                              "epilogue_p50_max": [round(float(np.median(rel[:, 3] - rel[:, 2])), 2),
+                                                   round(float((rel[:, 3] - rel[:, 2]).max()), 2)],
+                              "last_done": round(float(rel[:, 3].max()), 2)}
     pt = float(np.median(per_tile))
     out["cycles_per_ktile_median"] = int(pt)
     out["mfma_busy_implied"] = round(2 * 64 * 16 / pt, 3)
