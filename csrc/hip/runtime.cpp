@@ -291,7 +291,7 @@ struct GpuCtx {
   // (EWMA of the sample duration); 0 disables the cap.
   // Measured on the 4-tenant mix: a 25 % duty (lean set, 1.15 ms) cost the
   // flagship 5 % of its aggregate, 5 % duty (4 ms) 0.5 %.
-  int hwc_duty_pct = 2;  // GPBS_HWC_DUTY (profiles/r3/cmp_4mix_*: 5 % costs 0.01 of aggregate, 2 % 0.005)
+  int hwc_duty_pct = 1;  // GPBS_HWC_DUTY (profiles/r3: 5 % costs 0.01 of 4mix aggregate, 2 % 0.004, 1 % none measurable)
   int hwc_burst_ms = 20;  // GPBS_HWC_BURST_MS: 1 ms hardware sampling after a trigger
   int hwc_watch = 1;      // GPBS_HWC_WATCH: read the modeled block every tick (the burst trigger)
   int64_t hwc_next_period_ns = 1000000;
@@ -994,6 +994,16 @@ MaskedStreams& masked_pool() {
   static MaskedStreams* p = new MaskedStreams;  // never destroyed: streams outlive static teardown order
   return *p;
 }
+// GPBS_ONE_MASKED=1: a runner that moves between class halves gives its old
+// masked stream back before taking the other, so the process holds at most
+// one masked queue per runner (8mix: 8 instead of 16).
+bool one_masked() {
+  static const bool v = [] {
+    const char* e = std::getenv("GPBS_ONE_MASKED");
+    return e && std::atoi(e) != 0;
+  }();
+  return v;
+}
 hipStream_t masked_acquire(const uint32_t m[8]) {
   int dev = 0;
   hipGetDevice(&dev);
@@ -1159,6 +1169,11 @@ struct Runner {
   hipStream_t half_se_stream(int half) {
     if (!se_stream[half]) {
       uint32_t m[8];
+      if (one_masked() && se_stream[half ^ 1]) {  // hold one masked queue per runner at a time
+        se_half_mask(half ^ 1, m);
+        masked_release(m, se_stream[half ^ 1]);
+        se_stream[half ^ 1] = nullptr;
+      }
       se_half_mask(half, m);
       se_stream[half] = masked_acquire(m);
       if (!se_stream[half]) return stream;
