@@ -4,9 +4,10 @@ profiles/pmc/: MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x
 GRBM_GUI_ACTIVE / 8 XCDs), LDS bank-conflict and wait shares of wave cycles,
 L2 hit rate.
 
-    python scripts/pmc_summary.py KERNEL_SUBSTR csv [csv ...]
+    python scripts/pmc_summary.py KERNEL_SUBSTR file [file ...]   (rocpd .db or counter_collection .csv)
 """
 import csv
+import sqlite3
 import sys
 from collections import defaultdict
 
@@ -16,6 +17,13 @@ def main():
     tot = defaultdict(float)
     disp = set()
     for f in files:
+        if f.endswith(".db"):
+            c = sqlite3.connect(f)
+            q = ("select dispatch_id, counter_name, value from counters_collection where kernel_name like ?")
+            for did, name, val in c.execute(q, (f"%{sub}%",)):
+                disp.add((f, did))
+                tot[name] += float(val)
+            continue
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 name = row.get("Kernel_Name") or row.get("Kernel-Name") or ""
