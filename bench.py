@@ -6,8 +6,10 @@
 Runs the BASELINE.json metric -- co-run slowdown vs solo + aggregate
 throughput of the 4-tenant mix (MFMA GEMM + HBM stream + all-reduce + idle)
 per MI355X -- under the gpbs PBS adaptive credit scheduler, one rank per GPU
-(weak scaling: every GPU hosts its own mix; the all-reduce tenant spans all
-GPUs over RCCL/xGMI when N > 1).  Rank 0 prints ONE JSON line.
+(weak scaling: every GPU hosts its own mix; at N > 1 the all-reduce tenant
+spans all GPUs over xGMI -- a gpbs kernel on IPC-mapped peer buffers, gated
+per workgroup like every tenant, with RCCL as --coll rccl and as the fallback
+when its one-unit self-test fails).  Rank 0 prints ONE JSON line.
 
 ``value`` = aggregate normalized throughput of the headline mix summed over
 all GPUs (sum over throughput tenants of co-run rate / solo rate,
@@ -16,7 +18,8 @@ same steady protocol as the co-run (backlogged, W + K windows, alone).
 Comparison policies run on the same box, 5 randomized reps each: none
 (default hardware sharing), static (equal XCD split), static-se (the
 hand-picked shader-engine layout, no engine, no counters), the PBS ablations
-(credit-fixed*, gpbs-ts) and gpbs-lat (latency hold).
+(credit-fixed*: fixed quantum; gpbs-split: crowded class regions split by
+XCD blocks instead of time-shared) and gpbs-lat (latency hold).
 
 By default two more mixes run after the headline and are reported under
 ``mixes``: "phase" (a tenant alternating GEMM <-> stream every 300 ms and a
@@ -206,7 +209,7 @@ def main():
         default = {"4mix": "none,static,static-se,credit-fixed,gpbs-nolane,gpbs-lat,gpbs",
                    "gemm2": "none,static,static-se,credit-fixed,gpbs",
                    "phase": "none,static-se,credit-fixed,gpbs",
-                   "8mix": "none,static-se,credit-fixed-ts,gpbs-ts,gpbs"}[mix]
+                   "8mix": "none,static-se,credit-fixed-ts,gpbs-split,gpbs"}[mix]
         spec = args.policies if (args.policies and mix == mixes[0]) else default
         pols = tuple(p for p in spec.split(",") if p)
         reps = args.reps if mix == mixes[0] else args.reps_extra

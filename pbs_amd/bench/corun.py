@@ -179,14 +179,20 @@ POLICY_ENGINES = {
     #        kernel gate mode, partition-table location + runtime options)
     # flagship: counter-driven SE budgets (csrc/core/engine.cpp budget_layout)
     # -- every present tenant gets shader engines sized from the classes
-    # present, a crowded class region is split by whole-XCD blocks; runners
-    # launch on CU-masked class-half streams; the latency tenant runs outside
-    # the partitions in the latency lane (its GEMV CU-masked to the memory
-    # half, raised wave priority)
-    "gpbs": (4, dict(BUDGET_OVERRIDES), True, "device,se,waveprio,latco,budget,latmem"),
+    # present; a class region with more tenants than its aligned blocks hold
+    # is time-shared under credit with PBS adaptive quanta (class_budget 1);
+    # runners launch on CU-masked class-half streams; the latency tenant runs
+    # outside the partitions in the latency lane (its GEMV CU-masked to the
+    # memory half, raised wave priority).  Uncrowded mixes (4mix, phase) lay
+    # out exactly as gpbs-split; on the crowded 8mix time-sharing with PBS
+    # quanta measured ahead of the XCD-block split on 3 of 4 boxes
+    # (profiles/r3/q8_*.json, bench_full_5rep_b.json, bench_all_pool_2rep.json).
+    "gpbs": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
+    # crowded class regions split by whole-XCD blocks instead (class_budget 2)
+    "gpbs-split": (4, dict(BUDGET_OVERRIDES), True, "device,se,waveprio,latco,budget,latmem"),
     "credit-fixed": (4, dict(BUDGET_OVERRIDES, sched="credit-fixed"), True, "device,se,waveprio,latco,budget,latmem"),
-    # crowded class regions time-shared under credit with PBS adaptive quanta
-    # (credit-fixed-ts: the fixed quantum) -- where PBS quanta act (8mix)
+    # round-3 name of the flagship on crowded mixes (time-shared, PBS quanta;
+    # credit-fixed-ts: the fixed quantum)
     "gpbs-ts": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
     "credit-fixed-ts": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="credit-fixed"), True,
                         "device,se,waveprio,latco,budget,latmem"),
