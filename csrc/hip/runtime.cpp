@@ -997,7 +997,7 @@ MaskedStreams& masked_pool() {
 // A runner that moves between class halves gives its old masked stream back
 // before taking the other, so the process holds at most one masked queue per
 // runner (8mix: 8 instead of 16).  Measured on the 8mix, 3 reps
-// (profiles/r3/q8_*.json): with both halves' queues kept, every partitioned
+// (profiles/r3/8mix_queues_q8_*.json): with both halves' queues kept, every partitioned
 // policy lost 0.1-0.2 of aggregate in some repetitions (static-se IQR 0.049,
 // gpbs-ts 0.123); with one, static-se IQR 0.0009, gpbs-ts 0.018.
 // GPBS_ONE_MASKED=0 restores the old behaviour.

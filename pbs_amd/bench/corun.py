@@ -186,7 +186,7 @@ POLICY_ENGINES = {
     # memory half, raised wave priority).  Uncrowded mixes (4mix, phase) lay
     # out exactly as gpbs-split; on the crowded 8mix time-sharing with PBS
     # quanta measured ahead of the XCD-block split on 3 of 4 boxes
-    # (profiles/r3/q8_*.json, bench_full_5rep_b.json, bench_all_pool_2rep.json).
+    # (profiles/r3/8mix_queues_q8_*.json, bench_full_5rep_b.json, bench_all_pool_2rep.json).
     "gpbs": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
     # crowded class regions split by whole-XCD blocks instead (class_budget 2)
     "gpbs-split": (4, dict(BUDGET_OVERRIDES), True, "device,se,waveprio,latco,budget,latmem"),
