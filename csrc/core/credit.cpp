@@ -148,6 +148,27 @@ class CreditScheduler : public Scheduler {
   CSlot& sv(int id) { return sv(*E.slots[id]); }
   CDom& sd(Tenant& d) { return *static_cast<CDom*>(d.priv.get()); }
   CDom& sd_of(Slot& v) { return sd(*E.tenants[v.tenant]); }
+
+  // PBS quantum of a slot (:1796-1804).  A tenant in a time-shared class
+  // region (class_budget 1, budget_shared) runs the REGION's quantum: the
+  // largest adaptive quantum among the present co-sharers of its class, so
+  // the region rotates in equal turns.  Per-tenant quanta there are unfair
+  // under credit: a co-sharer that sees no clean counter window keeps the
+  // floor quantum (Q14 skips its periods) while its partners hold 11 ms, and
+  // credit round-robins in quanta -- 2.2 vs 5.8 of 16 partitions in
+  // simulation (tests/test_budget_layout.py), a memory tenant at 0.006 of
+  // the time on MI355X (profiles/r3/bench_full_5rep_c.json, 8mix, gpbs).
+  // The class region is one gang; its quantum still follows the counters.
+  uint32_t pbs_quantum_us(Slot& v) {
+    const Tenant& t = *E.tenants[v.tenant];
+    uint32_t q = sd(*E.tenants[v.tenant]).adapt.tslice_us;
+    if (!t.budget_shared || t.cls < 0) return q;
+    for (auto& tp : E.tenants)
+      if (tp && tp->alive && tp->priv && tp->pool == t.pool && tp->budget_shared && tp->cls == t.cls &&
+          tp->budget_ctx != 0)
+        q = std::max(q, sd(*tp).adapt.tslice_us);
+    return q;
+  }
   Slot& curr(int cpu) { return E.curr_of(cpu); }
   Mask online() { return E.pools[pool_]->cpus; }
 
@@ -1217,7 +1238,7 @@ class CreditScheduler : public Scheduler {
       tslice = std::max<int64_t>((int64_t)ratelimit_us_ * 1000 - runtime, 1000);
     } else if (!snext->is_idle()) {
       if (mode_ == Mode::PBS)
-        tslice = (int64_t)sd_of(*snext).adapt.tslice_us * 1000;
+        tslice = (int64_t)pbs_quantum_us(*snext) * 1000;
       else if (mode_ == Mode::ATC)
         tslice = (int64_t)tslice_us_ * 1000;  // global slice (atc :1916)
     } else {

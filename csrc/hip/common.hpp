@@ -61,6 +61,33 @@ struct alignas(64) WorkQueue {
 // Exit protocol of every tenant kernel: the last workgroup to leave publishes
 // the unit count to the host-visible status word (pinned, system scope), so the
 // runner learns "finished or revoked" from the completion event alone.
+// finish_nf: the same protocol without the agent-scope fences.  On a
+// multi-XCD gfx950 an agent-scope release writes back the XCD's whole L2, so
+// 256 workgroups each fencing after storing their C tiles pay for the dirty
+// lines of everyone's output; ordering is all the protocol needs -- every
+// done increment must be performed before the same workgroup's exited
+// increment -- and a vmcnt(0) wait (atomics count in vmcnt on gfx9) gives
+// exactly that.  Kernel completion still releases C to the host / next
+// kernel.
+__device__ __forceinline__ void finish_nf(WorkQueue* q, u32* status, u32 total) {
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const u32 old = atomicAdd(&q->exited, 1u);
+    if (old == gridDim.x - 1) {
+      const u32 d = __hip_atomic_load(&q->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (status) __hip_atomic_store(status, d | 0x80000000u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (d >= total) {
+        __hip_atomic_store(&q->next, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&q->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&q->exited, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&q->stopped, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int x = 0; x < kXcds; ++x) __hip_atomic_store(&q->xnext[x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
 __device__ __forceinline__ void finish(WorkQueue* q, u32* status, u32 total) {
   if (threadIdx.x == 0) {
     __threadfence();

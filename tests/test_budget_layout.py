@@ -180,3 +180,34 @@ def test_crowded_regions_split_by_xcd_blocks_with_class_budget_2():
         share = (e.tenant_info(t).run_ns - base[t]) / dt
         assert abs(share - _online(e, t)) < 0.2, (t, share, _online(e, t))
     assert e.check() == ""
+
+
+def test_time_shared_region_rotates_in_one_quantum():
+    """A time-shared class region (class_budget 1) rotates its co-sharers in
+    the region's quantum -- the largest adaptive quantum among them -- so a
+    co-sharer whose counters stop (no clean window on the hardware: the PBS
+    idle-sample rule skips its periods and its quantum stays at the floor)
+    still gets its equal turn instead of 1 ms per 11 ms of its partners
+    (csrc/core/credit.cpp pbs_quantum_us; the 8mix: 3 GEMMs + 4 memory
+    tenants of 8 slots each)."""
+    e, parts = _engine(present_us=10000)
+    gs = [e.tenant_create(f"g{i}", nslots=8) for i in range(3)]
+    ms = [e.tenant_create(f"m{i}", nslots=8) for i in range(4)]
+    rates = {**{t: COMPUTE for t in gs}, **{t: MEMORY for t in ms}}
+    for t in rates:
+        e.wake(t)
+    _settle(e, rates, 800)
+    assert all(e.tenant_info(m).tslice_us > 5000 for m in ms)
+    st = e.adapt_state(ms[3])
+    st.tslice_us, st.tick_period_us = 1000, 333
+    e.set_adapt_state(ms[3], st)
+    rates[ms[3]] = (0, 0)  # its counters stop
+    base = {t: e.tenant_info(t).run_ns for t in rates}
+    t0 = e.now()
+    _settle(e, rates, 1600)
+    dt = e.now() - t0
+    share = {t: (e.tenant_info(t).run_ns - base[t]) / dt for t in rates}
+    assert e.tenant_info(ms[3]).tslice_us == 1000  # its own quantum did not move
+    mem = [share[m] for m in ms]
+    assert min(mem) > 3.5 and max(mem) - min(mem) < 0.6, share
+    assert e.check() == ""
