@@ -132,8 +132,16 @@ def test_torn_page_fault_is_caught_by_the_seqlock():
         th.start()
         for t in (r["tenant"] for r in regs):
             d.engine.wake(t)
-        for _ in range(300):
+        import time
+        deadline = time.monotonic() + 10.0
+        k = 0
+        # at least 300 steps; then until the reader has met a torn page (the
+        # torn window is wall-clock: the bridge completes it later)
+        while k < 300 or (seen["retries"] == 0 and time.monotonic() < deadline):
             d.advance_us(250)
+            k += 1
+            if k >= 300 and seen["retries"] == 0:
+                time.sleep(0.001)
         stop.set()
         th.join()
         lib.gpbs_ctl_close(C.c_void_p(h), 0)
