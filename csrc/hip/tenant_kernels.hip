@@ -539,15 +539,21 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
   int units_seen = 0;
 
   for (;;) {
-    const int tile = grab_unit(q, table, mode, me, xcc, s_slot, (u32)ntiles);
+    const int tile = (mode & kGemmXRange) ? grab_unit_x(q, table, mode, me, xcc, s_slot, (u32)ntiles)
+                                          : grab_unit(q, table, mode, me, xcc, s_slot, (u32)ntiles);
     if (tile < 0) break;
     int tm = tile / tiles_n, tn = tile % tiles_n;
     if ((mode & kGemmBlock2D) && (tiles_m & 3) == 0 && (tiles_n & 1) == 0 && ntiles % kXcds == 0) {
-      // 2-D per-XCD blocks (as k_gemm256_bf16_tn): ticket mod 8 follows the
-      // round-robin dispatch, so an XCD's tiles form a (tiles_m/4) x
-      // (tiles_n/2) block: 12 operand-panel slices per K-step in its L2
-      // instead of 18 (PMC: L2 hit rate 0.68 with row-major dealing)
-      const int bm = tiles_m / 4, bn = tiles_n / 2, g = tile % kXcds, jj = tile / kXcds;
+      // 2-D per-XCD blocks (as k_gemm256_bf16_tn): an XCD's tiles form a
+      // (tiles_m/4) x (tiles_n/2) block, 12 operand-panel slices per K-step
+      // in its L2 instead of 18 (PMC: L2 hit rate 0.68 with row-major
+      // dealing).  The XCD of a tile: its range (XCD-range queue: the
+      // workgroup's own XCD), or ticket mod 8 (plain queue: tickets follow
+      // the round-robin dispatch only approximately)
+      const int per = ntiles / kXcds;
+      const int bm = tiles_m / 4, bn = tiles_n / 2;
+      const int g = (mode & kGemmXRange) ? tile / per : tile % kXcds;
+      const int jj = (mode & kGemmXRange) ? tile % per : tile / kXcds;
       tm = (g >> 1) * bm + jj / bn;
       tn = (g & 1) * bn + jj % bn;
     }

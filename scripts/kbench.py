@@ -61,7 +61,7 @@ def main():
              12: "staggered-2d-blocks", 13: "staggered-xcd-range-2d-blocks"}
     if os.environ.get("KBENCH_GEMM_ONLY"):
         names = {4: "staggered-groups", 256: "2phase", 256 | 2048: "2phase-nofence", 256 | 2048 | 1024: "2phase-nofence-ntC",
-                 256 | 2048 | 8: "2phase-nofence-2d"}
+                 256 | 2048 | 8: "2phase-nofence-2d", 256 | 2048 | 9: "2phase-nofence-xrange-2d"}
     ab = {k: [] for k in names}
     for _ in range(5):
         for opt in names:
