@@ -61,15 +61,17 @@ struct alignas(64) WorkQueue {
 // Exit protocol of every tenant kernel: the last workgroup to leave publishes
 // the unit count to the host-visible status word (pinned, system scope), so the
 // runner learns "finished or revoked" from the completion event alone.
-// finish_nf: the same protocol without the agent-scope fences.  On a
+// Last workgroup out reports the unit and resets the queue.  No agent-scope
+// fence: on a
 // multi-XCD gfx950 an agent-scope release writes back the XCD's whole L2, so
 // 256 workgroups each fencing after storing their C tiles pay for the dirty
 // lines of everyone's output; ordering is all the protocol needs -- every
 // done increment must be performed before the same workgroup's exited
 // increment -- and a vmcnt(0) wait (atomics count in vmcnt on gfx9) gives
 // exactly that.  Kernel completion still releases C to the host / next
-// kernel.
-__device__ __forceinline__ void finish_nf(WorkQueue* q, u32* status, u32 total) {
+// kernel.  Measured on the 4096^3 GEMM: 1153 vs 1094 TF/s with the fences
+// (scripts/kbench.py, profiles/r3/kbench_gemm_h.log).
+__device__ __forceinline__ void finish(WorkQueue* q, u32* status, u32 total) {
   if (threadIdx.x == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const u32 old = atomicAdd(&q->exited, 1u);
@@ -88,29 +90,6 @@ __device__ __forceinline__ void finish_nf(WorkQueue* q, u32* status, u32 total) 
   }
 }
 
-__device__ __forceinline__ void finish(WorkQueue* q, u32* status, u32 total) {
-  if (threadIdx.x == 0) {
-    __threadfence();
-    const u32 old = atomicAdd(&q->exited, 1u);
-    if (old == gridDim.x - 1) {
-      __threadfence();
-      const u32 d = __hip_atomic_load(&q->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (status) __hip_atomic_store(status, d | 0x80000000u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      // Last one out of a fully completed invocation leaves the queue zeroed
-      // for the next launch (no per-launch memset on the tenant stream); a
-      // revoked one keeps next/done for the runner's relaunch.
-      if (d >= total) {
-        q->next = 0;
-        q->done = 0;
-        q->exited = 0;
-        q->stopped = 0;
-#pragma unroll
-        for (int x = 0; x < kXcds; ++x) q->xnext[x] = 0;
-        __threadfence();
-      }
-    }
-  }
-}
 
 // Gate modes passed to tenant kernels.
 // GATE_NONE: run anywhere; GATE_TABLE: leave revoked XCDs; GATE_PARK: sleep

@@ -218,7 +218,7 @@ constexpr u32 kGemmBlock2D = 1u << 17; // mode bit: 2-D per-XCD tile blocks
 // tile blocks (12 panel slices per XCD K-step instead of 18): 1129 vs 1117
 // TF/s plain, 1060 with the XCD-range queue (round 2, interleaved, same box;
 // torch.mm 1416) -- panel traffic is not what holds the kernel back.
-static int g_gemm_opts = 4;
+static int g_gemm_opts = 256;  // round 3: the 2-phase kernel (profiles/r3/kbench_gemm_h.log)
 constexpr int kG2Half = 128 * 128;           // bytes per half-tile
 constexpr int kG2Buf = 4 * kG2Half;          // A0 A1 B0 B1
 constexpr int kG2Lds = 2 * kG2Buf;           // 128 KiB
@@ -499,7 +499,7 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restr
 // barrier the reader passes before its read (g0 reads B, A0 of t+1 at int 4:
 // g0 retired them at int 2, g1 at int 3; g1 reads A1 at int 5: g0 retired
 // it at int 4).  Host opts bit 8.
-template <int STAMP, int NTC, int NF>
+template <int STAMP, int NTC>
 __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __restrict__ A, const u16* __restrict__ Bt,
                                                                u16* __restrict__ C, int M, int N, int K, WorkQueue* q,
                                                                const PartTable* table, u32 mode, u32 me, u64* cnt,
@@ -685,8 +685,7 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
     ++units_seen;
     count_unit(cnt, me, xcc, inst_per_tile, &t_last, refs_per_tile, miss_per_tile, q);
   }
-  if constexpr (NF) finish_nf(q, status, (u32)ntiles);
-  else finish(q, status, (u32)ntiles);
+  finish(q, status, (u32)ntiles);
 }
 
 // ------------------------------------------------ GEMM 256x256, 4 waves ----
@@ -1069,13 +1068,10 @@ int gpbs_hip_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int
                          (u32*)status);
       return hipGetLastError() == hipSuccess ? 0 : -5;
     }
-    if (g_gemm_opts & 256) {  // 2 phases per K-tile (4 barriers); bit 10: streaming C stores; bit 11: fence-free finish
-      const bool nt = g_gemm_opts & 1024, nf = g_gemm_opts & 2048;
-      auto k2 = (g_gemm_opts & 64)
-                    ? (nt ? (nf ? k_gemm256s2_bf16_tn<1, 1, 1> : k_gemm256s2_bf16_tn<1, 1, 0>)
-                          : (nf ? k_gemm256s2_bf16_tn<1, 0, 1> : k_gemm256s2_bf16_tn<1, 0, 0>))
-                    : (nt ? (nf ? k_gemm256s2_bf16_tn<0, 1, 1> : k_gemm256s2_bf16_tn<0, 1, 0>)
-                          : (nf ? k_gemm256s2_bf16_tn<0, 0, 1> : k_gemm256s2_bf16_tn<0, 0, 0>));
+    if (g_gemm_opts & 256) {  // 2 phases per K-tile (4 barriers); bit 10: streaming C stores
+      const bool nt = g_gemm_opts & 1024;
+      auto k2 = (g_gemm_opts & 64) ? (nt ? k_gemm256s2_bf16_tn<1, 1> : k_gemm256s2_bf16_tn<1, 0>)
+                                   : (nt ? k_gemm256s2_bf16_tn<0, 1> : k_gemm256s2_bf16_tn<0, 0>);
       hipLaunchKernelGGL(k2, dim3(grid), dim3(G2_NT), 0, s, (const u16*)A, (const u16*)Bt, (u16*)C, M, N, K,
                          (WorkQueue*)q, (const PartTable*)table, m2, me, (u64*)cnt, inst, refs, miss,
                          (u32*)status);

@@ -162,14 +162,16 @@ def test_device_adapt_bit_exact_vs_host():
         assert bytes(got[k].numpy().tobytes()) == ref, k
 
 
-@pytest.mark.parametrize("opts", [0, 1, 2, 3, 4, 5, 16, 32])
+@pytest.mark.parametrize("opts", [0, 1, 2, 3, 4, 5, 16, 32, 256, 256 | 8, 256 | 9, 256 | 1024, 256 | 64])
 def test_gemm256_variants_match_reference(opts):
     """Every 256x256 schedule variant (plain / XCD-range tile queue x one-half-
-    per-phase / deep prefetch) is exact against fp32 on prologue/tail shapes."""
+    per-phase / deep prefetch; the 2-phase kernel -- the default -- with 2-D
+    XCD blocks, streaming C stores and its stamp build) is exact against fp32
+    on prologue/tail shapes."""
     L = K.lib()
     old = L.gpbs_hip_set_gemm_opts(opts)
     try:
-        for M, Nn, Kd in ((256, 256, 64), (512, 256, 128), (256, 512, 192), (1024, 768, 1024)):
+        for M, Nn, Kd in ((256, 256, 64), (512, 256, 128), (256, 512, 192), (1024, 768, 1024), (1024, 512, 512)):
             g = torch.Generator(device="cuda").manual_seed(M * 7 + Kd)
             A = torch.randn(M, Kd, device="cuda", dtype=torch.bfloat16, generator=g)
             B = torch.randn(Nn, Kd, device="cuda", dtype=torch.bfloat16, generator=g)
