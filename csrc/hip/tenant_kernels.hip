@@ -499,7 +499,14 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restr
 // barrier the reader passes before its read (g0 reads B, A0 of t+1 at int 4:
 // g0 retired them at int 2, g1 at int 3; g1 reads A1 at int 5: g0 retired
 // it at int 4).  Host opts bit 8.
-template <int STAMP, int NTC>
+// BAL (opts bit 12): the stamps put interval 1 at ~1100 cycles against ~700
+// for the others -- g1 issues all 8 glds of t+1 there -- so the balanced
+// schedule spreads them: g0 int 0: B0, B1 of t+1, vmcnt(4); int 2: A0, A1,
+// vmcnt(4) (retires B); end of int 3: vmcnt(2) (retires A0 before g0 reads
+// it at int 4).  g1 int 1: B0, B1, A0; int 3: A1, vmcnt(2) (retires B, A0
+// before barrier 3|4); end of int 4: vmcnt(0) (A1, read by g1 at int 5).
+// WAR: g0's A0/A1 restage at int 2 (free from int 0 / int 1 of t).
+template <int STAMP, int NTC, int BAL>
 __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __restrict__ A, const u16* __restrict__ Bt,
                                                                u16* __restrict__ C, int M, int N, int K, WorkQueue* q,
                                                                const PartTable* table, u32 mode, u32 me, u64* cnt,
@@ -599,7 +606,19 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) a[i][s2] = frag(buf, 0, wr, i * 16, s2);
-      if (wr == 0) {
+      if constexpr (BAL) {
+        // balanced staging: g0 4 + 4 glds, g1 6 + 2 (see the schedule note)
+        if (wr == 0) {
+          if (more) {
+            stage(1, 0, t + 1); stage(1, 1, t + 1);
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // retires A0/A1(t) of int 2 of t-1
+          } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
+        } else if (more) {
+          stage(1, 0, t + 1); stage(1, 1, t + 1); stage(0, 0, t + 1);
+        }
+      } else if (wr == 0) {
         if (more) {
           stage(1, 0, t + 1); stage(1, 1, t + 1); stage(0, 0, t + 1);
           asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
@@ -628,7 +647,19 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) a[i][s2] = frag(buf, 0, wr, 64 + i * 16, s2);
-      if (wr == 0) {
+      if constexpr (BAL) {
+        if (wr == 0) {
+          if (more) {
+            stage(0, 0, t + 1); stage(0, 1, t + 1);
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // retires B0/B1(t+1)
+          }
+        } else if (more) {
+          stage(0, 1, t + 1);
+          asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // retires B0/B1/A0(t+1)
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+      } else if (wr == 0) {
         if (more) {
           stage(0, 1, t + 1);
           asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
@@ -648,6 +679,13 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
           for (int j = 0; j < 4; ++j)
             acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j][s2], a[i][s2], acc[4 + i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
+      if constexpr (BAL) {  // end of M_B: g0 retires its A0(t+1), g1 its A1(t+1), before the barrier
+        if (wr == 0) {
+          if (more) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+      }
       __builtin_amdgcn_s_barrier();
       stamp(t, 4);
     }
@@ -1069,9 +1107,10 @@ int gpbs_hip_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int
       return hipGetLastError() == hipSuccess ? 0 : -5;
     }
     if (g_gemm_opts & 256) {  // 2 phases per K-tile (4 barriers); bit 10: streaming C stores
-      const bool nt = g_gemm_opts & 1024;
-      auto k2 = (g_gemm_opts & 64) ? (nt ? k_gemm256s2_bf16_tn<1, 1> : k_gemm256s2_bf16_tn<1, 0>)
-                                   : (nt ? k_gemm256s2_bf16_tn<0, 1> : k_gemm256s2_bf16_tn<0, 0>);
+      const bool nt = g_gemm_opts & 1024, bal = g_gemm_opts & 4096;  // bit 12: balanced staging
+      auto k2 = (g_gemm_opts & 64)
+                    ? (bal ? k_gemm256s2_bf16_tn<1, 0, 1> : (nt ? k_gemm256s2_bf16_tn<1, 1, 0> : k_gemm256s2_bf16_tn<1, 0, 0>))
+                    : (bal ? k_gemm256s2_bf16_tn<0, 0, 1> : (nt ? k_gemm256s2_bf16_tn<0, 1, 0> : k_gemm256s2_bf16_tn<0, 0, 0>));
       hipLaunchKernelGGL(k2, dim3(grid), dim3(G2_NT), 0, s, (const u16*)A, (const u16*)Bt, (u16*)C, M, N, K,
                          (WorkQueue*)q, (const PartTable*)table, m2, me, (u64*)cnt, inst, refs, miss,
                          (u32*)status);
