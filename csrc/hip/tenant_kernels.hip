@@ -506,6 +506,14 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256_bf16_tn(const u16* __restr
 // it at int 4).  g1 int 1: B0, B1, A0; int 3: A1, vmcnt(2) (retires B, A0
 // before barrier 3|4); end of int 4: vmcnt(0) (A1, read by g1 at int 5).
 // WAR: g0's A0/A1 restage at int 2 (free from int 0 / int 1 of t).
+// BAL 2 (opts bit 13): A half h is read only by group h, so each group
+// stages its OWN A half alone (4 glds per wave) in its R_B interval, and both
+// groups stage their share of the B halves in R_A: 4 glds in every read
+// interval.  g0 int 0: B0, B1 of t+1; int 2: A0 of t+1, vmcnt(4) (retires
+// B); end of int 3: vmcnt(0) (A0 before g0 reads it at int 4).  g1 int 1:
+// B0, B1; int 3: A1, vmcnt(4) (B retired before barrier 3|4); end of int 4:
+// vmcnt(0) (A1 before g1 reads it at int 5).  WAR: A0 free from int 0 of t,
+// A1 from int 1, B from int 3 of t-1.
 template <int STAMP, int NTC, int BAL>
 __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __restrict__ A, const u16* __restrict__ Bt,
                                                                u16* __restrict__ C, int M, int N, int K, WorkQueue* q,
@@ -536,6 +544,14 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
   for (int j = 0; j < 2; ++j) {
     const int row = 8 * (2 * wid + j) + (lane >> 3);
     soff[j] = row * K + (((lane & 7) ^ g2_swz(row)) * 8);
+  }
+  // BAL 2: a group stages its own A half alone -- wave wc of the group
+  // writes rows 32 wc .. 32 wc + 31 (4 glds)
+  int soffa[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = 8 * (4 * (wid & 3) + j) + (lane >> 3);
+    soffa[j] = row * K + (((lane & 7) ^ g2_swz(row)) * 8);
   }
   const int l16 = lane & 15, lq = lane >> 4;
   const int bh = wc >> 1, bc = (wc & 1) * 64;
@@ -572,6 +588,12 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
       glds16(src + soff[0], dst);
       glds16(src + soff[1], dst + 1024);
     };
+    auto stage_own_a = [&](int t) {  // all of A half wr of K-tile t, by this group
+      const u16* src = Ab + (size_t)wr * 128 * K + t * G2_BK;
+      lds_t* dst = lds + (t & 1) * kG2Buf + wr * kG2Half + (wid & 3) * 4096;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) glds16(src + soffa[j], dst + j * 1024);
+    };
     auto frag = [&](int b, int kind, int h, int r0, int s) -> bf16x8 {
       const int r = r0 + l16;
       const lds_t* p = lds + b * kG2Buf + (kind * 2 + h) * kG2Half + r * 128 + (((4 * s + lq) ^ g2_swz(r)) << 4);
@@ -606,7 +628,13 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) a[i][s2] = frag(buf, 0, wr, i * 16, s2);
-      if constexpr (BAL) {
+      if constexpr (BAL == 2) {  // 4 glds per read interval: B halves here, own A half in R_B
+        if (more) {
+          stage(1, 0, t + 1); stage(1, 1, t + 1);
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+      } else if constexpr (BAL) {
         // balanced staging: g0 4 + 4 glds, g1 6 + 2 (see the schedule note)
         if (wr == 0) {
           if (more) {
@@ -647,7 +675,12 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) a[i][s2] = frag(buf, 0, wr, 64 + i * 16, s2);
-      if constexpr (BAL) {
+      if constexpr (BAL == 2) {
+        if (more) {
+          stage_own_a(t + 1);
+          asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // retires this group's B0/B1(t+1)
+        }
+      } else if constexpr (BAL) {
         if (wr == 0) {
           if (more) {
             stage(0, 0, t + 1); stage(0, 1, t + 1);
@@ -679,7 +712,9 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
           for (int j = 0; j < 4; ++j)
             acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j][s2], a[i][s2], acc[4 + i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
-      if constexpr (BAL) {  // end of M_B: g0 retires its A0(t+1), g1 its A1(t+1), before the barrier
+      if constexpr (BAL == 2) {  // end of M_B: the group's own A half of t+1 lands before its next R_A
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else if constexpr (BAL) {  // end of M_B: g0 retires its A0(t+1), g1 its A1(t+1), before the barrier
         if (wr == 0) {
           if (more) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
         } else {
@@ -1107,10 +1142,15 @@ int gpbs_hip_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int
       return hipGetLastError() == hipSuccess ? 0 : -5;
     }
     if (g_gemm_opts & 256) {  // 2 phases per K-tile (4 barriers); bit 10: streaming C stores
-      const bool nt = g_gemm_opts & 1024, bal = g_gemm_opts & 4096;  // bit 12: balanced staging
+      // bit 12: balanced staging; bit 13: each group stages its own A half (4 glds per read interval)
+      const bool nt = g_gemm_opts & 1024, bal = g_gemm_opts & 4096, own = g_gemm_opts & 8192;
       auto k2 = (g_gemm_opts & 64)
-                    ? (bal ? k_gemm256s2_bf16_tn<1, 0, 1> : (nt ? k_gemm256s2_bf16_tn<1, 1, 0> : k_gemm256s2_bf16_tn<1, 0, 0>))
-                    : (bal ? k_gemm256s2_bf16_tn<0, 0, 1> : (nt ? k_gemm256s2_bf16_tn<0, 1, 0> : k_gemm256s2_bf16_tn<0, 0, 0>));
+                    ? (own ? k_gemm256s2_bf16_tn<1, 0, 2>
+                           : bal ? k_gemm256s2_bf16_tn<1, 0, 1>
+                                 : (nt ? k_gemm256s2_bf16_tn<1, 1, 0> : k_gemm256s2_bf16_tn<1, 0, 0>))
+                    : (own ? k_gemm256s2_bf16_tn<0, 0, 2>
+                           : bal ? k_gemm256s2_bf16_tn<0, 0, 1>
+                                 : (nt ? k_gemm256s2_bf16_tn<0, 1, 0> : k_gemm256s2_bf16_tn<0, 0, 0>));
       hipLaunchKernelGGL(k2, dim3(grid), dim3(G2_NT), 0, s, (const u16*)A, (const u16*)Bt, (u16*)C, M, N, K,
                          (WorkQueue*)q, (const PartTable*)table, m2, me, (u64*)cnt, inst, refs, miss,
                          (u32*)status);
