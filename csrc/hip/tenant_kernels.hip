@@ -218,7 +218,7 @@ constexpr u32 kGemmBlock2D = 1u << 17; // mode bit: 2-D per-XCD tile blocks
 // tile blocks (12 panel slices per XCD K-step instead of 18): 1129 vs 1117
 // TF/s plain, 1060 with the XCD-range queue (round 2, interleaved, same box;
 // torch.mm 1416) -- panel traffic is not what holds the kernel back.
-static int g_gemm_opts = 256;  // round 3: the 2-phase kernel (profiles/r3/kbench_gemm_h.log)
+static int g_gemm_opts = 256 | 8192;  // round 3: the 2-phase kernel, own-A-half staging (profiles/r3/kbench_gemm_k.log)
 constexpr int kG2Half = 128 * 128;           // bytes per half-tile
 constexpr int kG2Buf = 4 * kG2Half;          // A0 A1 B0 B1
 constexpr int kG2Lds = 2 * kG2Buf;           // 128 KiB
