@@ -239,6 +239,9 @@ def main(argv=None):
             reps[p].append(r)
             print(f"[llm] {p} rep {rep}: {json.dumps({k: v for k, v in r.items() if not k.startswith('_')})}",
                   file=sys.stderr, flush=True)
+            if a.out:  # every finished run survives a time limit
+                with open(a.out + ".partial", "w") as f:
+                    json.dump({"solo": res.get("solo"), "reps": reps}, f)
             if "_hw" in r:
                 print(f"[llm] {p} rep {rep} hw: {json.dumps(r['_hw'])}", file=sys.stderr, flush=True)
     summary = {}
