@@ -58,7 +58,7 @@ def main():
                     help="steady: tenants backlogged over common step windows (weighted speedup, default); "
                          "quota: round-1 fixed per-step quotas (early finishers idle)")
     ap.add_argument("--step-ms", type=float, default=80.0, help="steady protocol: step window length")
-    ap.add_argument("--gang-transport", default="shm", choices=["shm", "dist"],
+    ap.add_argument("--gang-transport", default="shm", choices=["shm", "dist", "xgmi"],
                     help="N > 1 gang epochs: native shared memory among the node's ranks, or the 'gang' process "
                          "group (gloo; RCCL over xGMI with --gang-rccl)")
     ap.add_argument("--gang-rccl", action="store_true", help="with --gang-transport dist: the gang group is RCCL")

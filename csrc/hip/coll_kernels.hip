@@ -161,6 +161,73 @@ __global__ __launch_bounds__(CNT) void k_allreduce(const CollDesc* __restrict__ 
   }
 }
 
+// ---- gang epoch exchange over xGMI (the scheduler's cross-GPU
+// barrier on the device, next to the host shm transport) -------------------
+// Every rank owns a board in uncached device memory, IPC-mapped by every
+// peer: [2 parities][world][stride] int64 words, slot r = rank r's entry
+// (word 0: the exchange's sequence number, words 1..nvals: its values).  One
+// exchange (one 64-lane wave): write this rank's values into its slot of
+// EVERY peer's board, then its sequence number with a system-scope release;
+// wait until every slot of its own board carries the sequence; copy the rows
+// to the caller's pinned buffer.  Two parities: a rank starts exchange k+1
+// only after finishing k, which needs every peer's write of k, which each
+// peer makes only after finishing k-1 -- so k+1 never overwrites a slot
+// someone still reads for k-1... and k+2 (same parity as k) is written only
+// after every peer finished k.  A wait longer than yield_ticks leaves with
+// status 1 and the host relaunches (a spinning grid must not hold a GPU it
+// may share with a peer's queues; the lesson of k_allreduce).
+struct GangDesc {
+  long long* board[kCollMax];  // rank q's board, mapped into this process
+  u32 rank, world, stride, nvals;
+};
+
+__global__ __launch_bounds__(64) void k_gang_exchange(const GangDesc* __restrict__ d, u32 seq,
+                                                       const long long* __restrict__ vals, long long* out,
+                                                       u32* status, u64 yield_ticks) {
+  const u32 rank = d->rank, world = d->world, stride = d->stride, nv = d->nvals;
+  const u32 par = seq & 1u;
+  const size_t slot = ((size_t)par * world + rank) * stride;
+  // 1. publish: values, then the sequence number, into every peer's board
+  for (u32 s = 0; s < world; ++s)
+    for (u32 t = threadIdx.x; t < nv; t += 64)
+      __hip_atomic_store(d->board[s] + slot + 1 + t, vals[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: the values before the sequence numbers
+  __syncthreads();                                 // ... every lane's values, not just its own
+  if (threadIdx.x < world)
+    __hip_atomic_store(d->board[threadIdx.x] + slot, (long long)seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  // 2. wait for every rank's entry on this rank's board
+  long long* mine = d->board[rank] + (size_t)par * world * stride;
+  int ok = 1;
+  if (threadIdx.x == 0) {
+    const u64 t0 = wall_clock64();
+    for (;;) {
+      bool all = true;
+      for (u32 r = 0; r < world; ++r)
+        if (__hip_atomic_load(mine + (size_t)r * stride, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < (long long)seq)
+          all = false;
+      if (all) break;
+      if (wall_clock64() - t0 > yield_ticks) {
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  ok = __shfl(ok, 0);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  if (!ok) {
+    if (threadIdx.x == 0) __hip_atomic_store(status, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
+  // 3. every rank's row to the caller
+  for (u32 r = 0; r < world; ++r)
+    for (u32 t = threadIdx.x; t < nv; t += 64)
+      out[(size_t)r * nv + t] =
+          __hip_atomic_load(mine + (size_t)r * stride + 1 + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  if (threadIdx.x == 0) __hip_atomic_store(status, 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 }  // namespace gpbs_hip
 
 using namespace gpbs_hip;
@@ -168,6 +235,14 @@ using namespace gpbs_hip;
 extern "C" {
 
 int gpbs_hip_coll_desc_size(void) { return (int)sizeof(CollDesc); }
+int gpbs_hip_gang_desc_size(void) { return (int)sizeof(GangDesc); }
+
+int gpbs_hip_gang_exchange(const void* desc, unsigned seq, const void* vals, void* out, void* status,
+                           unsigned long long yield_ticks, hipStream_t s) {
+  hipLaunchKernelGGL(k_gang_exchange, dim3(1), dim3(64), 0, s, (const GangDesc*)desc, seq, (const long long*)vals,
+                     (long long*)out, (u32*)status, (u64)yield_ticks);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
 
 // desc: device CollDesc; bytes: per-buffer size (multiple of 16 * world);
 // seq: the unit's collective sequence number (0, 1, ...).

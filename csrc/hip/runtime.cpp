@@ -58,6 +58,8 @@ int gpbs_hip_switch_probe(const void*, int, unsigned*, int, unsigned, unsigned l
 int gpbs_hip_hwc_attribute(const void*, void*, void*, hipStream_t);
 int gpbs_hip_allreduce(const void*, unsigned, unsigned long long, unsigned, void*, const void*, unsigned, unsigned,
                        void*, void*, int, unsigned long long, unsigned long long, hipStream_t);
+int gpbs_hip_gang_desc_size(void);
+int gpbs_hip_gang_exchange(const void*, unsigned, const void*, void*, void*, unsigned long long, hipStream_t);
 int gpbs_hip_coll_desc_size(void);
 }
 
@@ -2443,6 +2445,162 @@ int gpbs_coll_copy(void* p, int which, void* dptr, unsigned long long bytes, int
   const hipError_t e = to_coll ? hipMemcpy(buf, dptr, bytes, hipMemcpyDeviceToDevice)
                                : hipMemcpy(dptr, buf, bytes, hipMemcpyDeviceToDevice);
   return e == hipSuccess ? 0 : -5;
+}
+
+// ---- gang epoch exchange over xGMI (coll_kernels.hip k_gang_exchange) ----
+struct GangDescHost {
+  long long* board[kCollMax];
+  u32 rank, world, stride, nvals;
+};
+
+struct GangX {
+  int device = 0, rank = 0, world = 1, nvals = 0;
+  size_t board_bytes = 0;
+  long long* board = nullptr;          // this rank's board (uncached VRAM)
+  void* peer[kCollMax] = {};           // opened IPC mappings
+  GangDescHost desc{};
+  void* d_desc = nullptr;
+  long long* h_vals = nullptr;         // pinned: this rank's values
+  long long* h_out = nullptr;          // pinned: world x nvals rows
+  u32* h_status = nullptr;             // pinned: 0 running, 1 yielded, 2 done
+  hipStream_t stream = nullptr;
+  uint64_t exchanges = 0, relaunches = 0, timeouts = 0;
+};
+
+void* gpbs_gangx_create(int device, int rank, int world, int nvals) {
+  if (world < 1 || world > kCollMax || rank < 0 || rank >= world || nvals < 1 || nvals > 256) return nullptr;
+  if ((int)sizeof(GangDescHost) != gpbs_hip_gang_desc_size()) return nullptr;
+  if (hipSetDevice(device) != hipSuccess) return nullptr;
+  auto* g = new GangX;
+  g->device = device;
+  g->rank = rank;
+  g->world = world;
+  g->nvals = nvals;
+  const u32 stride = (u32)((nvals + 1 + 7) & ~7);  // 64-byte rows
+  g->board_bytes = (size_t)2 * world * stride * sizeof(long long);
+  bool ok = hipExtMallocWithFlags((void**)&g->board, g->board_bytes, hipDeviceMallocUncached) == hipSuccess &&
+            hipMemset(g->board, 0, g->board_bytes) == hipSuccess &&
+            hipMalloc(&g->d_desc, sizeof(GangDescHost)) == hipSuccess &&
+            hipHostMalloc((void**)&g->h_vals, sizeof(long long) * nvals, hipHostMallocCoherent) == hipSuccess &&
+            hipHostMalloc((void**)&g->h_out, sizeof(long long) * nvals * world, hipHostMallocCoherent) == hipSuccess &&
+            hipHostMalloc((void**)&g->h_status, sizeof(u32), hipHostMallocCoherent) == hipSuccess &&
+            hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) == hipSuccess &&
+            hipDeviceSynchronize() == hipSuccess;
+  if (!ok) {
+    if (g->board) hipFree(g->board);
+    if (g->d_desc) hipFree(g->d_desc);
+    if (g->h_vals) hipHostFree(g->h_vals);
+    if (g->h_out) hipHostFree(g->h_out);
+    if (g->h_status) hipHostFree(g->h_status);
+    delete g;
+    return nullptr;
+  }
+  g->desc.rank = (u32)rank;
+  g->desc.world = (u32)world;
+  g->desc.stride = stride;
+  g->desc.nvals = (u32)nvals;
+  g->desc.board[rank] = g->board;
+  return g;
+}
+
+int gpbs_gangx_handle_bytes(void) { return (int)sizeof(hipIpcMemHandle_t); }
+
+int gpbs_gangx_export(void* p, void* out) {
+  GangX* g = (GangX*)p;
+  if (!g || !out) return -22;
+  hipSetDevice(g->device);
+  hipIpcMemHandle_t h;
+  if (hipIpcGetMemHandle(&h, g->board) != hipSuccess) return -5;
+  std::memcpy(out, &h, sizeof(h));
+  return (int)sizeof(h);
+}
+
+int gpbs_gangx_open(void* p, int peer, const void* handle) {
+  GangX* g = (GangX*)p;
+  if (!g || !handle || peer < 0 || peer >= g->world || peer == g->rank) return -22;
+  hipSetDevice(g->device);
+  if (!g->peer[peer]) {
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, handle, sizeof(h));
+    if (hipIpcOpenMemHandle(&g->peer[peer], h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+      g->peer[peer] = nullptr;
+      return -5;
+    }
+  }
+  g->desc.board[peer] = (long long*)g->peer[peer];
+  return 0;
+}
+
+int gpbs_gangx_finalize(void* p) {
+  GangX* g = (GangX*)p;
+  if (!g) return -22;
+  for (int r = 0; r < g->world; ++r)
+    if (!g->desc.board[r]) return -19;
+  hipSetDevice(g->device);
+  return hipMemcpy(g->d_desc, &g->desc, sizeof(g->desc), hipMemcpyHostToDevice) == hipSuccess ? 0 : -5;
+}
+
+// One exchange: this rank's n values in, every rank's rows out (world x
+// nvals, rank order).  seq: 1, 2, ... (the same on every rank).  Returns 0,
+// or -110 when deadline_ns (CLOCK_MONOTONIC) passed first -- the rank then
+// treats the gang as failed (the caller degrades to local scheduling); a
+// kernel still in flight leaves within its 200 us yield bound.
+int gpbs_gangx_exchange(void* p, unsigned seq, const long long* vals, int n, long long* out, long long deadline_ns) {
+  GangX* g = (GangX*)p;
+  if (!g || !vals || !out || n < 0 || n > g->nvals || seq == 0) return -22;
+  hipSetDevice(g->device);
+  hipStreamSynchronize(g->stream);  // a yielded / abandoned launch has left
+  for (int k = 0; k < g->nvals; ++k) g->h_vals[k] = k < n ? vals[k] : 0;
+  constexpr unsigned long long kYieldTicks = 20000;  // 200 us of the 100 MHz wall clock
+  for (;;) {
+    __atomic_store_n(g->h_status, 0u, __ATOMIC_RELEASE);
+    if (gpbs_hip_gang_exchange(g->d_desc, seq, g->h_vals, g->h_out, g->h_status, kYieldTicks, g->stream)) return -5;
+    u32 st = 0;
+    for (;;) {
+      st = __atomic_load_n(g->h_status, __ATOMIC_ACQUIRE);
+      if (st) break;
+      if (mono_ns() > deadline_ns) {
+        g->timeouts++;
+        return -110;
+      }
+      std::this_thread::yield();
+    }
+    if (st == 2) break;
+    g->relaunches++;
+    hipStreamSynchronize(g->stream);
+    if (mono_ns() > deadline_ns) {
+      g->timeouts++;
+      return -110;
+    }
+  }
+  std::memcpy(out, g->h_out, sizeof(long long) * (size_t)g->nvals * g->world);
+  g->exchanges++;
+  return 0;
+}
+
+int gpbs_gangx_stats(void* p, uint64_t* out3) {
+  GangX* g = (GangX*)p;
+  if (!g || !out3) return -22;
+  out3[0] = g->exchanges;
+  out3[1] = g->relaunches;
+  out3[2] = g->timeouts;
+  return 0;
+}
+
+void gpbs_gangx_destroy(void* p) {
+  GangX* g = (GangX*)p;
+  if (!g) return;
+  hipSetDevice(g->device);
+  hipStreamSynchronize(g->stream);
+  hipStreamDestroy(g->stream);
+  for (int r = 0; r < kCollMax; ++r)
+    if (g->peer[r]) hipIpcCloseMemHandle(g->peer[r]);
+  hipFree(g->board);
+  hipFree(g->d_desc);
+  hipHostFree(g->h_vals);
+  hipHostFree(g->h_out);
+  hipHostFree(g->h_status);
+  delete g;
 }
 
 void gpbs_coll_destroy(void* p) {

@@ -133,5 +133,14 @@ def bind(lib):
     _p(lib, "gpbs_coll_finalize", C.c_int, vp)
     _p(lib, "gpbs_coll_buffer", vp, vp, C.c_int)
     _p(lib, "gpbs_coll_destroy", None, vp)
+    _p(lib, "gpbs_gangx_create", vp, C.c_int, C.c_int, C.c_int, C.c_int)
+    _p(lib, "gpbs_gangx_handle_bytes", C.c_int)
+    _p(lib, "gpbs_gangx_export", C.c_int, vp, vp)
+    _p(lib, "gpbs_gangx_open", C.c_int, vp, C.c_int, vp)
+    _p(lib, "gpbs_gangx_finalize", C.c_int, vp)
+    _p(lib, "gpbs_gangx_exchange", C.c_int, vp, C.c_uint, C.POINTER(C.c_longlong), C.c_int,
+       C.POINTER(C.c_longlong), C.c_longlong)
+    _p(lib, "gpbs_gangx_stats", C.c_int, vp, C.POINTER(u64))
+    _p(lib, "gpbs_gangx_destroy", None, vp)
     _p(lib, "gpbs_coll_copy", C.c_int, vp, C.c_int, vp, C.c_ulonglong, C.c_int)
     _p(lib, "gpbs_runner_destroy", None, vp)

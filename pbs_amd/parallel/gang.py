@@ -176,6 +176,74 @@ class _ShmTransport:
             self.h = None
 
 
+class _XgmiTransport:
+    """Device-side epoch exchange over xGMI: every rank's board
+    in uncached VRAM, IPC-mapped by every peer; one exchange is one 64-lane
+    kernel that writes this rank's values and sequence number into every
+    peer's board and waits for every peer's (csrc/hip/coll_kernels.hip
+    ``k_gang_exchange``).  Handles are swapped once, at start-up, over the
+    host group; no host collective runs per epoch.  A missed deadline
+    degrades the rank to local scheduling (no re-formation: the view is the
+    rank set the boards were mapped for)."""
+
+    def __init__(self, rank: int, world: int, nvals: int, device: int, gather: Callable):
+        from ..ops.kernels import lib as hiplib
+        self.L = hiplib()
+        self.world, self.nvals = world, nvals
+        h = self.L.gpbs_gangx_create(device, rank, world, nvals)
+        if not h:
+            raise RuntimeError("gpbs_gangx_create failed")
+        self.h = C.c_void_p(h)
+        nb = self.L.gpbs_gangx_handle_bytes()
+        buf = (C.c_char * nb)()
+        if self.L.gpbs_gangx_export(self.h, buf) != nb:
+            self.close()
+            raise RuntimeError("hipIpcGetMemHandle (gang board) failed")
+        for peer, hb in enumerate(gather(bytes(buf))):
+            if peer != rank and self.L.gpbs_gangx_open(self.h, peer, (C.c_char * nb).from_buffer_copy(hb)):
+                self.close()
+                raise RuntimeError(f"hipIpcOpenMemHandle of rank {peer}'s gang board failed")
+        if self.L.gpbs_gangx_finalize(self.h):
+            self.close()
+            raise RuntimeError("gpbs_gangx_finalize failed")
+        self.seq = 0
+        self.members = list(range(world))
+        self.excluded = False
+        self.why = ""
+
+    def _gather(self, vals, deadline_ns):
+        n = self.nvals
+        vals = list(vals) + [0] * (n - len(vals))
+        self.seq += 1
+        src = (C.c_longlong * n)(*vals)
+        out = (C.c_longlong * (n * self.world))()
+        rc = self.L.gpbs_gangx_exchange(self.h, self.seq, src, n, out, int(deadline_ns))
+        if rc == -110:
+            self.why = "timeout"
+            return None
+        if rc:
+            raise RuntimeError(f"gang xGMI exchange failed ({rc})")
+        return [list(out[r * n:(r + 1) * n]) for r in range(self.world)]
+
+    def reduce_min(self, vals, deadline_ns):
+        rows = self._gather(vals, deadline_ns)
+        return None if rows is None else [min(c) for c in zip(*rows)][:len(vals)]
+
+    def reduce_sum(self, vals, deadline_ns):
+        rows = self._gather(vals, deadline_ns)
+        return None if rows is None else [sum(c) for c in zip(*rows)][:len(vals)]
+
+    def stats(self) -> Dict[str, int]:
+        o = (C.c_uint64 * 3)()
+        self.L.gpbs_gangx_stats(self.h, o)
+        return {"exchanges": o[0], "relaunches": o[1], "timeouts": o[2]}
+
+    def close(self):
+        if self.h:
+            self.L.gpbs_gangx_destroy(self.h)
+            self.h = None
+
+
 class GangCoordinator:
     def __init__(self, engine, group, tenants: List[int], epoch_ms: float = 4.0, share: float = 0.5,
                  device: Optional[str] = None, demand: Optional[Callable[[int], bool]] = None,
@@ -294,6 +362,16 @@ class GangCoordinator:
 
     # --------------------------------------------------------------- loop
     def _make_transport(self, nvals: int):
+        if self.transport == "xgmi":
+            dev = torch.device(self.device) if self.device else torch.device("cuda", torch.cuda.current_device())
+            group = self.group
+
+            def gather(obj):
+                out = [None] * self.world
+                dist.all_gather_object(out, obj, group=group)
+                return out
+            return _XgmiTransport(self.rank, self.world, max(nvals, 4 * len(self.metric_tenants)),
+                                  dev.index or 0, gather)
         if self.transport == "shm":
             if not self.shm_name:
                 raise ValueError("transport 'shm' needs shm_name (the same fresh name on every rank)")
