@@ -148,15 +148,21 @@ def run(policy: str, kinds, args: dict, seconds: float, warmup: float) -> Dict[s
         from ..runtime.daemon import Daemon
         sock = os.path.join(tempfile.mkdtemp(), "gpbsd.sock")
         daemon = Daemon(sock, gpus=[0], nctx=2, sim=False, profile="mi355x").start()
-    elif policy == "gpbs-se":
+    elif policy in ("gpbs-se", "gpbs-budget"):
         # SE-exclusive class split driven by LIVE hardware counters: the daemon
         # owns the GPU actuator + rocprofiler-sdk sampler; the tenants' kernels
         # run on streams masked to the shader engines they own, so the per-SE
         # counters are attributed to them by ownership (no declared counters).
         from ..runtime.daemon import Daemon
         sock = os.path.join(tempfile.mkdtemp(), "gpbsd.sock")
+        over = {"class_split": 2, "idle_skip": 1, "class_dwell": 8}
+        if policy == "gpbs-budget":
+            # the round-3 runner flagship's layout: demand-driven SE budgets
+            # (probe layout until both tenants are classified, then compute
+            # SEs {0,1} / memory SEs {2,3}), surplus slots offline
+            over.update(class_budget=1, present_us=10000)
         daemon = Daemon(sock, gpus=[0], nctx=4, sim=False, profile="mi355x", attach_gpu=True, se_mode=True,
-                        hw_counters=_HWC["on"], overrides={"class_split": 2, "idle_skip": 1, "class_dwell": 8}).start()
+                        hw_counters=_HWC["on"], overrides=over).start()
         args["slots"] = 16
         args["spatial"] = True
     ps = [ctx.Process(target=_tenant, args=(k, seconds, warmup, sock, q, start, args)) for k in kinds]
@@ -165,10 +171,21 @@ def run(policy: str, kinds, args: dict, seconds: float, warmup: float) -> Dict[s
     time.sleep(0.5)
     start.set()
     out = {}
+    hw_early = None
     try:
         for _ in ps:
             r = q.get(timeout=900)
             out[r["kind"]] = r
+            if hw_early is None and daemon is not None and daemon.gpu_ctx is not None and daemon.hw_counters:
+                # every tenant still registered: the first to finish is reaped
+                # soon after its process exits
+                e = daemon.engine
+                hw_early = {}
+                for t in e.tenants():
+                    att, _ = daemon.gpu_ctx.hwc_tenant(t)
+                    hw_early[e.tenant_info(t).name] = {
+                        "inst": round(att[0]), "miss_rate": round(att[3] * 1e5 / att[0]) if att[0] else None,
+                        "class": e.lib.gpbs_tenant_class(e.h, t), "owned_s": daemon.gpu_ctx.ownership(t)}
     finally:
         for p in ps:
             p.join(timeout=120)
@@ -181,7 +198,7 @@ def run(policy: str, kinds, args: dict, seconds: float, warmup: float) -> Dict[s
                     if att[0]:
                         hw[e.tenant_info(t).name] = {"inst": round(att[0]), "miss_rate": round(att[3] * 1e5 / att[0]),
                                                      "cpi_x1000": round(att[1] * 1e3 / att[0])}
-                out["_hw"] = {"tenant": hw, "stats": daemon.gpu_ctx.hwc_stats(),
+                out["_hw"] = {"tenant": hw, "at_first_finish": hw_early, "stats": daemon.gpu_ctx.hwc_stats(),
                               "owned_s": {e.tenant_info(t).name: daemon.gpu_ctx.ownership(t) for t in e.tenants()}}
             out["_engine"] = {"z": e.debug_keys("z")[-3000:], "tenants": {
                 e.tenant_info(t).name: {"tslice_us": e.tenant_info(t).tslice_us, "phase": e.tenant_info(t).phase,
@@ -216,7 +233,7 @@ def main(argv=None):
             "infer_weight": 512, "train_weight": 256, "fp8": a.fp8, "graph": a.graph and a.fp8}
     res = {}
     pols = [p for p in a.policies.split(",") if p]
-    if "gpbs-se" in pols:
+    if "gpbs-se" in pols or "gpbs-budget" in pols:
         _hwc_setup()
     if a.out and os.path.exists(a.out):
         raise SystemExit(f"{a.out} exists: results are never overwritten")
