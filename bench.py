@@ -70,6 +70,10 @@ def main():
                     help="N > 1 all-reduce tenant: ipc (gated gpbs kernel over IPC-mapped peer buffers, xGMI; "
                          "default) or rccl (torch.distributed all-reduce, not CU-confined)")
     ap.add_argument("--out", default="")
+    ap.add_argument("--rehearse-ipc", action="store_true",
+                    help="like --rehearse (every rank on GPU 0, gloo) but with the gated IPC all-reduce tenant on "
+                         "the GPU: rehearses the whole N > 1 path (IPC self-test, P2P-flag barrier, gang epochs, "
+                         "agreed stop) on one GPU; numbers are not a measurement")
     ap.add_argument("--rehearse", action="store_true",
                     help="multi-rank control-flow rehearsal on ONE GPU: every rank on cuda:0, gloo for the default "
                          "group and the all-reduce tenant (CPU tensors); numbers are not a measurement")
@@ -93,6 +97,8 @@ def main():
     if args.gpus > 1 and world == 1:
         print("bench.py: --gpus > 1 must be launched with torch.distributed.run (one rank per GPU)", file=sys.stderr)
         sys.exit(2)
+    if args.rehearse_ipc:
+        args.rehearse = True
     if args.rehearse:
         local = 0
     counters = args.counters
@@ -162,7 +168,8 @@ def main():
                           coll_impl=args.coll)
         if args.rehearse:
             cfg.coll_bytes = 4 << 20  # CPU gloo all-reduce stand-in
-        c = Corun(cfg, rank=rank, world=world, device=local, groups=groups, log=log, coll_on_cpu=args.rehearse)
+        c = Corun(cfg, rank=rank, world=world, device=local, groups=groups, log=log,
+                  coll_on_cpu=args.rehearse and not args.rehearse_ipc)
         c.calibrate()
         rng = random.Random(args.seed)
         runs = {p: [] for p in pols}
