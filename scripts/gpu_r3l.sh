@@ -14,3 +14,6 @@ step() {  # step NAME SECONDS cmd...
 }
 step gang_xgmi_test 200 python -u -m pytest tests/test_gpu_gang_xgmi.py -x -v -s --timeout 150 --timeout-method thread -p no:cacheprovider
 step bench_full_e 600 python -u bench.py --out gpurun_out/bench_full_e.json
+step rehearse_ipc2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+  --master-port 29531 bench.py --gpus 2 --rehearse-ipc --counters model --mix 4mix --policies none,gpbs --reps 1 \
+  --steps 5 --warmup 2 --out gpurun_out/rehearse_ipc2.json
