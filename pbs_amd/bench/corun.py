@@ -1055,6 +1055,7 @@ class Corun:
                 eng["gang"] = self.gang.stats()
                 names = {v: k for k, v in self.tid.items()}
                 eng["node_metrics"] = {names.get(t, t): m for t, m in self.gang.node_metrics.items()}
+                eng["node_totals"] = {names.get(t, t): m for t, m in self.gang.node_totals.items()}
             res["engine"] = eng
             diag = os.environ.get("GPBS_DIAG_DIR")
             if diag and self.rank == 0:

@@ -120,7 +120,8 @@ def metrics_sum_worker(rank: int, world: int, port: int, q, transport: str = "di
         time.sleep(0.005)
     node = {t: dict(g.node_metrics.get(t, {})) for t in ts}
     g.stop()
-    q.put({"rank": rank, "local": local, "node": node, "syncs": g.metric_syncs,
+    totals = {t: dict(g.node_totals.get(t, {})) for t in ts}
+    q.put({"rank": rank, "local": local, "node": node, "totals": totals, "syncs": g.metric_syncs,
            "still": {t: list(e.tenant_info(t).pmc) for t in ts}})
     dist.destroy_process_group()
 

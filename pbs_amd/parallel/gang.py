@@ -274,6 +274,9 @@ class GangCoordinator:
         self.metric_tenants = list(metric_tenants or [])
         self.metric_every = max(1, int(metric_every))
         self.node_metrics: Dict[int, Dict[str, int]] = {}
+        # node-wide totals over every metric exchange of the run (the last
+        # period alone reads zero once the tenants have drained)
+        self.node_totals: Dict[int, Dict[str, int]] = {}
         self.metric_syncs = 0
         self.transport = transport
         self.shm_name = shm_name
@@ -502,6 +505,11 @@ class GangCoordinator:
             out[t] = {"inst": inst, "cycles": cyc, "l2_refs": ref, "l2_misses": miss,
                       "miss_rate": miss * 100000 // inst if inst else 0}
         self.node_metrics = out
+        for t, m in out.items():
+            tot = self.node_totals.setdefault(t, {"inst": 0, "cycles": 0, "l2_refs": 0, "l2_misses": 0})
+            for k in tot:
+                tot[k] += m[k]
+            tot["miss_rate"] = tot["l2_misses"] * 100000 // tot["inst"] if tot["inst"] else 0
         self.metric_syncs += 1
         return True
 

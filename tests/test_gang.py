@@ -122,6 +122,9 @@ def test_node_metrics_are_exactly_the_sum_of_per_rank_counters(transport):
             n = out[r]["node"][t]
             assert [n["inst"], n["cycles"], n["l2_refs"], n["l2_misses"]] == want, (t, r, n, want)
             assert n["miss_rate"] == want[3] * 100000 // want[0]
+            # run totals: every exchange added the same frozen node-wide deltas
+            tot = out[r]["totals"][t]
+            assert tot["inst"] % want[0] == 0 and tot["inst"] // want[0] >= out[r]["syncs"] - 1, (tot, want)
 
 
 def test_eight_node_local_ranks_switch_at_the_same_epochs():
