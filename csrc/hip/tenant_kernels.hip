@@ -609,10 +609,62 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (wr == 1) __builtin_amdgcn_s_barrier();  // g1 runs one barrier behind
-    bf16x8 a[4][2], b[4][2];
     if constexpr (STAMP) {
       if (units_seen == 0) ph[1] = (u32)__builtin_amdgcn_s_memrealtime();
     }
+    if constexpr (BAL == 3) {
+      // ONE phase per K-tile (2 barriers): a wave reads all 24 fragments of
+      // K-tile t, then runs its 64 MFMAs.  Global intervals: g0 reads at 2t,
+      // MFMAs at 2t+1; g1 reads at 2t+1, MFMAs at 2t+2.  Buffer (t+1)&1 is
+      // free from interval 2t+1 (g1's reads of tile t-1 retired at 2t).
+      // Staging of t+1: g0 stages both B halves and its A0 (12 glds) at the
+      // top of its MFMA interval and retires them at its end (g0 reads them
+      // at 2t+2, g1 the B halves at 2t+3); g1 stages its A1 (4 glds) in its
+      // read interval and retires it at the end of its MFMA interval.
+      bf16x8 a8[8][2], b4[4][2];
+      for (int t = 0; t < nt; ++t) {
+        const int buf = t & 1;
+        const bool more = t + 1 < nt;
+        stamp(t, 9);
+        stamp(t, 0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) b4[j][s2] = frag(buf, 1, bh, bc + j * 16, s2);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) a8[i][s2] = frag(buf, 0, wr, i * 16, s2);
+        if (wr == 1 && more) stage_own_a(t + 1);
+        __builtin_amdgcn_s_barrier();
+        stamp(t, 1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (wr == 0 && more) {
+          // g0: B halves (both waves' rows: 4 glds per half per wave) and A0
+          for (int h = 0; h < 2; ++h) {
+            const u16* src = Bb + (size_t)h * 128 * K + (t + 1) * G2_BK;
+            lds_t* dst = lds + ((t + 1) & 1) * kG2Buf + (2 + h) * kG2Half + (wid & 3) * 4096;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) glds16(src + soffa[jj], dst + jj * 1024);
+          }
+          stage_own_a(t + 1);
+        }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b4[j][s2], a8[i][s2], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        if (more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        stamp(t, 2);
+      }
+    } else {
+    bf16x8 a[4][2], b[4][2];
     for (int t = 0; t < nt; ++t) {
       const int buf = t & 1;
       const bool more = t + 1 < nt;
@@ -724,6 +776,7 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
       __builtin_amdgcn_s_barrier();
       stamp(t, 4);
     }
+    }  // BAL != 3
     if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the groups
     if constexpr (STAMP) {
       if (units_seen == 0) ph[2] = (u32)__builtin_amdgcn_s_memrealtime();
@@ -1144,7 +1197,9 @@ int gpbs_hip_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int
     if (g_gemm_opts & 256) {  // 2 phases per K-tile (4 barriers); bit 10: streaming C stores
       // bit 12: balanced staging; bit 13: each group stages its own A half (4 glds per read interval)
       const bool nt = g_gemm_opts & 1024, bal = g_gemm_opts & 4096, own = g_gemm_opts & 8192;
-      auto k2 = (g_gemm_opts & 64)
+      const bool one = g_gemm_opts & 16384;  // bit 14: one phase per K-tile
+      auto k2 = one ? ((g_gemm_opts & 64) ? k_gemm256s2_bf16_tn<1, 0, 3> : k_gemm256s2_bf16_tn<0, 0, 3>)
+                : (g_gemm_opts & 64)
                     ? (own ? k_gemm256s2_bf16_tn<1, 0, 2>
                            : bal ? k_gemm256s2_bf16_tn<1, 0, 1>
                                  : (nt ? k_gemm256s2_bf16_tn<1, 1, 0> : k_gemm256s2_bf16_tn<1, 0, 0>))
