@@ -27,7 +27,7 @@ TILES, SLOTS, WGS = 16, 10, 64
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
     base = int(sys.argv[2]) if len(sys.argv) > 2 else 4
-    nint = 4 if base & 256 else 8  # barrier intervals per K-tile
+    nint = 2 if base & 16384 else (4 if base & 256 else 8)  # barrier intervals per K-tile
     L = K.lib()
     L.gpbs_hip_set_gemm_dbg.restype = C.c_int
     L.gpbs_hip_set_gemm_dbg.argtypes = [C.c_void_p]
