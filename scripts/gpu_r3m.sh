@@ -15,3 +15,4 @@ step() {  # step NAME SECONDS cmd...
 step gemm_variant_tests_m 300 python -u -m pytest tests/test_gpu_kernels.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider -k "gemm"
 KBENCH_GEMM_ONLY=1 step kbench_gemm_m 200 python -u scripts/kbench.py
 step stamps_1phase 120 python -u scripts/gemm_stamps.py 4096 16640
+step smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()"
