@@ -306,6 +306,37 @@ int gpbs_fault_hits(gpbs_engine_t* e, uint64_t* out, int n);
 /* --- cross-GPU gang windows (pbs_amd/parallel/gang.py) --- */
 int gpbs_gang_set(gpbs_engine_t* e, int tenant, int state, int64_t until_ns); /* 0 none 1 favour 2 exclude */
 
+/* Native gang coordinator (csrc/comm/gang_coord.cpp): the per-rank epoch loop
+ * on the shm transport as a C++ thread bound to the engine. */
+#define GPBS_GANG_MAX_TENANTS 32
+typedef struct gpbs_gang_cfg {
+  int32_t rank, ntenants, nmetric, metric_every;
+  int32_t tenants[GPBS_GANG_MAX_TENANTS];        /* gang tenants (windows) */
+  int32_t metric_tenants[GPBS_GANG_MAX_TENANTS]; /* node-metric SUM tenants */
+  int64_t epoch_ns, slack_ns, deadline_ns, start_ns, join_ns;
+  double share;          /* fraction of the 8-epoch period given to gang windows */
+  int32_t atc_pool;      /* -1: no ATC exchange */
+  int32_t wait_driven;   /* windows only while the worst rank's K10 wait is high */
+  double wait_on_frac;   /* wait EWMA >= frac * epoch turns a tenant's windows on */
+  int32_t wait_hold_epochs, reform;
+  void (*roctx_push)(const char*); /* optional marker ranges (libgpbs_hip) */
+  void (*roctx_pop)(void);
+} gpbs_gang_cfg_t;
+
+typedef struct gpbs_gang_stats {
+  int64_t epochs, sync_p50_ns, sync_p99_ns, sync_max_ns, skew_p50_ns, skew_max_ns;
+  int64_t timeouts, degraded, reforms, members, atc_global_us, metric_syncs, gang_switches, error, finished;
+} gpbs_gang_stats_t;
+
+void* gpbs_gang_coord_start(gpbs_engine_t* e, void* shm, int world, int nvals, const gpbs_gang_cfg_t* cfg);
+int gpbs_gang_coord_stop(void* c, int64_t timeout_ns);
+int gpbs_gang_coord_running(void* c);
+int gpbs_gang_coord_stats(void* c, gpbs_gang_stats_t* out);
+int gpbs_gang_coord_tenant(void* c, int i, int64_t out[3]);
+int gpbs_gang_coord_metrics(void* c, int i, int64_t last[4], int64_t totals[4]);
+int gpbs_gang_coord_history(void* c, int64_t* epochs, int32_t* states, int max);
+void gpbs_gang_coord_destroy(void* c);
+
 /* --- counters / actuation backends --- */
 int gpbs_set_counter_ops(gpbs_engine_t* e, const gpbs_counter_ops_t* ops);
 int gpbs_set_actuator_ops(gpbs_engine_t* e, const gpbs_actuator_ops_t* ops);

@@ -120,6 +120,21 @@ class LockProf(C.Structure):
 
 _lock = threading.Lock()
 _core = None
+class GangCfg(C.Structure):
+    _fields_ = [("rank", C.c_int32), ("ntenants", C.c_int32), ("nmetric", C.c_int32), ("metric_every", C.c_int32),
+                ("tenants", C.c_int32 * 32), ("metric_tenants", C.c_int32 * 32),
+                ("epoch_ns", C.c_int64), ("slack_ns", C.c_int64), ("deadline_ns", C.c_int64),
+                ("start_ns", C.c_int64), ("join_ns", C.c_int64), ("share", C.c_double), ("atc_pool", C.c_int32),
+                ("wait_driven", C.c_int32), ("wait_on_frac", C.c_double), ("wait_hold_epochs", C.c_int32),
+                ("reform", C.c_int32), ("roctx_push", C.c_void_p), ("roctx_pop", C.c_void_p)]
+
+
+class GangStats(C.Structure):
+    _fields_ = [(n, C.c_int64) for n in ("epochs", "sync_p50_ns", "sync_p99_ns", "sync_max_ns", "skew_p50_ns",
+                                         "skew_max_ns", "timeouts", "degraded", "reforms", "members",
+                                         "atc_global_us", "metric_syncs", "gang_switches", "error", "finished")]
+
+
 _hip = None
 
 
@@ -212,6 +227,14 @@ def load_core(build_if_missing=True):
         P(lib, "gpbs_gang_shm_allgather", C.c_int, C.c_void_p, u64, C.POINTER(i64), C.POINTER(i64), i64)
         P(lib, "gpbs_gang_shm_close", None, C.c_void_p)
         P(lib, "gpbs_gang_shm_reform", C.c_int, C.c_void_p, i64, i64, C.POINTER(u64), C.POINTER(u64))
+        P(lib, "gpbs_gang_coord_start", C.c_void_p, E, C.c_void_p, C.c_int, C.c_int, C.POINTER(GangCfg))
+        P(lib, "gpbs_gang_coord_stop", C.c_int, C.c_void_p, i64)
+        P(lib, "gpbs_gang_coord_running", C.c_int, C.c_void_p)
+        P(lib, "gpbs_gang_coord_stats", C.c_int, C.c_void_p, C.POINTER(GangStats))
+        P(lib, "gpbs_gang_coord_tenant", C.c_int, C.c_void_p, C.c_int, C.POINTER(i64))
+        P(lib, "gpbs_gang_coord_metrics", C.c_int, C.c_void_p, C.c_int, C.POINTER(i64), C.POINTER(i64))
+        P(lib, "gpbs_gang_coord_history", C.c_int, C.c_void_p, C.POINTER(i64), C.POINTER(C.c_int32), C.c_int)
+        P(lib, "gpbs_gang_coord_destroy", None, C.c_void_p)
         P(lib, "gpbs_slot_set_pmc", C.c_int, E, C.c_int, C.POINTER(u64))
         P(lib, "gpbs_now", i64, E)
         P(lib, "gpbs_advance", C.c_int, E, i64)

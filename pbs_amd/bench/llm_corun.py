@@ -29,7 +29,34 @@ from typing import Dict, Optional
 os.environ["GPU_MAX_HW_QUEUES"] = str(max(8, int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)))
 
 
+def _kfd_queues(pid: int) -> Optional[int]:
+    """Hardware queues KFD holds for process `pid` (sysfs; None where not exposed)."""
+    try:
+        return len(os.listdir(f"/sys/class/kfd/kfd/proc/{pid}/queues"))
+    except OSError:
+        return None
+
+
+def _timeline(rows, t0: float, bin_s: float = 0.25):
+    """Per-step rows (t, gate_ms, run_ms, key) -> per-bin summary: steps, mean
+    gate wait, mean run time, the most frequent SE set."""
+    bins: Dict[int, list] = {}
+    for (t, g, r, k) in rows:
+        bins.setdefault(int((t - t0) / bin_s), []).append((g, r, k))
+    out = []
+    for b in sorted(bins):
+        xs = bins[b]
+        keys: Dict[str, int] = {}
+        for _, _, k in xs:
+            keys[k] = keys.get(k, 0) + 1
+        out.append([round(b * bin_s, 2), len(xs), round(statistics.mean(g for g, _, _ in xs), 3),
+                    round(statistics.mean(r for _, r, _ in xs), 3), max(keys, key=keys.get)])
+    return out
+
+
 def _tenant(kind: str, seconds: float, warmup: float, socket: Optional[str], q, start_evt, args: dict):
+    if args.get("tenant_hwq"):  # before anything initialises HIP in this process
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args["tenant_hwq"])
     import torch
 
     from ..models.llama import PRESETS, LlamaDecoder, LlamaTrainer
@@ -39,6 +66,8 @@ def _tenant(kind: str, seconds: float, warmup: float, socket: Optional[str], q, 
         from ..runtime.tenant import TenantClient
         t = TenantClient(kind, socket, slots=args.get("slots", 8), weight=args.get(f"{kind}_weight", 256),
                          spatial=args.get("spatial", False), priority=args.get(f"{kind}_prio", 0))
+        if args.get("prestream") and t.se_mode:
+            t.prepare_streams()
     if kind == "infer":
         w = LlamaDecoder(PRESETS[args["infer_model"]], batch=args["infer_batch"], context=args["context"],
                          fp8=args.get("fp8", False), graph=args.get("graph", False))
@@ -71,17 +100,25 @@ def _tenant(kind: str, seconds: float, warmup: float, socket: Optional[str], q, 
     torch.cuda.synchronize()
     start_evt.wait()
     lat = []
+    rows = []
     halves: Dict[str, int] = {}
-    t_warm = time.monotonic() + warmup
+    t_start = time.monotonic()
+    t_warm = t_start + warmup
     t_end = t_warm + seconds
     n = 0
+    queues_mid = None
     while True:
         now = time.monotonic()
         if now >= t_end:
             break
+        if queues_mid is None and now >= t_warm + seconds / 2:
+            queues_mid = _kfd_queues(os.getpid())
         t0 = time.perf_counter()
+        key = ""
+        g_ms = 0.0
         if t is not None:
             with t.slice(timeout_s=30.0):
+                g_ms = 1e3 * (time.perf_counter() - t0)
                 key = ",".join(str(h) for h in sorted({c for (_, c) in t.owned()}))
                 halves[key] = halves.get(key, 0) + 1
                 unit()
@@ -95,15 +132,21 @@ def _tenant(kind: str, seconds: float, warmup: float, socket: Optional[str], q, 
             unit()
             torch.cuda.synchronize()
         dt = time.perf_counter() - t0
+        rows.append((now, g_ms, 1e3 * dt - g_ms, key))
         if now >= t_warm:
             lat.append(dt)
             n += 1
     if t is not None:
         t.close(destroy=False)  # keep it registered for the daemon's dump
     span = sum(lat)
+    timed = [r for r in rows if r[0] >= t_warm]
     q.put({"kind": kind, "units": n, "tokens_per_s": n * per_unit_tokens / span if span else 0.0,
            "p50_ms": 1e3 * statistics.median(lat) if lat else 0.0,
-           "p99_ms": 1e3 * sorted(lat)[int(0.99 * (len(lat) - 1))] if lat else 0.0, "halves": halves})
+           "p99_ms": 1e3 * sorted(lat)[int(0.99 * (len(lat) - 1))] if lat else 0.0, "halves": halves,
+           "gate_p50_ms": round(statistics.median(r[1] for r in timed), 3) if timed else 0.0,
+           "run_p50_ms": round(statistics.median(r[2] for r in timed), 3) if timed else 0.0,
+           "kfd_queues": queues_mid, "hwq": os.environ.get("GPU_MAX_HW_QUEUES"),
+           "timeline": _timeline(rows, t_start)})
 
 
 def parse_se_policy(policy: str):
@@ -141,9 +184,18 @@ def run(policy: str, kinds, args: dict, seconds: float, warmup: float) -> Dict[s
     base = policy.split("@")[0]
     if base.startswith("se:"):  # static SE split; "se:I/T@solo" runs the given kinds alone on their masks
         args["infer_ses"], args["train_ses"] = parse_se_policy(base)
-    if policy.endswith("+prio"):
-        args["infer_prio"] = 1
-        policy = policy[:-5]
+    # variant suffixes: +prio (high-priority decode queue), +hwqN (tenant
+    # GPU_MAX_HW_QUEUES=N), +pre (both SE-half streams created at registration)
+    policy, *mods = policy.split("+")
+    for m in mods:
+        if m == "prio":
+            args["infer_prio"] = 1
+        elif m.startswith("hwq"):
+            args["tenant_hwq"] = int(m[3:])
+        elif m == "pre":
+            args["prestream"] = True
+        else:
+            raise ValueError(f"unknown policy variant +{m}")
     if policy in ("gpbs", "gpbs-spatial"):
         from ..runtime.daemon import Daemon
         sock = os.path.join(tempfile.mkdtemp(), "gpbsd.sock")
@@ -180,7 +232,7 @@ def run(policy: str, kinds, args: dict, seconds: float, warmup: float) -> Dict[s
                 # every tenant still registered: the first to finish is reaped
                 # soon after its process exits
                 e = daemon.engine
-                hw_early = {}
+                hw_early = {"_daemon_kfd_queues": _kfd_queues(os.getpid())}
                 for t in e.tenants():
                     att, _ = daemon.gpu_ctx.hwc_tenant(t)
                     hw_early[e.tenant_info(t).name] = {
@@ -226,11 +278,16 @@ def main(argv=None):
     ap.add_argument("--fp8", action="store_true", help="decode tenant streams e4m3fn weights (fp8 MFMA linears)")
     ap.add_argument("--graph", action="store_true", help="with --fp8: decode step replayed from a HIP graph")
     ap.add_argument("--reps", type=int, default=1, help="repetitions of every co-run policy (median reported)")
+    ap.add_argument("--tenant-hwq", type=int, default=0,
+                    help="GPU_MAX_HW_QUEUES of the tenant processes (default: inherit, >= 8)")
+    ap.add_argument("--prestream", action="store_true",
+                    help="shim tenants create both SE-half masked streams at registration")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     args = {"infer_model": a.infer_model, "train_model": a.train_model, "infer_batch": a.infer_batch,
             "prompt": a.prompt, "context": a.context, "train_batch": a.train_batch, "train_seq": a.train_seq,
-            "infer_weight": 512, "train_weight": 256, "fp8": a.fp8, "graph": a.graph and a.fp8}
+            "infer_weight": 512, "train_weight": 256, "fp8": a.fp8, "graph": a.graph and a.fp8,
+            "tenant_hwq": a.tenant_hwq, "prestream": a.prestream}
     res = {}
     pols = [p for p in a.policies.split(",") if p]
     if "gpbs-se" in pols or "gpbs-budget" in pols:
@@ -254,7 +311,8 @@ def main(argv=None):
             else:
                 r = run(p, ["infer", "train"], args, a.seconds, a.warmup)
             reps[p].append(r)
-            print(f"[llm] {p} rep {rep}: {json.dumps({k: v for k, v in r.items() if not k.startswith('_')})}",
+            brief = {k: {kk: vv for kk, vv in v.items() if kk != "timeline"} for k, v in r.items() if not k.startswith('_')}
+            print(f"[llm] {p} rep {rep}: {json.dumps(brief)}",
                   file=sys.stderr, flush=True)
             if a.out:  # every finished run survives a time limit
                 with open(a.out + ".partial", "w") as f:

@@ -173,7 +173,8 @@ def hang_worker(rank: int, world: int, port: int, q, transport: str, shm_name: s
     os._exit(0)  # a gloo collective abandoned at the deadline must not block exit
 
 
-def node_worker(rank: int, world: int, name: str, q, seconds: float = 1.0, epoch_ms: float = 5.0, ready=None):
+def node_worker(rank: int, world: int, name: str, q, seconds: float = 1.0, epoch_ms: float = 5.0, ready=None,
+                native: bool = True):
     """One of `world` node-local scheduler ranks on the native shm gang
     transport (the 8-GPU node layout, rehearsed on CPU): every rank runs its
     own engine with a hog and a gang tenant; returns the decision history and
@@ -191,7 +192,7 @@ def node_worker(rank: int, world: int, name: str, q, seconds: float = 1.0, epoch
     if ready is not None:  # every rank imported and built its engine (spawn start-up skew is seconds on a busy host)
         ready.wait(120)
     g = GangCoordinator(e, None, [coll], epoch_ms=epoch_ms, share=0.5, transport="shm", shm_name=name,
-                        rank=rank, world=world, deadline_ms=5000.0).start()
+                        rank=rank, world=world, deadline_ms=5000.0, native=native).start()
     time.sleep(seconds)
     g.stop()
     recs = [r.a[1] for r in e.trace(max_records=1 << 16, from_start=True)

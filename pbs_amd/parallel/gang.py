@@ -252,8 +252,18 @@ class GangCoordinator:
                  transport: str = "dist", shm_name: Optional[str] = None, rank: Optional[int] = None,
                  world: Optional[int] = None, deadline_ms: float = 200.0, wait_driven: bool = False,
                  wait_on_frac: float = 0.02, wait_hold_epochs: int = 64, reform: bool = False,
-                 join_ms: Optional[float] = None, start_grace_ms: float = 2000.0):
+                 join_ms: Optional[float] = None, start_grace_ms: float = 2000.0,
+                 native: Optional[bool] = None):
         self.engine = engine
+        # the epoch loop as a C++ thread (csrc/comm/gang_coord.cpp) on the shm
+        # transport with the engine's own demand; the Python loop stays for the
+        # dist/xgmi transports and custom demand callables
+        can_native = transport == "shm" and demand is None and engine is not None and hasattr(engine, "h")
+        self.native = can_native if native is None else bool(native)
+        if self.native and not can_native:
+            raise ValueError("native gang coordinator needs transport='shm', an Engine and the engine demand")
+        self._nc = None   # native coordinator handle
+        self._ntr = None  # its shm transport (owned here)
         self.group = group
         self.tenants = list(tenants)
         self.epoch_ns = int(epoch_ms * 1e6)
@@ -263,7 +273,7 @@ class GangCoordinator:
         self.slack_ns = int(slack_ms * 1e6)
         self.epoch = 0
         self.state: Dict[int, int] = {t: NONE for t in self.tenants}
-        self.history: List[tuple] = []  # (epoch, {tenant: state}) -- bounded
+        self._history: List[tuple] = []  # (epoch, {tenant: state}) -- bounded
         self.lat_ns: List[int] = []
         self.skew_ns: List[int] = []
         self._want_stop = False
@@ -273,10 +283,10 @@ class GangCoordinator:
         self.atc_global_us = 0
         self.metric_tenants = list(metric_tenants or [])
         self.metric_every = max(1, int(metric_every))
-        self.node_metrics: Dict[int, Dict[str, int]] = {}
+        self._node_metrics: Dict[int, Dict[str, int]] = {}
         # node-wide totals over every metric exchange of the run (the last
         # period alone reads zero once the tenants have drained)
-        self.node_totals: Dict[int, Dict[str, int]] = {}
+        self._node_totals: Dict[int, Dict[str, int]] = {}
         self.metric_syncs = 0
         self.transport = transport
         self.shm_name = shm_name
@@ -445,9 +455,9 @@ class GangCoordinator:
                 for t, st in dec.items():
                     self.engine.gang_set(t, st, until)
                 self.state = dec
-                self.history.append((self.epoch, dict(dec)))
-                if len(self.history) > 8192:
-                    del self.history[:4096]
+                self._history.append((self.epoch, dict(dec)))
+                if len(self._history) > 8192:
+                    del self._history[:4096]
                 self.epoch += 1
                 rest = self.epoch_ns - (time.monotonic_ns() - t1)
                 if rest > 0:
@@ -504,16 +514,120 @@ class GangCoordinator:
             inst, cyc, ref, miss = red[4 * i:4 * i + 4]
             out[t] = {"inst": inst, "cycles": cyc, "l2_refs": ref, "l2_misses": miss,
                       "miss_rate": miss * 100000 // inst if inst else 0}
-        self.node_metrics = out
+        self._node_metrics = out
         for t, m in out.items():
-            tot = self.node_totals.setdefault(t, {"inst": 0, "cycles": 0, "l2_refs": 0, "l2_misses": 0})
+            tot = self._node_totals.setdefault(t, {"inst": 0, "cycles": 0, "l2_refs": 0, "l2_misses": 0})
             for k in tot:
                 tot[k] += m[k]
             tot["miss_rate"] = tot["l2_misses"] * 100000 // tot["inst"] if tot["inst"] else 0
         self.metric_syncs += 1
         return True
 
+    # ------------------------------------------------------ native loop
+    def _start_native(self):
+        from .. import _native as N
+        nt, nm = len(self.tenants), len(self.metric_tenants)
+        if nt > 32 or nm > 32:
+            raise ValueError("native gang coordinator: at most 32 gang / metric tenants")
+        nvals = max(2 * nt + 4, 4 * nm)
+        self._ntr = _ShmTransport(self.shm_name, self.rank, self.world, nvals)
+        cfg = N.GangCfg()
+        cfg.rank, cfg.ntenants, cfg.nmetric, cfg.metric_every = self.rank, nt, nm, self.metric_every
+        for i, t in enumerate(self.tenants):
+            cfg.tenants[i] = t
+        for i, t in enumerate(self.metric_tenants):
+            cfg.metric_tenants[i] = t
+        cfg.epoch_ns, cfg.slack_ns, cfg.deadline_ns = self.epoch_ns, self.slack_ns, self.deadline_ns
+        cfg.start_ns, cfg.join_ns = self.start_ns, int(self.join_ms * 1e6)
+        cfg.share = self.share
+        cfg.atc_pool = -1 if self.atc_pool is None else int(self.atc_pool)
+        cfg.wait_driven, cfg.wait_on_frac, cfg.wait_hold_epochs = int(self.wait_driven), self.wait_on_frac, self.wait_hold
+        cfg.reform = int(self.reform)
+        hip = N._hip
+        if hip is not None:  # marker ranges on rocprofv3 timelines, as the Python loop's roctx.range
+            cfg.roctx_push = C.cast(hip.gpbs_roctx_push, C.c_void_p).value
+            cfg.roctx_pop = C.cast(hip.gpbs_roctx_pop, C.c_void_p).value
+        self._cfg = cfg  # the thread copies it; keep the function pointers' owner alive anyway
+        lib = self.engine.lib
+        h = lib.gpbs_gang_coord_start(self.engine.h, C.c_void_p(self._ntr.h), self.world, nvals, C.byref(cfg))
+        if not h:
+            self._ntr.close()
+            raise RuntimeError("gpbs_gang_coord_start failed")
+        self._nc = C.c_void_p(h)
+
+    def _pull(self):
+        """Refresh the Python view of the native loop's state."""
+        if self._nc is None:
+            return
+        from .. import _native as N
+        lib = self.engine.lib
+        st = N.GangStats()
+        lib.gpbs_gang_coord_stats(self._nc, C.byref(st))
+        self._nstats = st
+        self._epoch, self.timeouts, self._degraded = st.epochs, st.timeouts, bool(st.degraded)
+        self.reforms, self.metric_syncs, self.gang_switches = st.reforms, st.metric_syncs, st.gang_switches
+        self.atc_global_us = st.atc_global_us
+        self.members = [r for r in range(self.world) if (st.members >> r) & 1]
+        o = (C.c_int64 * 3)()
+        for i, t in enumerate(self.tenants):
+            lib.gpbs_gang_coord_tenant(self._nc, i, o)
+            self.state[t], self.gang_on[t], self.wait_ewma_us[t] = int(o[0]), bool(o[1]), int(o[2])
+        last, tot = (C.c_int64 * 4)(), (C.c_int64 * 4)()
+        nm, nt_ = {}, {}
+        for i, t in enumerate(self.metric_tenants):
+            lib.gpbs_gang_coord_metrics(self._nc, i, last, tot)
+            for dst, src in ((nm, last), (nt_, tot)):
+                inst, cyc, ref, miss = (int(x) for x in src)
+                dst[t] = {"inst": inst, "cycles": cyc, "l2_refs": ref, "l2_misses": miss,
+                          "miss_rate": miss * 100000 // inst if inst else 0}
+        if st.metric_syncs:
+            self._node_metrics, self._node_totals = nm, nt_
+        nt = len(self.tenants)
+        cap = 8192
+        eps = (C.c_int64 * cap)()
+        sts = (C.c_int32 * max(1, cap * nt))()
+        n = lib.gpbs_gang_coord_history(self._nc, eps, sts, cap)
+        self._history = [(int(eps[j]), {t: int(sts[j * nt + i]) for i, t in enumerate(self.tenants)})
+                         for j in range(max(0, n))]
+
+    # live views of the native loop's state (plain attributes for the Python loop)
+    @property
+    def degraded(self) -> bool:
+        self._pull()
+        return self._degraded
+
+    @degraded.setter
+    def degraded(self, v: bool):
+        self._degraded = v
+
+    @property
+    def epoch(self) -> int:
+        self._pull()
+        return self._epoch
+
+    @epoch.setter
+    def epoch(self, v: int):
+        self._epoch = v
+
+    @property
+    def history(self) -> List[tuple]:
+        self._pull()
+        return self._history
+
+    @property
+    def node_metrics(self) -> Dict[int, Dict[str, int]]:
+        self._pull()
+        return self._node_metrics
+
+    @property
+    def node_totals(self) -> Dict[int, Dict[str, int]]:
+        self._pull()
+        return self._node_totals
+
     def start(self):
+        if self.native:
+            self._start_native()
+            return self
         self._th = threading.Thread(target=self._loop, daemon=True, name="gpbs-gang")
         self._th.start()
         return self
@@ -522,12 +636,37 @@ class GangCoordinator:
         """Collective: returns once every rank has left the epoch loop (a
         degraded rank has already left it)."""
         self._want_stop = True
+        if self._nc is not None:
+            rc = self.engine.lib.gpbs_gang_coord_stop(self._nc, int(timeout * 1e9))
+            self._pull()
+            if rc == 0:
+                err = self._nstats.error
+                self.engine.lib.gpbs_gang_coord_destroy(self._nc)
+                self._nc = None
+                if not self.degraded:
+                    self._ntr.close()
+                if err:
+                    raise RuntimeError(f"gang shm exchange failed ({err})")
+            return
         if self._th is not None:
             self._th.join(timeout)
         if self.error:
             raise self.error
 
     def stats(self) -> Dict[str, float]:
+        if self.native:
+            self._pull()
+            st = getattr(self, "_nstats", None)
+            if st is not None:
+                return {"epochs": self.epoch, "transport": self.transport, "native": True,
+                        "sync_p50_us": st.sync_p50_ns / 1e3, "sync_p99_us": st.sync_p99_ns / 1e3,
+                        "sync_max_us": st.sync_max_ns / 1e3, "skew_p50_us": st.skew_p50_ns / 1e3,
+                        "skew_max_us": st.skew_max_ns / 1e3, "timeouts": self.timeouts,
+                        "degraded": self.degraded, "reforms": self.reforms, "members": list(self.members),
+                        "atc_global_us": self.atc_global_us, "metric_syncs": self.metric_syncs,
+                        "wait_driven": self.wait_driven, "gang_on": {str(t): v for t, v in self.gang_on.items()},
+                        "wait_ewma_us": {str(t): v for t, v in self.wait_ewma_us.items()},
+                        "gang_switches": self.gang_switches}
         lat = sorted(self.lat_ns) or [0]
         skew = sorted(self.skew_ns) or [0]
         return {"epochs": self.epoch, "transport": self.transport, "sync_p50_us": lat[len(lat) // 2] / 1e3,

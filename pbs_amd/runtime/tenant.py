@@ -131,6 +131,18 @@ class TenantClient:
         return rc == 1
 
     # ------------------------------------------------------------- streams
+    def prepare_streams(self):
+        """SE mode: create both class-half masked streams now, in a fixed
+        order, before the tenant's own work creates queues (the queue set
+        then no longer depends on which layout the first slices saw)."""
+        import torch
+
+        from ..ops import kernels as K
+        for ses in ((0, 1), (2, 3)):
+            if ("se",) + ses not in self._streams:
+                self._streams[("se",) + ses] = torch.cuda.ExternalStream(
+                    K.cumask_stream(se_cu_words(ses), device=self.gpu))
+
     def stream(self, owned: Optional[List[Tuple[int, int]]] = None):
         """torch stream masked to the CU halves this tenant holds.  The mask is
         quantised to {half 0, half 1, both} across all XCDs: a CU mask is a

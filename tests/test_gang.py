@@ -127,18 +127,21 @@ def test_node_metrics_are_exactly_the_sum_of_per_rank_counters(transport):
             assert tot["inst"] % want[0] == 0 and tot["inst"] // want[0] >= out[r]["syncs"] - 1, (tot, want)
 
 
-def test_eight_node_local_ranks_switch_at_the_same_epochs():
+@pytest.mark.parametrize("native", [True, False], ids=["native-loop", "python-loop"])
+def test_eight_node_local_ranks_switch_at_the_same_epochs(native):
     """SURVEY §4.2 item 5 on CPU: 8 scheduler ranks of one node on the native
     shm gang transport agree on every epoch's decision, and the GANG_EPOCH
-    records of the 8 trace rings carry the same state sequence."""
+    records of the 8 trace rings carry the same state sequence -- with the
+    epoch loop as a C++ thread (csrc/comm/gang_coord.cpp, the default) and as
+    the Python thread."""
     import os
     from pbs_amd.parallel._gang_selftest import node_worker
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     world = 8
-    name = f"gpbs-gang-node8-{os.getpid()}"
+    name = f"gpbs-gang-node8-{os.getpid()}-{int(native)}"
     ready = ctx.Barrier(world)
-    ps = [ctx.Process(target=node_worker, args=(r, world, name, q, 1.0, 5.0, ready)) for r in range(world)]
+    ps = [ctx.Process(target=node_worker, args=(r, world, name, q, 1.0, 5.0, ready, native)) for r in range(world)]
     for p in ps:
         p.start()
     out = {}
@@ -163,3 +166,38 @@ def test_eight_node_local_ranks_switch_at_the_same_epochs():
     for r in range(world):
         st = out[r]["stats"]
         assert st["timeouts"] == 0 and st["transport"] == "shm", st
+        assert st.get("native", False) == native, st
+
+
+def test_native_loop_decides_as_the_python_decision_function():
+    """World 1 on the shm transport: every epoch's window of the C++ loop is
+    GangCoordinator.decide() of that epoch (period 8, share 0.5 -> 4 gang
+    epochs, round-robin), and the loop leaves on stop."""
+    import os
+    import time
+
+    from pbs_amd.core.engine import Engine
+    e = Engine(partitions=[(0, x) for x in range(2)], quantum_align_us=0)
+    e.tenant_create("Domain-0", nslots=1)
+    a = e.tenant_create("a", nslots=2)
+    b = e.tenant_create("b", nslots=2)
+    e.start()
+    e.wake(a)
+    e.wake(b)
+    try:
+        g = GangCoordinator(e, None, [a, b], epoch_ms=1.0, share=0.5, transport="shm",
+                            shm_name=f"gpbs-gang-w1-{os.getpid()}", rank=0, world=1, metric_tenants=[a, b],
+                            metric_every=2).start()
+        assert g.native
+        time.sleep(0.2)
+        g.stop()
+        hist = g.history
+        assert len(hist) >= 50
+        ref = GangCoordinator(engine=None, group=None, tenants=[a, b], share=0.5)
+        for ep, st in hist:
+            assert st == ref.decide(ep, [1, 1]), (ep, st)
+        st = g.stats()
+        assert st["native"] and st["timeouts"] == 0 and st["metric_syncs"] >= len(hist) // 2
+        assert set(g.node_totals) == {a, b}
+    finally:
+        e.stop()

@@ -101,6 +101,25 @@ gt = [threading.Thread(target=grank, args=(k,)) for k in range(3)]
 assert res[0] == (60, 1) and res[1] == (60, 1), res
 for h in gh[::-1]:
     lib.gpbs_gang_shm_close(h)
+# native gang coordinator threads (csrc/comm/gang_coord.cpp): three ranks'
+# engines in one process, their C++ epoch loops racing stats/history readers
+from pbs_amd.parallel.gang import GangCoordinator
+engs, gcs = [], []
+for k in range(3):
+    ek = Engine(partitions=[(k, x) for x in range(2)], quantum_align_us=0)
+    ek.tenant_create("Domain-0", nslots=1)
+    tk = ek.tenant_create("coll", nslots=2)
+    ek.start(); ek.wake(tk)
+    engs.append(ek)
+    gcs.append(GangCoordinator(ek, None, [tk], epoch_ms=1.0, share=0.5, transport="shm",
+                               shm_name="san-gc-%d" % os.getpid(), rank=k, world=3, metric_tenants=[tk],
+                               metric_every=1, deadline_ms=2000.0, native=True).start())
+for _ in range(40):
+    [(g.stats(), g.history, g.node_metrics) for g in gcs]
+    time.sleep(0.005)
+[g.stop() for g in gcs]
+assert all(g.stats()["epochs"] >= 10 and g.stats()["timeouts"] == 0 for g in gcs), [g.stats() for g in gcs]
+[(ek.stop(), ek.close()) for ek in engs]
 r.stop(); r.close()
 print("OK")
 """
