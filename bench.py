@@ -246,7 +246,8 @@ def main():
         "vs_baseline": None,
         "dtype": "bf16",
         "data": "synthetic (random-init bf16 tensors; 4096^3 GEMM, 1 GiB stream, 256 MiB reduce/all-reduce, "
-                "8192^2 GEMV; the N=1 'all-reduce' tenant is a local reduce-copy kernel, RCCL all-reduce at N>1)",
+                "8192^2 GEMV; the N=1 'all-reduce' tenant is a local reduce-copy kernel; at N>1 it is the gated "
+                "all-reduce kernel over IPC-mapped peer buffers on xGMI, RCCL only as fallback or --coll rccl)",
         "config": {"model": names[head], "global_batch": world * 4, "seq_len": 0,
                    "parallelism": f"dp{world}" if world > 1 else "dp1",
                    "tenants_per_gpu": len(MIXES[head]["tenants"]),

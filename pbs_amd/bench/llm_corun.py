@@ -282,8 +282,12 @@ def main(argv=None):
                     help="GPU_MAX_HW_QUEUES of the tenant processes (default: inherit, >= 8)")
     ap.add_argument("--prestream", action="store_true",
                     help="shim tenants create both SE-half masked streams at registration")
+    ap.add_argument("--daemon-hwq", type=int, default=0,
+                    help="GPU_MAX_HW_QUEUES of this (daemon) process (default: >= 8)")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
+    if a.daemon_hwq:  # before anything initialises HIP in this process
+        os.environ["GPU_MAX_HW_QUEUES"] = str(a.daemon_hwq)
     args = {"infer_model": a.infer_model, "train_model": a.train_model, "infer_batch": a.infer_batch,
             "prompt": a.prompt, "context": a.context, "train_batch": a.train_batch, "train_seq": a.train_seq,
             "infer_weight": 512, "train_weight": 256, "fp8": a.fp8, "graph": a.graph and a.fp8,
