@@ -93,9 +93,15 @@ def _tenant(kind: str, seconds: float, warmup: float, socket: Optional[str], q, 
     if t is None and args.get(f"{kind}_prio", 0):
         prio_stream = torch.cuda.Stream(priority=-abs(args[f"{kind}_prio"]))
     ses = args.get(f"{kind}_ses")
+    swap_stream = None
     if t is None and ses is not None:  # static shader-engine split (se:I/T policies)
         from ..ops import kernels as K
         from ..runtime.tenant import se_cu_words
+        if args.get("swap_s"):
+            # +swapN: the first N seconds on the OTHER half (the swapped layout
+            # the daemon's probe phase sometimes starts from), then this half
+            other = tuple(sorted({0, 1, 2, 3} - set(ses)))
+            swap_stream = torch.cuda.ExternalStream(K.cumask_stream(se_cu_words(other)))
         prio_stream = torch.cuda.ExternalStream(K.cumask_stream(se_cu_words(ses)))
     torch.cuda.synchronize()
     start_evt.wait()
@@ -125,9 +131,11 @@ def _tenant(kind: str, seconds: float, warmup: float, socket: Optional[str], q, 
                 torch.cuda.current_stream().synchronize()
             t.account(flops=flops, bytes_moved=bytes_, busy_ns=int((time.perf_counter() - t0) * 1e9))
         elif prio_stream is not None:
-            with torch.cuda.stream(prio_stream):
+            st = swap_stream if swap_stream is not None and now < t_start + args["swap_s"] else prio_stream
+            key = "swap" if st is swap_stream else ""
+            with torch.cuda.stream(st):
                 unit()
-            prio_stream.synchronize()
+            st.synchronize()
         else:
             unit()
             torch.cuda.synchronize()
@@ -180,13 +188,15 @@ def run(policy: str, kinds, args: dict, seconds: float, warmup: float) -> Dict[s
     daemon = None
     sock = None
     args = dict(args, spatial=policy == "gpbs-spatial")
+    # variant suffixes: +prio (high-priority decode queue), +hwqN (tenant
+    # GPU_MAX_HW_QUEUES=N), +pre (both SE-half streams created at registration),
+    # +nohwc (daemon on modeled counters), +swapN (static split: the first N s
+    # on the swapped halves)
+    policy, *mods = policy.split("+")
     policy = ALIASES.get(policy, policy)
     base = policy.split("@")[0]
     if base.startswith("se:"):  # static SE split; "se:I/T@solo" runs the given kinds alone on their masks
         args["infer_ses"], args["train_ses"] = parse_se_policy(base)
-    # variant suffixes: +prio (high-priority decode queue), +hwqN (tenant
-    # GPU_MAX_HW_QUEUES=N), +pre (both SE-half streams created at registration)
-    policy, *mods = policy.split("+")
     for m in mods:
         if m == "prio":
             args["infer_prio"] = 1
@@ -194,6 +204,10 @@ def run(policy: str, kinds, args: dict, seconds: float, warmup: float) -> Dict[s
             args["tenant_hwq"] = int(m[3:])
         elif m == "pre":
             args["prestream"] = True
+        elif m == "nohwc":
+            args["nohwc"] = True
+        elif m.startswith("swap"):
+            args["swap_s"] = float(m[4:])
         else:
             raise ValueError(f"unknown policy variant +{m}")
     if policy in ("gpbs", "gpbs-spatial"):
@@ -214,7 +228,7 @@ def run(policy: str, kinds, args: dict, seconds: float, warmup: float) -> Dict[s
             # SEs {0,1} / memory SEs {2,3}), surplus slots offline
             over.update(class_budget=1, present_us=10000)
         daemon = Daemon(sock, gpus=[0], nctx=4, sim=False, profile="mi355x", attach_gpu=True, se_mode=True,
-                        hw_counters=_HWC["on"], overrides=over).start()
+                        hw_counters=_HWC["on"] and not args.get("nohwc"), overrides=over).start()
         args["slots"] = 16
         args["spatial"] = True
     ps = [ctx.Process(target=_tenant, args=(k, seconds, warmup, sock, q, start, args)) for k in kinds]
