@@ -65,7 +65,8 @@ def _tenant(kind: str, seconds: float, warmup: float, socket: Optional[str], q, 
     if socket:
         from ..runtime.tenant import TenantClient
         t = TenantClient(kind, socket, slots=args.get("slots", 8), weight=args.get(f"{kind}_weight", 256),
-                         spatial=args.get("spatial", False), priority=args.get(f"{kind}_prio", 0))
+                         spatial=args.get("spatial", False), priority=args.get(f"{kind}_prio", 0),
+                         one_queue=not args.get("multiq"))
         if args.get("prestream") and t.se_mode:
             t.prepare_streams()
     if kind == "infer":
@@ -123,9 +124,11 @@ def _tenant(kind: str, seconds: float, warmup: float, socket: Optional[str], q, 
         key = ""
         g_ms = 0.0
         if t is not None:
-            with t.slice(timeout_s=30.0):
+            with t.slice(timeout_s=30.0) as s_used:
                 g_ms = 1e3 * (time.perf_counter() - t0)
-                key = ",".join(str(h) for h in sorted({c for (_, c) in t.owned()}))
+                used = next((k for k, v in t._streams.items() if v is s_used), None)
+                key = ",".join(str(h) for h in sorted({c for (_, c) in t.owned()})) + (
+                    "|m" + "".join(str(x) for x in used[1:]) if used else "|u")
                 halves[key] = halves.get(key, 0) + 1
                 unit()
                 torch.cuda.current_stream().synchronize()
@@ -204,6 +207,8 @@ def run(policy: str, kinds, args: dict, seconds: float, warmup: float) -> Dict[s
             args["tenant_hwq"] = int(m[3:])
         elif m == "pre":
             args["prestream"] = True
+        elif m == "multiq":  # shim tenants may use both SE-half masked queues (pre-fix behaviour)
+            args["multiq"] = True
         elif m == "nohwc":
             args["nohwc"] = True
         elif m.startswith("swap"):

@@ -73,7 +73,7 @@ def se_cu_words(ses) -> List[int]:
 class TenantClient:
     def __init__(self, name: str, socket_path: str = DEFAULT_SOCKET, slots: int = 8, weight: int = -1,
                  cap: int = -1, pool=None, gpu: int = 0, heartbeat_s: float = 0.05, spatial: bool = True,
-                 priority: int = 0):
+                 priority: int = 0, one_queue: bool = True):
         self.name = name
         self.gpu = gpu
         self.spatial = spatial
@@ -95,6 +95,8 @@ class TenantClient:
             raise RuntimeError(f"cannot open control region {r['ctl']!r}")
         self.ctl = C.c_void_p(h)
         self._streams: Dict[Tuple, object] = {}
+        self.one_queue = one_queue  # SE mode: one masked queue, on the class home half (see stream())
+        self._home: Optional[Tuple[int, int]] = None
         self._progress = 0
         self._stop = threading.Event()
         self._hb = threading.Thread(target=self._beat, args=(heartbeat_s,), daemon=True, name=f"gpbs-hb-{name}")
@@ -161,11 +163,18 @@ class TenantClient:
             # Quantised to the class halves SEs {0,1} / {2,3}, as the native
             # runners do: every distinct CU mask is a hardware queue this
             # process keeps, and config #5 runs that saw five or six distinct
-            # SE sets per tenant (probe and transition layouts) collapsed to
-            # 0.17 of the decode tenant's solo rate while the layout itself was
-            # right (profiles/llm5/config5_r3b_5rep.json) -- the hardware
-            # scheduler time-slicing an over-subscribed queue set.  A set that
-            # spans both halves runs unmasked (transitions only).
+            # SE sets per tenant collapsed (profiles/llm5/config5_r3b_5rep.json).
+            # A set that spans both halves runs unmasked (transitions only).
+            #
+            # One masked queue per tenant, on its class's home half only
+            # (compute {0,1}, memory {2,3}: the budget layout's homes): two
+            # processes that each moved their kernels from one CU-masked
+            # queue to the other collapsed together -- decode 17 vs 5.7 ms per
+            # step, the trainer 240 vs 188 ms -- and stayed collapsed on
+            # disjoint masks, with no daemon at all (a static split that
+            # starts on the swapped halves: profiles/llm5/config5_r3g_swap_nohwc.json).
+            # A transitional layout (the tenant on the other class's half) and
+            # a later class flip run unmasked instead.
             ses = {c for (_, c) in parts}
             if ses <= {0, 1}:
                 ses = (0, 1)
@@ -173,6 +182,12 @@ class TenantClient:
                 ses = (2, 3)
             else:
                 return torch.cuda.current_stream()
+            if self.one_queue:
+                cls = self.vpmu()["class"]
+                home = (0, 1) if cls == 0 else (2, 3) if cls == 1 else None
+                if home != ses or (self._home is not None and self._home != ses):
+                    return torch.cuda.current_stream()
+                self._home = ses
             s = self._streams.get(("se",) + ses)
             if s is None:
                 s = torch.cuda.ExternalStream(K.cumask_stream(se_cu_words(ses), device=self.gpu))

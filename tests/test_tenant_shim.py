@@ -81,3 +81,35 @@ def test_reaper_destroys_tenant_whose_process_died():
         assert not d.pages  # page released
     finally:
         d.stop()
+
+
+def test_se_mode_stream_uses_one_masked_queue_on_the_class_home_half(monkeypatch):
+    """SE mode: a shim tenant launches on ONE CU-masked queue for its life --
+    the home half of its class (compute {0,1}, memory {2,3}); a transitional
+    layout on the other class's half, an unclassified tenant and a later
+    class flip run on the unmasked stream (two processes that each moved
+    their kernels between two masked queues collapsed together:
+    profiles/llm5/config5_r3g_swap_nohwc.json)."""
+    import torch
+
+    from pbs_amd.ops import kernels as K
+    from pbs_amd.runtime.tenant import TenantClient, se_cu_words
+    made = []
+    monkeypatch.setattr(K, "cumask_stream", lambda words, device=0: made.append(tuple(words)) or len(made))
+    monkeypatch.setattr(torch.cuda, "ExternalStream", lambda h: ("masked", h))
+    monkeypatch.setattr(torch.cuda, "current_stream", lambda: "unmasked")
+    t = object.__new__(TenantClient)
+    t.se_mode, t.spatial, t.gpu, t.one_queue, t._home, t._streams = True, True, 0, True, None, {}
+    cls = {"v": -1}
+    t.vpmu = lambda: {"class": cls["v"]}
+    lo = [(x, c) for x in range(8) for c in (0, 1)]
+    hi = [(x, c) for x in range(8) for c in (2, 3)]
+    assert t.stream(lo) == "unmasked"          # not classified yet
+    cls["v"] = 1                                # memory class: home {2,3}
+    assert t.stream(lo) == "unmasked"          # transitional layout on the compute half
+    assert t.stream(hi) == ("masked", 1) and made == [tuple(se_cu_words((2, 3)))]
+    assert t.stream(lo + hi) == "unmasked"     # a set across both halves
+    cls["v"] = 0                                # class flip: its home would be {0,1}
+    assert t.stream(lo) == "unmasked" and len(made) == 1   # never a second masked queue
+    t.one_queue, t._home = False, None          # pre-fix behaviour: any owned half gets its queue
+    assert t.stream(lo) == ("masked", 2) and len(made) == 2
