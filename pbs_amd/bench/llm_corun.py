@@ -66,7 +66,7 @@ def _tenant(kind: str, seconds: float, warmup: float, socket: Optional[str], q, 
         from ..runtime.tenant import TenantClient
         t = TenantClient(kind, socket, slots=args.get("slots", 8), weight=args.get(f"{kind}_weight", 256),
                          spatial=args.get("spatial", False), priority=args.get(f"{kind}_prio", 0),
-                         one_queue=not args.get("multiq"))
+                         one_queue=bool(args.get("one_queue")), queue_probe=args.get("queue_probe", 0))
         if args.get("prestream") and t.se_mode:
             t.prepare_streams()
     if kind == "infer":
@@ -194,7 +194,8 @@ def run(policy: str, kinds, args: dict, seconds: float, warmup: float) -> Dict[s
     # variant suffixes: +prio (high-priority decode queue), +hwqN (tenant
     # GPU_MAX_HW_QUEUES=N), +pre (both SE-half streams created at registration),
     # +nohwc (daemon on modeled counters), +swapN (static split: the first N s
-    # on the swapped halves)
+    # on the swapped halves), +one (one masked queue per shim tenant), +qpK
+    # (K masked queues per half, chosen by measured slice time)
     policy, *mods = policy.split("+")
     policy = ALIASES.get(policy, policy)
     base = policy.split("@")[0]
@@ -207,8 +208,10 @@ def run(policy: str, kinds, args: dict, seconds: float, warmup: float) -> Dict[s
             args["tenant_hwq"] = int(m[3:])
         elif m == "pre":
             args["prestream"] = True
-        elif m == "multiq":  # shim tenants may use both SE-half masked queues (pre-fix behaviour)
-            args["multiq"] = True
+        elif m == "one":  # shim tenants: one masked queue, class home half only
+            args["one_queue"] = True
+        elif m.startswith("qp"):  # shim tenants: K masked queues per half, the fastest by measurement
+            args["queue_probe"] = int(m[2:])
         elif m == "nohwc":
             args["nohwc"] = True
         elif m.startswith("swap"):

@@ -70,10 +70,77 @@ def se_cu_words(ses) -> List[int]:
     return words
 
 
+class QueueProber:
+    """Choose, among K CU-masked queues of the same mask, the one whose slices
+    run fastest, and re-choose when the chosen one degrades.
+
+    Which hardware pipe a queue lands on is decided by the hardware scheduler
+    from the node-wide queue set, not by the process.  Two processes whose
+    active queues share a pipe measured a head-of-line stall: a decode-like
+    step of 96 small GEMVs ran 16.5 ms instead of 2.5 ms next to a GEMM on
+    the other shader engines, bimodally by run and unchanged for the whole
+    run (scripts/queue_switch_probe.py, profiles/llm5/queue_switch_probe.json),
+    which is config #5's collapse.  Equal masks, different queues: the fast
+    and the slow queue differ only in where they were mapped.
+
+    Explore each queue for ``explore`` slices (the median of its last
+    ``keep``), exploit the fastest, and explore again when the exploited
+    queue's EWMA exceeds ``drift`` x its explored median -- at most once per
+    ``cooldown`` slices, doubling after every re-exploration that changed
+    nothing.  Pure bookkeeping (CPU-testable); the caller times the slices."""
+
+    def __init__(self, k: int, explore: int = 6, keep: int = 4, drift: float = 1.6, cooldown: int = 100):
+        self.k, self.explore, self.keep, self.drift = int(k), int(explore), int(keep), float(drift)
+        self.cooldown0 = self.cooldown = int(cooldown)
+        self.idx = 0
+        self.exploring = True
+        self.samples: List[List[float]] = [[] for _ in range(self.k)]
+        self.ref = 0.0
+        self.ewma = 0.0
+        self.since = 0
+        self.explorations = 0
+        self.choices: List[int] = []
+
+    def current(self) -> int:
+        return self.idx
+
+    @staticmethod
+    def _median(xs: List[float]) -> float:
+        xs = sorted(xs)
+        n = len(xs)
+        return xs[n // 2] if n % 2 else 0.5 * (xs[n // 2 - 1] + xs[n // 2])
+
+    def record(self, ms: float):
+        if self.exploring:
+            self.samples[self.idx].append(ms)
+            if len(self.samples[self.idx]) < self.explore:
+                return
+            if self.idx + 1 < self.k:
+                self.idx += 1
+                return
+            meds = [self._median(x[-self.keep:]) for x in self.samples]
+            best = min(range(self.k), key=lambda i: meds[i])
+            prev = self.choices[-1] if self.choices else None
+            if prev is not None and best == prev:
+                self.cooldown *= 2  # nothing changed: back off
+            else:
+                self.cooldown = self.cooldown0
+            self.idx, self.ref, self.ewma = best, meds[best], meds[best]
+            self.exploring, self.since = False, 0
+            self.choices.append(best)
+            self.explorations += 1
+            return
+        self.since += 1
+        self.ewma = 0.8 * self.ewma + 0.2 * ms
+        if self.since >= self.cooldown and self.ewma > self.drift * self.ref:
+            self.samples = [[] for _ in range(self.k)]
+            self.idx, self.exploring = 0, True
+
+
 class TenantClient:
     def __init__(self, name: str, socket_path: str = DEFAULT_SOCKET, slots: int = 8, weight: int = -1,
                  cap: int = -1, pool=None, gpu: int = 0, heartbeat_s: float = 0.05, spatial: bool = True,
-                 priority: int = 0, one_queue: bool = True):
+                 priority: int = 0, one_queue: bool = False, queue_probe: int = 0):
         self.name = name
         self.gpu = gpu
         self.spatial = spatial
@@ -97,6 +164,12 @@ class TenantClient:
         self._streams: Dict[Tuple, object] = {}
         self.one_queue = one_queue  # SE mode: one masked queue, on the class home half (see stream())
         self._home: Optional[Tuple[int, int]] = None
+        # SE mode: K masked queues per half, the fastest chosen by measurement
+        # (QueueProber); the slice body must end synchronised (the decode and
+        # training loops do) for its time to mean anything
+        self.queue_probe = int(queue_probe)
+        self._probers: Dict[Tuple, QueueProber] = {}
+        self._probe_key: Optional[Tuple] = None
         self._progress = 0
         self._stop = threading.Event()
         self._hb = threading.Thread(target=self._beat, args=(heartbeat_s,), daemon=True, name=f"gpbs-hb-{name}")
@@ -188,6 +261,15 @@ class TenantClient:
                 if home != ses or (self._home is not None and self._home != ses):
                     return torch.cuda.current_stream()
                 self._home = ses
+            if self.queue_probe > 1:
+                pr = self._probers.get(ses)
+                if pr is None:
+                    pr = self._probers[ses] = QueueProber(self.queue_probe)
+                    for i in range(self.queue_probe):  # all K at once: the set the prober chooses from
+                        self._streams[("se",) + ses + (i,)] = torch.cuda.ExternalStream(
+                            K.cumask_stream(se_cu_words(ses), device=self.gpu))
+                self._probe_key = ses
+                return self._streams[("se",) + ses + (pr.current(),)]
             s = self._streams.get(("se",) + ses)
             if s is None:
                 s = torch.cuda.ExternalStream(K.cumask_stream(se_cu_words(ses), device=self.gpu))
@@ -215,9 +297,14 @@ class TenantClient:
         if not self.gate(timeout_s):
             raise TimeoutError(f"tenant {self.name}: gate closed for {timeout_s}s")
         waited = time.monotonic_ns() - t0
+        self._probe_key = None
         s = self.stream()
+        key = self._probe_key
+        t1 = time.perf_counter()
         with torch.cuda.stream(s):
             yield s
+        if key is not None:
+            self._probers[key].record(1e3 * (time.perf_counter() - t1))
         self._progress += 1
         if waited > 0:
             self.report_wait(waited)

@@ -16,6 +16,8 @@ per step.  Arms (every arm a fresh pair of processes):
   pre       like swap, but each process creates both masked streams up front
             and the swap is a choice between two existing queues
   fixed-graph / swap-graph   as fixed / swap, the lat step replayed from a HIP graph
+  rotate / rotate-graph      lat creates 4 queues with the SAME mask {2,3} and
+            times 12 steps on each while bulk runs (per-queue medians)
 Output: per arm and rep, per-process step-time medians before / after the
 swap and a 250 ms timeline; JSON on stdout.
 """
@@ -42,6 +44,8 @@ def _proc(kind, arm, seconds, swap_at, start, q):
     home = (2, 3) if kind == "lat" else (0, 1)
     other = (0, 1) if kind == "lat" else (2, 3)
     moves = arm in ("swap", "pre", "swap-graph") or (arm == "lat-only" and kind == "lat")
+    if arm.startswith("rotate") and kind == "bulk":
+        seconds = max(seconds, 3.0)
     first = other if moves else home
     streams = {}
 
@@ -52,6 +56,9 @@ def _proc(kind, arm, seconds, swap_at, start, q):
     if arm == "pre":
         stream((0, 1))
         stream((2, 3))
+    rot = []
+    if arm.startswith("rotate") and kind == "lat":  # K queues with the same mask, created together
+        rot = [torch.cuda.ExternalStream(K.cumask_stream(se_cu_words(home))) for _ in range(4)]
     if kind == "lat":
         x = torch.randn(8, 4096, device="cuda", dtype=torch.bfloat16)
         ws = [torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16) for _ in range(12)]
@@ -77,6 +84,20 @@ def _proc(kind, arm, seconds, swap_at, start, q):
         step()
         torch.cuda.synchronize()
     start.wait(timeout=600)
+    if rot:  # 12 steps on each queue after 0.5 s of the bulk running; medians of the last 8
+        time.sleep(0.5)
+        per = []
+        for s in rot:
+            ts = []
+            for _ in range(12):
+                t1 = time.perf_counter()
+                with torch.cuda.stream(s):
+                    step()
+                s.synchronize()
+                ts.append(1e3 * (time.perf_counter() - t1))
+            per.append(round(statistics.median(ts[4:]), 2))
+        q.put({"kind": kind, "per_queue_ms": per, "before_ms": None, "after_ms": None, "timeline": []})
+        return
     t0 = time.monotonic()
     rows = []
     while True:
@@ -128,7 +149,8 @@ def main():
         for arm in a.arms.split(","):
             r = run_arm(arm, a.seconds, a.swap_at)
             res.setdefault(arm, []).append(r)
-            print(f"[probe] {arm} rep {rep}: lat {r['lat']['before_ms']} -> {r['lat']['after_ms']} ms, "
+            print(f"[probe] {arm} rep {rep}: lat {r['lat']['before_ms']} -> {r['lat']['after_ms']} ms "
+                  f"{r['lat'].get('per_queue_ms', '')}, "
                   f"bulk {r['bulk']['before_ms']} -> {r['bulk']['after_ms']} ms", file=sys.stderr, flush=True)
     print(json.dumps(res))
 

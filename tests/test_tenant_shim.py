@@ -100,6 +100,7 @@ def test_se_mode_stream_uses_one_masked_queue_on_the_class_home_half(monkeypatch
     monkeypatch.setattr(torch.cuda, "current_stream", lambda: "unmasked")
     t = object.__new__(TenantClient)
     t.se_mode, t.spatial, t.gpu, t.one_queue, t._home, t._streams = True, True, 0, True, None, {}
+    t.queue_probe, t._probers = 0, {}
     cls = {"v": -1}
     t.vpmu = lambda: {"class": cls["v"]}
     lo = [(x, c) for x in range(8) for c in (0, 1)]
@@ -113,3 +114,32 @@ def test_se_mode_stream_uses_one_masked_queue_on_the_class_home_half(monkeypatch
     assert t.stream(lo) == "unmasked" and len(made) == 1   # never a second masked queue
     t.one_queue, t._home = False, None          # pre-fix behaviour: any owned half gets its queue
     assert t.stream(lo) == ("masked", 2) and len(made) == 2
+
+
+def test_queue_prober_explores_exploits_and_reexplores_on_drift():
+    """Per SE half, K masked queues: explore each, exploit the fastest,
+    explore again when the chosen one's slices drift above 1.6x its explored
+    median (the head-of-line stall of a queue mapped onto a busy pipe)."""
+    from pbs_amd.runtime.tenant import QueueProber
+    speed = {0: 16.5, 1: 2.5, 2: 16.4}   # ms per slice on each queue
+    p = QueueProber(3, explore=4, keep=3, drift=1.6, cooldown=10)
+    seen = []
+    for _ in range(12):
+        seen.append(p.current())
+        p.record(speed[p.current()])
+    assert seen == [0] * 4 + [1] * 4 + [2] * 4 and not p.exploring and p.current() == 1
+    for _ in range(50):                  # steady: stays on the fast queue
+        p.record(speed[p.current()])
+    assert p.current() == 1 and p.explorations == 1
+    speed[1] = 17.0                       # its pipe became busy: re-explore, queue 2 is now the fast one
+    speed[2] = 2.6
+    for _ in range(40):
+        p.record(speed[p.current()])
+    assert p.current() == 2 and p.explorations == 2
+    # a re-exploration that picks the same queue backs the cooldown off
+    c = p.cooldown
+    speed[0] = speed[1] = 30.0
+    speed[2] = 5.0                        # everything slower (more load), queue 2 still best
+    for _ in range(200):
+        p.record(speed[p.current()])
+    assert p.current() == 2 and p.cooldown > c
