@@ -66,7 +66,7 @@ def _tenant(kind: str, seconds: float, warmup: float, socket: Optional[str], q, 
         from ..runtime.tenant import TenantClient
         t = TenantClient(kind, socket, slots=args.get("slots", 8), weight=args.get(f"{kind}_weight", 256),
                          spatial=args.get("spatial", False), priority=args.get(f"{kind}_prio", 0),
-                         one_queue=bool(args.get("one_queue")), queue_probe=args.get("queue_probe", 0))
+                         one_queue=bool(args.get("one_queue")), queue_probe=args.get("queue_probe", -1))
         if args.get("prestream") and t.se_mode:
             t.prepare_streams()
     if kind == "infer":

@@ -84,13 +84,16 @@ class QueueProber:
     and the slow queue differ only in where they were mapped.
 
     Explore each queue for ``explore`` slices (the median of its last
-    ``keep``), exploit the fastest, and explore again when the exploited
+    ``keep``; a queue whose first slice is ``abort`` x slower than the best so
+    far is left at once), exploit the fastest, and explore again when the exploited
     queue's EWMA exceeds ``drift`` x its explored median -- at most once per
     ``cooldown`` slices, doubling after every re-exploration that changed
     nothing.  Pure bookkeeping (CPU-testable); the caller times the slices."""
 
-    def __init__(self, k: int, explore: int = 6, keep: int = 4, drift: float = 1.6, cooldown: int = 100):
+    def __init__(self, k: int, explore: int = 4, keep: int = 3, drift: float = 1.6, cooldown: int = 100,
+                 abort: float = 2.0):
         self.k, self.explore, self.keep, self.drift = int(k), int(explore), int(keep), float(drift)
+        self.abort = float(abort)
         self.cooldown0 = self.cooldown = int(cooldown)
         self.idx = 0
         self.exploring = True
@@ -113,12 +116,16 @@ class QueueProber:
     def record(self, ms: float):
         if self.exploring:
             self.samples[self.idx].append(ms)
-            if len(self.samples[self.idx]) < self.explore:
+            done = [self._median(x[-self.keep:]) for x in self.samples[:self.idx] if x]
+            # a stalled queue shows on its first slice: leave it after one
+            # (the stall costs one slow slice per exploration, not `explore`)
+            stalled = bool(done) and ms > self.abort * min(done)
+            if len(self.samples[self.idx]) < self.explore and not stalled:
                 return
             if self.idx + 1 < self.k:
                 self.idx += 1
                 return
-            meds = [self._median(x[-self.keep:]) for x in self.samples]
+            meds = [self._median(x[-self.keep:]) if x else float("inf") for x in self.samples]
             best = min(range(self.k), key=lambda i: meds[i])
             prev = self.choices[-1] if self.choices else None
             if prev is not None and best == prev:
@@ -140,7 +147,7 @@ class QueueProber:
 class TenantClient:
     def __init__(self, name: str, socket_path: str = DEFAULT_SOCKET, slots: int = 8, weight: int = -1,
                  cap: int = -1, pool=None, gpu: int = 0, heartbeat_s: float = 0.05, spatial: bool = True,
-                 priority: int = 0, one_queue: bool = False, queue_probe: int = 0):
+                 priority: int = 0, one_queue: bool = False, queue_probe: int = -1):
         self.name = name
         self.gpu = gpu
         self.spatial = spatial
@@ -167,7 +174,7 @@ class TenantClient:
         # SE mode: K masked queues per half, the fastest chosen by measurement
         # (QueueProber); the slice body must end synchronised (the decode and
         # training loops do) for its time to mean anything
-        self.queue_probe = int(queue_probe)
+        self.queue_probe = int(queue_probe) if queue_probe >= 0 else (3 if self.se_mode else 0)
         self._probers: Dict[Tuple, QueueProber] = {}
         self._probe_key: Optional[Tuple] = None
         self._progress = 0
