@@ -17,6 +17,8 @@
 // csched_dom_metric_update (X:xen/common/sched_credit.c:416-424) without a
 // master.  A missed deadline records GANG_TIMEOUT and either re-forms the view
 // among the survivors (gpbs_gang_shm_reform) or degrades to local scheduling.
+#include <stdio.h>
+#include <stdlib.h>
 #include <time.h>
 
 #include <algorithm>
@@ -78,6 +80,7 @@ struct Coord {
   std::vector<Metric> node, totals;
   int64_t timeouts = 0, reforms = 0, metric_syncs = 0, switches = 0, atc_global = 0;
   int degraded = 0, error = 0;
+  bool debug = false;
 };
 
 // ------------------------------------------------------------------ engine
@@ -165,6 +168,9 @@ bool reform(Coord* c) {
   const int rc = gpbs_gang_shm_reform(c->shm, c->cfg.join_ns, mono_ns() + c->cfg.join_ns + c->cfg.deadline_ns, &m,
                                       &base);
   range_pop(c);
+  if (c->debug)
+    fprintf(stderr, "[gang_coord] rank %d epoch %llu: reform rc %d members %llx base %llu\n", c->cfg.rank,
+            (unsigned long long)c->epoch, rc, (unsigned long long)m, (unsigned long long)base);
   if (rc) return false;
   std::lock_guard<std::mutex> g(c->mu);
   ++c->reforms;
@@ -254,9 +260,13 @@ void loop(Coord* c) {
     std::vector<int64_t> red;
     int why = 0;
     range_push(c, c->epoch);
+    const int64_t tg = mono_ns();
     const bool ok = reduce(c, vec, red, t0 + dl, &why, [](int64_t a, int64_t b) { return std::min(a, b); });
     range_pop(c);
     const int64_t t1 = mono_ns();
+    if (c->debug && (c->epoch < 4 || !ok))
+      fprintf(stderr, "[gang_coord] rank %d epoch %llu: vector %lld us, exchange %lld us, ok %d\n", c->cfg.rank,
+              (unsigned long long)c->epoch, (long long)(tg - t0) / 1000, (long long)(t1 - tg) / 1000, (int)ok);
     if (!ok) {
       if (why < 0 || !fail(why, t0)) break;
       continue;
@@ -334,6 +344,8 @@ void* gpbs_gang_coord_start(gpbs_engine_t* e, void* shm, int world, int nvals, c
   c->wait_prev.assign(nt, 0);
   c->wait_seen.assign(nt, false);
   c->node.assign(cfg->nmetric, Metric{});
+  const char* dbg = getenv("GPBS_GANG_DEBUG");
+  c->debug = dbg && dbg[0] == '1';
   c->totals.assign(cfg->nmetric, Metric{});
   c->th = std::thread(loop, c);
   return c;

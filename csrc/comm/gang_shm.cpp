@@ -138,16 +138,22 @@ int gpbs_gang_shm_allgather(void* h, uint64_t epoch, const int64_t* in, int64_t*
     int spins = 0;
     while (o.seq.load(std::memory_order_acquire) < epoch) {
       // the peers normally arrive within microseconds: busy-poll first
-      // (PAUSE), then yield, then sleep until the deadline
-      if (++spins < 4096) {
+      // (PAUSE), then yield, then sleep until the deadline.  The deadline is
+      // checked in every phase: on a loaded host one sched_yield can give
+      // the CPU away for a whole time slice, and 256 of them overran a
+      // 200 ms deadline by up to 0.5 s (tests/test_gang_deadline.py under
+      // pytest -n 4)
+      ++spins;
+      if (spins < 4096) {
         __builtin_ia32_pause();
+        if ((spins & 255) == 0 && now_ns() > deadline_ns) return -110;
         continue;
       }
+      if (now_ns() > deadline_ns) return -110;
       if (spins < 4096 + 256) {
         std::this_thread::yield();
         continue;
       }
-      if (now_ns() > deadline_ns) return -110;
       if (g->r->view_gen.load(std::memory_order_acquire) != g->gen) return -116;
       if (g->r->claim.load(std::memory_order_acquire) > g->gen) return -117;
       timespec ts{0, 2000};  // 2 us
