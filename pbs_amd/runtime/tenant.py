@@ -283,6 +283,21 @@ class TenantClient:
                 self._streams[("se",) + ses] = s
             return s
         halves = tuple(sorted({c for (_, c) in parts})) if self.spatial else (0, 1)
+        if self.queue_probe > 1:  # K queues of this kind, the fastest by measurement (QueueProber)
+            key = ("p",) + halves
+            pr = self._probers.get(key)
+            if pr is None:
+                pr = self._probers[key] = QueueProber(self.queue_probe)
+                for i in range(self.queue_probe):
+                    if self.spatial:
+                        h = K.cumask_stream(half_cu_words([(x, c) for x in range(XCDS) for c in halves]),
+                                            device=self.gpu)
+                        st = torch.cuda.ExternalStream(h)
+                    else:
+                        st = torch.cuda.Stream(device=self.gpu, priority=-1 if self.priority > 0 else 0)
+                    self._streams[key + (i,)] = st
+            self._probe_key = key
+            return self._streams[key + (pr.current(),)]
         s = self._streams.get(halves)
         if s is None and not self.spatial:
             s = torch.cuda.Stream(device=self.gpu, priority=-1 if self.priority > 0 else 0)

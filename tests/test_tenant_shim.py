@@ -144,3 +144,24 @@ def test_queue_prober_explores_exploits_and_reexplores_on_drift():
     for _ in range(200):
         p.record(speed[p.current()])
     assert p.current() == 2 and p.cooldown > c
+
+
+def test_co_resident_stream_probes_k_unmasked_queues(monkeypatch):
+    """Co-resident contexts (no CU mask): with queue_probe=K the shim keeps K
+    streams of the tenant's priority and launches on the one QueueProber
+    chose (two unmasked queues on one pipe block each other too: `none` is
+    bimodal in config #5)."""
+    import torch
+
+    from pbs_amd.runtime.tenant import TenantClient
+    made = []
+    monkeypatch.setattr(torch.cuda, "Stream", lambda device=0, priority=0: made.append(priority) or f"q{len(made)}")
+    t = object.__new__(TenantClient)
+    t.se_mode, t.spatial, t.gpu, t.one_queue, t._home, t._streams = False, False, 0, False, None, {}
+    t.queue_probe, t._probers, t.priority = 3, {}, 1
+    parts = [(x, c) for x in range(8) for c in (0, 1)]
+    assert t.stream(parts) == "q1" and made == [-1, -1, -1]
+    pr = t._probers[("p", 0, 1)]
+    for ms in (9.0, 9.0, 9.0, 9.0, 2.0, 2.0, 2.0, 2.0, 9.5):
+        pr.record(ms)
+    assert t.stream(parts) == "q2" and len(made) == 3
