@@ -69,6 +69,8 @@ def main():
     ap.add_argument("--coll", default="ipc", choices=["ipc", "rccl"],
                     help="N > 1 all-reduce tenant: ipc (gated gpbs kernel over IPC-mapped peer buffers, xGMI; "
                          "default) or rccl (torch.distributed all-reduce, not CU-confined)")
+    ap.add_argument("--resolo", action="store_true",
+                    help="diagnostic: measure the solo rates again after each mix's runs (reported, not used)")
     ap.add_argument("--out", default="")
     ap.add_argument("--rehearse-ipc", action="store_true",
                     help="like --rehearse (every rank on GPU 0, gloo) but with the gated IPC all-reduce tenant on "
@@ -181,6 +183,12 @@ def main():
         for p in order:
             runs[p].append(c.run_policy(p, args.steps, args.warmup))
         solo = c.solo_report()
+        if args.resolo:  # diagnostic: the solo rates again after the runs (drift over the mix)
+            start = dict(c.solo_unit_ms)
+            c.calibrate()
+            solo["_end_over_start_rate"] = {k: round(start[k] / c.solo_unit_ms[k], 4) for k in start
+                                            if k in c.solo_unit_ms and c.solo_unit_ms[k]}
+            c.solo_unit_ms = start
         c.close()
         del c
         torch.cuda.empty_cache()
