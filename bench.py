@@ -262,6 +262,7 @@ def main():
                    "policy": "gpbs (counter-driven SE budgets, PBS credit, hw counters)", "mix": head},
         "mean_slowdown_pct": hs["mean_slowdown_pct"],
         "counters": counters,
+        "hwc_restarts": (hwc.restarts() if counters == "hw" else 0),
         "protocol": {"kind": args.protocol, "step_ms": args.step_ms if args.protocol == "steady" else None,
                      "reps": max(1, args.reps), "order": "randomized per repetition", "seed": args.seed,
                      "statistic": "median over reps (IQR = q75 - q25)", "solo": "steady (same protocol, alone)"},

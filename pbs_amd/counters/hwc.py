@@ -87,3 +87,10 @@ def sample_se():
 
 def stop():
     _lib().gpbs_hwc_stop()
+
+
+def restarts() -> int:
+    """Counting-context restarts so far (GPBS_HWC_RESTART samples apart)."""
+    f = _lib().gpbs_hwc_restarts
+    f.restype = __import__("ctypes").c_long
+    return int(f())
