@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round-3 GPU session w: the driver's bench command on the final tree (counting
+# context restarts), then the GPU suite and smoke.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+timeout -k 10 900 python -u bench.py --gpus 1 --steps 20 --warmup 5 --resolo --out gpurun_out/bench_driver_w.json > gpurun_out/bench_driver_w.log 2>&1
+rc=$?; echo "bench rc=$rc"; case $rc in 0) ;; *) exit $rc ;; esac
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests_w.log 2>&1
+rc=$?; echo "gpu tests rc=$rc"; case $rc in 0) ;; *) exit $rc ;; esac
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_w.log 2>&1
+echo "smoke rc=$?"
