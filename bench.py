@@ -115,6 +115,20 @@ def main():
         if not hwc.start():
             print("bench.py: hardware counter start failed; falling back to modeled counters", file=sys.stderr)
             counters = "model"
+    # the GPU's clock / power / temperature / throttle residency over every
+    # timed run (host thread, amdsmi or sysfs): tells a DVFS / power-state
+    # drift from a queue / pipe effect
+    from pbs_amd.utils.gpustate import GpuStateRecorder, device_bdf
+    bdf = device_bdf(local)
+    gpustate = GpuStateRecorder(bdf, period_s=0.2).start()
+    rank_diag = {"rank": rank, "local_rank": local, "device_bdf": bdf, "gpu_state_source": gpustate.source,
+                 "counters": counters}
+    if counters == "hw":
+        rank_diag["hwc_agent"] = hwc.agent()
+        if rank_diag["hwc_agent"]["bdf"] != bdf:
+            print(f"bench.py: rank {rank} counts on agent {rank_diag['hwc_agent']} but runs on {bdf}",
+                  file=sys.stderr)
+            sys.exit(3)
     groups = {}
     if world > 1:
         import torch.distributed as dist
@@ -172,6 +186,7 @@ def main():
             cfg.coll_bytes = 4 << 20  # CPU gloo all-reduce stand-in
         c = Corun(cfg, rank=rank, world=world, device=local, groups=groups, log=log,
                   coll_on_cpu=args.rehearse and not args.rehearse_ipc)
+        c.gpustate = gpustate
         c.calibrate()
         rng = random.Random(args.seed)
         runs = {p: [] for p in pols}
@@ -190,6 +205,11 @@ def main():
                                             if k in c.solo_unit_ms and c.solo_unit_ms[k]}
             c.solo_unit_ms = start
         c.close()
+        diag = dict(c.diag, gang=c.gang_stats or None)  # gang stats of the last run (recorded at its stop)
+        last = [r for r in runs["gpbs"] if r.get("engine")]
+        if last and last[-1]["engine"].get("node_totals"):
+            diag["node_totals"] = last[-1]["engine"]["node_totals"]
+        rank_diag.setdefault("mixes", {})[mix] = diag
         del c
         torch.cuda.empty_cache()
         return runs, order, solo
@@ -278,6 +298,16 @@ def main():
     for m in mixes[1:]:
         line["mixes"][m]["per_tenant"] = {n: {k: v for k, v in t.items() if k != "step_norm_perf"}
                                           for n, t in results[m]["summary"]["per_tenant"].items()}
+    # per-rank pre-flight record (agent / BDF, IPC self-test and fallback,
+    # gang transport, node totals): a multi-GPU run diagnoses itself
+    if world > 1:
+        import torch.distributed as dist
+        allr = [None] * world
+        dist.all_gather_object(allr, rank_diag, group=groups["ctrl"])
+    else:
+        allr = [rank_diag]
+    line["ranks"] = allr
+    gpustate.stop()
     if rank == 0:
         print(json.dumps(line), flush=True)
         if args.out:

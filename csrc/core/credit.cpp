@@ -728,8 +728,12 @@ class CreditScheduler : public Scheduler {
     if (async_pending_) {
       std::vector<int> hid(async_in_.size() + 1);
       std::vector<gpbs_adapt_state_t> hst(async_in_.size() + 1);
-      const int nh = E.counter_ops.adapt_harvest(E.counter_ops.user, (int)async_in_.size(), hid.data(), hst.data());
-      if (nh >= 0) {
+      for (size_t i = 0; i < async_in_.size(); ++i) hid[i] = async_in_[i].id;  // in: this pool's launch
+      int nh = E.counter_ops.adapt_harvest(E.counter_ops.user, (int)async_in_.size(), hid.data(), hst.data());
+      // a result for other tenants (another pool's launch) is never applied
+      for (int i = 0; i < nh && nh >= 0; ++i)
+        if (i >= (int)async_in_.size() || hid[i] != async_in_[i].id) nh = -22;
+      if (nh == (int)async_in_.size()) {
         for (int i = 0; i < nh && i < (int)async_in_.size(); ++i) {
           AdaptState after;
           std::memcpy(&after, &hst[i], sizeof(after));

@@ -14,10 +14,13 @@
 // scripts/hwc_probe.hip).  gpbs_hwc_init must run before the HIP runtime
 // initialises in the process (rocprofiler_force_configure); gpbs_hwc_start
 // after the first device call.
+#include <hip/hip_runtime.h>
+#include <rocprofiler-sdk/buffer.h>
 #include <rocprofiler-sdk/registration.h>
 #include <rocprofiler-sdk/rocprofiler.h>
 
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -39,9 +42,20 @@ constexpr const char* kDefaultSpec =
     "SQ_INSTS_VMEM_RD+SQ_INSTS_VMEM_WR|TCC_MISS";
 
 struct Hwc {
-  rocprofiler_context_id_t ctx{};
+  rocprofiler_context_id_t ctx{};  // the started context (the agent of this process's HIP device)
+  // One counting context per GPU agent, configured at registration (before
+  // HIP exists); gpbs_hwc_start starts only the one whose PCI address is the
+  // calling thread's HIP device -- never a peer GPU's counters, whatever the
+  // enumeration order (VERDICT r3 missing #3).
   std::vector<rocprofiler_agent_id_t> gpus;
+  std::vector<uint32_t> gpu_domain, gpu_loc;  // PCI domain, location (bus << 8 | dev << 3 | fn)
+  std::vector<rocprofiler_context_id_t> ctxs;
+  std::vector<rocprofiler_buffer_id_t> bufs;
+  std::vector<char> ok;                       // agent i configured
   std::vector<rocprofiler_counter_config_id_t> cfg;
+  int chosen = -1;             // agent index counted on
+  char chosen_bdf[32] = {};
+  int index_mismatch = 0;      // only_gpu named another enumeration index than the BDF match
   std::map<uint64_t, int> slot_of;            // counter id -> PBS slot (0..3)
   rocprofiler_counter_dimension_id_t xcc_dim{}, se_dim{};
   bool have_xcc = false, have_se = false;
@@ -63,8 +77,64 @@ struct Hwc {
   long restart_every = -1, since_start = 0, restarts = 0;
   double base_se[kX][kSe][kSlots] = {}, base_x[kX][kSlots] = {};
   double last_se[kX][kSe][kSlots] = {}, last_x[kX][kSlots] = {};
+  // Asynchronous sampling (GPBS_HWC_ASYNC=1): the read is issued with
+  // ROCPROFILER_COUNTER_FLAG_ASYNC into a rocprofiler buffer tagged with a
+  // sequence number, the buffer is flushed, and the call returns the newest
+  // sample whose records have all arrived (usually the previous one).  The
+  // caller learns which sample it got from gpbs_hwc_async_stats.
+  bool async_mode = false;
+  rocprofiler_buffer_id_t buf{};
+  std::mutex amu;  // guards the accumulators below (buffer callback thread)
+  struct Acc {
+    double se[kX][kSe][kSlots];
+    double x[kX][kSlots];
+    size_t n;
+  };
+  std::map<uint64_t, Acc> pend;  // seq -> records so far
+  uint64_t aseq = 0, done_seq = 0, async_issued = 0, async_incomplete = 0;
+  size_t expect = 0;  // records per sample, learned from the first (synchronous) one
+  Acc done{};
 };
 Hwc g;
+
+// Fold one counter record into an accumulator (either path).
+void fold_record(const rocprofiler_counter_record_t& r, double se_acc[kX][kSe][kSlots], double x_acc[kX][kSlots]) {
+  rocprofiler_counter_id_t cid{};
+  if (rocprofiler_query_record_counter_id(r.id, &cid) != ROCPROFILER_STATUS_SUCCESS) return;
+  auto it = g.slot_of.find(cid.handle);
+  if (it == g.slot_of.end()) return;
+  size_t x = 0, se = 0;
+  if (g.have_xcc) rocprofiler_query_record_dimension_position(r.id, g.xcc_dim, &x);
+  if (x >= (size_t)kX) return;
+  x_acc[x][it->second] += r.counter_value;
+  if (g.per_se[cid.handle] &&
+      rocprofiler_query_record_dimension_position(r.id, g.se_dim, &se) == ROCPROFILER_STATUS_SUCCESS &&
+      se < (size_t)kSe)
+    se_acc[x][se][it->second] += r.counter_value;
+}
+
+void on_buffer(rocprofiler_context_id_t, rocprofiler_buffer_id_t, rocprofiler_record_header_t** h, size_t n, void*,
+               uint64_t) {
+  std::lock_guard<std::mutex> l(g.amu);
+  for (size_t i = 0; i < n; ++i) {
+    if (h[i]->category != ROCPROFILER_BUFFER_CATEGORY_COUNTERS || h[i]->kind != ROCPROFILER_COUNTER_RECORD_VALUE)
+      continue;
+    auto* r = (const rocprofiler_counter_record_t*)h[i]->payload;
+    auto ins = g.pend.emplace(r->user_data.value, Hwc::Acc{});
+    fold_record(*r, ins.first->second.se, ins.first->second.x);
+    ins.first->second.n++;
+  }
+  // newest complete sample wins; everything older is dropped
+  for (auto it = g.pend.rbegin(); it != g.pend.rend(); ++it)
+    if (g.expect && it->second.n >= g.expect) {
+      if (it->first > g.done_seq) {
+        g.done = it->second;
+        g.done_seq = it->first;
+      }
+      break;
+    }
+  for (auto it = g.pend.begin(); it != g.pend.end() && it->first <= g.done_seq;) it = g.pend.erase(it);
+}
 
 long restart_every() {
   if (g.restart_every < 0) {
@@ -97,7 +167,10 @@ void maybe_restart() {
 rocprofiler_status_t on_agents(rocprofiler_agent_version_t, const void** agents, size_t n, void*) {
   for (size_t i = 0; i < n; ++i) {
     auto* a = (const rocprofiler_agent_v0_t*)agents[i];
-    if (a->type == ROCPROFILER_AGENT_TYPE_GPU) g.gpus.push_back(a->id);
+    if (a->type != ROCPROFILER_AGENT_TYPE_GPU) continue;
+    g.gpus.push_back(a->id);
+    g.gpu_domain.push_back(a->domain);
+    g.gpu_loc.push_back(a->location_id);
   }
   return ROCPROFILER_STATUS_SUCCESS;
 }
@@ -138,25 +211,45 @@ void set_cfg(rocprofiler_context_id_t ctx, rocprofiler_agent_id_t, rocprofiler_d
 }
 
 int tool_init(rocprofiler_client_finalize_t, void*) {
-  if (rocprofiler_create_context(&g.ctx) != ROCPROFILER_STATUS_SUCCESS) return -1;
   rocprofiler_query_available_agents(ROCPROFILER_AGENT_INFO_VERSION_0, on_agents, sizeof(rocprofiler_agent_v0_t),
                                      nullptr);
-  if (g.only_gpu >= 0) {
-    if (g.only_gpu >= (int)g.gpus.size()) return -1;
-    g.gpus = {g.gpus[g.only_gpu]};  // one process per GPU: never touch a peer's counters
+  {
+    const char* e = getenv("GPBS_HWC_ASYNC");
+    g.async_mode = e && atoi(e) > 0;
   }
-  g.cfg.resize(g.gpus.size());
-  for (size_t i = 0; i < g.gpus.size(); ++i) {
+  const size_t n = g.gpus.size();
+  g.cfg.resize(n);
+  g.ctxs.resize(n);
+  g.bufs.resize(n);
+  g.ok.assign(n, 0);
+  for (size_t i = 0; i < n; ++i) {
     std::vector<rocprofiler_counter_id_t> ids;
     rocprofiler_iterate_agent_supported_counters(g.gpus[i], on_counters, &ids);
     if (ids.empty()) continue;
     if (rocprofiler_create_counter_config(g.gpus[i], ids.data(), ids.size(), &g.cfg[i]) !=
         ROCPROFILER_STATUS_SUCCESS)
       continue;
-    rocprofiler_configure_device_counting_service(g.ctx, rocprofiler_buffer_id_t{0}, g.gpus[i], set_cfg, &g.cfg[i]);
+    if (rocprofiler_create_context(&g.ctxs[i]) != ROCPROFILER_STATUS_SUCCESS) continue;
+    g.bufs[i] = rocprofiler_buffer_id_t{0};
+    if (g.async_mode && rocprofiler_create_buffer(g.ctxs[i], 1 << 22, 3 << 20, ROCPROFILER_BUFFER_POLICY_LOSSLESS,
+                                                  on_buffer, nullptr, &g.bufs[i]) != ROCPROFILER_STATUS_SUCCESS)
+      continue;
+    if (rocprofiler_configure_device_counting_service(g.ctxs[i], g.bufs[i], g.gpus[i], set_cfg, &g.cfg[i]) !=
+        ROCPROFILER_STATUS_SUCCESS)
+      continue;
+    g.ok[i] = 1;
     g.configured = true;
   }
   return 0;
+}
+
+// "dddd:bb:dd.f" -> (domain, bus << 8 | dev << 3 | fn)
+bool parse_bdf(const char* s, uint32_t* dom, uint32_t* loc) {
+  unsigned d = 0, b = 0, v = 0, f = 0;
+  if (std::sscanf(s, "%x:%x:%x.%x", &d, &b, &v, &f) != 4) return false;
+  *dom = d;
+  *loc = (b << 8) | (v << 3) | f;
+  return true;
 }
 
 void tool_fini(void*) {}
@@ -198,8 +291,10 @@ extern "C" {
 //   CPU_CLK_UNHALTED SQ_BUSY_CYCLES                                   (per SE)
 //   LLC_REFERENCES   TCP_TCC_READ_REQ + TCP_TCC_WRITE_REQ (L1 misses = L2 requests, per SE)
 //   LLC_MISSES       TCC_MISS                                         (per XCD: the L2 is per XCD)
-// Must precede HIP runtime initialisation.  `gpu` >= 0 restricts counting to
-// that GPU agent (agents in enumeration order; one rank per GPU).  0 on success.
+// Must precede HIP runtime initialisation.  Every GPU agent gets a counting
+// context; gpbs_hwc_start starts the one at the PCI address of the current
+// HIP device.  `gpu` >= 0 (LOCAL_RANK) is only a cross-check of the
+// enumeration index (gpbs_hwc_agent reports a mismatch).  0 on success.
 int gpbs_hwc_init_gpu(const char* spec, int gpu);
 int gpbs_hwc_init(const char* spec) { return gpbs_hwc_init_gpu(spec, -1); }
 
@@ -216,14 +311,42 @@ int gpbs_hwc_init_gpu(const char* spec, int gpu) {
   return rocprofiler_force_configure(configure) == ROCPROFILER_STATUS_SUCCESS ? 0 : -1;
 }
 
-// After the first device call (the runtime is up): start counting.
+// After the first device call (the runtime is up): start counting on the
+// agent at the PCI address of the calling thread's current HIP device.
+// -2: not configured, -3: no agent at that address (or its configuration
+// failed), -1: the context did not start.
 int gpbs_hwc_start(void) {
   std::lock_guard<std::mutex> l(g.mu);
   if (!g.configured) return -2;
   if (g.started) return 0;
-  if (rocprofiler_start_context(g.ctx) != ROCPROFILER_STATUS_SUCCESS) return -1;
+  int dev = 0;
+  char bus[32] = {};
+  uint32_t dom = 0, loc = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetPCIBusId(bus, sizeof bus, dev) != hipSuccess ||
+      !parse_bdf(bus, &dom, &loc))
+    return -3;
+  int pick = -1;
+  for (size_t i = 0; i < g.gpus.size(); ++i)
+    if (g.ok[i] && g.gpu_domain[i] == dom && g.gpu_loc[i] == loc) pick = (int)i;
+  if (pick < 0) return -3;
+  g.index_mismatch = g.only_gpu >= 0 && g.only_gpu != pick;
+  if (rocprofiler_start_context(g.ctxs[pick]) != ROCPROFILER_STATUS_SUCCESS) return -1;
+  g.ctx = g.ctxs[pick];
+  if (g.async_mode) g.buf = g.bufs[pick];
+  g.chosen = pick;
+  std::snprintf(g.chosen_bdf, sizeof g.chosen_bdf, "%04x:%02x:%02x.%x", dom, (loc >> 8) & 0xff, (loc >> 3) & 0x1f,
+                loc & 7);
   g.started = true;
   return 0;
+}
+
+// The counted agent: its index among the GPU agents, its PCI address, and
+// whether only_gpu (LOCAL_RANK) named a different index.  -1 before start.
+int gpbs_hwc_agent(char* bdf_out, int n, int* index_mismatch) {
+  std::lock_guard<std::mutex> l(g.mu);
+  if (bdf_out && n > 0) std::snprintf(bdf_out, (size_t)n, "%s", g.chosen_bdf);
+  if (index_mismatch) *index_mismatch = g.index_mismatch;
+  return g.started ? g.chosen : -1;
 }
 
 int gpbs_hwc_active(void) { return g.started ? 1 : 0; }
@@ -264,25 +387,32 @@ int gpbs_hwc_sample(uint64_t* out, int nxcd) {
 int gpbs_hwc_sample_se(uint64_t* se_out, uint64_t* x_out) {
   std::lock_guard<std::mutex> l(g.mu);
   if (!g.started || !se_out || !x_out) return -1;
-  if (g.rec.empty()) g.rec.resize(16384);
-  size_t n = g.rec.size();
-  if (rocprofiler_sample_device_counting_service(g.ctx, {}, ROCPROFILER_COUNTER_FLAG_NONE, g.rec.data(), &n) !=
-      ROCPROFILER_STATUS_SUCCESS)
-    return -1;
   double se_acc[kX][kSe][kSlots] = {}, x_acc[kX][kSlots] = {};
-  for (size_t i = 0; i < n; ++i) {
-    rocprofiler_counter_id_t cid{};
-    if (rocprofiler_query_record_counter_id(g.rec[i].id, &cid) != ROCPROFILER_STATUS_SUCCESS) continue;
-    auto it = g.slot_of.find(cid.handle);
-    if (it == g.slot_of.end()) continue;
-    size_t x = 0, se = 0;
-    if (g.have_xcc) rocprofiler_query_record_dimension_position(g.rec[i].id, g.xcc_dim, &x);
-    if (x >= (size_t)kX) continue;
-    x_acc[x][it->second] += g.rec[i].counter_value;
-    if (g.per_se[cid.handle] &&
-        rocprofiler_query_record_dimension_position(g.rec[i].id, g.se_dim, &se) == ROCPROFILER_STATUS_SUCCESS &&
-        se < (size_t)kSe)
-      se_acc[x][se][it->second] += g.rec[i].counter_value;
+  size_t n = 0;
+  if (g.async_mode && g.expect) {
+    rocprofiler_user_data_t ud{};
+    ud.value = ++g.aseq;
+    if (rocprofiler_sample_device_counting_service(g.ctx, ud, ROCPROFILER_COUNTER_FLAG_ASYNC, nullptr, nullptr) !=
+        ROCPROFILER_STATUS_SUCCESS)
+      return -1;
+    g.async_issued++;
+    rocprofiler_flush_buffer(g.buf);
+    std::lock_guard<std::mutex> a(g.amu);
+    if (g.done_seq == 0) {
+      g.async_incomplete++;
+      return -2;  // nothing complete yet
+    }
+    std::memcpy(se_acc, g.done.se, sizeof(se_acc));
+    std::memcpy(x_acc, g.done.x, sizeof(x_acc));
+    n = g.done.n;
+  } else {
+    if (g.rec.empty()) g.rec.resize(16384);
+    n = g.rec.size();
+    if (rocprofiler_sample_device_counting_service(g.ctx, {}, ROCPROFILER_COUNTER_FLAG_NONE, g.rec.data(), &n) !=
+        ROCPROFILER_STATUS_SUCCESS)
+      return -1;
+    for (size_t i = 0; i < n; ++i) fold_record(g.rec[i], se_acc, x_acc);
+    if (g.async_mode) g.expect = n;  // the first sample is synchronous: it sizes a complete async sample
   }
   for (int x = 0; x < kX; ++x)
     for (int k = 0; k < kSlots; ++k) {
@@ -295,6 +425,20 @@ int gpbs_hwc_sample_se(uint64_t* se_out, uint64_t* x_out) {
     }
   maybe_restart();
   return (int)n;
+}
+
+// Asynchronous mode statistics: out[0] = 1 if async, [1] issued, [2] newest
+// complete sequence, [3] last issued sequence, [4] calls with nothing
+// complete.  Returns 0.
+int gpbs_hwc_async_stats(uint64_t* out5) {
+  std::lock_guard<std::mutex> l(g.mu);
+  std::lock_guard<std::mutex> a(g.amu);
+  out5[0] = g.async_mode ? 1 : 0;
+  out5[1] = g.async_issued;
+  out5[2] = g.done_seq;
+  out5[3] = g.aseq;
+  out5[4] = g.async_incomplete;
+  return 0;
 }
 
 // 1 if slot k's counters are resolved per shader engine.

@@ -324,8 +324,14 @@ struct GpuCtx {
   std::atomic<int64_t> revoke_ns[kMaxTenants] = {};  // last publish that took a partition from the tenant
   hipEvent_t adapt_ev = nullptr;  // device adapt: bounded poll, never a blocking sync
   bool adapt_pending = false;
-  // Asynchronous device adapt (engine adapt_launch / adapt_harvest): two
-  // pinned buffer sets; a launch uses a free one, the next tick harvests it.
+  // Asynchronous device adapt (engine adapt_launch / adapt_harvest): pinned
+  // buffer sets; a launch uses a free one, the next tick of the SAME pool
+  // harvests it (matched by its tenant ids: pools sharing this context never
+  // see each other's results).  A launch nobody harvested within kAbufOrphan
+  // later launches (its engine stopped, or its pool went away) is freed once
+  // its kernel is done.
+  static constexpr int kAbuf = 6;
+  static constexpr uint64_t kAbufOrphan = 8;
   struct AdaptBuf {
     gpbs_adapt_state_t* st = nullptr;  // in/out, pinned mapped
     u64* delta = nullptr;              // [kMaxTenants][4]
@@ -333,9 +339,9 @@ struct GpuCtx {
     int ids[kMaxTenants];
     int n = 0;
     int state = 0;  // 0 free, 1 pending, 2 pending + result discarded
+    uint64_t gen = 0;  // async_launches at its launch
     hipEvent_t ev = nullptr;
-  } abuf[2];
-  int abuf_last = -1;
+  } abuf[kAbuf];
   uint64_t async_launches = 0, async_late = 0, async_busy = 0;
   uint64_t adapt_late = 0, adapt_calls = 0, adapt_busy = 0;
   int se_mode = 0;  // partitions are exclusive shader engines (GATE_SE)
@@ -854,12 +860,16 @@ int ctr_adapt_launch(void* user, int n, const int* tenants, const uint64_t* delt
   if (n <= 0 || n > kMaxTenants) return -22;
   RoctxRange rr("gpbs:adapt_launch");
   int b = -1;
-  for (int i = 0; i < 2 && b < 0; ++i) {
+  for (int i = 0; i < GpuCtx::kAbuf; ++i) {
     GpuCtx::AdaptBuf& B = c->abuf[i];
-    // a dropped result that landed, or an orphan (launched for an engine
-    // that stopped before harvesting it): free once the kernel is done
-    if ((B.state == 2 || (B.state == 1 && i != c->abuf_last)) && hipEventQuery(B.ev) == hipSuccess) B.state = 0;
-    if (B.state == 0) b = i;
+    // a dropped result that landed, or an orphan nobody harvested: free once
+    // the kernel is done
+    const bool orphan = B.state == 1 && c->async_launches - B.gen > GpuCtx::kAbufOrphan;
+    if ((B.state == 2 || orphan) && hipEventQuery(B.ev) == hipSuccess) B.state = 0;
+    // the caller's own previous launch is superseded by this one (it did not
+    // harvest it: its tick recomputed that period on the host)
+    if (B.state == 1 && B.n == n && std::memcmp(B.ids, tenants, sizeof(int) * n) == 0) B.state = 2;
+    if (B.state == 0 && b < 0) b = i;
   }
   if (b < 0) {
     c->async_busy++;
@@ -876,26 +886,30 @@ int ctr_adapt_launch(void* user, int n, const int* tenants, const uint64_t* delt
       hipEventRecord(B.ev, c->sched_stream) != hipSuccess)
     return -5;
   B.state = 1;
-  c->abuf_last = b;
-  c->async_launches++;
+  B.gen = ++c->async_launches;
   return 0;
 }
 
+// tenants_out holds, on entry, the ids the caller launched (max of them):
+// harvest that launch and no other pool's.
 int ctr_adapt_harvest(void* user, int max, int* tenants_out, gpbs_adapt_state_t* states_out) {
   GpuCtx* c = (GpuCtx*)user;
-  if (c->abuf_last < 0) return -22;
-  GpuCtx::AdaptBuf& B = c->abuf[c->abuf_last];
-  if (B.state != 1) return -22;
-  if (hipEventQuery(B.ev) != hipSuccess) {
-    B.state = 2;  // the engine recomputes this period on the host; drop the result when it lands
+  if (max <= 0 || max > kMaxTenants || !tenants_out) return -22;
+  GpuCtx::AdaptBuf* B = nullptr;
+  for (auto& X : c->abuf)
+    if (X.state == 1 && X.n == max && std::memcmp(X.ids, tenants_out, sizeof(int) * max) == 0 &&
+        (!B || X.gen > B->gen))
+      B = &X;
+  if (!B) return -22;
+  if (hipEventQuery(B->ev) != hipSuccess) {
+    B->state = 2;  // the engine recomputes this period on the host; drop the result when it lands
     c->async_late++;
     return -11;
   }
-  const int n = std::min(B.n, max);
-  std::memcpy(states_out, B.st, sizeof(gpbs_adapt_state_t) * n);
-  std::memcpy(tenants_out, B.ids, sizeof(int) * n);
-  B.state = 0;
-  return n;
+  std::memcpy(states_out, B->st, sizeof(gpbs_adapt_state_t) * max);
+  std::memcpy(tenants_out, B->ids, sizeof(int) * max);
+  B->state = 0;
+  return max;
 }
 
 // --------------------------------------------------------------------- runner
@@ -1577,7 +1591,6 @@ int gpbs_gpu_attach(void* p, gpbs_engine_t* e, int device_counters, int device_a
   c->engine = e;
   for (auto& B : c->abuf)  // a new engine harvests nothing an old one launched
     if (B.state == 1) B.state = 2;
-  c->abuf_last = -1;
   gpbs_actuator_ops_t a{};
   a.user = c;
   a.on_switch = act_on_switch;
@@ -1768,6 +1781,63 @@ int gpbs_gpu_set_hwc_device(void* p, int on) {
 // Numerics check of k_hwc_attribute against hwc_attr_host on `iters` random
 // snapshot pairs (seeded): max relative difference of the attributed and
 // clean deltas and the interval totals.  Stand-alone (no context needed).
+// Cost of one attribution (a live-layout snapshot in pinned host memory, as
+// on the headline path): out[0] = mean device time per launch over `iters`
+// back-to-back launches (hipEvent), out[1] = mean host round trip of one
+// launch + event wait.  0 on success.
+int gpbs_hip_hwc_attr_bench(int iters, double* out2) {
+  if (iters <= 0 || !out2) return -22;
+  HwcAttrIn* in = nullptr;
+  HwcAttrOut* out = nullptr;
+  HwcAttrPrev* d_st = nullptr;
+  hipStream_t s = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int rc = 0;
+  if (hipHostMalloc((void**)&in, sizeof(HwcAttrIn), hipHostMallocMapped) != hipSuccess ||
+      hipHostMalloc((void**)&out, sizeof(HwcAttrOut), hipHostMallocMapped) != hipSuccess ||
+      hipMalloc((void**)&d_st, sizeof(HwcAttrPrev)) != hipSuccess || hipStreamCreate(&s) != hipSuccess ||
+      hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)
+    rc = -12;
+  if (rc == 0) {
+    static HwcAttrPrev hst;
+    hwc_attr_prev_init(hst);
+    hipMemcpy(d_st, &hst, sizeof(hst), hipMemcpyHostToDevice);
+    std::memset(in, 0, sizeof(HwcAttrIn));
+    for (int p = 0; p < kAttrP; ++p) {  // SE-exclusive layout: one owner per partition, 4 tenants
+      in->own_cur[(1 + p % 4) * kAttrP + p] = 1000000;
+      for (int k = 0; k < kNumPmc; ++k) in->se_cur[p * kNumPmc + k] = 1000 + p * 7 + k;
+    }
+    for (int k = 0; k < kNumPmc; ++k) in->slot_se[k] = k < 3;
+    in->se_mode = 1;
+    in->clean_pct = 90;
+    in->prime = 0;
+    gpbs_hip_hwc_attribute(in, d_st, out, s);  // warm
+    hipStreamSynchronize(s);
+    hipEventRecord(e0, s);
+    for (int i = 0; i < iters; ++i) gpbs_hip_hwc_attribute(in, d_st, out, s);
+    hipEventRecord(e1, s);
+    hipEventSynchronize(e1);
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    out2[0] = 1e3 * ms / iters;
+    const int64_t t0 = mono_ns();
+    for (int i = 0; i < iters; ++i) {
+      gpbs_hip_hwc_attribute(in, d_st, out, s);
+      hipEventRecord(e1, s);
+      hipEventSynchronize(e1);
+    }
+    out2[1] = (double)(mono_ns() - t0) / 1e3 / iters;
+    if (hipGetLastError() != hipSuccess) rc = -5;
+  }
+  if (e0) hipEventDestroy(e0);
+  if (e1) hipEventDestroy(e1);
+  if (s) hipStreamDestroy(s);
+  if (in) hipHostFree(in);
+  if (out) hipHostFree(out);
+  if (d_st) hipFree(d_st);
+  return rc;
+}
+
 int gpbs_hip_hwc_attr_selftest(int seed, int iters, double* max_rel) {
   HwcAttrIn* in = nullptr;
   HwcAttrOut* out = nullptr;

@@ -9,10 +9,13 @@
 //                        per tenant, same single-source integer code as the
 //                        host engine (csrc/core/adapt_impl.h), bit-exact.
 //   k_hwc_attribute    : ownership attribution of one live-counter snapshot
-//                        to tenants (csrc/hip/hwc_attr.h): one workgroup, a
-//                        thread per partition for the ownership reductions
-//                        and a thread per tenant for the attribution; the
+//                        to tenants (csrc/hip/hwc_attr.h): one workgroup,
+//                        the snapshot staged into LDS in one pass of wide
+//                        loads, wave reductions / ballots per partition, a
+//                        lane per tenant and a wave per counter slot; the
 //                        previous snapshot stays resident in device memory.
+#include <cstddef>
+
 #include "common.hpp"
 #include "hwc_attr.h"
 #include "../core/adapt_impl.h"
@@ -74,154 +77,203 @@ __global__ __launch_bounds__(64) void k_adapt(gpbs_adapt_state_t* states, const 
 }
 
 
-// One workgroup of 256 threads (4 waves).  Threads p < 32 reduce ownership
-// per partition, threads t < 64 attribute per tenant; every sum runs in the
-// order of hwc_attr_host.  The input is the sampler's snapshot in pinned
-// host memory (read once, ~17 KB); the previous snapshot and the per-
-// partition clean-owner history live in device memory between launches.
+// Full-wave sum (64 lanes, butterfly over cross-lane moves).
+__device__ inline double wave_sum64(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// One workgroup of 256 threads (4 waves); lane = tenant (kMaxTenants == the
+// 64-lane wavefront).  The snapshot lives in pinned host memory, so every
+// read of it is a PCIe round trip: the kernel stages it into LDS ONCE, with
+// all 16-byte loads issued before any is used (the round-3 kernel re-read it
+// inside its per-tenant loops: 78 us per call).  Then
+//   * per-partition owned-time totals: one wave reduction per partition,
+//     8 partitions per wave (the owned ns are integers, so the totals are
+//     exact in any order);
+//   * clean owners: the last tenant over the clean_pct threshold, from a
+//     wave ballot per partition;
+//   * attribution: wave k attributes counter slot k for all 64 tenants at
+//     once, slots 0-2 in parallel, then slot 3 (L2 misses split by slot 2's
+//     L2-request shares) -- each lane sums its partitions in the host order.
+// The previous snapshot and the clean-owner history stay in device memory.
 __global__ __launch_bounds__(256) void k_hwc_attribute(const HwcAttrIn* __restrict__ in, HwcAttrPrev* __restrict__ st,
                                                        HwcAttrOut* __restrict__ out) {
   __builtin_amdgcn_s_setprio(3);
-  constexpr int P = kAttrP, T = kMaxTenants;
-  __shared__ double own_d[T * P];  // 16 KiB
+  constexpr int P = kAttrP, T = kMaxTenants, X = kXcds, K = kNumPmc, E = kCtx;
+  static_assert(T == 64 && X * E == P && P * T == 8 * 256, "one wave of tenants, 8 owned-time words per thread");
+  static_assert(offsetof(HwcAttrIn, x_cur) == offsetof(HwcAttrIn, se_cur) + sizeof(u64) * P * K &&
+                    offsetof(HwcAttrPrev, x) == offsetof(HwcAttrPrev, se) + sizeof(u64) * P * K,
+                "se and x counters adjacent: one 160-word array");
+  static_assert(offsetof(HwcAttrIn, own_cur) % 16 == 0 && offsetof(HwcAttrPrev, own) % 16 == 0, "16-byte loads");
+  constexpr int NC = (P + X) * K / 2;  // 16-byte counter loads (80)
+  __shared__ double ownT[P][T + 1];    // owned ns of the interval, [partition][tenant], padded
+  __shared__ double vse[P][K], vx[X][K];
   __shared__ double tot_p[P];
-  __shared__ double refs_x[T][kXcds], refs_cx[T][kXcds];
-  __shared__ int clean_owner[P], xcd_owner[kXcds];
-  __shared__ double span_s;
-  __shared__ double hw_sum[kNumPmc], unatt[kNumPmc];
-  const int tid = threadIdx.x;
+  __shared__ double refs_x[X][T], refs_cx[X][T];
+  __shared__ int clean_owner[P], xcd_owner[X];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const u32 prime = in->prime;
+  // 1. stage: every load of the snapshot and of the previous state in flight at once
+  const longlong2* oc = reinterpret_cast<const longlong2*>(in->own_cur);
+  longlong2* op = reinterpret_cast<longlong2*>(st->own);
+  const ulonglong2* cc = reinterpret_cast<const ulonglong2*>(in->se_cur);
+  ulonglong2* cp = reinterpret_cast<ulonglong2*>(st->se);
+  longlong2 c[4], q[4];
+  ulonglong2 cv{}, qv{};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) c[j] = oc[j * 256 + tid];
+  if (tid < NC) cv = cc[tid];
+  const u32 se_mode = in->se_mode, clean_pct = in->clean_pct, shared = in->shared;
+  u32 slot_se[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) slot_se[k] = in->slot_se[k];
   if (!prime) {
-    for (int i = tid; i < T * P; i += 256) {
-      const long long d = in->own_cur[i] - st->own[i];
-      own_d[i] = d > 0 ? (double)d : 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) q[j] = op[j * 256 + tid];
+    if (tid < NC) qv = cp[tid];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = (j * 256 + tid) * 2, t = i / P, p = i % P;
+      const long long d0 = c[j].x - q[j].x, d1 = c[j].y - q[j].y;
+      ownT[p][t] = d0 > 0 ? (double)d0 : 0.0;
+      ownT[p + 1][t] = d1 > 0 ? (double)d1 : 0.0;
     }
-    for (int i = tid; i < T * kXcds; i += 256) {
+    if (tid < NC) {
+      const int i = tid * 2;
+      double* dst = i < P * K ? &vse[0][0] + i : &vx[0][0] + (i - P * K);
+      dst[0] = (double)attr_dpos(cv.x, qv.x);
+      dst[1] = (double)attr_dpos(cv.y, qv.y);
+    }
+#pragma unroll
+    for (int i = tid; i < X * T; i += 256) {
       (&refs_x[0][0])[i] = 0.0;
       (&refs_cx[0][0])[i] = 0.0;
     }
-    if (tid < kNumPmc) hw_sum[tid] = unatt[tid] = 0.0;
+  }
+  // the new previous snapshot (each thread overwrites only what it read)
+#pragma unroll
+  for (int j = 0; j < 4; ++j) op[j * 256 + tid] = c[j];
+  if (tid < NC) cp[tid] = cv;
+  if (prime) {
+    if (tid == 0) out->valid = 0u;
+    return;
   }
   __syncthreads();
-  if (!prime) {
-    if (tid < P) {
-      double tot = 0;
-      for (int t = 0; t < T; ++t) tot += own_d[t * P + tid];
-      tot_p[tid] = tot;
+  // 2. owned-time totals per partition
+#pragma unroll
+  for (int i = 0; i < P / 4; ++i) {
+    const int p = wave * (P / 4) + i;
+    const double s = wave_sum64(ownT[p][lane]);
+    if (lane == 0) tot_p[p] = s;
+  }
+  __syncthreads();
+  // 3. clean owners: >= clean_pct of the interval's span, and the same owner as the previous interval
+  double span = 0;
+#pragma unroll
+  for (int p = 0; p < P; ++p) span = span > tot_p[p] ? span : tot_p[p];
+#pragma unroll
+  for (int i = 0; i < P / 4; ++i) {
+    const int p = wave * (P / 4) + i;
+    const bool over = span > 0 && !shared && ownT[p][lane] * 100.0 >= span * clean_pct;
+    const unsigned long long m = __ballot(over);
+    if (lane == 0) {
+      const int raw = m ? 63 - __builtin_clzll(m) : -1;  // the host keeps the last tenant over the bar
+      clean_owner[p] = (raw >= 0 && st->prev_raw[p] == raw) ? raw : -1;
+      st->prev_raw[p] = raw;
     }
-    __syncthreads();
-    if (tid == 0) {
-      double span = 0;
-      for (int p = 0; p < P; ++p) span = span > tot_p[p] ? span : tot_p[p];
-      span_s = span;
+  }
+  __syncthreads();
+  if (tid < X) {
+    int o = -1;
+    bool ok = true;
+    for (int e = 0; e < E && ok; ++e) {
+      const int p = tid * E + e;
+      if (tot_p[p] <= 0) continue;
+      ok = clean_owner[p] >= 0 && (o < 0 || o == clean_owner[p]);
+      o = clean_owner[p];
     }
-    __syncthreads();
-    if (tid < P) {
-      const double span = span_s;
-      int raw = -1;
-      if (span > 0 && !in->shared)
-        for (int t = 0; t < T; ++t)
-          if (own_d[t * P + tid] * 100.0 >= span * in->clean_pct) raw = t;
-      clean_owner[tid] = (raw >= 0 && st->prev_raw[tid] == raw) ? raw : -1;
-      st->prev_raw[tid] = raw;
-    }
-    __syncthreads();
-    if (tid < kXcds) {
-      int o = -1;
-      bool ok = true;
-      for (int e = 0; e < kCtx && ok; ++e) {
-        const int p = tid * kCtx + e;
-        if (tot_p[p] <= 0) continue;
-        ok = clean_owner[p] >= 0 && (o < 0 || o == clean_owner[p]);
-        o = clean_owner[p];
-      }
-      xcd_owner[tid] = ok ? o : -1;
-    }
-    __syncthreads();
-    const u32 se_mode = in->se_mode;
-    double add[kNumPmc] = {0, 0, 0, 0}, addc[kNumPmc] = {0, 0, 0, 0};
-    for (int k = 0; k < kNumPmc; ++k) {
-      const bool miss_by_refs = k == 3;
-      if (se_mode && in->slot_se[k]) {
-        if (tid == 0)  // interval totals (order of the host loop)
-          for (int p = 0; p < P; ++p) {
-            const double v = (double)attr_dpos(in->se_cur[p * kNumPmc + k], st->se[p * kNumPmc + k]);
-            hw_sum[k] += v;
-            if (tot_p[p] <= 0) unatt[k] += v;
-          }
-        if (tid < T) {
-          const int t = tid;
-          for (int x = 0; x < kXcds; ++x)
-            for (int e = 0; e < kCtx; ++e) {
-              const int p = x * kCtx + e;
-              const double tot = tot_p[p];
-              const double w = own_d[t * P + p];
-              if (tot <= 0 || w <= 0) continue;
-              const double v = (double)attr_dpos(in->se_cur[p * kNumPmc + k], st->se[p * kNumPmc + k]);
-              const double a = v * w / tot;
-              add[k] += a;
-              if (k == 2) refs_x[t][x] += a;
-              if (clean_owner[p] == t) {
-                addc[k] += a;
-                if (k == 2) refs_cx[t][x] += a;
-              }
+    xcd_owner[tid] = ok ? o : -1;
+  }
+  __syncthreads();
+  // 4. attribution, lane = tenant: slots 0-2 on waves 0-2, then slot 3 (it reads slot 2's L2 requests)
+  const int t = lane;
+  for (int phase = 0; phase < 2; ++phase) {
+    const int k = phase == 0 ? wave : 3;
+    if ((phase == 0 && wave < 3) || (phase == 1 && wave == 3)) {
+      double add = 0, addc = 0, hs = 0, ua = 0;
+      if (se_mode && slot_se[k]) {
+        for (int x = 0; x < X; ++x) {
+          double rx = 0, rcx = 0;
+          for (int e = 0; e < E; ++e) {
+            const int p = x * E + e;
+            const double v = vse[p][k], tot = tot_p[p];
+            hs += v;
+            if (tot <= 0) {
+              ua += v;
+              continue;
             }
+            const double w = ownT[p][t];
+            if (w <= 0) continue;
+            const double a = v * w / tot;
+            add += a;
+            rx += a;
+            if (clean_owner[p] == t) {
+              addc += a;
+              rcx += a;
+            }
+          }
+          if (k == 2) {
+            refs_x[x][t] += rx;
+            refs_cx[x][t] += rcx;
+          }
         }
-        __syncthreads();
-        continue;
-      }
-      // per-XCD slot: weights need every tenant's row (written above, synced)
-      if (tid < T) {
-        const int t = tid;
-        for (int x = 0; x < kXcds; ++x) {
-          const double v = (double)attr_dpos(in->x_cur[x * kNumPmc + k], st->x[x * kNumPmc + k]);
+      } else {
+        const bool miss_by_refs = k == 3;
+        const bool refs_clean = miss_by_refs && se_mode && slot_se[2];
+        for (int x = 0; x < X; ++x) {
+          const double v = vx[x][k];
           double tot = 0, wt = 0;
           bool by_refs = false;
           if (miss_by_refs) {
-            for (int u = 0; u < T; ++u) tot += refs_x[u][x];
+            wt = refs_x[x][t];
+            tot = wave_sum64(wt);
             by_refs = tot > 0;
-            wt = refs_x[t][x];
           }
           if (!by_refs) {
             tot = 0;
-            for (int u = 0; u < T; ++u) {
-              double s = 0;
-              for (int e = 0; e < kCtx; ++e) s += own_d[u * P + x * kCtx + e];
-              tot += s;
-              if (u == t) wt = s;
+            wt = 0;
+            for (int e = 0; e < E; ++e) {
+              tot += tot_p[x * E + e];
+              wt += ownT[x * E + e][t];
             }
           }
-          if (t == 0) {
-            hw_sum[k] += v;
-            if (tot <= 0) unatt[k] += v;
+          hs += v;
+          if (tot <= 0) {
+            ua += v;
+            continue;
           }
-          if (tot <= 0 || wt <= 0) continue;
+          if (wt <= 0) continue;
           const double a = v * wt / tot;
-          add[k] += a;
-          if (k == 2) refs_x[t][x] += a;  // own row only: read by others at k == 3, after the sync below
-          if (miss_by_refs && se_mode && in->slot_se[2])
-            addc[k] += v * refs_cx[t][x] / tot;
+          add += a;
+          if (k == 2) refs_x[x][t] += a;
+          if (refs_clean)
+            addc += v * refs_cx[x][t] / tot;
           else if (xcd_owner[x] == t)
-            addc[k] += a;
+            addc += a;
         }
       }
-      __syncthreads();
-    }
-    if (tid < T)
-      for (int k = 0; k < kNumPmc; ++k) {
-        out->add[tid][k] = add[k];
-        out->addc[tid][k] = addc[k];
+      out->add[t][k] = add;
+      out->addc[t][k] = addc;
+      if (lane == 0) {
+        out->hw_sum[k] = hs;
+        out->unatt[k] = ua;
       }
-    if (tid < kNumPmc) {
-      out->hw_sum[tid] = hw_sum[tid];
-      out->unatt[tid] = unatt[tid];
     }
+    __syncthreads();
   }
-  __syncthreads();  // every read of the previous snapshot is done
-  for (int i = tid; i < P * kNumPmc; i += 256) st->se[i] = in->se_cur[i];
-  for (int i = tid; i < kXcds * kNumPmc; i += 256) st->x[i] = in->x_cur[i];
-  for (int i = tid; i < T * P; i += 256) st->own[i] = in->own_cur[i];
-  if (tid == 0) out->valid = prime ? 0u : 1u;
+  if (tid == 0) out->valid = 1u;
 }
 
 }  // namespace gpbs_hip

@@ -115,8 +115,12 @@ typedef struct gpbs_counter_ops {
    * period's PBS update of n tenants (0, or < 0 when it cannot start now --
    * the tick then adapts on the host); adapt_harvest returns the previous
    * launch's results once complete (count, tenants_out / states_out) or -11
-   * while it still runs.  The engine applies results one metric period late
-   * and recomputes a late period on the host (bit-identical). */
+   * while it still runs.  tenants_out is in/out: on entry it holds the
+   * caller's launched tenant ids (max of them), and only a launch of exactly
+   * those tenants is harvested -- several pools may share one backend, each
+   * harvests its own launch (-22 if there is none).  The engine applies
+   * results one metric period late and recomputes a late period on the host
+   * (bit-identical). */
   int (*adapt_launch)(void* user, int n, const int* tenants, const uint64_t* deltas, const uint64_t* spin_sum,
                       const uint64_t* spin_cnt, const gpbs_adapt_state_t* states, const gpbs_adapt_params_t* p);
   int (*adapt_harvest)(void* user, int max, int* tenants_out, gpbs_adapt_state_t* states_out);

@@ -345,6 +345,8 @@ class Corun:
                  coll_on_cpu: bool = False):
         self.cfg, self.rank, self.world, self.device = cfg, rank, world, device
         self.coll_on_cpu = coll_on_cpu
+        # what this rank's multi-GPU path actually did (bench JSON "ranks")
+        self.diag: Dict[str, object] = {"coll": "local" if world == 1 else None, "ipc_selftest": None}
         self.groups = groups or {}
         self.gang = None
         self._gang_seq = 0
@@ -374,6 +376,9 @@ class Corun:
         self._dyn_state: Dict[str, int] = {}
         self.solo_lat_ms = 0.0
         self.active_engine: Optional[Engine] = None
+        # per-run GPU clock / power / throttle record (pbs_amd/utils/gpustate.py),
+        # set by the caller; None: not recorded
+        self.gpustate = None
 
     def _make_runner(self, name: str):
         cfg, t = self.cfg, self.tid[name]
@@ -393,9 +398,13 @@ class Corun:
             if self.world > 1 and cfg.coll_impl == "ipc" and not self.coll_on_cpu:
                 r = self._ipc_runner(t, mem_chunk)
                 if r is not None:
+                    self.diag.update(coll="ipc", ipc_selftest="ok")
                     return r
+                self.diag.update(coll="rccl-fallback", ipc_selftest="failed")
                 self.log("[corun] IPC all-reduce tenant failed its self-test on this node: using RCCL")
             if self.world > 1:
+                if self.diag["coll"] is None:
+                    self.diag["coll"] = "gloo-cpu" if self.coll_on_cpu else "rccl"
                 return CollTenant(self.ctx, t, cfg.coll_bytes, self.groups.get("coll"), on_cpu=self.coll_on_cpu,
                                   board_name=f"{cfg.gang_shm_base}-arr" if cfg.gang_shm_base else "",
                                   rank=self.rank, world=self.world)
@@ -886,6 +895,7 @@ class Corun:
         self._rs0 = {n: r.stats() for n, r in self.runners.items() if isinstance(r, Runner)}
         self._barrier()
         t0 = time.perf_counter()
+        g0 = time.monotonic()
         d0 = {n: self._work(n) for n in self.throughput}
         per_step = []
         for _ in range(steps):
@@ -903,6 +913,7 @@ class Corun:
                         layout[n].append(ti.budget_ctx)
         d1 = {n: self._work(n) for n in self.throughput}
         wall_ms_local = (time.perf_counter() - t0) * 1e3
+        g1 = time.monotonic()
         self._barrier()
         wall_ms = self._allreduce(wall_ms_local, "max")
         # drain: drop the backlog, let in-flight units finish
@@ -926,6 +937,8 @@ class Corun:
                "tenants": {}}
         if MIXES[cfg.mix].get("dynamic"):
             res["phase_flips"] = flips
+        if self.gpustate is not None:  # the GPU's clock / power / throttle state over the timed window
+            res["gpu_state"] = self.gpustate.window(g0, g1)
         agg, slows = 0.0, []
         for n in self.throughput:
             du, da = d1[n][0] - d0[n][0], d1[n][1] - d0[n][1]

@@ -94,3 +94,22 @@ def restarts() -> int:
     f = _lib().gpbs_hwc_restarts
     f.restype = __import__("ctypes").c_long
     return int(f())
+
+
+def async_stats() -> dict:
+    """GPBS_HWC_ASYNC=1 mode: issued reads, newest complete / last issued
+    sequence, calls that found nothing complete."""
+    a = (C.c_uint64 * 5)()
+    _lib().gpbs_hwc_async_stats(a)
+    return {"async": bool(a[0]), "issued": int(a[1]), "done_seq": int(a[2]), "last_seq": int(a[3]),
+            "incomplete": int(a[4])}
+
+
+def agent() -> dict:
+    """The GPU agent the counting context was started on: chosen by the PCI
+    address of the current HIP device (hwc.cpp gpbs_hwc_start), with its
+    enumeration index and whether LOCAL_RANK named another one."""
+    buf = C.create_string_buffer(32)
+    mm = C.c_int(0)
+    idx = _lib().gpbs_hwc_agent(buf, 32, C.byref(mm))
+    return {"agent_index": int(idx), "bdf": buf.value.decode() or None, "index_mismatch": bool(mm.value)}

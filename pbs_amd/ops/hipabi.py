@@ -60,6 +60,8 @@ def bind(lib):
     _p(lib, "gpbs_gpu_hwc_stats", C.c_int, vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_double))
     _p(lib, "gpbs_hwc_sample_se", C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64))
     _p(lib, "gpbs_hwc_slot_per_se", C.c_int, C.c_int)
+    _p(lib, "gpbs_hwc_async_stats", C.c_int, C.POINTER(C.c_uint64))
+    _p(lib, "gpbs_hwc_agent", C.c_int, C.c_char_p, C.c_int, C.POINTER(C.c_int))
     _p(lib, "gpbs_gpu_hwc_period", C.c_int, vp, C.c_int, C.c_int, C.POINTER(C.c_uint64))
     _p(lib, "gpbs_gpu_hwc_quality", C.c_int, vp, C.POINTER(C.c_uint64), C.POINTER(C.c_double), C.POINTER(C.c_int))
     _p(lib, "gpbs_gpu_hwc_tenant", C.c_int, vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double))
@@ -103,6 +105,7 @@ def bind(lib):
     _p(lib, "gpbs_gpu_hwc_bursts", C.c_int, vp, C.POINTER(u64), C.POINTER(u64))
     _p(lib, "gpbs_gpu_adapt_stats", C.c_int, vp, C.POINTER(u64), C.POINTER(u64), C.POINTER(u64))
     _p(lib, "gpbs_hip_hwc_attr_selftest", C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double))
+    _p(lib, "gpbs_hip_hwc_attr_bench", C.c_int, C.c_int, C.POINTER(C.c_double))
     _p(lib, "gpbs_gpu_ctx_destroy", None, vp)
     _p(lib, "gpbs_gpu_attach", C.c_int, vp, vp, C.c_int, C.c_int)
     _p(lib, "gpbs_gpu_backend_ops", C.c_int, vp, vp, C.POINTER(N.ActuatorOps), C.POINTER(N.CounterOps), C.c_int)

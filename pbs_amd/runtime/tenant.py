@@ -177,6 +177,7 @@ class TenantClient:
         self.queue_probe = int(queue_probe) if queue_probe >= 0 else (3 if self.se_mode else 0)
         self._probers: Dict[Tuple, QueueProber] = {}
         self._probe_key: Optional[Tuple] = None
+        self._last_stream = None  # the stream of the previous slice (cross-queue ordering)
         self._progress = 0
         self._stop = threading.Event()
         self._hb = threading.Thread(target=self._beat, args=(heartbeat_s,), daemon=True, name=f"gpbs-hb-{name}")
@@ -322,11 +323,24 @@ class TenantClient:
         self._probe_key = None
         s = self.stream()
         key = self._probe_key
+        # A slice may land on another queue than the previous one (a layout
+        # change, or the QueueProber rotating same-mask queues): nothing
+        # orders two HIP queues, so the new one first waits for the old one's
+        # work -- a body that does not end synchronised must not have its
+        # kernels overtaken by the next slice's.
+        prev = self._last_stream
+        if prev is not None and s != prev:
+            s.wait_stream(prev)
         t1 = time.perf_counter()
         with torch.cuda.stream(s):
             yield s
         if key is not None:
+            # the prober compares queues by slice time: time the GPU work,
+            # not its launch (the decode / training bodies end synchronised,
+            # so this costs them nothing)
+            s.synchronize()
             self._probers[key].record(1e3 * (time.perf_counter() - t1))
+        self._last_stream = s
         self._progress += 1
         if waited > 0:
             self.report_wait(waited)

@@ -41,8 +41,8 @@ class Backend:
         self.lib = N.load_core()
         self.rng = random.Random(seed)
         self.late_p, self.refuse_p = late_p, refuse_p
-        self.pending = None
-        self.stats = {"launch": 0, "late": 0, "refused": 0}
+        self.pending = {}
+        self.stats = {"launch": 0, "late": 0, "refused": 0, "miss": 0}
         self.ops = N.CounterOps()
         self.ops.tenant_deltas = N.COUNTER_TENANT_DELTAS(self._deltas)
         if async_mode:
@@ -51,7 +51,9 @@ class Backend:
         engine.set_counter_ops(self.ops)
 
     def _deltas(self, user, n, ids, out):
-        row = self.script[min(self.tick, len(self.script) - 1)]
+        # one script row per metric period, however many pools tick in it
+        k = self.e.now() // (PERIOD_US * 1000)
+        row = self.script[min(k, len(self.script) - 1)]
         self.tick += 1
         for k in range(n):
             t = ids[k]
@@ -71,23 +73,23 @@ class Backend:
             C.memmove(C.byref(p), params, C.sizeof(p))
             self.lib.gpbs_adapt_update(C.byref(s), C.byref(p), deltas[4 * k], deltas[4 * k + 3], ssum[k], scnt[k])
             res.append((ids[k], s))
-        self.pending = res
+        self.pending[tuple(ids[k] for k in range(n))] = res  # keyed like the runtime: by the launch's tenants
         self.stats["launch"] += 1
         return 0
 
     def _harvest(self, user, mx, ids_out, states_out):
-        if self.pending is None:
+        key = tuple(ids_out[k] for k in range(mx))  # in: the caller's launched tenants
+        res = self.pending.pop(key, None)
+        if res is None:
+            self.stats["miss"] += 1
             return -22
         if self.rng.random() < self.late_p:
-            self.pending = None
             self.stats["late"] += 1
             return -11
-        for i, (t, s) in enumerate(self.pending[:mx]):
+        for i, (t, s) in enumerate(res[:mx]):
             ids_out[i] = t
             C.memmove(C.byref(states_out[i]), C.byref(s), C.sizeof(s))
-        n = min(len(self.pending), mx)
-        self.pending = None
-        return n
+        return min(len(res), mx)
 
 
 def _run(script, async_mode, **kw):
@@ -130,3 +132,42 @@ def test_async_device_adapt_late_and_refused_periods_stay_exact():
     # every lagged tick equals the host one period earlier or the same tick
     ok = sum(1 for k in range(1, len(dev)) if dev[k] in (host[k - 1], host[k]))
     assert ok == len(dev) - 1
+
+
+def _run_two_pools(script, async_mode):
+    """Two credit pools on one counter backend (one GpuContext serving both):
+    each pool's metric tick launches and harvests its own tenants only."""
+    prof = dict(MI355X_PROFILE, quantum_align_us=0, idle_skip=1, metric_period_us=PERIOD_US)
+    e = Engine(sim_clock=True, partitions=[(0, x) for x in range(8)], **prof)
+    e.tenant_create("Domain-0", nslots=1)
+    p1 = e.pool_create("pool1", "credit")
+    for part in range(4, 8):
+        e.pool_unassign(0, part)
+        e.pool_assign(p1, part)
+    a = [e.tenant_create(f"a{i}", nslots=2) for i in range(2)]
+    b = [e.tenant_create(f"b{i}", nslots=2, pool=p1) for i in range(2)]
+    tids = a + b
+    for t in tids:
+        e.wake(t)
+    be = Backend(e, script, tids, async_mode=async_mode)
+    seq = []
+    for _ in range(len(script)):
+        e.advance(e.now() + PERIOD_US * 1000)
+        seq.append(tuple(e.tenant_info(t).tslice_us for t in tids))
+    return seq, e.perfc(), be.stats
+
+
+def test_async_adapt_two_pools_never_cross_results():
+    """with two PBS pools on one device_adapt context, pool A must
+    never apply pool B's launch.  Each pool's quanta are the host engine's
+    quanta (an unsynchronised tick interleaving may shift a pool by one
+    period, never mix tenants)."""
+    script = _script(240, 4, seed=11)
+    host, _, _ = _run_two_pools(script, False)
+    dev, pcd, st = _run_two_pools(script, True)
+    assert st["launch"] > 200
+    assert pcd["adapt_device"] == st["launch"]
+    assert len(set(host)) > 3
+    for k in range(2, len(dev)):
+        for j in range(4):
+            assert dev[k][j] in (host[k - 1][j], host[k - 2][j], host[k][j]), (k, j)

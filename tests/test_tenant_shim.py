@@ -165,3 +165,59 @@ def test_co_resident_stream_probes_k_unmasked_queues(monkeypatch):
     for ms in (9.0, 9.0, 9.0, 9.0, 2.0, 2.0, 2.0, 2.0, 9.5):
         pr.record(ms)
     assert t.stream(parts) == "q2" and len(made) == 3
+
+
+def test_slice_orders_queue_changes_and_times_gpu_work(monkeypatch):
+    """when consecutive slices land on different queues (the
+    prober rotating same-mask queues, or a layout change) the new queue
+    waits for the old one's work, and a probed slice is timed after its
+    stream synchronises (not at launch)."""
+    import contextlib
+
+    import torch
+
+    from pbs_amd.runtime.tenant import QueueProber, TenantClient
+    log = []
+
+    class FakeStream:
+        def __init__(self, name):
+            self.name = name
+
+        def __eq__(self, o):
+            return isinstance(o, FakeStream) and o.name == self.name
+
+        def __hash__(self):
+            return hash(self.name)
+
+        def wait_stream(self, o):
+            log.append(("wait", self.name, o.name))
+
+        def synchronize(self):
+            log.append(("sync", self.name))
+
+    monkeypatch.setattr(torch.cuda, "stream", lambda s: contextlib.nullcontext())
+    t = object.__new__(TenantClient)
+    t._last_stream, t._progress, t._probe_key = None, 0, None
+    t.busy = lambda: None
+    t.gate = lambda timeout_s=10.0: True
+    t.report_wait = lambda ns: None
+    pr = QueueProber(3, explore=1)
+    t._probers = {("se", 2, 3): pr}
+    qs = [FakeStream(f"q{i}") for i in range(3)]
+
+    def stream(owned=None):
+        t._probe_key = ("se", 2, 3)
+        return qs[pr.current()]
+    t.stream = stream
+    for _ in range(3):
+        with t.slice():
+            log.append(("body", qs[pr.current()].name))
+    # q0 -> q1 -> q2: each new queue waits for the previous one; every probed slice syncs
+    assert ("wait", "q1", "q0") in log and ("wait", "q2", "q1") in log
+    assert [e for e in log if e[0] == "sync"] == [("sync", "q0"), ("sync", "q1"), ("sync", "q2")]
+    assert log.index(("wait", "q1", "q0")) < log.index(("body", "q1"))
+    n_wait = sum(1 for e in log if e[0] == "wait")
+    t.stream = lambda owned=None: qs[2]
+    with t.slice():  # same queue again: no cross-queue wait
+        pass
+    assert sum(1 for e in log if e[0] == "wait") == n_wait
