@@ -83,11 +83,15 @@ def main():
                     help="PBS metric source: live CDNA4 hardware counters (rocprofiler-sdk device counting, "
                          "attributed to tenants by shader-engine ownership; default), or the modeled per-tile "
                          "counters of the tenant kernels (debug cross-check)")
-    ap.add_argument("--mix", default="all", choices=["all", "4mix", "gemm2", "phase", "8mix"],
+    ap.add_argument("--mix", default="all", choices=["all", "4mix", "gemm2", "phase", "8mix", "llm5"],
                     help="all (default): 4mix (headline, BASELINE config #3) + phase (phase-changing mix) + 8mix "
-                         "(config #4's 8 tenants on one GPU); gemm2: config #2 (two 4096^2 GEMM tenants)")
+                         "(config #4's 8 tenants on one GPU); gemm2: config #2 (two 4096^2 GEMM tenants); "
+                         "llm5: config #5 (Llama-3-8B fp8 decode + Llama-1B-shaped bf16 trainer, torch tenants "
+                         "on the shim under gpbsd; not in the default run)")
     ap.add_argument("--reps-extra", type=int, default=5, help="reps of the non-headline mixes")
     args = ap.parse_args()
+    if args.mix == "llm5":  # its own process tree (daemon + torch tenants); nothing here touches HIP first
+        return run_llm5(args)
     if os.environ.get("GPBS_HANG_DUMP_S"):  # diagnostics: every thread's stack when a run stops progressing
         import faulthandler
         faulthandler.dump_traceback_later(float(os.environ["GPBS_HANG_DUMP_S"]), repeat=True)
@@ -244,7 +248,7 @@ def main():
         default = {"4mix": "none,static,static-se,credit-fixed,gpbs-nolane,gpbs-lat,gpbs",
                    "gemm2": "none,static,static-se,credit-fixed,gpbs",
                    "phase": "none,static-se,credit-fixed,gpbs",
-                   "8mix": "none,static-se,credit-fixed-ts,gpbs-split,gpbs"}[mix]
+                   "8mix": "none,static-se,credit-fixed-ts,gpbs-split,atc,gpbs"}[mix]
         spec = args.policies if (args.policies and mix == mixes[0]) else default
         pols = tuple(p for p in spec.split(",") if p)
         reps = args.reps if mix == mixes[0] else args.reps_extra
@@ -318,6 +322,62 @@ def main():
         import torch.distributed as dist
         dist.barrier(group=groups["ctrl"])
         dist.destroy_process_group()
+
+def run_llm5(args):
+    """Config #5 in the bench contract: solo, none,
+    static-se and gpbs (the daemon's demand-driven SE budgets on live
+    counters; shim tenants on CU-masked queues chosen by measurement, the
+    choice remembered across runs), --reps runs each; decode p50 / p99 and
+    both tenants' shares per policy.  One JSON line (the driver contract's
+    fields, config #5)."""
+    import contextlib
+    import tempfile
+
+    from pbs_amd.bench import llm_corun
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        print("bench.py --mix llm5 runs on one GPU", file=sys.stderr)
+        sys.exit(2)
+    secs = max(4.0, args.steps * args.step_ms / 1e3)
+    warm = max(2.0, args.warmup * args.step_ms / 1e3)
+    out = os.path.join(tempfile.mkdtemp(), "llm5.json")
+    os.environ.setdefault("GPBS_QPROBE_CACHE", os.path.join(os.path.dirname(out), "qprobe.json"))
+    pols = args.policies or "solo,none,static-se,gpbs-budget"
+    with contextlib.redirect_stdout(sys.stderr):  # rank 0 prints ONE line: ours
+        llm_corun.main(["--fp8", "--graph", "--seconds", str(secs), "--warmup", str(warm), "--reps", str(args.reps),
+                        "--policies", pols, "--out", out])
+    res = json.load(open(out))
+    summ = res["summary"]
+    g = summ.get("gpbs-budget") or next(iter(summ.values()))
+    pol = {("gpbs" if p == "gpbs-budget" else p): {
+        "aggregate": v["aggregate"], "mean_slowdown_pct": v["mean_slowdown_pct"],
+        "decode_share": v["norm"].get("infer"), "trainer_share": v["norm"].get("train"),
+        "decode_p50_ms": v["infer_p50_ms"], "decode_p99_ms": v["infer_p99_ms"],
+        "runs": [r["aggregate"] for r in v["runs"]]} for p, v in summ.items()}
+    ss = pol.get("static-se")
+    line = {
+        "metric": json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"],
+        "value": g["aggregate"],
+        "unit": "solo-equivalents (decode tokens/s + trainer tokens/s, each over its solo rate)",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": g["infer_p50_ms"], "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "bf16 (decode weights fp8 e4m3fn)",
+        "data": "synthetic tokens, random-init Llama-3-8B / Llama-3.2-1B-shaped weights",
+        "config": {"model": "#5 Llama-3-8B fp8 decode (batch 8) + Llama-1B-shaped bf16 trainer (4 x 2048)",
+                   "global_batch": 8, "seq_len": 2048, "parallelism": "dp1", "mix": "llm5",
+                   "seconds_per_run": secs, "reps": args.reps},
+        "mean_slowdown_pct": g["mean_slowdown_pct"],
+        "policies": pol,
+    }
+    if ss and "gpbs" in pol:
+        line["gpbs_vs_static_se"] = {
+            "delta_aggregate": round(pol["gpbs"]["aggregate"] - ss["aggregate"], 4),
+            "decode_p99_ratio": round(pol["gpbs"]["decode_p99_ms"] / ss["decode_p99_ms"], 3)
+            if ss["decode_p99_ms"] else None}
+    print(json.dumps(line), flush=True)
+    if args.out:
+        with open(args.out, "w") as f:
+            json.dump({"line": line, "raw": res}, f, indent=1)
+
 
 if __name__ == "__main__":
     main()

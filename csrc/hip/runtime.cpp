@@ -295,6 +295,30 @@ struct GpuCtx {
   // flagship 5 % of its aggregate, 5 % duty (4 ms) 0.5 %.
   int hwc_duty_pct = 1;  // GPBS_HWC_DUTY (profiles/r3: 5 % costs 0.01 of 4mix aggregate, 2 % 0.004, 1 % none measurable)
   int hwc_burst_ms = 20;  // GPBS_HWC_BURST_MS: 1 ms hardware sampling after a trigger
+  // Sample budget (round 4): a token bucket over EVERY hardware sample,
+  // bursts included -- the round-3 bursts re-armed back to back in
+  // time-shared regions (every quantum is an owner change: 1539 samples per
+  // 8mix run).  Tokens accrue so that samples take at most hwc_budget_pct %
+  // of the time on average (EWMA sample time), up to hwc_bucket samples
+  // banked; a burst tick without a token is skipped.  0: no budget.
+  int hwc_budget_pct = 2;    // GPBS_HWC_BUDGET
+  int hwc_bucket = 20;       // GPBS_HWC_BUCKET
+  double hwc_tokens = 20;
+  int64_t hwc_tok_ns = 0;
+  uint64_t hwc_denied = 0;   // burst ticks skipped for lack of a token
+  // Owner changes open bursts only with hwc_owner_burst (GPBS_HWC_OWNER_BURST;
+  // phase triggers always do): with the model fallback below a tenant whose
+  // partitions changed owners gets its metric from the modeled counters, so
+  // owner changes no longer need clean hardware windows.
+  int hwc_owner_burst = 0;
+  // Model fallback (GPBS_HWC_MODEL_FALLBACK, default on): a tenant that ran
+  // in an interval but owned no partition in a settled exclusive window --
+  // time-shared, or just re-placed -- reports the interval's MODELED deltas
+  // (its kernels' own per-tile counts) to the PBS metric instead of nothing.
+  int model_fallback = 1;
+  double mod_cur[kMaxTenants][kNumPmc] = {};       // modeled deltas of the newest consumed snapshot
+  double mod_inflight[kMaxTenants][kNumPmc] = {};  // ... of the snapshot whose attribution is in flight
+  uint64_t fallback_periods = 0, clean_periods = 0;
   int hwc_watch = 1;      // GPBS_HWC_WATCH: read the modeled block every tick (the burst trigger)
   int64_t hwc_next_period_ns = 1000000;
   std::atomic<uint64_t> hwc_triggers{0};
@@ -601,7 +625,7 @@ void hwc_loop(GpuCtx* c) {
     watch_primed = true;
     if (sw != last_sw) {
       last_change = t0;
-      trig = true;
+      if (c->hwc_owner_burst) trig = true;
     }
     last_sw = sw;
     if (trig) {
@@ -614,8 +638,20 @@ void hwc_loop(GpuCtx* c) {
     int64_t period = slow ? (int64_t)c->hwc_slow_us * 1000 : tick;
     if (c->hwc_duty_pct > 0) period = std::max(period, (int64_t)(c->hwc_dt_ewma * 100.0 / c->hwc_duty_pct));
     c->hwc_next_period_ns = period;
-    const bool burst = t0 < burst_until;
-    if (burst || t0 - last_hw >= period - tick / 4) {
+    if (c->hwc_budget_pct > 0) {  // refill the sample budget
+      const double dt = c->hwc_dt_ewma > 0 ? c->hwc_dt_ewma : 150000.0;
+      if (c->hwc_tok_ns) c->hwc_tokens += (double)(t0 - c->hwc_tok_ns) * c->hwc_budget_pct / 100.0 / dt;
+      c->hwc_tokens = std::min(c->hwc_tokens, (double)c->hwc_bucket);
+      c->hwc_tok_ns = t0;
+    }
+    const bool due = t0 - last_hw >= period - tick / 4;
+    bool burst = t0 < burst_until && !due;
+    if (burst && c->hwc_budget_pct > 0 && c->hwc_tokens < 1.0) {
+      burst = false;
+      c->hwc_denied++;
+    }
+    if (burst || due) {
+      if (c->hwc_budget_pct > 0) c->hwc_tokens -= 1.0;
       RoctxRange rr("gpbs:hwc_sample");
       const int64_t s0 = mono_ns();
       const int rc = gpbs_hwc_sample_se(reinterpret_cast<uint64_t*>(se.data()), reinterpret_cast<uint64_t*>(xs.data()));
@@ -650,19 +686,25 @@ void hwc_loop(GpuCtx* c) {
 
 
 // Fold one attribution result into the per-tenant totals and the pending
-// metric deltas (snap_mu held).
-void hwc_fold(GpuCtx* c, const HwcAttrOut& o) {
+// metric deltas (snap_mu held).  `mod`: the same interval's modeled deltas
+// (model fallback for tenants without a clean window).
+void hwc_fold(GpuCtx* c, const HwcAttrOut& o, const double (*mod)[kNumPmc]) {
   if (!o.valid) return;
-  for (int t = 0; t < kMaxTenants; ++t)
+  for (int t = 0; t < kMaxTenants; ++t) {
+    const bool clean = c->clean_pct <= 0 || o.addc[t][0] > 0;
+    const bool fallback = !clean && c->model_fallback && mod && o.add[t][0] > 0 && mod[t][0] > 0;
+    if (clean && o.add[t][0] > 0) c->clean_periods++;
+    if (fallback) c->fallback_periods++;
     for (int k = 0; k < kNumPmc; ++k) {
       if (o.add[t][k] > 0) c->att_total[t][k] += o.add[t][k];
-      const double m = c->clean_pct > 0 ? o.addc[t][k] : o.add[t][k];
+      const double m = fallback ? mod[t][k] : (c->clean_pct > 0 ? o.addc[t][k] : o.add[t][k]);
       if (m > 0) {
         c->last_delta[t][k] += (u64)(m + 0.5);
         c->metric_sum[k] += m;
         c->met_total[t][k] += m;
       }
     }
+  }
   for (int k = 0; k < kNumPmc; ++k) {
     c->hw_sum[k] += o.hw_sum[k];
     c->unatt[k] += o.unatt[k];
@@ -683,6 +725,7 @@ void hwc_fill_in(GpuCtx* c, HwcAttrIn& in) {
 
 // Modeled per-tile counters over the same interval (cross-check, host).
 void hwc_model(GpuCtx* c) {
+  std::memset(c->mod_cur, 0, sizeof(c->mod_cur));
   if (!c->hw_primed) return;
   for (int t = 0; t < kMaxTenants; ++t)
     for (int k = 0; k < kNumPmc; ++k) {
@@ -691,6 +734,7 @@ void hwc_model(GpuCtx* c) {
         const size_t i = ((size_t)t * kXcds + x) * kNumPmc + k;
         md += (double)dpos(c->snap_blk[i], c->blk_prev[i]);
       }
+      c->mod_cur[t][k] = md;
       c->mod_total[t][k] += md;
       c->model_sum[k] += md;
     }
@@ -706,7 +750,7 @@ int hwc_consume(GpuCtx* c, bool wait) {
   if (c->dev_attr && c->attr_pending) {
     const hipError_t q = wait ? hipEventSynchronize(c->attr_ev) : hipEventQuery(c->attr_ev);
     if (q == hipSuccess) {
-      hwc_fold(c, *c->h_aout);
+      hwc_fold(c, *c->h_aout, c->mod_inflight);
       c->attr_pending = false;
     } else {
       c->attr_busy_skips++;
@@ -723,9 +767,10 @@ int hwc_consume(GpuCtx* c, bool wait) {
         hipEventRecord(c->attr_ev, c->sched_stream) == hipSuccess) {
       c->attr_pending = true;
       c->attr_launches++;
+      std::memcpy(c->mod_inflight, c->mod_cur, sizeof(c->mod_cur));
       done = true;
       if (wait && hipEventSynchronize(c->attr_ev) == hipSuccess) {
-        hwc_fold(c, *c->h_aout);
+        hwc_fold(c, *c->h_aout, c->mod_inflight);
         c->attr_pending = false;
       }
     }
@@ -735,7 +780,7 @@ int hwc_consume(GpuCtx* c, bool wait) {
     static thread_local HwcAttrOut out;
     hwc_fill_in(c, in);
     hwc_attr_host(in, c->hst, out);
-    hwc_fold(c, out);
+    hwc_fold(c, out, c->mod_cur);
     c->attr_host++;
   }
   c->blk_prev = c->snap_blk;
@@ -1462,6 +1507,11 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
   if (const char* v = std::getenv("GPBS_HWC_SLOW_US")) c->hwc_slow_us = std::max(0, std::atoi(v));
   if (const char* v = std::getenv("GPBS_HWC_DUTY")) c->hwc_duty_pct = std::max(0, std::min(100, std::atoi(v)));
   if (const char* v = std::getenv("GPBS_HWC_BURST_MS")) c->hwc_burst_ms = std::max(0, std::atoi(v));
+  if (const char* v = std::getenv("GPBS_HWC_BUDGET")) c->hwc_budget_pct = std::max(0, std::min(100, std::atoi(v)));
+  if (const char* v = std::getenv("GPBS_HWC_BUCKET")) c->hwc_bucket = std::max(1, std::atoi(v));
+  c->hwc_tokens = c->hwc_bucket;
+  if (const char* v = std::getenv("GPBS_HWC_OWNER_BURST")) c->hwc_owner_burst = std::atoi(v) != 0;
+  if (const char* v = std::getenv("GPBS_HWC_MODEL_FALLBACK")) c->model_fallback = std::atoi(v) != 0;
   if (const char* v = std::getenv("GPBS_HWC_WATCH")) c->hwc_watch = std::atoi(v) != 0;
   if (const char* v = std::getenv("GPBS_SHARE_PROBE")) {
     c->probe_every = std::max(0, std::atoi(v));
@@ -1769,7 +1819,7 @@ int gpbs_gpu_set_hwc_device(void* p, int on) {
   if (on >= 0 && on != old) {
     if (c->attr_pending) {
       hipEventSynchronize(c->attr_ev);
-      hwc_fold(c, *c->h_aout);
+      hwc_fold(c, *c->h_aout, c->mod_inflight);
       c->attr_pending = false;
     }
     c->dev_attr = on ? 1 : 0;
@@ -1927,6 +1977,24 @@ int gpbs_gpu_hwc_reset(void* p) {
   c->hwc_period_sum_ns = 0;
   c->hwc_burst_samples = 0;
   c->hwc_triggers = 0;
+  c->hwc_denied = 0;
+  c->fallback_periods = c->clean_periods = 0;
+  return 0;
+}
+
+// Sample budget and model-fallback statistics: out[0] budget %, [1] burst
+// ticks denied a token, [2] tenant-periods that reported modeled deltas
+// (no clean window), [3] tenant-periods with a clean hardware window,
+// [4] owner-change bursts on (0/1).
+int gpbs_gpu_hwc_budget_stats(void* p, uint64_t* out5) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c || !out5) return -22;
+  std::lock_guard<std::mutex> g(c->snap_mu);
+  out5[0] = (uint64_t)c->hwc_budget_pct;
+  out5[1] = c->hwc_denied;
+  out5[2] = c->fallback_periods;
+  out5[3] = c->clean_periods;
+  out5[4] = (uint64_t)c->hwc_owner_burst;
   return 0;
 }
 

@@ -196,6 +196,10 @@ POLICY_ENGINES = {
     "gpbs-ts": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
     "credit-fixed-ts": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="credit-fixed"), True,
                         "device,se,waveprio,latco,budget,latmem"),
+    # the ATC policy (X:xen/common/sched_credit_atc.c:291-543): one global
+    # quantum for the pool, driven by the tenants' wait reports (K10); the
+    # same time-shared budget layout as the flagship
+    "atc": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="atc"), True, "device,se,waveprio,latco,budget,latmem"),
     # the same without the latency lane (GEMV co-resident on every CU)
     "gpbs-nolane": (4, dict(BUDGET_OVERRIDES), True, "device,se,waveprio,latco,budget"),
     # round-2 flagship: fixed class halves, memory tenants one SE each by

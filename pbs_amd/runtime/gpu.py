@@ -161,7 +161,11 @@ class GpuContext:
         duty = self.L.gpbs_gpu_hwc_duty(self.h, -1, C.byref(mp))
         tr, bsm = C.c_uint64(0), C.c_uint64(0)
         self.L.gpbs_gpu_hwc_bursts(self.h, C.byref(tr), C.byref(bsm))
-        return {"attr_device": bool(dev), "attr_kernel_launches": la.value, "attr_busy_skips": bs.value,
+        bud = (C.c_uint64 * 5)()
+        self.L.gpbs_gpu_hwc_budget_stats(self.h, bud)
+        return {"budget_pct": bud[0], "burst_denied": bud[1], "model_fallback_periods": bud[2],
+                "clean_periods": bud[3], "owner_bursts": bool(bud[4]),
+                "attr_device": bool(dev), "attr_kernel_launches": la.value, "attr_busy_skips": bs.value,
                 "attr_host": ho.value, "duty_cap_pct": duty, "mean_period_us": round(mp.value / 1e3, 1),
                 "burst_triggers": tr.value, "burst_samples": bsm.value,
                 "samples": n.value, "slow_samples": slow.value, "mean_sample_us": round(ns.value / 1e3, 1), "max_sample_us": round(mx.value / 1e3, 1),

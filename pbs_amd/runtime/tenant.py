@@ -91,7 +91,7 @@ class QueueProber:
     nothing.  Pure bookkeeping (CPU-testable); the caller times the slices."""
 
     def __init__(self, k: int, explore: int = 4, keep: int = 3, drift: float = 1.6, cooldown: int = 100,
-                 abort: float = 2.0):
+                 abort: float = 2.0, start: Optional[int] = None, ref_ms: float = 0.0, probation: int = 3):
         self.k, self.explore, self.keep, self.drift = int(k), int(explore), int(keep), float(drift)
         self.abort = float(abort)
         self.cooldown0 = self.cooldown = int(cooldown)
@@ -103,6 +103,16 @@ class QueueProber:
         self.since = 0
         self.explorations = 0
         self.choices: List[int] = []
+        # Remembered winner (a previous run's choice for this tenant and
+        # mask): exploit it at once; if its first
+        # `probation` slices run slower than drift x the remembered time,
+        # explore after all.  Exploring costs one slow slice per stalled queue.
+        self.probation = 0
+        if start is not None and 0 <= int(start) < self.k and ref_ms > 0:
+            self.idx, self.exploring = int(start), False
+            self.ref = self.ewma = float(ref_ms)
+            self.probation = int(probation)
+            self._prob: List[float] = []
 
     def current(self) -> int:
         return self.idx
@@ -137,11 +147,66 @@ class QueueProber:
             self.choices.append(best)
             self.explorations += 1
             return
+        if self.probation > 0:
+            self._prob.append(ms)
+            if len(self._prob) < self.probation:
+                return
+            self.probation = 0
+            if self._median(self._prob) > self.drift * self.ref:  # the remembered queue is not fast here
+                self.samples = [[] for _ in range(self.k)]
+                self.idx, self.exploring = 0, True
+                return
+            self.choices.append(self.idx)
+            return
         self.since += 1
         self.ewma = 0.8 * self.ewma + 0.2 * ms
         if self.since >= self.cooldown and self.ewma > self.drift * self.ref:
             self.samples = [[] for _ in range(self.k)]
             self.idx, self.exploring = 0, True
+
+    def state(self) -> Optional[Dict[str, float]]:
+        """The current choice, worth remembering once settled (None while exploring)."""
+        if self.exploring or self.probation > 0 or self.ref <= 0:
+            return None
+        return {"idx": self.idx, "ref_ms": round(self.ref, 4)}
+
+
+def _qprobe_cache_path() -> str:
+    return os.environ.get("GPBS_QPROBE_CACHE") or os.path.join(
+        os.environ.get("TMPDIR", "/tmp"), f"gpbs-qprobe-{os.getuid()}.json")
+
+
+def qprobe_load(key: str) -> Optional[Dict[str, float]]:
+    """A remembered QueueProber choice for `key` ("tenant:mask"), or None."""
+    import json
+    try:
+        with open(_qprobe_cache_path()) as f:
+            v = json.load(f).get(key)
+        return v if isinstance(v, dict) and "idx" in v and "ref_ms" in v else None
+    except (OSError, ValueError):
+        return None
+
+
+def qprobe_store(key: str, st: Dict[str, float]):
+    """Remember a settled choice (atomic replace; concurrent tenants keep each other's keys)."""
+    import fcntl
+    import json
+    path = _qprobe_cache_path()
+    try:
+        with open(path + ".lock", "w") as lk:
+            fcntl.flock(lk, fcntl.LOCK_EX)
+            try:
+                with open(path) as f:
+                    d = json.load(f)
+            except (OSError, ValueError):
+                d = {}
+            d[key] = st
+            tmp = f"{path}.{os.getpid()}"
+            with open(tmp, "w") as f:
+                json.dump(d, f)
+            os.replace(tmp, path)
+    except OSError:
+        pass
 
 
 class TenantClient:
@@ -272,7 +337,9 @@ class TenantClient:
             if self.queue_probe > 1:
                 pr = self._probers.get(ses)
                 if pr is None:
-                    pr = self._probers[ses] = QueueProber(self.queue_probe)
+                    mem = qprobe_load(f"{self.name}:se{ses[0]}{ses[1]}:{self.queue_probe}")
+                    pr = self._probers[ses] = QueueProber(self.queue_probe, start=mem and mem["idx"],
+                                                          ref_ms=mem["ref_ms"] if mem else 0.0)
                     for i in range(self.queue_probe):  # all K at once: the set the prober chooses from
                         self._streams[("se",) + ses + (i,)] = torch.cuda.ExternalStream(
                             K.cumask_stream(se_cu_words(ses), device=self.gpu))
@@ -339,7 +406,13 @@ class TenantClient:
             # not its launch (the decode / training bodies end synchronised,
             # so this costs them nothing)
             s.synchronize()
-            self._probers[key].record(1e3 * (time.perf_counter() - t1))
+            pr = self._probers[key]
+            n_choices = len(pr.choices)
+            pr.record(1e3 * (time.perf_counter() - t1))
+            if len(pr.choices) != n_choices and len(key) == 2 and isinstance(key[0], int):
+                st = pr.state()  # a (re)settled SE-mode choice: remember it for the next run
+                if st is not None:
+                    qprobe_store(f"{self.name}:se{key[0]}{key[1]}:{self.queue_probe}", st)
         self._last_stream = s
         self._progress += 1
         if waited > 0:

@@ -221,3 +221,32 @@ def test_slice_orders_queue_changes_and_times_gpu_work(monkeypatch):
     with t.slice():  # same queue again: no cross-queue wait
         pass
     assert sum(1 for e in log if e[0] == "wait") == n_wait
+
+
+def test_queue_prober_remembered_winner_skips_exploration(tmp_path, monkeypatch):
+    """VERDICT r3 item 6: a settled choice is remembered per tenant and mask;
+    the next run exploits it at once (no slow exploration slices) and
+    explores only if its first slices drift above 1.6x the remembered time."""
+    from pbs_amd.runtime.tenant import QueueProber, qprobe_load, qprobe_store
+    monkeypatch.setenv("GPBS_QPROBE_CACHE", str(tmp_path / "qp.json"))
+    assert qprobe_load("infer:se23:3") is None
+    qprobe_store("infer:se23:3", {"idx": 2, "ref_ms": 5.0})
+    qprobe_store("train:se01:3", {"idx": 0, "ref_ms": 190.0})
+    mem = qprobe_load("infer:se23:3")
+    assert mem == {"idx": 2, "ref_ms": 5.0} and qprobe_load("train:se01:3")["idx"] == 0
+    # remembered queue still fast: never explores
+    p = QueueProber(3, start=mem["idx"], ref_ms=mem["ref_ms"])
+    seen = []
+    for _ in range(20):
+        seen.append(p.current())
+        p.record(5.2)
+    assert seen == [2] * 20 and p.explorations == 0 and p.state() == {"idx": 2, "ref_ms": 5.0}
+    # remembered queue now stalled (another mapping this run): explore after the probation
+    speed = {0: 5.1, 1: 17.0, 2: 16.5}
+    p = QueueProber(3, explore=2, start=2, ref_ms=5.0)
+    seen = []
+    for _ in range(12):
+        seen.append(p.current())
+        p.record(speed[p.current()])
+    assert seen[:3] == [2, 2, 2] and p.explorations == 1 and p.current() == 0
+    assert p.state()["idx"] == 0
