@@ -280,17 +280,17 @@ void split(const char* s, std::vector<std::string>& out) {
 extern "C" {
 
 // spec: four '|'-separated groups of '+'-joined counter names, one per PBS
-// slot; NULL = kDefaultSpec (the PBS event set on gfx950, one pass: 7 SQ,
-// 2 TCP and 1 TCC counters, within the 8/4/4 per-block limits):
-//   INST_RETIRED     SQ_INSTS_VALU + SALU + VMEM_RD + VMEM_WR + LDS wave-instructions
-//                    + SQ_INSTS_VALU_MFMA_MOPS_BF16 (matrix ops / 512)   (per SE)
-//                    -- work-normalised: one 16x16x32 MFMA does the arithmetic of
-//                    ~32 wave-instructions, and counting it once made an LDS-tiled
-//                    GEMM's panel re-reads (L2 misses that hit the Infinity Cache)
-//                    look as miss-dense as an HBM stream's (2.1e4 vs 1.1e5 per 1e5)
-//   CPU_CLK_UNHALTED SQ_BUSY_CYCLES                                   (per SE)
-//   LLC_REFERENCES   TCP_TCC_READ_REQ + TCP_TCC_WRITE_REQ (L1 misses = L2 requests, per SE)
-//   LLC_MISSES       TCC_MISS                                         (per XCD: the L2 is per XCD)
+// slot; NULL = kDefaultSpec, the "lean2" set (6 SQ + 1 TCC counters, one pass):
+//   INST_RETIRED     SQ_INSTS_VALU + SQ_INSTS_SALU + SQ_INSTS_VALU_MFMA_MOPS_BF16  (per SE)
+//                    -- work-normalised: the MFMA term counts matrix ops, so an
+//                    LDS-tiled GEMM's instruction count reflects its arithmetic
+//   CPU_CLK_UNHALTED SQ_BUSY_CYCLES                                          (per SE)
+//   LLC_REFERENCES   SQ_INSTS_VMEM_RD + SQ_INSTS_VMEM_WR (vector memory instructions,
+//                    per SE: the L2-request shares that split the per-XCD misses)
+//   LLC_MISSES       TCC_MISS                                                (per XCD: the L2 is per XCD)
+// A sample's cost grows with the records it returns (one per SE for SQ, one per
+// CU for TCP, one per channel for TCC), which is why the round-2 TCP request
+// counters were replaced by SQ memory instructions (pbs_amd/counters/hwc.py).
 // Must precede HIP runtime initialisation.  Every GPU agent gets a counting
 // context; gpbs_hwc_start starts the one at the PCI address of the current
 // HIP device.  `gpu` >= 0 (LOCAL_RANK) is only a cross-check of the

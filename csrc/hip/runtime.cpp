@@ -1982,13 +1982,28 @@ int gpbs_gpu_hwc_reset(void* p) {
   return 0;
 }
 
+// Sampler policy: budget % (token bucket over every hardware sample, 0: no
+// budget), owner-change bursts (0/1), model fallback (0/1); -1 keeps a
+// setting.  Returns 0.
+int gpbs_gpu_hwc_sampler(void* p, int budget_pct, int owner_burst, int fallback) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c) return -22;
+  std::lock_guard<std::mutex> g(c->snap_mu);
+  if (budget_pct >= 0) c->hwc_budget_pct = std::min(100, budget_pct);
+  if (owner_burst >= 0) c->hwc_owner_burst = owner_burst != 0;
+  if (fallback >= 0) c->model_fallback = fallback != 0;
+  c->hwc_tokens = c->hwc_bucket;
+  return 0;
+}
+
 // Sample budget and model-fallback statistics: out[0] budget %, [1] burst
 // ticks denied a token, [2] tenant-periods that reported modeled deltas
 // (no clean window), [3] tenant-periods with a clean hardware window,
-// [4] owner-change bursts on (0/1).
+// [4] owner-change bursts on (0/1), [5] model fallback on (0/1).
 int gpbs_gpu_hwc_budget_stats(void* p, uint64_t* out5) {
   GpuCtx* c = (GpuCtx*)p;
   if (!c || !out5) return -22;
+  out5[5] = (uint64_t)c->model_fallback;
   std::lock_guard<std::mutex> g(c->snap_mu);
   out5[0] = (uint64_t)c->hwc_budget_pct;
   out5[1] = c->hwc_denied;

@@ -200,6 +200,12 @@ POLICY_ENGINES = {
     # quantum for the pool, driven by the tenants' wait reports (K10); the
     # same time-shared budget layout as the flagship
     "atc": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="atc"), True, "device,se,waveprio,latco,budget,latmem"),
+    # the flagship under other counter-sampler policies (same engine and
+    # layout; SAMPLER below): round-3 sampler (owner-change bursts, no budget,
+    # no model fallback), and modeled counters only (no hardware sample)
+    "gpbs-r3s": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
+    "gpbs-b5": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
+    "gpbs-model": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
     # the same without the latency lane (GEMV co-resident on every CU)
     "gpbs-nolane": (4, dict(BUDGET_OVERRIDES), True, "device,se,waveprio,latco,budget"),
     # round-2 flagship: fixed class halves, memory tenants one SE each by
@@ -227,6 +233,16 @@ POLICY_ENGINES = {
     "gpbs-exit": (2, {}, True, "host"),
     "gpbs1": (1, {"coschedule": 0}, True, "host"),
     "sedf": (4, dict(SE_OVERRIDES, sched="sedf"), True, "device,se,waveprio"),
+}
+
+
+# Counter-sampler policy per scheduler policy (GpuContext.set_hwc_sampler
+# arguments; "model": no hardware samples, the modeled per-tile counters feed
+# the metric).  Policies not listed run the process defaults (env / runtime).
+SAMPLER = {
+    "gpbs-r3s": dict(budget_pct=0, owner_burst=1, fallback=0),
+    "gpbs-b5": dict(budget_pct=5, owner_burst=1, fallback=1),
+    "gpbs-model": "model",
 }
 
 
@@ -380,6 +396,7 @@ class Corun:
         self._dyn_state: Dict[str, int] = {}
         self.solo_lat_ms = 0.0
         self.active_engine: Optional[Engine] = None
+        self._sampler_default = None  # the process's sampler policy (restored after a SAMPLER variant)
         # per-run GPU clock / power / throttle record (pbs_amd/utils/gpustate.py),
         # set by the caller; None: not recorded
         self.gpustate = None
@@ -537,8 +554,14 @@ class Corun:
             # device hot path: counter attribution (k_hwc_attribute) and the
             # PBS update (k_adapt) run on the GPU
             self.ctx.attach(e, nctx=e._gpbs_nctx, device_adapt=True)
-            if self.cfg.hw_counters:
+            smp = SAMPLER.get(policy)
+            if self.cfg.hw_counters and smp != "model":
+                if self._sampler_default is None:
+                    self._sampler_default = self.ctx.hwc_sampler()
+                self.ctx.set_hwc_sampler(**(smp or self._sampler_default))
                 self.ctx.set_hwc(True)
+            elif self.cfg.hw_counters:
+                self.ctx.set_hwc(False)  # modeled counters feed the metric this run
             e.start()
             self.active_engine = e
             for name, r in self.runners.items():
@@ -1030,7 +1053,7 @@ class Corun:
                                       "adapt_rearm", "migrate_queued", "vcpu_wake_runnable", "tickle_idlers_some",
                                       "class_change", "relayout")}
             eng["gpu"] = self.ctx.stats()
-            if self.cfg.hw_counters:
+            if self.cfg.hw_counters and SAMPLER.get(policy) != "model":
                 eng["hwc"] = self.ctx.hwc_stats()
                 eng["hwc"]["share_frac"] = round(self.ctx.share_ns() / (wall_ms * 1e6), 4)
                 # Hardware-derived PBS metrics per tenant over the timed window

@@ -25,7 +25,7 @@ from .. import _native as N
 # counting sample's cost grows with the counter RECORDS it returns (SQ: one per
 # SE, TCP: one per CU, TCC: one per channel) and the memory-path (TCC) ones
 # perturb the tenants most; measured with a backlogged GEMM alone
-# (scripts/hwc_cost.py, profiles/hwc/hwc_cost_r3.jsonl): the round-2 "full"
+# (scripts/hwc_cost.py, profiles/r3/hwc_cost_gemm_r3a.jsonl): the round-2 "full"
 # set (7 SQ + 2 TCP + 1 TCC) costs 3.9 % of the GEMM's throughput at a 1 ms
 # period (324 us per sample), a 2 SQ + 1 TCP + 1 TCC set 0.75 % (188 us).
 LEAN_SPEC = ("SQ_INSTS_VALU+SQ_INSTS_VMEM_RD+SQ_INSTS_VMEM_WR+SQ_INSTS_VALU_MFMA_MOPS_BF16|SQ_BUSY_CYCLES|"
@@ -39,7 +39,7 @@ LEAN2_SPEC = ("SQ_INSTS_VALU+SQ_INSTS_SALU+SQ_INSTS_VALU_MFMA_MOPS_BF16|SQ_BUSY_
               "SQ_INSTS_VMEM_RD+SQ_INSTS_VMEM_WR|TCC_MISS")
 SPECS = {"lean": LEAN_SPEC, "full": FULL_SPEC, "lean2": LEAN2_SPEC}
 # Measured on one MI355X, 4-tenant mix, gpbs vs the same layout without a
-# sampler (profiles/r3/sampler_ab.md): lean at 1 ms -5 %, lean at 4 ms
+# sampler (profiles/r3/cmp_4mix_*.json, README "Sampler cost"): lean at 1 ms -5 %, lean at 4 ms
 # -0.5 %, lean2 at 1 ms -2 % (131 us per sample).  Default: lean2, with the
 # runtime's duty-cycle cap stretching the period to ~20 sample times.
 DEFAULT_SPEC = LEAN2_SPEC

@@ -129,7 +129,7 @@ if mode in ("sync", "async"):
     hwc.stop()
     out["after_stop"] = solo()
 base = out["seg0"]
-last = out.get("after_stop") or segs[-1]
+last = out.get("after_stop") or (segs[-1] if segs else base)
 out["rel_last_seg"] = {k: round(segs[-1][k] / base[k], 4) for k in ("gemm", "stream")} if segs else {}
 out["rel_after_stop"] = {k: round(last[k] / base[k], 4) for k in ("gemm", "stream")}
 g.close(); s.close(); ctx.close(); rec.stop()
@@ -155,14 +155,25 @@ def main():
             env["GPBS_HWC_ASYNC"] = "1"
         code = CHILD % {"root": ROOT, "mode": mode, "segs": segs, "load_s": args.load_s, "solo_s": args.solo_s}
         t0 = time.time()
-        p = subprocess.run([sys.executable, "-u", "-c", code], capture_output=True, text=True, env=env,
-                           timeout=args.timeout)
-        line = [x for x in p.stdout.splitlines() if x.startswith("RESULT ")]
+        # the child's SEG lines stream through (a long variant is never silent)
+        p = subprocess.Popen([sys.executable, "-u", "-c", code], stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                             text=True, env=env)
+        lines = []
+        try:
+            for ln in p.stdout:
+                lines.append(ln)
+                if ln.startswith("SEG "):
+                    print(f"[{v}] {ln.strip()}", flush=True)
+            p.wait(timeout=args.timeout)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+        line = [x for x in lines if x.startswith("RESULT ")]
         rec = {"variant": v, "rc": p.returncode, "wall_s": round(time.time() - t0, 1)}
         if line:
             rec.update(json.loads(line[-1][7:]))
         else:
-            rec["err"] = (p.stdout + p.stderr)[-2500:]
+            rec["err"] = "".join(lines)[-2500:]
         brief = {k: rec.get(k) for k in ("variant", "rc", "wall_s", "rel_last_seg", "rel_after_stop")}
         brief["seg0"] = {k: rec.get("seg0", {}).get(k) for k in ("gemm", "stream")}
         print(json.dumps(brief), flush=True)
