@@ -83,9 +83,10 @@ def main():
                     help="PBS metric source: live CDNA4 hardware counters (rocprofiler-sdk device counting, "
                          "attributed to tenants by shader-engine ownership; default), or the modeled per-tile "
                          "counters of the tenant kernels (debug cross-check)")
-    ap.add_argument("--mix", default="all", choices=["all", "4mix", "gemm2", "phase", "8mix", "llm5"],
+    ap.add_argument("--mix", default="all", choices=["all", "4mix", "gemm2", "phase", "phase-ts", "8mix", "llm5"],
                     help="all (default): 4mix (headline, BASELINE config #3) + phase (phase-changing mix) + 8mix "
                          "(config #4's 8 tenants on one GPU); gemm2: config #2 (two 4096^2 GEMM tenants); "
+                         "phase-ts: the phase mix with a time-shared memory region; "
                          "llm5: config #5 (Llama-3-8B fp8 decode + Llama-1B-shaped bf16 trainer, torch tenants "
                          "on the shim under gpbsd; not in the default run)")
     ap.add_argument("--reps-extra", type=int, default=5, help="reps of the non-headline mixes")
@@ -248,6 +249,7 @@ def main():
         default = {"4mix": "none,static,static-se,credit-fixed,gpbs-nolane,gpbs-lat,gpbs",
                    "gemm2": "none,static,static-se,credit-fixed,gpbs",
                    "phase": "none,static-se,credit-fixed,gpbs",
+                   "phase-ts": "none,static-se,credit-fixed-ts,gpbs",
                    "8mix": "none,static-se,credit-fixed-ts,gpbs-split,atc,gpbs"}[mix]
         spec = args.policies if (args.policies and mix == mixes[0]) else default
         pols = tuple(p for p in spec.split(",") if p)
@@ -261,6 +263,8 @@ def main():
     names = {"4mix": "4-tenant mix (MFMA GEMM + HBM-stream + all-reduce + idle)",
              "gemm2": "2 bf16 4096^2 GEMM tenants",
              "phase": "phase-changing mix (GEMM + GEMM<->stream phase tenant + on/off stream + idle)",
+             "phase-ts": "time-shared phase mix (GEMM + GEMM<->stream phase tenant + on/off stream + stream + "
+                         "reduce + idle)",
              "8mix": "8-tenant mix (3 GEMMs + 3 streams + all-reduce + idle)"}
     line = {
         "metric": base["metric"],

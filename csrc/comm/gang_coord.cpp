@@ -214,16 +214,20 @@ std::vector<int32_t> decide(Coord* c, uint64_t epoch, const int64_t* demand_all)
   return out;
 }
 
+// C11: SUM over ranks of each metric tenant's last-period deltas (node
+// metrics) and of its CUMULATIVE counters (gpbs_tenant_vpmu: the node-wide
+// run totals are exact, whatever the exchange cadence -- summing sampled
+// last periods would count ~1 period in every metric_every epochs).
 bool sync_metrics(Coord* c, int* why) {
   const int nm = c->cfg.nmetric;
-  std::vector<int64_t> vals;
+  std::vector<int64_t> vals(8 * nm, 0);
   for (int i = 0; i < nm; ++i) {
     gpbs_tenant_info_t ti;
-    if (gpbs_tenant_info(c->e, c->cfg.metric_tenants[i], &ti)) {
-      vals.insert(vals.end(), {0, 0, 0, 0});
-    } else {
-      for (int k = 0; k < 4; ++k) vals.push_back((int64_t)ti.pmc[k]);
-    }
+    uint64_t cum[4] = {0, 0, 0, 0};
+    if (!gpbs_tenant_info(c->e, c->cfg.metric_tenants[i], &ti))
+      for (int k = 0; k < 4; ++k) vals[4 * i + k] = (int64_t)ti.pmc[k];
+    if (!gpbs_tenant_vpmu(c->e, c->cfg.metric_tenants[i], cum))
+      for (int k = 0; k < 4; ++k) vals[4 * nm + 4 * i + k] = (int64_t)cum[k];
   }
   std::vector<int64_t> red;
   if (!reduce(c, vals, red, mono_ns() + c->cfg.deadline_ns, why, [](int64_t a, int64_t b) { return a + b; }))
@@ -232,7 +236,7 @@ bool sync_metrics(Coord* c, int* why) {
   for (int i = 0; i < nm; ++i)
     for (int k = 0; k < 4; ++k) {
       c->node[i].v[k] = red[4 * i + k];
-      c->totals[i].v[k] += red[4 * i + k];
+      c->totals[i].v[k] = red[4 * nm + 4 * i + k];
     }
   ++c->metric_syncs;
   return true;
@@ -328,7 +332,7 @@ void* gpbs_gang_coord_start(gpbs_engine_t* e, void* shm, int world, int nvals, c
   if (!e || !shm || !cfg || cfg->ntenants < 0 || cfg->ntenants > GPBS_GANG_MAX_TENANTS || cfg->nmetric < 0 ||
       cfg->nmetric > GPBS_GANG_MAX_TENANTS || world < 1 || world > 64 || cfg->epoch_ns <= 0)
     return nullptr;
-  if (nvals < 2 * cfg->ntenants + 4 || nvals < 4 * cfg->nmetric) return nullptr;
+  if (nvals < 2 * cfg->ntenants + 4 || nvals < 8 * cfg->nmetric) return nullptr;
   auto* c = new Coord;
   c->e = e;
   c->shm = shm;

@@ -101,6 +101,12 @@ MIXES = {
     "gemm2": {"tenants": (("gemm", 8), ("gemm_b", 8)), "throughput": ("gemm", "gemm_b")},
     "phase": {"tenants": (("gemm", 8), ("phase", 8), ("hbm", 8), ("idle", 8)),
               "throughput": ("gemm", "phase", "hbm"), "dynamic": True},
+    # time-shared phase mix: the phase tenant flips into a
+    # memory region that already holds two or three memory tenants (hbm on /
+    # off), so the region is time-shared and PBS's re-arm moves quanta that
+    # rotate real co-sharers
+    "phase-ts": {"tenants": (("gemm", 8), ("phase", 8), ("hbm", 8), ("hbm_b", 8), ("coll", 8), ("idle", 8)),
+                 "throughput": ("gemm", "phase", "hbm", "hbm_b", "coll"), "dynamic": True},
     "8mix": {"tenants": (("gemm", 8), ("gemm_b", 8), ("gemm_s", 8), ("hbm", 8), ("hbm_b", 8), ("hbm_s", 8),
                          ("coll", 8), ("idle", 8)),
              "throughput": ("gemm", "gemm_b", "gemm_s", "hbm", "hbm_b", "hbm_s", "coll")},
@@ -115,6 +121,8 @@ STATIC_SE = {
     "4mix": {"gemm": (_ALLX, (0, 1)), "hbm": (_ALLX, (2,)), "coll": (_ALLX, (3,))},
     "gemm2": {"gemm": (_ALLX, (0, 1)), "gemm_b": (_ALLX, (2, 3))},
     "phase": {"gemm": (_ALLX, (0, 1)), "phase": (_ALLX, (2,)), "hbm": (_ALLX, (3,))},
+    "phase-ts": {"gemm": (_ALLX, (0, 1)), "phase": ((0, 1, 2, 3), (2,)), "hbm": ((4, 5, 6, 7), (2,)),
+                 "hbm_b": ((0, 1, 2, 3), (3,)), "coll": ((4, 5, 6, 7), (3,))},
     "8mix": {"gemm": (_ALLX, (0,)), "gemm_b": (tuple(range(6)), (1,)), "gemm_s": ((6, 7), (1,)),
              "hbm": ((0, 1, 2, 3), (2,)), "hbm_b": ((4, 5, 6, 7), (2,)), "coll": ((0, 1, 2, 3), (3,)),
              "hbm_s": ((4, 5, 6, 7), (3,))},
@@ -200,6 +208,11 @@ POLICY_ENGINES = {
     # quantum for the pool, driven by the tenants' wait reports (K10); the
     # same time-shared budget layout as the flagship
     "atc": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="atc"), True, "device,se,waveprio,latco,budget,latmem"),
+    # switch-cost probes: every quantum (fixed) or the adaptive floor at 4 ms
+    "credit-fixed-ts4": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="credit-fixed", tslice_us=4000), True,
+                         "device,se,waveprio,latco,budget,latmem"),
+    "gpbs-f4": (4, dict(BUDGET_OVERRIDES, class_budget=1, adapt=dict(MI355X_PROFILE["adapt"], min_us=4000)), True,
+                "device,se,waveprio,latco,budget,latmem"),
     # the flagship under other counter-sampler policies (same engine and
     # layout; SAMPLER below): round-3 sampler (owner-change bursts, no budget,
     # no model fallback), and modeled counters only (no hardware sample)

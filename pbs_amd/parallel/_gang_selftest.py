@@ -122,7 +122,8 @@ def metrics_sum_worker(rank: int, world: int, port: int, q, transport: str = "di
     g.stop()
     totals = {t: dict(g.node_totals.get(t, {})) for t in ts}
     q.put({"rank": rank, "local": local, "node": node, "totals": totals, "syncs": g.metric_syncs,
-           "still": {t: list(e.tenant_info(t).pmc) for t in ts}})
+           "still": {t: list(e.tenant_info(t).pmc) for t in ts},
+           "vpmu": {t: list(e.tenant_vpmu(t).values()) for t in ts}})
     dist.destroy_process_group()
 
 

@@ -287,8 +287,8 @@ class GangCoordinator:
         self.metric_tenants = list(metric_tenants or [])
         self.metric_every = max(1, int(metric_every))
         self._node_metrics: Dict[int, Dict[str, int]] = {}
-        # node-wide totals over every metric exchange of the run (the last
-        # period alone reads zero once the tenants have drained)
+        # node-wide cumulative counters (SUM over ranks of gpbs_tenant_vpmu)
+        # at the last metric exchange: exact run totals
         self._node_totals: Dict[int, Dict[str, int]] = {}
         self.metric_syncs = 0
         self.transport = transport
@@ -386,12 +386,12 @@ class GangCoordinator:
                 out = [None] * self.world
                 dist.all_gather_object(out, obj, group=group)
                 return out
-            return _XgmiTransport(self.rank, self.world, max(nvals, 4 * len(self.metric_tenants)),
+            return _XgmiTransport(self.rank, self.world, max(nvals, 8 * len(self.metric_tenants)),
                                   dev.index or 0, gather)
         if self.transport == "shm":
             if not self.shm_name:
                 raise ValueError("transport 'shm' needs shm_name (the same fresh name on every rank)")
-            return _ShmTransport(self.shm_name, self.rank, self.world, max(nvals, 4 * len(self.metric_tenants)))
+            return _ShmTransport(self.shm_name, self.rank, self.world, max(nvals, 8 * len(self.metric_tenants)))
         return _DistTransport(self.group, self.device)
 
     def _timeout(self, waited_ns: int):
@@ -502,14 +502,20 @@ class GangCoordinator:
         return v if v > 0 else NO_ATC
 
     def _sync_metrics(self, tr) -> bool:
-        """SUM-reduce the metric tenants' last-period counter deltas."""
-        vals = []
+        """SUM-reduce the metric tenants' last-period counter deltas (node
+        metrics) and their cumulative counters (exact node-wide run totals)."""
+        vals, cum = [], []
         for t in self.metric_tenants:
             try:
                 vals += [int(x) for x in self.engine.tenant_info(t).pmc]
             except Exception:
                 vals += [0, 0, 0, 0]
-        red = tr.reduce_sum(vals, time.monotonic_ns() + self.deadline_ns)
+            try:
+                v = self.engine.tenant_vpmu(t)
+                cum += [int(v[k]) for k in v]
+            except Exception:
+                cum += [0, 0, 0, 0]
+        red = tr.reduce_sum(vals + cum, time.monotonic_ns() + self.deadline_ns)
         if red is None:
             return False
         out = {}
@@ -518,11 +524,11 @@ class GangCoordinator:
             out[t] = {"inst": inst, "cycles": cyc, "l2_refs": ref, "l2_misses": miss,
                       "miss_rate": miss * 100000 // inst if inst else 0}
         self._node_metrics = out
-        for t, m in out.items():
-            tot = self._node_totals.setdefault(t, {"inst": 0, "cycles": 0, "l2_refs": 0, "l2_misses": 0})
-            for k in tot:
-                tot[k] += m[k]
-            tot["miss_rate"] = tot["l2_misses"] * 100000 // tot["inst"] if tot["inst"] else 0
+        nm = len(self.metric_tenants)
+        for i, t in enumerate(self.metric_tenants):
+            inst, cyc, ref, miss = red[4 * nm + 4 * i:4 * nm + 4 * i + 4]
+            self._node_totals[t] = {"inst": inst, "cycles": cyc, "l2_refs": ref, "l2_misses": miss,
+                                    "miss_rate": miss * 100000 // inst if inst else 0}
         self.metric_syncs += 1
         return True
 
@@ -532,7 +538,7 @@ class GangCoordinator:
         nt, nm = len(self.tenants), len(self.metric_tenants)
         if nt > 32 or nm > 32:
             raise ValueError("native gang coordinator: at most 32 gang / metric tenants")
-        nvals = max(2 * nt + 4, 4 * nm)
+        nvals = max(2 * nt + 4, 8 * nm)
         self._ntr = _ShmTransport(self.shm_name, self.rank, self.world, nvals)
         cfg = N.GangCfg()
         cfg.rank, cfg.ntenants, cfg.nmetric, cfg.metric_every = self.rank, nt, nm, self.metric_every

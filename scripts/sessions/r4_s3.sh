@@ -14,7 +14,7 @@ timeout -k 10 200 python -u scripts/hwc_drift.py --variants async --segs 2 --loa
   --out gpurun_out/r4/s3_async.json > gpurun_out/r4/s3_async.log 2>&1
 echo "async rc=$?"; tail -5 gpurun_out/r4/s3_async.log
 echo "== 8mix sampler policies $(date +%T)"
-timeout -k 10 600 python -u bench.py --gpus 1 --mix 8mix --reps 6 --resolo --steps 20 --warmup 3 \
-  --policies none,credit-fixed-ts,gpbs-model,gpbs-r3s,gpbs-b5,gpbs \
+timeout -k 10 800 python -u bench.py --gpus 1 --mix 8mix --reps 6 --resolo --steps 20 --warmup 3 \
+  --policies none,credit-fixed-ts,credit-fixed-ts4,gpbs-model,gpbs-r3s,gpbs-b5,gpbs-f4,gpbs \
   > gpurun_out/r4/s3_8mix_sampler.json 2> gpurun_out/r4/s3_8mix_sampler.log
 echo "8mix rc=$? $(date +%T)"
