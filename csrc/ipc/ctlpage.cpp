@@ -293,6 +293,12 @@ void br_on_flush(void* user, int64_t now) {
     Page* pg = &c->pages[i];
     const int tid = pg->tenant_id.load(std::memory_order_relaxed);
     if (tid < 0 || tid >= (int)c->pend_mask.size() / 2) continue;
+    // A torn publish of this page still pending (GPBS_FAULT torn_page) lands
+    // first: the fields read below and the equality test must see the page
+    // as it will be, not half-written (the deferred quantum was
+    // otherwise overwritten with the stale value, and a mask equal to the
+    // half-written one skipped its publish).
+    if (c->torn[i].active) complete_torn(pg, c->torn[i]);
     const uint64_t m[2] = {c->pend_mask[2 * tid], c->pend_mask[2 * tid + 1]};
     if (m[0] == pg->mask[0].load(std::memory_order_relaxed) && m[1] == pg->mask[1].load(std::memory_order_relaxed)) continue;
     publish_page(pg, (m[0] | m[1]) ? 1u : 0u, m, pg->quantum_us.load(std::memory_order_relaxed),

@@ -144,9 +144,26 @@ def test_torn_page_fault_is_caught_by_the_seqlock():
                 time.sleep(0.001)
         stop.set()
         th.join()
-        lib.gpbs_ctl_close(C.c_void_p(h), 0)
         assert d.engine.fault_hits()["torn_page"] > 0
         assert seen["reads"] > 0 and seen["retries"] > 0, seen
         assert seen["bad"] == 0, seen
+        # a publish that meets a pending torn one completes it
+        # first, so once the last torn publish lands the page holds exactly
+        # the engine's assignment (no stale mask word, no lost quantum)
+        d.engine.fault_set("")
+        d.advance_us(250)
+        time.sleep(0.05)  # the bridge completes the last deferred half
+        g, q, ep = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        m = (C.c_uint64 * 2)()
+        pr, tid = C.c_int32(), C.c_int32()
+        assert lib.gpbs_ctl_read(C.c_void_p(h), page, C.byref(g), m, C.byref(q), C.byref(pr), C.byref(tid),
+                                 C.byref(ep)) >= 0
+        want = 0
+        for p in range(d.engine.num_partitions):
+            if d.engine.partition_info(p)["curr_tenant"] == regs[0]["tenant"]:
+                want |= 1 << p
+        assert (m[0] | (m[1] << 64)) == want, (hex(m[0]), hex(m[1]), hex(want))
+        assert bool(g.value) == bool(want)
+        lib.gpbs_ctl_close(C.c_void_p(h), 0)
     finally:
         d.stop()
