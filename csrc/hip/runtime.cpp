@@ -38,6 +38,7 @@
 using namespace gpbs_hip;
 
 extern "C" {
+int gpbs_adapt_update(gpbs_adapt_state_t*, const gpbs_adapt_params_t*, uint64_t, uint64_t, uint64_t, uint64_t);
 int gpbs_hip_gemm_units(int, int);
 int gpbs_hwc_sample(uint64_t* out, int nxcd);
 int gpbs_hwc_sample_se(uint64_t* se_out, uint64_t* x_out);
@@ -1835,6 +1836,71 @@ int gpbs_gpu_set_hwc_device(void* p, int on) {
 // on the headline path): out[0] = mean device time per launch over `iters`
 // back-to-back launches (hipEvent), out[1] = mean host round trip of one
 // launch + event wait.  0 on success.
+// Two pools on one GpuContext, device adapt: pool A launches
+// for tenants {1,2}, pool B for {3,4}, interleaved and harvested in both
+// orders; every harvest must return the caller's own tenants with the host
+// adapt_update's states.  Returns 0, or the first failing step (< 0).
+int gpbs_hip_adapt_pools_selftest(int rounds) {
+  void* h = gpbs_gpu_ctx_create(0, 0, 0, 4);
+  if (!h) return -12;
+  GpuCtx* c = (GpuCtx*)h;
+  gpbs_adapt_params_t p{};
+  p.threshold = 2000;
+  p.band_lo = 70;
+  p.band_hi = 130;
+  p.min_us = 1000;
+  p.max_us = 11000;
+  p.inc_us = 1000;
+  p.dec_us = 2000;
+  p.switch_boundary = 9000;
+  p.ticks_per_tslice = 3;
+  gpbs_adapt_state_t sa[2] = {}, sb[2] = {};
+  for (auto* s : {&sa[0], &sa[1], &sb[0], &sb[1]}) {
+    s->tslice_us = 1000;
+    s->tick_period_us = 333;
+    s->window_left = 5;
+  }
+  const int ia[2] = {1, 2}, ib[2] = {3, 4};
+  int rc = 0;
+  for (int r = 0; r < rounds && !rc; ++r) {
+    uint64_t da[8], db[8], z[2] = {0, 0};
+    for (int k = 0; k < 2; ++k) {  // phases that move the quanta: A high-miss, B low-miss, alternating
+      const uint64_t inst = 1000000 + 1000 * r + k;
+      da[4 * k] = db[4 * k] = inst;
+      da[4 * k + 1] = db[4 * k + 1] = 2 * inst;
+      da[4 * k + 2] = db[4 * k + 2] = inst / 10;
+      da[4 * k + 3] = ((r / 7) & 1) ? inst / 1000 : inst / 20;
+      db[4 * k + 3] = ((r / 5) & 1) ? inst / 20 : inst / 1000;
+    }
+    if (ctr_adapt_launch(c, 2, ia, da, z, z, sa, &p) || ctr_adapt_launch(c, 2, ib, db, z, z, sb, &p)) {
+      rc = -1;
+      break;
+    }
+    hipDeviceSynchronize();
+    int ta[2] = {ia[0], ia[1]}, tb[2] = {ib[0], ib[1]};
+    gpbs_adapt_state_t oa[2], ob[2];
+    const bool a_first = r & 1;
+    const int na = a_first ? ctr_adapt_harvest(c, 2, ta, oa) : 0;
+    const int nb = ctr_adapt_harvest(c, 2, tb, ob);
+    const int na2 = a_first ? na : ctr_adapt_harvest(c, 2, ta, oa);
+    if (na2 != 2 || nb != 2 || ta[0] != 1 || ta[1] != 2 || tb[0] != 3 || tb[1] != 4) {
+      rc = -2;
+      break;
+    }
+    for (int k = 0; k < 2 && !rc; ++k) {
+      gpbs_adapt_update(&sa[k], &p, da[4 * k], da[4 * k + 3], 0, 0);
+      gpbs_adapt_update(&sb[k], &p, db[4 * k], db[4 * k + 3], 0, 0);
+      if (std::memcmp(&sa[k], &oa[k], sizeof(sa[k])) || std::memcmp(&sb[k], &ob[k], sizeof(sb[k]))) rc = -3;
+    }
+  }
+  // a harvest for tenants nobody launched finds nothing
+  int tx[2] = {5, 6};
+  gpbs_adapt_state_t ox[2];
+  if (!rc && ctr_adapt_harvest(c, 2, tx, ox) != -22) rc = -4;
+  gpbs_gpu_ctx_destroy(h);
+  return rc;
+}
+
 int gpbs_hip_hwc_attr_bench(int iters, double* out2) {
   if (iters <= 0 || !out2) return -22;
   HwcAttrIn* in = nullptr;

@@ -108,6 +108,7 @@ def bind(lib):
     _p(lib, "gpbs_gpu_adapt_stats", C.c_int, vp, C.POINTER(u64), C.POINTER(u64), C.POINTER(u64))
     _p(lib, "gpbs_hip_hwc_attr_selftest", C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double))
     _p(lib, "gpbs_hip_hwc_attr_bench", C.c_int, C.c_int, C.POINTER(C.c_double))
+    _p(lib, "gpbs_hip_adapt_pools_selftest", C.c_int, C.c_int)
     _p(lib, "gpbs_gpu_ctx_destroy", None, vp)
     _p(lib, "gpbs_gpu_attach", C.c_int, vp, vp, C.c_int, C.c_int)
     _p(lib, "gpbs_gpu_backend_ops", C.c_int, vp, vp, C.POINTER(N.ActuatorOps), C.POINTER(N.CounterOps), C.c_int)

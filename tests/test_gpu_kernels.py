@@ -140,6 +140,14 @@ def test_hwc_attribute_kernel_cost():
     assert out[0] <= 10.0, out[0]
 
 
+def test_async_device_adapt_two_pools_harvest_their_own():
+    """two PBS pools on one GPU context with device adapt.  Each
+    pool's launch is harvested by that pool only (matched by its tenants),
+    in either order, with states bit-identical to the host adapt_update;
+    a harvest for tenants nobody launched finds nothing."""
+    assert K.lib().gpbs_hip_adapt_pools_selftest(60) == 0
+
+
 def test_device_adapt_bit_exact_vs_host():
     """The batched HIP adapt kernel equals the host engine's adapt_update."""
     lib = N.load_core()
