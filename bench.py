@@ -69,8 +69,11 @@ def main():
     ap.add_argument("--coll", default="ipc", choices=["ipc", "rccl"],
                     help="N > 1 all-reduce tenant: ipc (gated gpbs kernel over IPC-mapped peer buffers, xGMI; "
                          "default) or rccl (torch.distributed all-reduce, not CU-confined)")
-    ap.add_argument("--resolo", action="store_true",
-                    help="diagnostic: measure the solo rates again after each mix's runs (reported, not used)")
+    ap.add_argument("--resolo", dest="resolo", action="store_true", default=True,
+                    help="measure the solo rates again after each mix's runs (reported as "
+                         "solo._end_over_start_rate, not used): a GPU that got slower over the runs shows here "
+                         "(default on)")
+    ap.add_argument("--no-resolo", dest="resolo", action="store_false")
     ap.add_argument("--out", default="")
     ap.add_argument("--rehearse-ipc", action="store_true",
                     help="like --rehearse (every rank on GPU 0, gloo) but with the gated IPC all-reduce tenant on "
@@ -230,13 +233,41 @@ def main():
             eng = [r.get("engine") for r in rs if r.get("engine")]
             if eng:
                 pol[p]["adapt_rearm"] = [e.get("adapt_rearm", 0) for e in eng]
+                pol[p]["adapt_inc"] = [e.get("adapt_inc", 0) for e in eng]
+                pol[p]["adapt_dec"] = [e.get("adapt_dec", 0) for e in eng]
                 pol[p]["relayout"] = [e.get("relayout", 0) for e in eng]
+                # the quantum each contention class ran with (class 0 compute, 1 memory)
+                by = {}
+                for e in eng:
+                    for n, ts in (e.get("mean_tslice_us") or {}).items():
+                        c = (e.get("class") or {}).get(n, -1)
+                        if n != "idle" and c >= 0:
+                            by.setdefault(str(c), []).append(ts)
+                pol[p]["mean_tslice_us_by_class"] = {c: round(q(v, 0.5), 1) for c, v in sorted(by.items())}
             if "idle" in rs[0]["tenants"]:
                 pol[p]["idle_p50_ms"] = round(q([r["tenants"]["idle"]["p50_ms"] for r in rs], 0.5), 4)
         out = {"value": round(q([r["aggregate_all_gpus"] for r in runs["gpbs"]], 0.5), 4),
                "mean_slowdown_pct": round(q([r["mean_slowdown_pct"] for r in runs["gpbs"]], 0.5), 2),
                "reps": max(1, reps), "policies": pol, "per_tenant": g["tenants"], "engine": g.get("engine", {}),
-               "ms_per_step": round(g["ms_per_step"], 3), "solo": solo}
+               "ms_per_step": round(g["ms_per_step"], 3), "solo": solo, "drift": out_drift, "gpu_state": out_gs}
+        # drift over the mix's runs (chronological): the last five gpbs runs
+        # against the first five, and the GPU state of the first and last run
+        xs = [r["aggregate_all_gpus"] for r in runs["gpbs"]]
+        if len(xs) >= 6:
+            k = min(5, len(xs) // 2)
+            f, l = xs[:k], xs[-k:]
+            out_drift = {"first_median": round(q(f, 0.5), 4), "last_median": round(q(l, 0.5), 4),
+                         "first_iqr": round(q(f, 0.75) - q(f, 0.25), 4), "n": k}
+            out_drift["last_within_first_iqr"] = abs(out_drift["last_median"] - out_drift["first_median"]) <= \
+                max(out_drift["first_iqr"], 1e-9)
+        else:
+            out_drift = None
+        gs = [r.get("gpu_state") for r in runs["gpbs"] if r.get("gpu_state")]
+        if gs:
+            pick = ("gfxclk_mhz", "power_w", "ppt_frac", "temp_hotspot_c_max")
+            out_gs = {"first_run": {k: gs[0].get(k) for k in pick}, "last_run": {k: gs[-1].get(k) for k in pick}}
+        else:
+            out_gs = None
         if "static-se" in runs:
             a, b = pol["gpbs"]["aggregate_all_gpus"], pol["static-se"]["aggregate_all_gpus"]
             out["gpbs_vs_static_se"] = {"delta_median": round(a["median"] - b["median"], 4),
@@ -298,6 +329,8 @@ def main():
         "policies": hs["policies"],
         "solo": hs["solo"],
         "engine": hs["engine"],
+        "drift": hs["drift"],
+        "gpu_state": hs["gpu_state"],
     }
     if "gpbs_vs_static_se" in hs:
         line["gpbs_vs_static_se"] = hs["gpbs_vs_static_se"]

@@ -366,6 +366,14 @@ class CollTenant:
         self._loop.stop(agree)
 
 
+def kfd_queues(pid: Optional[int] = None) -> Optional[int]:
+    """Hardware queues KFD holds for a process (sysfs; None where not exposed)."""
+    try:
+        return len(os.listdir(f"/sys/class/kfd/kfd/proc/{pid or os.getpid()}/queues"))
+    except OSError:
+        return None
+
+
 def _pct(xs, q):
     if not xs:
         return 0.0
@@ -979,6 +987,9 @@ class Corun:
             res["phase_flips"] = flips
         if self.gpustate is not None:  # the GPU's clock / power / throttle state over the timed window
             res["gpu_state"] = self.gpustate.window(g0, g1)
+        nq = kfd_queues()
+        if nq is not None:  # hardware queues this process holds (KFD): oversubscription shows here
+            res["kfd_queues"] = nq
         agg, slows = 0.0, []
         for n in self.throughput:
             du, da = d1[n][0] - d0[n][0], d1[n][1] - d0[n][1]
