@@ -41,6 +41,74 @@ sys.path.insert(0, ROOT)
 os.environ["GPU_MAX_HW_QUEUES"] = str(max(8, int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)))
 
 
+def q(xs, f):
+    xs = sorted(xs)
+    k = (len(xs) - 1) * f
+    lo, hi = int(k), min(int(k) + 1, len(xs) - 1)
+    return xs[lo] + (xs[hi] - xs[lo]) * (k - lo)
+
+
+
+def summ(rs, key):
+    xs = [r[key] for r in rs]
+    return {"median": round(q(xs, 0.5), 4), "iqr": round(q(xs, 0.75) - q(xs, 0.25), 4),
+            "min": round(min(xs), 4), "max": round(max(xs), 4)}
+
+
+def mix_summary(mix, runs, solo, reps):
+    gr = sorted(runs["gpbs"], key=lambda r: r["aggregate_all_gpus"])
+    g = gr[(len(gr) - 1) // 2]  # headline run = the gpbs run with the median aggregate
+    pol = {p: {"aggregate_all_gpus": summ(rs, "aggregate_all_gpus"),
+               "mean_slowdown_pct": summ(rs, "mean_slowdown_pct"),
+               "ms_per_step": round(q([r["ms_per_step"] for r in rs], 0.5), 3),
+               "runs": [round(r["aggregate_all_gpus"], 4) for r in rs]} for p, rs in runs.items()}
+    for p, rs in runs.items():
+        eng = [r.get("engine") for r in rs if r.get("engine")]
+        if eng:
+            pol[p]["adapt_rearm"] = [e.get("adapt_rearm", 0) for e in eng]
+            pol[p]["adapt_inc"] = [e.get("adapt_inc", 0) for e in eng]
+            pol[p]["adapt_dec"] = [e.get("adapt_dec", 0) for e in eng]
+            pol[p]["relayout"] = [e.get("relayout", 0) for e in eng]
+            # the quantum each contention class ran with (class 0 compute, 1 memory)
+            by = {}
+            for e in eng:
+                for n, ts in (e.get("mean_tslice_us") or {}).items():
+                    c = (e.get("class") or {}).get(n, -1)
+                    if n != "idle" and c >= 0:
+                        by.setdefault(str(c), []).append(ts)
+            pol[p]["mean_tslice_us_by_class"] = {c: round(q(v, 0.5), 1) for c, v in sorted(by.items())}
+        if "idle" in rs[0]["tenants"]:
+            pol[p]["idle_p50_ms"] = round(q([r["tenants"]["idle"]["p50_ms"] for r in rs], 0.5), 4)
+    # drift over the mix's runs (chronological): the last five gpbs runs
+    # against the first five, and the GPU state of the first and last run
+    xs = [r["aggregate_all_gpus"] for r in runs["gpbs"]]
+    if len(xs) >= 6:
+        k = min(5, len(xs) // 2)
+        f, l = xs[:k], xs[-k:]
+        out_drift = {"first_median": round(q(f, 0.5), 4), "last_median": round(q(l, 0.5), 4),
+                     "first_iqr": round(q(f, 0.75) - q(f, 0.25), 4), "n": k}
+        out_drift["last_within_first_iqr"] = abs(out_drift["last_median"] - out_drift["first_median"]) <= \
+            max(out_drift["first_iqr"], 1e-9)
+    else:
+        out_drift = None
+    gs = [r.get("gpu_state") for r in runs["gpbs"] if r.get("gpu_state")]
+    if gs:
+        pick = ("gfxclk_mhz", "power_w", "ppt_frac", "temp_hotspot_c_max")
+        out_gs = {"first_run": {k: gs[0].get(k) for k in pick}, "last_run": {k: gs[-1].get(k) for k in pick}}
+    else:
+        out_gs = None
+    out = {"value": round(q([r["aggregate_all_gpus"] for r in runs["gpbs"]], 0.5), 4),
+           "mean_slowdown_pct": round(q([r["mean_slowdown_pct"] for r in runs["gpbs"]], 0.5), 2),
+           "reps": max(1, reps), "policies": pol, "per_tenant": g["tenants"], "engine": g.get("engine", {}),
+           "ms_per_step": round(g["ms_per_step"], 3), "solo": solo, "drift": out_drift, "gpu_state": out_gs}
+    if "static-se" in runs:
+        a, b = pol["gpbs"]["aggregate_all_gpus"], pol["static-se"]["aggregate_all_gpus"]
+        out["gpbs_vs_static_se"] = {"delta_median": round(a["median"] - b["median"], 4),
+                                    "iqr_gpbs": a["iqr"], "iqr_static_se": b["iqr"],
+                                    "beats_by_more_than_iqr": a["median"] - b["median"] > max(a["iqr"], b["iqr"])}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -168,17 +236,6 @@ def main():
     log = (lambda *a: print(*a, file=sys.stderr, flush=True))
     import random
 
-    def q(xs, f):
-        xs = sorted(xs)
-        k = (len(xs) - 1) * f
-        lo, hi = int(k), min(int(k) + 1, len(xs) - 1)
-        return xs[lo] + (xs[hi] - xs[lo]) * (k - lo)
-
-    def summ(rs, key):
-        xs = [r[key] for r in rs]
-        return {"median": round(q(xs, 0.5), 4), "iqr": round(q(xs, 0.75) - q(xs, 0.25), 4),
-                "min": round(min(xs), 4), "max": round(max(xs), 4)}
-
     def run_mix(mix, pols, reps):
         """Calibrate solo rates, then every policy `reps` times in a fresh
         random order per repetition (the same on every rank)."""
@@ -211,6 +268,17 @@ def main():
             c.calibrate()
             solo["_end_over_start_rate"] = {k: round(start[k] / c.solo_unit_ms[k], 4) for k in start
                                             if k in c.solo_unit_ms and c.solo_unit_ms[k]}
+            if counters == "hw" and mix == mixes[-1]:
+                # the same with the device-counting context stopped and the GPU
+                # idle for a second: a slowdown that survives it is not the
+                # counter service's (queue state), one that goes away is
+                import time as _t
+                hwc.stop()
+                _t.sleep(1.0)
+                c.calibrate()
+                solo["_end_over_start_rate_ctx_stopped"] = {
+                    k: round(start[k] / c.solo_unit_ms[k], 4) for k in start
+                    if k in c.solo_unit_ms and c.solo_unit_ms[k]}
             c.solo_unit_ms = start
         c.close()
         diag = dict(c.diag, gang=c.gang_stats or None)  # gang stats of the last run (recorded at its stop)
@@ -221,59 +289,6 @@ def main():
         del c
         torch.cuda.empty_cache()
         return runs, order, solo
-
-    def mix_summary(mix, runs, solo, reps):
-        gr = sorted(runs["gpbs"], key=lambda r: r["aggregate_all_gpus"])
-        g = gr[(len(gr) - 1) // 2]  # headline run = the gpbs run with the median aggregate
-        pol = {p: {"aggregate_all_gpus": summ(rs, "aggregate_all_gpus"),
-                   "mean_slowdown_pct": summ(rs, "mean_slowdown_pct"),
-                   "ms_per_step": round(q([r["ms_per_step"] for r in rs], 0.5), 3),
-                   "runs": [round(r["aggregate_all_gpus"], 4) for r in rs]} for p, rs in runs.items()}
-        for p, rs in runs.items():
-            eng = [r.get("engine") for r in rs if r.get("engine")]
-            if eng:
-                pol[p]["adapt_rearm"] = [e.get("adapt_rearm", 0) for e in eng]
-                pol[p]["adapt_inc"] = [e.get("adapt_inc", 0) for e in eng]
-                pol[p]["adapt_dec"] = [e.get("adapt_dec", 0) for e in eng]
-                pol[p]["relayout"] = [e.get("relayout", 0) for e in eng]
-                # the quantum each contention class ran with (class 0 compute, 1 memory)
-                by = {}
-                for e in eng:
-                    for n, ts in (e.get("mean_tslice_us") or {}).items():
-                        c = (e.get("class") or {}).get(n, -1)
-                        if n != "idle" and c >= 0:
-                            by.setdefault(str(c), []).append(ts)
-                pol[p]["mean_tslice_us_by_class"] = {c: round(q(v, 0.5), 1) for c, v in sorted(by.items())}
-            if "idle" in rs[0]["tenants"]:
-                pol[p]["idle_p50_ms"] = round(q([r["tenants"]["idle"]["p50_ms"] for r in rs], 0.5), 4)
-        out = {"value": round(q([r["aggregate_all_gpus"] for r in runs["gpbs"]], 0.5), 4),
-               "mean_slowdown_pct": round(q([r["mean_slowdown_pct"] for r in runs["gpbs"]], 0.5), 2),
-               "reps": max(1, reps), "policies": pol, "per_tenant": g["tenants"], "engine": g.get("engine", {}),
-               "ms_per_step": round(g["ms_per_step"], 3), "solo": solo, "drift": out_drift, "gpu_state": out_gs}
-        # drift over the mix's runs (chronological): the last five gpbs runs
-        # against the first five, and the GPU state of the first and last run
-        xs = [r["aggregate_all_gpus"] for r in runs["gpbs"]]
-        if len(xs) >= 6:
-            k = min(5, len(xs) // 2)
-            f, l = xs[:k], xs[-k:]
-            out_drift = {"first_median": round(q(f, 0.5), 4), "last_median": round(q(l, 0.5), 4),
-                         "first_iqr": round(q(f, 0.75) - q(f, 0.25), 4), "n": k}
-            out_drift["last_within_first_iqr"] = abs(out_drift["last_median"] - out_drift["first_median"]) <= \
-                max(out_drift["first_iqr"], 1e-9)
-        else:
-            out_drift = None
-        gs = [r.get("gpu_state") for r in runs["gpbs"] if r.get("gpu_state")]
-        if gs:
-            pick = ("gfxclk_mhz", "power_w", "ppt_frac", "temp_hotspot_c_max")
-            out_gs = {"first_run": {k: gs[0].get(k) for k in pick}, "last_run": {k: gs[-1].get(k) for k in pick}}
-        else:
-            out_gs = None
-        if "static-se" in runs:
-            a, b = pol["gpbs"]["aggregate_all_gpus"], pol["static-se"]["aggregate_all_gpus"]
-            out["gpbs_vs_static_se"] = {"delta_median": round(a["median"] - b["median"], 4),
-                                        "iqr_gpbs": a["iqr"], "iqr_static_se": b["iqr"],
-                                        "beats_by_more_than_iqr": a["median"] - b["median"] > max(a["iqr"], b["iqr"])}
-        return out
 
     results = {}
     for mix in mixes:

@@ -29,6 +29,8 @@ struct HwcAttrIn {
   u32 clean_pct;                         // exclusive-ownership window threshold (%), 0: pro rata
   u32 shared;                            // class-share time in the interval (no clean windows)
   u32 prime;                             // 1: only record the snapshot as the new previous one
+  u32 nt_hi;                             // rows t >= nt_hi of own_cur are zero (and were: owned time only grows);
+                                         // the device path reads rows < nt_hi only (0 = all rows)
 };
 
 struct HwcAttrPrev {  // carried from one snapshot to the next
@@ -45,7 +47,7 @@ struct HwcAttrOut {
   double hw_sum[kNumPmc];             // all hardware counts of the interval
   double unatt[kNumPmc];              // counts no owner explains
   u32 valid;                          // 0: a priming call (no deltas)
-  u32 pad[3];
+  u32 pad[3];                         // device path: [0] / [1] = 100 MHz wall clock at kernel entry / exit
 };
 
 __host__ __device__ inline u64 attr_dpos(u64 a, u64 b) { return a >= b ? a - b : 0; }  // Q5

@@ -722,6 +722,14 @@ void hwc_fill_in(GpuCtx* c, HwcAttrIn& in) {
   in.clean_pct = (u32)c->clean_pct;
   in.shared = c->snap_share > c->share_prev;
   in.prime = !c->hw_primed;
+  u32 hi = 0;  // tenants that ever owned a partition (owned time only grows)
+  for (int t = kMaxTenants - 1; t >= 0 && !hi; --t)
+    for (int x = 0; x < kAttrP; ++x)
+      if (in.own_cur[t * kAttrP + x]) {
+        hi = (u32)t + 1;
+        break;
+      }
+  in.nt_hi = hi ? hi : 1;
 }
 
 // Modeled per-tile counters over the same interval (cross-check, host).
@@ -1833,9 +1841,10 @@ int gpbs_gpu_set_hwc_device(void* p, int on) {
 // snapshot pairs (seeded): max relative difference of the attributed and
 // clean deltas and the interval totals.  Stand-alone (no context needed).
 // Cost of one attribution (a live-layout snapshot in pinned host memory, as
-// on the headline path): out[0] = mean device time per launch over `iters`
-// back-to-back launches (hipEvent), out[1] = mean host round trip of one
-// launch + event wait.  0 on success.
+// on the headline path): out[0] = mean interval per launch over `iters`
+// back-to-back launches (hipEvent: kernel + dispatch gap), out[1] = mean host
+// round trip of one launch + event wait, out[2] = mean kernel duration from
+// the kernel's own entry / exit wall-clock stamps.  0 on success.
 // Two pools on one GpuContext, device adapt: pool A launches
 // for tenants {1,2}, pool B for {3,4}, interleaved and harvested in both
 // orders; every harvest must return the caller's own tenants with the host
@@ -1927,6 +1936,7 @@ int gpbs_hip_hwc_attr_bench(int iters, double* out2) {
     in->se_mode = 1;
     in->clean_pct = 90;
     in->prime = 0;
+    in->nt_hi = 5;  // tenants 1..4 own partitions
     gpbs_hip_hwc_attribute(in, d_st, out, s);  // warm
     hipStreamSynchronize(s);
     hipEventRecord(e0, s);
@@ -1937,12 +1947,15 @@ int gpbs_hip_hwc_attr_bench(int iters, double* out2) {
     hipEventElapsedTime(&ms, e0, e1);
     out2[0] = 1e3 * ms / iters;
     const int64_t t0 = mono_ns();
+    double ticks = 0;
     for (int i = 0; i < iters; ++i) {
       gpbs_hip_hwc_attribute(in, d_st, out, s);
       hipEventRecord(e1, s);
       hipEventSynchronize(e1);
+      ticks += (double)(uint32_t)(out->pad[1] - out->pad[0]);
     }
     out2[1] = (double)(mono_ns() - t0) / 1e3 / iters;
+    out2[2] = ticks * 0.01 / iters;  // 100 MHz ticks -> us
     if (hipGetLastError() != hipSuccess) rc = -5;
   }
   if (e0) hipEventDestroy(e0);
@@ -1998,6 +2011,7 @@ int gpbs_hip_hwc_attr_selftest(int seed, int iters, double* max_rel) {
     in->clean_pct = it % 7 == 3 ? 0 : 90;
     in->shared = it % 11 == 10;
     in->prime = it == 0;
+    in->nt_hi = it % 3 == 2 ? 0 : 7;  // tenants 1..6 own partitions (0: read every row)
     hwc_attr_host(*in, hst, ref);
     if (gpbs_hip_hwc_attribute(in, d_st, out, nullptr) || hipDeviceSynchronize() != hipSuccess) {
       rc = -5;

@@ -95,12 +95,15 @@ __device__ inline double wave_sum64(double v) {
 //   * clean owners: the last tenant over the clean_pct threshold, from a
 //     wave ballot per partition;
 //   * attribution: wave k attributes counter slot k for all 64 tenants at
-//     once, slots 0-2 in parallel, then slot 3 (L2 misses split by slot 2's
-//     L2-request shares) -- each lane sums its partitions in the host order.
+//     once, the four waves independently (wave 3 recomputes slot 2's
+//     L2-request shares in registers to split the L2 misses) -- each lane
+//     sums its partitions in the host order, dividing by a per-partition
+//     reciprocal computed once.
 // The previous snapshot and the clean-owner history stay in device memory.
 __global__ __launch_bounds__(256) void k_hwc_attribute(const HwcAttrIn* __restrict__ in, HwcAttrPrev* __restrict__ st,
                                                        HwcAttrOut* __restrict__ out) {
   __builtin_amdgcn_s_setprio(3);
+  const u32 t_entry = (u32)__builtin_amdgcn_s_memrealtime();  // 100 MHz: the kernel's own duration -> out->pad
   constexpr int P = kAttrP, T = kMaxTenants, X = kXcds, K = kNumPmc, E = kCtx;
   static_assert(T == 64 && X * E == P && P * T == 8 * 256, "one wave of tenants, 8 owned-time words per thread");
   static_assert(offsetof(HwcAttrIn, x_cur) == offsetof(HwcAttrIn, se_cur) + sizeof(u64) * P * K &&
@@ -110,8 +113,7 @@ __global__ __launch_bounds__(256) void k_hwc_attribute(const HwcAttrIn* __restri
   constexpr int NC = (P + X) * K / 2;  // 16-byte counter loads (80)
   __shared__ double ownT[P][T + 1];    // owned ns of the interval, [partition][tenant], padded
   __shared__ double vse[P][K], vx[X][K];
-  __shared__ double tot_p[P];
-  __shared__ double refs_x[X][T], refs_cx[X][T];
+  __shared__ double tot_p[P], inv_p[P], tot_x[X], inv_x[X];
   __shared__ int clean_owner[P], xcd_owner[X];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const u32 prime = in->prime;
@@ -122,8 +124,11 @@ __global__ __launch_bounds__(256) void k_hwc_attribute(const HwcAttrIn* __restri
   ulonglong2* cp = reinterpret_cast<ulonglong2*>(st->se);
   longlong2 c[4], q[4];
   ulonglong2 cv{}, qv{};
+  // only the rows of tenants that ever owned a partition cross PCIe
+  const u32 nth = in->nt_hi;
+  const int nload = (nth == 0 || nth > (u32)T) ? T * P / 2 : (int)nth * P / 2;  // 16-byte loads
 #pragma unroll
-  for (int j = 0; j < 4; ++j) c[j] = oc[j * 256 + tid];
+  for (int j = 0; j < 4; ++j) c[j] = j * 256 + tid < nload ? oc[j * 256 + tid] : longlong2{0, 0};
   if (tid < NC) cv = cc[tid];
   const u32 se_mode = in->se_mode, clean_pct = in->clean_pct, shared = in->shared;
   u32 slot_se[K];
@@ -131,7 +136,7 @@ __global__ __launch_bounds__(256) void k_hwc_attribute(const HwcAttrIn* __restri
   for (int k = 0; k < K; ++k) slot_se[k] = in->slot_se[k];
   if (!prime) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) q[j] = op[j * 256 + tid];
+    for (int j = 0; j < 4; ++j) q[j] = j * 256 + tid < nload ? op[j * 256 + tid] : longlong2{0, 0};
     if (tid < NC) qv = cp[tid];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -146,15 +151,11 @@ __global__ __launch_bounds__(256) void k_hwc_attribute(const HwcAttrIn* __restri
       dst[0] = (double)attr_dpos(cv.x, qv.x);
       dst[1] = (double)attr_dpos(cv.y, qv.y);
     }
-#pragma unroll
-    for (int i = tid; i < X * T; i += 256) {
-      (&refs_x[0][0])[i] = 0.0;
-      (&refs_cx[0][0])[i] = 0.0;
-    }
   }
   // the new previous snapshot (each thread overwrites only what it read)
 #pragma unroll
-  for (int j = 0; j < 4; ++j) op[j * 256 + tid] = c[j];
+  for (int j = 0; j < 4; ++j)
+    if (j * 256 + tid < nload) op[j * 256 + tid] = c[j];
   if (tid < NC) cp[tid] = cv;
   if (prime) {
     if (tid == 0) out->valid = 0u;
@@ -166,7 +167,10 @@ __global__ __launch_bounds__(256) void k_hwc_attribute(const HwcAttrIn* __restri
   for (int i = 0; i < P / 4; ++i) {
     const int p = wave * (P / 4) + i;
     const double s = wave_sum64(ownT[p][lane]);
-    if (lane == 0) tot_p[p] = s;
+    if (lane == 0) {
+      tot_p[p] = s;
+      inv_p[p] = s > 0 ? 1.0 / s : 0.0;
+    }
   }
   __syncthreads();
   // 3. clean owners: >= clean_pct of the interval's span, and the same owner as the previous interval
@@ -195,75 +199,87 @@ __global__ __launch_bounds__(256) void k_hwc_attribute(const HwcAttrIn* __restri
       o = clean_owner[p];
     }
     xcd_owner[tid] = ok ? o : -1;
+    // an XCD's owned time over its shader engines (exact: integer ns)
+    double tx = 0;
+    for (int e = 0; e < E; ++e) tx += tot_p[tid * E + e];
+    tot_x[tid] = tx;
+    inv_x[tid] = tx > 0 ? 1.0 / tx : 0.0;
   }
   __syncthreads();
-  // 4. attribution, lane = tenant: slots 0-2 on waves 0-2, then slot 3 (it reads slot 2's L2 requests)
+  // 4. attribution, lane = tenant, wave k = counter slot k; the four waves
+  // never wait for each other: wave 3's L2 misses are split by slot 2's L2
+  // requests, which it recomputes itself (registers) before its own pass
   const int t = lane;
-  for (int phase = 0; phase < 2; ++phase) {
-    const int k = phase == 0 ? wave : 3;
-    if ((phase == 0 && wave < 3) || (phase == 1 && wave == 3)) {
-      double add = 0, addc = 0, hs = 0, ua = 0;
-      if (se_mode && slot_se[k]) {
-        for (int x = 0; x < X; ++x) {
-          double rx = 0, rcx = 0;
-          for (int e = 0; e < E; ++e) {
-            const int p = x * E + e;
-            const double v = vse[p][k], tot = tot_p[p];
-            hs += v;
-            if (tot <= 0) {
-              ua += v;
-              continue;
-            }
-            const double w = ownT[p][t];
-            if (w <= 0) continue;
-            const double a = v * w / tot;
-            add += a;
-            rx += a;
-            if (clean_owner[p] == t) {
-              addc += a;
-              rcx += a;
-            }
-          }
-          if (k == 2) {
-            refs_x[x][t] += rx;
-            refs_cx[x][t] += rcx;
-          }
-        }
-      } else {
-        const bool miss_by_refs = k == 3;
-        const bool refs_clean = miss_by_refs && se_mode && slot_se[2];
-        for (int x = 0; x < X; ++x) {
-          const double v = vx[x][k];
-          double tot = 0, wt = 0;
-          bool by_refs = false;
-          if (miss_by_refs) {
-            wt = refs_x[x][t];
-            tot = wave_sum64(wt);
-            by_refs = tot > 0;
-          }
-          if (!by_refs) {
-            tot = 0;
-            wt = 0;
-            for (int e = 0; e < E; ++e) {
-              tot += tot_p[x * E + e];
-              wt += ownT[x * E + e][t];
-            }
-          }
+  double rx[X], rcx[X];
+#pragma unroll
+  for (int x = 0; x < X; ++x) rx[x] = rcx[x] = 0.0;
+  auto pass = [&](const int k, const bool emit) {
+    double add = 0, addc = 0, hs = 0, ua = 0;
+    if (se_mode && slot_se[k]) {
+#pragma unroll
+      for (int x = 0; x < X; ++x) {
+        double sx = 0, scx = 0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int p = x * E + e;
+          const double v = vse[p][k];
           hs += v;
-          if (tot <= 0) {
+          if (tot_p[p] <= 0) {
             ua += v;
             continue;
           }
-          if (wt <= 0) continue;
-          const double a = v * wt / tot;
+          const double w = ownT[p][t];
+          if (w <= 0) continue;
+          const double a = v * w * inv_p[p];
           add += a;
-          if (k == 2) refs_x[x][t] += a;
-          if (refs_clean)
-            addc += v * refs_cx[x][t] / tot;
-          else if (xcd_owner[x] == t)
+          sx += a;
+          if (clean_owner[p] == t) {
             addc += a;
+            scx += a;
+          }
+        }
+        if (k == 2) {
+          rx[x] = sx;
+          rcx[x] = scx;
         }
       }
+    } else {
+      const bool miss_by_refs = k == 3;
+      const bool refs_clean = miss_by_refs && se_mode && slot_se[2];
+#pragma unroll
+      for (int x = 0; x < X; ++x) {
+        const double v = vx[x][k];
+        double tot = 0, wt = 0, inv = 0;
+        bool by_refs = false;
+        if (miss_by_refs) {
+          wt = rx[x];
+          tot = wave_sum64(wt);
+          by_refs = tot > 0;
+          inv = by_refs ? 1.0 / tot : 0.0;
+        }
+        if (!by_refs) {
+          tot = tot_x[x];
+          inv = inv_x[x];
+          wt = 0;
+#pragma unroll
+          for (int e = 0; e < E; ++e) wt += ownT[x * E + e][t];
+        }
+        hs += v;
+        if (tot <= 0) {
+          ua += v;
+          continue;
+        }
+        if (wt <= 0) continue;
+        const double a = v * wt * inv;
+        add += a;
+        if (k == 2) rx[x] = a;
+        if (refs_clean)
+          addc += v * rcx[x] * inv;
+        else if (xcd_owner[x] == t)
+          addc += a;
+      }
+    }
+    if (emit) {
       out->add[t][k] = add;
       out->addc[t][k] = addc;
       if (lane == 0) {
@@ -271,9 +287,15 @@ __global__ __launch_bounds__(256) void k_hwc_attribute(const HwcAttrIn* __restri
         out->unatt[k] = ua;
       }
     }
-    __syncthreads();
+  };
+  if (wave == 3) pass(2, false);  // slot 2's L2-request shares, this lane's
+  pass(wave, true);
+  __syncthreads();
+  if (tid == 0) {
+    out->pad[0] = t_entry;
+    out->pad[1] = (u32)__builtin_amdgcn_s_memrealtime();
+    out->valid = 1u;
   }
-  if (tid == 0) out->valid = 1u;
 }
 
 }  // namespace gpbs_hip
