@@ -2306,6 +2306,17 @@ int gpbs_gpu_adapt_stats(void* p, uint64_t* calls, uint64_t* late, uint64_t* bus
   return 0;
 }
 
+// Process-wide CU-masked queue pool: out[0] masked streams ever created,
+// out[1] currently free (the rest are held by runners).  Every created one is
+// a hardware queue this process keeps.
+int gpbs_gpu_masked_pool(uint64_t* out2) {
+  MaskedStreams& P = masked_pool();
+  std::lock_guard<std::mutex> g(P.mu);
+  out2[0] = (uint64_t)P.created;
+  out2[1] = (uint64_t)P.free.size();
+  return 0;
+}
+
 int gpbs_gpu_stats(void* p, uint64_t* out4) {
   GpuCtx* c = (GpuCtx*)p;
   out4[0] = c->switches.load();

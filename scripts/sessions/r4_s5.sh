@@ -20,3 +20,4 @@ echo "qb rc=$?"; grep -v RESULT gpurun_out/r4/s5_qbudget.log | tail -14
 echo "== queue budget, counters $(date +%T)"
 timeout -k 10 240 python -u scripts/queue_budget.py --counters --step 4 --max 48 > gpurun_out/r4/s5_qbudget_hwc.log 2>&1
 echo "qb hwc rc=$?"; grep -v RESULT gpurun_out/r4/s5_qbudget_hwc.log | tail -14
+bash scripts/sessions/r4_s6.sh
