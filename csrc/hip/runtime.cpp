@@ -1050,63 +1050,88 @@ namespace {
 // therefore take masked streams from this pool and return them (drained)
 // when they close, so the process holds at most as many masked queues as it
 // ever used at once.
+// Process-wide pool of CU-masked streams.  Every CU-masked stream is a
+// hardware queue of its own and the process never gets one back; past the
+// hardware scheduler's queue slots it oversubscribes and time-slices ALL
+// queues, idle ones included.  Measured (scripts/queue_budget.py,
+// profiles/r4/queue_budget*.log): a solo GEMM keeps its rate up to 20 extra
+// masked queues and loses 24 % at 24, 63 % at 48; with the device-counting
+// context running the knee moves down by about four queues (the profiler's
+// own).  The round-3 live-counter "drift" and the bimodal 8mix runs were this
+// oversubscription.
+//
+// So masked queues are SHARED by key: runners that hold the same set of
+// (XCD, SE) partitions -- co-sharers of a time-shared region, which never run
+// at the same time -- launch on one queue; runners on disjoint sets (split
+// layouts, which run concurrently) get their own.  A queue nobody holds is
+// re-keyed before a new one is created, so the process holds about as many
+// masked queues as there are concurrently running layouts (8mix: compute
+// region, memory region, latency lane = 3), not one per runner.  Key 0 =
+// exclusive (never shared).  GPBS_SHARE_QUEUES=0: every acquire exclusive
+// (the round-3 behaviour).
 struct MaskedStreams {
   struct Ent {
     int device;
     uint32_t m[8];
     hipStream_t s;
+    uint32_t key;
+    int refs;
   };
   std::mutex mu;
-  std::vector<Ent> free;
+  std::vector<Ent> ents;
   int created = 0;
 };
 MaskedStreams& masked_pool() {
   static MaskedStreams* p = new MaskedStreams;  // never destroyed: streams outlive static teardown order
   return *p;
 }
-// A runner that moves between class halves gives its old masked stream back
-// before taking the other, so the process holds at most one masked queue per
-// runner (8mix: 8 instead of 16).  Measured on the 8mix, 3 reps
-// (profiles/r3/8mix_queues_q8_*.json): with both halves' queues kept, every partitioned
-// policy lost 0.1-0.2 of aggregate in some repetitions (static-se IQR 0.049,
-// gpbs-ts 0.123); with one, static-se IQR 0.0009, gpbs-ts 0.018.
-// GPBS_ONE_MASKED=0 restores the old behaviour.
-bool one_masked() {
+bool share_queues() {
   static const bool v = [] {
-    const char* e = std::getenv("GPBS_ONE_MASKED");
+    const char* e = std::getenv("GPBS_SHARE_QUEUES");
     return !e || std::atoi(e) != 0;
   }();
   return v;
 }
-hipStream_t masked_acquire(const uint32_t m[8]) {
+hipStream_t masked_acquire_key(const uint32_t m[8], uint32_t key) {
   int dev = 0;
   hipGetDevice(&dev);
+  if (!share_queues()) key = 0;
   MaskedStreams& P = masked_pool();
   {
     std::lock_guard<std::mutex> g(P.mu);
-    for (size_t i = 0; i < P.free.size(); ++i)
-      if (P.free[i].device == dev && std::memcmp(P.free[i].m, m, sizeof(P.free[i].m)) == 0) {
-        hipStream_t s = P.free[i].s;
-        P.free.erase(P.free.begin() + (long)i);
-        return s;
+    MaskedStreams::Ent* idle = nullptr;
+    for (auto& e : P.ents) {
+      if (e.device != dev || std::memcmp(e.m, m, sizeof(e.m)) != 0) continue;
+      if (key && e.key == key && e.refs > 0) {  // the same layout: share its queue
+        e.refs++;
+        return e.s;
       }
+      if (e.refs == 0 && (!idle || (key && e.key == key))) idle = &e;
+    }
+    if (idle) {  // re-key a queue nobody holds
+      idle->key = key;
+      idle->refs = 1;
+      return idle->s;
+    }
   }
   hipStream_t s = nullptr;
   if (hipExtStreamCreateWithCUMask(&s, 8, const_cast<uint32_t*>(m)) != hipSuccess) return nullptr;
   std::lock_guard<std::mutex> g(P.mu);
+  P.ents.push_back({dev, {}, s, key, 1});
+  std::memcpy(P.ents.back().m, m, sizeof(P.ents.back().m));
   P.created++;
   return s;
 }
-void masked_release(const uint32_t m[8], hipStream_t s) {
+hipStream_t masked_acquire(const uint32_t m[8]) { return masked_acquire_key(m, 0); }
+void masked_release(const uint32_t*, hipStream_t s) {
   if (!s) return;
-  int dev = 0;
-  hipGetDevice(&dev);
-  hipStreamSynchronize(s);
-  MaskedStreams::Ent e{dev, {}, s};
-  std::memcpy(e.m, m, sizeof(e.m));
   MaskedStreams& P = masked_pool();
   std::lock_guard<std::mutex> g(P.mu);
-  P.free.push_back(e);
+  for (auto& e : P.ents)
+    if (e.s == s && e.refs > 0) {
+      e.refs--;
+      return;
+    }
 }
 
 // CU mask of one half of every XCD.  hipExtStreamCreateWithCUMask bit b
@@ -1143,7 +1168,10 @@ struct Runner {
   // free resources before it is even dispatched, and the kernel -- and the
   // next one on the stream -- completes only after it has.  Confining the
   // grid to the owned CUs removes that coupling (GATE_SE still revokes).
-  hipStream_t se_stream[2] = {nullptr, nullptr};  // SEs {0,1} / {2,3} of every XCD
+  hipStream_t se_stream[2] = {nullptr, nullptr};  // SEs {0,1} / {2,3} of every XCD (latency lane only)
+  hipStream_t key_stream = nullptr;  // gated SE mode: the masked queue of the layout it holds (shared by key)
+  uint32_t key_bits = 0;             // ... its key: the owned (XCD, SE) partition set
+  int key_half = -1;
   int cur_grid = 0;  // grid for the stream pick_stream chose (0: kernel default)
   WorkQueue* d_q = nullptr;  // ring of depth+1 queues
   u32* h_status = nullptr;   // pinned status words
@@ -1221,16 +1249,26 @@ struct Runner {
   // after run).  An owned set that fits neither half (work-conserving steals
   // across classes) launches unmasked and gates per workgroup.
   hipStream_t pick_se_stream() {
-    u32 any = 0;
+    u32 any = 0, bits = 0;
     for (int x = 0; x < kXcds; ++x)
       for (int e = 0; e < kCtx; ++e)
-        if ((__atomic_load_n(&ctx->h_table->owner[kCtx * x + e], __ATOMIC_ACQUIRE) & kOwnerMask) == (u32)cfg.tenant)
+        if ((__atomic_load_n(&ctx->h_table->owner[kCtx * x + e], __ATOMIC_ACQUIRE) & kOwnerMask) == (u32)cfg.tenant) {
           any |= 1u << e;
+          bits |= 1u << (kCtx * x + e);
+        }
     const int half = (any & ~0x3u) == 0 ? 0 : ((any & ~0xCu) == 0 ? 1 : -1);
     if (!any || half < 0) return stream;
-    hipStream_t s = half_se_stream(half);
-    if (s != stream) cur_grid = (work(cur_alt).kind == K_GEMV) ? 0 : 128;  // one persistent WG per CU of the half
-    return s;
+    if (!key_stream || bits != key_bits || half != key_half) {  // a new layout: its queue (shared with co-sharers)
+      uint32_t m[8];
+      se_half_mask(half, m);
+      if (key_stream) masked_release(m, key_stream);
+      key_stream = masked_acquire_key(m, bits);
+      key_bits = bits;
+      key_half = half;
+      if (!key_stream) return stream;
+    }
+    cur_grid = (work(cur_alt).kind == K_GEMV) ? 0 : 128;  // one persistent WG per CU of the half
+    return key_stream;
   }
 
   bool shared() const { return cfg.gate && ctx->share.load(std::memory_order_acquire); }
@@ -1243,7 +1281,7 @@ struct Runner {
   hipStream_t half_se_stream(int half) {
     if (!se_stream[half]) {
       uint32_t m[8];
-      if (one_masked() && se_stream[half ^ 1]) {  // hold one masked queue per runner at a time
+      if (se_stream[half ^ 1]) {  // hold one masked queue per runner at a time
         se_half_mask(half ^ 1, m);
         masked_release(m, se_stream[half ^ 1]);
         se_stream[half ^ 1] = nullptr;
@@ -1489,6 +1527,7 @@ struct Runner {
       if (h) hipStreamSynchronize(h);
     for (hipStream_t h : se_stream)
       if (h) hipStreamSynchronize(h);
+    if (key_stream) hipStreamSynchronize(key_stream);
     for (int qi = 0; qi < nq; ++qi) hold_drop(qi);  // stopped with latency units in flight
     std::lock_guard<std::mutex> g(mu);
     idle_cv.notify_all();
@@ -2313,7 +2352,9 @@ int gpbs_gpu_masked_pool(uint64_t* out2) {
   MaskedStreams& P = masked_pool();
   std::lock_guard<std::mutex> g(P.mu);
   out2[0] = (uint64_t)P.created;
-  out2[1] = (uint64_t)P.free.size();
+  uint64_t idle = 0;
+  for (auto& e : P.ents) idle += e.refs == 0;
+  out2[1] = idle;
   return 0;
 }
 
@@ -2578,6 +2619,7 @@ void gpbs_runner_destroy(void* p) {
       masked_release(m, r->se_stream[h]);
     }
   }
+  if (r->key_stream) masked_release(nullptr, r->key_stream);
   hipFree(r->d_q);
   hipHostFree(r->h_status);
   delete r;

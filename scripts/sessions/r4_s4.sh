@@ -6,6 +6,11 @@
 set -o pipefail
 cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out/r4
+echo "== 8mix gpbs, shared queues $(date +%T)"
+timeout -k 10 200 python -u bench.py --gpus 1 --mix 8mix --policies gpbs --reps 8 --steps 20 --warmup 3 \
+  > gpurun_out/r4/s4_8mix_shared.json 2> gpurun_out/r4/s4_8mix_shared.log
+echo "8mix rc=$?"; python scripts/corun_log_policies.py gpurun_out/r4/s4_8mix_shared.log | head -2
+grep -o '"masked_queues_created": [0-9]*' gpurun_out/r4/s4_8mix_shared.log | sort | uniq -c | head -3
 echo "== gpu tests $(date +%T)"
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
   > gpurun_out/r4/s4_gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -40 gpurun_out/r4/s4_gpu_tests.log; exit 1; }
