@@ -56,7 +56,7 @@ int gpbs_hip_partition_switch(void*, unsigned, const unsigned*, hipStream_t);
 int gpbs_hip_counter_reduce(void*, void*, const int*, int, void*, hipStream_t);
 int gpbs_hip_adapt(void*, const void*, const void*, const void*, int, const gpbs_adapt_params_t*, int*, hipStream_t);
 int gpbs_hip_switch_probe(const void*, int, unsigned*, int, unsigned, unsigned long long, hipStream_t);
-int gpbs_hip_hwc_attribute(const void*, void*, void*, hipStream_t);
+int gpbs_hip_hwc_attribute(const void*, void*, void*, void*, hipStream_t);
 int gpbs_hip_allreduce(const void*, unsigned, unsigned long long, unsigned, void*, const void*, unsigned, unsigned,
                        void*, void*, int, unsigned long long, unsigned long long, hipStream_t);
 int gpbs_hip_gang_desc_size(void);
@@ -262,7 +262,8 @@ struct GpuCtx {
   // wait), on the host with GPBS_HWC_DEVICE=0.
   int dev_attr = 1;
   HwcAttrPrev hst;                  // host path state
-  HwcAttrIn* h_ain = nullptr;       // pinned, read by the kernel
+  HwcAttrIn* h_ain = nullptr;       // pinned: the snapshot the metric tick fills
+  HwcAttrIn* d_ain = nullptr;       // device staging copy the kernel reads
   HwcAttrOut* h_aout = nullptr;     // pinned mapped, written by the kernel
   HwcAttrPrev* d_ast = nullptr;     // device-resident previous snapshot
   hipEvent_t attr_ev = nullptr;
@@ -772,7 +773,7 @@ int hwc_consume(GpuCtx* c, bool wait) {
   bool done = false;
   if (c->dev_attr) {
     hwc_fill_in(c, *c->h_ain);
-    if (gpbs_hip_hwc_attribute(c->h_ain, c->d_ast, c->h_aout, c->sched_stream) == 0 &&
+    if (gpbs_hip_hwc_attribute(c->h_ain, c->d_ain, c->d_ast, c->h_aout, c->sched_stream) == 0 &&
         hipEventRecord(c->attr_ev, c->sched_stream) == hipSuccess) {
       c->attr_pending = true;
       c->attr_launches++;
@@ -1581,6 +1582,7 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
   hwc_attr_prev_init(c->hst);
   if (const char* v = std::getenv("GPBS_HWC_DEVICE")) c->dev_attr = std::atoi(v) != 0;
   ok = ok && hipHostMalloc((void**)&c->h_ain, sizeof(HwcAttrIn), hipHostMallocMapped) == hipSuccess;
+  ok = ok && hipMalloc((void**)&c->d_ain, sizeof(HwcAttrIn)) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_aout, sizeof(HwcAttrOut), hipHostMallocMapped) == hipSuccess;
   ok = ok && hipMalloc((void**)&c->d_ast, sizeof(HwcAttrPrev)) == hipSuccess;
   ok = ok && hipMemcpy(c->d_ast, &c->hst, sizeof(HwcAttrPrev), hipMemcpyHostToDevice) == hipSuccess;
@@ -1665,6 +1667,7 @@ void gpbs_gpu_ctx_destroy(void* p) {
   if (c->h_ain) hipHostFree(c->h_ain);
   if (c->h_aout) hipHostFree(c->h_aout);
   if (c->d_ast) hipFree(c->d_ast);
+  if (c->d_ain) hipFree(c->d_ain);
   for (auto& B : c->abuf) {
     if (B.ev) {
       hipEventSynchronize(B.ev);
@@ -1952,12 +1955,14 @@ int gpbs_hip_adapt_pools_selftest(int rounds) {
 int gpbs_hip_hwc_attr_bench(int iters, double* out2) {
   if (iters <= 0 || !out2) return -22;
   HwcAttrIn* in = nullptr;
+  HwcAttrIn* d_in = nullptr;
   HwcAttrOut* out = nullptr;
   HwcAttrPrev* d_st = nullptr;
   hipStream_t s = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   int rc = 0;
   if (hipHostMalloc((void**)&in, sizeof(HwcAttrIn), hipHostMallocMapped) != hipSuccess ||
+      hipMalloc((void**)&d_in, sizeof(HwcAttrIn)) != hipSuccess ||
       hipHostMalloc((void**)&out, sizeof(HwcAttrOut), hipHostMallocMapped) != hipSuccess ||
       hipMalloc((void**)&d_st, sizeof(HwcAttrPrev)) != hipSuccess || hipStreamCreate(&s) != hipSuccess ||
       hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)
@@ -1976,10 +1981,10 @@ int gpbs_hip_hwc_attr_bench(int iters, double* out2) {
     in->clean_pct = 90;
     in->prime = 0;
     in->nt_hi = 5;  // tenants 1..4 own partitions
-    gpbs_hip_hwc_attribute(in, d_st, out, s);  // warm
+    gpbs_hip_hwc_attribute(in, d_in, d_st, out, s);  // warm
     hipStreamSynchronize(s);
     hipEventRecord(e0, s);
-    for (int i = 0; i < iters; ++i) gpbs_hip_hwc_attribute(in, d_st, out, s);
+    for (int i = 0; i < iters; ++i) gpbs_hip_hwc_attribute(in, d_in, d_st, out, s);
     hipEventRecord(e1, s);
     hipEventSynchronize(e1);
     float ms = 0;
@@ -1988,7 +1993,7 @@ int gpbs_hip_hwc_attr_bench(int iters, double* out2) {
     const int64_t t0 = mono_ns();
     double ticks = 0;
     for (int i = 0; i < iters; ++i) {
-      gpbs_hip_hwc_attribute(in, d_st, out, s);
+      gpbs_hip_hwc_attribute(in, d_in, d_st, out, s);
       hipEventRecord(e1, s);
       hipEventSynchronize(e1);
       ticks += (double)(uint32_t)(out->pad[1] - out->pad[0]);
@@ -2000,6 +2005,7 @@ int gpbs_hip_hwc_attr_bench(int iters, double* out2) {
   if (e0) hipEventDestroy(e0);
   if (e1) hipEventDestroy(e1);
   if (s) hipStreamDestroy(s);
+  if (d_in) hipFree(d_in);
   if (in) hipHostFree(in);
   if (out) hipHostFree(out);
   if (d_st) hipFree(d_st);
@@ -2008,9 +2014,11 @@ int gpbs_hip_hwc_attr_bench(int iters, double* out2) {
 
 int gpbs_hip_hwc_attr_selftest(int seed, int iters, double* max_rel) {
   HwcAttrIn* in = nullptr;
+  HwcAttrIn* d_in = nullptr;
   HwcAttrOut* out = nullptr;
   HwcAttrPrev* d_st = nullptr;
   if (hipHostMalloc((void**)&in, sizeof(HwcAttrIn), hipHostMallocMapped) != hipSuccess ||
+      hipMalloc((void**)&d_in, sizeof(HwcAttrIn)) != hipSuccess ||
       hipHostMalloc((void**)&out, sizeof(HwcAttrOut), hipHostMallocMapped) != hipSuccess ||
       hipMalloc((void**)&d_st, sizeof(HwcAttrPrev)) != hipSuccess)
     return -12;
@@ -2052,7 +2060,7 @@ int gpbs_hip_hwc_attr_selftest(int seed, int iters, double* max_rel) {
     in->prime = it == 0;
     in->nt_hi = it % 3 == 2 ? 0 : 7;  // tenants 1..6 own partitions (0: read every row)
     hwc_attr_host(*in, hst, ref);
-    if (gpbs_hip_hwc_attribute(in, d_st, out, nullptr) || hipDeviceSynchronize() != hipSuccess) {
+    if (gpbs_hip_hwc_attribute(in, d_in, d_st, out, nullptr) || hipDeviceSynchronize() != hipSuccess) {
       rc = -5;
       break;
     }
@@ -2072,6 +2080,7 @@ int gpbs_hip_hwc_attr_selftest(int seed, int iters, double* max_rel) {
     }
   }
   if (max_rel) *max_rel = worst;
+  hipFree(d_in);
   hipHostFree(in);
   hipHostFree(out);
   hipFree(d_st);

@@ -100,8 +100,13 @@ __device__ inline double wave_sum64(double v) {
 //     sums its partitions in the host order, dividing by a per-partition
 //     reciprocal computed once.
 // The previous snapshot and the clean-owner history stay in device memory.
+struct AttrArgs {  // the snapshot's scalars, by value (no dependent load before the staging loads)
+  u32 slot_se[kNumPmc];
+  u32 se_mode, clean_pct, shared, prime, nt_hi;
+};
+
 __global__ __launch_bounds__(256) void k_hwc_attribute(const HwcAttrIn* __restrict__ in, HwcAttrPrev* __restrict__ st,
-                                                       HwcAttrOut* __restrict__ out) {
+                                                       HwcAttrOut* __restrict__ out, AttrArgs args) {
   __builtin_amdgcn_s_setprio(3);
   const u32 t_entry = (u32)__builtin_amdgcn_s_memrealtime();  // 100 MHz: the kernel's own duration -> out->pad
   constexpr int P = kAttrP, T = kMaxTenants, X = kXcds, K = kNumPmc, E = kCtx;
@@ -116,7 +121,7 @@ __global__ __launch_bounds__(256) void k_hwc_attribute(const HwcAttrIn* __restri
   __shared__ double tot_p[P], inv_p[P], tot_x[X], inv_x[X];
   __shared__ int clean_owner[P], xcd_owner[X];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const u32 prime = in->prime;
+  const u32 prime = args.prime;
   // 1. stage: every load of the snapshot and of the previous state in flight at once
   const longlong2* oc = reinterpret_cast<const longlong2*>(in->own_cur);
   longlong2* op = reinterpret_cast<longlong2*>(st->own);
@@ -124,16 +129,16 @@ __global__ __launch_bounds__(256) void k_hwc_attribute(const HwcAttrIn* __restri
   ulonglong2* cp = reinterpret_cast<ulonglong2*>(st->se);
   longlong2 c[4], q[4];
   ulonglong2 cv{}, qv{};
-  // only the rows of tenants that ever owned a partition cross PCIe
-  const u32 nth = in->nt_hi;
+  // only the rows of tenants that ever owned a partition (copied by the host)
+  const u32 nth = args.nt_hi;
   const int nload = (nth == 0 || nth > (u32)T) ? T * P / 2 : (int)nth * P / 2;  // 16-byte loads
 #pragma unroll
   for (int j = 0; j < 4; ++j) c[j] = j * 256 + tid < nload ? oc[j * 256 + tid] : longlong2{0, 0};
   if (tid < NC) cv = cc[tid];
-  const u32 se_mode = in->se_mode, clean_pct = in->clean_pct, shared = in->shared;
+  const u32 se_mode = args.se_mode, clean_pct = args.clean_pct, shared = args.shared;
   u32 slot_se[K];
 #pragma unroll
-  for (int k = 0; k < K; ++k) slot_se[k] = in->slot_se[k];
+  for (int k = 0; k < K; ++k) slot_se[k] = args.slot_se[k];
   if (!prime) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) q[j] = j * 256 + tid < nload ? op[j * 256 + tid] : longlong2{0, 0};
@@ -361,11 +366,26 @@ int gpbs_hip_adapt(void* states, const void* deltas, const void* spin_sum, const
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-// Ownership attribution of one counter snapshot (in: host-visible HwcAttrIn;
-// st: device HwcAttrPrev; out: host-visible HwcAttrOut).
-int gpbs_hip_hwc_attribute(const void* in, void* st, void* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_hwc_attribute, dim3(1), dim3(256), 0, s, (const HwcAttrIn*)in, (HwcAttrPrev*)st,
-                     (HwcAttrOut*)out);
+// Ownership attribution of one counter snapshot.  h_in: the snapshot in
+// pinned host memory; d_in: a device staging buffer (HwcAttrIn-sized) -- the
+// counters and the live tenants' owned-time rows are copied there first
+// (one DMA-sized copy on the same stream) so the kernel's loads never wait
+// on PCIe; the scalars travel as kernel arguments.  st: device HwcAttrPrev;
+// out: host-visible HwcAttrOut.
+int gpbs_hip_hwc_attribute(const void* h_in, void* d_in, void* st, void* out, hipStream_t s) {
+  const HwcAttrIn* hin = (const HwcAttrIn*)h_in;
+  AttrArgs a{};
+  for (int k = 0; k < kNumPmc; ++k) a.slot_se[k] = hin->slot_se[k];
+  a.se_mode = hin->se_mode;
+  a.clean_pct = hin->clean_pct;
+  a.shared = hin->shared;
+  a.prime = hin->prime;
+  a.nt_hi = hin->nt_hi;
+  const u32 rows = (a.nt_hi == 0 || a.nt_hi > (u32)kMaxTenants) ? (u32)kMaxTenants : a.nt_hi;
+  const size_t bytes = offsetof(HwcAttrIn, own_cur) + (size_t)rows * kAttrP * sizeof(long long);
+  if (hipMemcpyAsync(d_in, h_in, bytes, hipMemcpyHostToDevice, s) != hipSuccess) return -5;
+  hipLaunchKernelGGL(k_hwc_attribute, dim3(1), dim3(256), 0, s, (const HwcAttrIn*)d_in, (HwcAttrPrev*)st,
+                     (HwcAttrOut*)out, a);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
