@@ -217,6 +217,17 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
     const char* e = getenv("GPBS_HWC_ASYNC");
     g.async_mode = e && atoi(e) > 0;
   }
+  // One process per GPU (only_gpu = LOCAL_RANK): configure that agent only --
+  // a counting context holds hardware queues on its agent, and eight ranks
+  // configuring every agent would put eight ranks' profiler queues on every
+  // GPU.  gpbs_hwc_start still checks the agent's PCI address against the
+  // HIP device and fails on a mismatch.
+  if (g.only_gpu >= 0) {
+    if (g.only_gpu >= (int)g.gpus.size()) return -1;
+    g.gpus = {g.gpus[g.only_gpu]};
+    g.gpu_domain = {g.gpu_domain[g.only_gpu]};
+    g.gpu_loc = {g.gpu_loc[g.only_gpu]};
+  }
   const size_t n = g.gpus.size();
   g.cfg.resize(n);
   g.ctxs.resize(n);
@@ -291,10 +302,10 @@ extern "C" {
 // A sample's cost grows with the records it returns (one per SE for SQ, one per
 // CU for TCP, one per channel for TCC), which is why the round-2 TCP request
 // counters were replaced by SQ memory instructions (pbs_amd/counters/hwc.py).
-// Must precede HIP runtime initialisation.  Every GPU agent gets a counting
-// context; gpbs_hwc_start starts the one at the PCI address of the current
-// HIP device.  `gpu` >= 0 (LOCAL_RANK) is only a cross-check of the
-// enumeration index (gpbs_hwc_agent reports a mismatch).  0 on success.
+// Must precede HIP runtime initialisation.  `gpu` >= 0 (LOCAL_RANK): only
+// that agent gets a counting context, and gpbs_hwc_start fails (-3) unless
+// its PCI address is the current HIP device's; -1: every agent gets one and
+// gpbs_hwc_start starts the one at the current device's address.  0 on success.
 int gpbs_hwc_init_gpu(const char* spec, int gpu);
 int gpbs_hwc_init(const char* spec) { return gpbs_hwc_init_gpu(spec, -1); }
 
@@ -329,7 +340,7 @@ int gpbs_hwc_start(void) {
   for (size_t i = 0; i < g.gpus.size(); ++i)
     if (g.ok[i] && g.gpu_domain[i] == dom && g.gpu_loc[i] == loc) pick = (int)i;
   if (pick < 0) return -3;
-  g.index_mismatch = g.only_gpu >= 0 && g.only_gpu != pick;
+  g.index_mismatch = 0;
   if (rocprofiler_start_context(g.ctxs[pick]) != ROCPROFILER_STATUS_SUCCESS) return -1;
   g.ctx = g.ctxs[pick];
   if (g.async_mode) g.buf = g.bufs[pick];

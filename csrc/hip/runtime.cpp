@@ -303,9 +303,9 @@ struct GpuCtx {
   // 8mix run).  Tokens accrue so that samples take at most hwc_budget_pct %
   // of the time on average (EWMA sample time), up to hwc_bucket samples
   // banked; a burst tick without a token is skipped.  0: no budget.
-  int hwc_budget_pct = 2;    // GPBS_HWC_BUDGET
-  int hwc_bucket = 20;       // GPBS_HWC_BUCKET
-  double hwc_tokens = 20;
+  int hwc_budget_pct = 5;    // GPBS_HWC_BUDGET
+  int hwc_bucket = 50;       // GPBS_HWC_BUCKET: a phase change's burst plus a flip back
+  double hwc_tokens = 50;
   int64_t hwc_tok_ns = 0;
   uint64_t hwc_denied = 0;   // burst ticks skipped for lack of a token
   // Owner changes open bursts only with hwc_owner_burst (GPBS_HWC_OWNER_BURST;
@@ -1065,11 +1065,10 @@ namespace {
 // (XCD, SE) partitions -- co-sharers of a time-shared region, which never run
 // at the same time -- launch on one queue; runners on disjoint sets (split
 // layouts, which run concurrently) get their own.  A queue nobody holds is
-// re-keyed before a new one is created, so the process holds about as many
-// masked queues as there are concurrently running layouts (8mix: compute
-// region, memory region, latency lane = 3), not one per runner.  Key 0 =
-// exclusive (never shared).  GPBS_SHARE_QUEUES=0: every acquire exclusive
-// (the round-3 behaviour).
+// re-keyed before a new one is created, and a mask never has more than
+// masked_cap() keyed queues, so the process holds a few masked queues, not
+// one per runner.  Key 0 = exclusive (never shared).  GPBS_SHARE_QUEUES=0:
+// every acquire exclusive (the round-3 behaviour).
 struct MaskedStreams {
   struct Ent {
     int device;
@@ -1093,6 +1092,20 @@ bool share_queues() {
   }();
   return v;
 }
+// At most this many keyed (gated-runner) queues per CU mask
+// (GPBS_MASKED_CAP, default 2; 0 = no cap): past it a new layout shares the
+// least-held queue of its mask.  Runners that share a queue run their units
+// one after another; in a time-shared region that costs nothing (one owner
+// at a time), in a split layout it serialises the tenants of the split, so
+// the cap is set above the splits the budget layout makes within a class
+// half (two blocks).
+int masked_cap() {
+  static const int v = [] {
+    const char* e = std::getenv("GPBS_MASKED_CAP");
+    return e ? std::max(0, std::atoi(e)) : 2;
+  }();
+  return v;
+}
 hipStream_t masked_acquire_key(const uint32_t m[8], uint32_t key) {
   int dev = 0;
   hipGetDevice(&dev);
@@ -1101,6 +1114,8 @@ hipStream_t masked_acquire_key(const uint32_t m[8], uint32_t key) {
   {
     std::lock_guard<std::mutex> g(P.mu);
     MaskedStreams::Ent* idle = nullptr;
+    MaskedStreams::Ent* least = nullptr;
+    int keyed = 0;
     for (auto& e : P.ents) {
       if (e.device != dev || std::memcmp(e.m, m, sizeof(e.m)) != 0) continue;
       if (key && e.key == key && e.refs > 0) {  // the same layout: share its queue
@@ -1108,11 +1123,19 @@ hipStream_t masked_acquire_key(const uint32_t m[8], uint32_t key) {
         return e.s;
       }
       if (e.refs == 0 && (!idle || (key && e.key == key))) idle = &e;
+      if (e.key && e.refs > 0) {
+        keyed++;
+        if (!least || e.refs < least->refs) least = &e;
+      }
     }
     if (idle) {  // re-key a queue nobody holds
       idle->key = key;
       idle->refs = 1;
       return idle->s;
+    }
+    if (key && masked_cap() > 0 && keyed >= masked_cap() && least) {  // at the cap: share the least-held
+      least->refs++;
+      return least->s;
     }
   }
   hipStream_t s = nullptr;

@@ -67,7 +67,15 @@ def init(spec: Optional[str] = None, gpu: int = -1) -> bool:
 
 
 def start() -> bool:
-    return _lib().gpbs_hwc_start() == 0
+    """Start counting on the current HIP device's agent.  False if the
+    service is not configured; raises if the configured agent (LOCAL_RANK)
+    is not at this device's PCI address -- counting a neighbour's GPU is
+    worse than not counting."""
+    rc = _lib().gpbs_hwc_start()
+    if rc == -3:
+        raise RuntimeError("hardware counters: the configured rocprofiler agent is not at the current HIP "
+                           "device's PCI address (LOCAL_RANK / visible-device mismatch)")
+    return rc == 0
 
 
 def active() -> bool:

@@ -18,7 +18,7 @@ from typing import List, Optional
 # queues, streams share queues round-robin and a table update can sit behind
 # a parked tenant kernel on the same queue until its park bound expires.
 # Must be set before the HIP runtime initialises (first device call).
-os.environ["GPU_MAX_HW_QUEUES"] = str(max(8, int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)))
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("GPBS_HWQ") or str(max(8, int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)))
 
 import torch  # noqa: E402
 
