@@ -1181,6 +1181,14 @@ void se_cu_mask(const u32 se_bits[kXcds], uint32_t m[8]) {
     if (se_bits[b % 8] & (1u << ((b / 8) % 4))) m[b / 32] |= 1u << (b % 32);
 }
 
+int runner_poll_us() {
+  static const int v = [] {
+    const char* e = std::getenv("GPBS_RUNNER_POLL_US");
+    return e ? std::max(0, std::atoi(e)) : 0;
+  }();
+  return v;
+}
+
 struct Runner {
   GpuCtx* ctx;
   gpbs_runner_cfg_t cfg;
@@ -1484,7 +1492,10 @@ struct Runner {
         fl.pop_front();
         while (hipEventQuery(ev[f.ev]) == hipErrorNotReady) {
           if (stop) break;
-          std::this_thread::yield();
+          if (runner_poll_us() > 0)  // GPBS_RUNNER_POLL_US: sleep between polls (host CPU vs detection latency)
+            std::this_thread::sleep_for(std::chrono::microseconds(runner_poll_us()));
+          else
+            std::this_thread::yield();
         }
         const u32 s = __atomic_load_n(&h_status[f.qi], __ATOMIC_ACQUIRE);
         const u32 done = s & 0x3fffffffu;

@@ -366,6 +366,34 @@ class CollTenant:
         self._loop.stop(agree)
 
 
+def host_cpu_sample() -> Dict[str, float]:
+    """This process's CPU time and context switches, and the cgroup's CPU
+    throttling (where readable): a run whose launch-bound tenants lose rate
+    while the GPU is idle shows here if the host threads were starved."""
+    out: Dict[str, float] = {}
+    try:
+        t = os.times()
+        out["cpu_s"] = t.user + t.system
+        with open("/proc/self/status") as f:
+            for ln in f:
+                if ln.startswith(("voluntary_ctxt_switches", "nonvoluntary_ctxt_switches")):
+                    k, v = ln.split(":")
+                    out[k.strip()] = float(v)
+    except OSError:
+        pass
+    for path in ("/sys/fs/cgroup/cpu.stat", "/sys/fs/cgroup/cpu/cpu.stat"):
+        try:
+            with open(path) as f:
+                for ln in f:
+                    k, v = ln.split()
+                    if k in ("nr_throttled", "throttled_usec", "throttled_time"):
+                        out["cg_" + k] = float(v)
+            break
+        except (OSError, ValueError):
+            continue
+    return out
+
+
 def kfd_queues(pid: Optional[int] = None) -> Optional[int]:
     """Hardware queues KFD holds for a process (sysfs; None where not exposed)."""
     try:
@@ -944,6 +972,7 @@ class Corun:
         self._barrier()
         t0 = time.perf_counter()
         g0 = time.monotonic()
+        h0 = host_cpu_sample()
         d0 = {n: self._work(n) for n in self.throughput}
         per_step = []
         for _ in range(steps):
@@ -962,6 +991,7 @@ class Corun:
         d1 = {n: self._work(n) for n in self.throughput}
         wall_ms_local = (time.perf_counter() - t0) * 1e3
         g1 = time.monotonic()
+        h1 = host_cpu_sample()
         self._barrier()
         wall_ms = self._allreduce(wall_ms_local, "max")
         # drain: drop the backlog, let in-flight units finish
@@ -990,6 +1020,9 @@ class Corun:
         nq = kfd_queues()
         if nq is not None:  # hardware queues this process holds (KFD): oversubscription shows here
             res["kfd_queues"] = nq
+        res["host"] = {k: round(h1[k] - h0[k], 3) for k in h1 if k in h0}
+        if "cpu_s" in res["host"]:
+            res["host"]["cpu_util"] = round(res["host"]["cpu_s"] / (wall_ms_local / 1e3), 2)  # cores busy
         agg, slows = 0.0, []
         for n in self.throughput:
             du, da = d1[n][0] - d0[n][0], d1[n][1] - d0[n][1]
