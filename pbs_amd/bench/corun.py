@@ -1157,9 +1157,11 @@ class Corun:
             diag = os.environ.get("GPBS_DIAG_DIR")
             if diag and self.rank == 0:
                 os.makedirs(diag, exist_ok=True)
-                recs = e.trace(max_records=1 << 18, from_start=True)
-                with open(os.path.join(diag, f"trace_{policy}.json"), "w") as f:
-                    json.dump({"tid": self.tid, "lat_ms": lats,
+                import gzip
+                recs = e.trace(max_records=1 << 16, from_start=False)
+                self._diag_n = getattr(self, "_diag_n", 0) + 1
+                with gzip.open(os.path.join(diag, f"trace_{policy}_{self._diag_n:02d}.json.gz"), "wt") as f:
+                    json.dump({"tid": self.tid, "lat_ms": lats, "aggregate": agg, "engine": eng,
                                "trace": [[r.t_ns, r.event, r.cpu, *r.a] for r in recs]}, f)
 
     def close(self):
