@@ -129,6 +129,7 @@ void gpbs_boot_defaults(gpbs_boot_params_t* p) {
   p->class_dwell = 2;
   p->class_budget = 0;
   p->present_us = 10000;
+  p->sibling_steal = 0;
   AdaptParams a;
   std::memcpy(&p->adapt, &a, sizeof(a));
   AtcParams t;

@@ -171,6 +171,16 @@ class CreditScheduler : public Scheduler {
   }
   Slot& curr(int cpu) { return E.curr_of(cpu); }
   Mask online() { return E.pools[pool_]->cpus; }
+  // Another runnable slot of v's tenant on `cpu` (running there or queued).
+  bool sibling_on(int cpu, const Slot& v) {
+    const Slot& c = curr(cpu);
+    if (&c != &v && !c.is_idle() && c.tenant == v.tenant && E.runnable(c)) return true;
+    for (int sid : pc(cpu).runq) {
+      const Slot& w = *E.slots[sid];
+      if (&w != &v && w.tenant == v.tenant) return true;
+    }
+    return false;
+  }
 
   void alloc_pdata(int cpu) override {
     auto p = std::make_unique<CPcpu>();
@@ -933,6 +943,18 @@ class CreditScheduler : public Scheduler {
         if (!soft_pass && !v.soft.empty() && !v.soft.test(cpu) &&
             E.now() - v.homed_at < std::max<int64_t>(1000000, 4 * (int64_t)ratelimit_us_ * 1000))
           continue;
+        // Budget layout, time-shared class region: every tenant of the region
+        // has a home slot on every partition of it, so a steal onto a
+        // partition that already holds a runnable sibling of the slot only
+        // stacks the tenant there and leaves a hole at the peer -- zero-sum
+        // for the tenant's share, and the class tick then sends it home
+        // (sleep + migrate + wake, a revocation of the runner's SEs each).
+        // 8mix traces: ~1900 such steals per GEMM tenant per run in the slow
+        // mode (0.68-1.00) vs ~500 in the fast one (1.13-1.17).
+        if (E.boot.class_budget && E.boot.class_split > 1 && !E.boot.sibling_steal && sibling_on(cpu, v)) {
+          E.perfc.incr(PC_steal_sibling_skip);
+          continue;
+        }
         if (!v.is_running && !hot && v.affinity.test(cpu)) {
           s.stats.migrate_q++;
           E.perfc.incr(PC_migrate_queued);

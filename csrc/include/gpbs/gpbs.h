@@ -16,7 +16,7 @@
 extern "C" {
 #endif
 
-#define GPBS_ABI_VERSION 3
+#define GPBS_ABI_VERSION 4
 
 /* Validation ranges (sysctl.h:568-579, libxl.c:4026-4101). Q1: the new API
  * also accepts the reference's boot default of 100us (see docs). */
@@ -84,6 +84,10 @@ typedef struct gpbs_boot_params {
                                   crowded region is split by blocks of whole XCDs instead of time-shared */
   int32_t present_us;          /* class_budget: a tenant with no runnable slot for this long leaves the layout
                                   (default 10000) */
+  int32_t sibling_steal;       /* class_budget: 1 = let an in-class steal stack a tenant's slot onto a partition that
+                                  already holds a runnable sibling (Xen semantics); 0 (default) skips such a peer slot --
+                                  in a time-shared region every tenant has a home on every partition, so the steal is
+                                  zero-sum and the class tick undoes it */
   gpbs_adapt_params_t adapt;
   gpbs_atc_params_t atc;
 } gpbs_boot_params_t;

@@ -27,7 +27,7 @@ class AtcParams(C.Structure):
                                    "wait_unit_ns")]
 
 
-ABI_VERSION = 3  # GPBS_ABI_VERSION in csrc/include/gpbs/gpbs.h
+ABI_VERSION = 4  # GPBS_ABI_VERSION in csrc/include/gpbs/gpbs.h
 
 
 class BootParams(C.Structure):
@@ -35,7 +35,7 @@ class BootParams(C.Structure):
         "tslice_us", "ratelimit_us", "smt_power_savings", "tickle_one_idle", "default_yield", "migration_delay_us",
         "metric_period_us", "slice_apply_us", "sim_clock", "pmu_refresh_us", "dom0_quirk", "heartbeat_timeout_us",
         "trace_capacity", "quantum_align_us", "coschedule", "class_period_us", "boost_exclusive",
-        "class_split", "idle_skip", "class_dwell", "class_budget", "present_us")] + [("adapt", AdaptParams),
+        "class_split", "idle_skip", "class_dwell", "class_budget", "present_us", "sibling_steal")] + [("adapt", AdaptParams),
                                                                                     ("atc", AtcParams)]
 
 

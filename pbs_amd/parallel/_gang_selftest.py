@@ -24,6 +24,7 @@ def worker(rank: int, world: int, port: int, q, seconds: float = 0.8, epoch_ms: 
     e.start()
     e.wake(hog)
     e.wake(coll)
+    dist.barrier()
     g = GangCoordinator(e, None, [coll], epoch_ms=epoch_ms, share=0.5).start()
     samples = []  # (epoch, state, fraction of partitions running coll)
     t_end = time.monotonic() + seconds
@@ -61,6 +62,7 @@ def atc_worker(rank: int, world: int, port: int, q, seconds: float = 0.8, epoch_
     t = e.tenant_create("t", nslots=2)
     e.start()
     e.wake(t)
+    dist.barrier()  # spawn start-up skew on a busy host would eat the short window
     g = GangCoordinator(e, None, [t], epoch_ms=epoch_ms, share=0.0, atc_pool=0, metric_tenants=[t],
                         metric_every=2).start()
     t_end = time.monotonic() + seconds

@@ -211,3 +211,35 @@ def test_time_shared_region_rotates_in_one_quantum():
     mem = [share[m] for m in ms]
     assert min(mem) > 3.5 and max(mem) - min(mem) < 0.6, share
     assert e.check() == ""
+
+
+def test_time_shared_region_steals_no_stacking_siblings():
+    """8mix shape (3 compute + 4 memory tenants, 16 slots each online): every
+    tenant of a time-shared class region has a home slot on every partition
+    of it, so an in-class steal onto a partition that already holds the
+    tenant's sibling only stacks it (and the class tick undoes it: sleep +
+    migrate + wake, a runner revocation each).  Round-4 MI355X traces of the
+    slow 8mix mode showed ~1900 such steals per GEMM tenant per 1.6 s run.
+    The default skips them (perfc steal_sibling_skip) without changing the
+    shares; sibling_steal=1 restores the Xen behaviour."""
+    out = {}
+    for ss in (1, 0):
+        e, parts = _engine(sibling_steal=ss)
+        ws = (512, 256, 256, 256, 256, 256, 256)  # a heavier tenant keeps UNDER slots queued on busy peers
+        ts = [e.tenant_create(f"t{i}", nslots=32, weight=w) for i, w in enumerate(ws)]
+        rates = {t: (COMPUTE if i < 3 else MEMORY) for i, t in enumerate(ts)}
+        for t in ts:
+            e.wake(t)
+        _settle(e, rates, 300)
+        e.perfc_reset()
+        r0 = {t: e.tenant_info(t).run_ns for t in ts}
+        _settle(e, rates, 2000)
+        pc = e.perfc()
+        share = [(e.tenant_info(t).run_ns - r0[t]) / 200e6 for t in ts]
+        out[ss] = (pc["migrate_queued"], pc["steal_sibling_skip"], pc["vcpu_sleep"], share)
+        assert e.check() == ""
+    assert out[1][0] > 20 and out[1][1] == 0, out  # Xen semantics: stacking steals happen
+    assert out[0][0] == 0 and out[0][1] > 0 and out[0][2] == 0, out  # guarded: none, no send-home churn
+    for a, b in zip(out[0][3][:3], out[1][3][:3]):  # the compute region's shares unchanged (partitions' worth);
+        assert abs(a - b) < 0.3, out                # the memory tenants' 11 ms quanta are too coarse for 200 ms
+    assert out[0][3][0] > max(out[0][3][1:3]) + 1.0, out  # the weight still counts
