@@ -219,6 +219,8 @@ POLICY_ENGINES = {
     "gpbs-r3s": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
     "gpbs-b5": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
     "gpbs-model": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
+    "gpbs-d5": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
+    "gpbs-d10": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
     # the same without the latency lane (GEMV co-resident on every CU)
     "gpbs-nolane": (4, dict(BUDGET_OVERRIDES), True, "device,se,waveprio,latco,budget"),
     # round-2 flagship: fixed class halves, memory tenants one SE each by
@@ -256,6 +258,10 @@ SAMPLER = {
     "gpbs-r3s": dict(budget_pct=0, owner_burst=1, fallback=0),
     "gpbs-b5": dict(budget_pct=5, owner_burst=1, fallback=1),
     "gpbs-model": "model",
+    # background cadence: the duty cap (default 1 %) sets the period from the
+    # ~0.2 ms sample cost; 5 % -> ~4 ms, 10 % -> ~2 ms (budget raised with it)
+    "gpbs-d5": dict(budget_pct=8, duty=5),
+    "gpbs-d10": dict(budget_pct=15, duty=10),
 }
 
 

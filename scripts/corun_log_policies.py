@@ -17,8 +17,13 @@ for path in sys.argv[1:]:
     for l in open(path):
         if l.startswith("[corun] ") and ': {"policy"' in l:
             pol = l[len("[corun] "):l.index(":")]
-            runs.setdefault(pol, []).append(json.loads(l[l.index("{"):]))
-for pol, rs in sorted(runs.items(), key=lambda kv: -q([r["aggregate"] for r in kv[1]], 0.5)):
+            r = json.loads(l[l.index("{"):])
+            mix = "+".join(sorted(r.get("tenants", {})))  # one log can hold several mixes: key by tenant set
+            runs.setdefault((mix, pol), []).append(r)
+mixes = sorted({k[0] for k in runs})
+for (mix, pol), rs in sorted(runs.items(), key=lambda kv: (kv[0][0], -q([r["aggregate"] for r in kv[1]], 0.5))):
+    if len(mixes) > 1:
+        pol = f"[{'/'.join(t[:4] for t in mix.split('+'))}] {pol}"
     a = [r["aggregate"] for r in rs]
     e = [r.get("engine", {}) for r in rs]
     ten = {n: round(statistics.median(r["tenants"][n]["norm_perf"] for r in rs), 3) for n in rs[0]["tenants"]}
