@@ -2010,7 +2010,9 @@ int gpbs_hip_hwc_attr_bench(int iters, double* out2) {
       in->own_cur[(1 + p % 4) * kAttrP + p] = 1000000;
       for (int k = 0; k < kNumPmc; ++k) in->se_cur[p * kNumPmc + k] = 1000 + p * 7 + k;
     }
-    for (int k = 0; k < kNumPmc; ++k) in->slot_se[k] = k < 3;
+    // slot layouts: the default (0-2 per SE, 3 per XCD), slot 2 per XCD (the
+    // L2-miss split by XCD-level requests), every slot per SE
+    for (int k = 0; k < kNumPmc; ++k) in->slot_se[k] = it % 6 == 1 ? (k < 2) : it % 6 == 5 ? 1u : (k < 3);
     in->se_mode = 1;
     in->clean_pct = 90;
     in->prime = 0;
@@ -2073,7 +2075,8 @@ int gpbs_hip_hwc_attr_selftest(int seed, int iters, double* max_rel) {
   for (int it = 0; it <= iters && rc == 0; ++it) {
     // a random ownership pattern: most partitions with one dominant owner, some time-shared, some idle
     for (int p = 0; p < kAttrP; ++p) {
-      const int kind = (int)(rnd() % 8);
+      int kind = (int)(rnd() % 8);
+      if (it % 4 == 2 && p / kCtx == 5) kind = 7;  // a whole idle XCD (no owner: unexplained counts)
       const int a = 1 + (int)(rnd() % 6), b = 1 + (int)(rnd() % 6);
       const long long span = 1000000;
       for (int t = 0; t < kMaxTenants; ++t) {
@@ -2087,7 +2090,9 @@ int gpbs_hip_hwc_attr_selftest(int seed, int iters, double* max_rel) {
       for (int k = 0; k < kNumPmc; ++k) in->se_cur[p * kNumPmc + k] += rnd() % 100000000ull;
     }
     for (int i = 0; i < kXcds * kNumPmc; ++i) in->x_cur[i] += rnd() % 1000000000ull;
-    for (int k = 0; k < kNumPmc; ++k) in->slot_se[k] = k < 3;
+    // slot layouts: the default (0-2 per SE, 3 per XCD), slot 2 per XCD (the
+    // L2-miss split by XCD-level requests), every slot per SE
+    for (int k = 0; k < kNumPmc; ++k) in->slot_se[k] = it % 6 == 1 ? (k < 2) : it % 6 == 5 ? 1u : (k < 3);
     in->se_mode = (it % 5) != 4;
     in->clean_pct = it % 7 == 3 ? 0 : 90;
     in->shared = it % 11 == 10;

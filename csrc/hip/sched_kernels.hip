@@ -118,7 +118,7 @@ __global__ __launch_bounds__(256) void k_hwc_attribute(const HwcAttrIn* __restri
   constexpr int NC = (P + X) * K / 2;  // 16-byte counter loads (80)
   __shared__ double ownT[P][T + 1];    // owned ns of the interval, [partition][tenant], padded
   __shared__ double vse[P][K], vx[X][K];
-  __shared__ double tot_p[P], inv_p[P], tot_x[X], inv_x[X];
+  __shared__ double tot_p[P], inv_p[P], tot_x[X], inv_x[X], vsc[P][K], refx[X], inv_refx[X];
   __shared__ int clean_owner[P], xcd_owner[X];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const u32 prime = args.prime;
@@ -194,6 +194,27 @@ __global__ __launch_bounds__(256) void k_hwc_attribute(const HwcAttrIn* __restri
     }
   }
   __syncthreads();
+  // 3b. everything lane-independent, once: per-XCD owners and totals (threads
+  // 0-7), each (partition, SE slot)'s count scaled by its partition's
+  // reciprocal (64-191), the per-slot hardware sums / unexplained counts
+  // (192-195) and slot 2's attributable L2 requests per XCD (200-207, the
+  // denominator of the miss split -- the sum over tenants of their slot-2
+  // shares, so no wave reduction is needed for it)
+  const bool se2 = se_mode && slot_se[2];
+  auto refs_tot = [&](const int x) {
+    double r = 0;
+    if (se2) {
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        if (tot_p[x * E + e] > 0) r += vse[x * E + e][2];
+    } else {
+      double tx = 0;
+#pragma unroll
+      for (int e = 0; e < E; ++e) tx += tot_p[x * E + e];
+      if (tx > 0) r = vx[x][2];
+    }
+    return r;
+  };
   if (tid < X) {
     int o = -1;
     bool ok = true;
@@ -209,92 +230,88 @@ __global__ __launch_bounds__(256) void k_hwc_attribute(const HwcAttrIn* __restri
     for (int e = 0; e < E; ++e) tx += tot_p[tid * E + e];
     tot_x[tid] = tx;
     inv_x[tid] = tx > 0 ? 1.0 / tx : 0.0;
+  } else if (tid >= 64 && tid < 64 + P * K) {
+    const int p = (tid - 64) / K, k = (tid - 64) % K;
+    vsc[p][k] = tot_p[p] > 0 ? vse[p][k] * inv_p[p] : 0.0;
+  } else if (tid >= 192 && tid < 192 + K) {
+    const int k = tid - 192;
+    double hs = 0, ua = 0;
+    if (se_mode && slot_se[k]) {
+      for (int p = 0; p < P; ++p) {
+        hs += vse[p][k];
+        if (tot_p[p] <= 0) ua += vse[p][k];
+      }
+    } else {
+      for (int x = 0; x < X; ++x) {
+        double tx = 0;
+        for (int e = 0; e < E; ++e) tx += tot_p[x * E + e];
+        const double tot = (k == 3 && refs_tot(x) > 0) ? 1.0 : tx;
+        hs += vx[x][k];
+        if (tot <= 0) ua += vx[x][k];
+      }
+    }
+    out->hw_sum[k] = hs;
+    out->unatt[k] = ua;
+  } else if (tid >= 200 && tid < 200 + X) {
+    const double r = refs_tot(tid - 200);
+    refx[tid - 200] = r;
+    inv_refx[tid - 200] = r > 0 ? 1.0 / r : 0.0;
   }
   __syncthreads();
   // 4. attribution, lane = tenant, wave k = counter slot k; the four waves
-  // never wait for each other: wave 3's L2 misses are split by slot 2's L2
-  // requests, which it recomputes itself (registers) before its own pass
+  // never wait for each other: wave 3's L2 misses are split by this lane's
+  // slot-2 shares, which it recomputes in registers (a few FMAs per XCD)
   const int t = lane;
-  double rx[X], rcx[X];
+  const int k = wave;
+  double add = 0, addc = 0;
+  if (se_mode && slot_se[k]) {
 #pragma unroll
-  for (int x = 0; x < X; ++x) rx[x] = rcx[x] = 0.0;
-  auto pass = [&](const int k, const bool emit) {
-    double add = 0, addc = 0, hs = 0, ua = 0;
-    if (se_mode && slot_se[k]) {
-#pragma unroll
-      for (int x = 0; x < X; ++x) {
-        double sx = 0, scx = 0;
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          const int p = x * E + e;
-          const double v = vse[p][k];
-          hs += v;
-          if (tot_p[p] <= 0) {
-            ua += v;
-            continue;
-          }
-          const double w = ownT[p][t];
-          if (w <= 0) continue;
-          const double a = v * w * inv_p[p];
-          add += a;
-          sx += a;
-          if (clean_owner[p] == t) {
-            addc += a;
-            scx += a;
-          }
-        }
-        if (k == 2) {
-          rx[x] = sx;
-          rcx[x] = scx;
-        }
-      }
-    } else {
-      const bool miss_by_refs = k == 3;
-      const bool refs_clean = miss_by_refs && se_mode && slot_se[2];
-#pragma unroll
-      for (int x = 0; x < X; ++x) {
-        const double v = vx[x][k];
-        double tot = 0, wt = 0, inv = 0;
-        bool by_refs = false;
-        if (miss_by_refs) {
-          wt = rx[x];
-          tot = wave_sum64(wt);
-          by_refs = tot > 0;
-          inv = by_refs ? 1.0 / tot : 0.0;
-        }
-        if (!by_refs) {
-          tot = tot_x[x];
-          inv = inv_x[x];
-          wt = 0;
-#pragma unroll
-          for (int e = 0; e < E; ++e) wt += ownT[x * E + e][t];
-        }
-        hs += v;
-        if (tot <= 0) {
-          ua += v;
-          continue;
-        }
-        if (wt <= 0) continue;
-        const double a = v * wt * inv;
-        add += a;
-        if (k == 2) rx[x] = a;
-        if (refs_clean)
-          addc += v * rcx[x] * inv;
-        else if (xcd_owner[x] == t)
-          addc += a;
-      }
+    for (int p = 0; p < P; ++p) {
+      const double a = ownT[p][t] * vsc[p][k];  // 0 for an unowned partition or an idle tenant
+      add += a;
+      if (clean_owner[p] == t) addc += a;
     }
-    if (emit) {
-      out->add[t][k] = add;
-      out->addc[t][k] = addc;
-      if (lane == 0) {
-        out->hw_sum[k] = hs;
-        out->unatt[k] = ua;
+  } else {
+    const bool miss_by_refs = k == 3;
+#pragma unroll
+    for (int x = 0; x < X; ++x) {
+      const double v = vx[x][k];
+      double wt = 0, inv = inv_x[x], rcx = 0;
+      bool by_refs = false;
+      if (miss_by_refs && refx[x] > 0) {  // this lane's slot-2 share on XCD x
+        by_refs = true;
+        inv = inv_refx[x];
+        if (se2) {
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            const int p = x * E + e;
+            const double a = ownT[p][t] * vsc[p][2];
+            wt += a;
+            if (clean_owner[p] == t) rcx += a;
+          }
+        } else {
+          double w = 0;
+#pragma unroll
+          for (int e = 0; e < E; ++e) w += ownT[x * E + e][t];
+          wt = vx[x][2] * w * inv_x[x];
+        }
       }
+      if (!by_refs) {
+        if (tot_x[x] <= 0) continue;
+#pragma unroll
+        for (int e = 0; e < E; ++e) wt += ownT[x * E + e][t];
+      }
+      if (wt <= 0) continue;
+      const double a = v * wt * inv;
+      add += a;
+      if (miss_by_refs && se2)
+        addc += v * rcx * inv;
+      else if (xcd_owner[x] == t)
+        addc += a;
     }
-  };
-  if (wave == 3) pass(2, false);  // slot 2's L2-request shares, this lane's
-  pass(wave, true);
+  }
+  out->add[t][k] = add;
+  out->addc[t][k] = addc;
   __syncthreads();
   if (tid == 0) {
     out->pad[0] = t_entry;
