@@ -2010,9 +2010,7 @@ int gpbs_hip_hwc_attr_bench(int iters, double* out2) {
       in->own_cur[(1 + p % 4) * kAttrP + p] = 1000000;
       for (int k = 0; k < kNumPmc; ++k) in->se_cur[p * kNumPmc + k] = 1000 + p * 7 + k;
     }
-    // slot layouts: the default (0-2 per SE, 3 per XCD), slot 2 per XCD (the
-    // L2-miss split by XCD-level requests), every slot per SE
-    for (int k = 0; k < kNumPmc; ++k) in->slot_se[k] = it % 6 == 1 ? (k < 2) : it % 6 == 5 ? 1u : (k < 3);
+    for (int k = 0; k < kNumPmc; ++k) in->slot_se[k] = k < 3;
     in->se_mode = 1;
     in->clean_pct = 90;
     in->prime = 0;

@@ -11,7 +11,7 @@
 //   k_hwc_attribute    : ownership attribution of one live-counter snapshot
 //                        to tenants (csrc/hip/hwc_attr.h): one workgroup,
 //                        the snapshot staged into LDS in one pass of wide
-//                        loads, wave reductions / ballots per partition, a
+//                        loads, 8-lane reductions / ballots per partition, a
 //                        lane per tenant and a wave per counter slot; the
 //                        previous snapshot stays resident in device memory.
 #include <cstddef>
@@ -77,28 +77,21 @@ __global__ __launch_bounds__(64) void k_adapt(gpbs_adapt_state_t* states, const 
 }
 
 
-// Full-wave sum (64 lanes, butterfly over cross-lane moves).
-__device__ inline double wave_sum64(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
-
 // One workgroup of 256 threads (4 waves); lane = tenant (kMaxTenants == the
-// 64-lane wavefront).  The snapshot lives in pinned host memory, so every
-// read of it is a PCIe round trip: the kernel stages it into LDS ONCE, with
-// all 16-byte loads issued before any is used (the round-3 kernel re-read it
-// inside its per-tenant loops: 78 us per call).  Then
-//   * per-partition owned-time totals: one wave reduction per partition,
-//     8 partitions per wave (the owned ns are integers, so the totals are
-//     exact in any order);
+// 64-lane wavefront).  The host copies the live rows of the snapshot to
+// device memory first (hipMemcpyAsync; round 3 read pinned host memory inside
+// the per-tenant loops: 78 us per call); the kernel stages them into LDS with
+// every 16-byte load in flight at once.  Then
+//   * per-partition owned-time totals: 8 threads per partition, a 3-step
+//     butterfly (integer ns: exact in any order);
 //   * clean owners: the last tenant over the clean_pct threshold, from a
 //     wave ballot per partition;
+//   * everything lane-independent once: per-XCD owners and totals, each
+//     (partition, SE slot)'s count times its partition's reciprocal, the
+//     per-slot hardware sums, slot 2's attributable L2 requests per XCD;
 //   * attribution: wave k attributes counter slot k for all 64 tenants at
-//     once, the four waves independently (wave 3 recomputes slot 2's
-//     L2-request shares in registers to split the L2 misses) -- each lane
-//     sums its partitions in the host order, dividing by a per-partition
-//     reciprocal computed once.
+//     once, the four waves independently (wave 3 splits the L2 misses by its
+//     lane's slot-2 shares, a few FMAs per XCD in registers).
 // The previous snapshot and the clean-owner history stay in device memory.
 struct AttrArgs {  // the snapshot's scalars, by value (no dependent load before the staging loads)
   u32 slot_se[kNumPmc];
@@ -167,12 +160,20 @@ __global__ __launch_bounds__(256) void k_hwc_attribute(const HwcAttrIn* __restri
     return;
   }
   __syncthreads();
-  // 2. owned-time totals per partition
+  // 2. owned-time totals per partition: 8 threads per partition sum 8
+  // tenants each, then a 3-step butterfly (the owned ns are integers, so the
+  // totals are exact in any order) -- 3 cross-lane steps instead of a 6-step
+  // wave reduction per partition, and the 32 reciprocals in parallel
+  {
+    static_assert(P * 8 == 256 && T == 64, "8 threads x 8 tenants per partition");
+    const int p = tid >> 3, part = tid & 7;
+    double s = 0;
 #pragma unroll
-  for (int i = 0; i < P / 4; ++i) {
-    const int p = wave * (P / 4) + i;
-    const double s = wave_sum64(ownT[p][lane]);
-    if (lane == 0) {
+    for (int j = 0; j < 8; ++j) s += ownT[p][part * 8 + j];
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    s += __shfl_xor(s, 4, 64);
+    if (part == 0) {
       tot_p[p] = s;
       inv_p[p] = s > 0 ? 1.0 / s : 0.0;
     }
