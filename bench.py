@@ -155,9 +155,10 @@ def main():
                          "attributed to tenants by shader-engine ownership; default), or the modeled per-tile "
                          "counters of the tenant kernels (debug cross-check)")
     ap.add_argument("--mix", default="all", choices=["all", "4mix", "gemm2", "phase", "phase-ts", "8mix", "llm5"],
-                    help="all (default): 4mix (headline, BASELINE config #3) + phase (phase-changing mix) + 8mix "
-                         "(config #4's 8 tenants on one GPU); gemm2: config #2 (two 4096^2 GEMM tenants); "
-                         "phase-ts: the phase mix with a time-shared memory region; "
+                    help="all (default): 4mix (headline, BASELINE config #3) + phase (phase-changing mix) + "
+                         "phase-ts (the phase mix with a time-shared memory region, where the adaptive quantum "
+                         "matters) + 8mix (config #4's 8 tenants on one GPU); gemm2: config #2 (two 4096^2 GEMM "
+                         "tenants); "
                          "llm5: config #5 (Llama-3-8B fp8 decode + Llama-1B-shaped bf16 trainer, torch tenants "
                          "on the shim under gpbsd; not in the default run)")
     ap.add_argument("--reps-extra", type=int, default=5, help="reps of the non-headline mixes")
@@ -232,7 +233,7 @@ def main():
         dist.broadcast(nonce, src=0, group=groups["ctrl"])
         gang_base = f"gpbs-gang-{int(nonce.item()):08x}"
 
-    mixes = ["4mix", "phase", "8mix"] if args.mix == "all" else [args.mix]
+    mixes = ["4mix", "phase", "phase-ts", "8mix"] if args.mix == "all" else [args.mix]
     log = (lambda *a: print(*a, file=sys.stderr, flush=True))
     import random
 

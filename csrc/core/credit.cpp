@@ -982,7 +982,9 @@ class CreditScheduler : public Scheduler {
     // partition first; then, only for an otherwise idle partition, any slot
     // hard affinity allows (cross-class work conservation).
     for (int step = 0; step < 2; ++step) {
-      if (step == 1 && s.pri != PRI_IDLE) break;
+      if (step == 1 && (s.pri != PRI_IDLE ||
+                        (E.boot.class_budget && E.boot.class_split > 1 && !E.boot.class_steal)))
+        break;
       Mask workers = online().andnot(idlers_);
       workers.clear(cpu);
       int peer = cpu;

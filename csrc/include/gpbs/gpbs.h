@@ -88,6 +88,10 @@ typedef struct gpbs_boot_params {
                                   already holds a runnable sibling (Xen semantics); 0 (default) skips such a peer slot --
                                   in a time-shared region every tenant has a home on every partition, so the steal is
                                   zero-sum and the class tick undoes it */
+  int32_t class_steal;         /* class_budget: 1 (default) = an idle partition may steal a slot of the other class
+                                  (Xen 4.5's second balance step, work conservation); 0 = only the relayout after
+                                  present_us hands an absent class's partitions over -- a short gap in one tenant's
+                                  work no longer pulls the other class's runner onto an unmasked queue */
   gpbs_adapt_params_t adapt;
   gpbs_atc_params_t atc;
 } gpbs_boot_params_t;

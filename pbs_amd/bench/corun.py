@@ -220,6 +220,9 @@ POLICY_ENGINES = {
     "gpbs-b5": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
     "gpbs-model": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
     "gpbs-d5": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
+    # no cross-class steals by idle partitions (boot class_steal=0)
+    "gpbs-nox": (4, dict(BUDGET_OVERRIDES, class_budget=1, class_steal=0), True,
+                 "device,se,waveprio,latco,budget,latmem"),
     "gpbs-d10": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
     # the same without the latency lane (GEMV co-resident on every CU)
     "gpbs-nolane": (4, dict(BUDGET_OVERRIDES), True, "device,se,waveprio,latco,budget"),

@@ -195,7 +195,8 @@ def run(policy: str, kinds, args: dict, seconds: float, warmup: float) -> Dict[s
     # GPU_MAX_HW_QUEUES=N), +pre (both SE-half streams created at registration),
     # +nohwc (daemon on modeled counters), +swapN (static split: the first N s
     # on the swapped halves), +one (one masked queue per shim tenant), +qpK
-    # (K masked queues per half, chosen by measured slice time)
+    # (K masked queues per half, chosen by measured slice time), +nox (no
+    # cross-class steals by idle partitions)
     policy, *mods = policy.split("+")
     policy = ALIASES.get(policy, policy)
     base = policy.split("@")[0]
@@ -214,6 +215,8 @@ def run(policy: str, kinds, args: dict, seconds: float, warmup: float) -> Dict[s
             args["queue_probe"] = int(m[2:])
         elif m == "nohwc":
             args["nohwc"] = True
+        elif m == "nox":  # budget layout without cross-class steals (boot class_steal=0)
+            args["class_steal"] = 0
         elif m.startswith("swap"):
             args["swap_s"] = float(m[4:])
         else:
@@ -235,6 +238,8 @@ def run(policy: str, kinds, args: dict, seconds: float, warmup: float) -> Dict[s
             # (probe layout until both tenants are classified, then compute
             # SEs {0,1} / memory SEs {2,3}), surplus slots offline
             over.update(class_budget=1, present_us=10000)
+            if "class_steal" in args:
+                over["class_steal"] = args["class_steal"]
         daemon = Daemon(sock, gpus=[0], nctx=4, sim=False, profile="mi355x", attach_gpu=True, se_mode=True,
                         hw_counters=_HWC["on"] and not args.get("nohwc"), overrides=over).start()
         args["slots"] = 16

@@ -243,3 +243,38 @@ def test_time_shared_region_steals_no_stacking_siblings():
     for a, b in zip(out[0][3][:3], out[1][3][:3]):  # the compute region's shares unchanged (partitions' worth);
         assert abs(a - b) < 0.3, out                # the memory tenants' 11 ms quanta are too coarse for 200 ms
     assert out[0][3][0] > max(out[0][3][1:3]) + 1.0, out  # the weight still counts
+
+
+def test_class_steal_off_keeps_a_short_gap_in_its_class():
+    """boot class_steal=0: while the compute tenant pauses for 3 ms (less than
+    present_us, so the layout stays), slots waiting in the time-shared memory
+    region do not steal the idle compute partitions (on a GPU every such
+    steal moves a runner onto an unmasked queue next to the returning owner --
+    config #5's decode p99).  class_steal=1 keeps Xen's cross-class work
+    conservation (load_balance's second step)."""
+    out = {}
+    for cs in (1, 0):
+        e, parts = _engine(class_steal=cs)
+        # three memory tenants time-share the two memory SEs: slots wait there
+        g, h, r, h2 = (e.tenant_create(n, nslots=32) for n in ("gemm", "hbm", "coll", "hbm_b"))
+        rates = {g: COMPUTE, h: MEMORY, r: MEMORY, h2: MEMORY}
+        for t in rates:
+            e.wake(t)
+        _settle(e, rates)
+        mig0 = e.perfc()["migrate_queued"]
+        e.block(g)
+        on_compute = 0
+        for i in range(30):  # 3 ms; the all-reduce's runner drains and refills every ms (wakes tickle idlers)
+            if i % 10 == 5:
+                e.block(r)
+            elif i % 10 == 6:
+                e.wake(r)
+            _feed(e, {h: MEMORY, r: MEMORY, h2: MEMORY}, 100)
+            own = _ctx_owners(e, parts)
+            on_compute = max(on_compute, sum(own[c][t] for c in (0, 1) for t in (h, r, h2)))
+        e.wake(g)
+        _settle(e, rates, 100)
+        out[cs] = (on_compute, e.perfc()["migrate_queued"] - mig0, _online(e, g))
+        assert e.check() == ""
+    assert out[1][0] > 0 and out[1][1] > 0, out  # Xen semantics: the idle compute SEs run memory slots
+    assert out[0][0] == 0 and out[0][2] == 16, out  # guarded: the gap stays a gap, the layout unchanged
