@@ -321,7 +321,7 @@ def main(argv=None):
             "tenant_hwq": a.tenant_hwq, "prestream": a.prestream}
     res = {}
     pols = [p for p in a.policies.split(",") if p]
-    if "gpbs-se" in pols or "gpbs-budget" in pols:
+    if any(p.split("+")[0] in ("gpbs-se", "gpbs-budget") for p in pols):  # variants (+hwq2, +nox ...) too
         _hwc_setup()
     if a.out and os.path.exists(a.out):
         raise SystemExit(f"{a.out} exists: results are never overwritten")
