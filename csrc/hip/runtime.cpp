@@ -322,6 +322,19 @@ struct GpuCtx {
   double mod_inflight[kMaxTenants][kNumPmc] = {};  // ... of the snapshot whose attribution is in flight
   uint64_t fallback_periods = 0, clean_periods = 0;
   int hwc_watch = 1;      // GPBS_HWC_WATCH: read the modeled block every tick (the burst trigger)
+  // Fused metric (GPBS_HWC_FUSE, K9): a hardware sample stalls the command
+  // processor ~0.2 ms, so at the 1 % duty cap live data arrives every ~20 ms
+  // (faster cadence measured a net loss, profiles/r4/hwc_cadence_s13.txt).
+  // With the fuse on, the PBS metric gets a value EVERY tick: the tick's
+  // modeled per-tile deltas (the watch read, no command-processor work)
+  // scaled per tenant and counter by the hardware/model ratio of its latest
+  // hardware windows (EWMA); the hardware samples calibrate instead of
+  // reporting.  Tenants without modeled counters (shim tenants) keep the
+  // hardware deltas.
+  int hwc_fuse = 0;
+  double cal[kMaxTenants][kNumPmc] = {};  // 0: not calibrated yet (raw modeled deltas)
+  std::vector<u64> tick_blk, tick_prev;   // newest watch read / the one the previous tick consumed (snap_mu)
+  uint64_t tick_seq = 0, tick_used = 0, fuse_ticks = 0, cal_updates = 0;
   int64_t hwc_next_period_ns = 1000000;
   std::atomic<uint64_t> hwc_triggers{0};
   uint64_t hwc_burst_samples = 0;
@@ -608,6 +621,11 @@ void hwc_loop(GpuCtx* c) {
       hipEventRecord(c->blk_ev, c->hwc_stream);
       hipEventSynchronize(c->blk_ev);
       std::memcpy(blk.data(), c->h_blk, sizeof(u64) * kBlk);
+      if (c->hwc_fuse) {  // the metric tick's modeled deltas
+        std::lock_guard<std::mutex> g(c->snap_mu);
+        c->tick_blk = blk;
+        c->tick_seq++;
+      }
     }
     bool trig = false;
     for (int t = 0; t < kMaxTenants; ++t) {
@@ -697,8 +715,19 @@ void hwc_fold(GpuCtx* c, const HwcAttrOut& o, const double (*mod)[kNumPmc]) {
     const bool fallback = !clean && c->model_fallback && mod && o.add[t][0] > 0 && mod[t][0] > 0;
     if (clean && o.add[t][0] > 0) c->clean_periods++;
     if (fallback) c->fallback_periods++;
+    // fused metric: a modeled tenant's hardware window calibrates its ticks
+    const bool fused = c->hwc_fuse && mod && mod[t][0] > 0;
+    if (fused && o.add[t][0] > 0) {
+      for (int k = 0; k < kNumPmc; ++k)
+        if (mod[t][k] > 0) {
+          const double r = o.add[t][k] / mod[t][k];
+          c->cal[t][k] = c->cal[t][k] > 0 ? 0.75 * c->cal[t][k] + 0.25 * r : r;
+        }
+      c->cal_updates++;
+    }
     for (int k = 0; k < kNumPmc; ++k) {
       if (o.add[t][k] > 0) c->att_total[t][k] += o.add[t][k];
+      if (fused) continue;  // its metric comes from the calibrated ticks
       const double m = fallback ? mod[t][k] : (c->clean_pct > 0 ? o.addc[t][k] : o.add[t][k]);
       if (m > 0) {
         c->last_delta[t][k] += (u64)(m + 0.5);
@@ -805,9 +834,29 @@ int hwc_tenant_deltas(GpuCtx* c, int n, const int* tenants, uint64_t* out) {
   {
     std::lock_guard<std::mutex> g(c->snap_mu);
     hwc_consume(c, false);
+    if (c->hwc_fuse && c->tick_seq != c->tick_used && !c->tick_blk.empty()) {
+      if (c->tick_prev.size() == c->tick_blk.size())
+        for (int t = 0; t < kMaxTenants; ++t)
+          for (int k = 0; k < kNumPmc; ++k) {
+            double md = 0;
+            for (int x = 0; x < kXcds; ++x) {
+              const size_t i = ((size_t)t * kXcds + x) * kNumPmc + k;
+              md += (double)dpos(c->tick_blk[i], c->tick_prev[i]);
+            }
+            if (md <= 0) continue;
+            const double m = c->cal[t][k] > 0 ? md * c->cal[t][k] : md;
+            c->last_delta[t][k] += (u64)(m + 0.5);
+            c->metric_sum[k] += m;
+            c->met_total[t][k] += m;
+          }
+      c->tick_prev.swap(c->tick_blk);
+      c->tick_blk.clear();
+      c->tick_used = c->tick_seq;
+      c->fuse_ticks++;
+    }
   }
-  // No new snapshot since the previous tick: every tenant reads zero
-  // instructions and the PBS idle-sample rule (Q14) skips the period.
+  // No new snapshot since the previous tick (fuse off): every tenant reads
+  // zero instructions and the PBS idle-sample rule (Q14) skips the period.
   for (int k = 0; k < n; ++k)
     for (int i = 0; i < kNumPmc; ++i) {
       const int t = tenants[k];
@@ -1596,6 +1645,7 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
   if (const char* v = std::getenv("GPBS_HWC_OWNER_BURST")) c->hwc_owner_burst = std::atoi(v) != 0;
   if (const char* v = std::getenv("GPBS_HWC_MODEL_FALLBACK")) c->model_fallback = std::atoi(v) != 0;
   if (const char* v = std::getenv("GPBS_HWC_WATCH")) c->hwc_watch = std::atoi(v) != 0;
+  if (const char* v = std::getenv("GPBS_HWC_FUSE")) c->hwc_fuse = std::atoi(v) != 0;
   if (const char* v = std::getenv("GPBS_SHARE_PROBE")) {
     c->probe_every = std::max(0, std::atoi(v));
     if (const char* k = std::strchr(v, ':')) c->probe_len = std::max(0, std::atoi(k + 1));
@@ -2144,6 +2194,7 @@ int gpbs_gpu_hwc_reset(void* p) {
   c->hwc_triggers = 0;
   c->hwc_denied = 0;
   c->fallback_periods = c->clean_periods = 0;
+  c->fuse_ticks = c->cal_updates = 0;
   return 0;
 }
 
@@ -2159,6 +2210,27 @@ int gpbs_gpu_hwc_sampler(void* p, int budget_pct, int owner_burst, int fallback)
   if (fallback >= 0) c->model_fallback = fallback != 0;
   c->hwc_tokens = c->hwc_bucket;
   return 0;
+}
+
+// Fused metric (K9): on = 1 / 0 sets, -1 keeps; returns the old setting.
+// stats (optional): [0] ticks that reported calibrated modeled deltas,
+// [1] calibration updates from hardware windows.
+int gpbs_gpu_hwc_fuse(void* p, int on, uint64_t* stats2) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c) return -22;
+  std::lock_guard<std::mutex> g(c->snap_mu);
+  const int old = c->hwc_fuse;
+  if (on >= 0 && (on != 0) != (old != 0)) {
+    c->hwc_fuse = on != 0;
+    c->tick_blk.clear();
+    c->tick_prev.clear();
+    std::memset(c->cal, 0, sizeof(c->cal));
+  }
+  if (stats2) {
+    stats2[0] = c->fuse_ticks;
+    stats2[1] = c->cal_updates;
+  }
+  return old;
 }
 
 // Sample budget and model-fallback statistics: out[0] budget %, [1] burst

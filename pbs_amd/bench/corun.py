@@ -220,6 +220,7 @@ POLICY_ENGINES = {
     "gpbs-b5": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
     "gpbs-model": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
     "gpbs-d5": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
+    "gpbs-fuse": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
     # no cross-class steals by idle partitions (boot class_steal=0)
     "gpbs-nox": (4, dict(BUDGET_OVERRIDES, class_budget=1, class_steal=0), True,
                  "device,se,waveprio,latco,budget,latmem"),
@@ -265,6 +266,8 @@ SAMPLER = {
     # ~0.2 ms sample cost; 5 % -> ~4 ms, 10 % -> ~2 ms (budget raised with it)
     "gpbs-d5": dict(budget_pct=8, duty=5),
     "gpbs-d10": dict(budget_pct=15, duty=10),
+    # the PBS metric every tick from hardware-calibrated modeled deltas
+    "gpbs-fuse": dict(fuse=1),
 }
 
 

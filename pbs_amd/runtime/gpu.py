@@ -163,7 +163,10 @@ class GpuContext:
         self.L.gpbs_gpu_hwc_bursts(self.h, C.byref(tr), C.byref(bsm))
         bud = (C.c_uint64 * 6)()
         self.L.gpbs_gpu_hwc_budget_stats(self.h, bud)
-        return {"budget_pct": bud[0], "burst_denied": bud[1], "model_fallback_periods": bud[2],
+        fz = (C.c_uint64 * 2)()
+        fuse = self.L.gpbs_gpu_hwc_fuse(self.h, -1, fz)
+        return {"fuse": bool(fuse), "fuse_ticks": fz[0], "cal_updates": fz[1],
+                "budget_pct": bud[0], "burst_denied": bud[1], "model_fallback_periods": bud[2],
                 "clean_periods": bud[3], "owner_bursts": bool(bud[4]),
                 "attr_device": bool(dev), "attr_kernel_launches": la.value, "attr_busy_skips": bs.value,
                 "attr_host": ho.value, "duty_cap_pct": duty, "mean_period_us": round(mp.value / 1e3, 1),
@@ -175,22 +178,28 @@ class GpuContext:
                 # exclusive-ownership windows: share of the counts that reached the PBS metric
                 "clean_pct": pct, "metric_frac": [round(x, 4) for x in cf]}
 
-    def set_hwc_sampler(self, budget_pct: int = -1, owner_burst: int = -1, fallback: int = -1, duty: int = -1):
+    def set_hwc_sampler(self, budget_pct: int = -1, owner_burst: int = -1, fallback: int = -1, duty: int = -1,
+                        fuse: int = -1):
         """Sampler policy: `budget_pct` caps the time all hardware samples may
         take, bursts included (token bucket; 0: no budget); `owner_burst`:
         owner changes open a 1 ms sampling burst; `fallback`: a tenant without
         a settled exclusive window reports its modeled deltas; `duty`: the
-        background cadence's duty-cycle cap (set_hwc_duty).  -1 keeps."""
+        background cadence's duty-cycle cap (set_hwc_duty); `fuse`: the PBS
+        metric every tick from hardware-calibrated modeled deltas (the
+        hardware samples only calibrate).  -1 keeps."""
         self.L.gpbs_gpu_hwc_sampler(self.h, int(budget_pct), int(owner_burst), int(fallback))
         if duty >= 0:
             self.set_hwc_duty(duty)
+        if fuse >= 0:
+            self.L.gpbs_gpu_hwc_fuse(self.h, int(fuse), None)
 
     def hwc_sampler(self) -> dict:
         """The current sampler policy (set_hwc_sampler's arguments)."""
         bud = (C.c_uint64 * 6)()
         self.L.gpbs_gpu_hwc_budget_stats(self.h, bud)
         return {"budget_pct": int(bud[0]), "owner_burst": int(bud[4]), "fallback": int(bud[5]),
-                "duty": int(self.L.gpbs_gpu_hwc_duty(self.h, -1, None))}
+                "duty": int(self.L.gpbs_gpu_hwc_duty(self.h, -1, None)),
+                "fuse": int(self.L.gpbs_gpu_hwc_fuse(self.h, -1, None))}
 
     def set_hwc_duty(self, pct: int) -> int:
         """Sampler duty-cycle cap: the period stretches so that sampling takes

@@ -102,9 +102,12 @@ print("RESULT " + json.dumps(out))
 """
 
 
-def test_budget_layout_follows_a_phase_change_on_live_counters():
-    r = subprocess.run([sys.executable, "-c", CODE % ROOT], capture_output=True, text=True, timeout=180,
-                       env=dict(os.environ))
+@pytest.mark.parametrize("fuse", [0, 1])
+def test_budget_layout_follows_a_phase_change_on_live_counters(fuse):
+    """fuse=1 (GPBS_HWC_FUSE): the PBS metric every tick from the modeled
+    deltas calibrated by the hardware windows -- the same layout moves."""
+    env = dict(os.environ, GPBS_HWC_FUSE=str(fuse))
+    r = subprocess.run([sys.executable, "-c", CODE % ROOT], capture_output=True, text=True, timeout=180, env=env)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     out = json.loads([x for x in r.stdout.splitlines() if x.startswith("RESULT ")][-1][7:])
     print(json.dumps(out, indent=1))
@@ -117,3 +120,5 @@ def test_budget_layout_follows_a_phase_change_on_live_counters():
     assert out["class_change"] >= 2 and out["relayout"] >= 2, out
     assert out["adapt_rearm"] > 0, out
     assert out["check"] == ""
+    if fuse:  # every metric tick reported; hardware windows calibrated the model
+        assert out["hwc"]["fuse"] and out["hwc"]["fuse_ticks"] > 100 and out["hwc"]["cal_updates"] > 0, out["hwc"]
