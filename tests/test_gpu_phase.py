@@ -121,4 +121,4 @@ def test_budget_layout_follows_a_phase_change_on_live_counters(fuse):
     assert out["adapt_rearm"] > 0, out
     assert out["check"] == ""
     if fuse:  # every metric tick reported; hardware windows calibrated the model
-        assert out["hwc"]["fuse"] and out["hwc"]["fuse_ticks"] > 100 and out["hwc"]["cal_updates"] > 0, out["hwc"]
+        assert out["hwc"]["fuse"] and out["hwc"]["fuse_ticks"] > 20 and out["hwc"]["cal_updates"] > 0, out["hwc"]
