@@ -943,6 +943,7 @@ class CreditScheduler : public Scheduler {
         if (!soft_pass && !v.soft.empty() && !v.soft.test(cpu) &&
             E.now() - v.homed_at < std::max<int64_t>(1000000, 4 * (int64_t)ratelimit_us_ * 1000))
           continue;
+        // (gpbs extension of csched_runq_steal, X:xen/common/sched_credit.c:1560-1605.)
         // Budget layout, time-shared class region: every tenant of the region
         // has a home slot on every partition of it, so a steal onto a
         // partition that already holds a runnable sibling of the slot only
@@ -978,9 +979,11 @@ class CreditScheduler : public Scheduler {
       E.perfc.incr(PC_load_balance_over);
     else
       E.perfc.incr(PC_load_balance_other);
-    // Two balance steps (Xen 4.5): slots whose soft affinity includes this
-    // partition first; then, only for an otherwise idle partition, any slot
-    // hard affinity allows (cross-class work conservation).
+    // Two balance steps (Xen 4.5's soft-affinity form of csched_load_balance,
+    // X:xen/common/sched_credit.c:1607-1672 in 4.2.1): slots whose soft
+    // affinity includes this partition first; then, only for an otherwise
+    // idle partition, any slot hard affinity allows (cross-class work
+    // conservation; off in the budget layout with boot class_steal=0).
     for (int step = 0; step < 2; ++step) {
       if (step == 1 && (s.pri != PRI_IDLE ||
                         (E.boot.class_budget && E.boot.class_split > 1 && !E.boot.class_steal)))
