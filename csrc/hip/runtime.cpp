@@ -1129,7 +1129,6 @@ struct MaskedStreams {
   std::mutex mu;
   std::vector<Ent> ents;
   int created = 0;
-  int destroyed = 0;
 };
 MaskedStreams& masked_pool() {
   static MaskedStreams* p = new MaskedStreams;  // never destroyed: streams outlive static teardown order
@@ -1197,41 +1196,15 @@ hipStream_t masked_acquire_key(const uint32_t m[8], uint32_t key) {
   return s;
 }
 hipStream_t masked_acquire(const uint32_t m[8]) { return masked_acquire_key(m, 0); }
-// Queues nobody holds that the pool keeps for re-keying (GPBS_MASKED_IDLE,
-// default 2; -1 = keep all).  Every CU-masked stream is a hardware queue the
-// process holds, idle or not, and past the hardware scheduler's queue slots
-// all of them are time-sliced (profiles/r4/queue_budget*.log: the knee is
-// ~16-20 queues per process); a released queue beyond the reserve is
-// destroyed (work still queued on it completes first).
-int masked_idle_reserve() {
-  static const int v = [] {
-    const char* e = std::getenv("GPBS_MASKED_IDLE");
-    return e ? std::atoi(e) : 2;
-  }();
-  return v;
-}
 void masked_release(const uint32_t*, hipStream_t s) {
   if (!s) return;
   MaskedStreams& P = masked_pool();
-  hipStream_t drop = nullptr;
-  {
-    std::lock_guard<std::mutex> g(P.mu);
-    for (size_t i = 0; i < P.ents.size(); ++i) {
-      auto& e = P.ents[i];
-      if (e.s != s || e.refs <= 0) continue;
-      if (--e.refs == 0 && masked_idle_reserve() >= 0) {
-        int idle = 0;
-        for (auto& o : P.ents) idle += o.device == e.device && o.refs == 0;
-        if (idle > masked_idle_reserve()) {
-          drop = e.s;
-          P.ents.erase(P.ents.begin() + (long)i);
-          P.destroyed++;
-        }
-      }
-      break;
+  std::lock_guard<std::mutex> g(P.mu);
+  for (auto& e : P.ents)
+    if (e.s == s && e.refs > 0) {
+      e.refs--;
+      return;
     }
-  }
-  if (drop) (void)hipStreamDestroy(drop);
 }
 
 // CU mask of one half of every XCD.  hipExtStreamCreateWithCUMask bit b
@@ -2493,16 +2466,13 @@ int gpbs_gpu_adapt_stats(void* p, uint64_t* calls, uint64_t* late, uint64_t* bus
 // Process-wide CU-masked queue pool: out[0] masked streams ever created,
 // out[1] currently free (the rest are held by runners).  Every created one is
 // a hardware queue this process keeps.
-// out3: [0] masked queues created, [1] held idle now, [2] destroyed (past
-// the idle reserve); created - destroyed = the masked queues alive.
-int gpbs_gpu_masked_pool(uint64_t* out3) {
+int gpbs_gpu_masked_pool(uint64_t* out2) {
   MaskedStreams& P = masked_pool();
   std::lock_guard<std::mutex> g(P.mu);
-  out3[0] = (uint64_t)P.created;
+  out2[0] = (uint64_t)P.created;
   uint64_t idle = 0;
   for (auto& e : P.ents) idle += e.refs == 0;
-  out3[1] = idle;
-  out3[2] = (uint64_t)P.destroyed;
+  out2[1] = idle;
   return 0;
 }
 

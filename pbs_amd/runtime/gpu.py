@@ -308,11 +308,11 @@ class GpuContext:
         self.L.gpbs_gpu_stats(self.h, out)
         ca, la, bu = C.c_uint64(0), C.c_uint64(0), C.c_uint64(0)
         self.L.gpbs_gpu_adapt_stats(self.h, C.byref(ca), C.byref(la), C.byref(bu))
-        mp = (C.c_uint64 * 3)()
+        mp = (C.c_uint64 * 2)()
         self.L.gpbs_gpu_masked_pool(mp)
         return {"switches": out[0], "flushes": out[1], "metric_calls": out[2], "metric_ns": out[3],
                 "adapt_device_calls": ca.value, "adapt_device_late": la.value, "adapt_device_busy": bu.value,
-                "masked_queues_created": mp[0], "masked_queues_free": mp[1], "masked_queues_destroyed": mp[2]}
+                "masked_queues_created": mp[0], "masked_queues_free": mp[1]}
 
     def close(self):
         if getattr(self, "h", None):

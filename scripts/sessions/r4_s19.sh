@@ -17,8 +17,3 @@ echo "rc=$? $(date +%T)"; python -c "
 import json; d=[json.loads(l) for l in open('gpurun_out/r4/s19_rehearse4.json') if l.startswith('{')][-1]
 print('value', d['value'], 'n_gpus', d['n_gpus'], 'mixes', {m: v.get('value') for m, v in d.get('mixes', {}).items()})
 for r in d['ranks']: print(r['rank'], {m: (x['coll'], x['ipc_selftest'], (x.get('gang') or {}).get('timeouts')) for m, x in r['mixes'].items()})"
-echo "== 8mix with the idle-queue reserve $(date +%T)"
-timeout -k 10 300 python -u bench.py --gpus 1 --mix 8mix --policies gpbs,none --reps 6 \
-  --steps 20 --warmup 3 --no-resolo > gpurun_out/r4/s19_8mix.json 2> gpurun_out/r4/s19_8mix.log
-echo "rc=$? $(date +%T)"; python scripts/corun_log_policies.py gpurun_out/r4/s19_8mix.log | grep -v "^   "
-grep -o '"masked_queues_created": [0-9]*, "masked_queues_free": [0-9]*, "masked_queues_destroyed": [0-9]*' gpurun_out/r4/s19_8mix.log | sort | uniq -c
