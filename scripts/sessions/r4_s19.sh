@@ -1,14 +1,10 @@
 #!/bin/bash
 # Round 4 session 19: the default bench's every mix (4mix, phase, phase-ts,
 # 8mix) through the multi-rank path: 4 ranks on one GPU (--rehearse-ipc,
-# modeled counters), 1 rep each; first a GEMM kbench with the static-priority
-# variant (opts bit 15).
+# modeled counters), 1 rep each.
 set -o pipefail
 cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out/r4
-echo "== kbench gemm $(date +%T)"
-KBENCH_GEMM_ONLY=1 timeout -k 10 300 python -u scripts/kbench.py --iters 20 > gpurun_out/r4/s19_kbench.jsonl 2>&1 || exit $?
-cat gpurun_out/r4/s19_kbench.jsonl | grep -v "^W2026"
 echo "== rehearse4 all mixes $(date +%T)"
 timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29513 \
   bench.py --gpus 4 --rehearse-ipc --steps 5 --warmup 1 --reps 1 --reps-extra 1 --counters model \
