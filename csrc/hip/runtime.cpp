@@ -1155,6 +1155,17 @@ int masked_cap() {
   }();
   return v;
 }
+// Queues per layout key (GPBS_KEY_QUEUES, default 1): the co-sharers of a
+// time-shared region spread over this many queues (least-held first), so an
+// incoming owner's kernel need not wait in order behind the outgoing owner's
+// draining one on a single queue.
+int key_queues() {
+  static const int v = [] {
+    const char* e = std::getenv("GPBS_KEY_QUEUES");
+    return e ? std::max(1, std::atoi(e)) : 1;
+  }();
+  return v;
+}
 hipStream_t masked_acquire_key(const uint32_t m[8], uint32_t key) {
   int dev = 0;
   hipGetDevice(&dev);
@@ -1164,18 +1175,23 @@ hipStream_t masked_acquire_key(const uint32_t m[8], uint32_t key) {
     std::lock_guard<std::mutex> g(P.mu);
     MaskedStreams::Ent* idle = nullptr;
     MaskedStreams::Ent* least = nullptr;
-    int keyed = 0;
+    MaskedStreams::Ent* same = nullptr;  // least-held queue of this layout
+    int keyed = 0, nsame = 0;
     for (auto& e : P.ents) {
       if (e.device != dev || std::memcmp(e.m, m, sizeof(e.m)) != 0) continue;
-      if (key && e.key == key && e.refs > 0) {  // the same layout: share its queue
-        e.refs++;
-        return e.s;
+      if (key && e.key == key && e.refs > 0) {
+        nsame++;
+        if (!same || e.refs < same->refs) same = &e;
       }
       if (e.refs == 0 && (!idle || (key && e.key == key))) idle = &e;
       if (e.key && e.refs > 0) {
         keyed++;
         if (!least || e.refs < least->refs) least = &e;
       }
+    }
+    if (same && (nsame >= key_queues() || (!idle && masked_cap() > 0 && keyed >= masked_cap()))) {
+      same->refs++;  // the same layout: share its (least-held) queue
+      return same->s;
     }
     if (idle) {  // re-key a queue nobody holds
       idle->key = key;
