@@ -2269,13 +2269,15 @@ int gpbs_gpu_hwc_budget_stats(void* p, uint64_t* out5) {
 // Sampler cadence: fast and steady-state periods (us, < 0 leaves them), and
 // *slow_samples = samples taken at the steady-state period since the last
 // hwc reset.
+// Returns the previous slow (back-off) period in us.
 int gpbs_gpu_hwc_period(void* p, int fast_us, int slow_us, uint64_t* slow_samples) {
   GpuCtx* c = (GpuCtx*)p;
   if (!c) return -22;
+  const int old = c->hwc_slow_us;
   if (fast_us >= 0) c->hwc_period_us = std::max(100, fast_us);
   if (slow_us >= 0) c->hwc_slow_us = slow_us;
   if (slow_samples) *slow_samples = c->hwc_slow_samples;
-  return 0;
+  return old;
 }
 
 // Burst statistics since the last hwc reset: triggers (owner changes and

@@ -221,6 +221,7 @@ POLICY_ENGINES = {
     "gpbs-model": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
     "gpbs-d5": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
     "gpbs-fuse": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
+    "gpbs-slow50": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
     # no cross-class steals by idle partitions (boot class_steal=0)
     "gpbs-nox": (4, dict(BUDGET_OVERRIDES, class_budget=1, class_steal=0), True,
                  "device,se,waveprio,latco,budget,latmem"),
@@ -268,6 +269,8 @@ SAMPLER = {
     "gpbs-d10": dict(budget_pct=15, duty=10),
     # the PBS metric every tick from hardware-calibrated modeled deltas
     "gpbs-fuse": dict(fuse=1),
+    # hardware sampling backs off to 50 ms once no owner changed for 20 ms
+    "gpbs-slow50": dict(slow_us=50000),
 }
 
 

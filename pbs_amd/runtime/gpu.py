@@ -179,19 +179,22 @@ class GpuContext:
                 "clean_pct": pct, "metric_frac": [round(x, 4) for x in cf]}
 
     def set_hwc_sampler(self, budget_pct: int = -1, owner_burst: int = -1, fallback: int = -1, duty: int = -1,
-                        fuse: int = -1):
+                        fuse: int = -1, slow_us: int = -1):
         """Sampler policy: `budget_pct` caps the time all hardware samples may
         take, bursts included (token bucket; 0: no budget); `owner_burst`:
         owner changes open a 1 ms sampling burst; `fallback`: a tenant without
         a settled exclusive window reports its modeled deltas; `duty`: the
         background cadence's duty-cycle cap (set_hwc_duty); `fuse`: the PBS
         metric every tick from hardware-calibrated modeled deltas (the
-        hardware samples only calibrate).  -1 keeps."""
+        hardware samples only calibrate); `slow_us`: the back-off period once
+        no owner has changed for 20 ms (0: none).  -1 keeps."""
         self.L.gpbs_gpu_hwc_sampler(self.h, int(budget_pct), int(owner_burst), int(fallback))
         if duty >= 0:
             self.set_hwc_duty(duty)
         if fuse >= 0:
             self.L.gpbs_gpu_hwc_fuse(self.h, int(fuse), None)
+        if slow_us >= 0:
+            self.set_hwc_period(-1, int(slow_us))
 
     def hwc_sampler(self) -> dict:
         """The current sampler policy (set_hwc_sampler's arguments)."""
@@ -199,7 +202,8 @@ class GpuContext:
         self.L.gpbs_gpu_hwc_budget_stats(self.h, bud)
         return {"budget_pct": int(bud[0]), "owner_burst": int(bud[4]), "fallback": int(bud[5]),
                 "duty": int(self.L.gpbs_gpu_hwc_duty(self.h, -1, None)),
-                "fuse": int(self.L.gpbs_gpu_hwc_fuse(self.h, -1, None))}
+                "fuse": int(self.L.gpbs_gpu_hwc_fuse(self.h, -1, None)),
+                "slow_us": int(self.L.gpbs_gpu_hwc_period(self.h, -1, -1, None))}
 
     def set_hwc_duty(self, pct: int) -> int:
         """Sampler duty-cycle cap: the period stretches so that sampling takes
