@@ -2112,6 +2112,77 @@ int gpbs_hip_hwc_attr_bench(int iters, double* out2) {
   return rc;
 }
 
+// One random attribution input (the previous one advanced): most partitions
+// with one dominant owner, some time-shared, some idle; every few steps a
+// whole idle XCD, another slot layout, co-resident mode, no clean windows, a
+// class-share interval; step 0 primes.
+}  // extern "C" (a template needs C++ linkage)
+template <class Rnd>
+static void attr_random_step(HwcAttrIn& in, int it, Rnd& rnd) {
+  for (int p = 0; p < kAttrP; ++p) {
+    int kind = (int)(rnd() % 8);
+    if (it % 4 == 2 && p / kCtx == 5) kind = 7;  // a whole idle XCD (no owner: unexplained counts)
+    const int a = 1 + (int)(rnd() % 6), b = 1 + (int)(rnd() % 6);
+    const long long span = 1000000;
+    for (int t = 0; t < kMaxTenants; ++t) {
+      long long add = 0;
+      if (kind < 5 && t == a) add = span;
+      else if (kind == 5 && t == a) add = span / 2 + (long long)(rnd() % 1000);
+      else if (kind == 5 && t == b) add = span / 2;
+      else if (kind == 6 && t == a) add = span * 95 / 100;
+      in.own_cur[t * kAttrP + p] += add;
+    }
+    for (int k = 0; k < kNumPmc; ++k) in.se_cur[p * kNumPmc + k] += rnd() % 100000000ull;
+  }
+  for (int i = 0; i < kXcds * kNumPmc; ++i) in.x_cur[i] += rnd() % 1000000000ull;
+  // slot layouts: the default (0-2 per SE, 3 per XCD), slot 2 per XCD (the
+  // L2-miss split by XCD-level requests), every slot per SE
+  for (int k = 0; k < kNumPmc; ++k) in.slot_se[k] = it % 6 == 1 ? (k < 2) : it % 6 == 5 ? 1u : (k < 3);
+  in.se_mode = (it % 5) != 4;
+  in.clean_pct = it % 7 == 3 ? 0 : 90;
+  in.shared = it % 11 == 10;
+  in.prime = it == 0;
+  in.nt_hi = it % 3 == 2 ? 0 : 7;  // tenants 1..6 own partitions (0: read every row)
+}
+
+extern "C" {
+
+// Host-only properties of hwc_attr_host (no GPU): per counter slot the
+// attributed counts plus the unexplained ones add up to the hardware sum
+// (out2[0]: worst relative error), and no tenant's clean part exceeds its
+// attributed part (out2[1]: worst relative excess).  Returns 0.
+int gpbs_hip_hwc_attr_host_check(int seed, int iters, double* out2) {
+  static HwcAttrIn in;
+  static HwcAttrPrev st;
+  static HwcAttrOut o;
+  std::memset(&in, 0, sizeof(in));
+  hwc_attr_prev_init(st);
+  uint64_t r = 0x9E3779B97F4A7C15ull ^ (uint64_t)seed;
+  auto rnd = [&]() {
+    r ^= r << 13;
+    r ^= r >> 7;
+    r ^= r << 17;
+    return r;
+  };
+  double cons = 0, excess = 0;
+  for (int it = 0; it <= iters; ++it) {
+    attr_random_step(in, it, rnd);
+    hwc_attr_host(in, st, o);
+    if (!o.valid) continue;
+    for (int k = 0; k < kNumPmc; ++k) {
+      double sum = o.unatt[k];
+      for (int t = 0; t < kMaxTenants; ++t) {
+        sum += o.add[t][k];
+        if (o.add[t][k] > 0) excess = std::max(excess, (o.addc[t][k] - o.add[t][k]) / o.add[t][k]);
+      }
+      if (o.hw_sum[k] > 0) cons = std::max(cons, std::fabs(sum - o.hw_sum[k]) / o.hw_sum[k]);
+    }
+  }
+  out2[0] = cons;
+  out2[1] = excess;
+  return 0;
+}
+
 int gpbs_hip_hwc_attr_selftest(int seed, int iters, double* max_rel) {
   HwcAttrIn* in = nullptr;
   HwcAttrIn* d_in = nullptr;
@@ -2137,31 +2208,7 @@ int gpbs_hip_hwc_attr_selftest(int seed, int iters, double* max_rel) {
   double worst = 0;
   int rc = 0;
   for (int it = 0; it <= iters && rc == 0; ++it) {
-    // a random ownership pattern: most partitions with one dominant owner, some time-shared, some idle
-    for (int p = 0; p < kAttrP; ++p) {
-      int kind = (int)(rnd() % 8);
-      if (it % 4 == 2 && p / kCtx == 5) kind = 7;  // a whole idle XCD (no owner: unexplained counts)
-      const int a = 1 + (int)(rnd() % 6), b = 1 + (int)(rnd() % 6);
-      const long long span = 1000000;
-      for (int t = 0; t < kMaxTenants; ++t) {
-        long long add = 0;
-        if (kind < 5 && t == a) add = span;
-        else if (kind == 5 && t == a) add = span / 2 + (long long)(rnd() % 1000);
-        else if (kind == 5 && t == b) add = span / 2;
-        else if (kind == 6 && t == a) add = span * 95 / 100;
-        in->own_cur[t * kAttrP + p] += add;
-      }
-      for (int k = 0; k < kNumPmc; ++k) in->se_cur[p * kNumPmc + k] += rnd() % 100000000ull;
-    }
-    for (int i = 0; i < kXcds * kNumPmc; ++i) in->x_cur[i] += rnd() % 1000000000ull;
-    // slot layouts: the default (0-2 per SE, 3 per XCD), slot 2 per XCD (the
-    // L2-miss split by XCD-level requests), every slot per SE
-    for (int k = 0; k < kNumPmc; ++k) in->slot_se[k] = it % 6 == 1 ? (k < 2) : it % 6 == 5 ? 1u : (k < 3);
-    in->se_mode = (it % 5) != 4;
-    in->clean_pct = it % 7 == 3 ? 0 : 90;
-    in->shared = it % 11 == 10;
-    in->prime = it == 0;
-    in->nt_hi = it % 3 == 2 ? 0 : 7;  // tenants 1..6 own partitions (0: read every row)
+    attr_random_step(*in, it, rnd);
     hwc_attr_host(*in, hst, ref);
     if (gpbs_hip_hwc_attribute(in, d_in, d_st, out, nullptr) || hipDeviceSynchronize() != hipSuccess) {
       rc = -5;
