@@ -286,7 +286,12 @@ struct GpuCtx {
   // (scripts/hwc_cost.py), so the sampler keeps the reference's 1 ms period
   // (CSCHED_METRIC_TICK_PERIOD, X:xen/common/sched_credit.c:55) and no longer
   // backs off; GPBS_HWC_SLOW_US=4000 restores the round-2 back-off.
-  int hwc_slow_us = 0;  // GPBS_HWC_SLOW_US (0: never back off)
+  // Round 4: back off to 50 ms once no owner has changed for 20 ms (phase
+  // triggers still open 1 ms bursts): config #5 1.2343 vs 1.2249 (the shim
+  // tenants' layout is steady; profiles/r4/llm5_backoff_s22.txt), runner mixes
+  // equal or +0.003 with a quarter of the samples on steady layouts
+  // (sampler_backoff_s23.txt).  0: never back off.
+  int hwc_slow_us = 50000;  // GPBS_HWC_SLOW_US
   // Duty-cycle cap: a sample stalls the command processor for its duration
   // (every counter record is a register read it performs), and what that
   // costs the tenants varies from box to box (145-190 us per lean sample on
