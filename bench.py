@@ -379,8 +379,9 @@ def main():
 def run_llm5(args):
     """Config #5 in the bench contract: solo, none,
     static-se and gpbs (the daemon's demand-driven SE budgets on live
-    counters; shim tenants on CU-masked queues chosen by measurement, the
-    choice remembered across runs), --reps runs each; decode p50 / p99 and
+    counters; shim tenants on CU-masked queues chosen by measurement in
+    every run -- remembering the choice across runs was measured harmful,
+    runtime/tenant.py qprobe_load), --reps runs each; decode p50 / p99 and
     both tenants' shares per policy.  One JSON line (the driver contract's
     fields, config #5)."""
     import contextlib
@@ -393,7 +394,6 @@ def run_llm5(args):
     secs = max(4.0, args.steps * args.step_ms / 1e3)
     warm = max(2.0, args.warmup * args.step_ms / 1e3)
     out = os.path.join(tempfile.mkdtemp(), "llm5.json")
-    os.environ.setdefault("GPBS_QPROBE_CACHE", os.path.join(os.path.dirname(out), "qprobe.json"))
     pols = args.policies or "solo,none,static-se,gpbs-budget"
     with contextlib.redirect_stdout(sys.stderr):  # rank 0 prints ONE line: ours
         llm_corun.main(["--fp8", "--graph", "--seconds", str(secs), "--warmup", str(warm), "--reps", str(args.reps),

@@ -160,7 +160,12 @@ class QueueProber:
             return
         self.since += 1
         self.ewma = 0.8 * self.ewma + 0.2 * ms
-        if self.since >= self.cooldown and self.ewma > self.drift * self.ref:
+        # a stall (abort x the explored time) re-explores at once; a milder
+        # drift only after the cooldown.  Config #5 (s24): a queue that began
+        # sharing a pipe with the trainer's ran 3x slower for 1.5 s while the
+        # 100-slice cooldown ran out.
+        severe = self.since >= 3 and self.ewma > self.abort * self.ref
+        if severe or (self.since >= self.cooldown and self.ewma > self.drift * self.ref):
             self.samples = [[] for _ in range(self.k)]
             self.idx, self.exploring = 0, True
 
@@ -172,13 +177,21 @@ class QueueProber:
 
 
 def _qprobe_cache_path() -> str:
-    return os.environ.get("GPBS_QPROBE_CACHE") or os.path.join(
-        os.environ.get("TMPDIR", "/tmp"), f"gpbs-qprobe-{os.getuid()}.json")
+    return os.environ.get("GPBS_QPROBE_CACHE", "")
 
 
 def qprobe_load(key: str) -> Optional[Dict[str, float]]:
-    """A remembered QueueProber choice for `key` ("tenant:mask"), or None."""
+    """A remembered QueueProber choice for `key` ("tenant:mask"), or None.
+
+    Opt-in (GPBS_QPROBE_CACHE=<file>): which hardware pipe a queue lands on is
+    decided per process, so a queue index that was fast in one run can share
+    the trainer's pipe in the next, and a reference time remembered from a
+    slow exploration hides it (config #5, profiles/r4/llm5_s24.txt: 1.5 s on
+    a 3x slower queue).  By default every process explores (a stalled queue
+    costs one slice) and remembers nothing."""
     import json
+    if not _qprobe_cache_path():
+        return None
     try:
         with open(_qprobe_cache_path()) as f:
             v = json.load(f).get(key)
@@ -192,6 +205,8 @@ def qprobe_store(key: str, st: Dict[str, float]):
     import fcntl
     import json
     path = _qprobe_cache_path()
+    if not path:
+        return
     try:
         with open(path + ".lock", "w") as lk:
             fcntl.flock(lk, fcntl.LOCK_EX)

@@ -250,3 +250,28 @@ def test_queue_prober_remembered_winner_skips_exploration(tmp_path, monkeypatch)
         p.record(speed[p.current()])
     assert seen[:3] == [2, 2, 2] and p.explorations == 1 and p.current() == 0
     assert p.state()["idx"] == 0
+
+
+def test_prober_leaves_a_stalled_queue_without_waiting_for_the_cooldown():
+    """A queue that starts stalling mid-run (3x its explored time) is left
+    within a few slices, not after the cooldown; a mild drift still waits."""
+    from pbs_amd.runtime.tenant import QueueProber
+    p = QueueProber(3, explore=2, keep=2, cooldown=100)
+    for ms in (5.0, 5.0, 9.0, 9.0, 6.0, 6.0):  # queue 0 fastest
+        p.record(ms)
+    assert not p.exploring and p.current() == 0
+    for _ in range(20):  # mild drift (1.3x): stays
+        p.record(6.5)
+    assert not p.exploring
+    n = 0
+    while not p.exploring and n < 50:  # stall (3x)
+        p.record(15.0)
+        n += 1
+    assert p.exploring and n <= 8, n
+
+
+def test_remembered_winner_is_opt_in(monkeypatch):
+    from pbs_amd.runtime.tenant import qprobe_load, qprobe_store
+    monkeypatch.delenv("GPBS_QPROBE_CACHE", raising=False)
+    qprobe_store("infer:se23:3", {"idx": 1, "ref_ms": 5.0})  # no cache configured: a no-op
+    assert qprobe_load("infer:se23:3") is None
