@@ -392,7 +392,12 @@ def run_llm5(args):
         print("bench.py --mix llm5 runs on one GPU", file=sys.stderr)
         sys.exit(2)
     secs = max(4.0, args.steps * args.step_ms / 1e3)
-    warm = max(2.0, args.warmup * args.step_ms / 1e3)
+    # untimed warm-up, the same for every policy: the trainer's first step
+    # compiles for ~2 s, and a scheduler then needs ~1 s to classify and place
+    # the arriving tenant (its 190 ms training steps run wherever they were
+    # launched); steady state is what config #5 measures (s25 timelines:
+    # profiles/r4/llm5_s25.txt)
+    warm = max(5.0, args.warmup * args.step_ms / 1e3)
     out = os.path.join(tempfile.mkdtemp(), "llm5.json")
     pols = args.policies or "solo,none,static-se,gpbs-budget"
     with contextlib.redirect_stdout(sys.stderr):  # rank 0 prints ONE line: ours
