@@ -59,9 +59,9 @@ def test_survivors_reform_the_gang_without_the_hung_rank():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    # 300 ms (not 200): on a host loaded by the rest of the suite a survivor's
+    # 500 ms (not 200): on a host loaded by the rest of the suite a survivor's
     # scheduling hiccup must not count as its second miss (dropped twice = local)
-    world, hung, hang_ms, deadline_ms = 4, 2, 1500, 300.0
+    world, hung, hang_ms, deadline_ms = 4, 2, 1500, 500.0
     name = f"gpbs-gang-reform-{os.getpid()}-{port}"
     ps = [ctx.Process(target=hang_worker, args=(r, world, port, q, "shm", name, hung, hang_ms, deadline_ms, True))
           for r in range(world)]
