@@ -847,6 +847,27 @@ void Engine::budget_layout(Pool& pl, int64_t n, bool force) {
       }
     return m;
   };
+  // Two present tenants in SE-exclusive mode: the probe shares are the two
+  // class halves (a classified tenant keeps its class's half, an unclassified
+  // one takes the other).  A torch tenant on the shim launches a whole slice
+  // on a queue masked to its half only when it owns a clean half of every
+  // XCD; with XCD blocks both tenants' slices ran unmasked over each other
+  // until the newcomer was classified (config #5: ~1 s of 15-20 ms decode
+  // steps whenever the trainer arrived, profiles/r4/llm5_s25.txt).
+  const int psplit = std::max(1, boot.class_split);
+  if (probe && sig.size() == 2 && psplit > 1 && psplit < nctx) {
+    const uint32_t lo = (1u << psplit) - 1, hi = ctx_all & ~lo;
+    int first = 0;  // the tenant that takes the compute half (contexts [0, split))
+    if (sig[0].second == 1 || sig[1].second == 0) first = 1;
+    for (int i = 0; i < 2; ++i) {
+      Tenant& t = *tenants[sig[i].first];
+      t.budget_shared = false;
+      place_budget(t, pl, i == first ? lo : hi, 0, 0);
+    }
+    perfc.incr(PC_probe_layout);
+    process_softirqs();
+    return;
+  }
   if (probe && (int)sig.size() <= nx) {
     for (size_t i = 0; i < sig.size(); ++i) {
       Tenant& t = *tenants[sig[i].first];

@@ -278,3 +278,29 @@ def test_class_steal_off_keeps_a_short_gap_in_its_class():
         assert e.check() == ""
     assert out[1][0] > 0 and out[1][1] > 0, out  # Xen semantics: the idle compute SEs run memory slots
     assert out[0][0] == 0 and out[0][2] == 16, out  # guarded: the gap stays a gap, the layout unchanged
+
+
+def test_two_tenant_probe_gives_class_halves():
+    """A newcomer next to one classified tenant (config #5: the trainer
+    arriving next to the decode server): while it is probed, the incumbent
+    keeps its class's half of every XCD and the newcomer takes the other
+    half -- clean halves, so shim tenants launch on masked queues instead of
+    running unmasked over each other until the newcomer is classified."""
+    e, parts = _engine()
+    h = e.tenant_create("decode", nslots=32)
+    e.wake(h)
+    _settle(e, {h: MEMORY}, 200)
+    assert e.lib.gpbs_tenant_class(e.h, h) == 1
+    g = e.tenant_create("trainer", nslots=32)
+    e.wake(g)
+    for _ in range(50):  # 5 ms of relayout ticks; the newcomer reports no counters yet: unclassified
+        _feed(e, {h: MEMORY}, 100)
+    assert e.lib.gpbs_tenant_class(e.h, g) < 0
+    own = _ctx_owners(e, parts)
+    assert own[0][g] == 8 and own[1][g] == 8, own  # newcomer: the compute half
+    assert own[2][h] == 8 and own[3][h] == 8, own  # incumbent memory tenant: its half
+    assert e.perfc()["probe_layout"] >= 1
+    _settle(e, {h: MEMORY, g: COMPUTE}, 300)  # classified: the class layout is the same split
+    own = _ctx_owners(e, parts)
+    assert own[0][g] == 8 and own[1][g] == 8 and own[2][h] == 8 and own[3][h] == 8, own
+    assert e.check() == ""
