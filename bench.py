@@ -397,7 +397,7 @@ def run_llm5(args):
     # the arriving tenant (its 190 ms training steps run wherever they were
     # launched); steady state is what config #5 measures (s25 timelines:
     # profiles/r4/llm5_s25.txt)
-    warm = max(5.0, args.warmup * args.step_ms / 1e3)
+    warm = max(float(os.environ.get("GPBS_LLM5_WARM_S", "5")), args.warmup * args.step_ms / 1e3)
     out = os.path.join(tempfile.mkdtemp(), "llm5.json")
     pols = args.policies or "solo,none,static-se,gpbs-budget"
     with contextlib.redirect_stdout(sys.stderr):  # rank 0 prints ONE line: ours
