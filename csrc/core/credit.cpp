@@ -692,7 +692,10 @@ class CreditScheduler : public Scheduler {
         d.cache_miss_rate = inst ? miss * 100000 / inst : 0;  // Q3 fix: per tenant
         d.cpi = inst ? cyc * 1000 / inst : 0;
       }
-      if (inst) d.rate_ewma = (3 * d.rate_ewma + d.cache_miss_rate) / 4;
+      if (inst)  // class_fall: follow a drop at alpha 1/2 (rises cross the threshold in one sample anyway)
+        d.rate_ewma = (E.boot.class_fall && d.cache_miss_rate < d.rate_ewma)
+                          ? (d.rate_ewma + d.cache_miss_rate) / 2
+                          : (3 * d.rate_ewma + d.cache_miss_rate) / 4;
       E.emit(TRC_METRIC, master_, (uint32_t)ids[k], (uint32_t)inst, (uint32_t)miss, (uint32_t)d.cache_miss_rate);
       d.spinlock_metric_update = 0;
       d.spinlock_count = 0;

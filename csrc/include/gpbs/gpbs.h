@@ -92,6 +92,9 @@ typedef struct gpbs_boot_params {
                                   (Xen 4.5's second balance step, work conservation); 0 = only the relayout after
                                   present_us hands an absent class's partitions over -- a short gap in one tenant's
                                   work no longer pulls the other class's runner onto an unmasked queue */
+  int32_t class_fall;          /* contention classes: the smoothed miss rate follows a DROP at alpha 1/2 instead of
+                                  1/4 (a rise already crosses the threshold in one sample): a memory-bound phase
+                                  that ends is re-classified in ~6 periods instead of ~14.  0 = symmetric 1/4 */
   gpbs_adapt_params_t adapt;
   gpbs_atc_params_t atc;
 } gpbs_boot_params_t;

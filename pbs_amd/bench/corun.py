@@ -213,6 +213,9 @@ POLICY_ENGINES = {
                          "device,se,waveprio,latco,budget,latmem"),
     "gpbs-f4": (4, dict(BUDGET_OVERRIDES, class_budget=1, adapt=dict(MI355X_PROFILE["adapt"], min_us=4000)), True,
                 "device,se,waveprio,latco,budget,latmem"),
+    # the class EWMA follows a drop at alpha 1/2 (boot class_fall=1)
+    "gpbs-fall": (4, dict(BUDGET_OVERRIDES, class_budget=1, class_fall=1), True,
+                  "device,se,waveprio,latco,budget,latmem"),
     # PBS quantum range stretched 3x at the top (memory tenants up to 33 ms)
     "gpbs-q33": (4, dict(BUDGET_OVERRIDES, class_budget=1,
                          adapt=dict(MI355X_PROFILE["adapt"], max_us=33000, inc_us=3000, dec_us=6000)), True,

@@ -304,3 +304,27 @@ def test_two_tenant_probe_gives_class_halves():
     own = _ctx_owners(e, parts)
     assert own[0][g] == 8 and own[1][g] == 8 and own[2][h] == 8 and own[3][h] == 8, own
     assert e.check() == ""
+
+
+def test_class_fall_reclassifies_an_ended_memory_phase_sooner():
+    """boot class_fall=1: the classifier's smoothed miss rate follows a drop
+    at alpha 1/2, so a phase tenant whose memory-bound phase ends is back in
+    the compute class in fewer metric periods (a rise already crosses the
+    threshold in one sample either way)."""
+    took = {}
+    for cf in (0, 1):
+        e, parts = _engine(class_fall=cf)
+        g, p, s = (e.tenant_create(n, nslots=32) for n in ("gemm", "phase", "hbm"))
+        rates = {g: COMPUTE, p: MEMORY, s: MEMORY}
+        for t in rates:
+            e.wake(t)
+        _settle(e, rates)
+        assert e.lib.gpbs_tenant_class(e.h, p) == 1
+        rates[p] = COMPUTE
+        n = 0
+        while e.lib.gpbs_tenant_class(e.h, p) != 0 and n < 2000:
+            _feed(e, rates, 100)
+            n += 1
+        took[cf] = n
+        assert e.check() == ""
+    assert took[1] < 2000 and took[1] < took[0], took
