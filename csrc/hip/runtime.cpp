@@ -2720,6 +2720,21 @@ int gpbs_runner_stats(void* p, gpbs_runner_stats_t* out) {
   return 0;
 }
 
+// Which CU-masked queue of the process pool the runner launches on now
+// (the pool index, stable for the process: entries are never removed; the
+// latency lane's class-half queue if it has one), or -1 (its own stream).
+// Diagnostics: which hardware queue -- and so which pipe -- a slow run used.
+int gpbs_runner_queue(void* p) {
+  Runner* r = (Runner*)p;
+  hipStream_t s = r->key_stream ? r->key_stream : (r->se_stream[0] ? r->se_stream[0] : r->se_stream[1]);
+  if (!s) return -1;
+  MaskedStreams& P = masked_pool();
+  std::lock_guard<std::mutex> g(P.mu);
+  for (size_t i = 0; i < P.ents.size(); ++i)
+    if (P.ents[i].s == s) return (int)i;
+  return -1;
+}
+
 // Copy up to max latency samples (ns); returns count.
 int gpbs_runner_latencies(void* p, int64_t* out, int max, int clear) {
   Runner* r = (Runner*)p;

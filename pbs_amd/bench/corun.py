@@ -1165,6 +1165,7 @@ class Corun:
                      for k in ("launches", "relaunches", "waits_owner", "drain_count", "drain_sum_ns")}
                 # revocation drain: table publish -> the interrupted unit's grid gone
                 d["drain_us_mean"] = round(d.pop("drain_sum_ns") / d["drain_count"] / 1e3, 1) if d["drain_count"] else None
+                d["queue"] = r.queue_index()  # which masked queue (hardware pipe) the run ended on
                 eng["runner"][n] = d
             eng["hold_raises"] = self.ctx.hold_raises()  # latency-request holds (cumulative, gpbs-lat)
             coll = self.runners.get("coll")

@@ -454,6 +454,10 @@ class Runner:
             raise RuntimeError(f"runner {self.kind} failed rc={rc}")
         return rc
 
+    def queue_index(self) -> int:
+        """The process pool's CU-masked queue this runner launches on (-1: its own stream)."""
+        return int(self.L.gpbs_runner_queue(self.h))
+
     def stats(self) -> RunnerStats:
         s = hipabi.RunnerStats()
         self.L.gpbs_runner_stats(self.h, C.byref(s))
