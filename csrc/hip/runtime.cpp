@@ -1171,6 +1171,35 @@ int key_queues() {
   }();
   return v;
 }
+void se_cu_mask(const u32 se_bits[kXcds], uint32_t m[8]);
+// GPBS_QUEUE_PREALLOC=1: create the device's class-half queues up front, back
+// to back and interleaved (compute, memory, memory, compute, memory), before
+// anything else takes a masked queue.  Which pipe a hardware queue lands on
+// follows its creation order; queues created one by one as layouts come and
+// go put the compute region's and a memory region's queue on one pipe in
+// some runs (8mix: every slow run had the GEMMs on pool queue 5 and a stream
+// on queue 1, profiles/r4/queue_index_s32.txt), where a dispatch that waits
+// for CUs blocks the other queue's dispatches.
+void masked_prealloc_locked(MaskedStreams& P, int dev) {
+  static const bool on = [] {
+    const char* e = std::getenv("GPBS_QUEUE_PREALLOC");
+    return e && std::atoi(e) != 0;
+  }();
+  if (!on) return;
+  for (auto& e : P.ents)
+    if (e.device == dev) return;
+  for (int h : {0, 1, 1, 0, 1}) {
+    u32 bits[kXcds];
+    for (int x = 0; x < kXcds; ++x) bits[x] = h ? 0xCu : 0x3u;
+    uint32_t m[8];
+    se_cu_mask(bits, m);
+    hipStream_t s = nullptr;
+    if (hipExtStreamCreateWithCUMask(&s, 8, m) != hipSuccess) return;
+    P.ents.push_back({dev, {}, s, 0u, 0});
+    std::memcpy(P.ents.back().m, m, sizeof(P.ents.back().m));
+    P.created++;
+  }
+}
 hipStream_t masked_acquire_key(const uint32_t m[8], uint32_t key) {
   int dev = 0;
   hipGetDevice(&dev);
@@ -1178,6 +1207,7 @@ hipStream_t masked_acquire_key(const uint32_t m[8], uint32_t key) {
   MaskedStreams& P = masked_pool();
   {
     std::lock_guard<std::mutex> g(P.mu);
+    masked_prealloc_locked(P, dev);
     MaskedStreams::Ent* idle = nullptr;
     MaskedStreams::Ent* least = nullptr;
     MaskedStreams::Ent* same = nullptr;  // least-held queue of this layout
