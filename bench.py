@@ -143,6 +143,8 @@ def main():
                          "(default on)")
     ap.add_argument("--no-resolo", dest="resolo", action="store_false")
     ap.add_argument("--out", default="")
+    ap.add_argument("--no-cu-check", dest="cu_check", action="store_false",
+                    help="skip the CU-mask layout check (scripts/cu_map_check.py) run before the bench")
     ap.add_argument("--rehearse-ipc", action="store_true",
                     help="like --rehearse (every rank on GPU 0, gloo) but with the gated IPC all-reduce tenant on "
                          "the GPU: rehearses the whole N > 1 path (IPC self-test, P2P-flag barrier, gang epochs, "
@@ -180,6 +182,22 @@ def main():
         args.rehearse = True
     if args.rehearse:
         local = 0
+    # the CU-mask layout every SE-exclusive policy assumes, checked on this
+    # rank's device in a child process before this one touches the GPU
+    # (scripts/cu_map_check.py; a rehearsal checks once, on rank 0)
+    cu_map = None
+    if args.cu_check and (not args.rehearse or rank == 0):
+        import subprocess
+        try:
+            p = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "cu_map_check.py"), "--device", str(local)],
+                               capture_output=True, text=True, timeout=240)
+            line = [x for x in p.stdout.splitlines() if x.startswith("{")]
+            cu_map = json.loads(line[-1]) if line else {"ok": None, "rc": p.returncode, "err": p.stderr[-400:]}
+        except subprocess.TimeoutExpired:
+            cu_map = {"ok": None, "err": "timeout"}
+        if cu_map.get("ok") is False:
+            print(f"bench.py: rank {rank}: CU-mask bits do not map to shader engines as assumed: {cu_map}",
+                  file=sys.stderr)
     counters = args.counters
     if counters == "hw":  # must register with rocprofiler before the HIP runtime starts
         from pbs_amd.counters import hwc
@@ -199,7 +217,7 @@ def main():
     bdf = device_bdf(local)
     gpustate = GpuStateRecorder(bdf, period_s=0.2).start()
     rank_diag = {"rank": rank, "local_rank": local, "device_bdf": bdf, "gpu_state_source": gpustate.source,
-                 "counters": counters}
+                 "counters": counters, "cu_map_ok": cu_map.get("ok") if cu_map else None}
     if counters == "hw":
         rank_diag["hwc_agent"] = hwc.agent()
         if rank_diag["hwc_agent"]["bdf"] != bdf:

@@ -14,7 +14,10 @@ and reports which (XCD, SE) the workgroups really ran on.  Four queues, no
 churn.  Prints one JSON line; "ok": every workgroup on its intended SE and
 every XCD covered.
 
-    python scripts/cu_map_check.py [--blocks 2048]
+    python scripts/cu_map_check.py [--blocks 2048] [--device 0]
+
+bench.py runs it in a child process before it touches the GPU and records
+the verdict per rank (`ranks[i].cu_map_ok`).
 """
 from __future__ import annotations
 
@@ -31,16 +34,18 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--blocks", type=int, default=2048)
+    ap.add_argument("--device", type=int, default=0)
     args = ap.parse_args()
     import torch
+    torch.cuda.set_device(args.device)
 
     from pbs_amd.ops import kernels as K
     from pbs_amd.runtime.tenant import se_cu_words
     L = K.lib()
-    out = torch.zeros(args.blocks * 4, dtype=torch.int32, device="cuda")
+    out = torch.zeros(args.blocks * 4, dtype=torch.int32, device=f"cuda:{args.device}")
     res = {"ok": True, "se": {}}
     for s in range(4):
-        h = K.cumask_stream(se_cu_words((s,)), device=0)
+        h = K.cumask_stream(se_cu_words((s,)), device=args.device)
         out.zero_()
         rc = L.gpbs_hip_census(K._ptr(out), args.blocks, None, 0, 0, C.c_void_p(h))
         torch.cuda.synchronize()
