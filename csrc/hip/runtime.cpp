@@ -1380,17 +1380,7 @@ struct Runner {
   // masked streams at every policy change added ~10 ms stalls that grew run
   // after run).  An owned set that fits neither half (work-conserving steals
   // across classes) launches unmasked and gates per workgroup.
-  // GPBS_SE_MASKED=0: SE-mode runners launch on their own (unmasked) stream
-  // and rely on the per-workgroup SE gate alone -- no CU-masked queues.
-  static bool se_masked() {
-    static const bool v = [] {
-      const char* e = std::getenv("GPBS_SE_MASKED");
-      return !e || std::atoi(e) != 0;
-    }();
-    return v;
-  }
   hipStream_t pick_se_stream() {
-    if (!se_masked()) return stream;
     u32 any = 0, bits = 0;
     for (int x = 0; x < kXcds; ++x)
       for (int e = 0; e < kCtx; ++e)
