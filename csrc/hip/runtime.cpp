@@ -1134,7 +1134,6 @@ struct MaskedStreams {
   std::mutex mu;
   std::vector<Ent> ents;
   int created = 0;
-  uint64_t shared_at_max = 0;  // acquisitions that shared a queue at the GPBS_MASKED_MAX budget
 };
 MaskedStreams& masked_pool() {
   static MaskedStreams* p = new MaskedStreams;  // never destroyed: streams outlive static teardown order
@@ -1201,19 +1200,6 @@ void masked_prealloc_locked(MaskedStreams& P, int dev) {
     P.created++;
   }
 }
-// Masked queues a process creates per device before new layouts share
-// existing queues of their mask (GPBS_MASKED_MAX, 0 = no limit).  Every
-// masked stream is a hardware queue the process keeps; with HIP's own queues
-// and the profiler's, the eighth masked queue put the process past the
-// hardware scheduler's queue slots on some boxes: every 8mix run whose
-// regions used pool queue 7 ran ~25 % slow (profiles/r4/queue_index_s37.txt).
-int masked_max() {
-  static const int v = [] {
-    const char* e = std::getenv("GPBS_MASKED_MAX");
-    return e ? std::max(0, std::atoi(e)) : 0;
-  }();
-  return v;
-}
 hipStream_t masked_acquire_key(const uint32_t m[8], uint32_t key) {
   int dev = 0;
   hipGetDevice(&dev);
@@ -1250,21 +1236,6 @@ hipStream_t masked_acquire_key(const uint32_t m[8], uint32_t key) {
     if (key && masked_cap() > 0 && keyed >= masked_cap() && least) {  // at the cap: share the least-held
       least->refs++;
       return least->s;
-    }
-    // At the process's queue budget: share this mask's least-held queue
-    // rather than add a hardware queue (GPBS_MASKED_MAX).
-    int ndev = 0;
-    MaskedStreams::Ent* any = nullptr;
-    for (auto& e : P.ents) {
-      if (e.device != dev) continue;
-      ndev++;
-      if (std::memcmp(e.m, m, sizeof(e.m)) == 0 && (!any || e.refs < any->refs)) any = &e;
-    }
-    if (masked_max() > 0 && ndev >= masked_max() && any) {
-      if (any->refs == 0) any->key = key;
-      any->refs++;
-      P.shared_at_max++;
-      return any->s;
     }
   }
   hipStream_t s = nullptr;
