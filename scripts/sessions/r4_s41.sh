@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round 4 session 41: HIP's own hardware queues per process 8 (default) vs 16 vs 12
+# (GPBS_HWQ) on the 8mix slow-run mode, one process each, same box.
+set -o pipefail
+cd "$(dirname "$0")/../.."
+mkdir -p gpurun_out/r4
+for hq in 8 16 12; do
+  echo "== hwq=$hq $(date +%T)"
+  GPBS_HWQ=$hq timeout -k 10 400 python -u bench.py --gpus 1 --mix 8mix --policies gpbs,credit-fixed-ts --reps 8 \
+    --steps 20 --warmup 3 --no-resolo --no-cu-check > gpurun_out/r4/s41_hwq$hq.json 2> gpurun_out/r4/s41_hwq$hq.log || exit $?
+  python scripts/corun_log_policies.py gpurun_out/r4/s41_hwq$hq.log | grep -v "^   "
+done
