@@ -38,7 +38,7 @@ import sys
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 # one HW queue per tenant/scheduler stream (see pbs_amd/runtime/gpu.py)
-os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("GPBS_HWQ") or str(max(8, int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)))
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("GPBS_HWQ") or str(max(12, int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)))
 
 
 def q(xs, f):

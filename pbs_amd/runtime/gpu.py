@@ -17,8 +17,12 @@ from typing import List, Optional
 # stream (partition-table updates, counter reduce).  With the HIP default of 4
 # queues, streams share queues round-robin and a table update can sit behind
 # a parked tenant kernel on the same queue until its park bound expires.
+# Round 4: 12, not 8 -- the 8mix (8 runners plus the scheduler's streams) ran
+# ~+0.006 higher and hit its masked-queue slow mode in 1 of 32 runs instead of
+# 3 of 32; 4 and 2 made that mode far more frequent
+# (profiles/r4/hip_queues_s40.txt, _s41.txt, _s42.txt).  GPBS_HWQ overrides.
 # Must be set before the HIP runtime initialises (first device call).
-os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("GPBS_HWQ") or str(max(8, int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)))
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("GPBS_HWQ") or str(max(12, int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)))
 
 import torch  # noqa: E402
 
