@@ -521,9 +521,6 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
                                                                u32 inst_per_tile, u32 refs_per_tile,
                                                                u32 miss_per_tile, u32* status) {
   constexpr int kStampLds = STAMP ? 8 * kStampTiles * kStampSlots * 4 : 0;
-  // BAL 4 / 5 (kbench variants): BAL 2's schedule with no priority flips /
-  // with the MFMA segments at s_setprio 3 instead of 1
-  constexpr int SCHED = (BAL == 4 || BAL == 5) ? 2 : BAL;
   __shared__ __attribute__((aligned(16))) char smem[kG2Lds + 16 + kStampLds];
   lds_t* lds = (lds_t*)smem;
   int* s_slot = (int*)(smem + kG2Lds);
@@ -615,7 +612,7 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
     if constexpr (STAMP) {
       if (units_seen == 0) ph[1] = (u32)__builtin_amdgcn_s_memrealtime();
     }
-    if constexpr (SCHED == 3) {
+    if constexpr (BAL == 3) {
       // ONE phase per K-tile (2 barriers): a wave reads all 24 fragments of
       // K-tile t, then runs its 64 MFMAs.  Global intervals: g0 reads at 2t,
       // MFMAs at 2t+1; g1 reads at 2t+1, MFMAs at 2t+2.  Buffer (t+1)&1 is
@@ -683,13 +680,13 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) a[i][s2] = frag(buf, 0, wr, i * 16, s2);
-      if constexpr (SCHED == 2) {  // 4 glds per read interval: B halves here, own A half in R_B
+      if constexpr (BAL == 2) {  // 4 glds per read interval: B halves here, own A half in R_B
         if (more) {
           stage(1, 0, t + 1); stage(1, 1, t + 1);
         } else {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-      } else if constexpr (SCHED) {
+      } else if constexpr (BAL) {
         // balanced staging: g0 4 + 4 glds, g1 6 + 2 (see the schedule note)
         if (wr == 0) {
           if (more) {
@@ -714,8 +711,7 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
       __builtin_amdgcn_s_barrier();
       stamp(t, 1);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if constexpr (BAL == 5) __builtin_amdgcn_s_setprio(3);
-      else if constexpr (BAL != 4) __builtin_amdgcn_s_setprio(1);
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
@@ -723,7 +719,7 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
 #pragma unroll
           for (int j = 0; j < 4; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j][s2], a[i][s2], acc[i][j], 0, 0, 0);
-      if constexpr (BAL != 4) __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_s_barrier();
       stamp(t, 2);
       // ---- R_B: A rows 64-127
@@ -731,12 +727,12 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) a[i][s2] = frag(buf, 0, wr, 64 + i * 16, s2);
-      if constexpr (SCHED == 2) {
+      if constexpr (BAL == 2) {
         if (more) {
           stage_own_a(t + 1);
           asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // retires this group's B0/B1(t+1)
         }
-      } else if constexpr (SCHED) {
+      } else if constexpr (BAL) {
         if (wr == 0) {
           if (more) {
             stage(0, 0, t + 1); stage(0, 1, t + 1);
@@ -759,8 +755,7 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
       __builtin_amdgcn_s_barrier();
       stamp(t, 3);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if constexpr (BAL == 5) __builtin_amdgcn_s_setprio(3);
-      else if constexpr (BAL != 4) __builtin_amdgcn_s_setprio(1);
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
@@ -768,10 +763,10 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
 #pragma unroll
           for (int j = 0; j < 4; ++j)
             acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j][s2], a[i][s2], acc[4 + i][j], 0, 0, 0);
-      if constexpr (BAL != 4) __builtin_amdgcn_s_setprio(0);
-      if constexpr (SCHED == 2) {  // end of M_B: the group's own A half of t+1 lands before its next R_A
+      __builtin_amdgcn_s_setprio(0);
+      if constexpr (BAL == 2) {  // end of M_B: the group's own A half of t+1 lands before its next R_A
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      } else if constexpr (SCHED) {  // end of M_B: g0 retires its A0(t+1), g1 its A1(t+1), before the barrier
+      } else if constexpr (BAL) {  // end of M_B: g0 retires its A0(t+1), g1 its A1(t+1), before the barrier
         if (wr == 0) {
           if (more) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
         } else {
@@ -1203,15 +1198,12 @@ int gpbs_hip_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int
       // bit 12: balanced staging; bit 13: each group stages its own A half (4 glds per read interval)
       const bool nt = g_gemm_opts & 1024, bal = g_gemm_opts & 4096, own = g_gemm_opts & 8192;
       const bool one = g_gemm_opts & 16384;  // bit 14: one phase per K-tile
-      const int pv = own ? (g_gemm_opts & 32768 ? 4 : g_gemm_opts & 65536 ? 5 : 0) : 0;  // bits 15 / 16: kbench
       auto k2 = one ? ((g_gemm_opts & 64) ? k_gemm256s2_bf16_tn<1, 0, 3> : k_gemm256s2_bf16_tn<0, 0, 3>)
                 : (g_gemm_opts & 64)
-                    ? (pv == 4 ? k_gemm256s2_bf16_tn<1, 0, 4> : pv == 5 ? k_gemm256s2_bf16_tn<1, 0, 5>
-                       : own ? k_gemm256s2_bf16_tn<1, 0, 2>
+                    ? (own ? k_gemm256s2_bf16_tn<1, 0, 2>
                            : bal ? k_gemm256s2_bf16_tn<1, 0, 1>
                                  : (nt ? k_gemm256s2_bf16_tn<1, 1, 0> : k_gemm256s2_bf16_tn<1, 0, 0>))
-                    : (pv == 4 ? k_gemm256s2_bf16_tn<0, 0, 4> : pv == 5 ? k_gemm256s2_bf16_tn<0, 0, 5>
-                       : own ? k_gemm256s2_bf16_tn<0, 0, 2>
+                    : (own ? k_gemm256s2_bf16_tn<0, 0, 2>
                            : bal ? k_gemm256s2_bf16_tn<0, 0, 1>
                                  : (nt ? k_gemm256s2_bf16_tn<0, 1, 0> : k_gemm256s2_bf16_tn<0, 0, 0>));
       hipLaunchKernelGGL(k2, dim3(grid), dim3(G2_NT), 0, s, (const u16*)A, (const u16*)Bt, (u16*)C, M, N, K,
