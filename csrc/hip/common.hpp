@@ -19,6 +19,7 @@ constexpr uint32_t kOwnerMask = 0x7FFFFFFFu;
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned short u16;
 typedef unsigned int u32;

@@ -600,10 +600,23 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
       return *(const __attribute__((address_space(3))) bf16x8*)p;
     };
     f32x4 acc[8][4];
+    f32x16 acc32[4][2];  // BAL 6
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc32[i][j][e] = 0.f;
+    // 32x32x16 operand: lane l holds row r0 + l%32, k = 16 s + 8 (l/32) .. +7
+    auto frag32 = [&](int b, int kind, int h, int r0, int s) -> bf16x8 {
+      const int r = r0 + (lane & 31);
+      const lds_t* p = lds + b * kG2Buf + (kind * 2 + h) * kG2Half + r * 128 + (((2 * s + (lane >> 5)) ^ g2_swz(r)) << 4);
+      return *(const __attribute__((address_space(3))) bf16x8*)p;
+    };
     // prologue: all of tile 0 from every wave, landed and visible
     stage(1, 0, 0); stage(1, 1, 0); stage(0, 0, 0); stage(0, 1, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -612,7 +625,65 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
     if constexpr (STAMP) {
       if (units_seen == 0) ph[1] = (u32)__builtin_amdgcn_s_memrealtime();
     }
-    if constexpr (BAL == 3) {
+    if constexpr (BAL == 6) {
+      // BAL 2's schedule and staging on v_mfma_f32_32x32x16_bf16: a phase is
+      // 2 (rows) x 2 (cols) blocks of 32x32 x 4 K-steps = 16 MFMAs of 16
+      // passes instead of 32 of 8.  Same 16 fragments per phase (LDS traffic
+      // per flop is set by the 128x64 wave tile, not the MFMA shape); half
+      // the MFMA issues and one accumulator block per 32x32.
+      bf16x8 a[2][4], b[2][4];
+      for (int t = 0; t < nt; ++t) {
+        const int buf = t & 1;
+        const bool more = t + 1 < nt;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int s = 0; s < 4; ++s) b[j][s] = frag32(buf, 1, bh, bc + j * 32, s);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int s = 0; s < 4; ++s) a[i][s] = frag32(buf, 0, wr, i * 32, s);
+        if (more) {
+          stage(1, 0, t + 1); stage(1, 1, t + 1);
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              acc32[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[j][s], a[i][s], acc32[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_barrier();
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int s = 0; s < 4; ++s) a[i][s] = frag32(buf, 0, wr, 64 + i * 32, s);
+        if (more) {
+          stage_own_a(t + 1);
+          asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // retires this group's B0/B1(t+1)
+        }
+        __builtin_amdgcn_s_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              acc32[2 + i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[j][s], a[i][s], acc32[2 + i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // own A half of t+1 before the next R_A
+        __builtin_amdgcn_s_barrier();
+      }
+    } else if constexpr (BAL == 3) {
       // ONE phase per K-tile (2 barriers): a wave reads all 24 fragments of
       // K-tile t, then runs its 64 MFMAs.  Global intervals: g0 reads at 2t,
       // MFMAs at 2t+1; g1 reads at 2t+1, MFMAs at 2t+2.  Buffer (t+1)&1 is
@@ -781,6 +852,22 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
     if constexpr (STAMP) {
       if (units_seen == 0) ph[2] = (u32)__builtin_amdgcn_s_memrealtime();
     }
+    if constexpr (BAL == 6) {
+      // mfma32(B, A) holds C^T per 32x32 block: lane owns C[m = .. + l%32][n =
+      // .. + 8 g + 4 (l/32) + r], element 4 g + r: one 8-byte store per g
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int m = tm * G2_BM + wr * 128 + i * 32 + (lane & 31);
+            const int n = tn * G2_BM + wc * 64 + j * 32 + 8 * g + 4 * (lane >> 5);
+            const u32 lo = (u32)f2bf(acc32[i][j][4 * g]) | ((u32)f2bf(acc32[i][j][4 * g + 1]) << 16);
+            const u32 hi = (u32)f2bf(acc32[i][j][4 * g + 2]) | ((u32)f2bf(acc32[i][j][4 * g + 3]) << 16);
+            *(uint2*)(C + (size_t)m * N + n) = make_uint2(lo, hi);
+          }
+    } else {
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -795,6 +882,7 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
           *(uint2*)(C + (size_t)m * N + n) = make_uint2(lo, hi);
         }
       }
+    }  // BAL != 6
     if constexpr (STAMP) {
       if (units_seen == 0) {
         ph[3] = (u32)__builtin_amdgcn_s_memrealtime();
@@ -1197,13 +1285,13 @@ int gpbs_hip_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int
     if (g_gemm_opts & 256) {  // 2 phases per K-tile (4 barriers); bit 10: streaming C stores
       // bit 12: balanced staging; bit 13: each group stages its own A half (4 glds per read interval)
       const bool nt = g_gemm_opts & 1024, bal = g_gemm_opts & 4096, own = g_gemm_opts & 8192;
-      const bool one = g_gemm_opts & 16384;  // bit 14: one phase per K-tile
+      const bool one = g_gemm_opts & 16384;  // bit 14: one phase per K-tile; bit 15 (with 13): 32x32x16 MFMAs
       auto k2 = one ? ((g_gemm_opts & 64) ? k_gemm256s2_bf16_tn<1, 0, 3> : k_gemm256s2_bf16_tn<0, 0, 3>)
                 : (g_gemm_opts & 64)
                     ? (own ? k_gemm256s2_bf16_tn<1, 0, 2>
                            : bal ? k_gemm256s2_bf16_tn<1, 0, 1>
                                  : (nt ? k_gemm256s2_bf16_tn<1, 1, 0> : k_gemm256s2_bf16_tn<1, 0, 0>))
-                    : (own ? k_gemm256s2_bf16_tn<0, 0, 2>
+                    : (own ? ((g_gemm_opts & 32768) ? k_gemm256s2_bf16_tn<0, 0, 6> : k_gemm256s2_bf16_tn<0, 0, 2>)
                            : bal ? k_gemm256s2_bf16_tn<0, 0, 1>
                                  : (nt ? k_gemm256s2_bf16_tn<0, 1, 0> : k_gemm256s2_bf16_tn<0, 0, 0>));
       hipLaunchKernelGGL(k2, dim3(grid), dim3(G2_NT), 0, s, (const u16*)A, (const u16*)Bt, (u16*)C, M, N, K,

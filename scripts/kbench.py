@@ -60,7 +60,8 @@ def main():
     names = {0: "plain-queue", 1: "xcd-range", 2: "deep-prefetch", 4: "staggered-groups",
              12: "staggered-2d-blocks", 13: "staggered-xcd-range-2d-blocks"}
     if os.environ.get("KBENCH_GEMM_ONLY"):
-        names = {4: "staggered-groups", 256 | 4096: "2phase-balanced", 256 | 8192: "2phase-own-a", 256 | 16384: "1phase"}
+        names = {4: "staggered-groups", 256 | 4096: "2phase-balanced", 256 | 8192: "2phase-own-a", 256 | 16384: "1phase",
+                 256 | 8192 | 32768: "2phase-own-a-mfma32"}
     ab = {k: [] for k in names}
     for _ in range(5):
         for opt in names:
