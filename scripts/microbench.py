@@ -79,7 +79,9 @@ def _spawn(target, world, args):
         p.start()
     lat = []
     for _ in ps:
-        _, xs = q.get(timeout=300)
+        r, xs = q.get(timeout=300)
+        if xs is None:
+            raise RuntimeError(f"rank {r}: gang exchange timed out")
         lat += xs
     for p in ps:
         p.join(timeout=60)

@@ -31,9 +31,10 @@ def test_two_daemons_in_one_process_with_exited_tenant():
         d = Daemon(_sock(), gpus=[0], nctx=2, sim=False).start(reaper_s=0.01)
         child = subprocess.Popen([sys.executable, "-c", "pass"])
         child.wait()
-        # registered, then "unregistered" without destroy: its pid stays tracked
-        d.register(name=f"llm{round_}", slots=4, pid=child.pid)
-        d.pids[d.engine.tenant_find(f"llm{round_}")] = child.pid
+        # registered, then "unregistered" without destroy: register() tracks
+        # its pid (a tenant_find here would race the 10 ms reaper)
+        r = d.register(name=f"llm{round_}", slots=4, pid=child.pid)
+        assert r["tenant"] >= 0
         time.sleep(0.05)  # the reaper runs concurrently with the stop below
         d.stop()
         assert d.engine.closed

@@ -91,6 +91,7 @@ def test_survivors_reform_the_gang_without_the_hung_rank():
     common = set(hs[0]) & set(hs[1]) & set(hs[2])
     assert len(common) >= 100
     assert all(hs[0][k] == hs[1][k] == hs[2][k] for k in common)
-    assert max(out[r]["stats"]["timeouts"] for r in survivors) >= 2
+    # two drops, each seen by at least one survivor (not necessarily the same one)
+    assert sum(out[r]["stats"]["timeouts"] for r in survivors) >= 2
     st = out[hung]["stats"]
     assert st["degraded"] and st["reforms"] >= 1, st  # rejoined once, then out for good
