@@ -218,7 +218,9 @@ constexpr u32 kGemmBlock2D = 1u << 17; // mode bit: 2-D per-XCD tile blocks
 // tile blocks (12 panel slices per XCD K-step instead of 18): 1129 vs 1117
 // TF/s plain, 1060 with the XCD-range queue (round 2, interleaved, same box;
 // torch.mm 1416) -- panel traffic is not what holds the kernel back.
-static int g_gemm_opts = 256 | 8192;  // round 3: the 2-phase kernel, own-A-half staging (profiles/r3/kbench_gemm_k.log)
+// round 3: the 2-phase kernel, own-A-half staging (profiles/r3/kbench_gemm_k.log); round 4: C
+// staged through LDS, +1.1-1.3 % in three processes on two boxes (profiles/r4/kbench_gemm_ldsc_s51_s52.jsonl)
+static int g_gemm_opts = 256 | 8192 | 65536;
 constexpr int kG2Half = 128 * 128;           // bytes per half-tile
 constexpr int kG2Buf = 4 * kG2Half;          // A0 A1 B0 B1
 constexpr int kG2Lds = 2 * kG2Buf;           // 128 KiB
@@ -735,6 +737,7 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
         stamp(t, 2);
       }
     } else {
+    constexpr int SB = BAL == 7 ? 2 : BAL;  // BAL 7: BAL 2's loop, LDS-staged C
     bf16x8 a[4][2], b[4][2];
     for (int t = 0; t < nt; ++t) {
       const int buf = t & 1;
@@ -751,13 +754,13 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) a[i][s2] = frag(buf, 0, wr, i * 16, s2);
-      if constexpr (BAL == 2) {  // 4 glds per read interval: B halves here, own A half in R_B
+      if constexpr (SB == 2) {  // 4 glds per read interval: B halves here, own A half in R_B
         if (more) {
           stage(1, 0, t + 1); stage(1, 1, t + 1);
         } else {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-      } else if constexpr (BAL) {
+      } else if constexpr (SB) {
         // balanced staging: g0 4 + 4 glds, g1 6 + 2 (see the schedule note)
         if (wr == 0) {
           if (more) {
@@ -798,12 +801,12 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) a[i][s2] = frag(buf, 0, wr, 64 + i * 16, s2);
-      if constexpr (BAL == 2) {
+      if constexpr (SB == 2) {
         if (more) {
           stage_own_a(t + 1);
           asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // retires this group's B0/B1(t+1)
         }
-      } else if constexpr (BAL) {
+      } else if constexpr (SB) {
         if (wr == 0) {
           if (more) {
             stage(0, 0, t + 1); stage(0, 1, t + 1);
@@ -835,9 +838,9 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
           for (int j = 0; j < 4; ++j)
             acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j][s2], a[i][s2], acc[4 + i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
-      if constexpr (BAL == 2) {  // end of M_B: the group's own A half of t+1 lands before its next R_A
+      if constexpr (SB == 2) {  // end of M_B: the group's own A half of t+1 lands before its next R_A
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      } else if constexpr (BAL) {  // end of M_B: g0 retires its A0(t+1), g1 its A1(t+1), before the barrier
+      } else if constexpr (SB) {  // end of M_B: g0 retires its A0(t+1), g1 its A1(t+1), before the barrier
         if (wr == 0) {
           if (more) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
         } else {
@@ -867,6 +870,31 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
             const u32 hi = (u32)f2bf(acc32[i][j][4 * g + 2]) | ((u32)f2bf(acc32[i][j][4 * g + 3]) << 16);
             *(uint2*)(C + (size_t)m * N + n) = make_uint2(lo, hi);
           }
+    } else if constexpr (BAL == 7) {
+      // C through LDS (the K loop's two buffers are exactly the 256x256 bf16
+      // tile): each wave writes its 8-byte fragments at row m, 8-byte chunk
+      // n/4 XOR 2 (m & 15) (16 rows of one write land in 16 distinct bank
+      // groups), then the workgroup stores 16 rows per pass, each row as 32
+      // contiguous 16-byte stores: full 128-byte lines instead of 32-byte runs.
+      // Every wave's K-loop reads retired before the re-align barrier above.
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int m = wr * 128 + i * 16 + l16;
+          const int c8 = wc * 16 + j * 4 + lq;
+          const u32 lo = (u32)f2bf(acc[i][j][0]) | ((u32)f2bf(acc[i][j][1]) << 16);
+          const u32 hi = (u32)f2bf(acc[i][j][2]) | ((u32)f2bf(acc[i][j][3]) << 16);
+          *(__attribute__((address_space(3))) u32x2*)(lds + m * 512 + ((c8 ^ ((m & 15) << 1)) << 3)) = u32x2{lo, hi};
+        }
+      __syncthreads();
+#pragma unroll
+      for (int p = 0; p < 16; ++p) {
+        const int row = p * 16 + (tid >> 5), c16 = tid & 31;
+        const u32x4 v = *(const __attribute__((address_space(3))) u32x4*)(lds + row * 512 + (((2 * c16) ^ ((row & 15) << 1)) << 3));
+        *(u32x4*)(C + (size_t)(tm * G2_BM + row) * N + tn * G2_BM + c16 * 8) = v;
+      }
+      __syncthreads();  // the next tile's prologue restages buffer 0
     } else {
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -1285,13 +1313,15 @@ int gpbs_hip_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int
     if (g_gemm_opts & 256) {  // 2 phases per K-tile (4 barriers); bit 10: streaming C stores
       // bit 12: balanced staging; bit 13: each group stages its own A half (4 glds per read interval)
       const bool nt = g_gemm_opts & 1024, bal = g_gemm_opts & 4096, own = g_gemm_opts & 8192;
-      const bool one = g_gemm_opts & 16384;  // bit 14: one phase per K-tile; bit 15 (with 13): 32x32x16 MFMAs
+      const bool one = g_gemm_opts & 16384;  // bit 14: one phase per K-tile; bit 15 (with 13): 32x32x16 MFMAs; bit 16 (with 13): C staged through LDS
       auto k2 = one ? ((g_gemm_opts & 64) ? k_gemm256s2_bf16_tn<1, 0, 3> : k_gemm256s2_bf16_tn<0, 0, 3>)
                 : (g_gemm_opts & 64)
                     ? (own ? k_gemm256s2_bf16_tn<1, 0, 2>
                            : bal ? k_gemm256s2_bf16_tn<1, 0, 1>
                                  : (nt ? k_gemm256s2_bf16_tn<1, 1, 0> : k_gemm256s2_bf16_tn<1, 0, 0>))
-                    : (own ? ((g_gemm_opts & 32768) ? k_gemm256s2_bf16_tn<0, 0, 6> : k_gemm256s2_bf16_tn<0, 0, 2>)
+                    : (own ? ((g_gemm_opts & 32768)   ? k_gemm256s2_bf16_tn<0, 0, 6>
+                           : (g_gemm_opts & 65536) ? k_gemm256s2_bf16_tn<0, 0, 7>
+                                                   : k_gemm256s2_bf16_tn<0, 0, 2>)
                            : bal ? k_gemm256s2_bf16_tn<0, 0, 1>
                                  : (nt ? k_gemm256s2_bf16_tn<0, 1, 0> : k_gemm256s2_bf16_tn<0, 0, 0>));
       hipLaunchKernelGGL(k2, dim3(grid), dim3(G2_NT), 0, s, (const u16*)A, (const u16*)Bt, (u16*)C, M, N, K,

@@ -61,14 +61,15 @@ def main():
              12: "staggered-2d-blocks", 13: "staggered-xcd-range-2d-blocks"}
     if os.environ.get("KBENCH_GEMM_ONLY"):
         names = {4: "staggered-groups", 256 | 4096: "2phase-balanced", 256 | 8192: "2phase-own-a", 256 | 16384: "1phase",
-                 256 | 8192 | 32768: "2phase-own-a-mfma32"}
+                 256 | 8192 | 32768: "2phase-own-a-mfma32",
+                 256 | 8192 | 65536: "2phase-own-a-lds-c"}
     ab = {k: [] for k in names}
     for _ in range(5):
         for opt in names:
             L.gpbs_hip_set_gemm_opts(opt)
             ab[opt].append(timed(lambda: L.gpbs_hip_gemm_bf16(K._ptr(A), K._ptr(B), K._ptr(Cm), n, n, n, K._ptr(q),
                                                               None, 0, 0, None, None, 0, s), args.iters, zero))
-    L.gpbs_hip_set_gemm_opts(256 | 8192)
+    L.gpbs_hip_set_gemm_opts(256 | 8192 | 65536)
     for opt, v in ab.items():
         ms = sorted(v)[len(v) // 2]
         out.append({"kernel": "gemm_bf16", "variant": names[opt], "shape": [n, n, n],
@@ -86,7 +87,7 @@ def main():
         err = (Cm[:512].float() - ref).abs().max().item()
         out.append({"kernel": "gemm_bf16", "variant": names[opt], "check_max_abs_err": err,
                     "ok": err < 0.02 * ref.abs().max().item()})
-    L.gpbs_hip_set_gemm_opts(256 | 8192)
+    L.gpbs_hip_set_gemm_opts(256 | 8192 | 65536)
     if os.environ.get("KBENCH_GEMM_ONLY"):
         for r in out:
             print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}))
