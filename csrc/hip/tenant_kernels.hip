@@ -737,7 +737,7 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
         stamp(t, 2);
       }
     } else {
-    constexpr int SB = BAL == 7 ? 2 : BAL;  // BAL 7: BAL 2's loop, LDS-staged C
+    constexpr int SB = (BAL == 7 || BAL == 8) ? 2 : BAL;  // BAL 7/8: BAL 2's loop, LDS-staged C
     bf16x8 a[4][2], b[4][2];
     for (int t = 0; t < nt; ++t) {
       const int buf = t & 1;
@@ -870,7 +870,7 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
             const u32 hi = (u32)f2bf(acc32[i][j][4 * g + 2]) | ((u32)f2bf(acc32[i][j][4 * g + 3]) << 16);
             *(uint2*)(C + (size_t)m * N + n) = make_uint2(lo, hi);
           }
-    } else if constexpr (BAL == 7) {
+    } else if constexpr (BAL == 7 || BAL == 8) {
       // C through LDS (the K loop's two buffers are exactly the 256x256 bf16
       // tile): each wave writes its 8-byte fragments at row m, 8-byte chunk
       // n/4 XOR 2 (m & 15) (16 rows of one write land in 16 distinct bank
@@ -892,7 +892,12 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
       for (int p = 0; p < 16; ++p) {
         const int row = p * 16 + (tid >> 5), c16 = tid & 31;
         const u32x4 v = *(const __attribute__((address_space(3))) u32x4*)(lds + row * 512 + (((2 * c16) ^ ((row & 15) << 1)) << 3));
-        *(u32x4*)(C + (size_t)(tm * G2_BM + row) * N + tn * G2_BM + c16 * 8) = v;
+        u32x4* dst = (u32x4*)(C + (size_t)(tm * G2_BM + row) * N + tn * G2_BM + c16 * 8);
+        if constexpr (BAL == 8) {  // streaming full-line stores (opts bit 17)
+          __builtin_nontemporal_store(v, dst);
+        } else {
+          *dst = v;
+        }
       }
       __syncthreads();  // the next tile's prologue restages buffer 0
     } else {
@@ -1313,14 +1318,14 @@ int gpbs_hip_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int
     if (g_gemm_opts & 256) {  // 2 phases per K-tile (4 barriers); bit 10: streaming C stores
       // bit 12: balanced staging; bit 13: each group stages its own A half (4 glds per read interval)
       const bool nt = g_gemm_opts & 1024, bal = g_gemm_opts & 4096, own = g_gemm_opts & 8192;
-      const bool one = g_gemm_opts & 16384;  // bit 14: one phase per K-tile; bit 15 (with 13): 32x32x16 MFMAs; bit 16 (with 13): C staged through LDS
+      const bool one = g_gemm_opts & 16384;  // bit 14: one phase per K-tile; bit 15 (with 13): 32x32x16 MFMAs; bit 16 (with 13): C staged through LDS; bit 17 (with 16): its stores non-temporal
       auto k2 = one ? ((g_gemm_opts & 64) ? k_gemm256s2_bf16_tn<1, 0, 3> : k_gemm256s2_bf16_tn<0, 0, 3>)
                 : (g_gemm_opts & 64)
                     ? (own ? k_gemm256s2_bf16_tn<1, 0, 2>
                            : bal ? k_gemm256s2_bf16_tn<1, 0, 1>
                                  : (nt ? k_gemm256s2_bf16_tn<1, 1, 0> : k_gemm256s2_bf16_tn<1, 0, 0>))
                     : (own ? ((g_gemm_opts & 32768)   ? k_gemm256s2_bf16_tn<0, 0, 6>
-                           : (g_gemm_opts & 65536) ? k_gemm256s2_bf16_tn<0, 0, 7>
+                           : (g_gemm_opts & 65536) ? ((g_gemm_opts & 131072) ? k_gemm256s2_bf16_tn<0, 0, 8> : k_gemm256s2_bf16_tn<0, 0, 7>)
                                                    : k_gemm256s2_bf16_tn<0, 0, 2>)
                            : bal ? k_gemm256s2_bf16_tn<0, 0, 1>
                                  : (nt ? k_gemm256s2_bf16_tn<0, 1, 0> : k_gemm256s2_bf16_tn<0, 0, 0>));

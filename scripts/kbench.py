@@ -62,7 +62,8 @@ def main():
     if os.environ.get("KBENCH_GEMM_ONLY"):
         names = {4: "staggered-groups", 256 | 4096: "2phase-balanced", 256 | 8192: "2phase-own-a", 256 | 16384: "1phase",
                  256 | 8192 | 32768: "2phase-own-a-mfma32",
-                 256 | 8192 | 65536: "2phase-own-a-lds-c"}
+                 256 | 8192 | 65536: "2phase-own-a-lds-c",
+                 256 | 8192 | 65536 | 131072: "2phase-own-a-lds-c-nt"}
     ab = {k: [] for k in names}
     for _ in range(5):
         for opt in names:
