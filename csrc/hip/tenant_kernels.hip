@@ -219,8 +219,10 @@ constexpr u32 kGemmBlock2D = 1u << 17; // mode bit: 2-D per-XCD tile blocks
 // TF/s plain, 1060 with the XCD-range queue (round 2, interleaved, same box;
 // torch.mm 1416) -- panel traffic is not what holds the kernel back.
 // round 3: the 2-phase kernel, own-A-half staging (profiles/r3/kbench_gemm_k.log); round 4: C
-// staged through LDS, +1.1-1.3 % in three processes on two boxes (profiles/r4/kbench_gemm_ldsc_s51_s52.jsonl)
-static int g_gemm_opts = 256 | 8192 | 65536;
+// staged through LDS, +1.1-1.3 % in three processes on two boxes (profiles/r4/kbench_gemm_ldsc_s51_s52.jsonl),
+// its full-line stores non-temporal, another +1.0-1.3 % in three processes on two boxes
+// (profiles/r4/kbench_gemm_ldsc_nt_s54_s55.jsonl)
+static int g_gemm_opts = 256 | 8192 | 65536 | 131072;
 constexpr int kG2Half = 128 * 128;           // bytes per half-tile
 constexpr int kG2Buf = 4 * kG2Half;          // A0 A1 B0 B1
 constexpr int kG2Lds = 2 * kG2Buf;           // 128 KiB
