@@ -213,17 +213,21 @@ def main():
     # the GPU's clock / power / temperature / throttle residency over every
     # timed run (host thread, amdsmi or sysfs): tells a DVFS / power-state
     # drift from a queue / pipe effect
-    from pbs_amd.utils.gpustate import GpuStateRecorder, device_bdf
+    from pbs_amd.utils.gpustate import GpuStateRecorder, bdf_mismatch, device_bdf
     bdf = device_bdf(local)
     gpustate = GpuStateRecorder(bdf, period_s=0.2).start()
     rank_diag = {"rank": rank, "local_rank": local, "device_bdf": bdf, "gpu_state_source": gpustate.source,
                  "counters": counters, "cu_map_ok": cu_map.get("ok") if cu_map else None}
     if counters == "hw":
         rank_diag["hwc_agent"] = hwc.agent()
-        if rank_diag["hwc_agent"]["bdf"] != bdf:
+        ag = rank_diag["hwc_agent"].get("bdf")
+        if bdf_mismatch(ag, bdf):
             print(f"bench.py: rank {rank} counts on agent {rank_diag['hwc_agent']} but runs on {bdf}",
                   file=sys.stderr)
-            sys.exit(3)
+            if world == 1:
+                sys.exit(3)
+        elif not ag or not bdf:  # an unknown address is no evidence of a mismatch
+            print(f"bench.py: rank {rank}: counted agent {ag} / device {bdf} not both known", file=sys.stderr)
     groups = {}
     if world > 1:
         import torch.distributed as dist
@@ -236,6 +240,14 @@ def main():
         # cross-GPU gang epochs (own thread); only used with --gang-transport dist
         groups["gang"] = dist.new_group(backend="nccl" if args.gang_rccl and not args.rehearse else "gloo")
         groups["coll"] = dist.new_group(backend="gloo" if args.rehearse else "nccl")
+        # a rank counting on another GPU's agent fails the whole job, after
+        # the rendezvous so no peer is left waiting in it
+        bad = torch.tensor([1 if counters == "hw" and bdf_mismatch(rank_diag["hwc_agent"].get("bdf"), bdf) else 0])
+        dist.all_reduce(bad, group=groups["ctrl"])
+        if int(bad.item()):
+            print(f"bench.py: {int(bad.item())} rank(s) count on the wrong agent", file=sys.stderr)
+            dist.destroy_process_group()
+            sys.exit(3)
 
     from pbs_amd import build
     if rank == 0:  # one builder per node; the others wait (no concurrent relink)
@@ -384,11 +396,20 @@ def main():
     line["ranks"] = allr
     gpustate.stop()
     if rank == 0:
-        print(json.dumps(line), flush=True)
-        if args.out:
-            with open(args.out, "w") as f:
+        # the detail record (every policy table, per-tenant rows, ranks, GPU
+        # state) goes to --out; stdout gets the compact contract line, last
+        from pbs_amd.bench.report import compact_line, mix_digest
+        out = args.out or os.path.join(ROOT, "gpurun_out", "bench_detail.json")
+        try:
+            os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
+            with open(out, "w") as f:
                 json.dump({"line": line, "results": {m: {"runs": r["runs"], "order": r["order"]}
                                                      for m, r in results.items()}}, f, indent=1)
+        except OSError as ex:
+            print(f"bench.py: detail record not written: {ex}", file=sys.stderr)
+            out = ""
+        digests = {m: mix_digest(results[m]["summary"], results[m]["runs"]) for m in mixes}
+        print(json.dumps(compact_line(line, digests, os.path.relpath(out, ROOT) if out else "")), flush=True)
     if world > 1:
         import torch.distributed as dist
         dist.barrier(group=groups["ctrl"])

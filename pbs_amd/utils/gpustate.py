@@ -60,6 +60,28 @@ def device_bdf(device: int = 0) -> Optional[str]:
         return None
 
 
+def bdf_key(bdf: Optional[str]):
+    """(domain, bus, device) of a "dddd:bb:dd.f" / "bb:dd.f" address, the
+    function dropped; None when it does not parse."""
+    if not bdf:
+        return None
+    try:
+        parts = bdf.lower().split(":")
+        dom = int(parts[0], 16) if len(parts) == 3 else 0
+        bus = int(parts[-2], 16)
+        dev = int(parts[-1].split(".")[0], 16)
+        return (dom, bus, dev)
+    except (ValueError, IndexError):
+        return None
+
+
+def bdf_mismatch(a: Optional[str], b: Optional[str]) -> bool:
+    """True only when both addresses are known and name different devices
+    (an unknown address is no evidence of a mismatch)."""
+    ka, kb = bdf_key(a), bdf_key(b)
+    return ka is not None and kb is not None and ka != kb
+
+
 class _AmdSmi:
     def __init__(self, bdf: Optional[str]):
         import amdsmi
