@@ -1096,34 +1096,27 @@ typedef struct gpbs_runner_stats {
 namespace {
 
 // Process-wide pool of CU-masked streams.  Every CU-masked stream is a
-// hardware queue of its own, and destroying one does not give the queue back
-// for good: a process that built and tore down runners mix after mix (bench.py
-// --mix all: 4mix, then phase, then 8mix) ran its last mix with the
-// SE-partitioned policies at 0.71 of what the same mix measured in a fresh
-// process (1.14, profiles/r3/bench_full_5rep_a.json vs b8_alone.json) -- the
-// hardware scheduler time-slicing an over-subscribed queue set.  Runners
-// therefore take masked streams from this pool and return them (drained)
-// when they close, so the process holds at most as many masked queues as it
-// ever used at once.
-// Process-wide pool of CU-masked streams.  Every CU-masked stream is a
 // hardware queue of its own and the process never gets one back; past the
 // hardware scheduler's queue slots it oversubscribes and time-slices ALL
 // queues, idle ones included.  Measured (scripts/queue_budget.py,
 // profiles/r4/queue_budget*.log): a solo GEMM keeps its rate up to 20 extra
 // masked queues and loses 24 % at 24, 63 % at 48; with the device-counting
-// context running the knee moves down by about four queues (the profiler's
-// own).  The round-3 live-counter "drift" and the bimodal 8mix runs were this
-// oversubscription.
-//
-// So masked queues are SHARED by key: runners that hold the same set of
-// (XCD, SE) partitions -- co-sharers of a time-shared region, which never run
-// at the same time -- launch on one queue; runners on disjoint sets (split
-// layouts, which run concurrently) get their own.  A queue nobody holds is
-// re-keyed before a new one is created, and a mask never has more than
-// masked_cap() keyed queues, so the process holds a few masked queues, not
-// one per runner.  Key 0 = exclusive (never shared).  GPBS_SHARE_QUEUES=0:
-// every acquire exclusive (the round-3 behaviour).
-struct MaskedStreams {
+// context running the knee moves down by about four queues.  So queues are
+// pooled (a runner returns its queue when it closes or changes layout) and
+// SHARED by key: runners that hold the same set of (XCD, SE) partitions --
+// co-sharers of a time-shared region, which never run at the same time --
+// launch on one queue.  Runners on different sets run concurrently and get
+// their own queue: two of them on one queue run their units one after
+// another (round 4 capped keyed queues at two per mask, and the 8mix split
+// layouts -- three or four concurrent layouts per class half -- collapsed
+// from 1.10 to 0.78 solo-equivalents).  Only past kMaskedBudget live queues
+// on a device does a new layout share another key's least-held queue, and
+// every such share is counted (cross_key_shares, reported with the run).
+// The policy is host-only code (MaskedPoolCore), checked on the CPU by
+// gpbs_hip_masked_pool_selftest with fake queue handles.
+constexpr int kMaskedBudget = 16;
+
+struct MaskedPoolCore {
   struct Ent {
     int device;
     uint32_t m[8];
@@ -1133,130 +1126,78 @@ struct MaskedStreams {
   };
   std::mutex mu;
   std::vector<Ent> ents;
-  int created = 0;
-};
-MaskedStreams& masked_pool() {
-  static MaskedStreams* p = new MaskedStreams;  // never destroyed: streams outlive static teardown order
-  return *p;
-}
-bool share_queues() {
-  static const bool v = [] {
-    const char* e = std::getenv("GPBS_SHARE_QUEUES");
-    return !e || std::atoi(e) != 0;
-  }();
-  return v;
-}
-// At most this many keyed (gated-runner) queues per CU mask
-// (GPBS_MASKED_CAP, default 2; 0 = no cap): past it a new layout shares the
-// least-held queue of its mask.  Runners that share a queue run their units
-// one after another; in a time-shared region that costs nothing (one owner
-// at a time), in a split layout it serialises the tenants of the split, so
-// the cap is set above the splits the budget layout makes within a class
-// half (two blocks).
-int masked_cap() {
-  static const int v = [] {
-    const char* e = std::getenv("GPBS_MASKED_CAP");
-    return e ? std::max(0, std::atoi(e)) : 2;
-  }();
-  return v;
-}
-// Queues per layout key (GPBS_KEY_QUEUES, default 1): the co-sharers of a
-// time-shared region spread over this many queues (least-held first), so an
-// incoming owner's kernel need not wait in order behind the outgoing owner's
-// draining one on a single queue.
-int key_queues() {
-  static const int v = [] {
-    const char* e = std::getenv("GPBS_KEY_QUEUES");
-    return e ? std::max(1, std::atoi(e)) : 1;
-  }();
-  return v;
-}
-void se_cu_mask(const u32 se_bits[kXcds], uint32_t m[8]);
-// GPBS_QUEUE_PREALLOC=1: create the device's class-half queues up front, back
-// to back and interleaved (compute, memory, memory, compute, memory), before
-// anything else takes a masked queue.  Which pipe a hardware queue lands on
-// follows its creation order; queues created one by one as layouts come and
-// go put the compute region's and a memory region's queue on one pipe in
-// some runs (8mix: every slow run had the GEMMs on pool queue 5 and a stream
-// on queue 1, profiles/r4/queue_index_s32.txt), where a dispatch that waits
-// for CUs blocks the other queue's dispatches.
-void masked_prealloc_locked(MaskedStreams& P, int dev) {
-  static const bool on = [] {
-    const char* e = std::getenv("GPBS_QUEUE_PREALLOC");
-    return e && std::atoi(e) != 0;
-  }();
-  if (!on) return;
-  for (auto& e : P.ents)
-    if (e.device == dev) return;
-  for (int h : {0, 1, 1, 0, 1}) {
-    u32 bits[kXcds];
-    for (int x = 0; x < kXcds; ++x) bits[x] = h ? 0xCu : 0x3u;
-    uint32_t m[8];
-    se_cu_mask(bits, m);
-    hipStream_t s = nullptr;
-    if (hipExtStreamCreateWithCUMask(&s, 8, m) != hipSuccess) return;
-    P.ents.push_back({dev, {}, s, 0u, 0});
-    std::memcpy(P.ents.back().m, m, sizeof(P.ents.back().m));
-    P.created++;
+  uint64_t created = 0, cross_key_shares = 0;
+  int held_max = 0;  // high-water mark of queues held at once (reset with reset_max)
+
+  int held_locked(int dev) const {
+    int n = 0;
+    for (const auto& e : ents) n += e.device == dev && e.refs > 0;
+    return n;
   }
+  // key 0: exclusive (never shared).  create(m) makes a new queue (nullptr on
+  // failure).  Caller does not hold mu.
+  template <class Create>
+  hipStream_t acquire(int dev, const uint32_t m[8], uint32_t key, Create&& create) {
+    std::lock_guard<std::mutex> g(mu);
+    Ent* same = nullptr;   // this layout's queue
+    Ent* idle = nullptr;   // a queue of this mask nobody holds (same key preferred)
+    Ent* least = nullptr;  // least-held keyed queue of this mask
+    int live = 0;
+    for (auto& e : ents) {
+      if (e.device != dev) continue;
+      live++;
+      if (std::memcmp(e.m, m, sizeof(e.m)) != 0) continue;
+      if (key && e.key == key && e.refs > 0 && (!same || e.refs < same->refs)) same = &e;
+      if (e.refs == 0 && (!idle || (key && e.key == key && idle->key != key))) idle = &e;
+      if (e.key && e.refs > 0 && (!least || e.refs < least->refs)) least = &e;
+    }
+    hipStream_t s = nullptr;
+    if (same) {
+      same->refs++;
+      s = same->s;
+    } else if (idle) {
+      idle->key = key;
+      idle->refs = 1;
+      s = idle->s;
+    } else if (live < kMaskedBudget || !key || !least) {
+      s = create(m);
+      if (!s) return nullptr;
+      ents.push_back({dev, {}, s, key, 1});
+      std::memcpy(ents.back().m, m, sizeof(ents.back().m));
+      created++;
+    } else {  // over budget: share another layout's queue (serialises the two)
+      least->refs++;
+      cross_key_shares++;
+      s = least->s;
+    }
+    held_max = std::max(held_max, held_locked(dev));
+    return s;
+  }
+  void release(hipStream_t s) {
+    if (!s) return;
+    std::lock_guard<std::mutex> g(mu);
+    for (auto& e : ents)
+      if (e.s == s && e.refs > 0) {
+        e.refs--;
+        return;
+      }
+  }
+};
+MaskedPoolCore& masked_pool() {
+  static MaskedPoolCore* p = new MaskedPoolCore;  // never destroyed: streams outlive static teardown order
+  return *p;
 }
 hipStream_t masked_acquire_key(const uint32_t m[8], uint32_t key) {
   int dev = 0;
   hipGetDevice(&dev);
-  if (!share_queues()) key = 0;
-  MaskedStreams& P = masked_pool();
-  {
-    std::lock_guard<std::mutex> g(P.mu);
-    masked_prealloc_locked(P, dev);
-    MaskedStreams::Ent* idle = nullptr;
-    MaskedStreams::Ent* least = nullptr;
-    MaskedStreams::Ent* same = nullptr;  // least-held queue of this layout
-    int keyed = 0, nsame = 0;
-    for (auto& e : P.ents) {
-      if (e.device != dev || std::memcmp(e.m, m, sizeof(e.m)) != 0) continue;
-      if (key && e.key == key && e.refs > 0) {
-        nsame++;
-        if (!same || e.refs < same->refs) same = &e;
-      }
-      if (e.refs == 0 && (!idle || (key && e.key == key))) idle = &e;
-      if (e.key && e.refs > 0) {
-        keyed++;
-        if (!least || e.refs < least->refs) least = &e;
-      }
-    }
-    if (same && (nsame >= key_queues() || (!idle && masked_cap() > 0 && keyed >= masked_cap()))) {
-      same->refs++;  // the same layout: share its (least-held) queue
-      return same->s;
-    }
-    if (idle) {  // re-key a queue nobody holds
-      idle->key = key;
-      idle->refs = 1;
-      return idle->s;
-    }
-    if (key && masked_cap() > 0 && keyed >= masked_cap() && least) {  // at the cap: share the least-held
-      least->refs++;
-      return least->s;
-    }
-  }
-  hipStream_t s = nullptr;
-  if (hipExtStreamCreateWithCUMask(&s, 8, const_cast<uint32_t*>(m)) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> g(P.mu);
-  P.ents.push_back({dev, {}, s, key, 1});
-  std::memcpy(P.ents.back().m, m, sizeof(P.ents.back().m));
-  P.created++;
-  return s;
+  return masked_pool().acquire(dev, m, key, [](const uint32_t* mm) -> hipStream_t {
+    hipStream_t s = nullptr;
+    return hipExtStreamCreateWithCUMask(&s, 8, const_cast<uint32_t*>(mm)) == hipSuccess ? s : nullptr;
+  });
 }
 hipStream_t masked_acquire(const uint32_t m[8]) { return masked_acquire_key(m, 0); }
-void masked_release(const uint32_t*, hipStream_t s) {
-  if (!s) return;
-  MaskedStreams& P = masked_pool();
-  std::lock_guard<std::mutex> g(P.mu);
-  for (auto& e : P.ents)
-    if (e.s == s && e.refs > 0) {
-      e.refs--;
-      return;
-    }
-}
+void masked_release(const uint32_t*, hipStream_t s) { masked_pool().release(s); }
+void se_cu_mask(const u32 se_bits[kXcds], uint32_t m[8]);
 
 // CU mask of one half of every XCD.  hipExtStreamCreateWithCUMask bit b
 // selects logical CU b/8 of XCD b%8 (an XCD left with no bit runs
@@ -1302,6 +1243,34 @@ struct Runner {
   // grid to the owned CUs removes that coupling (GATE_SE still revokes).
   hipStream_t se_stream[2] = {nullptr, nullptr};  // SEs {0,1} / {2,3} of every XCD (latency lane only)
   hipStream_t key_stream = nullptr;  // gated SE mode: the masked queue of the layout it holds (shared by key)
+  // Units launched on a queue this runner has since given back (a layout
+  // change) may still run: an event recorded on the old queue at the switch,
+  // waited for at stop before the hold words and queue memory are released.
+  std::vector<hipEvent_t> retired_ev;
+  void retire_stream(hipStream_t s) {
+    for (size_t i = 0; i < retired_ev.size();)  // drop the ones already passed
+      if (hipEventQuery(retired_ev[i]) == hipSuccess) {
+        hipEventDestroy(retired_ev[i]);
+        retired_ev[i] = retired_ev.back();
+        retired_ev.pop_back();
+      } else {
+        ++i;
+      }
+    hipEvent_t e = nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+      hipStreamSynchronize(s);
+      return;
+    }
+    hipEventRecord(e, s);
+    retired_ev.push_back(e);
+  }
+  void drain_retired() {
+    for (hipEvent_t e : retired_ev) {
+      hipEventSynchronize(e);
+      hipEventDestroy(e);
+    }
+    retired_ev.clear();
+  }
   uint32_t key_bits = 0;             // ... its key: the owned (XCD, SE) partition set
   int key_half = -1;
   int cur_grid = 0;  // grid for the stream pick_stream chose (0: kernel default)
@@ -1393,7 +1362,10 @@ struct Runner {
     if (!key_stream || bits != key_bits || half != key_half) {  // a new layout: its queue (shared with co-sharers)
       uint32_t m[8];
       se_half_mask(half, m);
-      if (key_stream) masked_release(m, key_stream);
+      if (key_stream) {
+        retire_stream(key_stream);
+        masked_release(m, key_stream);
+      }
       key_stream = masked_acquire_key(m, bits);
       key_bits = bits;
       key_half = half;
@@ -1415,6 +1387,7 @@ struct Runner {
       uint32_t m[8];
       if (se_stream[half ^ 1]) {  // hold one masked queue per runner at a time
         se_half_mask(half ^ 1, m);
+        retire_stream(se_stream[half ^ 1]);
         masked_release(m, se_stream[half ^ 1]);
         se_stream[half ^ 1] = nullptr;
       }
@@ -1663,6 +1636,7 @@ struct Runner {
     for (hipStream_t h : se_stream)
       if (h) hipStreamSynchronize(h);
     if (key_stream) hipStreamSynchronize(key_stream);
+    drain_retired();
     for (int qi = 0; qi < nq; ++qi) hold_drop(qi);  // stopped with latency units in flight
     std::lock_guard<std::mutex> g(mu);
     idle_cv.notify_all();
@@ -2564,15 +2538,64 @@ int gpbs_gpu_adapt_stats(void* p, uint64_t* calls, uint64_t* late, uint64_t* bus
 }
 
 // Process-wide CU-masked queue pool: out[0] masked streams ever created,
-// out[1] currently free (the rest are held by runners).  Every created one is
-// a hardware queue this process keeps.
-int gpbs_gpu_masked_pool(uint64_t* out2) {
-  MaskedStreams& P = masked_pool();
+// out[1] currently free (the rest are held by runners), out[2] acquires that
+// had to share another layout's queue (over the budget: those layouts ran
+// serialised), out[3] most queues held at once since the last reset.  Every
+// created one is a hardware queue this process keeps.  reset: restart the
+// high-water mark at the number held now.
+int gpbs_gpu_masked_pool(uint64_t* out4, int reset) {
+  MaskedPoolCore& P = masked_pool();
+  int dev = 0;
+  hipGetDevice(&dev);
   std::lock_guard<std::mutex> g(P.mu);
-  out2[0] = (uint64_t)P.created;
+  if (reset) P.held_max = P.held_locked(dev);
+  if (!out4) return 0;
+  out4[0] = P.created;
   uint64_t idle = 0;
   for (auto& e : P.ents) idle += e.refs == 0;
-  out2[1] = idle;
+  out4[1] = idle;
+  out4[2] = P.cross_key_shares;
+  out4[3] = (uint64_t)P.held_max;
+  return 0;
+}
+
+// Host check of the masked-queue pool policy: fake queue handles,
+// no HIP call.  Returns 0 or the number of the first failed check.
+int gpbs_hip_masked_pool_selftest(void) {
+  MaskedPoolCore P;
+  uintptr_t next = 0x1000;
+  auto mk = [&](const uint32_t*) -> hipStream_t { return (hipStream_t)(next += 0x10); };
+  uint32_t mc[8], mm[8];
+  for (int w = 0; w < 8; ++w) mc[w] = 0x33333333u, mm[w] = 0xCCCCCCCCu;
+  // 1. co-sharers of one layout share one queue
+  hipStream_t a = P.acquire(0, mc, 0x11, mk), b = P.acquire(0, mc, 0x11, mk);
+  if (!a || a != b || P.created != 1) return 1;
+  // 2. concurrent layouts on one mask get their own queues (no cap below the budget)
+  hipStream_t c = P.acquire(0, mc, 0x22, mk), d = P.acquire(0, mc, 0x44, mk), e = P.acquire(0, mc, 0x88, mk);
+  if (c == a || d == a || e == a || c == d || d == e || c == e || P.created != 4 || P.cross_key_shares) return 2;
+  // 3. an exclusive acquire never gets a queue held under another key
+  hipStream_t x = P.acquire(0, mc, 0, mk);
+  if (x == a || x == c || x == d || x == e || P.created != 5) return 3;
+  // 4. a released queue is re-keyed before a new one is created; refs drop to zero first
+  P.release(c);
+  hipStream_t f = P.acquire(0, mc, 0x99, mk);
+  if (f != c || P.created != 5) return 4;
+  P.release(a);
+  hipStream_t g2 = P.acquire(0, mc, 0x55, mk);  // a still held once (b): not idle
+  if (g2 == a || P.created != 6) return 5;
+  // 5. another mask / device never shares
+  hipStream_t h = P.acquire(0, mm, 0x11, mk), i = P.acquire(1, mc, 0x11, mk);
+  if (h == a || i == a || h == i || P.created != 8) return 6;
+  // 6. past the budget a new layout shares the least-held keyed queue, counted
+  for (int k = 0; (int)P.created < kMaskedBudget + 1; ++k) P.acquire(0, mm, 0x1000u + k, mk);
+  const uint64_t cr = P.created;
+  hipStream_t j = P.acquire(0, mc, 0x7777, mk);
+  if (P.created != cr || P.cross_key_shares != 1 || !j) return 7;
+  // 7. an exclusive acquire past the budget still gets a queue of its own
+  hipStream_t k2 = P.acquire(0, mc, 0, mk);
+  for (auto& en : P.ents)
+    if (en.s == k2 && en.refs != 1) return 8;
+  if (P.held_max < kMaskedBudget) return 9;
   return 0;
 }
 
@@ -2758,7 +2781,7 @@ int gpbs_runner_queue(void* p) {
   Runner* r = (Runner*)p;
   hipStream_t s = r->key_stream ? r->key_stream : (r->se_stream[0] ? r->se_stream[0] : r->se_stream[1]);
   if (!s) return -1;
-  MaskedStreams& P = masked_pool();
+  MaskedPoolCore& P = masked_pool();
   std::lock_guard<std::mutex> g(P.mu);
   for (size_t i = 0; i < P.ents.size(); ++i)
     if (P.ents[i].s == s) return (int)i;

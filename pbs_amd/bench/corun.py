@@ -991,6 +991,7 @@ class Corun:
         quanta = {n: [] for n in self.tid}
         layout = {n: [] for n in self.throughput}  # budget SE sets per step (bit c = SE c)
         self._rs0 = {n: r.stats() for n, r in self.runners.items() if isinstance(r, Runner)}
+        self.ctx.masked_pool_reset()
         self._barrier()
         t0 = time.perf_counter()
         g0 = time.monotonic()
@@ -1042,6 +1043,11 @@ class Corun:
         nq = kfd_queues()
         if nq is not None:  # hardware queues this process holds (KFD): oversubscription shows here
             res["kfd_queues"] = nq
+        # CU-masked queues held at once over the run and acquires that had to
+        # share another layout's queue (serialised layouts)
+        gs = self.ctx.stats()
+        res["masked_queues"] = {"held_max": gs["masked_queues_held_max"], "created": gs["masked_queues_created"],
+                                "cross_key_shares": gs["masked_cross_key_shares"]}
         res["host"] = {k: round(h1[k] - h0[k], 3) for k in h1 if k in h0}
         if "cpu_s" in res["host"]:
             res["host"]["cpu_util"] = round(res["host"]["cpu_s"] / (wall_ms_local / 1e3), 2)  # cores busy

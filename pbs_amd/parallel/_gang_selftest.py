@@ -46,10 +46,15 @@ def worker(rank: int, world: int, port: int, q, seconds: float = 0.8, epoch_ms: 
     dist.destroy_process_group()
 
 
-def atc_worker(rank: int, world: int, port: int, q, seconds: float = 0.8, epoch_ms: float = 5.0):
+def atc_worker(rank: int, world: int, port: int, q, epoch_ms: float = 5.0, periods: int = 40):
     """Node-level sync over the gang epochs: an ATC pool per rank (rank 0's
     tenant reports heavy spin-waits, so its local minimum slice is small) and
-    per-rank counters; returns each rank's applied slice and node metrics."""
+    per-rank counters; returns each rank's applied slice and node metrics.
+
+    Deterministic under any host load: the engines run on a simulated clock,
+    so every ATC apply happens in the load phase below and the local minima
+    are frozen before the gang starts; the check then waits for named gang
+    epochs (three exchanges after the start on every rank), not wall time."""
     import torch.distributed as dist
 
     from pbs_amd.core.engine import Engine
@@ -57,34 +62,43 @@ def atc_worker(rank: int, world: int, port: int, q, seconds: float = 0.8, epoch_
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    e = Engine(sched="atc", partitions=[(rank, x) for x in range(2)], quantum_align_us=0)
+    e = Engine(sched="atc", sim_clock=True, partitions=[(rank, x) for x in range(2)], quantum_align_us=0)
     e.tenant_create("Domain-0", nslots=1)
     t = e.tenant_create("t", nslots=2)
-    e.start()
     e.wake(t)
-    dist.barrier()  # spawn start-up skew on a busy host would eat the short window
-    g = GangCoordinator(e, None, [t], epoch_ms=epoch_ms, share=0.0, atc_pool=0, metric_tenants=[t],
-                        metric_every=2).start()
-    t_end = time.monotonic() + seconds
-    k = 0
-    node = {}
-    while time.monotonic() < t_end:
-        k += 1
-        m = g.node_metrics.get(t, {})
-        if m.get("inst", 0) > node.get("inst", 0):
-            node = dict(m)
+    period_ns = 21_000_000  # the ATC apply period
+    for k in range(1, periods + 1):
         if rank == 0:
             e.report_wait(t, 200_000)  # heavy lock-holder preemption symptom
         for s in range(2):  # modeled counters: rank r retires (r+1) x 1e6 instructions per ms
             e.set_pmc(e.slot_id(t, s), [k * (rank + 1) * 500_000, k * 1_000_000, k * 1000, k * 100 * (rank + 1)])
-        time.sleep(0.001)
-    time.sleep(0.05)
-    local = e.atc_sync(0, 0)
+        e.advance(e.now() + period_ns)
+    # one more count and up to the first metric tick after it: the period's
+    # deltas (what the gang SUM-reduces) are non-zero when the clock stops
+    k = periods + 1
+    for s in range(2):
+        e.set_pmc(e.slot_id(t, s), [k * (rank + 1) * 500_000, k * 1_000_000, k * 1000, k * 100 * (rank + 1)])
+    for _ in range(100):
+        e.advance(e.now() + 50_000)
+        if e.tenant_info(t).pmc[0]:
+            break
+    local = e.atc_sync(0, 0)  # frozen from here on: the clock no longer moves
+    dist.barrier()
+    g = GangCoordinator(e, None, [t], epoch_ms=epoch_ms, share=0.0, atc_pool=0, metric_tenants=[t],
+                        metric_every=1).start()
+    t_end = time.monotonic() + 30.0
+    while (g.metric_syncs < 3 or g.atc_global_us <= 0) and time.monotonic() < t_end:
+        time.sleep(0.002)
+    syncs = g.metric_syncs
+    node = dict(g.node_metrics.get(t, {}))
+    # one more named epoch past the one read, so both ranks' applies are in
+    target = g.epoch + 2
+    while g.epoch < target and time.monotonic() < t_end:
+        time.sleep(0.002)
     g.stop()
     info = e.tenant_info(t)
-    e.stop()
     q.put({"rank": rank, "local_min": local, "tslice": info.tslice_us, "stats": g.stats(),
-           "node": node})
+           "node": node, "syncs_seen": syncs})
     dist.destroy_process_group()
 
 

@@ -25,7 +25,13 @@ def wait_worker(rank: int, world: int, port: int, q, lag_ms: float, board_name: 
     e.wake(t)
     board = ArrivalBoard(board_name, rank, world)
     dist.barrier()
-    probe = WaitProbe(engine_sink(e, t), board=board)
+    sink = engine_sink(e, t)
+    waits = []  # every reported wait (ns), for a per-collective comparison
+
+    def record(ns):
+        waits.append(int(ns))
+        return sink(ns)
+    probe = WaitProbe(record, board=board)
     buf = torch.ones(1 << 14)
     now = 0
     traj = []
@@ -46,7 +52,7 @@ def wait_worker(rank: int, world: int, port: int, q, lag_ms: float, board_name: 
     dist.barrier()
     board.close()
     q.put({"rank": rank, "traj": traj, "tslice": info.tslice_us, "spin_latency": info.spin_latency,
-           "reports": info.report_count, "stats": probe.stats()})
+           "reports": info.report_count, "stats": probe.stats(), "waits": waits, "collectives": nsteps + 4})
     dist.destroy_process_group()
 
 

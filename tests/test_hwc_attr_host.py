@@ -21,3 +21,14 @@ def test_attribution_conserves_counts():
         assert L.gpbs_hip_hwc_attr_host_check(seed, 200, out) == 0
         assert out[0] < 1e-12, (seed, out[0])  # attributed + unexplained == hardware sum
         assert out[1] < 1e-12, (seed, out[1])  # clean part <= attributed part
+
+
+def test_masked_queue_pool_policy():
+    """The process-wide CU-masked queue pool (csrc/hip/runtime.cpp
+    MaskedPoolCore) on fake handles: co-sharers of one layout share a queue,
+    concurrent layouts on one mask each get their own below the budget, an
+    exclusive acquire never lands on another key's queue, idle queues are
+    re-keyed before new ones are made, masks and devices never mix, and past
+    the budget a share across keys happens and is counted."""
+    from pbs_amd.ops import kernels as K
+    assert K.lib().gpbs_hip_masked_pool_selftest() == 0

@@ -118,7 +118,14 @@ def test_descheduled_peer_produces_waits_and_atc_shrinks(lag_ms):
         # rank 0 waits ~lag at every collective; the late rank does not
         assert r0["stats"]["reports"] >= 20, r0
         assert r0["stats"]["wait_ns_total"] >= 20 * 0.7 * lag_ms * 1e6, r0
-        assert r1["stats"]["wait_ns_total"] < 0.2 * r0["stats"]["wait_ns_total"], r1
+        # the late rank waits only when host scheduling noise delays rank 0:
+        # a per-collective median (zeros for collectives without a report),
+        # not a total, so a few ms-scale deschedules on a loaded host do not count
+        def med(r):
+            xs = sorted(r["waits"] + [0] * max(0, r["collectives"] - len(r["waits"])))
+            return xs[len(xs) // 2]
+        assert med(r0) >= 0.7 * lag_ms * 1e6, r0["waits"]
+        assert med(r1) < 0.3 * lag_ms * 1e6, r1["waits"]
         assert r0["spin_latency"] >= 20 * 0.7 * lag_ms * 1e6
         # ATC: 3 ms waits (bucket 16) drive the slice to its 300 us floor
         assert r0["tslice"] == 300 and min(r0["traj"]) == 300, r0["traj"]
