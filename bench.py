@@ -326,8 +326,8 @@ def main():
         default = {"4mix": "none,static,static-se,credit-fixed,gpbs-nolane,gpbs-lat,gpbs",
                    "gemm2": "none,static,static-se,credit-fixed,gpbs",
                    "phase": "none,static-se,credit-fixed,gpbs",
-                   "phase-ts": "none,static-se,credit-fixed-ts,gpbs",
-                   "8mix": "none,static-se,credit-fixed-ts,gpbs-split,atc,gpbs"}[mix]
+                   "phase-ts": "none,static-se,credit-fixed-ts,credit-classq,gpbs",
+                   "8mix": "none,static-se,credit-fixed-ts,credit-classq,gpbs-split,atc,gpbs"}[mix]
         spec = args.policies if (args.policies and mix == mixes[0]) else default
         pols = tuple(p for p in spec.split(",") if p)
         reps = args.reps if mix == mixes[0] else args.reps_extra

@@ -499,6 +499,14 @@ int gpbs_tenant_class(gpbs_engine_t* e, int t) {
   return d ? d->cls : -1;
 }
 
+int gpbs_tenant_bound_stats(gpbs_engine_t* e, int t, uint64_t* out3, int reset) {
+  LOCK(e);
+  Tenant* d = live(e, t);
+  if (!d) return GPBS_ENOENT;
+  Scheduler* s = e->e->sched_of_tenant(t);
+  return s ? s->bound_stats(*d, out3, reset != 0) : GPBS_EINVAL;
+}
+
 int gpbs_tenant_heartbeat(gpbs_engine_t* e, int t) {
   LOCK(e);
   Tenant* d = live(e, t);

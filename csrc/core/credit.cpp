@@ -20,6 +20,12 @@
 //
 // Modes: "credit"       PBS adaptive credit (the reference's built default),
 //        "credit-fixed" upstream credit (global quantum, no adaptation),
+//        "credit-classq" fixed per-class quanta, no phase detector: the
+//                       contention class (the same counters, EWMA and band)
+//                       maps straight to the PBS bounds -- memory class
+//                       max_us, compute class min_us.  The ablation that
+//                       tells what the detector (:302-389) adds over a
+//                       class -> quantum table,
 //        "atc"          spin-latency driven global re-slicing.
 #include <algorithm>
 #include <cinttypes>
@@ -46,7 +52,7 @@ std::string fmt(const char* f, ...) {
   return buf;
 }
 
-enum class Mode { PBS, FIXED, ATC };
+enum class Mode { PBS, FIXED, ATC, CLASSQ };
 
 struct CSlot : SchedSlotData {
   int runq_cpu = -1;  // != -1 while on a runq (__vcpu_on_runq)
@@ -76,6 +82,7 @@ struct CDom : SchedTenantData {
   uint64_t pending_requests = 0;
   uint64_t cache_miss_rate = 0, cpi = 0;
   uint64_t rate_ewma = 0;  // smoothed miss rate (alpha 1/4) for contention classes
+  uint64_t bound_periods = 0, bound_min = 0, bound_max = 0;  // measured periods / at min_us / at max_us
   AtcState atc{};
 };
 
@@ -97,7 +104,7 @@ class CreditScheduler : public Scheduler {
                               : (mode_ == Mode::PBS ? "SMP Credit Scheduler (PBS)" : "SMP Credit Scheduler");
   }
   const char* opt_name() const override {
-    return mode_ == Mode::ATC ? "atc" : (mode_ == Mode::PBS ? "credit" : "credit-fixed");
+    return mode_ == Mode::ATC ? "atc" : (mode_ == Mode::PBS ? "credit" : (mode_ == Mode::CLASSQ ? "credit-classq" : "credit-fixed"));
   }
 
   // ------------------------------------------------------------- init ----
@@ -168,6 +175,16 @@ class CreditScheduler : public Scheduler {
           tp->budget_ctx != 0)
         q = std::max(q, sd(*tp).adapt.tslice_us);
     return q;
+  }
+  // credit-classq: the class's bound (unknown class: the global quantum)
+  uint32_t classq_us(const Tenant& t) const {
+    return t.cls == 1 ? E.adapt_params.max_us : (t.cls == 0 ? E.adapt_params.min_us : tslice_us_);
+  }
+  // The quantum a tenant runs with in this mode (fill_tenant_info, bound stats).
+  uint32_t mode_quantum_us(Tenant& t) {
+    if (mode_ == Mode::PBS) return sd(t).adapt.tslice_us;
+    if (mode_ == Mode::CLASSQ) return classq_us(t);
+    return tslice_us_;
   }
   Slot& curr(int cpu) { return E.curr_of(cpu); }
   Mask online() { return E.pools[pool_]->cpus; }
@@ -590,6 +607,8 @@ class CreditScheduler : public Scheduler {
     Slot& c2 = curr(cpu);
     uint32_t period = tick_period_us_;
     if (!c2.is_idle() && mode_ == Mode::PBS) period = sd_of(c2).adapt.tick_period_us;
+    if (!c2.is_idle() && mode_ == Mode::CLASSQ)
+      period = classq_us(*E.tenants[c2.tenant]) / std::max<uint32_t>(1, E.adapt_params.ticks_per_tslice);
     E.timer_set(p.ticker, now + (int64_t)std::max<uint32_t>(1, period) * 1000);
   }
 
@@ -697,6 +716,12 @@ class CreditScheduler : public Scheduler {
                           ? (d.rate_ewma + d.cache_miss_rate) / 2
                           : (3 * d.rate_ewma + d.cache_miss_rate) / 4;
       E.emit(TRC_METRIC, master_, (uint32_t)ids[k], (uint32_t)inst, (uint32_t)miss, (uint32_t)d.cache_miss_rate);
+      if (inst) {  // a measured period: where the quantum sits
+        const uint32_t q = mode_quantum_us(*E.tenants[ids[k]]);
+        d.bound_periods++;
+        d.bound_min += q <= E.adapt_params.min_us;
+        d.bound_max += q >= E.adapt_params.max_us;
+      }
       d.spinlock_metric_update = 0;
       d.spinlock_count = 0;
     }
@@ -1273,6 +1298,8 @@ class CreditScheduler : public Scheduler {
     } else if (!snext->is_idle()) {
       if (mode_ == Mode::PBS)
         tslice = (int64_t)pbs_quantum_us(*snext) * 1000;
+      else if (mode_ == Mode::CLASSQ)
+        tslice = (int64_t)classq_us(*E.tenants[snext->tenant]) * 1000;
       else if (mode_ == Mode::ATC)
         tslice = (int64_t)tslice_us_ * 1000;  // global slice (atc :1916)
     } else {
@@ -1346,6 +1373,17 @@ class CreditScheduler : public Scheduler {
     return d.rate_ewma >= thr ? 1 : 0;
   }
 
+  int bound_stats(Tenant& t, uint64_t* out3, bool reset) override {
+    CDom& d = sd(t);
+    if (out3) {
+      out3[0] = d.bound_periods;
+      out3[1] = d.bound_min;
+      out3[2] = d.bound_max;
+    }
+    if (reset) d.bound_periods = d.bound_min = d.bound_max = 0;
+    return 0;
+  }
+
   bool tenant_adapt(Tenant& d, AdaptState* out) override {
     *out = sd(d).adapt;
     return true;
@@ -1360,8 +1398,10 @@ class CreditScheduler : public Scheduler {
     o.weight = d.weight;
     o.cap = d.cap;
     o.active_slots = d.active_vcpu_count;
-    o.tslice_us = mode_ == Mode::PBS ? d.adapt.tslice_us : (mode_ == Mode::ATC ? tslice_us_ : tslice_us_);
-    o.tick_period_us = mode_ == Mode::PBS ? d.adapt.tick_period_us : tick_period_us_;
+    o.tslice_us = mode_quantum_us(dom);
+    o.tick_period_us = mode_ == Mode::PBS ? d.adapt.tick_period_us
+                                          : (mode_ == Mode::CLASSQ ? o.tslice_us / E.adapt_params.ticks_per_tslice
+                                                                   : tick_period_us_);
     o.phase = d.adapt.phase;
     o.window_left = d.adapt.window_left;
     o.last_err = d.adapt.last_err;
@@ -1502,6 +1542,7 @@ std::unique_ptr<Scheduler> make_arinc653_scheduler(Engine& e, int pool);
 std::unique_ptr<Scheduler> make_scheduler(const std::string& name, Engine& e, int pool) {
   if (name == "credit" || name == "pbs") return std::make_unique<CreditScheduler>(e, pool, Mode::PBS);
   if (name == "credit-fixed") return std::make_unique<CreditScheduler>(e, pool, Mode::FIXED);
+  if (name == "credit-classq") return std::make_unique<CreditScheduler>(e, pool, Mode::CLASSQ);
   if (name == "atc") return std::make_unique<CreditScheduler>(e, pool, Mode::ATC);
   if (name == "static") return make_static_scheduler(e, pool);
   if (name == "arinc653") return make_arinc653_scheduler(e, pool);

@@ -179,6 +179,9 @@ class Scheduler {
   // gpbs additions: the paravirtual wait report routed by tenant id (Q6 fix)
   virtual void report(Tenant&, uint64_t, int) {}
   virtual bool tenant_adapt(Tenant&, AdaptState*) { return false; }
+  // Metric periods with a measurement, and of those the ones whose quantum
+  // sat at the adapt bounds (min_us, max_us); reset clears them.
+  virtual int bound_stats(Tenant&, uint64_t*, bool) { return GPBS_EINVAL; }
   // Contention class from the counters: -1 unknown (no recent samples), 0 compute-bound, 1 memory-bound.
   virtual int classify(Tenant&) { return -1; }
   // Trace word of a slot: (priority + 128) in bits 0-7, credit (clamped to

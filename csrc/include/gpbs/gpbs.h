@@ -275,6 +275,9 @@ int gpbs_slot_yield(gpbs_engine_t* e, int tenant, int index);
 int gpbs_slot_pin(gpbs_engine_t* e, int tenant, int index, const uint64_t* mask4); /* vcpu-pin */
 int gpbs_tenant_info(gpbs_engine_t* e, int tenant, gpbs_tenant_info_t* out);
 int gpbs_tenant_class(gpbs_engine_t* e, int tenant); /* contention class: 0 compute, 1 memory, -1 unknown */
+/* Metric periods with a measurement / with the quantum at min_us / at max_us
+ * (credit modes); reset != 0 clears them after the read. */
+int gpbs_tenant_bound_stats(gpbs_engine_t* e, int tenant, uint64_t* out3, int reset);
 /* Cumulative INST, CYCLES, LLC refs, LLC misses the scheduler measured and
  * attributed to the tenant (sum over metric periods; the vPMU mirror). */
 int gpbs_tenant_vpmu(gpbs_engine_t* e, int tenant, uint64_t* total4);

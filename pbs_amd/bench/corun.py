@@ -204,6 +204,10 @@ POLICY_ENGINES = {
     "gpbs-ts": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
     "credit-fixed-ts": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="credit-fixed"), True,
                         "device,se,waveprio,latco,budget,latmem"),
+    # fixed per-class quanta (memory class max_us, compute class min_us), no
+    # phase detector: what PBS's detector adds over a class -> quantum table
+    "credit-classq": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="credit-classq"), True,
+                      "device,se,waveprio,latco,budget,latmem"),
     # the ATC policy (X:xen/common/sched_credit_atc.c:291-543): one global
     # quantum for the pool, driven by the tenants' wait reports (K10); the
     # same time-shared budget layout as the flagship
@@ -986,6 +990,8 @@ class Corun:
         if e is not None:
             e.perfc_reset()
             run0 = {n: e.tenant_info(self.tid[n]).run_ns for n in self.tid}
+            for n in self.throughput:
+                e.bound_stats(self.tid[n], reset=True)
             if self.cfg.hw_counters:
                 self.ctx.hwc_reset()
         quanta = {n: [] for n in self.tid}
@@ -1156,6 +1162,8 @@ class Corun:
             eng["miss_rate"] = {n: e.tenant_info(self.tid[n]).cache_miss_rate for n in self.tid}
             eng["class"] = {n: e.lib.gpbs_tenant_class(e.h, self.tid[n]) for n in self.tid}
             eng["mean_tslice_us"] = {n: round(statistics.mean(q), 1) for n, q in quanta.items() if q}
+            # measured metric periods and, of those, at the quantum bounds
+            eng["at_bound"] = {n: e.bound_stats(self.tid[n]) for n in self.throughput}
             eng["run_share"] = {n: round((e.tenant_info(self.tid[n]).run_ns - run0[n]) / (wall_ms * 1e6), 3)
                                 for n in self.tid}
             eng["phase"] = {n: e.tenant_info(self.tid[n]).phase for n in self.tid}

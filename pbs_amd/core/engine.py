@@ -458,6 +458,15 @@ class Engine:
     def perfc_reset(self):
         return self.lib.gpbs_perfc_reset(self.h)
 
+    def bound_stats(self, t: int, reset: bool = False) -> Dict[str, int]:
+        """Metric periods the tenant was measured in and, of those, the ones
+        its quantum sat at the adapt bounds (min_us / max_us)."""
+        o = (C.c_uint64 * 3)()
+        rc = self.lib.gpbs_tenant_bound_stats(self.h, t, o, int(reset))
+        if rc < 0:
+            return {"periods": 0, "at_min": 0, "at_max": 0}
+        return {"periods": int(o[0]), "at_min": int(o[1]), "at_max": int(o[2])}
+
     def perfc_prometheus(self, prefix: str = "gpbs") -> str:
         """perfc counters in the Prometheus text exposition format."""
         lines = [f"# TYPE {prefix}_perfc_total counter"]

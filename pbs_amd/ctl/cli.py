@@ -97,7 +97,7 @@ def cmd_sched_credit(c: Client, argv: List[str]) -> int:
             pools = match
         doms = c.call("domain_list")
         for p in pools:
-            if p["sched"] not in ("credit", "credit-fixed", "atc"):  # credit2 / sedf: their own verbs
+            if p["sched"] not in ("credit", "credit-fixed", "credit-classq", "atc"):  # credit2 / sedf: their own verbs
                 continue
             _pool_line(c, p["id"])
             _dom_header()

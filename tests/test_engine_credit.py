@@ -529,3 +529,50 @@ def test_boost_exclusive_parks_memory_siblings_during_a_request():
     for m in mems:
         assert run1[m] >= 0.8 * run0[m], (m, run0, run1)
     assert e1.check() == ""
+
+
+def _two_class_engine(sched):
+    from pbs_amd.core.config import MI355X_PROFILE
+    prof = dict(MI355X_PROFILE)
+    prof["sched"] = sched
+    e = Engine(sim_clock=True, partitions=[(0, 0), (0, 1)], **prof)
+    e.tenant_create("Domain-0", nslots=1)
+    a = e.tenant_create("mem", nslots=1)
+    b = e.tenant_create("cmp", nslots=1)
+    e.wake(a)
+    e.wake(b)
+    return e, a, b
+
+
+def _feed_classes(e, a, b, periods, k0=1):
+    for k in range(k0, k0 + periods):  # mem: 5e4 misses / 1e5 inst; cmp: 10 / 1e5
+        e.set_pmc(e.slot_id(a, 0), [k * 1_000_000, k * 1_000_000, k * 1000, k * 500_000])
+        e.set_pmc(e.slot_id(b, 0), [k * 1_000_000, k * 1_000_000, k * 1000, k * 100])
+        e.advance(e.now() + 1_000_000)
+
+
+def test_credit_classq_maps_class_to_bound_without_detector():
+    """credit-classq (VERDICT r4 item 3 ablation): the memory-class tenant runs
+    with max_us and the compute-class one with min_us as soon as classified,
+    with no PBS detector activity (no adapt inc / dec / re-arm)."""
+    e, a, b = _two_class_engine("credit-classq")
+    _feed_classes(e, a, b, 60)
+    assert e.lib.gpbs_tenant_class(e.h, a) == 1 and e.lib.gpbs_tenant_class(e.h, b) == 0
+    assert e.tenant_info(a).tslice_us == 11000 and e.tenant_info(b).tslice_us == 1000
+    pc = e.perfc()
+    assert pc["adapt_inc"] == 0 and pc["adapt_dec"] == 0 and pc["adapt_rearm"] == 0
+    ba, bb = e.bound_stats(a), e.bound_stats(b)
+    assert ba["periods"] == 60 and bb["at_min"] == 60
+    assert ba["at_max"] >= 50  # at max from its classification on
+
+
+def test_bound_stats_count_pbs_quantum_at_the_bounds_and_reset():
+    """PBS mode: a steady memory-bound tenant's quantum climbs to max_us and
+    stays; bound_stats counts the measured periods at each bound and resets."""
+    e, a, b = _two_class_engine("credit")
+    _feed_classes(e, a, b, 40)
+    assert e.tenant_info(a).tslice_us == 11000 and e.tenant_info(b).tslice_us == 1000
+    st = e.bound_stats(a, reset=True)
+    assert st["periods"] == 40 and 0 < st["at_max"] < 40 and st["at_min"] <= 5  # from the initial quantum
+    _feed_classes(e, a, b, 10, k0=41)
+    assert e.bound_stats(a) == {"periods": 10, "at_min": 0, "at_max": 10}
