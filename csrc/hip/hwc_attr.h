@@ -31,6 +31,8 @@ struct HwcAttrIn {
   u32 prime;                             // 1: only record the snapshot as the new previous one
   u32 nt_hi;                             // rows t >= nt_hi of own_cur are zero (and were: owned time only grows);
                                          // the device path reads rows < nt_hi only (0 = all rows)
+  u32 drained;                           // bit p: partition p's last owner change was at least the drain
+                                         // guard before this interval began (its previous owner is gone)
 };
 
 struct HwcAttrPrev {  // carried from one snapshot to the next
@@ -72,9 +74,14 @@ inline void hwc_attr_record(const HwcAttrIn& in, HwcAttrPrev& st) {
 //    over its contexts; LLC misses (TCC, per XCD) by each tenant's attributed
 //    share of the XCD's L2 requests.
 //  * Clean (metric) part: a partition counts only when one tenant owned it
-//    for >= clean_pct % of this interval AND of the previous one, so a
-//    revoked tenant's draining workgroups never land in the next owner's
-//    window; XCD-wide counts are clean only with one owner on the XCD.
+//    for >= clean_pct % of this interval AND its previous owner had drained
+//    before the interval began -- either the same tenant held it over the
+//    previous interval too, or its last owner change was at least the drain
+//    guard before this interval's first sample (bit p of `drained`: the
+//    switch-aligned sampler takes that sample right after the guard, so the
+//    window of a new owner's tenure opens clean); a revoked tenant's draining
+//    workgroups never land in the next owner's window.  XCD-wide counts are
+//    clean only with one owner on the XCD.
 inline void hwc_attr_host(const HwcAttrIn& in, HwcAttrPrev& st, HwcAttrOut& out) {
   constexpr int P = kAttrP, T = kMaxTenants;
   for (int t = 0; t < T; ++t)
@@ -104,7 +111,7 @@ inline void hwc_attr_host(const HwcAttrIn& in, HwcAttrPrev& st, HwcAttrOut& out)
     if (span > 0 && !in.shared)
       for (int t = 0; t < T; ++t)
         if (own_d[t * P + p] * 100.0 >= span * in.clean_pct) raw = t;
-    clean_owner[p] = (raw >= 0 && st.prev_raw[p] == raw) ? raw : -1;
+    clean_owner[p] = (raw >= 0 && (((in.drained >> p) & 1u) || st.prev_raw[p] == raw)) ? raw : -1;
     st.prev_raw[p] = raw;
   }
   int xcd_owner[kXcds];

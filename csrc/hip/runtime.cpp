@@ -313,33 +313,59 @@ struct GpuCtx {
   double hwc_tokens = 50;
   int64_t hwc_tok_ns = 0;
   uint64_t hwc_denied = 0;   // burst ticks skipped for lack of a token
-  // Owner changes open bursts only with hwc_owner_burst (GPBS_HWC_OWNER_BURST;
-  // phase triggers always do): with the model fallback below a tenant whose
-  // partitions changed owners gets its metric from the modeled counters, so
-  // owner changes no longer need clean hardware windows.
-  int hwc_owner_burst = 0;
-  // Model fallback (GPBS_HWC_MODEL_FALLBACK, default on): a tenant that ran
-  // in an interval but owned no partition in a settled exclusive window --
-  // time-shared, or just re-placed -- reports the interval's MODELED deltas
-  // (its kernels' own per-tile counts) to the PBS metric instead of nothing.
+  // Switch-aligned sampling (round 5; the per-vCPU PMU save at every context
+  // switch, X:xen/arch/x86/domain.c:1600,1619 -> perfctr.c:1547-1572): every
+  // table publish that changes an owner records, per partition, when it
+  // changed and the quantum the new owner was given, and wakes the sampler.
+  // The sampler takes a hardware sample one drain guard after the switch --
+  // the revoked workgroups have left the partition, the new owner's tenure
+  // starts -- so sample intervals coincide with tenures and a time-shared
+  // tenant's window is clean (csrc/hip/hwc_attr.h, `drained`).  Which switches
+  // get a sample, under the token budget:
+  //   * one that ends a tenure whose start was sampled (closes a window);
+  //   * one that starts a tenure of at least hwc_long_us (opens a window:
+  //     memory-class quanta, 11 ms in the MI355X profile);
+  //   * a short tenure (compute quanta, 1 ms) opens a window -- a sample pair
+  //     -- only when the bucket holds the pair plus a reserve, at a
+  //     pseudo-random subset of switches so co-sharers rotating in lockstep
+  //     all get measured.
+  int hwc_align = 1;          // switch-aligned samples on
+  int hwc_guard_us = 150;     // publish -> sample: a revoked GEMM tile / stream chunk drains in ~50-150 us
+  int hwc_long_us = 3000;     // tenures at least this long open a window at every switch
+  int64_t part_chg_ns[kXcds * kCtx] = {};  // publish time of each partition's last owner change (mu)
+  u32 q_pending[kXcds * kCtx] = {};        // quantum (us) of the owner each pending entry names (mu)
+  u32 part_q_us[kXcds * kCtx] = {};        // ... as published (mu)
+  u32 sw_changed = 0;                      // partitions changed since the sampler last looked (mu)
+  int64_t sw_first_ns = 0, sw_last_ns = 0; // first / latest publish among them (mu)
+  std::vector<int64_t> snap_chg;           // part_chg_ns at the newest snapshot (snap_mu)
+  int64_t snap_t = 0;                      // its sample time (snap_mu)
+  std::vector<int64_t> used_chg;           // ... of the last consumed snapshot (snap_mu)
+  int64_t used_t = 0;
+  std::vector<int64_t> own_prev;           // owned ns at the last consumed snapshot (host copy, snap_mu)
+  uint64_t align_samples = 0, align_close = 0, align_long = 0, align_short = 0, align_denied = 0;
+  int64_t ts_gap_sum = 0;                  // sample-to-sample gaps over intervals with a switch (time-shared)
+  uint64_t ts_gaps = 0;
+  // Model fallback (default on): a tenant that ran substantially in an
+  // interval without a clean window, and whose last clean window is older
+  // than hwc_stale_us, reports the interval's MODELED deltas scaled per
+  // counter by its hardware/model ratio from its own clean windows (EWMA);
+  // uncalibrated, the period reports nothing.  Otherwise such a period is
+  // skipped (the PBS idle-sample rule), and a sliver -- a tenant that held
+  // its partitions for less than (100 - clean_pct) % of the interval, the
+  // edge of a neighbouring tenure -- never counts.
   int model_fallback = 1;
+  int hwc_stale_us = 50000;
   double mod_cur[kMaxTenants][kNumPmc] = {};       // modeled deltas of the newest consumed snapshot
   double mod_inflight[kMaxTenants][kNumPmc] = {};  // ... of the snapshot whose attribution is in flight
-  uint64_t fallback_periods = 0, clean_periods = 0;
+  double pres_cur[kMaxTenants] = {};               // largest owned share of a partition over the interval
+  double pres_inflight[kMaxTenants] = {};
+  int64_t t_inflight = 0;                          // sample time of the in-flight attribution
+  double cal[kMaxTenants][kNumPmc] = {};           // hardware / model per counter (0: not calibrated)
+  int64_t last_clean_ns[kMaxTenants] = {};
+  uint64_t fallback_periods = 0, clean_periods = 0, skipped_periods = 0, sliver_periods = 0;
+  uint64_t t_clean[kMaxTenants] = {}, t_fallback[kMaxTenants] = {}, t_skipped[kMaxTenants] = {},
+           t_sliver[kMaxTenants] = {};
   int hwc_watch = 1;      // GPBS_HWC_WATCH: read the modeled block every tick (the burst trigger)
-  // Fused metric (GPBS_HWC_FUSE, K9): a hardware sample stalls the command
-  // processor ~0.2 ms, so at the 1 % duty cap live data arrives every ~20 ms
-  // (faster cadence measured a net loss, profiles/r4/hwc_cadence_s13.txt).
-  // With the fuse on, the PBS metric gets a value EVERY tick: the tick's
-  // modeled per-tile deltas (the watch read, no command-processor work)
-  // scaled per tenant and counter by the hardware/model ratio of its latest
-  // hardware windows (EWMA); the hardware samples calibrate instead of
-  // reporting.  Tenants without modeled counters (shim tenants) keep the
-  // hardware deltas.
-  int hwc_fuse = 0;
-  double cal[kMaxTenants][kNumPmc] = {};  // 0: not calibrated yet (raw modeled deltas)
-  std::vector<u64> tick_blk, tick_prev;   // newest watch read / the one the previous tick consumed (snap_mu)
-  uint64_t tick_seq = 0, tick_used = 0, fuse_ticks = 0, cal_updates = 0;
   int64_t hwc_next_period_ns = 1000000;
   std::atomic<uint64_t> hwc_triggers{0};
   uint64_t hwc_burst_samples = 0;
@@ -351,7 +377,10 @@ struct GpuCtx {
   double hw_sum[kNumPmc] = {}, model_sum[kNumPmc] = {};  // attributed vs modeled totals
   double unatt[kNumPmc] = {};                             // hardware counts no owner explains
   double metric_sum[kNumPmc] = {};                        // counts delivered to the PBS metric (clean windows)
-  int clean_pct = 90;  // exclusive-ownership window: min % of an interval one owner must hold (0: pro rata)
+  // exclusive-ownership window: min % of an interval one owner must hold (0:
+  // pro rata).  80: a switch-aligned 1 ms compute tenure keeps ~85 % of its
+  // interval (the next tenure's first drain guard closes it).
+  int clean_pct = 80;
   double att_total[kMaxTenants][kNumPmc] = {};            // per-tenant attributed hardware totals
   double met_total[kMaxTenants][kNumPmc] = {};            // per-tenant totals that reached the PBS metric
   double mod_total[kMaxTenants][kNumPmc] = {};            // per-tenant modeled totals (cross-check)
@@ -419,7 +448,7 @@ void own_snapshot_locked(const GpuCtx* c, int64_t* out) {
 
 // ---------------------------------------------------------------- engine hooks
 
-void act_on_switch(void* user, int part, int, int next, int, int32_t, int64_t) {
+void act_on_switch(void* user, int part, int, int next, int, int32_t quantum_us, int64_t) {
   GpuCtx* c = (GpuCtx*)user;
   const int i = part - c->part_base;
   if (i < 0 || i >= kXcds * c->nctx) return;
@@ -427,6 +456,7 @@ void act_on_switch(void* user, int part, int, int next, int, int32_t, int64_t) {
   {
     std::lock_guard<std::mutex> g(c->mu);
     c->pending[x * kCtx + ctx] = next >= 0 ? (u32)next : kNoOwner;
+    c->q_pending[x * kCtx + ctx] = quantum_us > 0 ? (u32)quantum_us : 0u;
   }
   c->switches++;
   if (roctx_switch_marks()) {  // TRC_SCHED_SWITCH analog (X:xen/common/schedule.c:1138-1151)
@@ -481,7 +511,14 @@ bool publish_locked(GpuCtx* c) {
     c->last_pub_ns = t;
     for (int x = 0; x < kXcds * kCtx; ++x) {
       const u32 o = c->h_table->owner[x] & kOwnerMask;
-      if (o < (u32)kMaxTenants && (c->pending[x] & kOwnerMask) != o) c->revoke_ns[o].store(t, std::memory_order_relaxed);
+      if ((c->pending[x] & kOwnerMask) == o) continue;
+      if (o < (u32)kMaxTenants) c->revoke_ns[o].store(t, std::memory_order_relaxed);
+      // switch-aligned sampling: when and to whom this partition changed
+      c->part_chg_ns[x] = t;
+      c->part_q_us[x] = c->q_pending[x];
+      c->sw_changed |= 1u << x;
+      if (!c->sw_first_ns) c->sw_first_ns = t;
+      c->sw_last_ns = t;
     }
     for (int x = 0; x < kXcds * kCtx; ++x) __atomic_store_n(&c->h_table->owner[x], c->pending[x], __ATOMIC_RELEASE);
     c->epoch++;
@@ -592,154 +629,248 @@ inline u64 dpos(u64 a, u64 b) { return a >= b ? a - b : 0; }  // Q5: a counter r
 // counter block (a 16 KiB device-to-host copy: no command-processor work) and
 // watches each tenant's modeled miss rate; a HARDWARE sample -- which stalls
 // the command processor for its duration and perturbs the tenants -- is taken
-//   * in a burst, every tick, for burst_ms after a trigger: an owner change
-//     in the partition table, or a tenant whose modeled miss rate moved by
-//     more than 3x (a phase change), so the classifier sees the change at
-//     1 ms resolution;
+//   * one drain guard after a table publish that changed owners, when the
+//     switch closes or opens a tenure window (switch-aligned, see GpuCtx);
+//   * in a burst, every tick, for burst_ms after a tenant's modeled miss rate
+//     moved by more than 3x (a phase change), so the classifier sees the
+//     change at 1 ms resolution;
 //   * otherwise when the duty-cycle cap allows (sample time <= hwc_duty_pct %
-//     of the time), which bounds what steady-state sampling costs.
-// Classification and PBS decisions use the hardware counters only; the
-// modeled counters are the trigger.
+//     of the time), backing off to hwc_slow_us once no owner changed for
+//     20 ms, which bounds what steady-state sampling costs.
+// Every sample spends a token of the budget.  Classification and PBS
+// decisions use the hardware counters; the modeled counters are the trigger
+// and the calibrated fallback.
 void hwc_loop(GpuCtx* c) {
   hipSetDevice(c->device);
   constexpr int kBlk = kMaxTenants * kXcds * kNumPmc;
   constexpr int kOwn = kMaxTenants * kXcds * kCtx;
+  constexpr int P = kXcds * kCtx;
   std::vector<u64> blk(kBlk), se(kXcds * kCtx * kNumPmc), xs(kXcds * kNumPmc);
   std::vector<u64> watch_prev(kBlk, 0);
   std::vector<double> watch_rate(kMaxTenants, -1.0);
-  std::vector<int64_t> own(kOwn);
+  std::vector<int64_t> own(kOwn), chg(P);
   roctxNameOsThread("gpbs-hwc-sampler");
   constexpr int64_t kSteadyNs = 20000000;  // slow_us back-off: no owner change for 20 ms
   uint64_t last_sw = c->flushes.load();
   int64_t last_change = mono_ns(), last_hw = 0, burst_until = mono_ns() + (int64_t)c->hwc_burst_ms * 1000000;
-  bool watch_primed = false;
+  int64_t next_tick = mono_ns(), seen_pub = 0;
+  bool watch_primed = false, sw_since_hw = false, slow = false, burst = false;
+  u32 open = 0;  // partitions whose current tenure began with a (switch-aligned) sample
+  uint64_t rng = 0x2545F4914F6CDD1Dull;
+  // one hardware sample plus the snapshot it belongs to; false if the read failed
+  auto sample = [&](int64_t t0) -> bool {
+    if (c->hwc_budget_pct > 0) c->hwc_tokens -= 1.0;
+    RoctxRange rr("gpbs:hwc_sample");
+    const int64_t s0 = mono_ns();
+    const int rc = gpbs_hwc_sample_se(reinterpret_cast<uint64_t*>(se.data()), reinterpret_cast<uint64_t*>(xs.data()));
+    {
+      std::lock_guard<std::mutex> g(c->mu);
+      own_snapshot_locked(c, own.data());
+      std::memcpy(chg.data(), c->part_chg_ns, sizeof(c->part_chg_ns));
+    }
+    share_update(c);  // the interval just sampled: shared time counted up to now
+    if (rc >= 0) {
+      const int64_t dt = mono_ns() - s0;
+      c->hwc_dt_ewma = c->hwc_dt_ewma > 0 ? 0.875 * c->hwc_dt_ewma + 0.125 * (double)dt : (double)dt;
+      std::lock_guard<std::mutex> g(c->snap_mu);
+      c->snap_blk = blk;
+      c->snap_se.swap(se);
+      c->snap_x.swap(xs);
+      c->snap_own.swap(own);
+      c->snap_chg.swap(chg);
+      c->snap_t = s0;
+      c->snap_share = c->share_ns;
+      c->snap_seq++;
+      c->hwc_ns += dt;
+      if (dt > c->hwc_ns_max) c->hwc_ns_max = dt;
+      c->hwc_samples++;
+      c->hwc_period_sum_ns += last_hw ? s0 - last_hw : (int64_t)c->hwc_period_us * 1000;
+      if (sw_since_hw && last_hw) {  // an interval the table changed in: the time-shared cadence
+        c->ts_gap_sum += s0 - last_hw;
+        c->ts_gaps++;
+      }
+      if (burst) c->hwc_burst_samples++;
+      if (slow) c->hwc_slow_samples.fetch_add(1, std::memory_order_relaxed);
+    }
+    sw_since_hw = false;
+    last_hw = s0;
+    (void)t0;
+    return rc >= 0;
+  };
   while (!c->hwc_stop.load(std::memory_order_acquire)) {
     const int64_t t0 = mono_ns();
     const int64_t tick = (int64_t)c->hwc_period_us * 1000;
-    // 1. watch: the modeled block (every tick with the watch on, else only
-    //    with a hardware sample)
-    const uint64_t sw = c->flushes.load(std::memory_order_relaxed);  // table publishes that changed an owner
-    const bool due_hw = sw != last_sw || t0 < burst_until || t0 - last_hw >= c->hwc_next_period_ns - tick / 4;
-    if (c->hwc_watch || due_hw) {
-      if (hipMemcpyAsync(c->h_blk, c->d_cnt, sizeof(u64) * kBlk, hipMemcpyDeviceToHost, c->hwc_stream) != hipSuccess)
-        break;
-      hipEventRecord(c->blk_ev, c->hwc_stream);
-      hipEventSynchronize(c->blk_ev);
-      std::memcpy(blk.data(), c->h_blk, sizeof(u64) * kBlk);
-      if (c->hwc_fuse) {  // the metric tick's modeled deltas
-        std::lock_guard<std::mutex> g(c->snap_mu);
-        c->tick_blk = blk;
-        c->tick_seq++;
+    const bool on_tick = t0 >= next_tick;
+    bool sampled = false;
+    if (on_tick) {
+      next_tick = t0 + tick;
+      // 1. watch: the modeled block (every tick with the watch on, else only
+      //    with a hardware sample)
+      const uint64_t sw = c->flushes.load(std::memory_order_relaxed);  // table publishes that changed an owner
+      if (c->hwc_watch || sw != last_sw || t0 < burst_until || t0 - last_hw >= c->hwc_next_period_ns - tick / 4) {
+        if (hipMemcpyAsync(c->h_blk, c->d_cnt, sizeof(u64) * kBlk, hipMemcpyDeviceToHost, c->hwc_stream) != hipSuccess)
+          break;
+        hipEventRecord(c->blk_ev, c->hwc_stream);
+        hipEventSynchronize(c->blk_ev);
+        std::memcpy(blk.data(), c->h_blk, sizeof(u64) * kBlk);
+      }
+      bool trig = false;
+      for (int t = 0; t < kMaxTenants; ++t) {
+        u64 di = 0, dm = 0;
+        for (int x = 0; x < kXcds; ++x) {
+          const size_t i = ((size_t)t * kXcds + x) * kNumPmc;
+          di += dpos(blk[i], watch_prev[i]);
+          dm += dpos(blk[i + 3], watch_prev[i + 3]);
+        }
+        if (di < 1000000) continue;  // too little work in this tick to judge
+        const double r = (double)(dm + 1) / (double)di;
+        if (watch_primed && watch_rate[t] > 0 && (r > 3.0 * watch_rate[t] || r * 3.0 < watch_rate[t])) trig = true;
+        watch_rate[t] = watch_rate[t] > 0 ? 0.5 * watch_rate[t] + 0.5 * r : r;
+      }
+      std::copy(blk.begin(), blk.end(), watch_prev.begin());
+      watch_primed = true;
+      if (sw != last_sw) last_change = t0;
+      last_sw = sw;
+      if (trig) {
+        burst_until = t0 + (int64_t)c->hwc_burst_ms * 1000000;
+        c->hwc_triggers.fetch_add(1, std::memory_order_relaxed);
+      }
+      if (c->hwc_budget_pct > 0) {  // refill the sample budget
+        const double dt = c->hwc_dt_ewma > 0 ? c->hwc_dt_ewma : 150000.0;
+        if (c->hwc_tok_ns) c->hwc_tokens += (double)(t0 - c->hwc_tok_ns) * c->hwc_budget_pct / 100.0 / dt;
+        c->hwc_tokens = std::min(c->hwc_tokens, (double)c->hwc_bucket);
+        c->hwc_tok_ns = t0;
       }
     }
-    bool trig = false;
-    for (int t = 0; t < kMaxTenants; ++t) {
-      u64 di = 0, dm = 0;
-      for (int x = 0; x < kXcds; ++x) {
-        const size_t i = ((size_t)t * kXcds + x) * kNumPmc;
-        di += dpos(blk[i], watch_prev[i]);
-        dm += dpos(blk[i + 3], watch_prev[i + 3]);
+    // 2. switch-aligned sample: one drain guard after the latest publish of
+    //    a burst of them (at most 4 guards after the first)
+    int64_t wake_at = next_tick;
+    u32 changed = 0, q[P];
+    int64_t first = 0, lastp = 0;
+    {
+      std::lock_guard<std::mutex> g(c->mu);
+      changed = c->sw_changed;
+      first = c->sw_first_ns;
+      lastp = c->sw_last_ns;
+      std::memcpy(q, c->part_q_us, sizeof(q));
+    }
+    seen_pub = lastp;
+    if (changed) sw_since_hw = true;
+    if (changed && !c->hwc_align) {
+      std::lock_guard<std::mutex> g(c->mu);
+      c->sw_changed &= ~changed;
+      if (!c->sw_changed) c->sw_first_ns = c->sw_last_ns = 0;
+    } else if (changed) {
+      const int64_t guard = (int64_t)c->hwc_guard_us * 1000;
+      const int64_t due = std::min(lastp + guard, first + 4 * guard);
+      if (t0 >= due) {
+        const u32 close = changed & open;
+        bool lng = false;
+        for (int p = 0; p < P; ++p)
+          if (((changed >> p) & 1u) && q[p] >= (u32)c->hwc_long_us) lng = true;
+        rng ^= rng << 13;
+        rng ^= rng >> 7;
+        rng ^= rng << 17;
+        const bool budgeted = c->hwc_budget_pct > 0;
+        const bool shrt = !lng && !close && (!budgeted || c->hwc_tokens >= 3.0) && rng % 3 == 0;
+        const bool want = close || lng || shrt;
+        {
+          std::lock_guard<std::mutex> g(c->mu);
+          c->sw_changed &= ~changed;
+          if (!c->sw_changed) c->sw_first_ns = c->sw_last_ns = 0;
+        }
+        if (want && (!budgeted || c->hwc_tokens >= 1.0)) {
+          burst = slow = false;
+          sampled = sample(t0);
+          c->align_samples++;
+          if (close) c->align_close++;
+          if (lng) c->align_long++;
+          if (shrt) c->align_short++;
+          open = (open & ~changed) | ((lng || shrt) ? changed : 0u);
+        } else {
+          if (want) c->align_denied++;
+          open &= ~changed;
+        }
+      } else {
+        wake_at = std::min(wake_at, due);
       }
-      if (di < 1000000) continue;  // too little work in this tick to judge
-      const double r = (double)(dm + 1) / (double)di;
-      if (watch_primed && watch_rate[t] > 0 && (r > 3.0 * watch_rate[t] || r * 3.0 < watch_rate[t])) trig = true;
-      watch_rate[t] = watch_rate[t] > 0 ? 0.5 * watch_rate[t] + 0.5 * r : r;
     }
-    watch_prev.swap(blk);
-    blk = watch_prev;  // keep a copy for the snapshot below
-    watch_primed = true;
-    if (sw != last_sw) {
-      last_change = t0;
-      if (c->hwc_owner_burst) trig = true;
-    }
-    last_sw = sw;
-    if (trig) {
-      burst_until = t0 + (int64_t)c->hwc_burst_ms * 1000000;
-      c->hwc_triggers.fetch_add(1, std::memory_order_relaxed);
-    }
-    // 2. hardware sample: in a burst every tick, else at the duty-capped /
-    //    back-off period
-    const bool slow = c->hwc_slow_us > c->hwc_period_us && t0 - last_change >= kSteadyNs;
-    int64_t period = slow ? (int64_t)c->hwc_slow_us * 1000 : tick;
-    if (c->hwc_duty_pct > 0) period = std::max(period, (int64_t)(c->hwc_dt_ewma * 100.0 / c->hwc_duty_pct));
-    c->hwc_next_period_ns = period;
-    if (c->hwc_budget_pct > 0) {  // refill the sample budget
-      const double dt = c->hwc_dt_ewma > 0 ? c->hwc_dt_ewma : 150000.0;
-      if (c->hwc_tok_ns) c->hwc_tokens += (double)(t0 - c->hwc_tok_ns) * c->hwc_budget_pct / 100.0 / dt;
-      c->hwc_tokens = std::min(c->hwc_tokens, (double)c->hwc_bucket);
-      c->hwc_tok_ns = t0;
-    }
-    const bool due = t0 - last_hw >= period - tick / 4;
-    bool burst = t0 < burst_until && !due;
-    if (burst && c->hwc_budget_pct > 0 && c->hwc_tokens < 1.0) {
-      burst = false;
-      c->hwc_denied++;
-    }
-    if (burst || due) {
-      if (c->hwc_budget_pct > 0) c->hwc_tokens -= 1.0;
-      RoctxRange rr("gpbs:hwc_sample");
-      const int64_t s0 = mono_ns();
-      const int rc = gpbs_hwc_sample_se(reinterpret_cast<uint64_t*>(se.data()), reinterpret_cast<uint64_t*>(xs.data()));
-      {
-        std::lock_guard<std::mutex> g(c->mu);
-        own_snapshot_locked(c, own.data());
+    // 3. burst / background sample on a tick
+    if (on_tick && !sampled) {
+      slow = c->hwc_slow_us > c->hwc_period_us && t0 - last_change >= kSteadyNs;
+      int64_t period = slow ? (int64_t)c->hwc_slow_us * 1000 : tick;
+      if (c->hwc_duty_pct > 0) period = std::max(period, (int64_t)(c->hwc_dt_ewma * 100.0 / c->hwc_duty_pct));
+      c->hwc_next_period_ns = period;
+      const bool due = t0 - last_hw >= period - tick / 4;
+      burst = t0 < burst_until && !due;
+      if (burst && c->hwc_budget_pct > 0 && c->hwc_tokens < 1.0) {
+        burst = false;
+        c->hwc_denied++;
       }
-      share_update(c);  // the interval just sampled: shared time counted up to now
-      if (rc >= 0) {
-        const int64_t dt = mono_ns() - s0;
-        c->hwc_dt_ewma = c->hwc_dt_ewma > 0 ? 0.875 * c->hwc_dt_ewma + 0.125 * (double)dt : (double)dt;
-        std::lock_guard<std::mutex> g(c->snap_mu);
-        c->snap_blk.swap(blk);
-        c->snap_se.swap(se);
-        c->snap_x.swap(xs);
-        c->snap_own.swap(own);
-        c->snap_share = c->share_ns;
-        c->snap_seq++;
-        c->hwc_ns += dt;
-        if (dt > c->hwc_ns_max) c->hwc_ns_max = dt;
-        c->hwc_samples++;
-        c->hwc_period_sum_ns += last_hw ? s0 - last_hw : tick;
-        if (burst) c->hwc_burst_samples++;
-        if (slow) c->hwc_slow_samples.fetch_add(1, std::memory_order_relaxed);
-      }
-      last_hw = s0;
+      if (burst || due) sample(t0);
     }
-    const int64_t rest = tick - (mono_ns() - t0);
-    if (rest > 0) std::this_thread::sleep_for(std::chrono::nanoseconds(rest));
+    // 4. sleep until the next tick, a pending switch sample, or a new publish
+    std::unique_lock<std::mutex> lk(c->mu);
+    c->cv.wait_until(lk, std::chrono::steady_clock::time_point(std::chrono::nanoseconds(wake_at)), [&] {
+      return c->hwc_stop.load(std::memory_order_acquire) || (c->hwc_align && c->sw_last_ns != seen_pub && c->sw_changed);
+    });
   }
 }
 
 
 // Fold one attribution result into the per-tenant totals and the pending
-// metric deltas (snap_mu held).  `mod`: the same interval's modeled deltas
-// (model fallback for tenants without a clean window).
-void hwc_fold(GpuCtx* c, const HwcAttrOut& o, const double (*mod)[kNumPmc]) {
+// metric deltas (snap_mu held).  `mod`: the same interval's modeled deltas,
+// `pres`: each tenant's largest owned share of a partition over it, `t_s`:
+// the interval's closing sample time.  Per tenant that ran:
+//   clean     a clean window: its clean counts reach the PBS metric, and a
+//             window that covers all its counts recalibrates hardware/model;
+//   fallback  no clean window, substantial presence, the last clean window
+//             older than hwc_stale_us and a calibration: modeled x ratio;
+//   skipped   no clean window, substantial presence, otherwise: nothing;
+//   sliver    owned < (100 - clean_pct) % of the interval: nothing.
+void hwc_fold(GpuCtx* c, const HwcAttrOut& o, const double (*mod)[kNumPmc], const double* pres, int64_t t_s) {
   if (!o.valid) return;
+  const double sub = c->clean_pct > 0 ? (100.0 - c->clean_pct) / 100.0 : 0.0;
   for (int t = 0; t < kMaxTenants; ++t) {
-    const bool clean = c->clean_pct <= 0 || o.addc[t][0] > 0;
-    const bool fallback = !clean && c->model_fallback && mod && o.add[t][0] > 0 && mod[t][0] > 0;
-    if (clean && o.add[t][0] > 0) c->clean_periods++;
-    if (fallback) c->fallback_periods++;
-    // fused metric: a modeled tenant's hardware window calibrates its ticks
-    const bool fused = c->hwc_fuse && mod && mod[t][0] > 0;
-    if (fused && o.add[t][0] > 0) {
-      for (int k = 0; k < kNumPmc; ++k)
-        if (mod[t][k] > 0) {
-          const double r = o.add[t][k] / mod[t][k];
-          c->cal[t][k] = c->cal[t][k] > 0 ? 0.75 * c->cal[t][k] + 0.25 * r : r;
-        }
-      c->cal_updates++;
-    }
-    for (int k = 0; k < kNumPmc; ++k) {
+    for (int k = 0; k < kNumPmc; ++k)
       if (o.add[t][k] > 0) c->att_total[t][k] += o.add[t][k];
-      if (fused) continue;  // its metric comes from the calibrated ticks
-      const double m = fallback ? mod[t][k] : (c->clean_pct > 0 ? o.addc[t][k] : o.add[t][k]);
-      if (m > 0) {
-        c->last_delta[t][k] += (u64)(m + 0.5);
-        c->metric_sum[k] += m;
-        c->met_total[t][k] += m;
+    if (o.add[t][0] <= 0) continue;  // did not run in the interval
+    const bool clean = c->clean_pct <= 0 || o.addc[t][0] > 0;
+    double m[kNumPmc] = {0, 0, 0, 0};
+    if (clean) {
+      c->clean_periods++;
+      c->t_clean[t]++;
+      c->last_clean_ns[t] = t_s;
+      for (int k = 0; k < kNumPmc; ++k) m[k] = c->clean_pct > 0 ? o.addc[t][k] : o.add[t][k];
+      // the window holds (nearly) all the tenant ran: hardware over modeled
+      if (mod && mod[t][0] > 0 && o.addc[t][0] >= 0.9 * o.add[t][0])
+        for (int k = 0; k < kNumPmc; ++k)
+          if (mod[t][k] > 0 && o.add[t][k] > 0) {
+            const double r = o.add[t][k] / mod[t][k];
+            c->cal[t][k] = c->cal[t][k] > 0 ? 0.75 * c->cal[t][k] + 0.25 * r : r;
+          }
+    } else if (pres && pres[t] < sub) {
+      c->sliver_periods++;
+      c->t_sliver[t]++;
+      continue;
+    } else {
+      const bool stale = t_s - c->last_clean_ns[t] > (int64_t)c->hwc_stale_us * 1000;
+      if (c->model_fallback && stale && mod && mod[t][0] > 0 && c->cal[t][0] > 0) {
+        c->fallback_periods++;
+        c->t_fallback[t]++;
+        for (int k = 0; k < kNumPmc; ++k) m[k] = mod[t][k] * c->cal[t][k];
+      } else {
+        c->skipped_periods++;
+        c->t_skipped[t]++;
+        continue;
       }
     }
+    for (int k = 0; k < kNumPmc; ++k)
+      if (m[k] > 0) {
+        c->last_delta[t][k] += (u64)(m[k] + 0.5);
+        c->metric_sum[k] += m[k];
+        c->met_total[t][k] += m[k];
+      }
   }
   for (int k = 0; k < kNumPmc; ++k) {
     c->hw_sum[k] += o.hw_sum[k];
@@ -765,11 +896,23 @@ void hwc_fill_in(GpuCtx* c, HwcAttrIn& in) {
         break;
       }
   in.nt_hi = hi ? hi : 1;
+  // drain guard: the interval opens at the last consumed sample; a partition
+  // whose last owner change came at least a guard before it starts clean
+  u32 dr = 0;
+  if (c->used_t && c->used_chg.size() == (size_t)kAttrP) {
+    const int64_t guard = (int64_t)c->hwc_guard_us * 1000;
+    for (int p = 0; p < kAttrP; ++p)
+      if (c->used_t - c->used_chg[p] >= guard) dr |= 1u << p;
+  }
+  in.drained = dr;
 }
 
-// Modeled per-tile counters over the same interval (cross-check, host).
+// Modeled per-tile counters over the same interval (cross-check and
+// calibrated fallback), and each tenant's largest owned share of a
+// partition over it (host).
 void hwc_model(GpuCtx* c) {
   std::memset(c->mod_cur, 0, sizeof(c->mod_cur));
+  std::memset(c->pres_cur, 0, sizeof(c->pres_cur));
   if (!c->hw_primed) return;
   for (int t = 0; t < kMaxTenants; ++t)
     for (int k = 0; k < kNumPmc; ++k) {
@@ -781,6 +924,23 @@ void hwc_model(GpuCtx* c) {
       c->mod_cur[t][k] = md;
       c->mod_total[t][k] += md;
       c->model_sum[k] += md;
+    }
+  if (c->own_prev.size() != c->snap_own.size()) return;
+  double span = 0;
+  static thread_local double tot[kAttrP];
+  for (int p = 0; p < kAttrP; ++p) {
+    tot[p] = 0;
+    for (int t = 0; t < kMaxTenants; ++t) {
+      const int64_t d = c->snap_own[(size_t)t * kAttrP + p] - c->own_prev[(size_t)t * kAttrP + p];
+      if (d > 0) tot[p] += (double)d;
+    }
+    span = std::max(span, tot[p]);
+  }
+  if (span <= 0) return;
+  for (int t = 0; t < kMaxTenants; ++t)
+    for (int p = 0; p < kAttrP; ++p) {
+      const int64_t d = c->snap_own[(size_t)t * kAttrP + p] - c->own_prev[(size_t)t * kAttrP + p];
+      if (d > 0) c->pres_cur[t] = std::max(c->pres_cur[t], (double)d / span);
     }
 }
 
@@ -794,7 +954,7 @@ int hwc_consume(GpuCtx* c, bool wait) {
   if (c->dev_attr && c->attr_pending) {
     const hipError_t q = wait ? hipEventSynchronize(c->attr_ev) : hipEventQuery(c->attr_ev);
     if (q == hipSuccess) {
-      hwc_fold(c, *c->h_aout, c->mod_inflight);
+      hwc_fold(c, *c->h_aout, c->mod_inflight, c->pres_inflight, c->t_inflight);
       c->attr_pending = false;
     } else {
       c->attr_busy_skips++;
@@ -812,9 +972,11 @@ int hwc_consume(GpuCtx* c, bool wait) {
       c->attr_pending = true;
       c->attr_launches++;
       std::memcpy(c->mod_inflight, c->mod_cur, sizeof(c->mod_cur));
+      std::memcpy(c->pres_inflight, c->pres_cur, sizeof(c->pres_cur));
+      c->t_inflight = c->snap_t;
       done = true;
       if (wait && hipEventSynchronize(c->attr_ev) == hipSuccess) {
-        hwc_fold(c, *c->h_aout, c->mod_inflight);
+        hwc_fold(c, *c->h_aout, c->mod_inflight, c->pres_inflight, c->t_inflight);
         c->attr_pending = false;
       }
     }
@@ -824,10 +986,13 @@ int hwc_consume(GpuCtx* c, bool wait) {
     static thread_local HwcAttrOut out;
     hwc_fill_in(c, in);
     hwc_attr_host(in, c->hst, out);
-    hwc_fold(c, out, c->mod_cur);
+    hwc_fold(c, out, c->mod_cur, c->pres_cur, c->snap_t);
     c->attr_host++;
   }
   c->blk_prev = c->snap_blk;
+  c->own_prev = c->snap_own;
+  c->used_chg = c->snap_chg;
+  c->used_t = c->snap_t;
   c->share_prev = c->snap_share;
   c->hw_primed = true;
   return 1;
@@ -839,29 +1004,9 @@ int hwc_tenant_deltas(GpuCtx* c, int n, const int* tenants, uint64_t* out) {
   {
     std::lock_guard<std::mutex> g(c->snap_mu);
     hwc_consume(c, false);
-    if (c->hwc_fuse && c->tick_seq != c->tick_used && !c->tick_blk.empty()) {
-      if (c->tick_prev.size() == c->tick_blk.size())
-        for (int t = 0; t < kMaxTenants; ++t)
-          for (int k = 0; k < kNumPmc; ++k) {
-            double md = 0;
-            for (int x = 0; x < kXcds; ++x) {
-              const size_t i = ((size_t)t * kXcds + x) * kNumPmc + k;
-              md += (double)dpos(c->tick_blk[i], c->tick_prev[i]);
-            }
-            if (md <= 0) continue;
-            const double m = c->cal[t][k] > 0 ? md * c->cal[t][k] : md;
-            c->last_delta[t][k] += (u64)(m + 0.5);
-            c->metric_sum[k] += m;
-            c->met_total[t][k] += m;
-          }
-      c->tick_prev.swap(c->tick_blk);
-      c->tick_blk.clear();
-      c->tick_used = c->tick_seq;
-      c->fuse_ticks++;
-    }
   }
-  // No new snapshot since the previous tick (fuse off): every tenant reads
-  // zero instructions and the PBS idle-sample rule (Q14) skips the period.
+  // No new snapshot since the previous tick: every tenant reads zero
+  // instructions and the PBS idle-sample rule (Q14) skips the period.
   for (int k = 0; k < n; ++k)
     for (int i = 0; i < kNumPmc; ++i) {
       const int t = tenants[k];
@@ -1667,10 +1812,8 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
   if (const char* v = std::getenv("GPBS_HWC_BUDGET")) c->hwc_budget_pct = std::max(0, std::min(100, std::atoi(v)));
   if (const char* v = std::getenv("GPBS_HWC_BUCKET")) c->hwc_bucket = std::max(1, std::atoi(v));
   c->hwc_tokens = c->hwc_bucket;
-  if (const char* v = std::getenv("GPBS_HWC_OWNER_BURST")) c->hwc_owner_burst = std::atoi(v) != 0;
   if (const char* v = std::getenv("GPBS_HWC_MODEL_FALLBACK")) c->model_fallback = std::atoi(v) != 0;
   if (const char* v = std::getenv("GPBS_HWC_WATCH")) c->hwc_watch = std::atoi(v) != 0;
-  if (const char* v = std::getenv("GPBS_HWC_FUSE")) c->hwc_fuse = std::atoi(v) != 0;
   if (const char* v = std::getenv("GPBS_SHARE_PROBE")) {
     c->probe_every = std::max(0, std::atoi(v));
     if (const char* k = std::strchr(v, ':')) c->probe_len = std::max(0, std::atoi(k + 1));
@@ -1979,7 +2122,7 @@ int gpbs_gpu_set_hwc_device(void* p, int on) {
   if (on >= 0 && on != old) {
     if (c->attr_pending) {
       hipEventSynchronize(c->attr_ev);
-      hwc_fold(c, *c->h_aout, c->mod_inflight);
+      hwc_fold(c, *c->h_aout, c->mod_inflight, c->pres_inflight, c->t_inflight);
       c->attr_pending = false;
     }
     c->dev_attr = on ? 1 : 0;
@@ -2152,6 +2295,7 @@ static void attr_random_step(HwcAttrIn& in, int it, Rnd& rnd) {
   in.shared = it % 11 == 10;
   in.prime = it == 0;
   in.nt_hi = it % 3 == 2 ? 0 : 7;  // tenants 1..6 own partitions (0: read every row)
+  in.drained = it % 3 == 1 ? (u32)rnd() : (it % 3 == 2 ? 0xFFFFFFFFu : 0u);  // switch-aligned windows
 }
 
 extern "C" {
@@ -2189,6 +2333,81 @@ int gpbs_hip_hwc_attr_host_check(int seed, int iters, double* out2) {
   }
   out2[0] = cons;
   out2[1] = excess;
+  return 0;
+}
+
+// Host check of the metric fold: a tenant whose hardware rates
+// differ from its modeled ones by large factors (the measured 24x on
+// instructions, 0.13x on L2 traffic) alternates between clean windows and
+// stale unclean periods; the calibrated fallback must deliver the hardware
+// miss rate (within 10 %), so the tenant keeps its class.  An uncalibrated
+// or fresh unclean period is skipped, a sliver never counts.  No HIP call.
+// Returns 0 or the number of the first failed check.
+int gpbs_hip_hwc_fold_selftest(void) {
+  static GpuCtx c;  // host fields only; nothing here touches the device
+  std::memset(c.last_delta, 0, sizeof(c.last_delta));
+  c.clean_pct = 80;
+  const int t = 3;
+  const double hw_inst = 2.0e6, hw_miss = 6.0e5;                    // 3e4 misses per 1e5: memory class
+  const double md_inst = hw_inst / 24.0, md_miss = hw_miss / 0.13;  // what the kernels model
+  static HwcAttrOut o;
+  static double mod[kMaxTenants][kNumPmc], pres[kMaxTenants];
+  auto period = [&](bool clean, double share) {
+    std::memset(&o, 0, sizeof(o));
+    std::memset(mod, 0, sizeof(mod));
+    std::memset(pres, 0, sizeof(pres));
+    o.valid = 1;
+    const double f = share;
+    o.add[t][0] = hw_inst * f;
+    o.add[t][1] = hw_inst * f;
+    o.add[t][2] = hw_miss * 2 * f;
+    o.add[t][3] = hw_miss * f;
+    if (clean)
+      for (int k = 0; k < kNumPmc; ++k) o.addc[t][k] = o.add[t][k];
+    mod[t][0] = md_inst * f;
+    mod[t][1] = md_inst * f;
+    mod[t][2] = md_miss * 2 * f;
+    mod[t][3] = md_miss * f;
+    pres[t] = share;
+  };
+  auto take = [&](double* inst, double* miss) {
+    *inst = (double)c.last_delta[t][0];
+    *miss = (double)c.last_delta[t][3];
+    for (int k = 0; k < kNumPmc; ++k) c.last_delta[t][k] = 0;
+  };
+  double in = 0, mi = 0;
+  int64_t now = 1000000000;
+  // 1. unclean before any calibration: skipped, nothing delivered
+  period(false, 1.0);
+  hwc_fold(&c, o, mod, pres, now);
+  take(&in, &mi);
+  if (in != 0 || c.t_skipped[t] != 1) return 1;
+  const double thr = 20000;
+  for (int round = 0; round < 20; ++round) {
+    // a clean window (calibrates), then unclean periods: fresh (skipped), stale (fallback), sliver
+    now += 11000000;
+    period(true, 1.0);
+    hwc_fold(&c, o, mod, pres, now);
+    take(&in, &mi);
+    if (in <= 0 || std::fabs(mi * 1e5 / in - hw_miss * 1e5 / hw_inst) > 1.0) return 2;
+    now += 11000000;
+    period(false, 0.9);
+    hwc_fold(&c, o, mod, pres, now);  // 11 ms after a clean window: not stale
+    take(&in, &mi);
+    if (in != 0) return 3;
+    now += 60000000;
+    period(false, 0.9);
+    hwc_fold(&c, o, mod, pres, now);  // 71 ms: stale -> calibrated fallback
+    take(&in, &mi);
+    if (in <= 0) return 4;
+    const double rate = mi * 1e5 / in, want = hw_miss * 1e5 / hw_inst;
+    if (std::fabs(rate - want) > 0.1 * want || rate < thr) return 5;  // same class as the clean windows
+    period(false, 0.05);
+    hwc_fold(&c, o, mod, pres, now + 1000000);  // the edge of another tenure
+    take(&in, &mi);
+    if (in != 0) return 6;
+  }
+  if (c.t_clean[t] != 20 || c.t_fallback[t] != 20 || c.t_sliver[t] != 20 || c.t_skipped[t] != 21) return 7;
   return 0;
 }
 
@@ -2265,50 +2484,82 @@ int gpbs_gpu_hwc_reset(void* p) {
   c->hwc_burst_samples = 0;
   c->hwc_triggers = 0;
   c->hwc_denied = 0;
-  c->fallback_periods = c->clean_periods = 0;
-  c->fuse_ticks = c->cal_updates = 0;
+  c->fallback_periods = c->clean_periods = c->skipped_periods = c->sliver_periods = 0;
+  std::memset(c->t_clean, 0, sizeof(c->t_clean));
+  std::memset(c->t_fallback, 0, sizeof(c->t_fallback));
+  std::memset(c->t_skipped, 0, sizeof(c->t_skipped));
+  std::memset(c->t_sliver, 0, sizeof(c->t_sliver));
+  c->align_samples = c->align_close = c->align_long = c->align_short = c->align_denied = 0;
+  c->ts_gap_sum = 0;
+  c->ts_gaps = 0;
   return 0;
 }
 
 // Sampler policy: budget % (token bucket over every hardware sample, 0: no
-// budget), owner-change bursts (0/1), model fallback (0/1); -1 keeps a
-// setting.  Returns 0.
-int gpbs_gpu_hwc_sampler(void* p, int budget_pct, int owner_burst, int fallback) {
+// budget), switch-aligned samples (0/1), calibrated model fallback (0/1); -1
+// keeps a setting.  Returns 0.
+int gpbs_gpu_hwc_sampler(void* p, int budget_pct, int align, int fallback) {
   GpuCtx* c = (GpuCtx*)p;
   if (!c) return -22;
   std::lock_guard<std::mutex> g(c->snap_mu);
   if (budget_pct >= 0) c->hwc_budget_pct = std::min(100, budget_pct);
-  if (owner_burst >= 0) c->hwc_owner_burst = owner_burst != 0;
+  if (align >= 0) c->hwc_align = align != 0;
   if (fallback >= 0) c->model_fallback = fallback != 0;
   c->hwc_tokens = c->hwc_bucket;
   return 0;
 }
 
-// Fused metric (K9): on = 1 / 0 sets, -1 keeps; returns the old setting.
-// stats (optional): [0] ticks that reported calibrated modeled deltas,
-// [1] calibration updates from hardware windows.
-int gpbs_gpu_hwc_fuse(void* p, int on, uint64_t* stats2) {
+// Switch-aligned sampling parameters (< 0 keeps): drain guard between a
+// publish and its sample (us), the tenure length that opens a window at
+// every switch (us), and how old a tenant's last clean window must be before
+// the calibrated fallback stands in (us).  out8 (optional): aligned samples,
+// of which closing a window / opening a long one / opening a short pair,
+// switch samples denied by the budget, mean sample gap over intervals with a
+// switch (ns, the time-shared cadence), clean-window tenant periods, skipped
+// ones.
+int gpbs_gpu_hwc_align(void* p, int guard_us, int long_us, int stale_us, uint64_t* out8) {
   GpuCtx* c = (GpuCtx*)p;
   if (!c) return -22;
   std::lock_guard<std::mutex> g(c->snap_mu);
-  const int old = c->hwc_fuse;
-  if (on >= 0 && (on != 0) != (old != 0)) {
-    c->hwc_fuse = on != 0;
-    c->tick_blk.clear();
-    c->tick_prev.clear();
-    std::memset(c->cal, 0, sizeof(c->cal));
+  if (guard_us >= 0) c->hwc_guard_us = guard_us;
+  if (long_us >= 0) c->hwc_long_us = long_us;
+  if (stale_us >= 0) c->hwc_stale_us = stale_us;
+  if (out8) {
+    out8[0] = c->align_samples;
+    out8[1] = c->align_close;
+    out8[2] = c->align_long;
+    out8[3] = c->align_short;
+    out8[4] = c->align_denied;
+    out8[5] = c->ts_gaps ? (uint64_t)(c->ts_gap_sum / (int64_t)c->ts_gaps) : 0;
+    out8[6] = c->clean_periods;
+    out8[7] = c->skipped_periods;
   }
-  if (stats2) {
-    stats2[0] = c->fuse_ticks;
-    stats2[1] = c->cal_updates;
+  return c->hwc_align;
+}
+
+// One tenant's metric periods since the last hwc reset: out4 = clean window,
+// calibrated fallback, skipped (no clean window, not stale or uncalibrated),
+// sliver (the edge of another tenure); out_cal4 (optional) its current
+// hardware/model ratio per counter.
+int gpbs_gpu_hwc_tenant_periods(void* p, int t, uint64_t* out4, double* out_cal4) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c || t < 0 || t >= kMaxTenants) return -22;
+  std::lock_guard<std::mutex> g(c->snap_mu);
+  if (out4) {
+    out4[0] = c->t_clean[t];
+    out4[1] = c->t_fallback[t];
+    out4[2] = c->t_skipped[t];
+    out4[3] = c->t_sliver[t];
   }
-  return old;
+  if (out_cal4)
+    for (int k = 0; k < kNumPmc; ++k) out_cal4[k] = c->cal[t][k];
+  return 0;
 }
 
 // Sample budget and model-fallback statistics: out[0] budget %, [1] burst
-// ticks denied a token, [2] tenant-periods that reported modeled deltas
-// (no clean window), [3] tenant-periods with a clean hardware window,
-// [4] owner-change bursts on (0/1), [5] model fallback on (0/1).
+// ticks denied a token, [2] tenant-periods that reported calibrated modeled
+// deltas (no clean window), [3] tenant-periods with a clean hardware window,
+// [4] switch-aligned samples on (0/1), [5] model fallback on (0/1).
 int gpbs_gpu_hwc_budget_stats(void* p, uint64_t* out5) {
   GpuCtx* c = (GpuCtx*)p;
   if (!c || !out5) return -22;
@@ -2318,7 +2569,7 @@ int gpbs_gpu_hwc_budget_stats(void* p, uint64_t* out5) {
   out5[1] = c->hwc_denied;
   out5[2] = c->fallback_periods;
   out5[3] = c->clean_periods;
-  out5[4] = (uint64_t)c->hwc_owner_burst;
+  out5[4] = (uint64_t)c->hwc_align;
   return 0;
 }
 

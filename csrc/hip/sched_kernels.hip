@@ -95,7 +95,7 @@ __global__ __launch_bounds__(64) void k_adapt(gpbs_adapt_state_t* states, const 
 // The previous snapshot and the clean-owner history stay in device memory.
 struct AttrArgs {  // the snapshot's scalars, by value (no dependent load before the staging loads)
   u32 slot_se[kNumPmc];
-  u32 se_mode, clean_pct, shared, prime, nt_hi;
+  u32 se_mode, clean_pct, shared, prime, nt_hi, drained;
 };
 
 __global__ __launch_bounds__(256) void k_hwc_attribute(const HwcAttrIn* __restrict__ in, HwcAttrPrev* __restrict__ st,
@@ -179,7 +179,9 @@ __global__ __launch_bounds__(256) void k_hwc_attribute(const HwcAttrIn* __restri
     }
   }
   __syncthreads();
-  // 3. clean owners: >= clean_pct of the interval's span, and the same owner as the previous interval
+  // 3. clean owners: >= clean_pct of the interval's span, and the previous
+  // owner drained before the interval (the same owner as the previous
+  // interval, or the last owner change a drain guard before it: args.drained)
   double span = 0;
 #pragma unroll
   for (int p = 0; p < P; ++p) span = span > tot_p[p] ? span : tot_p[p];
@@ -190,7 +192,7 @@ __global__ __launch_bounds__(256) void k_hwc_attribute(const HwcAttrIn* __restri
     const unsigned long long m = __ballot(over);
     if (lane == 0) {
       const int raw = m ? 63 - __builtin_clzll(m) : -1;  // the host keeps the last tenant over the bar
-      clean_owner[p] = (raw >= 0 && st->prev_raw[p] == raw) ? raw : -1;
+      clean_owner[p] = (raw >= 0 && (((args.drained >> p) & 1u) || st->prev_raw[p] == raw)) ? raw : -1;
       st->prev_raw[p] = raw;
     }
   }
@@ -399,6 +401,7 @@ int gpbs_hip_hwc_attribute(const void* h_in, void* d_in, void* st, void* out, hi
   a.shared = hin->shared;
   a.prime = hin->prime;
   a.nt_hi = hin->nt_hi;
+  a.drained = hin->drained;
   const u32 rows = (a.nt_hi == 0 || a.nt_hi > (u32)kMaxTenants) ? (u32)kMaxTenants : a.nt_hi;
   const size_t bytes = offsetof(HwcAttrIn, own_cur) + (size_t)rows * kAttrP * sizeof(long long);
   if (hipMemcpyAsync(d_in, h_in, bytes, hipMemcpyHostToDevice, s) != hipSuccess) return -5;

@@ -227,12 +227,9 @@ POLICY_ENGINES = {
     # the flagship under other counter-sampler policies (same engine and
     # layout; SAMPLER below): round-3 sampler (owner-change bursts, no budget,
     # no model fallback), and modeled counters only (no hardware sample)
-    "gpbs-r3s": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
-    "gpbs-b5": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
     "gpbs-model": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
+    "gpbs-noalign": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
     "gpbs-d5": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
-    "gpbs-fuse": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
-    "gpbs-slow50": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
     # no cross-class steals by idle partitions (boot class_steal=0)
     "gpbs-nox": (4, dict(BUDGET_OVERRIDES, class_budget=1, class_steal=0), True,
                  "device,se,waveprio,latco,budget,latmem"),
@@ -271,17 +268,14 @@ POLICY_ENGINES = {
 # arguments; "model": no hardware samples, the modeled per-tile counters feed
 # the metric).  Policies not listed run the process defaults (env / runtime).
 SAMPLER = {
-    "gpbs-r3s": dict(budget_pct=0, owner_burst=1, fallback=0),
-    "gpbs-b5": dict(budget_pct=5, owner_burst=1, fallback=1),
+    # the round-4 sampler: no switch-aligned samples (periodic / phase bursts
+    # only), the same calibrated fallback
+    "gpbs-noalign": dict(align=0),
     "gpbs-model": "model",
     # background cadence: the duty cap (default 1 %) sets the period from the
     # ~0.2 ms sample cost; 5 % -> ~4 ms, 10 % -> ~2 ms (budget raised with it)
     "gpbs-d5": dict(budget_pct=8, duty=5),
     "gpbs-d10": dict(budget_pct=15, duty=10),
-    # the PBS metric every tick from hardware-calibrated modeled deltas
-    "gpbs-fuse": dict(fuse=1),
-    # hardware sampling backs off to 50 ms once no owner changed for 20 ms
-    "gpbs-slow50": dict(slow_us=50000),
 }
 
 
@@ -1159,6 +1153,15 @@ class Corun:
                              "cpi_x1000": round(att[1] * 1e3 / inst) if inst else 0,
                              "model_miss_rate": round(mod[3] * 1e5 / mod[0]) if mod[0] else 0}
                 eng["hw_tenant"] = hw
+                # per throughput tenant: metric periods from a clean hardware
+                # window vs the calibrated modeled fallback (and skipped ones)
+                per = {n: self.ctx.hwc_tenant_periods(self.tid[n]) for n in self.throughput}
+                eng["hwc"]["tenant_periods"] = per
+                frac = {}
+                for n, v in per.items():
+                    m = v["clean"] + v["fallback"]
+                    frac[n] = round(v["clean"] / m, 3) if m else 0.0
+                eng["hwc"]["per_tenant_clean_frac"] = frac
             eng["miss_rate"] = {n: e.tenant_info(self.tid[n]).cache_miss_rate for n in self.tid}
             eng["class"] = {n: e.lib.gpbs_tenant_class(e.h, self.tid[n]) for n in self.tid}
             eng["mean_tslice_us"] = {n: round(statistics.mean(q), 1) for n, q in quanta.items() if q}

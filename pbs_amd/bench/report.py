@@ -39,19 +39,22 @@ def _mi(p: Optional[dict]) -> Optional[List[float]]:
 
 def _hw_digest(runs: List[dict]) -> Optional[dict]:
     """Median over the gpbs runs of the clean / fallback shares of the metric
-    periods (every throughput tenant's worst share when per-tenant counts are
-    recorded) and the mean hardware period."""
+    periods (periods that fed the PBS metric: a clean hardware window or the
+    calibrated modeled fallback), the worst throughput tenant's clean share,
+    the mean hardware period and the one over intervals with a switch (the
+    time-shared cadence)."""
     hw = [r.get("engine", {}).get("hwc") for r in runs]
     hw = [h for h in hw if h]
     if not hw:
         return None
-    clean, fb, worst, period = [], [], [], []
+    clean, fb, worst, period, skip = [], [], [], [], []
     for h in hw:
         c, f = h.get("clean_periods", 0), h.get("model_fallback_periods", 0)
-        tot = h.get("metric_periods") or (c + f)
+        tot = c + f
         if tot:
             clean.append(c / tot)
             fb.append(f / tot)
+            skip.append(h.get("skipped_periods", 0) / (tot + h.get("skipped_periods", 0)))
         pt = h.get("per_tenant_clean_frac")
         if pt:
             worst.append(min(pt.values()))
@@ -61,6 +64,7 @@ def _hw_digest(runs: List[dict]) -> Optional[dict]:
     if clean:
         out["clean_frac"] = round(_q(clean, 0.5), 3)
         out["fallback_frac"] = round(_q(fb, 0.5), 3)
+        out["skipped_frac"] = round(_q(skip, 0.5), 3)
     if worst:
         out["worst_tenant_clean_frac"] = round(_q(worst, 0.5), 3)
     if period:

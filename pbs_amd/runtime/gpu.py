@@ -167,11 +167,12 @@ class GpuContext:
         self.L.gpbs_gpu_hwc_bursts(self.h, C.byref(tr), C.byref(bsm))
         bud = (C.c_uint64 * 6)()
         self.L.gpbs_gpu_hwc_budget_stats(self.h, bud)
-        fz = (C.c_uint64 * 2)()
-        fuse = self.L.gpbs_gpu_hwc_fuse(self.h, -1, fz)
-        return {"fuse": bool(fuse), "fuse_ticks": fz[0], "cal_updates": fz[1],
-                "budget_pct": bud[0], "burst_denied": bud[1], "model_fallback_periods": bud[2],
-                "clean_periods": bud[3], "owner_bursts": bool(bud[4]),
+        al = (C.c_uint64 * 8)()
+        align = self.L.gpbs_gpu_hwc_align(self.h, -1, -1, -1, al)
+        return {"budget_pct": bud[0], "burst_denied": bud[1], "model_fallback_periods": bud[2],
+                "clean_periods": bud[3], "skipped_periods": al[7], "metric_periods": bud[2] + bud[3],
+                "align": bool(align), "align_samples": al[0], "align_close": al[1], "align_long": al[2],
+                "align_short": al[3], "align_denied": al[4], "ts_period_us": round(al[5] / 1e3, 1),
                 "attr_device": bool(dev), "attr_kernel_launches": la.value, "attr_busy_skips": bs.value,
                 "attr_host": ho.value, "duty_cap_pct": duty, "mean_period_us": round(mp.value / 1e3, 1),
                 "burst_triggers": tr.value, "burst_samples": bsm.value,
@@ -182,21 +183,31 @@ class GpuContext:
                 # exclusive-ownership windows: share of the counts that reached the PBS metric
                 "clean_pct": pct, "metric_frac": [round(x, 4) for x in cf]}
 
-    def set_hwc_sampler(self, budget_pct: int = -1, owner_burst: int = -1, fallback: int = -1, duty: int = -1,
-                        fuse: int = -1, slow_us: int = -1):
+    def hwc_tenant_periods(self, tenant: int) -> dict:
+        """A tenant's metric periods since the last hwc reset: clean window,
+        calibrated model fallback, skipped (no clean window), sliver (the edge
+        of another tenure); and its hardware/model calibration."""
+        o = (C.c_uint64 * 4)()
+        cal = (C.c_double * 4)()
+        self.L.gpbs_gpu_hwc_tenant_periods(self.h, int(tenant), o, cal)
+        return {"clean": o[0], "fallback": o[1], "skipped": o[2], "sliver": o[3],
+                "cal": [round(x, 4) for x in cal]}
+
+    def set_hwc_sampler(self, budget_pct: int = -1, align: int = -1, fallback: int = -1, duty: int = -1,
+                        slow_us: int = -1, guard_us: int = -1, long_us: int = -1, stale_us: int = -1):
         """Sampler policy: `budget_pct` caps the time all hardware samples may
-        take, bursts included (token bucket; 0: no budget); `owner_burst`:
-        owner changes open a 1 ms sampling burst; `fallback`: a tenant without
-        a settled exclusive window reports its modeled deltas; `duty`: the
-        background cadence's duty-cycle cap (set_hwc_duty); `fuse`: the PBS
-        metric every tick from hardware-calibrated modeled deltas (the
-        hardware samples only calibrate); `slow_us`: the back-off period once
-        no owner has changed for 20 ms (0: none).  -1 keeps."""
-        self.L.gpbs_gpu_hwc_sampler(self.h, int(budget_pct), int(owner_burst), int(fallback))
+        take (token bucket; 0: no budget); `align`: switch-aligned samples (a
+        sample one drain guard of `guard_us` after an owner change that closes
+        or opens a tenure window; tenures of `long_us` or more open one at
+        every switch); `fallback`: a tenant without a clean window for
+        `stale_us` reports its modeled deltas scaled by its hardware/model
+        ratio; `duty`: the background cadence's duty-cycle cap
+        (set_hwc_duty); `slow_us`: the back-off period once no owner has
+        changed for 20 ms (0: none).  -1 keeps."""
+        self.L.gpbs_gpu_hwc_sampler(self.h, int(budget_pct), int(align), int(fallback))
+        self.L.gpbs_gpu_hwc_align(self.h, int(guard_us), int(long_us), int(stale_us), None)
         if duty >= 0:
             self.set_hwc_duty(duty)
-        if fuse >= 0:
-            self.L.gpbs_gpu_hwc_fuse(self.h, int(fuse), None)
         if slow_us >= 0:
             self.set_hwc_period(-1, int(slow_us))
 
@@ -204,9 +215,8 @@ class GpuContext:
         """The current sampler policy (set_hwc_sampler's arguments)."""
         bud = (C.c_uint64 * 6)()
         self.L.gpbs_gpu_hwc_budget_stats(self.h, bud)
-        return {"budget_pct": int(bud[0]), "owner_burst": int(bud[4]), "fallback": int(bud[5]),
+        return {"budget_pct": int(bud[0]), "align": int(bud[4]), "fallback": int(bud[5]),
                 "duty": int(self.L.gpbs_gpu_hwc_duty(self.h, -1, None)),
-                "fuse": int(self.L.gpbs_gpu_hwc_fuse(self.h, -1, None)),
                 "slow_us": int(self.L.gpbs_gpu_hwc_period(self.h, -1, -1, None))}
 
     def set_hwc_duty(self, pct: int) -> int:

@@ -51,6 +51,7 @@ s = e.tenant_create("hbm", nslots=32)
 ctx = GpuContext(0, nctx=4, table_mode="device")
 ctx.set_se_mode(True)
 ctx.attach(e, nctx=4)
+ctx.set_hwc_sampler(align=%d)
 ctx.set_hwc(True)
 e.start()
 rg = Runner(ctx, "gemm", g, M=4096, N=4096, K=4096)
@@ -102,12 +103,12 @@ print("RESULT " + json.dumps(out))
 """
 
 
-@pytest.mark.parametrize("fuse", [0, 1])
-def test_budget_layout_follows_a_phase_change_on_live_counters(fuse):
-    """fuse=1 (GPBS_HWC_FUSE): the PBS metric every tick from the modeled
-    deltas calibrated by the hardware windows -- the same layout moves."""
-    env = dict(os.environ, GPBS_HWC_FUSE=str(fuse))
-    r = subprocess.run([sys.executable, "-c", CODE % ROOT], capture_output=True, text=True, timeout=180, env=env)
+@pytest.mark.parametrize("align", [1, 0])
+def test_budget_layout_follows_a_phase_change_on_live_counters(align):
+    """align=1 (default): switch-aligned samples open each new layout's
+    windows one drain guard after the relayout; align=0: periodic and
+    phase-burst samples only -- the same layout moves either way."""
+    r = subprocess.run([sys.executable, "-c", CODE % (ROOT, align)], capture_output=True, text=True, timeout=180)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     out = json.loads([x for x in r.stdout.splitlines() if x.startswith("RESULT ")][-1][7:])
     print(json.dumps(out, indent=1))
@@ -120,5 +121,7 @@ def test_budget_layout_follows_a_phase_change_on_live_counters(fuse):
     assert out["class_change"] >= 2 and out["relayout"] >= 2, out
     assert out["adapt_rearm"] > 0, out
     assert out["check"] == ""
-    if fuse:  # every metric tick reported; hardware windows calibrated the model
-        assert out["hwc"]["fuse"] and out["hwc"]["fuse_ticks"] > 20 and out["hwc"]["cal_updates"] > 0, out["hwc"]
+    if align:  # the relayouts' switches were sampled one guard after the publish
+        assert out["hwc"]["align"] and out["hwc"]["align_samples"] > 0, out["hwc"]
+    else:
+        assert out["hwc"]["align_samples"] == 0, out["hwc"]

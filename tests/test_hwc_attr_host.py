@@ -32,3 +32,14 @@ def test_masked_queue_pool_policy():
     the budget a share across keys happens and is counted."""
     from pbs_amd.ops import kernels as K
     assert K.lib().gpbs_hip_masked_pool_selftest() == 0
+
+
+def test_metric_fold_calibrated_fallback_keeps_the_class():
+    """The PBS metric fold (csrc/hip/runtime.cpp hwc_fold, host only): a
+    tenant whose modeled counters are off by 24x / 0.13x alternates between
+    clean hardware windows and stale unclean periods; the fallback, scaled by
+    its hardware/model ratio, delivers the hardware miss rate within 10 %, so
+    its class holds.  Uncalibrated or fresh unclean periods are skipped and
+    the edge of another tenure (a sliver) never counts."""
+    from pbs_amd.ops import kernels as K
+    assert K.lib().gpbs_hip_hwc_fold_selftest() == 0
