@@ -164,12 +164,15 @@ def main():
                          "llm5: config #5 (Llama-3-8B fp8 decode + Llama-1B-shaped bf16 trainer, torch tenants "
                          "on the shim under gpbsd; not in the default run)")
     ap.add_argument("--reps-extra", type=int, default=5, help="reps of the non-headline mixes")
+    ap.add_argument("--hang-dump-s", type=float, default=0.0,
+                    help="diagnostics: dump every thread's stack every this many seconds (0: off)")
+    ap.add_argument("--llm5-warm-s", type=float, default=5.0, help="--mix llm5: untimed warm-up seconds")
     args = ap.parse_args()
     if args.mix == "llm5":  # its own process tree (daemon + torch tenants); nothing here touches HIP first
         return run_llm5(args)
-    if os.environ.get("GPBS_HANG_DUMP_S"):  # diagnostics: every thread's stack when a run stops progressing
+    if args.hang_dump_s > 0:  # diagnostics: every thread's stack when a run stops progressing
         import faulthandler
-        faulthandler.dump_traceback_later(float(os.environ["GPBS_HANG_DUMP_S"]), repeat=True)
+        faulthandler.dump_traceback_later(args.hang_dump_s, repeat=True)
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -367,7 +370,6 @@ def main():
                    "policy": "gpbs (counter-driven SE budgets, PBS credit, hw counters)", "mix": head},
         "mean_slowdown_pct": hs["mean_slowdown_pct"],
         "counters": counters,
-        "hwc_restarts": (hwc.restarts() if counters == "hw" else 0),
         "protocol": {"kind": args.protocol, "step_ms": args.step_ms if args.protocol == "steady" else None,
                      "reps": max(1, args.reps), "order": "randomized per repetition", "seed": args.seed,
                      "statistic": "median over reps (IQR = q75 - q25)", "solo": "steady (same protocol, alone)"},
@@ -436,7 +438,7 @@ def run_llm5(args):
     # the arriving tenant (its 190 ms training steps run wherever they were
     # launched); steady state is what config #5 measures (s25 timelines:
     # profiles/r4/llm5_s25.txt)
-    warm = max(float(os.environ.get("GPBS_LLM5_WARM_S", "5")), args.warmup * args.step_ms / 1e3)
+    warm = max(args.llm5_warm_s, args.warmup * args.step_ms / 1e3)
     out = os.path.join(tempfile.mkdtemp(), "llm5.json")
     pols = args.policies or "solo,none,static-se,gpbs-budget"
     with contextlib.redirect_stdout(sys.stderr):  # rank 0 prints ONE line: ours

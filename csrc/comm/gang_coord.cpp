@@ -80,7 +80,6 @@ struct Coord {
   std::vector<Metric> node, totals;
   int64_t timeouts = 0, reforms = 0, metric_syncs = 0, switches = 0, atc_global = 0;
   int degraded = 0, error = 0;
-  bool debug = false;
 };
 
 // ------------------------------------------------------------------ engine
@@ -168,9 +167,6 @@ bool reform(Coord* c) {
   const int rc = gpbs_gang_shm_reform(c->shm, c->cfg.join_ns, mono_ns() + c->cfg.join_ns + c->cfg.deadline_ns, &m,
                                       &base);
   range_pop(c);
-  if (c->debug)
-    fprintf(stderr, "[gang_coord] rank %d epoch %llu: reform rc %d members %llx base %llu\n", c->cfg.rank,
-            (unsigned long long)c->epoch, rc, (unsigned long long)m, (unsigned long long)base);
   if (rc) return false;
   std::lock_guard<std::mutex> g(c->mu);
   ++c->reforms;
@@ -268,9 +264,6 @@ void loop(Coord* c) {
     const bool ok = reduce(c, vec, red, t0 + dl, &why, [](int64_t a, int64_t b) { return std::min(a, b); });
     range_pop(c);
     const int64_t t1 = mono_ns();
-    if (c->debug && (c->epoch < 4 || !ok))
-      fprintf(stderr, "[gang_coord] rank %d epoch %llu: vector %lld us, exchange %lld us, ok %d\n", c->cfg.rank,
-              (unsigned long long)c->epoch, (long long)(tg - t0) / 1000, (long long)(t1 - tg) / 1000, (int)ok);
     if (!ok) {
       if (why < 0 || !fail(why, t0)) break;
       continue;
@@ -348,8 +341,6 @@ void* gpbs_gang_coord_start(gpbs_engine_t* e, void* shm, int world, int nvals, c
   c->wait_prev.assign(nt, 0);
   c->wait_seen.assign(nt, false);
   c->node.assign(cfg->nmetric, Metric{});
-  const char* dbg = getenv("GPBS_GANG_DEBUG");
-  c->debug = dbg && dbg[0] == '1';
   c->totals.assign(cfg->nmetric, Metric{});
   c->th = std::thread(loop, c);
   return c;

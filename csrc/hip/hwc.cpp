@@ -65,35 +65,6 @@ struct Hwc {
   int only_gpu = -1;  // count on this GPU agent only (rank-local), -1 = all
   std::mutex mu;
   std::vector<rocprofiler_counter_record_t> rec;
-  // Periodic context restart (GPBS_HWC_RESTART samples; default 0 = never):
-  // the GPU measured ~11 % slower -- solo tenants too, GEMMs and streams
-  // alike -- after the 8mix's device-counting samples in one context, and
-  // not with modeled counters (profiles/r3/bench_8mix_*).  A restart every
-  // 1000 samples removed the drift in an 8mix-only run, but in the full
-  // bench the 4mix's partitioned policies stepped from 1.19 to 1.05 after
-  // 17 runs and the 8mix still drifted (profiles/r3/bench_driver_w_restart.json),
-  // so it is off by default.  The readings stay cumulative across a restart:
-  // base_* holds what the previous context had counted.
-  long restart_every = -1, since_start = 0, restarts = 0;
-  double base_se[kX][kSe][kSlots] = {}, base_x[kX][kSlots] = {};
-  double last_se[kX][kSe][kSlots] = {}, last_x[kX][kSlots] = {};
-  // Asynchronous sampling (GPBS_HWC_ASYNC=1): the read is issued with
-  // ROCPROFILER_COUNTER_FLAG_ASYNC into a rocprofiler buffer tagged with a
-  // sequence number, the buffer is flushed, and the call returns the newest
-  // sample whose records have all arrived (usually the previous one).  The
-  // caller learns which sample it got from gpbs_hwc_async_stats.
-  bool async_mode = false;
-  rocprofiler_buffer_id_t buf{};
-  std::mutex amu;  // guards the accumulators below (buffer callback thread)
-  struct Acc {
-    double se[kX][kSe][kSlots];
-    double x[kX][kSlots];
-    size_t n;
-  };
-  std::map<uint64_t, Acc> pend;  // seq -> records so far
-  uint64_t aseq = 0, done_seq = 0, async_issued = 0, async_incomplete = 0;
-  size_t expect = 0;  // records per sample, learned from the first (synchronous) one
-  Acc done{};
 };
 Hwc g;
 
@@ -111,57 +82,6 @@ void fold_record(const rocprofiler_counter_record_t& r, double se_acc[kX][kSe][k
       rocprofiler_query_record_dimension_position(r.id, g.se_dim, &se) == ROCPROFILER_STATUS_SUCCESS &&
       se < (size_t)kSe)
     se_acc[x][se][it->second] += r.counter_value;
-}
-
-void on_buffer(rocprofiler_context_id_t, rocprofiler_buffer_id_t, rocprofiler_record_header_t** h, size_t n, void*,
-               uint64_t) {
-  std::lock_guard<std::mutex> l(g.amu);
-  for (size_t i = 0; i < n; ++i) {
-    if (h[i]->category != ROCPROFILER_BUFFER_CATEGORY_COUNTERS || h[i]->kind != ROCPROFILER_COUNTER_RECORD_VALUE)
-      continue;
-    auto* r = (const rocprofiler_counter_record_t*)h[i]->payload;
-    auto ins = g.pend.emplace(r->user_data.value, Hwc::Acc{});
-    fold_record(*r, ins.first->second.se, ins.first->second.x);
-    ins.first->second.n++;
-  }
-  // newest complete sample wins; everything older is dropped
-  for (auto it = g.pend.rbegin(); it != g.pend.rend(); ++it)
-    if (g.expect && it->second.n >= g.expect) {
-      if (it->first > g.done_seq) {
-        g.done = it->second;
-        g.done_seq = it->first;
-      }
-      break;
-    }
-  for (auto it = g.pend.begin(); it != g.pend.end() && it->first <= g.done_seq;) it = g.pend.erase(it);
-}
-
-long restart_every() {
-  if (g.restart_every < 0) {
-    const char* e = getenv("GPBS_HWC_RESTART");
-    g.restart_every = e ? atol(e) : 0;
-  }
-  return g.restart_every;
-}
-
-// Under g.mu, after a sample: stop and start the counting context, carrying
-// the counts so far into the bases.
-void maybe_restart() {
-  const long every = restart_every();
-  if (every <= 0 || ++g.since_start < every) return;
-  for (int x = 0; x < kX; ++x)
-    for (int k = 0; k < kSlots; ++k) {
-      g.base_x[x][k] += g.last_x[x][k];
-      g.last_x[x][k] = 0;
-      for (int e = 0; e < kSe; ++e) {
-        g.base_se[x][e][k] += g.last_se[x][e][k];
-        g.last_se[x][e][k] = 0;
-      }
-    }
-  rocprofiler_stop_context(g.ctx);
-  if (rocprofiler_start_context(g.ctx) != ROCPROFILER_STATUS_SUCCESS) g.started = false;
-  g.since_start = 0;
-  g.restarts++;
 }
 
 rocprofiler_status_t on_agents(rocprofiler_agent_version_t, const void** agents, size_t n, void*) {
@@ -213,10 +133,6 @@ void set_cfg(rocprofiler_context_id_t ctx, rocprofiler_agent_id_t, rocprofiler_d
 int tool_init(rocprofiler_client_finalize_t, void*) {
   rocprofiler_query_available_agents(ROCPROFILER_AGENT_INFO_VERSION_0, on_agents, sizeof(rocprofiler_agent_v0_t),
                                      nullptr);
-  {
-    const char* e = getenv("GPBS_HWC_ASYNC");
-    g.async_mode = e && atoi(e) > 0;
-  }
   // One process per GPU (only_gpu = LOCAL_RANK): configure that agent only --
   // a counting context holds hardware queues on its agent, and eight ranks
   // configuring every agent would put eight ranks' profiler queues on every
@@ -242,9 +158,6 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
       continue;
     if (rocprofiler_create_context(&g.ctxs[i]) != ROCPROFILER_STATUS_SUCCESS) continue;
     g.bufs[i] = rocprofiler_buffer_id_t{0};
-    if (g.async_mode && rocprofiler_create_buffer(g.ctxs[i], 1 << 22, 3 << 20, ROCPROFILER_BUFFER_POLICY_LOSSLESS,
-                                                  on_buffer, nullptr, &g.bufs[i]) != ROCPROFILER_STATUS_SUCCESS)
-      continue;
     if (rocprofiler_configure_device_counting_service(g.ctxs[i], g.bufs[i], g.gpus[i], set_cfg, &g.cfg[i]) !=
         ROCPROFILER_STATUS_SUCCESS)
       continue;
@@ -343,7 +256,6 @@ int gpbs_hwc_start(void) {
   g.index_mismatch = 0;
   if (rocprofiler_start_context(g.ctxs[pick]) != ROCPROFILER_STATUS_SUCCESS) return -1;
   g.ctx = g.ctxs[pick];
-  if (g.async_mode) g.buf = g.bufs[pick];
   g.chosen = pick;
   std::snprintf(g.chosen_bdf, sizeof g.chosen_bdf, "%04x:%02x:%02x.%x", dom, (loc >> 8) & 0xff, (loc >> 3) & 0x1f,
                 loc & 7);
@@ -382,11 +294,7 @@ int gpbs_hwc_sample(uint64_t* out, int nxcd) {
     if (x < (size_t)kX) acc[x][it->second] += g.rec[i].counter_value;
   }
   for (int x = 0; x < kX; ++x)
-    for (int s = 0; s < kSlots; ++s) {
-      g.last_x[x][s] = acc[x][s];
-      out[x * kSlots + s] = (uint64_t)(g.base_x[x][s] + acc[x][s]);
-    }
-  maybe_restart();
+    for (int s = 0; s < kSlots; ++s) out[x * kSlots + s] = (uint64_t)acc[x][s];
   return (int)n;
 }
 
@@ -399,57 +307,18 @@ int gpbs_hwc_sample_se(uint64_t* se_out, uint64_t* x_out) {
   std::lock_guard<std::mutex> l(g.mu);
   if (!g.started || !se_out || !x_out) return -1;
   double se_acc[kX][kSe][kSlots] = {}, x_acc[kX][kSlots] = {};
-  size_t n = 0;
-  if (g.async_mode && g.expect) {
-    rocprofiler_user_data_t ud{};
-    ud.value = ++g.aseq;
-    if (rocprofiler_sample_device_counting_service(g.ctx, ud, ROCPROFILER_COUNTER_FLAG_ASYNC, nullptr, nullptr) !=
-        ROCPROFILER_STATUS_SUCCESS)
-      return -1;
-    g.async_issued++;
-    rocprofiler_flush_buffer(g.buf);
-    std::lock_guard<std::mutex> a(g.amu);
-    if (g.done_seq == 0) {
-      g.async_incomplete++;
-      return -2;  // nothing complete yet
-    }
-    std::memcpy(se_acc, g.done.se, sizeof(se_acc));
-    std::memcpy(x_acc, g.done.x, sizeof(x_acc));
-    n = g.done.n;
-  } else {
-    if (g.rec.empty()) g.rec.resize(16384);
-    n = g.rec.size();
-    if (rocprofiler_sample_device_counting_service(g.ctx, {}, ROCPROFILER_COUNTER_FLAG_NONE, g.rec.data(), &n) !=
-        ROCPROFILER_STATUS_SUCCESS)
-      return -1;
-    for (size_t i = 0; i < n; ++i) fold_record(g.rec[i], se_acc, x_acc);
-    if (g.async_mode) g.expect = n;  // the first sample is synchronous: it sizes a complete async sample
-  }
+  if (g.rec.empty()) g.rec.resize(16384);
+  size_t n = g.rec.size();
+  if (rocprofiler_sample_device_counting_service(g.ctx, {}, ROCPROFILER_COUNTER_FLAG_NONE, g.rec.data(), &n) !=
+      ROCPROFILER_STATUS_SUCCESS)
+    return -1;
+  for (size_t i = 0; i < n; ++i) fold_record(g.rec[i], se_acc, x_acc);
   for (int x = 0; x < kX; ++x)
     for (int k = 0; k < kSlots; ++k) {
-      g.last_x[x][k] = x_acc[x][k];
-      x_out[x * kSlots + k] = (uint64_t)(g.base_x[x][k] + x_acc[x][k]);
-      for (int e = 0; e < kSe; ++e) {
-        g.last_se[x][e][k] = se_acc[x][e][k];
-        se_out[(x * kSe + e) * kSlots + k] = (uint64_t)(g.base_se[x][e][k] + se_acc[x][e][k]);
-      }
+      x_out[x * kSlots + k] = (uint64_t)x_acc[x][k];
+      for (int e = 0; e < kSe; ++e) se_out[(x * kSe + e) * kSlots + k] = (uint64_t)se_acc[x][e][k];
     }
-  maybe_restart();
   return (int)n;
-}
-
-// Asynchronous mode statistics: out[0] = 1 if async, [1] issued, [2] newest
-// complete sequence, [3] last issued sequence, [4] calls with nothing
-// complete.  Returns 0.
-int gpbs_hwc_async_stats(uint64_t* out5) {
-  std::lock_guard<std::mutex> l(g.mu);
-  std::lock_guard<std::mutex> a(g.amu);
-  out5[0] = g.async_mode ? 1 : 0;
-  out5[1] = g.async_issued;
-  out5[2] = g.done_seq;
-  out5[3] = g.aseq;
-  out5[4] = g.async_incomplete;
-  return 0;
 }
 
 // 1 if slot k's counters are resolved per shader engine.
@@ -460,8 +329,6 @@ int gpbs_hwc_slot_per_se(int k) {
     if (kv.second == k) return g.per_se[kv.first] ? 1 : 0;
   return 0;
 }
-
-long gpbs_hwc_restarts(void) { return g.restarts; }
 
 int gpbs_hwc_stop(void) {
   std::lock_guard<std::mutex> l(g.mu);

@@ -216,7 +216,6 @@ struct GpuCtx {
   // until a whole GEMM unit ends.
   int lat_half = -1;
   int hold_enable = 0;           // latency requests hold the memory-class tenants (GATE_HOLD)
-  int hold_all = 0;              // GPBS_HOLD_ALL=1: hold every gated tenant, compute class too (ablation)
   // Latency-request hold: count of latency units in flight and the hold
   // word derived from it, changed together under hold_mu.  hold_gen changes
   // whenever the hold is switched off (holds reset): a runner releases only
@@ -259,7 +258,7 @@ struct GpuCtx {
   // Attribution of a snapshot (csrc/hip/hwc_attr.h): on the GPU by default
   // (k_hwc_attribute on the scheduler stream, launched by one metric tick and
   // harvested by the next -- the engine lock is never held across a device
-  // wait), on the host with GPBS_HWC_DEVICE=0.
+  // wait), on the host with param device_attr 0.
   int dev_attr = 1;
   HwcAttrPrev hst;                  // host path state
   HwcAttrIn* h_ain = nullptr;       // pinned: the snapshot the metric tick fills
@@ -285,13 +284,13 @@ struct GpuCtx {
   // Round 3: with the lean counter set a 1 ms sample costs a GEMM ~0.75 %
   // (scripts/hwc_cost.py), so the sampler keeps the reference's 1 ms period
   // (CSCHED_METRIC_TICK_PERIOD, X:xen/common/sched_credit.c:55) and no longer
-  // backs off; GPBS_HWC_SLOW_US=4000 restores the round-2 back-off.
+  // backs off; param slow_us 4000 restores the round-2 back-off.
   // Round 4: back off to 50 ms once no owner has changed for 20 ms (phase
   // triggers still open 1 ms bursts): config #5 1.2343 vs 1.2249 (the shim
   // tenants' layout is steady; profiles/r4/llm5_backoff_s22.txt), runner mixes
   // equal or +0.003 with a quarter of the samples on steady layouts
   // (sampler_backoff_s23.txt).  0: never back off.
-  int hwc_slow_us = 50000;  // GPBS_HWC_SLOW_US
+  int hwc_slow_us = 50000;  // param slow_us
   // Duty-cycle cap: a sample stalls the command processor for its duration
   // (every counter record is a register read it performs), and what that
   // costs the tenants varies from box to box (145-190 us per lean sample on
@@ -300,16 +299,16 @@ struct GpuCtx {
   // (EWMA of the sample duration); 0 disables the cap.
   // Measured on the 4-tenant mix: a 25 % duty (lean set, 1.15 ms) cost the
   // flagship 5 % of its aggregate, 5 % duty (4 ms) 0.5 %.
-  int hwc_duty_pct = 1;  // GPBS_HWC_DUTY (profiles/r3: 5 % costs 0.01 of 4mix aggregate, 2 % 0.004, 1 % none measurable)
-  int hwc_burst_ms = 20;  // GPBS_HWC_BURST_MS: 1 ms hardware sampling after a trigger
+  int hwc_duty_pct = 1;  // param duty_pct (profiles/r3: 5 % costs 0.01 of 4mix aggregate, 2 % 0.004, 1 % none measurable)
+  int hwc_burst_ms = 20;  // param burst_ms: 1 ms hardware sampling after a trigger
   // Sample budget (round 4): a token bucket over EVERY hardware sample,
   // bursts included -- the round-3 bursts re-armed back to back in
   // time-shared regions (every quantum is an owner change: 1539 samples per
   // 8mix run).  Tokens accrue so that samples take at most hwc_budget_pct %
   // of the time on average (EWMA sample time), up to hwc_bucket samples
   // banked; a burst tick without a token is skipped.  0: no budget.
-  int hwc_budget_pct = 5;    // GPBS_HWC_BUDGET
-  int hwc_bucket = 50;       // GPBS_HWC_BUCKET: a phase change's burst plus a flip back
+  int hwc_budget_pct = 5;    // param budget_pct
+  int hwc_bucket = 50;       // param bucket: a phase change's burst plus a flip back
   double hwc_tokens = 50;
   int64_t hwc_tok_ns = 0;
   uint64_t hwc_denied = 0;   // burst ticks skipped for lack of a token
@@ -365,7 +364,7 @@ struct GpuCtx {
   uint64_t fallback_periods = 0, clean_periods = 0, skipped_periods = 0, sliver_periods = 0;
   uint64_t t_clean[kMaxTenants] = {}, t_fallback[kMaxTenants] = {}, t_skipped[kMaxTenants] = {},
            t_sliver[kMaxTenants] = {};
-  int hwc_watch = 1;      // GPBS_HWC_WATCH: read the modeled block every tick (the burst trigger)
+  int hwc_watch = 1;      // param watch: read the modeled block every tick (the burst trigger)
   int64_t hwc_next_period_ns = 1000000;
   std::atomic<uint64_t> hwc_triggers{0};
   uint64_t hwc_burst_samples = 0;
@@ -429,7 +428,7 @@ struct GpuCtx {
   std::atomic<int> share{0};
   int64_t share_ns = 0, share_since = 0;  // cumulative shared time (sampler thread)
   uint64_t share_tick = 0;
-  int probe_every = 40, probe_len = 4;  // GPBS_SHARE_PROBE="every:len" (every 0: no probe windows)
+  int probe_every = 40, probe_len = 4;  // params probe_every / probe_len (every 0: no probe windows)
   int64_t snap_share = 0, share_prev = 0, share_base = 0;
   int muxed = 0;    // ops installed through the engine's backend mux
 };
@@ -981,7 +980,7 @@ int hwc_consume(GpuCtx* c, bool wait) {
       }
     }
   }
-  if (!done) {  // host path (GPBS_HWC_DEVICE=0, or a failed launch)
+  if (!done) {  // host path (param device_attr 0, or a failed launch)
     static thread_local HwcAttrIn in;
     static thread_local HwcAttrOut out;
     hwc_fill_in(c, in);
@@ -1367,14 +1366,6 @@ void se_cu_mask(const u32 se_bits[kXcds], uint32_t m[8]) {
     if (se_bits[b % 8] & (1u << ((b / 8) % 4))) m[b / 32] |= 1u << (b % 32);
 }
 
-int runner_poll_us() {
-  static const int v = [] {
-    const char* e = std::getenv("GPBS_RUNNER_POLL_US");
-    return e ? std::max(0, std::atoi(e)) : 0;
-  }();
-  return v;
-}
-
 struct Runner {
   GpuCtx* ctx;
   gpbs_runner_cfg_t cfg;
@@ -1580,7 +1571,7 @@ struct Runner {
     // memory-class tenants pause at unit boundaries while a latency request
     // is in flight (only where the host can write the hold word: host / BAR table)
     const bool hold = gate && ctx->hold_enable && tm != 1 && w.kind != K_GEMV && ctx->engine &&
-                      (ctx->hold_all || ctx->cls_cache[cfg.tenant].load(std::memory_order_relaxed) == 1);
+                      ctx->cls_cache[cfg.tenant].load(std::memory_order_relaxed) == 1;
     const unsigned mode = (gate ? (cfg.gate == 2 ? GATE_PARK : GATE_TABLE) : GATE_NONE) | (dev ? GATE_DEVTABLE : 0) |
                           (gate && ctx->spatial ? GATE_SPATIAL : 0) |
                           (gate && __atomic_load_n(&ctx->se_mode, __ATOMIC_ACQUIRE) ? GATE_SE : 0) |
@@ -1710,10 +1701,7 @@ struct Runner {
         fl.pop_front();
         while (hipEventQuery(ev[f.ev]) == hipErrorNotReady) {
           if (stop) break;
-          if (runner_poll_us() > 0)  // GPBS_RUNNER_POLL_US: sleep between polls (host CPU vs detection latency)
-            std::this_thread::sleep_for(std::chrono::microseconds(runner_poll_us()));
-          else
-            std::this_thread::yield();
+          std::this_thread::yield();
         }
         const u32 s = __atomic_load_n(&h_status[f.qi], __ATOMIC_ACQUIRE);
         const u32 done = s & 0x3fffffffu;
@@ -1803,22 +1791,7 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
   std::memset(c->own_ns, 0, sizeof(c->own_ns));
   std::memset(c->own_base, 0, sizeof(c->own_base));
   for (auto& k : c->cls_cache) k.store(-1, std::memory_order_relaxed);
-  if (const char* v = std::getenv("GPBS_SHARE")) c->share_enable = std::atoi(v) != 0;
-  if (const char* v = std::getenv("GPBS_HOLD_ALL")) c->hold_all = std::atoi(v) != 0;
-  if (const char* v = std::getenv("GPBS_HWC_PERIOD_US")) c->hwc_period_us = std::max(100, std::atoi(v));
-  if (const char* v = std::getenv("GPBS_HWC_SLOW_US")) c->hwc_slow_us = std::max(0, std::atoi(v));
-  if (const char* v = std::getenv("GPBS_HWC_DUTY")) c->hwc_duty_pct = std::max(0, std::min(100, std::atoi(v)));
-  if (const char* v = std::getenv("GPBS_HWC_BURST_MS")) c->hwc_burst_ms = std::max(0, std::atoi(v));
-  if (const char* v = std::getenv("GPBS_HWC_BUDGET")) c->hwc_budget_pct = std::max(0, std::min(100, std::atoi(v)));
-  if (const char* v = std::getenv("GPBS_HWC_BUCKET")) c->hwc_bucket = std::max(1, std::atoi(v));
   c->hwc_tokens = c->hwc_bucket;
-  if (const char* v = std::getenv("GPBS_HWC_MODEL_FALLBACK")) c->model_fallback = std::atoi(v) != 0;
-  if (const char* v = std::getenv("GPBS_HWC_WATCH")) c->hwc_watch = std::atoi(v) != 0;
-  if (const char* v = std::getenv("GPBS_SHARE_PROBE")) {
-    c->probe_every = std::max(0, std::atoi(v));
-    if (const char* k = std::strchr(v, ':')) c->probe_len = std::max(0, std::atoi(k + 1));
-  }
-  if (const char* v = std::getenv("GPBS_HWC_CLEAN")) c->clean_pct = std::max(0, std::min(100, std::atoi(v)));
   bool ok = hipHostMalloc((void**)&c->h_table, sizeof(PartTable), hipHostMallocCoherent | hipHostMallocMapped) ==
             hipSuccess;
   ok = ok && hipMalloc((void**)&c->d_cnt, sizeof(u64) * kMaxTenants * kXcds * kNumPmc) == hipSuccess;
@@ -1832,7 +1805,6 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
   c->snap_x.assign((size_t)kXcds * kNumPmc, 0);
   c->snap_own.assign((size_t)kMaxTenants * kXcds * kCtx, 0);
   hwc_attr_prev_init(c->hst);
-  if (const char* v = std::getenv("GPBS_HWC_DEVICE")) c->dev_attr = std::atoi(v) != 0;
   ok = ok && hipHostMalloc((void**)&c->h_ain, sizeof(HwcAttrIn), hipHostMallocMapped) == hipSuccess;
   ok = ok && hipMalloc((void**)&c->d_ain, sizeof(HwcAttrIn)) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_aout, sizeof(HwcAttrOut), hipHostMallocMapped) == hipSuccess;
@@ -2465,6 +2437,55 @@ int gpbs_hip_hwc_attr_selftest(int seed, int iters, double* max_rel) {
   return rc;
 }
 
+// Runtime parameters by name (gpbs.toml [runtime], pbs_amd/core/config.py):
+// sets `name` to `value` (value < 0 reads only) and returns the value before,
+// or -22 for an unknown name.  Sampler parameters: period_us (tick),
+// slow_us (steady-state back-off), duty_pct (background duty cap), burst_ms
+// (phase-trigger burst), budget_pct / bucket (token bucket over every
+// sample), clean_pct (exclusive-window share), device_attr (attribution on
+// the GPU), fallback (calibrated model fallback), stale_us, watch (modeled
+// block every tick), align / guard_us / long_us (switch-aligned samples);
+// class-share mode: share, probe_every, probe_len.
+int gpbs_gpu_param(void* p, const char* name, int value) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c || !name) return -22;
+  struct Ent {
+    const char* n;
+    int* f;
+    int lo, hi;
+  };
+  const Ent tab[] = {
+      {"period_us", &c->hwc_period_us, 100, 1000000},   {"slow_us", &c->hwc_slow_us, 0, 10000000},
+      {"duty_pct", &c->hwc_duty_pct, 0, 100},           {"burst_ms", &c->hwc_burst_ms, 0, 10000},
+      {"budget_pct", &c->hwc_budget_pct, 0, 100},       {"bucket", &c->hwc_bucket, 1, 100000},
+      {"clean_pct", &c->clean_pct, 0, 100},             {"device_attr", &c->dev_attr, 0, 1},
+      {"fallback", &c->model_fallback, 0, 1},           {"stale_us", &c->hwc_stale_us, 0, 100000000},
+      {"watch", &c->hwc_watch, 0, 1},                   {"align", &c->hwc_align, 0, 1},
+      {"guard_us", &c->hwc_guard_us, 0, 100000},        {"long_us", &c->hwc_long_us, 0, 100000000},
+      {"share", &c->share_enable, 0, 1},                {"probe_every", &c->probe_every, 0, 1000000},
+      {"probe_len", &c->probe_len, 0, 1000000},
+  };
+  for (const Ent& e : tab)
+    if (std::strcmp(e.n, name) == 0) {
+      std::lock_guard<std::mutex> g(c->snap_mu);
+      const int old = *e.f;
+      if (value >= 0) {
+        if (e.f == &c->dev_attr && (value != 0) != (old != 0)) {  // the other path's state is stale: re-prime
+          if (c->attr_pending) {
+            hipEventSynchronize(c->attr_ev);
+            hwc_fold(c, *c->h_aout, c->mod_inflight, c->pres_inflight, c->t_inflight);
+            c->attr_pending = false;
+          }
+          c->hw_primed = false;
+        }
+        *e.f = std::max(e.lo, std::min(e.hi, value));
+        if (e.f == &c->hwc_bucket || e.f == &c->hwc_budget_pct) c->hwc_tokens = c->hwc_bucket;
+      }
+      return old;
+    }
+  return -22;
+}
+
 int gpbs_gpu_hwc_reset(void* p) {
   GpuCtx* c = (GpuCtx*)p;
   if (!c) return -22;
@@ -2614,7 +2635,7 @@ int gpbs_gpu_hwc_duty(void* p, int pct, uint64_t* mean_period_ns) {
 
 // SE-exclusive partitions: the nctx (= 4) partitions of an XCD are its shader
 // engines; gated tenant kernels run only on SEs their tenant owns.
-// Class-share mode on/off (default off; GPBS_SHARE=1 enables at creation).
+// Class-share mode on/off (default off; param share).
 // Returns the previous setting; *share_ns (optional) = cumulative time in
 // class-share mode since the last hwc reset.
 int gpbs_gpu_set_share(void* p, int on, int64_t* share_ns) {

@@ -164,6 +164,7 @@ class CorunConfig:
     phase_ms: float = 300.0      # mix "phase": the phase tenant alternates gemm <-> stream this often
     onoff_ms: float = 500.0      # mix "phase": the hbm tenant runs / stops for this long, alternately
     solo_steps: int = 0          # solo calibration windows (0: the co-run's K); warmup = the co-run's W
+    mem_chunk: int = 0           # memory tenants' chunk bytes (0: the runner default, 512 KiB)
 
 
 # SE-exclusive flagship (the four partitions of an XCD are its shader engines,
@@ -474,10 +475,10 @@ class Corun:
         cfg, t = self.cfg, self.tid[name]
         spec = dict(SPECS[name])
         kind = spec.pop("kind")
-        # GPBS_MEM_CHUNK: unit-boundary granularity of the memory tenants (bytes
-        # per work-queue chunk, default 512 KiB) -- how soon a hold or a
+        # mem_chunk: unit-boundary granularity of the memory tenants (bytes per
+        # work-queue chunk, default 512 KiB) -- how soon a hold or a
         # revocation takes effect
-        mem_chunk = {"chunk_bytes": int(os.environ["GPBS_MEM_CHUNK"])} if os.environ.get("GPBS_MEM_CHUNK") else {}
+        mem_chunk = {"chunk_bytes": int(cfg.mem_chunk)} if cfg.mem_chunk else {}
         if "alt" in spec and spec["alt"]["kind"] in ("stream", "reduce"):
             spec["alt"] = dict(spec["alt"], **mem_chunk)
         if kind == "gemm":
@@ -602,11 +603,7 @@ class Corun:
             e._gpbs_used = True
             _, _, gate, table = POLICY_ENGINES[policy]
             opts = table.split(",")
-            # GPBS_TABLE_MODE=bar: policies on the device table use the
-            # host-written VRAM table instead (no k_partition_switch dispatch)
             tmode = opts[0]
-            if tmode == "device" and os.environ.get("GPBS_TABLE_MODE", "") in ("bar", "device"):
-                tmode = os.environ["GPBS_TABLE_MODE"]
             try:
                 self.ctx.set_table_mode(tmode)
             except RuntimeError as ex:  # no host-accessible fine-grained VRAM pool: the pinned host table

@@ -3,8 +3,9 @@
 Three levels mirror the reference: ``[boot]`` (daemon start flags, the Xen
 boot parameters), ``[policy]`` (PBS constants, #defines in the reference, here
 runtime-tunable with reference defaults) and ``[tenant.<name>]`` (xl.cfg-like
-per-tenant keys: pool, weight, cap, slots, pin).  Environment variables
-``GPBS_<KEY>`` override boot keys (e.g. ``GPBS_TSLICE_US=2000``).
+per-tenant keys: pool, weight, cap, slots, pin); ``[runtime]`` holds the GPU
+runtime's counter-sampler parameters (RUNTIME_KEYS).  ``GPBS_CONFIG`` names the
+file a process loads when none is passed (GpuContext, gpbsd).
 """
 from __future__ import annotations
 
@@ -49,6 +50,13 @@ MI355X_PROFILE: Dict[str, Any] = dict(
     atc=dict(wait_unit_ns=8),
 )
 
+# GPU runtime parameters (gpbs.toml ``[runtime]``; csrc/hip/runtime.cpp
+# gpbs_gpu_param): the live-counter sampler and class-share mode.  Empty =
+# the runtime's built-in defaults; a key set here is applied to every
+# GpuContext the process creates.
+RUNTIME_KEYS = ("period_us", "slow_us", "duty_pct", "burst_ms", "budget_pct", "bucket", "clean_pct", "device_attr",
+                "fallback", "stale_us", "watch", "align", "guard_us", "long_us", "share", "probe_every", "probe_len")
+
 BOOT_KEYS = ("sched", "tslice_us", "ratelimit_us", "smt_power_savings", "tickle_one_idle", "default_yield",
              "migration_delay_us", "metric_period_us", "slice_apply_us", "pmu_refresh_us", "dom0_quirk",
              "heartbeat_timeout_us", "trace_capacity", "quantum_align_us", "coschedule", "class_period_us",
@@ -61,7 +69,7 @@ def load(path: str | None = None, profile: Dict[str, Any] | None = None) -> Dict
     base = dict(profile or REFERENCE_PROFILE)
     cfg: Dict[str, Any] = {"boot": {k: v for k, v in base.items() if k not in ("adapt", "atc")},
                            "policy": dict(base.get("adapt", {})), "atc": dict(base.get("atc", {})),
-                           "tenants": {}, "pools": {}}
+                           "tenants": {}, "pools": {}, "runtime": {}}
     if path:
         with open(path, "rb") as f:
             doc = _toml.load(f)
@@ -70,10 +78,11 @@ def load(path: str | None = None, profile: Dict[str, Any] | None = None) -> Dict
         cfg["atc"].update(doc.get("atc", {}))
         cfg["tenants"].update(doc.get("tenant", {}))
         cfg["pools"].update(doc.get("pool", {}))
-    for k in BOOT_KEYS:
-        ev = os.environ.get("GPBS_" + k.upper())
-        if ev is not None:
-            cfg["boot"][k] = ev if k == "sched" else int(ev)
+        rt = doc.get("runtime", {})
+        bad = set(rt) - set(RUNTIME_KEYS)
+        if bad:
+            raise ValueError(f"{path}: unknown [runtime] keys {sorted(bad)}")
+        cfg["runtime"].update(rt)
     return cfg
 
 

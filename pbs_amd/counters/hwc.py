@@ -103,22 +103,6 @@ def stop():
     _lib().gpbs_hwc_stop()
 
 
-def restarts() -> int:
-    """Counting-context restarts so far (GPBS_HWC_RESTART samples apart)."""
-    f = _lib().gpbs_hwc_restarts
-    f.restype = __import__("ctypes").c_long
-    return int(f())
-
-
-def async_stats() -> dict:
-    """GPBS_HWC_ASYNC=1 mode: issued reads, newest complete / last issued
-    sequence, calls that found nothing complete."""
-    a = (C.c_uint64 * 5)()
-    _lib().gpbs_hwc_async_stats(a)
-    return {"async": bool(a[0]), "issued": int(a[1]), "done_seq": int(a[2]), "last_seq": int(a[3]),
-            "incomplete": int(a[4])}
-
-
 def agent() -> dict:
     """The GPU agent the counting context was started on: chosen by the PCI
     address of the current HIP device (hwc.cpp gpbs_hwc_start), with its

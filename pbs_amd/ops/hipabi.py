@@ -60,7 +60,6 @@ def bind(lib):
     _p(lib, "gpbs_gpu_hwc_stats", C.c_int, vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_double))
     _p(lib, "gpbs_hwc_sample_se", C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64))
     _p(lib, "gpbs_hwc_slot_per_se", C.c_int, C.c_int)
-    _p(lib, "gpbs_hwc_async_stats", C.c_int, C.POINTER(C.c_uint64))
     _p(lib, "gpbs_hwc_agent", C.c_int, C.c_char_p, C.c_int, C.POINTER(C.c_int))
     _p(lib, "gpbs_gpu_hwc_period", C.c_int, vp, C.c_int, C.c_int, C.POINTER(C.c_uint64))
     _p(lib, "gpbs_gpu_hwc_quality", C.c_int, vp, C.POINTER(C.c_uint64), C.POINTER(C.c_double), C.POINTER(C.c_int))
@@ -105,6 +104,7 @@ def bind(lib):
     _p(lib, "gpbs_gpu_hwc_bursts", C.c_int, vp, C.POINTER(u64), C.POINTER(u64))
     _p(lib, "gpbs_gpu_hwc_budget_stats", C.c_int, vp, C.POINTER(u64))
     _p(lib, "gpbs_gpu_hwc_sampler", C.c_int, vp, C.c_int, C.c_int, C.c_int)
+    _p(lib, "gpbs_gpu_param", C.c_int, vp, C.c_char_p, C.c_int)
     _p(lib, "gpbs_gpu_hwc_align", C.c_int, vp, C.c_int, C.c_int, C.c_int, C.POINTER(u64))
     _p(lib, "gpbs_gpu_hwc_tenant_periods", C.c_int, vp, C.c_int, C.POINTER(u64), C.POINTER(C.c_double))
     _p(lib, "gpbs_runner_queue", C.c_int, vp)

@@ -67,7 +67,6 @@ clock) rides the exchange and is reported in ``stats()``.
 from __future__ import annotations
 
 import ctypes as C
-import os
 import threading
 import time
 from typing import Callable, Dict, List, Optional
@@ -260,8 +259,6 @@ class GangCoordinator:
         # transport with the engine's own demand; the Python loop stays for the
         # dist/xgmi transports and custom demand callables
         can_native = transport == "shm" and demand is None and engine is not None and hasattr(engine, "h")
-        if native is None and os.environ.get("GPBS_GANG_NATIVE", "1") == "0":
-            native = False
         self.native = can_native if native is None else bool(native)
         if self.native and not can_native:
             raise ValueError("native gang coordinator needs transport='shm', an Engine and the engine demand")

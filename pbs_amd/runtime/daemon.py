@@ -40,7 +40,7 @@ class Daemon:
                  ctl_pages: int = 64, state_path: Optional[str] = None, attach_gpu: bool = False,
                  overrides: Optional[Dict[str, Any]] = None, se_mode: bool = False, hw_counters: bool = False):
         prof = cfgmod.MI355X_PROFILE if profile == "mi355x" else cfgmod.REFERENCE_PROFILE
-        self.cfg = cfgmod.load(config_path, prof)
+        self.cfg = cfgmod.load(config_path or os.environ.get("GPBS_CONFIG") or None, prof)
         kw = cfgmod.engine_kwargs(self.cfg)
         kw.update(overrides or {})
         kw["sim_clock"] = int(sim)
@@ -90,7 +90,7 @@ class Daemon:
     # ------------------------------------------------------ GPU backends
     def _gpu_backend(self, gpu: int, part_lo: int):
         from .gpu import GpuContext
-        ctx = GpuContext(gpu, part_base=part_lo, nctx=self.nctx)
+        ctx = GpuContext(gpu, part_base=part_lo, nctx=self.nctx, params=self.cfg.get("runtime", {}))
         ctx.attach_mux(self.engine, nctx=self.nctx)
         if self.se_mode:
             ctx.set_se_mode(True)

@@ -11,7 +11,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 from dataclasses import dataclass
-from typing import List, Optional
+from typing import Dict, List, Optional
 
 # One hardware queue per stream: every tenant runner stream plus the scheduler
 # stream (partition-table updates, counter reduce).  With the HIP default of 4
@@ -36,7 +36,10 @@ CTX = 4  # issue contexts per XCD in the partition table (SMT-sibling analog)
 
 class GpuContext:
     def __init__(self, device: int = 0, engine=None, part_base: int = 0, table_mode: str = "host",
-                 device_counters: bool = True, device_adapt: bool = False, nctx: int = 1):
+                 device_counters: bool = True, device_adapt: bool = False, nctx: int = 1,
+                 params: Optional[Dict[str, int]] = None):
+        """``params``: runtime parameters by name (gpbs.toml ``[runtime]``,
+        see :meth:`param`); None applies the loaded configuration's."""
         self.L = hiplib()
         self.device = device
         self.part_base = part_base
@@ -45,11 +48,27 @@ class GpuContext:
         if not h:
             raise RuntimeError(f"gpbs_gpu_ctx_create failed on device {device}")
         self.h = C.c_void_p(h)
+        if params is None:
+            from ..core.config import load
+            params = load(os.environ.get("GPBS_CONFIG") or None).get("runtime", {})
+        for k, v in params.items():
+            self.param(k, int(v))
         if table_mode == "bar":
             self.set_table_mode("bar")
         self.engine = None
         if engine is not None:
             self.attach(engine, device_counters, device_adapt)
+
+    def param(self, name: str, value: int = -1) -> int:
+        """Set a runtime parameter (value >= 0) and return its previous value:
+        sampler period_us / slow_us / duty_pct / burst_ms / budget_pct /
+        bucket / clean_pct / device_attr / fallback / stale_us / watch /
+        align / guard_us / long_us, class-share share / probe_every /
+        probe_len (csrc/hip/runtime.cpp gpbs_gpu_param)."""
+        r = self.L.gpbs_gpu_param(self.h, name.encode(), int(value))
+        if r == -22:
+            raise KeyError(f"unknown runtime parameter {name!r}")
+        return r
 
     def attach(self, engine, device_counters=True, device_adapt=False, nctx=None):
         """Bind the GPU actuator + counter backend to ``engine`` (whose

@@ -176,54 +176,6 @@ class QueueProber:
         return {"idx": self.idx, "ref_ms": round(self.ref, 4)}
 
 
-def _qprobe_cache_path() -> str:
-    return os.environ.get("GPBS_QPROBE_CACHE", "")
-
-
-def qprobe_load(key: str) -> Optional[Dict[str, float]]:
-    """A remembered QueueProber choice for `key` ("tenant:mask"), or None.
-
-    Opt-in (GPBS_QPROBE_CACHE=<file>): which hardware pipe a queue lands on is
-    decided per process, so a queue index that was fast in one run can share
-    the trainer's pipe in the next, and a reference time remembered from a
-    slow exploration hides it (config #5, profiles/r4/llm5_s24.txt: 1.5 s on
-    a 3x slower queue).  By default every process explores (a stalled queue
-    costs one slice) and remembers nothing."""
-    import json
-    if not _qprobe_cache_path():
-        return None
-    try:
-        with open(_qprobe_cache_path()) as f:
-            v = json.load(f).get(key)
-        return v if isinstance(v, dict) and "idx" in v and "ref_ms" in v else None
-    except (OSError, ValueError):
-        return None
-
-
-def qprobe_store(key: str, st: Dict[str, float]):
-    """Remember a settled choice (atomic replace; concurrent tenants keep each other's keys)."""
-    import fcntl
-    import json
-    path = _qprobe_cache_path()
-    if not path:
-        return
-    try:
-        with open(path + ".lock", "w") as lk:
-            fcntl.flock(lk, fcntl.LOCK_EX)
-            try:
-                with open(path) as f:
-                    d = json.load(f)
-            except (OSError, ValueError):
-                d = {}
-            d[key] = st
-            tmp = f"{path}.{os.getpid()}"
-            with open(tmp, "w") as f:
-                json.dump(d, f)
-            os.replace(tmp, path)
-    except OSError:
-        pass
-
-
 class TenantClient:
     def __init__(self, name: str, socket_path: str = DEFAULT_SOCKET, slots: int = 8, weight: int = -1,
                  cap: int = -1, pool=None, gpu: int = 0, heartbeat_s: float = 0.05, spatial: bool = True,
@@ -352,9 +304,7 @@ class TenantClient:
             if self.queue_probe > 1:
                 pr = self._probers.get(ses)
                 if pr is None:
-                    mem = qprobe_load(f"{self.name}:se{ses[0]}{ses[1]}:{self.queue_probe}")
-                    pr = self._probers[ses] = QueueProber(self.queue_probe, start=mem and mem["idx"],
-                                                          ref_ms=mem["ref_ms"] if mem else 0.0)
+                    pr = self._probers[ses] = QueueProber(self.queue_probe)
                     for i in range(self.queue_probe):  # all K at once: the set the prober chooses from
                         self._streams[("se",) + ses + (i,)] = torch.cuda.ExternalStream(
                             K.cumask_stream(se_cu_words(ses), device=self.gpu))
@@ -421,13 +371,7 @@ class TenantClient:
             # not its launch (the decode / training bodies end synchronised,
             # so this costs them nothing)
             s.synchronize()
-            pr = self._probers[key]
-            n_choices = len(pr.choices)
-            pr.record(1e3 * (time.perf_counter() - t1))
-            if len(pr.choices) != n_choices and len(key) == 2 and isinstance(key[0], int):
-                st = pr.state()  # a (re)settled SE-mode choice: remember it for the next run
-                if st is not None:
-                    qprobe_store(f"{self.name}:se{key[0]}{key[1]}:{self.queue_probe}", st)
+            self._probers[key].record(1e3 * (time.perf_counter() - t1))
         self._last_stream = s
         self._progress += 1
         if waited > 0:

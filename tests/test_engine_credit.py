@@ -576,3 +576,19 @@ def test_bound_stats_count_pbs_quantum_at_the_bounds_and_reset():
     assert st["periods"] == 40 and 0 < st["at_max"] < 40 and st["at_min"] <= 5  # from the initial quantum
     _feed_classes(e, a, b, 10, k0=41)
     assert e.bound_stats(a) == {"periods": 10, "at_min": 0, "at_max": 10}
+
+
+def test_runtime_section_of_gpbs_toml(tmp_path):
+    """gpbs.toml [runtime] carries the GPU runtime's sampler parameters
+    (the round-4 GPBS_HWC_* environment knobs); unknown keys are refused."""
+    from pbs_amd.core import config as cfgmod
+    p = tmp_path / "gpbs.toml"
+    p.write_text("[boot]\ntslice_us = 2000\n[runtime]\nbudget_pct = 8\nguard_us = 200\nalign = 1\n")
+    cfg = cfgmod.load(str(p), cfgmod.MI355X_PROFILE)
+    assert cfg["boot"]["tslice_us"] == 2000
+    assert cfg["runtime"] == {"budget_pct": 8, "guard_us": 200, "align": 1}
+    assert set(cfg["runtime"]) <= set(cfgmod.RUNTIME_KEYS)
+    p.write_text("[runtime]\nowner_burst = 1\n")
+    with pytest.raises(ValueError):
+        cfgmod.load(str(p))
+    assert cfgmod.load(None)["runtime"] == {}

@@ -223,17 +223,11 @@ def test_slice_orders_queue_changes_and_times_gpu_work(monkeypatch):
     assert sum(1 for e in log if e[0] == "wait") == n_wait
 
 
-def test_queue_prober_remembered_winner_skips_exploration(tmp_path, monkeypatch):
-    """VERDICT r3 item 6: a settled choice is remembered per tenant and mask;
-    the next run exploits it at once (no slow exploration slices) and
-    explores only if its first slices drift above 1.6x the remembered time."""
-    from pbs_amd.runtime.tenant import QueueProber, qprobe_load, qprobe_store
-    monkeypatch.setenv("GPBS_QPROBE_CACHE", str(tmp_path / "qp.json"))
-    assert qprobe_load("infer:se23:3") is None
-    qprobe_store("infer:se23:3", {"idx": 2, "ref_ms": 5.0})
-    qprobe_store("train:se01:3", {"idx": 0, "ref_ms": 190.0})
-    mem = qprobe_load("infer:se23:3")
-    assert mem == {"idx": 2, "ref_ms": 5.0} and qprobe_load("train:se01:3")["idx"] == 0
+def test_queue_prober_started_on_a_known_winner_skips_exploration():
+    """A prober started on a known-fast queue (start / ref_ms) exploits it at
+    once and explores only if its first slices drift above 1.6x that time."""
+    from pbs_amd.runtime.tenant import QueueProber
+    mem = {"idx": 2, "ref_ms": 5.0}
     # remembered queue still fast: never explores
     p = QueueProber(3, start=mem["idx"], ref_ms=mem["ref_ms"])
     seen = []
@@ -268,10 +262,3 @@ def test_prober_leaves_a_stalled_queue_without_waiting_for_the_cooldown():
         p.record(15.0)
         n += 1
     assert p.exploring and n <= 8, n
-
-
-def test_remembered_winner_is_opt_in(monkeypatch):
-    from pbs_amd.runtime.tenant import qprobe_load, qprobe_store
-    monkeypatch.delenv("GPBS_QPROBE_CACHE", raising=False)
-    qprobe_store("infer:se23:3", {"idx": 1, "ref_ms": 5.0})  # no cache configured: a no-op
-    assert qprobe_load("infer:se23:3") is None
