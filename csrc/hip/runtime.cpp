@@ -665,7 +665,7 @@ void hwc_loop(GpuCtx* c) {
     {
       std::lock_guard<std::mutex> g(c->mu);
       own_snapshot_locked(c, own.data());
-      std::memcpy(chg.data(), c->part_chg_ns, sizeof(c->part_chg_ns));
+      chg.assign(c->part_chg_ns, c->part_chg_ns + P);  // (chg came back from a swap with the snapshot)
     }
     share_update(c);  // the interval just sampled: shared time counted up to now
     if (rc >= 0) {
@@ -1804,6 +1804,7 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
   c->snap_se.assign((size_t)kXcds * kCtx * kNumPmc, 0);
   c->snap_x.assign((size_t)kXcds * kNumPmc, 0);
   c->snap_own.assign((size_t)kMaxTenants * kXcds * kCtx, 0);
+  c->snap_chg.assign((size_t)kXcds * kCtx, 0);
   hwc_attr_prev_init(c->hst);
   ok = ok && hipHostMalloc((void**)&c->h_ain, sizeof(HwcAttrIn), hipHostMallocMapped) == hipSuccess;
   ok = ok && hipMalloc((void**)&c->d_ain, sizeof(HwcAttrIn)) == hipSuccess;
