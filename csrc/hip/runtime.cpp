@@ -624,6 +624,15 @@ void share_update(GpuCtx* c) {
 
 inline u64 dpos(u64 a, u64 b) { return a >= b ? a - b : 0; }  // Q5: a counter reset is no negative delta
 
+// The drain guard in effect: hwc_guard_us covers a revoked tile / chunk
+// (~50-150 us) once workgroups see the new owner word, which takes ~16 us on
+// the device / BAR tables and ~340 us polling the pinned host table over
+// PCIe (p50 for a 1024-workgroup grid, profiles/micro/microbench_r2.json).
+int64_t guard_ns(const GpuCtx* c) {
+  const int host = __atomic_load_n(&c->table_mode, __ATOMIC_ACQUIRE) == 0;
+  return ((int64_t)c->hwc_guard_us + (host ? 400 : 0)) * 1000;
+}
+
 // Sampler thread.  Every hwc_period_us (1 ms) it reads the modeled per-tile
 // counter block (a 16 KiB device-to-host copy: no command-processor work) and
 // watches each tenant's modeled miss rate; a HARDWARE sample -- which stalls
@@ -760,7 +769,7 @@ void hwc_loop(GpuCtx* c) {
       c->sw_changed &= ~changed;
       if (!c->sw_changed) c->sw_first_ns = c->sw_last_ns = 0;
     } else if (changed) {
-      const int64_t guard = (int64_t)c->hwc_guard_us * 1000;
+      const int64_t guard = guard_ns(c);
       const int64_t due = std::min(lastp + guard, first + 4 * guard);
       if (t0 >= due) {
         const u32 close = changed & open;
@@ -896,10 +905,12 @@ void hwc_fill_in(GpuCtx* c, HwcAttrIn& in) {
       }
   in.nt_hi = hi ? hi : 1;
   // drain guard: the interval opens at the last consumed sample; a partition
-  // whose last owner change came at least a guard before it starts clean
+  // whose last owner change came at least a guard before it starts clean --
+  // in an interval of at least four guards, so a drain that outlasts the
+  // guard stays a small part of the window
   u32 dr = 0;
-  if (c->used_t && c->used_chg.size() == (size_t)kAttrP) {
-    const int64_t guard = (int64_t)c->hwc_guard_us * 1000;
+  const int64_t guard = guard_ns(c);
+  if (c->used_t && c->used_chg.size() == (size_t)kAttrP && c->snap_t - c->used_t >= 4 * guard) {
     for (int p = 0; p < kAttrP; ++p)
       if (c->used_t - c->used_chg[p] >= guard) dr |= 1u << p;
   }
