@@ -875,9 +875,15 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
     } else if constexpr (BAL == 7 || BAL == 8) {
       // C through LDS (the K loop's two buffers are exactly the 256x256 bf16
       // tile): each wave writes its 8-byte fragments at row m, 8-byte chunk
-      // n/4 XOR 2 (m & 15) (16 rows of one write land in 16 distinct bank
-      // groups), then the workgroup stores 16 rows per pass, each row as 32
-      // contiguous 16-byte stores: full 128-byte lines instead of 32-byte runs.
+      // n/4 XOR (m & 15), then the workgroup stores 16 rows per pass, each row
+      // as 32 contiguous 16-byte stores: full 128-byte lines instead of
+      // 32-byte runs.  Banking (MI355X_MICROARCH.md §LDS): a ds_write_b64 is
+      // four groups of 16 contiguous lanes on (a/4) mod 32 -- one group is 16
+      // rows of one chunk column, and XOR (m & 15) puts them on 16 distinct
+      // 8-byte positions of the 128-byte bank row (round 4's XOR 2 (m & 15)
+      // used 8: a 2-way conflict on every C write, 2.6 M extra cycles per
+      // 4096^3 GEMM); a ds_read_b128 group reads one row's 16 distinct 16-byte
+      // slots.  An odd row's two 8-byte chunks of a slot come swapped.
       // Every wave's K-loop reads retired before the re-align barrier above.
 #pragma unroll
       for (int i = 0; i < 8; ++i)
@@ -887,13 +893,14 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
           const int c8 = wc * 16 + j * 4 + lq;
           const u32 lo = (u32)f2bf(acc[i][j][0]) | ((u32)f2bf(acc[i][j][1]) << 16);
           const u32 hi = (u32)f2bf(acc[i][j][2]) | ((u32)f2bf(acc[i][j][3]) << 16);
-          *(__attribute__((address_space(3))) u32x2*)(lds + m * 512 + ((c8 ^ ((m & 15) << 1)) << 3)) = u32x2{lo, hi};
+          *(__attribute__((address_space(3))) u32x2*)(lds + m * 512 + ((c8 ^ (m & 15)) << 3)) = u32x2{lo, hi};
         }
       __syncthreads();
 #pragma unroll
       for (int p = 0; p < 16; ++p) {
         const int row = p * 16 + (tid >> 5), c16 = tid & 31;
-        const u32x4 v = *(const __attribute__((address_space(3))) u32x4*)(lds + row * 512 + (((2 * c16) ^ ((row & 15) << 1)) << 3));
+        u32x4 v = *(const __attribute__((address_space(3))) u32x4*)(lds + row * 512 + (((2 * c16) ^ (row & 14)) << 3));
+        if (row & 1) v = u32x4{v.z, v.w, v.x, v.y};
         u32x4* dst = (u32x4*)(C + (size_t)(tm * G2_BM + row) * N + tn * G2_BM + c16 * 8);
         if constexpr (BAL == 8) {  // streaming full-line stores (opts bit 17)
           __builtin_nontemporal_store(v, dst);
