@@ -268,6 +268,10 @@ struct GpuCtx {
   hipEvent_t attr_ev = nullptr;
   bool attr_pending = false;
   uint64_t attr_launches = 0, attr_busy_skips = 0, attr_host = 0;
+  // in-run cost of k_hwc_attribute, from its own 100 MHz entry / exit stamps,
+  // and launch -> harvest latency (the metric period it lags by)
+  uint64_t attr_harvested = 0, attr_ticks_sum = 0, attr_ticks_max = 0;
+  int64_t attr_launch_ns = 0, attr_lag_sum_ns = 0;
   hipEvent_t blk_ev = nullptr;
   hipStream_t hwc_stream = nullptr;
   std::thread hwc_th;
@@ -966,6 +970,11 @@ int hwc_consume(GpuCtx* c, bool wait) {
     if (q == hipSuccess) {
       hwc_fold(c, *c->h_aout, c->mod_inflight, c->pres_inflight, c->t_inflight);
       c->attr_pending = false;
+      const uint64_t tk = (uint32_t)(c->h_aout->pad[1] - c->h_aout->pad[0]);
+      c->attr_harvested++;
+      c->attr_ticks_sum += tk;
+      c->attr_ticks_max = std::max(c->attr_ticks_max, tk);
+      c->attr_lag_sum_ns += mono_ns() - c->attr_launch_ns;
     } else {
       c->attr_busy_skips++;
       return 0;
@@ -981,6 +990,7 @@ int hwc_consume(GpuCtx* c, bool wait) {
         hipEventRecord(c->attr_ev, c->sched_stream) == hipSuccess) {
       c->attr_pending = true;
       c->attr_launches++;
+      c->attr_launch_ns = mono_ns();
       std::memcpy(c->mod_inflight, c->mod_cur, sizeof(c->mod_cur));
       std::memcpy(c->pres_inflight, c->pres_cur, sizeof(c->pres_cur));
       c->t_inflight = c->snap_t;
@@ -2097,6 +2107,21 @@ int gpbs_gpu_hwc_attr_stats(void* p, uint64_t* launches, uint64_t* busy_skips, u
   return c->dev_attr;
 }
 
+// In-run timing of the device attribution since the last hwc reset: out4 =
+// attributions harvested, mean and max k_hwc_attribute duration (ns, the
+// kernel's own wall-clock stamps), mean launch -> harvest latency (ns).
+int gpbs_gpu_hwc_attr_timing(void* p, uint64_t* out4) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c || !out4) return -22;
+  std::lock_guard<std::mutex> g(c->snap_mu);
+  const uint64_t n = c->attr_harvested;
+  out4[0] = n;
+  out4[1] = n ? c->attr_ticks_sum * 10 / n : 0;  // 100 MHz ticks -> ns
+  out4[2] = c->attr_ticks_max * 10;
+  out4[3] = n ? (uint64_t)(c->attr_lag_sum_ns / (int64_t)n) : 0;
+  return 0;
+}
+
 // Device attribution on (1) / off (0, host reference); returns the old value.
 int gpbs_gpu_set_hwc_device(void* p, int on) {
   GpuCtx* c = (GpuCtx*)p;
@@ -2523,6 +2548,8 @@ int gpbs_gpu_hwc_reset(void* p) {
   std::memset(c->t_skipped, 0, sizeof(c->t_skipped));
   std::memset(c->t_sliver, 0, sizeof(c->t_sliver));
   c->align_samples = c->align_close = c->align_long = c->align_short = c->align_denied = 0;
+  c->attr_harvested = c->attr_ticks_sum = c->attr_ticks_max = 0;
+  c->attr_lag_sum_ns = 0;
   c->ts_gap_sum = 0;
   c->ts_gaps = 0;
   return 0;

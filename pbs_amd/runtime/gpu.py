@@ -188,12 +188,16 @@ class GpuContext:
         self.L.gpbs_gpu_hwc_budget_stats(self.h, bud)
         al = (C.c_uint64 * 8)()
         align = self.L.gpbs_gpu_hwc_align(self.h, -1, -1, -1, al)
+        at = (C.c_uint64 * 4)()
+        self.L.gpbs_gpu_hwc_attr_timing(self.h, at)
         return {"budget_pct": bud[0], "burst_denied": bud[1], "model_fallback_periods": bud[2],
                 "clean_periods": bud[3], "skipped_periods": al[7], "metric_periods": bud[2] + bud[3],
                 "align": bool(align), "align_samples": al[0], "align_close": al[1], "align_long": al[2],
                 "align_short": al[3], "align_denied": al[4], "ts_period_us": round(al[5] / 1e3, 1),
                 "attr_device": bool(dev), "attr_kernel_launches": la.value, "attr_busy_skips": bs.value,
-                "attr_host": ho.value, "duty_cap_pct": duty, "mean_period_us": round(mp.value / 1e3, 1),
+                "attr_host": ho.value, "attr_harvested": at[0], "attr_kernel_us_mean": round(at[1] / 1e3, 2),
+                "attr_kernel_us_max": round(at[2] / 1e3, 2), "attr_harvest_lag_us": round(at[3] / 1e3, 1),
+                "duty_cap_pct": duty, "mean_period_us": round(mp.value / 1e3, 1),
                 "burst_triggers": tr.value, "burst_samples": bsm.value,
                 "samples": n.value, "slow_samples": slow.value, "mean_sample_us": round(ns.value / 1e3, 1), "max_sample_us": round(mx.value / 1e3, 1),
                 "hw_over_model": [round(x, 4) for x in r],
