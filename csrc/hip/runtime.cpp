@@ -338,8 +338,9 @@ struct GpuCtx {
   int64_t part_chg_ns[kXcds * kCtx] = {};  // publish time of each partition's last owner change (mu)
   u32 q_pending[kXcds * kCtx] = {};        // quantum (us) of the owner each pending entry names (mu)
   u32 part_q_us[kXcds * kCtx] = {};        // ... as published (mu)
-  u32 sw_changed = 0;                      // partitions changed since the sampler last looked (mu)
-  int64_t sw_first_ns = 0, sw_last_ns = 0; // first / latest publish among them (mu)
+  u32 sw_changed = 0;                      // partitions changed since the sampler consumed them (mu)
+  int64_t sw_first_p[kXcds * kCtx] = {};   // per pending partition: its first change since (mu)
+  int64_t sw_last_ns = 0;                  // latest publish that changed an owner (mu)
   std::vector<int64_t> snap_chg;           // part_chg_ns at the newest snapshot (snap_mu)
   int64_t snap_t = 0;                      // its sample time (snap_mu)
   std::vector<int64_t> used_chg;           // ... of the last consumed snapshot (snap_mu)
@@ -519,8 +520,8 @@ bool publish_locked(GpuCtx* c) {
       // switch-aligned sampling: when and to whom this partition changed
       c->part_chg_ns[x] = t;
       c->part_q_us[x] = c->q_pending[x];
+      if (!((c->sw_changed >> x) & 1u)) c->sw_first_p[x] = t;
       c->sw_changed |= 1u << x;
-      if (!c->sw_first_ns) c->sw_first_ns = t;
       c->sw_last_ns = t;
     }
     for (int x = 0; x < kXcds * kCtx; ++x) __atomic_store_n(&c->h_table->owner[x], c->pending[x], __ATOMIC_RELEASE);
@@ -754,58 +755,79 @@ void hwc_loop(GpuCtx* c) {
         c->hwc_tok_ns = t0;
       }
     }
-    // 2. switch-aligned sample: one drain guard after the latest publish of
-    //    a burst of them (at most 4 guards after the first)
+    // 2. switch-aligned samples.  Per partition p: settled = its last change
+    //    is a drain guard old; open = a sample fell inside its current
+    //    tenure, at least a guard after the tenure began (the tenure has a
+    //    window that its next switch closes).  A sample is taken
+    //    * one guard after the FIRST change of an open partition (closes its
+    //      window, however soon further changes follow);
+    //    * when a changed partition settles into a long tenure (>= long_us
+    //      left of its quantum, or a quantum the table's writer did not give:
+    //      manual tables) -- opens its window at the start;
+    //    * for short tenures, as a budgeted pair: when one settles, the bucket
+    //      holds 3 tokens, and a pseudo-random third of the time.
     int64_t wake_at = next_tick;
     u32 changed = 0, q[P];
-    int64_t first = 0, lastp = 0;
+    int64_t chg[P], first[P];
     {
       std::lock_guard<std::mutex> g(c->mu);
       changed = c->sw_changed;
-      first = c->sw_first_ns;
-      lastp = c->sw_last_ns;
+      std::memcpy(chg, c->part_chg_ns, sizeof(chg));
+      std::memcpy(first, c->sw_first_p, sizeof(first));
       std::memcpy(q, c->part_q_us, sizeof(q));
+      seen_pub = c->sw_last_ns;
     }
-    seen_pub = lastp;
+    const int64_t guard = guard_ns(c);
+    const int64_t long_ns = (int64_t)c->hwc_long_us * 1000;
+    auto consume = [&](u32 bits) {
+      std::lock_guard<std::mutex> g(c->mu);
+      c->sw_changed &= ~bits;
+    };
     if (changed) sw_since_hw = true;
     if (changed && !c->hwc_align) {
-      std::lock_guard<std::mutex> g(c->mu);
-      c->sw_changed &= ~changed;
-      if (!c->sw_changed) c->sw_first_ns = c->sw_last_ns = 0;
+      consume(changed);
+      open = 0;
     } else if (changed) {
-      const int64_t guard = guard_ns(c);
-      const int64_t due = std::min(lastp + guard, first + 4 * guard);
-      if (t0 >= due) {
-        const u32 close = changed & open;
-        bool lng = false;
-        for (int p = 0; p < P; ++p)
-          if (((changed >> p) & 1u) && q[p] >= (u32)c->hwc_long_us) lng = true;
-        rng ^= rng << 13;
-        rng ^= rng >> 7;
-        rng ^= rng << 17;
-        const bool budgeted = c->hwc_budget_pct > 0;
-        const bool shrt = !lng && !close && (!budgeted || c->hwc_tokens >= 3.0) && rng % 3 == 0;
-        const bool want = close || lng || shrt;
-        {
-          std::lock_guard<std::mutex> g(c->mu);
-          c->sw_changed &= ~changed;
-          if (!c->sw_changed) c->sw_first_ns = c->sw_last_ns = 0;
-        }
-        if (want && (!budgeted || c->hwc_tokens >= 1.0)) {
-          burst = slow = false;
-          sampled = sample(t0);
-          c->align_samples++;
-          if (close) c->align_close++;
-          if (lng) c->align_long++;
-          if (shrt) c->align_short++;
-          open = (open & ~changed) | ((lng || shrt) ? changed : 0u);
+      u32 settled = 0, lngb = 0;
+      int64_t next_settle = INT64_MAX, close_due = INT64_MAX;
+      for (int p = 0; p < P; ++p) {
+        if (!((changed >> p) & 1u)) continue;
+        if (t0 - chg[p] >= guard) {
+          settled |= 1u << p;
+          if (q[p] == 0 || chg[p] + (int64_t)q[p] * 1000 - t0 >= long_ns) lngb |= 1u << p;
         } else {
-          if (want) c->align_denied++;
-          open &= ~changed;
+          next_settle = std::min(next_settle, chg[p] + guard);
         }
-      } else {
-        wake_at = std::min(wake_at, due);
+        if ((open >> p) & 1u) close_due = std::min(close_due, first[p] + guard);
       }
+      const u32 close = changed & open;
+      const bool want_close = close && t0 >= close_due;
+      rng ^= rng << 13;
+      rng ^= rng >> 7;
+      rng ^= rng << 17;
+      const bool budgeted = c->hwc_budget_pct > 0;
+      const bool lng = lngb != 0;
+      const bool shrt = settled && !lng && (!budgeted || c->hwc_tokens >= 3.0) && rng % 3 == 0;
+      const bool want = want_close || lng || shrt;
+      if (want && (!budgeted || c->hwc_tokens >= 1.0)) {
+        burst = slow = false;
+        sampled = sample(t0);
+        c->align_samples++;
+        if (want_close) c->align_close++;
+        if (lng) c->align_long++;
+        if (shrt) c->align_short++;
+        open &= ~changed;  // every changed partition's previous tenure ended
+        open |= lng ? lngb : (shrt ? settled : 0u);
+        consume(settled);  // an unsettled change is decided once it settles
+      } else {
+        if (want) c->align_denied++;
+        if (settled) {  // settled without a sample: no window for these tenures
+          open &= ~settled;
+          consume(settled);
+        }
+        if (close && !want_close) wake_at = std::min(wake_at, close_due);
+      }
+      if (next_settle != INT64_MAX) wake_at = std::min(wake_at, next_settle);
     }
     // 3. burst / background sample on a tick
     if (on_tick && !sampled) {
@@ -819,12 +841,20 @@ void hwc_loop(GpuCtx* c) {
         burst = false;
         c->hwc_denied++;
       }
-      if (burst || due) sample(t0);
+      if (burst || due) {
+        sample(t0);
+        // a sample inside a settled long tenure opens its window (closed at its next switch)
+        std::lock_guard<std::mutex> g(c->mu);
+        for (int p = 0; p < P; ++p)
+          if (!((c->sw_changed >> p) & 1u) && t0 - c->part_chg_ns[p] >= guard &&
+              (c->part_q_us[p] == 0 || c->part_chg_ns[p] + (int64_t)c->part_q_us[p] * 1000 - t0 >= long_ns))
+            open |= 1u << p;
+      }
     }
     // 4. sleep until the next tick, a pending switch sample, or a new publish
     std::unique_lock<std::mutex> lk(c->mu);
     c->cv.wait_until(lk, std::chrono::steady_clock::time_point(std::chrono::nanoseconds(wake_at)), [&] {
-      return c->hwc_stop.load(std::memory_order_acquire) || (c->hwc_align && c->sw_last_ns != seen_pub && c->sw_changed);
+      return c->hwc_stop.load(std::memory_order_acquire) || (c->hwc_align && c->sw_last_ns != seen_pub);
     });
   }
 }
