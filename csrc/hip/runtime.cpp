@@ -829,6 +829,34 @@ void hwc_loop(GpuCtx* c) {
       }
       if (next_settle != INT64_MAX) wake_at = std::min(wake_at, next_settle);
     }
+    // 2b. a short window closes BEFORE its tenure's switch: one sample time
+    //     plus a margin ahead of the end of the quantum its owner was given
+    //     (after the switch, the drain guard and the sample itself would take
+    //     a third of a 1 ms tenure); a switch that comes early closes it as above
+    if (c->hwc_align && !sampled && open) {
+      const int64_t lead = (int64_t)c->hwc_dt_ewma + 50000;
+      u32 pre = 0;
+      int64_t pre_due = INT64_MAX;
+      for (int p = 0; p < P; ++p) {
+        if (!((open >> p) & 1u) || ((changed >> p) & 1u) || q[p] == 0 || (int64_t)q[p] * 1000 >= long_ns) continue;
+        const int64_t due = chg[p] + (int64_t)q[p] * 1000 - lead;
+        if (t0 >= due)
+          pre |= 1u << p;
+        else
+          pre_due = std::min(pre_due, due);
+      }
+      if (pre && (c->hwc_budget_pct <= 0 || c->hwc_tokens >= 1.0)) {
+        burst = slow = false;
+        sampled = sample(t0);
+        c->align_samples++;
+        c->align_close++;
+        open &= ~pre;
+      } else if (pre) {
+        c->align_denied++;
+        open &= ~pre;
+      }
+      if (pre_due != INT64_MAX) wake_at = std::min(wake_at, pre_due);
+    }
     // 3. burst / background sample on a tick
     if (on_tick && !sampled) {
       slow = c->hwc_slow_us > c->hwc_period_us && t0 - last_change >= kSteadyNs;
@@ -940,11 +968,11 @@ void hwc_fill_in(GpuCtx* c, HwcAttrIn& in) {
   in.nt_hi = hi ? hi : 1;
   // drain guard: the interval opens at the last consumed sample; a partition
   // whose last owner change came at least a guard before it starts clean --
-  // in an interval of at least four guards, so a drain that outlasts the
+  // in an interval of at least three guards, so a drain that outlasts the
   // guard stays a small part of the window
   u32 dr = 0;
   const int64_t guard = guard_ns(c);
-  if (c->used_t && c->used_chg.size() == (size_t)kAttrP && c->snap_t - c->used_t >= 4 * guard) {
+  if (c->used_t && c->used_chg.size() == (size_t)kAttrP && c->snap_t - c->used_t >= 3 * guard) {
     for (int p = 0; p < kAttrP; ++p)
       if (c->used_t - c->used_chg[p] >= guard) dr |= 1u << p;
   }
