@@ -328,13 +328,14 @@ struct GpuCtx {
   //   * one that ends a tenure whose start was sampled (closes a window);
   //   * one that starts a tenure of at least hwc_long_us (opens a window:
   //     memory-class quanta, 11 ms in the MI355X profile);
-  //   * a short tenure (compute quanta, 1 ms) opens a window -- a sample pair
-  //     -- only when the bucket holds the pair plus a reserve, at a
-  //     pseudo-random subset of switches so co-sharers rotating in lockstep
-  //     all get measured.
+  //   * a short tenure (compute quanta, 1 ms) opens a window -- a sample pair,
+  //     the second one ahead of the quantum's end -- about once per
+  //     hwc_pair_gap_us (jittered, so co-sharers rotating in lockstep all get
+  //     measured) when the bucket holds the pair plus a reserve.
   int hwc_align = 1;          // switch-aligned samples on
   int hwc_guard_us = 150;     // publish -> sample: a revoked GEMM tile / stream chunk drains in ~50-150 us
   int hwc_long_us = 3000;     // tenures at least this long open a window at every switch
+  int hwc_pair_gap_us = 20000;  // short tenures: about one measured pair per this long
   int64_t part_chg_ns[kXcds * kCtx] = {};  // publish time of each partition's last owner change (mu)
   u32 q_pending[kXcds * kCtx] = {};        // quantum (us) of the owner each pending entry names (mu)
   u32 part_q_us[kXcds * kCtx] = {};        // ... as published (mu)
@@ -351,14 +352,14 @@ struct GpuCtx {
   uint64_t ts_gaps = 0;
   // Model fallback (default on): a tenant that ran substantially in an
   // interval without a clean window, and whose last clean window is older
-  // than hwc_stale_us, reports the interval's MODELED deltas scaled per
+  // than hwc_stale_us (250 ms), reports the interval's MODELED deltas scaled per
   // counter by its hardware/model ratio from its own clean windows (EWMA);
   // uncalibrated, the period reports nothing.  Otherwise such a period is
   // skipped (the PBS idle-sample rule), and a sliver -- a tenant that held
   // its partitions for less than (100 - clean_pct) % of the interval, the
   // edge of a neighbouring tenure -- never counts.
   int model_fallback = 1;
-  int hwc_stale_us = 50000;
+  int hwc_stale_us = 250000;
   double mod_cur[kMaxTenants][kNumPmc] = {};       // modeled deltas of the newest consumed snapshot
   double mod_inflight[kMaxTenants][kNumPmc] = {};  // ... of the snapshot whose attribution is in flight
   double pres_cur[kMaxTenants] = {};               // largest owned share of a partition over the interval
@@ -666,7 +667,7 @@ void hwc_loop(GpuCtx* c) {
   constexpr int64_t kSteadyNs = 20000000;  // slow_us back-off: no owner change for 20 ms
   uint64_t last_sw = c->flushes.load();
   int64_t last_change = mono_ns(), last_hw = 0, burst_until = mono_ns() + (int64_t)c->hwc_burst_ms * 1000000;
-  int64_t next_tick = mono_ns(), seen_pub = 0;
+  int64_t next_tick = mono_ns(), seen_pub = 0, next_pair = 0;
   bool watch_primed = false, sw_since_hw = false, slow = false, burst = false;
   u32 open = 0;  // partitions whose current tenure began with a (switch-aligned) sample
   uint64_t rng = 0x2545F4914F6CDD1Dull;
@@ -765,7 +766,7 @@ void hwc_loop(GpuCtx* c) {
     //      left of its quantum, or a quantum the table's writer did not give:
     //      manual tables) -- opens its window at the start;
     //    * for short tenures, as a budgeted pair: when one settles, the bucket
-    //      holds 3 tokens, and a pseudo-random third of the time.
+    //      holds 3 tokens, and the pair gap has passed.
     int64_t wake_at = next_tick;
     u32 changed = 0, q[P];
     int64_t chg[P], first[P];
@@ -807,7 +808,7 @@ void hwc_loop(GpuCtx* c) {
       rng ^= rng << 17;
       const bool budgeted = c->hwc_budget_pct > 0;
       const bool lng = lngb != 0;
-      const bool shrt = settled && !lng && (!budgeted || c->hwc_tokens >= 3.0) && rng % 3 == 0;
+      const bool shrt = settled && !lng && (!budgeted || c->hwc_tokens >= 3.0) && t0 >= next_pair;
       const bool want = want_close || lng || shrt;
       if (want && (!budgeted || c->hwc_tokens >= 1.0)) {
         burst = slow = false;
@@ -815,7 +816,12 @@ void hwc_loop(GpuCtx* c) {
         c->align_samples++;
         if (want_close) c->align_close++;
         if (lng) c->align_long++;
-        if (shrt) c->align_short++;
+        if (shrt) {
+          c->align_short++;
+          // the next pair a jittered pair_gap_us on: at most ~1/gap short windows,
+          // landing on every co-sharer of a lockstep rotation in turn
+          next_pair = t0 + (int64_t)c->hwc_pair_gap_us * 1000 * (3 + (int64_t)(rng % 3)) / 4;
+        }
         open &= ~changed;  // every changed partition's previous tenure ended
         open |= lng ? lngb : (shrt ? settled : 0u);
         consume(settled);  // an unsettled change is decided once it settles
@@ -1338,6 +1344,18 @@ namespace {
 // The policy is host-only code (MaskedPoolCore), checked on the CPU by
 // gpbs_hip_masked_pool_selftest with fake queue handles.
 constexpr int kMaskedBudget = 16;
+// Hardware queues land on the command processor's pipes round-robin in
+// creation order (4 pipes): CU-masked queues whose creation indexes differ by
+// a multiple of 4 share a pipe, and a GEMM dispatch waiting there for CUs
+// holds up the other queue's dispatches -- a stream copy on the other half
+// of the GPU keeps 0.61-0.64 of its rate next to back-to-back GEMMs on a
+// same-pipe queue, 0.88-0.89 on any other (scripts/pipe_probe.py,
+// profiles/r5/pipe_probe.txt).  That was the round-4 "bimodal 8mix" (slow
+// runs had the GEMMs' queue and a stream's 4 pool indexes apart).  So a
+// layout takes the queue whose pipe is least shared with the layouts running
+// now -- another class half's queue costs 10, same half 1 -- creating one
+// (its pipe: the creation count mod 4) when that is cheaper, under the budget.
+constexpr int kPipes = 4;
 
 struct MaskedPoolCore {
   struct Ent {
@@ -1346,16 +1364,26 @@ struct MaskedPoolCore {
     hipStream_t s;
     uint32_t key;
     int refs;
+    int pipe;  // creation index mod kPipes
   };
   std::mutex mu;
   std::vector<Ent> ents;
-  uint64_t created = 0, cross_key_shares = 0;
+  uint64_t created = 0, cross_key_shares = 0, pipe_shared_other = 0;
   int held_max = 0;  // high-water mark of queues held at once (reset with reset_max)
+  int dev_created[16] = {};
 
   int held_locked(int dev) const {
     int n = 0;
     for (const auto& e : ents) n += e.device == dev && e.refs > 0;
     return n;
+  }
+  // cost of running a layout of mask m / key k on `pipe` next to the held queues
+  int pipe_cost(int dev, int pipe, const uint32_t m[8], uint32_t key, const Ent* self) const {
+    int cost = 0;
+    for (const auto& e : ents)
+      if (&e != self && e.device == dev && e.refs > 0 && e.pipe == pipe && (key == 0 || e.key != key))
+        cost += std::memcmp(e.m, m, sizeof(e.m)) != 0 ? 10 : 1;
+    return cost;
   }
   // key 0: exclusive (never shared).  create(m) makes a new queue (nullptr on
   // failure).  Caller does not hold mu.
@@ -1363,38 +1391,48 @@ struct MaskedPoolCore {
   hipStream_t acquire(int dev, const uint32_t m[8], uint32_t key, Create&& create) {
     std::lock_guard<std::mutex> g(mu);
     Ent* same = nullptr;   // this layout's queue
-    Ent* idle = nullptr;   // a queue of this mask nobody holds (same key preferred)
+    Ent* idle = nullptr;   // the cheapest queue of this mask nobody holds
     Ent* least = nullptr;  // least-held keyed queue of this mask
-    int live = 0;
+    int live = 0, idle_cost = 1 << 30;
     for (auto& e : ents) {
       if (e.device != dev) continue;
       live++;
       if (std::memcmp(e.m, m, sizeof(e.m)) != 0) continue;
       if (key && e.key == key && e.refs > 0 && (!same || e.refs < same->refs)) same = &e;
-      if (e.refs == 0 && (!idle || (key && e.key == key && idle->key != key))) idle = &e;
+      if (e.refs == 0) {
+        const int cst = pipe_cost(dev, e.pipe, m, key, &e) * 2 + (key && e.key == key ? 0 : 1);
+        if (cst < idle_cost) idle = &e, idle_cost = cst;
+      }
       if (e.key && e.refs > 0 && (!least || e.refs < least->refs)) least = &e;
     }
+    const int dv = dev >= 0 && dev < 16 ? dev : 0;
+    const int new_pipe = dev_created[dv] % kPipes;
+    const int new_cost = pipe_cost(dev, new_pipe, m, key, nullptr) * 2 + 1;
     hipStream_t s = nullptr;
+    Ent* got = nullptr;
     if (same) {
       same->refs++;
-      s = same->s;
-    } else if (idle) {
+      got = same;
+    } else if (idle && (idle_cost <= new_cost || live >= kMaskedBudget)) {
       idle->key = key;
       idle->refs = 1;
-      s = idle->s;
+      got = idle;
     } else if (live < kMaskedBudget || !key || !least) {
       s = create(m);
       if (!s) return nullptr;
-      ents.push_back({dev, {}, s, key, 1});
+      ents.push_back({dev, {}, s, key, 1, new_pipe});
       std::memcpy(ents.back().m, m, sizeof(ents.back().m));
       created++;
+      dev_created[dv]++;
+      got = &ents.back();
     } else {  // over budget: share another layout's queue (serialises the two)
       least->refs++;
       cross_key_shares++;
-      s = least->s;
+      got = least;
     }
+    if (got != same && pipe_cost(dev, got->pipe, m, key, got) >= 10) pipe_shared_other++;
     held_max = std::max(held_max, held_locked(dev));
-    return s;
+    return got->s;
   }
   void release(hipStream_t s) {
     if (!s) return;
@@ -1404,6 +1442,12 @@ struct MaskedPoolCore {
         e.refs--;
         return;
       }
+  }
+  int pipe_of(hipStream_t s) {
+    std::lock_guard<std::mutex> g(mu);
+    for (auto& e : ents)
+      if (e.s == s) return e.pipe;
+    return -1;
   }
 };
 MaskedPoolCore& masked_pool() {
@@ -1913,6 +1957,9 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
   int lo = 0, hi = 0;
   hipDeviceGetStreamPriorityRange(&lo, &hi);
   ok = ok && hipStreamCreateWithPriority(&c->sched_stream, hipStreamNonBlocking, hi) == hipSuccess;
+  // the sampler's stream too: a hardware queue created later, between two
+  // CU-masked ones, would shift the masked pool's pipe arithmetic (MaskedPoolCore)
+  ok = ok && hipStreamCreateWithFlags(&c->hwc_stream, hipStreamNonBlocking) == hipSuccess;
   ok = ok && hipMalloc((void**)&c->d_table, sizeof(PartTable)) == hipSuccess;
   if (!ok) {
     fprintf(stderr, "[gpbs-hip] ctx_create failed on device %d\n", device);
@@ -2557,6 +2604,7 @@ int gpbs_gpu_param(void* p, const char* name, int value) {
       {"fallback", &c->model_fallback, 0, 1},           {"stale_us", &c->hwc_stale_us, 0, 100000000},
       {"watch", &c->hwc_watch, 0, 1},                   {"align", &c->hwc_align, 0, 1},
       {"guard_us", &c->hwc_guard_us, 0, 100000},        {"long_us", &c->hwc_long_us, 0, 100000000},
+      {"pair_gap_us", &c->hwc_pair_gap_us, 0, 10000000},
       {"share", &c->share_enable, 0, 1},                {"probe_every", &c->probe_every, 0, 1000000},
       {"probe_len", &c->probe_len, 0, 1000000},
   };
@@ -2909,22 +2957,24 @@ int gpbs_gpu_adapt_stats(void* p, uint64_t* calls, uint64_t* late, uint64_t* bus
 // Process-wide CU-masked queue pool: out[0] masked streams ever created,
 // out[1] currently free (the rest are held by runners), out[2] acquires that
 // had to share another layout's queue (over the budget: those layouts ran
-// serialised), out[3] most queues held at once since the last reset.  Every
+// serialised), out[3] most queues held at once since the last reset, out[4]
+// acquires that had to run on a pipe another class half's queue was using.  Every
 // created one is a hardware queue this process keeps.  reset: restart the
 // high-water mark at the number held now.
-int gpbs_gpu_masked_pool(uint64_t* out4, int reset) {
+int gpbs_gpu_masked_pool(uint64_t* out5, int reset) {
   MaskedPoolCore& P = masked_pool();
   int dev = 0;
   hipGetDevice(&dev);
   std::lock_guard<std::mutex> g(P.mu);
   if (reset) P.held_max = P.held_locked(dev);
-  if (!out4) return 0;
-  out4[0] = P.created;
+  if (!out5) return 0;
+  out5[0] = P.created;
   uint64_t idle = 0;
   for (auto& e : P.ents) idle += e.refs == 0;
-  out4[1] = idle;
-  out4[2] = P.cross_key_shares;
-  out4[3] = (uint64_t)P.held_max;
+  out5[1] = idle;
+  out5[2] = P.cross_key_shares;
+  out5[3] = (uint64_t)P.held_max;
+  out5[4] = P.pipe_shared_other;
   return 0;
 }
 
@@ -2965,6 +3015,21 @@ int gpbs_hip_masked_pool_selftest(void) {
   for (auto& en : P.ents)
     if (en.s == k2 && en.refs != 1) return 8;
   if (P.held_max < kMaskedBudget) return 9;
+  // 8. pipes: queues created consecutively sit on consecutive pipes; a memory
+  //    layout next to a running compute queue avoids the compute queue's pipe
+  MaskedPoolCore Q;
+  hipStream_t c0 = Q.acquire(0, mc, 0x1, mk);  // index 0: pipe 0
+  hipStream_t m1 = Q.acquire(0, mm, 0x2, mk), m2 = Q.acquire(0, mm, 0x3, mk), m3 = Q.acquire(0, mm, 0x4, mk);
+  hipStream_t m4 = Q.acquire(0, mm, 0x5, mk);  // index 4: pipe 0, the compute queue's
+  if (Q.pipe_of(c0) != 0 || Q.pipe_of(m1) != 1 || Q.pipe_of(m4) != 0 || Q.pipe_shared_other != 1) return 10;
+  Q.release(m1);
+  Q.release(m4);
+  hipStream_t n1 = Q.acquire(0, mm, 0x9, mk);  // idle on pipes 1 and 0: takes pipe 1
+  if (n1 != m1) return 11;
+  hipStream_t n2 = Q.acquire(0, mm, 0xA, mk);  // idle m4 shares the compute pipe: a new one (index 5, pipe 1) is cheaper
+  if (n2 == m4 || Q.pipe_of(n2) != 1 || Q.created != 6) return 12;
+  (void)m2;
+  (void)m3;
   return 0;
 }
 

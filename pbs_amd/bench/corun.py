@@ -1044,7 +1044,8 @@ class Corun:
         # share another layout's queue (serialised layouts)
         gs = self.ctx.stats()
         res["masked_queues"] = {"held_max": gs["masked_queues_held_max"], "created": gs["masked_queues_created"],
-                                "cross_key_shares": gs["masked_cross_key_shares"]}
+                                "cross_key_shares": gs["masked_cross_key_shares"],
+                                "pipe_shared_other": gs["masked_pipe_shared_other"]}
         res["host"] = {k: round(h1[k] - h0[k], 3) for k in h1 if k in h0}
         if "cpu_s" in res["host"]:
             res["host"]["cpu_util"] = round(res["host"]["cpu_s"] / (wall_ms_local / 1e3), 2)  # cores busy

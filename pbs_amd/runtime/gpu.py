@@ -349,12 +349,13 @@ class GpuContext:
         self.L.gpbs_gpu_stats(self.h, out)
         ca, la, bu = C.c_uint64(0), C.c_uint64(0), C.c_uint64(0)
         self.L.gpbs_gpu_adapt_stats(self.h, C.byref(ca), C.byref(la), C.byref(bu))
-        mp = (C.c_uint64 * 4)()
+        mp = (C.c_uint64 * 5)()
         self.L.gpbs_gpu_masked_pool(mp, 0)
         return {"switches": out[0], "flushes": out[1], "metric_calls": out[2], "metric_ns": out[3],
                 "adapt_device_calls": ca.value, "adapt_device_late": la.value, "adapt_device_busy": bu.value,
                 "masked_queues_created": mp[0], "masked_queues_free": mp[1],
-                "masked_cross_key_shares": mp[2], "masked_queues_held_max": mp[3]}
+                "masked_cross_key_shares": mp[2], "masked_queues_held_max": mp[3],
+                "masked_pipe_shared_other": mp[4]}
 
     def masked_pool_reset(self):
         """Restart the held-queues high-water mark (per timed run)."""
