@@ -1343,7 +1343,14 @@ namespace {
 // every such share is counted (cross_key_shares, reported with the run).
 // The policy is host-only code (MaskedPoolCore), checked on the CPU by
 // gpbs_hip_masked_pool_selftest with fake queue handles.
-constexpr int kMaskedBudget = 16;
+// Budget 10: the most layouts any mix runs at once is 8 (the 8mix static
+// split: 3 compute blocks, 4 memory blocks, the latency lane); every created
+// queue stays with the process, and past ~24 hardware queues in all (these,
+// the 12 plain-stream queues, the profiler's) the hardware scheduler
+// time-slices every queue: a full bench process that had created 16 ran its
+// 8mix at 0.84-0.97 instead of 1.26-1.28 (profiles/r5/bench_s6_queue_growth.txt).
+constexpr int kMaskedBudget = 10;
+constexpr int kPipeCreateCap = 8;  // creating a queue only for a better pipe stops here
 // Hardware queues land on the command processor's pipes round-robin in
 // creation order (4 pipes): CU-masked queues whose creation indexes differ by
 // a multiple of 4 share a pipe, and a GEMM dispatch waiting there for CUs
@@ -1413,7 +1420,7 @@ struct MaskedPoolCore {
     if (same) {
       same->refs++;
       got = same;
-    } else if (idle && (idle_cost <= new_cost || live >= kMaskedBudget)) {
+    } else if (idle && (idle_cost <= new_cost || live >= kPipeCreateCap)) {
       idle->key = key;
       idle->refs = 1;
       got = idle;
