@@ -2511,14 +2511,15 @@ int gpbs_hip_hwc_fold_selftest(void) {
     hwc_fold(&c, o, mod, pres, now);
     take(&in, &mi);
     if (in <= 0 || std::fabs(mi * 1e5 / in - hw_miss * 1e5 / hw_inst) > 1.0) return 2;
-    now += 11000000;
+    const int64_t stale = (int64_t)c.hwc_stale_us * 1000;
+    now += stale / 5;
     period(false, 0.9);
-    hwc_fold(&c, o, mod, pres, now);  // 11 ms after a clean window: not stale
+    hwc_fold(&c, o, mod, pres, now);  // a fifth of the staleness after a clean window: skipped
     take(&in, &mi);
     if (in != 0) return 3;
-    now += 60000000;
+    now += stale;
     period(false, 0.9);
-    hwc_fold(&c, o, mod, pres, now);  // 71 ms: stale -> calibrated fallback
+    hwc_fold(&c, o, mod, pres, now);  // past it: stale -> calibrated fallback
     take(&in, &mi);
     if (in <= 0) return 4;
     const double rate = mi * 1e5 / in, want = hw_miss * 1e5 / hw_inst;
