@@ -507,36 +507,58 @@ class Corun:
     def _ipc_runner(self, t: int, mem_chunk: dict):
         """The gated IPC all-reduce tenant, after a one-unit self-test on
         every rank: inputs rank + 1, every output element must be the sum
-        over ranks (exact in bf16); any rank failing makes all fall back."""
+        over ranks (exact in bf16); any rank failing makes all fall back.
+        Every step ends in an agreement over the ranks (a MIN of the local
+        outcome), so a rank that fails a step never runs ahead into a
+        collective its peers are not in."""
         from ..parallel.ipc_coll import IpcColl
-        ok, r = 1.0, None
-        try:
-            self.coll_buf = IpcColl(self.device, self.rank, self.world, self.cfg.coll_bytes,
-                                    group=self.groups.get("ctrl"))
-            n = self.coll_buf.nbytes // 2
-            self.coll_buf.fill(torch.full((n,), float(self.rank + 1), dtype=torch.bfloat16, device="cuda"))
-            r = Runner(self.ctx, "allreduce", t, depth=self.cfg.depth, gate=False, engine_wake=False,
-                       coll=self.coll_buf, timeout_ms=10000, **mem_chunk)
-            self._barrier()
-            r.submit(1)
-            r.wait(60.0)
-            torch.cuda.synchronize()
-        except Exception as ex:  # noqa: BLE001 -- any failure: agree on the fallback
-            self.log(f"[corun] IPC all-reduce: {ex}")
-            ok = 0.0
-        ok = -self._allreduce(-ok, "max")  # min over ranks
-        if ok > 0:
-            self._barrier()
-            want = float(self.world * (self.world + 1) // 2)
-            good = bool((self.coll_buf.read(1) == want).all().item())
-            ok = -self._allreduce(-float(good), "max")
-        if ok <= 0:
+        r = None
+
+        def agree(ok: bool) -> bool:
+            return -self._allreduce(-(1.0 if ok else 0.0), "max") > 0  # MIN over ranks
+
+        def fail():
             if r is not None:
                 r.close()
             if self.coll_buf is not None:
                 self.coll_buf.close()
                 self.coll_buf = None
             return None
+        try:  # the exchanges inside raise on every rank together
+            self.coll_buf = IpcColl(self.device, self.rank, self.world, self.cfg.coll_bytes,
+                                    group=self.groups.get("ctrl"))
+        except Exception as ex:  # noqa: BLE001
+            self.log(f"[corun] IPC all-reduce: {ex}")
+            self.coll_buf = None
+            return None
+        ok = True
+        try:
+            n = self.coll_buf.nbytes // 2
+            self.coll_buf.fill(torch.full((n,), float(self.rank + 1), dtype=torch.bfloat16, device="cuda"))
+            r = Runner(self.ctx, "allreduce", t, depth=self.cfg.depth, gate=False, engine_wake=False,
+                       coll=self.coll_buf, timeout_ms=10000, **mem_chunk)
+            torch.cuda.synchronize()
+        except Exception as ex:  # noqa: BLE001
+            self.log(f"[corun] IPC all-reduce runner: {ex}")
+            ok = False
+        if not agree(ok):
+            return fail()
+        try:  # one collective unit on every rank (a P2P-flag barrier inside)
+            r.submit(1)
+            r.wait(60.0)
+            torch.cuda.synchronize()
+        except Exception as ex:  # noqa: BLE001
+            self.log(f"[corun] IPC all-reduce self-test unit: {ex}")
+            ok = False
+        if not agree(ok):
+            return fail()
+        want = float(self.world * (self.world + 1) // 2)
+        try:
+            good = bool((self.coll_buf.read(1) == want).all().item())
+        except Exception:  # noqa: BLE001
+            good = False
+        if not agree(good):
+            return fail()
         g = torch.Generator(device="cuda").manual_seed(4321 + self.rank)
         self.coll_buf.fill(torch.randn(self.coll_buf.nbytes // 2, dtype=torch.bfloat16, device="cuda", generator=g))
         r.set_engine_wake(True)

@@ -33,18 +33,9 @@ class IpcColl:
         (default: ``torch.distributed.all_gather_object`` on ``group``)."""
         self.L = hiplib()
         self.device, self.rank, self.world = device, rank, world
+        self.h = None
         align = 16 * world
         self.nbytes = (int(nbytes) + align - 1) // align * align
-        h = self.L.gpbs_coll_create(device, rank, world, self.nbytes)
-        if not h:
-            raise RuntimeError("gpbs_coll_create failed")
-        self.h = C.c_void_p(h)
-        nb = self.L.gpbs_coll_handle_bytes()
-        buf = (C.c_char * nb)()
-        if self.L.gpbs_coll_export(self.h, buf) != nb:
-            self.close()
-            raise RuntimeError("hipIpcGetMemHandle failed")
-        mine = bytes(buf)
         if gather is None:
             import torch.distributed as dist
 
@@ -52,18 +43,45 @@ class IpcColl:
                 out = [None] * world
                 dist.all_gather_object(out, obj, group=group)
                 return out
+        # Every rank makes exactly two exchanges whatever fails locally (its
+        # handle or None, then its error or None), and all ranks raise
+        # together: a rank that failed alone and moved on to the caller's
+        # next collective would leave its peers waiting in this one (the
+        # round-5 8-rank rehearsal hung that way).
+        mine, err = None, None
+        try:
+            h = self.L.gpbs_coll_create(device, rank, world, self.nbytes)
+            if not h:
+                raise RuntimeError("gpbs_coll_create failed")
+            self.h = C.c_void_p(h)
+            nb = self.L.gpbs_coll_handle_bytes()
+            buf = (C.c_char * nb)()
+            if self.L.gpbs_coll_export(self.h, buf) != nb:
+                raise RuntimeError("hipIpcGetMemHandle failed")
+            mine = bytes(buf)
+        except Exception as ex:  # noqa: BLE001 -- reported through the exchange
+            err = f"rank {rank}: {ex}"
         allh = gather(mine)
-        for peer, hb in enumerate(allh):
-            if peer == rank:
-                continue
-            arr = (C.c_char * nb).from_buffer_copy(hb)
-            rc = self.L.gpbs_coll_open(self.h, peer, arr)
-            if rc:
-                self.close()
-                raise RuntimeError(f"hipIpcOpenMemHandle of rank {peer} failed ({rc})")
-        if self.L.gpbs_coll_finalize(self.h):
+        if err is None and any(hb is None for hb in allh):
+            err = f"rank {rank}: a peer failed to export its buffers"
+        if err is None:
+            try:
+                nb = self.L.gpbs_coll_handle_bytes()
+                for peer, hb in enumerate(allh):
+                    if peer == rank:
+                        continue
+                    arr = (C.c_char * nb).from_buffer_copy(hb)
+                    rc = self.L.gpbs_coll_open(self.h, peer, arr)
+                    if rc:
+                        raise RuntimeError(f"hipIpcOpenMemHandle of rank {peer} failed ({rc})")
+                if self.L.gpbs_coll_finalize(self.h):
+                    raise RuntimeError("gpbs_coll_finalize failed")
+            except Exception as ex:  # noqa: BLE001
+                err = f"rank {rank}: {ex}"
+        errs = [e for e in gather(err) if e]
+        if errs:
             self.close()
-            raise RuntimeError("gpbs_coll_finalize failed")
+            raise RuntimeError("IPC all-reduce setup failed: " + "; ".join(errs[:4]))
         self.desc = self.L.gpbs_coll_buffer(self.h, 3)
 
     def fill(self, t: torch.Tensor, which: int = 0):

@@ -5,8 +5,7 @@
 set -o pipefail
 O=gpurun_out/r5
 mkdir -p $O
-S=${1:-s5}
-timeout -k 10 120 python -u scripts/pipe_probe.py --queues 8 --ms 150 > $O/${S}_pipe_probe.log 2>&1 &&
-timeout -k 10 300 python -u -m pytest tests/test_gpu_se_hwc.py tests/test_gpu_phase.py tests/test_gpu_kernels.py -x -q --timeout 150 --timeout-method thread > $O/${S}_gputest.log 2>&1 &&
-timeout -k 10 400 python -u bench.py --mix 8mix --reps 3 --policies none,static-se,credit-classq,gpbs --out $O/${S}_8mix.json > $O/${S}_8mix.log 2>&1 &&
-timeout -k 10 400 python -u bench.py --mix phase-ts --reps 3 --out $O/${S}_phasets.json > $O/${S}_phasets.log 2>&1
+S=${1:-s8}
+timeout -k 10 300 python -u bench.py --mix 4mix --reps 5 --policies static-se,gpbs,gpbs-model,gpbs-noalign \
+  --out $O/${S}_4mix_ab.json > $O/${S}_4mix_ab.out 2> $O/${S}_4mix_ab.log &&
+timeout -k 10 700 python -u bench.py --gpus 1 --steps 20 --warmup 5 --out $O/${S}_bench.json > $O/${S}_bench.out 2> $O/${S}_bench.log
