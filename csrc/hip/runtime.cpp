@@ -1360,9 +1360,20 @@ constexpr int kPipeCreateCap = 8;  // creating a queue only for a better pipe st
 // profiles/r5/pipe_probe.txt).  That was the round-4 "bimodal 8mix" (slow
 // runs had the GEMMs' queue and a stream's 4 pool indexes apart).  So a
 // layout takes the queue whose pipe is least shared with the layouts running
-// now -- another class half's queue costs 10, same half 1 -- creating one
-// (its pipe: the creation count mod 4) when that is cheaper, under the budget.
+// now -- another class half's queue costs 10, same half 1.
+// The pipe is the index in the PROCESS's queue creation order, which also
+// counts the plain-stream queues HIP creates lazily and the profiler's: a
+// pool index mod 4 predicted nothing in a full bench process (s8: slow 8mix
+// runs had the GEMMs on pool queue 6 and the streams on 5, 7 or 8).  So the
+// pool creates all its queues in ONE burst at first use, nothing else
+// creating queues in between (prealloc, under the pool lock), in the plan
+// kPlan -- compute half on burst indexes 0, 4, 8 (one pipe), memory half on
+// the other three pipes -- and only the relative pipes within the burst are
+// used.  Round 4's preallocation (C M M C M) put a memory queue on the
+// compute pipe, which is why it measured no better.
 constexpr int kPipes = 4;
+constexpr int kPlanLen = kMaskedBudget;
+constexpr int kPlan[kPlanLen] = {0, 1, 1, 1, 0, 1, 1, 1, 0, 1};  // class half per burst index
 
 struct MaskedPoolCore {
   struct Ent {
@@ -1371,13 +1382,37 @@ struct MaskedPoolCore {
     hipStream_t s;
     uint32_t key;
     int refs;
-    int pipe;  // creation index mod kPipes
+    int pipe;  // creation index mod kPipes (in the device's burst)
   };
   std::mutex mu;
   std::vector<Ent> ents;
   uint64_t created = 0, cross_key_shares = 0, pipe_shared_other = 0;
   int held_max = 0;  // high-water mark of queues held at once (reset with reset_max)
   int dev_created[16] = {};
+  bool dev_burst[16] = {};
+
+  // Create the device's queues in one burst: plan[i] picks masks[plan[i]]
+  // for burst index i (pipe i mod kPipes).  Once per device; later creations
+  // (an exclusive acquire with no idle queue) continue the count.
+  template <class Create>
+  int prealloc(int dev, const uint32_t* const masks[2], const int* plan, int n, Create&& create) {
+    std::lock_guard<std::mutex> g(mu);
+    const int dv = dev >= 0 && dev < 16 ? dev : 0;
+    if (dev_burst[dv]) return 0;
+    dev_burst[dv] = true;
+    int made = 0;
+    for (auto& e : ents) made += e.device == dev;
+    if (made) return 0;  // queues exist already: their pipes are unknown, keep the incremental policy
+    for (int i = 0; i < n; ++i) {
+      hipStream_t s = create(masks[plan[i]]);
+      if (!s) return -1;
+      ents.push_back({dev, {}, s, 0, 0, i % kPipes});
+      std::memcpy(ents.back().m, masks[plan[i]], sizeof(ents.back().m));
+      created++;
+      dev_created[dv]++;
+    }
+    return n;
+  }
 
   int held_locked(int dev) const {
     int n = 0;
@@ -1461,13 +1496,20 @@ MaskedPoolCore& masked_pool() {
   static MaskedPoolCore* p = new MaskedPoolCore;  // never destroyed: streams outlive static teardown order
   return *p;
 }
+void half_mask(int h, uint32_t m[8]);
 hipStream_t masked_acquire_key(const uint32_t m[8], uint32_t key) {
   int dev = 0;
   hipGetDevice(&dev);
-  return masked_pool().acquire(dev, m, key, [](const uint32_t* mm) -> hipStream_t {
+  auto create = [](const uint32_t* mm) -> hipStream_t {
     hipStream_t s = nullptr;
     return hipExtStreamCreateWithCUMask(&s, 8, const_cast<uint32_t*>(mm)) == hipSuccess ? s : nullptr;
-  });
+  };
+  uint32_t mc[8], mm[8];
+  half_mask(0, mc);
+  half_mask(1, mm);
+  const uint32_t* masks[2] = {mc, mm};
+  masked_pool().prealloc(dev, masks, kPlan, kPlanLen, create);
+  return masked_pool().acquire(dev, m, key, create);
 }
 hipStream_t masked_acquire(const uint32_t m[8]) { return masked_acquire_key(m, 0); }
 void masked_release(const uint32_t*, hipStream_t s) { masked_pool().release(s); }
@@ -3038,6 +3080,22 @@ int gpbs_hip_masked_pool_selftest(void) {
   if (n2 == m4 || Q.pipe_of(n2) != 1 || Q.created != 6) return 12;
   (void)m2;
   (void)m3;
+  // 9. the burst: the plan's queues on consecutive pipes, compute alone on
+  //    pipe 0; a compute layout and three memory layouts never share a pipe
+  MaskedPoolCore R;
+  const uint32_t* masks[2] = {mc, mm};
+  if (R.prealloc(0, masks, kPlan, kPlanLen, mk) != kPlanLen || R.created != (uint64_t)kPlanLen) return 13;
+  if (R.prealloc(0, masks, kPlan, kPlanLen, mk) != 0) return 14;
+  hipStream_t rc = R.acquire(0, mc, 0x1, mk);
+  hipStream_t r1 = R.acquire(0, mm, 0x2, mk), r2 = R.acquire(0, mm, 0x4, mk), r3 = R.acquire(0, mm, 0x8, mk);
+  if (R.pipe_of(rc) != 0 || R.pipe_of(r1) == 0 || R.pipe_of(r2) == 0 || R.pipe_of(r3) == 0) return 15;
+  if (R.pipe_of(r1) == R.pipe_of(r2) || R.pipe_of(r2) == R.pipe_of(r3) || R.pipe_of(r1) == R.pipe_of(r3)) return 16;
+  // the 8mix static split (3 compute, 4 memory, the exclusive lane): no
+  // creation past the burst, no cross-key share, no memory queue on pipe 0
+  hipStream_t rc2 = R.acquire(0, mc, 0x10, mk), rc3 = R.acquire(0, mc, 0x20, mk);
+  hipStream_t r4 = R.acquire(0, mm, 0x40, mk), lane = R.acquire(0, mm, 0, mk);
+  if (R.created != (uint64_t)kPlanLen || R.cross_key_shares || R.pipe_shared_other) return 17;
+  if (R.pipe_of(rc2) != 0 || R.pipe_of(rc3) != 0 || R.pipe_of(r4) == 0 || R.pipe_of(lane) == 0) return 18;
   return 0;
 }
 

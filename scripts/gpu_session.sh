@@ -5,7 +5,8 @@
 set -o pipefail
 O=gpurun_out/r5
 mkdir -p $O
-S=${1:-s8}
-timeout -k 10 300 python -u bench.py --mix 4mix --reps 5 --policies static-se,gpbs,gpbs-model,gpbs-noalign \
-  --out $O/${S}_4mix_ab.json > $O/${S}_4mix_ab.out 2> $O/${S}_4mix_ab.log &&
-timeout -k 10 700 python -u bench.py --gpus 1 --steps 20 --warmup 5 --out $O/${S}_bench.json > $O/${S}_bench.out 2> $O/${S}_bench.log
+S=${1:-s10}
+timeout -k 10 420 python -u bench.py --mix 8mix --reps 5 --policies none,static-se,gpbs-split,credit-fixed-ts,credit-classq,gpbs \
+  --out $O/${S}_8mix.json > $O/${S}_8mix.out 2> $O/${S}_8mix.log &&
+timeout -k 10 300 python -u bench.py --mix phase-ts --reps 5 \
+  --out $O/${S}_phasets.json > $O/${S}_phasets.out 2> $O/${S}_phasets.log

@@ -8,6 +8,7 @@ or generated ones)."""
 import copy
 import json
 import os
+import socket
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -93,6 +94,71 @@ def test_oversized_line_raises():
     except ValueError:
         return
     raise AssertionError("no size check")
+
+
+R5_REHEARSAL = os.path.join(ROOT, "profiles", "r5", "s9_rehearse8_detail.json")
+R5_LINE = os.path.join(ROOT, "profiles", "r5", "s9_rehearse8_line.txt")
+
+
+def test_recorded_eight_rank_rehearsal_line():
+    """The round-5 8-rank --rehearse-ipc run on one MI355X (every rank on
+    cuda:0) printed its contract line under 4 KB with no rank failing."""
+    with open(R5_LINE) as f:
+        ln = [x for x in f if x.startswith("{")][-1]
+    assert len(ln.encode()) < MAX_LINE_BYTES
+    line = json.loads(ln)
+    assert line["n_gpus"] == 8 and line["ranks"] == {"n": 8, "coll": ["ipc"], "failures": []}
+
+
+def _gloo_rank(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    with open(R5_REHEARSAL) as f:
+        rec = json.load(f)
+    diag = copy.deepcopy(rec["line"]["ranks"][rank % len(rec["line"]["ranks"])])
+    diag["rank"] = rank
+    if rank == 6:  # one rank's counter agent sits on another device
+        diag["hwc_agent"]["bdf"] = "0000:01:00.0"
+    allr = [None] * world
+    dist.all_gather_object(allr, diag)  # bench.py's per-rank pre-flight gather
+    if rank == 0:
+        line = dict(rec["line"], ranks=allr)
+        digests = {m: mix_digest(_summary(r["runs"]), r["runs"]) for m, r in rec["results"].items()}
+        q.put(json.dumps(compact_line(line, digests, "gpurun_out/r5/s9_rehearse8.json")))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _summary(runs):
+    import bench
+    return bench.mix_summary("4mix", runs, {"gemm": {}}, 4)
+
+
+def test_gloo_eight_rank_rehearsal_compact_line():
+    """8 gloo ranks on the CPU gather their pre-flight records the way
+    bench.py does at N > 1 and rank 0 prints the compact line: under 4 KB,
+    with the one bad rank listed as a failure."""
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_gloo_rank, args=(r, 8, port, q)) for r in range(8)]
+    for p in ps:
+        p.start()
+    try:
+        out = q.get(timeout=240)
+    finally:
+        for p in ps:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    assert len(out.encode()) < MAX_LINE_BYTES
+    line = json.loads(out)
+    assert line["ranks"]["n"] == 8
+    assert [f["rank"] for f in line["ranks"]["failures"]] == [6]
+    assert line["mixes"]["4mix"]["gpbs"][0] > 0
 
 
 def test_bdf_mismatch_normalises():
