@@ -507,6 +507,14 @@ int gpbs_tenant_bound_stats(gpbs_engine_t* e, int t, uint64_t* out3, int reset) 
   return s ? s->bound_stats(*d, out3, reset != 0) : GPBS_EINVAL;
 }
 
+int gpbs_tenant_measure(gpbs_engine_t* e, int t, uint32_t us) {
+  LOCK(e);
+  Tenant* d = live(e, t);
+  if (!d) return GPBS_ENOENT;
+  if (us != UINT32_MAX) d->measure_us = us;
+  return (int)std::min<uint64_t>(d->measure_granted, INT32_MAX);
+}
+
 int gpbs_tenant_heartbeat(gpbs_engine_t* e, int t) {
   LOCK(e);
   Tenant* d = live(e, t);

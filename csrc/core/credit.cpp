@@ -1305,6 +1305,18 @@ class CreditScheduler : public Scheduler {
     } else {
       tslice = (int64_t)tslice_us_ * 1000;
     }
+    // Measurement tenure (hardware counters): the first tenure that starts
+    // after the sampler's request runs at least the requested length, once.
+    // Credit still charges every microsecond of it, so the tenant's share
+    // is unchanged over a few accounting periods.
+    if (snext != &scurr && !snext->is_idle() && !held) {
+      Tenant& tn = *E.tenants[snext->tenant];
+      if (tn.measure_us) {
+        tslice = std::max<int64_t>(tslice, (int64_t)tn.measure_us * 1000);
+        tn.measure_us = 0;
+        tn.measure_granted++;
+      }
+    }
     // A parked partition re-checks at least every 200 us (the request may
     // lose BOOST while still running, which kicks nobody).
     ret.time_ns = parked ? 200000 : (snext->is_idle() ? -1 : tslice);

@@ -102,6 +102,12 @@ struct Tenant {  // struct domain
   int gang_state = 0;
   int64_t gang_until = 0;
   int gang(int64_t now) const { return now < gang_until ? gang_state : 0; }
+  // Measurement tenure: the hardware-counter sampler asks that the tenant's
+  // next tenure on some partition last at least measure_us, so a clean
+  // counter window fits in it (a 1 ms quantum minus the drain guard and the
+  // closing sample leaves none); granted = tenures so extended.
+  uint32_t measure_us = 0;
+  uint64_t measure_granted = 0;
   // Watchdogs (SCHEDOP_watchdog): timer ids, in-use bits, shutdown reason.
   int wd_timer[GPBS_WATCHDOGS] = {-1, -1};
   uint32_t wd_inuse = 0;

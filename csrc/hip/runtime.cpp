@@ -367,6 +367,17 @@ struct GpuCtx {
   int64_t t_inflight = 0;                          // sample time of the in-flight attribution
   double cal[kMaxTenants][kNumPmc] = {};           // hardware / model per counter (0: not calibrated)
   int64_t last_clean_ns[kMaxTenants] = {};
+  // Measurement tenures: a tenant that ran without a clean window for
+  // hwc_measure_ms asks the engine (gpbs_tenant_measure) for one tenure of
+  // long_us + the drain guard + two sample times on some partition -- the
+  // switch-aligned long window then covers it.  Tenants on 1 ms quanta
+  // (compute-bound, at min_us) otherwise get clean windows only from the
+  // budgeted short pairs, which the host table's 550 us guard mostly leaves
+  // as slivers (s10 8mix: GEMM tenants clean in 0.16-0.39 of their periods).
+  int hwc_measure_ms = 40;
+  int64_t last_ran_ns[kMaxTenants] = {};   // last interval the tenant ran in (snap_mu)
+  int64_t measure_req_ns[kMaxTenants] = {};
+  uint64_t measure_reqs = 0;
   uint64_t fallback_periods = 0, clean_periods = 0, skipped_periods = 0, sliver_periods = 0;
   uint64_t t_clean[kMaxTenants] = {}, t_fallback[kMaxTenants] = {}, t_skipped[kMaxTenants] = {},
            t_sliver[kMaxTenants] = {};
@@ -885,6 +896,24 @@ void hwc_loop(GpuCtx* c) {
             open |= 1u << p;
       }
     }
+    // 3b. measurement tenures for tenants with no clean window lately (no
+    //     lock of ours held: the engine call takes the engine lock, whose
+    //     holders take c->mu)
+    if (on_tick && c->hwc_align && c->hwc_measure_ms > 0 && c->engine && !c->muxed) {
+      const int64_t ms = (int64_t)c->hwc_measure_ms * 1000000;
+      int64_t ran[kMaxTenants], cln[kMaxTenants];
+      {
+        std::lock_guard<std::mutex> g(c->snap_mu);
+        std::memcpy(ran, c->last_ran_ns, sizeof(ran));
+        std::memcpy(cln, c->last_clean_ns, sizeof(cln));
+      }
+      const uint32_t want = (uint32_t)(c->hwc_long_us + guard_ns(c) / 1000 + 2 * (int64_t)(c->hwc_dt_ewma / 1000) + 300);
+      for (int t = 0; t < kMaxTenants; ++t)
+        if (ran[t] && t0 - ran[t] < ms && t0 - cln[t] > ms && t0 - c->measure_req_ns[t] > ms) {
+          c->measure_req_ns[t] = t0;
+          if (gpbs_tenant_measure(c->engine, t, want) >= 0) c->measure_reqs++;
+        }
+    }
     // 4. sleep until the next tick, a pending switch sample, or a new publish
     std::unique_lock<std::mutex> lk(c->mu);
     c->cv.wait_until(lk, std::chrono::steady_clock::time_point(std::chrono::nanoseconds(wake_at)), [&] {
@@ -911,6 +940,7 @@ void hwc_fold(GpuCtx* c, const HwcAttrOut& o, const double (*mod)[kNumPmc], cons
     for (int k = 0; k < kNumPmc; ++k)
       if (o.add[t][k] > 0) c->att_total[t][k] += o.add[t][k];
     if (o.add[t][0] <= 0) continue;  // did not run in the interval
+    c->last_ran_ns[t] = t_s;
     const bool clean = c->clean_pct <= 0 || o.addc[t][0] > 0;
     double m[kNumPmc] = {0, 0, 0, 0};
     if (clean) {
@@ -2654,7 +2684,7 @@ int gpbs_gpu_param(void* p, const char* name, int value) {
       {"fallback", &c->model_fallback, 0, 1},           {"stale_us", &c->hwc_stale_us, 0, 100000000},
       {"watch", &c->hwc_watch, 0, 1},                   {"align", &c->hwc_align, 0, 1},
       {"guard_us", &c->hwc_guard_us, 0, 100000},        {"long_us", &c->hwc_long_us, 0, 100000000},
-      {"pair_gap_us", &c->hwc_pair_gap_us, 0, 10000000},
+      {"pair_gap_us", &c->hwc_pair_gap_us, 0, 10000000}, {"measure_ms", &c->hwc_measure_ms, 0, 100000},
       {"share", &c->share_enable, 0, 1},                {"probe_every", &c->probe_every, 0, 1000000},
       {"probe_len", &c->probe_len, 0, 1000000},
   };
@@ -2692,6 +2722,7 @@ int gpbs_gpu_hwc_reset(void* p) {
   std::memset(c->met_total, 0, sizeof(c->met_total));
   c->share_base = c->snap_share;
   c->hwc_ns = c->hwc_ns_max = 0;
+  c->measure_reqs = 0;
   c->hwc_samples = 0;
   c->hwc_slow_samples = 0;
   c->hwc_period_sum_ns = 0;
@@ -2733,6 +2764,14 @@ int gpbs_gpu_hwc_sampler(void* p, int budget_pct, int align, int fallback) {
 // switch samples denied by the budget, mean sample gap over intervals with a
 // switch (ns, the time-shared cadence), clean-window tenant periods, skipped
 // ones.
+// Measurement-tenure requests the sampler made since the last hwc reset.
+uint64_t gpbs_gpu_hwc_measure_reqs(void* p) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c) return 0;
+  std::lock_guard<std::mutex> g(c->snap_mu);
+  return c->measure_reqs;
+}
+
 int gpbs_gpu_hwc_align(void* p, int guard_us, int long_us, int stale_us, uint64_t* out8) {
   GpuCtx* c = (GpuCtx*)p;
   if (!c) return -22;

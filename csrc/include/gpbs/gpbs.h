@@ -278,6 +278,10 @@ int gpbs_tenant_class(gpbs_engine_t* e, int tenant); /* contention class: 0 comp
 /* Metric periods with a measurement / with the quantum at min_us / at max_us
  * (credit modes); reset != 0 clears them after the read. */
 int gpbs_tenant_bound_stats(gpbs_engine_t* e, int tenant, uint64_t* out3, int reset);
+/* Measurement tenure: the tenant's next tenure (on any partition) lasts at
+ * least `us` (0 cancels, UINT32_MAX only reads); returns the tenures so
+ * extended so far, or <0. */
+int gpbs_tenant_measure(gpbs_engine_t* e, int tenant, uint32_t us);
 /* Cumulative INST, CYCLES, LLC refs, LLC misses the scheduler measured and
  * attributed to the tenant (sum over metric periods; the vPMU mirror). */
 int gpbs_tenant_vpmu(gpbs_engine_t* e, int tenant, uint64_t* total4);

@@ -279,6 +279,7 @@ def _bind_ipc(lib):
     P(lib, "gpbs_gang_set", C.c_int, C.c_void_p, C.c_int, C.c_int, i64)
     P(lib, "gpbs_tenant_class", C.c_int, C.c_void_p, C.c_int)
     P(lib, "gpbs_tenant_bound_stats", C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_uint64), C.c_int)
+    P(lib, "gpbs_tenant_measure", C.c_int, C.c_void_p, C.c_int, C.c_uint32)
     P(lib, "gpbs_tenant_vpmu", C.c_int, C.c_void_p, C.c_int, C.POINTER(u64))
     P(lib, "gpbs_fault_set", C.c_int, C.c_void_p, C.c_char_p)
     P(lib, "gpbs_fault_hits", C.c_int, C.c_void_p, C.POINTER(u64), C.c_int)

@@ -1187,6 +1187,7 @@ class Corun:
             eng["mean_tslice_us"] = {n: round(statistics.mean(q), 1) for n, q in quanta.items() if q}
             # measured metric periods and, of those, at the quantum bounds
             eng["at_bound"] = {n: e.bound_stats(self.tid[n]) for n in self.throughput}
+            eng["measure_tenures"] = {n: e.measure(self.tid[n]) for n in self.throughput}
             eng["run_share"] = {n: round((e.tenant_info(self.tid[n]).run_ns - run0[n]) / (wall_ms * 1e6), 3)
                                 for n in self.tid}
             eng["phase"] = {n: e.tenant_info(self.tid[n]).phase for n in self.tid}

@@ -103,7 +103,12 @@ def _tenant(kind: str, seconds: float, warmup: float, socket: Optional[str], q, 
             # the daemon's probe phase sometimes starts from), then this half
             other = tuple(sorted({0, 1, 2, 3} - set(ses)))
             swap_stream = torch.cuda.ExternalStream(K.cumask_stream(se_cu_words(other)))
+        # +shiftN: N idle masked queues created first (kept), so the tenant's
+        # own queue lands N places later in the hardware scheduler's queue
+        # order (a probe of cross-process pipe coupling)
+        pads = [K.cumask_stream(se_cu_words(ses)) for _ in range(args.get(f"{kind}_shift", 0))]
         prio_stream = torch.cuda.ExternalStream(K.cumask_stream(se_cu_words(ses)))
+        args["_pads"] = pads
     torch.cuda.synchronize()
     start_evt.wait()
     lat = []
@@ -196,7 +201,8 @@ def run(policy: str, kinds, args: dict, seconds: float, warmup: float) -> Dict[s
     # +nohwc (daemon on modeled counters), +swapN (static split: the first N s
     # on the swapped halves), +one (one masked queue per shim tenant), +qpK
     # (K masked queues per half, chosen by measured slice time), +nox (no
-    # cross-class steals by idle partitions)
+    # cross-class steals by idle partitions), +ishiftN / +tshiftN (static
+    # split: N idle masked queues created before the decode / trainer queue)
     policy, *mods = policy.split("+")
     policy = ALIASES.get(policy, policy)
     base = policy.split("@")[0]
@@ -219,6 +225,10 @@ def run(policy: str, kinds, args: dict, seconds: float, warmup: float) -> Dict[s
             args["class_steal"] = 0
         elif m.startswith("swap"):
             args["swap_s"] = float(m[4:])
+        elif m.startswith("ishift"):  # static split: the decode tenant's queue N places later
+            args["infer_shift"] = int(m[6:])
+        elif m.startswith("tshift"):  # ... the trainer's
+            args["train_shift"] = int(m[6:])
         else:
             raise ValueError(f"unknown policy variant +{m}")
     if policy in ("gpbs", "gpbs-spatial"):

@@ -467,6 +467,11 @@ class Engine:
             return {"periods": 0, "at_min": 0, "at_max": 0}
         return {"periods": int(o[0]), "at_min": int(o[1]), "at_max": int(o[2])}
 
+    def measure(self, t: int, us: int = -1) -> int:
+        """Ask for a measurement tenure of at least `us` for the tenant's next
+        tenure (0 cancels; -1 only reads).  Returns the tenures extended so far."""
+        return int(self.lib.gpbs_tenant_measure(self.h, t, 0xFFFFFFFF if us < 0 else int(us)))
+
     def perfc_prometheus(self, prefix: str = "gpbs") -> str:
         """perfc counters in the Prometheus text exposition format."""
         lines = [f"# TYPE {prefix}_perfc_total counter"]

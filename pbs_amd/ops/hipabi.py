@@ -106,6 +106,7 @@ def bind(lib):
     _p(lib, "gpbs_gpu_hwc_sampler", C.c_int, vp, C.c_int, C.c_int, C.c_int)
     _p(lib, "gpbs_gpu_param", C.c_int, vp, C.c_char_p, C.c_int)
     _p(lib, "gpbs_gpu_hwc_attr_timing", C.c_int, vp, C.POINTER(u64))
+    _p(lib, "gpbs_gpu_hwc_measure_reqs", C.c_uint64, vp)
     _p(lib, "gpbs_gpu_hwc_align", C.c_int, vp, C.c_int, C.c_int, C.c_int, C.POINTER(u64))
     _p(lib, "gpbs_gpu_hwc_tenant_periods", C.c_int, vp, C.c_int, C.POINTER(u64), C.POINTER(C.c_double))
     _p(lib, "gpbs_runner_queue", C.c_int, vp)

@@ -194,6 +194,7 @@ class GpuContext:
                 "clean_periods": bud[3], "skipped_periods": al[7], "metric_periods": bud[2] + bud[3],
                 "align": bool(align), "align_samples": al[0], "align_close": al[1], "align_long": al[2],
                 "align_short": al[3], "align_denied": al[4], "ts_period_us": round(al[5] / 1e3, 1),
+                "measure_requests": int(self.L.gpbs_gpu_hwc_measure_reqs(self.h)),
                 "attr_device": bool(dev), "attr_kernel_launches": la.value, "attr_busy_skips": bs.value,
                 "attr_host": ho.value, "attr_harvested": at[0], "attr_kernel_us_mean": round(at[1] / 1e3, 2),
                 "attr_kernel_us_max": round(at[2] / 1e3, 2), "attr_harvest_lag_us": round(at[3] / 1e3, 1),

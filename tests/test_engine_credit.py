@@ -592,3 +592,28 @@ def test_runtime_section_of_gpbs_toml(tmp_path):
     with pytest.raises(ValueError):
         cfgmod.load(str(p))
     assert cfgmod.load(None)["runtime"] == {}
+
+
+def test_measurement_tenure_extends_one_tenure_once():
+    """The counter sampler's measurement tenure (gpbs_tenant_measure): the
+    next tenure of the tenant that starts after the request runs at least the
+    requested length -- once -- and later tenures return to its quantum."""
+    from pbs_amd.core.config import MI355X_PROFILE
+    prof = dict(MI355X_PROFILE)
+    prof["sched"] = "credit"
+    e = Engine(sim_clock=True, partitions=[(0, 0)], **prof)
+    a = e.tenant_create("mem", nslots=1)
+    b = e.tenant_create("cmp", nslots=1)
+    e.wake(a)
+    e.wake(b)
+    _feed_classes(e, a, b, 30)
+    assert e.tenant_info(b).tslice_us == 1000
+    e.trace(from_start=True)  # move the cursor past the history
+    assert e.measure(b) == 0
+    assert e.measure(b, 4500) == 0
+    _feed_classes(e, a, b, 40, k0=31)
+    sw = [r for r in e.trace() if r.event == "SWITCH" and r.a[1] == b]
+    assert sw, "no tenure of the tenant"
+    assert sw[0].a[2] >= 4500  # the first tenure after the request
+    assert all(r.a[2] < 4500 for r in sw[1:])
+    assert e.measure(b) == 1
