@@ -55,8 +55,8 @@ MI355X_PROFILE: Dict[str, Any] = dict(
 # the runtime's built-in defaults; a key set here is applied to every
 # GpuContext the process creates.
 RUNTIME_KEYS = ("period_us", "slow_us", "duty_pct", "burst_ms", "budget_pct", "bucket", "clean_pct", "device_attr",
-                "fallback", "stale_us", "watch", "align", "guard_us", "long_us", "pair_gap_us", "share", "probe_every",
-                "probe_len")
+                "fallback", "stale_us", "watch", "align", "guard_us", "long_us", "pair_gap_us", "measure_ms", "share",
+                "probe_every", "probe_len")
 
 BOOT_KEYS = ("sched", "tslice_us", "ratelimit_us", "smt_power_savings", "tickle_one_idle", "default_yield",
              "migration_delay_us", "metric_period_us", "slice_apply_us", "pmu_refresh_us", "dom0_quirk",

@@ -63,7 +63,8 @@ def main():
         names = {4: "staggered-groups", 256 | 4096: "2phase-balanced", 256 | 8192: "2phase-own-a", 256 | 16384: "1phase",
                  256 | 8192 | 32768: "2phase-own-a-mfma32",
                  256 | 8192 | 65536: "2phase-own-a-lds-c",
-                 256 | 8192 | 65536 | 131072: "2phase-own-a-lds-c-nt"}
+                 256 | 8192 | 65536 | 131072: "2phase-own-a-lds-c-nt",
+                 256 | 8192 | 65536 | 131072 | 8: "2phase-own-a-lds-c-nt-2d-blocks"}
     ab = {k: [] for k in names}
     for _ in range(5):
         for opt in names:
