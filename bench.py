@@ -164,6 +164,9 @@ def main():
                          "llm5: config #5 (Llama-3-8B fp8 decode + Llama-1B-shaped bf16 trainer, torch tenants "
                          "on the shim under gpbsd; not in the default run)")
     ap.add_argument("--reps-extra", type=int, default=5, help="reps of the non-headline mixes")
+    ap.add_argument("--kernel-trace", action="store_true",
+                    help="per-run kernel dispatch statistics from this process's own rocprofiler-sdk context "
+                         "(the live counters stay on; rocprofv3 would take the SDK from them) -> --out")
     ap.add_argument("--hang-dump-s", type=float, default=0.0,
                     help="diagnostics: dump every thread's stack every this many seconds (0: off)")
     ap.add_argument("--llm5-warm-s", type=float, default=5.0, help="--mix llm5: untimed warm-up seconds")
@@ -204,6 +207,8 @@ def main():
     counters = args.counters
     if counters == "hw":  # must register with rocprofiler before the HIP runtime starts
         from pbs_amd.counters import hwc
+        if args.kernel_trace:
+            hwc.trace_enable(True)
         if not hwc.init(gpu=local):
             print("bench.py: hardware counter init failed; falling back to modeled counters", file=sys.stderr)
             counters = "model"
@@ -280,7 +285,7 @@ def main():
                           protocol=args.protocol, step_ms=args.step_ms, gang_transport=args.gang_transport,
                           gang_shm_base=f"{gang_base}-{mix}" if gang_base else "",
                           gang_wait_driven=args.gang_wait_driven, fresh_engine=not args.keep_engines,
-                          coll_impl=args.coll)
+                          coll_impl=args.coll, kernel_trace=args.kernel_trace and counters == "hw")
         if args.rehearse:
             cfg.coll_bytes = 4 << 20  # CPU gloo all-reduce stand-in
         c = Corun(cfg, rank=rank, world=world, device=local, groups=groups, log=log,
@@ -441,6 +446,8 @@ def run_llm5(args):
     warm = max(args.llm5_warm_s, args.warmup * args.step_ms / 1e3)
     out = os.path.join(tempfile.mkdtemp(), "llm5.json")
     pols = args.policies or "solo,none,static-se,gpbs-budget"
+    if "solo" not in pols.split(","):  # every share is over the solo rates
+        pols = "solo," + pols
     with contextlib.redirect_stdout(sys.stderr):  # rank 0 prints ONE line: ours
         llm_corun.main(["--fp8", "--graph", "--seconds", str(secs), "--warmup", str(warm), "--reps", str(args.reps),
                         "--policies", pols, "--out", out])

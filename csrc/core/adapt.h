@@ -31,7 +31,9 @@ struct AdaptParams {
   // (struct event_sample, :176-181).  strict_ref=1 reproduces that (Q7);
   // strict_ref=0 keeps full 64-bit samples (GPU counter rates overflow u32).
   uint32_t strict_ref = 0;
-  uint32_t reserved = 0;
+  // gpbs extension (0 = the reference's additive steps): proportional growth
+  // of the stable branch, grow_pct % per step (adapt_impl.h inc)
+  uint32_t grow_pct = 0;
 };
 
 struct FilterEntry {

@@ -27,8 +27,21 @@ GPBS_HD uint32_t dec(uint32_t t, const P& p) {
   return t >= p.min_us + p.dec_us ? t - p.dec_us : p.min_us;
 }
 
+// grow_pct > 0 (MI355X profile): proportional growth, at least inc_us -- a
+// 1 -> 11 ms climb in 4 stable steps instead of 10, because on time-shared
+// GPU partitions a tenant's metric updates arrive once per clean counter
+// window (5-10 ms), not every 1 ms tick, and a phase lasts a few hundred ms.
+// (Growing while the window refills too was tried: it put the gang-switched
+// memory region out of step for good -- tests/test_se_mode.py, 0.5 aligned.)
 template <class P>
-GPBS_HD uint32_t inc(uint32_t t, const P& p) { return t + p.inc_us >= p.max_us ? p.max_us : t + p.inc_us; }
+GPBS_HD uint32_t inc(uint32_t t, const P& p) {
+  uint32_t n = t + p.inc_us;
+  if (p.grow_pct) {
+    const uint64_t m = (uint64_t)t * (100 + p.grow_pct) / 100;
+    if (m > n) n = m > p.max_us ? p.max_us : (uint32_t)m;
+  }
+  return n >= p.max_us ? p.max_us : n;
+}
 
 template <class E, class P>
 GPBS_HD void put(E& e, const P& p, uint64_t spin, uint64_t inst, uint64_t miss) {

@@ -16,9 +16,12 @@
 // after the first device call.
 #include <hip/hip_runtime.h>
 #include <rocprofiler-sdk/buffer.h>
+#include <rocprofiler-sdk/buffer_tracing.h>
+#include <rocprofiler-sdk/callback_tracing.h>
 #include <rocprofiler-sdk/registration.h>
 #include <rocprofiler-sdk/rocprofiler.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -67,6 +70,68 @@ struct Hwc {
   std::vector<rocprofiler_counter_record_t> rec;
 };
 Hwc g;
+
+// In-process kernel trace: the rocprofv3 --kernel-trace --stats analog that
+// runs WITH the live counters (under rocprofv3 its own tool holds the SDK,
+// force_configure fails and the scheduler falls back to modeled counters, so
+// a rocprofv3 trace can never show the hardware-counter path in situ).  A
+// second context of this tool: code-object callbacks name the kernels,
+// buffered kernel-dispatch records give each dispatch's GPU start / end.
+struct KStat {
+  uint64_t calls = 0, total_ns = 0, max_ns = 0;
+};
+struct Trace {
+  bool want = false, on = false;
+  rocprofiler_context_id_t ctx{};
+  rocprofiler_buffer_id_t buf{};
+  std::mutex mu;
+  std::map<uint64_t, std::string> name;  // kernel id -> symbol
+  std::map<uint64_t, KStat> stat;        // kernel id -> durations
+  uint64_t first_ns = UINT64_MAX, last_ns = 0, dispatches = 0, dropped = 0;
+};
+Trace tr;
+
+void on_code_object(rocprofiler_callback_tracing_record_t rec, rocprofiler_user_data_t*, void*) {
+  if (rec.kind != ROCPROFILER_CALLBACK_TRACING_CODE_OBJECT ||
+      rec.operation != ROCPROFILER_CODE_OBJECT_DEVICE_KERNEL_SYMBOL_REGISTER || rec.phase != ROCPROFILER_CALLBACK_PHASE_LOAD)
+    return;
+  auto* d = static_cast<rocprofiler_callback_tracing_code_object_kernel_symbol_register_data_t*>(rec.payload);
+  std::lock_guard<std::mutex> l(tr.mu);
+  tr.name[d->kernel_id] = d->kernel_name ? d->kernel_name : "?";
+}
+
+void on_trace_buffer(rocprofiler_context_id_t, rocprofiler_buffer_id_t, rocprofiler_record_header_t** h, size_t n,
+                     void*, uint64_t drop) {
+  std::lock_guard<std::mutex> l(tr.mu);
+  tr.dropped += drop;
+  for (size_t i = 0; i < n; ++i) {
+    if (h[i]->category != ROCPROFILER_BUFFER_CATEGORY_TRACING || h[i]->kind != ROCPROFILER_BUFFER_TRACING_KERNEL_DISPATCH)
+      continue;
+    auto* r = static_cast<const rocprofiler_buffer_tracing_kernel_dispatch_record_t*>(h[i]->payload);
+    const uint64_t d = r->end_timestamp > r->start_timestamp ? r->end_timestamp - r->start_timestamp : 0;
+    KStat& s = tr.stat[r->dispatch_info.kernel_id];
+    s.calls++;
+    s.total_ns += d;
+    s.max_ns = std::max(s.max_ns, d);
+    tr.first_ns = std::min<uint64_t>(tr.first_ns, r->start_timestamp);
+    tr.last_ns = std::max<uint64_t>(tr.last_ns, r->end_timestamp);
+    tr.dispatches++;
+  }
+}
+
+void trace_setup() {
+  if (rocprofiler_create_context(&tr.ctx) != ROCPROFILER_STATUS_SUCCESS) return;
+  if (rocprofiler_configure_callback_tracing_service(tr.ctx, ROCPROFILER_CALLBACK_TRACING_CODE_OBJECT, nullptr, 0,
+                                                     on_code_object, nullptr) != ROCPROFILER_STATUS_SUCCESS)
+    return;
+  if (rocprofiler_create_buffer(tr.ctx, 1u << 22, 1u << 21, ROCPROFILER_BUFFER_POLICY_LOSSLESS, on_trace_buffer,
+                                nullptr, &tr.buf) != ROCPROFILER_STATUS_SUCCESS)
+    return;
+  if (rocprofiler_configure_buffer_tracing_service(tr.ctx, ROCPROFILER_BUFFER_TRACING_KERNEL_DISPATCH, nullptr, 0,
+                                                   tr.buf) != ROCPROFILER_STATUS_SUCCESS)
+    return;
+  tr.on = rocprofiler_start_context(tr.ctx) == ROCPROFILER_STATUS_SUCCESS;
+}
 
 // Fold one counter record into an accumulator (either path).
 void fold_record(const rocprofiler_counter_record_t& r, double se_acc[kX][kSe][kSlots], double x_acc[kX][kSlots]) {
@@ -164,6 +229,7 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
     g.ok[i] = 1;
     g.configured = true;
   }
+  if (tr.want) trace_setup();  // before any code object loads
   return 0;
 }
 
@@ -273,6 +339,46 @@ int gpbs_hwc_agent(char* bdf_out, int n, int* index_mismatch) {
 }
 
 int gpbs_hwc_active(void) { return g.started ? 1 : 0; }
+
+// Kernel trace (see Trace): enable before gpbs_hwc_init; 1 if it will run.
+int gpbs_hwc_trace_enable(int on) {
+  tr.want = on != 0;
+  return tr.want ? 1 : 0;
+}
+
+// Per-kernel dispatch statistics since the last reset, as JSON into out[cap]:
+// {"dispatches", "dropped", "span_ns", "kernels": [[name, calls, total_ns,
+// max_ns], ...] by total time}.  Flushes the trace buffer first.  Returns the
+// length written, -needed if cap is too small, -1 if the trace is not running.
+int gpbs_hwc_trace_stats(char* out, int cap, int reset) {
+  if (!tr.on) return -1;
+  rocprofiler_flush_buffer(tr.buf);
+  std::lock_guard<std::mutex> l(tr.mu);
+  std::vector<std::pair<uint64_t, KStat>> v(tr.stat.begin(), tr.stat.end());
+  std::sort(v.begin(), v.end(), [](const auto& a, const auto& b) { return a.second.total_ns > b.second.total_ns; });
+  std::string s = "{\"dispatches\": " + std::to_string(tr.dispatches) + ", \"dropped\": " + std::to_string(tr.dropped) +
+                  ", \"span_ns\": " + std::to_string(tr.last_ns > tr.first_ns ? tr.last_ns - tr.first_ns : 0) +
+                  ", \"kernels\": [";
+  for (size_t i = 0; i < v.size(); ++i) {
+    auto it = tr.name.find(v[i].first);
+    std::string nm = it != tr.name.end() ? it->second : "kernel_" + std::to_string(v[i].first);
+    std::string esc;
+    for (char ch : nm)
+      if (ch == '"' || ch == '\\') esc += '\\', esc += ch;
+      else if ((unsigned char)ch >= 0x20) esc += ch;
+    s += (i ? ", [\"" : "[\"") + esc + "\", " + std::to_string(v[i].second.calls) + ", " +
+         std::to_string(v[i].second.total_ns) + ", " + std::to_string(v[i].second.max_ns) + "]";
+  }
+  s += "]}";
+  if ((int)s.size() + 1 > cap) return -(int)(s.size() + 1);
+  std::memcpy(out, s.c_str(), s.size() + 1);
+  if (reset) {
+    tr.stat.clear();
+    tr.first_ns = UINT64_MAX;
+    tr.last_ns = tr.dispatches = tr.dropped = 0;
+  }
+  return (int)s.size();
+}
 
 // Cumulative counters per XCD: out[xcd * 4 + slot].  Synchronous sample.
 int gpbs_hwc_sample(uint64_t* out, int nxcd) {

@@ -63,7 +63,7 @@ __global__ __launch_bounds__(64) void k_counter_reduce(u64* cnt, u64* prev, cons
 
 struct DevParams {
   u32 threshold, band_lo, band_hi, min_us, max_us, inc_us, dec_us, switch_boundary, ticks_per_tslice, spin_floor,
-      scale, strict_ref, reserved;
+      scale, strict_ref, grow_pct;
 };
 
 __global__ __launch_bounds__(64) void k_adapt(gpbs_adapt_state_t* states, const u64* deltas, const u64* spin_sum,

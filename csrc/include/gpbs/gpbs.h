@@ -41,7 +41,8 @@ extern "C" {
 
 typedef struct gpbs_adapt_params {
   uint32_t threshold, band_lo, band_hi, min_us, max_us, inc_us, dec_us, switch_boundary;
-  uint32_t ticks_per_tslice, spin_floor, scale, strict_ref, reserved;
+  uint32_t ticks_per_tslice, spin_floor, scale, strict_ref;
+  uint32_t grow_pct; /* 0: the reference's additive steps; >0: proportional growth (adapt_impl.h) */
 } gpbs_adapt_params_t;
 
 typedef struct gpbs_atc_params {

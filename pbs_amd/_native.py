@@ -18,7 +18,7 @@ u32, i32, u64, i64 = C.c_uint32, C.c_int32, C.c_uint64, C.c_int64
 class AdaptParams(C.Structure):
     _fields_ = [(n, u32) for n in ("threshold", "band_lo", "band_hi", "min_us", "max_us", "inc_us", "dec_us",
                                    "switch_boundary", "ticks_per_tslice", "spin_floor", "scale", "strict_ref",
-                                   "reserved")]
+                                   "grow_pct")]
 
 
 class AtcParams(C.Structure):

@@ -165,6 +165,7 @@ class CorunConfig:
     onoff_ms: float = 500.0      # mix "phase": the hbm tenant runs / stops for this long, alternately
     solo_steps: int = 0          # solo calibration windows (0: the co-run's K); warmup = the co-run's W
     mem_chunk: int = 0           # memory tenants' chunk bytes (0: the runner default, 512 KiB)
+    kernel_trace: bool = False   # per-run in-process kernel trace (counters/hwc.py trace_stats)
 
 
 # SE-exclusive flagship (the four partitions of an XCD are its shader engines,
@@ -1011,6 +1012,9 @@ class Corun:
         layout = {n: [] for n in self.throughput}  # budget SE sets per step (bit c = SE c)
         self._rs0 = {n: r.stats() for n, r in self.runners.items() if isinstance(r, Runner)}
         self.ctx.masked_pool_reset()
+        if self.cfg.kernel_trace:
+            from ..counters import hwc as _hwc
+            _hwc.trace_stats(reset=True)
         self._barrier()
         t0 = time.perf_counter()
         g0 = time.monotonic()
@@ -1068,6 +1072,11 @@ class Corun:
         res["masked_queues"] = {"held_max": gs["masked_queues_held_max"], "created": gs["masked_queues_created"],
                                 "cross_key_shares": gs["masked_cross_key_shares"],
                                 "pipe_shared_other": gs["masked_pipe_shared_other"]}
+        if self.cfg.kernel_trace:  # in-process kernel trace of the run (live counters on)
+            from ..counters import hwc as _hwc
+            ks = _hwc.trace_stats(reset=True)
+            if ks:
+                res["kernel_trace"] = ks
         res["host"] = {k: round(h1[k] - h0[k], 3) for k in h1 if k in h0}
         if "cpu_s" in res["host"]:
             res["host"]["cpu_util"] = round(res["host"]["cpu_s"] / (wall_ms_local / 1e3), 2)  # cores busy

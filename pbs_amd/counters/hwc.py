@@ -66,6 +66,31 @@ def init(spec: Optional[str] = None, gpu: int = -1) -> bool:
     return _lib().gpbs_hwc_init_gpu(spec.encode(), int(gpu)) == 0
 
 
+def trace_enable(on: bool = True) -> bool:
+    """In-process kernel trace (rocprofiler-sdk kernel-dispatch records in
+    this tool's own context, so it runs WITH the live counters -- rocprofv3
+    cannot: its tool takes the SDK and the scheduler falls back to modeled
+    counters).  Call before init()."""
+    return bool(_lib().gpbs_hwc_trace_enable(1 if on else 0))
+
+
+def trace_stats(reset: bool = False) -> Optional[dict]:
+    """Per-kernel GPU time since the last reset: {"dispatches", "dropped",
+    "span_ns", "kernels": [[name, calls, total_ns, max_ns], ...]} by total
+    time; None if the trace is not running."""
+    import json
+    cap = 1 << 16
+    for _ in range(4):
+        buf = C.create_string_buffer(cap)
+        n = _lib().gpbs_hwc_trace_stats(buf, cap, 1 if reset else 0)
+        if n == -1:
+            return None
+        if n >= 0:
+            return json.loads(buf.value.decode())
+        cap = -n + 1024
+    return None
+
+
 def start() -> bool:
     """Start counting on the current HIP device's agent.  False if the
     service is not configured; raises if the configured agent (LOCAL_RANK)

@@ -54,6 +54,8 @@ def bind(lib):
     _p(lib, "gpbs_hwc_init_gpu", C.c_int, C.c_char_p, C.c_int)
     _p(lib, "gpbs_hwc_start", C.c_int)
     _p(lib, "gpbs_hwc_active", C.c_int)
+    _p(lib, "gpbs_hwc_trace_enable", C.c_int, C.c_int)
+    _p(lib, "gpbs_hwc_trace_stats", C.c_int, C.c_char_p, C.c_int, C.c_int)
     _p(lib, "gpbs_hwc_sample", C.c_int, C.POINTER(C.c_uint64), C.c_int)
     _p(lib, "gpbs_hwc_stop", C.c_int)
     _p(lib, "gpbs_gpu_set_hwc", C.c_int, vp, C.c_int)

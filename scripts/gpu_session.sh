@@ -5,10 +5,9 @@
 set -o pipefail
 O=gpurun_out/r5
 mkdir -p $O
-S=${1:-s11}
-timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_gpu_se_hwc.py tests/test_gpu_phase.py \
-  > $O/${S}_gputest.log 2>&1 &&
-timeout -k 10 420 python -u bench.py --mix 8mix --reps 5 --policies static-se,credit-fixed-ts,credit-classq,gpbs \
-  --out $O/${S}_8mix.json > $O/${S}_8mix.out 2> $O/${S}_8mix.log &&
-timeout -k 10 300 python -u bench.py --mix 4mix --reps 5 --policies static-se,credit-fixed,gpbs \
-  --out $O/${S}_4mix.json > $O/${S}_4mix.out 2> $O/${S}_4mix.log
+S=${1:-s12}
+timeout -k 10 300 python -u bench.py --mix phase-ts --reps 5 \
+  --out $O/${S}_phasets.json > $O/${S}_phasets.out 2> $O/${S}_phasets.log &&
+timeout -k 10 420 python -u bench.py --mix llm5 --reps 2 --policies static-se,static-se+ishift1,static-se+ishift2,static-se+ishift3,static-se+tshift1 \
+  --out $O/${S}_llm5.json > $O/${S}_llm5.out 2> $O/${S}_llm5.log &&
+timeout -k 10 700 python -u bench.py --gpus 1 --steps 20 --warmup 5 --out $O/${S}_bench.json > $O/${S}_bench.out 2> $O/${S}_bench.log

@@ -66,6 +66,15 @@ def main(path, verbose=False):
                 print(f"      per-tenant clean frac {h.get('per_tenant_clean_frac')}")
                 if verbose:
                     print(f"      tenant periods {h.get('tenant_periods')}")
+            kt = [x["kernel_trace"] for x in rs if x.get("kernel_trace")]
+            if kt:  # in-process kernel trace (bench.py --kernel-trace): the median run by dispatches
+                k = sorted(kt, key=lambda z: z["dispatches"])[len(kt) // 2]
+                tot = sum(r[2] for r in k["kernels"]) or 1
+                print(f"      kernel trace: {k['dispatches']} dispatches, span {k['span_ns'] / 1e6:.1f} ms, "
+                      f"dropped {k['dropped']}")
+                for name, calls, tns, mx in k["kernels"][:12]:
+                    print(f"        {name[:58]:58s} {calls:7d} {tns / 1e6:9.2f} ms {tns / calls / 1e3:8.1f} us avg "
+                          f"{mx / 1e3:8.1f} us max {100 * tns / tot:6.2f} %")
             if verbose:
                 for x in rs:
                     print("       ", round(x["aggregate_all_gpus"], 4),

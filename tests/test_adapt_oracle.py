@@ -176,3 +176,24 @@ def test_atc_bucket_edges():
     assert O.atc_bucket(0) == 1 and O.atc_bucket(1023) == 1
     assert O.atc_bucket(1024) == 7 and O.atc_bucket(1535) == 7 and O.atc_bucket(1536) == 8
     assert O.atc_bucket(32767) == 15 and O.atc_bucket(32768) == 16 and O.atc_bucket(10 ** 9) == 16
+
+
+def test_grow_pct_doubles_the_stable_quantum_to_max():
+    """gpbs extension (MI355X profile grow_pct=100): the stable branch grows
+    the quantum proportionally -- 1 -> 2 -> 4 -> 8 -> 11 ms in four steps
+    after the 5-sample window, where the reference's +1 ms steps take ten --
+    and grow_pct=0 keeps the reference's additive trajectory."""
+    lib = N.load_core()
+    traj = {}
+    for g in (0, 100):
+        p = native_params(threshold=20000, min_us=1000, max_us=11000, inc_us=1000, dec_us=2000,
+                          switch_boundary=9000, ticks_per_tslice=3, grow_pct=g)
+        s = N.AdaptState()
+        lib.gpbs_adapt_init(C.byref(s), C.byref(p), 1000)
+        seq = []
+        for _ in range(16):  # a steady memory-bound tenant: 5e4 misses per 1e5 inst
+            native_step(lib, s, p, 1_000_000, 500_000)
+            seq.append(s.tslice_us)
+        traj[g] = seq
+    assert traj[100][:9] == [1000] * 5 + [2000, 4000, 8000, 11000]
+    assert traj[0][:8] == [1000] * 5 + [2000, 3000, 4000] and traj[0][-1] == 11000

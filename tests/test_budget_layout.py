@@ -224,7 +224,9 @@ def test_time_shared_region_steals_no_stacking_siblings():
     shares; sibling_steal=1 restores the Xen behaviour."""
     out = {}
     for ss in (1, 0):
-        e, parts = _engine(sibling_steal=ss)
+        # the reference's additive quantum steps: the steal pattern this
+        # guards against was traced with them (round 4)
+        e, parts = _engine(sibling_steal=ss, adapt=dict(MI355X_PROFILE["adapt"], grow_pct=0))
         ws = (512, 256, 256, 256, 256, 256, 256)  # a heavier tenant keeps UNDER slots queued on busy peers
         ts = [e.tenant_create(f"t{i}", nslots=32, weight=w) for i, w in enumerate(ws)]
         rates = {t: (COMPUTE if i < 3 else MEMORY) for i, t in enumerate(ts)}
