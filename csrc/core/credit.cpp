@@ -753,6 +753,9 @@ class CreditScheduler : public Scheduler {
   void async_apply(int id, const AdaptState& before, const AdaptState& after) {
     Tenant* t = E.tenant(id);
     if (!t || !t->alive || !t->priv || t->pool != pool_) return;
+    // the state moved since the launch (a class-change seed, an API set):
+    // the newer state wins over a result computed from the old one
+    if (std::memcmp(&sd(*t).adapt, &before, sizeof(before)) != 0) return;
     sd(*t).adapt = after;
     const int dir = after.tslice_us > before.tslice_us ? 1 : (after.tslice_us < before.tslice_us ? -1 : 0);
     const bool rearm = after.window_left == kWindow - 1 && before.window_left == 0;
@@ -1383,6 +1386,26 @@ class CreditScheduler : public Scheduler {
     if (t.cls == 1) return d.rate_ewma >= thr * 3 / 4 ? 1 : 0;
     if (t.cls == 0) return d.rate_ewma >= thr * 5 / 4 ? 1 : 0;
     return d.rate_ewma >= thr ? 1 : 0;
+  }
+
+  // PBS with the gpbs detector extensions (grow_pct > 0): a confirmed class
+  // change is a phase change the detector would otherwise find only after
+  // refilling its window and climbing step by step -- with metric updates
+  // once per clean counter window that is most of a 300 ms phase (phase-ts:
+  // the phase tenant sat at min_us in 0.65 of its periods under gpbs, 0.54
+  // under credit-classq).  Restart the detector from the new class's bound:
+  // memory -> max_us, compute -> min_us, window re-armed.  Not at the first
+  // classification: a jump of every tenant of a gang-switched region from
+  // the initial quantum at once put the region out of step in simulation
+  // (tests/test_se_mode.py), and the detector's own climb is fine there.
+  void class_changed(Tenant& t, int from, int to) override {
+    if (mode_ != Mode::PBS || !E.adapt_params.grow_pct || from < 0 || to < 0 || from == to) return;
+    AdaptState& a = sd(t).adapt;
+    a.tslice_us = to == 1 ? E.adapt_params.max_us : E.adapt_params.min_us;
+    a.tick_period_us = a.tslice_us / std::max<uint32_t>(1, E.adapt_params.ticks_per_tslice);
+    a.window_left = kWindow;
+    a.stable_count = 0;
+    for (auto& f : a.filter) f = FilterEntry{};
   }
 
   int bound_stats(Tenant& t, uint64_t* out3, bool reset) override {

@@ -1073,6 +1073,7 @@ void Engine::classify_tick(int64_t n) {
       }
       continue;
     }
+    pl->sched->class_changed(t, t.cls, c);
     t.cls = c;
     perfc.incr(PC_class_change);
     changed.push_back(t.id);

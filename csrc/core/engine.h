@@ -190,6 +190,8 @@ class Scheduler {
   virtual int bound_stats(Tenant&, uint64_t*, bool) { return GPBS_EINVAL; }
   // Contention class from the counters: -1 unknown (no recent samples), 0 compute-bound, 1 memory-bound.
   virtual int classify(Tenant&) { return -1; }
+  // A confirmed class change (after class_dwell): from -> to.
+  virtual void class_changed(Tenant&, int, int) {}
   // Trace word of a slot: (priority + 128) in bits 0-7, credit (clamped to
   // +-2^23) in bits 8-31.  Carried by WAKE records (who could preempt whom).
   virtual uint32_t trace_word(Slot&) { return 0; }

@@ -93,7 +93,10 @@ class Backend:
 
 
 def _run(script, async_mode, **kw):
-    prof = dict(MI355X_PROFILE, quantum_align_us=0, idle_skip=1, metric_period_us=PERIOD_US)
+    # the detector alone (grow_pct 0): the class-change seed is an engine
+    # event on its own clock, outside the one-period-late relation
+    prof = dict(MI355X_PROFILE, quantum_align_us=0, idle_skip=1, metric_period_us=PERIOD_US,
+                adapt=dict(MI355X_PROFILE["adapt"], grow_pct=0))
     e = Engine(sim_clock=True, partitions=[(0, x) for x in range(4)], **prof)
     e.tenant_create("Domain-0", nslots=1)
     tids = [e.tenant_create(f"t{i}", nslots=2) for i in range(3)]
@@ -137,7 +140,8 @@ def test_async_device_adapt_late_and_refused_periods_stay_exact():
 def _run_two_pools(script, async_mode):
     """Two credit pools on one counter backend (one GpuContext serving both):
     each pool's metric tick launches and harvests its own tenants only."""
-    prof = dict(MI355X_PROFILE, quantum_align_us=0, idle_skip=1, metric_period_us=PERIOD_US)
+    prof = dict(MI355X_PROFILE, quantum_align_us=0, idle_skip=1, metric_period_us=PERIOD_US,
+                adapt=dict(MI355X_PROFILE["adapt"], grow_pct=0))  # the detector alone, as _run
     e = Engine(sim_clock=True, partitions=[(0, x) for x in range(8)], **prof)
     e.tenant_create("Domain-0", nslots=1)
     p1 = e.pool_create("pool1", "credit")

@@ -617,3 +617,39 @@ def test_measurement_tenure_extends_one_tenure_once():
     assert sw[0].a[2] >= 4500  # the first tenure after the request
     assert all(r.a[2] < 4500 for r in sw[1:])
     assert e.measure(b) == 1
+
+
+def test_class_change_seeds_the_detector_at_the_class_bound():
+    """PBS with grow_pct (MI355X profile): a confirmed class change restarts
+    the detector from the new class's bound -- a tenant turning memory-bound
+    runs max_us at once instead of climbing from min_us -- while the
+    reference detector (grow_pct 0) climbs step by step."""
+    from pbs_amd.core.config import MI355X_PROFILE
+    out = {}
+    for g in (100, 0):
+        prof = dict(MI355X_PROFILE)
+        prof["sched"] = "credit"
+        prof["adapt"] = dict(MI355X_PROFILE["adapt"], grow_pct=g)
+        e = Engine(sim_clock=True, partitions=[(0, 0), (0, 1)], **prof)
+        e.tenant_create("Domain-0", nslots=1)
+        a = e.tenant_create("phase", nslots=1)
+        b = e.tenant_create("cmp", nslots=1)
+        e.wake(a)
+        e.wake(b)
+        for k in range(1, 41):  # both compute-bound: a settles at min_us
+            e.set_pmc(e.slot_id(a, 0), [k * 1_000_000, k * 1_000_000, k * 1000, k * 100])
+            e.set_pmc(e.slot_id(b, 0), [k * 1_000_000, k * 1_000_000, k * 1000, k * 100])
+            e.advance(e.now() + 1_000_000)
+        assert e.lib.gpbs_tenant_class(e.h, a) == 0 and e.tenant_info(a).tslice_us == 1000
+        seen = []
+        m0 = 40 * 100
+        for k in range(41, 61):  # a turns memory-bound (5e4 misses / 1e5 inst)
+            e.set_pmc(e.slot_id(a, 0), [k * 1_000_000, k * 1_000_000, k * 1000, m0 + (k - 40) * 500_000])
+            e.set_pmc(e.slot_id(b, 0), [k * 1_000_000, k * 1_000_000, k * 1000, k * 100])
+            e.advance(e.now() + 1_000_000)
+            seen.append((e.lib.gpbs_tenant_class(e.h, a), e.tenant_info(a).tslice_us))
+        out[g] = seen
+    first = next(i for i, (c, _) in enumerate(out[100]) if c == 1)
+    assert out[100][first][1] == 11000  # seeded at the class change
+    assert all(q == 11000 for _, q in out[100][first:])
+    assert out[0][first][1] < 11000  # the reference detector is still climbing
