@@ -944,6 +944,184 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
   finish(q, status, (u32)ntiles);
 }
 
+// ------------------------- GEMM 256x256, 8 waves, pipelined fragments ----
+// The 2-phase kernel's four barrier intervals per K-tile cost ~200 cycles
+// each on top of 512 MFMA cycles (stamps, see above): MFMA busy 0.53.  This
+// variant keeps the 8 waves (2 per SIMD: each SIMD's two waves cover each
+// other's LDS latency), the 128x64 wave tile, the LDS image, its swizzle and
+// the LDS-staged C epilogue of BAL 8, but runs ONE barrier per K-tile and
+// reads fragments into a second register set while the current set's MFMAs
+// run (sched_group_barrier interleaves one ds_read per two MFMAs):
+//   substep (t, 0): 32 MFMA on X  | reads of (t, 1) -> Y
+//   substep (t, 1): 16 MFMA on Y;  lgkmcnt(0) (no read of buffer t&1 left),
+//                   vmcnt(0) (this wave's part of tile t+1 landed);
+//                   s_barrier (tile t+1 in LDS; buffer t&1 free everywhere);
+//                   stage tile t+2 -> buffer t&1 (8 glds);
+//                   16 MFMA on Y  | reads of (t+1, 0) -> X
+// Registers: 128 accumulators + 64 fragment registers (one A set, re-read
+// block by block behind its MFMAs; two B sets).  The tile t+2
+// load has one K-tile (~2000 MFMA cycles per SIMD) to land.  Host opts bit
+// 18.
+__global__ __launch_bounds__(G2_NT, 1) void k_gemm256p_bf16_tn(const u16* __restrict__ A, const u16* __restrict__ Bt,
+                                                              u16* __restrict__ C, int M, int N, int K, WorkQueue* q,
+                                                              const PartTable* table, u32 mode, u32 me, u64* cnt,
+                                                              u32 inst_per_tile, u32 refs_per_tile, u32 miss_per_tile,
+                                                              u32* status) {
+  __shared__ __attribute__((aligned(16))) char smem[kG2Lds + 16];
+  lds_t* lds = (lds_t*)smem;
+  int* s_slot = (int*)(smem + kG2Lds);
+  const u32 xcc = xcc_id();
+  u64 t_last = __builtin_amdgcn_s_memtime();
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wu = __builtin_amdgcn_readfirstlane(wid);
+  const int wr = wu >> 2, wc = wu & 3;
+  const int tiles_n = N / G2_BM, ntiles = (M / G2_BM) * tiles_n;
+  const int nt = K / G2_BK;
+  int soff[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = 8 * (2 * wid + j) + (lane >> 3);
+    soff[j] = row * K + (((lane & 7) ^ g2_swz(row)) * 8);
+  }
+  const int l16 = lane & 15, lq = lane >> 4;
+  const int bh = wc >> 1, bc = (wc & 1) * 64;
+  for (;;) {
+    const int tile = grab_unit(q, table, mode, me, xcc, s_slot, (u32)ntiles);
+    if (tile < 0) break;
+    const int tm = tile / tiles_n, tn = tile % tiles_n;
+    const u16* Ab = A + (size_t)tm * G2_BM * K;
+    const u16* Bb = Bt + (size_t)tn * G2_BM * K;
+    auto stage_tile = [&](int t) {  // this wave's 2 KiB of each of the 4 half-tiles of K-tile t
+#pragma unroll
+      for (int kind = 0; kind < 2; ++kind)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const u16* src = (kind ? Bb : Ab) + (size_t)h * 128 * K + t * G2_BK;
+          lds_t* dst = lds + (t & 1) * kG2Buf + (kind * 2 + h) * kG2Half + wid * 2048;
+          glds16(src + soff[0], dst);
+          glds16(src + soff[1], dst + 1024);
+        }
+    };
+    auto frag = [&](int b, int kind, int h, int r0, int s) -> bf16x8 {
+      const int r = r0 + l16;
+      const lds_t* p = lds + b * kG2Buf + (kind * 2 + h) * kG2Half + r * 128 + (((4 * s + lq) ^ g2_swz(r)) << 4);
+      return *(const __attribute__((address_space(3))) bf16x8*)p;
+    };
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // One A set (an A fragment is re-read into its registers right after its
+    // 4 MFMAs issued) and two B sets (B fragments feed all 8 row blocks).
+    bf16x8 a[8], b0[4], b1[4];
+    // prologue: tiles 0 and 1 in flight; tile 0 landed and visible; (0, 0) read
+    stage_tile(0);
+    if (nt > 1) {
+      stage_tile(1);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b0[j] = frag(0, 1, bh, bc + j * 16, 0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = frag(0, 0, wr, i * 16, 0);
+    for (int t = 0; t < nt; ++t) {
+      const int buf = t & 1;
+      const bool more = t + 1 < nt;
+      // ---- substep 0: 32 MFMA on (b0, a); reads of (t, 1): b1, then a[i]
+      //      behind row block i's MFMAs
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b1[j] = frag(buf, 1, bh, bc + j * 16, 1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[j], a[i], acc[i][j], 0, 0, 0);
+        a[i] = frag(buf, 0, wr, i * 16, 1);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read (b1)
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMA
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);  // 3 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read (a[i])
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- substep 1, first half: 16 MFMA on (b1, a[0..3])
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j], a[i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every read of buffer t&1 by this wave retired
+      if (more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's part of tile t+1 landed
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (t + 2 < nt) stage_tile(t + 2);
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- substep 1, second half: 16 MFMA on (b1, a[4..7]); reads of
+      //      (t+1, 0): b0 and a[0..3] now, a[i] behind row block i's MFMAs
+      // (after the last K-tile these read the other buffer's stale tile,
+      // unused: straight-line code lets the compiler count lgkmcnt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b0[j] = frag(buf ^ 1, 1, bh, bc + j * 16, 0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = frag(buf ^ 1, 0, wr, i * 16, 0);
+#pragma unroll
+      for (int i = 4; i < 8; ++i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j], a[i], acc[i][j], 0, 0, 0);
+        a[i] = frag(buf ^ 1, 0, wr, i * 16, 0);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read (b0, a[0..3])
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read (a[4..7])
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's K-loop reads retired: the buffers take C
+    __builtin_amdgcn_sched_barrier(0);
+    // Epilogue: BAL 8's (C staged through the LDS at XOR (m & 15), full-line
+    // non-temporal stores)
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = wr * 128 + i * 16 + l16;
+        const int c8 = wc * 16 + j * 4 + lq;
+        const u32 lo = (u32)f2bf(acc[i][j][0]) | ((u32)f2bf(acc[i][j][1]) << 16);
+        const u32 hi = (u32)f2bf(acc[i][j][2]) | ((u32)f2bf(acc[i][j][3]) << 16);
+        *(__attribute__((address_space(3))) u32x2*)(lds + m * 512 + ((c8 ^ (m & 15)) << 3)) = u32x2{lo, hi};
+      }
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < 16; ++p) {
+      const int row = p * 16 + (tid >> 5), c16 = tid & 31;
+      u32x4 v = *(const __attribute__((address_space(3))) u32x4*)(lds + row * 512 + (((2 * c16) ^ (row & 14)) << 3));
+      if (row & 1) v = u32x4{v.z, v.w, v.x, v.y};
+      u32x4* dst = (u32x4*)(C + (size_t)(tm * G2_BM + row) * N + tn * G2_BM + c16 * 8);
+      __builtin_nontemporal_store(v, dst);
+    }
+    __syncthreads();  // the next tile's prologue restages buffer 0
+    count_unit(cnt, me, xcc, inst_per_tile, &t_last, refs_per_tile, miss_per_tile, q);
+  }
+  finish(q, status, (u32)ntiles);
+}
+
 // ------------------------------------------------ GEMM 256x256, 4 waves ----
 // The shape hipBLASLt picks for this GEMM on gfx950 (rocprofv3 kernel trace of
 // torch.mm 4096^3, profiles/kbench_r2_w4.md: MT256x256x64, MI16x16, 256
@@ -1320,6 +1498,12 @@ int gpbs_hip_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int
                    ((g_gemm_opts & 8) && ntiles % kXcds == 0 ? kGemmBlock2D : 0u);
     if ((g_gemm_opts & 32) && (K / G2_BK) % 2 == 0) {  // 4-wave 128x128-per-wave variant (plain tile queue)
       hipLaunchKernelGGL(k_gemm256w4_bf16_tn, dim3(grid), dim3(G4_NT), 0, s, (const u16*)A, (const u16*)Bt, (u16*)C,
+                         M, N, K, (WorkQueue*)q, (const PartTable*)table, mode, me, (u64*)cnt, inst, refs, miss,
+                         (u32*)status);
+      return hipGetLastError() == hipSuccess ? 0 : -5;
+    }
+    if (g_gemm_opts & 262144) {  // bit 18: one barrier per K-tile, pipelined fragments
+      hipLaunchKernelGGL(k_gemm256p_bf16_tn, dim3(grid), dim3(G2_NT), 0, s, (const u16*)A, (const u16*)Bt, (u16*)C,
                          M, N, K, (WorkQueue*)q, (const PartTable*)table, mode, me, (u64*)cnt, inst, refs, miss,
                          (u32*)status);
       return hipGetLastError() == hipSuccess ? 0 : -5;

@@ -43,7 +43,13 @@ MI355X_PROFILE: Dict[str, Any] = dict(
     sched="credit", tslice_us=1000, ratelimit_us=250, metric_period_us=1000, quantum_align_us=250,
     coschedule=3, class_period_us=2000,
     adapt=dict(threshold=20000, band_lo=70, band_hi=130, min_us=1000, max_us=11000, inc_us=1000, dec_us=2000,
-               switch_boundary=9000, ticks_per_tslice=3, grow_pct=100),
+               switch_boundary=9000, ticks_per_tslice=3,
+               # grow_pct > 0: proportional growth + a restart at the class bound
+               # on a class change (adapt_impl.h, credit.cpp class_changed).
+               # Measured at 100 on phase / phase-ts / 8mix (s13, s14): no gain
+               # over the additive steps, and the live phase-change test moved
+               # to the memory half in 128 ms instead of < 100 -- off by default.
+               grow_pct=0),
     # ATC (sched="atc"): waits arrive in ns from the K10 probes
     # (runtime/waitprobe.py); the reference buckets spin-loop iterations, one
     # PAUSE-loop iteration taken as ~8 ns.

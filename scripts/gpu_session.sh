@@ -5,10 +5,7 @@
 set -o pipefail
 O=gpurun_out/r5
 mkdir -p $O
-S=${1:-s13}
-timeout -k 10 120 python -u bench.py --mix 8mix --reps 1 --policies gpbs --kernel-trace \
-  --out $O/${S}_8mix_ktrace.json > $O/${S}_8mix_ktrace.out 2> $O/${S}_8mix_ktrace.log &&
-timeout -k 10 300 python -u bench.py --mix phase-ts --reps 5 \
-  --out $O/${S}_phasets.json > $O/${S}_phasets.out 2> $O/${S}_phasets.log &&
-KBENCH_GEMM_ONLY=1 timeout -k 10 120 python -u scripts/kbench.py > $O/${S}_kbench.jsonl 2> $O/${S}_kbench.log &&
-timeout -k 10 700 python -u bench.py --gpus 1 --steps 20 --warmup 5 --out $O/${S}_bench.json > $O/${S}_bench.out 2> $O/${S}_bench.log
+S=${1:-s16}
+timeout -k 10 180 python -u -m pytest tests/test_gpu_kernels.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider \
+  -k "gemm256_variants and 262144" > $O/${S}_gemmp_test.log 2>&1 &&
+KBENCH_GEMM_ONLY=1 timeout -k 10 120 python -u scripts/kbench.py > $O/${S}_kbench.jsonl 2> $O/${S}_kbench.log
