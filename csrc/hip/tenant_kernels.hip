@@ -1122,6 +1122,189 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256p_bf16_tn(const u16* __rest
   finish(q, status, (u32)ntiles);
 }
 
+// The same schedule with the fragment reads as inline-asm ds_read_b128 and
+// counted lgkmcnt waits (the compiler's waits above are lgkmcnt(0) at both
+// substep boundaries, stalling the two waves of a SIMD together).  Reads
+// are issued in one fixed order per substep -- B set, then A blocks 0..7 --
+// so block i of the next substep needs only the reads up to its own: a
+// substep's waits are lgkmcnt(7) (B + A block 0 of the previous substep's
+// 12), then lgkmcnt(11) for each later block of substep 0 (its 4 B + i A
+// reads of substep 1 issued since) and lgkmcnt(7 - i) in substep 1.  An
+// empty asm "+v" on each operand after its wait keeps the MFMA behind it.
+// Host opts bit 19.
+#define GPBS_DSR(dst, p) asm volatile("ds_read_b128 %0, %1" : "=v"(dst) : "v"((u32)(size_t)(p)))
+#define GPBS_TOUCH(x) asm volatile("" : "+v"(x))
+#define GPBS_LGKM(n) asm volatile("s_waitcnt lgkmcnt(" #n ")" ::: "memory")
+__global__ __launch_bounds__(G2_NT, 1) void k_gemm256p2_bf16_tn(const u16* __restrict__ A, const u16* __restrict__ Bt,
+                                                               u16* __restrict__ C, int M, int N, int K, WorkQueue* q,
+                                                               const PartTable* table, u32 mode, u32 me, u64* cnt,
+                                                               u32 inst_per_tile, u32 refs_per_tile, u32 miss_per_tile,
+                                                               u32* status) {
+  __shared__ __attribute__((aligned(16))) char smem[kG2Lds + 16];
+  lds_t* lds = (lds_t*)smem;
+  int* s_slot = (int*)(smem + kG2Lds);
+  const u32 xcc = xcc_id();
+  u64 t_last = __builtin_amdgcn_s_memtime();
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wu = __builtin_amdgcn_readfirstlane(wid);
+  const int wr = wu >> 2, wc = wu & 3;
+  const int tiles_n = N / G2_BM, ntiles = (M / G2_BM) * tiles_n;
+  const int nt = K / G2_BK;
+  int soff[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = 8 * (2 * wid + j) + (lane >> 3);
+    soff[j] = row * K + (((lane & 7) ^ g2_swz(row)) * 8);
+  }
+  const int l16 = lane & 15, lq = lane >> 4;
+  const int bh = wc >> 1, bc = (wc & 1) * 64;
+  for (;;) {
+    const int tile = grab_unit(q, table, mode, me, xcc, s_slot, (u32)ntiles);
+    if (tile < 0) break;
+    const int tm = tile / tiles_n, tn = tile % tiles_n;
+    const u16* Ab = A + (size_t)tm * G2_BM * K;
+    const u16* Bb = Bt + (size_t)tn * G2_BM * K;
+    auto stage_tile = [&](int t) {
+#pragma unroll
+      for (int kind = 0; kind < 2; ++kind)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const u16* src = (kind ? Bb : Ab) + (size_t)h * 128 * K + t * G2_BK;
+          lds_t* dst = lds + (t & 1) * kG2Buf + (kind * 2 + h) * kG2Half + wid * 2048;
+          glds16(src + soff[0], dst);
+          glds16(src + soff[1], dst + 1024);
+        }
+    };
+    auto fp = [&](int b, int kind, int h, int r0, int s) -> const lds_t* {
+      const int r = r0 + l16;
+      return lds + b * kG2Buf + (kind * 2 + h) * kG2Half + r * 128 + (((4 * s + lq) ^ g2_swz(r)) << 4);
+    };
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 a[8], b0[4], b1[4];
+    stage_tile(0);
+    if (nt > 1) {
+      stage_tile(1);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) GPBS_DSR(b0[j], fp(0, 1, bh, bc + j * 16, 0));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) GPBS_DSR(a[i], fp(0, 0, wr, i * 16, 0));
+    for (int t = 0; t < nt; ++t) {
+      const int buf = t & 1;
+      const bool more = t + 1 < nt;
+      // ---- substep 0: (b0, a) of (t, 0); reads of (t, 1): b1, then a[i] behind block i
+      __builtin_amdgcn_sched_barrier(0);
+      GPBS_LGKM(7);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) GPBS_TOUCH(b0[j]);
+      GPBS_TOUCH(a[0]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[j], a[0], acc[0][j], 0, 0, 0);
+        GPBS_DSR(b1[j], fp(buf, 1, bh, bc + j * 16, 1));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      GPBS_DSR(a[0], fp(buf, 0, wr, 0, 1));
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 1; i < 8; ++i) {
+        GPBS_LGKM(11);
+        GPBS_TOUCH(a[i]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[j], a[i], acc[i][j], 0, 0, 0);
+        GPBS_DSR(a[i], fp(buf, 0, wr, i * 16, 1));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // ---- substep 1, first half: (b1, a[0..3]) of (t, 1)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (i == 0) GPBS_LGKM(7);
+        if (i == 1) GPBS_LGKM(6);
+        if (i == 2) GPBS_LGKM(5);
+        if (i == 3) GPBS_LGKM(4);
+        if (i == 0)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) GPBS_TOUCH(b1[j]);
+        GPBS_TOUCH(a[i]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j], a[i], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      GPBS_LGKM(0);  // every read of buffer t&1 by this wave retired (a[4..7] too)
+#pragma unroll
+      for (int i = 4; i < 8; ++i) GPBS_TOUCH(a[i]);
+      if (more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's part of tile t+1 landed
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (t + 2 < nt) stage_tile(t + 2);
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- substep 1, second half: (b1, a[4..7]); reads of (t+1, 0) in the
+      //      order b0[0..3], a[0..3] (free), then a[i] behind block i
+      //      (after the last K-tile they read the other buffer's stale tile, unused)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[4][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j], a[4], acc[4][j], 0, 0, 0);
+        GPBS_DSR(b0[j], fp(buf ^ 1, 1, bh, bc + j * 16, 0));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[5][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j], a[5], acc[5][j], 0, 0, 0);
+        GPBS_DSR(a[j], fp(buf ^ 1, 0, wr, j * 16, 0));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      GPBS_DSR(a[4], fp(buf ^ 1, 0, wr, 64, 0));
+      GPBS_DSR(a[5], fp(buf ^ 1, 0, wr, 80, 0));
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[6][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j], a[6], acc[6][j], 0, 0, 0);
+      GPBS_DSR(a[6], fp(buf ^ 1, 0, wr, 96, 0));
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[7][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j], a[7], acc[7][j], 0, 0, 0);
+      GPBS_DSR(a[7], fp(buf ^ 1, 0, wr, 112, 0));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    GPBS_LGKM(0);
+    __builtin_amdgcn_s_barrier();  // every wave's K-loop reads retired: the buffers take C
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = wr * 128 + i * 16 + l16;
+        const int c8 = wc * 16 + j * 4 + lq;
+        const u32 lo = (u32)f2bf(acc[i][j][0]) | ((u32)f2bf(acc[i][j][1]) << 16);
+        const u32 hi = (u32)f2bf(acc[i][j][2]) | ((u32)f2bf(acc[i][j][3]) << 16);
+        *(__attribute__((address_space(3))) u32x2*)(lds + m * 512 + ((c8 ^ (m & 15)) << 3)) = u32x2{lo, hi};
+      }
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < 16; ++p) {
+      const int row = p * 16 + (tid >> 5), c16 = tid & 31;
+      u32x4 v = *(const __attribute__((address_space(3))) u32x4*)(lds + row * 512 + (((2 * c16) ^ (row & 14)) << 3));
+      if (row & 1) v = u32x4{v.z, v.w, v.x, v.y};
+      u32x4* dst = (u32x4*)(C + (size_t)(tm * G2_BM + row) * N + tn * G2_BM + c16 * 8);
+      __builtin_nontemporal_store(v, dst);
+    }
+    __syncthreads();
+    count_unit(cnt, me, xcc, inst_per_tile, &t_last, refs_per_tile, miss_per_tile, q);
+  }
+  finish(q, status, (u32)ntiles);
+}
+#undef GPBS_DSR
+#undef GPBS_TOUCH
+#undef GPBS_LGKM
+
 // ------------------------------------------------ GEMM 256x256, 4 waves ----
 // The shape hipBLASLt picks for this GEMM on gfx950 (rocprofv3 kernel trace of
 // torch.mm 4096^3, profiles/kbench_r2_w4.md: MT256x256x64, MI16x16, 256
@@ -1498,6 +1681,12 @@ int gpbs_hip_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int
                    ((g_gemm_opts & 8) && ntiles % kXcds == 0 ? kGemmBlock2D : 0u);
     if ((g_gemm_opts & 32) && (K / G2_BK) % 2 == 0) {  // 4-wave 128x128-per-wave variant (plain tile queue)
       hipLaunchKernelGGL(k_gemm256w4_bf16_tn, dim3(grid), dim3(G4_NT), 0, s, (const u16*)A, (const u16*)Bt, (u16*)C,
+                         M, N, K, (WorkQueue*)q, (const PartTable*)table, mode, me, (u64*)cnt, inst, refs, miss,
+                         (u32*)status);
+      return hipGetLastError() == hipSuccess ? 0 : -5;
+    }
+    if (g_gemm_opts & 524288) {  // bit 19: bit 18's schedule, counted waits on asm fragment reads
+      hipLaunchKernelGGL(k_gemm256p2_bf16_tn, dim3(grid), dim3(G2_NT), 0, s, (const u16*)A, (const u16*)Bt, (u16*)C,
                          M, N, K, (WorkQueue*)q, (const PartTable*)table, mode, me, (u64*)cnt, inst, refs, miss,
                          (u32*)status);
       return hipGetLastError() == hipSuccess ? 0 : -5;

@@ -65,7 +65,8 @@ def main():
                  256 | 8192 | 65536: "2phase-own-a-lds-c",
                  256 | 8192 | 65536 | 131072: "2phase-own-a-lds-c-nt",
                  256 | 8192 | 65536 | 131072 | 8: "2phase-own-a-lds-c-nt-2d-blocks",
-                 262144: "pipelined-1-barrier"}
+                 262144: "pipelined-1-barrier",
+                 524288: "pipelined-1-barrier-asm-reads"}
     ab = {k: [] for k in names}
     for _ in range(5):
         for opt in names:
