@@ -43,3 +43,14 @@ def test_metric_fold_calibrated_fallback_keeps_the_class():
     the edge of another tenure (a sliver) never counts."""
     from pbs_amd.ops import kernels as K
     assert K.lib().gpbs_hip_hwc_fold_selftest() == 0
+
+
+def test_kernel_trace_is_off_unless_enabled_before_init():
+    """The in-process kernel trace (csrc/hip/hwc.cpp Trace) only exists when
+    enabled before the counter tool registers: here (no rocprofiler-sdk
+    configuration in this process) its statistics read back as not running,
+    and bench.py carries the switch into the co-run config."""
+    from pbs_amd.bench.corun import CorunConfig
+    from pbs_amd.counters import hwc
+    assert hwc.trace_stats() is None
+    assert CorunConfig().kernel_trace is False
