@@ -164,6 +164,8 @@ def main():
                          "llm5: config #5 (Llama-3-8B fp8 decode + Llama-1B-shaped bf16 trainer, torch tenants "
                          "on the shim under gpbsd; not in the default run)")
     ap.add_argument("--reps-extra", type=int, default=5, help="reps of the non-headline mixes")
+    ap.add_argument("--gemm-opts", type=int, default=-1,
+                    help="GEMM tenant kernel variant bits (csrc/hip/tenant_kernels.hip g_gemm_opts; -1 = default)")
     ap.add_argument("--kernel-trace", action="store_true",
                     help="per-run kernel dispatch statistics from this process's own rocprofiler-sdk context "
                          "(the live counters stay on; rocprofv3 would take the SDK from them) -> --out")
@@ -213,6 +215,9 @@ def main():
             print("bench.py: hardware counter init failed; falling back to modeled counters", file=sys.stderr)
             counters = "model"
     torch.cuda.set_device(local)
+    if args.gemm_opts >= 0:
+        from pbs_amd.ops import kernels as _K
+        _K.lib().gpbs_hip_set_gemm_opts(args.gemm_opts)
     if counters == "hw":
         torch.zeros(1, device="cuda")
         if not hwc.start():

@@ -3,13 +3,11 @@
 # with && so the first failure ends the session.  Overwritten per session;
 # the commit history holds the earlier ones.
 set -o pipefail
-R=$(pwd)
-O=$R/gpurun_out/r5
+O=gpurun_out/r5
 mkdir -p $O
-S=${1:-s19}
-export TMPDIR=/tmp
-timeout -k 10 180 python -u -m pytest tests/test_gpu_kernels.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider \
-  -k "gemm256_variants and (262144 or 524288)" > $O/${S}_gemmp_test.log 2>&1 &&
-KBENCH_GEMM_ONLY=1 timeout -k 10 150 python -u scripts/kbench.py > $O/${S}_kbench.jsonl 2> $O/${S}_kbench.log &&
-timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE \
-  -d $O/${S}_pmc_p2 -o gemm --output-format csv -- python3 $R/scripts/gemm_only.py 4096 524288 > $O/${S}_pmc_p2.log 2>&1
+S=${1:-s21}
+# GEMM tile-to-XCD mapping A/B under co-run: default (205056) vs + 2-D XCD blocks (bit 3), separate processes
+timeout -k 10 240 python -u bench.py --mix 4mix --reps 5 --policies static-se,gpbs --out $O/${S}_4mix_def.json > $O/${S}_4mix_def.out 2> $O/${S}_4mix_def.log &&
+timeout -k 10 240 python -u bench.py --mix 4mix --reps 5 --policies static-se,gpbs --gemm-opts 205064 --out $O/${S}_4mix_2d.json > $O/${S}_4mix_2d.out 2> $O/${S}_4mix_2d.log &&
+timeout -k 10 300 python -u bench.py --mix 8mix --reps 5 --policies credit-classq,gpbs --out $O/${S}_8mix_def.json > $O/${S}_8mix_def.out 2> $O/${S}_8mix_def.log &&
+timeout -k 10 300 python -u bench.py --mix 8mix --reps 5 --policies credit-classq,gpbs --gemm-opts 205064 --out $O/${S}_8mix_2d.json > $O/${S}_8mix_2d.out 2> $O/${S}_8mix_2d.log
