@@ -221,8 +221,12 @@ constexpr u32 kGemmBlock2D = 1u << 17; // mode bit: 2-D per-XCD tile blocks
 // round 3: the 2-phase kernel, own-A-half staging (profiles/r3/kbench_gemm_k.log); round 4: C
 // staged through LDS, +1.1-1.3 % in three processes on two boxes (profiles/r4/kbench_gemm_ldsc_s51_s52.jsonl),
 // its full-line stores non-temporal, another +1.0-1.3 % in three processes on two boxes
-// (profiles/r4/kbench_gemm_ldsc_nt_s54_s55.jsonl)
-static int g_gemm_opts = 256 | 8192 | 65536 | 131072;
+// (profiles/r4/kbench_gemm_ldsc_nt_s54_s55.jsonl); round 5: + 2-D per-XCD
+// tile blocks (bit 3).  Solo that is worth 0.2-0.5 %; in the co-runs,
+// where the memory tenants stream through the same L2s, the GEMM keeps its
+// panels and runs 13 % faster: 4mix 1.169 -> 1.250, 8mix 1.275 -> 1.340,
+// static-se and gpbs alike (profiles/r5/s21_gemm_blocks_ab.txt).
+static int g_gemm_opts = 256 | 8192 | 65536 | 131072 | 8;
 constexpr int kG2Half = 128 * 128;           // bytes per half-tile
 constexpr int kG2Buf = 4 * kG2Half;          // A0 A1 B0 B1
 constexpr int kG2Lds = 2 * kG2Buf;           // 128 KiB

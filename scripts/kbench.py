@@ -65,6 +65,7 @@ def main():
                  256 | 8192 | 65536: "2phase-own-a-lds-c",
                  256 | 8192 | 65536 | 131072: "2phase-own-a-lds-c-nt",
                  256 | 8192 | 65536 | 131072 | 8: "2phase-own-a-lds-c-nt-2d-blocks",
+                 256 | 8192 | 65536 | 131072 | 8 | 1: "2phase-own-a-lds-c-nt-2d-blocks-xcd-range",
                  262144: "pipelined-1-barrier",
                  524288: "pipelined-1-barrier-asm-reads"}
     ab = {k: [] for k in names}
@@ -73,7 +74,7 @@ def main():
             L.gpbs_hip_set_gemm_opts(opt)
             ab[opt].append(timed(lambda: L.gpbs_hip_gemm_bf16(K._ptr(A), K._ptr(B), K._ptr(Cm), n, n, n, K._ptr(q),
                                                               None, 0, 0, None, None, 0, s), args.iters, zero))
-    L.gpbs_hip_set_gemm_opts(256 | 8192 | 65536 | 131072)
+    L.gpbs_hip_set_gemm_opts(256 | 8192 | 65536 | 131072 | 8)
     for opt, v in ab.items():
         ms = sorted(v)[len(v) // 2]
         out.append({"kernel": "gemm_bf16", "variant": names[opt], "shape": [n, n, n],
@@ -91,7 +92,7 @@ def main():
         err = (Cm[:512].float() - ref).abs().max().item()
         out.append({"kernel": "gemm_bf16", "variant": names[opt], "check_max_abs_err": err,
                     "ok": err < 0.02 * ref.abs().max().item()})
-    L.gpbs_hip_set_gemm_opts(256 | 8192 | 65536 | 131072)
+    L.gpbs_hip_set_gemm_opts(256 | 8192 | 65536 | 131072 | 8)
     if os.environ.get("KBENCH_GEMM_ONLY"):
         for r in out:
             print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}))
