@@ -166,6 +166,10 @@ def main():
     ap.add_argument("--reps-extra", type=int, default=5, help="reps of the non-headline mixes")
     ap.add_argument("--gemm-opts", type=int, default=-1,
                     help="GEMM tenant kernel variant bits (csrc/hip/tenant_kernels.hip g_gemm_opts; -1 = default)")
+    ap.add_argument("--reduce-opts", type=int, default=-1,
+                    help="reduce-copy tenant variant bits (g_reduce_opts; -1 = default)")
+    ap.add_argument("--stream-opts", type=int, default=-1,
+                    help="HBM-stream tenant variant bits (g_stream_opts; -1 = default)")
     ap.add_argument("--kernel-trace", action="store_true",
                     help="per-run kernel dispatch statistics from this process's own rocprofiler-sdk context "
                          "(the live counters stay on; rocprofv3 would take the SDK from them) -> --out")
@@ -215,9 +219,11 @@ def main():
             print("bench.py: hardware counter init failed; falling back to modeled counters", file=sys.stderr)
             counters = "model"
     torch.cuda.set_device(local)
-    if args.gemm_opts >= 0:
+    if max(args.gemm_opts, args.reduce_opts, args.stream_opts) >= 0:  # tenant kernel variants (A/B runs)
         from pbs_amd.ops import kernels as _K
-        _K.lib().gpbs_hip_set_gemm_opts(args.gemm_opts)
+        _K.lib().gpbs_hip_set_gemm_opts(args.gemm_opts)  # -1 keeps
+        _K.lib().gpbs_hip_set_reduce_opts(args.reduce_opts)
+        _K.lib().gpbs_hip_set_stream_opts(args.stream_opts)
     if counters == "hw":
         torch.zeros(1, device="cuda")
         if not hwc.start():
