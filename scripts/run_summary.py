@@ -75,10 +75,11 @@ def main(path, verbose=False):
                 for name, calls, tns, mx in k["kernels"][:12]:
                     print(f"        {name[:58]:58s} {calls:7d} {tns / 1e6:9.2f} ms {tns / calls / 1e3:8.1f} us avg "
                           f"{mx / 1e3:8.1f} us max {100 * tns / tot:6.2f} %")
-            if verbose:
+            if verbose:  # normalised shares and absolute rates (a slower solo kernel inflates the former)
                 for x in rs:
                     print("       ", round(x["aggregate_all_gpus"], 4),
-                          {n: t["norm_perf"] for n, t in x["tenants"].items()})
+                          {n: t["norm_perf"] for n, t in x["tenants"].items()},
+                          {n: t.get("units_per_ms") for n, t in x["tenants"].items() if "units_per_ms" in t})
         solo = d["line"].get("solo") if mix == list(d["results"])[0] else None
         if solo:
             print("  solo:", json.dumps(solo)[:400])
