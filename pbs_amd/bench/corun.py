@@ -226,6 +226,11 @@ POLICY_ENGINES = {
     "gpbs-q33": (4, dict(BUDGET_OVERRIDES, class_budget=1,
                          adapt=dict(MI355X_PROFILE["adapt"], max_us=33000, inc_us=3000, dec_us=6000)), True,
                  "device,se,waveprio,latco,budget,latmem"),
+    # PBS quantum range capped lower at the top (memory tenants up to 4 / 6 ms)
+    "gpbs-max4": (4, dict(BUDGET_OVERRIDES, class_budget=1, adapt=dict(MI355X_PROFILE["adapt"], max_us=4000)), True,
+                  "device,se,waveprio,latco,budget,latmem"),
+    "gpbs-max6": (4, dict(BUDGET_OVERRIDES, class_budget=1, adapt=dict(MI355X_PROFILE["adapt"], max_us=6000)), True,
+                  "device,se,waveprio,latco,budget,latmem"),
     # the flagship under other counter-sampler policies (same engine and
     # layout; SAMPLER below): round-3 sampler (owner-change bursts, no budget,
     # no model fallback), and modeled counters only (no hardware sample)
