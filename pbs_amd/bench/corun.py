@@ -231,6 +231,12 @@ POLICY_ENGINES = {
                   "device,se,waveprio,latco,budget,latmem"),
     "gpbs-max6": (4, dict(BUDGET_OVERRIDES, class_budget=1, adapt=dict(MI355X_PROFILE["adapt"], max_us=6000)), True,
                   "device,se,waveprio,latco,budget,latmem"),
+    # class changes must persist 100 / 300 ms (class_dwell x class_period_us)
+    # before a tenant is re-homed: flap damping for phase-changing tenants
+    "gpbs-dwell50": (4, dict(BUDGET_OVERRIDES, class_budget=1, class_dwell=50), True,
+                     "device,se,waveprio,latco,budget,latmem"),
+    "gpbs-dwell150": (4, dict(BUDGET_OVERRIDES, class_budget=1, class_dwell=150), True,
+                      "device,se,waveprio,latco,budget,latmem"),
     # the flagship under other counter-sampler policies (same engine and
     # layout; SAMPLER below): round-3 sampler (owner-change bursts, no budget,
     # no model fallback), and modeled counters only (no hardware sample)

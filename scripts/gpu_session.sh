@@ -5,9 +5,8 @@
 set -o pipefail
 O=gpurun_out/r5
 mkdir -p $O
-S=${1:-s21}
-# GEMM tile-to-XCD mapping A/B under co-run: default (205056) vs + 2-D XCD blocks (bit 3), separate processes
-timeout -k 10 240 python -u bench.py --mix 4mix --reps 5 --policies static-se,gpbs --out $O/${S}_4mix_def.json > $O/${S}_4mix_def.out 2> $O/${S}_4mix_def.log &&
-timeout -k 10 240 python -u bench.py --mix 4mix --reps 5 --policies static-se,gpbs --gemm-opts 205064 --out $O/${S}_4mix_2d.json > $O/${S}_4mix_2d.out 2> $O/${S}_4mix_2d.log &&
-timeout -k 10 300 python -u bench.py --mix 8mix --reps 5 --policies credit-classq,gpbs --out $O/${S}_8mix_def.json > $O/${S}_8mix_def.out 2> $O/${S}_8mix_def.log &&
-timeout -k 10 300 python -u bench.py --mix 8mix --reps 5 --policies credit-classq,gpbs --gemm-opts 205064 --out $O/${S}_8mix_2d.json > $O/${S}_8mix_2d.out 2> $O/${S}_8mix_2d.log
+S=${1:-s25}
+timeout -k 10 360 python -u bench.py --mix phase-ts --reps 5 --policies credit-fixed-ts,gpbs,gpbs-dwell50,gpbs-dwell150 \
+  --out $O/${S}_phasets.json > $O/${S}_phasets.out 2> $O/${S}_phasets.log &&
+timeout -k 10 360 python -u bench.py --mix phase --reps 5 --policies credit-fixed,gpbs,gpbs-dwell50,gpbs-dwell150,static-se \
+  --out $O/${S}_phase.json > $O/${S}_phase.out 2> $O/${S}_phase.log
