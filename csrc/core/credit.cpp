@@ -170,9 +170,13 @@ class CreditScheduler : public Scheduler {
     const Tenant& t = *E.tenants[v.tenant];
     uint32_t q = sd(*E.tenants[v.tenant]).adapt.tslice_us;
     if (!t.budget_shared || t.cls < 0) return q;
+    // co-sharers: the tenants laid out in the same class region (a flapping
+    // tenant pinned to the memory region by class_pin_us counts there)
+    const int64_t now = E.now(), pin = (int64_t)E.boot.class_pin_us * 1000;
+    const int lc = t.layout_cls(now, pin);
     for (auto& tp : E.tenants)
-      if (tp && tp->alive && tp->priv && tp->pool == t.pool && tp->budget_shared && tp->cls == t.cls &&
-          tp->budget_ctx != 0)
+      if (tp && tp->alive && tp->priv && tp->pool == t.pool && tp->budget_shared && tp->cls >= 0 &&
+          tp->layout_cls(now, pin) == lc && tp->budget_ctx != 0)
         q = std::max(q, sd(*tp).adapt.tslice_us);
     return q;
   }

@@ -808,7 +808,7 @@ void Engine::budget_layout(Pool& pl, int64_t n, bool force) {
     if (busy && t.pause_count == 0) t.last_busy = n;
     // class -1: busy but not classified yet
     const bool present = n - t.last_busy <= present_ns;
-    if (present) sig.emplace_back(t.id, t.cls >= 0 ? t.cls : -1);
+    if (present) sig.emplace_back(t.id, t.cls >= 0 ? t.layout_cls(n, (int64_t)boot.class_pin_us * 1000) : -1);
     else t.budget_ctx = 0;
   }
   if (!force && sig == pl.budget_sig) return;
@@ -1074,6 +1074,11 @@ void Engine::classify_tick(int64_t n) {
       continue;
     }
     pl->sched->class_changed(t, t.cls, c);
+    if (t.cls >= 0) {  // a change of class (not the first classification)
+      t.cls_chg_ns[0] = t.cls_chg_ns[1];
+      t.cls_chg_ns[1] = t.cls_chg_ns[2];
+      t.cls_chg_ns[2] = n;
+    }
     t.cls = c;
     perfc.incr(PC_class_change);
     changed.push_back(t.id);

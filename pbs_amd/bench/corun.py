@@ -231,6 +231,10 @@ POLICY_ENGINES = {
                   "device,se,waveprio,latco,budget,latmem"),
     "gpbs-max6": (4, dict(BUDGET_OVERRIDES, class_budget=1, adapt=dict(MI355X_PROFILE["adapt"], max_us=6000)), True,
                   "device,se,waveprio,latco,budget,latmem"),
+    # a tenant flapping between classes (3 changes within 2 s) is laid out in
+    # the memory region until it settles (boot class_pin_us)
+    "gpbs-pin": (4, dict(BUDGET_OVERRIDES, class_budget=1, class_pin_us=2000000), True,
+                 "device,se,waveprio,latco,budget,latmem"),
     # class changes must persist 100 / 300 ms (class_dwell x class_period_us)
     # before a tenant is re-homed: flap damping for phase-changing tenants
     "gpbs-dwell50": (4, dict(BUDGET_OVERRIDES, class_budget=1, class_dwell=50), True,

@@ -330,3 +330,34 @@ def test_class_fall_reclassifies_an_ended_memory_phase_sooner():
         took[cf] = n
         assert e.check() == ""
     assert took[1] < 2000 and took[1] < took[0], took
+
+
+def test_flapping_tenant_is_laid_out_in_the_memory_region():
+    """class_pin_us: a tenant whose last three class changes fall within the
+    window is laid out as memory class -- it joins the time-shared memory
+    region instead of taking compute SEs from the GEMM tenant on every
+    compute phase (phase-ts, s23/s24: the move halved the GEMM's SEs for no
+    gain to the phase tenant).  Its first changes still move it (the live
+    phase-change test needs that), and without the pin it keeps moving."""
+    def run(pin_us):
+        e, parts = _engine(class_pin_us=pin_us)
+        g, p, h = (e.tenant_create(n, nslots=32) for n in ("gemm", "phase", "hbm"))
+        rates = {g: COMPUTE, p: COMPUTE, h: MEMORY}
+        for t in (g, p, h):
+            e.wake(t)
+        _settle(e, rates, 600)
+        seen = []
+        for k in range(8):  # 8 phases of 60 ms: memory, compute, memory, ...
+            rates[p] = MEMORY if k % 2 == 0 else COMPUTE
+            _settle(e, rates, 600)
+            seen.append((e.lib.gpbs_tenant_class(e.h, p), e.tenant_info(p).budget_ctx & 0xF,
+                         e.tenant_info(g).budget_ctx & 0xF))
+        assert e.check() == ""
+        return seen
+    free = run(0)
+    pinned = run(2_000_000)
+    # without the pin, every compute phase takes a compute SE from the GEMM
+    assert all(c == 0 and (ctx & 0x3) and gctx != 0x3 for c, ctx, gctx in free[1::2]), free
+    # with it, the first change-back still moves it; after the third change it stays
+    assert pinned[1][0] == 0 and pinned[1][1] & 0x3, pinned
+    assert all(ctx & 0x3 == 0 and gctx == 0x3 for c, ctx, gctx in pinned[3:]), pinned
