@@ -172,11 +172,10 @@ class CreditScheduler : public Scheduler {
     if (!t.budget_shared || t.cls < 0) return q;
     // co-sharers: the tenants laid out in the same class region (a flapping
     // tenant pinned to the memory region by class_pin_us counts there)
-    const int64_t now = E.now(), pin = (int64_t)E.boot.class_pin_us * 1000;
-    const int lc = t.layout_cls(now, pin);
+    const int lc = t.lay_cls >= 0 ? t.lay_cls : t.cls;
     for (auto& tp : E.tenants)
       if (tp && tp->alive && tp->priv && tp->pool == t.pool && tp->budget_shared && tp->cls >= 0 &&
-          tp->layout_cls(now, pin) == lc && tp->budget_ctx != 0)
+          (tp->lay_cls >= 0 ? tp->lay_cls : tp->cls) == lc && tp->budget_ctx != 0)
         q = std::max(q, sd(*tp).adapt.tslice_us);
     return q;
   }

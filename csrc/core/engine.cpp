@@ -808,8 +808,25 @@ void Engine::budget_layout(Pool& pl, int64_t n, bool force) {
     if (busy && t.pause_count == 0) t.last_busy = n;
     // class -1: busy but not classified yet
     const bool present = n - t.last_busy <= present_ns;
-    if (present) sig.emplace_back(t.id, t.cls >= 0 ? t.layout_cls(n, (int64_t)boot.class_pin_us * 1000) : -1);
+    if (present) sig.emplace_back(t.id, t.cls);
     else t.budget_ctx = 0;
+  }
+  // class_pin_us: a flapping compute-phase tenant joins the memory region
+  // when that region is time-shared already (two or more other memory-class
+  // tenants): a fourth co-sharer costs each of them a quarter of their turns,
+  // while its moves into the compute region halved the GEMM tenant's SEs for
+  // no gain of its own (phase-ts).  Next to a single memory tenant it would
+  // halve that tenant's SEs instead (phase mix: measured -0.008), so there it
+  // keeps moving.
+  {
+    const int64_t pin_ns = (int64_t)std::max(0, boot.class_pin_us) * 1000;
+    int mem = 0;
+    for (auto& e : sig) mem += e.second == 1;
+    for (auto& e : sig) {
+      Tenant& t = *tenants[e.first];
+      if (e.second == 0 && mem >= 2 && t.flapping(n, pin_ns)) e.second = 1;
+      t.lay_cls = e.second;
+    }
   }
   if (!force && sig == pl.budget_sig) return;
   pl.budget_sig = sig;

@@ -97,10 +97,9 @@ struct Tenant {  // struct domain
   int cls_pending = -1;  // hysteresis: a new class must be seen on consecutive ticks
   int cls_count = 0;
   int64_t cls_chg_ns[3] = {INT64_MIN / 2, INT64_MIN / 2, INT64_MIN / 2};  // last three confirmed class changes
-  // class_pin_us: laid out as memory class while flapping (budget_layout)
-  int layout_cls(int64_t now, int64_t pin_ns) const {
-    return pin_ns > 0 && cls >= 0 && now - cls_chg_ns[0] <= pin_ns ? 1 : cls;
-  }
+  // class_pin_us: flapping = its last three class changes within the window
+  bool flapping(int64_t now, int64_t pin_ns) const { return pin_ns > 0 && cls >= 0 && now - cls_chg_ns[0] <= pin_ns; }
+  int lay_cls = -1;  // the class budget_layout placed it by (a pinned flapping tenant: 1)
   // Cross-GPU gang window (parallel/gang.py): 1 favoured (run on every
   // partition that holds a slot), 2 excluded (its peers on other GPUs are not
   // running it), until gang_until (engine clock).

@@ -42,6 +42,10 @@ REFERENCE_PROFILE: Dict[str, Any] = dict(
 MI355X_PROFILE: Dict[str, Any] = dict(
     sched="credit", tslice_us=1000, ratelimit_us=250, metric_period_us=1000, quantum_align_us=250,
     coschedule=3, class_period_us=2000,
+    # class_budget layouts: a tenant flapping between classes (3 changes in
+    # 2 s) joins an already time-shared memory region instead of splitting
+    # the compute region (phase-ts +0.016, s26; engine.cpp budget_layout)
+    class_pin_us=2000000,
     adapt=dict(threshold=20000, band_lo=70, band_hi=130, min_us=1000, max_us=11000, inc_us=1000, dec_us=2000,
                switch_boundary=9000, ticks_per_tslice=3,
                # grow_pct > 0: proportional growth + a restart at the class bound

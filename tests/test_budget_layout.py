@@ -334,16 +334,20 @@ def test_class_fall_reclassifies_an_ended_memory_phase_sooner():
 
 def test_flapping_tenant_is_laid_out_in_the_memory_region():
     """class_pin_us: a tenant whose last three class changes fall within the
-    window is laid out as memory class -- it joins the time-shared memory
-    region instead of taking compute SEs from the GEMM tenant on every
-    compute phase (phase-ts, s23/s24: the move halved the GEMM's SEs for no
-    gain to the phase tenant).  Its first changes still move it (the live
-    phase-change test needs that), and without the pin it keeps moving."""
-    def run(pin_us):
+    window is laid out as memory class when the memory region is already
+    time-shared (two or more other memory tenants: phase-ts) -- it joins
+    that region instead of taking compute SEs from the GEMM tenant on every
+    compute phase (s23/s24: the move halved the GEMM's SEs for no gain to
+    the phase tenant).  Its first changes still move it (the live
+    phase-change test needs that); next to a single memory tenant (the phase
+    mix) it keeps moving, and without the pin it always does."""
+    def run(pin_us, n_mem):
         e, parts = _engine(class_pin_us=pin_us)
-        g, p, h = (e.tenant_create(n, nslots=32) for n in ("gemm", "phase", "hbm"))
-        rates = {g: COMPUTE, p: COMPUTE, h: MEMORY}
-        for t in (g, p, h):
+        g, p = (e.tenant_create(n, nslots=32) for n in ("gemm", "phase"))
+        ms = [e.tenant_create(f"m{i}", nslots=32) for i in range(n_mem)]
+        rates = {g: COMPUTE, p: COMPUTE}
+        rates.update({m: MEMORY for m in ms})
+        for t in rates:
             e.wake(t)
         _settle(e, rates, 600)
         seen = []
@@ -354,10 +358,13 @@ def test_flapping_tenant_is_laid_out_in_the_memory_region():
                          e.tenant_info(g).budget_ctx & 0xF))
         assert e.check() == ""
         return seen
-    free = run(0)
-    pinned = run(2_000_000)
+    free = run(0, 3)
+    pinned = run(2_000_000, 3)
+    single = run(2_000_000, 1)
     # without the pin, every compute phase takes a compute SE from the GEMM
     assert all(c == 0 and (ctx & 0x3) and gctx != 0x3 for c, ctx, gctx in free[1::2]), free
     # with it, the first change-back still moves it; after the third change it stays
     assert pinned[1][0] == 0 and pinned[1][1] & 0x3, pinned
     assert all(ctx & 0x3 == 0 and gctx == 0x3 for c, ctx, gctx in pinned[3:]), pinned
+    # a single memory tenant: no pin, the compute phases still move it
+    assert all(c == 0 and (ctx & 0x3) for c, ctx, gctx in single[1::2]), single
