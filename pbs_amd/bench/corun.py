@@ -1027,6 +1027,7 @@ class Corun:
         layout = {n: [] for n in self.throughput}  # budget SE sets per step (bit c = SE c)
         self._rs0 = {n: r.stats() for n, r in self.runners.items() if isinstance(r, Runner)}
         self.ctx.masked_pool_reset()
+        _gs0 = self.ctx.stats()  # the pool's counters are process-wide: this run's share is the delta
         if self.cfg.kernel_trace:
             from ..counters import hwc as _hwc
             _hwc.trace_stats(reset=True)
@@ -1085,8 +1086,8 @@ class Corun:
         # share another layout's queue (serialised layouts)
         gs = self.ctx.stats()
         res["masked_queues"] = {"held_max": gs["masked_queues_held_max"], "created": gs["masked_queues_created"],
-                                "cross_key_shares": gs["masked_cross_key_shares"],
-                                "pipe_shared_other": gs["masked_pipe_shared_other"]}
+                                "cross_key_shares": gs["masked_cross_key_shares"] - _gs0["masked_cross_key_shares"],
+                                "pipe_shared_other": gs["masked_pipe_shared_other"] - _gs0["masked_pipe_shared_other"]}
         if self.cfg.kernel_trace:  # in-process kernel trace of the run (live counters on)
             from ..counters import hwc as _hwc
             ks = _hwc.trace_stats(reset=True)
