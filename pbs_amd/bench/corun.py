@@ -214,6 +214,8 @@ POLICY_ENGINES = {
     # quantum for the pool, driven by the tenants' wait reports (K10); the
     # same time-shared budget layout as the flagship
     "atc": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="atc"), True, "device,se,waveprio,latco,budget,latmem"),
+    "atc-nox": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="atc", class_steal=0), True,
+                "device,se,waveprio,latco,budget,latmem"),
     # switch-cost probes: every quantum (fixed) or the adaptive floor at 4 ms
     "credit-fixed-ts4": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="credit-fixed", tslice_us=4000), True,
                          "device,se,waveprio,latco,budget,latmem"),

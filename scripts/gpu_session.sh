@@ -5,8 +5,8 @@
 set -o pipefail
 O=gpurun_out/r5
 mkdir -p $O
-S=${1:-s25}
-timeout -k 10 360 python -u bench.py --mix phase-ts --reps 5 --policies credit-fixed-ts,gpbs,gpbs-dwell50,gpbs-dwell150 \
-  --out $O/${S}_phasets.json > $O/${S}_phasets.out 2> $O/${S}_phasets.log &&
-timeout -k 10 360 python -u bench.py --mix phase --reps 5 --policies credit-fixed,gpbs,gpbs-dwell50,gpbs-dwell150,static-se \
-  --out $O/${S}_phase.json > $O/${S}_phase.out 2> $O/${S}_phase.log
+S=${1:-s29}
+timeout -k 10 300 python -u bench.py --mix 8mix --reps 3 --policies atc,atc-nox,gpbs,gpbs-nox \
+  --out $O/${S}_8mix.json > $O/${S}_8mix.out 2> $O/${S}_8mix.log &&
+timeout -k 10 300 python -u bench.py --mix 4mix --reps 3 --policies atc,atc-nox,gpbs \
+  --out $O/${S}_4mix.json > $O/${S}_4mix.out 2> $O/${S}_4mix.log
