@@ -368,3 +368,29 @@ def test_flapping_tenant_is_laid_out_in_the_memory_region():
     assert all(ctx & 0x3 == 0 and gctx == 0x3 for c, ctx, gctx in pinned[3:]), pinned
     # a single memory tenant: no pin, the compute phases still move it
     assert all(c == 0 and (ctx & 0x3) for c, ctx, gctx in single[1::2]), single
+
+
+def test_atc_keeps_the_class_budget_layout():
+    """sched=atc on a class_budget layout: the budget places every slot (one
+    per partition of its tenant's SEs); ATC's hard-affinity spreading of a
+    tenant's slots (X:xen/common/sched_credit_atc.c:634-651) is skipped there
+    -- on top of the layout it pinned slots away from their class homes and
+    left half the partitions idle (4mix under atc: 0.58, s29)."""
+    e, parts = _engine(sched="atc")
+    ts = [e.tenant_create(n, nslots=32) for n in ("gemm", "hbm", "coll")]
+    rates = {t: (COMPUTE if i == 0 else MEMORY) for i, t in enumerate(ts)}
+    for t in ts:
+        e.wake(t)
+    _settle(e, rates, 3000)
+    busy = foreign = n = 0
+    for _ in range(100):
+        _settle(e, rates, 5)
+        for p, (_, x, c) in enumerate(parts):
+            cur = e.partition_info(p)["curr_tenant"]
+            n += 1
+            if cur in ts:
+                busy += 1
+                foreign += (ts.index(cur) == 0) != (c < 2)
+    assert busy == n and foreign == 0, (busy, n, foreign)
+    assert [e.tenant_info(t).budget_ctx & 0xF for t in ts] == [0x3, 0x4, 0x8]
+    assert e.check() == ""
