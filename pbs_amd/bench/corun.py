@@ -228,6 +228,13 @@ POLICY_ENGINES = {
     "gpbs-q33": (4, dict(BUDGET_OVERRIDES, class_budget=1,
                          adapt=dict(MI355X_PROFILE["adapt"], max_us=33000, inc_us=3000, dec_us=6000)), True,
                  "device,se,waveprio,latco,budget,latmem"),
+    # long quanta everywhere: 30 ms fixed (the ATC default without its wait
+    # feedback), and the PBS range moved up to 4-30 ms
+    "credit-fixed-ts30": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="credit-fixed", tslice_us=30000), True,
+                          "device,se,waveprio,latco,budget,latmem"),
+    "gpbs-w": (4, dict(BUDGET_OVERRIDES, class_budget=1,
+                       adapt=dict(MI355X_PROFILE["adapt"], min_us=4000, max_us=30000, inc_us=4000, dec_us=8000,
+                                  switch_boundary=30000)), True, "device,se,waveprio,latco,budget,latmem"),
     # PBS quantum range capped lower at the top (memory tenants up to 4 / 6 ms)
     "gpbs-max4": (4, dict(BUDGET_OVERRIDES, class_budget=1, adapt=dict(MI355X_PROFILE["adapt"], max_us=4000)), True,
                   "device,se,waveprio,latco,budget,latmem"),

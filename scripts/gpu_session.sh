@@ -5,8 +5,8 @@
 set -o pipefail
 O=gpurun_out/r5
 mkdir -p $O
-S=${1:-s29}
-timeout -k 10 300 python -u bench.py --mix 8mix --reps 3 --policies atc,atc-nox,gpbs,gpbs-nox \
-  --out $O/${S}_8mix.json > $O/${S}_8mix.out 2> $O/${S}_8mix.log &&
-timeout -k 10 300 python -u bench.py --mix 4mix --reps 3 --policies atc,atc-nox,gpbs \
-  --out $O/${S}_4mix.json > $O/${S}_4mix.out 2> $O/${S}_4mix.log
+S=${1:-s31}
+for M in 8mix phase-ts phase 4mix; do
+  timeout -k 10 300 python -u bench.py --mix $M --reps 3 --policies gpbs,atc,credit-fixed-ts30,gpbs-w \
+    --out $O/${S}_$M.json > $O/${S}_$M.out 2> $O/${S}_$M.log || exit $?
+done
