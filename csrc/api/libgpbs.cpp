@@ -132,6 +132,7 @@ void gpbs_boot_defaults(gpbs_boot_params_t* p) {
   p->sibling_steal = 0;
   p->class_steal = 1;
   p->class_fall = 0;
+  p->shared_q_us = 0;
   p->class_pin_us = 0;
   AdaptParams a;
   std::memcpy(&p->adapt, &a, sizeof(a));

@@ -177,6 +177,11 @@ class CreditScheduler : public Scheduler {
       if (tp && tp->alive && tp->priv && tp->pool == t.pool && tp->budget_shared && tp->cls >= 0 &&
           (tp->lay_cls >= 0 ? tp->lay_cls : tp->cls) == lc && tp->budget_ctx != 0)
         q = std::max(q, sd(*tp).adapt.tslice_us);
+    // shared_q_us: a time-shared region rotates at least this long -- a
+    // switch drains the outgoing tenant's in-flight tiles and the incoming
+    // one refills the XCDs' L2s, so on a GPU the cost falls with the quantum
+    // whatever the class (8mix: 30 ms for all 1.359 vs PBS 1 / 11 ms 1.331, s31)
+    if (E.boot.shared_q_us > 0) q = std::max(q, (uint32_t)E.boot.shared_q_us);
     return q;
   }
   // credit-classq: the class's bound (unknown class: the global quantum)

@@ -96,6 +96,8 @@ typedef struct gpbs_boot_params {
   int32_t class_fall;          /* contention classes: the smoothed miss rate follows a DROP at alpha 1/2 instead of
                                   1/4 (a rise already crosses the threshold in one sample): a memory-bound phase
                                   that ends is re-classified in ~6 periods instead of ~14.  0 = symmetric 1/4 */
+  int32_t shared_q_us;         /* class_budget: a time-shared class region rotates at least this quantum (PBS mode;
+                                  0 = the largest adaptive quantum of its co-sharers only) */
   int32_t class_pin_us;        /* class_budget: a tenant whose last THREE class changes fall within this window is
                                   laid out as memory class (its region time-shares; it takes no compute SEs from a
                                   compute tenant) until it settles.  0 = off */

@@ -36,7 +36,7 @@ class BootParams(C.Structure):
         "metric_period_us", "slice_apply_us", "sim_clock", "pmu_refresh_us", "dom0_quirk", "heartbeat_timeout_us",
         "trace_capacity", "quantum_align_us", "coschedule", "class_period_us", "boost_exclusive",
         "class_split", "idle_skip", "class_dwell", "class_budget", "present_us", "sibling_steal", "class_steal", "class_fall",
-        "class_pin_us")] + [("adapt", AdaptParams),
+        "shared_q_us", "class_pin_us")] + [("adapt", AdaptParams),
                                                                                     ("atc", AtcParams)]
 
 

@@ -235,6 +235,11 @@ POLICY_ENGINES = {
     "gpbs-w": (4, dict(BUDGET_OVERRIDES, class_budget=1,
                        adapt=dict(MI355X_PROFILE["adapt"], min_us=4000, max_us=30000, inc_us=4000, dec_us=8000,
                                   switch_boundary=30000)), True, "device,se,waveprio,latco,budget,latmem"),
+    # time-shared class regions rotate at >= 11 / 30 ms (boot shared_q_us)
+    "gpbs-sq11": (4, dict(BUDGET_OVERRIDES, class_budget=1, shared_q_us=11000), True,
+                  "device,se,waveprio,latco,budget,latmem"),
+    "gpbs-sq30": (4, dict(BUDGET_OVERRIDES, class_budget=1, shared_q_us=30000), True,
+                  "device,se,waveprio,latco,budget,latmem"),
     # PBS quantum range capped lower at the top (memory tenants up to 4 / 6 ms)
     "gpbs-max4": (4, dict(BUDGET_OVERRIDES, class_budget=1, adapt=dict(MI355X_PROFILE["adapt"], max_us=4000)), True,
                   "device,se,waveprio,latco,budget,latmem"),

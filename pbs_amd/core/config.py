@@ -72,7 +72,7 @@ BOOT_KEYS = ("sched", "tslice_us", "ratelimit_us", "smt_power_savings", "tickle_
              "migration_delay_us", "metric_period_us", "slice_apply_us", "pmu_refresh_us", "dom0_quirk",
              "heartbeat_timeout_us", "trace_capacity", "quantum_align_us", "coschedule", "class_period_us",
              "boost_exclusive", "class_split", "idle_skip", "class_dwell", "class_budget", "present_us",
-             "sibling_steal", "class_steal", "class_fall", "class_pin_us")
+             "sibling_steal", "class_steal", "class_fall", "shared_q_us", "class_pin_us")
 
 
 def load(path: str | None = None, profile: Dict[str, Any] | None = None) -> Dict[str, Any]:
