@@ -46,6 +46,12 @@ MI355X_PROFILE: Dict[str, Any] = dict(
     # 2 s) joins an already time-shared memory region instead of splitting
     # the compute region (phase-ts +0.016, s26; engine.cpp budget_layout)
     class_pin_us=2000000,
+    # a time-shared class region rotates at >= 30 ms whatever its classes: a
+    # switch drains the outgoing tenant's tiles and refills the L2s, so on the
+    # GPU the throughput cost falls with the quantum (8mix 1.354 -> 1.378, s32;
+    # phase / phase-ts / 4mix level).  The per-tenant PBS quantum still rules
+    # the partitions a tenant holds alone.
+    shared_q_us=30000,
     adapt=dict(threshold=20000, band_lo=70, band_hi=130, min_us=1000, max_us=11000, inc_us=1000, dec_us=2000,
                switch_boundary=9000, ticks_per_tslice=3,
                # grow_pct > 0: proportional growth + a restart at the class bound

@@ -101,7 +101,7 @@ def test_budget_follows_phase_change_and_a_stopped_tenant():
 
 
 def test_budget_time_shares_a_crowded_class_region():
-    e, parts = _engine()
+    e, parts = _engine(shared_q_us=0)  # PBS region quanta: shares even out within the 200 ms window
     g = e.tenant_create("gemm", nslots=32)
     mem = [e.tenant_create(f"m{i}", nslots=32) for i in range(3)]
     rates = {g: COMPUTE, **{m: MEMORY for m in mem}}
@@ -226,7 +226,7 @@ def test_time_shared_region_steals_no_stacking_siblings():
     for ss in (1, 0):
         # the reference's additive quantum steps: the steal pattern this
         # guards against was traced with them (round 4)
-        e, parts = _engine(sibling_steal=ss, adapt=dict(MI355X_PROFILE["adapt"], grow_pct=0))
+        e, parts = _engine(sibling_steal=ss, adapt=dict(MI355X_PROFILE["adapt"], grow_pct=0), shared_q_us=0)
         ws = (512, 256, 256, 256, 256, 256, 256)  # a heavier tenant keeps UNDER slots queued on busy peers
         ts = [e.tenant_create(f"t{i}", nslots=32, weight=w) for i, w in enumerate(ws)]
         rates = {t: (COMPUTE if i < 3 else MEMORY) for i, t in enumerate(ts)}
@@ -394,3 +394,24 @@ def test_atc_keeps_the_class_budget_layout():
     assert busy == n and foreign == 0, (busy, n, foreign)
     assert [e.tenant_info(t).budget_ctx & 0xF for t in ts] == [0x3, 0x4, 0x8]
     assert e.check() == ""
+
+
+def test_shared_region_quantum_floor():
+    """shared_q_us (MI355X profile 30 ms): a time-shared class region rotates
+    at least that long -- three GEMM tenants sharing the compute region
+    switch every 30 ms, not at their 1 ms PBS floor; 0 keeps the PBS
+    region quantum (the largest adaptive quantum of the co-sharers)."""
+    out = {}
+    for sq in (0, 30000):
+        e, parts = _engine(shared_q_us=sq)
+        ts = [e.tenant_create(f"g{i}", nslots=32) for i in range(3)] + [e.tenant_create("hbm", nslots=32)]
+        rates = {t: (COMPUTE if i < 3 else MEMORY) for i, t in enumerate(ts)}
+        for t in ts:
+            e.wake(t)
+        _settle(e, rates, 600)
+        e.trace(from_start=True)
+        _settle(e, rates, 1000)
+        q = [r.a[2] for r in e.trace() if r.event == "SWITCH" and r.a[1] in ts[:3]]
+        out[sq] = sorted(q)[len(q) // 2] if q else 0
+        assert e.check() == ""
+    assert out[0] <= 2000 and out[30000] >= 30000, out
