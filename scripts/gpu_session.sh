@@ -5,8 +5,8 @@
 set -o pipefail
 O=gpurun_out/r5
 mkdir -p $O
-S=${1:-s31}
-for M in 8mix phase-ts phase 4mix; do
-  timeout -k 10 300 python -u bench.py --mix $M --reps 3 --policies gpbs,atc,credit-fixed-ts30,gpbs-w \
-    --out $O/${S}_$M.json > $O/${S}_$M.out 2> $O/${S}_$M.log || exit $?
-done
+S=${1:-s33}
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread -p no:cacheprovider \
+  > $O/${S}_gputests.log 2>&1 &&
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/${S}_smoke.log 2>&1 &&
+timeout -k 10 700 python -u bench.py --out $O/${S}_bench.json > $O/${S}_bench.out 2> $O/${S}_bench.log
