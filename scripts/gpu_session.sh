@@ -5,8 +5,6 @@
 set -o pipefail
 O=gpurun_out/r5
 mkdir -p $O
-S=${1:-s33}
-timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread -p no:cacheprovider \
-  > $O/${S}_gputests.log 2>&1 &&
+S=${1:-s34}
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/${S}_smoke.log 2>&1 &&
 timeout -k 10 700 python -u bench.py --out $O/${S}_bench.json > $O/${S}_bench.out 2> $O/${S}_bench.log
