@@ -3,16 +3,10 @@
 # with && so the first failure ends the session.  Overwritten per session;
 # the commit history holds the earlier ones.
 set -o pipefail
-R=$(pwd)
-O=$R/gpurun_out/r5
+O=gpurun_out/r5
 mkdir -p $O
-S=${1:-s35}
-export TMPDIR=/tmp
-# solo PMC of the default GEMM (2-D per-XCD tile blocks, opts 205064) and of the previous default (205056)
-timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE \
-  -d $O/${S}_pmc_2d -o gemm --output-format csv -- python3 $R/scripts/gemm_only.py 4096 205064 > $O/${S}_pmc_2d.log 2>&1 &&
-timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE \
-  -d $O/${S}_pmc_2d_l2 -o gemm --output-format csv -- python3 $R/scripts/gemm_only.py 4096 205064 > $O/${S}_pmc_2d_l2.log 2>&1 &&
-timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE \
-  -d $O/${S}_pmc_rr_l2 -o gemm --output-format csv -- python3 $R/scripts/gemm_only.py 4096 205056 > $O/${S}_pmc_rr_l2.log 2>&1 &&
-KBENCH_GEMM_ONLY=1 timeout -k 10 150 python -u scripts/kbench.py > $O/${S}_kbench.jsonl 2> $O/${S}_kbench.log
+S=${1:-s36}
+# 8-rank --rehearse-ipc of the headline mix on one GPU (every rank on cuda:0), final tree
+timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29535 \
+  bench.py --gpus 8 --mix 4mix --steps 3 --warmup 1 --reps 1 --rehearse-ipc --policies none,gpbs --hang-dump-s 120 \
+  --out $O/${S}_rehearse8.json > $O/${S}_rehearse8.out 2> $O/${S}_rehearse8.log
