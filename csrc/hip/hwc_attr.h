@@ -54,6 +54,32 @@ struct HwcAttrOut {
 
 __host__ __device__ inline u64 attr_dpos(u64 a, u64 b) { return a >= b ? a - b : 0; }  // Q5
 
+// HwcAttrIn::drained for the interval (used_t, snap_t] (host): bit p when the
+// partition's owner at the interval's first sample had held it for at least
+// `guard` (its predecessor's tiles are gone) AND that owner is the only one
+// that can be the interval's >= clean_pct owner -- no owner change landed in
+// the first (100 - clean_pct) % of the interval.  A change there hands the
+// window to a new owner whose predecessor was still running and draining at
+// its head (with only the first condition, up to 20 % of another
+// tenant's counts reached the new owner's clean window).  used_chg / snap_chg:
+// each partition's last owner-change time as of the opening / closing sample.
+// Intervals shorter than three guards get no bits: a drain that outlasts the
+// guard must stay a small part of the window.
+inline u32 hwc_drained_bits(int64_t used_t, int64_t snap_t, const int64_t* used_chg, const int64_t* snap_chg,
+                            int64_t guard, u32 clean_pct) {
+  if (used_t <= 0 || snap_t - used_t < 3 * guard) return 0;
+  const int64_t span = snap_t - used_t;
+  const int64_t head = clean_pct <= 100 ? (int64_t)(100 - clean_pct) : 0;
+  u32 dr = 0;
+  for (int p = 0; p < kAttrP; ++p) {
+    if (used_t - used_chg[p] < guard) continue;
+    const int64_t chg = snap_chg[p];
+    if (chg > used_t && (chg - used_t) * 100 <= head * span) continue;
+    dr |= 1u << p;
+  }
+  return dr;
+}
+
 inline void hwc_attr_prev_init(HwcAttrPrev& st) {
   for (int i = 0; i < kAttrP * kNumPmc; ++i) st.se[i] = 0;
   for (int i = 0; i < kXcds * kNumPmc; ++i) st.x[i] = 0;

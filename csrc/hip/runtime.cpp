@@ -27,6 +27,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <deque>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -1006,12 +1007,11 @@ void hwc_fill_in(GpuCtx* c, HwcAttrIn& in) {
   // whose last owner change came at least a guard before it starts clean --
   // in an interval of at least three guards, so a drain that outlasts the
   // guard stays a small part of the window
+  // (and no owner change in the interval's head: hwc_drained_bits)
   u32 dr = 0;
-  const int64_t guard = guard_ns(c);
-  if (c->used_t && c->used_chg.size() == (size_t)kAttrP && c->snap_t - c->used_t >= 3 * guard) {
-    for (int p = 0; p < kAttrP; ++p)
-      if (c->used_t - c->used_chg[p] >= guard) dr |= 1u << p;
-  }
+  if (c->used_chg.size() == (size_t)kAttrP && c->snap_chg.size() == (size_t)kAttrP)
+    dr = hwc_drained_bits(c->used_t, c->snap_t, c->used_chg.data(), c->snap_chg.data(), guard_ns(c),
+                          (u32)c->clean_pct);
   in.drained = dr;
 }
 
@@ -2537,7 +2537,11 @@ int gpbs_hip_hwc_attr_host_check(int seed, int iters, double* out2) {
 // or fresh unclean period is skipped, a sliver never counts.  No HIP call.
 // Returns 0 or the number of the first failed check.
 int gpbs_hip_hwc_fold_selftest(void) {
-  static GpuCtx c;  // host fields only; nothing here touches the device
+  // a fresh context per call (host fields only; nothing here touches the
+  // device): the per-tenant period counts, calibration and last clean window
+  // start from zero however often the check runs in one process
+  std::unique_ptr<GpuCtx> cp(new GpuCtx());
+  GpuCtx& c = *cp;
   std::memset(c.last_delta, 0, sizeof(c.last_delta));
   c.clean_pct = 80;
   const int t = 3;
@@ -2602,6 +2606,50 @@ int gpbs_hip_hwc_fold_selftest(void) {
     if (in != 0) return 6;
   }
   if (c.t_clean[t] != 20 || c.t_fallback[t] != 20 || c.t_sliver[t] != 20 || c.t_skipped[t] != 21) return 7;
+  return 0;
+}
+
+// Host check of hwc_drained_bits: random owner-change times per
+// partition around an interval; a bit may be set only when the opening owner
+// had held the partition a guard and no change landed in the interval's head,
+// and must be set when both hold.  Also the two cases named in the advice:
+// a takeover at the head (no bit) and a switch-aligned close at the tail (bit).
+// Returns 0 or the number of the first failed check.  No HIP call.
+int gpbs_hip_hwc_drained_selftest(int seed, int iters) {
+  uint64_t r = 0x2545F4914F6CDD1Dull ^ (uint64_t)seed;
+  auto rnd = [&]() {
+    r ^= r << 13;
+    r ^= r >> 7;
+    r ^= r << 17;
+    return r;
+  };
+  int64_t used_chg[kAttrP], snap_chg[kAttrP];
+  const int64_t guard = 150000;
+  for (int it = 0; it < iters; ++it) {
+    const int64_t used_t = 1000000000 + (int64_t)(rnd() % 1000000);
+    const int64_t span = (int64_t)(rnd() % 8000000);
+    const int64_t snap_t = used_t + span;
+    const u32 cp = it % 5 == 4 ? 0u : (it % 2 ? 80u : 90u);
+    for (int p = 0; p < kAttrP; ++p) {
+      used_chg[p] = used_t - (int64_t)(rnd() % (4 * guard));
+      const int kind = (int)(rnd() % 3);  // no change / change in the interval
+      snap_chg[p] = kind == 0 ? used_chg[p] : used_t + 1 + (int64_t)(rnd() % (uint64_t)(span + 1));
+    }
+    const u32 dr = hwc_drained_bits(used_t, snap_t, used_chg, snap_chg, guard, cp);
+    for (int p = 0; p < kAttrP; ++p) {
+      const bool settled = used_t - used_chg[p] >= guard;
+      const bool head = snap_chg[p] > used_t && (snap_chg[p] - used_t) * 100 <= (int64_t)(100 - cp) * span;
+      const bool want = span >= 3 * guard && settled && !head;
+      if ((((dr >> p) & 1u) != 0) != want) return 1;
+    }
+  }
+  // the advice's two cases, 4 ms interval, clean_pct 80
+  for (int p = 0; p < kAttrP; ++p) used_chg[p] = 1000000000 - 2 * guard;
+  const int64_t t0 = 1000000000, t1 = t0 + 4000000;
+  for (int p = 0; p < kAttrP; ++p) snap_chg[p] = t0 + 300000;  // B takes over 0.3 ms in: B holds 92 %
+  if (hwc_drained_bits(t0, t1, used_chg, snap_chg, guard, 80) != 0) return 2;
+  for (int p = 0; p < kAttrP; ++p) snap_chg[p] = t1 - guard;  // A's tenure ends one guard before the close
+  if (hwc_drained_bits(t0, t1, used_chg, snap_chg, guard, 80) != 0xFFFFFFFFu) return 3;
   return 0;
 }
 

@@ -150,21 +150,44 @@ def ranks_digest(ranks: List[dict]) -> dict:
 
 def compact_line(full: dict, digests: Dict[str, dict], detail_path: str = "") -> dict:
     """The stdout line: the contract fields of `full`, the per-mix digests
-    and the ranks digest.  Raises if the result is over MAX_LINE_BYTES."""
+    and the ranks digest, at most MAX_LINE_BYTES.  An oversized line degrades
+    step by step instead of failing (a raise on rank 0 before the final
+    barrier would leave the other ranks waiting in it): the least
+    important digest fields go first, then the per-rank failure list is cut,
+    then the non-headline mixes keep only their policy medians; the contract
+    fields always stay."""
     keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
             "scaling", "vs_baseline", "dtype", "data", "config", "mean_slowdown_pct", "counters")
     line = {k: full[k] for k in keep if k in full}
     line["reps"] = full.get("protocol", {}).get("reps")
-    line["mixes"] = digests
+    line["mixes"] = {m: dict(d) for m, d in digests.items()}
     line["ranks"] = ranks_digest(full.get("ranks") or [])
     if detail_path:
         line["detail"] = detail_path
-    n = len(json.dumps(line))
-    if n > MAX_LINE_BYTES:  # drop the least important digest fields first
-        for m in line["mixes"].values():
-            for k in ("tslice_us_by_class", "lat_p50_ms", "quantum_at_bound"):
-                m.pop(k, None)
-        n = len(json.dumps(line))
-    if n > MAX_LINE_BYTES:
-        raise ValueError(f"bench line is {n} bytes (> {MAX_LINE_BYTES})")
+    head = next(iter(line["mixes"]), None)
+
+    def size() -> int:
+        return len(json.dumps(line))
+
+    steps = [
+        lambda: [m.pop(k, None) for m in line["mixes"].values()
+                 for k in ("tslice_us_by_class", "lat_p50_ms", "quantum_at_bound")],
+        lambda: [m.pop(k, None) for n, m in line["mixes"].items() if n != head
+                 for k in ("hw", "dispatched_q_us", "slo")],
+        lambda: line["ranks"].update(failures=line["ranks"]["failures"][:2],
+                                     n_failed=len(line["ranks"]["failures"])),
+        lambda: [line["mixes"].__setitem__(n, {k: v for k, v in m.items()
+                                               if k in ("gpbs", "none", "static-se", "best_ablation")})
+                 for n, m in list(line["mixes"].items()) if n != head],
+        lambda: line.update(data=str(line.get("data", ""))[:160], unit=str(line.get("unit", ""))[:160]),
+        lambda: line["mixes"].__setitem__(head, {k: v for k, v in line["mixes"][head].items()
+                                                 if k in ("gpbs", "none", "static-se", "best_ablation")})
+        if head else None,
+        lambda: line.update(mixes={head: line["mixes"][head]} if head else {}),
+        lambda: line.update(ranks={"n": line["ranks"].get("n"), "n_failed": len(line["ranks"].get("failures", []))}),
+    ]
+    for st in steps:
+        if size() <= MAX_LINE_BYTES:
+            break
+        st()
     return line

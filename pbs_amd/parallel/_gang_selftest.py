@@ -237,6 +237,24 @@ def gang_bench_worker(rank, world, name, iters, q):
     q.put((rank, lat[iters // 10:]))  # drop warm-up
 
 
+def spin_barrier_worker(rank, world, arr, iters, q):
+    """Host-noise baseline for the gang gate (tests/test_microbench.py): the
+    same back-to-back barrier among `world` processes, as a plain Python spin
+    on a shared counter array -- no gang code at all.  A loaded host slows it
+    the way it slows the native epoch, so the gate compares against it."""
+    lat = []
+    for i in range(1, iters + 1):
+        t0 = time.monotonic_ns()
+        arr[rank] = i
+        deadline = t0 + (60_000_000_000 if i == 1 else 10_000_000_000)
+        while min(arr[:world]) < i:
+            if time.monotonic_ns() > deadline:
+                q.put((rank, None))
+                raise RuntimeError("spin barrier timeout")
+        lat.append(time.monotonic_ns() - t0)
+    q.put((rank, lat[iters // 10:]))
+
+
 def gloo_bench_worker(rank, world, port, iters, q):
     import torch
     import torch.distributed as dist

@@ -61,6 +61,7 @@ def summ_us(ns):
 # ---------------------------------------------------------------- gang
 from pbs_amd.parallel._gang_selftest import gang_bench_worker as _gang_worker  # noqa: E402
 from pbs_amd.parallel._gang_selftest import gloo_bench_worker as _gloo_worker  # noqa: E402
+from pbs_amd.parallel._gang_selftest import spin_barrier_worker as _spin_worker  # noqa: E402
 
 
 def _port():
@@ -90,9 +91,15 @@ def _spawn(target, world, args):
     return lat
 
 
-def bench_gang(worlds=(2, 4, 8), iters=3000, gloo=True):
+def bench_gang(worlds=(2, 4, 8), iters=3000, gloo=True, baseline=False):
+    """``baseline``: also a plain Python shared-counter spin barrier among the
+    same processes (``spin_w{W}``), measured right before: the host-noise
+    reference the relative gate uses."""
     out = {}
     for w in worlds:
+        if baseline:
+            arr = mp.get_context("spawn").Array("q", [0] * w, lock=False)
+            out[f"spin_w{w}"] = summ_us(_spawn(_spin_worker, w, (arr, iters)))
         name = f"gpbs-mb-{os.getpid()}-{w}"
         out[f"shm_w{w}"] = summ_us(_spawn(_gang_worker, w, (name, iters)))
         if gloo:
@@ -172,7 +179,14 @@ def gates(res):
     h = res.get("hwc", {})
     if "sample" in h:
         vals["hwc_sample_p50_us"] = h["sample"]["p50_us"]
-    return {k: (v, THRESHOLDS[k], v <= THRESHOLDS[k]) for k, v in vals.items()}
+    lim = dict(THRESHOLDS)
+    # relative gate: on a loaded host the native epoch may be as slow as 3x a
+    # plain Python spin barrier among the same processes measured just before
+    # (an idle host keeps the absolute thresholds)
+    if "spin_w4" in g:
+        lim["gang_shm_w4_p50_us"] = max(lim["gang_shm_w4_p50_us"], 3.0 * g["spin_w4"]["p50_us"])
+        lim["gang_shm_w4_p99_us"] = max(lim["gang_shm_w4_p99_us"], 3.0 * g["spin_w4"]["p99_us"])
+    return {k: (v, lim[k], v <= lim[k]) for k, v in vals.items()}
 
 
 def main():

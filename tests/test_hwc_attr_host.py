@@ -43,6 +43,20 @@ def test_metric_fold_calibrated_fallback_keeps_the_class():
     the edge of another tenure (a sliver) never counts."""
     from pbs_amd.ops import kernels as K
     assert K.lib().gpbs_hip_hwc_fold_selftest() == 0
+    assert K.lib().gpbs_hip_hwc_fold_selftest() == 0  # a second call in the same process (fresh context)
+
+
+def test_drained_bit_needs_the_opening_owner_to_be_the_clean_one():
+    """The drained bit of a clean window (csrc/hip/hwc_attr.h
+    hwc_drained_bits): set only when the partition's owner at the
+    interval's first sample had held it a drain guard AND no owner change
+    landed in the interval's first (100 - clean_pct) %, so a tenant that takes
+    a partition over at the head of an interval never gets a clean window
+    holding its predecessor's head and drain; a switch-aligned close (the
+    change one guard before the closing sample) keeps its window."""
+    from pbs_amd.ops import kernels as K
+    for seed in (1, 5, 9):
+        assert K.lib().gpbs_hip_hwc_drained_selftest(seed, 2000) == 0
 
 
 def test_kernel_trace_is_off_unless_enabled_before_init():

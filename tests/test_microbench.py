@@ -14,18 +14,19 @@ _spec.loader.exec_module(MB)
 
 def test_gang_epoch_barrier_latency():
     """Native shm gang epoch among 4 node-local ranks, back to back.  The
-    ranks busy-poll: the gate is a latency bound only on a host with 4 idle
-    CPUs (it is skipped when other work -- pytest -n -- occupies them)."""
-    ncpu = len(os.sched_getaffinity(0))
-    if ncpu < 4 or os.getloadavg()[0] > ncpu - 4:
-        pytest.skip(f"host busy (load {os.getloadavg()[0]:.1f} on {ncpu} CPUs): latency gate not meaningful")
+    gate always runs: it is the absolute threshold on an idle host, and
+    relative to a plain Python spin barrier among the same number of
+    processes, measured in the same call, when the host is loaded (pytest -n,
+    other jobs) -- the baseline suffers the same preemption, so the gate
+    still catches a native epoch that got slower than it."""
     # a preempted poller shows up as a p99 outlier: one re-measurement before
     # the gate fails (the p50 gate is what a real regression moves)
     for attempt in range(2):
-        res = MB.bench_gang(worlds=(4,), iters=2000, gloo=False)
+        res = MB.bench_gang(worlds=(4,), iters=2000, gloo=False, baseline=True)
         g = MB.gates({"gang": res})
         if all(ok for _, _, ok in g.values()):
             break
+    assert "spin_w4" in res and res["spin_w4"]["n"] > 0
     for k, (v, lim, ok) in g.items():
         assert ok, (k, v, lim, res)
 
