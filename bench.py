@@ -79,6 +79,7 @@ def mix_summary(mix, runs, solo, reps):
             pol[p]["mean_tslice_us_by_class"] = {c: round(q(v, 0.5), 1) for c, v in sorted(by.items())}
         if "idle" in rs[0]["tenants"]:
             pol[p]["idle_p50_ms"] = round(q([r["tenants"]["idle"]["p50_ms"] for r in rs], 0.5), 4)
+            pol[p]["idle_p99_ms"] = round(q([r["tenants"]["idle"]["p99_ms"] for r in rs], 0.5), 4)
     # drift over the mix's runs (chronological): the last five gpbs runs
     # against the first five, and the GPU state of the first and last run
     xs = [r["aggregate_all_gpus"] for r in runs["gpbs"]]
@@ -101,6 +102,12 @@ def mix_summary(mix, runs, solo, reps):
            "mean_slowdown_pct": round(q([r["mean_slowdown_pct"] for r in runs["gpbs"]], 0.5), 2),
            "reps": max(1, reps), "policies": pol, "per_tenant": g["tenants"], "engine": g.get("engine", {}),
            "ms_per_step": round(g["ms_per_step"], 3), "solo": solo, "drift": out_drift, "gpu_state": out_gs}
+    from pbs_amd.bench.corun import MIXES
+    if MIXES.get(mix, {}).get("slo_p99_ms"):  # in-region latency tenant: its p99 target
+        out["slo"] = MIXES[mix]["slo_p99_ms"]
+        for p, v in pol.items():
+            if "idle_p99_ms" in v:
+                v["slo_met"] = v["idle_p99_ms"] <= out["slo"]
     if "static-se" in runs:
         a, b = pol["gpbs"]["aggregate_all_gpus"], pol["static-se"]["aggregate_all_gpus"]
         out["gpbs_vs_static_se"] = {"delta_median": round(a["median"] - b["median"], 4),
@@ -156,7 +163,7 @@ def main():
                     help="PBS metric source: live CDNA4 hardware counters (rocprofiler-sdk device counting, "
                          "attributed to tenants by shader-engine ownership; default), or the modeled per-tile "
                          "counters of the tenant kernels (debug cross-check)")
-    ap.add_argument("--mix", default="all", choices=["all", "4mix", "gemm2", "phase", "phase-ts", "8mix", "llm5"],
+    ap.add_argument("--mix", default="all", choices=["all", "4mix", "gemm2", "phase", "phase-ts", "8mix", "slo", "llm5"],
                     help="all (default): 4mix (headline, BASELINE config #3) + phase (phase-changing mix) + "
                          "phase-ts (the phase mix with a time-shared memory region, where the adaptive quantum "
                          "matters) + 8mix (config #4's 8 tenants on one GPU); gemm2: config #2 (two 4096^2 GEMM "
@@ -282,7 +289,7 @@ def main():
         dist.broadcast(nonce, src=0, group=groups["ctrl"])
         gang_base = f"gpbs-gang-{int(nonce.item()):08x}"
 
-    mixes = ["4mix", "phase", "phase-ts", "8mix"] if args.mix == "all" else [args.mix]
+    mixes = ["4mix", "phase", "phase-ts", "8mix", "slo"] if args.mix == "all" else [args.mix]
     log = (lambda *a: print(*a, file=sys.stderr, flush=True))
     import random
 
@@ -342,11 +349,16 @@ def main():
 
     results = {}
     for mix in mixes:
-        default = {"4mix": "none,static,static-se,credit-fixed,gpbs-nolane,gpbs-lat,gpbs",
+        # time-shared mixes (phase-ts, 8mix, slo) carry the long-quantum
+        # ablations: one 30 ms quantum for all
+        # (credit-fixed-ts30), the class map with the 30 ms floor
+        # (credit-classq-f), ATC, and round 5's region quantum (gpbs-sq30)
+        default = {"4mix": "none,static-se,credit-fixed,gpbs-lat,gpbs",
                    "gemm2": "none,static,static-se,credit-fixed,gpbs",
                    "phase": "none,static-se,credit-fixed,gpbs",
-                   "phase-ts": "none,static-se,credit-fixed-ts,credit-classq,gpbs",
-                   "8mix": "none,static-se,credit-fixed-ts,credit-classq,gpbs-split,atc,gpbs"}[mix]
+                   "phase-ts": "none,static-se,credit-fixed-ts30,credit-classq-f,atc,gpbs-sq30,gpbs",
+                   "8mix": "none,static-se,credit-fixed-ts30,credit-classq-f,gpbs-split,atc,gpbs-sq30,gpbs",
+                   "slo": "none,static-se,credit-fixed-ts30,credit-classq-f,atc,gpbs"}[mix]
         spec = args.policies if (args.policies and mix == mixes[0]) else default
         pols = tuple(p for p in spec.split(",") if p)
         reps = args.reps if mix == mixes[0] else args.reps_extra
@@ -361,7 +373,8 @@ def main():
              "phase": "phase-changing mix (GEMM + GEMM<->stream phase tenant + on/off stream + idle)",
              "phase-ts": "time-shared phase mix (GEMM + GEMM<->stream phase tenant + on/off stream + stream + "
                          "reduce + idle)",
-             "8mix": "8-tenant mix (3 GEMMs + 3 streams + all-reduce + idle)"}
+             "8mix": "8-tenant mix (3 GEMMs + 3 streams + all-reduce + idle)",
+             "slo": "latency-SLO mix (GEMM + 2 HBM streams + MALL-resident stream + in-region latency tenant)"}
     line = {
         "metric": base["metric"],
         "value": hs["value"],

@@ -134,6 +134,12 @@ void gpbs_boot_defaults(gpbs_boot_params_t* p) {
   p->class_fall = 0;
   p->shared_q_us = 0;
   p->class_pin_us = 0;
+  p->region_q = 0;
+  p->switch_floor_x = 0;
+  p->switch_floor_max_us = 0;
+  p->region_vt = 0;
+  p->slo_cap = 0;
+  p->probe_max_us = 0;
   AdaptParams a;
   std::memcpy(&p->adapt, &a, sizeof(a));
   AtcParams t;
@@ -439,6 +445,8 @@ int gpbs_tenant_info(gpbs_engine_t* e, int t, gpbs_tenant_info_t* o) {
   }
   o->budget_ctx = d->budget_ctx;
   o->budget_shared = d->budget_shared;
+  o->switch_cost_us = d->sw_cost_us;
+  o->slo_us = d->slo_us;
   return GPBS_OK;
 }
 
@@ -515,6 +523,23 @@ int gpbs_tenant_measure(gpbs_engine_t* e, int t, uint32_t us) {
   if (!d) return GPBS_ENOENT;
   if (us != UINT32_MAX) d->measure_us = us;
   return (int)std::min<uint64_t>(d->measure_granted, INT32_MAX);
+}
+
+int gpbs_tenant_switch_cost(gpbs_engine_t* e, int t, uint64_t ns) {
+  LOCK(e);
+  Tenant* d = live(e, t);
+  if (!d) return GPBS_ENOENT;
+  d->sw_cost_us = (uint32_t)std::min<uint64_t>((ns + 500) / 1000, 1000000);
+  return GPBS_OK;
+}
+
+int gpbs_tenant_slo(gpbs_engine_t* e, int t, uint32_t us) {
+  LOCK(e);
+  Tenant* d = live(e, t);
+  if (!d) return GPBS_ENOENT;
+  if (us > (uint32_t)GPBS_TSLICE_UMAX) return GPBS_ERANGE;
+  d->slo_us = us;
+  return GPBS_OK;
 }
 
 int gpbs_tenant_heartbeat(gpbs_engine_t* e, int t) {

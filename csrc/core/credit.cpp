@@ -83,6 +83,14 @@ struct CDom : SchedTenantData {
   uint64_t cache_miss_rate = 0, cpi = 0;
   uint64_t rate_ewma = 0;  // smoothed miss rate (alpha 1/4) for contention classes
   uint64_t bound_periods = 0, bound_min = 0, bound_max = 0;  // measured periods / at min_us / at max_us
+  // The quantum the dispatcher actually gave the tenant (s_timer, before the
+  // quantum_align grid and measurement tenures): last one, and since when
+  // (the reported quantum is the dispatched one; the
+  // adaptive target stays in adapt.tslice_us)
+  uint32_t q_disp_us = 0;
+  // region virtual time (boot region_vt): partition-ns the tenant ran in its
+  // time-shared class region, x 256 / weight
+  int64_t rvt = 0;
   AtcState atc{};
 };
 
@@ -92,7 +100,7 @@ struct CPcpu : SchedPartData {
   int ticker = -1;
   int metric_ticker = -1;
   uint32_t tick = 0;
-  int idle_bias = 0;
+  int idle_bias = 0;  int64_t rvt_mark = 0;  // region virtual time: the current runner is accounted up to here
 };
 
 class CreditScheduler : public Scheduler {
@@ -156,44 +164,85 @@ class CreditScheduler : public Scheduler {
   CDom& sd(Tenant& d) { return *static_cast<CDom*>(d.priv.get()); }
   CDom& sd_of(Slot& v) { return sd(*E.tenants[v.tenant]); }
 
-  // PBS quantum of a slot (:1796-1804).  A tenant in a time-shared class
-  // region (class_budget 1, budget_shared) runs the REGION's quantum: the
-  // largest adaptive quantum among the present co-sharers of its class, so
-  // the region rotates in equal turns.  Per-tenant quanta there are unfair
-  // under credit: a co-sharer that sees no clean counter window keeps the
-  // floor quantum (Q14 skips its periods) while its partners hold 11 ms, and
-  // credit round-robins in quanta -- 2.2 vs 5.8 of 16 partitions in
-  // simulation (tests/test_budget_layout.py), a memory tenant at 0.006 of
-  // the time on MI355X (profiles/r3/bench_full_5rep_c.json, 8mix, gpbs).
-  // The class region is one gang; its quantum still follows the counters.
-  uint32_t pbs_quantum_us(Slot& v) {
-    const Tenant& t = *E.tenants[v.tenant];
-    uint32_t q = sd(*E.tenants[v.tenant]).adapt.tslice_us;
-    if (!t.budget_shared || t.cls < 0) return q;
-    // co-sharers: the tenants laid out in the same class region (a flapping
-    // tenant pinned to the memory region by class_pin_us counts there)
-    const int lc = t.lay_cls >= 0 ? t.lay_cls : t.cls;
-    for (auto& tp : E.tenants)
-      if (tp && tp->alive && tp->priv && tp->pool == t.pool && tp->budget_shared && tp->cls >= 0 &&
-          (tp->lay_cls >= 0 ? tp->lay_cls : tp->cls) == lc && tp->budget_ctx != 0)
-        q = std::max(q, sd(*tp).adapt.tslice_us);
-    // shared_q_us: a time-shared region rotates at least this long -- a
-    // switch drains the outgoing tenant's in-flight tiles and the incoming
-    // one refills the XCDs' L2s, so on a GPU the cost falls with the quantum
-    // whatever the class (8mix: 30 ms for all 1.359 vs PBS 1 / 11 ms 1.331, s31)
-    if (E.boot.shared_q_us > 0) q = std::max(q, (uint32_t)E.boot.shared_q_us);
-    return q;
+  // ------------------------------------------------------- the quantum --
+  // A time-shared class region (class_budget 1, budget_shared): every tenant
+  // laid out there holds every partition of it, and they take turns.
+  static int region_cls(const Tenant& t) { return t.lay_cls >= 0 ? t.lay_cls : t.cls; }
+  static bool shared_region(const Tenant& t) { return t.budget_shared && region_cls(t) >= 0; }
+  bool cosharer(const Tenant& t, const Tenant& o) const {
+    return o.alive && o.priv && o.pool == t.pool && shared_region(o) && region_cls(o) == region_cls(t) &&
+           o.budget_ctx != 0;
   }
   // credit-classq: the class's bound (unknown class: the global quantum)
   uint32_t classq_us(const Tenant& t) const {
     return t.cls == 1 ? E.adapt_params.max_us : (t.cls == 0 ? E.adapt_params.min_us : tslice_us_);
   }
-  // The quantum a tenant runs with in this mode (fill_tenant_info, bound stats).
-  uint32_t mode_quantum_us(Tenant& t) {
+  // The policy's own quantum for a tenant: PBS its adaptive tslice (:1796-1804),
+  // classq its class's bound, otherwise the pool's global quantum.
+  uint32_t target_us(Tenant& t) {
     if (mode_ == Mode::PBS) return sd(t).adapt.tslice_us;
     if (mode_ == Mode::CLASSQ) return classq_us(t);
     return tslice_us_;
   }
+  // Per-tenant switch-cost floor (boot switch_floor_x): a tenant whose every
+  // switch costs c (its revoked tiles drain, then its grid ramps back in --
+  // measured by the GPU runtime per tenant) loses c / q of each turn, so its
+  // quantum is kept at >= x * c (x = 25: at most 4 % of a turn lost).  The
+  // GPU's stand-in for the reference's cache-warmth argument (a cache-
+  // sensitive domain gets the longer slice, :294-300): what a switch costs is
+  // measured per tenant instead of inferred from its miss rate.
+  uint32_t switch_floor_us(const Tenant& t) const {
+    if (E.boot.switch_floor_x <= 0 || !t.sw_cost_us) return 0;
+    const uint32_t cap = E.boot.switch_floor_max_us > 0 ? (uint32_t)E.boot.switch_floor_max_us : E.adapt_params.max_us;
+    uint64_t f = std::min<uint64_t>((uint64_t)t.sw_cost_us * (uint64_t)E.boot.switch_floor_x, cap);
+    if (E.boot.quantum_align_us > 0) {
+      const uint64_t a = (uint64_t)E.boot.quantum_align_us;
+      f = (f + a - 1) / a * a;
+    }
+    return (uint32_t)f;
+  }
+  // SLO cap (boot slo_cap): a co-sharer of a region that holds a tenant with a
+  // latency target gets at most that target minus one ratelimit as its
+  // quantum, so a request of the target tenant that arrives during the
+  // co-sharer's turn (and cannot preempt it: no BOOST for an OVER slot, or a
+  // strict_ref ratelimit hold) waits at most the target for the region.
+  uint32_t slo_cap_us(const Tenant& t) {
+    uint32_t cap = UINT32_MAX;
+    for (auto& tp : E.tenants)
+      if (tp && tp.get() != &t && tp->slo_us && cosharer(t, *tp))
+        cap = std::min<uint32_t>(cap, tp->slo_us > ratelimit_us_ ? tp->slo_us - ratelimit_us_ : tp->slo_us);
+    return cap;
+  }
+  // The quantum a slot of tenant t is dispatched with (the s_timer of
+  // :1796-1804).  Outside a time-shared region: the policy's own quantum.
+  // Inside one, per tenant (boot region_q 0):
+  //   PBS     its adaptive quantum, at least its switch-cost floor;
+  //   classq  its class's bound, at least shared_q_us (the classq+floor
+  //           ablation) when that is set;
+  //   others  the global quantum;
+  // then capped by a latency-target co-sharer (slo_cap), never below min_us.
+  // region_q 1 keeps round 5's region quantum: the largest adaptive quantum
+  // among the co-sharers, floored at shared_q_us -- every co-sharer the same.
+  // Per-tenant quanta stay weight-fair through the region's virtual time
+  // (region_pick): a tenant with twice the quantum gets half the turns.
+  uint32_t quantum_us(Tenant& t) {
+    uint32_t q = target_us(t);
+    if (!shared_region(t)) return q;
+    if (mode_ == Mode::PBS && E.boot.region_q) {
+      for (auto& tp : E.tenants)
+        if (tp && tp->priv && cosharer(t, *tp)) q = std::max(q, sd(*tp).adapt.tslice_us);
+      if (E.boot.shared_q_us > 0) q = std::max(q, (uint32_t)E.boot.shared_q_us);
+      return q;
+    }
+    if (mode_ == Mode::PBS) q = std::max(q, switch_floor_us(t));
+    if (mode_ == Mode::CLASSQ && E.boot.shared_q_us > 0) q = std::max(q, (uint32_t)E.boot.shared_q_us);
+    if (E.boot.slo_cap) q = std::max(std::min(q, slo_cap_us(t)), std::min(q, E.adapt_params.min_us));
+    return q;
+  }
+  // What tenant_info / bound stats report: the quantum the tenant is
+  // dispatched with now (the s_timer quantum; the last one actually given is
+  // CDom::q_disp_us, tenant_info.last_dispatch_us).
+  uint32_t reported_us(Tenant& t) { return quantum_us(t); }
   Slot& curr(int cpu) { return E.curr_of(cpu); }
   Mask online() { return E.pools[pool_]->cpus; }
   // Another runnable slot of v's tenant on `cpu` (running there or queued).
@@ -549,8 +598,17 @@ class CreditScheduler : public Scheduler {
         CSlot& s = sv(v);
         s.credit += (int32_t)credit_fair;
         int32_t credit = s.credit;
+        // A BOOSTed waker that has not been dispatched yet keeps BOOST (gpbs
+        // extension; Xen's acct walks only vCPUs that ran since their last
+        // activation, here a latency tenant's slots stay on the active list
+        // between requests): demoting it here put a woken in-region latency
+        // tenant behind its co-sharers' gang rotation -- a request arriving
+        // during a ratelimit hold waited 16-20 ms on MI355X (slo mix traces,
+        // profiles/r6/slo_diag_summary.txt).  Its first tick while running
+        // demotes it (vcpu_acct), as before.
+        const bool waker = s.pri == PRI_BOOST && !v.is_running && !E.adapt_params.strict_ref;
         if (credit < 0) {
-          s.pri = PRI_OVER;
+          s.pri = waker ? PRI_BOOST : PRI_OVER;
           // Park running slots of capped-out tenants (launch gate closes).
           if (d.cap != 0 && credit < -(int32_t)credit_cap && !(s.flags & FLAG_PARKED)) {
             E.perfc.incr(PC_vcpu_park);
@@ -565,7 +623,7 @@ class CreditScheduler : public Scheduler {
             s.credit = credit;
           }
         } else {
-          s.pri = PRI_UNDER;
+          s.pri = waker ? PRI_BOOST : PRI_UNDER;
           if (s.flags & FLAG_PARKED) {
             E.perfc.incr(PC_vcpu_unpark);
             E.vcpu_unpause(v);
@@ -729,7 +787,7 @@ class CreditScheduler : public Scheduler {
                           : (3 * d.rate_ewma + d.cache_miss_rate) / 4;
       E.emit(TRC_METRIC, master_, (uint32_t)ids[k], (uint32_t)inst, (uint32_t)miss, (uint32_t)d.cache_miss_rate);
       if (inst) {  // a measured period: where the quantum sits
-        const uint32_t q = mode_quantum_us(*E.tenants[ids[k]]);
+        const uint32_t q = reported_us(*E.tenants[ids[k]]);  // the dispatched quantum
         d.bound_periods++;
         d.bound_min += q <= E.adapt_params.min_us;
         d.bound_max += q >= E.adapt_params.max_us;
@@ -1223,11 +1281,68 @@ class CreditScheduler : public Scheduler {
       if (c != cpu && E.parts[c]->gpu == P.gpu && E.parts[c]->xcd == P.xcd) E.raise_softirq(c);
   }
 
+  // Region virtual time (boot region_vt; gpbs extension).  In a time-shared
+  // class region the co-sharers' credit cannot order them: the pool's fair
+  // share of a slot (a whole partition per weight share) exceeds what a
+  // crowded region can give, so every co-sharer sits at the credit ceiling,
+  // UNDER, and the runqueue order alone rotates them -- one turn each, so a
+  // tenant's share would follow its quantum.  Instead the region keeps the
+  // partition-time each tenant ran there (per weight) and the next turn goes
+  // to the least-served runnable co-sharer (a BOOSTed waker still first).
+  // Per-tenant quanta then set how often a tenant switches, not its share.
+  // A tenant that returns from an absence is lifted to the region's floor
+  // minus two long quanta, so it cannot monopolise the region to catch up.
+  int64_t rvt_floor_[2] = {0, 0};
+  int64_t rvt_lag() const {
+    return 2 * (int64_t)std::max<uint32_t>({E.adapt_params.max_us, tslice_us_,
+                                            (uint32_t)std::max(0, E.boot.shared_q_us)}) * 1000;
+  }
+  void rvt_account(int cpu, Slot& cur, int64_t now) {
+    CPcpu& p = pc(cpu);
+    if (cur.is_idle() || !E.boot.region_vt) {
+      p.rvt_mark = now;
+      return;
+    }
+    Tenant& t = *E.tenants[cur.tenant];
+    const int64_t from = std::max(p.rvt_mark, cur.rs_entry);
+    p.rvt_mark = now;
+    if (!shared_region(t) || now <= from) return;
+    CDom& d = sd(t);
+    d.rvt += (now - from) * 256 / std::max<int64_t>(1, d.weight);
+  }
+  Slot* region_pick(int cpu, Slot& head, int64_t now) {
+    if (!E.boot.region_vt || head.is_idle() || sv(head).pri == PRI_BOOST) return nullptr;
+    Tenant& ht = *E.tenants[head.tenant];
+    if (!shared_region(ht)) return nullptr;
+    const int rc = region_cls(ht) & 1;
+    const int64_t lag = rvt_lag();
+    Slot* best = nullptr;
+    int64_t bv = 0;
+    for (int sid : pc(cpu).runq) {
+      Slot& v = *E.slots[sid];
+      if (v.is_idle()) continue;
+      const int16_t p = sv(v).pri;
+      if (p == PRI_BOOST) return nullptr;  // a waker goes first (the runq head)
+      if (p < PRI_OVER || xgang(v, now) == 2) continue;
+      Tenant& t = *E.tenants[v.tenant];
+      if (!cosharer(ht, t)) continue;
+      CDom& d = sd(t);
+      if (d.rvt < rvt_floor_[rc] - lag) d.rvt = rvt_floor_[rc] - lag;
+      if (!best || d.rvt < bv) {
+        best = &v;
+        bv = d.rvt;
+      }
+    }
+    if (best) rvt_floor_[rc] = std::max(rvt_floor_[rc], bv);
+    return best == &head ? nullptr : best;
+  }
+
   TaskSlice do_schedule(int cpu, int64_t now) override {
     Slot& scurr = curr(cpu);
     CSlot& cs = sv(scurr);
     const bool was_req = in_request(scurr, now) || (!scurr.is_idle() && !E.runnable(scurr));
     E.perfc.incr(PC_schedule);
+    rvt_account(cpu, scurr, now);
     int64_t runtime = now - scurr.rs_entry;
     if (runtime < 0) runtime = 0;
     if (!scurr.is_idle()) {
@@ -1276,6 +1391,14 @@ class CreditScheduler : public Scheduler {
           follow = true;
         }
       }
+      if (!follow) {
+        if (Slot* r = region_pick(cpu, *snext, now)) {  // least-served co-sharer of a time-shared region
+          rq.remove(r->id);
+          rq.push_front(r->id);
+          snext = r;
+          follow = true;  // picked by region time, not by credit priority: no steal
+        }
+      }
       if (!follow && E.boot.coschedule && !snext->is_idle()) {
         Slot* alt = cosched_pick(cpu);
         if (alt && xgang(*alt, now) != 2) {  // same priority class, less contention
@@ -1311,12 +1434,12 @@ class CreditScheduler : public Scheduler {
     if (held && !E.adapt_params.strict_ref) {
       tslice = std::max<int64_t>((int64_t)ratelimit_us_ * 1000 - runtime, 1000);
     } else if (!snext->is_idle()) {
-      if (mode_ == Mode::PBS)
-        tslice = (int64_t)pbs_quantum_us(*snext) * 1000;
-      else if (mode_ == Mode::CLASSQ)
-        tslice = (int64_t)classq_us(*E.tenants[snext->tenant]) * 1000;
-      else if (mode_ == Mode::ATC)
-        tslice = (int64_t)tslice_us_ * 1000;  // global slice (atc :1916)
+      // per-tenant quantum (PBS :1796-1804; classq; the global slice of
+      // credit-fixed and atc :1916), with the region floors / caps
+      Tenant& nt = *E.tenants[snext->tenant];
+      const uint32_t q = quantum_us(nt);
+      tslice = (int64_t)q * 1000;
+      if (!held) sd(nt).q_disp_us = q;
     } else {
       tslice = (int64_t)tslice_us_ * 1000;
     }
@@ -1445,9 +1568,11 @@ class CreditScheduler : public Scheduler {
     o.weight = d.weight;
     o.cap = d.cap;
     o.active_slots = d.active_vcpu_count;
-    o.tslice_us = mode_quantum_us(dom);
+    o.tslice_us = reported_us(dom);  // dispatched
+    o.target_tslice_us = target_us(dom);
+    o.last_dispatch_us = d.q_disp_us;
     o.tick_period_us = mode_ == Mode::PBS ? d.adapt.tick_period_us
-                                          : (mode_ == Mode::CLASSQ ? o.tslice_us / E.adapt_params.ticks_per_tslice
+                                          : (mode_ == Mode::CLASSQ ? o.target_tslice_us / E.adapt_params.ticks_per_tslice
                                                                    : tick_period_us_);
     o.phase = d.adapt.phase;
     o.window_left = d.adapt.window_left;

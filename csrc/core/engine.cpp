@@ -808,7 +808,16 @@ void Engine::budget_layout(Pool& pl, int64_t n, bool force) {
     if (busy && t.pause_count == 0) t.last_busy = n;
     // class -1: busy but not classified yet
     const bool present = n - t.last_busy <= present_ns;
-    if (present) sig.emplace_back(t.id, t.cls);
+    int cls = t.cls;
+    if (!present || cls >= 0) {
+      t.unclassified_since = INT64_MIN / 2;
+    } else if (t.unclassified_since == INT64_MIN / 2) {
+      t.unclassified_since = n;
+    } else if (boot.probe_max_us > 0 && n - t.unclassified_since > (int64_t)boot.probe_max_us * 1000) {
+      cls = 1;  // no clean window yet after probe_max_us: laid out as memory class
+      perfc.incr(PC_probe_expired);
+    }
+    if (present) sig.emplace_back(t.id, cls);
     else t.budget_ctx = 0;
   }
   // class_pin_us: a flapping compute-phase tenant joins the memory region

@@ -100,6 +100,7 @@ struct Tenant {  // struct domain
   // class_pin_us: flapping = its last three class changes within the window
   bool flapping(int64_t now, int64_t pin_ns) const { return pin_ns > 0 && cls >= 0 && now - cls_chg_ns[0] <= pin_ns; }
   int lay_cls = -1;  // the class budget_layout placed it by (a pinned flapping tenant: 1)
+  int64_t unclassified_since = INT64_MIN / 2;  // present and unclassified since (probe_max_us)
   // Cross-GPU gang window (parallel/gang.py): 1 favoured (run on every
   // partition that holds a slot), 2 excluded (its peers on other GPUs are not
   // running it), until gang_until (engine clock).
@@ -112,6 +113,12 @@ struct Tenant {  // struct domain
   // closing sample leaves none); granted = tenures so extended.
   uint32_t measure_us = 0;
   uint64_t measure_granted = 0;
+  // Measured cost of one switch of its partitions (revocation drain + re-entry
+  // ramp, the GPU runtime's EWMA; 0 = unknown) and its latency target (0 =
+  // none): the per-tenant quantum floor / the co-sharers' cap in a
+  // time-shared class region (credit.cpp pbs_quantum_us).
+  uint32_t sw_cost_us = 0;
+  uint32_t slo_us = 0;
   // Watchdogs (SCHEDOP_watchdog): timer ids, in-use bits, shutdown reason.
   int wd_timer[GPBS_WATCHDOGS] = {-1, -1};
   uint32_t wd_inuse = 0;

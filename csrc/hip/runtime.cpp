@@ -412,6 +412,16 @@ struct GpuCtx {
   int64_t own_base[kMaxTenants][kXcds * kCtx];
   int64_t last_pub_ns = 0;
   std::atomic<int64_t> revoke_ns[kMaxTenants] = {};  // last publish that took a partition from the tenant
+  std::atomic<int64_t> grant_ns[kMaxTenants] = {};   // last publish that gave the tenant a partition
+  // Per-tenant switch cost (round 6; the runners measure it, the sampler
+  // thread hands it to the engine as the tenant's quantum floor basis):
+  // EWMA (1/8) of the revocation drain -- publish that took a partition ->
+  // the interrupted unit's grid has left (co-sharers of a region share one
+  // queue, so the next owner's grid starts only then) -- and of the re-entry
+  // ramp -- publish that gave a partition back -> the tenant's next launch.
+  std::atomic<int64_t> swc_drain_ns[kMaxTenants] = {}, swc_ramp_ns[kMaxTenants] = {};
+  std::atomic<uint64_t> swc_drain_n[kMaxTenants] = {}, swc_ramp_n[kMaxTenants] = {};
+  int64_t swc_pushed_ns[kMaxTenants] = {};  // sampler thread: the cost last given to the engine
   hipEvent_t adapt_ev = nullptr;  // device adapt: bounded poll, never a blocking sync
   bool adapt_pending = false;
   // Asynchronous device adapt (engine adapt_launch / adapt_harvest): pinned
@@ -530,6 +540,8 @@ bool publish_locked(GpuCtx* c) {
       const u32 o = c->h_table->owner[x] & kOwnerMask;
       if ((c->pending[x] & kOwnerMask) == o) continue;
       if (o < (u32)kMaxTenants) c->revoke_ns[o].store(t, std::memory_order_relaxed);
+      const u32 nw = c->pending[x] & kOwnerMask;
+      if (nw < (u32)kMaxTenants) c->grant_ns[nw].store(t, std::memory_order_relaxed);
       // switch-aligned sampling: when and to whom this partition changed
       c->part_chg_ns[x] = t;
       c->part_q_us[x] = c->q_pending[x];
@@ -1132,13 +1144,35 @@ int hwc_tenant_deltas(GpuCtx* c, int n, const int* tenants, uint64_t* out) {
   return 0;
 }
 
+// The runners' measured switch costs (drain + ramp) to the engine, where they
+// floor each tenant's quantum in a time-shared region (boot switch_floor_x).
+// Under the engine lock (the metric tick; the mutex is recursive), pushed when
+// a tenant's cost moved by more than 5 %.
+void push_switch_costs(GpuCtx* c, int n, const int* tenants) {
+  for (int k = 0; k < n; ++k) {
+    const int t = tenants[k];
+    if (t < 0 || t >= kMaxTenants) continue;
+    const uint64_t nd = c->swc_drain_n[t].load(std::memory_order_relaxed);
+    const uint64_t nr = c->swc_ramp_n[t].load(std::memory_order_relaxed);
+    if (!nd && !nr) continue;
+    const int64_t cost = (nd ? c->swc_drain_ns[t].load(std::memory_order_relaxed) : 0) +
+                         (nr ? c->swc_ramp_ns[t].load(std::memory_order_relaxed) : 0);
+    const int64_t last = c->swc_pushed_ns[t];
+    if (last && std::llabs(cost - last) * 20 < last) continue;
+    c->swc_pushed_ns[t] = cost;
+    gpbs_tenant_switch_cost(c->engine, t, (uint64_t)std::max<int64_t>(cost, 0));
+  }
+}
+
 int ctr_tenant_deltas(void* user, int n, const int* tenants, uint64_t* out) {
   GpuCtx* c = (GpuCtx*)user;
   if (n > kMaxTenants) return -22;
-  if (c->engine)  // engine lock held: refresh the class cache launch() reads
+  if (c->engine) {  // engine lock held: refresh the class cache launch() reads
     for (int k = 0; k < n; ++k)
       if (tenants[k] >= 0 && tenants[k] < kMaxTenants)
         c->cls_cache[tenants[k]].store(gpbs_tenant_class(c->engine, tenants[k]), std::memory_order_relaxed);
+    push_switch_costs(c, n, tenants);
+  }
   if (c->hwc) return hwc_tenant_deltas(c, n, tenants, out);
   const int64_t t0 = mono_ns();
   RoctxRange rr("gpbs:metric_tick");
@@ -1810,12 +1844,61 @@ struct Runner {
     return false;
   }
 
+  // Switch-cost measurement (round 6).  drain: a unit revoked mid-way is
+  // watched while the runner waits for ownership, so the moment its grid has
+  // left is seen within ~25 us (the runner's own loop only looks at it once
+  // it owns a partition again); ramp: the first launch after the wait.
+  int wo_qi = -1;               // in-flight unit to watch while waiting (the pipeline's oldest)
+  int64_t q_l0[16] = {};        // launch time of the unit in each queue slot (this launch)
+  int64_t drain_seen_rv = 0;    // the revocation whose drain was recorded
+  int64_t ramp_from = 0;        // wait_owner blocked since here: the next launch closes a ramp
+  static void ewma(std::atomic<int64_t>& a, std::atomic<uint64_t>& n, int64_t v) {
+    const int64_t o = a.load(std::memory_order_relaxed);
+    a.store(n.load(std::memory_order_relaxed) ? o + (v - o) / 8 : v, std::memory_order_relaxed);
+    n.fetch_add(1, std::memory_order_relaxed);
+  }
+  // The unit in queue slot qi has completed its grid at `now`: a revocation
+  // drain if it was interrupted (unfinished) by a publish after its launch.
+  void note_drain(int qi, int64_t now) {
+    if (cfg.tenant < 0 || cfg.tenant >= kMaxTenants) return;
+    const int64_t rv = ctx->revoke_ns[cfg.tenant].load(std::memory_order_relaxed);
+    if (!rv || rv == drain_seen_rv || rv < q_l0[qi] || now < rv) return;
+    const u32 s = __atomic_load_n(&h_status[qi], __ATOMIC_ACQUIRE);
+    if ((s & 0x80000000u) && (s & 0x3fffffffu) >= unit_total(work(q_alt[qi]))) return;  // finished, not revoked
+    drain_seen_rv = rv;
+    const int64_t dr = now - rv;
+    if (dr >= 1000000000) return;
+    st.drain_sum_ns += dr;
+    st.drain_count++;
+    if (dr > st.drain_max_ns) st.drain_max_ns = dr;
+    ewma(ctx->swc_drain_ns[cfg.tenant], ctx->swc_drain_n[cfg.tenant], dr);
+  }
+  void note_ramp(int64_t now) {
+    if (!ramp_from || cfg.tenant < 0 || cfg.tenant >= kMaxTenants) return;
+    const int64_t g = ctx->grant_ns[cfg.tenant].load(std::memory_order_relaxed);
+    if (g >= ramp_from && now >= g && now - g < 1000000000)
+      ewma(ctx->swc_ramp_ns[cfg.tenant], ctx->swc_ramp_n[cfg.tenant], now - g);
+    ramp_from = 0;
+  }
+
   void wait_owner() {
     if (owns_any()) return;
     st.waits_owner++;
     const int64_t t0 = mono_ns();
+    ramp_from = t0;
+    int watch = wo_qi;
     std::unique_lock<std::mutex> lk(ctx->mu);
-    while (!stop && !owns_any()) ctx->cv.wait_for(lk, std::chrono::microseconds(200));
+    while (!stop && !owns_any()) {
+      ctx->cv.wait_for(lk, std::chrono::microseconds(watch >= 0 ? 25 : 200));
+      if (watch >= 0) {
+        lk.unlock();
+        if (hipEventQuery(ev[watch]) != hipErrorNotReady) {
+          note_drain(watch, mono_ns());
+          watch = -1;
+        }
+        lk.lock();
+      }
+    }
     st.wait_owner_ns += mono_ns() - t0;
   }
 
@@ -1867,6 +1950,7 @@ struct Runner {
             if (qi < 0) break;
             fresh = true;
           }
+          wo_qi = fl.empty() ? -1 : fl.front().qi;
           wait_owner();
           if (stop) break;
           if (fresh) {
@@ -1889,6 +1973,8 @@ struct Runner {
             hipMemsetAsync(&d_q[qi].exited, 0, sizeof(u32) * 2, stream);
           }
           if (cfg.priority > 0 && ctx->hold_enable && fresh && !q_hold[qi]) q_hold[qi] = hold_acquire(ctx) + 1;
+          q_l0[qi] = mono_ns();
+          note_ramp(q_l0[qi]);
           if (launch(qi, stream) != 0) err = -5;
           const int e = qi;  // one event per queue slot
           hipEventRecord(ev[e], stream);
@@ -1944,14 +2030,9 @@ struct Runner {
           }
         } else {
           relaunch.push_back(f.qi);  // revoked mid-unit: resume when owned
-          const int64_t rv = cfg.tenant >= 0 && cfg.tenant < kMaxTenants
-                                 ? ctx->revoke_ns[cfg.tenant].load(std::memory_order_relaxed) : 0;
-          const int64_t dr = rv ? mono_ns() - rv : -1;
-          if (dr >= 0 && dr < 1000000000) {
-            st.drain_sum_ns += dr;
-            st.drain_count++;
-            if (dr > st.drain_max_ns) st.drain_max_ns = dr;
-          }
+          // seen at once (the runner did not wait for ownership in between;
+          // otherwise wait_owner recorded it)
+          note_drain(f.qi, mono_ns());
         }
         if (stop) break;
       }
@@ -2650,6 +2731,18 @@ int gpbs_hip_hwc_drained_selftest(int seed, int iters) {
   if (hwc_drained_bits(t0, t1, used_chg, snap_chg, guard, 80) != 0) return 2;
   for (int p = 0; p < kAttrP; ++p) snap_chg[p] = t1 - guard;  // A's tenure ends one guard before the close
   if (hwc_drained_bits(t0, t1, used_chg, snap_chg, guard, 80) != 0xFFFFFFFFu) return 3;
+  return 0;
+}
+
+// Measured switch cost of a tenant (round 6): out4 = drain EWMA ns, ramp
+// EWMA ns, drains measured, ramps measured.
+int gpbs_gpu_switch_cost(void* ctx, int tenant, int64_t* out4) {
+  GpuCtx* c = (GpuCtx*)ctx;
+  if (!c || tenant < 0 || tenant >= kMaxTenants || !out4) return -22;
+  out4[0] = c->swc_drain_ns[tenant].load(std::memory_order_relaxed);
+  out4[1] = c->swc_ramp_ns[tenant].load(std::memory_order_relaxed);
+  out4[2] = (int64_t)c->swc_drain_n[tenant].load(std::memory_order_relaxed);
+  out4[3] = (int64_t)c->swc_ramp_n[tenant].load(std::memory_order_relaxed);
   return 0;
 }
 

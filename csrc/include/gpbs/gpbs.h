@@ -16,7 +16,7 @@
 extern "C" {
 #endif
 
-#define GPBS_ABI_VERSION 4
+#define GPBS_ABI_VERSION 5
 
 /* Validation ranges (sysctl.h:568-579, libxl.c:4026-4101). Q1: the new API
  * also accepts the reference's boot default of 100us (see docs). */
@@ -101,6 +101,20 @@ typedef struct gpbs_boot_params {
   int32_t class_pin_us;        /* class_budget: a tenant whose last THREE class changes fall within this window is
                                   laid out as memory class (its region time-shares; it takes no compute SEs from a
                                   compute tenant) until it settles.  0 = off */
+  int32_t region_q;            /* class_budget, time-shared class region: 0 = every tenant runs its OWN quantum (PBS:
+                                  its adaptive quantum, at least its switch-cost floor); 1 = the round-5 region quantum
+                                  (the largest adaptive quantum of the co-sharers, floored at shared_q_us) */
+  int32_t switch_floor_x;      /* per-tenant quantum floor in a time-shared region = this x the tenant's measured
+                                  switch cost (revocation drain + re-entry ramp, gpbs_tenant_switch_cost); 0 = off */
+  int32_t switch_floor_max_us; /* ... capped here (0 = max_us) */
+  int32_t region_vt;           /* 1 = a time-shared region picks its next tenant by least region virtual time (owned
+                                  partition-time / weight) among the runnable co-sharers, BOOSTed wakers first, so
+                                  per-tenant quanta of any length stay weight-fair; 0 = credit priority + runq order */
+  int32_t slo_cap;             /* 1 = a co-sharer's quantum in a region that holds a tenant with a latency target
+                                  (gpbs_tenant_slo) is capped so the target's waiting time fits the target */
+  int32_t probe_max_us;        /* class_budget: a present tenant still unclassified after this long (its tenures are
+                                  too short for a clean counter window: a latency tenant's 50 us requests) is laid out
+                                  as memory class instead of holding every tenant in the probe layout; 0 = no limit */
   gpbs_adapt_params_t adapt;
   gpbs_atc_params_t atc;
 } gpbs_boot_params_t;
@@ -193,7 +207,11 @@ typedef struct gpbs_tenant_info {
   int32_t online_slots;     /* slots not offline (vcpu-set / class_budget) */
   uint32_t budget_ctx;      /* class_budget: contexts (shader engines) of every XCD the layout gave it (bit c) */
   int32_t budget_shared;    /* class_budget: its class region is time-shared */
-  int32_t reserved0;
+  uint32_t target_tslice_us;/* the policy's quantum target (PBS: the adaptive tslice); tslice_us above is the
+                               quantum the dispatcher gives the tenant now (region floors / caps applied) */
+  uint32_t switch_cost_us;  /* measured switch cost (drain + ramp, EWMA) the engine holds for the tenant */
+  uint32_t slo_us;          /* latency target, 0 = none */
+  uint32_t last_dispatch_us;/* the quantum of its last dispatch (0: never dispatched) */
 } gpbs_tenant_info_t;
 
 typedef struct gpbs_slot_info {
@@ -288,6 +306,14 @@ int gpbs_tenant_bound_stats(gpbs_engine_t* e, int tenant, uint64_t* out3, int re
  * least `us` (0 cancels, UINT32_MAX only reads); returns the tenures so
  * extended so far, or <0. */
 int gpbs_tenant_measure(gpbs_engine_t* e, int tenant, uint32_t us);
+/* Measured cost of one switch of the tenant's partitions (revocation drain +
+ * re-entry ramp, ns; the GPU runtime's EWMA): the per-tenant quantum floor of
+ * a time-shared region (boot switch_floor_x).  0 clears it. */
+int gpbs_tenant_switch_cost(gpbs_engine_t* e, int tenant, uint64_t ns);
+/* Latency target of a tenant (us; 0 = none): with boot slo_cap, the quanta of
+ * its co-sharers in a time-shared region are capped so it waits at most this
+ * long for a turn. */
+int gpbs_tenant_slo(gpbs_engine_t* e, int tenant, uint32_t us);
 /* Cumulative INST, CYCLES, LLC refs, LLC misses the scheduler measured and
  * attributed to the tenant (sum over metric periods; the vPMU mirror). */
 int gpbs_tenant_vpmu(gpbs_engine_t* e, int tenant, uint64_t* total4);

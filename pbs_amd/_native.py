@@ -27,7 +27,7 @@ class AtcParams(C.Structure):
                                    "wait_unit_ns")]
 
 
-ABI_VERSION = 4  # GPBS_ABI_VERSION in csrc/include/gpbs/gpbs.h
+ABI_VERSION = 5  # GPBS_ABI_VERSION in csrc/include/gpbs/gpbs.h
 
 
 class BootParams(C.Structure):
@@ -36,7 +36,8 @@ class BootParams(C.Structure):
         "metric_period_us", "slice_apply_us", "sim_clock", "pmu_refresh_us", "dom0_quirk", "heartbeat_timeout_us",
         "trace_capacity", "quantum_align_us", "coschedule", "class_period_us", "boost_exclusive",
         "class_split", "idle_skip", "class_dwell", "class_budget", "present_us", "sibling_steal", "class_steal", "class_fall",
-        "shared_q_us", "class_pin_us")] + [("adapt", AdaptParams),
+        "shared_q_us", "class_pin_us", "region_q", "switch_floor_x", "switch_floor_max_us", "region_vt",
+        "slo_cap", "probe_max_us")] + [("adapt", AdaptParams),
                                                                                     ("atc", AtcParams)]
 
 
@@ -98,7 +99,8 @@ class TenantInfo(C.Structure):
                [("last_err", i32), ("shutdown", i32), ("last_curr", i64), ("last_win", i64), ("pmc", u64 * 4),
                 ("cache_miss_rate", u64), ("cpi", u64), ("spin_latency", u64), ("report_count", u64),
                 ("pending_requests", u64), ("sched_count", u64), ("run_ns", i64), ("name", C.c_char * 64),
-                ("online_slots", i32), ("budget_ctx", u32), ("budget_shared", i32), ("reserved0", i32)]
+                ("online_slots", i32), ("budget_ctx", u32), ("budget_shared", i32), ("target_tslice_us", u32),
+                ("switch_cost_us", u32), ("slo_us", u32), ("last_dispatch_us", u32)]
 
 
 class SlotInfo(C.Structure):
@@ -281,6 +283,8 @@ def _bind_ipc(lib):
     P(lib, "gpbs_tenant_class", C.c_int, C.c_void_p, C.c_int)
     P(lib, "gpbs_tenant_bound_stats", C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_uint64), C.c_int)
     P(lib, "gpbs_tenant_measure", C.c_int, C.c_void_p, C.c_int, C.c_uint32)
+    P(lib, "gpbs_tenant_switch_cost", C.c_int, C.c_void_p, C.c_int, C.c_uint64)
+    P(lib, "gpbs_tenant_slo", C.c_int, C.c_void_p, C.c_int, C.c_uint32)
     P(lib, "gpbs_tenant_vpmu", C.c_int, C.c_void_p, C.c_int, C.POINTER(u64))
     P(lib, "gpbs_fault_set", C.c_int, C.c_void_p, C.c_char_p)
     P(lib, "gpbs_fault_hits", C.c_int, C.c_void_p, C.POINTER(u64), C.c_int)

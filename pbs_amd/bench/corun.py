@@ -84,6 +84,7 @@ SPECS = {
     "hbm": dict(kind="stream", bytes=1 << 30),
     "hbm_b": dict(kind="stream", bytes=1 << 30),
     "hbm_s": dict(kind="stream", bytes=256 << 20),
+    "mall": dict(kind="stream", bytes=96 << 20),
     "coll": dict(kind="reduce"),  # bytes = cfg.coll_bytes
     "phase": dict(kind="gemm", M=4096, N=4096, K=4096, alt=dict(kind="stream", bytes=1 << 30)),
     "idle": dict(kind="gemv"),
@@ -110,6 +111,14 @@ MIXES = {
     "8mix": {"tenants": (("gemm", 8), ("gemm_b", 8), ("gemm_s", 8), ("hbm", 8), ("hbm_b", 8), ("hbm_s", 8),
                          ("coll", 8), ("idle", 8)),
              "throughput": ("gemm", "gemm_b", "gemm_s", "hbm", "hbm_b", "hbm_s", "coll")},
+    # latency-SLO mix: the latency tenant is a co-sharer
+    # of the time-shared memory region (gated on its partitions, woken per
+    # request -- no latency lane), next to two HBM streamers and a tenant
+    # whose working set (2 x 96 MiB) fits the 256 MiB MALL
+    "slo": {"tenants": (("gemm", 8), ("hbm", 8), ("hbm_b", 8), ("mall", 8), ("idle", 8)),
+            "throughput": ("gemm", "hbm", "hbm_b", "mall"), "slo_in_region": True,
+            # p99 target of its 8192^2 GEMV requests (solo ~0.06 ms)
+            "slo_p99_ms": 1.0},
 }
 # Hand-picked static shader-engine layouts (policy "static-se": no engine, no
 # counters): tenant -> (XCDs, SEs) it owns.  The informed static alternative
@@ -126,6 +135,9 @@ STATIC_SE = {
     "8mix": {"gemm": (_ALLX, (0,)), "gemm_b": (tuple(range(6)), (1,)), "gemm_s": ((6, 7), (1,)),
              "hbm": ((0, 1, 2, 3), (2,)), "hbm_b": ((4, 5, 6, 7), (2,)), "coll": ((0, 1, 2, 3), (3,)),
              "hbm_s": ((4, 5, 6, 7), (3,))},
+    # the latency tenant gets dedicated memory SEs (idle between requests)
+    "slo": {"gemm": (_ALLX, (0, 1)), "hbm": ((0, 1, 2, 3), (2,)), "hbm_b": ((4, 5, 6, 7), (2,)),
+            "mall": ((0, 1, 2, 3), (3,)), "idle": ((4, 5, 6, 7), (3,))},
 }
 
 
@@ -236,10 +248,19 @@ POLICY_ENGINES = {
                        adapt=dict(MI355X_PROFILE["adapt"], min_us=4000, max_us=30000, inc_us=4000, dec_us=8000,
                                   switch_boundary=30000)), True, "device,se,waveprio,latco,budget,latmem"),
     # time-shared class regions rotate at >= 11 / 30 ms (boot shared_q_us)
-    "gpbs-sq11": (4, dict(BUDGET_OVERRIDES, class_budget=1, shared_q_us=11000), True,
+    "gpbs-sq11": (4, dict(BUDGET_OVERRIDES, class_budget=1, region_q=1, shared_q_us=11000), True,
                   "device,se,waveprio,latco,budget,latmem"),
-    "gpbs-sq30": (4, dict(BUDGET_OVERRIDES, class_budget=1, shared_q_us=30000), True,
+    # round 5's flagship: one region quantum (the co-sharers' largest adaptive
+    # quantum, floored at a global 30 ms)
+    "gpbs-sq30": (4, dict(BUDGET_OVERRIDES, class_budget=1, region_q=1, shared_q_us=30000), True,
                   "device,se,waveprio,latco,budget,latmem"),
+    # the PBS quantum without the measured switch-cost floors
+    "gpbs-nofloor": (4, dict(BUDGET_OVERRIDES, class_budget=1, switch_floor_x=0), True,
+                     "device,se,waveprio,latco,budget,latmem"),
+    # credit-classq with the global 30 ms floor in time-shared regions (the
+    # classq + floor ablation: what the class map does with round 5's floor)
+    "credit-classq-f": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="credit-classq", shared_q_us=30000), True,
+                        "device,se,waveprio,latco,budget,latmem"),
     # PBS quantum range capped lower at the top (memory tenants up to 4 / 6 ms)
     "gpbs-max4": (4, dict(BUDGET_OVERRIDES, class_budget=1, adapt=dict(MI355X_PROFILE["adapt"], max_us=4000)), True,
                   "device,se,waveprio,latco,budget,latmem"),
@@ -608,7 +629,10 @@ class Corun:
         ids = {}
         for name, ns in self.tenants:
             if "budget" in opts:  # one slot per partition; the layout sizes the share
-                n = ns if SPECS[name]["kind"] == "gemv" else XCDS * nctx
+                # (the latency tenant: one per XCD in its lane; a full set as a
+                # co-sharer of the region, so the gang leader's runqueue holds it)
+                lane = SPECS[name]["kind"] == "gemv" and not MIXES[self.cfg.mix].get("slo_in_region")
+                n = ns if lane else XCDS * nctx
             elif "se" in opts:
                 n = (SE8_SLOTS if "se8" in opts else SE_SLOTS).get(name, ns if SPECS[name]["kind"] == "gemv" else 16)
             else:
@@ -682,10 +706,11 @@ class Corun:
                 self.ctx.set_hwc(False)  # modeled counters feed the metric this run
             e.start()
             self.active_engine = e
+            in_region = bool(MIXES[self.cfg.mix].get("slo_in_region"))
             for name, r in self.runners.items():
                 if not isinstance(r, Runner):
                     continue
-                latco = name == "idle" and "latco" in opts
+                latco = name == "idle" and "latco" in opts and not in_region
                 r.set_gate(False if latco else gate)
                 r.set_engine_wake(not latco)
             if isinstance(coll, CollTenant):
@@ -749,9 +774,10 @@ class Corun:
             self.ctx.set_se_mode(True)
             self.ctx.set_waveprio(True)
             self.ctx.set_owners(owners)
+            in_region = bool(MIXES[self.cfg.mix].get("slo_in_region"))
             for name, r in self.runners.items():
                 if isinstance(r, Runner):
-                    r.set_gate(SPECS[name]["kind"] != "gemv")
+                    r.set_gate(SPECS[name]["kind"] != "gemv" or in_region)
             if isinstance(coll, CollTenant):
                 coll.gate = True
         else:
@@ -1038,6 +1064,7 @@ class Corun:
             if self.cfg.hw_counters:
                 self.ctx.hwc_reset()
         quanta = {n: [] for n in self.tid}
+        self._targets = {n: [] for n in self.tid}  # the policy's target quantum per step (PBS: adaptive)
         layout = {n: [] for n in self.throughput}  # budget SE sets per step (bit c = SE c)
         self._rs0 = {n: r.stats() for n, r in self.runners.items() if isinstance(r, Runner)}
         self.ctx.masked_pool_reset()
@@ -1061,7 +1088,8 @@ class Corun:
             if e is not None:
                 for n in self.tid:
                     ti = e.tenant_info(self.tid[n])
-                    quanta[n].append(ti.tslice_us)
+                    quanta[n].append(ti.tslice_us)  # dispatched (s_timer) quantum
+                    self._targets[n].append(ti.target_tslice_us)
                     if n in layout:
                         layout[n].append(ti.budget_ctx)
         d1 = {n: self._work(n) for n in self.throughput}
@@ -1223,7 +1251,14 @@ class Corun:
                 eng["hwc"]["per_tenant_clean_frac"] = frac
             eng["miss_rate"] = {n: e.tenant_info(self.tid[n]).cache_miss_rate for n in self.tid}
             eng["class"] = {n: e.lib.gpbs_tenant_class(e.h, self.tid[n]) for n in self.tid}
-            eng["mean_tslice_us"] = {n: round(statistics.mean(q), 1) for n, q in quanta.items() if q}
+            eng["mean_tslice_us"] = {n: round(statistics.mean(q), 1) for n, q in quanta.items() if q}  # dispatched
+            tg = getattr(self, "_targets", {})
+            eng["mean_target_tslice_us"] = {n: round(statistics.mean(q), 1) for n, q in tg.items() if q}
+            # measured switch costs (drain + ramp) and the engine's floor basis
+            eng["switch_cost"] = {n: dict(self.ctx.switch_cost(self.tid[n]),
+                                          engine_us=e.tenant_info(self.tid[n]).switch_cost_us)
+                                  for n in self.tid}
+            eng["shared"] = {n: e.tenant_info(self.tid[n]).budget_shared for n in self.tid}
             # measured metric periods and, of those, at the quantum bounds
             eng["at_bound"] = {n: e.bound_stats(self.tid[n]) for n in self.throughput}
             eng["measure_tenures"] = {n: e.measure(self.tid[n]) for n in self.throughput}

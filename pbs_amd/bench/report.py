@@ -121,7 +121,26 @@ def mix_digest(summary: dict, runs: Dict[str, List[dict]]) -> dict:
         d["quantum_at_bound"] = b
     if "idle_p50_ms" in g:
         d["lat_p50_ms"] = g["idle_p50_ms"]
+    if "idle_p99_ms" in g and summary.get("slo"):
+        # in-region latency tenant: p99 per policy against its target
+        d["slo"] = {"target_ms": summary["slo"], **{p: v.get("idle_p99_ms") for p, v in pol.items()
+                                                    if "idle_p99_ms" in v}}
+    q = _dispatched(runs.get("gpbs", []))
+    if q:
+        d["dispatched_q_us"] = q
     return d
+
+
+def _dispatched(runs: List[dict]) -> Optional[dict]:
+    """Median over gpbs runs of the quantum each time-shared tenant was
+    dispatched with (the s_timer quantum), us."""
+    per: Dict[str, List[float]] = {}
+    for r in runs:
+        e = r.get("engine") or {}
+        for n, q in (e.get("mean_tslice_us") or {}).items():
+            if (e.get("shared") or {}).get(n):
+                per.setdefault(n, []).append(q)
+    return {n: int(_q(v, 0.5)) for n, v in sorted(per.items())} or None
 
 
 def ranks_digest(ranks: List[dict]) -> dict:
@@ -173,7 +192,7 @@ def compact_line(full: dict, digests: Dict[str, dict], detail_path: str = "") ->
         lambda: [m.pop(k, None) for m in line["mixes"].values()
                  for k in ("tslice_us_by_class", "lat_p50_ms", "quantum_at_bound")],
         lambda: [m.pop(k, None) for n, m in line["mixes"].items() if n != head
-                 for k in ("hw", "dispatched_q_us", "slo")],
+                 for k in ("hw", "dispatched_q_us")],
         lambda: line["ranks"].update(failures=line["ranks"]["failures"][:2],
                                      n_failed=len(line["ranks"]["failures"])),
         lambda: [line["mixes"].__setitem__(n, {k: v for k, v in m.items()

@@ -46,12 +46,19 @@ MI355X_PROFILE: Dict[str, Any] = dict(
     # 2 s) joins an already time-shared memory region instead of splitting
     # the compute region (phase-ts +0.016, s26; engine.cpp budget_layout)
     class_pin_us=2000000,
-    # a time-shared class region rotates at >= 30 ms whatever its classes: a
-    # switch drains the outgoing tenant's tiles and refills the L2s, so on the
-    # GPU the throughput cost falls with the quantum (8mix 1.354 -> 1.378, s32;
-    # phase / phase-ts / 4mix level).  The per-tenant PBS quantum still rules
-    # the partitions a tenant holds alone.
-    shared_q_us=30000,
+    # Time-shared class regions (round 6): every co-sharer
+    # runs its OWN quantum -- its PBS adaptive quantum, at least switch_floor_x
+    # times its measured switch cost (revocation drain + re-entry ramp, per
+    # tenant, from the GPU runtime), at most switch_floor_max_us -- and the
+    # region's virtual time keeps the shares weight-fair whatever the quanta
+    # (credit.cpp quantum_us / region_pick).  Round 5's region quantum (the
+    # co-sharers' largest, floored at a global 30 ms: region_q=1,
+    # shared_q_us=30000) stays as the gpbs-sq30 ablation.
+    region_q=0, region_vt=1, switch_floor_x=100, switch_floor_max_us=30000, shared_q_us=0, slo_cap=0,
+    # a present tenant unclassified for 50 ms (a latency tenant whose 50 us
+    # requests never fill a clean counter window) joins the memory class
+    # instead of holding every tenant in the probe layout (slo mix, s2 diag)
+    probe_max_us=50000,
     adapt=dict(threshold=20000, band_lo=70, band_hi=130, min_us=1000, max_us=11000, inc_us=1000, dec_us=2000,
                switch_boundary=9000, ticks_per_tslice=3,
                # grow_pct > 0: proportional growth + a restart at the class bound
@@ -78,7 +85,8 @@ BOOT_KEYS = ("sched", "tslice_us", "ratelimit_us", "smt_power_savings", "tickle_
              "migration_delay_us", "metric_period_us", "slice_apply_us", "pmu_refresh_us", "dom0_quirk",
              "heartbeat_timeout_us", "trace_capacity", "quantum_align_us", "coschedule", "class_period_us",
              "boost_exclusive", "class_split", "idle_skip", "class_dwell", "class_budget", "present_us",
-             "sibling_steal", "class_steal", "class_fall", "shared_q_us", "class_pin_us")
+             "sibling_steal", "class_steal", "class_fall", "shared_q_us", "class_pin_us", "region_q", "switch_floor_x",
+             "switch_floor_max_us", "region_vt", "slo_cap", "probe_max_us")
 
 
 def load(path: str | None = None, profile: Dict[str, Any] | None = None) -> Dict[str, Any]:

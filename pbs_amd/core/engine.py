@@ -71,6 +71,10 @@ class TenantInfo:
     online_slots: int = 0
     budget_ctx: int = 0      # class_budget: shader engines of every XCD the layout gave the tenant (bit c)
     budget_shared: bool = False
+    target_tslice_us: int = 0  # the policy's quantum target (PBS: adaptive); tslice_us is the dispatched one
+    switch_cost_us: int = 0    # measured switch cost (drain + ramp) the engine holds
+    slo_us: int = 0            # latency target (0: none)
+    last_dispatch_us: int = 0  # quantum of its last dispatch
 
 
 @dataclass
@@ -250,7 +254,9 @@ class Engine:
                           cache_miss_rate=o.cache_miss_rate, cpi=o.cpi, spin_latency=o.spin_latency,
                           report_count=o.report_count, pending_requests=o.pending_requests,
                           sched_count=o.sched_count, run_ns=o.run_ns, shutdown=o.shutdown,
-                          online_slots=o.online_slots, budget_ctx=o.budget_ctx, budget_shared=bool(o.budget_shared))
+                          online_slots=o.online_slots, budget_ctx=o.budget_ctx, budget_shared=bool(o.budget_shared),
+                          target_tslice_us=o.target_tslice_us, switch_cost_us=o.switch_cost_us, slo_us=o.slo_us,
+                          last_dispatch_us=o.last_dispatch_us)
 
     def slot_info(self, sid: int) -> Dict:
         o = N.SlotInfo()
@@ -471,6 +477,16 @@ class Engine:
         """Ask for a measurement tenure of at least `us` for the tenant's next
         tenure (0 cancels; -1 only reads).  Returns the tenures extended so far."""
         return int(self.lib.gpbs_tenant_measure(self.h, t, 0xFFFFFFFF if us < 0 else int(us)))
+
+    def switch_cost(self, t: int, ns: int) -> int:
+        """Measured cost of one switch of the tenant's partitions (ns): its
+        per-tenant quantum floor in a time-shared region (boot switch_floor_x)."""
+        return int(self.lib.gpbs_tenant_switch_cost(self.h, t, int(ns)))
+
+    def set_slo(self, t: int, us: int) -> int:
+        """Latency target of a tenant (us, 0 = none): with boot slo_cap, its
+        co-sharers' quanta are capped to it."""
+        return int(self.lib.gpbs_tenant_slo(self.h, t, int(us)))
 
     def perfc_prometheus(self, prefix: str = "gpbs") -> str:
         """perfc counters in the Prometheus text exposition format."""

@@ -217,6 +217,16 @@ class GpuContext:
         return {"clean": o[0], "fallback": o[1], "skipped": o[2], "sliver": o[3],
                 "cal": [round(x, 4) for x in cal]}
 
+    def switch_cost(self, tenant: int) -> dict:
+        """The tenant's measured switch cost (round 6): EWMA revocation drain
+        (publish -> its interrupted unit's grid gone) and re-entry ramp
+        (publish -> its next launch), us, and how many of each were measured.
+        drain + ramp is what the engine floors its time-shared quantum on."""
+        o = (C.c_int64 * 4)()
+        self.L.gpbs_gpu_switch_cost(self.h, int(tenant), o)
+        return {"drain_us": round(o[0] / 1e3, 1), "ramp_us": round(o[1] / 1e3, 1), "n_drain": int(o[2]),
+                "n_ramp": int(o[3])}
+
     def set_hwc_sampler(self, budget_pct: int = -1, align: int = -1, fallback: int = -1, duty: int = -1,
                         slow_us: int = -1, guard_us: int = -1, long_us: int = -1, stale_us: int = -1):
         """Sampler policy: `budget_pct` caps the time all hardware samples may
