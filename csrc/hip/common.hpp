@@ -195,13 +195,17 @@ __device__ __forceinline__ bool owns(const PartTable* t, u32 mode, u32 me, u32 x
 }
 
 // Per-(tenant, xcd) software counter block, accumulated at workgroup exit.
+// System-scope atomics: the block lives in fine-grained VRAM that the host
+// sampler reads through the BAR every metric tick (csrc/hip/runtime.cpp
+// read_block), so each add is performed past the XCD's L2, where the host's
+// read sees it.
 __device__ __forceinline__ void count(u64* cnt, u32 me, u32 xcc, u64 inst, u64 cyc, u64 refs, u64 miss) {
   if (!cnt) return;
   u64* c = cnt + ((size_t)me * kXcds + (xcc & 7)) * kNumPmc;
-  if (inst) atomicAdd(c + 0, inst);
-  if (cyc) atomicAdd(c + 1, cyc);
-  if (refs) atomicAdd(c + 2, refs);
-  if (miss) atomicAdd(c + 3, miss);
+  if (inst) __hip_atomic_fetch_add(c + 0, inst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (cyc) __hip_atomic_fetch_add(c + 1, cyc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (refs) __hip_atomic_fetch_add(c + 2, refs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (miss) __hip_atomic_fetch_add(c + 3, miss, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Work-queue unit grab of a persistent tenant workgroup (thread 0 decides,

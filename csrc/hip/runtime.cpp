@@ -141,6 +141,42 @@ hsa_status_t bar_agent_cb(hsa_agent_t a, void* ud) {
   return HSA_STATUS_SUCCESS;
 }
 
+// Any size (the counter block too); zeroed through the mapping.
+void* finegrained_alloc(int device, size_t bytes) {
+  int bus = 0, dev = 0;
+  if (hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, device) != hipSuccess ||
+      hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, device) != hipSuccess)
+    return nullptr;
+  BarFind F;
+  F.bdf = ((uint32_t)bus << 8) | ((uint32_t)dev << 3);
+  hsa_iterate_agents(bar_agent_cb, &F);
+  if (!F.gpu_ok || !F.cpu_ok || !F.pool_ok) return nullptr;
+  void* p = nullptr;
+  bytes = (bytes + 4095) & ~(size_t)4095;
+  if (hsa_amd_memory_pool_allocate(F.pool, bytes, 0, &p) != HSA_STATUS_SUCCESS) return nullptr;
+  hsa_agent_t both[2] = {F.gpu, F.cpu};
+  if (hsa_amd_agents_allow_access(2, both, nullptr, p) != HSA_STATUS_SUCCESS) {
+    hsa_amd_memory_pool_free(p);
+    return nullptr;
+  }
+  volatile uint64_t* w = (volatile uint64_t*)p;
+  for (size_t i = 0; i < bytes / 8; ++i) w[i] = 0;
+  _mm_sfence();
+  return p;
+}
+
+// Host read of counter rows that the GPU keeps in fine-grained VRAM (round
+// 6): SSE4.1 streaming loads pull a whole 64-byte line
+// per PCIe read from the uncached BAR mapping, so the sampler's per-tick read
+// of the active tenants' rows (~2 KiB) costs tens of us of one host thread
+// and no GPU queue work -- no copyBuffer blit kernel on the tenants' CUs.
+__attribute__((target("sse4.1"))) void bar_read(const void* src, void* dst, size_t bytes) {
+  const __m128i* s = (const __m128i*)src;
+  __m128i* d = (__m128i*)dst;
+  for (size_t i = 0; i < bytes / 16; ++i) _mm_storeu_si128(d + i, _mm_stream_load_si128(const_cast<__m128i*>(s + i)));
+  _mm_mfence();
+}
+
 PartTable* bar_alloc(int device) {
   int bus = 0, dev = 0;
   if (hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, device) != hipSuccess ||
@@ -198,6 +234,8 @@ struct GpuCtx {
   PartTable* d_table = nullptr;  // device copy (table_mode 1)
   PartTable* b_table = nullptr;  // host-writable VRAM table (table_mode 2), allocated on first use
   u64* d_cnt = nullptr;          // [kMaxTenants][kXcds][kNumPmc]
+  bool cnt_bar = false;          // d_cnt lives in host-readable fine-grained VRAM (bar_read, no copy kernel)
+  std::atomic<int> cnt_rows{1};  // rows [0, cnt_rows) can be non-zero: the largest runner tenant id + 1
   u64* d_prev = nullptr;
   u64* h_out = nullptr;          // pinned mapped: deltas [kMaxTenants][4]
   int* h_ids = nullptr;          // pinned mapped
@@ -361,6 +399,19 @@ struct GpuCtx {
   // edge of a neighbouring tenure -- never counts.
   int model_fallback = 1;
   int hwc_stale_us = 250000;
+  // 1 ms metric cadence (round 6; param cadence, default
+  // on): every metric tick a calibrated tenant reports its MODELED deltas of
+  // that tick scaled per counter by its hardware/model ratio, and each clean
+  // hardware window re-anchors the ratio instead of reporting (it already
+  // did, tick by tick); a tenant not calibrated yet reports its clean
+  // windows as before.  The reference reads its PMU every 1 ms
+  // (X:xen/common/sched_credit.c:55,450-465).
+  int model_cadence = 1;
+  std::vector<u64> cad_prev;                   // the block at the previous tick (snap_mu)
+  bool cad_primed = false;
+  uint64_t t_model[kMaxTenants] = {};          // metric periods delivered from the calibrated model
+  uint64_t t_delivered[kMaxTenants] = {};      // metric periods with any delivery (clean, fallback, model)
+  int64_t t_first_ns[kMaxTenants] = {}, t_last_ns[kMaxTenants] = {};  // first / last delivery (period stats)
   double mod_cur[kMaxTenants][kNumPmc] = {};       // modeled deltas of the newest consumed snapshot
   double mod_inflight[kMaxTenants][kNumPmc] = {};  // ... of the snapshot whose attribution is in flight
   double pres_cur[kMaxTenants] = {};               // largest owned share of a partition over the interval
@@ -663,6 +714,25 @@ int64_t guard_ns(const GpuCtx* c) {
   return ((int64_t)c->hwc_guard_us + (host ? 400 : 0)) * 1000;
 }
 
+// The modeled counter block into `out` (kBlk u64): rows [0, cnt_rows) are
+// read, the rest left as they were.  Fine-grained VRAM: CPU streaming loads
+// through the BAR (no GPU queue work); device memory: a copy on hwc_stream.
+bool read_block(GpuCtx* c, u64* out) {
+  constexpr int kRow = kXcds * kNumPmc;
+  if (c->cnt_bar) {
+    const int rows = std::min(kMaxTenants, std::max(1, c->cnt_rows.load(std::memory_order_relaxed)));
+    bar_read(c->d_cnt, out, sizeof(u64) * (size_t)rows * kRow);
+    return true;
+  }
+  if (hipMemcpyAsync(c->h_blk, c->d_cnt, sizeof(u64) * kMaxTenants * kRow, hipMemcpyDeviceToHost, c->hwc_stream) !=
+      hipSuccess)
+    return false;
+  hipEventRecord(c->blk_ev, c->hwc_stream);
+  hipEventSynchronize(c->blk_ev);
+  std::memcpy(out, c->h_blk, sizeof(u64) * kMaxTenants * kRow);
+  return true;
+}
+
 // Sampler thread.  Every hwc_period_us (1 ms) it reads the modeled per-tile
 // counter block (a 16 KiB device-to-host copy: no command-processor work) and
 // watches each tenant's modeled miss rate; a HARDWARE sample -- which stalls
@@ -746,11 +816,7 @@ void hwc_loop(GpuCtx* c) {
       //    with a hardware sample)
       const uint64_t sw = c->flushes.load(std::memory_order_relaxed);  // table publishes that changed an owner
       if (c->hwc_watch || sw != last_sw || t0 < burst_until || t0 - last_hw >= c->hwc_next_period_ns - tick / 4) {
-        if (hipMemcpyAsync(c->h_blk, c->d_cnt, sizeof(u64) * kBlk, hipMemcpyDeviceToHost, c->hwc_stream) != hipSuccess)
-          break;
-        hipEventRecord(c->blk_ev, c->hwc_stream);
-        hipEventSynchronize(c->blk_ev);
-        std::memcpy(blk.data(), c->h_blk, sizeof(u64) * kBlk);
+        if (!read_block(c, blk.data())) break;
       }
       bool trig = false;
       for (int t = 0; t < kMaxTenants; ++t) {
@@ -955,6 +1021,10 @@ void hwc_fold(GpuCtx* c, const HwcAttrOut& o, const double (*mod)[kNumPmc], cons
     if (o.add[t][0] <= 0) continue;  // did not run in the interval
     c->last_ran_ns[t] = t_s;
     const bool clean = c->clean_pct <= 0 || o.addc[t][0] > 0;
+    // 1 ms cadence: a calibrated tenant reported this interval tick by tick
+    // from its calibrated model (cadence_tick); its hardware windows only
+    // re-anchor the calibration
+    const bool ticked = c->model_cadence && c->cnt_bar && c->cal[t][0] > 0;
     double m[kNumPmc] = {0, 0, 0, 0};
     if (clean) {
       c->clean_periods++;
@@ -968,9 +1038,12 @@ void hwc_fold(GpuCtx* c, const HwcAttrOut& o, const double (*mod)[kNumPmc], cons
             const double r = o.add[t][k] / mod[t][k];
             c->cal[t][k] = c->cal[t][k] > 0 ? 0.75 * c->cal[t][k] + 0.25 * r : r;
           }
+      if (ticked) continue;
     } else if (pres && pres[t] < sub) {
       c->sliver_periods++;
       c->t_sliver[t]++;
+      continue;
+    } else if (ticked) {
       continue;
     } else {
       const bool stale = t_s - c->last_clean_ns[t] > (int64_t)c->hwc_stale_us * 1000;
@@ -1124,12 +1197,57 @@ int hwc_consume(GpuCtx* c, bool wait) {
   return 1;
 }
 
+// One metric tick of the 1 ms cadence (snap_mu held): every calibrated
+// tenant's modeled deltas since the previous tick, scaled per counter by its
+// hardware/model ratio, go to its pending metric deltas.  The block is read
+// through the BAR (no GPU work); without a host-readable block the cadence
+// is off and the hardware windows report, as before.
+void cadence_tick(GpuCtx* c) {
+  constexpr int kRow = kXcds * kNumPmc;
+  if (!c->model_cadence || !c->cnt_bar) return;
+  const int rows = std::min(kMaxTenants, std::max(1, c->cnt_rows.load(std::memory_order_relaxed)));
+  static thread_local std::vector<u64> cur;
+  cur.assign((size_t)kMaxTenants * kRow, 0);
+  bar_read(c->d_cnt, cur.data(), sizeof(u64) * (size_t)rows * kRow);
+  if (!c->cad_primed || c->cad_prev.size() != cur.size()) {
+    c->cad_prev = cur;
+    c->cad_primed = true;
+    return;
+  }
+  for (int t = 0; t < rows; ++t) {
+    if (c->cal[t][0] <= 0) continue;
+    double md[kNumPmc] = {0, 0, 0, 0};
+    for (int x = 0; x < kXcds; ++x)
+      for (int k = 0; k < kNumPmc; ++k) {
+        const size_t i = ((size_t)t * kXcds + x) * kNumPmc + k;
+        md[k] += (double)dpos(cur[i], c->cad_prev[i]);
+      }
+    if (md[0] <= 0) continue;
+    for (int k = 0; k < kNumPmc; ++k) {
+      const double v = md[k] * c->cal[t][k];
+      if (v <= 0) continue;
+      c->last_delta[t][k] += (u64)(v + 0.5);
+      c->metric_sum[k] += v;
+      c->met_total[t][k] += v;
+    }
+    c->t_model[t]++;
+  }
+  c->cad_prev.swap(cur);
+}
+
 int hwc_tenant_deltas(GpuCtx* c, int n, const int* tenants, uint64_t* out) {
   const int64_t t0 = mono_ns();
   RoctxRange rr("gpbs:metric_tick");
   {
     std::lock_guard<std::mutex> g(c->snap_mu);
     hwc_consume(c, false);
+    cadence_tick(c);
+    for (int k = 0; k < n; ++k) {  // per-tenant metric cadence: periods that delivered anything
+      const int t = tenants[k];
+      if (t < 0 || t >= kMaxTenants || !c->last_delta[t][0]) continue;
+      if (!c->t_delivered[t]++) c->t_first_ns[t] = t0;
+      c->t_last_ns[t] = t0;
+    }
   }
   // No new snapshot since the previous tick: every tenant reads zero
   // instructions and the PBS idle-sample rule (Q14) skips the period.
@@ -2077,7 +2195,11 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
   c->hwc_tokens = c->hwc_bucket;
   bool ok = hipHostMalloc((void**)&c->h_table, sizeof(PartTable), hipHostMallocCoherent | hipHostMallocMapped) ==
             hipSuccess;
-  ok = ok && hipMalloc((void**)&c->d_cnt, sizeof(u64) * kMaxTenants * kXcds * kNumPmc) == hipSuccess;
+  // the modeled counter block: host-readable fine-grained VRAM where the
+  // system has it (bar_read, no copy kernel), device memory otherwise
+  c->d_cnt = (u64*)finegrained_alloc(device, sizeof(u64) * kMaxTenants * kXcds * kNumPmc);
+  c->cnt_bar = c->d_cnt != nullptr;
+  if (!c->cnt_bar) ok = ok && hipMalloc((void**)&c->d_cnt, sizeof(u64) * kMaxTenants * kXcds * kNumPmc) == hipSuccess;
   ok = ok && hipMalloc((void**)&c->d_prev, sizeof(u64) * kMaxTenants * kXcds * kNumPmc) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_blk, sizeof(u64) * kMaxTenants * kXcds * kNumPmc, hipHostMallocDefault) ==
                  hipSuccess;
@@ -2095,7 +2217,7 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
   ok = ok && hipMalloc((void**)&c->d_ast, sizeof(HwcAttrPrev)) == hipSuccess;
   ok = ok && hipMemcpy(c->d_ast, &c->hst, sizeof(HwcAttrPrev), hipMemcpyHostToDevice) == hipSuccess;
   ok = ok && hipEventCreateWithFlags(&c->attr_ev, hipEventDisableTiming) == hipSuccess;
-  ok = ok && hipMemset(c->d_cnt, 0, sizeof(u64) * kMaxTenants * kXcds * kNumPmc) == hipSuccess;
+  if (!c->cnt_bar) ok = ok && hipMemset(c->d_cnt, 0, sizeof(u64) * kMaxTenants * kXcds * kNumPmc) == hipSuccess;
   ok = ok && hipMemset(c->d_prev, 0, sizeof(u64) * kMaxTenants * kXcds * kNumPmc) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_out, sizeof(u64) * 4 * kMaxTenants, hipHostMallocMapped) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_ids, sizeof(int) * kMaxTenants, hipHostMallocMapped) == hipSuccess;
@@ -2157,7 +2279,10 @@ void gpbs_gpu_ctx_destroy(void* p) {
   }
   hipStreamDestroy(c->sched_stream);
   hipHostFree(c->h_table);
-  hipFree(c->d_cnt);
+  if (c->cnt_bar)
+    hsa_amd_memory_pool_free(c->d_cnt);
+  else
+    hipFree(c->d_cnt);
   hipFree(c->d_prev);
   hipHostFree(c->h_out);
   if (c->hwc_stream) hipStreamDestroy(c->hwc_stream);
@@ -2827,7 +2952,7 @@ int gpbs_gpu_param(void* p, const char* name, int value) {
       {"guard_us", &c->hwc_guard_us, 0, 100000},        {"long_us", &c->hwc_long_us, 0, 100000000},
       {"pair_gap_us", &c->hwc_pair_gap_us, 0, 10000000}, {"measure_ms", &c->hwc_measure_ms, 0, 100000},
       {"share", &c->share_enable, 0, 1},                {"probe_every", &c->probe_every, 0, 1000000},
-      {"probe_len", &c->probe_len, 0, 1000000},
+      {"probe_len", &c->probe_len, 0, 1000000},         {"cadence", &c->model_cadence, 0, 1},
   };
   for (const Ent& e : tab)
     if (std::strcmp(e.n, name) == 0) {
@@ -2875,6 +3000,10 @@ int gpbs_gpu_hwc_reset(void* p) {
   std::memset(c->t_fallback, 0, sizeof(c->t_fallback));
   std::memset(c->t_skipped, 0, sizeof(c->t_skipped));
   std::memset(c->t_sliver, 0, sizeof(c->t_sliver));
+  std::memset(c->t_model, 0, sizeof(c->t_model));
+  std::memset(c->t_delivered, 0, sizeof(c->t_delivered));
+  std::memset(c->t_first_ns, 0, sizeof(c->t_first_ns));
+  std::memset(c->t_last_ns, 0, sizeof(c->t_last_ns));
   c->align_samples = c->align_close = c->align_long = c->align_short = c->align_denied = 0;
   c->attr_harvested = c->attr_ticks_sum = c->attr_ticks_max = 0;
   c->attr_lag_sum_ns = 0;
@@ -2949,6 +3078,21 @@ int gpbs_gpu_hwc_tenant_periods(void* p, int t, uint64_t* out4, double* out_cal4
   }
   if (out_cal4)
     for (int k = 0; k < kNumPmc; ++k) out_cal4[k] = c->cal[t][k];
+  return 0;
+}
+
+// Metric cadence of a tenant since the last hwc reset (round 6): out4 =
+// metric periods delivered from the calibrated model (1 ms ticks), periods
+// that delivered anything, the mean ns between delivering periods (0: fewer
+// than two), and whether the 1 ms cadence is live (host-readable block).
+int gpbs_gpu_hwc_tenant_cadence(void* p, int t, int64_t* out4) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c || t < 0 || t >= kMaxTenants || !out4) return -22;
+  std::lock_guard<std::mutex> g(c->snap_mu);
+  out4[0] = (int64_t)c->t_model[t];
+  out4[1] = (int64_t)c->t_delivered[t];
+  out4[2] = c->t_delivered[t] > 1 ? (c->t_last_ns[t] - c->t_first_ns[t]) / (int64_t)(c->t_delivered[t] - 1) : 0;
+  out4[3] = c->model_cadence && c->cnt_bar;
   return 0;
 }
 
@@ -3148,7 +3292,12 @@ int gpbs_gpu_read_counters(void* p, int tenant, uint64_t* out4, uint64_t* per_xc
   GpuCtx* c = (GpuCtx*)p;
   if (tenant < 0 || tenant >= kMaxTenants) return -22;
   u64 buf[kXcds * kNumPmc];
-  HIPCHECK(hipMemcpy(buf, c->d_cnt + (size_t)tenant * kXcds * kNumPmc, sizeof(buf), hipMemcpyDeviceToHost));
+  if (c->cnt_bar) {
+    HIPCHECK(hipDeviceSynchronize());  // finished kernels' counts have landed
+    bar_read(c->d_cnt + (size_t)tenant * kXcds * kNumPmc, buf, sizeof(buf));
+  } else {
+    HIPCHECK(hipMemcpy(buf, c->d_cnt + (size_t)tenant * kXcds * kNumPmc, sizeof(buf), hipMemcpyDeviceToHost));
+  }
   for (int i = 0; i < 4; ++i) {
     out4[i] = 0;
     for (int x = 0; x < kXcds; ++x) out4[i] += buf[x * 4 + i];
@@ -3397,6 +3546,8 @@ void* gpbs_runner_create(void* ctx, const gpbs_runner_cfg_t* cfg) {
   if (cfg->alt_kind == K_GEMV && cfg->alt_K % 512) return nullptr;
   if (cfg->alt_kind < 0 || cfg->alt_kind > K_GEMV) return nullptr;
   hipSetDevice(c->device);
+  for (int have = c->cnt_rows.load(); have < cfg->tenant + 1 && !c->cnt_rows.compare_exchange_weak(have, cfg->tenant + 1);) {
+  }
   auto* r = new Runner;
   r->ctx = c;
   r->cfg = *cfg;

@@ -50,7 +50,7 @@ __global__ __launch_bounds__(64) void k_counter_reduce(u64* cnt, u64* prev, cons
   u64 d = 0;
   if (lane < kXcds * kNumPmc && tid >= 0 && tid < kMaxTenants) {
     const size_t off = (size_t)tid * kXcds * kNumPmc + lane;
-    const u64 c = __hip_atomic_load(cnt + off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const u64 c = __hip_atomic_load(cnt + off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const u64 p = prev[off];
     d = c >= p ? c - p : 0;  // Q5: counter reset -> no negative delta
     prev[off] = c;

@@ -254,6 +254,14 @@ POLICY_ENGINES = {
     # quantum, floored at a global 30 ms)
     "gpbs-sq30": (4, dict(BUDGET_OVERRIDES, class_budget=1, region_q=1, shared_q_us=30000), True,
                   "device,se,waveprio,latco,budget,latmem"),
+    # the long-quantum ablations with credit ordering the time-shared region
+    # (region_vt 0: round 5's dispatch core)
+    "credit-fixed-ts30-novt": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="credit-fixed", tslice_us=30000,
+                                       region_vt=0), True, "device,se,waveprio,latco,budget,latmem"),
+    "atc-novt": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="atc", region_vt=0), True,
+                 "device,se,waveprio,latco,budget,latmem"),
+    "gpbs-novt": (4, dict(BUDGET_OVERRIDES, class_budget=1, region_vt=0), True,
+                  "device,se,waveprio,latco,budget,latmem"),
     # the PBS quantum without the measured switch-cost floors
     "gpbs-nofloor": (4, dict(BUDGET_OVERRIDES, class_budget=1, switch_floor_x=0), True,
                      "device,se,waveprio,latco,budget,latmem"),
