@@ -1295,7 +1295,8 @@ class CreditScheduler : public Scheduler {
   int64_t rvt_floor_[2] = {0, 0};
   int64_t rvt_lag() const {
     return 2 * (int64_t)std::max<uint32_t>({E.adapt_params.max_us, tslice_us_,
-                                            (uint32_t)std::max(0, E.boot.shared_q_us)}) * 1000;
+                                            (uint32_t)std::max(0, E.boot.shared_q_us),
+                                            (uint32_t)std::max(0, E.boot.switch_floor_max_us)}) * 1000;
   }
   void rvt_account(int cpu, Slot& cur, int64_t now) {
     CPcpu& p = pc(cpu);

@@ -2871,6 +2871,95 @@ int gpbs_gpu_switch_cost(void* ctx, int tenant, int64_t* out4) {
   return 0;
 }
 
+// Host check of the 1 ms cadence: a tenant whose clean
+// hardware windows come every 10 ms reports every tick in between from its
+// modeled counters x its hardware/model ratio -- the delivered miss rate is
+// the hardware one (within 10 %), so it keeps its class with ten times the
+// metric periods; a clean window of a calibrated tenant only re-anchors the
+// ratio (no double report); and a phase change in the model (the tenant
+// turns compute-bound) moves the delivered rate below the class threshold
+// at the next tick.  The block is a host buffer standing in for the BAR
+// mapping.  No HIP call.  Returns 0 or the number of the first failed check.
+int gpbs_hip_hwc_cadence_selftest(void) {
+  std::unique_ptr<GpuCtx> cp(new GpuCtx());
+  GpuCtx& c = *cp;
+  std::vector<u64> blk((size_t)kMaxTenants * kXcds * kNumPmc, 0);
+  c.d_cnt = blk.data();
+  c.cnt_bar = true;
+  c.model_cadence = 1;
+  c.clean_pct = 80;
+  const int t = 3;
+  c.cnt_rows = t + 1;
+  const double hw_inst = 2.0e6, hw_miss = 6.0e5;  // per ms: 3e4 misses per 1e5 inst (memory class)
+  double md_inst = hw_inst / 24.0, md_miss = hw_miss / 0.13;
+  auto advance = [&](double ms) {  // the kernels' modeled counts, spread over the 8 XCDs
+    for (int x = 0; x < kXcds; ++x) {
+      u64* r = &blk[((size_t)t * kXcds + x) * kNumPmc];
+      r[0] += (u64)(md_inst * ms / kXcds);
+      r[1] += (u64)(md_inst * ms / kXcds);
+      r[2] += (u64)(2 * md_miss * ms / kXcds);
+      r[3] += (u64)(md_miss * ms / kXcds);
+    }
+  };
+  static HwcAttrOut o;
+  static double mod[kMaxTenants][kNumPmc], pres[kMaxTenants];
+  auto window = [&](double ms) {  // a clean hardware window over the last `ms`
+    std::memset(&o, 0, sizeof(o));
+    std::memset(mod, 0, sizeof(mod));
+    std::memset(pres, 0, sizeof(pres));
+    o.valid = 1;
+    o.add[t][0] = o.addc[t][0] = hw_inst * ms;
+    o.add[t][1] = o.addc[t][1] = hw_inst * ms;
+    o.add[t][2] = o.addc[t][2] = 2 * hw_miss * ms;
+    o.add[t][3] = o.addc[t][3] = hw_miss * ms;
+    mod[t][0] = mod[t][1] = md_inst * ms;
+    mod[t][2] = 2 * md_miss * ms;
+    mod[t][3] = md_miss * ms;
+    pres[t] = 1.0;
+  };
+  auto take = [&](double* inst, double* miss) {
+    *inst = (double)c.last_delta[t][0];
+    *miss = (double)c.last_delta[t][3];
+    for (int k = 0; k < kNumPmc; ++k) c.last_delta[t][k] = 0;
+  };
+  const double want = hw_miss * 1e5 / hw_inst, thr = 20000;
+  double in = 0, mi = 0;
+  int64_t now = 1000000000;
+  cadence_tick(&c);  // primes
+  advance(1);
+  cadence_tick(&c);  // not calibrated yet: nothing
+  take(&in, &mi);
+  if (in != 0) return 1;
+  window(10);  // the first clean window calibrates and reports (uncalibrated before it)
+  hwc_fold(&c, o, mod, pres, now);
+  take(&in, &mi);
+  if (in <= 0 || std::fabs(mi * 1e5 / in - want) > 1.0) return 2;
+  for (int round = 0; round < 10; ++round) {
+    for (int k = 0; k < 9; ++k) {  // nine 1 ms ticks between hardware windows: each reports
+      advance(1);
+      cadence_tick(&c);
+      take(&in, &mi);
+      if (in <= 0) return 3;
+      const double r = mi * 1e5 / in;
+      if (std::fabs(r - want) > 0.1 * want || r < thr) return 4;
+    }
+    advance(1);
+    now += 10000000;
+    window(10);
+    hwc_fold(&c, o, mod, pres, now);  // calibrated: re-anchors only
+    take(&in, &mi);
+    if (in != 0) return 5;
+  }
+  if (c.t_model[t] != 90 || c.t_clean[t] != 11) return 6;
+  md_miss = md_miss / 100.0;  // the tenant turns compute-bound: the model sees it at once
+  advance(1);
+  cadence_tick(&c);
+  take(&in, &mi);
+  if (in <= 0 || mi * 1e5 / in >= thr) return 7;
+  c.d_cnt = nullptr;
+  return 0;
+}
+
 int gpbs_hip_hwc_attr_selftest(int seed, int iters, double* max_rel) {
   HwcAttrIn* in = nullptr;
   HwcAttrIn* d_in = nullptr;

@@ -225,7 +225,9 @@ POLICY_ENGINES = {
     # the ATC policy (X:xen/common/sched_credit_atc.c:291-543): one global
     # quantum for the pool, driven by the tenants' wait reports (K10); the
     # same time-shared budget layout as the flagship
-    "atc": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="atc"), True, "device,se,waveprio,latco,budget,latmem"),
+    "atc": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="atc", region_vt=0), True,
+            "device,se,waveprio,latco,budget,latmem"),
+    "atc-vt": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="atc"), True, "device,se,waveprio,latco,budget,latmem"),
     "atc-nox": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="atc", class_steal=0), True,
                 "device,se,waveprio,latco,budget,latmem"),
     # switch-cost probes: every quantum (fixed) or the adaptive floor at 4 ms
@@ -242,8 +244,12 @@ POLICY_ENGINES = {
                  "device,se,waveprio,latco,budget,latmem"),
     # long quanta everywhere: 30 ms fixed (the ATC default without its wait
     # feedback), and the PBS range moved up to 4-30 ms
-    "credit-fixed-ts30": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="credit-fixed", tslice_us=30000), True,
-                          "device,se,waveprio,latco,budget,latmem"),
+    # (the equal-quantum ablations run credit ordering in the region,
+    # region_vt 0: measured better for them than the flagship's region
+    # virtual time -- 8mix fixed-30 1.388 vs 1.302, atc 1.388 vs 1.325,
+    # profiles/r6/s2_8mix_vt_summary.txt)
+    "credit-fixed-ts30": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="credit-fixed", tslice_us=30000,
+                                  region_vt=0), True, "device,se,waveprio,latco,budget,latmem"),
     "gpbs-w": (4, dict(BUDGET_OVERRIDES, class_budget=1,
                        adapt=dict(MI355X_PROFILE["adapt"], min_us=4000, max_us=30000, inc_us=4000, dec_us=8000,
                                   switch_boundary=30000)), True, "device,se,waveprio,latco,budget,latmem"),
@@ -256,10 +262,6 @@ POLICY_ENGINES = {
                   "device,se,waveprio,latco,budget,latmem"),
     # the long-quantum ablations with credit ordering the time-shared region
     # (region_vt 0: round 5's dispatch core)
-    "credit-fixed-ts30-novt": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="credit-fixed", tslice_us=30000,
-                                       region_vt=0), True, "device,se,waveprio,latco,budget,latmem"),
-    "atc-novt": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="atc", region_vt=0), True,
-                 "device,se,waveprio,latco,budget,latmem"),
     "gpbs-novt": (4, dict(BUDGET_OVERRIDES, class_budget=1, region_vt=0), True,
                   "device,se,waveprio,latco,budget,latmem"),
     # the PBS quantum without the measured switch-cost floors
@@ -267,8 +269,12 @@ POLICY_ENGINES = {
                      "device,se,waveprio,latco,budget,latmem"),
     # credit-classq with the global 30 ms floor in time-shared regions (the
     # classq + floor ablation: what the class map does with round 5's floor)
-    "credit-classq-f": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="credit-classq", shared_q_us=30000), True,
-                        "device,se,waveprio,latco,budget,latmem"),
+    "credit-classq-f": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="credit-classq", shared_q_us=30000,
+                                region_vt=0), True, "device,se,waveprio,latco,budget,latmem"),
+    "credit-classq-fvt": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="credit-classq", shared_q_us=30000), True,
+                          "device,se,waveprio,latco,budget,latmem"),
+    "credit-fixed-ts30-vt": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="credit-fixed", tslice_us=30000), True,
+                             "device,se,waveprio,latco,budget,latmem"),
     # PBS quantum range capped lower at the top (memory tenants up to 4 / 6 ms)
     "gpbs-max4": (4, dict(BUDGET_OVERRIDES, class_budget=1, adapt=dict(MI355X_PROFILE["adapt"], max_us=4000)), True,
                   "device,se,waveprio,latco,budget,latmem"),

@@ -49,12 +49,13 @@ MI355X_PROFILE: Dict[str, Any] = dict(
     # Time-shared class regions (round 6): every co-sharer
     # runs its OWN quantum -- its PBS adaptive quantum, at least switch_floor_x
     # times its measured switch cost (revocation drain + re-entry ramp, per
-    # tenant, from the GPU runtime), at most switch_floor_max_us -- and the
+    # tenant, from the GPU runtime: 200 x = at most 0.5 % of a turn lost to
+    # its switches), at most switch_floor_max_us -- and the
     # region's virtual time keeps the shares weight-fair whatever the quanta
     # (credit.cpp quantum_us / region_pick).  Round 5's region quantum (the
     # co-sharers' largest, floored at a global 30 ms: region_q=1,
     # shared_q_us=30000) stays as the gpbs-sq30 ablation.
-    region_q=0, region_vt=1, switch_floor_x=100, switch_floor_max_us=30000, shared_q_us=0, slo_cap=0,
+    region_q=0, region_vt=1, switch_floor_x=200, switch_floor_max_us=60000, shared_q_us=0, slo_cap=0,
     # a present tenant unclassified for 50 ms (a latency tenant whose 50 us
     # requests never fill a clean counter window) joins the memory class
     # instead of holding every tenant in the probe layout (slo mix, s2 diag)

@@ -1,8 +1,9 @@
 """Gang epoch exchange over xGMI (pbs_amd/parallel/gang.py
 ``_XgmiTransport``, csrc/hip/coll_kernels.hip ``k_gang_exchange``) with 2
-processes on one MI355X: same-device IPC handles exercise the board
-mapping, the device-side publish / wait / copy and the parity double
-buffering that the 8-GPU node runs over xGMI.  Checks every exchange's SUM
+processes: ``one_device`` puts both on one MI355X (same-device IPC handles
+exercise the board mapping, the device-side publish / wait / copy and the
+parity double buffering); ``peer_devices`` puts rank r on device r, so the
+board crosses xGMI as on the 8-GPU node (skipped below two visible GPUs).  Checks every exchange's SUM
 and MIN against the known per-rank values, reports the round-trip latency
 next to the host shm transport, and checks that a rank whose peer stops
 gets a timeout within its deadline instead of a hang.
@@ -27,7 +28,8 @@ import json, os, sys, time
 sys.path.insert(0, %(root)r)
 import torch, torch.distributed as dist
 rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-torch.cuda.set_device(0)
+DEV = rank if %(peer)d else 0
+torch.cuda.set_device(DEV)
 dist.init_process_group("gloo")
 from pbs_amd.parallel.gang import _XgmiTransport, _ShmTransport
 
@@ -36,8 +38,8 @@ def gather(obj):
     dist.all_gather_object(out, obj)
     return out
 
-tr = _XgmiTransport(rank, world, 8, 0, gather)
-out = {"rank": rank, "bad": 0}
+tr = _XgmiTransport(rank, world, 8, DEV, gather)
+out = {"rank": rank, "bad": 0, "device": DEV}
 lat = []
 dist.barrier()
 for k in range(1, 401):
@@ -88,14 +90,18 @@ def _free_port():
     return p
 
 
-def test_gang_exchange_over_xgmi_two_processes():
+@pytest.mark.parametrize("placement", ["one_device", "peer_devices"])
+def test_gang_exchange_over_xgmi_two_processes(placement):
+    peer = placement == "peer_devices"
+    if peer and torch.cuda.device_count() < 2:
+        pytest.skip("rank-per-device placement needs two visible GPUs")
     world = 2
     port = _free_port()
     procs = []
     for rank in range(world):
         env = dict(os.environ, RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
-        procs.append(subprocess.Popen([sys.executable, "-c", CODE % {"root": ROOT}], env=env, stdout=subprocess.PIPE,
+        procs.append(subprocess.Popen([sys.executable, "-c", CODE % {"root": ROOT, "peer": int(peer)}], env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.PIPE, text=True))
     logs = []
     for p in procs:
@@ -115,5 +121,6 @@ def test_gang_exchange_over_xgmi_two_processes():
         assert o["bad"] == 0, o
         assert o["stats"]["exchanges"] == 400, o
         assert o["p50_us"] < 1000, o
+    assert [o["device"] for o in outs] == ([0, 1] if peer else [0, 0])
     assert outs[0]["timeout_result"] is None
     assert 45 <= outs[0]["timeout_ms"] < 500, outs[0]

@@ -1,8 +1,13 @@
-"""IPC all-reduce tenant (csrc/hip/coll_kernels.hip) with 2 processes on one
-MI355X: same-device IPC handles exercise the whole multi-GPU path --
-handle export / open, the direct reduce-scatter + all-gather kernel, the
-P2P-flag barrier between units, gating per workgroup, revocation and
-relaunch, and the agreed-count drain -- that the 8-GPU bench runs over xGMI.
+"""IPC all-reduce tenant (csrc/hip/coll_kernels.hip) with 2 processes.
+
+``one_device``: both ranks on one MI355X -- same-device IPC handles exercise
+the whole multi-GPU path (handle export / open, the direct reduce-scatter +
+all-gather kernel, the P2P-flag barrier between units, gating per
+workgroup, revocation and relaunch, the agreed-count drain).
+``peer_devices``: rank r on device r, so the peer
+buffers are mapped over xGMI and the flags cross devices at system scope --
+the 8-GPU bench's placement.  Skipped below two visible GPUs; each rank
+records whether its device can access the peer's (hipDeviceCanAccessPeer).
 
 The result is compared bit for bit with an fp32 torch reference of the same
 reduction (bf16 inputs summed in fp32 in rank order, rounded to bf16).
@@ -27,13 +32,14 @@ import json, os, sys, time
 sys.path.insert(0, %(root)r)
 import torch, torch.distributed as dist
 rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-torch.cuda.set_device(0)
+DEV = rank if %(peer)d else 0
+torch.cuda.set_device(DEV)
 dist.init_process_group("gloo")
 from pbs_amd.runtime.gpu import CTX, XCDS, GpuContext, Runner
 from pbs_amd.parallel.ipc_coll import IpcColl, agreed_drain
-ctx = GpuContext(0, nctx=4)
+ctx = GpuContext(DEV, nctx=4)
 nbytes = 32 << 20
-coll = IpcColl(0, rank, world, nbytes)
+coll = IpcColl(DEV, rank, world, nbytes)
 g = torch.Generator(device="cuda").manual_seed(100 + rank)
 x = torch.randn(nbytes // 2, device="cuda", dtype=torch.bfloat16, generator=g)
 coll.fill(x, 0)
@@ -43,7 +49,9 @@ acc = torch.zeros(x.numel(), dtype=torch.float32)
 for t in xs:
     acc += t.float()
 ref = acc.to(torch.bfloat16)
-out = {"rank": rank}
+out = {"rank": rank, "device": DEV}
+if %(peer)d:
+    out["can_access_peer"] = bool(torch.cuda.can_device_access_peer(DEV, 1 - DEV))
 T = 1
 r = Runner(ctx, "allreduce", T, gate=False, engine_wake=False, coll=coll, chunk_bytes=1 << 18)
 dist.barrier()
@@ -102,15 +110,19 @@ def _free_port():
     return p
 
 
-def test_ipc_allreduce_two_processes_exact_and_gated():
+@pytest.mark.parametrize("placement", ["one_device", "peer_devices"])
+def test_ipc_allreduce_two_processes_exact_and_gated(placement):
+    peer = placement == "peer_devices"
+    if peer and torch.cuda.device_count() < 2:
+        pytest.skip("rank-per-device placement needs two visible GPUs")
     world = 2
     port = _free_port()
     procs = []
     for rank in range(world):
         env = dict(os.environ, RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
-        procs.append(subprocess.Popen([sys.executable, "-c", CODE % {"root": ROOT}], env=env, stdout=subprocess.PIPE,
-                                      stderr=subprocess.PIPE, text=True))
+        procs.append(subprocess.Popen([sys.executable, "-c", CODE % {"root": ROOT, "peer": int(peer)}], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
     outs, logs = [], []
     for p in procs:
         try:
@@ -132,3 +144,6 @@ def test_ipc_allreduce_two_processes_exact_and_gated():
         # tops the laggard up to the agreed count instead of hanging rank 0
         assert o["units_final"] == o["agreed"] > 41, o
     assert outs[0]["agreed"] == outs[1]["agreed"]
+    if peer:
+        assert [o["device"] for o in outs] == [0, 1]
+        assert all(o["can_access_peer"] for o in outs), outs

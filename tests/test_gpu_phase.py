@@ -90,6 +90,7 @@ pc = e.perfc()
 out["adapt_rearm"] = pc["adapt_rearm"]; out["relayout"] = pc["relayout"]; out["class_change"] = pc["class_change"]
 out["units_alt"] = rp.stats().units_alt
 out["hwc"] = ctx.hwc_stats()
+out["periods"] = {n: ctx.hwc_tenant_periods(t) for n, t in (("gemm", g), ("phase", p), ("hbm", s))}
 for r in (rg, rp, rs):
     r.cancel()
 for r in (rg, rp, rs):
@@ -113,13 +114,17 @@ def test_budget_layout_follows_a_phase_change_on_live_counters(align):
     out = json.loads([x for x in r.stdout.splitlines() if x.startswith("RESULT ")][-1][7:])
     print(json.dumps(out, indent=1))
     assert out["settle_ms"] >= 0, out
-    # within 150 metric periods (1 ms each) of the change in both directions:
+    # within 50 metric periods (1 ms each) of the change in both directions:
     # the classifier's EWMA (alpha 1/4 rising, 1/2 falling), its dwell and the
-    # class tick.  Round-5 boxes measured 108-128 ms compute -> memory (the
-    # rise needs several clean samples of the phase tenant's new phase) and
-    # 14-15 ms back.
-    assert 0 <= out["to_memory_ms"] < 150, out
-    assert 0 <= out["to_compute_ms"] < 150, out
+    # class tick.  Round 5 measured 108-128 ms compute -> memory (the rise
+    # waited for clean hardware windows of the new phase, 9-47 ms apart);
+    # with the 1 ms cadence (the calibrated model reports every tick, the
+    # hardware windows re-anchor it) the classifier sees the new phase at the
+    # next tick.
+    assert 0 <= out["to_memory_ms"] < 50, out
+    assert 0 <= out["to_compute_ms"] < 50, out
+    if out["periods"]["phase"]["cadence"]:  # host-readable counter block: the 1 ms cadence is live
+        assert out["periods"]["phase"]["model"] > 0, out["periods"]
     assert out["units_alt"] > 0
     assert out["class_change"] >= 2 and out["relayout"] >= 2, out
     assert out["adapt_rearm"] > 0, out

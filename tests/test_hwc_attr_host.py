@@ -68,3 +68,15 @@ def test_kernel_trace_is_off_unless_enabled_before_init():
     from pbs_amd.counters import hwc
     assert hwc.trace_stats() is None
     assert CorunConfig().kernel_trace is False
+
+
+def test_one_ms_cadence_from_the_calibrated_model_keeps_the_class():
+    """The 1 ms metric cadence (csrc/hip/runtime.cpp cadence_tick, VERDICT r5
+    item 3): between clean hardware windows 10 ms apart, every metric tick
+    reports the tenant's modeled deltas x its hardware/model ratio -- the
+    hardware miss rate within 10 %, so its class holds with ten times the
+    metric periods; a calibrated tenant's clean window only re-anchors the
+    ratio (nothing reported twice); a phase change in the model crosses the
+    class threshold at the next tick."""
+    from pbs_amd.ops import kernels as K
+    assert K.lib().gpbs_hip_hwc_cadence_selftest() == 0
