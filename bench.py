@@ -280,6 +280,22 @@ def main():
         build.build_all()
     if world > 1:
         dist.barrier(group=groups["ctrl"])
+    # masked-queue pipe pre-flight: the burst of
+    # CU-masked queues is made now -- after RCCL's communicators (one small
+    # all-reduce on the coll group brings them up) -- and checked against
+    # KFD's queue ids; a failed check is a rank failure in the line
+    try:
+        if world > 1 and not args.rehearse:
+            import torch.distributed as dist
+            dist.all_reduce(torch.ones(1, device="cuda"), group=groups["coll"])
+            torch.cuda.synchronize()
+        from pbs_amd.ops import kernels as _K
+        from pbs_amd.utils.pipes import pipe_preflight
+        rank_diag["pipes"] = pipe_preflight(_K.lib(), local)
+    except Exception as ex:  # noqa: BLE001
+        rank_diag["pipes"] = {"ok": False, "error": str(ex)[:200]}
+    if not rank_diag["pipes"].get("ok"):
+        print(f"bench.py: rank {rank}: masked-queue pipe pre-flight failed: {rank_diag['pipes']}", file=sys.stderr)
     from pbs_amd.bench.corun import MIXES, Corun, CorunConfig
     # gang epochs (N > 1): native shared-memory transport among the node's
     # ranks; the region name is a nonce from rank 0 so no stale region matches

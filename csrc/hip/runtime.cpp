@@ -3448,6 +3448,34 @@ int gpbs_gpu_masked_pool(uint64_t* out5, int reset) {
 
 // Host check of the masked-queue pool policy: fake queue handles,
 // no HIP call.  Returns 0 or the number of the first failed check.
+// Bench pre-flight: create this process's masked-queue
+// burst now (normally at first use) -- after RCCL has made its own queues --
+// and report it: returns the queues the pool holds on `device`, out[i] =
+// pipe | half << 8 of pool queue i (the burst-relative pipe and the class
+// half of its CU mask), max entries.  The caller compares the KFD queue ids
+// the process gained around this call with the burst (one contiguous run).
+int gpbs_hip_masked_pool_prealloc(int device, int* out, int max) {
+  if (hipSetDevice(device) != hipSuccess) return -19;
+  uint32_t mc[8], mm[8];
+  half_mask(0, mc);
+  half_mask(1, mm);
+  const uint32_t* masks[2] = {mc, mm};
+  auto create = [](const uint32_t* m) -> hipStream_t {
+    hipStream_t s = nullptr;
+    return hipExtStreamCreateWithCUMask(&s, 8, const_cast<uint32_t*>(m)) == hipSuccess ? s : nullptr;
+  };
+  MaskedPoolCore& P = masked_pool();
+  if (P.prealloc(device, masks, kPlan, kPlanLen, create) < 0) return -12;
+  std::lock_guard<std::mutex> g(P.mu);
+  int n = 0;
+  for (const auto& e : P.ents)
+    if (e.device == device) {
+      if (out && n < max) out[n] = e.pipe | ((std::memcmp(e.m, mm, sizeof(mm)) == 0 ? 1 : 0) << 8);
+      ++n;
+    }
+  return n;
+}
+
 int gpbs_hip_masked_pool_selftest(void) {
   MaskedPoolCore P;
   uintptr_t next = 0x1000;

@@ -155,6 +155,8 @@ def ranks_digest(ranks: List[dict]) -> dict:
             why.append("agent_bdf")
         if r.get("cu_map_ok") is False:
             why.append("cu_map")
+        if (r.get("pipes") or {}).get("ok") is False:
+            why.append("pipes")
         for mix, m in (r.get("mixes") or {}).items():
             if m.get("ipc_selftest") == "failed":
                 why.append(f"{mix}:ipc_selftest")

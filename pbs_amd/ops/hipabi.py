@@ -119,6 +119,7 @@ def bind(lib):
     _p(lib, "gpbs_hip_hwc_fold_selftest", C.c_int)
     _p(lib, "gpbs_hip_hwc_drained_selftest", C.c_int, C.c_int, C.c_int)
     _p(lib, "gpbs_hip_hwc_cadence_selftest", C.c_int)
+    _p(lib, "gpbs_hip_masked_pool_prealloc", C.c_int, C.c_int, C.POINTER(C.c_int), C.c_int)
     _p(lib, "gpbs_gpu_adapt_stats", C.c_int, vp, C.POINTER(u64), C.POINTER(u64), C.POINTER(u64))
     _p(lib, "gpbs_hip_hwc_attr_selftest", C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double))
     _p(lib, "gpbs_hip_hwc_attr_host_check", C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double))
