@@ -410,6 +410,8 @@ struct GpuCtx {
   std::vector<u64> cad_prev;                   // the block at the previous tick (snap_mu)
   bool cad_primed = false;
   uint64_t t_model[kMaxTenants] = {};          // metric periods delivered from the calibrated model
+  uint64_t t_moved[kMaxTenants] = {};          // ticks its modeled counters moved (calibrated or not)
+  uint64_t cad_calls = 0;                      // cadence ticks
   uint64_t t_delivered[kMaxTenants] = {};      // metric periods with any delivery (clean, fallback, model)
   int64_t t_first_ns[kMaxTenants] = {}, t_last_ns[kMaxTenants] = {};  // first / last delivery (period stats)
   double mod_cur[kMaxTenants][kNumPmc] = {};       // modeled deltas of the newest consumed snapshot
@@ -1214,8 +1216,8 @@ void cadence_tick(GpuCtx* c) {
     c->cad_primed = true;
     return;
   }
+  c->cad_calls++;
   for (int t = 0; t < rows; ++t) {
-    if (c->cal[t][0] <= 0) continue;
     double md[kNumPmc] = {0, 0, 0, 0};
     for (int x = 0; x < kXcds; ++x)
       for (int k = 0; k < kNumPmc; ++k) {
@@ -1223,6 +1225,8 @@ void cadence_tick(GpuCtx* c) {
         md[k] += (double)dpos(cur[i], c->cad_prev[i]);
       }
     if (md[0] <= 0) continue;
+    c->t_moved[t]++;
+    if (c->cal[t][0] <= 0) continue;
     for (int k = 0; k < kNumPmc; ++k) {
       const double v = md[k] * c->cal[t][k];
       if (v <= 0) continue;
@@ -3090,6 +3094,8 @@ int gpbs_gpu_hwc_reset(void* p) {
   std::memset(c->t_skipped, 0, sizeof(c->t_skipped));
   std::memset(c->t_sliver, 0, sizeof(c->t_sliver));
   std::memset(c->t_model, 0, sizeof(c->t_model));
+  std::memset(c->t_moved, 0, sizeof(c->t_moved));
+  c->cad_calls = 0;
   std::memset(c->t_delivered, 0, sizeof(c->t_delivered));
   std::memset(c->t_first_ns, 0, sizeof(c->t_first_ns));
   std::memset(c->t_last_ns, 0, sizeof(c->t_last_ns));
@@ -3170,10 +3176,39 @@ int gpbs_gpu_hwc_tenant_periods(void* p, int t, uint64_t* out4, double* out_cal4
   return 0;
 }
 
+// Freshness probe of the host-readable counter block (tools): `n` reads of
+// tenant t's instruction counter `gap_us` apart, through the BAR (mode 0) or
+// a device-to-host copy (mode 1); returns how many reads saw a new value.
+int gpbs_gpu_block_probe(void* p, int t, int n, int gap_us, int mode, int64_t* last) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c || t < 0 || t >= kMaxTenants || n <= 0) return -22;
+  if (mode == 0 && !c->cnt_bar) return -95;
+  u64 row[kXcds * kNumPmc];
+  u64 prev = 0;
+  int changed = 0;
+  for (int i = 0; i < n; ++i) {
+    if (mode == 0) {
+      bar_read(c->d_cnt + (size_t)t * kXcds * kNumPmc, row, sizeof(row));
+    } else if (hipMemcpy(row, c->d_cnt + (size_t)t * kXcds * kNumPmc, sizeof(row), hipMemcpyDeviceToHost) != hipSuccess) {
+      return -5;
+    }
+    u64 v = 0;
+    for (int x = 0; x < kXcds; ++x) v += row[x * kNumPmc];
+    if (i && v != prev) ++changed;
+    prev = v;
+    const int64_t t0 = mono_ns();
+    while (mono_ns() - t0 < (int64_t)gap_us * 1000) {
+    }
+  }
+  if (last) *last = (int64_t)prev;
+  return changed;
+}
+
 // Metric cadence of a tenant since the last hwc reset (round 6): out4 =
 // metric periods delivered from the calibrated model (1 ms ticks), periods
 // that delivered anything, the mean ns between delivering periods (0: fewer
-// than two), and whether the 1 ms cadence is live (host-readable block).
+// than two), whether the 1 ms cadence is live (host-readable block), the
+// ticks its modeled counters moved, and the cadence ticks so far (out6).
 int gpbs_gpu_hwc_tenant_cadence(void* p, int t, int64_t* out4) {
   GpuCtx* c = (GpuCtx*)p;
   if (!c || t < 0 || t >= kMaxTenants || !out4) return -22;
@@ -3182,6 +3217,8 @@ int gpbs_gpu_hwc_tenant_cadence(void* p, int t, int64_t* out4) {
   out4[1] = (int64_t)c->t_delivered[t];
   out4[2] = c->t_delivered[t] > 1 ? (c->t_last_ns[t] - c->t_first_ns[t]) / (int64_t)(c->t_delivered[t] - 1) : 0;
   out4[3] = c->model_cadence && c->cnt_bar;
+  out4[4] = (int64_t)c->t_moved[t];
+  out4[5] = (int64_t)c->cad_calls;
   return 0;
 }
 

@@ -214,14 +214,15 @@ class GpuContext:
         o = (C.c_uint64 * 4)()
         cal = (C.c_double * 4)()
         self.L.gpbs_gpu_hwc_tenant_periods(self.h, int(tenant), o, cal)
-        cd = (C.c_int64 * 4)()
+        cd = (C.c_int64 * 6)()
         self.L.gpbs_gpu_hwc_tenant_cadence(self.h, int(tenant), cd)
         # model: 1 ms ticks from the calibrated model; delivered: metric periods
         # with any delivery; period_ms: mean time between those (the effective
         # metric period of the tenant)
         return {"clean": o[0], "fallback": o[1], "skipped": o[2], "sliver": o[3],
                 "cal": [round(x, 4) for x in cal], "model": int(cd[0]), "delivered": int(cd[1]),
-                "period_ms": round(cd[2] / 1e6, 2), "cadence": bool(cd[3])}
+                "period_ms": round(cd[2] / 1e6, 2), "cadence": bool(cd[3]), "moved": int(cd[4]),
+                "ticks": int(cd[5])}
 
     def switch_cost(self, tenant: int) -> dict:
         """The tenant's measured switch cost (round 6): EWMA revocation drain

@@ -429,3 +429,57 @@ def test_shared_region_quantum_floor():
         out[sq] = sorted(q)[len(q) // 2] if q else 0
         assert e.check() == ""
     assert out[0] <= 2000 and out[30000] >= 30000, out
+
+
+def test_reported_quanta_are_the_switch_to_switch_run_lengths():
+    """the quantum the engine reports for a tenant of a
+    time-shared region (tenant_info.tslice_us, the bound statistics, the
+    bench's per-tenant quanta) is the s_timer quantum it is dispatched with:
+    on a simulated time-shared region, every tenure that ended at its quantum
+    (no wake / block in between) lasted exactly the SWITCH record's quantum,
+    and that is the tenant's reported quantum -- per tenant: the 1 ms
+    co-sharer and its 11 ms partners differ, and a tenant with a measured
+    switch cost gets its floor (switch_floor_x x cost), not its adaptive
+    target."""
+    e, parts = _engine(present_us=10000)
+    gs = [e.tenant_create(f"g{i}", nslots=8) for i in range(3)]
+    ms = [e.tenant_create(f"m{i}", nslots=8) for i in range(4)]
+    rates = {**{t: COMPUTE for t in gs}, **{t: MEMORY for t in ms}}
+    for t in rates:
+        e.wake(t)
+    _settle(e, rates, 800)
+    st = e.adapt_state(ms[3])
+    st.tslice_us, st.tick_period_us = 1000, 333
+    e.set_adapt_state(ms[3], st)
+    rates[ms[3]] = (0, 0)  # counters stop: its adaptive quantum stays at 1 ms
+    x = MI355X_PROFILE["switch_floor_x"]
+    e.switch_cost(ms[2], 75_000)  # a measured 75 us switch: floor x * 75 us
+    _settle(e, rates, 200)
+    e.trace(from_start=True)
+    _settle(e, rates, 2000)
+    recs = [r for r in e.trace() if r.event == "SWITCH"]
+    info = {m: e.tenant_info(m) for m in ms}
+    assert info[ms[3]].tslice_us == 1000
+    assert info[ms[2]].target_tslice_us == 11000 and info[ms[2]].tslice_us == max(11000, min(x * 75, 60000))
+    assert info[ms[2]].switch_cost_us == 75
+    # per partition, a tenure = from its SWITCH to the partition's next SWITCH.
+    # The s_timer fires every dispatched quantum; a tenant re-picked at the
+    # expiry (still the least-served co-sharer: region virtual time)
+    # continues without a switch, so a tenure that ended at an expiry lasted
+    # a whole number of its quanta.
+    by_part = {}
+    for r in recs:
+        by_part.setdefault(r.cpu, []).append(r)
+    checked = {m: 0 for m in ms}
+    for p, rs in by_part.items():
+        for a, b in zip(rs, rs[1:]):
+            nxt, q = a.a[1], a.a[2]
+            if nxt not in ms:
+                continue
+            assert q == info[nxt].tslice_us, (p, nxt, q, info[nxt].tslice_us)  # dispatched == reported
+            run_us = (b.t_ns - a.t_ns) / 1000
+            k = round(run_us / q)
+            if k >= 1 and abs(run_us - k * q) <= 1:  # ended at an expiry of its own s_timer
+                checked[nxt] += 1
+    assert all(checked[m] > 0 for m in ms), checked
+    assert e.check() == ""
