@@ -528,6 +528,11 @@ void Engine::runstate_change(Slot& v, Runstate rs, int64_t n) {
 
 void Engine::vcpu_wake(Slot& v) {
   if (runnable(v)) {
+    // a wake is work: the class_budget presence test sees a tenant whose
+    // requests are shorter than the class tick (an in-region latency tenant
+    // is blocked at almost every tick; round 6 slo mix: it flapped between
+    // present and absent, re-laying the region every ~10 ms)
+    if (!v.is_idle() && tenants[v.tenant]->pause_count == 0) tenants[v.tenant]->last_busy = now();
     if (v.rs >= RS_BLOCKED) runstate_change(v, RS_RUNNABLE, now());
     if (Scheduler* S = sched_of_tenant(v.tenant)) {
       if (pools[tenants[v.tenant]->pool]->cpus.empty()) return;  // pool without cpus: stays queued later
@@ -809,12 +814,12 @@ void Engine::budget_layout(Pool& pl, int64_t n, bool force) {
     // class -1: busy but not classified yet
     const bool present = n - t.last_busy <= present_ns;
     int cls = t.cls;
-    if (!present || cls >= 0) {
+    if (cls >= 0) {
       t.unclassified_since = INT64_MIN / 2;
-    } else if (t.unclassified_since == INT64_MIN / 2) {
-      t.unclassified_since = n;
-    } else if (boot.probe_max_us > 0 && n - t.unclassified_since > (int64_t)boot.probe_max_us * 1000) {
-      cls = 1;  // no clean window yet after probe_max_us: laid out as memory class
+    } else if (present && t.unclassified_since == INT64_MIN / 2) {
+      t.unclassified_since = n;  // (an absence does not restart the probe clock)
+    } else if (present && boot.probe_max_us > 0 && n - t.unclassified_since > (int64_t)boot.probe_max_us * 1000) {
+      cls = 1;  // no clean window yet after probe_max_us of presence: laid out as memory class
       perfc.incr(PC_probe_expired);
     }
     if (present) sig.emplace_back(t.id, cls);

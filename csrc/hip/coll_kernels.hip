@@ -149,14 +149,14 @@ __global__ __launch_bounds__(CNT) void k_allreduce(const CollDesc* __restrict__ 
         for (u32 s = 0; s < world; ++s)
           __hip_atomic_store(d->flags[s] + rank, seq + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       if (status) __hip_atomic_store(status, dn | err | 0x80000000u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      q->exited = 0;  // exit bookkeeping: reset for any relaunch (no fill kernel on the queue)
+      q->stopped = 0;
       if (dn >= nchunks || err) {  // zero the queue for the next launch
         q->next = 0;
         q->done = 0;
-        q->exited = 0;
-        q->stopped = 0;
         q->pad[0] = 0;
-        __threadfence();
       }
+      __threadfence();
     }
   }
 }

@@ -80,11 +80,14 @@ __device__ __forceinline__ void finish(WorkQueue* q, u32* status, u32 total) {
     if (old == gridDim.x - 1) {
       const u32 d = __hip_atomic_load(&q->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (status) __hip_atomic_store(status, d | 0x80000000u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      // the exit bookkeeping is reset by the last workgroup out in both
+      // cases -- a revoked unit's relaunch needs no fill kernel on the
+      // tenant's queue (round 6: 1443 fillBufferAligned per 8mix run before)
+      __hip_atomic_store(&q->exited, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&q->stopped, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (d >= total) {
         __hip_atomic_store(&q->next, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&q->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&q->exited, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&q->stopped, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
         for (int x = 0; x < kXcds; ++x) __hip_atomic_store(&q->xnext[x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }

@@ -2091,8 +2091,8 @@ struct Runner {
           } else {
             relaunch.pop_front();
             st.relaunches++;
-            // resume the same queue: clear exit bookkeeping only
-            hipMemsetAsync(&d_q[qi].exited, 0, sizeof(u32) * 2, stream);
+            // resume the same queue (its last workgroup out already cleared
+            // the exit bookkeeping: no fill kernel here)
           }
           if (cfg.priority > 0 && ctx->hold_enable && fresh && !q_hold[qi]) q_hold[qi] = hold_acquire(ctx) + 1;
           q_l0[qi] = mono_ns();

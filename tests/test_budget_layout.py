@@ -483,3 +483,38 @@ def test_reported_quanta_are_the_switch_to_switch_run_lengths():
                 checked[nxt] += 1
     assert all(checked[m] > 0 for m in ms), checked
     assert e.check() == ""
+
+
+def test_short_request_tenant_stays_present_and_leaves_the_probe_layout():
+    """An in-region latency tenant (round-6 slo mix): 100 us requests every
+    2 ms, so it is blocked at almost every class tick, and its tenures are too
+    short for a clean counter window (here: no counters at all).  Its wakes
+    count as work (presence), so the region is not re-laid every ~10 ms; and
+    after probe_max_us of presence without a class it is laid out as memory
+    class -- the GEMM keeps the compute half instead of an XCD-block probe
+    share."""
+    e, parts = _engine(present_us=10000, probe_max_us=50000)
+    g = e.tenant_create("gemm", nslots=32)
+    ms = [e.tenant_create(f"m{i}", nslots=32) for i in range(3)]
+    lat = e.tenant_create("lat", nslots=32)
+    rates = {g: COMPUTE, **{m: MEMORY for m in ms}}
+    for t in rates:
+        e.wake(t)
+    _settle(e, rates, 300)
+    relayouts = []
+    for k in range(200):  # 400 ms of 2 ms request cycles
+        e.wake(lat)
+        _feed(e, rates, 100)
+        e.block(lat)
+        for _ in range(19):
+            _feed(e, rates, 100)
+        if k == 99:
+            relayouts.append(e.perfc()["relayout"])
+    relayouts.append(e.perfc()["relayout"])
+    assert e.lib.gpbs_tenant_class(e.h, lat) < 0  # never classified ...
+    info = e.tenant_info(lat)
+    assert info.budget_ctx & 0xF == 0xC and info.budget_shared, info  # ... but laid out in the memory region
+    assert e.tenant_info(g).budget_ctx & 0xF == 0x3  # the GEMM keeps the compute half
+    assert relayouts[1] - relayouts[0] <= 1, relayouts  # the last 200 ms: a settled layout
+    assert e.perfc()["probe_expired"] > 0
+    assert e.check() == ""
