@@ -813,14 +813,24 @@ void Engine::budget_layout(Pool& pl, int64_t n, bool force) {
     if (busy && t.pause_count == 0) t.last_busy = n;
     // class -1: busy but not classified yet
     const bool present = n - t.last_busy <= present_ns;
+    // probe_max_us: a tenant that is present but blocked at class ticks (a
+    // latency tenant: 100 us requests every 2 ms) never fills a clean
+    // counter window; after probe_max_us it is laid out as memory class.  A
+    // backlogged tenant is never expired -- it only needs its first clean
+    // window (expiring one laid a GEMM out on a single memory SE next to a
+    // stream in the live phase test, and the two grids stalled each other)
     int cls = t.cls;
     if (cls >= 0) {
       t.unclassified_since = INT64_MIN / 2;
+      t.probe_gaps = false;
     } else if (present && t.unclassified_since == INT64_MIN / 2) {
       t.unclassified_since = n;  // (an absence does not restart the probe clock)
-    } else if (present && boot.probe_max_us > 0 && n - t.unclassified_since > (int64_t)boot.probe_max_us * 1000) {
-      cls = 1;  // no clean window yet after probe_max_us of presence: laid out as memory class
-      perfc.incr(PC_probe_expired);
+    } else if (present) {
+      if (!busy) t.probe_gaps = true;
+      if (t.probe_gaps && boot.probe_max_us > 0 && n - t.unclassified_since > (int64_t)boot.probe_max_us * 1000) {
+        cls = 1;
+        perfc.incr(PC_probe_expired);
+      }
     }
     if (present) sig.emplace_back(t.id, cls);
     else t.budget_ctx = 0;

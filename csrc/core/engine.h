@@ -101,6 +101,7 @@ struct Tenant {  // struct domain
   bool flapping(int64_t now, int64_t pin_ns) const { return pin_ns > 0 && cls >= 0 && now - cls_chg_ns[0] <= pin_ns; }
   int lay_cls = -1;  // the class budget_layout placed it by (a pinned flapping tenant: 1)
   int64_t unclassified_since = INT64_MIN / 2;  // present and unclassified since (probe_max_us)
+  bool probe_gaps = false;  // ... and seen blocked at a class tick meanwhile (short requests)
   // Cross-GPU gang window (parallel/gang.py): 1 favoured (run on every
   // partition that holds a slot), 2 excluded (its peers on other GPUs are not
   // running it), until gang_until (engine clock).

@@ -412,6 +412,7 @@ struct GpuCtx {
   uint64_t t_model[kMaxTenants] = {};          // metric periods delivered from the calibrated model
   uint64_t t_moved[kMaxTenants] = {};          // ticks its modeled counters moved (calibrated or not)
   uint64_t cad_calls = 0;                      // cadence ticks
+  int64_t cad_dbg[512][3] = {};                // debug ring: tick time, tenant 1 / 2 instruction sums
   uint64_t t_delivered[kMaxTenants] = {};      // metric periods with any delivery (clean, fallback, model)
   int64_t t_first_ns[kMaxTenants] = {}, t_last_ns[kMaxTenants] = {};  // first / last delivery (period stats)
   double mod_cur[kMaxTenants][kNumPmc] = {};       // modeled deltas of the newest consumed snapshot
@@ -1215,6 +1216,15 @@ void cadence_tick(GpuCtx* c) {
     c->cad_prev = cur;
     c->cad_primed = true;
     return;
+  }
+  {
+    int64_t* d = c->cad_dbg[c->cad_calls % 512];
+    d[0] = mono_ns();
+    for (int tt = 1; tt <= 2 && tt < rows; ++tt) {
+      u64 v = 0;
+      for (int x = 0; x < kXcds; ++x) v += cur[((size_t)tt * kXcds + x) * kNumPmc];
+      d[tt] = (int64_t)v;
+    }
   }
   c->cad_calls++;
   for (int t = 0; t < rows; ++t) {
@@ -3176,6 +3186,23 @@ int gpbs_gpu_hwc_tenant_periods(void* p, int t, uint64_t* out4, double* out_cal4
   return 0;
 }
 
+// Debug: the cadence ring (tick time, tenants 1 and 2 instruction sums) of
+// the last min(n, 512) ticks, oldest first; returns the count.
+int gpbs_gpu_cadence_ring(void* p, int64_t* out, int n) {
+  GpuCtx* c = (GpuCtx*)p;
+  if (!c || !out) return -22;
+  std::lock_guard<std::mutex> g(c->snap_mu);
+  const int have = (int)std::min<uint64_t>(c->cad_calls, 512);
+  const int k = std::min(n, have);
+  for (int i = 0; i < k; ++i) {
+    const int64_t* d = c->cad_dbg[(c->cad_calls - k + i) % 512];
+    out[3 * i] = d[0];
+    out[3 * i + 1] = d[1];
+    out[3 * i + 2] = d[2];
+  }
+  return k;
+}
+
 // Freshness probe of the host-readable counter block (tools): `n` reads of
 // tenant t's instruction counter `gap_us` apart, through the BAR (mode 0) or
 // a device-to-host copy (mode 1); returns how many reads saw a new value.
@@ -3298,9 +3325,17 @@ int gpbs_gpu_set_share(void* p, int on, int64_t* share_ns) {
   return old;
 }
 
+extern "C" int gpbs_hip_masked_pool_prealloc(int device, int* out, int max);
 int gpbs_gpu_set_se_mode(void* p, int on) {
   GpuCtx* c = (GpuCtx*)p;
   if (!c) return -22;
+  // SE mode launches on the process's CU-masked queue pool: make its burst
+  // now, before the runners run.  Creating a hardware queue remaps the
+  // process's runlist, which preempts every queue it has: the lazy burst at
+  // the first SE-exclusive relayout froze ALL runners for ~100 ms
+  // (profiles/r6/phase_debug_summary.txt).  A pool made earlier (the bench's
+  // pipe pre-flight) is kept.
+  if (on && gpbs_hip_masked_pool_prealloc(c->device, nullptr, 0) < 0) return -12;
   __atomic_store_n(&c->se_mode, on ? 1 : 0, __ATOMIC_RELEASE);
   if (!on) c->share.store(0, std::memory_order_release);  // class sharing exists only over SE partitions
   return 0;

@@ -113,6 +113,7 @@ def bind(lib):
     _p(lib, "gpbs_gpu_hwc_tenant_periods", C.c_int, vp, C.c_int, C.POINTER(u64), C.POINTER(C.c_double))
     _p(lib, "gpbs_gpu_switch_cost", C.c_int, vp, C.c_int, C.POINTER(i64))
     _p(lib, "gpbs_gpu_hwc_tenant_cadence", C.c_int, vp, C.c_int, C.POINTER(i64))
+    _p(lib, "gpbs_gpu_cadence_ring", C.c_int, vp, C.POINTER(i64), C.c_int)
     _p(lib, "gpbs_gpu_block_probe", C.c_int, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(i64))
     _p(lib, "gpbs_runner_queue", C.c_int, vp)
     _p(lib, "gpbs_gpu_masked_pool", C.c_int, C.POINTER(C.c_uint64), C.c_int)

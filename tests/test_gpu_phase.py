@@ -120,7 +120,7 @@ def test_budget_layout_follows_a_phase_change_on_live_counters(align):
     # waited for clean hardware windows of the new phase, 9-47 ms apart);
     # with the 1 ms cadence (the calibrated model reports every tick, the
     # hardware windows re-anchor it) the classifier sees the new phase at the
-    # next tick.
+    # next tick.  Round 6 measured 7.5 ms / 12-13 ms (profiles/r6/s8_phase.txt).
     assert 0 <= out["to_memory_ms"] < 50, out
     assert 0 <= out["to_compute_ms"] < 50, out
     if out["periods"]["phase"]["cadence"]:  # host-readable counter block: the 1 ms cadence is live
