@@ -12,6 +12,7 @@
 // headline path (csrc/hip/runtime.cpp, hwc_tenant_deltas).  Both sum in the
 // same order; tests/test_gpu_kernels.py compares them on random inputs.
 #pragma once
+#include <cstddef>
 #include <cstdint>
 
 #include "common.hpp"
@@ -34,6 +35,12 @@ struct HwcAttrIn {
   u32 drained;                           // bit p: partition p's last owner change was at least the drain
                                          // guard before this interval began (its previous owner is gone)
 };
+
+// The prefix of a snapshot the device path reads (rows < nt_hi of own_cur).
+inline size_t hwc_attr_in_bytes(const HwcAttrIn& in) {
+  const u32 rows = (in.nt_hi == 0 || in.nt_hi > (u32)kMaxTenants) ? (u32)kMaxTenants : in.nt_hi;
+  return offsetof(HwcAttrIn, own_cur) + (size_t)rows * kAttrP * sizeof(long long);
+}
 
 struct HwcAttrPrev {  // carried from one snapshot to the next
   u64 se[kAttrP * kNumPmc];

@@ -58,6 +58,7 @@ int gpbs_hip_counter_reduce(void*, void*, const int*, int, void*, hipStream_t);
 int gpbs_hip_adapt(void*, const void*, const void*, const void*, int, const gpbs_adapt_params_t*, int*, hipStream_t);
 int gpbs_hip_switch_probe(const void*, int, unsigned*, int, unsigned, unsigned long long, hipStream_t);
 int gpbs_hip_hwc_attribute(const void*, void*, void*, void*, hipStream_t);
+int gpbs_hip_hwc_attribute2(const void*, void*, void*, void*, hipStream_t, int);
 int gpbs_hip_allreduce(const void*, unsigned, unsigned long long, unsigned, void*, const void*, unsigned, unsigned,
                        void*, void*, int, unsigned long long, unsigned long long, hipStream_t);
 int gpbs_hip_gang_desc_size(void);
@@ -177,6 +178,16 @@ __attribute__((target("sse4.1"))) void bar_read(const void* src, void* dst, size
   _mm_mfence();
 }
 
+// Host write into fine-grained VRAM through the BAR: non-temporal 16-byte
+// stores out of the write-combining buffers, fenced before the launch that
+// reads them.
+__attribute__((target("sse4.1"))) void bar_store(void* dst, const void* src, size_t bytes) {
+  __m128i* d = (__m128i*)dst;
+  const __m128i* s = (const __m128i*)src;
+  for (size_t i = 0; i < (bytes + 15) / 16; ++i) _mm_stream_si128(d + i, _mm_loadu_si128(s + i));
+  _mm_sfence();
+}
+
 PartTable* bar_alloc(int device) {
   int bus = 0, dev = 0;
   if (hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, device) != hipSuccess ||
@@ -294,14 +305,17 @@ struct GpuCtx {
   std::vector<int64_t> snap_own;        // [kMaxTenants * kXcds * kCtx]
   uint64_t snap_seq = 0, used_seq = 0;
   bool hw_primed = false;
-  // Attribution of a snapshot (csrc/hip/hwc_attr.h): on the GPU by default
-  // (k_hwc_attribute on the scheduler stream, launched by one metric tick and
-  // harvested by the next -- the engine lock is never held across a device
-  // wait), on the host with param device_attr 0.
-  int dev_attr = 1;
+  // Attribution of a snapshot (csrc/hip/hwc_attr.h): on the host by default
+  // (round 6: hwc_attr_host, a few us of the metric tick, and no kernel that
+  // waits for a wave slot behind the tenants' persistent grids -- 40-60 us
+  // mean, 200-440 us max per k_hwc_attribute on a full GPU,
+  // profiles/r6/s13_*); param device_attr 1: k_hwc_attribute on the
+  // scheduler stream, launched by one metric tick and harvested by the next.
+  int dev_attr = 0;
   HwcAttrPrev hst;                  // host path state
   HwcAttrIn* h_ain = nullptr;       // pinned: the snapshot the metric tick fills
   HwcAttrIn* d_ain = nullptr;       // device staging copy the kernel reads
+  HwcAttrIn* f_ain = nullptr;       // fine-grained VRAM copy the host writes through the BAR (no blit)
   HwcAttrOut* h_aout = nullptr;     // pinned mapped, written by the kernel
   HwcAttrPrev* d_ast = nullptr;     // device-resident previous snapshot
   hipEvent_t attr_ev = nullptr;
@@ -1168,7 +1182,12 @@ int hwc_consume(GpuCtx* c, bool wait) {
   bool done = false;
   if (c->dev_attr) {
     hwc_fill_in(c, *c->h_ain);
-    if (gpbs_hip_hwc_attribute(c->h_ain, c->d_ain, c->d_ast, c->h_aout, c->sched_stream) == 0 &&
+    // the snapshot reaches the kernel through the BAR (host streaming
+    // stores into fine-grained VRAM): round 5's staging hipMemcpyAsync ran
+    // as a copyBuffer blit kernel on the tenants' CUs at every sample
+    if (c->f_ain) bar_store(c->f_ain, c->h_ain, hwc_attr_in_bytes(*c->h_ain));
+    if (gpbs_hip_hwc_attribute2(c->h_ain, c->f_ain ? c->f_ain : c->d_ain, c->d_ast, c->h_aout, c->sched_stream,
+                                c->f_ain ? 0 : 1) == 0 &&
         hipEventRecord(c->attr_ev, c->sched_stream) == hipSuccess) {
       c->attr_pending = true;
       c->attr_launches++;
@@ -2227,6 +2246,7 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
   hwc_attr_prev_init(c->hst);
   ok = ok && hipHostMalloc((void**)&c->h_ain, sizeof(HwcAttrIn), hipHostMallocMapped) == hipSuccess;
   ok = ok && hipMalloc((void**)&c->d_ain, sizeof(HwcAttrIn)) == hipSuccess;
+  c->f_ain = (HwcAttrIn*)finegrained_alloc(device, sizeof(HwcAttrIn));
   ok = ok && hipHostMalloc((void**)&c->h_aout, sizeof(HwcAttrOut), hipHostMallocMapped) == hipSuccess;
   ok = ok && hipMalloc((void**)&c->d_ast, sizeof(HwcAttrPrev)) == hipSuccess;
   ok = ok && hipMemcpy(c->d_ast, &c->hst, sizeof(HwcAttrPrev), hipMemcpyHostToDevice) == hipSuccess;
@@ -2318,6 +2338,7 @@ void gpbs_gpu_ctx_destroy(void* p) {
   if (c->h_aout) hipHostFree(c->h_aout);
   if (c->d_ast) hipFree(c->d_ast);
   if (c->d_ain) hipFree(c->d_ain);
+  if (c->f_ain) hsa_amd_memory_pool_free(c->f_ain);
   for (auto& B : c->abuf) {
     if (B.ev) {
       hipEventSynchronize(B.ev);

@@ -392,7 +392,9 @@ int gpbs_hip_adapt(void* states, const void* deltas, const void* spin_sum, const
 // (one DMA-sized copy on the same stream) so the kernel's loads never wait
 // on PCIe; the scalars travel as kernel arguments.  st: device HwcAttrPrev;
 // out: host-visible HwcAttrOut.
-int gpbs_hip_hwc_attribute(const void* h_in, void* d_in, void* st, void* out, hipStream_t s) {
+// copy 0: d_in already holds the snapshot (the runtime wrote it into
+// fine-grained VRAM through the BAR), so no copy runs on the GPU
+int gpbs_hip_hwc_attribute2(const void* h_in, void* d_in, void* st, void* out, hipStream_t s, int copy) {
   const HwcAttrIn* hin = (const HwcAttrIn*)h_in;
   AttrArgs a{};
   for (int k = 0; k < kNumPmc; ++k) a.slot_se[k] = hin->slot_se[k];
@@ -402,12 +404,14 @@ int gpbs_hip_hwc_attribute(const void* h_in, void* d_in, void* st, void* out, hi
   a.prime = hin->prime;
   a.nt_hi = hin->nt_hi;
   a.drained = hin->drained;
-  const u32 rows = (a.nt_hi == 0 || a.nt_hi > (u32)kMaxTenants) ? (u32)kMaxTenants : a.nt_hi;
-  const size_t bytes = offsetof(HwcAttrIn, own_cur) + (size_t)rows * kAttrP * sizeof(long long);
-  if (hipMemcpyAsync(d_in, h_in, bytes, hipMemcpyHostToDevice, s) != hipSuccess) return -5;
+  if (copy && hipMemcpyAsync(d_in, h_in, hwc_attr_in_bytes(*hin), hipMemcpyHostToDevice, s) != hipSuccess) return -5;
   hipLaunchKernelGGL(k_hwc_attribute, dim3(1), dim3(256), 0, s, (const HwcAttrIn*)d_in, (HwcAttrPrev*)st,
                      (HwcAttrOut*)out, a);
   return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+int gpbs_hip_hwc_attribute(const void* h_in, void* d_in, void* st, void* out, hipStream_t s) {
+  return gpbs_hip_hwc_attribute2(h_in, d_in, st, out, s, 1);
 }
 
 }  // extern "C"

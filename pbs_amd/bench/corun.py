@@ -196,6 +196,19 @@ SE_SLOTS = {"gemm": 16, "gemm_b": 16, "hbm": 16, "coll": 16, "idle": 8}
 # scheduler places them on disjoint memory SEs instead of time-sharing both.
 SE8_SLOTS = {"gemm": 16, "gemm_b": 16, "hbm": 8, "coll": 8, "idle": 8}
 
+# Runtime path of the SE-budget policies (round 6): the
+# partition table in fine-grained VRAM the host writes through the BAR (no
+# k_partition_switch), the PBS update and the counter attribution on the host
+# (the bit-exact twins of k_adapt / k_hwc_attribute), the modeled counter block
+# read through the BAR -- the scheduler puts no kernel and no blit on the GPU's
+# queues, so nothing it does waits behind the tenants' persistent grids
+# (profiles/r6/s13_*: 0 scheduler dispatches vs ~1000 k_adapt/s at 35-60 us
+# mean, 400+ us max, on the device path).  Every policy that lays out SE
+# budgets runs the same path, so the ablations differ from the flagship in
+# policy only.  RT_DEV: the round-5 device path (gpbs-dev).
+RT = "bar,se,waveprio,latco,budget,latmem,hostsched"
+RT_DEV = "device,se,waveprio,latco,budget,latmem"
+
 POLICY_ENGINES = {
     # name: (issue contexts per XCD, engine overrides on top of MI355X_PROFILE,
     #        kernel gate mode, partition-table location + runtime options)
@@ -209,39 +222,46 @@ POLICY_ENGINES = {
     # out exactly as gpbs-split; on the crowded 8mix time-sharing with PBS
     # quanta measured ahead of the XCD-block split on 3 of 4 boxes
     # (profiles/r3/8mix_queues_q8_*.json, bench_full_5rep_b.json, bench_all_pool_2rep.json).
-    "gpbs": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
+    "gpbs": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, RT),
     # crowded class regions split by whole-XCD blocks instead (class_budget 2)
-    "gpbs-split": (4, dict(BUDGET_OVERRIDES), True, "device,se,waveprio,latco,budget,latmem"),
-    "credit-fixed": (4, dict(BUDGET_OVERRIDES, sched="credit-fixed"), True, "device,se,waveprio,latco,budget,latmem"),
+    "gpbs-split": (4, dict(BUDGET_OVERRIDES), True, RT),
+    # the flagship on round 5's device path (device table + k_partition_switch,
+    # k_adapt, k_hwc_attribute), and with only the table moved to the BAR
+    "gpbs-dev": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, RT_DEV),
+    "gpbs-bar": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "bar,se,waveprio,latco,budget,latmem"),
+    # the flagship with a smaller hardware-sample budget (SAMPLER below)
+    "gpbs-b1": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, RT),
+    "gpbs-b2": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, RT),
+    "credit-fixed": (4, dict(BUDGET_OVERRIDES, sched="credit-fixed"), True, RT),
     # round-3 name of the flagship on crowded mixes (time-shared, PBS quanta;
     # credit-fixed-ts: the fixed quantum)
-    "gpbs-ts": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
+    "gpbs-ts": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, RT),
     "credit-fixed-ts": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="credit-fixed"), True,
-                        "device,se,waveprio,latco,budget,latmem"),
+                        RT),
     # fixed per-class quanta (memory class max_us, compute class min_us), no
     # phase detector: what PBS's detector adds over a class -> quantum table
     "credit-classq": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="credit-classq"), True,
-                      "device,se,waveprio,latco,budget,latmem"),
+                      RT),
     # the ATC policy (X:xen/common/sched_credit_atc.c:291-543): one global
     # quantum for the pool, driven by the tenants' wait reports (K10); the
     # same time-shared budget layout as the flagship
     "atc": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="atc", region_vt=0), True,
-            "device,se,waveprio,latco,budget,latmem"),
-    "atc-vt": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="atc"), True, "device,se,waveprio,latco,budget,latmem"),
+            RT),
+    "atc-vt": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="atc"), True, RT),
     "atc-nox": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="atc", class_steal=0), True,
-                "device,se,waveprio,latco,budget,latmem"),
+                RT),
     # switch-cost probes: every quantum (fixed) or the adaptive floor at 4 ms
     "credit-fixed-ts4": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="credit-fixed", tslice_us=4000), True,
-                         "device,se,waveprio,latco,budget,latmem"),
+                         RT),
     "gpbs-f4": (4, dict(BUDGET_OVERRIDES, class_budget=1, adapt=dict(MI355X_PROFILE["adapt"], min_us=4000)), True,
-                "device,se,waveprio,latco,budget,latmem"),
+                RT),
     # the class EWMA follows a drop at alpha 1/2 (boot class_fall=1)
     "gpbs-fall": (4, dict(BUDGET_OVERRIDES, class_budget=1, class_fall=1), True,
-                  "device,se,waveprio,latco,budget,latmem"),
+                  RT),
     # PBS quantum range stretched 3x at the top (memory tenants up to 33 ms)
     "gpbs-q33": (4, dict(BUDGET_OVERRIDES, class_budget=1,
                          adapt=dict(MI355X_PROFILE["adapt"], max_us=33000, inc_us=3000, dec_us=6000)), True,
-                 "device,se,waveprio,latco,budget,latmem"),
+                 RT),
     # long quanta everywhere: 30 ms fixed (the ATC default without its wait
     # feedback), and the PBS range moved up to 4-30 ms
     # (the equal-quantum ablations run credit ordering in the region,
@@ -249,57 +269,57 @@ POLICY_ENGINES = {
     # virtual time -- 8mix fixed-30 1.388 vs 1.302, atc 1.388 vs 1.325,
     # profiles/r6/s2_8mix_vt_summary.txt)
     "credit-fixed-ts30": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="credit-fixed", tslice_us=30000,
-                                  region_vt=0), True, "device,se,waveprio,latco,budget,latmem"),
+                                  region_vt=0), True, RT),
     "gpbs-w": (4, dict(BUDGET_OVERRIDES, class_budget=1,
                        adapt=dict(MI355X_PROFILE["adapt"], min_us=4000, max_us=30000, inc_us=4000, dec_us=8000,
-                                  switch_boundary=30000)), True, "device,se,waveprio,latco,budget,latmem"),
+                                  switch_boundary=30000)), True, RT),
     # time-shared class regions rotate at >= 11 / 30 ms (boot shared_q_us)
     "gpbs-sq11": (4, dict(BUDGET_OVERRIDES, class_budget=1, region_q=1, shared_q_us=11000), True,
-                  "device,se,waveprio,latco,budget,latmem"),
+                  RT),
     # round 5's flagship: one region quantum (the co-sharers' largest adaptive
     # quantum, floored at a global 30 ms)
     "gpbs-sq30": (4, dict(BUDGET_OVERRIDES, class_budget=1, region_q=1, shared_q_us=30000), True,
-                  "device,se,waveprio,latco,budget,latmem"),
+                  RT),
     # the long-quantum ablations with credit ordering the time-shared region
     # (region_vt 0: round 5's dispatch core)
     "gpbs-novt": (4, dict(BUDGET_OVERRIDES, class_budget=1, region_vt=0), True,
-                  "device,se,waveprio,latco,budget,latmem"),
+                  RT),
     # the PBS quantum without the measured switch-cost floors
     "gpbs-nofloor": (4, dict(BUDGET_OVERRIDES, class_budget=1, switch_floor_x=0), True,
-                     "device,se,waveprio,latco,budget,latmem"),
+                     RT),
     # credit-classq with the global 30 ms floor in time-shared regions (the
     # classq + floor ablation: what the class map does with round 5's floor)
     "credit-classq-f": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="credit-classq", shared_q_us=30000,
-                                region_vt=0), True, "device,se,waveprio,latco,budget,latmem"),
+                                region_vt=0), True, RT),
     "credit-classq-fvt": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="credit-classq", shared_q_us=30000), True,
-                          "device,se,waveprio,latco,budget,latmem"),
+                          RT),
     "credit-fixed-ts30-vt": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="credit-fixed", tslice_us=30000), True,
-                             "device,se,waveprio,latco,budget,latmem"),
+                             RT),
     # PBS quantum range capped lower at the top (memory tenants up to 4 / 6 ms)
     "gpbs-max4": (4, dict(BUDGET_OVERRIDES, class_budget=1, adapt=dict(MI355X_PROFILE["adapt"], max_us=4000)), True,
-                  "device,se,waveprio,latco,budget,latmem"),
+                  RT),
     "gpbs-max6": (4, dict(BUDGET_OVERRIDES, class_budget=1, adapt=dict(MI355X_PROFILE["adapt"], max_us=6000)), True,
-                  "device,se,waveprio,latco,budget,latmem"),
+                  RT),
     # a tenant flapping between classes (3 changes within 2 s) is laid out in
     # the memory region until it settles (boot class_pin_us)
     "gpbs-pin": (4, dict(BUDGET_OVERRIDES, class_budget=1, class_pin_us=2000000), True,
-                 "device,se,waveprio,latco,budget,latmem"),
+                 RT),
     # class changes must persist 100 / 300 ms (class_dwell x class_period_us)
     # before a tenant is re-homed: flap damping for phase-changing tenants
     "gpbs-dwell50": (4, dict(BUDGET_OVERRIDES, class_budget=1, class_dwell=50), True,
-                     "device,se,waveprio,latco,budget,latmem"),
+                     RT),
     "gpbs-dwell150": (4, dict(BUDGET_OVERRIDES, class_budget=1, class_dwell=150), True,
-                      "device,se,waveprio,latco,budget,latmem"),
+                      RT),
     # the flagship under other counter-sampler policies (same engine and
     # layout; SAMPLER below): round-3 sampler (owner-change bursts, no budget,
     # no model fallback), and modeled counters only (no hardware sample)
-    "gpbs-model": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
-    "gpbs-noalign": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
-    "gpbs-d5": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
+    "gpbs-model": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, RT),
+    "gpbs-noalign": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, RT),
+    "gpbs-d5": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, RT),
     # no cross-class steals by idle partitions (boot class_steal=0)
     "gpbs-nox": (4, dict(BUDGET_OVERRIDES, class_budget=1, class_steal=0), True,
-                 "device,se,waveprio,latco,budget,latmem"),
-    "gpbs-d10": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "device,se,waveprio,latco,budget,latmem"),
+                 RT),
+    "gpbs-d10": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, RT),
     # the same without the latency lane (GEMV co-resident on every CU)
     "gpbs-nolane": (4, dict(BUDGET_OVERRIDES), True, "device,se,waveprio,latco,budget"),
     # round-2 flagship: fixed class halves, memory tenants one SE each by
@@ -342,6 +362,10 @@ SAMPLER = {
     # ~0.2 ms sample cost; 5 % -> ~4 ms, 10 % -> ~2 ms (budget raised with it)
     "gpbs-d5": dict(budget_pct=8, duty=5),
     "gpbs-d10": dict(budget_pct=15, duty=10),
+    # hardware samples stall the command processor ~0.2 ms each: the budget
+    # is what a sample-hungry mix (frequent switches) pays in tenant time
+    "gpbs-b1": dict(budget_pct=1),
+    "gpbs-b2": dict(budget_pct=2),
 }
 
 
@@ -709,7 +733,11 @@ class Corun:
             self.ctx.set_lat_half(1 if "latmem" in opts else -1)
             # device hot path: counter attribution (k_hwc_attribute) and the
             # PBS update (k_adapt) run on the GPU
-            self.ctx.attach(e, nctx=e._gpbs_nctx, device_adapt=True)
+            # ("hostsched": both on the host -- the bit-exact host twins --
+            # so the scheduler puts no kernel on the GPU's queues)
+            host_sched = "hostsched" in opts
+            self.ctx.attach(e, nctx=e._gpbs_nctx, device_adapt=not host_sched)
+            self.ctx.param("device_attr", 0 if host_sched else 1)
             smp = SAMPLER.get(policy)
             if self.cfg.hw_counters and smp != "model":
                 if self._sampler_default is None:

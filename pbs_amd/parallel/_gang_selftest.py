@@ -255,6 +255,18 @@ def spin_barrier_worker(rank, world, arr, iters, q):
     q.put((rank, lat[iters // 10:]))
 
 
+def sem_barrier_worker(rank, world, bar, iters, q):
+    """The blocking counterpart of spin_barrier_worker: a multiprocessing
+    Barrier (semaphores: a futex sleep and wake per crossing), which a loaded
+    host slows the way it slows a native epoch that sleeps on its doorbell."""
+    lat = []
+    for _ in range(iters):
+        t0 = time.monotonic_ns()
+        bar.wait(60)
+        lat.append(time.monotonic_ns() - t0)
+    q.put((rank, lat[iters // 10:]))
+
+
 def gloo_bench_worker(rank, world, port, iters, q):
     import torch
     import torch.distributed as dist

@@ -93,6 +93,12 @@ class Daemon:
         ctx = GpuContext(gpu, part_base=part_lo, nctx=self.nctx, params=self.cfg.get("runtime", {}))
         ctx.attach_mux(self.engine, nctx=self.nctx)
         if self.se_mode:
+            # the partition table in BAR-written VRAM: switches put no kernel
+            # on the GPU (the pinned host table where no such pool exists)
+            try:
+                ctx.set_table_mode("bar")
+            except RuntimeError:
+                pass
             ctx.set_se_mode(True)
         if self.hw_counters:
             from ..counters import hwc

@@ -144,7 +144,7 @@ def test_eight_node_local_ranks_switch_at_the_same_epochs(native):
     world = 8
     name = f"gpbs-gang-node8-{os.getpid()}-{int(native)}"
     ready = ctx.Barrier(world)
-    ps = [ctx.Process(target=node_worker, args=(r, world, name, q, 1.0, 5.0, ready, native)) for r in range(world)]
+    ps = [ctx.Process(target=node_worker, args=(r, world, name, q, 2.0, 5.0, ready, native)) for r in range(world)]
     for p in ps:
         p.start()
     out = {}
