@@ -973,6 +973,21 @@ class CreditScheduler : public Scheduler {
       return;
     }
     E.perfc.incr(E.runnable(v) ? PC_vcpu_wake_runnable : PC_vcpu_wake_not_runnable);
+    // Budget layout: a slot that blocked outside its budget (it ran there
+    // before a relayout, or was stolen there) wakes at its class home -- it
+    // is on no runqueue, so the move is free.  Otherwise a short-request
+    // tenant (the slo mix's in-region latency tenant, blocked at every class
+    // tick, so never sent home) kept waking on a GEMM's shader engine and
+    // BOOST-preempted it at every request (round 6: the equal-quantum
+    // ablations ran it on SE0/SE1 + SE3, GEMM 0.48 instead of 0.53).
+    if (v.class_home >= 0 && !v.soft.empty() && !v.soft.test(v.processor) && v.affinity.test(v.class_home) &&
+        E.pools[E.tenants[v.tenant]->pool]->cpus.test(v.class_home)) {
+      const int from = v.processor;
+      v.processor = v.class_home;
+      v.homed_at = E.now();
+      E.perfc.incr(PC_wake_homed);
+      E.emit(TRC_MIGRATE, v.processor, v.tenant, v.index, from, v.processor);
+    }
     if (s.pri == PRI_UNDER && !(s.flags & FLAG_PARKED)) {
       s.pri = PRI_BOOST;  // wake-boost
       s.req_until = E.now() + kReqWindowNs;

@@ -1301,6 +1301,10 @@ class Corun:
                                           engine_us=e.tenant_info(self.tid[n]).switch_cost_us)
                                   for n in self.tid}
             eng["shared"] = {n: e.tenant_info(self.tid[n]).budget_shared for n in self.tid}
+            eng["budget_ctx"] = {n: e.tenant_info(self.tid[n]).budget_ctx for n in self.tid}
+            eng["online"] = {n: e.tenant_info(self.tid[n]).online_slots for n in self.tid}
+            eng["perfc"] = {k: v for k, v in e.perfc().items()
+                            if k in ("relayout", "probe_layout", "probe_expired", "class_change")}
             # measured metric periods and, of those, at the quantum bounds
             eng["at_bound"] = {n: e.bound_stats(self.tid[n]) for n in self.throughput}
             eng["measure_tenures"] = {n: e.measure(self.tid[n]) for n in self.throughput}
