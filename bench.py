@@ -365,16 +365,17 @@ def main():
 
     results = {}
     for mix in mixes:
-        # time-shared mixes (phase-ts, 8mix, slo) carry the long-quantum
-        # ablations: one 30 ms quantum for all
-        # (credit-fixed-ts30), the class map with the 30 ms floor
-        # (credit-classq-f), ATC, and round 5's region quantum (gpbs-sq30)
+        # crowded mixes (phase-ts, 8mix, slo) carry the long-quantum
+        # ablations on the flagship's layout: one 30 ms
+        # quantum for all (credit-fixed-ts30), the class map with the 30 ms
+        # floor (credit-classq-f), ATC -- and the layout ablation gpbs-ts
+        # (crowded memory regions time-shared, round 6's quanta)
         default = {"4mix": "none,static-se,credit-fixed,gpbs-lat,gpbs",
                    "gemm2": "none,static,static-se,credit-fixed,gpbs",
                    "phase": "none,static-se,credit-fixed,gpbs",
-                   "phase-ts": "none,static-se,credit-fixed-ts30,credit-classq-f,atc,gpbs-sq30,gpbs",
-                   "8mix": "none,static-se,credit-fixed-ts30,credit-classq-f,gpbs-split,atc,gpbs-sq30,gpbs",
-                   "slo": "none,static-se,credit-fixed-ts30,credit-classq-f,atc,gpbs"}[mix]
+                   "phase-ts": "none,static-se,credit-fixed-ts30,credit-classq-f,atc,gpbs-ts,gpbs",
+                   "8mix": "none,static-se,credit-fixed-ts30,credit-classq-f,gpbs-split,atc,gpbs-ts,gpbs",
+                   "slo": "none,static-se,credit-fixed-ts30,credit-classq-f,atc,gpbs-ts,gpbs"}[mix]
         spec = args.policies if (args.policies and mix == mixes[0]) else default
         pols = tuple(p for p in spec.split(",") if p)
         reps = args.reps if mix == mixes[0] else args.reps_extra

@@ -140,6 +140,7 @@ void gpbs_boot_defaults(gpbs_boot_params_t* p) {
   p->region_vt = 0;
   p->slo_cap = 0;
   p->probe_max_us = 0;
+  p->mem_split = 0;
   AdaptParams a;
   std::memcpy(&p->adapt, &a, sizeof(a));
   AtcParams t;

@@ -102,6 +102,10 @@ struct Tenant {  // struct domain
   int lay_cls = -1;  // the class budget_layout placed it by (a pinned flapping tenant: 1)
   int64_t unclassified_since = INT64_MIN / 2;  // present and unclassified since (probe_max_us)
   bool probe_gaps = false;  // ... and seen blocked at a class tick meanwhile (short requests)
+  // mem_split: share of class ticks the tenant was busy at (EWMA 1/16), and
+  // whether the layout treats it as light (hysteresis 0.4 / 0.6)
+  double busy_ewma = 1.0;
+  bool light = false;
   // Cross-GPU gang window (parallel/gang.py): 1 favoured (run on every
   // partition that holds a slot), 2 excluded (its peers on other GPUs are not
   // running it), until gang_until (engine clock).
@@ -230,6 +234,7 @@ struct Pool {
   // class_budget: (tenant id, class) of the present tenants the budgets were
   // last computed for
   std::vector<std::pair<int, int>> budget_sig;
+  std::vector<int> budget_light;  // mem_split: the light tenants of that layout
 };
 
 std::unique_ptr<Scheduler> make_scheduler(const std::string& name, Engine& e, int pool);
@@ -402,6 +407,7 @@ class Engine {
   void place_tenant_class(Tenant& t, Pool& pl, int layout);
   void budget_layout(Pool& pl, int64_t now, bool force);
   void place_budget(Tenant& t, Pool& pl, uint32_t ctx_mask, int stagger, uint32_t xcd_mask = 0);
+  void place_parts(Tenant& t, Pool& pl, const Mask& m);
   void set_affinity(Slot& v, const Mask& m, int home = -1);
   void place_class(Slot& v, const Mask& m, int home);
   void send_home(Slot& v);

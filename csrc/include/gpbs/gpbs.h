@@ -16,7 +16,7 @@
 extern "C" {
 #endif
 
-#define GPBS_ABI_VERSION 5
+#define GPBS_ABI_VERSION 6
 
 /* Validation ranges (sysctl.h:568-579, libxl.c:4026-4101). Q1: the new API
  * also accepts the reference's boot default of 100us (see docs). */
@@ -115,6 +115,13 @@ typedef struct gpbs_boot_params {
   int32_t probe_max_us;        /* class_budget: a present tenant still unclassified after this long (its tenures are
                                   too short for a clean counter window: a latency tenant's 50 us requests) is laid out
                                   as memory class instead of holding every tenant in the probe layout; 0 = no limit */
+  int32_t mem_split;           /* class_budget 1: a crowded MEMORY-class region is split among its tenants by
+                                  partitions (blocks of (shader engine, XCD) in context-major order) instead of
+                                  time-shared: each backlogged tenant an equal block, a light tenant (busy at under
+                                  half of the class ticks: a latency tenant) a small one.  Memory-bound tenants are
+                                  bandwidth-bound well below a whole region (concave in CUs), and tenants bound by
+                                  different paths (HBM vs the MALL) overlap; a crowded compute region stays
+                                  time-shared (a GEMM needs its tile count of CUs).  0 = time-share */
   gpbs_adapt_params_t adapt;
   gpbs_atc_params_t atc;
 } gpbs_boot_params_t;

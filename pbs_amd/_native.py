@@ -27,7 +27,7 @@ class AtcParams(C.Structure):
                                    "wait_unit_ns")]
 
 
-ABI_VERSION = 5  # GPBS_ABI_VERSION in csrc/include/gpbs/gpbs.h
+ABI_VERSION = 6  # GPBS_ABI_VERSION in csrc/include/gpbs/gpbs.h
 
 
 class BootParams(C.Structure):
@@ -37,7 +37,7 @@ class BootParams(C.Structure):
         "trace_capacity", "quantum_align_us", "coschedule", "class_period_us", "boost_exclusive",
         "class_split", "idle_skip", "class_dwell", "class_budget", "present_us", "sibling_steal", "class_steal", "class_fall",
         "shared_q_us", "class_pin_us", "region_q", "switch_floor_x", "switch_floor_max_us", "region_vt",
-        "slo_cap", "probe_max_us")] + [("adapt", AdaptParams),
+        "slo_cap", "probe_max_us", "mem_split")] + [("adapt", AdaptParams),
                                                                                     ("atc", AtcParams)]
 
 

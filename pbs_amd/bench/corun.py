@@ -120,6 +120,14 @@ MIXES = {
             # p99 target of its 8192^2 GEMV requests (solo ~0.06 ms)
             "slo_p99_ms": 1.0},
 }
+# Alternative hand layouts (policy "static-se2"), probes of the layout space
+STATIC_SE2 = {
+    # slo: the launch-bound MALL-sized tenant on a memory SE of its own on
+    # most XCDs, the two streams split the other memory SE
+    "slo": {"gemm": (tuple(range(8)), (0, 1)), "hbm": ((0, 1, 2, 3), (2,)), "hbm_b": ((4, 5, 6, 7), (2,)),
+            "mall": ((0, 1, 2, 3, 4, 5), (3,)), "idle": ((6, 7), (3,))},
+}
+
 # Hand-picked static shader-engine layouts (policy "static-se": no engine, no
 # counters): tenant -> (XCDs, SEs) it owns.  The informed static alternative
 # to the counter-driven layout: for the 4mix the compute tenant on SEs {0,1}
@@ -228,6 +236,8 @@ POLICY_ENGINES = {
     # the flagship on round 5's device path (device table + k_partition_switch,
     # k_adapt, k_hwc_attribute), and with only the table moved to the BAR
     "gpbs-dev": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, RT_DEV),
+    # crowded memory regions split by partitions instead of time-shared (boot mem_split)
+    "gpbs-ms": (4, dict(BUDGET_OVERRIDES, class_budget=1, mem_split=1), True, RT),  # (= gpbs since round 6)
     "gpbs-bar": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "bar,se,waveprio,latco,budget,latmem"),
     # the flagship with a smaller hardware-sample budget (SAMPLER below)
     "gpbs-b1": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, RT),
@@ -235,7 +245,9 @@ POLICY_ENGINES = {
     "credit-fixed": (4, dict(BUDGET_OVERRIDES, sched="credit-fixed"), True, RT),
     # round-3 name of the flagship on crowded mixes (time-shared, PBS quanta;
     # credit-fixed-ts: the fixed quantum)
-    "gpbs-ts": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, RT),
+    # the flagship with crowded memory regions time-shared (mem_split 0): the
+    # layout ablation of round 6
+    "gpbs-ts": (4, dict(BUDGET_OVERRIDES, class_budget=1, mem_split=0), True, RT),
     "credit-fixed-ts": (4, dict(BUDGET_OVERRIDES, class_budget=1, sched="credit-fixed"), True,
                         RT),
     # fixed per-class quanta (memory class max_us, compute class min_us), no
@@ -278,7 +290,7 @@ POLICY_ENGINES = {
                   RT),
     # round 5's flagship: one region quantum (the co-sharers' largest adaptive
     # quantum, floored at a global 30 ms)
-    "gpbs-sq30": (4, dict(BUDGET_OVERRIDES, class_budget=1, region_q=1, shared_q_us=30000), True,
+    "gpbs-sq30": (4, dict(BUDGET_OVERRIDES, class_budget=1, region_q=1, shared_q_us=30000, mem_split=0), True,
                   RT),
     # the long-quantum ablations with credit ordering the time-shared region
     # (region_vt 0: round 5's dispatch core)
@@ -803,12 +815,12 @@ class Corun:
                 r.set_gate(True)
             if isinstance(coll, CollTenant):
                 coll.gate = True
-        elif policy == "static-se":
+        elif policy in ("static-se", "static-se2"):
             # hand-picked shader-engine layout (STATIC_SE), no engine, no
             # counters: the same SE gating, CU-masked class-half streams and
             # latency tenant (co-resident, raised wave priority) as gpbs
             owners = [-1] * (XCDS * 4)
-            for name, (xs, ses) in STATIC_SE[self.cfg.mix].items():
+            for name, (xs, ses) in (STATIC_SE2 if policy == "static-se2" else STATIC_SE)[self.cfg.mix].items():
                 for x in xs:
                     for se in ses:
                         owners[x * 4 + se] = self.tid[name]

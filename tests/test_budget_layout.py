@@ -19,7 +19,10 @@ COMPUTE, MEMORY = (1000, 1), (100, 100)  # (inst, miss) per us: rate 100 vs 1e5 
 def _engine(**over):
     parts = [(0, x, c) for x in range(8) for c in range(4)]
     prof = dict(MI355X_PROFILE)
-    prof.update(class_split=2, idle_skip=1, quantum_align_us=0, class_budget=1, present_us=5000)
+    # mem_split 0: these tests pin the time-shared memory region (round 5's
+    # layout, still the compute region's); test_crowded_memory_region_* below
+    # covers the split
+    prof.update(class_split=2, idle_skip=1, quantum_align_us=0, class_budget=1, present_us=5000, mem_split=0)
     prof.update(over)
     e = Engine(sim_clock=True, partitions=parts, **prof)
     e.tenant_create("Domain-0", nslots=1)
@@ -517,4 +520,42 @@ def test_short_request_tenant_stays_present_and_leaves_the_probe_layout():
     assert e.tenant_info(g).budget_ctx & 0xF == 0x3  # the GEMM keeps the compute half
     assert relayouts[1] - relayouts[0] <= 1, relayouts  # the last 200 ms: a settled layout
     assert e.perfc()["probe_expired"] > 0
+    assert e.check() == ""
+
+
+def test_crowded_memory_region_is_split_by_partitions():
+    """boot mem_split (the MI355X profile's default): a crowded memory region
+    is split by partitions in context-major order -- an equal block per
+    backlogged tenant, a small one (an eighth of the region) for a light
+    tenant (a latency tenant busy at few class ticks) -- while a crowded
+    compute region stays time-shared."""
+    e, parts = _engine(present_us=10000, probe_max_us=50000, mem_split=1)
+    gs = [e.tenant_create(f"g{i}", nslots=32) for i in range(3)]
+    ms = [e.tenant_create(f"m{i}", nslots=32) for i in range(3)]
+    lat = e.tenant_create("lat", nslots=32)
+    rates = {**{g: COMPUTE for g in gs}, **{m: MEMORY for m in ms}}
+    for t in rates:
+        e.wake(t)
+    _settle(e, rates, 300)
+    for _ in range(200):  # 400 ms of 2 ms request cycles
+        e.wake(lat)
+        _feed(e, rates, 100)
+        e.block(lat)
+        for _ in range(19):
+            _feed(e, rates, 100)
+    info = {t: e.tenant_info(t) for t in gs + ms + [lat]}
+    # compute region: time-shared, every GEMM on both compute SEs
+    assert all(info[g].budget_shared and info[g].budget_ctx & 0xF == 0x3 for g in gs), info
+    # memory region: 16 partitions -> 6 / 5 / 5 / ... minus the light tenant's 2
+    sizes = [info[m].online_slots for m in ms]
+    assert sorted(sizes) == [4, 5, 5] and info[lat].online_slots == 2, (sizes, info[lat])
+    assert not any(info[m].budget_shared for m in ms + [lat])
+    owned = Counter()
+    for p, (_, _, c) in enumerate(parts):
+        if c >= 2:
+            owned[e.partition_info(p)["curr_tenant"]] += 1
+    # each memory tenant runs on its whole block (the light tenant's idle
+    # block may lend itself to a waiting slot: class_steal work conservation)
+    assert all(owned[m] == info[m].online_slots for m in ms), owned
+    assert e.perfc()["mem_split"] >= 1
     assert e.check() == ""

@@ -42,6 +42,7 @@ from pbs_amd.core.config import MI355X_PROFILE
 from pbs_amd.core.engine import Engine
 from pbs_amd.bench.corun import BUDGET_OVERRIDES
 prof = dict(MI355X_PROFILE); prof.update(BUDGET_OVERRIDES); prof["class_budget"] = 1
+prof["mem_split"] = 0  # the memory region time-shared: switches all the time
 e = Engine(**prof)
 for x in range(8):
     for c in range(4):
