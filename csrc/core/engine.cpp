@@ -1063,7 +1063,11 @@ void Engine::budget_layout(Pool& pl, int64_t n, bool force) {
       const int P = (int)reg.size();
       int lp = lite.empty() ? 0 : std::max(1, P / 8);
       while (!lite.empty() && lp > 1 && (int)lite.size() * lp > P / 2) --lp;
-      const int hp = P - (int)lite.size() * lp, nh = (int)heavy.size();
+      // mem_split 2: the light tenants' blocks overlap the last backlogged
+      // tenant's instead of sitting idle between requests -- a request
+      // BOOST-preempts that tenant on them
+      const bool overlap = boot.mem_split >= 2;
+      const int hp = overlap ? P : P - (int)lite.size() * lp, nh = (int)heavy.size();
       if (nh > 0 && hp >= nh) {
         int at = 0;
         auto give = [&](int id, int sz) {
@@ -1073,6 +1077,7 @@ void Engine::budget_layout(Pool& pl, int64_t n, bool force) {
           place_parts(*tenants[id], pl, m);
         };
         for (int i = 0; i < nh; ++i) give(heavy[i], hp / nh + (i < hp % nh ? 1 : 0));
+        if (overlap) at = P - (int)lite.size() * lp;
         for (int id : lite) give(id, lp);
         perfc.incr(PC_mem_split);
         continue;

@@ -121,7 +121,9 @@ typedef struct gpbs_boot_params {
                                   half of the class ticks: a latency tenant) a small one.  Memory-bound tenants are
                                   bandwidth-bound well below a whole region (concave in CUs), and tenants bound by
                                   different paths (HBM vs the MALL) overlap; a crowded compute region stays
-                                  time-shared (a GEMM needs its tile count of CUs).  0 = time-share */
+                                  time-shared (a GEMM needs its tile count of CUs).  2 = the light tenants' blocks
+                                  overlap the last backlogged tenant's (a request BOOST-preempts it there) instead of
+                                  idling between requests.  0 = time-share */
   gpbs_adapt_params_t adapt;
   gpbs_atc_params_t atc;
 } gpbs_boot_params_t;

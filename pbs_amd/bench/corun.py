@@ -238,6 +238,8 @@ POLICY_ENGINES = {
     "gpbs-dev": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, RT_DEV),
     # crowded memory regions split by partitions instead of time-shared (boot mem_split)
     "gpbs-ms": (4, dict(BUDGET_OVERRIDES, class_budget=1, mem_split=1), True, RT),  # (= gpbs since round 6)
+    # ... with the light (latency) tenant's block overlapping a backlogged tenant's
+    "gpbs-ms2": (4, dict(BUDGET_OVERRIDES, class_budget=1, mem_split=2), True, RT),
     "gpbs-bar": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "bar,se,waveprio,latco,budget,latmem"),
     # the flagship with a smaller hardware-sample budget (SAMPLER below)
     "gpbs-b1": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, RT),

@@ -64,8 +64,10 @@ MI355X_PROFILE: Dict[str, Any] = dict(
     # (engine.cpp budget_layout): memory-bound tenants keep most of their rate
     # on a fraction of the region, and an HBM stream next to a MALL-resident
     # or launch-bound tenant overlaps instead of taking turns -- measured
-    # 8mix 1.430 vs 1.380 time-shared, slo 1.338 vs 1.276 (profiles/r6/s21)
-    mem_split=1,
+    # 8mix 1.430 vs 1.380 time-shared, slo 1.338 vs 1.276 (profiles/r6/s21);
+    # 2: a light (latency) tenant's block overlaps a backlogged tenant's
+    # instead of idling between requests (slo 1.380 vs 1.339, same p99, s25)
+    mem_split=2,
     adapt=dict(threshold=20000, band_lo=70, band_hi=130, min_us=1000, max_us=11000, inc_us=1000, dec_us=2000,
                switch_boundary=9000, ticks_per_tslice=3,
                # grow_pct > 0: proportional growth + a restart at the class bound
