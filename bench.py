@@ -194,6 +194,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # stdout carries exactly one line, rank 0's JSON: the process's fd 1 goes
+    # to stderr until then (gloo prints its "[Gloo] Rank r is connected to N
+    # peer ranks" banners to stdout from C++, one per group and rank)
+    line_fd = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
     if args.gpus > 1 and world == 1:
         print("bench.py: --gpus > 1 must be launched with torch.distributed.run (one rank per GPU)", file=sys.stderr)
         sys.exit(2)
@@ -457,7 +463,10 @@ def main():
             print(f"bench.py: detail record not written: {ex}", file=sys.stderr)
             out = ""
         digests = {m: mix_digest(results[m]["summary"], results[m]["runs"]) for m in mixes}
+        sys.stdout.flush()
+        os.dup2(line_fd, 1)
         print(json.dumps(compact_line(line, digests, os.path.relpath(out, ROOT) if out else "")), flush=True)
+        os.dup2(2, 1)
     if world > 1:
         import torch.distributed as dist
         dist.barrier(group=groups["ctrl"])
