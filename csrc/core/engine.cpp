@@ -1020,11 +1020,37 @@ void Engine::budget_layout(Pool& pl, int64_t n, bool force) {
   const int split = std::min(std::max(1, boot.class_split), nctx);
   std::vector<int> cls_t[2];
   for (auto& e : sig) cls_t[e.second & 1].push_back(e.first);
+  // The two class halves are the same hardware when they are equal (SEs
+  // {0,1} and {2,3} of every XCD): which class holds which half only decides
+  // how many tenants move.  Keep the orientation that leaves more tenants on
+  // the half they hold -- a classifier that swaps two tenants' classes
+  // (config #5: the trainer's optimizer step streams 16 GB and out-misses the
+  // fp8 decode over some windows) then costs no relayout at all, instead of
+  // swapping both tenants' CU masks back and forth (profiles/r6/s28: decode
+  // ~45 % of its slices on the other half, aggregate 1.19 against 1.24
+  // without the swaps).
+  if (!cls_t[0].empty() && !cls_t[1].empty() && 2 * split == nctx) {
+    const uint32_t lo_m = (1u << split) - 1, hi_m = ((1u << nctx) - 1) & ~lo_m;
+    int nat = 0, mir = 0;
+    for (int c = 0; c < 2; ++c)
+      for (int id : cls_t[c]) {
+        const uint32_t b = tenants[id]->budget_ctx & 0xFFu;
+        const int h = !b ? -1 : (b & ~lo_m) == 0 ? 0 : (b & ~hi_m) == 0 ? 1 : -1;
+        if (h >= 0) (h == c ? nat : mir)++;
+      }
+    if (mir != nat) {
+      const bool m = mir > nat;
+      if (m != pl.mirror) perfc.incr(PC_mirror);
+      pl.mirror = m;
+    }
+  } else {
+    pl.mirror = false;
+  }
   for (int c = 0; c < 2; ++c) {
     if (cls_t[c].empty()) continue;
     int lo = 0, hi = nctx;  // class region [lo, hi)
     if (!cls_t[0].empty() && !cls_t[1].empty()) {
-      if (c == 0) hi = split;
+      if ((c == 0) != pl.mirror) hi = split;
       else lo = split;
     }
     const int r = hi - lo, k = (int)cls_t[c].size();

@@ -235,6 +235,9 @@ struct Pool {
   // last computed for
   std::vector<std::pair<int, int>> budget_sig;
   std::vector<int> budget_light;  // mem_split: the light tenants of that layout
+  // symmetric class halves (class_split = nctx / 2): the compute class holds
+  // the upper half and the memory class the lower one (a mirrored layout)
+  bool mirror = false;
 };
 
 std::unique_ptr<Scheduler> make_scheduler(const std::string& name, Engine& e, int pool);

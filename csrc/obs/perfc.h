@@ -19,7 +19,7 @@ namespace gpbs {
   X(vcpu_check) X(delay_ms) X(adapt_inc) X(adapt_dec) X(adapt_rearm) X(metric_tick) X(report_rx)     \
   X(gang_epoch) X(gang_timeout) X(counter_stale) X(counter_reset) X(tenant_dead) X(atc_apply) X(fault_injected)         \
   X(partition_switch) X(sched_irq) X(ratelimit_hold) X(boost_park) X(watchdog_fired) X(adapt_idle_skip) \
-  X(class_change) X(relayout) X(adapt_device) X(adapt_late) X(probe_layout) X(probe_expired) X(wake_homed) X(mem_split) \
+  X(class_change) X(relayout) X(adapt_device) X(adapt_late) X(probe_layout) X(probe_expired) X(wake_homed) X(mem_split) X(mirror) \
   X(steal_sibling_skip)
 
 enum PerfcId : int {

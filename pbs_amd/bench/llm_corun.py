@@ -229,6 +229,8 @@ def run(policy: str, kinds, args: dict, seconds: float, warmup: float) -> Dict[s
             args["infer_shift"] = int(m[6:])
         elif m.startswith("tshift"):  # ... the trainer's
             args["train_shift"] = int(m[6:])
+        elif m.startswith("slow"):  # daemon sampler: steady-layout back-off period N ms ([runtime] slow_us)
+            args["slow_us"] = int(m[4:]) * 1000
         else:
             raise ValueError(f"unknown policy variant +{m}")
     if policy in ("gpbs", "gpbs-spatial"):
@@ -236,6 +238,13 @@ def run(policy: str, kinds, args: dict, seconds: float, warmup: float) -> Dict[s
         sock = os.path.join(tempfile.mkdtemp(), "gpbsd.sock")
         daemon = Daemon(sock, gpus=[0], nctx=2, sim=False, profile="mi355x").start()
     elif policy in ("gpbs-se", "gpbs-budget"):
+        if args.get("slow_us"):  # the daemon's GpuContext reads [runtime] from GPBS_CONFIG
+            cfgp = os.path.join(tempfile.mkdtemp(), "gpbs.toml")
+            with open(cfgp, "w") as f:
+                f.write(f"[runtime]\nslow_us = {int(args['slow_us'])}\n")
+            os.environ["GPBS_CONFIG"] = cfgp
+        else:
+            os.environ.pop("GPBS_CONFIG", None)
         # SE-exclusive class split driven by LIVE hardware counters: the daemon
         # owns the GPU actuator + rocprofiler-sdk sampler; the tenants' kernels
         # run on streams masked to the shader engines they own, so the per-SE

@@ -565,3 +565,34 @@ def test_crowded_memory_region_is_split_by_partitions(mode):
         assert info[lat].budget_ctx & 0xF == 0x8, hex(info[lat].budget_ctx)
     assert e.perfc()["mem_split"] >= 1
     assert e.check() == ""
+
+
+def test_swapped_classes_mirror_the_halves_instead_of_moving_tenants():
+    """Equal class halves are the same hardware: when two tenants swap
+    classes (config #5's trainer out-missing the decode tenant over some
+    windows) the layout keeps both where they are and mirrors which half is
+    the compute one -- no CU-mask change, no revocation.  A single tenant
+    changing class still moves (it joins the other class's half)."""
+    e, parts = _engine()
+    a, b = e.tenant_create("a", nslots=32), e.tenant_create("b", nslots=32)
+    rates = {a: COMPUTE, b: MEMORY}
+    for t in rates:
+        e.wake(t)
+    _settle(e, rates)
+    before = {t: e.tenant_info(t).budget_ctx & 0xF for t in (a, b)}
+    assert before == {a: 0x3, b: 0xC}, before
+    rel = e.perfc()["relayout"]
+    _settle(e, {a: MEMORY, b: COMPUTE})
+    assert e.lib.gpbs_tenant_class(e.h, a) == 1 and e.lib.gpbs_tenant_class(e.h, b) == 0
+    after = {t: e.tenant_info(t).budget_ctx & 0xF for t in (a, b)}
+    assert after == before, after  # nobody moved
+    assert e.perfc()["mirror"] >= 1 and e.perfc()["relayout"] > rel
+    own = _ctx_owners(e, parts)
+    assert own[0][a] == 8 and own[1][a] == 8 and own[2][b] == 8 and own[3][b] == 8, own
+    # a third tenant of the compute class joins b's (compute) half
+    c = e.tenant_create("c", nslots=32)
+    e.wake(c)
+    _settle(e, {a: MEMORY, b: COMPUTE, c: COMPUTE})
+    assert e.tenant_info(c).budget_ctx & 0xF in (0x4, 0x8), hex(e.tenant_info(c).budget_ctx)
+    assert e.tenant_info(a).budget_ctx & 0xF == 0x3
+    assert e.check() == ""
