@@ -1598,6 +1598,7 @@ struct MaskedPoolCore {
     uint32_t key;
     int refs;
     int pipe;  // creation index mod kPipes (in the device's burst)
+    double load = 0;  // its holders' dispatch rates (launches / s, as they acquired it)
   };
   std::mutex mu;
   std::vector<Ent> ents;
@@ -1634,37 +1635,45 @@ struct MaskedPoolCore {
     for (const auto& e : ents) n += e.device == dev && e.refs > 0;
     return n;
   }
-  // cost of running a layout of mask m / key k on `pipe` next to the held queues
-  int pipe_cost(int dev, int pipe, const uint32_t m[8], uint32_t key, const Ent* self) const {
-    int cost = 0;
+  // cost of running a layout of mask m / key k on `pipe` next to the held
+  // queues: 10 per queue of the other class half (its dispatch waiting for
+  // CUs holds this pipe), 1 per queue of the same half -- each weighted by
+  // how busy that queue keeps the pipe (1 + its holders' launches per ms), so
+  // a launch-bound tenant shares its pipe with the latency tenant's idle
+  // queue rather than with a stream (slo mix: the MALL-sized tenant kept 0.284
+  // of its solo rate on a pipe of its own or next to the latency queue, 0.200
+  // next to a stream's queue, profiles/r6/s30)
+  double pipe_cost(int dev, int pipe, const uint32_t m[8], uint32_t key, const Ent* self) const {
+    double cost = 0;
     for (const auto& e : ents)
       if (&e != self && e.device == dev && e.refs > 0 && e.pipe == pipe && (key == 0 || e.key != key))
-        cost += std::memcmp(e.m, m, sizeof(e.m)) != 0 ? 10 : 1;
+        cost += (std::memcmp(e.m, m, sizeof(e.m)) != 0 ? 10.0 : 1.0) * (1.0 + e.load / 1000.0);
     return cost;
   }
   // key 0: exclusive (never shared).  create(m) makes a new queue (nullptr on
   // failure).  Caller does not hold mu.
   template <class Create>
-  hipStream_t acquire(int dev, const uint32_t m[8], uint32_t key, Create&& create) {
+  hipStream_t acquire(int dev, const uint32_t m[8], uint32_t key, Create&& create, double load = 0) {
     std::lock_guard<std::mutex> g(mu);
     Ent* same = nullptr;   // this layout's queue
     Ent* idle = nullptr;   // the cheapest queue of this mask nobody holds
     Ent* least = nullptr;  // least-held keyed queue of this mask
-    int live = 0, idle_cost = 1 << 30;
+    int live = 0;
+    double idle_cost = 1e30;
     for (auto& e : ents) {
       if (e.device != dev) continue;
       live++;
       if (std::memcmp(e.m, m, sizeof(e.m)) != 0) continue;
       if (key && e.key == key && e.refs > 0 && (!same || e.refs < same->refs)) same = &e;
       if (e.refs == 0) {
-        const int cst = pipe_cost(dev, e.pipe, m, key, &e) * 2 + (key && e.key == key ? 0 : 1);
+        const double cst = pipe_cost(dev, e.pipe, m, key, &e) * 2 + (key && e.key == key ? 0 : 1);
         if (cst < idle_cost) idle = &e, idle_cost = cst;
       }
       if (e.key && e.refs > 0 && (!least || e.refs < least->refs)) least = &e;
     }
     const int dv = dev >= 0 && dev < 16 ? dev : 0;
     const int new_pipe = dev_created[dv] % kPipes;
-    const int new_cost = pipe_cost(dev, new_pipe, m, key, nullptr) * 2 + 1;
+    const double new_cost = pipe_cost(dev, new_pipe, m, key, nullptr) * 2 + 1;
     hipStream_t s = nullptr;
     Ent* got = nullptr;
     if (same) {
@@ -1688,15 +1697,17 @@ struct MaskedPoolCore {
       got = least;
     }
     if (got != same && pipe_cost(dev, got->pipe, m, key, got) >= 10) pipe_shared_other++;
+    got->load += load;
     held_max = std::max(held_max, held_locked(dev));
     return got->s;
   }
-  void release(hipStream_t s) {
+  void release(hipStream_t s, double load = 0) {
     if (!s) return;
     std::lock_guard<std::mutex> g(mu);
     for (auto& e : ents)
       if (e.s == s && e.refs > 0) {
         e.refs--;
+        e.load = e.refs ? std::max(0.0, e.load - load) : 0.0;
         return;
       }
   }
@@ -1712,7 +1723,7 @@ MaskedPoolCore& masked_pool() {
   return *p;
 }
 void half_mask(int h, uint32_t m[8]);
-hipStream_t masked_acquire_key(const uint32_t m[8], uint32_t key) {
+hipStream_t masked_acquire_key(const uint32_t m[8], uint32_t key, double load = 0) {
   int dev = 0;
   hipGetDevice(&dev);
   auto create = [](const uint32_t* mm) -> hipStream_t {
@@ -1724,7 +1735,7 @@ hipStream_t masked_acquire_key(const uint32_t m[8], uint32_t key) {
   half_mask(1, mm);
   const uint32_t* masks[2] = {mc, mm};
   masked_pool().prealloc(dev, masks, kPlan, kPlanLen, create);
-  return masked_pool().acquire(dev, m, key, create);
+  return masked_pool().acquire(dev, m, key, create, load);
 }
 hipStream_t masked_acquire(const uint32_t m[8]) { return masked_acquire_key(m, 0); }
 void masked_release(const uint32_t*, hipStream_t s) { masked_pool().release(s); }
@@ -1796,6 +1807,9 @@ struct Runner {
   }
   uint32_t key_bits = 0;             // ... its key: the owned (XCD, SE) partition set
   int key_half = -1;
+  double key_load = 0;               // launches / s it acquired key_stream with
+  int64_t rate_t0 = 0;               // dispatch-rate window of the last layout
+  uint64_t rate_l0 = 0;
   int cur_grid = 0;  // grid for the stream pick_stream chose (0: kernel default)
   WorkQueue* d_q = nullptr;  // ring of depth+1 queues
   u32* h_status = nullptr;   // pinned status words
@@ -1887,9 +1901,15 @@ struct Runner {
       se_half_mask(half, m);
       if (key_stream) {
         retire_stream(key_stream);
-        masked_release(m, key_stream);
+        masked_pool().release(key_stream, key_load);
       }
-      key_stream = masked_acquire_key(m, bits);
+      // this runner's dispatch rate since its last layout change weights the
+      // pipe choice (MaskedPoolCore::pipe_cost)
+      const int64_t tnow = mono_ns();
+      key_load = rate_t0 && tnow > rate_t0 ? (double)(st.launches - rate_l0) * 1e9 / (double)(tnow - rate_t0) : 0.0;
+      rate_t0 = tnow;
+      rate_l0 = st.launches;
+      key_stream = masked_acquire_key(m, bits, key_load);
       key_bits = bits;
       key_half = half;
       if (!key_stream) return stream;
@@ -3635,6 +3655,23 @@ int gpbs_hip_masked_pool_selftest(void) {
   hipStream_t r4 = R.acquire(0, mm, 0x40, mk), lane = R.acquire(0, mm, 0, mk);
   if (R.created != (uint64_t)kPlanLen || R.cross_key_shares || R.pipe_shared_other) return 17;
   if (R.pipe_of(rc2) != 0 || R.pipe_of(rc3) != 0 || R.pipe_of(r4) == 0 || R.pipe_of(lane) == 0) return 18;
+  // 10. dispatch-rate weights: four memory layouts on three memory pipes --
+  //     two streams, a launch-bound tenant, a latency tenant -- the
+  //     launch-bound one never shares a pipe with a stream, in any order
+  const double loads[4] = {2500, 2500, 20000, 500};
+  const int orders[4][4] = {{0, 1, 2, 3}, {2, 0, 1, 3}, {3, 0, 1, 2}, {0, 3, 2, 1}};
+  for (const auto& ord : orders) {
+    MaskedPoolCore W;
+    if (W.prealloc(0, masks, kPlan, kPlanLen, mk) != kPlanLen) return 19;
+    W.acquire(0, mc, 0x1, mk, 100000);  // the compute layout on pipe 0
+    hipStream_t q4[4];
+    for (int i : ord) q4[i] = W.acquire(0, mm, 0x10u << i, mk, loads[i]);
+    const int pb = W.pipe_of(q4[2]);
+    if (pb == 0 || pb == W.pipe_of(q4[0]) || pb == W.pipe_of(q4[1])) return 20;
+    W.release(q4[2], loads[2]);
+    for (auto& en : W.ents)
+      if (en.s == q4[2] && (en.refs || en.load != 0)) return 21;
+  }
   return 0;
 }
 
@@ -3916,7 +3953,7 @@ void gpbs_runner_destroy(void* p) {
       masked_release(m, r->se_stream[h]);
     }
   }
-  if (r->key_stream) masked_release(nullptr, r->key_stream);
+  if (r->key_stream) masked_pool().release(r->key_stream, r->key_load);
   hipFree(r->d_q);
   hipHostFree(r->h_status);
   delete r;
