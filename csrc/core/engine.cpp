@@ -1102,7 +1102,47 @@ void Engine::budget_layout(Pool& pl, int64_t n, bool force) {
           at += sz;
           place_parts(*tenants[id], pl, m);
         };
-        for (int i = 0; i < nh; ++i) give(heavy[i], hp / nh + (i < hp % nh ? 1 : 0));
+        // Which backlogged tenant gets which block: greedily the pair with
+        // the most partitions the tenant holds already (its online slots'
+        // homes), so a tenant joining or leaving the region (a phase change)
+        // moves as few partitions as it can -- each moved partition is a
+        // revocation of the tenant that held it.  Newcomers take what is left.
+        std::vector<int> bstart(nh), bsize(nh), owner(nh, -1);
+        for (int i = 0, a = 0; i < nh; ++i) {
+          bstart[i] = a;
+          bsize[i] = hp / nh + (i < hp % nh ? 1 : 0);
+          a += bsize[i];
+        }
+        std::vector<std::vector<int>> ov(nh, std::vector<int>(nh, 0));
+        for (int ti = 0; ti < nh; ++ti)
+          for (int sid : tenants[heavy[ti]]->slots) {
+            const Slot& v = *slots[sid];
+            if (v.class_home < 0 || (v.pause_flags & VPF_DOWN)) continue;
+            for (int bi = 0; bi < nh; ++bi)
+              for (int j = bstart[bi]; j < bstart[bi] + bsize[bi]; ++j)
+                if (reg[j] == v.class_home) ov[ti][bi]++;
+          }
+        std::vector<bool> tdone(nh, false);
+        for (int round = 0; round < nh; ++round) {
+          int bt = -1, bb = -1, best = 0;
+          for (int ti = 0; ti < nh; ++ti)
+            for (int bi = 0; bi < nh && !tdone[ti]; ++bi)
+              if (owner[bi] < 0 && ov[ti][bi] > best) best = ov[ti][bi], bt = ti, bb = bi;
+          if (bt < 0) break;
+          owner[bb] = bt;
+          tdone[bt] = true;
+        }
+        for (int bi = 0, ti = 0; bi < nh; ++bi)
+          if (owner[bi] < 0) {
+            while (tdone[ti]) ++ti;
+            owner[bi] = ti;
+            tdone[ti] = true;
+          }
+        for (int bi = 0; bi < nh; ++bi) {
+          at = bstart[bi];
+          give(heavy[owner[bi]], bsize[bi]);
+        }
+        at = hp;
         if (overlap) at = P - (int)lite.size() * lp;
         for (int id : lite) give(id, lp);
         perfc.incr(PC_mem_split);

@@ -596,3 +596,31 @@ def test_swapped_classes_mirror_the_halves_instead_of_moving_tenants():
     assert e.tenant_info(c).budget_ctx & 0xF in (0x4, 0x8), hex(e.tenant_info(c).budget_ctx)
     assert e.tenant_info(a).budget_ctx & 0xF == 0x3
     assert e.check() == ""
+
+
+def test_split_blocks_stay_put_when_a_tenant_joins_the_region():
+    """A memory tenant joining a split region (a phase tenant turning
+    memory-bound) shrinks its neighbours' blocks in place: every incumbent
+    keeps most of the partitions it held (each moved partition is a
+    revocation), whatever the tenant ids."""
+    e, parts = _engine(mem_split=1)
+    g = e.tenant_create("gemm", nslots=32)
+    late = e.tenant_create("late", nslots=32)  # lowest id of the memory tenants
+    ms = [e.tenant_create(f"m{i}", nslots=32) for i in range(3)]
+    rates = {g: COMPUTE, late: COMPUTE, **{m: MEMORY for m in ms}}
+    for t in rates:
+        e.wake(t)
+    _settle(e, rates, 300)
+
+    def homes(t):
+        return {p for p, (_, _, c) in enumerate(parts) if c >= 2 and e.partition_info(p)["curr_tenant"] == t}
+
+    before = {m: homes(m) for m in ms}
+    assert all(len(v) >= 5 for v in before.values()), before
+    _settle(e, {**rates, late: MEMORY}, 300)  # its phase turns memory-bound
+    assert e.lib.gpbs_tenant_class(e.h, late) == 1
+    after = {m: homes(m) for m in ms}
+    assert len(homes(late)) == 4 and all(len(v) == 4 for v in after.values()), (after, homes(late))
+    for m in ms:
+        assert len(before[m] & after[m]) >= 3, (m, before[m], after[m])
+    assert e.check() == ""
