@@ -51,7 +51,7 @@ def main():
     zero = q.zero_
     dev = "cuda"
     out = []
-    n = 4096
+    n = 4096 if not os.environ.get("KBENCH_NO_GEMM") else 256  # KBENCH_NO_GEMM: streams / reduce only
     A = torch.randn(n, n, device=dev, dtype=torch.bfloat16)
     B = torch.randn(n, n, device=dev, dtype=torch.bfloat16)
     Cm = torch.empty(n, n, device=dev, dtype=torch.bfloat16)
