@@ -1,4 +1,113 @@
+"""Timeline of the live phase-change test (tests/test_gpu_phase.py) for
+debugging: the same three tenants (GEMM, phase GEMM<->stream, HBM stream)
+under the counter-driven SE budgets, with one row per poll -- units done,
+owner waits, budget masks, the first XCD's owners, the runners' masked-queue
+indexes, classes and miss rates.  Found the ~100 ms freeze of every runner at
+the first SE-exclusive relayout (the lazy masked-queue burst,
+profiles/r6/phase_debug_summary.txt).
+
+    python scripts/phase_debug.py <repo root> <align 0|1>   (prints RESULT {json})
+"""
+import json
 import sys
+import time
+
 ROOT = sys.argv[1]
 ALIGN = int(sys.argv[2])
-exec(compile('\nimport json, sys, time\nsys.path.insert(0, %r)\nfrom pbs_amd.counters import hwc\nassert hwc.init()\nimport torch\ntorch.cuda.set_device(0)\ntorch.zeros(1, device="cuda")\nassert hwc.start()\nfrom pbs_amd.runtime.gpu import GpuContext, Runner\nfrom pbs_amd.core.config import MI355X_PROFILE\nfrom pbs_amd.core.engine import Engine\nfrom pbs_amd.bench.corun import BUDGET_OVERRIDES\nprof = dict(MI355X_PROFILE); prof.update(BUDGET_OVERRIDES)\ne = Engine(**prof)\nfor x in range(8):\n    for c in range(4):\n        e.pool_assign(0, e.partition_add(0, x, c))\ne.tenant_create("Domain-0", nslots=1)\ng = e.tenant_create("gemm", nslots=32)\np = e.tenant_create("phase", nslots=32)\ns = e.tenant_create("hbm", nslots=32)\nctx = GpuContext(0, nctx=4, table_mode="device")\nctx.set_se_mode(True)\nctx.attach(e, nctx=4)\nctx.set_hwc_sampler(align=%d)\nctx.set_hwc(True)\ne.start()\nrg = Runner(ctx, "gemm", g, M=4096, N=4096, K=4096)\nrp = Runner(ctx, "gemm", p, M=4096, N=4096, K=4096, alt=dict(kind="stream", bytes=1 << 30))\nrs = Runner(ctx, "stream", s, bytes=1 << 30)\ndef topup():\n    for r, q in ((rg, 400), (rp, 400), (rs, 100)):\n        st = r.stats()\n        if st.submitted - st.units_done < q:\n            r.submit(q)\ndef info():\n    return {n: (e.lib.gpbs_tenant_class(e.h, t), e.tenant_info(t).budget_ctx) for n, t in (("gemm", g), ("phase", p), ("hbm", s))}\nTL = []\nT00 = time.perf_counter()\ndef run_until(pred, limit_s):\n    t0 = time.perf_counter()\n    while time.perf_counter() - t0 < limit_s:\n        topup()\n        i = info()\n        TL.append([round((time.perf_counter() - T00) * 1e3, 1), rg.stats().units_done, rp.stats().units_done,\n                   rs.stats().units_done, rg.stats().waits_owner, rp.stats().waits_owner, rs.stats().waits_owner,\n                   i["gemm"][1], i["phase"][1], i["hbm"][1], ctx.owners()[:4], [ctx.L.gpbs_runner_queue(r.h) for r in (rg, rp, rs)], [i[n][0] for n in ("gemm", "phase", "hbm")], [e.tenant_info(t).cache_miss_rate for t in (g, p, s)]])\n        if pred(i):\n            return (time.perf_counter() - t0) * 1e3\n        time.sleep(0.001)\n    return -1.0\nout = {"metric_period_us": prof["metric_period_us"]}\ndef compute_layout(i):\n    return i["phase"][0] == 0 and i["phase"][1] in (1, 2) and i["gemm"][1] in (1, 2) and i["hbm"][1] == 12\ndef memory_layout(i):\n    return i["phase"][0] == 1 and i["phase"][1] in (4, 8) and i["gemm"][1] == 3 and i["hbm"][1] in (4, 8)\nout["settle_ms"] = run_until(compute_layout, 5.0)\nout["layout0"] = info()\ne.perfc_reset()\nrp.set_phase(1)\nout["to_memory_ms"] = run_until(memory_layout, 3.0)\nout["layout1"] = info()\nrp.set_phase(0)\nout["to_compute_ms"] = run_until(compute_layout, 3.0)\nout["layout2"] = info()\npc = e.perfc()\nout["adapt_rearm"] = pc["adapt_rearm"]; out["relayout"] = pc["relayout"]; out["class_change"] = pc["class_change"]\nout["units_alt"] = rp.stats().units_alt\nout["hwc"] = ctx.hwc_stats()\nout["periods"] = {n: ctx.hwc_tenant_periods(t) for n, t in (("gemm", g), ("phase", p), ("hbm", s))}\nimport ctypes as _C\n_ring = (_C.c_int64 * (3 * 512))()\n_k = ctx.L.gpbs_gpu_cadence_ring(ctx.h, _ring, 512)\nout["ring"] = [[(_ring[3 * i] - _ring[0]) // 1000, _ring[3 * i + 1], _ring[3 * i + 2]] for i in range(_k)]\nfor r in (rg, rp, rs):\n    r.cancel()\nfor r in (rg, rp, rs):\n    r.wait(120)\ne.stop()\nout["check"] = e.check()\nfor r in (rg, rp, rs):\n    r.close()\nctx.close(); e.close()\nout["tl"] = TL\nprint("RESULT " + json.dumps(out))\n' % (ROOT, ALIGN), "phase_debug", "exec"))
+sys.path.insert(0, ROOT)
+
+from pbs_amd.counters import hwc  # noqa: E402
+
+assert hwc.init()
+import torch  # noqa: E402
+
+torch.cuda.set_device(0)
+torch.zeros(1, device="cuda")
+assert hwc.start()
+from pbs_amd.bench.corun import BUDGET_OVERRIDES  # noqa: E402
+from pbs_amd.core.config import MI355X_PROFILE  # noqa: E402
+from pbs_amd.core.engine import Engine  # noqa: E402
+from pbs_amd.runtime.gpu import GpuContext, Runner  # noqa: E402
+
+prof = dict(MI355X_PROFILE)
+prof.update(BUDGET_OVERRIDES)
+e = Engine(**prof)
+for x in range(8):
+    for c in range(4):
+        e.pool_assign(0, e.partition_add(0, x, c))
+e.tenant_create("Domain-0", nslots=1)
+g = e.tenant_create("gemm", nslots=32)
+p = e.tenant_create("phase", nslots=32)
+s = e.tenant_create("hbm", nslots=32)
+ctx = GpuContext(0, nctx=4, table_mode="device")
+ctx.set_se_mode(True)
+ctx.attach(e, nctx=4)
+ctx.set_hwc_sampler(align=ALIGN)
+ctx.set_hwc(True)
+e.start()
+rg = Runner(ctx, "gemm", g, M=4096, N=4096, K=4096)
+rp = Runner(ctx, "gemm", p, M=4096, N=4096, K=4096, alt=dict(kind="stream", bytes=1 << 30))
+rs = Runner(ctx, "stream", s, bytes=1 << 30)
+runners = (rg, rp, rs)
+tids = (("gemm", g), ("phase", p), ("hbm", s))
+
+
+def topup():
+    for r, q in ((rg, 400), (rp, 400), (rs, 100)):
+        st = r.stats()
+        if st.submitted - st.units_done < q:
+            r.submit(q)
+
+
+def info():
+    return {n: (e.lib.gpbs_tenant_class(e.h, t), e.tenant_info(t).budget_ctx) for n, t in tids}
+
+
+TL = []
+T00 = time.perf_counter()
+
+
+def run_until(pred, limit_s):
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < limit_s:
+        topup()
+        i = info()
+        st = [r.stats() for r in runners]
+        TL.append([round((time.perf_counter() - T00) * 1e3, 1)] + [x.units_done for x in st] +
+                  [x.waits_owner for x in st] + [i[n][1] for n, _ in tids] + [ctx.owners()[:4]] +
+                  [[ctx.L.gpbs_runner_queue(r.h) for r in runners]] + [[i[n][0] for n, _ in tids]] +
+                  [[e.tenant_info(t).cache_miss_rate for _, t in tids]])
+        if pred(i):
+            return (time.perf_counter() - t0) * 1e3
+        time.sleep(0.001)
+    return -1.0
+
+
+def compute_layout(i):
+    return i["phase"][0] == 0 and i["phase"][1] in (1, 2) and i["gemm"][1] in (1, 2) and i["hbm"][1] == 12
+
+
+def memory_layout(i):
+    return i["phase"][0] == 1 and i["phase"][1] in (4, 8) and i["gemm"][1] == 3 and i["hbm"][1] in (4, 8)
+
+
+out = {"metric_period_us": prof["metric_period_us"]}
+out["settle_ms"] = run_until(compute_layout, 5.0)
+e.perfc_reset()
+rp.set_phase(1)
+out["to_memory_ms"] = run_until(memory_layout, 3.0)
+rp.set_phase(0)
+out["to_compute_ms"] = run_until(compute_layout, 3.0)
+out["hwc"] = ctx.hwc_stats()
+for r in runners:
+    r.cancel()
+for r in runners:
+    r.wait(120)
+e.stop()
+out["check"] = e.check()
+for r in runners:
+    r.close()
+ctx.close()
+e.close()
+out["tl"] = TL
+print("RESULT " + json.dumps(out))
