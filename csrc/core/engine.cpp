@@ -952,6 +952,27 @@ void Engine::budget_layout(Pool& pl, int64_t n, bool force) {
     const uint32_t lo = (1u << psplit) - 1, hi = ctx_all & ~lo;
     int first = 0;  // the tenant that takes the compute half (contexts [0, split))
     if (sig[0].second == 1 || sig[1].second == 0) first = 1;
+    // Equal halves are the same hardware: two tenants that already hold one
+    // half each stay where they are, and the pool's orientation (mirror)
+    // follows the classified one -- config #5's trainer, classified while the
+    // decode tenant is still probing, used to swap halves with it (both
+    // tenants' CU masks, ~1 s of slow steps; profiles/r6/s35_llm5.json).
+    if (2 * psplit == nctx) {
+      auto half_of = [&](const Tenant& t) {
+        const uint32_t b = t.budget_ctx & 0xFFu;
+        return !b ? -1 : (b & ~lo) == 0 ? 0 : (b & ~hi) == 0 ? 1 : -1;
+      };
+      const int h0 = half_of(*tenants[sig[0].first]), h1 = half_of(*tenants[sig[1].first]);
+      if (h0 >= 0 && h1 >= 0 && h0 != h1) {
+        first = h0 == 0 ? 0 : 1;  // the tenant on the lower half keeps it
+        for (int i = 0; i < 2; ++i)
+          if (sig[i].second >= 0) {
+            const bool m = (sig[i].second == 0) != ((i == first) ? true : false);
+            if (m != pl.mirror) perfc.incr(PC_mirror);
+            pl.mirror = m;
+          }
+      }
+    }
     for (int i = 0; i < 2; ++i) {
       Tenant& t = *tenants[sig[i].first];
       t.budget_shared = false;

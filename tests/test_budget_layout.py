@@ -624,3 +624,25 @@ def test_split_blocks_stay_put_when_a_tenant_joins_the_region():
     for m in ms:
         assert len(before[m] & after[m]) >= 3, (m, before[m], after[m])
     assert e.check() == ""
+
+
+def test_two_tenant_probe_keeps_halves_when_one_is_classified():
+    """Two present tenants, both probing, hold a class half each.  When the
+    one on the upper half is classified compute first (config #5: the
+    trainer, while the decode tenant has no clean window yet), neither
+    moves: the pool's orientation is mirrored instead of swapping the two
+    tenants' CU masks."""
+    e, parts = _engine()
+    a, b = e.tenant_create("a", nslots=32), e.tenant_create("b", nslots=32)
+    e.wake(a)
+    e.wake(b)
+    _settle(e, {}, 50)  # no counters yet: the two-tenant probe (class halves)
+    assert e.tenant_info(a).budget_ctx & 0xF == 0x3 and e.tenant_info(b).budget_ctx & 0xF == 0xC
+    _settle(e, {b: COMPUTE}, 300)  # b classified compute; a still without counters
+    assert e.lib.gpbs_tenant_class(e.h, b) == 0 and e.lib.gpbs_tenant_class(e.h, a) < 0
+    assert e.tenant_info(a).budget_ctx & 0xF == 0x3 and e.tenant_info(b).budget_ctx & 0xF == 0xC
+    assert e.perfc()["mirror"] >= 1
+    _settle(e, {a: MEMORY, b: COMPUTE}, 300)  # a classified memory: the class layout, mirrored
+    assert e.lib.gpbs_tenant_class(e.h, a) == 1
+    assert e.tenant_info(a).budget_ctx & 0xF == 0x3 and e.tenant_info(b).budget_ctx & 0xF == 0xC
+    assert e.check() == ""
