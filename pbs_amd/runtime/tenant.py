@@ -288,11 +288,17 @@ class TenantClient:
             # starts on the swapped halves: profiles/llm5/config5_r3g_swap_nohwc.json).
             # A transitional layout (the tenant on the other class's half) and
             # a later class flip run unmasked instead.
+            # A transitional set of three SEs runs on the half it holds whole
+            # (round 6: run unmasked, it spread the decode tenant's kernels
+            # over the trainer's SE for ~0.8 s of every config #5 start-up
+            # while the two-tenant layout formed, profiles/r6/s37, s38).
             ses = {c for (_, c) in parts}
             if ses <= {0, 1}:
                 ses = (0, 1)
             elif ses <= {2, 3}:
                 ses = (2, 3)
+            elif len(ses) == 3:
+                ses = (0, 1) if {0, 1} <= ses else (2, 3)
             else:
                 return torch.cuda.current_stream()
             if self.one_queue:
