@@ -3389,8 +3389,10 @@ int gpbs_gpu_set_se_mode(void* p, int on) {
   // process's runlist, which preempts every queue it has: the lazy burst at
   // the first SE-exclusive relayout froze ALL runners for ~100 ms
   // (profiles/r6/phase_debug_summary.txt).  A pool made earlier (the bench's
-  // pipe pre-flight) is kept.
-  if (on && gpbs_hip_masked_pool_prealloc(c->device, nullptr, 0) < 0) return -12;
+  // pipe pre-flight) is kept.  on == 2: SE mode without the pool -- a
+  // process that launches no tenant kernel (gpbsd: its tenants are other
+  // processes) must not hold ten idle hardware queues.
+  if (on == 1 && gpbs_hip_masked_pool_prealloc(c->device, nullptr, 0) < 0) return -12;
   __atomic_store_n(&c->se_mode, on ? 1 : 0, __ATOMIC_RELEASE);
   if (!on) c->share.store(0, std::memory_order_release);  // class sharing exists only over SE partitions
   return 0;

@@ -99,7 +99,7 @@ class Daemon:
                 ctx.set_table_mode("bar")
             except RuntimeError:
                 pass
-            ctx.set_se_mode(True)
+            ctx.set_se_mode(True, pool=False)  # the tenants are other processes
         if self.hw_counters:
             from ..counters import hwc
             if not hwc.active():

@@ -316,10 +316,12 @@ class GpuContext:
         """Attribute the newest counter snapshot now (engine-less use)."""
         return self.L.gpbs_gpu_hwc_poll(self.h)
 
-    def set_se_mode(self, on: bool):
+    def set_se_mode(self, on: bool, pool: bool = True):
         """SE-exclusive partitions: the 4 partitions of each XCD are its shader
-        engines, each owned by one tenant at a time (GATE_SE gating)."""
-        rc = self.L.gpbs_gpu_set_se_mode(self.h, 1 if on else 0)
+        engines, each owned by one tenant at a time (GATE_SE gating).
+        ``pool``: make the process's CU-masked queue burst now (False in a
+        process that runs no tenant kernel, e.g. gpbsd)."""
+        rc = self.L.gpbs_gpu_set_se_mode(self.h, (1 if pool else 2) if on else 0)
         if rc:
             raise RuntimeError("set_se_mode failed")
 
