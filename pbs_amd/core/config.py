@@ -54,8 +54,11 @@ MI355X_PROFILE: Dict[str, Any] = dict(
     # region's virtual time keeps the shares weight-fair whatever the quanta
     # (credit.cpp quantum_us / region_pick).  Round 5's region quantum (the
     # co-sharers' largest, floored at a global 30 ms: region_q=1,
-    # shared_q_us=30000) stays as the gpbs-sq30 ablation.
-    region_q=0, region_vt=1, switch_floor_x=200, switch_floor_max_us=60000, shared_q_us=0, slo_cap=0,
+    # shared_q_us=30000) stays as the gpbs-sq30 ablation.  The cap is 30 ms:
+    # three GEMMs taking 60 ms turns got ~9 turns each in a 1.6 s window, so
+    # one turn more or less moved a GEMM's share by ~10 % (8mix runs 1.395 to
+    # 1.445, profiles/r6/s33), and a co-sharer waited 120 ms for its turn.
+    region_q=0, region_vt=1, switch_floor_x=200, switch_floor_max_us=30000, shared_q_us=0, slo_cap=0,
     # a present tenant unclassified for 50 ms (a latency tenant whose 50 us
     # requests never fill a clean counter window) joins the memory class
     # instead of holding every tenant in the probe layout (slo mix, s2 diag)
