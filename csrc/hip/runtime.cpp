@@ -300,6 +300,7 @@ struct GpuCtx {
   int slot_se[kNumPmc] = {1, 1, 1, 0};  // slot k resolved per shader engine
   u64* h_blk = nullptr;                 // pinned landing buffer of d_cnt copies
   std::vector<u64> snap_blk, blk_prev;  // newest published / last consumed model block
+  std::vector<u64> red_prev;            // modeled-counter mode: the block the last metric tick read
   std::vector<u64> snap_se;             // [kXcds * kCtx(=SEs) * kNumPmc]
   std::vector<u64> snap_x;              // [kXcds * kNumPmc]
   std::vector<int64_t> snap_own;        // [kMaxTenants * kXcds * kCtx]
@@ -1340,6 +1341,30 @@ int ctr_tenant_deltas(void* user, int n, const int* tenants, uint64_t* out) {
   if (c->hwc) return hwc_tenant_deltas(c, n, tenants, out);
   const int64_t t0 = mono_ns();
   RoctxRange rr("gpbs:metric_tick");
+  if (c->cnt_bar) {
+    // Modeled counters only (no live sampler): the block crosses the BAR and
+    // is reduced here -- no k_counter_reduce on the tenants' queues (a
+    // rocprofv3 kernel trace of --counters model showed it at 1 kHz,
+    // profiles/r6/s45_rocprof_summary.txt)
+    static thread_local std::vector<u64> blk;
+    blk.resize((size_t)kMaxTenants * kXcds * kNumPmc);
+    read_block(c, blk.data());
+    const int rows = std::min(kMaxTenants, std::max(1, c->cnt_rows.load(std::memory_order_relaxed)));
+    for (int k = 0; k < n; ++k) {
+      const int t = tenants[k];
+      for (int i = 0; i < kNumPmc; ++i) out[k * kNumPmc + i] = 0;
+      if (t < 0 || t >= rows) continue;
+      for (int x = 0; x < kXcds; ++x)
+        for (int i = 0; i < kNumPmc; ++i) {
+          const size_t j = ((size_t)t * kXcds + x) * kNumPmc + i;
+          out[k * kNumPmc + i] += dpos(blk[j], c->red_prev[j]);  // Q5
+          c->red_prev[j] = blk[j];
+        }
+    }
+    c->metric_calls++;
+    c->metric_ns += mono_ns() - t0;
+    return 0;
+  }
   if (c->red_pending && hipEventQuery(c->red_ev) == hipErrorNotReady) {
     // The previous reduce has not finished (a tail, ~0.1 % of periods): never
     // wait for it under the engine lock.  This period reports nothing (the
@@ -2271,6 +2296,7 @@ void* gpbs_gpu_ctx_create(int device, int part_base, int table_mode, int nctx) {
                  hipSuccess;
   ok = ok && hipEventCreateWithFlags(&c->blk_ev, hipEventDisableTiming) == hipSuccess;
   c->blk_prev.assign((size_t)kMaxTenants * kXcds * kNumPmc, 0);
+  c->red_prev.assign((size_t)kMaxTenants * kXcds * kNumPmc, 0);
   c->snap_blk.assign((size_t)kMaxTenants * kXcds * kNumPmc, 0);
   c->snap_se.assign((size_t)kXcds * kCtx * kNumPmc, 0);
   c->snap_x.assign((size_t)kXcds * kNumPmc, 0);
