@@ -561,8 +561,11 @@ def test_crowded_memory_region_is_split_by_partitions(mode):
     # each memory tenant runs on its whole block (the light tenant's idle
     # block may lend itself to a waiting slot: class_steal work conservation)
     assert all(owned[m] == info[m].online_slots for m in ms), owned
-    if mode == 2:  # the light block lies inside the last backlogged tenant's
-        assert info[lat].budget_ctx & 0xF == 0x8, hex(info[lat].budget_ctx)
+    if mode == 2:  # the light block lies inside the largest backlogged block (SE2 of XCDs 0-5)
+        assert info[lat].budget_ctx & 0xF == 0x4, hex(info[lat].budget_ctx)
+        big = max(ms, key=lambda m: info[m].online_slots)
+        lat_parts = {p for p in range(len(parts)) if parts[p][2] == 2 and parts[p][1] in (4, 5)}
+        assert info[big].online_slots == 6 and lat_parts, info[big]
     assert e.perfc()["mem_split"] >= 1
     assert e.check() == ""
 
