@@ -236,9 +236,10 @@ POLICY_ENGINES = {
     # the flagship on round 5's device path (device table + k_partition_switch,
     # k_adapt, k_hwc_attribute), and with only the table moved to the BAR
     "gpbs-dev": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, RT_DEV),
-    # crowded memory regions split by partitions instead of time-shared (boot mem_split)
-    "gpbs-ms": (4, dict(BUDGET_OVERRIDES, class_budget=1, mem_split=1), True, RT),  # (= gpbs since round 6)
-    # ... with the light (latency) tenant's block overlapping a backlogged tenant's
+    # crowded memory regions split by partitions with a dedicated light
+    # (latency) block (mem_split 1); gpbs-ms2 = the flagship's mem_split 2
+    # (the light block overlaps the largest backlogged block)
+    "gpbs-ms": (4, dict(BUDGET_OVERRIDES, class_budget=1, mem_split=1), True, RT),
     "gpbs-ms2": (4, dict(BUDGET_OVERRIDES, class_budget=1, mem_split=2), True, RT),
     "gpbs-bar": (4, dict(BUDGET_OVERRIDES, class_budget=1), True, "bar,se,waveprio,latco,budget,latmem"),
     # the flagship with a smaller hardware-sample budget (SAMPLER below)
