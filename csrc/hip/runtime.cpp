@@ -1756,9 +1756,30 @@ struct MaskedPoolCore {
     return -1;
   }
 };
+// The pool object is never destroyed (its streams must outlive any static
+// teardown order); its queues are destroyed at exit, by an atexit handler
+// registered after the HIP runtime came up -- so it runs before the runtime's
+// own teardown and before a profiler's tool finalizer registered earlier.
+// Left to the runtime's teardown, the CU-masked queues crashed every process
+// run under rocprofv3 in __cxa_finalize after the tool had finalized
+// (scripts/exit_probe.py: "pool" rc 139, "ctx0" without the pool rc 0).
+void masked_pool_teardown();
 MaskedPoolCore& masked_pool() {
-  static MaskedPoolCore* p = new MaskedPoolCore;  // never destroyed: streams outlive static teardown order
+  static MaskedPoolCore* p = [] {
+    auto* q = new MaskedPoolCore;
+    std::atexit(masked_pool_teardown);
+    return q;
+  }();
   return *p;
+}
+void masked_pool_teardown() {
+  MaskedPoolCore& P = masked_pool();
+  std::lock_guard<std::mutex> g(P.mu);
+  for (auto& e : P.ents)
+    if (e.s && hipStreamQuery(e.s) == hipSuccess) {  // never wait: a gated grid may be parked for good
+      hipStreamDestroy(e.s);
+      e.s = nullptr;
+    }
 }
 void half_mask(int h, uint32_t m[8]);
 hipStream_t masked_acquire_key(const uint32_t m[8], uint32_t key, double load = 0) {
