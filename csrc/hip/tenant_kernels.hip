@@ -1330,6 +1330,11 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256p2_bf16_tn(const u16* __res
 // accumulator registers AGPR <-> VGPR around every K-tile, and the 16-read /
 // 16-glds clumps leave the matrix pipe idle; interleaving them one per MFMA in
 // source order (sched_barrier fences) made the copies worse: 896 TF/s.
+// Round 6, ROCm 7.2 ISA: the compiler picks the VGPR form of every MFMA here
+// (accumulators in VGPRs, 476 registers) and uses the AGPRs as spill space:
+// 320 v_accvgpr_read + 544 v_accvgpr_write per unit, 96 + 64 of them inside
+// each 64-MFMA block.  Neither `-mllvm -amdgpu-mfma-vgpr-form=0` nor an
+// inline asm that clobbers an AGPR moves the accumulators into AGPRs.
 // Reaching the library needs the schedule in assembly, not in HIP.
 constexpr int G4_NT = 256;
 
