@@ -1305,9 +1305,6 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256p2_bf16_tn(const u16* __res
   }
   finish(q, status, (u32)ntiles);
 }
-#undef GPBS_DSR
-#undef GPBS_TOUCH
-#undef GPBS_LGKM
 
 // ------------------------------------------------ GEMM 256x256, 4 waves ----
 // The shape hipBLASLt picks for this GEMM on gfx950 (rocprofv3 kernel trace of
@@ -1338,6 +1335,23 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256p2_bf16_tn(const u16* __res
 // Reaching the library needs the schedule in assembly, not in HIP.
 constexpr int G4_NT = 256;
 
+// AS = 1 (host opts bit 20 with bit 5): the MFMAs as inline asm with the
+// accumulator tied to AGPRs ("+a"), so the 256 accumulators live in the AGPR
+// half of the register file and the fragments in VGPRs -- the split the
+// compiler does not choose by itself.  The asm is opaque to the hazard
+// recognizer, so the kernel pads the two hazards it creates itself: after
+// zeroing the accumulators (v_accvgpr_write -> MFMA SrcC) and after the last
+// MFMA (XDL write -> v_accvgpr_read in the epilogue).
+template <int AS>
+__device__ __forceinline__ void w4_mfma(f32x4& acc, const bf16x8& a, const bf16x8& b) {
+  if constexpr (AS) {
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+  } else {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+  }
+}
+
+template <int AS>
 __global__ __launch_bounds__(G4_NT, 1) void k_gemm256w4_bf16_tn(const u16* __restrict__ A,
                                                                const u16* __restrict__ Bt, u16* __restrict__ C,
                                                                int M, int N, int K, WorkQueue* q,
@@ -1390,6 +1404,7 @@ __global__ __launch_bounds__(G4_NT, 1) void k_gemm256w4_bf16_tn(const u16* __res
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (AS) asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
     bf16x8 xa[8], xb[8], ya[8], yb[8];
 
     stage_tile(0);
@@ -1411,7 +1426,7 @@ __global__ __launch_bounds__(G4_NT, 1) void k_gemm256w4_bf16_tn(const u16* __res
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xb[j], xa[i], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 8; ++j) w4_mfma<AS>(acc[i][j], xb[j], xa[i]);
       __builtin_amdgcn_sched_barrier(0);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (t + 1 < nt) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1427,11 +1442,12 @@ __global__ __launch_bounds__(G4_NT, 1) void k_gemm256w4_bf16_tn(const u16* __res
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(yb[j], ya[i], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 8; ++j) w4_mfma<AS>(acc[i][j], yb[j], ya[i]);
       __builtin_amdgcn_sched_barrier(0);
     }
     // (every read of this unit fed an MFMA above; grab_unit's barriers keep
     // the next unit's prologue staging behind all of them)
+    if constexpr (AS) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -1446,6 +1462,172 @@ __global__ __launch_bounds__(G4_NT, 1) void k_gemm256w4_bf16_tn(const u16* __res
   }
   finish(q, status, (u32)ntiles);
 }
+
+// --------------------------- GEMM 256x256, 4 waves, interleaved schedule ---
+// k_gemm256w4_bf16_tn<1>'s shape and register split (256 accumulators in
+// AGPRs through inline-asm MFMAs, the fragments of two K-substeps in VGPRs),
+// with the whole K loop in a fixed issue order: fragment reads are inline-asm
+// ds_read_b128 and every MFMA / read / staging load sits between
+// sched_barrier fences, so the 16 reads and 16 glds of a substep are spread
+// one per MFMA over the first half of its 64 MFMAs instead of issued in
+// clumps.  Per K-tile t (buffer b = t & 1, set X = substep (t, 0) in VGPRs):
+//   M1: 64 MFMA on X; reads of (t, 1) -> Y behind MFMAs 0, 2, .., 30;
+//       lgkmcnt(0), vmcnt(0) (my part of tile t+1 landed), s_barrier
+//       (buffer b read by nobody any more; tile t+1 visible everywhere);
+//   M2: 64 MFMA on Y; glds of tile t+2 -> buffer b behind MFMAs 1, 3, ..;
+//       reads of (t+1, 0) -> X from buffer b^1 behind MFMAs 0, 2, .., 30;
+//       lgkmcnt(0) at the next M1 (X landed).
+// Epilogue: C staged through LDS, full-line non-temporal stores (as BAL 8);
+// 2-D per-XCD tile blocks with opts bit 3.  Host opts bit 21 (with bit 5).
+__global__ __launch_bounds__(G4_NT, 1) void k_gemm256w4i_bf16_tn(const u16* __restrict__ A,
+                                                                const u16* __restrict__ Bt, u16* __restrict__ C,
+                                                                int M, int N, int K, WorkQueue* q,
+                                                                const PartTable* table, u32 mode, u32 me, u64* cnt,
+                                                                u32 inst_per_tile, u32 refs_per_tile,
+                                                                u32 miss_per_tile, u32* status) {
+  __shared__ __attribute__((aligned(16))) char smem[kG2Lds + 16];
+  lds_t* lds = (lds_t*)smem;
+  int* s_slot = (int*)(smem + kG2Lds);
+  const u32 xcc = xcc_id();
+  u64 t_last = __builtin_amdgcn_s_memtime();
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wu = __builtin_amdgcn_readfirstlane(wid);
+  const int wr = wu >> 1, wc = wu & 1;
+  const int tiles_m = M / G2_BM, tiles_n = N / G2_BM, ntiles = tiles_m * tiles_n;
+  const int nt = K / G2_BK;
+  int soff[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = 8 * (4 * wid + j) + (lane >> 3);
+    soff[j] = row * K + (((lane & 7) ^ g2_swz(row)) * 8);
+  }
+  const int l16 = lane & 15, lq = lane >> 4;
+  for (;;) {
+    const int tile = grab_unit(q, table, mode, me, xcc, s_slot, (u32)ntiles);
+    if (tile < 0) break;
+    int tm = tile / tiles_n, tn = tile % tiles_n;
+    if ((mode & kGemmBlock2D) && (tiles_m & 3) == 0 && (tiles_n & 1) == 0 && ntiles % kXcds == 0) {
+      const int bm = tiles_m / 4, bn = tiles_n / 2, g = tile % kXcds, jj = tile / kXcds;
+      tm = (g >> 1) * bm + jj / bn;
+      tn = (g & 1) * bn + jj % bn;
+    }
+    const u16* Ab = A + (size_t)tm * G2_BM * K;
+    const u16* Bb = Bt + (size_t)tn * G2_BM * K;
+    // glds n (0..15) of K-tile t: operand n >> 3, half (n >> 2) & 1, chunk n & 3
+    auto glds_n = [&](int t, int n) {
+      const int kind = n >> 3, h = (n >> 2) & 1, j = n & 3;
+      const u16* src = (kind ? Bb : Ab) + (size_t)h * 128 * K + t * G2_BK;
+      lds_t* dst = lds + (t & 1) * kG2Buf + (kind * 2 + h) * kG2Half + wid * 4096;
+      glds16(src + soff[j], dst + j * 1024);
+    };
+    auto fp = [&](int b, int kind, int h, int r0, int s) -> const lds_t* {
+      const int r = r0 + l16;
+      return lds + b * kG2Buf + (kind * 2 + h) * kG2Half + r * 128 + (((4 * s + lq) ^ g2_swz(r)) << 4);
+    };
+    // read n (0..15) of substep s from buffer b: B blocks 0..7, then A blocks 0..7
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+    bf16x8 xa[8], xb[8], ya[8], yb[8];
+
+#pragma unroll
+    for (int n = 0; n < 16; ++n) glds_n(0, n);
+    if (nt > 1) {
+#pragma unroll
+      for (int n = 0; n < 16; ++n) glds_n(1, n);
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) GPBS_DSR(xb[j], fp(0, 1, wc, j * 16, 0));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) GPBS_DSR(xa[i], fp(0, 0, wr, i * 16, 0));
+    __builtin_amdgcn_sched_barrier(0);
+
+    // one K-tile; PH 2: stage t+2 and read (t+1, 0), PH 1: read only, PH 0: last tile
+    auto ktile = [&](int t, auto ph) {
+      constexpr int PH = decltype(ph)::value;
+      const int b = t & 1;
+      // ---- M1: X; reads of (t, 1) -> Y
+      GPBS_LGKM(0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int k = 0; k < 64; ++k) {
+        w4_mfma<1>(acc[k >> 3][k & 7], xb[k & 7], xa[k >> 3]);
+        if ((k & 1) == 0 && k < 32) {
+          const int n = k >> 1;
+          if (n < 8) GPBS_DSR(yb[n], fp(b, 1, wc, n * 16, 1));
+          else GPBS_DSR(ya[n - 8], fp(b, 0, wr, (n - 8) * 16, 1));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      GPBS_LGKM(0);
+      if constexpr (PH > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- M2: Y; stage tile t+2 -> buffer b; reads of (t+1, 0) -> X
+#pragma unroll
+      for (int k = 0; k < 64; ++k) {
+        w4_mfma<1>(acc[k >> 3][k & 7], yb[k & 7], ya[k >> 3]);
+        if (k < 32) {
+          const int n = k >> 1;
+          if (k & 1) {
+            if constexpr (PH == 2) glds_n(t + 2, n);
+          } else if constexpr (PH > 0) {
+            if (n < 8) GPBS_DSR(xb[n], fp(b ^ 1, 1, wc, n * 16, 0));
+            else GPBS_DSR(xa[n - 8], fp(b ^ 1, 0, wr, (n - 8) * 16, 0));
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    int t = 0;
+    for (; t + 2 < nt; ++t) ktile(t, std::integral_constant<int, 2>());
+    if (t + 1 < nt) ktile(t++, std::integral_constant<int, 1>());
+    ktile(t, std::integral_constant<int, 0>());
+    // XDL results of the last MFMAs before the epilogue reads them
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7"
+                 : "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]), "+a"(acc[7][4]),
+                   "+a"(acc[7][5]), "+a"(acc[7][6]), "+a"(acc[7][7]));
+    asm volatile(""
+                 : "+a"(acc[6][0]), "+a"(acc[6][1]), "+a"(acc[6][2]), "+a"(acc[6][3]), "+a"(acc[6][4]),
+                   "+a"(acc[6][5]), "+a"(acc[6][6]), "+a"(acc[6][7]));
+    // C through LDS (every wave's reads retired before the last barrier;
+    // no staging load in flight): 8-byte fragments at row m, chunk c8 ^ (m & 15)
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int m = wr * 128 + i * 16 + l16;
+        const int c8 = wc * 32 + j * 4 + lq;
+        const u32 lo = (u32)f2bf(acc[i][j][0]) | ((u32)f2bf(acc[i][j][1]) << 16);
+        const u32 hi = (u32)f2bf(acc[i][j][2]) | ((u32)f2bf(acc[i][j][3]) << 16);
+        *(__attribute__((address_space(3))) u32x2*)(lds + m * 512 + ((c8 ^ (m & 15)) << 3)) = u32x2{lo, hi};
+      }
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < 32; ++p) {
+      const int row = p * 8 + (tid >> 5), c16 = tid & 31;
+      u32x4 v = *(const __attribute__((address_space(3))) u32x4*)(lds + row * 512 + (((2 * c16) ^ (row & 14)) << 3));
+      if (row & 1) v = u32x4{v.z, v.w, v.x, v.y};
+      u32x4* dst = (u32x4*)(C + (size_t)(tm * G2_BM + row) * N + tn * G2_BM + c16 * 8);
+      __builtin_nontemporal_store(v, dst);
+    }
+    __syncthreads();  // the next unit's prologue restages buffer 0
+    count_unit(cnt, me, xcc, inst_per_tile, &t_last, refs_per_tile, miss_per_tile, q);
+  }
+  finish(q, status, (u32)ntiles);
+}
+
+#undef GPBS_DSR
+#undef GPBS_TOUCH
+#undef GPBS_LGKM
 
 // ------------------------------------------------------------ HBM stream ---
 // dst = src (float4 copy), 16 B per lane, 16 loads in flight per thread: one
@@ -1689,9 +1871,14 @@ int gpbs_hip_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int
     const u32 m2 = mode | ((g_gemm_opts & 1) ? kGemmXRange : 0u) |
                    ((g_gemm_opts & 8) && ntiles % kXcds == 0 ? kGemmBlock2D : 0u);
     if ((g_gemm_opts & 32) && (K / G2_BK) % 2 == 0) {  // 4-wave 128x128-per-wave variant (plain tile queue)
-      hipLaunchKernelGGL(k_gemm256w4_bf16_tn, dim3(grid), dim3(G4_NT), 0, s, (const u16*)A, (const u16*)Bt, (u16*)C,
-                         M, N, K, (WorkQueue*)q, (const PartTable*)table, mode, me, (u64*)cnt, inst, refs, miss,
-                         (u32*)status);
+      if (g_gemm_opts & (1 << 21))
+        hipLaunchKernelGGL(k_gemm256w4i_bf16_tn, dim3(grid), dim3(G4_NT), 0, s, (const u16*)A, (const u16*)Bt,
+                           (u16*)C, M, N, K, (WorkQueue*)q, (const PartTable*)table, m2, me, (u64*)cnt, inst, refs,
+                           miss, (u32*)status);
+      else
+        hipLaunchKernelGGL((g_gemm_opts & (1 << 20)) ? k_gemm256w4_bf16_tn<1> : k_gemm256w4_bf16_tn<0>, dim3(grid),
+                           dim3(G4_NT), 0, s, (const u16*)A, (const u16*)Bt, (u16*)C, M, N, K, (WorkQueue*)q,
+                           (const PartTable*)table, mode, me, (u64*)cnt, inst, refs, miss, (u32*)status);
       return hipGetLastError() == hipSuccess ? 0 : -5;
     }
     if (g_gemm_opts & 524288) {  // bit 19: bit 18's schedule, counted waits on asm fragment reads

@@ -67,7 +67,10 @@ def main():
                  256 | 8192 | 65536 | 131072 | 8: "2phase-own-a-lds-c-nt-2d-blocks",
                  256 | 8192 | 65536 | 131072 | 8 | 1: "2phase-own-a-lds-c-nt-2d-blocks-xcd-range",
                  262144: "pipelined-1-barrier",
-                 524288: "pipelined-1-barrier-asm-reads"}
+                 524288: "pipelined-1-barrier-asm-reads",
+                 32: "4wave", 32 | (1 << 20): "4wave-agpr-acc"}
+        if os.environ.get("KBENCH_GEMM_VARIANTS"):  # comma-separated opts values
+            names = {int(v): names.get(int(v), str(v)) for v in os.environ["KBENCH_GEMM_VARIANTS"].split(",")}
     ab = {k: [] for k in names}
     for _ in range(5):
         for opt in names:
