@@ -1138,6 +1138,7 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256p_bf16_tn(const u16* __rest
 // Host opts bit 19.
 #define GPBS_DSR(dst, p) asm volatile("ds_read_b128 %0, %1" : "=v"(dst) : "v"((u32)(size_t)(p)))
 #define GPBS_TOUCH(x) asm volatile("" : "+v"(x))
+#define W4J_DSR(dst, base, off) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(base), "i"(off))
 #define GPBS_LGKM(n) asm volatile("s_waitcnt lgkmcnt(" #n ")" ::: "memory")
 __global__ __launch_bounds__(G2_NT, 1) void k_gemm256p2_bf16_tn(const u16* __restrict__ A, const u16* __restrict__ Bt,
                                                                u16* __restrict__ C, int M, int N, int K, WorkQueue* q,
@@ -1625,7 +1626,215 @@ __global__ __launch_bounds__(G4_NT, 1) void k_gemm256w4i_bf16_tn(const u16* __re
   finish(q, status, (u32)ntiles);
 }
 
+// --------------- GEMM 256x256, 4 waves, row-split phases, 1.5-tile load lead ---
+// PMC of k_gemm256w4i (profiles/r6/s56_gemm_pmc.txt): MFMA busy 0.49 with
+// almost no LDS waits (0.017 of wave cycles) but SQ_WAIT_ANY 0.22 -- the
+// mid-tile vmcnt(0) on tile t+1, whose loads had one K-tile of lead, against
+// an L2 that misses a quarter of them.  The lead is set by when a buffer is
+// free: w4i reads both K-substeps of every row from buffer t&1 until the
+// middle of K-tile t.  Here a phase splits the wave's 128 rows instead:
+//   M1(t): rows 0-63 of the wave tile (XA(t) x B(t), 64 MFMAs), reading
+//          YA(t) = its A rows 64-127; M2(t): rows 64-127 (YA(t) x B(t)),
+//          reading X(t+1) = XA(t+1) + B(t+1) into the other B register set.
+// So once X(t) is read (barrier at the start of M1(t)), the B halves and the
+// A rows 0-63 of buffer t&1 are free: part P0 of tile t+2 (B, A rows 0-63:
+// 12 glds per wave) is staged during M1(t); part P1 (A rows 64-127, 4 glds)
+// during M2(t), after the mid-tile barrier retires YA(t).  Both parts have
+// 1.5 K-tiles to land: P0(t+1) is retired by vmcnt(16) before the mid-tile
+// barrier of t (X(t+1) is read in M2(t)), P1(t) by vmcnt(16) before the
+// barrier opening M1(t).  Fragments: XA, YA 32 VGPRs each, B 2 x 64.
+// Host opts bit 22 (with bit 5).
+__global__ __launch_bounds__(G4_NT, 1) void k_gemm256w4j_bf16_tn(const u16* __restrict__ A,
+                                                                const u16* __restrict__ Bt, u16* __restrict__ C,
+                                                                int M, int N, int K, WorkQueue* q,
+                                                                const PartTable* table, u32 mode, u32 me, u64* cnt,
+                                                                u32 inst_per_tile, u32 refs_per_tile,
+                                                                u32 miss_per_tile, u32* status) {
+  __shared__ __attribute__((aligned(16))) char smem[kG2Lds + 16];
+  lds_t* lds = (lds_t*)smem;
+  int* s_slot = (int*)(smem + kG2Lds);
+  const u32 xcc = xcc_id();
+  u64 t_last = __builtin_amdgcn_s_memtime();
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wu = __builtin_amdgcn_readfirstlane(wid);
+  const int wr = wu >> 1, wc = wu & 1;
+  const int tiles_m = M / G2_BM, tiles_n = N / G2_BM, ntiles = tiles_m * tiles_n;
+  const int nt = K / G2_BK;
+  // 1 KiB glds chunk c of a half = rows 8c .. 8c+7: per-lane source offset
+  auto goff = [&](int c) {
+    const int row = 8 * c + (lane >> 3);
+    return row * K + (((lane & 7) ^ g2_swz(row)) * 8);
+  };
+  // P0: A chunks (wu & 1) * 4 + j of half wu >> 1, B chunks 4 wu + j of both
+  // halves; P1: A chunks 8 + (wu & 1) * 4 + j of half wu >> 1
+  int oa0[4], ob[4], oa1[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    oa0[j] = goff((wu & 1) * 4 + j);
+    ob[j] = goff(4 * wu + j);
+    oa1[j] = goff(8 + (wu & 1) * 4 + j);
+  }
+  const int l16 = lane & 15, lq = lane >> 4;
+  // fragment address = lane base [buffer][substep][A|B] + an immediate (row
+  // block r0 * 128; r0 a multiple of 16 leaves the swizzle (r >> 1) & 7 to the lane)
+  u32 fb[2][2][2];
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int kind = 0; kind < 2; ++kind)
+        fb[b][s2][kind] = (u32)(size_t)(lds + b * kG2Buf + (kind * 2 + (kind ? wc : wr)) * kG2Half + l16 * 128 +
+                                        (((4 * s2 + lq) ^ ((l16 >> 1) & 7)) << 4));
+  for (;;) {
+    const int tile = grab_unit(q, table, mode, me, xcc, s_slot, (u32)ntiles);
+    if (tile < 0) break;
+    int tm = tile / tiles_n, tn = tile % tiles_n;
+    if ((mode & kGemmBlock2D) && (tiles_m & 3) == 0 && (tiles_n & 1) == 0 && ntiles % kXcds == 0) {
+      const int bm = tiles_m / 4, bn = tiles_n / 2, g = tile % kXcds, jj = tile / kXcds;
+      tm = (g >> 1) * bm + jj / bn;
+      tn = (g & 1) * bn + jj % bn;
+    }
+    const u16* Ab = A + (size_t)tm * G2_BM * K;
+    const u16* Bb = Bt + (size_t)tn * G2_BM * K;
+    // glds n of part P0 (n 0..11: A 0..3, B half 0 4..7, B half 1 8..11) or P1 (n 0..3)
+    // (ts = the source K-tile, buffer t & 1; past the last tile the loop
+    // restages tile nt - 1 into the free buffer, which nobody reads)
+    auto g_p0 = [&](int t, int n) {
+      const int ts = t < nt ? t : nt - 1;
+      lds_t* base = lds + (t & 1) * kG2Buf;
+      if (n < 4) {
+        const int h = wu >> 1, c = (wu & 1) * 4 + n;
+        glds16(Ab + (size_t)h * 128 * K + ts * G2_BK + oa0[n], base + h * kG2Half + c * 1024);
+      } else {
+        const int h = (n - 4) >> 2, j = n & 3;
+        glds16(Bb + (size_t)h * 128 * K + ts * G2_BK + ob[j], base + (2 + h) * kG2Half + (4 * wu + j) * 1024);
+      }
+    };
+    auto g_p1 = [&](int t, int n) {
+      const int ts = t < nt ? t : nt - 1;
+      const int h = wu >> 1, c = 8 + (wu & 1) * 4 + n;
+      glds16(Ab + (size_t)h * 128 * K + ts * G2_BK + oa1[n], lds + (t & 1) * kG2Buf + h * kG2Half + c * 1024);
+    };
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+    bf16x8 xa[4][2], ya[4][2], b0[8][2], b1[8][2];
+
+    // prologue: tiles 0 and 1 (nt even, host), then X(0)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int n = 0; n < 12; ++n) g_p0(t, n);
+#pragma unroll
+      for (int n = 0; n < 4; ++n) g_p1(t, n);
+    }
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) W4J_DSR(b0[j][s2], fb[0][s2][1], (j * 16) * 128);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) W4J_DSR(xa[i][s2], fb[0][s2][0], (i * 16) * 128);
+    __builtin_amdgcn_sched_barrier(0);
+
+    // one K-tile: PH 2 stages tile t+2 and reads X(t+1); PH 1 reads only; PH 0 last
+    auto ktile = [&](int t, auto ph, auto bq, bf16x8 (&bc)[8][2], bf16x8 (&bn)[8][2]) {
+      constexpr int PH = decltype(ph)::value;
+      constexpr int b = decltype(bq)::value;  // t & 1
+      GPBS_LGKM(0);  // X(t) landed
+      if constexpr (PH == 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // P1(t)
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- M1: rows 0-63; read YA(t); stage P0(t+2)
+#pragma unroll
+      for (int k = 0; k < 64; ++k) {
+        const int s2 = k >> 5, i = (k >> 3) & 3, j = k & 7;
+        w4_mfma<1>(acc[i][j], bc[j][s2], xa[i][s2]);
+        if (k < 16 && (k & 1) == 0) {
+          const int n = k >> 1;
+          W4J_DSR(ya[n >> 1][n & 1], fb[b][n & 1][0], (64 + (n >> 1) * 16) * 128);
+        }
+        if constexpr (PH == 2) {
+          if ((k & 1) && k < 24) g_p0(t + 2, k >> 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      GPBS_LGKM(0);  // YA(t) landed
+      if constexpr (PH == 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // P0(t+1)
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- M2: rows 64-127; read X(t+1); stage P1(t+2)
+#pragma unroll
+      for (int k = 0; k < 64; ++k) {
+        const int s2 = k >> 5, i = (k >> 3) & 3, j = k & 7;
+        w4_mfma<1>(acc[4 + i][j], bc[j][s2], ya[i][s2]);
+        if constexpr (PH > 0) {
+          if (k < 48 && (k & 1) == 0) {
+            const int n = k >> 1;  // 0..23: B blocks, then A blocks
+            if (n < 16) W4J_DSR(bn[n >> 1][n & 1], fb[1 - b][n & 1][1], ((n >> 1) * 16) * 128);
+            else W4J_DSR(xa[(n - 16) >> 1][n & 1], fb[1 - b][n & 1][0], (((n - 16) >> 1) * 16) * 128);
+          }
+        }
+        if constexpr (PH == 2) {
+          if ((k & 1) && k < 8) g_p1(t + 2, k >> 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    using P2 = std::integral_constant<int, 2>;
+    using Q0 = std::integral_constant<int, 0>;
+    using Q1 = std::integral_constant<int, 1>;
+    // one loop body for every K-tile (nt even, host): the last two tiles
+    // stage and read clamped copies instead of a tail with its own register
+    // assignment (which spilled)
+    for (int t = 0; t < nt; t += 2) {
+      ktile(t, P2(), Q0(), b0, b1);
+      ktile(t + 1, P2(), Q1(), b1, b0);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7"
+                 : "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]), "+a"(acc[7][4]),
+                   "+a"(acc[7][5]), "+a"(acc[7][6]), "+a"(acc[7][7]));
+    asm volatile(""
+                 : "+a"(acc[6][0]), "+a"(acc[6][1]), "+a"(acc[6][2]), "+a"(acc[6][3]), "+a"(acc[6][4]),
+                   "+a"(acc[6][5]), "+a"(acc[6][6]), "+a"(acc[6][7]));
+    __syncthreads();  // every wave's last LDS reads retired before C overwrites the buffers
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int m = wr * 128 + i * 16 + l16;
+        const int c8 = wc * 32 + j * 4 + lq;
+        const u32 lo = (u32)f2bf(acc[i][j][0]) | ((u32)f2bf(acc[i][j][1]) << 16);
+        const u32 hi = (u32)f2bf(acc[i][j][2]) | ((u32)f2bf(acc[i][j][3]) << 16);
+        *(__attribute__((address_space(3))) u32x2*)(lds + m * 512 + ((c8 ^ (m & 15)) << 3)) = u32x2{lo, hi};
+      }
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < 32; ++p) {
+      const int row = p * 8 + (tid >> 5), c16 = tid & 31;
+      u32x4 v = *(const __attribute__((address_space(3))) u32x4*)(lds + row * 512 + (((2 * c16) ^ (row & 14)) << 3));
+      if (row & 1) v = u32x4{v.z, v.w, v.x, v.y};
+      u32x4* dst = (u32x4*)(C + (size_t)(tm * G2_BM + row) * N + tn * G2_BM + c16 * 8);
+      __builtin_nontemporal_store(v, dst);
+    }
+    __syncthreads();
+    count_unit(cnt, me, xcc, inst_per_tile, &t_last, refs_per_tile, miss_per_tile, q);
+  }
+  finish(q, status, (u32)ntiles);
+}
 #undef GPBS_DSR
+#undef W4J_DSR
 #undef GPBS_TOUCH
 #undef GPBS_LGKM
 
@@ -1871,7 +2080,11 @@ int gpbs_hip_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int
     const u32 m2 = mode | ((g_gemm_opts & 1) ? kGemmXRange : 0u) |
                    ((g_gemm_opts & 8) && ntiles % kXcds == 0 ? kGemmBlock2D : 0u);
     if ((g_gemm_opts & 32) && (K / G2_BK) % 2 == 0) {  // 4-wave 128x128-per-wave variant (plain tile queue)
-      if (g_gemm_opts & (1 << 21))
+      if (g_gemm_opts & (1 << 22))
+        hipLaunchKernelGGL(k_gemm256w4j_bf16_tn, dim3(grid), dim3(G4_NT), 0, s, (const u16*)A, (const u16*)Bt,
+                           (u16*)C, M, N, K, (WorkQueue*)q, (const PartTable*)table, m2, me, (u64*)cnt, inst, refs,
+                           miss, (u32*)status);
+      else if (g_gemm_opts & (1 << 21))
         hipLaunchKernelGGL(k_gemm256w4i_bf16_tn, dim3(grid), dim3(G4_NT), 0, s, (const u16*)A, (const u16*)Bt,
                            (u16*)C, M, N, K, (WorkQueue*)q, (const PartTable*)table, m2, me, (u64*)cnt, inst, refs,
                            miss, (u32*)status);
