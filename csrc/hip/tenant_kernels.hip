@@ -1480,6 +1480,10 @@ __global__ __launch_bounds__(G4_NT, 1) void k_gemm256w4_bf16_tn(const u16* __res
 //       lgkmcnt(0) at the next M1 (X landed).
 // Epilogue: C staged through LDS, full-line non-temporal stores (as BAL 8);
 // 2-D per-XCD tile blocks with opts bit 3.  Host opts bit 21 (with bit 5).
+// Measured (profiles/r6/s54, s55, s57; kbench, same process): the AGPR split
+// alone lifts the 4-wave kernel from 922 to 1077 TF/s; this issue order to
+// 1237-1254, against 1266-1273 for the shipped 8-wave kernel and 1281-1423
+// for torch.mm.  Not the default.
 __global__ __launch_bounds__(G4_NT, 1) void k_gemm256w4i_bf16_tn(const u16* __restrict__ A,
                                                                 const u16* __restrict__ Bt, u16* __restrict__ C,
                                                                 int M, int N, int K, WorkQueue* q,
@@ -1643,7 +1647,10 @@ __global__ __launch_bounds__(G4_NT, 1) void k_gemm256w4i_bf16_tn(const u16* __re
 // 1.5 K-tiles to land: P0(t+1) is retired by vmcnt(16) before the mid-tile
 // barrier of t (X(t+1) is read in M2(t)), P1(t) by vmcnt(16) before the
 // barrier opening M1(t).  Fragments: XA, YA 32 VGPRs each, B 2 x 64.
-// Host opts bit 22 (with bit 5).
+// Host opts bit 22 (with bit 5).  Measured 1232 TF/s vs 1237 for w4i in the
+// same process (profiles/r6/s57_kbench_w4j.jsonl): the longer lead buys
+// nothing, so the load lead is not what holds the 4-wave kernels at ~0.49
+// MFMA busy.  Not the default.
 __global__ __launch_bounds__(G4_NT, 1) void k_gemm256w4j_bf16_tn(const u16* __restrict__ A,
                                                                 const u16* __restrict__ Bt, u16* __restrict__ C,
                                                                 int M, int N, int K, WorkQueue* q,
