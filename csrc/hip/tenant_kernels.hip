@@ -208,6 +208,17 @@ __global__ __launch_bounds__(GNT, 2) void k_gemm_bf16_tn(const u16* __restrict__
 constexpr int G2_BM = 256, G2_BK = 64, G2_NT = 512;
 constexpr u32 kGemmXRange = 1u << 16;  // mode bit: XCD-range tile queues (grab_unit_x)
 constexpr u32 kGemmBlock2D = 1u << 17; // mode bit: 2-D per-XCD tile blocks
+// mode bit (host opts bit 23, ungated launches with one unit per workgroup
+// only): unit = blockIdx.x, no work-queue atomic.  A diagnostic of what the
+// persistent queue -- which gating, parking and relaunch need -- costs a
+// solo launch (scripts/gemm_shapes.py); never set by the runners.  Measured
+// (profiles/r6/s61_gemm_shapes.jsonl): 4096^3 0.1130 -> 0.1052 ms (1216 ->
+// 1306 TF/s; torch.mm 1475 on that box).  The queue costs ~8 us per launch:
+// each workgroup waits on three device-scope atomics with returns (its
+// grab, the grab that finds the queue empty, the exit count), a memory
+// round trip each, at the start and end of the kernel where nothing hides
+// them.  At 8192^3 (4 units per workgroup) the two tie.
+constexpr u32 kGemmStatic = 1u << 18;
 // host: bit 0 = XCD-range tile queues, bit 1 = DEEP prefetch variant, bit 2 =
 // staggered wave groups.  Default = staggered, plain queue: interleaved A/B
 // in one process at 4096^3 (profiles/kbench_r1.jsonl) measured staggered
@@ -570,8 +581,9 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
   int units_seen = 0;
 
   for (;;) {
-    const int tile = (mode & kGemmXRange) ? grab_unit_x(q, table, mode, me, xcc, s_slot, (u32)ntiles)
-                                          : grab_unit(q, table, mode, me, xcc, s_slot, (u32)ntiles);
+    const int tile = (mode & kGemmStatic) ? (units_seen ? -1 : (int)blockIdx.x)
+                     : (mode & kGemmXRange) ? grab_unit_x(q, table, mode, me, xcc, s_slot, (u32)ntiles)
+                                            : grab_unit(q, table, mode, me, xcc, s_slot, (u32)ntiles);
     if (tile < 0) break;
     int tm = tile / tiles_n, tn = tile % tiles_n;
     if ((mode & kGemmBlock2D) && (tiles_m & 3) == 0 && (tiles_n & 1) == 0 && ntiles % kXcds == 0) {
@@ -943,9 +955,9 @@ __global__ __launch_bounds__(G2_NT, 1) void k_gemm256s2_bf16_tn(const u16* __res
       }
     }
     ++units_seen;
-    count_unit(cnt, me, xcc, inst_per_tile, &t_last, refs_per_tile, miss_per_tile, q);
+    if (!(mode & kGemmStatic)) count_unit(cnt, me, xcc, inst_per_tile, &t_last, refs_per_tile, miss_per_tile, q);
   }
-  finish(q, status, (u32)ntiles);
+  if (!(mode & kGemmStatic)) finish(q, status, (u32)ntiles);  // (static: the queue was never touched)
 }
 
 // ------------------------- GEMM 256x256, 8 waves, pipelined fragments ----
@@ -2085,7 +2097,8 @@ int gpbs_hip_gemm_bf16(const void* A, const void* Bt, void* C, int M, int N, int
     const u32 refs = (u32)(((u64)2 * G2_BM * K * 2) / 128);
     const u32 miss = (u32)((((u64)M + N) * K * 2 / 128) / ntiles + (u64)G2_BM * G2_BM * 2 / 128);
     const u32 m2 = mode | ((g_gemm_opts & 1) ? kGemmXRange : 0u) |
-                   ((g_gemm_opts & 8) && ntiles % kXcds == 0 ? kGemmBlock2D : 0u);
+                   ((g_gemm_opts & 8) && ntiles % kXcds == 0 ? kGemmBlock2D : 0u) |
+                   ((g_gemm_opts & (1 << 23)) && (mode & 3) == GATE_NONE && grid == ntiles ? kGemmStatic : 0u);
     if ((g_gemm_opts & 32) && (K / G2_BK) % 2 == 0) {  // 4-wave 128x128-per-wave variant (plain tile queue)
       if (g_gemm_opts & (1 << 22))
         hipLaunchKernelGGL(k_gemm256w4j_bf16_tn, dim3(grid), dim3(G4_NT), 0, s, (const u16*)A, (const u16*)Bt,

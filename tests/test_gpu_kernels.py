@@ -184,7 +184,8 @@ def test_device_adapt_bit_exact_vs_host():
 
 @pytest.mark.parametrize("opts", [0, 1, 2, 3, 4, 5, 16, 32, 256, 256 | 8, 256 | 9, 256 | 1024, 256 | 64, 256 | 4096, 256 | 4096 | 64, 256 | 8192, 256 | 8192 | 64, 256 | 8192 | 32768, 256 | 8192 | 65536, 256 | 8192 | 65536 | 131072, 256 | 16384, 256 | 16384 | 64, 262144, 524288,
                                   256 | 8192 | 65536 | 131072 | 8, 256 | 8192 | 65536 | 131072 | 9,
-                                  32 | (1 << 20), 32 | (1 << 21), 32 | (1 << 21) | 8, 32 | (1 << 22), 32 | (1 << 22) | 8])
+                                  32 | (1 << 20), 32 | (1 << 21), 32 | (1 << 21) | 8, 32 | (1 << 22), 32 | (1 << 22) | 8,
+                                  256 | 8192 | 65536 | 131072 | 8 | (1 << 23)])
 def test_gemm256_variants_match_reference(opts):
     """Every 256x256 schedule variant (plain / XCD-range tile queue x one-half-
     per-phase / deep prefetch; the 2-phase kernel -- the default -- with 2-D
